@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Headline benchmark: validator-pod bf16 GEMM TFLOPS on 1/2/4/8 MI355X (+ time-to-first-GPU-result).
+
+BASELINE.json names the metric "validator-pod bf16 GEMM TFLOPS/GPU + time-to-first-GPU-pod,
+1/2/4/8 MI355X".  One *step* is what the operator's validator pod runs on each GPU it was
+allocated: one 8192×8192×8192 bf16 GEMM (C = A·Bᵀ, fp32 accumulate, bf16 out) through the
+hand-written gfx950 MFMA kernel (k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950.hip), on random
+[-1,1) operands (synthetic data).  Work per GPU is fixed as N grows → weak scaling.
+
+Launch contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 under
+``torch.distributed.run`` with one rank per GPU (RCCL backend).  W untimed steps, then exactly K
+timed steps bracketed by barrier + synchronize on both sides; the MAX elapsed over ranks is used;
+rank 0 prints ONE JSON line.  ``value`` is the whole-job aggregate TFLOPS over all N GPUs.
+
+Outside the timed region it also reports:
+* ``time_to_first_gpu_result_s`` — process start → first verified GPU result (HIP vectorAdd,
+  reference protocol), the in-process part of the "time-to-first-GPU-pod" metric;
+* ``numerics`` — sampled max error of the timed kernel against an fp32 on-device reference;
+* ``allreduce_busbw_gbps`` — RCCL all-reduce bus bandwidth over xGMI across the N ranks (N > 1).
+"""
+from __future__ import annotations
+
+import time
+
+_T_PROCESS_START = time.time()
+
+import argparse  # noqa: E402
+import json  # noqa: E402
+import os  # noqa: E402
+import sys  # noqa: E402
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from k8s_nvidia_gpus_amd.ops import kernels as K  # noqa: E402
+
+METRIC = "validator-pod bf16 GEMM TFLOPS/GPU + time-to-first-GPU-pod, 1/2/4/8 MI355X"
+BASELINE_VALUE = None  # BASELINE.json "published": {} — the reference publishes no numbers
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--size", type=int, default=8192, help="M = N = K of the validator GEMM")
+    ap.add_argument("--allreduce-mib", type=int, default=256,
+                    help="message size of the post-run RCCL all-reduce probe (N > 1)")
+    ap.add_argument("--no-allreduce", action="store_true")
+    return ap.parse_args(argv)
+
+
+def first_gpu_result(device: torch.device) -> float:
+    """Reference-protocol vectorAdd (50 000 fp32, 196×256) — returns seconds since process start."""
+    n = 50000
+    g = torch.Generator().manual_seed(1234)
+    ha, hb = torch.rand(n, generator=g), torch.rand(n, generator=g)
+    c = K.vector_add(ha.to(device), hb.to(device))
+    ok = torch.allclose(c.cpu(), ha + hb, atol=1e-5, rtol=0)
+    if not ok:
+        raise RuntimeError("vectorAdd verification failed")
+    return time.time() - _T_PROCESS_START
+
+
+def check_numerics(a, b, c, samples: int = 1024) -> float:
+    m, n = c.shape
+    g = torch.Generator().manual_seed(7)
+    coords = torch.stack([torch.randint(0, m, (samples,), generator=g),
+                          torch.randint(0, n, (samples,), generator=g)], dim=1).to(torch.int32)
+    ref = K.gemm_sample_check(a, b, coords)
+    got = c[coords[:, 0].long().to(c.device), coords[:, 1].long().to(c.device)].float()
+    err = (got - ref).abs()
+    tol = 0.01 * ref.abs() + 0.02 * (a.shape[1] ** 0.5) / 16
+    bad = int((err > tol).sum().item())
+    if bad:
+        raise RuntimeError(f"GEMM numerics check failed: {bad}/{samples} samples out of tolerance, "
+                           f"max err {err.max().item():.3e}")
+    return float((err / (ref.abs() + 1.0)).max().item())
+
+
+def allreduce_probe(device, world: int, mib: int) -> float:
+    count = mib * 1024 * 1024 // 4
+    x = torch.ones(count, dtype=torch.float32, device=device)
+    for _ in range(3):
+        dist.all_reduce(x)
+    torch.cuda.synchronize(device)
+    dist.barrier()
+    iters = 10
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(x)
+    torch.cuda.synchronize(device)
+    dt = (time.perf_counter() - t0) / iters
+    t = torch.tensor([dt], device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    algbw = count * 4 / t.item() / 1e9
+    return algbw * 2 * (world - 1) / world
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
+              file=sys.stderr)
+    distributed = world > 1
+    if not torch.cuda.is_available():
+        print("bench.py needs an MI355X (no GPU visible)", file=sys.stderr)
+        return 2
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if distributed:
+        dist.init_process_group(backend="nccl", device_id=device)
+
+    ttfr = first_gpu_result(device)
+
+    s = args.size
+    if not K.gemm_shape_supported(s, s, s):
+        raise SystemExit(f"--size {s} must be a multiple of 256")
+    a = torch.empty((s, s), dtype=torch.bfloat16, device=device)
+    b = torch.empty((s, s), dtype=torch.bfloat16, device=device)
+    c = torch.empty((s, s), dtype=torch.bfloat16, device=device)
+    K.fill_uniform_bf16(a, seed=1000 + rank)
+    K.fill_uniform_bf16(b, seed=2000 + rank)
+    K.gemm_bf16_nt(a, b, out=c)
+    max_rel_err = check_numerics(a, b, c)
+
+    for _ in range(args.warmup):
+        K.gemm_bf16_nt(a, b, out=c)
+    torch.cuda.synchronize(device)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        K.gemm_bf16_nt(a, b, out=c)
+    torch.cuda.synchronize(device)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+
+    per_gpu_tflops_local = 2.0 * s * s * s * args.steps / elapsed / 1e12
+    if distributed:
+        t = torch.tensor([elapsed, ttfr], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, ttfr = float(t[0].item()), float(t[1].item())
+        pg = torch.tensor([per_gpu_tflops_local], device=device, dtype=torch.float64)
+        gathered = [torch.zeros_like(pg) for _ in range(world)]
+        dist.all_gather(gathered, pg)
+        per_rank = [round(float(x.item()), 1) for x in gathered]
+    else:
+        per_rank = [round(per_gpu_tflops_local, 1)]
+    busbw = None
+    if distributed and not args.no_allreduce:
+        busbw = allreduce_probe(device, world, args.allreduce_mib)
+
+    total_flops = 2.0 * s * s * s * args.steps * world
+    value = total_flops / elapsed / 1e12
+    ms_per_step = elapsed / args.steps * 1e3
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "TFLOPS",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(value / BASELINE_VALUE, 3) if BASELINE_VALUE else None),
+            "dtype": "bf16",
+            "data": "synthetic (uniform [-1,1) bf16 operands generated on device)",
+            "config": {
+                "model": f"validator bf16 MFMA GEMM {s}x{s}x{s} (C=A*B^T, hand-written gfx950 kernel)",
+                "global_batch": world,
+                "seq_len": s,
+                "parallelism": f"dp{world}" if world > 1 else "single",
+                "m": s, "n": s, "k": s,
+                "kernel": "amdk8s_gemm_bf16_nt_256x256",
+            },
+            "tflops_per_gpu": round(value / world, 2),
+            "tflops_per_rank": per_rank,
+            "time_to_first_gpu_result_s": round(ttfr, 3),
+            "numerics_max_rel_err": max_rel_err,
+            "allreduce_busbw_gbps": (round(busbw, 2) if busbw is not None else None),
+            "device": torch.cuda.get_device_name(device),
+        }
+        print(json.dumps(out), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

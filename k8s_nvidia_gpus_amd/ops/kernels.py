@@ -1,0 +1,220 @@
+"""Python bindings for the hand-written gfx950 HIP kernels (``_lib/libamdk8s_kernels.so``).
+
+The library exposes a tiny C ABI (see ``csrc/*.hip``); we call it through ``ctypes`` with raw
+device pointers and the current torch stream, so the kernels run on torch tensors, inside torch
+streams and inside HIP-graph capture, without linking libtorch into the extension.
+
+``import torch`` happens before the library is loaded: torch has already mapped
+``libamdhip64.so.7`` and the extension's dependency on that soname binds to the same runtime.
+
+There is deliberately **no** silent fallback: on a machine with a GPU, a missing or unloadable
+library raises :class:`KernelLibraryError` (the validator must prove the native path ran).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+import torch
+
+from . import build as _build
+
+__all__ = [
+    "KernelLibraryError",
+    "library",
+    "library_path",
+    "gemm_bf16_nt",
+    "gemm_bf16",
+    "gemm_shape_supported",
+    "vector_add",
+    "vector_add_bandwidth",
+    "fill_uniform_bf16",
+    "gemm_sample_check",
+]
+
+GEMM_TILE_M = 256
+GEMM_TILE_N = 256
+GEMM_TILE_K = 64
+
+
+class KernelLibraryError(RuntimeError):
+    pass
+
+
+_lock = threading.Lock()
+_lib: Optional[ctypes.CDLL] = None
+
+
+def library_path() -> str:
+    return str(_build.KERNEL_LIB)
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    vp, ci, cl, cf, cu64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_ulonglong
+    lib.amdk8s_gemm_bf16_nt.argtypes = [vp, vp, vp, ci, ci, ci, ci, ci, ci, vp]
+    lib.amdk8s_gemm_bf16_nt.restype = ci
+    lib.amdk8s_gemm_bf16_nt_sample_check.argtypes = [vp, vp, vp, vp, ci, ci, ci, ci, vp]
+    lib.amdk8s_gemm_bf16_nt_sample_check.restype = ci
+    lib.amdk8s_vector_add_f32.argtypes = [vp, vp, vp, ci, vp]
+    lib.amdk8s_vector_add_f32.restype = ci
+    lib.amdk8s_vector_add_f32_bw.argtypes = [vp, vp, vp, cl, ci, vp]
+    lib.amdk8s_vector_add_f32_bw.restype = ci
+    lib.amdk8s_vector_add_blocks.argtypes = [ci]
+    lib.amdk8s_vector_add_blocks.restype = ci
+    lib.amdk8s_fill_uniform_bf16.argtypes = [vp, cl, cu64, cf, cf, vp]
+    lib.amdk8s_fill_uniform_bf16.restype = ci
+
+
+def library(build_if_missing: bool = True) -> ctypes.CDLL:
+    """Load (building first if needed and possible) the kernel library, once per process."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = _build.KERNEL_LIB
+        stale = (not path.exists()) or any(
+            s.stat().st_mtime > path.stat().st_mtime for s in _build.kernel_sources())
+        if stale and build_if_missing and _build.toolchain_available() \
+                and os.environ.get("AMDK8S_NO_BUILD") != "1":
+            _build.build_kernel_library()
+        if not path.exists():
+            raise KernelLibraryError(
+                f"{path} is missing; build it with `python -m k8s_nvidia_gpus_amd.ops.build kernels`")
+        try:
+            lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:  # pragma: no cover - depends on the host
+            raise KernelLibraryError(f"cannot load {path}: {e}") from e
+        _declare(lib)
+        _lib = lib
+        return lib
+
+
+def _stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise KernelLibraryError(f"{what} failed with hipError {rc}")
+
+
+def _require_gpu(t: torch.Tensor, name: str) -> None:
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must be a GPU tensor (got {t.device})")
+
+
+def gemm_shape_supported(m: int, n: int, k: int) -> bool:
+    return m > 0 and n > 0 and k > 0 and m % GEMM_TILE_M == 0 and n % GEMM_TILE_N == 0 \
+        and k % GEMM_TILE_K == 0
+
+
+def gemm_bf16_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``out = a @ b.T`` with the hand-written 256×256×64 MFMA kernel.
+
+    ``a``: [M, K] bf16, ``b``: [N, K] bf16 (nn.Linear weight layout), both row-major with unit
+    inner stride.  M and N must be multiples of 256 and K a multiple of 64 — use :func:`gemm_bf16`
+    for arbitrary shapes (it pads).
+    """
+    _require_gpu(a, "a")
+    _require_gpu(b, "b")
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        raise TypeError("gemm_bf16_nt expects bf16 operands")
+    if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[1]:
+        raise ValueError(f"shape mismatch: a {tuple(a.shape)} b {tuple(b.shape)}")
+    if a.stride(1) != 1 or b.stride(1) != 1:
+        raise ValueError("operands must have unit inner stride")
+    m, k = a.shape
+    n = b.shape[0]
+    if not gemm_shape_supported(m, n, k):
+        raise ValueError(f"gemm_bf16_nt needs M,N % 256 == 0 and K % 64 == 0 (got {m}x{n}x{k})")
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
+    elif out.shape != (m, n) or out.dtype != torch.bfloat16 or out.stride(1) != 1:
+        raise ValueError("bad out tensor")
+    lib = library()
+    rc = lib.amdk8s_gemm_bf16_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+                                 a.stride(0), b.stride(0), out.stride(0), _stream_handle(a.device))
+    _check(rc, "amdk8s_gemm_bf16_nt")
+    return out
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def gemm_bf16(a: torch.Tensor, b: torch.Tensor, *, b_layout: str = "nk") -> torch.Tensor:
+    """General ``a @ bᵀ`` (``b_layout='nk'``) or ``a @ b`` (``'kn'``) for any shape, via padding.
+
+    The MFMA kernel only runs whole 256×256×64 tiles, so ragged shapes are zero-padded (zeros in
+    K contribute nothing) and the result is sliced back.
+    """
+    if b_layout == "kn":
+        b = b.t()
+    elif b_layout != "nk":
+        raise ValueError("b_layout must be 'nk' or 'kn'")
+    m, k = a.shape
+    n = b.shape[0]
+    mp, np_, kp = _round_up(m, GEMM_TILE_M), _round_up(n, GEMM_TILE_N), _round_up(k, GEMM_TILE_K)
+    if (mp, np_, kp) == (m, n, k) and a.stride(1) == 1 and b.stride(1) == 1 \
+            and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0:
+        return gemm_bf16_nt(a, b)
+    ap = torch.zeros((mp, kp), dtype=torch.bfloat16, device=a.device)
+    ap[:m, :k] = a
+    bp = torch.zeros((np_, kp), dtype=torch.bfloat16, device=b.device)
+    bp[:n, :k] = b
+    return gemm_bf16_nt(ap, bp)[:m, :n]
+
+
+def gemm_sample_check(a: torch.Tensor, b: torch.Tensor, coords: torch.Tensor) -> torch.Tensor:
+    """fp32 on-device reference of ``(a @ b.T)[m, n]`` at ``coords`` ([S, 2] int32)."""
+    coords = coords.to(device=a.device, dtype=torch.int32).contiguous()
+    out = torch.empty(coords.shape[0], dtype=torch.float32, device=a.device)
+    rc = library().amdk8s_gemm_bf16_nt_sample_check(
+        a.data_ptr(), b.data_ptr(), coords.data_ptr(), out.data_ptr(), coords.shape[0], a.shape[1],
+        a.stride(0), b.stride(0), _stream_handle(a.device))
+    _check(rc, "amdk8s_gemm_bf16_nt_sample_check")
+    return out
+
+
+def vector_add(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 ``a + b`` with the reference-shaped kernel (256 threads, ⌈n/256⌉ blocks)."""
+    _require_gpu(a, "a")
+    if a.dtype != torch.float32 or b.dtype != torch.float32 or a.shape != b.shape:
+        raise ValueError("vector_add expects two fp32 tensors of the same shape")
+    a = a.contiguous()
+    b = b.contiguous()
+    if out is None:
+        out = torch.empty_like(a)
+    rc = library().amdk8s_vector_add_f32(a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(),
+                                         _stream_handle(a.device))
+    _check(rc, "amdk8s_vector_add_f32")
+    return out
+
+
+def vector_add_blocks(n: int) -> int:
+    return (n + 255) // 256
+
+
+def vector_add_bandwidth(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """Streaming (16 B/lane, grid-stride) fp32 add for bandwidth measurement."""
+    n = a.numel()
+    cus = torch.cuda.get_device_properties(a.device).multi_processor_count
+    rc = library().amdk8s_vector_add_f32_bw(a.data_ptr(), b.data_ptr(), out.data_ptr(), n, cus,
+                                            _stream_handle(a.device))
+    _check(rc, "amdk8s_vector_add_f32_bw")
+    return out
+
+
+def fill_uniform_bf16(t: torch.Tensor, seed: int, lo: float = -1.0, hi: float = 1.0) -> torch.Tensor:
+    """Fill a bf16 GPU tensor with counter-hash uniform values in [lo, hi) (on the device)."""
+    _require_gpu(t, "t")
+    if t.dtype != torch.bfloat16 or not t.is_contiguous():
+        raise ValueError("fill_uniform_bf16 expects a contiguous bf16 tensor")
+    rc = library().amdk8s_fill_uniform_bf16(t.data_ptr(), t.numel(), seed & (2 ** 64 - 1), lo, hi,
+                                            _stream_handle(t.device))
+    _check(rc, "amdk8s_fill_uniform_bf16")
+    return t

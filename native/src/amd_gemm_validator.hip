@@ -1,0 +1,211 @@
+// amd-gemm-validator — hand-written gfx950 bf16 MFMA GEMM load + numerics check.
+//
+// Plays the role NVIDIA's dcgmproftester tensor-core load plays for the reference's operator
+// (BASELINE.json configs 3/4): it drives the in-tree 256×256 MFMA kernel
+// (k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950.hip) on every device the pod was allocated, in
+// parallel (one host thread per device), on random [-1,1) bf16 data (never zeros — zero operands
+// inflate MFMA clocks), checks a sample of outputs against an fp32 on-device reference and reports
+// TFLOPS per GPU and in aggregate.  Output ends with "Test PASSED" / "Done" like amd-vectoradd.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "amdk8s_native.h"
+
+namespace {
+
+struct Options {
+  int m = 8192, n = 8192, k = 8192;
+  int iters = 50, warmup = 10;
+  int device = -1;  // -1 = every visible device
+  int samples = 2048;
+  bool json = false;
+  unsigned long long seed = 42;
+};
+
+struct Result {
+  int device = 0;
+  std::string name, arch;
+  int cus = 0;
+  double ms_per_iter = 0, tflops = 0, max_rel_err = 0;
+  int bad = 0;
+  bool ok = false;
+};
+
+std::atomic<int> g_ready{0};
+std::atomic<bool> g_go{false};
+
+float bf16_to_float(uint16_t b) {
+  uint32_t u = (uint32_t)b << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+void run(int dev, const Options& o, int nthreads, Result* r) {
+  AMDK8S_HIP_CHECK(hipSetDevice(dev));
+  hipDeviceProp_t prop;
+  AMDK8S_HIP_CHECK(hipGetDeviceProperties(&prop, dev));
+  r->device = dev;
+  r->name = prop.name;
+  r->arch = prop.gcnArchName;
+  r->cus = prop.multiProcessorCount;
+  const size_t M = o.m, N = o.n, K = o.k;
+  void *A, *B, *C;
+  AMDK8S_HIP_CHECK(hipMalloc(&A, M * K * 2));
+  AMDK8S_HIP_CHECK(hipMalloc(&B, N * K * 2));
+  AMDK8S_HIP_CHECK(hipMalloc(&C, M * N * 2));
+  hipStream_t s;
+  AMDK8S_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  AMDK8S_HIP_CHECK((hipError_t)amdk8s_fill_uniform_bf16(A, (long)(M * K), o.seed * 2 + 1, -1.f, 1.f, s));
+  AMDK8S_HIP_CHECK((hipError_t)amdk8s_fill_uniform_bf16(B, (long)(N * K), o.seed * 2 + 2, -1.f, 1.f, s));
+  AMDK8S_HIP_CHECK(hipMemsetAsync(C, 0xFF, M * N * 2, s));  // poison: NaN pattern
+
+  // numerics: sampled fp32 reference
+  std::vector<int> coords(2 * o.samples);
+  std::mt19937 rng(7 + dev);
+  for (int i = 0; i < o.samples; ++i) {
+    coords[2 * i] = (int)(rng() % M);
+    coords[2 * i + 1] = (int)(rng() % N);
+  }
+  int* dcoords;
+  float* dref;
+  AMDK8S_HIP_CHECK(hipMalloc(&dcoords, coords.size() * sizeof(int)));
+  AMDK8S_HIP_CHECK(hipMalloc(&dref, o.samples * sizeof(float)));
+  AMDK8S_HIP_CHECK(hipMemcpyAsync(dcoords, coords.data(), coords.size() * sizeof(int),
+                                  hipMemcpyHostToDevice, s));
+  int rc = amdk8s_gemm_bf16_nt(A, B, C, o.m, o.n, o.k, o.k, o.k, o.n, s);
+  if (rc != 0) {
+    std::fprintf(stderr, "device %d: GEMM launch rejected (error %d): shape %dx%dx%d must be "
+                 "multiples of 256x256x64\n", dev, rc, o.m, o.n, o.k);
+    return;
+  }
+  AMDK8S_HIP_CHECK((hipError_t)amdk8s_gemm_bf16_nt_sample_check(A, B, dcoords, dref, o.samples,
+                                                                o.k, o.k, o.k, s));
+  std::vector<float> ref(o.samples);
+  AMDK8S_HIP_CHECK(hipMemcpyAsync(ref.data(), dref, o.samples * sizeof(float),
+                                  hipMemcpyDeviceToHost, s));
+  std::vector<uint16_t> got(o.samples);
+  for (int i = 0; i < o.samples; ++i) {
+    const size_t off = (size_t)coords[2 * i] * N + coords[2 * i + 1];
+    AMDK8S_HIP_CHECK(hipMemcpyAsync(&got[i], (char*)C + off * 2, 2, hipMemcpyDeviceToHost, s));
+  }
+  AMDK8S_HIP_CHECK(hipStreamSynchronize(s));
+  double worst = 0;
+  int bad = 0;
+  for (int i = 0; i < o.samples; ++i) {
+    const double g = bf16_to_float(got[i]);
+    const double e = ref[i];
+    const double err = std::fabs(g - e);
+    const double tol = 0.01 * std::fabs(e) + 0.02 * std::sqrt((double)K) / 16.0;
+    if (!(err <= tol)) ++bad;
+    worst = std::max(worst, err / (std::fabs(e) + 1.0));
+  }
+  r->bad = bad;
+  r->max_rel_err = worst;
+
+  // timing: all device threads start the timed loop together
+  for (int i = 0; i < o.warmup; ++i) amdk8s_gemm_bf16_nt(A, B, C, o.m, o.n, o.k, o.k, o.k, o.n, s);
+  AMDK8S_HIP_CHECK(hipStreamSynchronize(s));
+  g_ready.fetch_add(1);
+  while (g_ready.load() < nthreads) std::this_thread::yield();
+  hipEvent_t e0, e1;
+  AMDK8S_HIP_CHECK(hipEventCreate(&e0));
+  AMDK8S_HIP_CHECK(hipEventCreate(&e1));
+  AMDK8S_HIP_CHECK(hipEventRecord(e0, s));
+  for (int i = 0; i < o.iters; ++i) amdk8s_gemm_bf16_nt(A, B, C, o.m, o.n, o.k, o.k, o.k, o.n, s);
+  AMDK8S_HIP_CHECK(hipEventRecord(e1, s));
+  AMDK8S_HIP_CHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  AMDK8S_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  r->ms_per_iter = ms / o.iters;
+  r->tflops = 2.0 * M * N * K / (r->ms_per_iter * 1e-3) / 1e12;
+  r->ok = (bad == 0);
+  hipFree(A);
+  hipFree(B);
+  hipFree(C);
+  hipFree(dcoords);
+  hipFree(dref);
+  hipStreamDestroy(s);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Options o;
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto next = [&]() -> const char* {
+      if (i + 1 >= argc) {
+        std::fprintf(stderr, "missing value for %s\n", a.c_str());
+        std::exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--m") o.m = std::atoi(next());
+    else if (a == "--n") o.n = std::atoi(next());
+    else if (a == "--k") o.k = std::atoi(next());
+    else if (a == "--size") o.m = o.n = o.k = std::atoi(next());
+    else if (a == "--iters") o.iters = std::atoi(next());
+    else if (a == "--warmup") o.warmup = std::atoi(next());
+    else if (a == "--device") o.device = std::atoi(next());
+    else if (a == "--samples") o.samples = std::atoi(next());
+    else if (a == "--seed") o.seed = std::strtoull(next(), nullptr, 10);
+    else if (a == "--json") o.json = true;
+    else {
+      std::printf("usage: amd-gemm-validator [--size S | --m M --n N --k K] [--iters I] "
+                  "[--warmup W] [--device D] [--samples S] [--json]\n");
+      return a == "-h" || a == "--help" ? 0 : 2;
+    }
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    std::fprintf(stderr, "No HIP device visible to this container\n");
+    return 1;
+  }
+  std::vector<int> devs;
+  for (int d = 0; d < ndev; ++d)
+    if (o.device < 0 || o.device == d) devs.push_back(d);
+  if (devs.empty()) {
+    std::fprintf(stderr, "device %d not visible (%d devices)\n", o.device, ndev);
+    return 1;
+  }
+  std::printf("[bf16 MFMA GEMM %dx%dx%d (C = A*B^T), %zu device(s), %d iters]\n", o.m, o.n, o.k,
+              devs.size(), o.iters);
+  std::vector<Result> res(devs.size());
+  std::vector<std::thread> th;
+  for (size_t i = 0; i < devs.size(); ++i)
+    th.emplace_back(run, devs[i], std::cref(o), (int)devs.size(), &res[i]);
+  for (auto& t : th) t.join();
+  bool ok = true;
+  double agg = 0;
+  for (auto& r : res) {
+    std::printf("device %d (%s, %s, %d CUs): %.3f ms/iter, %.1f TFLOPS, sampled max rel err %.2e, "
+                "%d/%d out of tolerance\n", r.device, r.name.c_str(), r.arch.c_str(), r.cus,
+                r.ms_per_iter, r.tflops, r.max_rel_err, r.bad, o.samples);
+    agg += r.tflops;
+    ok = ok && r.ok;
+    if (o.json)
+      std::printf("{\"check\": \"gemm_bf16\", \"device\": %d, \"arch\": \"%s\", \"m\": %d, \"n\": %d, "
+                  "\"k\": %d, \"ms_per_iter\": %.4f, \"tflops\": %.2f, \"bad_samples\": %d, "
+                  "\"passed\": %s}\n", r.device, r.arch.c_str(), o.m, o.n, o.k, r.ms_per_iter,
+                  r.tflops, r.bad, r.ok ? "true" : "false");
+  }
+  std::printf("aggregate: %.1f TFLOPS over %zu device(s) (%.1f TFLOPS/GPU)\n", agg, devs.size(),
+              agg / devs.size());
+  if (!ok) {
+    std::printf("Test FAILED\n");
+    return 1;
+  }
+  std::printf("Test PASSED\nDone\n");
+  return 0;
+}

@@ -1,0 +1,74 @@
+"""CPU-side checks that every native artefact builds for gfx950 and exports its C ABI."""
+import json
+import os
+import subprocess
+
+import pytest
+
+from k8s_nvidia_gpus_amd.ops import build as B
+
+pytestmark = pytest.mark.skipif(not B.toolchain_available(), reason="hipcc not available")
+
+
+@pytest.fixture(scope="module")
+def built():
+    B.build_all(jobs=4)
+    return True
+
+
+def _nm(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", str(path)], capture_output=True, text=True,
+                         check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_kernel_library_exports(built):
+    syms = _nm(B.KERNEL_LIB)
+    for s in ["amdk8s_gemm_bf16_nt", "amdk8s_gemm_bf16_nt_sample_check", "amdk8s_vector_add_f32",
+              "amdk8s_vector_add_f32_bw", "amdk8s_fill_uniform_bf16", "amdk8s_vector_add_blocks"]:
+        assert s in syms, s
+
+
+def test_kernel_library_targets_gfx950_only(built):
+    blob = B.KERNEL_LIB.read_bytes()
+    assert b"gfx950" in blob
+    for other in (b"gfx942", b"gfx90a", b"gfx1100", b"sm_"):
+        assert b"amdgcn-amd-amdhsa--" + other not in blob
+
+
+def test_native_tools_built(built):
+    for t in B.NATIVE_TARGETS:
+        p = B.NATIVE_BIN / t.name
+        assert p.exists() and os.access(p, os.X_OK), p
+
+
+def test_gemm_kernel_resource_budget(tmp_path):
+    """The main loop must fit 2 waves/SIMD (≤256 VGPRs), never spill, and stay within 160 KiB LDS."""
+    src = B.CSRC_DIR / "gemm_bf16_gfx950.hip"
+    r = subprocess.run([B.HIPCC, *B.HIP_FLAGS, "-c", str(src), "-o", str(tmp_path / "g.o"),
+                        "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    text = r.stderr
+    block = text.split("Function Name: amdk8s_gemm_bf16_nt_256x256")[1].split("Function Name:")[0]
+
+    def val(key):
+        line = [ln for ln in block.splitlines() if key in ln][0]
+        return int(line.split(key)[1].split()[0])
+
+    assert val("VGPRs:") <= 256
+    assert val("VGPRs Spill:") == 0
+    assert val("ScratchSize [bytes/lane]:") == 0
+    assert val("LDS Size [bytes/block]:") <= 160 * 1024
+    assert val("Occupancy [waves/SIMD]:") >= 2
+
+
+def test_kfd_probe_help(built):
+    r = subprocess.run([str(B.NATIVE_BIN / "kfd-probe"), "--help"], capture_output=True, text=True)
+    assert r.returncode == 0 and "usage" in r.stdout
+
+
+def test_kfd_probe_reports_missing_topology(built, tmp_path):
+    r = subprocess.run([str(B.NATIVE_BIN / "kfd-probe"), "--sysfs-root", str(tmp_path / "none"),
+                        "--dev-root", str(tmp_path)], capture_output=True, text=True)
+    assert r.returncode == 1
+    assert "not ready" in r.stderr

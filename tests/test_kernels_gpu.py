@@ -1,0 +1,134 @@
+"""Numerics of the hand-written gfx950 kernels against plain PyTorch fp32 references (MI355X)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    from k8s_nvidia_gpus_amd.ops import kernels
+
+    kernels.library()  # must load the in-tree .so — no fallback
+    return kernels
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda", 0)
+
+
+def _rand_bf16(shape, gen, dev):
+    return (torch.rand(shape, generator=gen, device=dev) * 2 - 1).to(torch.bfloat16)
+
+
+def test_vector_add_reference_shape(K, dev):
+    n = 50000
+    a = torch.rand(n, device=dev)
+    b = torch.rand(n, device=dev)
+    c = K.vector_add(a, b)
+    assert K.vector_add_blocks(n) == 196
+    torch.testing.assert_close(c, a + b, rtol=0, atol=0)
+
+
+def test_vector_add_bandwidth_form(K, dev):
+    n = 1 << 22
+    a = torch.rand(n, device=dev)
+    b = torch.rand(n, device=dev)
+    c = torch.empty_like(a)
+    K.vector_add_bandwidth(a, b, c)
+    torch.testing.assert_close(c, a + b, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("m,n,k", [
+    (256, 256, 64),      # one K-tile: prologue-only path
+    (256, 256, 128),     # two K-tiles: tail-only path
+    (256, 512, 192),     # three K-tiles: one steady tile
+    (512, 768, 320),     # rectangular, odd tile counts
+    (768, 256, 1024),
+    (1024, 1024, 4096),  # long K: steady-state vmcnt(8) pipeline
+    (2304, 1280, 576),   # nwg % 8 != 0: bijective XCD remap + ragged GROUP_M tail
+])
+def test_gemm_bf16_nt_matches_fp32(K, dev, m, n, k):
+    g = torch.Generator(device=dev).manual_seed(m * 131 + n * 7 + k)
+    a = _rand_bf16((m, k), g, dev)
+    b = _rand_bf16((n, k), g, dev)
+    c = K.gemm_bf16_nt(a, b)
+    ref = a.float() @ b.float().t()
+    # bf16 output rounding (2^-8 relative) + fp32 accumulation-order differences
+    torch.testing.assert_close(c.float(), ref, rtol=1e-2, atol=1e-2 * (k ** 0.5) / 8)
+
+
+def test_gemm_identity_asymmetric(K, dev):
+    """A = I with an asymmetric B must return exactly Bᵀ: catches any row/col swap in C."""
+    s = 256
+    a = torch.eye(s, device=dev, dtype=torch.bfloat16)
+    i = torch.arange(s, device=dev, dtype=torch.float32)
+    b = ((i[:, None] * 3 + i[None, :] * 0.5) / 64).to(torch.bfloat16)  # asymmetric, exact in bf16
+    c = K.gemm_bf16_nt(a, b)
+    assert torch.equal(c, b.t().contiguous())
+    c2 = K.gemm_bf16_nt(b, a)  # = B · Iᵀ = B
+    assert torch.equal(c2, b)
+
+
+def test_gemm_strided_leading_dims(K, dev):
+    g = torch.Generator(device=dev).manual_seed(3)
+    big_a = _rand_bf16((512, 640), g, dev)
+    big_b = _rand_bf16((256, 704), g, dev)
+    a = big_a[:, 64:576]   # lda = 640, K = 512
+    b = big_b[:, 128:640]  # ldb = 704
+    out = torch.empty((512, 384), device=dev, dtype=torch.bfloat16)[:, :256]
+    K.gemm_bf16_nt(a, b, out=out)
+    ref = a.float() @ b.float().t()
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=3e-2)
+
+
+def test_gemm_deterministic(K, dev):
+    g = torch.Generator(device=dev).manual_seed(11)
+    a = _rand_bf16((1024, 2048), g, dev)
+    b = _rand_bf16((1024, 2048), g, dev)
+    c1 = K.gemm_bf16_nt(a, b).clone()
+    for _ in range(5):
+        assert torch.equal(K.gemm_bf16_nt(a, b), c1)
+
+
+def test_gemm_padded_general_shapes(K, dev):
+    g = torch.Generator(device=dev).manual_seed(5)
+    a = _rand_bf16((300, 100), g, dev)
+    w = _rand_bf16((77, 100), g, dev)
+    y = K.gemm_bf16(a, w)
+    torch.testing.assert_close(y.float(), a.float() @ w.float().t(), rtol=1e-2, atol=2e-2)
+    bkn = _rand_bf16((100, 130), g, dev)
+    y2 = K.gemm_bf16(a, bkn, b_layout="kn")
+    torch.testing.assert_close(y2.float(), a.float() @ bkn.float(), rtol=1e-2, atol=2e-2)
+
+
+def test_gemm_rejects_bad_shapes(K, dev):
+    a = torch.zeros((200, 64), device=dev, dtype=torch.bfloat16)
+    b = torch.zeros((256, 64), device=dev, dtype=torch.bfloat16)
+    with pytest.raises(ValueError):
+        K.gemm_bf16_nt(a, b)
+
+
+def test_sample_check_matches_torch(K, dev):
+    g = torch.Generator(device=dev).manual_seed(9)
+    a = _rand_bf16((512, 1024), g, dev)
+    b = _rand_bf16((256, 1024), g, dev)
+    coords = torch.tensor([[0, 0], [511, 255], [17, 200], [300, 3]], dtype=torch.int32)
+    ref = K.gemm_sample_check(a, b, coords)
+    full = a.float() @ b.float().t()
+    exp = full[coords[:, 0].long(), coords[:, 1].long()]
+    torch.testing.assert_close(ref, exp, rtol=1e-4, atol=1e-3)
+
+
+def test_fill_uniform_bf16(K, dev):
+    t = torch.empty(1 << 20, device=dev, dtype=torch.bfloat16)
+    K.fill_uniform_bf16(t, seed=123)
+    f = t.float()
+    assert f.min().item() >= -1.0 and f.max().item() <= 1.0
+    assert abs(f.mean().item()) < 0.01
+    assert 0.3 < f.std().item() < 0.7  # uniform[-1,1) std = 0.577
+    t2 = torch.empty_like(t)
+    K.fill_uniform_bf16(t2, seed=123)
+    assert torch.equal(t, t2)
