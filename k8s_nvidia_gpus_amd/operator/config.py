@@ -1,0 +1,121 @@
+"""Operator configuration: one YAML document shared by every component.
+
+The reference configures its GPU stack through Helm values of an external chart (reference
+cluster-config/apps/gpu-operator/helmrelease.yaml:17-29) plus per-pod env.  Here the whole operator
+reads one in-repo file (ConfigMap ``amd-gpu-operator-config`` → ``/etc/amd-gpu-operator/operator.yaml``,
+cluster-config/apps/amd-gpu-operator/config.yaml); unknown keys are rejected so a typo cannot
+silently fall back to a default.
+"""
+from __future__ import annotations
+
+import copy
+from dataclasses import dataclass, field
+from typing import Any, Dict, Optional
+
+import yaml
+
+DEFAULTS: Dict[str, Any] = {
+    "resourceName": "amd.com/gpu",
+    "runtimeClass": "amd",
+    "minGfxTargetVersion": 90500,
+    "expectedGpusPerNode": 8,
+    "deviceIdStrategy": "uuid",
+    "allocation": {
+        "mode": "deviceSpecs",       # deviceSpecs | cdi
+        "cardNodes": False,          # also expose /dev/dri/card<N> (not needed by ROCm compute)
+        "preferXgmiLocality": True,
+    },
+    "health": {
+        "intervalSeconds": 10,
+        "eccUncorrectableThreshold": 1,
+    },
+    "partition": {
+        "compute": "SPX",
+        "memory": "NPS1",
+        "drainTimeoutSeconds": 600,
+    },
+    "exporter": {
+        "port": 9400,
+        "intervalSeconds": 5,
+    },
+    "validator": {
+        "vectorAdd": True,
+        "gemm": True,
+        "gemmSize": 8192,
+        "gemmMinTflops": 900,
+        "rccl": True,
+        "rcclMinBusbwGBps": 100,
+        "pluginTest": True,
+    },
+}
+
+COMPUTE_PARTITIONS = ("SPX", "DPX", "QPX", "CPX")
+MEMORY_PARTITIONS = ("NPS1", "NPS2", "NPS4")
+
+
+class ConfigError(ValueError):
+    pass
+
+
+def _merge(base: Dict[str, Any], over: Dict[str, Any], path: str = "") -> Dict[str, Any]:
+    out = copy.deepcopy(base)
+    for k, v in (over or {}).items():
+        where = f"{path}.{k}" if path else k
+        if k not in base:
+            raise ConfigError(f"unknown operator config key '{where}'")
+        if isinstance(base[k], dict):
+            if not isinstance(v, dict):
+                raise ConfigError(f"'{where}' must be a mapping")
+            out[k] = _merge(base[k], v, where)
+        else:
+            out[k] = v
+    return out
+
+
+@dataclass
+class OperatorConfig:
+    raw: Dict[str, Any] = field(default_factory=lambda: copy.deepcopy(DEFAULTS))
+
+    def __getitem__(self, key: str) -> Any:
+        return self.raw[key]
+
+    @property
+    def resource_name(self) -> str:
+        return self.raw["resourceName"]
+
+    @property
+    def min_gfx(self) -> int:
+        return int(self.raw["minGfxTargetVersion"])
+
+    def section(self, name: str) -> Dict[str, Any]:
+        return self.raw[name]
+
+    def validate(self) -> "OperatorConfig":
+        r = self.raw
+        if "/" not in r["resourceName"]:
+            raise ConfigError("resourceName must be vendor-qualified, e.g. amd.com/gpu")
+        if r["deviceIdStrategy"] not in ("uuid", "index"):
+            raise ConfigError("deviceIdStrategy must be 'uuid' or 'index'")
+        if r["allocation"]["mode"] not in ("deviceSpecs", "cdi"):
+            raise ConfigError("allocation.mode must be 'deviceSpecs' or 'cdi'")
+        if r["partition"]["compute"] not in COMPUTE_PARTITIONS:
+            raise ConfigError(f"partition.compute must be one of {COMPUTE_PARTITIONS}")
+        if r["partition"]["memory"] not in MEMORY_PARTITIONS:
+            raise ConfigError(f"partition.memory must be one of {MEMORY_PARTITIONS}")
+        if not 1 <= int(r["exporter"]["port"]) <= 65535:
+            raise ConfigError("exporter.port out of range")
+        if int(r["validator"]["gemmSize"]) % 256:
+            raise ConfigError("validator.gemmSize must be a multiple of 256 (MFMA block tile)")
+        return self
+
+
+def load_config(path: Optional[str] = None, text: Optional[str] = None) -> OperatorConfig:
+    if text is None and path:
+        with open(path) as f:
+            text = f.read()
+    data = yaml.safe_load(text) if text else {}
+    if data is None:
+        data = {}
+    if not isinstance(data, dict):
+        raise ConfigError("operator config must be a YAML mapping")
+    return OperatorConfig(_merge(DEFAULTS, data)).validate()

@@ -4,8 +4,10 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-if REPO not in sys.path:
-    sys.path.insert(0, REPO)
+TESTS = os.path.dirname(os.path.abspath(__file__))
+for p in (REPO, TESTS):
+    if p not in sys.path:
+        sys.path.insert(0, p)
 
 
 def pytest_configure(config):
