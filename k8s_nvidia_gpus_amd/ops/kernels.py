@@ -55,6 +55,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     vp, ci, cl, cf, cu64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_ulonglong
     lib.amdk8s_gemm_bf16_nt.argtypes = [vp, vp, vp, ci, ci, ci, ci, ci, ci, vp]
     lib.amdk8s_gemm_bf16_nt.restype = ci
+    lib.amdk8s_gemm_bf16_nt_w4.argtypes = [vp, vp, vp, ci, ci, ci, ci, ci, ci, vp]
+    lib.amdk8s_gemm_bf16_nt_w4.restype = ci
     lib.amdk8s_gemm_bf16_nt_sample_check.argtypes = [vp, vp, vp, vp, ci, ci, ci, ci, vp]
     lib.amdk8s_gemm_bf16_nt_sample_check.restype = ci
     lib.amdk8s_vector_add_f32.argtypes = [vp, vp, vp, ci, vp]
@@ -112,8 +114,25 @@ def gemm_shape_supported(m: int, n: int, k: int) -> bool:
         and k % GEMM_TILE_K == 0
 
 
-def gemm_bf16_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+GEMM_VARIANTS = ("auto", "w8", "w4")
+DEFAULT_GEMM_VARIANT = os.environ.get("AMDK8S_GEMM_VARIANT", "auto")
+# Operand footprint above which the 8-wave schedule wins (docs/gemm_tuning.md): w4 keeps one K-tile
+# of LDS-DMA lead, enough while A+B are served from the 256 MiB Infinity Cache, not once the DMA
+# pays HBM latency; w8's two waves per SIMD hide that latency.
+W4_MAX_OPERAND_BYTES = 192 << 20
+
+
+def pick_gemm_variant(m: int, n: int, k: int) -> str:
+    return "w4" if (m + n) * k * 2 <= W4_MAX_OPERAND_BYTES else "w8"
+
+
+def gemm_bf16_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 variant: Optional[str] = None) -> torch.Tensor:
     """``out = a @ b.T`` with the hand-written 256×256×64 MFMA kernel.
+
+    ``variant``: ``"w8"`` — 512 threads, 8 waves of 128×64 (gemm_bf16_gfx950.hip);
+    ``"w4"`` — 256 threads, one wave per SIMD owning 128×128 (gemm_bf16_gfx950_w4.hip);
+    ``"auto"`` (default) — :func:`pick_gemm_variant` by operand footprint.
 
     ``a``: [M, K] bf16, ``b``: [N, K] bf16 (nn.Linear weight layout), both row-major with unit
     inner stride.  M and N must be multiples of 256 and K a multiple of 64 — use :func:`gemm_bf16`
@@ -136,9 +155,15 @@ def gemm_bf16_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] =
     elif out.shape != (m, n) or out.dtype != torch.bfloat16 or out.stride(1) != 1:
         raise ValueError("bad out tensor")
     lib = library()
-    rc = lib.amdk8s_gemm_bf16_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
-                                 a.stride(0), b.stride(0), out.stride(0), _stream_handle(a.device))
-    _check(rc, "amdk8s_gemm_bf16_nt")
+    variant = variant or DEFAULT_GEMM_VARIANT
+    if variant not in GEMM_VARIANTS:
+        raise ValueError(f"unknown GEMM variant {variant!r} (have {GEMM_VARIANTS})")
+    if variant == "auto":
+        variant = pick_gemm_variant(m, n, k)
+    fn = {"w8": lib.amdk8s_gemm_bf16_nt, "w4": lib.amdk8s_gemm_bf16_nt_w4}[variant]
+    rc = fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+            a.stride(0), b.stride(0), out.stride(0), _stream_handle(a.device))
+    _check(rc, f"amdk8s_gemm_bf16_nt[{variant}]")
     return out
 
 

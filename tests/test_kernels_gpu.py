@@ -41,6 +41,7 @@ def test_vector_add_bandwidth_form(K, dev):
     torch.testing.assert_close(c, a + b, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("variant", ["w8", "w4", "auto"])
 @pytest.mark.parametrize("m,n,k", [
     (256, 256, 64),      # one K-tile: prologue-only path
     (256, 256, 128),     # two K-tiles: tail-only path
@@ -50,47 +51,58 @@ def test_vector_add_bandwidth_form(K, dev):
     (1024, 1024, 4096),  # long K: steady-state vmcnt(8) pipeline
     (2304, 1280, 576),   # nwg % 8 != 0: bijective XCD remap + ragged GROUP_M tail
 ])
-def test_gemm_bf16_nt_matches_fp32(K, dev, m, n, k):
+def test_gemm_bf16_nt_matches_fp32(K, dev, m, n, k, variant):
     g = torch.Generator(device=dev).manual_seed(m * 131 + n * 7 + k)
     a = _rand_bf16((m, k), g, dev)
     b = _rand_bf16((n, k), g, dev)
-    c = K.gemm_bf16_nt(a, b)
+    c = K.gemm_bf16_nt(a, b, variant=variant)
     ref = a.float() @ b.float().t()
     # bf16 output rounding (2^-8 relative) + fp32 accumulation-order differences
     torch.testing.assert_close(c.float(), ref, rtol=1e-2, atol=1e-2 * (k ** 0.5) / 8)
 
 
-def test_gemm_identity_asymmetric(K, dev):
+@pytest.mark.parametrize("variant", ["w8", "w4", "auto"])
+def test_gemm_identity_asymmetric(K, dev, variant):
     """A = I with an asymmetric B must return exactly Bᵀ: catches any row/col swap in C."""
     s = 256
     a = torch.eye(s, device=dev, dtype=torch.bfloat16)
     i = torch.arange(s, device=dev, dtype=torch.float32)
     b = ((i[:, None] * 3 + i[None, :] * 0.5) / 64).to(torch.bfloat16)  # asymmetric, exact in bf16
-    c = K.gemm_bf16_nt(a, b)
+    c = K.gemm_bf16_nt(a, b, variant=variant)
     assert torch.equal(c, b.t().contiguous())
-    c2 = K.gemm_bf16_nt(b, a)  # = B · Iᵀ = B
+    c2 = K.gemm_bf16_nt(b, a, variant=variant)  # = B · Iᵀ = B
     assert torch.equal(c2, b)
 
 
-def test_gemm_strided_leading_dims(K, dev):
+@pytest.mark.parametrize("variant", ["w8", "w4", "auto"])
+def test_gemm_strided_leading_dims(K, dev, variant):
     g = torch.Generator(device=dev).manual_seed(3)
     big_a = _rand_bf16((512, 640), g, dev)
     big_b = _rand_bf16((256, 704), g, dev)
     a = big_a[:, 64:576]   # lda = 640, K = 512
     b = big_b[:, 128:640]  # ldb = 704
     out = torch.empty((512, 384), device=dev, dtype=torch.bfloat16)[:, :256]
-    K.gemm_bf16_nt(a, b, out=out)
+    K.gemm_bf16_nt(a, b, out=out, variant=variant)
     ref = a.float() @ b.float().t()
     torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=3e-2)
 
 
-def test_gemm_deterministic(K, dev):
+@pytest.mark.parametrize("variant", ["w8", "w4", "auto"])
+def test_gemm_deterministic(K, dev, variant):
     g = torch.Generator(device=dev).manual_seed(11)
     a = _rand_bf16((1024, 2048), g, dev)
     b = _rand_bf16((1024, 2048), g, dev)
-    c1 = K.gemm_bf16_nt(a, b).clone()
+    c1 = K.gemm_bf16_nt(a, b, variant=variant).clone()
     for _ in range(5):
-        assert torch.equal(K.gemm_bf16_nt(a, b), c1)
+        assert torch.equal(K.gemm_bf16_nt(a, b, variant=variant), c1)
+
+
+def test_gemm_variants_agree_bitwise_at_8192(K, dev):
+    """Both schedules accumulate each output in the same K order → identical bits."""
+    g = torch.Generator(device=dev).manual_seed(21)
+    a = _rand_bf16((2048, 8192), g, dev)
+    b = _rand_bf16((2048, 8192), g, dev)
+    assert torch.equal(K.gemm_bf16_nt(a, b, variant="w8"), K.gemm_bf16_nt(a, b, variant="w4"))
 
 
 def test_gemm_padded_general_shapes(K, dev):

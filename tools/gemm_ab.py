@@ -39,7 +39,8 @@ def main():
         K.fill_uniform_bf16(b, 12)
         c = torch.empty((s, s), dtype=torch.bfloat16, device=dev)
         arms = {
-            "amdk8s": lambda: K.gemm_bf16_nt(a, b, out=c),
+            "amdk8s w8": lambda: K.gemm_bf16_nt(a, b, out=c, variant="w8"),
+            "amdk8s w4": lambda: K.gemm_bf16_nt(a, b, out=c, variant="w4"),
             "torch.matmul(hipBLASLt)": lambda: torch.matmul(a, b.t(), out=c),
         }
         for fn in arms.values():
@@ -54,9 +55,10 @@ def main():
             print(f"{s}^3 {k:28s} median {med:.4f} ms ({flop / med / 1e9:.1f} TFLOPS)  "
                   f"min {mn:.4f} ms ({flop / mn / 1e9:.1f} TFLOPS)")
         ref = torch.matmul(a, b.t())
-        K.gemm_bf16_nt(a, b, out=c)
-        err = (c.float() - ref.float()).abs().max().item()
-        print(f"{s}^3 max |amdk8s - hipBLASLt| = {err:.4e}")
+        for v in ("w8", "w4"):
+            K.gemm_bf16_nt(a, b, out=c, variant=v)
+            err = (c.float() - ref.float()).abs().max().item()
+            print(f"{s}^3 max |amdk8s {v} - hipBLASLt| = {err:.4e}")
         sys.stdout.flush()
 
 

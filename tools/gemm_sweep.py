@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of GEMM arms over (M, N, K) shapes in one process (random [-1,1) bf16 data).
+
+usage: gemm_sweep.py --shapes 4096x4096x4096 8192x8192x4096 ... [--arms w8 w4 blt] [--rounds 5]
+"""
+import argparse
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, ".")
+from k8s_nvidia_gpus_amd.ops import kernels as K  # noqa: E402
+
+
+def timed(fn, iters):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", nargs="+", default=["8192x8192x8192"])
+    ap.add_argument("--arms", nargs="+", default=["w8", "w4", "blt"])
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--min-ms", type=float, default=20.0, help="time per round per arm")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    for shp in args.shapes:
+        m, n, k = (int(x) for x in shp.split("x"))
+        a = torch.empty((m, k), dtype=torch.bfloat16, device=dev)
+        b = torch.empty((n, k), dtype=torch.bfloat16, device=dev)
+        K.fill_uniform_bf16(a, 11)
+        K.fill_uniform_bf16(b, 12)
+        c = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
+        arms = {}
+        for arm in args.arms:
+            if arm == "blt":
+                arms[arm] = lambda: torch.matmul(a, b.t(), out=c)
+            else:
+                arms[arm] = (lambda v: (lambda: K.gemm_bf16_nt(a, b, out=c, variant=v)))(arm)
+        est = {}
+        for name, fn in arms.items():
+            timed(fn, 3)
+            est[name] = max(1, int(args.min_ms / max(timed(fn, 3), 1e-3)))
+        res = {name: [] for name in arms}
+        for _ in range(args.rounds):
+            for name, fn in arms.items():
+                res[name].append(timed(fn, est[name]))
+        flop = 2.0 * m * n * k
+        line = [f"{shp:>18s}"]
+        for name, v in res.items():
+            med = statistics.median(v)
+            line.append(f"{name} {flop / med / 1e9:7.1f}")
+        print("  ".join(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
