@@ -1,0 +1,126 @@
+"""Node labeller (SURVEY.md §2.2 X4 — the GPU-Feature-Discovery / NFD role).
+
+The reference relies on the GPU operator's implicit GFD/NFD labels; its heterogeneous GTX 1060 +
+1070 node is why its SD15 Deployment carries an (optional) GPU-model nodeSelector (reference
+sd15-api/deployment.yaml:17-18).  Here every MI355X node gets labels derived from the KFD / DRM
+sysfs topology, so workloads select on product, architecture, partition mode or memory:
+
+    amd.com/gpu.present=true           amd.com/gpu.product=MI355X       amd.com/gpu.family=gfx950
+    amd.com/gpu.count=8                amd.com/gpu.asic-count=8         amd.com/gpu.cu-count=256
+    amd.com/gpu.vram=288G              amd.com/gpu.compute-partition=SPX
+    amd.com/gpu.memory-partition=NPS1  amd.com/gpu.xgmi-links=7         amd.com/gpu.device-id=75a3
+    amd.com/gpu.driver-version=...     amd.com/gpu.numa-nodes=2
+
+``amd.com/gpu.present`` is what schedules the rest of the operator's DaemonSets onto the node.
+Labels this component owns are removed again when the GPUs go away; labels owned by other
+components (``amd.com/gpu.validated``, ``amd.com/gpu.compute-partition.desired``) are left alone.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import re
+from typing import Dict, Optional
+
+from ..utils import topology as topo_mod
+
+log = logging.getLogger("amd-node-labeller")
+
+PREFIX = "amd.com/gpu"
+OWNED = ("present", "count", "asic-count", "product", "family", "device-id", "cu-count", "vram",
+         "compute-partition", "memory-partition", "xgmi-links", "driver-version", "numa-nodes")
+_LABEL_VALUE = re.compile(r"^(([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9])?$")
+
+
+def sanitize(value: str) -> str:
+    v = re.sub(r"[^A-Za-z0-9_.-]+", "_", value.strip())[:63]
+    v = v.strip("-_.")
+    return v if _LABEL_VALUE.match(v) else ""
+
+
+def driver_version(root: str = "/") -> Optional[str]:
+    for p in ("sys/module/amdgpu/version", "sys/module/amdgpu/srcversion"):
+        try:
+            with open(os.path.join(root, p)) as f:
+                v = f.read().strip()
+                if v:
+                    return v
+        except OSError:
+            continue
+    return None
+
+
+def compute_labels(root: str = "/", min_gfx: int = topo_mod.GFX950) -> Dict[str, Optional[str]]:
+    """Desired values for every owned label (None = remove)."""
+    labels: Dict[str, Optional[str]] = {f"{PREFIX}.{k}": None for k in OWNED}
+    try:
+        topo = topo_mod.read_topology(root, min_gfx)
+    except FileNotFoundError:
+        return labels
+    gpus = topo.gpus
+    if not gpus:
+        return labels
+    asics = topo.asics()
+    head = gpus[0]
+    vram_gib = round(sum(g.vram_bytes for g in asics[head.unique_id]) / (1 << 30))
+    labels.update({
+        f"{PREFIX}.present": "true",
+        f"{PREFIX}.count": str(len(gpus)),
+        f"{PREFIX}.asic-count": str(len(asics)),
+        f"{PREFIX}.product": sanitize(head.product),
+        f"{PREFIX}.family": head.gfx_name,
+        f"{PREFIX}.device-id": "%04x" % head.device_id,
+        f"{PREFIX}.cu-count": str(head.cu_count),
+        f"{PREFIX}.vram": f"{vram_gib}G",
+        f"{PREFIX}.compute-partition": head.compute_partition,
+        f"{PREFIX}.memory-partition": head.memory_partition,
+        f"{PREFIX}.xgmi-links": str(len({p for p in head.xgmi_peers
+                                         if p not in {g.node_id for g in asics[head.unique_id]}})
+                                    if head.partitions_on_asic == 1 else
+                                    len(asics) - 1),
+        f"{PREFIX}.numa-nodes": str(len({g.numa_node for g in gpus if g.numa_node >= 0}) or 1),
+    })
+    dv = driver_version(root)
+    if dv:
+        labels[f"{PREFIX}.driver-version"] = sanitize(dv) or None
+    return labels
+
+
+def diff_labels(current: Dict[str, str], desired: Dict[str, Optional[str]]) -> Dict[str, Optional[str]]:
+    patch = {}
+    for k, v in desired.items():
+        if v is None:
+            if k in current:
+                patch[k] = None
+        elif current.get(k) != v:
+            patch[k] = v
+    return patch
+
+
+class NodeLabeller:
+    def __init__(self, client, node_name: str, root: str = "/", min_gfx: int = topo_mod.GFX950):
+        self.client = client
+        self.node = node_name
+        self.root = root
+        self.min_gfx = min_gfx
+
+    def reconcile(self) -> Dict[str, Optional[str]]:
+        desired = compute_labels(self.root, self.min_gfx)
+        node = self.client.get_node(self.node)
+        current = node.get("metadata", {}).get("labels", {}) or {}
+        patch = diff_labels(current, desired)
+        if patch:
+            self.client.set_node_labels(self.node, patch)
+            log.info("node %s: %s", self.node, patch)
+        return patch
+
+    def run(self, interval: float = 60.0, stop_event=None) -> None:
+        import threading
+
+        stop_event = stop_event or threading.Event()
+        while not stop_event.is_set():
+            try:
+                self.reconcile()
+            except Exception as e:  # noqa: BLE001 - API server hiccups must not kill the agent
+                log.warning("reconcile failed: %s", e)
+            stop_event.wait(interval)

@@ -1,0 +1,213 @@
+"""Compute / memory partition manager (SURVEY.md §2.2 X7 — the MIG-manager role; BASELINE config 5).
+
+An MI355X can run as one GPU (SPX: 8 XCDs, 256 CUs, 288 GB) or be split into 2/4/8 compute
+partitions (DPX/QPX/CPX; CPX = 8 GPUs of 1 XCD / 32 CUs each), with the HBM as one NUMA domain
+(NPS1) or two (NPS2).  Changing mode needs the GPU idle, and the driver then re-enumerates: new
+KFD agents, new render minors, different device IDs.  The manager drives that safely:
+
+    IDLE ──desired≠current──▶ DRAINING ──no amd.com/gpu pods left──▶ APPLYING ──▶ REENUMERATING ──▶ IDLE
+                                  │ taint NoSchedule + pause marker           │ amd-smi / sysfs   │ KFD shows
+                                  │ (device plugin advertises 0 devices)      │ per ASIC          │ N × split agents
+                                  └──timeout──▶ FAILED (taint and marker removed, reason annotated)
+
+The desired mode comes from the node label ``amd.com/gpu.compute-partition.desired`` (and
+``…memory-partition.desired``), else from operator.yaml.  The state is published as the node
+annotation ``amd.com/gpu.partition-state`` so it survives agent restarts and is visible with kubectl.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import time
+from typing import Callable, Optional
+
+from ..utils import kube as kube_mod
+from ..utils import topology as topo_mod
+
+log = logging.getLogger("amd-partition-manager")
+
+LABEL_DESIRED = "amd.com/gpu.compute-partition.desired"
+LABEL_MEM_DESIRED = "amd.com/gpu.memory-partition.desired"
+ANNOT_STATE = "amd.com/gpu.partition-state"
+TAINT_KEY = "amd.com/gpu-partitioning"
+PAUSE_MARKER = "/run/amd/partition-in-progress"
+
+
+class PartitionError(RuntimeError):
+    pass
+
+
+class SysfsPartitionBackend:
+    """Writes ``current_{compute,memory}_partition`` of each ASIC's PCI device (needs root)."""
+
+    def __init__(self, root: str = "/"):
+        self.root = root
+
+    def _write(self, dev: topo_mod.GpuDevice, attr: str, value: str) -> None:
+        path = os.path.join(self.root, topo_mod.DRM_CLASS, f"card{dev.card_minor}", "device", attr)
+        with open(path, "w") as f:
+            f.write(value + "\n")
+
+    def set_compute(self, dev: topo_mod.GpuDevice, mode: str) -> None:
+        self._write(dev, "current_compute_partition", mode)
+
+    def set_memory(self, dev: topo_mod.GpuDevice, mode: str) -> None:
+        self._write(dev, "current_memory_partition", mode)
+
+
+class AmdSmiPartitionBackend:
+    def __init__(self, amdsmi_module=None):
+        if amdsmi_module is None:
+            import amdsmi as amdsmi_module  # noqa: N813
+        self.S = amdsmi_module
+        self.S.amdsmi_init()
+
+    def _handle(self, dev: topo_mod.GpuDevice):
+        for h in self.S.amdsmi_get_processor_handles():
+            if str(self.S.amdsmi_get_gpu_device_bdf(h)).lower() == dev.pci_bdf.lower():
+                return h
+        raise PartitionError(f"amd-smi has no handle for {dev.pci_bdf}")
+
+    def set_compute(self, dev: topo_mod.GpuDevice, mode: str) -> None:
+        self.S.amdsmi_set_gpu_compute_partition(
+            self._handle(dev), getattr(self.S.AmdSmiComputePartitionType, mode))
+
+    def set_memory(self, dev: topo_mod.GpuDevice, mode: str) -> None:
+        self.S.amdsmi_set_gpu_memory_partition(
+            self._handle(dev), getattr(self.S.AmdSmiMemoryPartitionType, mode))
+
+
+class PartitionManager:
+    def __init__(self, client: kube_mod.KubeClient, node_name: str, backend, root: str = "/",
+                 default_compute: str = "SPX", default_memory: str = "NPS1",
+                 drain_timeout: float = 600.0, reenum_timeout: float = 300.0, poll: float = 2.0,
+                 pause_marker: str = PAUSE_MARKER, min_gfx: int = topo_mod.GFX950,
+                 resource: str = "amd.com/gpu", sleep: Callable[[float], None] = time.sleep):
+        self.client = client
+        self.node = node_name
+        self.backend = backend
+        self.root = root
+        self.default_compute = default_compute
+        self.default_memory = default_memory
+        self.drain_timeout = drain_timeout
+        self.reenum_timeout = reenum_timeout
+        self.poll = poll
+        self.pause_marker = pause_marker
+        self.min_gfx = min_gfx
+        self.resource = resource
+        self.sleep = sleep
+
+    # ---------------------------------------------------------------- helpers
+    def _state(self, state: str, reason: str = "") -> None:
+        self.client.set_node_annotations(self.node, {ANNOT_STATE: f"{state}{': ' + reason if reason else ''}"})
+        log.info("partition state %s %s", state, reason)
+
+    def _pause(self, on: bool) -> None:
+        if on:
+            os.makedirs(os.path.dirname(self.pause_marker), exist_ok=True)
+            with open(self.pause_marker, "w") as f:
+                f.write(f"{time.time()}\n")
+        elif os.path.exists(self.pause_marker):
+            os.unlink(self.pause_marker)
+
+    def desired(self) -> tuple:
+        labels = self.client.get_node(self.node).get("metadata", {}).get("labels", {}) or {}
+        return (labels.get(LABEL_DESIRED, self.default_compute).upper(),
+                labels.get(LABEL_MEM_DESIRED, self.default_memory).upper())
+
+    def current(self) -> tuple:
+        topo = topo_mod.read_topology(self.root, self.min_gfx)
+        if not topo.gpus:
+            raise PartitionError("no GPUs in the KFD topology")
+        head = topo.gpus[0]
+        return head.compute_partition, head.memory_partition, topo
+
+    def gpu_pods(self) -> list:
+        pods = self.client.list_pods(field_selector=f"spec.nodeName={self.node}")
+        return [p for p in pods
+                if p.get("status", {}).get("phase") in ("Pending", "Running", "Unknown")
+                and kube_mod.pod_gpu_request(p, self.resource) > 0]
+
+    # ---------------------------------------------------------------- reconcile
+    def reconcile(self) -> str:
+        want_c, want_m = self.desired()
+        if want_c not in topo_mod.PARTITION_SPLIT:
+            self._state("failed", f"unknown compute partition {want_c}")
+            return "failed"
+        cur_c, cur_m, topo = self.current()
+        if (cur_c, cur_m) == (want_c, want_m):
+            self._pause(False)
+            self.client.set_taint(self.node, TAINT_KEY, "", present=False)
+            self._state("idle")
+            return "idle"
+        avail = topo_mod.available_partitions(self.root, topo.gpus[0])
+        if want_c not in avail:
+            self._state("failed", f"{want_c} not in available {','.join(avail)}")
+            return "failed"
+        asics = topo.asics()
+        log.info("node %s: %s/%s -> %s/%s on %d ASIC(s)", self.node, cur_c, cur_m, want_c, want_m,
+                 len(asics))
+        # 1. stop new GPU work landing here; hide devices from kubelet
+        self.client.set_taint(self.node, TAINT_KEY, want_c, present=True)
+        self._pause(True)
+        self._state("draining", f"{cur_c}->{want_c}")
+        deadline = time.monotonic() + self.drain_timeout
+        while True:
+            busy = self.gpu_pods()
+            if not busy:
+                break
+            if time.monotonic() >= deadline:
+                names = ",".join(p["metadata"]["name"] for p in busy[:5])
+                self._abort(f"drain timeout: GPU pods still running ({names})")
+                return "failed"
+            self.sleep(self.poll)
+        # 2. apply, memory partition first (the compute split must fit the memory layout)
+        self._state("applying", f"{want_c}/{want_m}")
+        try:
+            for members in asics.values():
+                head = members[0]
+                if cur_m != want_m:
+                    self.backend.set_memory(head, want_m)
+                if cur_c != want_c:
+                    self.backend.set_compute(head, want_c)
+        except Exception as e:  # noqa: BLE001
+            self._abort(f"apply failed: {e}")
+            return "failed"
+        # 3. wait for the driver to re-enumerate N × split agents
+        self._state("reenumerating")
+        expect = len(asics) * topo_mod.PARTITION_SPLIT[want_c]
+        deadline = time.monotonic() + self.reenum_timeout
+        while True:
+            try:
+                c, m, t2 = self.current()
+                if (c, m) == (want_c, want_m) and len(t2.gpus) == expect:
+                    break
+            except (PartitionError, FileNotFoundError):
+                pass
+            if time.monotonic() >= deadline:
+                self._abort(f"re-enumeration timeout (expected {expect} agents)")
+                return "failed"
+            self.sleep(self.poll)
+        # 4. resume
+        self._pause(False)
+        self.client.set_taint(self.node, TAINT_KEY, "", present=False)
+        self.client.set_node_labels(self.node, {"amd.com/gpu.compute-partition": want_c,
+                                                "amd.com/gpu.memory-partition": want_m})
+        self._state("idle", f"applied {want_c}/{want_m}")
+        return "applied"
+
+    def _abort(self, reason: str) -> None:
+        self._pause(False)
+        self.client.set_taint(self.node, TAINT_KEY, "", present=False)
+        self._state("failed", reason)
+
+    def run(self, interval: float = 30.0, stop_event=None) -> None:
+        import threading
+
+        stop_event = stop_event or threading.Event()
+        while not stop_event.is_set():
+            try:
+                self.reconcile()
+            except Exception as e:  # noqa: BLE001
+                log.warning("reconcile failed: %s", e)
+            stop_event.wait(interval)

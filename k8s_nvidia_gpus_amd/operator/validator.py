@@ -1,0 +1,303 @@
+"""Operator validator — the gate between "driver loaded" and "node usable".
+
+The reference reproduces NVIDIA's validator by hand: a ``cuda-sample:vectoradd`` Job whose log must
+end in ``Test PASSED`` / ``Done`` (reference README.md:264-299), plus a two-pod isolation check
+(README.md:301-387); multi-GPU-in-one-pod is "TBD" (README.md:389-391).  Here the chain runs
+automatically on every GPU node as init containers of the validator DaemonSet, each step gated on
+the previous one's marker under ``/run/amd/validations``:
+
+  driver    kfd-probe: ≥ expectedGpusPerNode gfx950 agents, /dev/kfd + render nodes usable
+  runtime   the runtime installer published runtime-ready (amd-container-runtime + CDI spec)
+  vectoradd hand-written HIP vectorAdd on every GPU, reference stdout protocol
+  gemm      hand-written gfx950 bf16 MFMA GEMM on every GPU: numerics vs fp32 + TFLOPS ≥ floor
+  rccl      RCCL all-reduce over xGMI across all GPUs of the node: exact sums + bus bandwidth floor
+  plugin    a pod requesting amd.com/gpu: 1 is scheduled THROUGH the device plugin and passes
+  report    node label amd.com/gpu.validated=true|false, validator-ready marker
+
+Each step writes ``<step>.json`` (the metrics exporter publishes TFLOPS / busbw / pass flags from
+them) and ``<step>-ready`` on success.  Command execution is injectable so the parsing and gating
+logic is tested on CPU against the real outputs the native tools produced on an MI355X
+(profiles/r01_*.log).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import re
+import subprocess
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+from .config import OperatorConfig
+
+log = logging.getLogger("amd-gpu-validator")
+
+STEPS = ("driver", "runtime", "vectoradd", "gemm", "rccl", "plugin", "report")
+LABEL_VALIDATED = "amd.com/gpu.validated"
+
+Runner = Callable[[Sequence[str], float], Tuple[int, str]]
+
+
+def default_runner(argv: Sequence[str], timeout: float) -> Tuple[int, str]:
+    try:
+        p = subprocess.run(list(argv), stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                           timeout=timeout)
+        return p.returncode, p.stdout
+    except subprocess.TimeoutExpired as e:
+        out = e.stdout.decode() if isinstance(e.stdout, bytes) else (e.stdout or "")
+        return 124, out + f"\n[validator] timed out after {timeout}s"
+    except FileNotFoundError as e:
+        return 127, str(e)
+
+
+def find_bin_dir() -> str:
+    env = os.environ.get("AMDK8S_BIN_DIR")
+    if env:
+        return env
+    here = os.path.dirname(os.path.abspath(__file__))
+    for cand in ("/opt/amd-gpu-operator/bin",
+                 os.path.normpath(os.path.join(here, "..", "..", "native", "bin"))):
+        if os.path.isdir(cand):
+            return cand
+    return "/opt/amd-gpu-operator/bin"
+
+
+def json_lines(text: str) -> List[dict]:
+    out = []
+    for line in text.splitlines():
+        line = line.strip()
+        if line.startswith("{") and line.endswith("}"):
+            try:
+                out.append(json.loads(line))
+            except ValueError:
+                continue
+    return out
+
+
+def protocol_passed(text: str) -> bool:
+    """Reference protocol: 'Test PASSED' then 'Done', no 'Test FAILED'."""
+    lines = [ln.strip() for ln in text.splitlines() if ln.strip()]
+    return ("Test PASSED" in lines and "Done" in lines and "Test FAILED" not in lines
+            and lines.index("Done") > lines.index("Test PASSED"))
+
+
+@dataclass
+class StepResult:
+    step: str
+    passed: bool
+    detail: Dict = field(default_factory=dict)
+    reason: str = ""
+
+    def to_json(self) -> dict:
+        d = {"step": self.step, "passed": self.passed, "reason": self.reason, "time": time.time()}
+        d.update(self.detail)
+        return d
+
+
+class Validator:
+    def __init__(self, config: OperatorConfig, marker_dir: str = "/run/amd/validations",
+                 bin_dir: Optional[str] = None, runner: Runner = default_runner, root: str = "/",
+                 kube=None, node_name: Optional[str] = None):
+        self.cfg = config
+        self.vcfg = config.section("validator")
+        self.marker_dir = marker_dir
+        self.bin_dir = bin_dir or find_bin_dir()
+        self.run_cmd = runner
+        self.root = root
+        self.kube = kube
+        self.node = node_name or os.environ.get("NODE_NAME", "")
+
+    # ---------------------------------------------------------------- markers
+    def _path(self, name: str) -> str:
+        return os.path.join(self.marker_dir, name)
+
+    def write_result(self, r: StepResult) -> None:
+        os.makedirs(self.marker_dir, exist_ok=True)
+        tmp = self._path(f".{r.step}.json.tmp")
+        with open(tmp, "w") as f:
+            json.dump(r.to_json(), f, indent=1)
+        os.replace(tmp, self._path(f"{r.step}.json"))
+        ready = self._path(f"{r.step}-ready")
+        if r.passed:
+            with open(ready, "w") as f:
+                f.write(f"{time.time()}\n")
+        elif os.path.exists(ready):
+            os.unlink(ready)
+
+    def ready(self, step: str) -> bool:
+        return os.path.exists(self._path(f"{step}-ready"))
+
+    def wait_for(self, marker: str, timeout: float, poll: float = 2.0) -> bool:
+        deadline = time.monotonic() + timeout
+        while not os.path.exists(self._path(marker)):
+            if time.monotonic() >= deadline:
+                return False
+            time.sleep(poll)
+        return True
+
+    def _bin(self, name: str) -> str:
+        return os.path.join(self.bin_dir, name)
+
+    # ---------------------------------------------------------------- steps
+    def step_driver(self) -> StepResult:
+        n = int(self.cfg["expectedGpusPerNode"])
+        argv = [self._bin("kfd-probe"), "--expect-gpus", str(n), "--min-gfx", str(self.cfg.min_gfx),
+                "--wait", "120"]
+        if self.root != "/":
+            argv += ["--sysfs-root", os.path.join(self.root, "sys/class/kfd/kfd/topology"),
+                     "--dev-root", os.path.join(self.root, "dev"), "--no-open"]
+        rc, out = self.run_cmd(argv, 180)
+        docs = json_lines(out)
+        detail = docs[-1] if docs else {}
+        ok = rc == 0 and bool(detail.get("ready"))
+        return StepResult("driver", ok, {"gpus": detail.get("gpus"), "agents": detail.get("agents", [])},
+                          "" if ok else (detail.get("reason") or out.strip()[-300:]))
+
+    def step_runtime(self, timeout: float = 600) -> StepResult:
+        ok = self.wait_for("runtime-ready", timeout)
+        return StepResult("runtime", ok, {}, "" if ok else "runtime-ready marker not published")
+
+    def step_vectoradd(self) -> StepResult:
+        rc, out = self.run_cmd([self._bin("amd-vectoradd"), "--json"], 300)
+        devs = [d for d in json_lines(out) if d.get("check") == "vectoradd"]
+        ok = rc == 0 and protocol_passed(out) and devs and all(d.get("passed") for d in devs)
+        return StepResult("vectoradd", bool(ok), {"devices": devs},
+                          "" if ok else f"rc={rc}: " + out.strip()[-300:])
+
+    def step_gemm(self) -> StepResult:
+        size = int(self.vcfg["gemmSize"])
+        floor = float(self.vcfg["gemmMinTflops"])
+        rc, out = self.run_cmd([self._bin("amd-gemm-validator"), "--size", str(size), "--iters", "50",
+                                "--json"], 900)
+        devs = [d for d in json_lines(out) if d.get("check") == "gemm_bf16"]
+        slow = [d for d in devs if float(d.get("tflops", 0)) < floor]
+        bad = [d for d in devs if not d.get("passed")]
+        ok = rc == 0 and protocol_passed(out) and devs and not slow and not bad
+        reason = ""
+        if not ok:
+            reason = (f"{len(bad)} GPU(s) failed numerics; " if bad else "") + \
+                     (f"{len(slow)} GPU(s) below {floor} TFLOPS; " if slow else "") + \
+                     (f"rc={rc}" if rc else "")
+        total = sum(float(d.get("tflops", 0)) for d in devs)
+        return StepResult("gemm", bool(ok), {"devices": devs, "size": size, "floor_tflops": floor,
+                                             "aggregate_tflops": round(total, 1)}, reason)
+
+    def step_rccl(self, ngpus: Optional[int] = None) -> StepResult:
+        if ngpus is not None and ngpus < 2:
+            return StepResult("rccl", True, {"ngpus": ngpus, "skipped": "single GPU"})
+        floor = float(self.vcfg["rcclMinBusbwGBps"])
+        rc, out = self.run_cmd([self._bin("rccl-allreduce-bench"), "-b", "1M", "-e", "1G", "-f", "4",
+                                "-n", "20", "--json"], 900)
+        docs = [d for d in json_lines(out) if d.get("check") == "rccl_allreduce"]
+        d = docs[-1] if docs else {}
+        n = d.get("ngpus", ngpus)
+        if n is not None and n < 2:
+            return StepResult("rccl", rc == 0, {"ngpus": n, "skipped": "single GPU"})
+        ok = rc == 0 and bool(d.get("passed")) and float(d.get("peak_busbw_gbps", 0)) >= floor
+        return StepResult("rccl", ok, d, "" if ok else
+                          f"rc={rc} wrong={d.get('wrong')} busbw={d.get('peak_busbw_gbps')} < {floor}?")
+
+    def step_plugin(self, timeout: float = 600) -> StepResult:
+        if self.kube is None or not self.node:
+            return StepResult("plugin", False, {}, "no Kubernetes API access / NODE_NAME")
+        ns = os.environ.get("POD_NAMESPACE", "amd-gpu-operator")
+        image = self._own_image(ns)
+        name = f"amd-gpu-plugin-validation-{self.node}"[:63].rstrip("-.")
+        pod = {
+            "apiVersion": "v1", "kind": "Pod",
+            "metadata": {"name": name, "namespace": ns,
+                         "labels": {"app": "amd-gpu-plugin-validation"}},
+            "spec": {
+                "restartPolicy": "Never",
+                "nodeName": self.node,
+                "runtimeClassName": self.cfg["runtimeClass"],
+                "tolerations": [{"operator": "Exists"}],
+                "containers": [{
+                    "name": "vectoradd", "image": image,
+                    "command": [os.path.join("/opt/amd-gpu-operator/bin", "amd-vectoradd")],
+                    "resources": {"limits": {self.cfg.resource_name: "1"}},
+                }],
+            },
+        }
+        self.kube.delete_pod(ns, name)
+        self.kube.create_pod(ns, pod)
+        try:
+            done = self.kube.wait_pod_phase(ns, name, timeout=timeout)
+            logs = self.kube.pod_logs(ns, name)
+        finally:
+            self.kube.delete_pod(ns, name)
+        phase = done.get("status", {}).get("phase")
+        ok = phase == "Succeeded" and protocol_passed(logs)
+        return StepResult("plugin", ok, {"pod": name, "phase": phase},
+                          "" if ok else f"phase={phase}: {logs.strip()[-300:]}")
+
+    def _own_image(self, ns: str) -> str:
+        pod_name = os.environ.get("POD_NAME")
+        if pod_name and self.kube is not None:
+            try:
+                pod = self.kube.get_pod(ns, pod_name)
+                for c in pod.get("spec", {}).get("initContainers", []) + pod.get("spec", {}).get("containers", []):
+                    if c.get("image"):
+                        return c["image"]
+            except Exception as e:  # noqa: BLE001
+                log.warning("cannot read own pod image: %s", e)
+        return os.environ.get("VALIDATOR_IMAGE", "ghcr.io/example-org/amd-gpu-operator:0.1.0")
+
+    def step_report(self) -> StepResult:
+        required = ["driver", "runtime"]
+        if self.vcfg["vectorAdd"]:
+            required.append("vectoradd")
+        if self.vcfg["gemm"]:
+            required.append("gemm")
+        if self.vcfg["rccl"]:
+            required.append("rccl")
+        if self.vcfg["pluginTest"]:
+            required.append("plugin")
+        missing = [s for s in required if not self.ready(s)]
+        ok = not missing
+        if self.kube is not None and self.node:
+            try:
+                self.kube.set_node_labels(self.node, {LABEL_VALIDATED: "true" if ok else "false"})
+            except Exception as e:  # noqa: BLE001
+                log.warning("cannot label node: %s", e)
+        r = StepResult("report", ok, {"required": required, "missing": missing},
+                       "" if ok else "failed/missing: " + ",".join(missing))
+        if ok:
+            with open(self._path("validator-ready"), "w") as f:
+                f.write(f"{time.time()}\n")
+        elif os.path.exists(self._path("validator-ready")):
+            os.unlink(self._path("validator-ready"))
+        return r
+
+    # ---------------------------------------------------------------- driver
+    def run_step(self, step: str) -> StepResult:
+        if step == "driver":
+            r = self.step_driver()
+        elif step == "runtime":
+            r = self.step_runtime()
+        elif step == "vectoradd":
+            r = self.step_vectoradd() if self.vcfg["vectorAdd"] else StepResult("vectoradd", True, {"skipped": True})
+        elif step == "gemm":
+            r = self.step_gemm() if self.vcfg["gemm"] else StepResult("gemm", True, {"skipped": True})
+        elif step == "rccl":
+            if not self.vcfg["rccl"]:
+                r = StepResult("rccl", True, {"skipped": True})
+            else:
+                gpus = None
+                try:
+                    with open(self._path("driver.json")) as f:
+                        gpus = json.load(f).get("gpus")
+                except (OSError, ValueError):
+                    pass
+                r = self.step_rccl(gpus)
+        elif step == "plugin":
+            r = self.step_plugin() if self.vcfg["pluginTest"] else StepResult("plugin", True, {"skipped": True})
+        elif step == "report":
+            r = self.step_report()
+        else:
+            raise ValueError(f"unknown step {step!r}; steps: {STEPS}")
+        self.write_result(r)
+        log.info("step %s: %s %s", step, "PASSED" if r.passed else "FAILED", r.reason)
+        return r

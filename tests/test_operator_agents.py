@@ -1,0 +1,301 @@
+"""Node agents of the AMD GPU operator against fakes: sysfs tree, Kubernetes API, amd-smi (CPU-only)."""
+import json
+import os
+import subprocess
+import sys
+import threading
+import urllib.request
+from pathlib import Path
+
+import pytest
+
+from fakes import sysfs as fake_sysfs
+from fakes.amdsmi import FakeAmdSmi
+from fakes.kubeapi import FakeKubeAPI
+from k8s_nvidia_gpus_amd.operator import exporter as ex
+from k8s_nvidia_gpus_amd.operator import labeller as lb
+from k8s_nvidia_gpus_amd.operator import partition as pm
+from k8s_nvidia_gpus_amd.operator import runtime as rt
+from k8s_nvidia_gpus_amd.operator.config import ConfigError, load_config
+from k8s_nvidia_gpus_amd.utils.kube import KubeClient, pod_gpu_request
+from k8s_nvidia_gpus_amd.utils.topology import read_topology
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+@pytest.fixture
+def api():
+    a = FakeKubeAPI().start()
+    a.add_node("gpu-node-1", {"kubernetes.io/os": "linux"})
+    yield a
+    a.stop()
+
+
+@pytest.fixture
+def client(api):
+    return KubeClient(base_url=api.url)
+
+
+# ----------------------------------------------------------------------------- config
+def test_config_defaults_and_validation():
+    cfg = load_config()
+    assert cfg.resource_name == "amd.com/gpu" and cfg.min_gfx == 90500
+    with pytest.raises(ConfigError):
+        load_config(text="resourceName: amd.com/gpu\nbogus: 1\n")
+    with pytest.raises(ConfigError):
+        load_config(text="partition: {compute: MIG}\n")
+    with pytest.raises(ConfigError):
+        load_config(text="validator: {gemmSize: 1000}\n")
+
+
+def test_shipped_operator_config_parses():
+    import yaml
+
+    cm = yaml.safe_load((REPO / "cluster-config/apps/amd-gpu-operator/config.yaml").read_text())
+    cfg = load_config(text=cm["data"]["operator.yaml"])
+    assert cfg["expectedGpusPerNode"] == 8
+    assert cfg.section("allocation")["mode"] == "deviceSpecs"
+
+
+# ----------------------------------------------------------------------------- labeller
+def test_labeller_labels_mi355x_node(tmp_path, api, client):
+    root = fake_sysfs.build_node(tmp_path / "r")
+    (root / "sys/module/amdgpu").mkdir(parents=True)
+    (root / "sys/module/amdgpu/version").write_text("6.16.6\n")
+    patch = lb.NodeLabeller(client, "gpu-node-1", str(root)).reconcile()
+    labels = api.nodes["gpu-node-1"]["metadata"]["labels"]
+    assert labels["amd.com/gpu.present"] == "true"
+    assert labels["amd.com/gpu.product"] == "MI355X"
+    assert labels["amd.com/gpu.family"] == "gfx950"
+    assert labels["amd.com/gpu.count"] == "8"
+    assert labels["amd.com/gpu.cu-count"] == "256"
+    assert labels["amd.com/gpu.vram"] == "288G"
+    assert labels["amd.com/gpu.compute-partition"] == "SPX"
+    assert labels["amd.com/gpu.xgmi-links"] == "7"
+    assert labels["amd.com/gpu.numa-nodes"] == "2"
+    assert labels["amd.com/gpu.driver-version"] == "6.16.6"
+    assert labels["kubernetes.io/os"] == "linux"  # untouched
+    assert patch
+    # idempotent: second pass patches nothing
+    assert lb.NodeLabeller(client, "gpu-node-1", str(root)).reconcile() == {}
+
+
+def test_labeller_cpx_and_removal(tmp_path, api, client):
+    root = fake_sysfs.build_node(tmp_path / "r", compute_partition="CPX")
+    lab = lb.NodeLabeller(client, "gpu-node-1", str(root))
+    lab.reconcile()
+    labels = api.nodes["gpu-node-1"]["metadata"]["labels"]
+    assert labels["amd.com/gpu.count"] == "64" and labels["amd.com/gpu.cu-count"] == "32"
+    assert labels["amd.com/gpu.compute-partition"] == "CPX"
+    api.nodes["gpu-node-1"]["metadata"]["labels"]["amd.com/gpu.validated"] = "true"
+    # GPUs gone (driver unloaded): owned labels removed, foreign ones kept
+    lb.NodeLabeller(client, "gpu-node-1", str(tmp_path / "empty")).reconcile()
+    labels = api.nodes["gpu-node-1"]["metadata"]["labels"]
+    assert not any(k in labels for k in ("amd.com/gpu.present", "amd.com/gpu.count"))
+    assert labels["amd.com/gpu.validated"] == "true"
+
+
+def test_label_value_sanitizer():
+    assert lb.sanitize("Linuxversion 6.18 (gcc)") == "Linuxversion_6.18_gcc"
+    assert len(lb.sanitize("x" * 100)) == 63
+
+
+# ----------------------------------------------------------------------------- exporter
+def _scrape(collector):
+    from prometheus_client import generate_latest
+
+    return generate_latest(ex.make_registry(collector)).decode()
+
+
+def _samples(text):
+    """{(metric, frozenset(labels)): value} from Prometheus text."""
+    from prometheus_client.parser import text_string_to_metric_families
+
+    out = {}
+    for fam in text_string_to_metric_families(text):
+        for s in fam.samples:
+            out[(s.name, frozenset(s.labels.items()))] = s.value
+    return out
+
+
+def _find(samples, name, **labels):
+    return [v for (n, ls), v in samples.items()
+            if n == name and all((k, str(val)) in ls for k, val in labels.items())]
+
+
+def test_exporter_amdsmi_backend_metrics(tmp_path):
+    marker = tmp_path / "v"
+    marker.mkdir()
+    (marker / "gemm.json").write_text(json.dumps({"passed": True, "devices": [
+        {"device": 0, "tflops": 1389.4}, {"device": 1, "tflops": 1380.0}]}))
+    (marker / "rccl.json").write_text(json.dumps({"passed": True, "ngpus": 8, "peak_busbw_gbps": 310.5}))
+    fake = FakeAmdSmi()
+    col = ex.GpuCollector(ex.AmdSmiBackend(fake), "gpu-node-1", str(marker))
+    text = _scrape(col)
+    sm = _samples(text)
+    assert _find(sm, "amd_gpu_exporter_up") == [1.0]
+    info = _find(sm, "amd_gpu_info")
+    assert len(info) == 8
+    assert _find(sm, "amd_gpu_info", product="AMD Instinct MI355 OAM", gfx="gfx950", gpu=0)
+    assert _find(sm, "amd_gpu_power_watts", gpu=0) == [249.0]
+    assert _find(sm, "amd_gpu_temperature_celsius", gpu=0, sensor="hotspot") == [45.0]
+    assert _find(sm, "amd_gpu_utilization_percent", gpu=3) == [30.0]
+    assert _find(sm, "amd_gpu_vram_total_bytes", gpu=0) == [294896 * 1024 * 1024]
+    links = _find(sm, "amd_gpu_xgmi_data_bytes_total", gpu=0, direction="read")
+    assert len(links) == 8 and max(links) > 1e10
+    assert _find(sm, "amd_gpu_ecc_errors_total", gpu=0, type="uncorrectable") == [0.0]
+    assert _find(sm, "amd_gpu_validator_gemm_tflops", gpu=0, node="gpu-node-1") == [1389.4]
+    assert _find(sm, "amd_gpu_validator_allreduce_busbw_gbps", ngpus=8) == [310.5]
+    assert _find(sm, "amd_gpu_validation_passed", step="gemm") == [1.0]
+    # N/A fields (edge temperature) are omitted, not exported as 0
+    assert not _find(sm, "amd_gpu_temperature_celsius", sensor="edge")
+
+
+def test_exporter_survives_unsupported_calls():
+    fake = FakeAmdSmi(n_gpus=2, fail={"amdsmi_get_gpu_metrics_info", "amdsmi_get_gpu_total_ecc_count"})
+    text = _scrape(ex.GpuCollector(ex.AmdSmiBackend(fake), "n", "/nonexistent"))
+    assert text.count("amd_gpu_info{") == 2
+    assert "amd_gpu_power_watts{" not in text
+    assert "amd_gpu_vram_used_bytes{" in text
+
+
+def test_exporter_sysfs_fallback(tmp_path):
+    root = fake_sysfs.build_node(tmp_path / "r")
+    text = _scrape(ex.GpuCollector(ex.SysfsBackend(str(root)), "n", "/nonexistent"))
+    assert text.count("amd_gpu_info{") == 8
+    assert 'amd_gpu_vram_total_bytes{gpu="0"' in text
+
+
+def test_exporter_http_server(tmp_path):
+    srv = ex.ExporterServer(ex.GpuCollector(ex.AmdSmiBackend(FakeAmdSmi(2)), "n", str(tmp_path)),
+                            port=0, host="127.0.0.1")
+    srv.serve_background()
+    try:
+        base = f"http://127.0.0.1:{srv.port}"
+        assert urllib.request.urlopen(base + "/healthz", timeout=5).read() == b"ok\n"
+        body = urllib.request.urlopen(base + "/metrics", timeout=5).read().decode()
+        assert "amd_gpu_info{" in body
+    finally:
+        srv.shutdown()
+
+
+# ----------------------------------------------------------------------------- partition manager
+class FakeSysfsPartitionBackend:
+    """Applies a mode by re-enumerating the fake sysfs tree, as the driver would."""
+
+    def __init__(self, root, n_gpus=8):
+        self.root, self.n = root, n_gpus
+        self.applied = []
+
+    def set_memory(self, dev, mode):
+        self.applied.append(("memory", dev.pci_bdf, mode))
+
+    def set_compute(self, dev, mode):
+        self.applied.append(("compute", dev.pci_bdf, mode))
+        if len([a for a in self.applied if a[0] == "compute"]) == self.n:
+            mem = next((a[2] for a in self.applied if a[0] == "memory"), "NPS1")
+            fake_sysfs.set_partition(self.root, self.n, mode, mem)
+
+
+def test_partition_manager_spx_to_cpx(tmp_path, api, client):
+    root = fake_sysfs.build_node(tmp_path / "r")
+    api.nodes["gpu-node-1"]["metadata"]["labels"][pm.LABEL_DESIRED] = "CPX"
+    backend = FakeSysfsPartitionBackend(root)
+    marker = tmp_path / "run/partition-in-progress"
+    mgr = pm.PartitionManager(client, "gpu-node-1", backend, str(root), poll=0.01,
+                              pause_marker=str(marker), sleep=lambda s: None)
+    assert mgr.reconcile() == "applied"
+    assert len(read_topology(str(root), 90500).gpus) == 64
+    assert not marker.exists()
+    node = api.nodes["gpu-node-1"]
+    assert node["metadata"]["annotations"][pm.ANNOT_STATE].startswith("idle")
+    assert not [t for t in node["spec"].get("taints", []) if t["key"] == pm.TAINT_KEY]
+    assert node["metadata"]["labels"]["amd.com/gpu.compute-partition"] == "CPX"
+    assert len([a for a in backend.applied if a[0] == "compute"]) == 8
+    # steady state
+    assert mgr.reconcile() == "idle"
+
+
+def test_partition_manager_waits_for_gpu_pods_then_times_out(tmp_path, api, client):
+    root = fake_sysfs.build_node(tmp_path / "r")
+    api.nodes["gpu-node-1"]["metadata"]["labels"][pm.LABEL_DESIRED] = "CPX"
+    api.add_pod("default", "busy", "gpu-node-1", gpus=1)
+    api.add_pod("default", "cpu-only", "gpu-node-1", gpus=0)
+    seen = {}
+
+    def sleep(_s):
+        node = api.nodes["gpu-node-1"]
+        seen["taint"] = [t for t in node["spec"].get("taints", []) if t["key"] == pm.TAINT_KEY]
+        seen["marker"] = os.path.exists(str(tmp_path / "pause"))
+
+    mgr = pm.PartitionManager(client, "gpu-node-1", FakeSysfsPartitionBackend(root), str(root),
+                              drain_timeout=0.05, poll=0.01, pause_marker=str(tmp_path / "pause"),
+                              sleep=sleep)
+    assert mgr.reconcile() == "failed"
+    assert seen["taint"] and seen["marker"]  # drained with taint + device-plugin pause
+    node = api.nodes["gpu-node-1"]
+    assert "drain timeout" in node["metadata"]["annotations"][pm.ANNOT_STATE]
+    assert not [t for t in node["spec"].get("taints", []) if t["key"] == pm.TAINT_KEY]
+    assert not os.path.exists(str(tmp_path / "pause"))
+    assert len(read_topology(str(root), 90500).gpus) == 8  # untouched
+
+
+def test_partition_manager_rejects_unavailable_mode(tmp_path, api, client):
+    root = fake_sysfs.build_node(tmp_path / "r")
+    api.nodes["gpu-node-1"]["metadata"]["labels"][pm.LABEL_DESIRED] = "XPX"
+    mgr = pm.PartitionManager(client, "gpu-node-1", FakeSysfsPartitionBackend(root), str(root),
+                              pause_marker=str(tmp_path / "p"), sleep=lambda s: None)
+    assert mgr.reconcile() == "failed"
+
+
+def test_amdsmi_partition_backend_maps_bdf(tmp_path):
+    fake = FakeAmdSmi()
+    root = fake_sysfs.build_node(tmp_path / "r")
+    dev = read_topology(str(root), 90500).gpus[5]
+    pm.AmdSmiPartitionBackend(fake).set_compute(dev, "CPX")
+    h = [fake.amdsmi_get_gpu_device_bdf(i) for i in range(8)].index(dev.pci_bdf)
+    assert fake.calls == [("compute", h, "CPX")]
+
+
+def test_pod_gpu_request():
+    assert pod_gpu_request({"spec": {"containers": [
+        {"resources": {"limits": {"amd.com/gpu": "2"}}}, {"resources": {"requests": {"amd.com/gpu": 1}}}]}}) == 3
+
+
+# ----------------------------------------------------------------------------- runtime / CDI
+def test_cdi_spec_and_runtime_install(tmp_path):
+    root = fake_sysfs.build_node(tmp_path / "r", compute_partition="CPX")
+    src = tmp_path / "amd-container-runtime"
+    src.write_bytes(b"#!/bin/sh\nexit 0\n")
+    dst = tmp_path / "host/usr/local/bin/amd-container-runtime"
+    info = rt.install_runtime(str(src), str(dst), str(tmp_path / "cdi"), str(tmp_path / "m"), str(root))
+    assert os.access(dst, os.X_OK) and info["updated"]
+    spec = json.loads((tmp_path / "cdi" / rt.CDI_FILE).read_text())
+    assert spec["kind"] == "amd.com/gpu" and spec["cdiVersion"] == "0.6.0"
+    assert len(spec["devices"]) == 65  # 64 CPX partitions + "all"
+    assert spec["containerEdits"]["deviceNodes"] == [{"path": "/dev/kfd", "permissions": "rw"}]
+    names = {d["name"] for d in spec["devices"]}
+    assert "all" in names and all(n == "all" or "-p" in n for n in names)
+    assert (tmp_path / "m" / "runtime-ready").exists()
+    assert rt.install_runtime(str(src), str(dst), str(tmp_path / "cdi"), str(tmp_path / "m"), str(root))["updated"] is False
+
+
+def test_wait_markers(tmp_path):
+    m = tmp_path / "x-ready"
+    assert rt.wait_markers([str(m)], timeout=0.05, poll=0.01) is False
+    threading.Timer(0.05, lambda: m.write_text("1")).start()
+    assert rt.wait_markers([str(m)], timeout=5, poll=0.01) is True
+
+
+def test_cli_topology_and_cdi(tmp_path):
+    root = fake_sysfs.build_node(tmp_path / "r")
+    env = dict(os.environ, PYTHONPATH=str(REPO))
+    out = subprocess.run([sys.executable, "-m", "k8s_nvidia_gpus_amd.operator", "topology",
+                          "--root", str(root), "--config", "/nonexistent"], capture_output=True,
+                         text=True, env=env, check=True).stdout
+    doc = json.loads(out)
+    assert len(doc["gpus"]) == 8 and doc["cpu_nodes"] == 2
+    out = subprocess.run([sys.executable, "-m", "k8s_nvidia_gpus_amd.operator", "cdi",
+                          "--root", str(root), "--config", "/nonexistent"], capture_output=True,
+                         text=True, env=env, check=True).stdout
+    assert json.loads(out)["kind"] == "amd.com/gpu"

@@ -1,0 +1,176 @@
+"""Validator chain: gating logic on the REAL outputs the native tools produced on an MI355X.
+
+profiles/r01_vectoradd.log and profiles/r01_gemm_validator.log are the stdout of native/bin/
+amd-vectoradd and amd-gemm-validator from the first gpurun session; the driver step runs the real
+kfd-probe binary (host C++, built here) against a fabricated MI355X sysfs tree.
+"""
+import json
+import os
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from fakes import sysfs as fake_sysfs
+from fakes.kubeapi import FakeKubeAPI
+from k8s_nvidia_gpus_amd.ops import build as B
+from k8s_nvidia_gpus_amd.operator.config import load_config
+from k8s_nvidia_gpus_amd.operator.validator import (Validator, json_lines, protocol_passed)
+from k8s_nvidia_gpus_amd.utils.kube import KubeClient
+
+REPO = Path(__file__).resolve().parent.parent
+VECTORADD_LOG = (REPO / "profiles/r01_vectoradd.log").read_text()
+GEMM_LOG = (REPO / "profiles/r01_gemm_validator.log").read_text()
+RCCL_8GPU = """# rccl-allreduce-bench: 8 GPU(s), RCCL 22703, in-place float sum, 20 iters
+{"check": "rccl_allreduce", "ngpus": 8, "peak_busbw_gbps": 301.20, "peak_algbw_gbps": 172.11, "peak_bytes": 1073741824, "wrong": 0, "passed": true}
+Test PASSED
+Done
+"""
+
+
+class Runner:
+    def __init__(self, outputs):
+        self.outputs = outputs
+        self.calls = []
+
+    def __call__(self, argv, timeout):
+        self.calls.append(list(argv))
+        name = os.path.basename(argv[0])
+        rc, out = self.outputs[name]
+        return rc, out
+
+
+@pytest.fixture
+def cfg():
+    return load_config(text="expectedGpusPerNode: 1\nvalidator: {gemmMinTflops: 900, rcclMinBusbwGBps: 100}\n")
+
+
+def test_protocol_parser():
+    assert protocol_passed(VECTORADD_LOG)
+    assert not protocol_passed("Test FAILED\nDone\n")
+    assert not protocol_passed("Test PASSED\n")  # no Done
+    assert len(json_lines(GEMM_LOG)) == 1
+
+
+def test_vectoradd_and_gemm_steps_on_real_outputs(tmp_path, cfg):
+    r = Runner({"amd-vectoradd": (0, VECTORADD_LOG), "amd-gemm-validator": (0, GEMM_LOG)})
+    v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=r)
+    va = v.run_step("vectoradd")
+    assert va.passed and va.detail["devices"][0]["elements"] == 50000
+    g = v.run_step("gemm")
+    assert g.passed
+    assert g.detail["devices"][0]["tflops"] > 1300
+    assert (tmp_path / "gemm-ready").exists()
+    assert json.loads((tmp_path / "gemm.json").read_text())["aggregate_tflops"] > 1300
+    assert r.calls[1][:3] == ["/x/amd-gemm-validator", "--size", "8192"]
+
+
+def test_gemm_step_enforces_tflops_floor(tmp_path):
+    cfg = load_config(text="validator: {gemmMinTflops: 2000}\n")
+    v = Validator(cfg, str(tmp_path), bin_dir="/x",
+                  runner=Runner({"amd-gemm-validator": (0, GEMM_LOG)}))
+    g = v.run_step("gemm")
+    assert not g.passed and "below 2000" in g.reason
+    assert not (tmp_path / "gemm-ready").exists()
+
+
+def test_gemm_step_fails_on_numerics(tmp_path, cfg):
+    bad = GEMM_LOG.replace('"passed": true', '"passed": false').replace("Test PASSED", "Test FAILED")
+    v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=Runner({"amd-gemm-validator": (1, bad)}))
+    assert not v.run_step("gemm").passed
+
+
+def test_rccl_step(tmp_path, cfg):
+    v = Validator(cfg, str(tmp_path), bin_dir="/x",
+                  runner=Runner({"rccl-allreduce-bench": (0, RCCL_8GPU)}))
+    r = v.step_rccl(8)
+    assert r.passed and r.detail["peak_busbw_gbps"] == pytest.approx(301.2)
+    assert v.step_rccl(1).passed  # single GPU: skipped
+    wrong = RCCL_8GPU.replace('"wrong": 0, "passed": true', '"wrong": 12, "passed": false')
+    v2 = Validator(cfg, str(tmp_path), bin_dir="/x",
+                   runner=Runner({"rccl-allreduce-bench": (1, wrong)}))
+    assert not v2.step_rccl(8).passed
+
+
+@pytest.mark.skipif(not B.toolchain_available(), reason="needs the native build")
+def test_driver_step_runs_real_kfd_probe(tmp_path):
+    B.build_native(only=["kfd-probe"])
+    root = fake_sysfs.build_node(tmp_path / "r")
+    cfg = load_config(text="expectedGpusPerNode: 8\n")
+    v = Validator(cfg, str(tmp_path / "m"), bin_dir=str(B.NATIVE_BIN), root=str(root))
+    r = v.run_step("driver")
+    assert r.passed, r.reason
+    assert r.detail["gpus"] == 8 and len(r.detail["agents"]) == 8
+    assert {a["render_minor"] for a in r.detail["agents"]} == set(range(128, 192, 8))
+    # one GPU falls off the bus → driver step fails, marker withdrawn
+    fake_sysfs.remove_gpu(root, 2)
+    cfg9 = load_config(text="expectedGpusPerNode: 8\n")
+    v9 = Validator(cfg9, str(tmp_path / "m"), bin_dir=str(B.NATIVE_BIN), root=str(root))
+    v9.run_cmd = lambda argv, t: _no_wait(argv, t)
+    r2 = v9.run_step("driver")
+    assert not r2.passed and "expected 8" in r2.reason
+    assert not (tmp_path / "m" / "driver-ready").exists()
+
+
+def _no_wait(argv, timeout):
+    argv = [a for a in argv]
+    i = argv.index("--wait")
+    argv[i + 1] = "0"
+    p = subprocess.run(argv, capture_output=True, text=True)
+    return p.returncode, p.stdout + p.stderr
+
+
+@pytest.mark.skipif(not B.toolchain_available(), reason="needs the native build")
+def test_kfd_probe_cpx_counts_partitions(tmp_path):
+    B.build_native(only=["kfd-probe"])
+    root = fake_sysfs.build_node(tmp_path / "r", compute_partition="CPX")
+    p = subprocess.run([str(B.NATIVE_BIN / "kfd-probe"), "--sysfs-root",
+                        str(root / "sys/class/kfd/kfd/topology"), "--dev-root", str(root / "dev"),
+                        "--no-open", "--expect-gpus", "64"], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+    doc = json.loads(p.stdout)
+    assert doc["gpus"] == 64 and {a["cu"] for a in doc["agents"]} == {32}
+    assert {a["num_xcc"] for a in doc["agents"]} == {1}
+
+
+def test_plugin_step_schedules_a_gpu_pod(tmp_path, cfg, monkeypatch):
+    api = FakeKubeAPI().start()
+    api.add_node("gpu-node-1")
+    api.pods[("amd-gpu-operator", "validator-xyz")] = {
+        "metadata": {"name": "validator-xyz", "namespace": "amd-gpu-operator"},
+        "spec": {"nodeName": "gpu-node-1", "initContainers": [
+            {"name": "driver-validation", "image": "ghcr.io/example-org/amd-gpu-operator:9.9.9"}],
+            "containers": []},
+        "status": {"phase": "Running"}}
+    created = []
+
+    def kubelet(a, pod):  # play kubelet: the pod ran and printed the reference protocol
+        created.append(pod)
+        pod["status"]["phase"] = "Succeeded"
+        a.logs[("amd-gpu-operator", pod["metadata"]["name"])] = VECTORADD_LOG
+
+    api.on_pod_created = kubelet
+    monkeypatch.setenv("POD_NAME", "validator-xyz")
+    monkeypatch.setenv("POD_NAMESPACE", "amd-gpu-operator")
+    try:
+        v = Validator(cfg, str(tmp_path), kube=KubeClient(base_url=api.url), node_name="gpu-node-1")
+        r = v.run_step("plugin")
+        assert r.passed, r.reason
+        (pod,) = created
+        c = pod["spec"]["containers"][0]
+        assert c["resources"]["limits"] == {"amd.com/gpu": "1"}
+        assert c["image"] == "ghcr.io/example-org/amd-gpu-operator:9.9.9"
+        assert pod["spec"]["runtimeClassName"] == "amd" and pod["spec"]["nodeName"] == "gpu-node-1"
+        assert ("amd-gpu-operator", pod["metadata"]["name"]) not in api.pods  # cleaned up
+        # report: label the node
+        for s in ("driver", "runtime", "vectoradd", "gemm", "rccl"):
+            (tmp_path / f"{s}-ready").write_text("1")
+        rep = v.run_step("report")
+        assert rep.passed and api.nodes["gpu-node-1"]["metadata"]["labels"]["amd.com/gpu.validated"] == "true"
+        assert (tmp_path / "validator-ready").exists()
+        os.unlink(tmp_path / "gemm-ready")
+        rep2 = v.run_step("report")
+        assert not rep2.passed and "gemm" in rep2.reason
+        assert api.nodes["gpu-node-1"]["metadata"]["labels"]["amd.com/gpu.validated"] == "false"
+    finally:
+        api.stop()
