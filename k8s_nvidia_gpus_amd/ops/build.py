@@ -74,6 +74,8 @@ NATIVE_TARGETS: List[NativeTarget] = [
     NativeTarget("rccl-allreduce-bench", ["native/src/rccl_allreduce_bench.hip"], "hipcc",
                  libs=["-lrccl", "-lpthread"]),
     NativeTarget("kfd-probe", ["native/src/kfd_probe.cpp", "native/src/kfd_topology.cpp"], "cxx"),
+    NativeTarget("amd-container-runtime", ["native/src/amd_container_runtime.cpp"], "cxx",
+                 extra_flags=["-static-libstdc++", "-static-libgcc"]),
 ]
 
 
