@@ -256,11 +256,27 @@ class GenerationWorker:
                 j.done.set()
 
 
+try:
+    from pydantic import BaseModel
+
+    class GenReq(BaseModel):
+        """Request body of POST /generate (same fields and defaults as the reference's GenReq)."""
+
+        prompt: str
+        steps: Optional[int] = 30
+        guidance_scale: Optional[float] = 7.5
+        seed: Optional[int] = None
+        width: Optional[int] = 512
+        height: Optional[int] = 512
+        negative_prompt: Optional[str] = None
+except ImportError:  # pragma: no cover - pydantic ships with fastapi in the serving image
+    GenReq = None
+
+
 def create_app(settings: Optional[Settings] = None,
                pipeline_factory: Optional[Callable[[Settings], Any]] = None):
     from fastapi import FastAPI, HTTPException
     from fastapi.responses import HTMLResponse, PlainTextResponse, Response
-    from pydantic import BaseModel
 
     try:
         import prometheus_client as prom
@@ -281,15 +297,6 @@ def create_app(settings: Optional[Settings] = None,
                                  buckets=(1, 2, 4, 8, 16, 32), registry=registry)
         prom.Gauge("sd15_queue_depth", "queued requests", registry=registry).set_function(
             worker.queue_depth)
-
-    class GenReq(BaseModel):
-        prompt: str
-        steps: Optional[int] = 30
-        guidance_scale: Optional[float] = 7.5
-        seed: Optional[int] = None
-        width: Optional[int] = 512
-        height: Optional[int] = 512
-        negative_prompt: Optional[str] = None
 
     app = FastAPI(title="SD1.5 API (MI355X)")
     app.state.worker = worker

@@ -1,0 +1,331 @@
+"""Static/offline checks of the GitOps tree, Ansible layer and Renovate config (SURVEY.md §4 layer 1).
+
+The reference has no automated tests; its correctness is only ever checked by applying it to a
+live cluster.  These checks catch, offline, the classes of defects the survey found in it:
+Flux-only fields inside a kustomize file (reference gpu-operator/kustomization.yaml:8-9),
+deprecated Flux APIs (apps-kustomization.yaml v1beta2), dangling references (the unused
+sd15-api/helmrelease.yaml pointing at an undefined HelmRepository), env-var GPU visibility
+(NVIDIA_VISIBLE_DEVICES=all), `:latest` images, and a Renovate regex that must keep matching.
+"""
+import re
+from pathlib import Path
+
+import pytest
+import yaml
+
+REPO = Path(__file__).resolve().parent.parent
+CC = REPO / "cluster-config"
+ANS = REPO / "rke2-installation"
+
+
+def load_all(path: Path):
+    return [d for d in yaml.safe_load_all(path.read_text()) if d is not None]
+
+
+def all_yaml(base: Path):
+    return sorted(p for p in base.rglob("*") if p.suffix in (".yaml", ".yml"))
+
+
+def kustomization_dirs():
+    return sorted(p.parent for p in CC.rglob("kustomization.yaml"))
+
+
+def resources_of(kdir: Path):
+    k = yaml.safe_load((kdir / "kustomization.yaml").read_text())
+    out = []
+    for r in k.get("resources", []):
+        if r.startswith("https://"):
+            continue
+        p = kdir / r
+        if p.is_dir():
+            out.extend(resources_of(p))
+        else:
+            out.extend(load_all(p))
+    return k, out
+
+
+# ----------------------------------------------------------------------------- YAML + kustomize
+@pytest.mark.parametrize("path", all_yaml(CC) + all_yaml(ANS), ids=lambda p: str(p.relative_to(REPO)))
+def test_every_yaml_parses(path):
+    if path.name.endswith(".j2"):
+        return
+    load_all(path)
+
+
+@pytest.mark.parametrize("kdir", kustomization_dirs(), ids=lambda p: str(p.relative_to(REPO)))
+def test_kustomization_resources_resolve_and_are_pure_kustomize(kdir):
+    k = yaml.safe_load((kdir / "kustomization.yaml").read_text())
+    assert k["apiVersion"] == "kustomize.config.k8s.io/v1beta1" and k["kind"] == "Kustomization"
+    allowed = {"apiVersion", "kind", "namespace", "resources", "labels", "images",
+               "configMapGenerator", "patches", "commonAnnotations", "generatorOptions"}
+    extra = set(k) - allowed
+    assert not extra, f"non-kustomize fields (Flux-only?) in {kdir}: {extra}"
+    for r in k.get("resources", []):
+        if r.startswith("https://"):
+            assert re.search(r"/releases/download/v\d", r), f"unpinned remote resource {r}"
+            continue
+        assert (kdir / r).exists(), f"{kdir}: missing resource {r}"
+    for gen in k.get("configMapGenerator", []):
+        for f in gen.get("files", []):
+            assert (kdir / f.split("=")[-1]).exists(), f"{kdir}: missing generator file {f}"
+
+
+def flux_kustomizations():
+    docs = load_all(CC / "cluster/flux-system/apps-kustomization.yaml") + \
+        load_all(CC / "cluster/flux-system/gotk-sync.yaml")
+    return [d for d in docs if d.get("kind") == "Kustomization"]
+
+
+def test_flux_kustomizations_use_ga_api_and_resolve():
+    ks = flux_kustomizations()
+    names = {k["metadata"]["name"] for k in ks}
+    sources = {d["metadata"]["name"] for d in load_all(CC / "cluster/flux-system/gotk-sync.yaml")
+               if d["kind"] == "GitRepository"}
+    assert {"amd-gpu-operator", "renovate", "llm", "sd15-api", "gpu-bench", "flux-system"} <= names
+    for k in ks:
+        assert k["apiVersion"] == "kustomize.toolkit.fluxcd.io/v1", k["metadata"]["name"]
+        path = REPO / k["spec"]["path"].lstrip("./")
+        assert path.is_dir(), k["spec"]["path"]
+        if k["metadata"]["name"] != "flux-system":
+            assert (path / "kustomization.yaml").exists()
+        assert k["spec"]["sourceRef"]["name"] in sources
+        for dep in k["spec"].get("dependsOn", []):
+            assert dep["name"] in names, f"{k['metadata']['name']} dependsOn unknown {dep['name']}"
+
+
+def test_gpu_workloads_depend_on_the_operator():
+    ks = {k["metadata"]["name"]: k for k in flux_kustomizations()}
+    for name in ("llm", "sd15-api", "gpu-bench"):
+        assert "amd-gpu-operator" in [d["name"] for d in ks[name]["spec"].get("dependsOn", [])]
+    assert ks["amd-gpu-operator"]["spec"]["wait"] is True
+
+
+def test_flux_bootstrap_entry():
+    k = yaml.safe_load((CC / "cluster/flux-system/kustomization.yaml").read_text())
+    assert k["namespace"] == "flux-system"
+    comp = yaml.safe_load((CC / "cluster/flux-system/gotk-components/kustomization.yaml").read_text())
+    (url,) = comp["resources"]
+    assert "fluxcd/flux2/releases/download/v2.5.1/install.yaml" in url  # same Flux as the reference
+
+
+# ----------------------------------------------------------------------------- workloads
+def pod_specs(objs):
+    for o in objs:
+        kind = o.get("kind")
+        if kind in ("Deployment", "DaemonSet", "StatefulSet", "Job"):
+            yield o, o["spec"]["template"]["spec"]
+        elif kind == "CronJob":
+            yield o, o["spec"]["jobTemplate"]["spec"]["template"]["spec"]
+        elif kind == "Pod":
+            yield o, o["spec"]
+
+
+def all_objects():
+    for kdir in kustomization_dirs():
+        if kdir.name in ("flux-system", "gotk-components"):
+            continue
+        k, objs = resources_of(kdir)
+        yield kdir, k, objs
+
+
+def _gpu_request(c):
+    res = c.get("resources", {}) or {}
+    return any("amd.com/gpu" in (res.get(x) or {}) for x in ("limits", "requests"))
+
+
+def test_gpu_pods_request_amd_gpu_with_runtime_class_and_no_visibility_env():
+    seen = 0
+    for kdir, k, objs in all_objects():
+        for o, spec in pod_specs(objs):
+            containers = spec.get("containers", []) + spec.get("initContainers", [])
+            if any(_gpu_request(c) for c in containers):
+                seen += 1
+                assert spec.get("runtimeClassName") == "amd", f"{kdir}/{o['metadata']['name']}"
+            for c in containers:
+                for e in c.get("env", []) or []:
+                    assert not re.match(r"(NVIDIA_|CUDA_|HIP_VISIBLE|ROCR_VISIBLE|AMD_VISIBLE)", e["name"]), \
+                        f"{o['metadata']['name']}: visibility/NVIDIA env {e['name']}"
+                res = c.get("resources", {}) or {}
+                for part in ("limits", "requests"):
+                    assert not any(x.startswith("nvidia.com") for x in (res.get(part) or {}))
+    assert seen >= 6  # llm, sd15, 4 gpu-bench jobs ...
+
+
+def test_no_nvidia_or_cuda_left_in_manifest_values():
+    bad = re.compile(r"nvidia|cuda", re.I)
+    for kdir, k, objs in all_objects():
+        for o in objs:
+            # the project's own package name (k8s-nvidia-gpus_amd) is not an NVIDIA dependency
+            text = re.sub(r"k8s[_-]nvidia[_-]gpus(_amd)?", "PKG", yaml.safe_dump(o))
+            assert not bad.search(text), f"{kdir}: {o['kind']}/{o['metadata']['name']} mentions NVIDIA/CUDA"
+
+
+def test_images_are_pinned():
+    for kdir, k, objs in all_objects():
+        for o, spec in pod_specs(objs):
+            for c in spec.get("containers", []) + spec.get("initContainers", []):
+                img = c["image"]
+                assert not img.endswith(":latest"), img
+                if img in ("amd-gpu-operator", "amd-gpu-bench"):
+                    assert any(i["name"] == img for i in k.get("images", [])), f"{kdir}: {img} not rewritten"
+                else:
+                    assert ":" in img, f"unpinned image {img}"
+
+
+def test_namespaced_objects_match_kustomization_namespace():
+    for kdir, k, objs in all_objects():
+        ns = k.get("namespace")
+        declared = {o["metadata"]["name"] for o in objs if o["kind"] == "Namespace"}
+        for o in objs:
+            if o["kind"] in ("Namespace", "PersistentVolume", "ClusterRole", "ClusterRoleBinding",
+                             "RuntimeClass", "CustomResourceDefinition"):
+                continue
+            got = o["metadata"].get("namespace", ns)
+            assert got == ns, f"{kdir}: {o['kind']}/{o['metadata']['name']} in {got} != {ns}"
+            assert ns in declared or kdir.name == "gateway-api", f"{kdir}: namespace {ns} not declared"
+
+
+def test_operator_daemonsets_gate_on_markers_and_share_config():
+    _, objs = resources_of(CC / "apps/amd-gpu-operator")
+    ds = {o["metadata"]["name"]: o for o in objs if o["kind"] == "DaemonSet"}
+    assert set(ds) == {"amd-gpu-driver", "amd-gpu-runtime", "amd-gpu-device-plugin",
+                       "amd-gpu-node-labeller", "amd-gpu-metrics-exporter",
+                       "amd-gpu-partition-manager", "amd-gpu-validator"}
+    for name, d in ds.items():
+        spec = d["spec"]["template"]["spec"]
+        assert any(v.get("configMap", {}).get("name") == "amd-gpu-operator-config"
+                   for v in spec["volumes"]), name
+        if name not in ("amd-gpu-driver", "amd-gpu-node-labeller"):
+            assert spec["nodeSelector"] == {"amd.com/gpu.present": "true"}, name
+    val = ds["amd-gpu-validator"]["spec"]["template"]["spec"]
+    steps = [c["command"][-1] for c in val["initContainers"]]
+    assert steps == ["--step=driver", "--step=runtime", "--step=vectoradd", "--step=gemm",
+                     "--step=rccl", "--step=plugin"]
+    plug = ds["amd-gpu-device-plugin"]["spec"]["template"]["spec"]
+    assert {"driver-ready", "runtime-ready"} <= {m.split("/")[-1] for m in plug["initContainers"][0]["command"] if "ready" in m}
+    rc = [o for o in objs if o["kind"] == "RuntimeClass"][0]
+    assert rc["handler"] == "amd" and rc["metadata"]["name"] == "amd"
+
+
+def test_sd15_app_source_in_sync_and_no_pypi_torch():
+    app = (CC / "apps/sd15-api/app/app.py").read_text()
+    assert app == (REPO / "k8s_nvidia_gpus_amd/models/sd15_api.py").read_text(), \
+        "run: python -m k8s_nvidia_gpus_amd.utils.sync_apps"
+    reqs = (CC / "apps/sd15-api/app/requirements.txt").read_text().splitlines()
+    pkgs = [r.split("==")[0].split("[")[0].strip().lower() for r in reqs if r.strip() and not r.startswith("#")]
+    assert "torch" not in pkgs and "torchvision" not in pkgs
+
+
+def test_sd15_service_keeps_reference_nodeport():
+    svc = load_all(CC / "apps/sd15-api/service.yaml")[0]
+    assert svc["spec"]["ports"][0]["nodePort"] == 30800
+
+
+# ----------------------------------------------------------------------------- renovate
+def _py_regex(js: str) -> str:
+    return js.replace("(?<", "(?P<")
+
+
+def test_renovate_regexes_match_annotated_pins():
+    import json
+
+    cfg = json.loads((REPO / "renovate.json").read_text())
+    managers = cfg["customManagers"]
+    bundles = next(m for m in managers if "bundles" in m["managerFilePatterns"][0])
+    rx = re.compile(_py_regex(bundles["matchStrings"][0]))
+    found = [m.groupdict() for m in rx.finditer((REPO / "bundles.yaml").read_text())]
+    assert {f["depName"] for f in found} == {"nginx", "rocm/pytorch", "rocm/dev-ubuntu-22.04"}
+    assert {"datasource": "docker", "depName": "nginx", "registryUrl": "https://registry-1.docker.io",
+            "currentValue": "1.28.0"} in found
+    # every "# renovate:" annotation in the manifests is captured by one of the managers
+    img_rx = [re.compile(_py_regex(s)) for m in managers for s in m["matchStrings"]]
+    for path in list(CC.rglob("*.yaml")) + [ANS / "group_vars/all.yaml"]:
+        text = path.read_text()
+        n_ann = text.count("# renovate:")
+        if not n_ann:
+            continue
+        hits = sum(len(list(r.finditer(text))) for r in img_rx)
+        assert hits >= n_ann, f"{path}: {n_ann} annotations, {hits} regex matches"
+
+
+def test_renovate_cronjob_hardened():
+    cj = load_all(CC / "apps/renovate/cronjob.yaml")[0]
+    assert cj["spec"]["concurrencyPolicy"] == "Forbid"
+    pod = cj["spec"]["jobTemplate"]["spec"]["template"]["spec"]
+    assert pod["automountServiceAccountToken"] is False
+    assert pod["securityContext"]["runAsNonRoot"] is True
+    tok = [e for e in pod["containers"][0]["env"] if e["name"] == "RENOVATE_TOKEN"][0]
+    assert tok["valueFrom"]["secretKeyRef"] == {"name": "renovate-secrets", "key": "RENOVATE_TOKEN"}
+
+
+def test_bundles_point_at_rke2_not_k3s():
+    for b in yaml.safe_load((REPO / "bundles.yaml").read_text())["bundles"]:
+        assert "/rke2/" in b["info_path"] and "k3s" not in b["info_path"]
+
+
+# ----------------------------------------------------------------------------- ansible
+def _inventory_groups():
+    groups = {}
+    cur = None
+    for line in (ANS / "inventory.ini").read_text().splitlines():
+        line = line.strip()
+        if not line or line.startswith(("#", ";")):
+            continue
+        if line.startswith("["):
+            cur = line.strip("[]")
+            groups[cur] = []
+        elif cur:
+            groups[cur].append(line.split()[0])
+    return groups
+
+
+def test_inventory_layout_matches_reference():
+    g = _inventory_groups()
+    assert g["masters"] == ["masters-01"]
+    assert g["k8s_cluster:children"] == ["masters"]
+
+
+def test_playbooks_target_existing_groups_and_roles():
+    groups = set(_inventory_groups()) | {"all"}
+    for pb in ("install-rke2.yaml", "fetch-kubeconfig.yaml", "uninstall-rke2.yaml"):
+        plays = load_all(ANS / pb)[0]
+        for play in plays:
+            assert play["hosts"] in groups, f"{pb}: hosts {play['hosts']}"
+            for role in play.get("roles", []):
+                name = role["role"] if isinstance(role, dict) else role
+                if name == "lablabs.rke2":
+                    continue  # Galaxy role, auto-installed by the play
+                assert (ANS / "roles" / name / "tasks" / "main.yaml").exists(), name
+
+
+def test_group_vars_have_rke2_inputs_and_no_plaintext_token():
+    v = yaml.safe_load((ANS / "group_vars/all.yaml").read_text())
+    for k in ("rke2_ha_mode", "rke2_version", "rke2_role", "rke2_node_name", "rke2_node_ip",
+              "rke2_server", "rke2_token", "rke2_cni"):
+        assert k in v, k
+    assert "lookup(" in v["rke2_token"], "join token must not be committed in plain text"
+    assert v["rke2_cni"] == ["cilium"]
+    assert v["amd_gpu_min_gfx_target"] == 90500
+
+
+def test_amd_host_prep_role_files_exist():
+    role = ANS / "roles/amd-host-prep"
+    main = load_all(role / "tasks/main.yaml")[0]
+    for t in main:
+        inc = t.get("ansible.builtin.import_tasks")
+        if inc:
+            assert (role / "tasks" / inc).exists(), inc
+    for t in load_all(role / "tasks/containerd.yaml")[0]:
+        tpl = t.get("ansible.builtin.template")
+        if tpl:
+            assert (role / "templates" / tpl["src"]).exists()
+    tmpl = (role / "templates/config-v3.toml.tmpl.j2").read_text()
+    assert 'template "base"' in tmpl and "BinaryName" in tmpl and "amd.com/gpu.*" in tmpl
+
+
+def test_uninstall_finds_cli_tools_on_the_node_not_the_controller():
+    plays = load_all(ANS / "uninstall-rke2.yaml")[0]
+    text = yaml.safe_dump(plays)  # comments stripped
+    assert "first_found" not in text  # the reference's lookup ran on the control host
+    pre = plays[0]["pre_tasks"]
+    assert any("ansible.builtin.stat" in t and "rke2_cli_dirs" in str(t.get("loop")) for t in pre)
