@@ -4,8 +4,9 @@
 BASELINE.json names the metric "validator-pod bf16 GEMM TFLOPS/GPU + time-to-first-GPU-pod,
 1/2/4/8 MI355X".  One *step* is what the operator's validator pod runs on each GPU it was
 allocated: one 8192×8192×8192 bf16 GEMM (C = A·Bᵀ, fp32 accumulate, bf16 out) through the
-hand-written gfx950 MFMA kernel (k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950.hip), on random
-[-1,1) operands (synthetic data).  Work per GPU is fixed as N grows → weak scaling.
+hand-written gfx950 MFMA kernels (k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950*.hip, variant
+picked by operand footprint), on random [-1,1) operands (synthetic data).  Work per GPU is fixed as
+N grows → weak scaling.
 
 Launch contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 under
 ``torch.distributed.run`` with one rank per GPU (RCCL backend).  W untimed steps, then exactly K
@@ -15,8 +16,11 @@ rank 0 prints ONE JSON line.  ``value`` is the whole-job aggregate TFLOPS over a
 Outside the timed region it also reports:
 * ``time_to_first_gpu_result_s`` — process start → first verified GPU result (HIP vectorAdd,
   reference protocol), the in-process part of the "time-to-first-GPU-pod" metric;
-* ``numerics`` — sampled max error of the timed kernel against an fp32 on-device reference;
+* ``numerics_max_rel_err`` — sampled error of the timed kernel against an fp32 on-device reference;
 * ``allreduce_busbw_gbps`` — RCCL all-reduce bus bandwidth over xGMI across the N ranks (N > 1).
+
+``--cpu-smoke`` exercises the same launch/timing/JSON path on CPU (fp32 torch.matmul, gloo) for
+tests; its numbers are not measurements and are labelled as such.
 """
 from __future__ import annotations
 
@@ -32,8 +36,6 @@ import sys  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from k8s_nvidia_gpus_amd.ops import kernels as K  # noqa: E402
-
 METRIC = "validator-pod bf16 GEMM TFLOPS/GPU + time-to-first-GPU-pod, 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # BASELINE.json "published": {} — the reference publishes no numbers
 
@@ -44,25 +46,26 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--size", type=int, default=8192, help="M = N = K of the validator GEMM")
+    ap.add_argument("--variant", default=None, help="GEMM variant (auto | w8 | w4)")
     ap.add_argument("--allreduce-mib", type=int, default=256,
                     help="message size of the post-run RCCL all-reduce probe (N > 1)")
     ap.add_argument("--no-allreduce", action="store_true")
+    ap.add_argument("--cpu-smoke", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
-def first_gpu_result(device: torch.device) -> float:
+def first_gpu_result(K, device: torch.device) -> float:
     """Reference-protocol vectorAdd (50 000 fp32, 196×256) — returns seconds since process start."""
     n = 50000
     g = torch.Generator().manual_seed(1234)
     ha, hb = torch.rand(n, generator=g), torch.rand(n, generator=g)
     c = K.vector_add(ha.to(device), hb.to(device))
-    ok = torch.allclose(c.cpu(), ha + hb, atol=1e-5, rtol=0)
-    if not ok:
+    if not torch.allclose(c.cpu(), ha + hb, atol=1e-5, rtol=0):
         raise RuntimeError("vectorAdd verification failed")
     return time.time() - _T_PROCESS_START
 
 
-def check_numerics(a, b, c, samples: int = 1024) -> float:
+def check_numerics(K, a, b, c, samples: int = 1024) -> float:
     m, n = c.shape
     g = torch.Generator().manual_seed(7)
     coords = torch.stack([torch.randint(0, m, (samples,), generator=g),
@@ -78,88 +81,97 @@ def check_numerics(a, b, c, samples: int = 1024) -> float:
     return float((err / (ref.abs() + 1.0)).max().item())
 
 
-def allreduce_probe(device, world: int, mib: int) -> float:
-    count = mib * 1024 * 1024 // 4
-    x = torch.ones(count, dtype=torch.float32, device=device)
-    for _ in range(3):
-        dist.all_reduce(x)
-    torch.cuda.synchronize(device)
-    dist.barrier()
-    iters = 10
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        dist.all_reduce(x)
-    torch.cuda.synchronize(device)
-    dt = (time.perf_counter() - t0) / iters
-    t = torch.tensor([dt], device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    algbw = count * 4 / t.item() / 1e9
-    return algbw * 2 * (world - 1) / world
-
-
 def main(argv=None) -> int:
     args = parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
-              file=sys.stderr)
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     distributed = world > 1
-    if not torch.cuda.is_available():
+    smoke = args.cpu_smoke
+    if not smoke and not torch.cuda.is_available():
         print("bench.py needs an MI355X (no GPU visible)", file=sys.stderr)
         return 2
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
-    if distributed:
-        dist.init_process_group(backend="nccl", device_id=device)
+    from k8s_nvidia_gpus_amd.parallel.collectives import init_distributed, measure
 
-    ttfr = first_gpu_result(device)
+    if distributed:
+        device = init_distributed("gloo" if smoke else "nccl")
+    elif smoke:
+        device = torch.device("cpu")
+    else:
+        device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(device)
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
 
     s = args.size
-    if not K.gemm_shape_supported(s, s, s):
-        raise SystemExit(f"--size {s} must be a multiple of 256")
-    a = torch.empty((s, s), dtype=torch.bfloat16, device=device)
-    b = torch.empty((s, s), dtype=torch.bfloat16, device=device)
-    c = torch.empty((s, s), dtype=torch.bfloat16, device=device)
-    K.fill_uniform_bf16(a, seed=1000 + rank)
-    K.fill_uniform_bf16(b, seed=2000 + rank)
-    K.gemm_bf16_nt(a, b, out=c)
-    max_rel_err = check_numerics(a, b, c)
+    max_rel_err = None
+    ttfr = None
+    variant = None
+    if smoke:
+        a = torch.rand((s, s)) * 2 - 1
+        b = torch.rand((s, s)) * 2 - 1
+        c = torch.empty((s, s))
+
+        def step():
+            torch.matmul(a, b.t(), out=c)
+    else:
+        from k8s_nvidia_gpus_amd.ops import kernels as K
+
+        ttfr = first_gpu_result(K, device)
+        if not K.gemm_shape_supported(s, s, s):
+            raise SystemExit(f"--size {s} must be a multiple of 256")
+        a = torch.empty((s, s), dtype=torch.bfloat16, device=device)
+        b = torch.empty((s, s), dtype=torch.bfloat16, device=device)
+        c = torch.empty((s, s), dtype=torch.bfloat16, device=device)
+        K.fill_uniform_bf16(a, seed=1000 + rank)
+        K.fill_uniform_bf16(b, seed=2000 + rank)
+        variant = args.variant or K.DEFAULT_GEMM_VARIANT
+        if variant == "auto":
+            variant = K.pick_gemm_variant(s, s, s)
+        K.gemm_bf16_nt(a, b, out=c, variant=variant)
+        max_rel_err = check_numerics(K, a, b, c)
+
+        def step():
+            K.gemm_bf16_nt(a, b, out=c, variant=variant)
 
     for _ in range(args.warmup):
-        K.gemm_bf16_nt(a, b, out=c)
-    torch.cuda.synchronize(device)
+        step()
+    sync()
     if distributed:
         dist.barrier()
-    torch.cuda.synchronize(device)
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        K.gemm_bf16_nt(a, b, out=c)
-    torch.cuda.synchronize(device)
+        step()
+    sync()
     if distributed:
         dist.barrier()
-    torch.cuda.synchronize(device)
+    sync()
     elapsed = time.perf_counter() - t0
 
-    per_gpu_tflops_local = 2.0 * s * s * s * args.steps / elapsed / 1e12
+    flop_per_gpu = 2.0 * s * s * s * args.steps
+    per_rank = [round(flop_per_gpu / elapsed / 1e12, 2)]
     if distributed:
-        t = torch.tensor([elapsed, ttfr], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed, ttfr or 0.0], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, ttfr = float(t[0].item()), float(t[1].item())
-        pg = torch.tensor([per_gpu_tflops_local], device=device, dtype=torch.float64)
-        gathered = [torch.zeros_like(pg) for _ in range(world)]
-        dist.all_gather(gathered, pg)
-        per_rank = [round(float(x.item()), 1) for x in gathered]
-    else:
-        per_rank = [round(per_gpu_tflops_local, 1)]
+        elapsed = float(t[0].item())
+        ttfr = float(t[1].item()) if ttfr is not None else None
+        mine = torch.tensor([per_rank[0]], device=device, dtype=torch.float64)
+        gathered = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(gathered, mine)
+        per_rank = [round(float(x.item()), 2) for x in gathered]
     busbw = None
     if distributed and not args.no_allreduce:
-        busbw = allreduce_probe(device, world, args.allreduce_mib)
+        r = measure("all_reduce", (1 if smoke else args.allreduce_mib) << 20, iters=3 if smoke else 10,
+                    warmup=1 if smoke else 3, device=device)
+        if r.wrong:
+            raise RuntimeError(f"all-reduce returned {r.wrong} wrong elements")
+        busbw = r.busbw_gbps
 
-    total_flops = 2.0 * s * s * s * args.steps * world
-    value = total_flops / elapsed / 1e12
-    ms_per_step = elapsed / args.steps * 1e3
+    value = flop_per_gpu * world / elapsed / 1e12
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -168,26 +180,27 @@ def main(argv=None) -> int:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(value / BASELINE_VALUE, 3) if BASELINE_VALUE else None),
-            "dtype": "bf16",
-            "data": "synthetic (uniform [-1,1) bf16 operands generated on device)",
+            "dtype": "fp32 (cpu smoke test, not a measurement)" if smoke else "bf16",
+            "data": "synthetic (uniform [-1,1) operands generated on device)",
             "config": {
                 "model": f"validator bf16 MFMA GEMM {s}x{s}x{s} (C=A*B^T, hand-written gfx950 kernel)",
                 "global_batch": world,
                 "seq_len": s,
                 "parallelism": f"dp{world}" if world > 1 else "single",
                 "m": s, "n": s, "k": s,
-                "kernel": "amdk8s_gemm_bf16_nt_256x256",
+                "kernel": {"w8": "amdk8s_gemm_bf16_nt_256x256", "w4": "amdk8s_gemm_bf16_nt_256x256_w4"}
+                .get(variant, "torch.matmul (cpu smoke)"),
             },
             "tflops_per_gpu": round(value / world, 2),
             "tflops_per_rank": per_rank,
-            "time_to_first_gpu_result_s": round(ttfr, 3),
+            "time_to_first_gpu_result_s": round(ttfr, 3) if ttfr is not None else None,
             "numerics_max_rel_err": max_rel_err,
             "allreduce_busbw_gbps": (round(busbw, 2) if busbw is not None else None),
-            "device": torch.cuda.get_device_name(device),
+            "device": torch.cuda.get_device_name(device) if device.type == "cuda" else "cpu",
         }
         print(json.dumps(out), flush=True)
     if distributed:

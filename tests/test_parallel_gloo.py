@@ -1,0 +1,106 @@
+"""Collectives + gradient bucketing across real processes on the gloo backend (CPU, world 2 and 4)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+import torch.multiprocessing as mp
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch
+    import torch.distributed as dist
+
+    from k8s_nvidia_gpus_amd.parallel import collectives as C
+
+    try:
+        C.init_distributed("gloo")
+        out = {}
+        for op in ("all_reduce", "all_gather", "reduce_scatter", "all_to_all", "broadcast"):
+            r = C.measure(op, 1 << 16, iters=3, warmup=1)
+            out[op] = (r.wrong, r.world, r.bytes, r.busbw_gbps > 0)
+        rows = C.sweep("all_reduce", 1 << 10, 1 << 14, factor=4, iters=2, warmup=1)
+        out["sweep"] = [r.bytes for r in rows]
+        # bucketed gradient all-reduce: rank r holds r+1 → average (world+1)/2 everywhere
+        tensors = [torch.full((n,), float(rank + 1)) for n in (1000, 3, 70000, 12)]
+        tensors.append(torch.full((5,), float(rank + 1), dtype=torch.float64))
+        b = C.GradientBucketer(tensors, bucket_bytes=64 * 1024)
+        b.start()
+        b.wait()
+        out["buckets"] = len(b.buckets)
+        out["avg_ok"] = all(bool((t == (world + 1) / 2).all()) for t in tensors)
+        q.put((rank, out))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - surfaced in the parent
+        q.put((rank, {"error": repr(e)}))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_collectives_correct_on_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, out in res.items():
+        assert "error" not in out, out
+        for op in ("all_reduce", "all_gather", "reduce_scatter", "all_to_all", "broadcast"):
+            wrong, w, nbytes, positive = out[op]
+            assert wrong == 0 and w == world and positive, (op, out[op])
+        assert out["sweep"] == [1024, 4096, 16384]
+        assert out["avg_ok"] and out["buckets"] >= 3  # fp64 tensor forces its own bucket
+
+
+def test_busbw_factors():
+    from k8s_nvidia_gpus_amd.parallel.collectives import BUSBW_FACTOR
+
+    assert BUSBW_FACTOR["all_reduce"](8) == pytest.approx(1.75)
+    assert BUSBW_FACTOR["all_gather"](8) == pytest.approx(0.875)
+
+
+def _torchrun(args, nproc, timeout=300):
+    env = dict(os.environ, PYTHONPATH=str(REPO), OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
+    return subprocess.run(cmd, capture_output=True, text=True, env=env, cwd=str(REPO), timeout=timeout)
+
+
+def test_parallel_bench_cli_under_torchrun_gloo():
+    p = _torchrun(["-m", "k8s_nvidia_gpus_amd.parallel.bench", "--backend", "gloo", "--op",
+                   "all_reduce", "-b", "4K", "-e", "64K", "-n", "2", "-w", "1"], 2)
+    assert p.returncode == 0, p.stderr[-2000:]
+    doc = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert doc["passed"] and doc["world"] == 2 and doc["wrong"] == 0
+
+
+def test_bench_py_distributed_contract_on_cpu():
+    """bench.py --cpu-smoke under torchrun (gloo): one JSON line, MAX over ranks, N-rank aggregate."""
+    p = _torchrun(["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--cpu-smoke",
+                   "--size", "256"], 2)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    doc = json.loads(lines[0])
+    assert doc["n_gpus"] == 2 and doc["steps"] == 2 and doc["warmup"] == 1
+    assert doc["higher_is_better"] is True and doc["scaling"] == "weak"
+    assert doc["config"]["parallelism"] == "dp2"
+    assert len(doc["tflops_per_rank"]) == 2
+    assert doc["value"] == pytest.approx(sum(doc["tflops_per_rank"]), rel=0.6)
