@@ -70,6 +70,7 @@ NATIVE_TARGETS: List[NativeTarget] = [
                                    "k8s_nvidia_gpus_amd/ops/csrc/vector_add.hip"], "hipcc"),
     NativeTarget("amd-gemm-validator", ["native/src/amd_gemm_validator.hip",
                                         "k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950.hip",
+                                        "k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950_w4.hip",
                                         "k8s_nvidia_gpus_amd/ops/csrc/fill.hip"], "hipcc"),
     NativeTarget("rccl-allreduce-bench", ["native/src/rccl_allreduce_bench.hip"], "hipcc",
                  libs=["-lrccl", "-lpthread"]),

@@ -23,12 +23,23 @@
 
 namespace {
 
+// Kernel variant: "w8" (8 waves, 2/SIMD), "w4" (4 waves, 1/SIMD, 128x128 per wave) or "auto"
+// (w4 while A+B fit the 256 MiB Infinity Cache, else w8; docs/gemm_tuning.md).
+int gemm(const std::string& variant, const void* A, const void* B, void* C, int m, int n, int k,
+         hipStream_t s) {
+  const bool w4 = variant == "w4" ||
+                  (variant == "auto" && (double)(m + n) * k * 2 <= 192.0 * 1024 * 1024);
+  return w4 ? amdk8s_gemm_bf16_nt_w4(A, B, C, m, n, k, k, k, n, s)
+            : amdk8s_gemm_bf16_nt(A, B, C, m, n, k, k, k, n, s);
+}
+
 struct Options {
   int m = 8192, n = 8192, k = 8192;
   int iters = 50, warmup = 10;
   int device = -1;  // -1 = every visible device
   int samples = 2048;
   bool json = false;
+  std::string variant = "auto";
   unsigned long long seed = 42;
 };
 
@@ -83,7 +94,7 @@ void run(int dev, const Options& o, int nthreads, Result* r) {
   AMDK8S_HIP_CHECK(hipMalloc(&dref, o.samples * sizeof(float)));
   AMDK8S_HIP_CHECK(hipMemcpyAsync(dcoords, coords.data(), coords.size() * sizeof(int),
                                   hipMemcpyHostToDevice, s));
-  int rc = amdk8s_gemm_bf16_nt(A, B, C, o.m, o.n, o.k, o.k, o.k, o.n, s);
+  int rc = gemm(o.variant, A, B, C, o.m, o.n, o.k, s);
   if (rc != 0) {
     std::fprintf(stderr, "device %d: GEMM launch rejected (error %d): shape %dx%dx%d must be "
                  "multiples of 256x256x64\n", dev, rc, o.m, o.n, o.k);
@@ -114,7 +125,7 @@ void run(int dev, const Options& o, int nthreads, Result* r) {
   r->max_rel_err = worst;
 
   // timing: all device threads start the timed loop together
-  for (int i = 0; i < o.warmup; ++i) amdk8s_gemm_bf16_nt(A, B, C, o.m, o.n, o.k, o.k, o.k, o.n, s);
+  for (int i = 0; i < o.warmup; ++i) gemm(o.variant, A, B, C, o.m, o.n, o.k, s);
   AMDK8S_HIP_CHECK(hipStreamSynchronize(s));
   g_ready.fetch_add(1);
   while (g_ready.load() < nthreads) std::this_thread::yield();
@@ -122,7 +133,7 @@ void run(int dev, const Options& o, int nthreads, Result* r) {
   AMDK8S_HIP_CHECK(hipEventCreate(&e0));
   AMDK8S_HIP_CHECK(hipEventCreate(&e1));
   AMDK8S_HIP_CHECK(hipEventRecord(e0, s));
-  for (int i = 0; i < o.iters; ++i) amdk8s_gemm_bf16_nt(A, B, C, o.m, o.n, o.k, o.k, o.k, o.n, s);
+  for (int i = 0; i < o.iters; ++i) gemm(o.variant, A, B, C, o.m, o.n, o.k, s);
   AMDK8S_HIP_CHECK(hipEventRecord(e1, s));
   AMDK8S_HIP_CHECK(hipEventSynchronize(e1));
   float ms = 0;
@@ -161,9 +172,10 @@ int main(int argc, char** argv) {
     else if (a == "--samples") o.samples = std::atoi(next());
     else if (a == "--seed") o.seed = std::strtoull(next(), nullptr, 10);
     else if (a == "--json") o.json = true;
+    else if (a == "--variant") o.variant = next();
     else {
       std::printf("usage: amd-gemm-validator [--size S | --m M --n N --k K] [--iters I] "
-                  "[--warmup W] [--device D] [--samples S] [--json]\n");
+                  "[--warmup W] [--device D] [--samples S] [--variant auto|w8|w4] [--json]\n");
       return a == "-h" || a == "--help" ? 0 : 2;
     }
   }
