@@ -70,8 +70,9 @@ class AmdSmiBackend:
             return None
 
     def _identity(self, h) -> Dict[str, Any]:
-        if h in self._static:
-            return self._static[h]
+        key = getattr(h, "value", h) or 0  # real handles are ctypes.c_void_p (unhashable)
+        if key in self._static:
+            return self._static[key]
         asic = self._call("amdsmi_get_gpu_asic_info", h) or {}
         enum = self._call("amdsmi_get_gpu_enumeration_info", h) or {}
         kfd = self._call("amdsmi_get_gpu_kfd_info", h) or {}
@@ -87,7 +88,7 @@ class AmdSmiBackend:
         }
         drv = self._call("amdsmi_get_gpu_driver_info", h) or {}
         ident["driver"] = drv.get("driver_version", "unknown")[:48]
-        self._static[h] = ident
+        self._static[key] = ident
         return ident
 
     def samples(self) -> List[GpuSample]:

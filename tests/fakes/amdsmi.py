@@ -8,6 +8,7 @@ render minor, so exporter and partition-manager code paths run against real fiel
 from __future__ import annotations
 
 import copy
+import ctypes
 import enum
 import json
 from pathlib import Path
@@ -29,6 +30,15 @@ class AmdSmiMemoryPartitionType(enum.Enum):
     NPS1 = 0
     NPS2 = 1
     NPS4 = 2
+
+
+class Handle(ctypes.c_void_p):
+    """Like amdsmi's processor handles: a c_void_p (unhashable) that also indexes our tables."""
+
+    __hash__ = None
+
+    def __index__(self):
+        return int(self.value or 0)
 
 
 class FakeAmdSmi:
@@ -58,33 +68,34 @@ class FakeAmdSmi:
         self.inited = False
 
     def amdsmi_get_processor_handles(self):
-        return list(range(self.n))
+        # the real library returns ctypes.c_void_p handles, which are unhashable
+        return [Handle(i) for i in range(self.n)]
 
     def amdsmi_get_gpu_device_bdf(self, h):
-        return _LAYOUT["gpus"][h]["bdf"]
+        return _LAYOUT["gpus"][int(h)]["bdf"]
 
     def amdsmi_get_gpu_device_uuid(self, h):
-        return "%08x-0000-1000-8000-%012x" % (h, int(_LAYOUT["gpus"][h]["unique_id_hex"], 16) & 0xFFFFFFFFFFFF)
+        return "%08x-0000-1000-8000-%012x" % (int(h), int(_LAYOUT["gpus"][int(h)]["unique_id_hex"], 16) & 0xFFFFFFFFFFFF)
 
     def amdsmi_get_gpu_asic_info(self, h):
         return self._rec(h, "amdsmi_get_gpu_asic_info")
 
     def amdsmi_get_gpu_enumeration_info(self, h):
         r = self._rec(h, "amdsmi_get_gpu_enumeration_info")
-        r["drm_render"] = _LAYOUT["gpus"][h]["render"]
-        r["drm_card"] = _LAYOUT["gpus"][h]["card"]
-        r["hip_id"] = h
+        r["drm_render"] = _LAYOUT["gpus"][int(h)]["render"]
+        r["drm_card"] = _LAYOUT["gpus"][int(h)]["card"]
+        r["hip_id"] = int(h)
         return r
 
     def amdsmi_get_gpu_kfd_info(self, h):
-        return {"kfd_id": 1000 + h, "node_id": 2 + h, "current_partition_id": 0}
+        return {"kfd_id": 1000 + int(h), "node_id": 2 + int(h), "current_partition_id": 0}
 
     def amdsmi_get_gpu_driver_info(self, h):
         return self._rec(h, "amdsmi_get_gpu_driver_info")
 
     def amdsmi_get_gpu_metrics_info(self, h):
         r = self._rec(h, "amdsmi_get_gpu_metrics_info")
-        r["average_gfx_activity"] = 10 * h
+        r["average_gfx_activity"] = 10 * int(h)
         return r
 
     def amdsmi_get_gpu_vram_usage(self, h):
@@ -92,22 +103,22 @@ class FakeAmdSmi:
 
     def amdsmi_get_gpu_total_ecc_count(self, h):
         r = self._rec(h, "amdsmi_get_gpu_total_ecc_count")
-        r["uncorrectable_count"] = self.ecc_uncorrectable[h]
+        r["uncorrectable_count"] = self.ecc_uncorrectable[int(h)]
         return r
 
     def amdsmi_get_gpu_compute_partition(self, h):
-        return self.compute[h]
+        return self.compute[int(h)]
 
     def amdsmi_get_gpu_memory_partition(self, h):
-        return self.memory[h]
+        return self.memory[int(h)]
 
     def amdsmi_get_gpu_process_list(self, h):
         return self._rec(h, "amdsmi_get_gpu_process_list")
 
     def amdsmi_set_gpu_compute_partition(self, h, mode):
-        self.calls.append(("compute", h, mode.name))
-        self.compute[h] = mode.name
+        self.calls.append(("compute", int(h), mode.name))
+        self.compute[int(h)] = mode.name
 
     def amdsmi_set_gpu_memory_partition(self, h, mode):
-        self.calls.append(("memory", h, mode.name))
-        self.memory[h] = mode.name
+        self.calls.append(("memory", int(h), mode.name))
+        self.memory[int(h)] = mode.name
