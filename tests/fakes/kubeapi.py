@@ -107,6 +107,11 @@ class FakeKubeAPI:
 
     # ----------------------------------------------------------------- routing
     def _handle(self, method, parts, q, body):
+        if parts == ["api", "v1", "nodes"] and method == "GET":
+            sel = [c.split("=", 1) for c in q.get("labelSelector", "").split(",") if "=" in c]
+            items = [n for n in self.nodes.values()
+                     if all(n["metadata"].get("labels", {}).get(k) == v for k, v in sel)]
+            return 200, {"items": items}, None
         # /api/v1/nodes/<name>
         if parts[:3] == ["api", "v1", "nodes"] and len(parts) == 4:
             name = parts[3]

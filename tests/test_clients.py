@@ -212,3 +212,28 @@ def test_isolation_checker():
     assert not ok and any("shares GPU" in r for r in rep)
     ok, _ = mod.check({"a": _pod_log("111"), "b": _pod_log("222", passed=False)})
     assert not ok
+
+
+def test_time_to_first_gpu_pod_tool():
+    import time
+
+    from fakes.kubeapi import FakeKubeAPI
+
+    api = FakeKubeAPI().start()
+    api.add_node("gpu-node-1")
+
+    def kubelet(a, pod):
+        pod["status"]["phase"] = "Succeeded"
+        a.logs[(pod["metadata"]["namespace"], pod["metadata"]["name"])] = "Test PASSED\nDone\n"
+
+    api.on_pod_created = kubelet
+    threading.Timer(0.2, lambda: api.nodes["gpu-node-1"]["metadata"]["labels"].update(
+        {"amd.com/gpu.validated": "true"})).start()
+    try:
+        mod = _load(REPO / "tools/time_to_first_gpu_pod.py", "ttfgp")
+        t0 = time.time()
+        rc = mod.main(["--api", api.url, "--since", str(t0), "--poll", "0.05", "--timeout", "10"])
+        assert rc == 0
+        assert not [k for k in api.pods if k[1].startswith("ttfgp-")]  # cleaned up
+    finally:
+        api.stop()

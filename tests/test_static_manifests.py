@@ -95,7 +95,7 @@ def test_flux_kustomizations_use_ga_api_and_resolve():
 
 def test_gpu_workloads_depend_on_the_operator():
     ks = {k["metadata"]["name"]: k for k in flux_kustomizations()}
-    for name in ("llm", "sd15-api", "gpu-bench"):
+    for name in ("llm", "sd15-api", "gpu-bench", "comfyui"):
         assert "amd-gpu-operator" in [d["name"] for d in ks[name]["spec"].get("dependsOn", [])]
     assert ks["amd-gpu-operator"]["spec"]["wait"] is True
 
