@@ -24,6 +24,7 @@
 // 16-B aligned base pointers.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace {
 
@@ -44,6 +45,17 @@ constexpr int GROUP_M = 8;
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+#ifdef AMDK8S_W4_STAMPS
+// Diagnostic build only (tools/gemm_w4_stamps.hip): s_memtime of wave 0 at every K-tile start.
+__device__ unsigned long long* g_w4_stamps;
+__device__ int g_w4_stamp_stride;
+#define AMDK8S_W4_STAMP(T)                                                                  \
+  if (tid == 0 && (T) < g_w4_stamp_stride)                                                  \
+    g_w4_stamps[(size_t)blockIdx.x * g_w4_stamp_stride + (T)] = __builtin_amdgcn_s_memtime();
+#else
+#define AMDK8S_W4_STAMP(T)
+#endif
+
 __device__ __forceinline__ void barrier_raw() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_barrier" ::: "memory");
@@ -58,7 +70,8 @@ __device__ __forceinline__ bf16x8 lds_read16(const char* p) {
 
 extern "C" __global__ void __launch_bounds__(NT, 1)
 amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
-               uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+               uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc,
+               int superblock) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
 
   const int tid = threadIdx.x;
@@ -77,12 +90,28 @@ amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* _
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  const int group = wgid / (GROUP_M * tiles_n);
-  const int first_m = group * GROUP_M;
-  const int gsz = min(tiles_m - first_m, GROUP_M);
-  const int in_group = wgid - group * GROUP_M * tiles_n;
-  const int m0 = (first_m + in_group % gsz) * BM;
-  const int n0 = (in_group / gsz) * BN;
+  int m0, n0;
+  if (superblock) {
+    // Round-major 16×16-tile super-blocks: the 256 tiles in flight at once (one per CU) form a
+    // 4096×4096 block of C whose A/B panels (128 MiB at K = 8192) stay in the Infinity Cache; XCD x
+    // owns a 4(M)×8(N) corner of it. Super-blocks are walked in snake order so consecutive rounds
+    // share a panel set. Host guarantees tiles_m % 16 == tiles_n % 16 == 0.
+    const int xcd = bid & 7, i = bid >> 3;
+    const int round = i >> 5, j = i & 31;
+    const int sb_n_count = tiles_n >> 4;
+    const int sbm = round / sb_n_count;
+    int sbn = round - sbm * sb_n_count;
+    if (sbm & 1) sbn = sb_n_count - 1 - sbn;
+    m0 = (sbm * 16 + (xcd >> 1) * 4 + (j & 3)) * BM;
+    n0 = (sbn * 16 + (xcd & 1) * 8 + (j >> 2)) * BN;
+  } else {
+    const int group = wgid / (GROUP_M * tiles_n);
+    const int first_m = group * GROUP_M;
+    const int gsz = min(tiles_m - first_m, GROUP_M);
+    const int in_group = wgid - group * GROUP_M * tiles_n;
+    m0 = (first_m + in_group % gsz) * BM;
+    n0 = (in_group / gsz) * BN;
+  }
 
   // ---- LDS-DMA sources: instr j of wave w fills rows (j*4+w)*8 .. +8 of a 128-row half ----
   // Wave-uniform 64-bit bases (SGPRs) + one 32-bit per-lane offset per operand, so every DMA
@@ -130,6 +159,7 @@ amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* _
     for (int p = 0; p < 16; ++p) dma_piece(t, p);
   };
 
+
 #define AMDK8S_W4_READ(FA, FB, BUF, FO)                                     \
   _Pragma("unroll") for (int i = 0; i < 8; ++i) {                           \
     FA[i] = lds_read16((BUF) + a_off + i * 2048 + (FO));                    \
@@ -176,14 +206,15 @@ amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* _
   // One K-tile: K-half 0 on (fa0, fb0) while K-half 1 is read; barrier; K-half 1 on (fa1, fb1)
   // while K-half 0 of the next tile is read and (DMA) the tile after next is staged.
   // NEXT: a next tile exists; DMA: tile t+2 exists.  Peeled so the steady loop has no branches.
-#define AMDK8S_W4_TILE(NEXT, DMA)                                                     \
+#define AMDK8S_W4_TILE(NEXT, DMA)                                                 \
   {                                                                                   \
     const char* cur = lds + (t & 1) * TILE_BYTES;                                     \
     const char* nxt = lds + ((t + 1) & 1) * TILE_BYTES;                               \
+    AMDK8S_W4_STAMP(t)                                                                \
     AMDK8S_W4_PHASE(fa0, fb0, fa1, fb1, cur, fo1, true, false, t)                     \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                \
     if (NEXT) {                                                                       \
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* own DMA of tile t+1 landed */ \
       barrier_raw();                                                                  \
       AMDK8S_W4_PHASE(fa1, fb1, fa0, fb0, nxt, fo0, true, DMA, t + 2)                 \
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                              \
@@ -236,7 +267,11 @@ extern "C" int amdk8s_gemm_bf16_nt_w4(const void* A, const void* B, void* C, int
   if (lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N) return (int)hipErrorInvalidValue;
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return (int)hipErrorInvalidValue;
   const int nwg = (M / BM) * (N / BN);
+  // 16×16-tile super-block order whenever the tile grid allows it (AMDK8S_W4_SUPERBLOCK=0 turns
+  // it off for A/B runs): +8-10 % at 8192³ and 16384²×4096 (docs/gemm_tuning.md)
+  const char* sbenv = getenv("AMDK8S_W4_SUPERBLOCK");
+  const int sb = (M / BM) % 16 == 0 && (N / BN) % 16 == 0 && !(sbenv && sbenv[0] == '0');
   hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4, dim3(nwg), dim3(NT), 0, stream,
-                     (const uint16_t*)A, (const uint16_t*)B, (uint16_t*)C, M, N, K, lda, ldb, ldc);
+                     (const uint16_t*)A, (const uint16_t*)B, (uint16_t*)C, M, N, K, lda, ldb, ldc, sb);
   return (int)hipGetLastError();
 }

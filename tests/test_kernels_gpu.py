@@ -144,3 +144,17 @@ def test_fill_uniform_bf16(K, dev):
     t2 = torch.empty_like(t)
     K.fill_uniform_bf16(t2, seed=123)
     assert torch.equal(t, t2)
+
+
+@pytest.mark.parametrize("superblock", ["1", "0"])
+def test_gemm_w4_superblock_order_matches_w8(K, dev, superblock, monkeypatch):
+    """4096x4096 tiles (16x16 grid) take the super-block order in w4; output must not change."""
+    monkeypatch.setenv("AMDK8S_W4_SUPERBLOCK", superblock)
+    g = torch.Generator(device=dev).manual_seed(31)
+    a = _rand_bf16((4096, 512), g, dev)
+    b = _rand_bf16((4096, 512), g, dev)
+    c4 = K.gemm_bf16_nt(a, b, variant="w4")
+    c8 = K.gemm_bf16_nt(a, b, variant="w8")
+    assert torch.equal(c4, c8)
+    ref = a[:512].float() @ b[:256].float().t()
+    torch.testing.assert_close(c4[:512, :256].float(), ref, rtol=1e-2, atol=3e-2)

@@ -4,6 +4,7 @@
 usage: gemm_sweep.py --shapes 4096x4096x4096 8192x8192x4096 ... [--arms w8 w4 blt] [--rounds 5]
 """
 import argparse
+import os
 import statistics
 import sys
 import time
@@ -42,6 +43,12 @@ def main():
         for arm in args.arms:
             if arm == "blt":
                 arms[arm] = lambda: torch.matmul(a, b.t(), out=c)
+            elif arm == "w4x":  # w4 without the super-block tile order (A/B)
+                def f():
+                    os.environ["AMDK8S_W4_SUPERBLOCK"] = "0"
+                    K.gemm_bf16_nt(a, b, out=c, variant="w4")
+                    os.environ.pop("AMDK8S_W4_SUPERBLOCK", None)
+                arms[arm] = f
             else:
                 arms[arm] = (lambda v: (lambda: K.gemm_bf16_nt(a, b, out=c, variant=v)))(arm)
         est = {}
