@@ -96,8 +96,11 @@ def main(argv=None) -> int:
         if args.root != "/":
             extra = ["--sysfs-root", os.path.join(args.root, "sys/class/kfd/kfd/topology"),
                      "--dev-root", os.path.join(args.root, "dev"), "--no-open"]
+        drv = cfg.section("driver")
         driver_ready_loop(os.path.join(_bin_dir(), "kfd-probe"), int(cfg["expectedGpusPerNode"]),
-                          cfg.min_gfx, args.marker_dir, args.interval or 30.0, extra=extra)
+                          cfg.min_gfx, args.marker_dir, args.interval or 30.0, extra=extra,
+                          load_module=bool(drv["loadModule"]),
+                          dev_root=os.path.join(args.root, "dev"), host_root=drv["hostRoot"])
         return 0
 
     if c == "runtime-install":

@@ -25,6 +25,10 @@ DEFAULTS: Dict[str, Any] = {
         "cardNodes": False,          # also expose /dev/dri/card<N> (not needed by ROCm compute)
         "preferXgmiLocality": True,
     },
+    "driver": {
+        "loadModule": True,          # modprobe amdgpu (chroot into hostRoot) if /dev/kfd is missing
+        "hostRoot": "/host",
+    },
     "health": {
         "intervalSeconds": 10,
         "eccUncorrectableThreshold": 1,
@@ -43,6 +47,7 @@ DEFAULTS: Dict[str, Any] = {
         "gemm": True,
         "gemmSize": 8192,
         "gemmMinTflops": 900,
+        "rocprof": False,            # run the GEMM step under rocprofv3 --kernel-trace --stats
         "rccl": True,
         "rcclMinBusbwGBps": 100,
         "pluginTest": True,

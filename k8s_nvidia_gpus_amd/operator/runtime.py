@@ -117,15 +117,45 @@ def run_kfd_probe(bin_path: str, expect: int, min_gfx: int, marker: str,
     return subprocess.run(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
 
 
+def ensure_module(dev_root: str = "/dev", host_root: str = "/host", runner=None) -> Optional[bool]:
+    """If /dev/kfd is missing, try ``chroot <host_root> modprobe amdgpu`` once.
+
+    The reference's driver container compiles and loads the NVIDIA module inside the cluster
+    (README.md:514-517); amdgpu ships inbox / as DKMS on the host (amd-host-prep), so loading the
+    host's own module is all that can be needed here.  Returns None when nothing was attempted,
+    else whether modprobe succeeded."""
+    if os.path.exists(os.path.join(dev_root, "kfd")):
+        return None
+    if not os.path.isdir(host_root):
+        log.warning("/dev/kfd missing and no host root at %s to modprobe from", host_root)
+        return False
+    argv = ["chroot", host_root, "modprobe", "amdgpu"]
+    if runner is None:
+        p = subprocess.run(argv, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        rc, out = p.returncode, p.stdout
+    else:
+        rc, out = runner(argv)
+    if rc != 0:
+        log.error("modprobe amdgpu failed (%d): %s", rc, out.strip())
+    else:
+        log.info("loaded amdgpu from the host's module tree")
+    return rc == 0
+
+
 def driver_ready_loop(bin_path: str, expect: int, min_gfx: int, marker_dir: str,
-                      interval: float = 30.0, stop_event=None, extra: Optional[List[str]] = None) -> None:
+                      interval: float = 30.0, stop_event=None, extra: Optional[List[str]] = None,
+                      load_module: bool = False, dev_root: str = "/dev",
+                      host_root: str = "/host") -> None:
     import threading
 
     stop_event = stop_event or threading.Event()
     marker = os.path.join(marker_dir, "driver-ready")
     os.makedirs(marker_dir, exist_ok=True)
     was_ready = None
+    tried_modprobe = False
     while not stop_event.is_set():
+        if load_module and not tried_modprobe:
+            tried_modprobe = ensure_module(dev_root, host_root) is not None
         p = run_kfd_probe(bin_path, expect, min_gfx, marker, extra)
         ready = p.returncode == 0
         if ready != was_ready:

@@ -83,6 +83,21 @@ def protocol_passed(text: str) -> bool:
             and lines.index("Done") > lines.index("Test PASSED"))
 
 
+def rocprof_kernel_stats(prof_dir: str) -> List[dict]:
+    """Rows of rocprofv3's *_kernel_stats.csv (name, calls, average ns) under ``prof_dir``."""
+    import csv
+    import glob
+
+    rows = []
+    for f in glob.glob(os.path.join(prof_dir, "**", "*kernel_stats.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                rows.append({"name": r.get("Name", "")[:120], "calls": int(r.get("Calls", 0) or 0),
+                             "avg_ns": float(r.get("AverageNs", 0) or 0),
+                             "percent": float(r.get("Percentage", 0) or 0)})
+    return sorted(rows, key=lambda r: -r["percent"])
+
+
 @dataclass
 class StepResult:
     step: str
@@ -169,8 +184,15 @@ class Validator:
     def step_gemm(self) -> StepResult:
         size = int(self.vcfg["gemmSize"])
         floor = float(self.vcfg["gemmMinTflops"])
-        rc, out = self.run_cmd([self._bin("amd-gemm-validator"), "--size", str(size), "--iters", "50",
-                                "--json"], 900)
+        argv = [self._bin("amd-gemm-validator"), "--size", str(size), "--iters", "50", "--json"]
+        prof_dir = None
+        if self.vcfg.get("rocprof"):
+            # BASELINE config 3: the validator GEMM "shown in rocprof" — kernel trace + stats of the
+            # validator run itself, kept next to the step result (and exported as an artefact)
+            prof_dir = self._path("gemm-rocprof")
+            argv = ["rocprofv3", "--kernel-trace", "--stats", "-d", prof_dir, "-o", "gemm",
+                    "--output-format", "csv", "--"] + argv
+        rc, out = self.run_cmd(argv, 900)
         devs = [d for d in json_lines(out) if d.get("check") == "gemm_bf16"]
         slow = [d for d in devs if float(d.get("tflops", 0)) < floor]
         bad = [d for d in devs if not d.get("passed")]
@@ -181,8 +203,11 @@ class Validator:
                      (f"{len(slow)} GPU(s) below {floor} TFLOPS; " if slow else "") + \
                      (f"rc={rc}" if rc else "")
         total = sum(float(d.get("tflops", 0)) for d in devs)
-        return StepResult("gemm", bool(ok), {"devices": devs, "size": size, "floor_tflops": floor,
-                                             "aggregate_tflops": round(total, 1)}, reason)
+        detail = {"devices": devs, "size": size, "floor_tflops": floor,
+                  "aggregate_tflops": round(total, 1)}
+        if prof_dir:
+            detail["rocprof_kernels"] = rocprof_kernel_stats(prof_dir)
+        return StepResult("gemm", bool(ok), detail, reason)
 
     def step_rccl(self, ngpus: Optional[int] = None) -> StepResult:
         if ngpus is not None and ngpus < 2:

@@ -299,3 +299,39 @@ def test_cli_topology_and_cdi(tmp_path):
                           "--root", str(root), "--config", "/nonexistent"], capture_output=True,
                          text=True, env=env, check=True).stdout
     assert json.loads(out)["kind"] == "amd.com/gpu"
+
+
+def test_driver_module_loading(tmp_path):
+    calls = []
+    dev = tmp_path / "dev"
+    dev.mkdir()
+    host = tmp_path / "host"
+    host.mkdir()
+    runner = lambda argv: (calls.append(argv) or (0, ""))  # noqa: E731
+    assert rt.ensure_module(str(dev), str(host), runner) is True
+    assert calls == [["chroot", str(host), "modprobe", "amdgpu"]]
+    (dev / "kfd").write_text("")
+    assert rt.ensure_module(str(dev), str(host), runner) is None  # driver already up
+    os.unlink(dev / "kfd")
+    assert rt.ensure_module(str(dev), str(host), lambda a: (1, "FATAL: Module amdgpu not found")) is False
+
+
+def test_validator_gemm_step_under_rocprof(tmp_path):
+    from k8s_nvidia_gpus_amd.operator.validator import Validator
+
+    log = (Path(__file__).resolve().parent.parent / "profiles/r01_gemm_validator.log").read_text()
+    seen = []
+
+    def runner(argv, timeout):
+        seen.append(argv)
+        d = Path(argv[argv.index("-d") + 1]) / "run"
+        d.mkdir(parents=True)
+        (d / "gemm_kernel_stats.csv").write_text(
+            '"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\n'
+            '"amdk8s_gemm_bf16_nt_256x256",60,47700000,795000.0,98.9,782807,1030849,66849.2\n')
+        return 0, log
+
+    cfg = load_config(text="validator: {rocprof: true}\n")
+    r = Validator(cfg, str(tmp_path), bin_dir="/b", runner=runner).run_step("gemm")
+    assert r.passed and seen[0][:3] == ["rocprofv3", "--kernel-trace", "--stats"]
+    assert r.detail["rocprof_kernels"][0]["name"] == "amdk8s_gemm_bf16_nt_256x256"
