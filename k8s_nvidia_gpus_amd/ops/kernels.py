@@ -116,14 +116,20 @@ def gemm_shape_supported(m: int, n: int, k: int) -> bool:
 
 GEMM_VARIANTS = ("auto", "w8", "w4")
 DEFAULT_GEMM_VARIANT = os.environ.get("AMDK8S_GEMM_VARIANT", "auto")
-# Operand footprint above which the 8-wave schedule wins (docs/gemm_tuning.md): w4 keeps one K-tile
-# of LDS-DMA lead, enough while A+B are served from the 256 MiB Infinity Cache, not once the DMA
-# pays HBM latency; w8's two waves per SIMD hide that latency.
+# w4 (one wave per SIMD) keeps one K-tile of LDS-DMA lead: enough while A+B are served from the
+# 256 MiB Infinity Cache, and — with its 16×16-tile super-block order — on grids of ≥ 4 super-blocks
+# (≥ 1024 tiles), where it beats w8 by 2-4 % (8192³, 12288²×8192, 16384²×8192). A single super-block
+# with 256 MiB of operands (4096²×16384) is w8's case. Evidence: docs/gemm_tuning.md.
 W4_MAX_OPERAND_BYTES = 192 << 20
 
 
 def pick_gemm_variant(m: int, n: int, k: int) -> str:
-    return "w4" if (m + n) * k * 2 <= W4_MAX_OPERAND_BYTES else "w8"
+    if (m + n) * k * 2 <= W4_MAX_OPERAND_BYTES:
+        return "w4"
+    tm, tn = m // GEMM_TILE_M, n // GEMM_TILE_N
+    if tm % 16 == 0 and tn % 16 == 0 and tm * tn >= 1024:
+        return "w4"
+    return "w8"
 
 
 def gemm_bf16_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
