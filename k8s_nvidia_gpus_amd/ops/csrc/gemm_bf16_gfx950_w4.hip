@@ -31,6 +31,7 @@ namespace {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 
 constexpr int BM = 256;
 constexpr int BN = 256;
@@ -45,15 +46,24 @@ constexpr int GROUP_M = 8;
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// Timing-only ablations (tools/gemm_w4_ablate.hip; results are WRONG): bit 0 drops the in-loop
+// tile staging, bit 1 the in-loop fragment reads, bit 2 the per-K-tile barrier, bit 3 the
+// per-K-tile vmcnt(0).
+#ifndef AMDK8S_W4_ABLATE
+#define AMDK8S_W4_ABLATE 0
+#endif
+
 #ifdef AMDK8S_W4_STAMPS
-// Diagnostic build only (tools/gemm_w4_stamps.hip): s_memtime of wave 0 at every K-tile start.
+// Diagnostic build only (tools/gemm_w4_stamps.hip): s_memtime of wave 0 at 4 points of every K-tile
+// (0 start, 1 K-half 0 done, 2 past the barrier, 3 K-half 1 done); stride = 4 × K-tiles.
 __device__ unsigned long long* g_w4_stamps;
 __device__ int g_w4_stamp_stride;
-#define AMDK8S_W4_STAMP(T)                                                                  \
-  if (tid == 0 && (T) < g_w4_stamp_stride)                                                  \
-    g_w4_stamps[(size_t)blockIdx.x * g_w4_stamp_stride + (T)] = __builtin_amdgcn_s_memtime();
+#define AMDK8S_W4_STAMP(T, SLOT)                                                            \
+  if (tid == 0 && (T) * 4 + (SLOT) < g_w4_stamp_stride)                                     \
+    g_w4_stamps[(size_t)blockIdx.x * g_w4_stamp_stride + (T) * 4 + (SLOT)] =                \
+        __builtin_amdgcn_s_memtime();
 #else
-#define AMDK8S_W4_STAMP(T)
+#define AMDK8S_W4_STAMP(T, SLOT)
 #endif
 
 __device__ __forceinline__ void barrier_raw() {
@@ -68,12 +78,20 @@ __device__ __forceinline__ bf16x8 lds_read16(const char* p) {
 
 }  // namespace
 
-extern "C" __global__ void __launch_bounds__(NT, 1)
+// MODE 0: tiles staged by LDS-DMA with global_load_lds (64-bit per-lane address per piece);
+// MODE 2: the same DMA as buffer_load_dwordx4 … lds — one 32-bit lane offset for every piece, the
+// piece's row offset in an SGPR soffset, no per-piece address VALU; MODE 1: staged through 64
+// VGPRs (global_load_dwordx4 → ds_write_b128 of the same lane-linear image), two phases of lead;
+// MODE 3: MODE 0 with the next K-half's B fragments read first (all by mid-phase, A fragments as
+// their rows retire) and no lgkmcnt(0) at the K-tile boundary (hipcc's counted waits instead).
+template <int MODE>
+__global__ void __launch_bounds__(NT, 1)
 amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc,
                int superblock) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
 
+  constexpr bool REG = MODE == 1;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -138,14 +156,31 @@ amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* _
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  // B fragments double-buffered by K-half; A fragments single-buffered: row I's next-K-half
+  // fragment is read into fa[I] as soon as row I's 8 MFMAs of the current K-half are issued.
+  bf16x8 fa[8], fb0[8], fb1[8];
 
   const int T = K / BK;
 
   // piece p (0..15) of K-tile t: j = p >> 2 (32-row stripe), h = (p >> 1) & 1 (half), p & 1: A/B
+  // MODE 2 descriptors: the block's 256-row A / B panels (wave-uniform inputs only)
+  const __amdgpu_buffer_rsrc_t rsrc_a = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<char*>(a_base), (short)0, (int)(256u * lda_b), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsrc_b = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<char*>(b_base), (short)0, (int)(256u * ldb_b), 0x00020000);
   auto dma_piece = [&](int t, int p) {
     const int j = p >> 2, h = (p >> 1) & 1;
     char* dst = lds + (t & 1) * TILE_BYTES + wave * 1024 + j * 4096;
+    if (MODE == 2) {
+      const uint32_t rows = (uint32_t)(j * 32 + h * 128);
+      if ((p & 1) == 0)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void*)(dst + h * HALF_BYTES), 16, a_voff,
+                                                 rows * lda_b + (uint32_t)t * (BK * 2), 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_b, (lds_void*)(dst + (2 + h) * HALF_BYTES), 16,
+                                                 b_voff, rows * ldb_b + (uint32_t)t * (BK * 2), 0, 0);
+      return;
+    }
     if ((p & 1) == 0) {
       const char* src = a_base + (size_t)t * BK * 2 + (uint32_t)(j * 32 + h * 128) * lda_b + a_voff;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + h * HALF_BYTES), 16, 0, 0);
@@ -157,6 +192,21 @@ amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* _
   auto dma_tile = [&](int t) {
 #pragma unroll
     for (int p = 0; p < 16; ++p) dma_piece(t, p);
+  };
+  // register staging: the same piece → S[p] (16 B/lane), later written lane-linearly to LDS
+  u32x4 S[16];
+  auto stage_load = [&](int t, int p) {
+    const int j = p >> 2, h = (p >> 1) & 1;
+    const char* src = (p & 1) == 0
+        ? a_base + (size_t)t * BK * 2 + ((uint32_t)(j * 32 + h * 128) * lda_b + a_voff)
+        : b_base + (size_t)t * BK * 2 + ((uint32_t)(j * 32 + h * 128) * ldb_b + b_voff);
+    S[p] = *reinterpret_cast<const u32x4*>(__builtin_assume_aligned(src, 16));
+  };
+  auto stage_write = [&](int t, int p) {
+    const int j = p >> 2, h = (p >> 1) & 1;
+    char* dst = lds + (t & 1) * TILE_BYTES + wave * 1024 + j * 4096 +
+                ((p & 1) ? (2 + h) : h) * HALF_BYTES + lane * 16;
+    *reinterpret_cast<u32x4*>(__builtin_assume_aligned(dst, 16)) = S[p];
   };
 
 
@@ -180,27 +230,55 @@ amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* _
   AMDK8S_W4_MFMA1((G) >> 1, ((G) & 1) * 4 + 3, FA, FB)
   // one K-half of MFMAs on (FA, FB) with the next fragment set (NA, NB) read from BUF+FO
   // (READ) and one DMA piece per 4 MFMAs (DMA)
-#define AMDK8S_W4_PHASE(FA, FB, NA, NB, BUF, FO, READ, DMA, TD)                         \
+// REG staging: every other group writes S[PB + g/2] (tile TW) to LDS when W, then reloads it
+// with the same piece of tile TL when L (TL clamped to the last tile: a harmless re-read).
+#define AMDK8S_W4_PHASE(FA, FB, NB, BUF, FO, READ, DMA, TD, W, TW, L, TL, PB)           \
   _Pragma("unroll") for (int g = 0; g < 16; ++g) {                                      \
     AMDK8S_W4_MFMA4(g, FA, FB);                                                         \
-    if (READ) {                                                                         \
-      if (g < 8) NA[g] = lds_read16((BUF) + a_off + g * 2048 + (FO));                  \
-      else NB[g - 8] = lds_read16((BUF) + b_off + (g - 8) * 2048 + (FO));               \
+    if ((READ) && !(AMDK8S_W4_ABLATE & 2)) {                                            \
+      if (MODE == 3) {                                                                  \
+        if (g < 8) NB[g] = lds_read16((BUF) + b_off + g * 2048 + (FO));                 \
+        if (g & 1) FA[g >> 1] = lds_read16((BUF) + a_off + (g >> 1) * 2048 + (FO));     \
+      } else if (g & 1) {                                                               \
+        FA[g >> 1] = lds_read16((BUF) + a_off + (g >> 1) * 2048 + (FO));                \
+      } else {                                                                          \
+        NB[g >> 1] = lds_read16((BUF) + b_off + (g >> 1) * 2048 + (FO));                \
+      }                                                                                 \
     }                                                                                   \
-    if (DMA) dma_piece(TD, g);                                                          \
+    if (!REG && (DMA) && !(AMDK8S_W4_ABLATE & 1)) dma_piece(TD, g);                     \
+    if (REG && (g & 1) && !(AMDK8S_W4_ABLATE & 1)) {                                    \
+      if (W) stage_write(TW, (PB) + (g >> 1));                                          \
+      if (L) stage_load(min((TL), T - 1), (PB) + (g >> 1));                             \
+    }                                                                                   \
   }
 
   // ---- prologue: tiles 0 (and 1) in flight; K-half 0 of tile 0 into registers ----
-  dma_tile(0);
-  if (T > 1) {
-    dma_tile(1);
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  if (REG) {
+    // buf0 = tile 0, buf1 = tile 1 pieces 0..7; S[8..15] = tile 1 pieces 8..15 (written in tile
+    // 0's first K-half), S[0..7] = tile 2 pieces 0..7 (written in tile 0's second K-half)
+#pragma unroll
+    for (int p = 0; p < 16; ++p) stage_load(0, p);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) stage_write(0, p);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) stage_load(min(1, T - 1), p);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) stage_write(1, p);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) stage_load(min(2, T - 1), p);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    dma_tile(0);
+    if (T > 1) {
+      dma_tile(1);
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   barrier_raw();
-  AMDK8S_W4_READ(fa0, fb0, lds, fo0)
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  AMDK8S_W4_READ(fa, fb0, lds, fo0)
+  if (MODE != 3) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 
   // One K-tile: K-half 0 on (fa0, fb0) while K-half 1 is read; barrier; K-half 1 on (fa1, fb1)
@@ -210,16 +288,23 @@ amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* _
   {                                                                                   \
     const char* cur = lds + (t & 1) * TILE_BYTES;                                     \
     const char* nxt = lds + ((t + 1) & 1) * TILE_BYTES;                               \
-    AMDK8S_W4_STAMP(t)                                                                \
-    AMDK8S_W4_PHASE(fa0, fb0, fa1, fb1, cur, fo1, true, false, t)                     \
+    AMDK8S_W4_STAMP(t, 0)                                                             \
+    AMDK8S_W4_PHASE(fa, fb0, fb1, cur, fo1, true, false, t,                           \
+                    NEXT, t + 1, DMA, t + 2, 8)                                       \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                \
+    AMDK8S_W4_STAMP(t, 1)                                                             \
     if (NEXT) {                                                                       \
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* own DMA of tile t+1 landed */ \
-      barrier_raw();                                                                  \
-      AMDK8S_W4_PHASE(fa1, fb1, fa0, fb0, nxt, fo0, true, DMA, t + 2)                 \
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                              \
+      if (!REG && !(AMDK8S_W4_ABLATE & 8))                                            \
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* tile t+1 landed */        \
+      if (!(AMDK8S_W4_ABLATE & 4)) barrier_raw();                                     \
+      AMDK8S_W4_STAMP(t, 2)                                                           \
+      AMDK8S_W4_PHASE(fa, fb1, fb0, nxt, fo0, true, DMA, t + 2,                       \
+                      DMA, t + 2, DMA, t + 3, 0)                                      \
+      if (MODE != 3) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");               \
+      AMDK8S_W4_STAMP(t, 3)                                                           \
     } else {                                                                          \
-      AMDK8S_W4_PHASE(fa1, fb1, fa0, fb0, nxt, fo0, false, false, t)                  \
+      AMDK8S_W4_PHASE(fa, fb1, fb0, nxt, fo0, false, false, t,                        \
+                      false, t, false, t, 0)                                          \
     }                                                                                 \
   }
 
@@ -271,7 +356,19 @@ extern "C" int amdk8s_gemm_bf16_nt_w4(const void* A, const void* B, void* C, int
   // it off for A/B runs): +8-10 % at 8192³ and 16384²×4096 (docs/gemm_tuning.md)
   const char* sbenv = getenv("AMDK8S_W4_SUPERBLOCK");
   const int sb = (M / BM) % 16 == 0 && (N / BN) % 16 == 0 && !(sbenv && sbenv[0] == '0');
-  hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4, dim3(nwg), dim3(NT), 0, stream,
-                     (const uint16_t*)A, (const uint16_t*)B, (uint16_t*)C, M, N, K, lda, ldb, ldc, sb);
+  const char* menv = getenv("AMDK8S_W4_MODE");
+  const int mode = menv ? atoi(menv) : 0;
+  if (mode == 1)
+    hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4<1>, dim3(nwg), dim3(NT), 0, stream,
+                       (const uint16_t*)A, (const uint16_t*)B, (uint16_t*)C, M, N, K, lda, ldb, ldc, sb);
+  else if (mode == 3)
+    hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4<3>, dim3(nwg), dim3(NT), 0, stream,
+                       (const uint16_t*)A, (const uint16_t*)B, (uint16_t*)C, M, N, K, lda, ldb, ldc, sb);
+  else if (mode == 2)
+    hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4<2>, dim3(nwg), dim3(NT), 0, stream,
+                       (const uint16_t*)A, (const uint16_t*)B, (uint16_t*)C, M, N, K, lda, ldb, ldc, sb);
+  else
+    hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4<0>, dim3(nwg), dim3(NT), 0, stream,
+                       (const uint16_t*)A, (const uint16_t*)B, (uint16_t*)C, M, N, K, lda, ldb, ldc, sb);
   return (int)hipGetLastError();
 }

@@ -43,11 +43,17 @@ def main():
         for arm in args.arms:
             if arm == "blt":
                 arms[arm] = lambda: torch.matmul(a, b.t(), out=c)
-            elif arm == "w4x":  # w4 without the super-block tile order (A/B)
-                def f():
-                    os.environ["AMDK8S_W4_SUPERBLOCK"] = "0"
-                    K.gemm_bf16_nt(a, b, out=c, variant="w4")
-                    os.environ.pop("AMDK8S_W4_SUPERBLOCK", None)
+            elif "@" in arm or arm == "w4x":
+                # VARIANT@ENV=VALUE: the variant with a launcher env knob set (A/B of kernel options);
+                # w4x = w4 without the super-block tile order
+                spec = "w4@AMDK8S_W4_SUPERBLOCK=0" if arm == "w4x" else arm
+                var, kv = spec.split("@", 1)
+                key, val = kv.split("=", 1)
+
+                def f(var=var, key=key, val=val):
+                    os.environ[key] = val
+                    K.gemm_bf16_nt(a, b, out=c, variant=var)
+                    os.environ.pop(key, None)
                 arms[arm] = f
             else:
                 arms[arm] = (lambda v: (lambda: K.gemm_bf16_nt(a, b, out=c, variant=v)))(arm)
