@@ -3,7 +3,7 @@
 // cycles go (MFMA phases vs the vmcnt/barrier wait). Not part of the product build.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DAMDK8S_W4_STAMPS tools/gemm_w4_stamps.hip \
 //     k8s_nvidia_gpus_amd/ops/csrc/fill.hip -o /tmp/w4stamps && /tmp/w4stamps 4096 4096 16384
-// AMDK8S_W4_MODE=1|2 in the environment stamps the register-staged / buffer-load-DMA variant.
+// Stamps the INTERLEAVED schedule (the launcher is forced to it: AMDK8S_W4_SCHEDULE=interleaved).
 #include "../k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950_w4.hip"
 #include <algorithm>
 #include <cstdio>
@@ -18,6 +18,7 @@ static long long median(std::vector<long long> v) {
 }
 
 int main(int argc, char** argv) {
+  setenv("AMDK8S_W4_SCHEDULE", "interleaved", 1);
   int M = argc > 1 ? atoi(argv[1]) : 4096, N = argc > 2 ? atoi(argv[2]) : 4096,
       K = argc > 3 ? atoi(argv[3]) : 16384;
   void *A, *B, *C;
@@ -35,8 +36,8 @@ int main(int argc, char** argv) {
   std::vector<unsigned long long> h((size_t)nwg * stride);
   hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
   auto at = [&](int b, int t, int s) { return (long long)h[(size_t)b * stride + t * 4 + s]; };
-  printf("# %dx%dx%d  mode=%s  [s_memtime ticks = shader cycles, medians over blocks]\n", M, N, K,
-         getenv("AMDK8S_W4_MODE") ? getenv("AMDK8S_W4_MODE") : "0");
+  printf("# %dx%dx%d  schedule=%s  [s_memtime ticks = shader cycles, medians over blocks]\n", M, N, K,
+         "interleaved");
   printf("# K-tile   total  khalf0  wait+barrier  khalf1   (ideal per K-half: 64 MFMA x 16 = 1024)\n");
   std::vector<long long> all_tot, all_a, all_w, all_b;
   for (int t = 1; t + 2 < T; ++t) {
