@@ -143,10 +143,11 @@ def main(argv=None) -> int:
         return 0
 
     if c == "partition-manager":
-        from .partition import (AmdSmiPartitionBackend, PartitionManager,
-                                SysfsPartitionBackend)
+        from .partition import PartitionManager, SysfsPartitionBackend
 
         try:
+            from .partition_amdsmi import AmdSmiPartitionBackend
+
             backend = AmdSmiPartitionBackend()
         except Exception:  # noqa: BLE001
             backend = SysfsPartitionBackend(args.root)

@@ -55,28 +55,6 @@ class SysfsPartitionBackend:
         self._write(dev, "current_memory_partition", mode)
 
 
-class AmdSmiPartitionBackend:
-    def __init__(self, amdsmi_module=None):
-        if amdsmi_module is None:
-            import amdsmi as amdsmi_module  # noqa: N813
-        self.S = amdsmi_module
-        self.S.amdsmi_init()
-
-    def _handle(self, dev: topo_mod.GpuDevice):
-        for h in self.S.amdsmi_get_processor_handles():
-            if str(self.S.amdsmi_get_gpu_device_bdf(h)).lower() == dev.pci_bdf.lower():
-                return h
-        raise PartitionError(f"amd-smi has no handle for {dev.pci_bdf}")
-
-    def set_compute(self, dev: topo_mod.GpuDevice, mode: str) -> None:
-        self.S.amdsmi_set_gpu_compute_partition(
-            self._handle(dev), getattr(self.S.AmdSmiComputePartitionType, mode))
-
-    def set_memory(self, dev: topo_mod.GpuDevice, mode: str) -> None:
-        self.S.amdsmi_set_gpu_memory_partition(
-            self._handle(dev), getattr(self.S.AmdSmiMemoryPartitionType, mode))
-
-
 class PartitionManager:
     def __init__(self, client: kube_mod.KubeClient, node_name: str, backend, root: str = "/",
                  default_compute: str = "SPX", default_memory: str = "NPS1",

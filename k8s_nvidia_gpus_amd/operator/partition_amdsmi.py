@@ -1,0 +1,33 @@
+"""amd-smi backend of the partition manager (operator/partition.py): applies a compute / memory
+partition mode to one ASIC through the amdsmi Python bindings.
+
+Kept in its own module and imported only by the ``partition-manager`` component (and its CPU
+test): it is the one piece of the operator that changes a device-wide setting, and nothing that
+runs on a shared GPU box (bench, validator, GPU tests) ever needs it (listed in .gpurunignore).
+"""
+from __future__ import annotations
+
+from ..utils import topology as topo_mod
+from .partition import PartitionError
+
+
+class AmdSmiPartitionBackend:
+    def __init__(self, amdsmi_module=None):
+        if amdsmi_module is None:
+            import amdsmi as amdsmi_module  # noqa: N813
+        self.S = amdsmi_module
+        self.S.amdsmi_init()
+
+    def _handle(self, dev: topo_mod.GpuDevice):
+        for h in self.S.amdsmi_get_processor_handles():
+            if str(self.S.amdsmi_get_gpu_device_bdf(h)).lower() == dev.pci_bdf.lower():
+                return h
+        raise PartitionError(f"amd-smi has no handle for {dev.pci_bdf}")
+
+    def set_compute(self, dev: topo_mod.GpuDevice, mode: str) -> None:
+        self.S.amdsmi_set_gpu_compute_partition(
+            self._handle(dev), getattr(self.S.AmdSmiComputePartitionType, mode))
+
+    def set_memory(self, dev: topo_mod.GpuDevice, mode: str) -> None:
+        self.S.amdsmi_set_gpu_memory_partition(
+            self._handle(dev), getattr(self.S.AmdSmiMemoryPartitionType, mode))

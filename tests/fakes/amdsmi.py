@@ -114,11 +114,3 @@ class FakeAmdSmi:
 
     def amdsmi_get_gpu_process_list(self, h):
         return self._rec(h, "amdsmi_get_gpu_process_list")
-
-    def amdsmi_set_gpu_compute_partition(self, h, mode):
-        self.calls.append(("compute", int(h), mode.name))
-        self.compute[int(h)] = mode.name
-
-    def amdsmi_set_gpu_memory_partition(self, h, mode):
-        self.calls.append(("memory", int(h), mode.name))
-        self.memory[int(h)] = mode.name

@@ -249,10 +249,13 @@ def test_partition_manager_rejects_unavailable_mode(tmp_path, api, client):
 
 
 def test_amdsmi_partition_backend_maps_bdf(tmp_path):
-    fake = FakeAmdSmi()
+    from fakes.amdsmi_partition import FakeAmdSmiPartitionable
+    from k8s_nvidia_gpus_amd.operator.partition_amdsmi import AmdSmiPartitionBackend
+
+    fake = FakeAmdSmiPartitionable()
     root = fake_sysfs.build_node(tmp_path / "r")
     dev = read_topology(str(root), 90500).gpus[5]
-    pm.AmdSmiPartitionBackend(fake).set_compute(dev, "CPX")
+    AmdSmiPartitionBackend(fake).set_compute(dev, "CPX")
     h = [fake.amdsmi_get_gpu_device_bdf(i) for i in range(8)].index(dev.pci_bdf)
     assert fake.calls == [("compute", h, "CPX")]
 
