@@ -116,20 +116,12 @@ def gemm_shape_supported(m: int, n: int, k: int) -> bool:
 
 GEMM_VARIANTS = ("auto", "w8", "w4")
 DEFAULT_GEMM_VARIANT = os.environ.get("AMDK8S_GEMM_VARIANT", "auto")
-# w4 (one wave per SIMD) keeps one K-tile of LDS-DMA lead: enough while A+B are served from the
-# 256 MiB Infinity Cache, and — with its 16×16-tile super-block order — on grids of ≥ 4 super-blocks
-# (≥ 1024 tiles), where it beats w8 by 2-4 % (8192³, 12288²×8192, 16384²×8192). A single super-block
-# with 256 MiB of operands (4096²×16384) is w8's case. Evidence: docs/gemm_tuning.md.
-W4_MAX_OPERAND_BYTES = 192 << 20
-
-
+# w4 (one wave per SIMD) with its REGION schedule for operands that stream from MALL/HBM beats the
+# 8-wave w8 kernel on every measured shape, including the single-super-block 4096²×16384 that was
+# w8's case under the former SPLIT schedule (1469-1492 vs ≈1416 TFLOPS): docs/gemm_tuning.md,
+# profiles/r01_session3/.  w8 stays selectable for A/B runs.
 def pick_gemm_variant(m: int, n: int, k: int) -> str:
-    if (m + n) * k * 2 <= W4_MAX_OPERAND_BYTES:
-        return "w4"
-    tm, tn = m // GEMM_TILE_M, n // GEMM_TILE_N
-    if tm % 16 == 0 and tn % 16 == 0 and tm * tn >= 1024:
-        return "w4"
-    return "w8"
+    return "w4"
 
 
 def gemm_bf16_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,

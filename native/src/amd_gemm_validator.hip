@@ -24,13 +24,10 @@
 namespace {
 
 // Kernel variant: "w8" (8 waves, 2/SIMD), "w4" (4 waves, 1/SIMD, 128x128 per wave) or "auto"
-// (w4 while A+B fit the 256 MiB Infinity Cache, else w8; docs/gemm_tuning.md).
+// (= w4, which picks its own K-loop schedule by operand footprint; docs/gemm_tuning.md).
 int gemm(const std::string& variant, const void* A, const void* B, void* C, int m, int n, int k,
          hipStream_t s) {
-  const int tm = m / 256, tn = n / 256;
-  const bool fits = (double)(m + n) * k * 2 <= 192.0 * 1024 * 1024;
-  const bool superblocks = tm % 16 == 0 && tn % 16 == 0 && tm * tn >= 1024;
-  const bool w4 = variant == "w4" || (variant == "auto" && (fits || superblocks));
+  const bool w4 = variant != "w8";
   return w4 ? amdk8s_gemm_bf16_nt_w4(A, B, C, m, n, k, k, k, n, s)
             : amdk8s_gemm_bf16_nt(A, B, C, m, n, k, k, k, n, s);
 }

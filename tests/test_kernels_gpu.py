@@ -160,11 +160,12 @@ def test_gemm_w4_superblock_order_matches_w8(K, dev, superblock, monkeypatch):
     torch.testing.assert_close(c4[:512, :256].float(), ref, rtol=1e-2, atol=3e-2)
 
 
-@pytest.mark.parametrize("schedule", ["interleaved", "split"])
-@pytest.mark.parametrize("m,n,k", [(256, 256, 128), (768, 512, 1024), (4096, 4096, 640)])
+@pytest.mark.parametrize("schedule", ["interleaved", "region"])
+@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (256, 256, 128), (512, 256, 192),
+                                   (768, 512, 1024), (4096, 4096, 640)])
 def test_gemm_w4_schedules_match_fp32_and_w8(K, dev, schedule, m, n, k, monkeypatch):
-    """Both w4 schedules (forced) against an fp32 reference and bit-for-bit against w8; split
-    needs K % 128 == 0 and falls back to interleaved otherwise (k = 640 runs both paths)."""
+    """Both w4 schedules (forced) against an fp32 reference and bit-for-bit against w8 (k = 64 is
+    a single K-tile — the clamped restage and the unused "tile T" reads —, 192 an odd count)."""
     monkeypatch.setenv("AMDK8S_W4_SCHEDULE", schedule)
     g = torch.Generator(device=dev).manual_seed(41 + m + k)
     a = _rand_bf16((m, k), g, dev)
@@ -176,10 +177,12 @@ def test_gemm_w4_schedules_match_fp32_and_w8(K, dev, schedule, m, n, k, monkeypa
     torch.testing.assert_close(c4[:rows, :cols].float(), ref, rtol=1e-2, atol=1e-2 * (k ** 0.5) / 8)
 
 
-def test_gemm_w4_split_schedule_repeatable_under_load(K, dev, monkeypatch):
-    """The split schedule's DMA/read phases are ordered only by counted waits + barriers: repeat a
-    large grid several times and require identical bits every time (a race shows up as drift)."""
-    monkeypatch.setenv("AMDK8S_W4_SCHEDULE", "split")
+@pytest.mark.parametrize("schedule", ["region"])
+def test_gemm_w4_schedule_repeatable_under_load(K, dev, schedule, monkeypatch):
+    """The region schedule's DMA/read phases are ordered only by counted waits + barriers:
+    repeat a large grid several times and require identical bits every time (a race shows up as
+    drift)."""
+    monkeypatch.setenv("AMDK8S_W4_SCHEDULE", schedule)
     g = torch.Generator(device=dev).manual_seed(77)
     a = _rand_bf16((4096, 2048), g, dev)
     b = _rand_bf16((4096, 2048), g, dev)
@@ -188,3 +191,4 @@ def test_gemm_w4_split_schedule_repeatable_under_load(K, dev, monkeypatch):
         assert torch.equal(K.gemm_bf16_nt(a, b, variant="w4"), c0)
     monkeypatch.setenv("AMDK8S_W4_SCHEDULE", "interleaved")
     assert torch.equal(K.gemm_bf16_nt(a, b, variant="w4"), c0)
+

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Run ONE GEMM arm for a fixed number of iterations (for rocprofv3 counter collection)."""
 import argparse
+import os
 import sys
 
 import torch
@@ -13,6 +14,9 @@ ap.add_argument("--arm", default="w4")
 ap.add_argument("--shape", default="8192x8192x8192")
 ap.add_argument("--iters", type=int, default=20)
 args = ap.parse_args()
+if "@" in args.arm:  # VARIANT@ENV=VALUE, as in tools/gemm_sweep.py
+    args.arm, kvs = args.arm.split("@", 1)
+    os.environ.update(dict(kv.split("=", 1) for kv in kvs.split(",")))
 m, n, k = (int(x) for x in args.shape.split("x"))
 dev = torch.device("cuda", 0)
 a = torch.empty((m, k), dtype=torch.bfloat16, device=dev)

@@ -47,13 +47,14 @@ def main():
                 # VARIANT@ENV=VALUE: the variant with a launcher env knob set (A/B of kernel options);
                 # w4x = w4 without the super-block tile order
                 spec = "w4@AMDK8S_W4_SUPERBLOCK=0" if arm == "w4x" else arm
-                var, kv = spec.split("@", 1)
-                key, val = kv.split("=", 1)
+                var, kvs = spec.split("@", 1)
+                env = dict(kv.split("=", 1) for kv in kvs.split(","))  # VARIANT@K1=V1,K2=V2
 
-                def f(var=var, key=key, val=val):
-                    os.environ[key] = val
+                def f(var=var, env=env):
+                    os.environ.update(env)
                     K.gemm_bf16_nt(a, b, out=c, variant=var)
-                    os.environ.pop(key, None)
+                    for key in env:
+                        os.environ.pop(key, None)
                 arms[arm] = f
             else:
                 arms[arm] = (lambda v: (lambda: K.gemm_bf16_nt(a, b, out=c, variant=v)))(arm)
