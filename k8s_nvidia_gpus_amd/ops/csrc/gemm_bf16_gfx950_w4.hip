@@ -10,15 +10,16 @@
 // software-pipelines itself.  The LDS holds two full K-tiles (2 × 64 KiB) filled by LDS-DMA with
 // the source-side XOR swizzle of gemm_bf16_gfx950.hip; two schedules share everything else:
 //
+//   REGION (default): each operand's half of an LDS buffer is restaged as soon as every wave has
+//     read it, so the DMA pieces spread over both K-halves (three barriers per tile); reads and DMA
+//     pieces go one per MFMA gap; the next tile's fragments are never drained at the tile boundary
+//     (hipcc's counted lgkmcnt waits sit at their first use).  Ties INTERLEAVED where A + B sit in
+//     the Infinity Cache, +4…34 % where they stream from MALL/HBM (profiles/r01_session3/,
+//     docs/gemm_tuning.md).
 //   INTERLEAVED: K-half 0's 64 MFMAs run while K-half 1's 16 fragments are read; barrier; K-half
 //     1's MFMAs run while the next tile's K-half 0 is read AND tile t+2's 16 DMA pieces are issued
-//     (1 read + 1 global_load_lds per 4 MFMAs).  One vmcnt(0) + barrier per tile.  Best where A+B
-//     sit in the Infinity Cache.
-//   REGION: each operand's half of an LDS buffer is restaged as soon as every wave has read it,
-//     so the DMA pieces spread over both K-halves (three barriers per tile), and the next tile's
-//     fragments are never drained at the tile boundary (hipcc's counted lgkmcnt waits sit at their
-//     first use).  +2…12 % over INTERLEAVED and +1…8 % over the former two-phase SPLIT schedule
-//     where the operands stream from MALL/HBM (profiles/r01_session3/, docs/gemm_tuning.md).
+//     (1 read + 1 global_load_lds per 4 MFMAs).  One vmcnt(0) + barrier per tile.  Fallback for
+//     panels past 32-bit buffer offsets; A/B reference.
 //
 // Shape contract (host-checked): M % 256 == 0, N % 256 == 0, K % 64 == 0, lda/ldb/ldc % 8 == 0,
 // 16-B aligned base pointers.
@@ -229,6 +230,10 @@ amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* _
       else if (x < 9) b1[x - 1] = lds_read16(buf + b_off + (x - 1) * 2048 + fo1);
       else a1[x - 8] = lds_read16(buf + a_off + (x - 8) * 2048 + fo1);
     };
+    // at(k): the MFMA of a group after which its k-th kind of op is issued — one op per MFMA gap
+    // (an MFMA leaves ≈8 issue cycles of slack; bundling a group's reads + DMA behind its 4th
+    // MFMA cost 2.3-3.2 % on the streaming shapes, profiles/r01_session3/sweep_fine.txt)
+    auto at = [](int k) { return k; };
     dma_tile(0);
     dma_tile(min(1, T - 1));
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
@@ -242,35 +247,42 @@ amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* _
       const int td = min(t + 2, T - 1);
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
-        AMDK8S_W4_MFMA4(g, a0, b0);
-        if (g < 4) {
-          read_k1(cur, 2 * g);
-          read_k1(cur, 2 * g + 1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          AMDK8S_W4_MFMA1(g >> 1, (g & 1) * 4 + q, a0, b0);
+          if (q == at(0)) {
+            if (g < 4) read_k1(cur, 2 * g);
+            if (g == 4) read_k1(cur, 8);                 // b1[7]
+            if (g >= 6 && g < 13) read_k1(cur, g + 3);   // a1[1..7]
+          }
+          if (q == at(2) && g < 4) read_k1(cur, 2 * g + 1);
+          if (q == at(1) && g >= 6 && g < 14) dma_piece(td, 2 * (g - 6) + 1);  // odd pieces: B
+          if (q == 3 && g == 5) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            barrier_raw();  // the B region of cur is free (every b1 read is done)
+          }
         }
-        if (g == 4) read_k1(cur, 8);  // b1[7]
-        if (g == 5) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          barrier_raw();  // the B region of cur is free (every b1 read is done)
-        }
-        if (g >= 6 && g < 13) read_k1(cur, g + 3);               // a1[1..7]
-        if (g >= 6 && g < 14) dma_piece(td, 2 * (g - 6) + 1);    // B pieces are the odd ones
       }
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
-        AMDK8S_W4_MFMA4(g, a1, b1);
-        if (g == 1) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          barrier_raw();  // the A region of cur is free
-        }
-        if (g >= 2 && g < 10) dma_piece(td, 2 * (g - 2));  // A pieces are the even ones
-        if (g == 9) {
-          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile t+1 landed (this wave)
-          barrier_raw();                                       // ... for every wave
-        }
-        if (g >= 10) {
-          const int x0 = (g - 10) * 16 / 6, x1 = (g - 9) * 16 / 6;
 #pragma unroll
-          for (int x = x0; x < x1; ++x) read_k0(nxt, x);
+        for (int q = 0; q < 4; ++q) {
+          AMDK8S_W4_MFMA1(g >> 1, (g & 1) * 4 + q, a1, b1);
+          if (q == at(1) && g >= 2 && g < 10) dma_piece(td, 2 * (g - 2));  // even pieces: A
+          if (g >= 10) {  // 16 next-tile reads over groups 10-15: 2, 3, 3, 2, 3, 3
+            const int x0 = (g - 10) * 16 / 6, x1 = (g - 9) * 16 / 6;
+            if (q == at(0)) read_k0(nxt, x0);
+            if (q == at(2) && x0 + 1 < x1) read_k0(nxt, x0 + 1);
+            if (q == at(3) && x0 + 2 < x1) read_k0(nxt, x0 + 2);
+          }
+          if (q == 3 && g == 1) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            barrier_raw();  // the A region of cur is free
+          }
+          if (q == 3 && g == 9) {
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile t+1 landed (this wave)
+            barrier_raw();                                       // ... for every wave
+          }
         }
       }
       if (t + 1 >= T) {
@@ -381,8 +393,9 @@ amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* _
   }
 }
 
-// Schedule choice: REGION when A + B exceed 128 MiB (operands stream from MALL/HBM), else
-// INTERLEAVED. AMDK8S_W4_SCHEDULE=interleaved|region forces one (A/B runs).
+// Schedule choice: REGION (ties INTERLEAVED where A + B sit in the Infinity Cache, +4…34 % where
+// they stream from MALL/HBM); INTERLEAVED when a 256-row panel needs offsets past 2 GiB, or with
+// AMDK8S_W4_SCHEDULE=interleaved (A/B runs).
 extern "C" int amdk8s_gemm_bf16_nt_w4(const void* A, const void* B, void* C, int M, int N, int K,
                                       int lda, int ldb, int ldc, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
@@ -397,10 +410,7 @@ extern "C" int amdk8s_gemm_bf16_nt_w4(const void* A, const void* B, void* C, int
   const char* sbenv = getenv("AMDK8S_W4_SUPERBLOCK");
   const int sb = (M / BM) % 16 == 0 && (N / BN) % 16 == 0 && !(sbenv && sbenv[0] == '0');
   const char* schenv = getenv("AMDK8S_W4_SCHEDULE");
-  bool region = (unsigned long long)(M + N) * K * 2 > (128ull << 20);
-  if (schenv && schenv[0] == 'i') region = false;
-  if (schenv && schenv[0] == 'r') region = true;
-  region = region && panel_fits;
+  const bool region = panel_fits && !(schenv && schenv[0] == 'i');
   const uint16_t* a = (const uint16_t*)A;
   const uint16_t* b = (const uint16_t*)B;
   uint16_t* c = (uint16_t*)C;
