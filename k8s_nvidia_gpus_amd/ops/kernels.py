@@ -57,6 +57,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.amdk8s_gemm_bf16_nt.restype = ci
     lib.amdk8s_gemm_bf16_nt_w4.argtypes = [vp, vp, vp, ci, ci, ci, ci, ci, ci, vp]
     lib.amdk8s_gemm_bf16_nt_w4.restype = ci
+    lib.amdk8s_gemm_fp8_nt.argtypes = [vp, vp, vp, ci, ci, ci, ci, ci, ci, vp]
+    lib.amdk8s_gemm_fp8_nt.restype = ci
     lib.amdk8s_gemm_bf16_nt_sample_check.argtypes = [vp, vp, vp, vp, ci, ci, ci, ci, vp]
     lib.amdk8s_gemm_bf16_nt_sample_check.restype = ci
     lib.amdk8s_vector_add_f32.argtypes = [vp, vp, vp, ci, vp]
@@ -163,6 +165,51 @@ def gemm_bf16_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] =
             a.stride(0), b.stride(0), out.stride(0), _stream_handle(a.device))
     _check(rc, f"amdk8s_gemm_bf16_nt[{variant}]")
     return out
+
+
+FP8_DTYPE = torch.float8_e4m3fn  # OCP e4m3: gfx950's fp8 (not MI300's e4m3fnuz)
+
+
+def gemm_fp8_shape_supported(m: int, n: int, k: int) -> bool:
+    return m > 0 and n > 0 and k > 0 and m % 256 == 0 and n % 256 == 0 and k % 256 == 0
+
+
+def gemm_fp8_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``out = a @ b.T`` in fp8 (OCP e4m3) with fp32 accumulation and a bf16 result.
+
+    The hand-written gfx950 kernel (gemm_fp8_gfx950.hip) runs ``v_mfma_scale_f32_16x16x128_f8f6f4``
+    with unit block scales — 2× the bf16 MFMA rate — on the bf16 w4 kernel's data path.
+    ``a``: [M, K], ``b``: [N, K], both ``torch.float8_e4m3fn``, row-major with unit inner stride and
+    leading dimensions that are multiples of 16; M, N multiples of 256 and K a multiple of 256.
+    """
+    _require_gpu(a, "a")
+    _require_gpu(b, "b")
+    if a.dtype != FP8_DTYPE or b.dtype != FP8_DTYPE:
+        raise TypeError("gemm_fp8_nt expects torch.float8_e4m3fn operands")
+    if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[1]:
+        raise ValueError(f"shape mismatch: a {tuple(a.shape)} b {tuple(b.shape)}")
+    if a.stride(1) != 1 or b.stride(1) != 1:
+        raise ValueError("operands must have unit inner stride")
+    m, k = a.shape
+    n = b.shape[0]
+    if not gemm_fp8_shape_supported(m, n, k):
+        raise ValueError(f"gemm_fp8_nt needs M,N % 256 == 0 and K % 256 == 0 (got {m}x{n}x{k})")
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
+    elif out.shape != (m, n) or out.dtype != torch.bfloat16 or out.stride(1) != 1:
+        raise ValueError("bad out tensor")
+    rc = library().amdk8s_gemm_fp8_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+                                      a.stride(0), b.stride(0), out.stride(0),
+                                      _stream_handle(a.device))
+    _check(rc, "amdk8s_gemm_fp8_nt")
+    return out
+
+
+def uniform_fp8(shape, seed: int, device: torch.device) -> torch.Tensor:
+    """Uniform [-1, 1) operands rounded to e4m3 (via the bf16 fill kernel)."""
+    t = torch.empty(shape, dtype=torch.bfloat16, device=device)
+    fill_uniform_bf16(t, seed=seed)
+    return t.to(FP8_DTYPE)
 
 
 def _round_up(x: int, m: int) -> int:

@@ -192,3 +192,33 @@ def test_gemm_w4_schedule_repeatable_under_load(K, dev, schedule, monkeypatch):
     monkeypatch.setenv("AMDK8S_W4_SCHEDULE", "interleaved")
     assert torch.equal(K.gemm_bf16_nt(a, b, variant="w4"), c0)
 
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 256), (512, 256, 768), (768, 512, 2048),
+                                   (4096, 4096, 512), (2304, 1280, 1024)])
+def test_gemm_fp8_matches_fp32(K, dev, m, n, k):
+    """fp8 e4m3 GEMM against an fp32 matmul of the same (exactly representable) fp8 values."""
+    a = K.uniform_fp8((m, k), seed=m + 3 * k, device=dev)
+    b = K.uniform_fp8((n, k), seed=n + 5 * k, device=dev)
+    c = K.gemm_fp8_nt(a, b)
+    ref = a.float() @ b.float().t()
+    torch.testing.assert_close(c.float(), ref, rtol=1e-2, atol=1e-2 * (k ** 0.5) / 8)
+    assert torch.equal(K.gemm_fp8_nt(a, b), c)  # deterministic
+
+
+def test_gemm_fp8_identity_asymmetric(K, dev):
+    """A = I (exact in e4m3) with an asymmetric small-integer B returns Bᵀ exactly."""
+    s = 256
+    a = torch.eye(s, device=dev).to(K.FP8_DTYPE)
+    i = torch.arange(s, device=dev)
+    b = ((i[:, None] * 3 + i[None, :]) % 17 - 8).float().to(K.FP8_DTYPE)  # |v| ≤ 8: exact
+    c = K.gemm_fp8_nt(a, b)
+    assert torch.equal(c.float(), b.float().t())
+
+
+def test_gemm_fp8_rejects_bad_shapes(K, dev):
+    a = torch.zeros((256, 128), device=dev).to(K.FP8_DTYPE)
+    with pytest.raises(ValueError):
+        K.gemm_fp8_nt(a, a)  # K % 256 != 0
+    with pytest.raises(TypeError):
+        K.gemm_fp8_nt(a.float(), a.float())
