@@ -17,7 +17,10 @@ Outside the timed region it also reports:
 * ``time_to_first_gpu_result_s`` — process start → first verified GPU result (HIP vectorAdd,
   reference protocol), the in-process part of the "time-to-first-GPU-pod" metric;
 * ``numerics_max_rel_err`` — sampled error of the timed kernel against an fp32 on-device reference;
-* ``allreduce_busbw_gbps`` — RCCL all-reduce bus bandwidth over xGMI across the N ranks (N > 1).
+* ``allreduce_busbw_gbps`` — RCCL all-reduce bus bandwidth over xGMI across the N ranks (N > 1);
+* ``fp8_tflops`` — the validator's second precision: the same GEMM shape in OCP fp8 e4m3 through
+  the hand-written ``v_mfma_scale_f32_16x16x128_f8f6f4`` kernel, whole-job aggregate, timed the
+  same way (extra field; the headline ``value`` stays bf16).
 
 ``--cpu-smoke`` exercises the same launch/timing/JSON path on CPU (fp32 torch.matmul, gloo) for
 tests; its numbers are not measurements and are labelled as such.
@@ -50,6 +53,7 @@ def parse_args(argv=None):
     ap.add_argument("--allreduce-mib", type=int, default=256,
                     help="message size of the post-run RCCL all-reduce probe (N > 1)")
     ap.add_argument("--no-allreduce", action="store_true")
+    ap.add_argument("--no-fp8", action="store_true", help="skip the fp8 GEMM extra measurement")
     ap.add_argument("--cpu-smoke", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -163,6 +167,32 @@ def main(argv=None) -> int:
         gathered = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(gathered, mine)
         per_rank = [round(float(x.item()), 2) for x in gathered]
+    fp8_tflops = None
+    if not smoke and not args.no_fp8 and K.gemm_fp8_shape_supported(s, s, s):
+        del a, b
+        a8 = K.uniform_fp8((s, s), seed=3000 + rank, device=device)
+        b8 = K.uniform_fp8((s, s), seed=4000 + rank, device=device)
+        for _ in range(args.warmup):
+            K.gemm_fp8_nt(a8, b8, out=c)
+        sync()
+        if distributed:
+            dist.barrier()
+        sync()
+        t8 = time.perf_counter()
+        for _ in range(args.steps):
+            K.gemm_fp8_nt(a8, b8, out=c)
+        sync()
+        if distributed:
+            dist.barrier()
+        sync()
+        e8 = time.perf_counter() - t8
+        if distributed:
+            t = torch.tensor([e8], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            e8 = float(t[0].item())
+        fp8_tflops = flop_per_gpu * world / e8 / 1e12
+        del a8, b8
+
     busbw = None
     if distributed and not args.no_allreduce:
         r = measure("all_reduce", (1 if smoke else args.allreduce_mib) << 20, iters=3 if smoke else 10,
@@ -200,6 +230,7 @@ def main(argv=None) -> int:
             "time_to_first_gpu_result_s": round(ttfr, 3) if ttfr is not None else None,
             "numerics_max_rel_err": max_rel_err,
             "allreduce_busbw_gbps": (round(busbw, 2) if busbw is not None else None),
+            "fp8_tflops": (round(fp8_tflops, 2) if fp8_tflops is not None else None),
             "device": torch.cuda.get_device_name(device) if device.type == "cuda" else "cpu",
         }
         print(json.dumps(out), flush=True)

@@ -47,6 +47,8 @@ DEFAULTS: Dict[str, Any] = {
         "gemm": True,
         "gemmSize": 8192,
         "gemmMinTflops": 900,
+        "gemmFp8": True,             # also run the fp8 (OCP e4m3) MFMA GEMM
+        "gemmFp8MinTflops": 1800,
         "rocprof": False,            # run the GEMM step under rocprofv3 --kernel-trace --stats
         "rccl": True,
         "rcclMinBusbwGBps": 100,

@@ -276,6 +276,9 @@ class GpuCollector:
                                    labels=["node", "step"])
         tflops = GaugeMetricFamily("amd_gpu_validator_gemm_tflops",
                                    "bf16 MFMA GEMM TFLOPS measured by the validator", labels=["node", "gpu"])
+        tflops8 = GaugeMetricFamily("amd_gpu_validator_gemm_fp8_tflops",
+                                    "fp8 (e4m3) MFMA GEMM TFLOPS measured by the validator",
+                                    labels=["node", "gpu"])
         busbw = GaugeMetricFamily("amd_gpu_validator_allreduce_busbw_gbps",
                                   "RCCL all-reduce bus bandwidth measured by the validator",
                                   labels=["node", "ngpus"])
@@ -286,10 +289,14 @@ class GpuCollector:
                 for r in v.get("devices", []):
                     if r.get("tflops") is not None:
                         tflops.add_metric([self.node, str(r.get("device"))], float(r["tflops"]))
+                for r in (v.get("fp8") or {}).get("devices", []):
+                    if r.get("tflops") is not None:
+                        tflops8.add_metric([self.node, str(r.get("device"))], float(r["tflops"]))
             if step == "rccl" and isinstance(v, dict) and v.get("peak_busbw_gbps") is not None:
                 busbw.add_metric([self.node, str(v.get("ngpus"))], float(v["peak_busbw_gbps"]))
         yield passed
         yield tflops
+        yield tflops8
         yield busbw
 
 

@@ -9,7 +9,8 @@ the previous one's marker under ``/run/amd/validations``:
   driver    kfd-probe: ≥ expectedGpusPerNode gfx950 agents, /dev/kfd + render nodes usable
   runtime   the runtime installer published runtime-ready (amd-container-runtime + CDI spec)
   vectoradd hand-written HIP vectorAdd on every GPU, reference stdout protocol
-  gemm      hand-written gfx950 bf16 MFMA GEMM on every GPU: numerics vs fp32 + TFLOPS ≥ floor
+  gemm      hand-written gfx950 bf16 (and fp8 e4m3) MFMA GEMMs on every GPU: numerics vs fp32 +
+            TFLOPS ≥ floor per precision
   rccl      RCCL all-reduce over xGMI across all GPUs of the node: exact sums + bus bandwidth floor
   plugin    a pod requesting amd.com/gpu: 1 is scheduled THROUGH the device plugin and passes
   report    node label amd.com/gpu.validated=true|false, validator-ready marker
@@ -181,32 +182,44 @@ class Validator:
         return StepResult("vectoradd", bool(ok), {"devices": devs},
                           "" if ok else f"rc={rc}: " + out.strip()[-300:])
 
-    def step_gemm(self) -> StepResult:
-        size = int(self.vcfg["gemmSize"])
-        floor = float(self.vcfg["gemmMinTflops"])
+    def _gemm_run(self, dtype: str, size: int, floor: float, rocprof: bool) -> Tuple[bool, Dict, str]:
         argv = [self._bin("amd-gemm-validator"), "--size", str(size), "--iters", "50", "--json"]
+        if dtype != "bf16":
+            argv += ["--dtype", dtype]
         prof_dir = None
-        if self.vcfg.get("rocprof"):
+        if rocprof:
             # BASELINE config 3: the validator GEMM "shown in rocprof" — kernel trace + stats of the
             # validator run itself, kept next to the step result (and exported as an artefact)
-            prof_dir = self._path("gemm-rocprof")
+            prof_dir = self._path("gemm-rocprof" if dtype == "bf16" else f"gemm-{dtype}-rocprof")
             argv = ["rocprofv3", "--kernel-trace", "--stats", "-d", prof_dir, "-o", "gemm",
                     "--output-format", "csv", "--"] + argv
         rc, out = self.run_cmd(argv, 900)
-        devs = [d for d in json_lines(out) if d.get("check") == "gemm_bf16"]
+        devs = [d for d in json_lines(out) if d.get("check") == f"gemm_{dtype}"]
         slow = [d for d in devs if float(d.get("tflops", 0)) < floor]
         bad = [d for d in devs if not d.get("passed")]
-        ok = rc == 0 and protocol_passed(out) and devs and not slow and not bad
+        ok = rc == 0 and protocol_passed(out) and bool(devs) and not slow and not bad
         reason = ""
         if not ok:
-            reason = (f"{len(bad)} GPU(s) failed numerics; " if bad else "") + \
-                     (f"{len(slow)} GPU(s) below {floor} TFLOPS; " if slow else "") + \
-                     (f"rc={rc}" if rc else "")
+            reason = (f"{len(bad)} GPU(s) failed {dtype} numerics; " if bad else "") + \
+                     (f"{len(slow)} GPU(s) below {floor} {dtype} TFLOPS; " if slow else "") + \
+                     (f"{dtype} rc={rc}" if rc else "") + ("" if devs else f" no {dtype} result")
         total = sum(float(d.get("tflops", 0)) for d in devs)
         detail = {"devices": devs, "size": size, "floor_tflops": floor,
                   "aggregate_tflops": round(total, 1)}
         if prof_dir:
             detail["rocprof_kernels"] = rocprof_kernel_stats(prof_dir)
+        return ok, detail, reason.strip()
+
+    def step_gemm(self) -> StepResult:
+        size = int(self.vcfg["gemmSize"])
+        rocprof = bool(self.vcfg.get("rocprof"))
+        ok, detail, reason = self._gemm_run("bf16", size, float(self.vcfg["gemmMinTflops"]), rocprof)
+        if self.vcfg.get("gemmFp8"):
+            ok8, detail8, reason8 = self._gemm_run("fp8", size, float(self.vcfg["gemmFp8MinTflops"]),
+                                                   rocprof)
+            detail["fp8"] = detail8
+            ok = ok and ok8
+            reason = "; ".join(r for r in (reason, reason8) if r)
         return StepResult("gemm", bool(ok), detail, reason)
 
     def step_rccl(self, ngpus: Optional[int] = None) -> StepResult:

@@ -246,3 +246,40 @@ extern "C" int amdk8s_gemm_fp8_nt(const void* A, const void* B, void* C, int M, 
                      (const uint8_t*)A, (const uint8_t*)B, (uint16_t*)C, M, N, K, lda, ldb, ldc, sb);
   return (int)hipGetLastError();
 }
+
+// out[s] = Σ_k A[m_s,k]·B[n_s,k] in fp32 for a list of sample coordinates (fp8 decoded by
+// v_cvt_f32_fp8, independent of the MFMA path).
+extern "C" __global__ void amdk8s_gemm_fp8_nt_sample_ref(const uint8_t* __restrict__ A,
+                                                         const uint8_t* __restrict__ B,
+                                                         const int* __restrict__ coords,
+                                                         float* __restrict__ out, int nsamples,
+                                                         int K, int lda, int ldb) {
+  const int s = blockIdx.x;
+  if (s >= nsamples) return;
+  const int m = coords[2 * s], n = coords[2 * s + 1];
+  float sum = 0.f;
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    const float a = __builtin_amdgcn_cvt_f32_fp8((int)A[(size_t)m * lda + k], 0);
+    const float b = __builtin_amdgcn_cvt_f32_fp8((int)B[(size_t)n * ldb + k], 0);
+    sum = fmaf(a, b, sum);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) sum += __shfl_down(sum, off, 64);
+  __shared__ float part[16];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int w = 0; w < (int)(blockDim.x + 63) / 64; ++w) tot += part[w];
+    out[s] = tot;
+  }
+}
+
+extern "C" int amdk8s_gemm_fp8_nt_sample_check(const void* A, const void* B, const int* coords,
+                                               float* out, int nsamples, int K, int lda, int ldb,
+                                               hipStream_t stream) {
+  if (nsamples <= 0) return 0;
+  hipLaunchKernelGGL(amdk8s_gemm_fp8_nt_sample_ref, dim3(nsamples), dim3(256), 0, stream,
+                     (const uint8_t*)A, (const uint8_t*)B, coords, out, nsamples, K, lda, ldb);
+  return (int)hipGetLastError();
+}

@@ -69,6 +69,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.amdk8s_vector_add_blocks.restype = ci
     lib.amdk8s_fill_uniform_bf16.argtypes = [vp, cl, cu64, cf, cf, vp]
     lib.amdk8s_fill_uniform_bf16.restype = ci
+    lib.amdk8s_fill_uniform_fp8.argtypes = [vp, cl, cu64, cf, cf, vp]
+    lib.amdk8s_fill_uniform_fp8.restype = ci
 
 
 def library(build_if_missing: bool = True) -> ctypes.CDLL:
@@ -205,11 +207,16 @@ def gemm_fp8_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = 
     return out
 
 
-def uniform_fp8(shape, seed: int, device: torch.device) -> torch.Tensor:
-    """Uniform [-1, 1) operands rounded to e4m3 (via the bf16 fill kernel)."""
-    t = torch.empty(shape, dtype=torch.bfloat16, device=device)
-    fill_uniform_bf16(t, seed=seed)
-    return t.to(FP8_DTYPE)
+def uniform_fp8(shape, seed: int, device: torch.device, lo: float = -1.0,
+                hi: float = 1.0) -> torch.Tensor:
+    """Uniform [lo, hi) operands rounded to OCP e4m3 on the device (v_cvt_pk_fp8_f32)."""
+    t = torch.empty(shape, dtype=FP8_DTYPE, device=device)
+    if t.numel() % 4:
+        raise ValueError("uniform_fp8 fills whole 4-byte words: numel must be a multiple of 4")
+    rc = library().amdk8s_fill_uniform_fp8(t.data_ptr(), t.numel(), seed & (2 ** 64 - 1), lo, hi,
+                                           _stream_handle(t.device))
+    _check(rc, "amdk8s_fill_uniform_fp8")
+    return t
 
 
 def _round_up(x: int, m: int) -> int:

@@ -24,6 +24,11 @@ int amdk8s_gemm_bf16_nt_w4(const void* A, const void* B, void* C, int M, int N, 
                            int ldb, int ldc, hipStream_t stream);
 int amdk8s_gemm_bf16_nt_sample_check(const void* A, const void* B, const int* coords, float* out,
                                      int nsamples, int K, int lda, int ldb, hipStream_t stream);
+// k8s_nvidia_gpus_amd/ops/csrc/gemm_fp8_gfx950.hip
+int amdk8s_gemm_fp8_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                       int ldb, int ldc, hipStream_t stream);
+int amdk8s_gemm_fp8_nt_sample_check(const void* A, const void* B, const int* coords, float* out,
+                                    int nsamples, int K, int lda, int ldb, hipStream_t stream);
 // k8s_nvidia_gpus_amd/ops/csrc/vector_add.hip
 int amdk8s_vector_add_f32(const float* a, const float* b, float* c, int n, hipStream_t stream);
 int amdk8s_vector_add_f32_bw(const float* a, const float* b, float* c, long n, int num_cus,
@@ -32,6 +37,8 @@ int amdk8s_vector_add_blocks(int n);
 // k8s_nvidia_gpus_amd/ops/csrc/fill.hip
 int amdk8s_fill_uniform_bf16(void* dst, long n, unsigned long long seed, float lo, float hi,
                              hipStream_t stream);
+int amdk8s_fill_uniform_fp8(void* dst, long n, unsigned long long seed, float lo, float hi,
+                            hipStream_t stream);
 }
 #endif  // __HIPCC__
 

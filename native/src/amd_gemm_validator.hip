@@ -1,4 +1,4 @@
-// amd-gemm-validator — hand-written gfx950 bf16 MFMA GEMM load + numerics check.
+// amd-gemm-validator — hand-written gfx950 bf16 / fp8 MFMA GEMM load + numerics check.
 //
 // Plays the role NVIDIA's dcgmproftester tensor-core load plays for the reference's operator
 // (BASELINE.json configs 3/4): it drives the in-tree 256×256 MFMA kernel
@@ -6,6 +6,7 @@
 // parallel (one host thread per device), on random [-1,1) bf16 data (never zeros — zero operands
 // inflate MFMA clocks), checks a sample of outputs against an fp32 on-device reference and reports
 // TFLOPS per GPU and in aggregate.  Output ends with "Test PASSED" / "Done" like amd-vectoradd.
+// --dtype fp8 runs the OCP-e4m3 kernel (gemm_fp8_gfx950.hip, 2× the bf16 MFMA rate) instead.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -27,6 +28,7 @@ namespace {
 // (= w4, which picks its own K-loop schedule by operand footprint; docs/gemm_tuning.md).
 int gemm(const std::string& variant, const void* A, const void* B, void* C, int m, int n, int k,
          hipStream_t s) {
+  if (variant == "fp8") return amdk8s_gemm_fp8_nt(A, B, C, m, n, k, k, k, n, s);
   const bool w4 = variant != "w8";
   return w4 ? amdk8s_gemm_bf16_nt_w4(A, B, C, m, n, k, k, k, n, s)
             : amdk8s_gemm_bf16_nt(A, B, C, m, n, k, k, k, n, s);
@@ -39,6 +41,7 @@ struct Options {
   int samples = 2048;
   bool json = false;
   std::string variant = "auto";
+  std::string dtype = "bf16";
   unsigned long long seed = 42;
 };
 
@@ -70,14 +73,18 @@ void run(int dev, const Options& o, int nthreads, Result* r) {
   r->arch = prop.gcnArchName;
   r->cus = prop.multiProcessorCount;
   const size_t M = o.m, N = o.n, K = o.k;
+  const bool fp8 = o.dtype == "fp8";
+  const std::string variant = fp8 ? "fp8" : o.variant;
+  const size_t esz = fp8 ? 1 : 2;  // operand element bytes
   void *A, *B, *C;
-  AMDK8S_HIP_CHECK(hipMalloc(&A, M * K * 2));
-  AMDK8S_HIP_CHECK(hipMalloc(&B, N * K * 2));
+  AMDK8S_HIP_CHECK(hipMalloc(&A, M * K * esz));
+  AMDK8S_HIP_CHECK(hipMalloc(&B, N * K * esz));
   AMDK8S_HIP_CHECK(hipMalloc(&C, M * N * 2));
   hipStream_t s;
   AMDK8S_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  AMDK8S_HIP_CHECK((hipError_t)amdk8s_fill_uniform_bf16(A, (long)(M * K), o.seed * 2 + 1, -1.f, 1.f, s));
-  AMDK8S_HIP_CHECK((hipError_t)amdk8s_fill_uniform_bf16(B, (long)(N * K), o.seed * 2 + 2, -1.f, 1.f, s));
+  auto fill = fp8 ? amdk8s_fill_uniform_fp8 : amdk8s_fill_uniform_bf16;
+  AMDK8S_HIP_CHECK((hipError_t)fill(A, (long)(M * K), o.seed * 2 + 1, -1.f, 1.f, s));
+  AMDK8S_HIP_CHECK((hipError_t)fill(B, (long)(N * K), o.seed * 2 + 2, -1.f, 1.f, s));
   AMDK8S_HIP_CHECK(hipMemsetAsync(C, 0xFF, M * N * 2, s));  // poison: NaN pattern
 
   // numerics: sampled fp32 reference
@@ -93,14 +100,14 @@ void run(int dev, const Options& o, int nthreads, Result* r) {
   AMDK8S_HIP_CHECK(hipMalloc(&dref, o.samples * sizeof(float)));
   AMDK8S_HIP_CHECK(hipMemcpyAsync(dcoords, coords.data(), coords.size() * sizeof(int),
                                   hipMemcpyHostToDevice, s));
-  int rc = gemm(o.variant, A, B, C, o.m, o.n, o.k, s);
+  int rc = gemm(variant, A, B, C, o.m, o.n, o.k, s);
   if (rc != 0) {
     std::fprintf(stderr, "device %d: GEMM launch rejected (error %d): shape %dx%dx%d must be "
-                 "multiples of 256x256x64\n", dev, rc, o.m, o.n, o.k);
+                 "multiples of 256x256x%d\n", dev, rc, o.m, o.n, o.k, fp8 ? 256 : 64);
     return;
   }
-  AMDK8S_HIP_CHECK((hipError_t)amdk8s_gemm_bf16_nt_sample_check(A, B, dcoords, dref, o.samples,
-                                                                o.k, o.k, o.k, s));
+  auto check = fp8 ? amdk8s_gemm_fp8_nt_sample_check : amdk8s_gemm_bf16_nt_sample_check;
+  AMDK8S_HIP_CHECK((hipError_t)check(A, B, dcoords, dref, o.samples, o.k, o.k, o.k, s));
   std::vector<float> ref(o.samples);
   AMDK8S_HIP_CHECK(hipMemcpyAsync(ref.data(), dref, o.samples * sizeof(float),
                                   hipMemcpyDeviceToHost, s));
@@ -124,7 +131,7 @@ void run(int dev, const Options& o, int nthreads, Result* r) {
   r->max_rel_err = worst;
 
   // timing: all device threads start the timed loop together
-  for (int i = 0; i < o.warmup; ++i) gemm(o.variant, A, B, C, o.m, o.n, o.k, s);
+  for (int i = 0; i < o.warmup; ++i) gemm(variant, A, B, C, o.m, o.n, o.k, s);
   AMDK8S_HIP_CHECK(hipStreamSynchronize(s));
   g_ready.fetch_add(1);
   while (g_ready.load() < nthreads) std::this_thread::yield();
@@ -132,7 +139,7 @@ void run(int dev, const Options& o, int nthreads, Result* r) {
   AMDK8S_HIP_CHECK(hipEventCreate(&e0));
   AMDK8S_HIP_CHECK(hipEventCreate(&e1));
   AMDK8S_HIP_CHECK(hipEventRecord(e0, s));
-  for (int i = 0; i < o.iters; ++i) gemm(o.variant, A, B, C, o.m, o.n, o.k, s);
+  for (int i = 0; i < o.iters; ++i) gemm(variant, A, B, C, o.m, o.n, o.k, s);
   AMDK8S_HIP_CHECK(hipEventRecord(e1, s));
   AMDK8S_HIP_CHECK(hipEventSynchronize(e1));
   float ms = 0;
@@ -172,9 +179,11 @@ int main(int argc, char** argv) {
     else if (a == "--seed") o.seed = std::strtoull(next(), nullptr, 10);
     else if (a == "--json") o.json = true;
     else if (a == "--variant") o.variant = next();
+    else if (a == "--dtype") o.dtype = next();
     else {
       std::printf("usage: amd-gemm-validator [--size S | --m M --n N --k K] [--iters I] "
-                  "[--warmup W] [--device D] [--samples S] [--variant auto|w8|w4] [--json]\n");
+                  "[--warmup W] [--device D] [--samples S] [--variant auto|w8|w4] [--dtype bf16|fp8] "
+                  "[--json]\n");
       return a == "-h" || a == "--help" ? 0 : 2;
     }
   }
@@ -190,8 +199,12 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "device %d not visible (%d devices)\n", o.device, ndev);
     return 1;
   }
-  std::printf("[bf16 MFMA GEMM %dx%dx%d (C = A*B^T), %zu device(s), %d iters]\n", o.m, o.n, o.k,
-              devs.size(), o.iters);
+  if (o.dtype != "bf16" && o.dtype != "fp8") {
+    std::fprintf(stderr, "--dtype must be bf16 or fp8\n");
+    return 2;
+  }
+  std::printf("[%s MFMA GEMM %dx%dx%d (C = A*B^T), %zu device(s), %d iters]\n", o.dtype.c_str(),
+              o.m, o.n, o.k, devs.size(), o.iters);
   std::vector<Result> res(devs.size());
   std::vector<std::thread> th;
   for (size_t i = 0; i < devs.size(); ++i)
@@ -206,9 +219,9 @@ int main(int argc, char** argv) {
     agg += r.tflops;
     ok = ok && r.ok;
     if (o.json)
-      std::printf("{\"check\": \"gemm_bf16\", \"device\": %d, \"arch\": \"%s\", \"m\": %d, \"n\": %d, "
+      std::printf("{\"check\": \"gemm_%s\", \"device\": %d, \"arch\": \"%s\", \"m\": %d, \"n\": %d, "
                   "\"k\": %d, \"ms_per_iter\": %.4f, \"tflops\": %.2f, \"bad_samples\": %d, "
-                  "\"passed\": %s}\n", r.device, r.arch.c_str(), o.m, o.n, o.k, r.ms_per_iter,
+                  "\"passed\": %s}\n", o.dtype.c_str(), r.device, r.arch.c_str(), o.m, o.n, o.k, r.ms_per_iter,
                   r.tflops, r.bad, r.ok ? "true" : "false");
   }
   std::printf("aggregate: %.1f TFLOPS over %zu device(s) (%.1f TFLOPS/GPU)\n", agg, devs.size(),

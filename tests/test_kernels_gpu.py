@@ -222,3 +222,14 @@ def test_gemm_fp8_rejects_bad_shapes(K, dev):
         K.gemm_fp8_nt(a, a)  # K % 256 != 0
     with pytest.raises(TypeError):
         K.gemm_fp8_nt(a.float(), a.float())
+
+
+def test_fill_uniform_fp8_is_ocp_e4m3(K, dev):
+    """The device fill's bytes decode (as torch.float8_e4m3fn) to the e4m3 rounding of values in
+    [-1, 1): the in-kernel v_cvt_pk_fp8_f32 produces OCP e4m3, the format the GEMM assumes."""
+    t = K.uniform_fp8((1024, 1024), seed=5, device=dev)
+    f = t.float()
+    assert f.min().item() >= -1.0 and f.max().item() <= 1.0
+    assert abs(f.mean().item()) < 0.01 and 0.5 < f.std().item() < 0.65
+    assert torch.equal(f.to(K.FP8_DTYPE).float(), f)  # every value is an e4m3 value
+    assert len(torch.unique(f)) > 100

@@ -127,7 +127,8 @@ def test_exporter_amdsmi_backend_metrics(tmp_path):
     marker = tmp_path / "v"
     marker.mkdir()
     (marker / "gemm.json").write_text(json.dumps({"passed": True, "devices": [
-        {"device": 0, "tflops": 1389.4}, {"device": 1, "tflops": 1380.0}]}))
+        {"device": 0, "tflops": 1389.4}, {"device": 1, "tflops": 1380.0}],
+        "fp8": {"devices": [{"device": 0, "tflops": 2858.1}]}}))
     (marker / "rccl.json").write_text(json.dumps({"passed": True, "ngpus": 8, "peak_busbw_gbps": 310.5}))
     fake = FakeAmdSmi()
     col = ex.GpuCollector(ex.AmdSmiBackend(fake), "gpu-node-1", str(marker))
@@ -145,6 +146,7 @@ def test_exporter_amdsmi_backend_metrics(tmp_path):
     assert len(links) == 8 and max(links) > 1e10
     assert _find(sm, "amd_gpu_ecc_errors_total", gpu=0, type="uncorrectable") == [0.0]
     assert _find(sm, "amd_gpu_validator_gemm_tflops", gpu=0, node="gpu-node-1") == [1389.4]
+    assert _find(sm, "amd_gpu_validator_gemm_fp8_tflops", gpu=0) == [2858.1]
     assert _find(sm, "amd_gpu_validator_allreduce_busbw_gbps", ngpus=8) == [310.5]
     assert _find(sm, "amd_gpu_validation_passed", step="gemm") == [1.0]
     # N/A fields (edge temperature) are omitted, not exported as 0
@@ -322,19 +324,24 @@ def test_driver_module_loading(tmp_path):
 def test_validator_gemm_step_under_rocprof(tmp_path):
     from k8s_nvidia_gpus_amd.operator.validator import Validator
 
-    log = (Path(__file__).resolve().parent.parent / "profiles/r01_gemm_validator.log").read_text()
+    prof = Path(__file__).resolve().parent.parent / "profiles"
+    logs = {"bf16": (prof / "r01_gemm_validator.log").read_text(),
+            "fp8": (prof / "r01_gemm_validator_fp8.log").read_text()}
+    kernels = {"bf16": "amdk8s_gemm_bf16_nt_256x256", "fp8": "amdk8s_gemm_fp8_nt_256x256"}
     seen = []
 
     def runner(argv, timeout):
         seen.append(argv)
+        dtype = argv[argv.index("--dtype") + 1] if "--dtype" in argv else "bf16"
         d = Path(argv[argv.index("-d") + 1]) / "run"
         d.mkdir(parents=True)
         (d / "gemm_kernel_stats.csv").write_text(
             '"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\n'
-            '"amdk8s_gemm_bf16_nt_256x256",60,47700000,795000.0,98.9,782807,1030849,66849.2\n')
-        return 0, log
+            f'"{kernels[dtype]}",60,47700000,795000.0,98.9,782807,1030849,66849.2\n')
+        return 0, logs[dtype]
 
     cfg = load_config(text="validator: {rocprof: true}\n")
     r = Validator(cfg, str(tmp_path), bin_dir="/b", runner=runner).run_step("gemm")
     assert r.passed and seen[0][:3] == ["rocprofv3", "--kernel-trace", "--stats"]
     assert r.detail["rocprof_kernels"][0]["name"] == "amdk8s_gemm_bf16_nt_256x256"
+    assert r.detail["fp8"]["rocprof_kernels"][0]["name"] == "amdk8s_gemm_fp8_nt_256x256"

@@ -21,6 +21,7 @@ from k8s_nvidia_gpus_amd.utils.kube import KubeClient
 REPO = Path(__file__).resolve().parent.parent
 VECTORADD_LOG = (REPO / "profiles/r01_vectoradd.log").read_text()
 GEMM_LOG = (REPO / "profiles/r01_gemm_validator.log").read_text()
+GEMM_FP8_LOG = (REPO / "profiles/r01_gemm_validator_fp8.log").read_text()
 RCCL_8GPU = """# rccl-allreduce-bench: 8 GPU(s), RCCL 22703, in-place float sum, 20 iters
 {"check": "rccl_allreduce", "ngpus": 8, "peak_busbw_gbps": 301.20, "peak_algbw_gbps": 172.11, "peak_bytes": 1073741824, "wrong": 0, "passed": true}
 Test PASSED
@@ -36,6 +37,8 @@ class Runner:
     def __call__(self, argv, timeout):
         self.calls.append(list(argv))
         name = os.path.basename(argv[0])
+        if "--dtype" in argv:  # e.g. "amd-gemm-validator:fp8"
+            name += ":" + argv[argv.index("--dtype") + 1]
         rc, out = self.outputs[name]
         return rc, out
 
@@ -53,7 +56,8 @@ def test_protocol_parser():
 
 
 def test_vectoradd_and_gemm_steps_on_real_outputs(tmp_path, cfg):
-    r = Runner({"amd-vectoradd": (0, VECTORADD_LOG), "amd-gemm-validator": (0, GEMM_LOG)})
+    r = Runner({"amd-vectoradd": (0, VECTORADD_LOG), "amd-gemm-validator": (0, GEMM_LOG),
+                "amd-gemm-validator:fp8": (0, GEMM_FP8_LOG)})
     v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=r)
     va = v.run_step("vectoradd")
     assert va.passed and va.detail["devices"][0]["elements"] == 50000
@@ -68,7 +72,8 @@ def test_vectoradd_and_gemm_steps_on_real_outputs(tmp_path, cfg):
 def test_gemm_step_enforces_tflops_floor(tmp_path):
     cfg = load_config(text="validator: {gemmMinTflops: 2000}\n")
     v = Validator(cfg, str(tmp_path), bin_dir="/x",
-                  runner=Runner({"amd-gemm-validator": (0, GEMM_LOG)}))
+                  runner=Runner({"amd-gemm-validator": (0, GEMM_LOG),
+                                 "amd-gemm-validator:fp8": (0, GEMM_FP8_LOG)}))
     g = v.run_step("gemm")
     assert not g.passed and "below 2000" in g.reason
     assert not (tmp_path / "gemm-ready").exists()
@@ -76,7 +81,8 @@ def test_gemm_step_enforces_tflops_floor(tmp_path):
 
 def test_gemm_step_fails_on_numerics(tmp_path, cfg):
     bad = GEMM_LOG.replace('"passed": true', '"passed": false').replace("Test PASSED", "Test FAILED")
-    v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=Runner({"amd-gemm-validator": (1, bad)}))
+    v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=Runner({
+        "amd-gemm-validator": (1, bad), "amd-gemm-validator:fp8": (0, GEMM_FP8_LOG)}))
     assert not v.run_step("gemm").passed
 
 
@@ -174,3 +180,29 @@ def test_plugin_step_schedules_a_gpu_pod(tmp_path, cfg, monkeypatch):
         assert api.nodes["gpu-node-1"]["metadata"]["labels"]["amd.com/gpu.validated"] == "false"
     finally:
         api.stop()
+
+
+def test_gemm_step_runs_fp8_on_real_output(tmp_path, cfg):
+    """The fp8 half of the GEMM step: parsed from the native validator's real MI355X output,
+    reported next to bf16, and held to its own floor."""
+    r = Runner({"amd-gemm-validator": (0, GEMM_LOG), "amd-gemm-validator:fp8": (0, GEMM_FP8_LOG)})
+    v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=r)
+    g = v.run_step("gemm")
+    assert g.passed, g.reason
+    assert r.calls[-1][-2:] == ["--dtype", "fp8"]
+    d = json.loads((tmp_path / "gemm.json").read_text())
+    assert d["fp8"]["aggregate_tflops"] > 2 * 1300
+    assert d["fp8"]["devices"][0]["check"] == "gemm_fp8"
+
+    strict = load_config(text="validator: {gemmFp8MinTflops: 10000}\n")
+    v2 = Validator(strict, str(tmp_path / "s"), bin_dir="/x", runner=r)
+    g2 = v2.run_step("gemm")
+    assert not g2.passed and "fp8" in g2.reason
+
+
+def test_gemm_step_fp8_can_be_disabled(tmp_path):
+    cfg = load_config(text="validator: {gemmFp8: false}\n")
+    r = Runner({"amd-gemm-validator": (0, GEMM_LOG)})  # no fp8 output available: must not be run
+    v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=r)
+    assert v.run_step("gemm").passed
+    assert len(r.calls) == 1 and "fp8" not in json.loads((tmp_path / "gemm.json").read_text())

@@ -12,8 +12,10 @@ tail -3 gpurun_out/session/pytest_gpu.log
 echo "== bench.py (defaults)"
 timeout -k 10 600 python bench.py > gpurun_out/session/bench.json 2> gpurun_out/session/bench.err || { cat gpurun_out/session/bench.err | tail -20; exit 1; }
 cat gpurun_out/session/bench.json
-echo "== bench.py --variant w4 (A/B)"
-timeout -k 10 600 python bench.py --variant w4 > gpurun_out/session/bench_w4.json 2>/dev/null && cat gpurun_out/session/bench_w4.json
+echo "== native validator (bf16 + fp8)"
+timeout -k 10 300 native/bin/amd-gemm-validator --size 8192 --iters 50 --json > gpurun_out/session/gemm_validator_bf16.log 2>&1
+timeout -k 10 300 native/bin/amd-gemm-validator --dtype fp8 --size 8192 --iters 50 --json > gpurun_out/session/gemm_validator_fp8.log 2>&1
+grep -h '"check"' gpurun_out/session/gemm_validator_*.log
 if [[ "${PROFILE:-1}" == 1 ]]; then
   echo "== rocprofv3 kernel stats"
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/session/prof -o bench --output-format csv -- python3 bench.py --steps 20 --warmup 5 > gpurun_out/session/prof.log 2>&1 || { tail -20 gpurun_out/session/prof.log; exit 1; }
