@@ -100,6 +100,20 @@ def test_gpu_workloads_depend_on_the_operator():
     assert ks["amd-gpu-operator"]["spec"]["wait"] is True
 
 
+def test_cpu_only_plumbing_app_reconciles_without_gpu():
+    """BASELINE config 1: a Flux Kustomization with no dependency on the GPU operator whose busybox
+    pod requests no GPU, so Git → Flux → node is provable on its own."""
+    ks = {k["metadata"]["name"]: k for k in flux_kustomizations()}
+    spec = ks["plumbing"]["spec"]
+    assert spec["path"] == "./cluster-config/apps/plumbing" and spec["wait"] is True
+    assert not spec.get("dependsOn") and not spec.get("suspend")
+    k, objs = resources_of(CC / "apps/plumbing")
+    (dep,) = [o for o in objs if o["kind"] == "Deployment"]
+    (c,) = dep["spec"]["template"]["spec"]["containers"]
+    assert c["image"].startswith("busybox:") and not _gpu_request(c)
+    assert "runtimeClassName" not in dep["spec"]["template"]["spec"]
+
+
 def test_flux_bootstrap_entry():
     k = yaml.safe_load((CC / "cluster/flux-system/kustomization.yaml").read_text())
     assert k["namespace"] == "flux-system"
