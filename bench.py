@@ -4,8 +4,8 @@
 BASELINE.json names the metric "validator-pod bf16 GEMM TFLOPS/GPU + time-to-first-GPU-pod,
 1/2/4/8 MI355X".  One *step* is what the operator's validator pod runs on each GPU it was
 allocated: one 8192×8192×8192 bf16 GEMM (C = A·Bᵀ, fp32 accumulate, bf16 out) through the
-hand-written gfx950 MFMA kernels (k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950*.hip, variant
-picked by operand footprint), on random [-1,1) operands (synthetic data).  Work per GPU is fixed as
+hand-written gfx950 MFMA kernels (k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950*.hip; default
+w4a, whose K-loop is generated assembly), on random [-1,1) operands (synthetic data).  Work per GPU is fixed as
 N grows → weak scaling.
 
 Launch contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 under
@@ -222,7 +222,8 @@ def main(argv=None) -> int:
                 "seq_len": s,
                 "parallelism": f"dp{world}" if world > 1 else "single",
                 "m": s, "n": s, "k": s,
-                "kernel": {"w8": "amdk8s_gemm_bf16_nt_256x256", "w4": "amdk8s_gemm_bf16_nt_256x256_w4"}
+                "kernel": {"w8": "amdk8s_gemm_bf16_nt_256x256", "w4": "amdk8s_gemm_bf16_nt_256x256_w4",
+                           "w4a": "amdk8s_gemm_bf16_nt_256x256_w4a"}
                 .get(variant, "torch.matmul (cpu smoke)"),
             },
             "tflops_per_gpu": round(value / world, 2),

@@ -71,6 +71,7 @@ NATIVE_TARGETS: List[NativeTarget] = [
     NativeTarget("amd-gemm-validator", ["native/src/amd_gemm_validator.hip",
                                         "k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950.hip",
                                         "k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950_w4.hip",
+                                        "k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950_w4a.hip",
                                         "k8s_nvidia_gpus_amd/ops/csrc/gemm_fp8_gfx950.hip",
                                         "k8s_nvidia_gpus_amd/ops/csrc/fill.hip"], "hipcc"),
     NativeTarget("rccl-allreduce-bench", ["native/src/rccl_allreduce_bench.hip"], "hipcc",
@@ -101,7 +102,8 @@ def kernel_sources() -> List[Path]:
 
 
 def _headers() -> List[Path]:
-    return sorted(CSRC_DIR.glob("*.h")) + sorted((NATIVE_DIR / "include").glob("*.h*"))
+    return (sorted(CSRC_DIR.glob("*.h")) + sorted(CSRC_DIR.glob("*.inc"))
+            + sorted((NATIVE_DIR / "include").glob("*.h*")))
 
 
 def build_kernel_library(force: bool = False, verbose: bool = False, jobs: int = 4) -> Path:

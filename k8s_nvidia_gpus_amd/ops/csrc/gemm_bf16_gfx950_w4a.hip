@@ -1,0 +1,138 @@
+// Hand-scheduled bf16 MFMA GEMM for MI355X (gfx950): the w4 kernel (gemm_bf16_gfx950_w4.hip) with
+// its whole K-loop as generated assembly.
+//
+//   C[M,N] (bf16) = A[M,K] (bf16, row-major) · B[N,K]ᵀ (bf16, row-major), fp32 accumulation.
+//
+// Same geometry, LDS image and REGION op placement as w4 (256×256×64 block tile, 4 waves of
+// 128×128, v_mfma_f32_16x16x32_bf16 into 256 AGPRs, two 64 KiB LDS-DMA buffers with the
+// source-side XOR swizzle, one op per MFMA gap, three barriers per K-tile). What changes is who
+// writes the instruction stream: tools/gen_gemm_w4a_kloop.py emits the prologue DMA, the K-loop
+// (unrolled over the two buffer parities) and the accumulator → bf16 → LDS C-image conversion with
+// every register explicit. hipcc's version of the same loop carries ≈ 27 more non-MFMA instructions
+// per K-tile than hipBLASLt's assembly kernel of this geometry (counted lgkmcnt waits that also
+// count LDS-DMA, s_mov m0 + s_nop pairs, per-piece SALU address math); here the DMA source advances
+// by one 64-bit rsrc add per operand per K-tile, M0 is set one MFMA ahead of its DMA, and the
+// lgkmcnt before each MFMA is the exact in-order count (docs/gemm_tuning.md, session 4).
+//
+// Shape contract (host-checked): M % 256 == 0, N % 256 == 0, K % 64 == 0, lda/ldb/ldc % 8 == 0,
+// 16-B aligned base pointers, 256·lda·2 and 256·ldb·2 < 2³¹ (32-bit panel offsets).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "gemm_bf16_gfx950_w4a_kloop.inc"
+
+namespace {
+
+constexpr int BM = 256;
+constexpr int BN = 256;
+constexpr int BK = 64;
+constexpr int NT = 256;
+constexpr int HALF_BYTES = 128 * BK * 2;     // 128 rows × 128 B
+constexpr int C_STRIDE = BN * 2 + 16;        // padded epilogue row (matches the generator)
+constexpr int LDS_BYTES = BM * C_STRIDE;     // 135168 ≥ 2 × 64 KiB K-tile buffers
+constexpr int GROUP_M = 8;
+
+typedef __attribute__((address_space(3))) char lds_char;
+
+}  // namespace
+
+__global__ void __launch_bounds__(NT, 1)
+amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                                uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
+                                int ldc, int superblock) {
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1;  // A half this wave reads
+  const int wc = wave & 1;   // B half
+
+  // ---- block → tile: the w4 kernel's XCD-aware super-block / GROUP_M order ----
+  const int tiles_m = M / BM;
+  const int tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  int m0, n0;
+  if (superblock) {
+    const int xcd = bid & 7, i = bid >> 3;
+    const int round = i >> 5, j = i & 31;
+    const int sb_n_count = tiles_n >> 4;
+    const int sbm = round / sb_n_count;
+    int sbn = round - sbm * sb_n_count;
+    if (sbm & 1) sbn = sb_n_count - 1 - sbn;
+    m0 = (sbm * 16 + (xcd >> 1) * 4 + (j & 3)) * BM;
+    n0 = (sbn * 16 + (xcd & 1) * 8 + (j >> 2)) * BN;
+  } else {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int group = wgid / (GROUP_M * tiles_n);
+    const int first_m = group * GROUP_M;
+    const int gsz = min(tiles_m - first_m, GROUP_M);
+    const int in_group = wgid - group * GROUP_M * tiles_n;
+    m0 = (first_m + in_group % gsz) * BM;
+    n0 = (in_group / gsz) * BN;
+  }
+
+  // ---- operands of the generated body (register map in tools/gen_gemm_w4a_kloop.py) ----
+  const uint32_t lda_b = (uint32_t)lda * 2, ldb_b = (uint32_t)ldb * 2;
+  const int drow = wave * 8 + (lane >> 3);
+  const int dchunk = (lane & 7) ^ ((drow >> 1) & 7);
+  const uint32_t a_voff = (uint32_t)drow * lda_b + dchunk * 16;
+  const uint32_t b_voff = (uint32_t)drow * ldb_b + dchunk * 16;
+  const int frow = lane & 15;
+  const int fq = lane >> 4;
+  const uint32_t fo0 = frow * 128 + (((0 + fq) ^ (frow >> 1)) << 4);
+  const uint32_t fo1 = frow * 128 + (((4 + fq) ^ (frow >> 1)) << 4);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)lds;
+  const uint32_t ra0 = lds0 + wr * HALF_BYTES + fo0;
+  const uint32_t ra1 = lds0 + wr * HALF_BYTES + fo1;
+  const uint32_t rb0 = lds0 + (2 + wc) * HALF_BYTES + fo0;
+  const uint32_t rb1 = lds0 + (2 + wc) * HALF_BYTES + fo1;
+  const uint32_t cbase = lds0 + (wr * 128 + frow) * C_STRIDE + (wc * 128 + fq * 4) * 2;
+  const uint32_t dma_lds = lds0 + wave * 1024;
+  const uint64_t a_addr = (uint64_t)(uintptr_t)A + (uint64_t)m0 * lda_b;
+  const uint64_t b_addr = (uint64_t)(uintptr_t)B + (uint64_t)n0 * ldb_b;
+  const uint32_t a_lo = (uint32_t)a_addr, a_hi = (uint32_t)(a_addr >> 32);
+  const uint32_t b_lo = (uint32_t)b_addr, b_hi = (uint32_t)(b_addr >> 32);
+  const uint32_t nrec_a = 256u * lda_b, nrec_b = 256u * ldb_b;
+  const int T = K / BK;
+
+  asm volatile(AMDK8S_W4A_ASM
+               :
+               : "s"(T), "s"(a_lo), "s"(a_hi), "s"(nrec_a), "s"(b_lo), "s"(b_hi), "s"(nrec_b),
+                 "s"(lda_b), "s"(ldb_b), "s"(dma_lds), "v"(ra0), "v"(ra1), "v"(rb0), "v"(rb1),
+                 "v"(a_voff), "v"(b_voff), "v"(cbase)
+               : AMDK8S_W4A_CLOBBERS);
+  __syncthreads();  // every wave's quarter of the bf16 C image is in LDS
+
+  // ---- 16-B coalesced stores of the 256×256 bf16 tile ----
+  char* cbase_g = reinterpret_cast<char*>(C) + ((size_t)m0 * ldc + n0) * 2;
+  const size_t ldc_b = (size_t)ldc * 2;
+#pragma unroll 4
+  for (int it = 0; it < BM * BN * 2 / (NT * 16); ++it) {
+    const int row = it * 8 + (tid >> 5);
+    const int ch = tid & 31;
+    const uint4 v = *reinterpret_cast<const uint4*>(lds + row * C_STRIDE + ch * 16);
+    *reinterpret_cast<uint4*>(cbase_g + row * ldc_b + ch * 16) = v;
+  }
+}
+
+extern "C" int amdk8s_gemm_bf16_nt_w4a(const void* A, const void* B, void* C, int M, int N, int K,
+                                       int lda, int ldb, int ldc, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
+  if (M % BM || N % BN || K % BK) return (int)hipErrorInvalidValue;
+  if (lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return (int)hipErrorInvalidValue;
+  // each 256-row panel is addressed with 32-bit buffer offsets
+  if (256ull * (unsigned long long)(lda > ldb ? lda : ldb) * 2 >= (1ull << 31))
+    return (int)hipErrorInvalidValue;
+  const int nwg = (M / BM) * (N / BN);
+  const char* sbenv = getenv("AMDK8S_W4_SUPERBLOCK");
+  const int sb = (M / BM) % 16 == 0 && (N / BN) % 16 == 0 && !(sbenv && sbenv[0] == '0');
+  hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4a, dim3(nwg), dim3(NT), 0, stream,
+                     (const uint16_t*)A, (const uint16_t*)B, (uint16_t*)C, M, N, K, lda, ldb, ldc,
+                     sb);
+  return (int)hipGetLastError();
+}

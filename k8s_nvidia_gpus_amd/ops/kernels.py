@@ -57,6 +57,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.amdk8s_gemm_bf16_nt.restype = ci
     lib.amdk8s_gemm_bf16_nt_w4.argtypes = [vp, vp, vp, ci, ci, ci, ci, ci, ci, vp]
     lib.amdk8s_gemm_bf16_nt_w4.restype = ci
+    lib.amdk8s_gemm_bf16_nt_w4a.argtypes = [vp, vp, vp, ci, ci, ci, ci, ci, ci, vp]
+    lib.amdk8s_gemm_bf16_nt_w4a.restype = ci
     lib.amdk8s_gemm_fp8_nt.argtypes = [vp, vp, vp, ci, ci, ci, ci, ci, ci, vp]
     lib.amdk8s_gemm_fp8_nt.restype = ci
     lib.amdk8s_gemm_bf16_nt_sample_check.argtypes = [vp, vp, vp, vp, ci, ci, ci, ci, vp]
@@ -118,14 +120,19 @@ def gemm_shape_supported(m: int, n: int, k: int) -> bool:
         and k % GEMM_TILE_K == 0
 
 
-GEMM_VARIANTS = ("auto", "w8", "w4")
+GEMM_VARIANTS = ("auto", "w8", "w4", "w4a")
 DEFAULT_GEMM_VARIANT = os.environ.get("AMDK8S_GEMM_VARIANT", "auto")
-# w4 (one wave per SIMD) with its REGION schedule for operands that stream from MALL/HBM beats the
-# 8-wave w8 kernel on every measured shape, including the single-super-block 4096²×16384 that was
-# w8's case under the former SPLIT schedule (1469-1492 vs ≈1416 TFLOPS): docs/gemm_tuning.md,
-# profiles/r01_session3/.  w8 stays selectable for A/B runs.
-def pick_gemm_variant(m: int, n: int, k: int) -> str:
-    return "w4"
+# w4a — the one-wave-per-SIMD w4 kernel with its K-loop as generated assembly — is bit-identical to
+# w4 and 3-4 % faster on every measured shape, 98-100 % of hipBLASLt (docs/gemm_tuning.md,
+# profiles/r01_session4/).  It addresses a 256-row panel with 32-bit buffer offsets; beyond that
+# (K ≳ 4M) w4's INTERLEAVED schedule takes over.  w8 and w4 stay selectable for A/B runs.
+W4A_MAX_PANEL_BYTES = 1 << 31
+
+
+def pick_gemm_variant(m: int, n: int, k: int, lda: Optional[int] = None,
+                      ldb: Optional[int] = None) -> str:
+    ld = max(lda or k, ldb or k)
+    return "w4a" if 256 * ld * 2 < W4A_MAX_PANEL_BYTES else "w4"
 
 
 def gemm_bf16_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
@@ -134,6 +141,7 @@ def gemm_bf16_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] =
 
     ``variant``: ``"w8"`` — 512 threads, 8 waves of 128×64 (gemm_bf16_gfx950.hip);
     ``"w4"`` — 256 threads, one wave per SIMD owning 128×128 (gemm_bf16_gfx950_w4.hip);
+    ``"w4a"`` — w4 with its K-loop as generated assembly (gemm_bf16_gfx950_w4a.hip, bit-identical);
     ``"auto"`` (default) — :func:`pick_gemm_variant` by operand footprint.
 
     ``a``: [M, K] bf16, ``b``: [N, K] bf16 (nn.Linear weight layout), both row-major with unit
@@ -161,8 +169,9 @@ def gemm_bf16_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] =
     if variant not in GEMM_VARIANTS:
         raise ValueError(f"unknown GEMM variant {variant!r} (have {GEMM_VARIANTS})")
     if variant == "auto":
-        variant = pick_gemm_variant(m, n, k)
-    fn = {"w8": lib.amdk8s_gemm_bf16_nt, "w4": lib.amdk8s_gemm_bf16_nt_w4}[variant]
+        variant = pick_gemm_variant(m, n, k, a.stride(0), b.stride(0))
+    fn = {"w8": lib.amdk8s_gemm_bf16_nt, "w4": lib.amdk8s_gemm_bf16_nt_w4,
+          "w4a": lib.amdk8s_gemm_bf16_nt_w4a}[variant]
     rc = fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
             a.stride(0), b.stride(0), out.stride(0), _stream_handle(a.device))
     _check(rc, f"amdk8s_gemm_bf16_nt[{variant}]")

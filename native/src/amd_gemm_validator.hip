@@ -24,14 +24,17 @@
 
 namespace {
 
-// Kernel variant: "w8" (8 waves, 2/SIMD), "w4" (4 waves, 1/SIMD, 128x128 per wave) or "auto"
-// (= w4, which picks its own K-loop schedule by operand footprint; docs/gemm_tuning.md).
+// Kernel variant: "w8" (8 waves, 2/SIMD), "w4" (4 waves, 1/SIMD, 128x128 per wave, hipcc-scheduled
+// K-loop), "w4a" (the same kernel with its K-loop as generated assembly) or "auto" (= w4a, falling
+// back to w4 for panels past 32-bit offsets; docs/gemm_tuning.md).
 int gemm(const std::string& variant, const void* A, const void* B, void* C, int m, int n, int k,
          hipStream_t s) {
   if (variant == "fp8") return amdk8s_gemm_fp8_nt(A, B, C, m, n, k, k, k, n, s);
-  const bool w4 = variant != "w8";
-  return w4 ? amdk8s_gemm_bf16_nt_w4(A, B, C, m, n, k, k, k, n, s)
-            : amdk8s_gemm_bf16_nt(A, B, C, m, n, k, k, k, n, s);
+  if (variant == "w8") return amdk8s_gemm_bf16_nt(A, B, C, m, n, k, k, k, n, s);
+  if (variant == "w4") return amdk8s_gemm_bf16_nt_w4(A, B, C, m, n, k, k, k, n, s);
+  const int rc = amdk8s_gemm_bf16_nt_w4a(A, B, C, m, n, k, k, k, n, s);
+  if (rc != (int)hipErrorInvalidValue || variant == "w4a") return rc;
+  return amdk8s_gemm_bf16_nt_w4(A, B, C, m, n, k, k, k, n, s);
 }
 
 struct Options {
@@ -182,7 +185,7 @@ int main(int argc, char** argv) {
     else if (a == "--dtype") o.dtype = next();
     else {
       std::printf("usage: amd-gemm-validator [--size S | --m M --n N --k K] [--iters I] "
-                  "[--warmup W] [--device D] [--samples S] [--variant auto|w8|w4] [--dtype bf16|fp8] "
+                  "[--warmup W] [--device D] [--samples S] [--variant auto|w8|w4|w4a] [--dtype bf16|fp8] "
                   "[--json]\n");
       return a == "-h" || a == "--help" ? 0 : 2;
     }

@@ -41,7 +41,7 @@ def test_vector_add_bandwidth_form(K, dev):
     torch.testing.assert_close(c, a + b, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("variant", ["w8", "w4", "auto"])
+@pytest.mark.parametrize("variant", ["w8", "w4", "w4a", "auto"])
 @pytest.mark.parametrize("m,n,k", [
     (256, 256, 64),      # one K-tile: prologue-only path
     (256, 256, 128),     # two K-tiles: tail-only path
@@ -61,7 +61,7 @@ def test_gemm_bf16_nt_matches_fp32(K, dev, m, n, k, variant):
     torch.testing.assert_close(c.float(), ref, rtol=1e-2, atol=1e-2 * (k ** 0.5) / 8)
 
 
-@pytest.mark.parametrize("variant", ["w8", "w4", "auto"])
+@pytest.mark.parametrize("variant", ["w8", "w4", "w4a", "auto"])
 def test_gemm_identity_asymmetric(K, dev, variant):
     """A = I with an asymmetric B must return exactly Bᵀ: catches any row/col swap in C."""
     s = 256
@@ -74,7 +74,7 @@ def test_gemm_identity_asymmetric(K, dev, variant):
     assert torch.equal(c2, b)
 
 
-@pytest.mark.parametrize("variant", ["w8", "w4", "auto"])
+@pytest.mark.parametrize("variant", ["w8", "w4", "w4a", "auto"])
 def test_gemm_strided_leading_dims(K, dev, variant):
     g = torch.Generator(device=dev).manual_seed(3)
     big_a = _rand_bf16((512, 640), g, dev)
@@ -87,7 +87,7 @@ def test_gemm_strided_leading_dims(K, dev, variant):
     torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=3e-2)
 
 
-@pytest.mark.parametrize("variant", ["w8", "w4", "auto"])
+@pytest.mark.parametrize("variant", ["w8", "w4", "w4a", "auto"])
 def test_gemm_deterministic(K, dev, variant):
     g = torch.Generator(device=dev).manual_seed(11)
     a = _rand_bf16((1024, 2048), g, dev)
@@ -98,11 +98,36 @@ def test_gemm_deterministic(K, dev, variant):
 
 
 def test_gemm_variants_agree_bitwise_at_8192(K, dev):
-    """Both schedules accumulate each output in the same K order → identical bits."""
+    """All variants accumulate each output in the same K order → identical bits."""
     g = torch.Generator(device=dev).manual_seed(21)
     a = _rand_bf16((2048, 8192), g, dev)
     b = _rand_bf16((2048, 8192), g, dev)
-    assert torch.equal(K.gemm_bf16_nt(a, b, variant="w8"), K.gemm_bf16_nt(a, b, variant="w4"))
+    c8 = K.gemm_bf16_nt(a, b, variant="w8")
+    assert torch.equal(c8, K.gemm_bf16_nt(a, b, variant="w4"))
+    assert torch.equal(c8, K.gemm_bf16_nt(a, b, variant="w4a"))
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (256, 256, 128), (512, 256, 192),
+                                   (768, 512, 1024), (4096, 4096, 640), (8192, 4096, 192)])
+def test_gemm_w4a_matches_fp32_and_w4(K, dev, m, n, k):
+    """The generated-assembly K-loop against an fp32 reference and bit-for-bit against hipcc's w4
+    (T = 1: clamped restage into the read buffer; T = 2/3: odd tail of the parity-unrolled loop;
+    4096² and 8192×4096: super-block order), written over a NaN-filled output."""
+    g = torch.Generator(device=dev).manual_seed(43 + m + k)
+    a = _rand_bf16((m, k), g, dev)
+    b = _rand_bf16((n, k), g, dev)
+    c = torch.full((m, n), float("nan"), dtype=torch.bfloat16, device=dev)
+    K.gemm_bf16_nt(a, b, out=c, variant="w4a")
+    assert not torch.isnan(c.float()).any()
+    assert torch.equal(c, K.gemm_bf16_nt(a, b, variant="w4"))
+    rows, cols = min(m, 512), min(n, 256)
+    ref = a[:rows].float() @ b[:cols].float().t()
+    torch.testing.assert_close(c[:rows, :cols].float(), ref, rtol=1e-2, atol=1e-2 * (k ** 0.5) / 8)
+
+
+def test_gemm_auto_picks_generated_assembly_kernel(K):
+    assert K.pick_gemm_variant(8192, 8192, 8192) == "w4a"
+    assert K.pick_gemm_variant(256, 256, 1 << 22) == "w4"   # panel past 32-bit buffer offsets
 
 
 def test_gemm_padded_general_shapes(K, dev):

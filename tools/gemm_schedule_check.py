@@ -6,7 +6,8 @@ counts and multi-round grids, and checks (a) no NaN from the NaN-filled output, 
 against an fp32 torch reference, (c) bit-equality with the default REGION schedule (same per-lane
 MFMA order, so any difference is a schedule bug).
 
-usage: python tools/gemm_schedule_check.py interleaved   (any AMDK8S_W4_SCHEDULE value)
+usage: python tools/gemm_schedule_check.py interleaved   (any AMDK8S_W4_SCHEDULE value, or a
+       GEMM variant name such as w4a)
 """
 import os
 import sys
@@ -30,9 +31,12 @@ def main() -> int:
         b = torch.empty((n, k), dtype=torch.bfloat16, device=dev)
         K.fill_uniform_bf16(a, 1)
         K.fill_uniform_bf16(b, 2)
-        os.environ["AMDK8S_W4_SCHEDULE"] = sched
         c = torch.full((m, n), float("nan"), dtype=torch.bfloat16, device=dev)
-        K.gemm_bf16_nt(a, b, out=c, variant="w4")
+        if sched in K.GEMM_VARIANTS:  # a whole variant, e.g. w4a
+            K.gemm_bf16_nt(a, b, out=c, variant=sched)
+        else:
+            os.environ["AMDK8S_W4_SCHEDULE"] = sched
+            K.gemm_bf16_nt(a, b, out=c, variant="w4")
         os.environ["AMDK8S_W4_SCHEDULE"] = "region"
         c2 = K.gemm_bf16_nt(a, b, variant="w4")
         ref = a.float() @ b.float().t()
