@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "gemm_bf16_gfx950_w4a_kloop.inc"
 
@@ -37,6 +38,7 @@ typedef __attribute__((address_space(3))) char lds_char;
 
 }  // namespace
 
+template <int SCHED>
 __global__ void __launch_bounds__(NT, 1)
 amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                 uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
@@ -62,8 +64,13 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
     const int sbm = round / sb_n_count;
     int sbn = round - sbm * sb_n_count;
     if (sbm & 1) sbn = sb_n_count - 1 - sbn;
-    m0 = (sbm * 16 + (xcd >> 1) * 4 + (j & 3)) * BM;
-    n0 = (sbn * 16 + (xcd & 1) * 8 + (j >> 2)) * BN;
+    if (superblock == 2) {  // XCD corner 8(M)×4(N) (A/B knob)
+      m0 = (sbm * 16 + (xcd & 1) * 8 + (j & 7)) * BM;
+      n0 = (sbn * 16 + (xcd >> 1) * 4 + (j >> 3)) * BN;
+    } else {                // XCD corner 4(M)×8(N)
+      m0 = (sbm * 16 + (xcd >> 1) * 4 + (j & 3)) * BM;
+      n0 = (sbn * 16 + (xcd & 1) * 8 + (j >> 2)) * BN;
+    }
   } else {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
@@ -99,12 +106,16 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
   const uint32_t nrec_a = 256u * lda_b, nrec_b = 256u * ldb_b;
   const int T = K / BK;
 
-  asm volatile(AMDK8S_W4A_ASM
-               :
-               : "s"(T), "s"(a_lo), "s"(a_hi), "s"(nrec_a), "s"(b_lo), "s"(b_hi), "s"(nrec_b),
-                 "s"(lda_b), "s"(ldb_b), "s"(dma_lds), "v"(ra0), "v"(ra1), "v"(rb0), "v"(rb1),
-                 "v"(a_voff), "v"(b_voff), "v"(cbase)
-               : AMDK8S_W4A_CLOBBERS);
+#define AMDK8S_W4A_OPERANDS                                                                \
+  : "s"(T), "s"(a_lo), "s"(a_hi), "s"(nrec_a), "s"(b_lo), "s"(b_hi), "s"(nrec_b), "s"(lda_b),  \
+    "s"(ldb_b), "s"(dma_lds), "v"(ra0), "v"(ra1), "v"(rb0), "v"(rb1), "v"(a_voff), "v"(b_voff), \
+    "v"(cbase)                                                                                 \
+  : AMDK8S_W4A_CLOBBERS
+  static_assert(AMDK8S_W4A_NUM_SCHEDULES == 3, "one branch per generated schedule");
+  if constexpr (SCHED == 0) asm volatile(AMDK8S_W4A_ASM_0 : AMDK8S_W4A_OPERANDS);
+  else if constexpr (SCHED == 1) asm volatile(AMDK8S_W4A_ASM_1 : AMDK8S_W4A_OPERANDS);
+  else asm volatile(AMDK8S_W4A_ASM_2 : AMDK8S_W4A_OPERANDS);
+#undef AMDK8S_W4A_OPERANDS
   __syncthreads();  // every wave's quarter of the bf16 C image is in LDS
 
   // ---- 16-B coalesced stores of the 256×256 bf16 tile ----
@@ -130,9 +141,26 @@ extern "C" int amdk8s_gemm_bf16_nt_w4a(const void* A, const void* B, void* C, in
     return (int)hipErrorInvalidValue;
   const int nwg = (M / BM) * (N / BN);
   const char* sbenv = getenv("AMDK8S_W4_SUPERBLOCK");
-  const int sb = (M / BM) % 16 == 0 && (N / BN) % 16 == 0 && !(sbenv && sbenv[0] == '0');
-  hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4a, dim3(nwg), dim3(NT), 0, stream,
-                     (const uint16_t*)A, (const uint16_t*)B, (uint16_t*)C, M, N, K, lda, ldb, ldc,
-                     sb);
+  int sb = (M / BM) % 16 == 0 && (N / BN) % 16 == 0 && !(sbenv && sbenv[0] == '0');
+  if (sb && sbenv && sbenv[0] == '2') sb = 2;
+  // K-loop schedule: the generator's default, or AMDK8S_W4A_SCHEDULE=<name> for A/B runs
+  int sched = AMDK8S_W4A_DEFAULT_SCHEDULE;
+  if (const char* e = getenv("AMDK8S_W4A_SCHEDULE")) {
+    static const char* const names[] = AMDK8S_W4A_SCHEDULE_NAMES;
+    for (int i = 0; i < AMDK8S_W4A_NUM_SCHEDULES; ++i)
+      if (!strcmp(e, names[i])) sched = i;
+  }
+  const uint16_t* a = (const uint16_t*)A;
+  const uint16_t* b = (const uint16_t*)B;
+  uint16_t* c = (uint16_t*)C;
+  if (sched == 1)
+    hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4a<1>, dim3(nwg), dim3(NT), 0, stream, a, b, c,
+                       M, N, K, lda, ldb, ldc, sb);
+  else if (sched == 2)
+    hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4a<2>, dim3(nwg), dim3(NT), 0, stream, a, b, c,
+                       M, N, K, lda, ldb, ldc, sb);
+  else
+    hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4a<0>, dim3(nwg), dim3(NT), 0, stream, a, b, c,
+                       M, N, K, lda, ldb, ldc, sb);
   return (int)hipGetLastError();
 }

@@ -7,7 +7,7 @@ against an fp32 torch reference, (c) bit-equality with the default REGION schedu
 MFMA order, so any difference is a schedule bug).
 
 usage: python tools/gemm_schedule_check.py interleaved   (any AMDK8S_W4_SCHEDULE value, or a
-       GEMM variant name such as w4a)
+       GEMM variant name such as w4a, or w4a:<schedule>)
 """
 import os
 import sys
@@ -32,8 +32,12 @@ def main() -> int:
         K.fill_uniform_bf16(a, 1)
         K.fill_uniform_bf16(b, 2)
         c = torch.full((m, n), float("nan"), dtype=torch.bfloat16, device=dev)
-        if sched in K.GEMM_VARIANTS:  # a whole variant, e.g. w4a
-            K.gemm_bf16_nt(a, b, out=c, variant=sched)
+        if sched.split(":")[0] in K.GEMM_VARIANTS:  # a variant, optionally variant:schedule
+            variant, _, w4a_sched = sched.partition(":")
+            if w4a_sched:
+                os.environ["AMDK8S_W4A_SCHEDULE"] = w4a_sched
+            K.gemm_bf16_nt(a, b, out=c, variant=variant)
+            os.environ.pop("AMDK8S_W4A_SCHEDULE", None)
         else:
             os.environ["AMDK8S_W4_SCHEDULE"] = sched
             K.gemm_bf16_nt(a, b, out=c, variant="w4")

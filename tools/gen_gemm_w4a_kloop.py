@@ -1,14 +1,24 @@
 #!/usr/bin/env python3
-"""Generate the hand-scheduled gfx950 assembly body of the w4a bf16 GEMM kernel.
+"""Generate the hand-scheduled gfx950 assembly bodies of the w4a bf16 GEMM kernel.
 
 Writes ``k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950_w4a_kloop.inc``: one ``asm volatile`` body
-(prologue DMA, the K-loop unrolled by two LDS-buffer parities, the accumulator → bf16 → LDS
-C-image epilogue) with every register explicit, so no compiler-inserted instruction sits between
-the MFMAs. Op placement is the REGION schedule of ``gemm_bf16_gfx950_w4.hip`` (one op per MFMA
-gap, three barriers per K-tile); the counted ``s_waitcnt lgkmcnt`` before each MFMA is computed
-here by simulating the in-order LDS return queue, instead of hipcc's conservative counting.
+per K-loop schedule (prologue DMA, the K-loop unrolled by the two LDS-buffer parities, the
+accumulator → bf16 → LDS C-image epilogue), every register explicit, so no compiler-inserted
+instruction sits between the MFMAs. The kernel (``gemm_bf16_gfx950_w4a.hip``) instantiates one
+template per schedule; ``AMDK8S_W4A_SCHEDULE=<name>`` picks one for A/B runs.
 
-Register map (kernel side passes operands; the asm copies them into these):
+A schedule is a list of (MFMA slot, op) pairs for one K-tile of 128 MFMAs (an op in slot k issues
+right after MFMA k). The generator places each DMA's M0 write one slot earlier (so an MFMA covers
+the M0 → LDS-DMA hazard), spreads the 7 SALU ops that advance the clamped DMA source over slots
+1..13, computes the exact ``s_waitcnt lgkmcnt`` before every MFMA by simulating the in-order LDS
+return queue, sets the vmcnt of barrier #3 from the number of DMA pieces issued before it, and
+asserts the buffer discipline of the REGION design:
+  * barrier #1 (lgkmcnt(0) + s_barrier) follows every K-half-1 B read of the current buffer and
+    precedes every B DMA piece into it; barrier #2 does the same for A;
+  * barrier #3 (vmcnt + s_barrier: K-tile t+1 landed everywhere) precedes every read of the next
+    buffer; K-half-1 reads sit in K-half 0, next-tile reads in K-half 1 (register reuse).
+
+Register map (the kernel passes operands; the asm copies them into these):
   v[0:31]  a0 fragments (a0[i] = v[4i:4i+3])      v[32:63] b0      v[64:95] a1      v[96:127] b1
   v128..v131  LDS read bases, buffer 0: A K-half 0, A K-half 1, B K-half 0, B K-half 1
   v132..v135  same for buffer 1 (+64 KiB)         v136/v137 DMA lane offsets A/B   v138 C-image base
@@ -28,6 +38,8 @@ OUT = os.path.join(os.path.dirname(__file__), "..", "k8s_nvidia_gpus_amd", "ops"
 HALF = 16384          # bytes of one 128-row operand half in a K-tile buffer
 TILE = 4 * HALF       # A0 A1 B0 B1
 C_STRIDE = 528        # padded C-image row (bytes)
+FIRST_USE = [("b", 0), ("b", 1), ("b", 2), ("b", 3), ("a", 0), ("b", 4), ("b", 5), ("b", 6),
+             ("b", 7), ("a", 1), ("a", 2), ("a", 3), ("a", 4), ("a", 5), ("a", 6), ("a", 7)]
 
 
 def frag(kind: str, idx: int) -> str:
@@ -35,137 +47,155 @@ def frag(kind: str, idx: int) -> str:
     return f"v[{base}:{base + 3}]"
 
 
-def read_order(x: int):
-    """x-th fragment read of a K-half in first-use order: b[0..3], a[0], b[4..7], a[1..7]."""
-    if x < 4:
-        return "b", x
-    if x == 4:
-        return "a", 0
-    if x < 9:
-        return "b", x - 1
-    return "a", x - 8
-
-
 def piece(p: int):
-    """DMA piece p: (operand, row-register, LDS byte offset inside a K-tile buffer)."""
+    """DMA piece p: (operand, row-offset SGPR, LDS byte offset inside a K-tile buffer)."""
     j, h = p >> 2, (p >> 1) & 1
-    e = p >> 1                                  # index among the 8 pieces of this operand
+    e = p >> 1
     if p % 2 == 0:
         return "A", f"s{80 + e}", j * 4096 + h * HALF
     return "B", f"s{88 + e}", j * 4096 + (2 + h) * HALF
 
 
-class Body:
-    """One K-tile (128 MFMA slots) with ops attached after MFMA k, plus the lgkm simulation."""
+# ------------------------------------------------------------------------------------------------
+# schedules: list of (slot, op); op = ("r1"|"r0", operand, index) | ("dma", piece) | ("bar", 1|2|3)
 
-    def __init__(self, parity: int):
-        self.P = parity
-        self.after = [[] for _ in range(128)]
-
-    # LDS read bases for this parity
-    def rd_base(self, which: str, operand: str, khalf: int) -> str:
-        buf = self.P if which == "cur" else 1 - self.P
-        return f"v{128 + 4 * buf + (0 if operand == 'a' else 2) + khalf}"
-
-    def read(self, which: str, khalf: int, x: int):
-        op, idx = read_order(x)
-        dst = frag(f"{op}{'1' if khalf else '0'}", idx)
-        base = self.rd_base(which, op, khalf)
-        return ("lds", f"{op}{'1' if khalf else '0'}{idx}",
-                f"ds_read_b128 {dst}, {base} offset:{idx * 2048}")
-
-    def dma(self, p: int):
-        opnd, row, off = piece(p)
-        rs = "s[64:67]" if opnd == "A" else "s[68:71]"
-        voff = "v136" if opnd == "A" else "v137"
-        m0 = ("salu", None, f"s_add_u32 m0, s74, {self.P * TILE + off}")
-        ld = ("vmem", None, f"buffer_load_dwordx4 {voff}, {rs}, {row} offen lds")
-        return m0, ld
-
-    def build(self):
-        A = self.after
-        # K-half 0 (a0, b0): K-half-1 reads of cur, B DMA pieces after barrier #1
-        for g in range(16):
-            for q in range(4):
-                k = 4 * g + q
-                if q == 0:
-                    if g < 4:
-                        A[k].append(self.read("cur", 1, 2 * g))
-                    if g == 4:
-                        A[k].append(self.read("cur", 1, 8))
-                    if 6 <= g < 13:
-                        A[k].append(self.read("cur", 1, g + 3))
-                if q == 2 and g < 4:
-                    A[k].append(self.read("cur", 1, 2 * g + 1))
-                if q == 1 and 6 <= g < 14:
-                    m0, ld = self.dma(2 * (g - 6) + 1)
-                    A[k - 1].append(m0)
-                    A[k].append(ld)
-                if q == 3 and g == 5:
-                    A[k].append(("wait0", None, "s_waitcnt lgkmcnt(0)"))
-                    A[k].append(("bar", None, "s_barrier"))
-        # K-half 1 (a1, b1): A DMA pieces after barrier #2, next K-tile's K-half-0 reads after #3
-        for g in range(16):
-            for q in range(4):
-                k = 64 + 4 * g + q
-                if q == 1 and 2 <= g < 10:
-                    m0, ld = self.dma(2 * (g - 2))
-                    A[k - 1].append(m0)
-                    A[k].append(ld)
-                if g >= 10:
-                    x0, x1 = (g - 10) * 16 // 6, (g - 9) * 16 // 6
-                    if q == 0:
-                        A[k].append(self.read("nxt", 0, x0))
-                    if q == 2 and x0 + 1 < x1:
-                        A[k].append(self.read("nxt", 0, x0 + 1))
-                    if q == 3 and x0 + 2 < x1:
-                        A[k].append(self.read("nxt", 0, x0 + 2))
-                if q == 3 and g == 1:
-                    A[k].append(("wait0", None, "s_waitcnt lgkmcnt(0)"))
-                    A[k].append(("bar", None, "s_barrier"))
-                if q == 3 and g == 9:
-                    A[k].append(("waitv", None, "s_waitcnt vmcnt(16)"))
-                    A[k].append(("bar", None, "s_barrier"))
-        # clamp-advance the DMA source one K-tile (before the first piece, one SALU per gap)
-        step = ["s_add_u32 s75, s73, 2", "s_cmp_lt_u32 s75, s72", "s_cselect_b32 s76, 0x80, 0",
-                "s_add_u32 s64, s64, s76", "s_addc_u32 s65, s65, 0",
-                "s_add_u32 s68, s68, s76", "s_addc_u32 s69, s69, 0"]
-        for i, ins in enumerate(step):
-            A[1 + 2 * i].append(("salu", None, ins))
-
-    def emit(self, lgkm_queue: list) -> list:
-        """Instructions of the body; lgkm_queue = outstanding LDS reads (oldest first), updated."""
-        out = []
-        for k in range(128):
-            khalf = k >= 64
-            I, J = (k % 64) >> 3, k & 7
-            fa, fb = (f"a1{I}", f"b1{J}") if khalf else (f"a0{I}", f"b0{J}")
-            need = [n for n, tag in enumerate(lgkm_queue) if tag in (fa, fb)]
-            if need:
-                keep = len(lgkm_queue) - need[-1] - 1
-                out.append(f"s_waitcnt lgkmcnt({min(keep, 15)})")
-                del lgkm_queue[: len(lgkm_queue) - min(keep, 15)]
-            n = 8 * I + J
-            src_a = frag("a1" if khalf else "a0", I)
-            src_b = frag("b1" if khalf else "b0", J)
-            out.append(f"v_mfma_f32_16x16x32_bf16 a[{4 * n}:{4 * n + 3}], {src_b}, {src_a}, "
-                       f"a[{4 * n}:{4 * n + 3}]")
-            for kind, tag, ins in self.after[k]:
-                if kind == "lds":
-                    lgkm_queue.append(tag)
-                elif kind == "wait0":
-                    lgkm_queue.clear()
-                out.append(ins)
-        return out
+def sched_region():
+    """REGION of the hipcc kernel: one op per MFMA gap; barriers after MFMAs 23, 71, 103."""
+    s = []
+    r1 = FIRST_USE
+    for g in range(4):
+        s += [(4 * g, ("r1",) + r1[2 * g]), (4 * g + 2, ("r1",) + r1[2 * g + 1])]
+    s.append((16, ("r1",) + r1[8]))
+    for g in range(6, 13):
+        s.append((4 * g, ("r1",) + r1[g + 3]))
+    s.append((23, ("bar", 1)))
+    s += [(4 * g + 1, ("dma", 2 * (g - 6) + 1)) for g in range(6, 14)]
+    s.append((71, ("bar", 2)))
+    s += [(64 + 4 * g + 1, ("dma", 2 * (g - 2))) for g in range(2, 10)]
+    s.append((103, ("bar", 3)))
+    for g in range(10, 16):
+        x0, x1 = (g - 10) * 16 // 6, (g - 9) * 16 // 6
+        for q, x in ((0, x0), (2, x0 + 1), (3, x0 + 2)):
+            if x < x1:
+                s.append((64 + 4 * g + q, ("r0",) + FIRST_USE[x]))
+    return s
 
 
-def prologue() -> list:
+def sched_early3():
+    """REGION with barrier #3 after MFMA 95: the A pieces are packed into groups 2-7 of K-half 1
+    and the 16 next-tile reads get 32 MFMAs (every other gap) instead of 24."""
+    s = [x for x in sched_region() if x[1][0] not in ("r0", "dma") and x[1] != ("bar", 3)]
+    s += [(4 * g + 1, ("dma", 2 * (g - 6) + 1)) for g in range(6, 14)]
+    a_slots = [73, 75, 77, 79, 81, 85, 89, 93]
+    s += [(slot, ("dma", 2 * e)) for e, slot in enumerate(a_slots)]
+    s.append((95, ("bar", 3)))
+    s += [(96 + 2 * x, ("r0",) + FIRST_USE[x]) for x in range(16)]
+    return s
+
+
+def sched_mirror():
+    """hipBLASLt's MT256x256x64_MI16x16x1 placement (docs/gemm_tuning.md, session 4): b1 reads in
+    slots 0-14, barrier #1 after 21, B pieces + a1 reads interleaved, barrier #2 after 51, A pieces,
+    barrier #3 after 92 with 3 A pieces still to come, next-tile reads 93-123."""
+    s = [(2 * j, ("r1", "b", j)) for j in range(8)]
+    s.append((21, ("bar", 1)))
+    s += [(slot, ("dma", 2 * e + 1)) for e, slot in enumerate([22, 25, 28, 31, 34, 52, 55, 58])]
+    s += [(slot, ("r1", "a", i)) for i, slot in enumerate([24, 27, 30, 33, 36, 38, 40, 42])]
+    s.append((51, ("bar", 2)))
+    s += [(slot, ("dma", 2 * e)) for e, slot in enumerate([61, 64, 85, 87, 89, 96, 100, 124])]
+    s.append((92, ("bar", 3)))
+    r0 = [93, 94, 95, 97, 98, 102, 103, 104, 105, 106, 109, 112, 114, 117, 120, 123]
+    s += [(slot, ("r0",) + FIRST_USE[x]) for x, slot in enumerate(r0)]
+    return s
+
+
+SCHEDULES = {"region": sched_region, "early3": sched_early3, "mirror": sched_mirror}
+DEFAULT = "region"
+
+
+# ------------------------------------------------------------------------------------------------
+
+def check(name: str, sched) -> None:
+    slots = {}
+    for slot, op in sched:
+        slots.setdefault(op, []).append(slot)
+        assert 0 <= slot < 128, (name, slot, op)
+    bar = {k: slots[("bar", k)][0] for k in (1, 2, 3)}
+    r1 = [(slot, op) for slot, op in sched if op[0] == "r1"]
+    r0 = [(slot, op) for slot, op in sched if op[0] == "r0"]
+    dma = [(slot, op[1]) for slot, op in sched if op[0] == "dma"]
+    assert sorted(op[1:] for _, op in r1) == sorted(FIRST_USE), name
+    assert sorted(op[1:] for _, op in r0) == sorted(FIRST_USE), name
+    assert sorted(p for _, p in dma) == list(range(16)), name
+    for slot, op in r1:
+        assert slot < 64 and slot < bar[1 if op[1] == "b" else 2], (name, slot, op)
+    for slot, p in dma:
+        assert slot >= 1 and slot > bar[1 if p % 2 else 2], (name, slot, p)
+    for slot, op in r0:
+        assert slot >= 64 and slot > bar[3], (name, slot, op)
+
+
+def body(name: str, sched, parity: int, queue: list) -> list:
+    """One K-tile of `sched` reading buffer `parity`; `queue` = outstanding LDS reads, updated."""
+    after = [[] for _ in range(128)]
+
+    def rd(which: str, khalf: int, opnd: str, idx: int):
+        buf = parity if which == "cur" else 1 - parity
+        base = f"v{128 + 4 * buf + (0 if opnd == 'a' else 2) + khalf}"
+        tag = f"{opnd}{khalf}{idx}"
+        return ("lds", tag, f"ds_read_b128 {frag(f'{opnd}{khalf}', idx)}, {base} offset:{idx * 2048}")
+
+    n_dma_before_bar3 = sum(1 for slot, op in sched if op[0] == "dma"
+                            and slot < dict((o, s) for s, o in sched)[("bar", 3)])
+    for slot, op in sorted(sched, key=lambda x: x[0]):
+        if op[0] == "r1":
+            after[slot].append(rd("cur", 1, op[1], op[2]))
+        elif op[0] == "r0":
+            after[slot].append(rd("nxt", 0, op[1], op[2]))
+        elif op[0] == "dma":
+            opnd, row, off = piece(op[1])
+            rs, voff = ("s[64:67]", "v136") if opnd == "A" else ("s[68:71]", "v137")
+            after[slot - 1].append(("salu", None, f"s_add_u32 m0, s74, {parity * TILE + off}"))
+            after[slot].append(("vmem", None, f"buffer_load_dwordx4 {voff}, {rs}, {row} offen lds"))
+        elif op == ("bar", 3):
+            after[slot] += [("waitv", None, f"s_waitcnt vmcnt({n_dma_before_bar3})"),
+                            ("bar", None, "s_barrier")]
+        else:
+            after[slot] += [("wait0", None, "s_waitcnt lgkmcnt(0)"), ("bar", None, "s_barrier")]
+    step = ["s_add_u32 s75, s73, 2", "s_cmp_lt_u32 s75, s72", "s_cselect_b32 s76, 0x80, 0",
+            "s_add_u32 s64, s64, s76", "s_addc_u32 s65, s65, 0",
+            "s_add_u32 s68, s68, s76", "s_addc_u32 s69, s69, 0"]
+    first_dma = min(slot for slot, op in sched if op[0] == "dma")
+    assert 1 + 2 * (len(step) - 1) < first_dma - 1, name
+    for i, ins in enumerate(step):
+        after[1 + 2 * i].append(("salu", None, ins))
+
     out = []
-    # operands → fixed registers (%0.. order must match the kernel's operand list)
-    out += ["s_mov_b32 s72, %0", "s_mov_b32 s64, %1", "s_and_b32 s65, %2, 0xffff",
-            "s_mov_b32 s66, %3", "s_mov_b32 s67, 0x20000", "s_mov_b32 s68, %4",
-            "s_and_b32 s69, %5, 0xffff", "s_mov_b32 s70, %6", "s_mov_b32 s71, 0x20000",
-            "s_mov_b32 s74, %9"]
+    for k in range(128):
+        khalf = 1 if k >= 64 else 0
+        I, J = (k % 64) >> 3, k & 7
+        need = [i for i, tag in enumerate(queue) if tag in (f"a{khalf}{I}", f"b{khalf}{J}")]
+        if need:
+            keep = min(len(queue) - need[-1] - 1, 15)
+            out.append(f"s_waitcnt lgkmcnt({keep})")
+            del queue[: len(queue) - keep]
+        n = 8 * I + J
+        out.append(f"v_mfma_f32_16x16x32_bf16 a[{4 * n}:{4 * n + 3}], {frag(f'b{khalf}', J)}, "
+                   f"{frag(f'a{khalf}', I)}, a[{4 * n}:{4 * n + 3}]")
+        for kind, tag, ins in after[k]:
+            if kind == "lds":
+                queue.append(tag)
+            elif kind == "wait0":
+                queue.clear()
+            out.append(ins)
+    return out
+
+
+def prologue(r0_order) -> list:
+    out = ["s_mov_b32 s72, %0", "s_mov_b32 s64, %1", "s_and_b32 s65, %2, 0xffff",
+           "s_mov_b32 s66, %3", "s_mov_b32 s67, 0x20000", "s_mov_b32 s68, %4",
+           "s_and_b32 s69, %5, 0xffff", "s_mov_b32 s70, %6", "s_mov_b32 s71, 0x20000",
+           "s_mov_b32 s74, %9"]
     for e in range(8):
         rows = (e >> 1) * 32 + (e & 1) * 128
         out.append(f"s_mul_i32 s{80 + e}, %7, {rows}")
@@ -175,8 +205,7 @@ def prologue() -> list:
         out.append(f"v_add_u32 v{132 + i}, {TILE}, %{10 + i}")
     out += ["v_mov_b32 v136, %14", "v_mov_b32 v137, %15", "v_mov_b32 v138, %16"]
     out += [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
-    # K-tiles 0 and min(1, T-1) in flight (buffers 0 and 1)
-    for buf in range(2):
+    for buf in range(2):                # K-tiles 0 and min(1, T-1) in flight (buffers 0 and 1)
         if buf == 1:
             out += ["s_cmp_gt_u32 s72, 1", "s_cselect_b32 s76, 0x80, 0",
                     "s_add_u32 s64, s64, s76", "s_addc_u32 s65, s65, 0",
@@ -187,9 +216,9 @@ def prologue() -> list:
             out += [f"s_add_u32 m0, s74, {buf * TILE + off}", "s_nop 0",
                     f"buffer_load_dwordx4 {voff}, {rs}, {row} offen lds"]
     out += ["s_waitcnt vmcnt(16)", "s_barrier"]
-    b = Body(1)   # reads "nxt" of parity 1 = buffer 0
-    for x in range(16):
-        out.append(b.read("nxt", 0, x)[2])
+    for opnd, idx in r0_order:          # the loop's own next-tile read order (same LDS queue)
+        base = f"v{128 + (0 if opnd == 'a' else 2)}"
+        out.append(f"ds_read_b128 {frag(f'{opnd}0', idx)}, {base} offset:{idx * 2048}")
     out.append("s_mov_b32 s73, 0")
     return out
 
@@ -214,16 +243,18 @@ def epilogue() -> list:
     return out
 
 
-def main():
-    lines = prologue()
-    queue = [f"{read_order(x)[0]}0{read_order(x)[1]}" for x in range(16)]
+def kernel_asm(name: str) -> list:
+    sched = SCHEDULES[name]()
+    check(name, sched)
+    r0_order = [op[1:] for _, op in sorted((x for x in sched if x[1][0] == "r0"),
+                                           key=lambda x: x[0])]
+    queue0 = [f"{o}0{i}" for o, i in r0_order]
+    lines = prologue(r0_order)
     bodies = []
-    for P in (0, 1):
-        b = Body(P)
-        b.build()
-        q = list(queue)
-        bodies.append(b.emit(q))
-        assert q == queue, "LDS read queue at the end of a K-tile must match its start"
+    for parity in (0, 1):
+        q = list(queue0)
+        bodies.append(body(name, sched, parity, q))
+        assert q == queue0, f"{name}: LDS read queue at the end of a K-tile must match its start"
     lines.append("amdk8s_w4a_loop_%=:")
     lines += bodies[0]
     lines += ["s_add_u32 s73, s73, 1", "s_cmp_ge_u32 s73, s72", "s_cbranch_scc1 amdk8s_w4a_end_%="]
@@ -231,18 +262,32 @@ def main():
     lines += ["s_add_u32 s73, s73, 1", "s_cmp_lt_u32 s73, s72", "s_cbranch_scc1 amdk8s_w4a_loop_%="]
     lines.append("amdk8s_w4a_end_%=:")
     lines += epilogue()
+    return lines
+
+
+def main():
+    names = list(SCHEDULES)
     clob = ([f'"v{i}"' for i in range(139)] + [f'"a{i}"' for i in range(256)]
-            + [f'"s{i}"' for i in range(64, 96)] + ['"scc"', '"memory"'])  # M0: reserved; no M0 user follows the asm
+            + [f'"s{i}"' for i in range(64, 96)] + ['"scc"', '"memory"'])
+    # M0 is a reserved register for hipcc (not clobberable); no M0 user follows the asm.
     with open(OUT, "w") as f:
         f.write("// GENERATED by tools/gen_gemm_w4a_kloop.py — do not edit by hand.\n")
-        f.write(f"// {sum(1 for l in lines if 'v_mfma' in l)} MFMAs, {len(lines)} instructions.\n")
-        f.write("#define AMDK8S_W4A_ASM \\\n")
-        for ln in lines:
-            f.write(f'  "{ln}\\n" \\\n')
-        f.write("  \"\"\n\n#define AMDK8S_W4A_CLOBBERS \\\n")
+        f.write(f"// schedules: {', '.join(f'{i} = {n}' for i, n in enumerate(names))}; "
+                f"default {DEFAULT}\n")
+        f.write(f"#define AMDK8S_W4A_NUM_SCHEDULES {len(names)}\n")
+        f.write(f"#define AMDK8S_W4A_DEFAULT_SCHEDULE {names.index(DEFAULT)}\n")
+        f.write("#define AMDK8S_W4A_SCHEDULE_NAMES {" + ", ".join(f'"{n}"' for n in names) + "}\n")
+        for i, n in enumerate(names):
+            lines = kernel_asm(n)
+            f.write(f"\n// {n}: {sum(1 for l in lines if 'v_mfma' in l)} MFMAs, "
+                    f"{len(lines)} instructions\n#define AMDK8S_W4A_ASM_{i} \\\n")
+            for ln in lines:
+                f.write(f'  "{ln}\\n" \\\n')
+            f.write("  \"\"\n")
+        f.write("\n#define AMDK8S_W4A_CLOBBERS \\\n")
         for i in range(0, len(clob), 12):
             f.write("  " + ", ".join(clob[i:i + 12]) + (", \\\n" if i + 12 < len(clob) else "\n"))
-    print(f"wrote {OUT}: {len(lines)} lines")
+    print(f"wrote {OUT}: schedules {names}")
 
 
 if __name__ == "__main__":
