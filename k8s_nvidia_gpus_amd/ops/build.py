@@ -73,6 +73,7 @@ NATIVE_TARGETS: List[NativeTarget] = [
                                         "k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950_w4.hip",
                                         "k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950_w4a.hip",
                                         "k8s_nvidia_gpus_amd/ops/csrc/gemm_fp8_gfx950.hip",
+                                        "k8s_nvidia_gpus_amd/ops/csrc/gemm_fp8_gfx950_f8a.hip",
                                         "k8s_nvidia_gpus_amd/ops/csrc/fill.hip"], "hipcc"),
     NativeTarget("rccl-allreduce-bench", ["native/src/rccl_allreduce_bench.hip"], "hipcc",
                  libs=["-lrccl", "-lpthread"]),

@@ -61,6 +61,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.amdk8s_gemm_bf16_nt_w4a.restype = ci
     lib.amdk8s_gemm_fp8_nt.argtypes = [vp, vp, vp, ci, ci, ci, ci, ci, ci, vp]
     lib.amdk8s_gemm_fp8_nt.restype = ci
+    lib.amdk8s_gemm_fp8_nt_f8a.argtypes = [vp, vp, vp, ci, ci, ci, ci, ci, ci, vp]
+    lib.amdk8s_gemm_fp8_nt_f8a.restype = ci
     lib.amdk8s_gemm_bf16_nt_sample_check.argtypes = [vp, vp, vp, vp, ci, ci, ci, ci, vp]
     lib.amdk8s_gemm_bf16_nt_sample_check.restype = ci
     lib.amdk8s_vector_add_f32.argtypes = [vp, vp, vp, ci, vp]
@@ -185,11 +187,18 @@ def gemm_fp8_shape_supported(m: int, n: int, k: int) -> bool:
     return m > 0 and n > 0 and k > 0 and m % 256 == 0 and n % 256 == 0 and k % 256 == 0
 
 
-def gemm_fp8_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+FP8_VARIANTS = ("f8a", "hipcc")
+DEFAULT_FP8_VARIANT = os.environ.get("AMDK8S_FP8_VARIANT", "f8a")
+
+
+def gemm_fp8_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
+                variant: Optional[str] = None) -> torch.Tensor:
     """``out = a @ b.T`` in fp8 (OCP e4m3) with fp32 accumulation and a bf16 result.
 
-    The hand-written gfx950 kernel (gemm_fp8_gfx950.hip) runs ``v_mfma_scale_f32_16x16x128_f8f6f4``
-    with unit block scales — 2× the bf16 MFMA rate — on the bf16 w4 kernel's data path.
+    The hand-written gfx950 kernels run ``v_mfma_scale_f32_16x16x128_f8f6f4`` with unit block
+    scales — 2× the bf16 MFMA rate — on the bf16 w4 kernel's data path: ``"f8a"`` (default) with
+    its K-loop as generated assembly (gemm_fp8_gfx950_f8a.hip), ``"hipcc"`` the compiler-scheduled
+    original (gemm_fp8_gfx950.hip); both give the same bits.
     ``a``: [M, K], ``b``: [N, K], both ``torch.float8_e4m3fn``, row-major with unit inner stride and
     leading dimensions that are multiples of 16; M, N multiples of 256 and K a multiple of 256.
     """
@@ -209,10 +218,14 @@ def gemm_fp8_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = 
         out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
     elif out.shape != (m, n) or out.dtype != torch.bfloat16 or out.stride(1) != 1:
         raise ValueError("bad out tensor")
-    rc = library().amdk8s_gemm_fp8_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
-                                      a.stride(0), b.stride(0), out.stride(0),
-                                      _stream_handle(a.device))
-    _check(rc, "amdk8s_gemm_fp8_nt")
+    variant = variant or DEFAULT_FP8_VARIANT
+    if variant not in FP8_VARIANTS:
+        raise ValueError(f"unknown fp8 GEMM variant {variant!r} (have {FP8_VARIANTS})")
+    lib = library()
+    fn = lib.amdk8s_gemm_fp8_nt_f8a if variant == "f8a" else lib.amdk8s_gemm_fp8_nt
+    rc = fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0), b.stride(0),
+            out.stride(0), _stream_handle(a.device))
+    _check(rc, f"amdk8s_gemm_fp8_nt[{variant}]")
     return out
 
 

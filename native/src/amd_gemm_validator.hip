@@ -29,7 +29,7 @@ namespace {
 // back to w4 for panels past 32-bit offsets; docs/gemm_tuning.md).
 int gemm(const std::string& variant, const void* A, const void* B, void* C, int m, int n, int k,
          hipStream_t s) {
-  if (variant == "fp8") return amdk8s_gemm_fp8_nt(A, B, C, m, n, k, k, k, n, s);
+  if (variant == "fp8") return amdk8s_gemm_fp8_nt_f8a(A, B, C, m, n, k, k, k, n, s);
   if (variant == "w8") return amdk8s_gemm_bf16_nt(A, B, C, m, n, k, k, k, n, s);
   if (variant == "w4") return amdk8s_gemm_bf16_nt_w4(A, B, C, m, n, k, k, k, n, s);
   const int rc = amdk8s_gemm_bf16_nt_w4a(A, B, C, m, n, k, k, k, n, s);

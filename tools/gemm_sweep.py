@@ -40,13 +40,15 @@ def main():
         K.fill_uniform_bf16(b, 12)
         c = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
         arms = {}
-        if any(x in ("f8", "blt8") for x in args.arms):
+        if any(x in ("f8", "f8h", "blt8") for x in args.arms):
             a8 = K.uniform_fp8((m, k), 13, dev)
             b8 = K.uniform_fp8((n, k), 14, dev)
             one = torch.ones((), device=dev)
         for arm in args.arms:
-            if arm == "f8":  # hand-written fp8 e4m3 kernel
+            if arm == "f8":  # hand-written fp8 e4m3 kernel (default: generated-assembly K-loop)
                 arms[arm] = lambda: K.gemm_fp8_nt(a8, b8, out=c)
+            elif arm == "f8h":  # the hipcc-scheduled fp8 kernel
+                arms[arm] = lambda: K.gemm_fp8_nt(a8, b8, out=c, variant="hipcc")
             elif arm == "blt8":  # hipBLASLt fp8 through torch._scaled_mm (unit scales)
                 arms[arm] = lambda: torch._scaled_mm(a8, b8.t(), scale_a=one, scale_b=one,
                                                      out_dtype=torch.bfloat16)
