@@ -222,13 +222,16 @@ def test_gemm_w4_schedule_repeatable_under_load(K, dev, schedule, monkeypatch):
 @pytest.mark.parametrize("m,n,k", [(256, 256, 256), (512, 256, 768), (768, 512, 2048),
                                    (4096, 4096, 512), (2304, 1280, 1024)])
 def test_gemm_fp8_matches_fp32(K, dev, m, n, k):
-    """fp8 e4m3 GEMM against an fp32 matmul of the same (exactly representable) fp8 values."""
+    """fp8 e4m3 GEMM against an fp32 matmul of the same (exactly representable) fp8 values; the
+    generated-assembly f8a kernel (default) and the hipcc-scheduled one give identical bits."""
     a = K.uniform_fp8((m, k), seed=m + 3 * k, device=dev)
     b = K.uniform_fp8((n, k), seed=n + 5 * k, device=dev)
-    c = K.gemm_fp8_nt(a, b)
+    c = torch.full((m, n), float("nan"), dtype=torch.bfloat16, device=dev)
+    K.gemm_fp8_nt(a, b, out=c)
     ref = a.float() @ b.float().t()
     torch.testing.assert_close(c.float(), ref, rtol=1e-2, atol=1e-2 * (k ** 0.5) / 8)
     assert torch.equal(K.gemm_fp8_nt(a, b), c)  # deterministic
+    assert torch.equal(K.gemm_fp8_nt(a, b, variant="hipcc"), c)
 
 
 def test_gemm_fp8_identity_asymmetric(K, dev):
