@@ -107,9 +107,11 @@ def body(parity: int, queue: list) -> list:
             del queue[: len(queue) - keep]
         n = 8 * I + J
         a_lo = int(a_reg(I, 0, parity)[2:].split(":")[0])
-        out.append(f"v_mfma_scale_f32_16x16x128_f8f6f4 a[{4 * n}:{4 * n + 3}], "
+        # the unscaled f8f6f4 MFMA (operand formats cbsz = blgp = 0: OCP e4m3) — what the unit E8M0
+        # scales of the _scale form compute, in an 8-byte encoding instead of 16
+        out.append(f"v_mfma_f32_16x16x128_f8f6f4 a[{4 * n}:{4 * n + 3}], "
                    f"v[{64 + 64 * parity + 8 * J}:{64 + 64 * parity + 8 * J + 7}], "
-                   f"v[{a_lo}:{a_lo + 7}], a[{4 * n}:{4 * n + 3}], v203, v203 op_sel_hi:[0,0,0]")
+                   f"v[{a_lo}:{a_lo + 7}], a[{4 * n}:{4 * n + 3}]")
         for kind, tag, ins in after[k]:
             if kind == "lds":
                 queue.append(tag)
