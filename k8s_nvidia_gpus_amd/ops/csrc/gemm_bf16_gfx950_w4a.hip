@@ -35,6 +35,7 @@ constexpr int LDS_BYTES = BM * C_STRIDE;     // 135168 ≥ 2 × 64 KiB K-tile bu
 constexpr int GROUP_M = 8;
 
 typedef __attribute__((address_space(3))) char lds_char;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
 }  // namespace
 
@@ -42,7 +43,7 @@ template <int SCHED>
 __global__ void __launch_bounds__(NT, 1)
 amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                 uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
-                                int ldc, int superblock) {
+                                int ldc, int superblock, int nt_store) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
 
   const int tid = threadIdx.x;
@@ -125,8 +126,12 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
   for (int it = 0; it < BM * BN * 2 / (NT * 16); ++it) {
     const int row = it * 8 + (tid >> 5);
     const int ch = tid & 31;
-    const uint4 v = *reinterpret_cast<const uint4*>(lds + row * C_STRIDE + ch * 16);
-    *reinterpret_cast<uint4*>(cbase_g + row * ldc_b + ch * 16) = v;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * C_STRIDE + ch * 16);
+    u32x4* dst = reinterpret_cast<u32x4*>(cbase_g + row * ldc_b + ch * 16);
+    if (nt_store)  // C streams out (nt: no L2/MALL retention) — the caches stay with A and B
+      asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(dst), "v"(v) : "memory");
+    else
+      *dst = v;
   }
 }
 
@@ -143,6 +148,9 @@ extern "C" int amdk8s_gemm_bf16_nt_w4a(const void* A, const void* B, void* C, in
   const char* sbenv = getenv("AMDK8S_W4_SUPERBLOCK");
   int sb = (M / BM) % 16 == 0 && (N / BN) % 16 == 0 && !(sbenv && sbenv[0] == '0');
   if (sb && sbenv && sbenv[0] == '2') sb = 2;
+  // non-temporal C stores (AMDK8S_GEMM_NT_STORE=0 turns them off for A/B runs)
+  const char* ntenv = getenv("AMDK8S_GEMM_NT_STORE");
+  const int nt = !(ntenv && ntenv[0] == '0');
   // K-loop schedule: the generator's default, or AMDK8S_W4A_SCHEDULE=<name> for A/B runs
   int sched = AMDK8S_W4A_DEFAULT_SCHEDULE;
   if (const char* e = getenv("AMDK8S_W4A_SCHEDULE")) {
@@ -155,12 +163,12 @@ extern "C" int amdk8s_gemm_bf16_nt_w4a(const void* A, const void* B, void* C, in
   uint16_t* c = (uint16_t*)C;
   if (sched == 1)
     hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4a<1>, dim3(nwg), dim3(NT), 0, stream, a, b, c,
-                       M, N, K, lda, ldb, ldc, sb);
+                       M, N, K, lda, ldb, ldc, sb, nt);
   else if (sched == 2)
     hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4a<2>, dim3(nwg), dim3(NT), 0, stream, a, b, c,
-                       M, N, K, lda, ldb, ldc, sb);
+                       M, N, K, lda, ldb, ldc, sb, nt);
   else
     hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4a<0>, dim3(nwg), dim3(NT), 0, stream, a, b, c,
-                       M, N, K, lda, ldb, ldc, sb);
+                       M, N, K, lda, ldb, ldc, sb, nt);
   return (int)hipGetLastError();
 }

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "gemm_fp8_gfx950_f8a_kloop.inc"
 
@@ -30,13 +31,15 @@ constexpr int LDS_BYTES = BM * C_STRIDE;     // 135168 ≥ 2 × 64 KiB K-tile bu
 constexpr int GROUP_M = 8;
 
 typedef __attribute__((address_space(3))) char lds_char;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
 }  // namespace
 
+template <int SCHED>
 __global__ void __launch_bounds__(NT, 1)
 amdk8s_gemm_fp8_nt_256x256_f8a(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                 uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
-                                int ldc, int superblock) {
+                                int ldc, int superblock, int nt_store) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
 
   const int tid = threadIdx.x;
@@ -100,12 +103,15 @@ amdk8s_gemm_fp8_nt_256x256_f8a(const uint8_t* __restrict__ A, const uint8_t* __r
   const uint32_t nrec_a = 256u * lda_b, nrec_b = 256u * ldb_b;
   const int T = K / BK;
 
-asm volatile(AMDK8S_F8A_ASM
-               :
-               : "s"(T), "s"(a_lo), "s"(a_hi), "s"(nrec_a), "s"(b_lo), "s"(b_hi), "s"(nrec_b),
-                 "s"(lda_b), "s"(ldb_b), "s"(dma_lds), "v"(ra0), "v"(ra1), "v"(rb0), "v"(rb1),
-                 "v"(a_voff), "v"(b_voff), "v"(cbase)
-               : AMDK8S_F8A_CLOBBERS);
+#define AMDK8S_F8A_OPERANDS                                                                \
+  : "s"(T), "s"(a_lo), "s"(a_hi), "s"(nrec_a), "s"(b_lo), "s"(b_hi), "s"(nrec_b), "s"(lda_b),  \
+    "s"(ldb_b), "s"(dma_lds), "v"(ra0), "v"(ra1), "v"(rb0), "v"(rb1), "v"(a_voff), "v"(b_voff), \
+    "v"(cbase)                                                                                 \
+  : AMDK8S_F8A_CLOBBERS
+  static_assert(AMDK8S_F8A_NUM_SCHEDULES == 2, "one branch per generated schedule");
+  if constexpr (SCHED == 0) asm volatile(AMDK8S_F8A_ASM_0 : AMDK8S_F8A_OPERANDS);
+  else asm volatile(AMDK8S_F8A_ASM_1 : AMDK8S_F8A_OPERANDS);
+#undef AMDK8S_F8A_OPERANDS
   __syncthreads();  // every wave's quarter of the bf16 C image is in LDS
 
   // ---- 16-B coalesced stores of the 256×256 bf16 tile ----
@@ -115,8 +121,12 @@ asm volatile(AMDK8S_F8A_ASM
   for (int it = 0; it < BM * BN * 2 / (NT * 16); ++it) {
     const int row = it * 8 + (tid >> 5);
     const int ch = tid & 31;
-    const uint4 v = *reinterpret_cast<const uint4*>(lds + row * C_STRIDE + ch * 16);
-    *reinterpret_cast<uint4*>(cbase_g + row * ldc_b + ch * 16) = v;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * C_STRIDE + ch * 16);
+    u32x4* dst = reinterpret_cast<u32x4*>(cbase_g + row * ldc_b + ch * 16);
+    if (nt_store)  // C streams out (nt: no L2/MALL retention) — the caches stay with A and B
+      asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(dst), "v"(v) : "memory");
+    else
+      *dst = v;
   }
 }
 
@@ -132,7 +142,24 @@ extern "C" int amdk8s_gemm_fp8_nt_f8a(const void* A, const void* B, void* C, int
   const char* sbenv = getenv("AMDK8S_W4_SUPERBLOCK");
   int sb = (M / BM) % 16 == 0 && (N / BN) % 16 == 0 && !(sbenv && sbenv[0] == '0');
   if (sb && sbenv && sbenv[0] == '2') sb = 2;
-  hipLaunchKernelGGL(amdk8s_gemm_fp8_nt_256x256_f8a, dim3(nwg), dim3(NT), 0, stream,
-                     (const uint8_t*)A, (const uint8_t*)B, (uint16_t*)C, M, N, K, lda, ldb, ldc, sb);
+  // non-temporal C stores (AMDK8S_GEMM_NT_STORE=0 turns them off for A/B runs)
+  const char* ntenv = getenv("AMDK8S_GEMM_NT_STORE");
+  const int nt = !(ntenv && ntenv[0] == '0');
+  // K-loop schedule: the generator's default, or AMDK8S_F8A_SCHEDULE=<name> for A/B runs
+  int sched = AMDK8S_F8A_DEFAULT_SCHEDULE;
+  if (const char* e = getenv("AMDK8S_F8A_SCHEDULE")) {
+    static const char* const names[] = AMDK8S_F8A_SCHEDULE_NAMES;
+    for (int i = 0; i < AMDK8S_F8A_NUM_SCHEDULES; ++i)
+      if (!strcmp(e, names[i])) sched = i;
+  }
+  const uint8_t* a = (const uint8_t*)A;
+  const uint8_t* b = (const uint8_t*)B;
+  uint16_t* c = (uint16_t*)C;
+  if (sched == 1)
+    hipLaunchKernelGGL(amdk8s_gemm_fp8_nt_256x256_f8a<1>, dim3(nwg), dim3(NT), 0, stream, a, b, c,
+                       M, N, K, lda, ldb, ldc, sb, nt);
+  else
+    hipLaunchKernelGGL(amdk8s_gemm_fp8_nt_256x256_f8a<0>, dim3(nwg), dim3(NT), 0, stream, a, b, c,
+                       M, N, K, lda, ldb, ldc, sb, nt);
   return (int)hipGetLastError();
 }

@@ -40,13 +40,23 @@ def main():
         K.fill_uniform_bf16(b, 12)
         c = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
         arms = {}
-        if any(x in ("f8", "f8h", "blt8") for x in args.arms):
+        if any(x in ("f8", "f8h", "blt8") or x.startswith("f8@") for x in args.arms):
             a8 = K.uniform_fp8((m, k), 13, dev)
             b8 = K.uniform_fp8((n, k), 14, dev)
             one = torch.ones((), device=dev)
         for arm in args.arms:
             if arm == "f8":  # hand-written fp8 e4m3 kernel (default: generated-assembly K-loop)
                 arms[arm] = lambda: K.gemm_fp8_nt(a8, b8, out=c)
+            elif arm.startswith("f8@"):  # f8@ENV=VALUE: the fp8 kernel with a launcher env knob
+                k_, v_ = arm[3:].split("=", 1)
+
+                def fn(k_=k_, v_=v_):
+                    os.environ[k_] = v_
+                    try:
+                        K.gemm_fp8_nt(a8, b8, out=c)
+                    finally:
+                        os.environ.pop(k_, None)
+                arms[arm] = fn
             elif arm == "f8h":  # the hipcc-scheduled fp8 kernel
                 arms[arm] = lambda: K.gemm_fp8_nt(a8, b8, out=c, variant="hipcc")
             elif arm == "blt8":  # hipBLASLt fp8 through torch._scaled_mm (unit scales)

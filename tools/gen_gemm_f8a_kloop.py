@@ -62,20 +62,28 @@ def b_reg(s: int, j: int, half: int) -> str:
     return f"v[{b}:{b + 3}]"
 
 
-def read_slots():
-    """(slot, operand, index, half) for the 32 next-tile reads, one per MFMA gap after barrier #2."""
-    out, slot = [], BAR2 + 1
+def read_slots(per_slot: int = 1):
+    """(slot, operand, index, half) for the 32 next-tile reads after barrier #2, `per_slot` per MFMA
+    gap, each in-place A'I no earlier than the slot after MFMA 8·I + 7."""
+    out, slot, used = [], BAR2 + 1, 0
     for opnd, idx in READS:
-        if opnd == "a" and idx > 0 and idx not in A_DOUBLE:
-            slot = max(slot, 8 * idx + 8)                    # after A[idx]'s last MFMA (8·idx + 7)
+        if opnd == "a" and idx > 0 and idx not in A_DOUBLE and slot < 8 * idx + 8:
+            slot, used = 8 * idx + 8, 0
         for half in (0, 1):
             out.append((min(slot, 63), opnd, idx, half))
-            slot += 1
+            used += 1
+            if used == per_slot:
+                slot, used = slot + 1, 0
     assert all(BAR2 < s <= 63 for s, *_ in out)
     return out
 
 
-def body(parity: int, queue: list) -> list:
+# schedules: name → reads per MFMA gap after barrier #2
+SCHEDULES = {"spread": 1, "dense": 2}
+DEFAULT = "dense"
+
+
+def body(parity: int, queue: list, per_slot: int = 1) -> list:
     """One K-tile: barrier #1 (lgkmcnt(0): every wave holds tile t) and the clamped DMA-source
     advance sit before MFMA 0; op lists after[k] issue right after MFMA k."""
     after = [[] for _ in range(64)]
@@ -91,7 +99,7 @@ def body(parity: int, queue: list) -> list:
         after[slot - 1].append(("salu", None, f"s_add_u32 m0, s74, {parity * TILE + off}"))
         after[slot].append(("vmem", None, f"buffer_load_dwordx4 {voff}, {rs}, {row} offen lds"))
     after[BAR2] += [("waitv", None, "s_waitcnt vmcnt(16)"), ("bar", None, "s_barrier")]
-    for slot, opnd, idx, half in read_slots():
+    for slot, opnd, idx, half in read_slots(per_slot):
         base = f"v{192 + 4 * nxt + (0 if opnd == 'a' else 2) + half}"
         dst = a_reg(idx, half, nxt) if opnd == "a" else b_reg(nxt, idx, half)
         tag = atag(idx, half, nxt) if opnd == "a" else f"b{nxt}{idx}{half}"
@@ -176,7 +184,7 @@ def epilogue() -> list:
     return out
 
 
-def main():
+def kernel_asm(per_slot: int) -> list:
     lines = prologue()
     bodies = []
     # LDS reads outstanding at the top of a K-tile of parity p: the 32 next-tile reads of the
@@ -185,7 +193,7 @@ def main():
                for p in (0, 1)}
     for parity in (0, 1):
         q = list(q_start[parity])
-        bodies.append(body(parity, q))
+        bodies.append(body(parity, q, per_slot))
         assert q == q_start[1 - parity], q
     lines.append("amdk8s_f8a_loop_%=:")
     lines += bodies[0]
@@ -194,18 +202,31 @@ def main():
     lines += ["s_add_u32 s73, s73, 1", "s_cmp_lt_u32 s73, s72", "s_cbranch_scc1 amdk8s_f8a_loop_%="]
     lines.append("amdk8s_f8a_end_%=:")
     lines += epilogue()
+    return lines
+
+
+def main():
+    names = list(SCHEDULES)
     clob = ([f'"v{i}"' for i in range(204 + 8 * len(A_DOUBLE))] + [f'"a{i}"' for i in range(256)]
             + [f'"s{i}"' for i in range(64, 96)] + ['"scc"', '"memory"'])
     with open(OUT, "w") as f:
         f.write("// GENERATED by tools/gen_gemm_f8a_kloop.py — do not edit by hand.\n")
-        f.write(f"// {sum(1 for l in lines if 'v_mfma' in l)} MFMAs, {len(lines)} instructions.\n")
-        f.write("#define AMDK8S_F8A_ASM \\\n")
-        for ln in lines:
-            f.write(f'  "{ln}\\n" \\\n')
-        f.write("  \"\"\n\n#define AMDK8S_F8A_CLOBBERS \\\n")
+        f.write(f"// schedules: {', '.join(f'{i} = {n}' for i, n in enumerate(names))}; "
+                f"default {DEFAULT}\n")
+        f.write(f"#define AMDK8S_F8A_NUM_SCHEDULES {len(names)}\n")
+        f.write(f"#define AMDK8S_F8A_DEFAULT_SCHEDULE {names.index(DEFAULT)}\n")
+        f.write("#define AMDK8S_F8A_SCHEDULE_NAMES {" + ", ".join(f'"{n}"' for n in names) + "}\n")
+        for i, n in enumerate(names):
+            lines = kernel_asm(SCHEDULES[n])
+            f.write(f"\n// {n}: {sum(1 for l in lines if 'v_mfma' in l)} MFMAs, "
+                    f"{len(lines)} instructions\n#define AMDK8S_F8A_ASM_{i} \\\n")
+            for ln in lines:
+                f.write(f'  "{ln}\\n" \\\n')
+            f.write("  \"\"\n")
+        f.write("\n#define AMDK8S_F8A_CLOBBERS \\\n")
         for i in range(0, len(clob), 12):
             f.write("  " + ", ".join(clob[i:i + 12]) + (", \\\n" if i + 12 < len(clob) else "\n"))
-    print(f"wrote {OUT}: {len(lines)} lines")
+    print(f"wrote {OUT}: schedules {names}")
 
 
 if __name__ == "__main__":
