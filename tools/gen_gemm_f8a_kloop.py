@@ -143,7 +143,9 @@ def prologue() -> list:
         out.append(f"v_add_u32 v{196 + i}, {TILE}, %{10 + i}")
     out += ["v_mov_b32 v200, %14", "v_mov_b32 v201, %15", "v_mov_b32 v202, %16",
             "v_mov_b32 v203, 0x7f7f7f7f"]
-    out += [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
+    # the 256 accumulator zero-writes fill the gaps between the 32 prologue DMA issues (8 per gap:
+    # they also cover the M0 → LDS-DMA hazard) instead of delaying the first DMA
+    zero = [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
     for buf in range(2):
         if buf == 1:
             out += ["s_cmp_gt_u32 s72, 1", "s_cselect_b32 s76, 0x80, 0",
@@ -152,7 +154,8 @@ def prologue() -> list:
         for p in range(16):
             opnd, row, off = piece(p)
             rs, voff = ("s[64:67]", "v200") if opnd == "A" else ("s[68:71]", "v201")
-            out += [f"s_add_u32 m0, s74, {buf * TILE + off}", "s_nop 0",
+            gap = zero[(buf * 16 + p) * 8:(buf * 16 + p + 1) * 8]
+            out += [f"s_add_u32 m0, s74, {buf * TILE + off}", *gap,
                     f"buffer_load_dwordx4 {voff}, {rs}, {row} offen lds"]
     out += ["s_waitcnt vmcnt(16)", "s_barrier"]
     for opnd, idx in READS:             # tile 0 into A and B set 0, in the loop's read order

@@ -204,7 +204,9 @@ def prologue(r0_order) -> list:
         out.append(f"v_mov_b32 v{128 + i}, %{10 + i}")
         out.append(f"v_add_u32 v{132 + i}, {TILE}, %{10 + i}")
     out += ["v_mov_b32 v136, %14", "v_mov_b32 v137, %15", "v_mov_b32 v138, %16"]
-    out += [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
+    # the 256 accumulator zero-writes fill the gaps between the 32 prologue DMA issues (8 per gap:
+    # they also cover the M0 → LDS-DMA hazard) instead of delaying the first DMA
+    zero = [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
     for buf in range(2):                # K-tiles 0 and min(1, T-1) in flight (buffers 0 and 1)
         if buf == 1:
             out += ["s_cmp_gt_u32 s72, 1", "s_cselect_b32 s76, 0x80, 0",
@@ -213,7 +215,8 @@ def prologue(r0_order) -> list:
         for p in range(16):
             opnd, row, off = piece(p)
             rs, voff = ("s[64:67]", "v136") if opnd == "A" else ("s[68:71]", "v137")
-            out += [f"s_add_u32 m0, s74, {buf * TILE + off}", "s_nop 0",
+            gap = zero[(buf * 16 + p) * 8:(buf * 16 + p + 1) * 8]
+            out += [f"s_add_u32 m0, s74, {buf * TILE + off}", *gap,
                     f"buffer_load_dwordx4 {voff}, {rs}, {row} offen lds"]
     out += ["s_waitcnt vmcnt(16)", "s_barrier"]
     for opnd, idx in r0_order:          # the loop's own next-tile read order (same LDS queue)
