@@ -15,7 +15,9 @@ rank 0 prints ONE JSON line.  ``value`` is the whole-job aggregate TFLOPS over a
 
 Outside the timed region it also reports:
 * ``time_to_first_gpu_result_s`` — process start → first verified GPU result (HIP vectorAdd,
-  reference protocol), the in-process part of the "time-to-first-GPU-pod" metric;
+  reference protocol), the in-process part of the "time-to-first-GPU-pod" metric (mostly
+  ``import torch``); ``time_to_first_gpu_result_native_s`` — the same check as the validator pod
+  runs it (native ``amd-vectoradd``, a child process started before torch loads, this rank's GPU);
 * ``numerics_max_rel_err`` — sampled error of the timed kernel against an fp32 on-device reference;
 * ``allreduce_busbw_gbps`` — RCCL all-reduce bus bandwidth over xGMI across the N ranks (N > 1);
 * ``fp8_tflops`` — the validator's second precision: the same GEMM shape in OCP fp8 e4m3 through
@@ -34,7 +36,28 @@ _T_PROCESS_START = time.time()
 import argparse  # noqa: E402
 import json  # noqa: E402
 import os  # noqa: E402
+import subprocess  # noqa: E402
 import sys  # noqa: E402
+
+
+def native_first_gpu_result():
+    """The validator pod's own first GPU result: seconds for ``native/bin/amd-vectoradd`` (reference
+    protocol, 50 000 fp32) to print ``Test PASSED`` on this rank's GPU, as a child process started
+    before this process imports torch or touches a GPU. None when the binary is not built."""
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "bin", "amd-vectoradd")
+    if "--cpu-smoke" in sys.argv or not os.access(exe, os.X_OK):
+        return None
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("LOCAL_RANK", "0"))
+    t0 = time.time()
+    try:
+        out = subprocess.run([exe], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                             text=True, timeout=120).stdout
+    except (OSError, subprocess.TimeoutExpired):
+        return None
+    return round(time.time() - t0, 3) if "Test PASSED" in out else None
+
+
+_NATIVE_TTFR = native_first_gpu_result()
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -229,6 +252,7 @@ def main(argv=None) -> int:
             "tflops_per_gpu": round(value / world, 2),
             "tflops_per_rank": per_rank,
             "time_to_first_gpu_result_s": round(ttfr, 3) if ttfr is not None else None,
+            "time_to_first_gpu_result_native_s": _NATIVE_TTFR,
             "numerics_max_rel_err": max_rel_err,
             "allreduce_busbw_gbps": (round(busbw, 2) if busbw is not None else None),
             "fp8_tflops": (round(fp8_tflops, 2) if fp8_tflops is not None else None),
