@@ -26,13 +26,14 @@ def test_committed_inc_matches_generator(gen, tmp_path, monkeypatch):
     assert out.read_text() == committed, f"rerun {gen.__name__}.py and commit its .inc"
 
 
-@pytest.mark.parametrize("name", list(w4a.SCHEDULES))
+@pytest.mark.parametrize("name", list(w4a.SCHEDULES) + list(w4a.EXPERIMENTS))
 def test_w4a_schedules_pass_discipline_checks(name):
-    sched = w4a.SCHEDULES[name]()
+    sched = {**w4a.SCHEDULES, **w4a.EXPERIMENTS}[name]()
     w4a.check(name, sched)
     lines = w4a.kernel_asm(name)
     assert sum("v_mfma_f32_16x16x32_bf16" in ln for ln in lines) == 256  # 2 parities x 128
-    assert sum(ln == "s_barrier" for ln in lines) == 2 * 3 + 2           # + prologue, epilogue
+    per_tile = 2 if any(op == ("bar", 12) for _, op in sched) else 3       # twobar merges #1/#2
+    assert sum(ln == "s_barrier" for ln in lines) == 2 * per_tile + 2    # + prologue, epilogue
 
 
 def test_w4a_rejects_dma_before_its_barrier():

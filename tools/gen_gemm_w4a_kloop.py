@@ -109,7 +109,40 @@ def sched_mirror():
     return s
 
 
+def sched_early():
+    """Everything ~30 MFMAs earlier: b1 reads two per gap (barrier #1 after MFMA 7), B pieces and
+    a1 reads every 4 gaps, barrier #2 after 39, A pieces every 4 gaps, barrier #3 after 71, next-tile
+    reads every other gap from 72 — more DMA lead for tile t+2 and more slack for the reads."""
+    s = []
+    b_first = [x for x in FIRST_USE if x[0] == "b"]
+    for j, (o, i) in enumerate(b_first):
+        s.append((j // 2, ("r1", o, i)))
+    s.append((4, ("r1", "a", 0)))
+    s.append((7, ("bar", 1)))
+    s += [(9 + 4 * e, ("dma", 2 * e + 1)) for e in range(8)]
+    s += [(8 + 4 * (i - 1), ("r1", "a", i)) for i in range(1, 8)]
+    s.append((39, ("bar", 2)))
+    s += [(41 + 4 * e, ("dma", 2 * e)) for e in range(8)]
+    s.append((71, ("bar", 3)))
+    s += [(72 + 2 * x, ("r0",) + FIRST_USE[x]) for x in range(16)]
+    return s
+
+
+def sched_twobar():
+    """Barriers #1 and #2 merged (after MFMA 47, once all 16 K-half-1 reads are done): the 16 DMA
+    pieces alternate B/A every 3 gaps from 49, barrier #3 after 103 as in REGION."""
+    s = [(3 * x, ("r1",) + FIRST_USE[x]) for x in range(16)]
+    s.append((47, ("bar", 12)))
+    s += [(49 + 3 * k, ("dma", k)) for k in range(16)]
+    s.append((103, ("bar", 3)))
+    s += [x for x in sched_region() if x[1][0] == "r0"]
+    return s
+
+
 SCHEDULES = {"region": sched_region, "early3": sched_early3, "mirror": sched_mirror}
+# measured and rejected (profiles/r01_session4/sweep_w4a_early_twobar.txt: −1.6…−4 % and −2…−6 %
+# against region); kept as checked specs, not built into the library
+EXPERIMENTS = {"early": sched_early, "twobar": sched_twobar}
 DEFAULT = "region"
 
 
@@ -120,6 +153,8 @@ def check(name: str, sched) -> None:
     for slot, op in sched:
         slots.setdefault(op, []).append(slot)
         assert 0 <= slot < 128, (name, slot, op)
+    if ("bar", 12) in slots:          # merged barrier #1/#2: frees both regions at once
+        slots[("bar", 1)] = slots[("bar", 2)] = slots[("bar", 12)]
     bar = {k: slots[("bar", k)][0] for k in (1, 2, 3)}
     r1 = [(slot, op) for slot, op in sched if op[0] == "r1"]
     r0 = [(slot, op) for slot, op in sched if op[0] == "r0"]
@@ -166,9 +201,10 @@ def body(name: str, sched, parity: int, queue: list) -> list:
             "s_add_u32 s64, s64, s76", "s_addc_u32 s65, s65, 0",
             "s_add_u32 s68, s68, s76", "s_addc_u32 s69, s69, 0"]
     first_dma = min(slot for slot, op in sched if op[0] == "dma")
-    assert 1 + 2 * (len(step) - 1) < first_dma - 1, name
+    odd = 1 + 2 * (len(step) - 1) < first_dma - 1      # one per other gap if the DMA starts late
+    assert odd or len(step) - 1 < first_dma - 1, name
     for i, ins in enumerate(step):
-        after[1 + 2 * i].append(("salu", None, ins))
+        after[1 + 2 * i if odd else i].append(("salu", None, ins))
 
     out = []
     for k in range(128):
@@ -247,7 +283,7 @@ def epilogue() -> list:
 
 
 def kernel_asm(name: str) -> list:
-    sched = SCHEDULES[name]()
+    sched = {**SCHEDULES, **EXPERIMENTS}[name]()
     check(name, sched)
     r0_order = [op[1:] for _, op in sorted((x for x in sched if x[1][0] == "r0"),
                                            key=lambda x: x[0])]
