@@ -1,12 +1,13 @@
 // amd-gemm-validator — hand-written gfx950 bf16 / fp8 MFMA GEMM load + numerics check.
 //
 // Plays the role NVIDIA's dcgmproftester tensor-core load plays for the reference's operator
-// (BASELINE.json configs 3/4): it drives the in-tree 256×256 MFMA kernel
-// (k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950.hip) on every device the pod was allocated, in
+// (BASELINE.json configs 3/4): it drives the in-tree 256×256 MFMA kernels
+// (k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950*.hip; default w4a, whose K-loop is generated
+// assembly) on every device the pod was allocated, in
 // parallel (one host thread per device), on random [-1,1) bf16 data (never zeros — zero operands
 // inflate MFMA clocks), checks a sample of outputs against an fp32 on-device reference and reports
 // TFLOPS per GPU and in aggregate.  Output ends with "Test PASSED" / "Done" like amd-vectoradd.
-// --dtype fp8 runs the OCP-e4m3 kernel (gemm_fp8_gfx950.hip, 2× the bf16 MFMA rate) instead.
+// --dtype fp8 runs the OCP-e4m3 kernel (gemm_fp8_gfx950_f8a.hip, 2× the bf16 MFMA rate) instead.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
