@@ -11,7 +11,9 @@ N grows → weak scaling.
 Launch contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 under
 ``torch.distributed.run`` with one rank per GPU (RCCL backend).  W untimed steps, then exactly K
 timed steps bracketed by barrier + synchronize on both sides; the MAX elapsed over ranks is used;
-rank 0 prints ONE JSON line.  ``value`` is the whole-job aggregate TFLOPS over all N GPUs.
+rank 0 prints ONE JSON line.  Before the W warmup steps each rank runs the GEMM back-to-back for
+``--settle-ms`` (default 250 ms, untimed) so that the timed window measures sustained throughput
+rather than the chip's power-management transient after a load step (see :func:`settle`).  ``value`` is the whole-job aggregate TFLOPS over all N GPUs.
 
 Outside the timed region it also reports:
 * ``time_to_first_gpu_result_s`` — process start → first verified GPU result (HIP vectorAdd,
@@ -69,8 +71,11 @@ BASELINE_VALUE = None  # BASELINE.json "published": {} — the reference publish
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--settle-ms", type=float, default=250.0,
+                    help="untimed back-to-back GEMMs before the warmup steps, until the chip's clock "
+                         "has left its load-step transient (see settle())")
     ap.add_argument("--size", type=int, default=8192, help="M = N = K of the validator GEMM")
     ap.add_argument("--variant", default=None, help="GEMM variant (auto | w8 | w4)")
     ap.add_argument("--allreduce-mib", type=int, default=256,
@@ -79,6 +84,32 @@ def parse_args(argv=None):
     ap.add_argument("--no-fp8", action="store_true", help="skip the fp8 GEMM extra measurement")
     ap.add_argument("--cpu-smoke", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
+
+
+def settle(step, sync, settle_ms: float, chunk: int = 8, max_launches: int = 4000) -> int:
+    """Run ``step`` back-to-back (untimed) for at least ``settle_ms`` of GPU time; return launches.
+
+    MI355X answers a load step with a power-management transient: in back-to-back 8192³ bf16
+    GEMMs the first 2 launches run at ~680 us, launches 4-6 at ~900 us, and the chip takes ~40
+    launches (~30 ms) to come back to its sustained ~663 us (1655 TFLOPS, flat over 2.6 s / 4000
+    launches; profiles/r01_session5/gemm_settle_probe_4000.txt).  A short timed window that starts
+    inside the transient measures the DVFS controller, not the kernel: K=20/W=5 read 1463 TFLOPS,
+    K=50/W=10 1595, K=200/W=50 1669 on the same box (bench_kw_sweep_before_settle.txt).  The
+    validator's number is *sustained* throughput, so every timed window starts after this phase.
+    Nothing is skipped inside the timed region: it still holds exactly K full GEMMs.
+    """
+    if settle_ms <= 0:
+        return 0
+    n = 0
+    t0 = time.perf_counter()
+    while n < max_launches:
+        for _ in range(chunk):
+            step()
+        n += chunk
+        sync()
+        if (time.perf_counter() - t0) * 1e3 >= settle_ms:
+            break
+    return n
 
 
 def first_gpu_result(K, device: torch.device) -> float:
@@ -164,6 +195,7 @@ def main(argv=None) -> int:
         def step():
             K.gemm_bf16_nt(a, b, out=c, variant=variant)
 
+    settle_launches = settle(step, sync, 0.0 if smoke else args.settle_ms)
     for _ in range(args.warmup):
         step()
     sync()
@@ -195,15 +227,20 @@ def main(argv=None) -> int:
         del a, b
         a8 = K.uniform_fp8((s, s), seed=3000 + rank, device=device)
         b8 = K.uniform_fp8((s, s), seed=4000 + rank, device=device)
-        for _ in range(args.warmup):
+
+        def step8():
             K.gemm_fp8_nt(a8, b8, out=c)
+
+        settle(step8, sync, args.settle_ms)
+        for _ in range(args.warmup):
+            step8()
         sync()
         if distributed:
             dist.barrier()
         sync()
         t8 = time.perf_counter()
         for _ in range(args.steps):
-            K.gemm_fp8_nt(a8, b8, out=c)
+            step8()
         sync()
         if distributed:
             dist.barrier()
@@ -251,6 +288,7 @@ def main(argv=None) -> int:
             },
             "tflops_per_gpu": round(value / world, 2),
             "tflops_per_rank": per_rank,
+            "settle": {"ms": 0.0 if smoke else args.settle_ms, "launches": settle_launches},
             "time_to_first_gpu_result_s": round(ttfr, 3) if ttfr is not None else None,
             "time_to_first_gpu_result_native_s": _NATIVE_TTFR,
             "numerics_max_rel_err": max_rel_err,

@@ -104,3 +104,26 @@ def test_bench_py_distributed_contract_on_cpu():
     assert doc["config"]["parallelism"] == "dp2"
     assert len(doc["tflops_per_rank"]) == 2
     assert doc["value"] == pytest.approx(sum(doc["tflops_per_rank"]), rel=0.6)
+
+
+def test_bench_settle_phase_bounds():
+    """bench.settle(): untimed launches until settle_ms of synchronized time, capped, off at 0."""
+    import importlib.util
+    import time
+
+    spec = importlib.util.spec_from_file_location("bench_mod", REPO / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    calls, syncs = [], []
+
+    def step():
+        calls.append(1)
+        time.sleep(0.001)
+
+    assert bench.settle(step, lambda: syncs.append(1), 0.0) == 0 and not calls
+    t0 = time.perf_counter()
+    n = bench.settle(step, lambda: syncs.append(1), 20.0, chunk=4)
+    assert (time.perf_counter() - t0) * 1e3 >= 20.0
+    assert n == len(calls) and n % 4 == 0 and len(syncs) == n // 4
+    calls.clear()
+    assert bench.settle(step, lambda: None, 1e6, chunk=4, max_launches=12) == 12 == len(calls)
