@@ -13,7 +13,8 @@ Launch contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for
 timed steps bracketed by barrier + synchronize on both sides; the MAX elapsed over ranks is used;
 rank 0 prints ONE JSON line.  Before the W warmup steps each rank runs the GEMM back-to-back for
 ``--settle-ms`` (default 250 ms, untimed) so that the timed window measures sustained throughput
-rather than the chip's power-management transient after a load step (see :func:`settle`).  ``value`` is the whole-job aggregate TFLOPS over all N GPUs.
+rather than the chip's power-management transient after a load step (see :func:`settle`).
+``value`` is the whole-job aggregate TFLOPS over all N GPUs.
 
 Outside the timed region it also reports:
 * ``time_to_first_gpu_result_s`` — process start → first verified GPU result (HIP vectorAdd,
@@ -145,7 +146,8 @@ def main(argv=None) -> int:
     rank = int(os.environ.get("RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    distributed = world > 1
+    # torchrun with one rank still takes the RCCL path (a 1-GPU rehearsal of the N>1 code)
+    distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
     smoke = args.cpu_smoke
     if not smoke and not torch.cuda.is_available():
         print("bench.py needs an MI355X (no GPU visible)", file=sys.stderr)

@@ -88,3 +88,30 @@ def test_rccl_bench_single_gpu_passes(native):
                         "--json"], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "Test PASSED" in p.stdout
+
+
+def test_bench_py_rccl_path_under_torchrun_one_rank():
+    """bench.py under torchrun with one rank takes the N>1 code path (RCCL process group, MAX over
+    ranks, all_gather of per-rank TFLOPS, post-run all-reduce probe) on the real GPU."""
+    import socket
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parent.parent
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "1",
+           "--steps", "5", "--warmup", "2", "--settle-ms", "20", "--size", "2048",
+           "--allreduce-mib", "16", "--no-fp8"]
+    p = subprocess.run(cmd, capture_output=True, text=True, cwd=str(repo), timeout=240,
+                       env=dict(os.environ, PYTHONPATH=str(repo)))
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    doc = json.loads(lines[0])
+    assert doc["n_gpus"] == 1 and doc["steps"] == 5 and doc["value"] > 0
+    assert doc["allreduce_busbw_gbps"] is not None and len(doc["tflops_per_rank"]) == 1
+    assert doc["settle"]["launches"] > 0
