@@ -50,7 +50,11 @@ def native_first_gpu_result():
     exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "bin", "amd-vectoradd")
     if "--cpu-smoke" in sys.argv or not os.access(exe, os.X_OK):
         return None
-    env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    visible = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+    ids = [d for d in visible.split(",") if d.strip()] if visible else []
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=ids[local] if local < len(ids) else str(local))
+    env.pop("CUDA_VISIBLE_DEVICES", None)
     t0 = time.time()
     try:
         out = subprocess.run([exe], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
