@@ -282,9 +282,16 @@ class GpuCollector:
         busbw = GaugeMetricFamily("amd_gpu_validator_allreduce_busbw_gbps",
                                   "RCCL all-reduce bus bandwidth measured by the validator",
                                   labels=["node", "ngpus"])
+        secs = GaugeMetricFamily("amd_gpu_validator_step_seconds",
+                                 "wall time of each validator step (report = sum of the required steps)",
+                                 labels=["node", "step"])
         for step, v in vals.items():
             if isinstance(v, dict) and "passed" in v:
                 passed.add_metric([self.node, step], 1.0 if v["passed"] else 0.0)
+            if isinstance(v, dict):
+                d = v.get("chain_seconds") if step == "report" else v.get("duration_s")
+                if d is not None:
+                    secs.add_metric([self.node, step], float(d))
             if step == "gemm" and isinstance(v, dict):
                 for r in v.get("devices", []):
                     if r.get("tflops") is not None:
@@ -298,6 +305,7 @@ class GpuCollector:
         yield tflops
         yield tflops8
         yield busbw
+        yield secs
 
 
 def make_registry(collector: GpuCollector):

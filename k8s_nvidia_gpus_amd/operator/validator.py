@@ -300,7 +300,18 @@ class Validator:
                 self.kube.set_node_labels(self.node, {LABEL_VALIDATED: "true" if ok else "false"})
             except Exception as e:  # noqa: BLE001
                 log.warning("cannot label node: %s", e)
-        r = StepResult("report", ok, {"required": required, "missing": missing},
+        durations = {}
+        for st in required:
+            try:
+                with open(self._path(f"{st}.json")) as f:
+                    d = json.load(f).get("duration_s")
+            except (OSError, ValueError):
+                d = None
+            if d is not None:
+                durations[st] = d
+        r = StepResult("report", ok, {"required": required, "missing": missing,
+                                      "step_seconds": durations,
+                                      "chain_seconds": round(sum(durations.values()), 3)},
                        "" if ok else "failed/missing: " + ",".join(missing))
         if ok:
             with open(self._path("validator-ready"), "w") as f:
@@ -311,6 +322,15 @@ class Validator:
 
     # ---------------------------------------------------------------- driver
     def run_step(self, step: str) -> StepResult:
+        t0 = time.monotonic()
+        r = self._run_step(step)
+        # per-step wall time: the report sums them into the node's time-to-validated breakdown
+        r.detail.setdefault("duration_s", round(time.monotonic() - t0, 3))
+        self.write_result(r)
+        log.info("step %s: %s %s", step, "PASSED" if r.passed else "FAILED", r.reason)
+        return r
+
+    def _run_step(self, step: str) -> StepResult:
         if step == "driver":
             r = self.step_driver()
         elif step == "runtime":
@@ -336,6 +356,4 @@ class Validator:
             r = self.step_report()
         else:
             raise ValueError(f"unknown step {step!r}; steps: {STEPS}")
-        self.write_result(r)
-        log.info("step %s: %s %s", step, "PASSED" if r.passed else "FAILED", r.reason)
         return r

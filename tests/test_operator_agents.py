@@ -128,8 +128,10 @@ def test_exporter_amdsmi_backend_metrics(tmp_path):
     marker.mkdir()
     (marker / "gemm.json").write_text(json.dumps({"passed": True, "devices": [
         {"device": 0, "tflops": 1389.4}, {"device": 1, "tflops": 1380.0}],
-        "fp8": {"devices": [{"device": 0, "tflops": 2858.1}]}}))
+        "fp8": {"devices": [{"device": 0, "tflops": 2858.1}]}, "duration_s": 2.25}))
     (marker / "rccl.json").write_text(json.dumps({"passed": True, "ngpus": 8, "peak_busbw_gbps": 310.5}))
+    (marker / "report.json").write_text(json.dumps({"passed": True, "chain_seconds": 7.5,
+                                                    "duration_s": 0.01}))
     fake = FakeAmdSmi()
     col = ex.GpuCollector(ex.AmdSmiBackend(fake), "gpu-node-1", str(marker))
     text = _scrape(col)
@@ -149,6 +151,8 @@ def test_exporter_amdsmi_backend_metrics(tmp_path):
     assert _find(sm, "amd_gpu_validator_gemm_fp8_tflops", gpu=0) == [2858.1]
     assert _find(sm, "amd_gpu_validator_allreduce_busbw_gbps", ngpus=8) == [310.5]
     assert _find(sm, "amd_gpu_validation_passed", step="gemm") == [1.0]
+    assert _find(sm, "amd_gpu_validator_step_seconds", step="gemm") == [2.25]
+    assert _find(sm, "amd_gpu_validator_step_seconds", step="report") == [7.5]
     # N/A fields (edge temperature) are omitted, not exported as 0
     assert not _find(sm, "amd_gpu_temperature_celsius", sensor="edge")
 

@@ -69,6 +69,26 @@ def test_vectoradd_and_gemm_steps_on_real_outputs(tmp_path, cfg):
     assert r.calls[1][:3] == ["/x/amd-gemm-validator", "--size", "8192"]
 
 
+def test_report_carries_per_step_durations(tmp_path):
+    """Every step records its wall time; the report sums the required ones (time-to-validated)."""
+    cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {gemmMinTflops: 900, rccl: false, "
+                           "pluginTest: false}\n")
+    r = Runner({"amd-vectoradd": (0, VECTORADD_LOG), "amd-gemm-validator": (0, GEMM_LOG),
+                "amd-gemm-validator:fp8": (0, GEMM_FP8_LOG)})
+    v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=r)
+    for st in ("driver", "runtime"):  # markers as the driver/runtime agents publish them
+        (tmp_path / f"{st}.json").write_text(json.dumps({"step": st, "passed": True, "duration_s": 1.5}))
+        (tmp_path / f"{st}-ready").write_text("0\n")
+    assert v.run_step("vectoradd").detail["duration_s"] >= 0
+    assert v.run_step("gemm").passed
+    rep = v.run_step("report")
+    assert rep.passed
+    steps = rep.detail["step_seconds"]
+    assert set(steps) >= {"driver", "runtime", "vectoradd", "gemm"}
+    assert rep.detail["chain_seconds"] == pytest.approx(sum(steps.values()), abs=1e-3)
+    assert json.loads((tmp_path / "report.json").read_text())["chain_seconds"] >= 3.0
+
+
 def test_gemm_step_enforces_tflops_floor(tmp_path):
     cfg = load_config(text="validator: {gemmMinTflops: 2000}\n")
     v = Validator(cfg, str(tmp_path), bin_dir="/x",
