@@ -41,6 +41,7 @@ def main():
         arms = {
             "amdk8s w8": lambda: K.gemm_bf16_nt(a, b, out=c, variant="w8"),
             "amdk8s w4": lambda: K.gemm_bf16_nt(a, b, out=c, variant="w4"),
+            "amdk8s w4a": lambda: K.gemm_bf16_nt(a, b, out=c, variant="w4a"),
             "torch.matmul(hipBLASLt)": lambda: torch.matmul(a, b.t(), out=c),
         }
         for fn in arms.values():
@@ -55,7 +56,7 @@ def main():
             print(f"{s}^3 {k:28s} median {med:.4f} ms ({flop / med / 1e9:.1f} TFLOPS)  "
                   f"min {mn:.4f} ms ({flop / mn / 1e9:.1f} TFLOPS)")
         ref = torch.matmul(a, b.t())
-        for v in ("w8", "w4"):
+        for v in ("w8", "w4", "w4a"):
             K.gemm_bf16_nt(a, b, out=c, variant=v)
             err = (c.float() - ref.float()).abs().max().item()
             print(f"{s}^3 max |amdk8s {v} - hipBLASLt| = {err:.4e}")
