@@ -74,6 +74,72 @@ class PresenceHealth:
         return out
 
 
+class AmdSmiEccReader:
+    """``ecc_fn`` for :class:`PresenceHealth`: the uncorrectable-ECC count of a device's ASIC, read
+    through amd-smi (``amdsmi_get_gpu_total_ecc_count``, the same call the exporter samples).
+
+    Devices are matched to amd-smi processor handles by PCI BDF.  A compute partition that amd-smi
+    does not list under its own BDF falls back to the ASIC's other functions (same
+    domain:bus:device): ECC is an HBM property, shared by every partition of one MI355X, so the
+    highest count among them is the ASIC's.  The BDF → handle map is rebuilt on a miss, because a
+    partition change re-enumerates the handles."""
+
+    def __init__(self, amdsmi_module=None):
+        if amdsmi_module is None:
+            import amdsmi as amdsmi_module  # noqa: N813 - optional dependency
+        self.S = amdsmi_module
+        self.S.amdsmi_init()
+        self._by_bdf: Dict[str, object] = {}
+
+    def _rebuild(self) -> None:
+        self._by_bdf = {}
+        for h in self.S.amdsmi_get_processor_handles() or []:
+            try:
+                self._by_bdf[str(self.S.amdsmi_get_gpu_device_bdf(h)).lower()] = h
+            except Exception as e:  # noqa: BLE001 - a handle without a BDF cannot be matched
+                log.debug("amd-smi BDF read failed: %s", e)
+
+    def _handles(self, bdf: str) -> List[object]:
+        for attempt in (0, 1):
+            if bdf in self._by_bdf:
+                return [self._by_bdf[bdf]]
+            asic = bdf.rsplit(".", 1)[0]
+            same = [h for b, h in self._by_bdf.items() if b.rsplit(".", 1)[0] == asic]
+            if same:
+                return same
+            if attempt == 0:
+                self._rebuild()
+        raise LookupError(f"no amd-smi handle for {bdf}")
+
+    def __call__(self, d: topo_mod.GpuDevice) -> int:
+        counts = []
+        for h in self._handles(d.pci_bdf.lower()):
+            ecc = self.S.amdsmi_get_gpu_total_ecc_count(h) or {}
+            counts.append(int(ecc.get("uncorrectable_count") or 0))
+        return max(counts)
+
+    def close(self) -> None:
+        try:
+            self.S.amdsmi_shut_down()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def default_ecc_fn(threshold: int) -> Optional[Callable]:
+    """The production ECC criterion: amd-smi backed when the threshold is enabled, else None.
+
+    Without amd-smi (no library, no device access) the plugin still runs on presence alone and
+    says so, instead of silently ignoring ``health.eccUncorrectableThreshold``."""
+    if threshold <= 0:
+        return None
+    try:
+        return AmdSmiEccReader()
+    except Exception as e:  # noqa: BLE001 - no amd-smi in this image / no device access
+        log.warning("amd-smi unavailable (%s): the uncorrectable-ECC health check "
+                    "(threshold %d) is disabled, presence checks only", e, threshold)
+        return None
+
+
 def preferred_allocation(available: Sequence[topo_mod.GpuDevice],
                          must_include: Sequence[topo_mod.GpuDevice], size: int) -> List[topo_mod.GpuDevice]:
     """Pick ``size`` devices: must_include first, then pack by ASIC, then NUMA node (best fit)."""
@@ -121,21 +187,25 @@ class AmdGpuDevicePlugin:
                  kubelet_dir: str = api.DEVICE_PLUGIN_PATH, socket_name: str = "amd-gpu.sock",
                  topology_fn: Optional[Callable[[], topo_mod.NodeTopology]] = None,
                  health_fn: Optional[HealthFn] = None, pause_marker: Optional[str] = PAUSE_MARKER,
-                 dev_prefix: str = "/dev"):
+                 dev_prefix: str = "/dev", ecc_fn: Optional[Callable] = None):
         self.config = config
         self.root = root
         self.kubelet_dir = kubelet_dir
         self.socket_path = os.path.join(kubelet_dir, socket_name)
         self.kubelet_socket = os.path.join(kubelet_dir, api.KUBELET_SOCKET)
         self.topology_fn = topology_fn or (lambda: topo_mod.read_topology(root, config.min_gfx))
-        self.health_fn = health_fn or PresenceHealth(
-            root, ecc_threshold=int(config.section("health")["eccUncorrectableThreshold"]))
+        if health_fn is None:
+            threshold = int(config.section("health")["eccUncorrectableThreshold"])
+            health_fn = PresenceHealth(root, ecc_fn=ecc_fn or default_ecc_fn(threshold),
+                                       ecc_threshold=threshold)
+        self.health_fn = health_fn
         self.pause_marker = pause_marker
         self.dev_prefix = dev_prefix
         self._cond = threading.Condition()
         self._version = 0
         self._devices: List[topo_mod.GpuDevice] = []
         self._health: Dict[str, str] = {}
+        self._index: Dict[str, int] = {}   # device_uid -> stable index (deviceIdStrategy: index)
         self._paused = False
         self._server = None
         self._stop = threading.Event()
@@ -143,11 +213,19 @@ class AmdGpuDevicePlugin:
         self.refresh()
 
     # ------------------------------------------------------------------ state
-    def _id(self, d: topo_mod.GpuDevice, i: int) -> str:
-        return str(i) if self.config["deviceIdStrategy"] == "index" else d.device_uid
+    def _id(self, d: topo_mod.GpuDevice) -> str:
+        """Kubelet-facing ID.  With ``deviceIdStrategy: index`` a device keeps the index it got when
+        first seen, for the plugin's lifetime: kubelet checkpoints allocated IDs, so an index must
+        never move to another physical GPU when an earlier one disappears."""
+        if self.config["deviceIdStrategy"] != "index":
+            return d.device_uid
+        idx = self._index.get(d.device_uid)
+        if idx is None:
+            idx = self._index[d.device_uid] = len(self._index)
+        return str(idx)
 
     def _id_map(self) -> Dict[str, topo_mod.GpuDevice]:
-        return {self._id(d, i): d for i, d in enumerate(self._devices)}
+        return {self._id(d): d for d in self._devices}
 
     def refresh(self) -> bool:
         """Re-enumerate + re-check health; returns True (and wakes ListAndWatch) on any change."""
@@ -174,6 +252,8 @@ class AmdGpuDevicePlugin:
                        or [d.device_uid for d in merged] != [d.device_uid for d in self._devices])
             if changed:
                 self._devices, self._health, self._paused = merged, health, paused
+                for d in merged:   # assign indices in enumeration order, once
+                    self._id(d)
                 self._version += 1
                 self._cond.notify_all()
         if changed:
@@ -184,8 +264,8 @@ class AmdGpuDevicePlugin:
     def list_response(self):
         resp = api.ListAndWatchResponse()
         with self._cond:
-            for i, d in enumerate(self._devices):
-                dev = resp.devices.add(ID=self._id(d, i), health=self._health.get(d.device_uid, api.UNHEALTHY))
+            for d in self._devices:
+                dev = resp.devices.add(ID=self._id(d), health=self._health.get(d.device_uid, api.UNHEALTHY))
                 if d.numa_node >= 0:
                     dev.topology.nodes.add(ID=d.numa_node)
         return resp

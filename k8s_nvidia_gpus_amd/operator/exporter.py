@@ -289,7 +289,9 @@ class GpuCollector:
             if isinstance(v, dict) and "passed" in v:
                 passed.add_metric([self.node, step], 1.0 if v["passed"] else 0.0)
             if isinstance(v, dict):
-                d = v.get("chain_seconds") if step == "report" else v.get("duration_s")
+                # an incomplete chain (some required step untimed) is not a time-to-validated
+                d = ((v.get("chain_seconds") if v.get("chain_complete", True) else None)
+                     if step == "report" else v.get("duration_s"))
                 if d is not None:
                     secs.add_metric([self.node, step], float(d))
             if step == "gemm" and isinstance(v, dict):

@@ -301,6 +301,7 @@ class Validator:
             except Exception as e:  # noqa: BLE001
                 log.warning("cannot label node: %s", e)
         durations = {}
+        no_duration = []
         for st in required:
             try:
                 with open(self._path(f"{st}.json")) as f:
@@ -309,9 +310,15 @@ class Validator:
                 d = None
             if d is not None:
                 durations[st] = d
+            else:
+                no_duration.append(st)
+        # chain_seconds is only a complete time-to-validated when every required step is timed;
+        # the untimed ones are listed instead of being silently counted as zero
         r = StepResult("report", ok, {"required": required, "missing": missing,
                                       "step_seconds": durations,
-                                      "chain_seconds": round(sum(durations.values()), 3)},
+                                      "step_seconds_missing": no_duration,
+                                      "chain_seconds": round(sum(durations.values()), 3),
+                                      "chain_complete": not no_duration},
                        "" if ok else "failed/missing: " + ",".join(missing))
         if ok:
             with open(self._path("validator-ready"), "w") as f:
@@ -322,8 +329,18 @@ class Validator:
 
     # ---------------------------------------------------------------- driver
     def run_step(self, step: str) -> StepResult:
+        """Run one step and ALWAYS record its outcome.  A step that raises (a validation pod that
+        never leaves Pending, an API error, a missing binary) is a failed step: its ``-ready``
+        marker is withdrawn and ``<step>.json`` says why, so neither a stale pass nor a stale
+        node label can survive on the hostPath marker dir."""
+        if step not in STEPS:
+            raise ValueError(f"unknown step {step!r}; steps: {STEPS}")
         t0 = time.monotonic()
-        r = self._run_step(step)
+        try:
+            r = self._run_step(step)
+        except Exception as e:  # noqa: BLE001 - any escape would leave the old markers in place
+            log.exception("step %s raised", step)
+            r = StepResult(step, False, {"exception": type(e).__name__}, repr(e)[:500])
         # per-step wall time: the report sums them into the node's time-to-validated breakdown
         r.detail.setdefault("duration_s", round(time.monotonic() - t0, 3))
         self.write_result(r)

@@ -107,6 +107,25 @@ def test_index_id_strategy(node, sockdir):
     assert [d.ID for d in p.list_response().devices] == [str(i) for i in range(8)]
 
 
+def test_index_ids_stay_with_their_gpu_when_one_disappears(tmp_path, sockdir):
+    """an index already handed to kubelet must keep naming the same physical GPU."""
+    root = fake_sysfs.build_node(tmp_path / "r")
+    p = make_plugin(root, sockdir, "deviceIdStrategy: index")
+    before = {i: d.device_uid for i, d in p._id_map().items()}
+    victim = before["0"]
+    bdfs = [g["bdf"] for g in fake_sysfs.LAYOUT["gpus"]]
+    gpu = next(g for g in read_topology(str(root), 90500).gpus if g.device_uid == victim)
+    fake_sysfs.remove_gpu(root, bdfs.index(gpu.pci_bdf))
+    assert p.refresh() is True
+    after = {i: d.device_uid for i, d in p._id_map().items()}
+    assert after == before
+    health = {d.ID: d.health for d in p.list_response().devices}
+    assert health["0"] == api.UNHEALTHY and list(health.values()).count(api.HEALTHY) == 7
+    # allocation by index still resolves to the same render node as before the removal
+    resp = p.container_response(["5"])
+    assert resp.annotations[ANNOT_DEVICE_IDS] == before["5"]
+
+
 def _pref(p, avail, must, size):
     req = api.PreferredAllocationRequest()
     req.container_requests.add(available_deviceIDs=avail, must_include_deviceIDs=must, allocation_size=size)
@@ -164,6 +183,37 @@ def test_health_ecc_threshold(node, sockdir):
     p = make_plugin(node, sockdir, health_fn=health)
     h = {d.ID: d.health for d in p.list_response().devices}
     assert h[bad] == api.UNHEALTHY and list(h.values()).count(api.HEALTHY) == 7
+
+
+def test_ecc_threshold_active_when_built_like_main(node, sockdir, monkeypatch):
+    """the plugin as main() builds it (no health_fn) must apply
+    health.eccUncorrectableThreshold through amd-smi, not only when a test injects an ecc_fn."""
+    import sys
+
+    from fakes.amdsmi import FakeAmdSmi
+
+    smi = FakeAmdSmi()
+    monkeypatch.setitem(sys.modules, "amdsmi", smi)
+    p = make_plugin(node, sockdir, "health:\n  eccUncorrectableThreshold: 2\n")
+    assert all(d.health == api.HEALTHY for d in p.list_response().devices)
+    smi.ecc_uncorrectable[3] = 1            # below the threshold: still healthy
+    assert p.refresh() is False
+    smi.ecc_uncorrectable[3] = 2            # reaches it: that GPU (and only it) goes Unhealthy
+    assert p.refresh() is True
+    bdf3 = smi.amdsmi_get_gpu_device_bdf(3)
+    bad = next(g.device_uid for g in read_topology(str(node), 90500).gpus if g.pci_bdf == bdf3)
+    h = {d.ID: d.health for d in p.list_response().devices}
+    assert h[bad] == api.UNHEALTHY and list(h.values()).count(api.HEALTHY) == 7
+
+
+def test_ecc_disabled_without_amdsmi_is_logged(node, sockdir, monkeypatch, caplog):
+    import sys
+
+    monkeypatch.setitem(sys.modules, "amdsmi", None)   # import fails like on a node without it
+    with caplog.at_level("WARNING", logger="amd-device-plugin"):
+        p = make_plugin(node, sockdir)
+    assert p.health_fn.ecc_fn is None
+    assert any("uncorrectable-ECC health check" in r.getMessage() for r in caplog.records)
 
 
 def test_pause_marker_hides_devices(node, sockdir):

@@ -157,6 +157,18 @@ def test_exporter_amdsmi_backend_metrics(tmp_path):
     assert not _find(sm, "amd_gpu_temperature_celsius", sensor="edge")
 
 
+def test_exporter_omits_incomplete_validation_chain_time(tmp_path):
+    marker = tmp_path / "v"
+    marker.mkdir()
+    (marker / "report.json").write_text(json.dumps({"passed": True, "chain_seconds": 1.2,
+                                                    "chain_complete": False,
+                                                    "step_seconds_missing": ["runtime"]}))
+    col = ex.GpuCollector(ex.AmdSmiBackend(FakeAmdSmi()), "n", str(marker))
+    sm = _samples(_scrape(col))
+    assert not _find(sm, "amd_gpu_validator_step_seconds", step="report")
+    assert _find(sm, "amd_gpu_validation_passed", step="report") == [1.0]
+
+
 def test_exporter_survives_unsupported_calls():
     fake = FakeAmdSmi(n_gpus=2, fail={"amdsmi_get_gpu_metrics_info", "amdsmi_get_gpu_total_ecc_count"})
     text = _scrape(ex.GpuCollector(ex.AmdSmiBackend(fake), "n", "/nonexistent"))

@@ -226,3 +226,69 @@ def test_gemm_step_fp8_can_be_disabled(tmp_path):
     v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=r)
     assert v.run_step("gemm").passed
     assert len(r.calls) == 1 and "fp8" not in json.loads((tmp_path / "gemm.json").read_text())
+
+
+class _PendingKube:
+    """A kube client whose validation pod never leaves Pending (0 devices advertised)."""
+
+    def __init__(self):
+        self.deleted = []
+
+    def get_pod(self, ns, name):
+        return {"spec": {"containers": [{"image": "img:1"}]}}
+
+    def delete_pod(self, ns, name):
+        self.deleted.append(name)
+
+    def create_pod(self, ns, pod):
+        pass
+
+    def wait_pod_phase(self, ns, name, timeout=600.0, **kw):
+        raise TimeoutError(f"pod {ns}/{name} not in ('Succeeded', 'Failed') (phase Pending)")
+
+    def pod_logs(self, ns, name):
+        return ""
+
+    def set_node_labels(self, node, labels):
+        self.labels = labels
+
+
+def test_step_that_raises_is_recorded_as_failed_and_withdraws_markers(tmp_path, cfg):
+    """a plugin pod stuck in Pending used to escape run_step, leaving the previous
+    plugin.json / plugin-ready (hostPath, survives restarts) and the node label untouched."""
+    kube = _PendingKube()
+    v = Validator(cfg, str(tmp_path), kube=kube, node_name="gpu-node-1")
+    (tmp_path / "plugin-ready").write_text("stale\n")
+    (tmp_path / "plugin.json").write_text(json.dumps({"step": "plugin", "passed": True}))
+    r = v.run_step("plugin")
+    assert not r.passed and "TimeoutError" in r.reason
+    assert not (tmp_path / "plugin-ready").exists()
+    rec = json.loads((tmp_path / "plugin.json").read_text())
+    assert rec["passed"] is False and rec["exception"] == "TimeoutError" and "duration_s" in rec
+    assert kube.deleted  # the pod was still cleaned up
+    # the report then fails the node instead of keeping the old pass
+    for s in ("driver", "runtime", "vectoradd", "gemm", "rccl"):
+        (tmp_path / f"{s}-ready").write_text("1")
+    rep = v.run_step("report")
+    assert not rep.passed and "plugin" in rep.detail["missing"]
+    assert kube.labels == {"amd.com/gpu.validated": "false"}
+
+
+def test_unknown_step_still_raises(tmp_path, cfg):
+    with pytest.raises(ValueError):
+        Validator(cfg, str(tmp_path)).run_step("nope")
+
+
+def test_report_lists_required_steps_without_duration(tmp_path):
+    """chain_seconds must not silently treat an untimed required step as 0 s."""
+    cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {rccl: false, pluginTest: false, "
+                           "gemm: false, vectorAdd: false}\n")
+    v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=Runner({}))
+    (tmp_path / "driver.json").write_text(json.dumps({"step": "driver", "passed": True, "duration_s": 2.0}))
+    for st in ("driver", "runtime"):
+        (tmp_path / f"{st}-ready").write_text("0\n")   # runtime marker without runtime.json timing
+    rep = v.run_step("report")
+    assert rep.passed
+    assert rep.detail["step_seconds"] == {"driver": 2.0}
+    assert rep.detail["step_seconds_missing"] == ["runtime"]
+    assert rep.detail["chain_complete"] is False

@@ -57,9 +57,13 @@ def main():
                   f"min {mn:.4f} ms ({flop / mn / 1e9:.1f} TFLOPS)")
         ref = torch.matmul(a, b.t())
         for v in ("w8", "w4", "w4a"):
-            K.gemm_bf16_nt(a, b, out=c, variant=v)
-            err = (c.float() - ref.float()).abs().max().item()
-            print(f"{s}^3 max |amdk8s {v} - hipBLASLt| = {err:.4e}")
+            # a fresh NaN-filled output per variant: a kernel that skipped any element of C shows
+            # up as NaN instead of inheriting the previous arm's (hipBLASLt's) result
+            out = torch.full((s, s), float("nan"), dtype=torch.bfloat16, device=dev)
+            K.gemm_bf16_nt(a, b, out=out, variant=v)
+            unwritten = int(torch.isnan(out).sum().item())
+            err = (out.float() - ref.float()).abs().max().item()
+            print(f"{s}^3 max |amdk8s {v} - hipBLASLt| = {err:.4e}  (NaN/unwritten: {unwritten})")
         sys.stdout.flush()
 
 
