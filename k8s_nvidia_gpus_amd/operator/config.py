@@ -50,6 +50,10 @@ DEFAULTS: Dict[str, Any] = {
         "gemmFp8": True,             # also run the fp8 (OCP e4m3) MFMA GEMM
         "gemmFp8MinTflops": 1800,
         "rocprof": False,            # run the GEMM step under rocprofv3 --kernel-trace --stats
+        "bandwidth": True,           # amd-proftester: HBM copy, PCIe H2D/D2H, xGMI peer copies
+        "hbmMinGBps": 4000,          # HBM3E copy (read + write bytes), per GPU
+        "pcieMinGBps": 20,           # pinned host <-> device, each direction, per GPU
+        "xgmiMinGBps": 30,           # each ordered GPU pair, SDMA peer copy (>= 2 GPUs)
         "rccl": True,
         "rcclMinBusbwGBps": 100,
         "pluginTest": True,

@@ -282,6 +282,9 @@ class GpuCollector:
         busbw = GaugeMetricFamily("amd_gpu_validator_allreduce_busbw_gbps",
                                   "RCCL all-reduce bus bandwidth measured by the validator",
                                   labels=["node", "ngpus"])
+        bw = GaugeMetricFamily("amd_gpu_validator_bandwidth_gbps",
+                               "HBM / PCIe / xGMI bandwidth measured by the validator (amd-proftester)",
+                               labels=["node", "gpu", "test", "peer", "engine"])
         secs = GaugeMetricFamily("amd_gpu_validator_step_seconds",
                                  "wall time of each validator step (report = sum of the required steps)",
                                  labels=["node", "step"])
@@ -303,10 +306,19 @@ class GpuCollector:
                         tflops8.add_metric([self.node, str(r.get("device"))], float(r["tflops"]))
             if step == "rccl" and isinstance(v, dict) and v.get("peak_busbw_gbps") is not None:
                 busbw.add_metric([self.node, str(v.get("ngpus"))], float(v["peak_busbw_gbps"]))
+            if step == "bandwidth" and isinstance(v, dict):
+                for r in v.get("results", []):
+                    if r.get("skipped") or r.get("value") is None:
+                        continue
+                    peer = r.get("peer", -1)
+                    bw.add_metric([self.node, str(r.get("device")), str(r.get("test")),
+                                   "" if peer is None or peer < 0 else str(peer), str(r.get("engine") or "")],
+                                  float(r["value"]))
         yield passed
         yield tflops
         yield tflops8
         yield busbw
+        yield bw
         yield secs
 
 

@@ -11,6 +11,8 @@ the previous one's marker under ``/run/amd/validations``:
   vectoradd hand-written HIP vectorAdd on every GPU, reference stdout protocol
   gemm      hand-written gfx950 bf16 (and fp8 e4m3) MFMA GEMMs on every GPU: numerics vs fp32 +
             TFLOPS ≥ floor per precision
+  bandwidth amd-proftester (the dcgmproftester counterpart): HBM3E copy, PCIe H2D / D2H and, with
+            ≥ 2 GPUs, every xGMI peer pair — verified copies, GB/s ≥ floor per link type
   rccl      RCCL all-reduce over xGMI across all GPUs of the node: exact sums + bus bandwidth floor
   plugin    a pod requesting amd.com/gpu: 1 is scheduled THROUGH the device plugin and passes
   report    node label amd.com/gpu.validated=true|false, validator-ready marker
@@ -35,7 +37,7 @@ from .config import OperatorConfig
 
 log = logging.getLogger("amd-gpu-validator")
 
-STEPS = ("driver", "runtime", "vectoradd", "gemm", "rccl", "plugin", "report")
+STEPS = ("driver", "runtime", "vectoradd", "gemm", "bandwidth", "rccl", "plugin", "report")
 LABEL_VALIDATED = "amd.com/gpu.validated"
 
 Runner = Callable[[Sequence[str], float], Tuple[int, str]]
@@ -222,6 +224,37 @@ class Validator:
             reason = "; ".join(r for r in (reason, reason8) if r)
         return StepResult("gemm", bool(ok), detail, reason)
 
+    def step_bandwidth(self) -> StepResult:
+        floors = {"hbm-copy": float(self.vcfg["hbmMinGBps"]), "pcie-h2d": float(self.vcfg["pcieMinGBps"]),
+                  "pcie-d2h": float(self.vcfg["pcieMinGBps"]), "xgmi": float(self.vcfg["xgmiMinGBps"])}
+        rc, out = self.run_cmd([self._bin("amd-proftester"), "-t", ",".join(floors), "--json"], 900)
+        docs = [d for d in json_lines(out) if d.get("check") == "proftester" and d.get("test") in floors]
+        # pairs: SDMA copies are gated; the copy-kernel pulls and the all-peer aggregate are reported
+        gated = [d for d in docs if not d.get("skipped")
+                 and (d.get("test") != "xgmi" or d.get("engine") == "sdma")]
+        slow = [d for d in gated if float(d.get("value", 0)) < floors[d["test"]]]
+        bad = [d for d in docs if not d.get("passed")]
+        seen = {d.get("test") for d in docs}
+        missing = [t for t in ("hbm-copy", "pcie-h2d", "pcie-d2h") if t not in seen]
+        ok = rc == 0 and protocol_passed(out) and not slow and not bad and not missing
+        summary: Dict[str, float] = {}
+        for d in docs:
+            if d.get("skipped"):
+                continue
+            key = d["test"] if d["test"] != "xgmi" else f"xgmi-{d.get('engine')}"
+            summary[key] = round(min(summary.get(key, float("inf")), float(d.get("value", 0))), 1)
+        reason = ""
+        if not ok:
+            reason = "; ".join(filter(None, [
+                f"{len(bad)} check(s) failed" if bad else "",
+                ", ".join(f"{d['test']} dev {d['device']}"
+                          + (f"<-{d['peer']}" if d.get("peer", -1) >= 0 else "")
+                          + f" {d['value']:.1f} < {floors[d['test']]}" for d in slow),
+                f"no result for {','.join(missing)}" if missing else "",
+                f"rc={rc}" if rc else ""]))
+        return StepResult("bandwidth", bool(ok), {"results": docs, "min_by_test_gbps": summary,
+                                                  "floors_gbps": floors}, reason)
+
     def step_rccl(self, ngpus: Optional[int] = None) -> StepResult:
         if ngpus is not None and ngpus < 2:
             return StepResult("rccl", True, {"ngpus": ngpus, "skipped": "single GPU"})
@@ -289,6 +322,8 @@ class Validator:
             required.append("vectoradd")
         if self.vcfg["gemm"]:
             required.append("gemm")
+        if self.vcfg["bandwidth"]:
+            required.append("bandwidth")
         if self.vcfg["rccl"]:
             required.append("rccl")
         if self.vcfg["pluginTest"]:
@@ -356,6 +391,8 @@ class Validator:
             r = self.step_vectoradd() if self.vcfg["vectorAdd"] else StepResult("vectoradd", True, {"skipped": True})
         elif step == "gemm":
             r = self.step_gemm() if self.vcfg["gemm"] else StepResult("gemm", True, {"skipped": True})
+        elif step == "bandwidth":
+            r = self.step_bandwidth() if self.vcfg["bandwidth"] else StepResult("bandwidth", True, {"skipped": True})
         elif step == "rccl":
             if not self.vcfg["rccl"]:
                 r = StepResult("rccl", True, {"skipped": True})

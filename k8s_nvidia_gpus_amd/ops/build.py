@@ -8,6 +8,7 @@ Two kinds of output, both built IN-TREE so they travel with the repository snaps
   ``libamdhip64.so.7`` already loaded by torch satisfies the library's dependency).
 * ``native/bin/*`` — standalone executables used by the operator DaemonSets / validator pods:
   ``amd-vectoradd`` (reference-compatible stdout protocol), ``amd-gemm-validator``,
+  ``amd-proftester`` (per-pipe load generator: tensor / HBM / fp32 / fp64 / PCIe / xGMI),
   ``rccl-allreduce-bench``, ``kfd-probe`` and the containerd OCI hook ``amd-oci-hook``.
 
 The reference has no in-tree native code at all (its GPU code lives in pulled images
@@ -75,6 +76,12 @@ NATIVE_TARGETS: List[NativeTarget] = [
                                         "k8s_nvidia_gpus_amd/ops/csrc/gemm_fp8_gfx950.hip",
                                         "k8s_nvidia_gpus_amd/ops/csrc/gemm_fp8_gfx950_f8a.hip",
                                         "k8s_nvidia_gpus_amd/ops/csrc/fill.hip"], "hipcc"),
+    NativeTarget("amd-proftester", ["native/src/amd_proftester.hip",
+                                    "k8s_nvidia_gpus_amd/ops/csrc/loadgen.hip",
+                                    "k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950_w4a.hip",
+                                    "k8s_nvidia_gpus_amd/ops/csrc/gemm_fp8_gfx950_f8a.hip",
+                                    "k8s_nvidia_gpus_amd/ops/csrc/fill.hip"], "hipcc",
+                 libs=["-lpthread"]),
     NativeTarget("rccl-allreduce-bench", ["native/src/rccl_allreduce_bench.hip"], "hipcc",
                  libs=["-lrccl", "-lpthread"]),
     NativeTarget("kfd-probe", ["native/src/kfd_probe.cpp", "native/src/kfd_topology.cpp"], "cxx"),

@@ -32,6 +32,9 @@ __all__ = [
     "vector_add_bandwidth",
     "fill_uniform_bf16",
     "gemm_sample_check",
+    "hbm_stream",
+    "fp32_fma",
+    "fp64_mfma",
 ]
 
 GEMM_TILE_M = 256
@@ -75,6 +78,18 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.amdk8s_fill_uniform_bf16.restype = ci
     lib.amdk8s_fill_uniform_fp8.argtypes = [vp, cl, cu64, cf, cf, vp]
     lib.amdk8s_fill_uniform_fp8.restype = ci
+    lib.amdk8s_hbm_stream.argtypes = [ci, vp, vp, cl, ci, ci, vp, vp]
+    lib.amdk8s_hbm_stream.restype = ci
+    lib.amdk8s_hbm_stream_variant.argtypes = [ci, vp, vp, cl, ci, ci, ci, ci, ci, ci, vp, vp]
+    lib.amdk8s_hbm_stream_variant.restype = ci
+    lib.amdk8s_fp32_fma.argtypes = [ci, ci, vp, vp]
+    lib.amdk8s_fp32_fma.restype = ci
+    lib.amdk8s_fp32_fma_flop.argtypes = [ci, ci]
+    lib.amdk8s_fp32_fma_flop.restype = ctypes.c_double
+    lib.amdk8s_fp64_mfma.argtypes = [ci, ci, vp, vp]
+    lib.amdk8s_fp64_mfma.restype = ci
+    lib.amdk8s_fp64_mfma_flop.argtypes = [ci, ci]
+    lib.amdk8s_fp64_mfma_flop.restype = ctypes.c_double
 
 
 def library(build_if_missing: bool = True) -> ctypes.CDLL:
@@ -317,3 +332,73 @@ def fill_uniform_bf16(t: torch.Tensor, seed: int, lo: float = -1.0, hi: float = 
                                             _stream_handle(t.device))
     _check(rc, "amdk8s_fill_uniform_bf16")
     return t
+
+
+# ------------------------------------------------------------------------------------------------
+# Load generators (csrc/loadgen.hip): the HBM / fp32 / fp64 targets of native/bin/amd-proftester.
+# ------------------------------------------------------------------------------------------------
+HBM_MODES = {"read": 0, "write": 1, "copy": 2}
+_SINKS: dict = {}
+
+
+def _sink(device: torch.device) -> torch.Tensor:
+    key = (device.type, device.index)
+    if key not in _SINKS:
+        _SINKS[key] = torch.zeros(16, dtype=torch.int32, device=device)
+    return _SINKS[key]
+
+
+def hbm_stream(mode: str, src: Optional[torch.Tensor], dst: Optional[torch.Tensor],
+               nbytes: Optional[int] = None, blocks_per_cu: int = 0,
+               variant: Optional[tuple] = None) -> int:
+    """Stream ``nbytes`` through HBM: ``mode`` = read (``src``), write (``dst``) or copy
+    (``src`` → ``dst``).  Returns the bytes moved (2× for copy).  ``variant`` = (nt_load, nt_store,
+    unroll) overrides the built-in policy for sweeps (tools/hbm_sweep.py)."""
+    if mode not in HBM_MODES:
+        raise ValueError(f"mode must be one of {tuple(HBM_MODES)}")
+    ref = src if src is not None else dst
+    if ref is None:
+        raise ValueError("need a buffer")
+    _require_gpu(ref, "buffer")
+    m = HBM_MODES[mode]
+    if m != 1 and (src is None or not src.is_contiguous()):
+        raise ValueError("read/copy need a contiguous src")
+    if m != 0 and (dst is None or not dst.is_contiguous()):
+        raise ValueError("write/copy need a contiguous dst")
+    avail = min(t.numel() * t.element_size() for t in (src, dst) if t is not None)
+    nbytes = avail if nbytes is None else nbytes
+    if nbytes > avail or nbytes % 16:
+        raise ValueError(f"nbytes {nbytes} must be a multiple of 16 and fit the buffers ({avail})")
+    cus = torch.cuda.get_device_properties(ref.device).multi_processor_count
+    lib = library()
+    sp = src.data_ptr() if src is not None else None
+    dp = dst.data_ptr() if dst is not None else None
+    sink = _sink(ref.device).data_ptr()
+    if variant is None:
+        rc = lib.amdk8s_hbm_stream(m, sp, dp, nbytes, cus, blocks_per_cu, sink, _stream_handle(ref.device))
+    else:
+        ntl, nts, unroll, chunked = (tuple(variant) + (0,))[:4]
+        rc = lib.amdk8s_hbm_stream_variant(m, sp, dp, nbytes, cus, blocks_per_cu or 8, int(ntl), int(nts),
+                                           int(unroll), int(chunked), sink, _stream_handle(ref.device))
+    _check(rc, f"amdk8s_hbm_stream[{mode}]")
+    return 2 * nbytes if m == 2 else nbytes
+
+
+def fp32_fma(device: torch.device, iters: int = 20000, blocks_per_cu: int = 8) -> float:
+    """One launch of the v_pk_fma_f32 load; returns the FLOP it executes."""
+    cus = torch.cuda.get_device_properties(device).multi_processor_count
+    lib = library()
+    blocks = cus * blocks_per_cu
+    _check(lib.amdk8s_fp32_fma(blocks, iters, _sink(device).data_ptr(), _stream_handle(device)),
+           "amdk8s_fp32_fma")
+    return lib.amdk8s_fp32_fma_flop(blocks, iters)
+
+
+def fp64_mfma(device: torch.device, iters: int = 3000, blocks_per_cu: int = 8) -> float:
+    """One launch of the v_mfma_f64_16x16x4_f64 load; returns the FLOP it executes."""
+    cus = torch.cuda.get_device_properties(device).multi_processor_count
+    lib = library()
+    blocks = cus * blocks_per_cu
+    _check(lib.amdk8s_fp64_mfma(blocks, iters, _sink(device).data_ptr(), _stream_handle(device)),
+           "amdk8s_fp64_mfma")
+    return lib.amdk8s_fp64_mfma_flop(blocks, iters)

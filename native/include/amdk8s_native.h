@@ -38,6 +38,13 @@ int amdk8s_vector_add_f32(const float* a, const float* b, float* c, int n, hipSt
 int amdk8s_vector_add_f32_bw(const float* a, const float* b, float* c, long n, int num_cus,
                              hipStream_t stream);
 int amdk8s_vector_add_blocks(int n);
+// k8s_nvidia_gpus_amd/ops/csrc/loadgen.hip
+int amdk8s_hbm_stream(int mode, const void* src, void* dst, long bytes, int num_cus,
+                      int blocks_per_cu, uint32_t* sink, hipStream_t stream);
+int amdk8s_fp32_fma(int blocks, int iters, float* sink, hipStream_t stream);
+double amdk8s_fp32_fma_flop(int blocks, int iters);
+int amdk8s_fp64_mfma(int blocks, int iters, double* sink, hipStream_t stream);
+double amdk8s_fp64_mfma_flop(int blocks, int iters);
 // k8s_nvidia_gpus_amd/ops/csrc/fill.hip
 int amdk8s_fill_uniform_bf16(void* dst, long n, unsigned long long seed, float lo, float hi,
                              hipStream_t stream);

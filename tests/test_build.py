@@ -25,7 +25,8 @@ def _nm(path):
 def test_kernel_library_exports(built):
     syms = _nm(B.KERNEL_LIB)
     for s in ["amdk8s_gemm_bf16_nt", "amdk8s_gemm_bf16_nt_sample_check", "amdk8s_vector_add_f32",
-              "amdk8s_vector_add_f32_bw", "amdk8s_fill_uniform_bf16", "amdk8s_vector_add_blocks"]:
+              "amdk8s_vector_add_f32_bw", "amdk8s_fill_uniform_bf16", "amdk8s_vector_add_blocks",
+              "amdk8s_hbm_stream", "amdk8s_hbm_stream_variant", "amdk8s_fp32_fma", "amdk8s_fp64_mfma"]:
         assert s in syms, s
 
 
@@ -72,3 +73,26 @@ def test_kfd_probe_reports_missing_topology(built, tmp_path):
                         "--dev-root", str(tmp_path)], capture_output=True, text=True)
     assert r.returncode == 1
     assert "not ready" in r.stderr
+
+
+def test_proftester_lists_tests_and_rejects_unknown_without_a_gpu(built):
+    exe = str(B.NATIVE_BIN / "amd-proftester")
+    p = subprocess.run([exe, "--list"], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0
+    assert p.stdout.split() == ["tensor", "tensor-fp8", "hbm-read", "hbm-write", "hbm-copy", "fp32",
+                                "fp64", "pcie-h2d", "pcie-d2h", "xgmi"]
+    p = subprocess.run([exe, "-t", "hbm-copy,bogus"], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 2 and "unknown test 'bogus'" in p.stderr
+
+
+def test_loadgen_kernels_use_the_intended_instructions(tmp_path):
+    """The fp32 load must be v_pk_fma_f32 (the 157 TF vector path), the fp64 load the f64 MFMA,
+    and the streaming kernels 16-B-per-lane accesses, non-temporal where the policy says so."""
+    src = B.CSRC_DIR / "loadgen.hip"
+    subprocess.run([B.HIPCC, *B.HIP_FLAGS, "--save-temps", "-c", str(src), "-o", str(tmp_path / "l.o")],
+                   cwd=tmp_path, check=True, capture_output=True)
+    (asm,) = tmp_path.glob("*gfx950*.s")
+    text = asm.read_text()
+    assert text.count("v_pk_fma_f32") >= 32 and text.count("v_mfma_f64_16x16x4") >= 16
+    assert "global_load_dwordx4" in text and "global_store_dwordx4" in text
+    assert " nt" in text and "scratch_" not in text

@@ -261,3 +261,80 @@ def test_fill_uniform_fp8_is_ocp_e4m3(K, dev):
     assert abs(f.mean().item()) < 0.01 and 0.5 < f.std().item() < 0.65
     assert torch.equal(f.to(K.FP8_DTYPE).float(), f)  # every value is an e4m3 value
     assert len(torch.unique(f)) > 100
+
+
+# ----------------------------------------------------------------------------- load generators
+def test_hbm_copy_is_exact_and_read_write_run(K, dev):
+    n = (256 << 20) // 4 + 12  # 256 MiB + a 48-B tail past the unrolled body
+    src = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device=dev)
+    dst = torch.zeros_like(src)
+    assert K.hbm_stream("copy", src, dst) == 2 * n * 4
+    torch.cuda.synchronize()
+    assert torch.equal(dst, src)
+    for variant in [(0, 0, 1, 0), (1, 1, 8, 1), (1, 0, 2, 1), (0, 1, 4, 0)]:
+        dst.zero_()
+        K.hbm_stream("copy", src, dst, variant=variant)
+        torch.cuda.synchronize()
+        assert torch.equal(dst, src), variant
+    w = torch.zeros_like(src)
+    K.hbm_stream("write", None, w)
+    torch.cuda.synchronize()
+    assert (w != 0).float().mean().item() > 0.99  # the toggling pattern, never zeros
+    K.hbm_stream("read", src, None)
+    torch.cuda.synchronize()
+    assert int(K._sink(dev)[0].item()) == 0  # the keep-alive store never fires
+
+
+def test_hbm_bandwidth_floors(K, dev):
+    nbytes = 2 << 30
+    src = torch.empty(nbytes // 4, dtype=torch.int32, device=dev)
+    dst = torch.empty_like(src)
+    K.hbm_stream("write", None, src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    rates = {}
+    for mode in ("read", "write", "copy"):
+        s, d = (src if mode != "write" else None), (dst if mode != "read" else None)
+        for _ in range(3):
+            K.hbm_stream(mode, s, d)
+        e0.record()
+        moved = sum(K.hbm_stream(mode, s, d) for _ in range(10))
+        e1.record()
+        e1.synchronize()
+        rates[mode] = moved / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    # measured 6.0-7.1 / 4.4-5.9 / 4.8-5.5 TB/s (profiles/r02_session1/hbm_sweep*.txt); floors at ~70 %
+    assert rates["read"] > 4500 and rates["write"] > 3500 and rates["copy"] > 3500, rates
+
+
+def test_fp32_and_fp64_loads(K, dev):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    K.fp32_fma(dev, iters=2000)
+    e0.record()
+    flop = sum(K.fp32_fma(dev, iters=5000) for _ in range(5))
+    e1.record()
+    e1.synchronize()
+    tf32 = flop / (e0.elapsed_time(e1) * 1e-3) / 1e12
+    K.fp64_mfma(dev, iters=500)
+    e0.record()
+    flop = sum(K.fp64_mfma(dev, iters=1500) for _ in range(5))
+    e1.record()
+    e1.synchronize()
+    tf64 = flop / (e0.elapsed_time(e1) * 1e-3) / 1e12
+    # 157.3 TF fp32 vector / 78.6 TF fp64 matrix peaks; measured 124 / 68 (proftester_all.log)
+    assert 80 < tf32 < 160 and 40 < tf64 < 80, (tf32, tf64)
+    assert int(K._sink(dev)[0].item()) == 0
+
+
+def test_proftester_native_protocol():
+    import json
+    import subprocess
+
+    from k8s_nvidia_gpus_amd.ops import build as B
+
+    p = subprocess.run([str(B.NATIVE_BIN / "amd-proftester"), "-t", "1005,1006,1007,1010,xgmi",
+                        "--iters", "5", "--settle-ms", "20", "--hbm-bytes", "1G", "--json"],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    docs = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert {d["test"] for d in docs} == {"hbm-copy", "fp64", "fp32", "pcie-h2d", "xgmi"}
+    assert all(d["passed"] for d in docs)
+    assert p.stdout.rstrip().endswith("Test PASSED\nDone")

@@ -66,7 +66,7 @@ def test_validator_chain_with_native_binaries(tmp_path, native):
     cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {gemmSize: 4096, gemmMinTflops: 600, "
                            "rccl: false, pluginTest: false}\n")
     v = Validator(cfg, str(tmp_path), bin_dir=str(native))
-    for step in ("driver", "vectoradd", "gemm"):
+    for step in ("driver", "vectoradd", "gemm", "bandwidth"):
         r = v.run_step(step)
         assert r.passed, (step, r.reason)
     (tmp_path / "runtime-ready").write_text("1")  # no runtime installer on the box
@@ -76,7 +76,7 @@ def test_validator_chain_with_native_binaries(tmp_path, native):
     out = os.environ.get("AMDK8S_EVIDENCE_DIR")
     if out:
         os.makedirs(out, exist_ok=True)
-        for f in ("driver.json", "vectoradd.json", "gemm.json", "report.json"):
+        for f in ("driver.json", "vectoradd.json", "gemm.json", "bandwidth.json", "report.json"):
             with open(tmp_path / f) as src, open(os.path.join(out, "validator_" + f), "w") as dst:
                 dst.write(src.read())
 

@@ -213,8 +213,11 @@ def test_operator_daemonsets_gate_on_markers_and_share_config():
             assert spec["nodeSelector"] == {"amd.com/gpu.present": "true"}, name
     val = ds["amd-gpu-validator"]["spec"]["template"]["spec"]
     steps = [c["command"][-1] for c in val["initContainers"]]
-    assert steps == ["--step=driver", "--step=runtime", "--step=vectoradd", "--step=gemm",
-                     "--step=rccl", "--step=plugin"]
+    from k8s_nvidia_gpus_amd.operator.validator import STEPS
+
+    # one init container per validator step, in the validator's order; the report is the main one
+    assert steps == [f"--step={s}" for s in STEPS if s != "report"]
+    assert steps[:4] == ["--step=driver", "--step=runtime", "--step=vectoradd", "--step=gemm"]
     plug = ds["amd-gpu-device-plugin"]["spec"]["template"]["spec"]
     assert {"driver-ready", "runtime-ready"} <= {m.split("/")[-1] for m in plug["initContainers"][0]["command"] if "ready" in m}
     rc = [o for o in objs if o["kind"] == "RuntimeClass"][0]

@@ -22,6 +22,14 @@ REPO = Path(__file__).resolve().parent.parent
 VECTORADD_LOG = (REPO / "profiles/r01_vectoradd.log").read_text()
 GEMM_LOG = (REPO / "profiles/r01_gemm_validator.log").read_text()
 GEMM_FP8_LOG = (REPO / "profiles/r01_gemm_validator_fp8.log").read_text()
+# stdout of native/bin/amd-proftester --json on one MI355X (round 2, session 1)
+PROFTESTER_LOG = (REPO / "profiles/r02_session1/proftester_all.log").read_text()
+
+
+def _pt_line(test, device, value, peer=-1, engine="", passed=True, skipped=False):
+    return json.dumps({"check": "proftester", "test": test, "device": device, "peer": peer,
+                       "engine": engine, "value": value, "min": value, "max": value, "unit": "GB/s",
+                       "seconds": 0.01, "skipped": skipped, "passed": passed, "note": ""})
 RCCL_8GPU = """# rccl-allreduce-bench: 8 GPU(s), RCCL 22703, in-place float sum, 20 iters
 {"check": "rccl_allreduce", "ngpus": 8, "peak_busbw_gbps": 301.20, "peak_algbw_gbps": 172.11, "peak_bytes": 1073741824, "wrong": 0, "passed": true}
 Test PASSED
@@ -74,17 +82,18 @@ def test_report_carries_per_step_durations(tmp_path):
     cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {gemmMinTflops: 900, rccl: false, "
                            "pluginTest: false}\n")
     r = Runner({"amd-vectoradd": (0, VECTORADD_LOG), "amd-gemm-validator": (0, GEMM_LOG),
-                "amd-gemm-validator:fp8": (0, GEMM_FP8_LOG)})
+                "amd-gemm-validator:fp8": (0, GEMM_FP8_LOG), "amd-proftester": (0, PROFTESTER_LOG)})
     v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=r)
     for st in ("driver", "runtime"):  # markers as the driver/runtime agents publish them
         (tmp_path / f"{st}.json").write_text(json.dumps({"step": st, "passed": True, "duration_s": 1.5}))
         (tmp_path / f"{st}-ready").write_text("0\n")
     assert v.run_step("vectoradd").detail["duration_s"] >= 0
     assert v.run_step("gemm").passed
+    assert v.run_step("bandwidth").passed
     rep = v.run_step("report")
     assert rep.passed
     steps = rep.detail["step_seconds"]
-    assert set(steps) >= {"driver", "runtime", "vectoradd", "gemm"}
+    assert set(steps) >= {"driver", "runtime", "vectoradd", "gemm", "bandwidth"}
     assert rep.detail["chain_seconds"] == pytest.approx(sum(steps.values()), abs=1e-3)
     assert json.loads((tmp_path / "report.json").read_text())["chain_seconds"] >= 3.0
 
@@ -189,7 +198,7 @@ def test_plugin_step_schedules_a_gpu_pod(tmp_path, cfg, monkeypatch):
         assert pod["spec"]["runtimeClassName"] == "amd" and pod["spec"]["nodeName"] == "gpu-node-1"
         assert ("amd-gpu-operator", pod["metadata"]["name"]) not in api.pods  # cleaned up
         # report: label the node
-        for s in ("driver", "runtime", "vectoradd", "gemm", "rccl"):
+        for s in ("driver", "runtime", "vectoradd", "gemm", "bandwidth", "rccl"):
             (tmp_path / f"{s}-ready").write_text("1")
         rep = v.run_step("report")
         assert rep.passed and api.nodes["gpu-node-1"]["metadata"]["labels"]["amd.com/gpu.validated"] == "true"
@@ -267,7 +276,7 @@ def test_step_that_raises_is_recorded_as_failed_and_withdraws_markers(tmp_path, 
     assert rec["passed"] is False and rec["exception"] == "TimeoutError" and "duration_s" in rec
     assert kube.deleted  # the pod was still cleaned up
     # the report then fails the node instead of keeping the old pass
-    for s in ("driver", "runtime", "vectoradd", "gemm", "rccl"):
+    for s in ("driver", "runtime", "vectoradd", "gemm", "bandwidth", "rccl"):
         (tmp_path / f"{s}-ready").write_text("1")
     rep = v.run_step("report")
     assert not rep.passed and "plugin" in rep.detail["missing"]
@@ -282,7 +291,7 @@ def test_unknown_step_still_raises(tmp_path, cfg):
 def test_report_lists_required_steps_without_duration(tmp_path):
     """chain_seconds must not silently treat an untimed required step as 0 s."""
     cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {rccl: false, pluginTest: false, "
-                           "gemm: false, vectorAdd: false}\n")
+                           "gemm: false, vectorAdd: false, bandwidth: false}\n")
     v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=Runner({}))
     (tmp_path / "driver.json").write_text(json.dumps({"step": "driver", "passed": True, "duration_s": 2.0}))
     for st in ("driver", "runtime"):
@@ -292,3 +301,61 @@ def test_report_lists_required_steps_without_duration(tmp_path):
     assert rep.detail["step_seconds"] == {"driver": 2.0}
     assert rep.detail["step_seconds_missing"] == ["runtime"]
     assert rep.detail["chain_complete"] is False
+
+
+# ----------------------------------------------------------------------------- bandwidth step
+def test_bandwidth_step_on_real_mi355x_output(tmp_path, cfg):
+    r = Runner({"amd-proftester": (0, PROFTESTER_LOG)})
+    v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=r)
+    b = v.run_step("bandwidth")
+    assert b.passed, b.reason
+    argv = r.calls[0]
+    assert argv[0] == "/x/amd-proftester" and argv[-1] == "--json"
+    assert set(argv[argv.index("-t") + 1].split(",")) == {"hbm-copy", "pcie-h2d", "pcie-d2h", "xgmi"}
+    summary = b.detail["min_by_test_gbps"]
+    assert summary["hbm-copy"] > 4000 and summary["pcie-h2d"] > 20
+    assert "xgmi-sdma" not in summary  # one GPU: the xGMI test is skipped, not failed
+    assert (tmp_path / "bandwidth-ready").exists()
+
+
+def test_bandwidth_step_enforces_floors(tmp_path):
+    cfg = load_config(text="validator: {hbmMinGBps: 9000}\n")
+    v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=Runner({"amd-proftester": (0, PROFTESTER_LOG)}))
+    b = v.run_step("bandwidth")
+    assert not b.passed and "hbm-copy dev 0" in b.reason and "< 9000" in b.reason
+    assert not (tmp_path / "bandwidth-ready").exists()
+
+
+def test_bandwidth_step_gates_every_sdma_xgmi_pair(tmp_path, cfg):
+    """Synthetic 2-GPU output (no 2-GPU box in this pool): one slow SDMA pair fails the node; the
+    copy-kernel pulls and the all-peer aggregate are reported but not gated."""
+    lines = [_pt_line("hbm-copy", d, 5200.0) for d in (0, 1)]
+    lines += [_pt_line(t, d, 56.0, engine="sdma") for t in ("pcie-h2d", "pcie-d2h") for d in (0, 1)]
+    lines += [_pt_line("xgmi", 1, 48.0, peer=0, engine="sdma"), _pt_line("xgmi", 0, 12.0, peer=1, engine="sdma"),
+              _pt_line("xgmi", 1, 5.0, peer=0, engine="kernel"), _pt_line("xgmi", 0, 90.0, engine="kernel-all-peers")]
+    out = "\n".join(lines) + "\nTest PASSED\nDone\n"
+    v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=Runner({"amd-proftester": (0, out)}))
+    b = v.run_step("bandwidth")
+    assert not b.passed and "xgmi dev 0<-1 12.0 < 30" in b.reason
+    assert "dev 1<-0" not in b.reason  # the slow copy-kernel pull is not gated
+    assert b.detail["min_by_test_gbps"]["xgmi-sdma"] == 12.0
+
+
+def test_bandwidth_step_fails_on_failed_copy_and_missing_tests(tmp_path, cfg):
+    out = _pt_line("hbm-copy", 0, 5200.0, passed=False) + "\nTest FAILED\n"
+    v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=Runner({"amd-proftester": (1, out)}))
+    b = v.run_step("bandwidth")
+    assert not b.passed and "1 check(s) failed" in b.reason and "pcie-h2d" in b.reason
+
+
+def test_exporter_publishes_bandwidth_results(tmp_path, cfg):
+    from prometheus_client import generate_latest
+
+    from k8s_nvidia_gpus_amd.operator import exporter as ex
+
+    v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=Runner({"amd-proftester": (0, PROFTESTER_LOG)}))
+    assert v.run_step("bandwidth").passed
+    col = ex.GpuCollector(ex.SysfsBackend(str(tmp_path / "nosys")), "node-a", str(tmp_path))  # no GPUs
+    text = generate_latest(ex.make_registry(col)).decode()
+    assert 'amd_gpu_validator_bandwidth_gbps{engine="",gpu="0",node="node-a",peer="",test="hbm-copy"}' in text
+    assert 'test="pcie-h2d"' in text and 'amd_gpu_validation_passed{node="node-a",step="bandwidth"} 1.0' in text
