@@ -11,6 +11,8 @@ Components (cluster-config/apps/amd-gpu-operator/*.yaml):
   wait-marker       block until marker file(s) exist (init containers)
   cdi               print the CDI spec for this node
   topology          print the node's GPU topology as JSON
+  bringup           node bring-up rehearsal: driver → runtime → plugin → allocate → container →
+                    validator on this node, timed (node-local time-to-first-GPU-pod)
 """
 from __future__ import annotations
 
@@ -63,6 +65,8 @@ def main(argv=None) -> int:
     ap.add_argument("--hold", action="store_true", help="validator: stay running after the step")
     ap.add_argument("--port", type=int, default=None)
     ap.add_argument("--log-level", default=os.environ.get("LOG_LEVEL", "INFO"))
+    ap.add_argument("--workdir", default=None, help="bringup: keep markers/bundle here")
+    ap.add_argument("--no-validate", action="store_true", help="bringup: stop after the first pod")
     args = ap.parse_args(argv)
     logging.basicConfig(level=args.log_level.upper(),
                         format='{"ts":"%(asctime)s","level":"%(levelname)s","logger":"%(name)s","msg":"%(message)s"}')
@@ -155,6 +159,11 @@ def main(argv=None) -> int:
         PartitionManager(_kube(optional=False), node, backend, args.root, p["compute"], p["memory"],
                          float(p["drainTimeoutSeconds"])).run(args.interval or 30)
         return 0
+
+    if c == "bringup":
+        from . import bringup
+
+        return bringup.main(args, cfg, _bin_dir())
 
     if c == "validator":
         import time

@@ -1,0 +1,257 @@
+"""Node bring-up rehearsal: the node-local half of time-to-first-GPU-pod, measured on real hardware.
+
+BASELINE.json's headline metric pairs the validator GEMM with *time-to-first-GPU-pod*.  On a
+cluster that is ``tools/time_to_first_gpu_pod.py`` (``kubectl apply`` → validated node → first
+``amd.com/gpu: 1`` pod passing vectorAdd).  The GPU pool this repository is measured on has
+MI355X boxes but no Kubernetes, so this module runs every node-local step of that path with the
+operator's REAL components against the real KFD sysfs, /dev nodes, amd-smi and GPU, and stands in
+only for the parts that are not on the node (API server, scheduler, image pull) and for kubelet's
+socket side (:class:`.kubelet_stub.KubeletStub`, the same stand-in the CPU tests use):
+
+  driver      kfd-probe sees the expected gfx950 agents and opens /dev/kfd + render nodes
+  runtime     amd-container-runtime + CDI spec installed (into the work dir's host prefix)
+  plugin      device plugin serves, registers with kubelet, first ListAndWatch: healthy devices
+  allocate    kubelet's GetPreferredAllocation + Allocate for ``amd.com/gpu: 1``
+  create      the runtime shim edits the pod's OCI spec from the Allocate annotations: /dev/kfd +
+              exactly the allocated render node, with device-cgroup rules
+  container   the pod's process (amd-vectoradd, reference protocol) on the allocated GPU
+              → time_to_first_gpu_pod_s
+  validate    (optional) the validator chain: vectorAdd, bf16/fp8 GEMM, bandwidth, report
+              → time_to_validated_s
+
+The reference has no such measurement; it budgets 90 minutes for its in-cluster driver build alone
+(reference cluster-config/apps/gpu-operator/helmrelease.yaml:7).  What this does NOT include: API
+server / scheduler latency, image pull, and runc's namespace/cgroup setup (no runc on the box; the
+container's view is approximated by HIP_VISIBLE_DEVICES on the allocated GPU).
+
+    python -m k8s_nvidia_gpus_amd.operator bringup [--no-validate] [--workdir DIR]
+"""
+from __future__ import annotations
+
+import copy
+import json
+import os
+import shutil
+import subprocess
+import tempfile
+import threading
+import time
+from dataclasses import asdict, dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence
+
+from . import deviceplugin_api as api
+from .config import OperatorConfig
+from .validator import Validator, default_runner, json_lines, protocol_passed
+
+ContainerRunner = Callable[[Sequence[str], Dict[str, str], float], subprocess.CompletedProcess]
+
+
+def _run_container(argv: Sequence[str], env: Dict[str, str], timeout: float) -> subprocess.CompletedProcess:
+    return subprocess.run(list(argv), env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                          text=True, timeout=timeout)
+
+
+@dataclass
+class Stage:
+    name: str
+    start_s: float
+    end_s: float
+    ok: bool
+    detail: Dict = field(default_factory=dict)
+
+
+class BringupError(RuntimeError):
+    pass
+
+
+def _pod_spec(bundle_dir: str, annotations: Dict[str, str], command: Sequence[str]) -> Dict:
+    """The OCI spec containerd would hand the runtime for the validator's vectorAdd pod."""
+    return {
+        "ociVersion": "1.2.0",
+        "process": {"args": list(command), "env": ["PATH=/usr/local/bin:/usr/bin:/bin"],
+                    "capabilities": {"bounding": ["CAP_CHOWN", "CAP_KILL"]}},
+        "root": {"path": os.path.join(bundle_dir, "rootfs")},
+        "annotations": dict(annotations, **{"io.kubernetes.cri.container-type": "container"}),
+        "linux": {"resources": {"devices": [{"allow": False, "access": "rwm"}]}, "devices": []},
+    }
+
+
+def rehearse(cfg: OperatorConfig, bin_dir: str, workdir: Optional[str] = None, root: str = "/",
+             validate: bool = True, runner=default_runner,
+             container_runner: ContainerRunner = _run_container,
+             container_cmd: Optional[Sequence[str]] = None, timeout: float = 120.0,
+             driver_wait: float = 120.0) -> Dict:
+    """Run the node-local bring-up once; returns a JSON-able report (raises nothing: a failed stage
+    ends the run and is reported)."""
+    from .device_plugin import AmdGpuDevicePlugin
+    from .kubelet_stub import KubeletStub
+    from .runtime import install_runtime
+
+    own_tmp = workdir is None
+    workdir = workdir or tempfile.mkdtemp(prefix="amdk8s-bringup-")
+    markers = os.path.join(workdir, "run-amd-validations")
+    host = os.path.join(workdir, "host")
+    os.makedirs(markers, exist_ok=True)
+    t0 = time.monotonic()
+    wall0 = time.time()
+    stages: List[Stage] = []
+    report: Dict = {"check": "bringup", "root": root, "workdir": workdir, "start_time": wall0}
+    dev_root = "" if root == "/" else root.rstrip("/")
+    plugin = kubelet = None
+    stop = threading.Event()
+
+    def stage(name: str, fn: Callable[[], Dict]) -> Dict:
+        s = time.monotonic() - t0
+        try:
+            detail = fn() or {}
+            ok = bool(detail.pop("_ok", True))
+        except Exception as e:  # noqa: BLE001 - every failure is a reported stage result
+            detail, ok = {"error": f"{type(e).__name__}: {e}"[:500]}, False
+        stages.append(Stage(name, round(s, 4), round(time.monotonic() - t0, 4), ok, detail))
+        if not ok:
+            raise BringupError(name)
+        return detail
+
+    # the plugin-pod step needs an API server; everything else in the chain is node-local
+    vraw = copy.deepcopy(cfg.raw)
+    vraw["validator"]["pluginTest"] = False
+    v = Validator(OperatorConfig(vraw), markers, bin_dir=bin_dir, runner=runner, root=root,
+                  driver_wait=driver_wait)
+    state: Dict = {}
+    try:
+        def driver():
+            r = v.run_step("driver")
+            return {"_ok": r.passed, "gpus": r.detail.get("gpus"), "reason": r.reason}
+
+        def runtime():
+            info = install_runtime(os.path.join(bin_dir, "amd-container-runtime"),
+                                   os.path.join(host, "usr/local/bin/amd-container-runtime"),
+                                   os.path.join(host, "etc/cdi"), markers, root=root,
+                                   min_gfx=cfg.min_gfx)
+            return {"cdi_devices": info["cdi_devices"]}
+
+        def plugin_up():
+            nonlocal plugin, kubelet
+            kdir = os.path.join(workdir, "kubelet-device-plugins")
+            kubelet = KubeletStub(kdir).start()
+            plugin = AmdGpuDevicePlugin(cfg, root=root, kubelet_dir=kdir, pause_marker=None,
+                                        dev_prefix=os.path.join(dev_root or "/", "dev"))
+            threading.Thread(target=plugin.run, kwargs={"poll": 0.05, "stop_event": stop},
+                             daemon=True).start()
+            if not kubelet.registered.wait(timeout):
+                raise BringupError("device plugin never registered with kubelet")
+            reg = kubelet.registrations[-1]
+            ch, stub = kubelet.plugin_stub()
+            first = next(stub.ListAndWatch(api.Empty(), timeout=timeout))
+            healthy = [d.ID for d in first.devices if d.health == api.HEALTHY]
+            state.update(channel=ch, stub=stub, healthy=healthy)
+            return {"_ok": bool(healthy), "resource": reg.resource_name, "endpoint": reg.endpoint,
+                    "advertised": len(first.devices), "healthy": len(healthy)}
+
+        def allocate():
+            stub = state["stub"]
+            pref = stub.GetPreferredAllocation(api.PreferredAllocationRequest(container_requests=[
+                api.ContainerPreferredAllocationRequest(available_deviceIDs=state["healthy"],
+                                                        allocation_size=1)]), timeout=timeout)
+            ids = list(pref.container_responses[0].deviceIDs)
+            req = api.AllocateRequest()
+            req.container_requests.add(devices_ids=ids)
+            (c,) = stub.Allocate(req, timeout=timeout).container_responses
+            state.update(ids=ids, alloc=c)
+            return {"device_ids": ids, "device_nodes": [d.host_path for d in c.devices],
+                    "annotations": dict(c.annotations)}
+
+        def create():
+            c = state["alloc"]
+            bundle = os.path.join(workdir, "bundle")
+            os.makedirs(os.path.join(bundle, "rootfs"), exist_ok=True)
+            cmd = list(container_cmd or [os.path.join(bin_dir, "amd-vectoradd")])
+            with open(os.path.join(bundle, "config.json"), "w") as f:
+                json.dump(_pod_spec(bundle, dict(c.annotations), cmd), f)
+            env = dict(os.environ)
+            if dev_root:
+                env["AMD_CONTAINER_RUNTIME_DEV_ROOT"] = dev_root
+            p = subprocess.run([os.path.join(host, "usr/local/bin/amd-container-runtime"),
+                                "--amd-edit-bundle", bundle], capture_output=True, text=True,
+                               env=env, timeout=timeout)
+            if p.returncode != 0:
+                raise BringupError(f"runtime shim rejected the spec: {p.stderr.strip()[-300:]}")
+            spec = json.loads(p.stdout)
+            nodes = sorted(d["path"] for d in spec["linux"]["devices"])
+            want = sorted(["/dev/kfd"] + [f"/dev/dri/renderD{m}" for m in
+                                          c.annotations["amd.com/gpu.render-minors"].split(",")])
+            rules = [r for r in spec["linux"]["resources"]["devices"] if r.get("allow")]
+            state["cmd"] = cmd
+            return {"_ok": nodes == want and len(rules) >= len(want), "device_nodes": nodes,
+                    "cgroup_allow_rules": len(rules)}
+
+        def container():
+            # the container sees only its render node; without runc on the box the same view is
+            # HIP_VISIBLE_DEVICES = the allocated GPU's HIP index (HIP enumerates in KFD order)
+            from ..utils.topology import read_topology
+
+            uid = state["ids"][0]
+            gpus = read_topology(root, cfg.min_gfx).gpus
+            order = [g.device_uid for g in gpus] + [str(i) for i in range(len(gpus))]
+            idx = order.index(uid) % max(1, len(gpus)) if uid in order else 0
+            env = dict(os.environ, HIP_VISIBLE_DEVICES=str(idx))
+            env.pop("CUDA_VISIBLE_DEVICES", None)
+            p = container_runner(state["cmd"], env, timeout)
+            out = p.stdout or ""
+            return {"_ok": p.returncode == 0 and protocol_passed(out), "hip_index": idx,
+                    "rc": p.returncode, "log_tail": out.strip().splitlines()[-2:]}
+
+        stage("driver", driver)
+        stage("runtime", runtime)
+        stage("plugin", plugin_up)
+        stage("allocate", allocate)
+        stage("create", create)
+        stage("container", container)
+        report["time_to_first_gpu_pod_s"] = stages[-1].end_s
+        if validate:
+            def validator_chain():
+                out = {}
+                for s in ("vectoradd", "gemm", "bandwidth", "rccl"):
+                    r = v.run_step(s)
+                    out[s] = {"passed": r.passed, "duration_s": r.detail.get("duration_s"),
+                              "reason": r.reason}
+                    if s == "gemm":
+                        out[s]["tflops"] = [d.get("tflops") for d in r.detail.get("devices", [])]
+                rep = v.run_step("report")
+                out["report"] = {"passed": rep.passed, "chain_seconds": rep.detail.get("chain_seconds"),
+                                 "missing": rep.detail.get("missing")}
+                out["_ok"] = rep.passed
+                return out
+
+            stage("validate", validator_chain)
+            report["time_to_validated_s"] = stages[-1].end_s
+    except BringupError:
+        pass
+    finally:
+        stop.set()
+        if plugin is not None:
+            plugin.stop()
+        if kubelet is not None:
+            kubelet.stop()
+        if "channel" in state:
+            state["channel"].close()
+        if own_tmp:
+            shutil.rmtree(workdir, ignore_errors=True)
+    report["stages"] = [asdict(s) for s in stages]
+    report["passed"] = bool(stages) and all(s.ok for s in stages)
+    report.setdefault("time_to_first_gpu_pod_s", None)
+    report.setdefault("time_to_validated_s", None)
+    return report
+
+
+def main(args, cfg: OperatorConfig, bin_dir: str) -> int:
+    rep = rehearse(cfg, bin_dir, workdir=args.workdir, root=args.root,
+                   validate=not args.no_validate)
+    for s in rep["stages"]:
+        print(f"{s['name']:10s} {'ok  ' if s['ok'] else 'FAIL'} {s['start_s']:8.3f} -> {s['end_s']:8.3f} s"
+              + ("" if s["ok"] else f"  {s['detail'].get('error') or s['detail']}"))
+    print(json.dumps(rep))
+    return 0 if rep["passed"] else 1
+
+
+__all__ = ["rehearse", "main", "json_lines"]

@@ -117,8 +117,9 @@ class StepResult:
 class Validator:
     def __init__(self, config: OperatorConfig, marker_dir: str = "/run/amd/validations",
                  bin_dir: Optional[str] = None, runner: Runner = default_runner, root: str = "/",
-                 kube=None, node_name: Optional[str] = None):
+                 kube=None, node_name: Optional[str] = None, driver_wait: float = 120):
         self.cfg = config
+        self.driver_wait = driver_wait  # kfd-probe --wait: how long the driver may take to appear
         self.vcfg = config.section("validator")
         self.marker_dir = marker_dir
         self.bin_dir = bin_dir or find_bin_dir()
@@ -162,11 +163,11 @@ class Validator:
     def step_driver(self) -> StepResult:
         n = int(self.cfg["expectedGpusPerNode"])
         argv = [self._bin("kfd-probe"), "--expect-gpus", str(n), "--min-gfx", str(self.cfg.min_gfx),
-                "--wait", "120"]
+                "--wait", str(int(self.driver_wait))]
         if self.root != "/":
             argv += ["--sysfs-root", os.path.join(self.root, "sys/class/kfd/kfd/topology"),
                      "--dev-root", os.path.join(self.root, "dev"), "--no-open"]
-        rc, out = self.run_cmd(argv, 180)
+        rc, out = self.run_cmd(argv, self.driver_wait + 60)
         docs = json_lines(out)
         detail = docs[-1] if docs else {}
         ok = rc == 0 and bool(detail.get("ready"))

@@ -115,3 +115,25 @@ def test_bench_py_rccl_path_under_torchrun_one_rank():
     assert doc["n_gpus"] == 1 and doc["steps"] == 5 and doc["value"] > 0
     assert doc["allreduce_busbw_gbps"] is not None and len(doc["tflops_per_rank"]) == 1
     assert doc["settle"]["launches"] > 0
+
+
+def test_node_bringup_rehearsal_on_real_hardware(tmp_path, native):
+    """Node-local time-to-first-GPU-pod: real kfd-probe, runtime shim + CDI, device plugin over gRPC
+    (kubelet stand-in), Allocate, OCI spec edit, vectorAdd on the allocated GPU, validator chain."""
+    import torch
+
+    from k8s_nvidia_gpus_amd.operator import bringup
+
+    n = torch.cuda.device_count()
+    cfg = load_config(text=f"expectedGpusPerNode: {n}\n")
+    rep = bringup.rehearse(cfg, str(native), workdir=str(tmp_path / "work"))
+    assert rep["passed"], json.dumps(rep["stages"][-1])
+    st = {s["name"]: s for s in rep["stages"]}
+    assert st["plugin"]["detail"]["healthy"] == n
+    assert st["create"]["detail"]["device_nodes"][-1] == "/dev/kfd"
+    assert rep["time_to_first_gpu_pod_s"] < 30 and rep["time_to_validated_s"] < 120
+    out = os.environ.get("AMDK8S_EVIDENCE_DIR")
+    if out:
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, "bringup.json"), "w") as f:
+            json.dump(rep, f, indent=1)
