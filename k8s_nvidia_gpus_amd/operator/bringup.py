@@ -133,6 +133,9 @@ def rehearse(cfg: OperatorConfig, bin_dir: str, workdir: Optional[str] = None, r
         def plugin_up():
             nonlocal plugin, kubelet
             kdir = os.path.join(workdir, "kubelet-device-plugins")
+            if len(kdir) > 80:  # unix socket paths are limited to 107 bytes
+                kdir = tempfile.mkdtemp(prefix="amdk8s-kubelet-")
+                state["kdir_tmp"] = kdir
             kubelet = KubeletStub(kdir).start()
             plugin = AmdGpuDevicePlugin(cfg, root=root, kubelet_dir=kdir, pause_marker=None,
                                         dev_prefix=os.path.join(dev_root or "/", "dev"))
@@ -235,6 +238,8 @@ def rehearse(cfg: OperatorConfig, bin_dir: str, workdir: Optional[str] = None, r
             kubelet.stop()
         if "channel" in state:
             state["channel"].close()
+        if "kdir_tmp" in state:
+            shutil.rmtree(state["kdir_tmp"], ignore_errors=True)
         if own_tmp:
             shutil.rmtree(workdir, ignore_errors=True)
     report["stages"] = [asdict(s) for s in stages]
