@@ -27,6 +27,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "tile_order.h"
+
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -86,7 +88,7 @@ template <int SCHED>
 __global__ void __launch_bounds__(NT, 1)
 amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
-                               int ldc, int superblock) {
+                               int ldc, int order) {
   constexpr bool BUFFER_DMA = SCHED == SCHED_REGION;
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
 
@@ -96,34 +98,17 @@ amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* _
   const int wr = wave >> 1;  // A half this wave reads (rows wr*128..)
   const int wc = wave & 1;   // B half
 
-  // ---- block → tile: bijective XCD remap, then super-block or GROUP_M-grouped order ----
+  // ---- block → tile: per-partition XCD corners of super-blocks, or GROUP_M order (tile_order.h) ----
   const int tiles_m = M / BM;
   const int tiles_n = N / BN;
   const int nwg = tiles_m * tiles_n;
   const int bid = blockIdx.x;
   int m0, n0;
-  if (superblock) {
-    // Round-major 16×16-tile super-blocks: the 256 tiles in flight at once (one per CU) form a
-    // 4096×4096 block of C whose A/B panels (128 MiB at K = 8192) stay in the Infinity Cache; XCD x
-    // owns a 4(M)×8(N) corner of it. Super-blocks are walked in snake order so consecutive rounds
-    // share a panel set. Host guarantees tiles_m % 16 == tiles_n % 16 == 0.
-    const int xcd = bid & 7, i = bid >> 3;
-    const int round = i >> 5, j = i & 31;
-    const int sb_n_count = tiles_n >> 4;
-    const int sbm = round / sb_n_count;
-    int sbn = round - sbm * sb_n_count;
-    if (sbm & 1) sbn = sb_n_count - 1 - sbn;
-    m0 = (sbm * 16 + (xcd >> 1) * 4 + (j & 3)) * BM;
-    n0 = (sbn * 16 + (xcd & 1) * 8 + (j >> 2)) * BN;
-  } else {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    const int group = wgid / (GROUP_M * tiles_n);
-    const int first_m = group * GROUP_M;
-    const int gsz = min(tiles_m - first_m, GROUP_M);
-    const int in_group = wgid - group * GROUP_M * tiles_n;
-    m0 = (first_m + in_group % gsz) * BM;
-    n0 = (in_group / gsz) * BN;
+  {
+    int tm, tn;
+    amdk8s::block_tile(bid, tiles_m, tiles_n, order, GROUP_M, tm, tn);  // tile_order.h
+    m0 = tm * BM;
+    n0 = tn * BN;
   }
 
   // ---- LDS-DMA sources: piece j of wave w fills rows (j*4+w)*8 .. +8 of a 128-row half ----
@@ -405,10 +390,9 @@ extern "C" int amdk8s_gemm_bf16_nt_w4(const void* A, const void* B, void* C, int
   // the REGION schedule addresses each 256-row panel with a 32-bit buffer offset
   const bool panel_fits = 256ull * (unsigned long long)(lda > ldb ? lda : ldb) * 2 < (1ull << 31);
   const int nwg = (M / BM) * (N / BN);
-  // 16×16-tile super-block order whenever the tile grid allows it (AMDK8S_W4_SUPERBLOCK=0 turns
-  // it off for A/B runs): +8-10 % at 8192³ and 16384²×4096 (docs/gemm_tuning.md)
-  const char* sbenv = getenv("AMDK8S_W4_SUPERBLOCK");
-  const int sb = (M / BM) % 16 == 0 && (N / BN) % 16 == 0 && !(sbenv && sbenv[0] == '0');
+  // super-block order whenever the tile grid allows it (AMDK8S_W4_SUPERBLOCK=0 turns it off for
+  // A/B runs): +8-10 % at 8192³ and 16384²×4096 in SPX (docs/gemm_tuning.md); partition-aware tile order (tile_order.h): XCD corners of super-blocks, or GROUP_M order
+  const int sb = amdk8s::tile_order_arg(M / BM, N / BN);
   const char* schenv = getenv("AMDK8S_W4_SCHEDULE");
   const bool region = panel_fits && !(schenv && schenv[0] == 'i');
   const uint16_t* a = (const uint16_t*)A;

@@ -23,6 +23,8 @@
 
 #include "gemm_bf16_gfx950_w4a_kloop.inc"
 
+#include "tile_order.h"
+
 namespace {
 
 constexpr int BM = 256;
@@ -43,7 +45,7 @@ template <int SCHED>
 __global__ void __launch_bounds__(NT, 1)
 amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                 uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
-                                int ldc, int superblock, int nt_store) {
+                                int ldc, int order, int nt_store) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
 
   const int tid = threadIdx.x;
@@ -52,35 +54,17 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
   const int wr = wave >> 1;  // A half this wave reads
   const int wc = wave & 1;   // B half
 
-  // ---- block → tile: the w4 kernel's XCD-aware super-block / GROUP_M order ----
+  // ---- block → tile: per-partition XCD corners of super-blocks, or GROUP_M order (tile_order.h) ----
   const int tiles_m = M / BM;
   const int tiles_n = N / BN;
   const int nwg = tiles_m * tiles_n;
   const int bid = blockIdx.x;
   int m0, n0;
-  if (superblock) {
-    const int xcd = bid & 7, i = bid >> 3;
-    const int round = i >> 5, j = i & 31;
-    const int sb_n_count = tiles_n >> 4;
-    const int sbm = round / sb_n_count;
-    int sbn = round - sbm * sb_n_count;
-    if (sbm & 1) sbn = sb_n_count - 1 - sbn;
-    if (superblock == 2) {  // XCD corner 8(M)×4(N) (A/B knob)
-      m0 = (sbm * 16 + (xcd & 1) * 8 + (j & 7)) * BM;
-      n0 = (sbn * 16 + (xcd >> 1) * 4 + (j >> 3)) * BN;
-    } else {                // XCD corner 4(M)×8(N)
-      m0 = (sbm * 16 + (xcd >> 1) * 4 + (j & 3)) * BM;
-      n0 = (sbn * 16 + (xcd & 1) * 8 + (j >> 2)) * BN;
-    }
-  } else {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    const int group = wgid / (GROUP_M * tiles_n);
-    const int first_m = group * GROUP_M;
-    const int gsz = min(tiles_m - first_m, GROUP_M);
-    const int in_group = wgid - group * GROUP_M * tiles_n;
-    m0 = (first_m + in_group % gsz) * BM;
-    n0 = (in_group / gsz) * BN;
+  {
+    int tm, tn;
+    amdk8s::block_tile(bid, tiles_m, tiles_n, order, GROUP_M, tm, tn);  // tile_order.h
+    m0 = tm * BM;
+    n0 = tn * BN;
   }
 
   // ---- operands of the generated body (register map in tools/gen_gemm_w4a_kloop.py) ----
@@ -145,9 +129,8 @@ extern "C" int amdk8s_gemm_bf16_nt_w4a(const void* A, const void* B, void* C, in
   if (256ull * (unsigned long long)(lda > ldb ? lda : ldb) * 2 >= (1ull << 31))
     return (int)hipErrorInvalidValue;
   const int nwg = (M / BM) * (N / BN);
-  const char* sbenv = getenv("AMDK8S_W4_SUPERBLOCK");
-  int sb = (M / BM) % 16 == 0 && (N / BN) % 16 == 0 && !(sbenv && sbenv[0] == '0');
-  if (sb && sbenv && sbenv[0] == '2') sb = 2;
+  // partition-aware tile order (tile_order.h): XCD corners of super-blocks, or GROUP_M order
+  const int sb = amdk8s::tile_order_arg(M / BM, N / BN);
   // non-temporal C stores (AMDK8S_GEMM_NT_STORE=0 turns them off for A/B runs)
   const char* ntenv = getenv("AMDK8S_GEMM_NT_STORE");
   const int nt = !(ntenv && ntenv[0] == '0');

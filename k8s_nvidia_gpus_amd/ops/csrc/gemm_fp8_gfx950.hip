@@ -27,6 +27,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "tile_order.h"
+
 namespace {
 
 typedef __attribute__((ext_vector_type(4))) int i32x4;
@@ -61,7 +63,7 @@ __device__ __forceinline__ i32x4 lds_read16(const char* p) {
 __global__ void __launch_bounds__(NT, 1)
 amdk8s_gemm_fp8_nt_256x256(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                            uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
-                           int ldc, int superblock) {
+                           int ldc, int order) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
 
   const int tid = threadIdx.x;
@@ -70,30 +72,17 @@ amdk8s_gemm_fp8_nt_256x256(const uint8_t* __restrict__ A, const uint8_t* __restr
   const int wr = wave >> 1;
   const int wc = wave & 1;
 
-  // ---- block → tile (as in gemm_bf16_gfx950_w4.hip) ----
+  // ---- block → tile: per-partition XCD corners of super-blocks, or GROUP_M order (tile_order.h) ----
   const int tiles_m = M / BM;
   const int tiles_n = N / BN;
   const int nwg = tiles_m * tiles_n;
   const int bid = blockIdx.x;
   int m0, n0;
-  if (superblock) {
-    const int xcd = bid & 7, i = bid >> 3;
-    const int round = i >> 5, j = i & 31;
-    const int sb_n_count = tiles_n >> 4;
-    const int sbm = round / sb_n_count;
-    int sbn = round - sbm * sb_n_count;
-    if (sbm & 1) sbn = sb_n_count - 1 - sbn;
-    m0 = (sbm * 16 + (xcd >> 1) * 4 + (j & 3)) * BM;
-    n0 = (sbn * 16 + (xcd & 1) * 8 + (j >> 2)) * BN;
-  } else {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    const int group = wgid / (GROUP_M * tiles_n);
-    const int first_m = group * GROUP_M;
-    const int gsz = min(tiles_m - first_m, GROUP_M);
-    const int in_group = wgid - group * GROUP_M * tiles_n;
-    m0 = (first_m + in_group % gsz) * BM;
-    n0 = (in_group / gsz) * BN;
+  {
+    int tm, tn;
+    amdk8s::block_tile(bid, tiles_m, tiles_n, order, GROUP_M, tm, tn);  // tile_order.h
+    m0 = tm * BM;
+    n0 = tn * BN;
   }
 
   // ---- LDS-DMA: piece p (0..15): j = p >> 2 (32-row stripe), h = (p >> 1) & 1, p & 1: A/B;
@@ -240,8 +229,8 @@ extern "C" int amdk8s_gemm_fp8_nt(const void* A, const void* B, void* C, int M, 
   if (256ull * (unsigned long long)(lda > ldb ? lda : ldb) >= (1ull << 31))
     return (int)hipErrorInvalidValue;
   const int nwg = (M / BM) * (N / BN);
-  const char* sbenv = getenv("AMDK8S_W4_SUPERBLOCK");
-  const int sb = (M / BM) % 16 == 0 && (N / BN) % 16 == 0 && !(sbenv && sbenv[0] == '0');
+  // partition-aware tile order (tile_order.h): XCD corners of super-blocks, or GROUP_M order
+  const int sb = amdk8s::tile_order_arg(M / BM, N / BN);
   hipLaunchKernelGGL(amdk8s_gemm_fp8_nt_256x256, dim3(nwg), dim3(NT), 0, stream,
                      (const uint8_t*)A, (const uint8_t*)B, (uint16_t*)C, M, N, K, lda, ldb, ldc, sb);
   return (int)hipGetLastError();

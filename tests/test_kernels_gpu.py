@@ -338,3 +338,26 @@ def test_proftester_native_protocol():
     assert {d["test"] for d in docs} == {"hbm-copy", "fp64", "fp32", "pcie-h2d", "xgmi"}
     assert all(d["passed"] for d in docs)
     assert p.stdout.rstrip().endswith("Test PASSED\nDone")
+
+
+@pytest.mark.parametrize("xcds", ["1", "2", "4", "8"])
+@pytest.mark.parametrize("m,n,k", [(8192, 4096, 256), (2304, 1280, 320)])  # super-block / GROUP_M grids
+def test_gemm_tile_order_per_partition_is_bitwise_identical(K, dev, xcds, m, n, k, monkeypatch):
+    """CPX/DPX/QPX tile orders (tile_order.h, forced with AMDK8S_GEMM_XCDS on this SPX device) cover
+    every tile exactly once: bit-identical C to the SPX order, for bf16 w4a/w4 and fp8 f8a."""
+    g = torch.Generator(device=dev).manual_seed(5)
+    a = _rand_bf16((m, k), g, dev)
+    b = _rand_bf16((n, k), g, dev)
+    monkeypatch.delenv("AMDK8S_GEMM_XCDS", raising=False)
+    ref = {v: K.gemm_bf16_nt(a, b, variant=v) for v in ("w4a", "w4")}
+    a8 = K.uniform_fp8((m, 512), seed=3, device=dev)
+    b8 = K.uniform_fp8((n, 512), seed=4, device=dev)
+    ref8 = K.gemm_fp8_nt(a8, b8)
+    monkeypatch.setenv("AMDK8S_GEMM_XCDS", xcds)
+    for v, r in ref.items():
+        out = torch.full((m, n), float("nan"), dtype=torch.bfloat16, device=dev)
+        K.gemm_bf16_nt(a, b, out=out, variant=v)
+        assert torch.equal(out, r), (v, xcds)
+    out8 = torch.full((m, n), float("nan"), dtype=torch.bfloat16, device=dev)
+    K.gemm_fp8_nt(a8, b8, out=out8)
+    assert torch.equal(out8, ref8), xcds
