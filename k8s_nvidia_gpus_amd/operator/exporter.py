@@ -5,8 +5,9 @@ installs no Prometheus (SURVEY.md §5 "Metrics"); its own observability is Flux'
 scrape annotations.  This exporter reads each MI355X through amd-smi (``amdsmi`` Python bindings
 over libamd_smi) and falls back to plain DRM sysfs when amd-smi is unavailable.  One
 ``amdsmi_get_gpu_metrics_info`` call per GPU per scrape returns the firmware metrics table
-(temperatures, activity, socket power, clocks, per-link xGMI byte accumulators, PCIe bandwidth,
-power-throttle residency), so a scrape costs 8 ioctls, not 8 × 15.  The validator's measured
+(temperatures, activity, socket power, clocks, per-link xGMI byte accumulators and link state,
+PCIe link speed / width / bandwidth and replay / recovery / NAK accumulators, power-throttle
+residency), so a scrape costs 8 ioctls, not 8 × 15.  The validator's measured
 results (bf16 GEMM TFLOPS per GPU, RCCL all-reduce bus bandwidth, pass/fail per step) are exported
 from /run/amd/validations so they can be graphed and alerted on like any other GPU metric.
 
@@ -108,10 +109,22 @@ class AmdSmiBackend:
             s["energy_acc"] = _num(m.get("energy_accumulator"))
             s["ppt_residency_acc"] = _num(m.get("ppt_residency_acc"))
             s["pcie_bw_acc"] = _num(m.get("pcie_bandwidth_acc"))
+            s["pcie_bw_gbps"] = _num(m.get("pcie_bandwidth_inst"))
             s["pcie_replay_acc"] = _num(m.get("pcie_replay_count_acc"))
+            s["pcie_recovery_acc"] = _num(m.get("pcie_l0_to_recov_count_acc"))
+            s["pcie_nak_sent_acc"] = _num(m.get("pcie_nak_sent_count_acc"))
+            s["pcie_nak_rcvd_acc"] = _num(m.get("pcie_nak_rcvd_count_acc"))
+            speed = _num(m.get("pcie_link_speed"))  # 0.1 GT/s units (320 = Gen5 x16's 32 GT/s)
+            s["pcie_speed_gts"] = speed / 10.0 if speed is not None else None
+            s["pcie_width"] = _num(m.get("pcie_link_width"))
+            s["xgmi_speed_gbps"] = _num(m.get("xgmi_link_speed"))
+            s["xgmi_width"] = _num(m.get("xgmi_link_width"))
             s["xgmi_read_kb"] = [_num(x) for x in (m.get("xgmi_read_data_acc") or [])]
             s["xgmi_write_kb"] = [_num(x) for x in (m.get("xgmi_write_data_acc") or [])]
             s["xgmi_link_status"] = [_num(x) for x in (m.get("xgmi_link_status") or [])]
+            pw = self._call("amdsmi_get_power_info", h) or {}
+            limit = _num(pw.get("power_limit"))  # µW
+            s["power_limit_w"] = limit / 1e6 if limit is not None else None
             vram = self._call("amdsmi_get_gpu_vram_usage", h) or {}
             if _num(vram.get("vram_total")) is not None:
                 s["vram_total_bytes"] = _num(vram["vram_total"]) * 1024 * 1024  # MiB → B
@@ -222,6 +235,12 @@ class GpuCollector:
             "vram_total_bytes": ("amd_gpu_vram_total_bytes", "HBM capacity"),
             "vram_used_bytes": ("amd_gpu_vram_used_bytes", "HBM in use"),
             "processes": ("amd_gpu_processes", "processes with the GPU open"),
+            "power_limit_w": ("amd_gpu_power_limit_watts", "socket power cap"),
+            "pcie_bw_gbps": ("amd_gpu_pcie_bandwidth_gbps", "instantaneous PCIe bandwidth (GB/s)"),
+            "pcie_speed_gts": ("amd_gpu_pcie_link_speed_gts", "PCIe link speed (GT/s)"),
+            "pcie_width": ("amd_gpu_pcie_link_width", "PCIe link width (lanes)"),
+            "xgmi_speed_gbps": ("amd_gpu_xgmi_link_speed_gbps", "xGMI link speed (Gb/s per lane)"),
+            "xgmi_width": ("amd_gpu_xgmi_link_width", "xGMI link width (lanes)"),
         }
         fams = {k: GaugeMetricFamily(n, h, labels=base) for k, (n, h) in gauges.items()}
         temp = GaugeMetricFamily("amd_gpu_temperature_celsius", "temperature", labels=base + ["sensor"])
@@ -233,6 +252,9 @@ class GpuCollector:
         xgmi = CounterMetricFamily("amd_gpu_xgmi_data_bytes", "xGMI bytes moved per link",
                                    labels=base + ["link", "direction"])
         xlink = GaugeMetricFamily("amd_gpu_xgmi_link_up", "xGMI link status", labels=base + ["link"])
+        # PCIe link health (dcgm-exporter's DCGM_FI_DEV_PCIE_REPLAY_COUNTER and friends)
+        pcie_ev = CounterMetricFamily("amd_gpu_pcie_events", "PCIe link events (firmware accumulators)",
+                                      labels=base + ["event"])
         for s in samples:
             lv = [str(s["index"]), str(s.get("uuid", "")), str(s.get("pci", "")), self.node]
             info.add_metric(lv + [str(s.get("product")), str(s.get("gfx")), str(s.get("driver")),
@@ -259,9 +281,13 @@ class GpuCollector:
             for link, v in enumerate(s.get("xgmi_link_status") or []):
                 if v is not None:
                     xlink.add_metric(lv + [str(link)], v)
+            for event, key in (("replay", "pcie_replay_acc"), ("recovery", "pcie_recovery_acc"),
+                               ("nak_sent", "pcie_nak_sent_acc"), ("nak_received", "pcie_nak_rcvd_acc")):
+                if s.get(key) is not None:
+                    pcie_ev.add_metric(lv + [event], float(s[key]))
         yield info
         yield from fams.values()
-        for fam in (temp, ecc, energy, throttle, xgmi, xlink):
+        for fam in (temp, ecc, energy, throttle, xgmi, xlink, pcie_ev):
             yield fam
         yield from self._validation_metrics()
         dur = GaugeMetricFamily("amd_gpu_exporter_scrape_seconds", "time to sample all GPUs")

@@ -98,6 +98,9 @@ class FakeAmdSmi:
         r["average_gfx_activity"] = 10 * int(h)
         return r
 
+    def amdsmi_get_power_info(self, h):
+        return self._rec(h, "amdsmi_get_power_info")
+
     def amdsmi_get_gpu_vram_usage(self, h):
         return self._rec(h, "amdsmi_get_gpu_vram_usage")
 

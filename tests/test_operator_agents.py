@@ -153,6 +153,13 @@ def test_exporter_amdsmi_backend_metrics(tmp_path):
     assert _find(sm, "amd_gpu_validation_passed", step="gemm") == [1.0]
     assert _find(sm, "amd_gpu_validator_step_seconds", step="gemm") == [2.25]
     assert _find(sm, "amd_gpu_validator_step_seconds", step="report") == [7.5]
+    # PCIe / xGMI link state and the power cap, from the recorded MI355X amd-smi output
+    assert _find(sm, "amd_gpu_pcie_link_speed_gts", gpu=0) == [32.0]
+    assert _find(sm, "amd_gpu_pcie_link_width", gpu=0) == [16.0]
+    assert _find(sm, "amd_gpu_pcie_events_total", gpu=0, event="replay") == [0.0]
+    assert _find(sm, "amd_gpu_pcie_events_total", gpu=0, event="nak_received") == [0.0]
+    assert _find(sm, "amd_gpu_power_limit_watts", gpu=0) == [1400.0]
+    assert _find(sm, "amd_gpu_xgmi_link_width", gpu=0) == [16.0]
     # N/A fields (edge temperature) are omitted, not exported as 0
     assert not _find(sm, "amd_gpu_temperature_celsius", sensor="edge")
 

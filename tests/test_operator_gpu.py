@@ -55,6 +55,7 @@ def test_exporter_on_real_amdsmi():
     assert "amd_gpu_exporter_up 1.0" in text
     assert "amd_gpu_info{" in text and 'gfx="gfx950"' in text
     assert "amd_gpu_vram_total_bytes{" in text
+    assert "amd_gpu_pcie_link_width{" in text and "amd_gpu_power_limit_watts{" in text
     out = os.environ.get("AMDK8S_EVIDENCE_DIR")
     if out:
         os.makedirs(out, exist_ok=True)
