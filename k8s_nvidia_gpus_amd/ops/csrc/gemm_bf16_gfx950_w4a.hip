@@ -41,6 +41,10 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
 }  // namespace
 
+// SCHED: generated K-loop schedule; SCHED == kF16 runs the default schedule on fp16 operands
+// (v_mfma_f32_16x16x32_f16, fp16 C) — same fragment layout, LDS image and cycles as bf16.
+constexpr int kF16 = 16;
+
 template <int SCHED>
 __global__ void __launch_bounds__(NT, 1)
 amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
@@ -97,7 +101,8 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
     "v"(cbase)                                                                                 \
   : AMDK8S_W4A_CLOBBERS
   static_assert(AMDK8S_W4A_NUM_SCHEDULES == 3, "one branch per generated schedule");
-  if constexpr (SCHED == 0) asm volatile(AMDK8S_W4A_ASM_0 : AMDK8S_W4A_OPERANDS);
+  if constexpr (SCHED == kF16) asm volatile(AMDK8S_W4A_F16_ASM : AMDK8S_W4A_OPERANDS);
+  else if constexpr (SCHED == 0) asm volatile(AMDK8S_W4A_ASM_0 : AMDK8S_W4A_OPERANDS);
   else if constexpr (SCHED == 1) asm volatile(AMDK8S_W4A_ASM_1 : AMDK8S_W4A_OPERANDS);
   else asm volatile(AMDK8S_W4A_ASM_2 : AMDK8S_W4A_OPERANDS);
 #undef AMDK8S_W4A_OPERANDS
@@ -119,8 +124,9 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
   }
 }
 
-extern "C" int amdk8s_gemm_bf16_nt_w4a(const void* A, const void* B, void* C, int M, int N, int K,
-                                       int lda, int ldb, int ldc, hipStream_t stream) {
+namespace {
+int launch_w4a(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+               hipStream_t stream, bool f16) {
   if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
   if (M % BM || N % BN || K % BK) return (int)hipErrorInvalidValue;
   if (lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N) return (int)hipErrorInvalidValue;
@@ -134,17 +140,21 @@ extern "C" int amdk8s_gemm_bf16_nt_w4a(const void* A, const void* B, void* C, in
   // non-temporal C stores (AMDK8S_GEMM_NT_STORE=0 turns them off for A/B runs)
   const char* ntenv = getenv("AMDK8S_GEMM_NT_STORE");
   const int nt = !(ntenv && ntenv[0] == '0');
-  // K-loop schedule: the generator's default, or AMDK8S_W4A_SCHEDULE=<name> for A/B runs
+  // K-loop schedule: the generator's default, or AMDK8S_W4A_SCHEDULE=<name> for A/B runs (bf16)
   int sched = AMDK8S_W4A_DEFAULT_SCHEDULE;
   if (const char* e = getenv("AMDK8S_W4A_SCHEDULE")) {
     static const char* const names[] = AMDK8S_W4A_SCHEDULE_NAMES;
     for (int i = 0; i < AMDK8S_W4A_NUM_SCHEDULES; ++i)
       if (!strcmp(e, names[i])) sched = i;
   }
+  if (f16) sched = kF16;
   const uint16_t* a = (const uint16_t*)A;
   const uint16_t* b = (const uint16_t*)B;
   uint16_t* c = (uint16_t*)C;
-  if (sched == 1)
+  if (sched == kF16)
+    hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4a<kF16>, dim3(nwg), dim3(NT), 0, stream, a, b,
+                       c, M, N, K, lda, ldb, ldc, sb, nt);
+  else if (sched == 1)
     hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4a<1>, dim3(nwg), dim3(NT), 0, stream, a, b, c,
                        M, N, K, lda, ldb, ldc, sb, nt);
   else if (sched == 2)
@@ -154,4 +164,16 @@ extern "C" int amdk8s_gemm_bf16_nt_w4a(const void* A, const void* B, void* C, in
     hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4a<0>, dim3(nwg), dim3(NT), 0, stream, a, b, c,
                        M, N, K, lda, ldb, ldc, sb, nt);
   return (int)hipGetLastError();
+}
+}  // namespace
+
+extern "C" int amdk8s_gemm_bf16_nt_w4a(const void* A, const void* B, void* C, int M, int N, int K,
+                                       int lda, int ldb, int ldc, hipStream_t stream) {
+  return launch_w4a(A, B, C, M, N, K, lda, ldb, ldc, stream, false);
+}
+
+// fp16 operands and fp16 output (fp32 accumulation), same shape contract as the bf16 entry.
+extern "C" int amdk8s_gemm_f16_nt_w4a(const void* A, const void* B, void* C, int M, int N, int K,
+                                      int lda, int ldb, int ldc, hipStream_t stream) {
+  return launch_w4a(A, B, C, M, N, K, lda, ldb, ldc, stream, true);
 }

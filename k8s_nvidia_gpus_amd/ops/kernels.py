@@ -27,6 +27,7 @@ __all__ = [
     "library_path",
     "gemm_bf16_nt",
     "gemm_bf16",
+    "gemm_f16_nt",
     "gemm_shape_supported",
     "vector_add",
     "vector_add_bandwidth",
@@ -62,6 +63,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.amdk8s_gemm_bf16_nt_w4.restype = ci
     lib.amdk8s_gemm_bf16_nt_w4a.argtypes = [vp, vp, vp, ci, ci, ci, ci, ci, ci, vp]
     lib.amdk8s_gemm_bf16_nt_w4a.restype = ci
+    lib.amdk8s_gemm_f16_nt_w4a.argtypes = [vp, vp, vp, ci, ci, ci, ci, ci, ci, vp]
+    lib.amdk8s_gemm_f16_nt_w4a.restype = ci
     lib.amdk8s_gemm_fp8_nt.argtypes = [vp, vp, vp, ci, ci, ci, ci, ci, ci, vp]
     lib.amdk8s_gemm_fp8_nt.restype = ci
     lib.amdk8s_gemm_fp8_nt_f8a.argtypes = [vp, vp, vp, ci, ci, ci, ci, ci, ci, vp]
@@ -192,6 +195,33 @@ def gemm_bf16_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] =
     rc = fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
             a.stride(0), b.stride(0), out.stride(0), _stream_handle(a.device))
     _check(rc, f"amdk8s_gemm_bf16_nt[{variant}]")
+    return out
+
+
+def gemm_f16_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``out = a @ b.T`` in fp16 (fp32 accumulation, fp16 result) with the w4a kernel's generated
+    K-loop on ``v_mfma_f32_16x16x32_f16`` — the same cycles per MFMA as bf16 on gfx950.
+    Same shape contract as :func:`gemm_bf16_nt`."""
+    _require_gpu(a, "a")
+    _require_gpu(b, "b")
+    if a.dtype != torch.float16 or b.dtype != torch.float16:
+        raise TypeError("gemm_f16_nt expects fp16 operands")
+    if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[1]:
+        raise ValueError(f"shape mismatch: a {tuple(a.shape)} b {tuple(b.shape)}")
+    if a.stride(1) != 1 or b.stride(1) != 1:
+        raise ValueError("operands must have unit inner stride")
+    m, k = a.shape
+    n = b.shape[0]
+    if not gemm_shape_supported(m, n, k):
+        raise ValueError(f"gemm_f16_nt needs M,N % 256 == 0 and K % 64 == 0 (got {m}x{n}x{k})")
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.float16, device=a.device)
+    elif out.shape != (m, n) or out.dtype != torch.float16 or out.stride(1) != 1:
+        raise ValueError("bad out tensor")
+    rc = library().amdk8s_gemm_f16_nt_w4a(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+                                          a.stride(0), b.stride(0), out.stride(0),
+                                          _stream_handle(a.device))
+    _check(rc, "amdk8s_gemm_f16_nt_w4a")
     return out
 
 

@@ -24,6 +24,8 @@ int amdk8s_gemm_bf16_nt_w4(const void* A, const void* B, void* C, int M, int N, 
                            int ldb, int ldc, hipStream_t stream);
 int amdk8s_gemm_bf16_nt_w4a(const void* A, const void* B, void* C, int M, int N, int K, int lda,
                             int ldb, int ldc, hipStream_t stream);
+int amdk8s_gemm_f16_nt_w4a(const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                           int ldb, int ldc, hipStream_t stream);
 int amdk8s_gemm_bf16_nt_sample_check(const void* A, const void* B, const int* coords, float* out,
                                      int nsamples, int K, int lda, int ldb, hipStream_t stream);
 // k8s_nvidia_gpus_amd/ops/csrc/gemm_fp8_gfx950.hip

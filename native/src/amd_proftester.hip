@@ -11,8 +11,8 @@
 //                                       hbm-read, hbm-write   the read-only / write-only forms
 //   1006   FP64 pipe active             fp64           v_mfma_f64_16x16x4_f64 chains (loadgen.hip)
 //   1007   FP32 pipe active             fp32           v_pk_fma_f32 chains (loadgen.hip)
-//   1008   FP16 pipe active             tensor         (bf16 and f16 MFMAs take the same cycles on
-//                                                      gfx950: MI355X_MICROARCH.md § Matrix cores)
+//   1008   FP16 pipe active             tensor-fp16    fp16 MFMA GEMM: the w4a loop on
+//                                                      v_mfma_f32_16x16x32_f16 (gemm_bf16_gfx950_w4a.hip)
 //   1009   PCIe TX bytes                pcie-d2h       hipMemcpyAsync device → pinned host
 //   1010   PCIe RX bytes                pcie-h2d       hipMemcpyAsync pinned host → device
 //   1011/2 NVLink TX/RX bytes           xgmi           every ordered GPU pair over xGMI: SDMA peer
@@ -240,6 +240,20 @@ void test_flops(const std::string& test, int dev, const Options& o, hipStream_t 
   hipFree(sink);
 }
 
+int tensor_gemm(const std::string& test, const void* A, const void* B, void* C, int n, hipStream_t s) {
+  if (test == "tensor-fp8") return amdk8s_gemm_fp8_nt_f8a(A, B, C, n, n, n, n, n, n, s);
+  if (test == "tensor-fp16") return amdk8s_gemm_f16_nt_w4a(A, B, C, n, n, n, n, n, n, s);
+  return amdk8s_gemm_bf16_nt_w4a(A, B, C, n, n, n, n, n, n, s);
+}
+
+__global__ void bf16_to_f16(uint16_t* p, long n) {  // reinterpret the bf16 fill as fp16 data
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float f = __uint_as_float((uint32_t)p[i] << 16);
+    const _Float16 h = (_Float16)f;
+    p[i] = *reinterpret_cast<const uint16_t*>(&h);
+  }
+}
+
 void test_tensor(const std::string& test, int dev, const Options& o, hipStream_t s) {
   const bool fp8 = test == "tensor-fp8";
   const size_t S = o.gemm_size, esz = fp8 ? 1 : 2;
@@ -250,21 +264,20 @@ void test_tensor(const std::string& test, int dev, const Options& o, hipStream_t
   auto fill = fp8 ? amdk8s_fill_uniform_fp8 : amdk8s_fill_uniform_bf16;
   AMDK8S_HIP_CHECK((hipError_t)fill(A, (long)(S * S), 11 + dev, -1.f, 1.f, s));
   AMDK8S_HIP_CHECK((hipError_t)fill(B, (long)(S * S), 12 + dev, -1.f, 1.f, s));
+  if (test == "tensor-fp16") {
+    hipLaunchKernelGGL(bf16_to_f16, dim3(4096), dim3(256), 0, s, (uint16_t*)A, (long)(S * S));
+    hipLaunchKernelGGL(bf16_to_f16, dim3(4096), dim3(256), 0, s, (uint16_t*)B, (long)(S * S));
+  }
   const int n = (int)S;
   Result res;
-  int rc = fp8 ? amdk8s_gemm_fp8_nt_f8a(A, B, C, n, n, n, n, n, n, s)
-               : amdk8s_gemm_bf16_nt_w4a(A, B, C, n, n, n, n, n, n, s);
+  int rc = tensor_gemm(test, A, B, C, n, s);
   if (rc != 0) {
     res.test = test;
     res.device = dev;
     res.note = "GEMM shape rejected (size must be a multiple of 256)";
     emit(res);
   } else {
-    auto launch = [&] {
-      const int r = fp8 ? amdk8s_gemm_fp8_nt_f8a(A, B, C, n, n, n, n, n, n, s)
-                        : amdk8s_gemm_bf16_nt_w4a(A, B, C, n, n, n, n, n, n, s);
-      AMDK8S_HIP_CHECK((hipError_t)r);
-    };
+    auto launch = [&] { AMDK8S_HIP_CHECK((hipError_t)tensor_gemm(test, A, B, C, n, s)); };
     emit(from_rate(test, dev, "TFLOPS", measure(s, launch, 2.0 * S * S * S, o), 1e-12));
   }
   hipFree(A);
@@ -441,12 +454,13 @@ void test_xgmi(const std::vector<int>& devs, const Options& o) {
   }
 }
 
-const char* kAllTests[] = {"tensor", "tensor-fp8", "hbm-read", "hbm-write", "hbm-copy",
+const char* kAllTests[] = {"tensor", "tensor-fp16", "tensor-fp8", "hbm-read", "hbm-write", "hbm-copy",
                            "fp32", "fp64", "pcie-h2d", "pcie-d2h", "xgmi"};
 
 std::string resolve(const std::string& t) {
   // dcgmproftester field IDs → tests
-  if (t == "1004" || t == "1008") return "tensor";
+  if (t == "1004") return "tensor";
+  if (t == "1008") return "tensor-fp16";
   if (t == "1005") return "hbm-copy";
   if (t == "1006") return "fp64";
   if (t == "1007") return "fp32";
@@ -465,7 +479,7 @@ void run_device(int dev, const Options& o, Barrier* bar) {
   for (const auto& t : o.tests) {
     if (t == "xgmi") continue;
     bar->wait();
-    if (t == "tensor" || t == "tensor-fp8") test_tensor(t, dev, o, s);
+    if (t.rfind("tensor", 0) == 0) test_tensor(t, dev, o, s);
     else if (t.rfind("hbm-", 0) == 0) test_hbm(t, dev, o, s, p.multiProcessorCount);
     else if (t == "fp32" || t == "fp64") test_flops(t, dev, o, s, p.multiProcessorCount);
     else if (t.rfind("pcie-", 0) == 0) test_pcie(t, dev, o, s, p.multiProcessorCount);
@@ -488,7 +502,7 @@ void usage() {
       "usage: amd-proftester [-t TEST[,TEST...]|FIELD] [--device D] [--duration S] [--iters N]\n"
       "                      [--hbm-bytes B] [--pcie-bytes B] [--xgmi-bytes B] [--gemm-size S]\n"
       "                      [--settle-ms MS] [--json] [--list]\n"
-      "tests: tensor tensor-fp8 hbm-read hbm-write hbm-copy fp32 fp64 pcie-h2d pcie-d2h xgmi all\n"
+      "tests: tensor tensor-fp16 tensor-fp8 hbm-read hbm-write hbm-copy fp32 fp64 pcie-h2d pcie-d2h xgmi all\n"
       "dcgmproftester field IDs: 1004 1005 1006 1007 1008 1009 1010 1011 1012\n");
 }
 

@@ -26,7 +26,8 @@ def test_kernel_library_exports(built):
     syms = _nm(B.KERNEL_LIB)
     for s in ["amdk8s_gemm_bf16_nt", "amdk8s_gemm_bf16_nt_sample_check", "amdk8s_vector_add_f32",
               "amdk8s_vector_add_f32_bw", "amdk8s_fill_uniform_bf16", "amdk8s_vector_add_blocks",
-              "amdk8s_hbm_stream", "amdk8s_hbm_stream_variant", "amdk8s_fp32_fma", "amdk8s_fp64_mfma"]:
+              "amdk8s_hbm_stream", "amdk8s_hbm_stream_variant", "amdk8s_fp32_fma", "amdk8s_fp64_mfma",
+              "amdk8s_gemm_f16_nt_w4a"]:
         assert s in syms, s
 
 
@@ -79,7 +80,7 @@ def test_proftester_lists_tests_and_rejects_unknown_without_a_gpu(built):
     exe = str(B.NATIVE_BIN / "amd-proftester")
     p = subprocess.run([exe, "--list"], capture_output=True, text=True, timeout=60)
     assert p.returncode == 0
-    assert p.stdout.split() == ["tensor", "tensor-fp8", "hbm-read", "hbm-write", "hbm-copy", "fp32",
+    assert p.stdout.split() == ["tensor", "tensor-fp16", "tensor-fp8", "hbm-read", "hbm-write", "hbm-copy", "fp32",
                                 "fp64", "pcie-h2d", "pcie-d2h", "xgmi"]
     p = subprocess.run([exe, "-t", "hbm-copy,bogus"], capture_output=True, text=True, timeout=60)
     assert p.returncode == 2 and "unknown test 'bogus'" in p.stderr

@@ -330,12 +330,12 @@ def test_proftester_native_protocol():
 
     from k8s_nvidia_gpus_amd.ops import build as B
 
-    p = subprocess.run([str(B.NATIVE_BIN / "amd-proftester"), "-t", "1005,1006,1007,1010,xgmi",
+    p = subprocess.run([str(B.NATIVE_BIN / "amd-proftester"), "-t", "1005,1006,1007,1008,1010,xgmi",
                         "--iters", "5", "--settle-ms", "20", "--hbm-bytes", "1G", "--json"],
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stdout + p.stderr
     docs = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
-    assert {d["test"] for d in docs} == {"hbm-copy", "fp64", "fp32", "pcie-h2d", "xgmi"}
+    assert {d["test"] for d in docs} == {"hbm-copy", "fp64", "fp32", "tensor-fp16", "pcie-h2d", "xgmi"}
     assert all(d["passed"] for d in docs)
     assert p.stdout.rstrip().endswith("Test PASSED\nDone")
 
@@ -361,3 +361,26 @@ def test_gemm_tile_order_per_partition_is_bitwise_identical(K, dev, xcds, m, n, 
     out8 = torch.full((m, n), float("nan"), dtype=torch.bfloat16, device=dev)
     K.gemm_fp8_nt(a8, b8, out=out8)
     assert torch.equal(out8, ref8), xcds
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 768, 320), (2304, 1280, 1024), (4096, 4096, 4096)])
+def test_gemm_f16_matches_fp32(K, dev, m, n, k):
+    g = torch.Generator(device=dev).manual_seed(11)
+    a = (torch.rand((m, k), generator=g, device=dev) * 2 - 1).half()
+    b = (torch.rand((n, k), generator=g, device=dev) * 2 - 1).half()
+    out = torch.full((m, n), float("nan"), dtype=torch.float16, device=dev)
+    K.gemm_f16_nt(a, b, out=out)
+    ref = a.float() @ b.float().t()
+    torch.testing.assert_close(out.float(), ref, rtol=2e-3, atol=2e-3 * (k ** 0.5))
+    # the fp16 kernel is the bf16 kernel's loop: identical sums, only the operand format differs
+    ab, bb = a.to(torch.bfloat16), b.to(torch.bfloat16)
+    assert torch.isfinite(K.gemm_bf16_nt(ab, bb, variant="w4a").float()).all()
+
+
+def test_gemm_f16_rejects_bad_dtype_and_shape(K, dev):
+    a = torch.zeros((256, 64), dtype=torch.bfloat16, device=dev)
+    with pytest.raises(TypeError):
+        K.gemm_f16_nt(a, a)
+    h = torch.zeros((256, 96), dtype=torch.float16, device=dev)
+    with pytest.raises(ValueError):
+        K.gemm_f16_nt(h, h)

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--sizes", type=int, nargs="+", default=[8192])
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--fp16", action="store_true", help="also A/B the fp16 kernel against hipBLASLt fp16")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     print(f"device {torch.cuda.get_device_name(dev)} torch {torch.__version__}")
@@ -44,6 +45,11 @@ def main():
             "amdk8s w4a": lambda: K.gemm_bf16_nt(a, b, out=c, variant="w4a"),
             "torch.matmul(hipBLASLt)": lambda: torch.matmul(a, b.t(), out=c),
         }
+        if args.fp16:
+            ah, bh = a.half(), b.half()
+            ch = torch.empty((s, s), dtype=torch.float16, device=dev)
+            arms["amdk8s w4a fp16"] = lambda: K.gemm_f16_nt(ah, bh, out=ch)
+            arms["torch.matmul fp16 (hipBLASLt)"] = lambda: torch.matmul(ah, bh.t(), out=ch)
         for fn in arms.values():
             time_arm(fn, 5)
         res = {k: [] for k in arms}
@@ -64,6 +70,13 @@ def main():
             unwritten = int(torch.isnan(out).sum().item())
             err = (out.float() - ref.float()).abs().max().item()
             print(f"{s}^3 max |amdk8s {v} - hipBLASLt| = {err:.4e}  (NaN/unwritten: {unwritten})")
+        if args.fp16:
+            out = torch.full((s, s), float("nan"), dtype=torch.float16, device=dev)
+            K.gemm_f16_nt(ah, bh, out=out)
+            ref16 = torch.matmul(ah, bh.t())
+            err = (out.float() - ref16.float()).abs().max().item()
+            print(f"{s}^3 max |amdk8s fp16 - hipBLASLt fp16| = {err:.4e}  "
+                  f"(NaN/unwritten: {int(torch.isnan(out).sum().item())})")
         sys.stdout.flush()
 
 

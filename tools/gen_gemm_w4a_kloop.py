@@ -2,7 +2,7 @@
 """Generate the hand-scheduled gfx950 assembly bodies of the w4a bf16 GEMM kernel.
 
 Writes ``k8s_nvidia_gpus_amd/ops/csrc/gemm_bf16_gfx950_w4a_kloop.inc``: one ``asm volatile`` body
-per K-loop schedule (prologue DMA, the K-loop unrolled by the two LDS-buffer parities, the
+per K-loop schedule (plus ``AMDK8S_W4A_F16_ASM``: the default schedule on fp16 operands) (prologue DMA, the K-loop unrolled by the two LDS-buffer parities, the
 accumulator → bf16 → LDS C-image epilogue), every register explicit, so no compiler-inserted
 instruction sits between the MFMAs. The kernel (``gemm_bf16_gfx950_w4a.hip``) instantiates one
 template per schedule; ``AMDK8S_W4A_SCHEDULE=<name>`` picks one for A/B runs.
@@ -323,6 +323,15 @@ def main():
             for ln in lines:
                 f.write(f'  "{ln}\\n" \\\n')
             f.write("  \"\"\n")
+        # fp16 operands: the same loop with the f16 MFMA (identical fragment layout and cycles on
+        # gfx950) and an fp32 -> fp16 epilogue conversion, default schedule only
+        lines = [ln.replace("v_mfma_f32_16x16x32_bf16", "v_mfma_f32_16x16x32_f16")
+                 .replace("v_cvt_pk_bf16_f32", "v_cvt_pk_f16_f32") for ln in kernel_asm(DEFAULT)]
+        f.write(f"\n// {DEFAULT}, fp16 operands and output: {sum(1 for l in lines if 'v_mfma' in l)} MFMAs\n"
+                "#define AMDK8S_W4A_F16_ASM \\\n")
+        for ln in lines:
+            f.write(f'  "{ln}\\n" \\\n')
+        f.write("  \"\"\n")
         f.write("\n#define AMDK8S_W4A_CLOBBERS \\\n")
         for i in range(0, len(clob), 12):
             f.write("  " + ", ".join(clob[i:i + 12]) + (", \\\n" if i + 12 < len(clob) else "\n"))
