@@ -91,18 +91,21 @@ def test_parallel_bench_cli_under_torchrun_gloo():
     assert doc["passed"] and doc["world"] == 2 and doc["wrong"] == 0
 
 
-def test_bench_py_distributed_contract_on_cpu():
-    """bench.py --cpu-smoke under torchrun (gloo): one JSON line, MAX over ranks, N-rank aggregate."""
-    p = _torchrun(["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--cpu-smoke",
-                   "--size", "256"], 2)
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_py_distributed_contract_on_cpu(world):
+    """bench.py --cpu-smoke under torchrun (gloo): one JSON line, MAX over ranks, N-rank aggregate.
+    world 8 rehearses the driver's 8-GPU launch shape (8 ranks, one per GPU)."""
+    p = _torchrun(["bench.py", "--gpus", str(world), "--steps", "2", "--warmup", "1", "--cpu-smoke",
+                   "--size", "256"], world)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout
     doc = json.loads(lines[0])
-    assert doc["n_gpus"] == 2 and doc["steps"] == 2 and doc["warmup"] == 1
+    assert doc["n_gpus"] == world and doc["steps"] == 2 and doc["warmup"] == 1
     assert doc["higher_is_better"] is True and doc["scaling"] == "weak"
-    assert doc["config"]["parallelism"] == "dp2"
-    assert len(doc["tflops_per_rank"]) == 2
+    assert doc["config"]["parallelism"] == f"dp{world}" and doc["config"]["global_batch"] == world
+    assert len(doc["tflops_per_rank"]) == world
+    assert doc["allreduce_busbw_gbps"] is not None
     assert doc["value"] == pytest.approx(sum(doc["tflops_per_rank"]), rel=0.6)
 
 
