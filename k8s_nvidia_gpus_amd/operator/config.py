@@ -50,6 +50,7 @@ DEFAULTS: Dict[str, Any] = {
         "gemmFp8": True,             # also run the fp8 (OCP e4m3) MFMA GEMM
         "gemmFp8MinTflops": 1800,
         "rocprof": False,            # run the GEMM step under rocprofv3 --kernel-trace --stats
+        "rocprofCounters": False,    # + one rocprofv3 --pmc pass: MFMA util, clock, L2 hit rate
         "bandwidth": True,           # amd-proftester: HBM copy, PCIe H2D/D2H, xGMI peer copies
         "hbmMinGBps": 4000,          # HBM3E copy (read + write bytes), per GPU
         "pcieMinGBps": 20,           # pinned host <-> device, each direction, per GPU

@@ -308,6 +308,9 @@ class GpuCollector:
         busbw = GaugeMetricFamily("amd_gpu_validator_allreduce_busbw_gbps",
                                   "RCCL all-reduce bus bandwidth measured by the validator",
                                   labels=["node", "ngpus"])
+        prof = GaugeMetricFamily("amd_gpu_validator_gemm_profile",
+                                 "rocprofv3 counters of the validator GEMM (mfma_util_pct, clock_ghz, "
+                                 "l2_hit_pct)", labels=["node", "quantity"])
         bw = GaugeMetricFamily("amd_gpu_validator_bandwidth_gbps",
                                "HBM / PCIe / xGMI bandwidth measured by the validator (amd-proftester)",
                                labels=["node", "gpu", "test", "peer", "engine"])
@@ -330,6 +333,10 @@ class GpuCollector:
                 for r in (v.get("fp8") or {}).get("devices", []):
                     if r.get("tflops") is not None:
                         tflops8.add_metric([self.node, str(r.get("device"))], float(r["tflops"]))
+                rc = v.get("rocprof_counters") or {}
+                for q in ("mfma_util_pct", "clock_ghz", "l2_hit_pct"):
+                    if rc.get(q) is not None:
+                        prof.add_metric([self.node, q], float(rc[q]))
             if step == "rccl" and isinstance(v, dict) and v.get("peak_busbw_gbps") is not None:
                 busbw.add_metric([self.node, str(v.get("ngpus"))], float(v["peak_busbw_gbps"]))
             if step == "bandwidth" and isinstance(v, dict):
@@ -344,6 +351,7 @@ class GpuCollector:
         yield tflops
         yield tflops8
         yield busbw
+        yield prof
         yield bw
         yield secs
 

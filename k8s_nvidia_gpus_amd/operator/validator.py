@@ -101,6 +101,56 @@ def rocprof_kernel_stats(prof_dir: str) -> List[dict]:
     return sorted(rows, key=lambda r: -r["percent"])
 
 
+# One rocprofv3 --pmc pass over the validator GEMM (BASELINE.json config 3: "with rocprof counters").
+# Within gfx950's per-pass limits (≤ 8 SQ, ≤ 4 TCC, ≤ 2 GRBM counters; MI355X_MICROARCH.md).
+GEMM_COUNTERS = ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_BF16",
+                 "GRBM_GUI_ACTIVE", "TCC_HIT_sum", "TCC_MISS_sum")
+
+
+def rocprof_counter_summary(prof_dir: str, cus: int, kernel_filter: str = "gemm") -> Dict:
+    """Median over the profiled GEMM dispatches of rocprofv3's counter_collection.csv, turned into
+    the numbers the validator reports: MFMA utilisation (busy MFMA cycles per SIMD-cycle), the
+    effective clock (GRBM_GUI_ACTIVE is summed over the XCDs: cycles = GRBM / XCDs), the L2 hit rate,
+    and the MFMA FLOPs the hardware counted (SQ_INSTS_VALU_MFMA_MOPS_* × 512), which must equal
+    2·M·N·K — a check that the counters measure the kernel that ran."""
+    import csv
+    import glob
+    import statistics
+
+    per: Dict[str, Dict[str, float]] = {}
+    for f in glob.glob(os.path.join(prof_dir, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                name = r.get("Kernel_Name", "")
+                if kernel_filter not in name or "sample" in name:
+                    continue
+                d = per.setdefault(r["Dispatch_Id"], {})
+                d[r["Counter_Name"]] = float(r["Counter_Value"])
+                try:
+                    d["duration_ns"] = float(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                except (KeyError, ValueError):
+                    pass
+    if not per:
+        return {}
+    keys = set().union(*per.values())
+    med = {k: statistics.median(d[k] for d in per.values() if k in d) for k in keys}
+    xcds = max(1, (cus + 16) // 32)
+    out: Dict = {"dispatches": len(per), "counters": {k: med[k] for k in sorted(keys)}}
+    cycles = med.get("GRBM_GUI_ACTIVE", 0) / xcds
+    if cycles and med.get("duration_ns"):
+        out["clock_ghz"] = round(cycles / med["duration_ns"], 3)
+    if cycles and "SQ_VALU_MFMA_BUSY_CYCLES" in med:
+        out["mfma_util_pct"] = round(100 * med["SQ_VALU_MFMA_BUSY_CYCLES"] / (cus * 4 * cycles), 2)
+    hit, miss = med.get("TCC_HIT_sum"), med.get("TCC_MISS_sum")
+    if hit is not None and miss is not None and hit + miss > 0:
+        out["l2_hit_pct"] = round(100 * hit / (hit + miss), 2)
+    if "SQ_INSTS_VALU_MFMA_MOPS_BF16" in med:
+        out["mfma_flop"] = med["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512
+        if med.get("duration_ns"):
+            out["tflops_profiled"] = round(out["mfma_flop"] / med["duration_ns"] / 1e3, 1)
+    return out
+
+
 @dataclass
 class StepResult:
     step: str
@@ -213,10 +263,28 @@ class Validator:
             detail["rocprof_kernels"] = rocprof_kernel_stats(prof_dir)
         return ok, detail, reason.strip()
 
+    def _gemm_counters(self, size: int, cus: int) -> Dict:
+        """A separate short rocprofv3 --pmc pass (counters never share a run with tracing domains)."""
+        prof_dir = self._path("gemm-rocprof-counters")
+        argv = ["rocprofv3", "--kernel-trace", "--pmc", *GEMM_COUNTERS, "-d", prof_dir, "-o", "pmc",
+                "--output-format", "csv", "--", self._bin("amd-gemm-validator"), "--size", str(size),
+                "--iters", "10", "--settle-ms", "50", "--json"]
+        rc, out = self.run_cmd(argv, 300)
+        summary = rocprof_counter_summary(prof_dir, cus) if rc == 0 else {}
+        if rc != 0:
+            summary["error"] = f"rocprofv3 --pmc rc={rc}: {out.strip()[-200:]}"
+        elif summary.get("mfma_flop") is not None:
+            # the hardware's MFMA FLOP count must match the GEMM that was asked for
+            summary["flop_matches_shape"] = summary["mfma_flop"] == 2.0 * size ** 3
+        return summary
+
     def step_gemm(self) -> StepResult:
         size = int(self.vcfg["gemmSize"])
         rocprof = bool(self.vcfg.get("rocprof"))
         ok, detail, reason = self._gemm_run("bf16", size, float(self.vcfg["gemmMinTflops"]), rocprof)
+        if self.vcfg.get("rocprofCounters") and ok:
+            cus = min((int(d.get("cus", 256)) for d in detail["devices"]), default=256)
+            detail["rocprof_counters"] = self._gemm_counters(size, cus)
         if self.vcfg.get("gemmFp8"):
             ok8, detail8, reason8 = self._gemm_run("fp8", size, float(self.vcfg["gemmFp8MinTflops"]),
                                                    rocprof)

@@ -237,10 +237,10 @@ int main(int argc, char** argv) {
     agg += r.tflops;
     ok = ok && r.ok;
     if (o.json)
-      std::printf("{\"check\": \"gemm_%s\", \"device\": %d, \"arch\": \"%s\", \"m\": %d, \"n\": %d, "
-                  "\"k\": %d, \"ms_per_iter\": %.4f, \"tflops\": %.2f, \"bad_samples\": %d, "
-                  "\"passed\": %s}\n", o.dtype.c_str(), r.device, r.arch.c_str(), o.m, o.n, o.k, r.ms_per_iter,
-                  r.tflops, r.bad, r.ok ? "true" : "false");
+      std::printf("{\"check\": \"gemm_%s\", \"device\": %d, \"arch\": \"%s\", \"cus\": %d, \"m\": %d, "
+                  "\"n\": %d, \"k\": %d, \"ms_per_iter\": %.4f, \"tflops\": %.2f, \"bad_samples\": %d, "
+                  "\"passed\": %s}\n", o.dtype.c_str(), r.device, r.arch.c_str(), r.cus, o.m, o.n, o.k,
+                  r.ms_per_iter, r.tflops, r.bad, r.ok ? "true" : "false");
   }
   std::printf("aggregate: %.1f TFLOPS over %zu device(s) (%.1f TFLOPS/GPU)\n", agg, devs.size(),
               agg / devs.size());

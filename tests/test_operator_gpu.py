@@ -65,7 +65,7 @@ def test_exporter_on_real_amdsmi():
 
 def test_validator_chain_with_native_binaries(tmp_path, native):
     cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {gemmSize: 4096, gemmMinTflops: 600, "
-                           "rccl: false, pluginTest: false}\n")
+                           "rccl: false, pluginTest: false, rocprofCounters: true}\n")
     v = Validator(cfg, str(tmp_path), bin_dir=str(native))
     for step in ("driver", "vectoradd", "gemm", "bandwidth"):
         r = v.run_step(step)
@@ -74,6 +74,9 @@ def test_validator_chain_with_native_binaries(tmp_path, native):
     assert v.run_step("report").passed
     gemm = json.loads((tmp_path / "gemm.json").read_text())
     assert all(d["tflops"] > 600 for d in gemm["devices"])
+    pmc = gemm["rocprof_counters"]
+    assert pmc.get("flop_matches_shape") is True, pmc  # MFMA FLOPs counted == 2·4096³
+    assert 50 < pmc["mfma_util_pct"] <= 100 and 1.0 < pmc["clock_ghz"] < 2.5
     out = os.environ.get("AMDK8S_EVIDENCE_DIR")
     if out:
         os.makedirs(out, exist_ok=True)

@@ -359,3 +359,52 @@ def test_exporter_publishes_bandwidth_results(tmp_path, cfg):
     text = generate_latest(ex.make_registry(col)).decode()
     assert 'amd_gpu_validator_bandwidth_gbps{engine="",gpu="0",node="node-a",peer="",test="hbm-copy"}' in text
     assert 'test="pcie-h2d"' in text and 'amd_gpu_validation_passed{node="node-a",step="bandwidth"} 1.0' in text
+
+
+# ----------------------------------------------------------------------------- rocprof counters
+PMC_DIR = REPO / "profiles/r02_session2/pmc_validator"
+
+
+def test_rocprof_counter_summary_on_real_mi355x_csv():
+    from k8s_nvidia_gpus_amd.operator.validator import rocprof_counter_summary
+
+    s = rocprof_counter_summary(str(PMC_DIR), cus=256)
+    assert s["dispatches"] >= 80  # settle + warmup + timed launches of the 8192³ GEMM
+    assert s["mfma_flop"] == 2.0 * 8192 ** 3  # the hardware counted exactly the requested GEMM
+    assert 1.5 < s["clock_ghz"] < 2.4 and 70 < s["mfma_util_pct"] < 100 and 60 < s["l2_hit_pct"] < 100
+    assert 1300 < s["tflops_profiled"] < 2000
+
+
+def test_gemm_step_runs_a_counter_pass(tmp_path):
+    import shutil
+
+    cfg = load_config(text="validator: {gemmMinTflops: 900, rocprofCounters: true, gemmFp8: false}\n")
+    gemm_log = GEMM_LOG.replace('"arch": "gfx950:sramecc+:xnack-", ', '"arch": "gfx950:sramecc+:xnack-", "cus": 256, ')
+    calls = []
+
+    def runner(argv, timeout):
+        calls.append(list(argv))
+        if argv[0] == "rocprofv3":
+            assert "--pmc" in argv and "--sys-trace" not in argv  # counters never share a traced run
+            d = argv[argv.index("-d") + 1]
+            shutil.copytree(PMC_DIR, d)
+            return 0, (PMC_DIR / "pmc.log").read_text()
+        return 0, gemm_log
+
+    v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=runner)
+    g = v.run_step("gemm")
+    assert g.passed, g.reason
+    rc = g.detail["rocprof_counters"]
+    assert rc["flop_matches_shape"] is True and rc["mfma_util_pct"] > 70
+    pmc = calls[-1]
+    assert pmc[pmc.index("--pmc") + 1:pmc.index("-d")] == ["SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES",
+                                                           "SQ_INSTS_VALU_MFMA_MOPS_BF16", "GRBM_GUI_ACTIVE",
+                                                           "TCC_HIT_sum", "TCC_MISS_sum"]
+
+    from prometheus_client import generate_latest
+
+    from k8s_nvidia_gpus_amd.operator import exporter as ex
+
+    col = ex.GpuCollector(ex.SysfsBackend(str(tmp_path / "nosys")), "n1", str(tmp_path))
+    text = generate_latest(ex.make_registry(col)).decode()
+    assert 'amd_gpu_validator_gemm_profile{node="n1",quantity="mfma_util_pct"}' in text
