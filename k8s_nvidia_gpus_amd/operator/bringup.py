@@ -214,7 +214,7 @@ def rehearse(cfg: OperatorConfig, bin_dir: str, workdir: Optional[str] = None, r
         if validate:
             def validator_chain():
                 out = {}
-                for s in ("vectoradd", "gemm", "bandwidth", "rccl"):
+                for s in ("vectoradd", "gemm", "bandwidth", "stress", "rccl"):
                     r = v.run_step(s)
                     out[s] = {"passed": r.passed, "duration_s": r.detail.get("duration_s"),
                               "reason": r.reason}

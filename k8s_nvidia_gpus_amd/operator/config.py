@@ -55,6 +55,10 @@ DEFAULTS: Dict[str, Any] = {
         "hbmMinGBps": 4000,          # HBM3E copy (read + write bytes), per GPU
         "pcieMinGBps": 20,           # pinned host <-> device, each direction, per GPU
         "xgmiMinGBps": 30,           # each ordered GPU pair, SDMA peer copy (>= 2 GPUs)
+        "stress": False,             # sustained MFMA load + amd-smi telemetry (DCGM diag level 3)
+        "stressSeconds": 30,
+        "stressMinFraction": 0.85,   # every 100 ms window >= this x the mean rate (no throttle cliffs)
+        "stressMaxHotspotC": 105,
         "rccl": True,
         "rcclMinBusbwGBps": 100,
         "pluginTest": True,

@@ -311,6 +311,10 @@ class GpuCollector:
         prof = GaugeMetricFamily("amd_gpu_validator_gemm_profile",
                                  "rocprofv3 counters of the validator GEMM (mfma_util_pct, clock_ghz, "
                                  "l2_hit_pct)", labels=["node", "quantity"])
+        stress = GaugeMetricFamily("amd_gpu_validator_stress",
+                                   "sustained-load stress result per GPU (tflops, tflops_min_window, "
+                                   "hotspot_max_c, power_mean_w, gfxclk_mean_mhz)",
+                                   labels=["node", "gpu", "quantity"])
         bw = GaugeMetricFamily("amd_gpu_validator_bandwidth_gbps",
                                "HBM / PCIe / xGMI bandwidth measured by the validator (amd-proftester)",
                                labels=["node", "gpu", "test", "peer", "engine"])
@@ -339,6 +343,12 @@ class GpuCollector:
                         prof.add_metric([self.node, q], float(rc[q]))
             if step == "rccl" and isinstance(v, dict) and v.get("peak_busbw_gbps") is not None:
                 busbw.add_metric([self.node, str(v.get("ngpus"))], float(v["peak_busbw_gbps"]))
+            if step == "stress" and isinstance(v, dict):
+                for gpu, g in (v.get("gpus") or {}).items():
+                    for q in ("tflops", "tflops_min_window", "hotspot_max_c", "power_mean_w",
+                              "gfxclk_mean_mhz"):
+                        if g.get(q) is not None:
+                            stress.add_metric([self.node, str(gpu), q], float(g[q]))
             if step == "bandwidth" and isinstance(v, dict):
                 for r in v.get("results", []):
                     if r.get("skipped") or r.get("value") is None:
@@ -352,6 +362,7 @@ class GpuCollector:
         yield tflops8
         yield busbw
         yield prof
+        yield stress
         yield bw
         yield secs
 

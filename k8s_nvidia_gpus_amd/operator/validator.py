@@ -13,6 +13,9 @@ the previous one's marker under ``/run/amd/validations``:
             TFLOPS ≥ floor per precision
   bandwidth amd-proftester (the dcgmproftester counterpart): HBM3E copy, PCIe H2D / D2H and, with
             ≥ 2 GPUs, every xGMI peer pair — verified copies, GB/s ≥ floor per link type
+  stress    (optional, DCGM diag level 3's targeted stress) every GPU under a sustained MFMA load
+            for stressSeconds while amd-smi telemetry is sampled: no uncorrectable ECC error, no
+            100 ms window below stressMinFraction of the mean rate, hotspot ≤ stressMaxHotspotC
   rccl      RCCL all-reduce over xGMI across all GPUs of the node: exact sums + bus bandwidth floor
   plugin    a pod requesting amd.com/gpu: 1 is scheduled THROUGH the device plugin and passes
   report    node label amd.com/gpu.validated=true|false, validator-ready marker
@@ -37,7 +40,7 @@ from .config import OperatorConfig
 
 log = logging.getLogger("amd-gpu-validator")
 
-STEPS = ("driver", "runtime", "vectoradd", "gemm", "bandwidth", "rccl", "plugin", "report")
+STEPS = ("driver", "runtime", "vectoradd", "gemm", "bandwidth", "stress", "rccl", "plugin", "report")
 LABEL_VALIDATED = "amd.com/gpu.validated"
 
 Runner = Callable[[Sequence[str], float], Tuple[int, str]]
@@ -167,8 +170,10 @@ class StepResult:
 class Validator:
     def __init__(self, config: OperatorConfig, marker_dir: str = "/run/amd/validations",
                  bin_dir: Optional[str] = None, runner: Runner = default_runner, root: str = "/",
-                 kube=None, node_name: Optional[str] = None, driver_wait: float = 120):
+                 kube=None, node_name: Optional[str] = None, driver_wait: float = 120,
+                 telemetry: Optional[Callable[[], List[Dict]]] = None):
         self.cfg = config
+        self.telemetry = telemetry  # per-GPU samples for the stress step (default: amd-smi)
         self.driver_wait = driver_wait  # kfd-probe --wait: how long the driver may take to appear
         self.vcfg = config.section("validator")
         self.marker_dir = marker_dir
@@ -324,6 +329,92 @@ class Validator:
         return StepResult("bandwidth", bool(ok), {"results": docs, "min_by_test_gbps": summary,
                                                   "floors_gbps": floors}, reason)
 
+    def _telemetry_fn(self) -> Optional[Callable[[], List[Dict]]]:
+        if self.telemetry is not None:
+            return self.telemetry
+        try:
+            from .exporter import AmdSmiBackend
+
+            return AmdSmiBackend().samples
+        except Exception as e:  # noqa: BLE001 - no amd-smi: the load still runs, unmonitored
+            log.warning("no amd-smi telemetry for the stress step: %s", e)
+            return None
+
+    def step_stress(self) -> StepResult:
+        import threading
+
+        secs = float(self.vcfg["stressSeconds"])
+        frac = float(self.vcfg["stressMinFraction"])
+        tmax = float(self.vcfg["stressMaxHotspotC"])
+        sample = self._telemetry_fn()
+        samples: List[List[Dict]] = []
+        stop = threading.Event()
+
+        def poll():
+            while not stop.is_set():
+                try:
+                    samples.append(sample())
+                except Exception as e:  # noqa: BLE001
+                    log.debug("telemetry sample failed: %s", e)
+                stop.wait(1.0)
+
+        th = threading.Thread(target=poll, daemon=True) if sample else None
+        if th:
+            th.start()
+        try:
+            rc, out = self.run_cmd([self._bin("amd-proftester"), "-t", "tensor", "--duration",
+                                    str(secs), "--json"], secs + 300)
+        finally:
+            stop.set()
+            if th:
+                th.join(5)
+        if sample:  # one more snapshot after the load: ECC counters raised at its very end count too
+            try:
+                samples.append(sample())
+            except Exception as e:  # noqa: BLE001
+                log.debug("telemetry sample failed: %s", e)
+        docs = [d for d in json_lines(out) if d.get("check") == "proftester" and d.get("test") == "tensor"]
+        problems = []
+        per_gpu: Dict[str, Dict] = {}
+        for d in docs:
+            g = per_gpu.setdefault(str(d["device"]), {})
+            g.update(tflops=d["value"], tflops_min_window=d["min"], seconds=d["seconds"])
+            if d["value"] <= 0 or d["min"] < frac * d["value"]:
+                problems.append(f"GPU {d['device']}: 100 ms window {d['min']:.0f} < {frac:.2f} x "
+                                f"mean {d['value']:.0f} TFLOPS")
+        if len(samples) >= 1:
+            first = {str(x.get("index")): x for x in samples[0]}
+            last = {str(x.get("index")): x for x in samples[-1]}
+            for idx, x in last.items():
+                g = per_gpu.setdefault(idx, {})
+                temps = [s_.get("temp_hotspot") for snap in samples for s_ in snap
+                         if str(s_.get("index")) == idx and s_.get("temp_hotspot") is not None]
+                power = [s_.get("power_w") for snap in samples for s_ in snap
+                         if str(s_.get("index")) == idx and s_.get("power_w") is not None]
+                clocks = [s_.get("gfxclk_mhz") for snap in samples for s_ in snap
+                          if str(s_.get("index")) == idx and s_.get("gfxclk_mhz") is not None]
+                if temps:
+                    g["hotspot_max_c"] = max(temps)
+                    if max(temps) > tmax:
+                        problems.append(f"GPU {idx}: hotspot {max(temps):.0f} C > {tmax:.0f} C")
+                if power:
+                    g["power_mean_w"] = round(sum(power) / len(power), 1)
+                if clocks:
+                    g["gfxclk_min_mhz"], g["gfxclk_mean_mhz"] = min(clocks), round(sum(clocks) / len(clocks))
+                u0, u1 = (first.get(idx) or {}).get("ecc_uncorrectable"), x.get("ecc_uncorrectable")
+                if u0 is not None and u1 is not None:
+                    g["ecc_uncorrectable_delta"] = u1 - u0
+                    if u1 > u0:
+                        problems.append(f"GPU {idx}: {u1 - u0:.0f} uncorrectable ECC error(s) under load")
+                c0, c1 = (first.get(idx) or {}).get("ecc_correctable"), x.get("ecc_correctable")
+                if c0 is not None and c1 is not None:
+                    g["ecc_correctable_delta"] = c1 - c0
+        ok = rc == 0 and protocol_passed(out) and bool(docs) and not problems
+        if rc != 0 or not docs:
+            problems.append(f"rc={rc}" + ("" if docs else ", no load result"))
+        return StepResult("stress", ok, {"seconds": secs, "gpus": per_gpu, "telemetry_samples": len(samples),
+                                         "min_fraction": frac, "max_hotspot_c": tmax}, "; ".join(problems))
+
     def step_rccl(self, ngpus: Optional[int] = None) -> StepResult:
         if ngpus is not None and ngpus < 2:
             return StepResult("rccl", True, {"ngpus": ngpus, "skipped": "single GPU"})
@@ -393,6 +484,8 @@ class Validator:
             required.append("gemm")
         if self.vcfg["bandwidth"]:
             required.append("bandwidth")
+        if self.vcfg["stress"]:
+            required.append("stress")
         if self.vcfg["rccl"]:
             required.append("rccl")
         if self.vcfg["pluginTest"]:
@@ -462,6 +555,8 @@ class Validator:
             r = self.step_gemm() if self.vcfg["gemm"] else StepResult("gemm", True, {"skipped": True})
         elif step == "bandwidth":
             r = self.step_bandwidth() if self.vcfg["bandwidth"] else StepResult("bandwidth", True, {"skipped": True})
+        elif step == "stress":
+            r = self.step_stress() if self.vcfg["stress"] else StepResult("stress", True, {"skipped": True})
         elif step == "rccl":
             if not self.vcfg["rccl"]:
                 r = StepResult("rccl", True, {"skipped": True})

@@ -141,3 +141,19 @@ def test_node_bringup_rehearsal_on_real_hardware(tmp_path, native):
         os.makedirs(out, exist_ok=True)
         with open(os.path.join(out, "bringup.json"), "w") as f:
             json.dump(rep, f, indent=1)
+
+
+def test_validator_stress_step_on_real_hardware(tmp_path, native):
+    """5 s of sustained MFMA load with real amd-smi telemetry: steady rate, no ECC, sane temperatures."""
+    cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {stress: true, stressSeconds: 5}\n")
+    v = Validator(cfg, str(tmp_path), bin_dir=str(native))
+    r = v.run_step("stress")
+    assert r.passed, r.reason
+    g = r.detail["gpus"]["0"]
+    assert g["tflops"] > 1000 and g["tflops_min_window"] >= 0.85 * g["tflops"]
+    assert r.detail["telemetry_samples"] >= 3 and g.get("ecc_uncorrectable_delta", 0) == 0
+    out = os.environ.get("AMDK8S_EVIDENCE_DIR")
+    if out:
+        os.makedirs(out, exist_ok=True)
+        with open(tmp_path / "stress.json") as src, open(os.path.join(out, "validator_stress.json"), "w") as dst:
+            dst.write(src.read())

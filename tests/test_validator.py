@@ -408,3 +408,62 @@ def test_gemm_step_runs_a_counter_pass(tmp_path):
     col = ex.GpuCollector(ex.SysfsBackend(str(tmp_path / "nosys")), "n1", str(tmp_path))
     text = generate_latest(ex.make_registry(col)).decode()
     assert 'amd_gpu_validator_gemm_profile{node="n1",quantity="mfma_util_pct"}' in text
+
+
+# ----------------------------------------------------------------------------- stress step
+def _stress_out(rows):
+    lines = [json.dumps({"check": "proftester", "test": "tensor", "device": d, "peer": -1, "engine": "",
+                         "value": mean, "min": lo, "max": hi, "unit": "TFLOPS", "seconds": 30.1,
+                         "skipped": False, "passed": True, "note": ""}) for d, mean, lo, hi in rows]
+    return "[amd-proftester: sustained load]\n" + "\n".join(lines) + "\nTest PASSED\nDone\n"
+
+
+class Telemetry:
+    """Synthetic amd-smi samples (exporter GpuSample keys); ``ecc_step`` adds uncorrectable errors."""
+
+    def __init__(self, n=2, hotspot=78.0, ecc_step=0):
+        self.n, self.hot, self.ecc_step, self.calls = n, hotspot, ecc_step, 0
+
+    def __call__(self):
+        self.calls += 1
+        return [{"index": i, "temp_hotspot": self.hot + i, "power_w": 1390.0, "gfxclk_mhz": 1900.0,
+                 "ecc_uncorrectable": float(self.ecc_step * self.calls if i == 1 else 0),
+                 "ecc_correctable": 3.0} for i in range(self.n)]
+
+
+def _stress_validator(tmp_path, out, tel, rc=0):
+    cfg = load_config(text="validator: {stress: true, stressSeconds: 0.3}\n")
+
+    def runner(argv, timeout):
+        import time as _t
+
+        assert argv[1:5] == ["-t", "tensor", "--duration", "0.3"]
+        _t.sleep(0.3)  # the load runs while telemetry is sampled
+        return rc, out
+
+    return Validator(cfg, str(tmp_path), bin_dir="/x", runner=runner, telemetry=tel)
+
+
+def test_stress_step_passes_under_steady_load(tmp_path):
+    tel = Telemetry()
+    v = _stress_validator(tmp_path, _stress_out([(0, 1650.0, 1601.0, 1702.0), (1, 1640.0, 1590.0, 1690.0)]), tel)
+    r = v.run_step("stress")
+    assert r.passed, r.reason
+    g = r.detail["gpus"]
+    assert g["0"]["tflops_min_window"] == 1601.0 and g["1"]["hotspot_max_c"] == 79.0
+    assert g["0"]["ecc_uncorrectable_delta"] == 0 and g["0"]["power_mean_w"] == 1390.0
+    assert r.detail["telemetry_samples"] >= 1 and (tmp_path / "stress-ready").exists()
+
+
+@pytest.mark.parametrize("case,needle", [
+    ("cliff", "GPU 1: 100 ms window 900 < 0.85"),
+    ("ecc", "GPU 1: "),
+    ("hot", "hotspot 111 C > 105 C"),
+])
+def test_stress_step_fails_on_throttle_ecc_or_heat(tmp_path, case, needle):
+    rows = [(0, 1650.0, 1601.0, 1702.0), (1, 1640.0, 900.0 if case == "cliff" else 1590.0, 1690.0)]
+    tel = Telemetry(hotspot=110.0 if case == "hot" else 78.0, ecc_step=1 if case == "ecc" else 0)
+    r = _stress_validator(tmp_path, _stress_out(rows), tel).run_step("stress")
+    assert not r.passed and needle in r.reason, r.reason
+    if case == "ecc":
+        assert "uncorrectable ECC error(s) under load" in r.reason
