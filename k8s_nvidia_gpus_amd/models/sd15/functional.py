@@ -1,0 +1,106 @@
+"""Hot-op dispatch of the SD1.5 model family: hand-written gfx950 HIP kernels on the GPU, PyTorch
+reference math elsewhere.
+
+Each op has one native implementation (``k8s_nvidia_gpus_amd/ops/csrc/sd_*.hip`` through
+``ops/sd_kernels.py``) and one plain-PyTorch reference used on CPU and by the numerics tests.
+There is no silent fallback on a GPU: with ``backend() == "native"`` (the default for CUDA/HIP
+tensors) a missing kernel library raises ``KernelLibraryError``.
+
+Ops (all activations are channels-last, i.e. NHWC memory = ``[N, H*W, C]`` token rows):
+
+* ``group_norm(x, w, b, groups, eps, silu)`` — GroupNorm with the SiLU that follows it in every
+  ResNet block fused into the same pass (SD1.5 UNet: 61 GroupNorms per forward).
+* ``attention(q, k, v, heads)`` — softmax(q·kᵀ/√d)·v over ``[N, L, heads*d]`` rows, head dims 40 /
+  80 / 160 (UNet) and 64 (CLIP-free paths); q/k/v may be strided column views of one fused
+  projection output.
+* ``geglu(x)`` — ``h * gelu(g)`` for ``x = [h | g]`` (the transformer feed-forward's gate).
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+_BACKEND = os.environ.get("AMDK8S_SD_BACKEND", "auto")   # auto | native | torch
+
+
+def set_backend(name: str) -> None:
+    global _BACKEND
+    if name not in ("auto", "native", "torch"):
+        raise ValueError(name)
+    _BACKEND = name
+
+
+def backend() -> str:
+    return _BACKEND
+
+
+def _native(t: torch.Tensor) -> bool:
+    if _BACKEND == "torch":
+        return False
+    if _BACKEND == "native":
+        if t.device.type != "cuda":
+            raise RuntimeError("native SD kernels need tensors on the GPU")
+        return True
+    return t.device.type == "cuda"
+
+
+def _sd():
+    from k8s_nvidia_gpus_amd.ops import sd_kernels
+
+    return sd_kernels
+
+
+# ---------------------------------------------------------------- GroupNorm (+SiLU)
+def group_norm_ref(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, groups: int,
+                   eps: float, silu: bool = False) -> torch.Tensor:
+    y = F.group_norm(x.float(), groups, weight.float(), bias.float(), eps).to(x.dtype)
+    return F.silu(y) if silu else y
+
+
+def group_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, groups: int,
+               eps: float, silu: bool = False) -> torch.Tensor:
+    """GroupNorm over a 4-D NCHW-shaped tensor (channels-last memory on the GPU path)."""
+    if _native(x) and _sd().group_norm_supported(x.shape[1] if x.dim() == 4 else x.shape[-1],
+                                                 groups):
+        return _sd().group_norm_nhwc(x, weight, bias, groups, eps, silu)
+    return group_norm_ref(x, weight, bias, groups, eps, silu)
+
+
+# ---------------------------------------------------------------- attention
+def attention_ref(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
+                  scale: Optional[float] = None) -> torch.Tensor:
+    n, lq, c = q.shape
+    lk = k.shape[1]
+    d = c // heads
+    qh = q.reshape(n, lq, heads, d).transpose(1, 2)
+    kh = k.reshape(n, lk, heads, d).transpose(1, 2)
+    vh = v.reshape(n, lk, heads, d).transpose(1, 2)
+    o = F.scaled_dot_product_attention(qh, kh, vh, scale=scale)
+    return o.transpose(1, 2).reshape(n, lq, c)
+
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
+              scale: Optional[float] = None) -> torch.Tensor:
+    """``[N, Lq, H*d]`` × ``[N, Lk, H*d]`` → ``[N, Lq, H*d]`` (no mask, SD's attention)."""
+    d = q.shape[-1] // heads
+    if scale is None:
+        scale = 1.0 / math.sqrt(d)
+    if _native(q) and _sd().attention_supported(q, k, v, heads):
+        return _sd().attention(q, k, v, heads, scale)
+    return attention_ref(q, k, v, heads, scale)
+
+
+# ---------------------------------------------------------------- GEGLU
+def geglu_ref(x: torch.Tensor) -> torch.Tensor:
+    h, g = x.chunk(2, dim=-1)
+    return h * F.gelu(g)
+
+
+def geglu(x: torch.Tensor) -> torch.Tensor:
+    if _native(x):
+        return _sd().geglu(x)
+    return geglu_ref(x)

@@ -1,0 +1,353 @@
+// GroupNorm (+ fused SiLU) over channels-last activations, and GEGLU, for the SD1.5 model family
+// (k8s_nvidia_gpus_amd/models/sd15).  gfx950, wave64, fp16 / bf16 storage, fp32 maths.
+//
+// GroupNorm on NHWC memory ([N, HW, C] rows): a group is Cg = C/G adjacent channels of every pixel,
+// so a 16-byte vector of 8 channels touches at most two groups (Cg >= 4 is required; SD1.5 has
+// Cg = 4..80).  Each thread owns ONE fixed 8-channel vector column (vc) and walks rows, so rows are
+// read fully coalesced (C*2 bytes contiguous per pixel) and the per-thread group split is a compile-
+// free constant.  Two launches:
+//   1. gn_partial: blocks = N x chunks.  Per (n, chunk, group): count / mean / M2 in fp32 (per-thread
+//      sums over a few hundred elements, then a deterministic in-block reduction).  The LAST block of
+//      each n to finish (atomic ticket) merges the chunks with Chan's parallel-variance formula into
+//      stats[n][g] = (mean, rstd) and re-arms the ticket (self-resetting: safe inside HIP graphs).
+//   2. gn_apply: y = x * a_c + b_c (a_c = rstd*w_c, b_c = bias_c - mean*a_c, per thread in
+//      registers), optional SiLU, 16-byte stores.
+// Deterministic: no float atomics anywhere; the ticket counts blocks only.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kMaxThreads = 1024;
+
+__device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
+
+__device__ __forceinline__ uint32_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return 0x7fc0u;  // NaN stays NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+template <bool BF16>
+__device__ __forceinline__ void unpack8(const uint4 v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if constexpr (BF16) {
+      f[2 * i] = bf16_to_f32(w[i] & 0xffffu);
+      f[2 * i + 1] = bf16_to_f32(w[i] >> 16);
+    } else {
+      _Float16 lo, hi;
+      uint16_t l = w[i] & 0xffffu, h = w[i] >> 16;
+      __builtin_memcpy(&lo, &l, 2);
+      __builtin_memcpy(&hi, &h, 2);
+      f[2 * i] = (float)lo;
+      f[2 * i + 1] = (float)hi;
+    }
+  }
+}
+
+template <bool BF16>
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if constexpr (BF16) {
+      w[i] = f32_to_bf16(f[2 * i]) | (f32_to_bf16(f[2 * i + 1]) << 16);
+    } else {
+      _Float16 lo = (_Float16)f[2 * i], hi = (_Float16)f[2 * i + 1];
+      uint16_t l, h;
+      __builtin_memcpy(&l, &lo, 2);
+      __builtin_memcpy(&h, &hi, 2);
+      w[i] = (uint32_t)l | ((uint32_t)h << 16);
+    }
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <bool BF16>
+__device__ __forceinline__ float load_scalar(const uint16_t* p, int i) {
+  uint32_t h = p[i];
+  if constexpr (BF16) {
+    return bf16_to_f32(h);
+  } else {
+    _Float16 x;
+    uint16_t b = (uint16_t)h;
+    __builtin_memcpy(&x, &b, 2);
+    return (float)x;
+  }
+}
+
+struct GnShape {
+  int N, HW, C, G, Cg, VC, R;  // VC = C/8 vector columns, R = rows in flight per block
+  int chunks1, rows1;          // stats pass: chunks per image, rows per chunk
+  int chunks2, rows2;          // apply pass
+};
+
+// Partial layout: part[((n * chunks1 + chunk) * G + g) * 3 + {count, mean, M2}]
+template <bool BF16>
+__global__ void gn_partial(const uint16_t* __restrict__ x, float* __restrict__ part,
+                           float* __restrict__ stats, int* __restrict__ ticket, GnShape s, float eps) {
+  const int tid = threadIdx.x;
+  const int chunk = blockIdx.x, n = blockIdx.y;
+  const int vc = tid % s.VC, r = tid / s.VC;
+  const int c0 = vc * 8;
+  const int g_lo = c0 / s.Cg;
+  const int split = min(8, (g_lo + 1) * s.Cg - c0);  // elements [0, split) are in g_lo
+  const int row0 = chunk * s.rows1, row1 = min(s.HW, row0 + s.rows1);
+  float s_lo = 0.f, q_lo = 0.f, s_hi = 0.f, q_hi = 0.f;
+  const uint16_t* base = x + ((size_t)n * s.HW) * s.C + c0;
+  for (int row = row0 + r; row < row1; row += s.R) {
+    const uint4 v = *reinterpret_cast<const uint4*>(base + (size_t)row * s.C);
+    float f[8];
+    unpack8<BF16>(v, f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i < split) {
+        s_lo += f[i];
+        q_lo += f[i] * f[i];
+      } else {
+        s_hi += f[i];
+        q_hi += f[i] * f[i];
+      }
+    }
+  }
+  // in-block reduction, deterministic: [R][VC][4] in LDS, row 0 sums over r, then one thread per group
+  extern __shared__ float lds[];
+  float* red = lds;  // R * VC * 4
+  red[(r * s.VC + vc) * 4 + 0] = s_lo;
+  red[(r * s.VC + vc) * 4 + 1] = q_lo;
+  red[(r * s.VC + vc) * 4 + 2] = s_hi;
+  red[(r * s.VC + vc) * 4 + 3] = q_hi;
+  __syncthreads();
+  if (r == 0) {
+    for (int rr = 1; rr < s.R; ++rr) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) red[vc * 4 + k] += red[(rr * s.VC + vc) * 4 + k];
+    }
+  }
+  __syncthreads();
+  const int rows_in_chunk = max(0, row1 - row0);
+  for (int g = tid; g < s.G; g += blockDim.x) {
+    const int cbeg = g * s.Cg, cend = cbeg + s.Cg;  // [cbeg, cend)
+    float sum = 0.f, sq = 0.f;
+    for (int v = cbeg / 8; v <= (cend - 1) / 8; ++v) {
+      const int vlo = v * 8 / s.Cg;  // group of the vector's first element
+      if (vlo == g) {
+        sum += red[v * 4 + 0];
+        sq += red[v * 4 + 1];
+      } else {
+        sum += red[v * 4 + 2];
+        sq += red[v * 4 + 3];
+      }
+    }
+    const float cnt = (float)rows_in_chunk * (float)s.Cg;
+    const float mean = cnt > 0.f ? sum / cnt : 0.f;
+    const float m2 = cnt > 0.f ? fmaxf(sq - sum * mean, 0.f) : 0.f;
+    float* p = part + (((size_t)n * s.chunks1 + chunk) * s.G + g) * 3;
+    p[0] = cnt;
+    p[1] = mean;
+    p[2] = m2;
+  }
+  // last block of image n merges all chunks: nsub threads per group each merge a strided subset
+  // of the chunks (independent loads, pipelined), then one thread per group merges the nsub results
+  __shared__ int last;
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) last = (atomicAdd(&ticket[n], 1) == s.chunks1 - 1);
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  const int nsub = max(1, (int)blockDim.x / s.G);
+  float* mrg = lds;  // [nsub][G][3], reuses the reduction scratch (>= that size, see host)
+  if (tid < nsub * s.G) {
+    const int g = tid % s.G, sub = tid / s.G;
+    float cnt = 0.f, mean = 0.f, m2 = 0.f;
+    for (int k = sub; k < s.chunks1; k += nsub) {
+      const float* p = part + (((size_t)n * s.chunks1 + k) * s.G + g) * 3;
+      const float cb = __hip_atomic_load(p + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float mb = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float m2b = __hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cb <= 0.f) continue;
+      const float tot = cnt + cb;
+      const float d = mb - mean;
+      mean += d * (cb / tot);
+      m2 += m2b + d * d * (cnt * cb / tot);
+      cnt = tot;
+    }
+    mrg[(sub * s.G + g) * 3 + 0] = cnt;
+    mrg[(sub * s.G + g) * 3 + 1] = mean;
+    mrg[(sub * s.G + g) * 3 + 2] = m2;
+  }
+  __syncthreads();
+  for (int g = tid; g < s.G; g += blockDim.x) {
+    float cnt = 0.f, mean = 0.f, m2 = 0.f;
+    for (int sub = 0; sub < nsub; ++sub) {
+      const float cb = mrg[(sub * s.G + g) * 3 + 0];
+      if (cb <= 0.f) continue;
+      const float mb = mrg[(sub * s.G + g) * 3 + 1], m2b = mrg[(sub * s.G + g) * 3 + 2];
+      const float tot = cnt + cb;
+      const float d = mb - mean;
+      mean += d * (cb / tot);
+      m2 += m2b + d * d * (cnt * cb / tot);
+      cnt = tot;
+    }
+    const float var = cnt > 0.f ? m2 / cnt : 0.f;
+    stats[((size_t)n * s.G + g) * 2 + 0] = mean;
+    stats[((size_t)n * s.G + g) * 2 + 1] = rsqrtf(var + eps);
+  }
+  if (tid == 0) atomicExch(&ticket[n], 0);
+}
+
+template <bool BF16, bool SILU>
+__global__ void gn_apply(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                         const uint16_t* __restrict__ w, const uint16_t* __restrict__ b,
+                         const float* __restrict__ stats, GnShape s) {
+  const int tid = threadIdx.x;
+  const int chunk = blockIdx.x, n = blockIdx.y;
+  const int vc = tid % s.VC, r = tid / s.VC;
+  const int c0 = vc * 8;
+  float a[8], sh[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = c0 + i;
+    const int g = c / s.Cg;
+    const float mean = stats[((size_t)n * s.G + g) * 2 + 0];
+    const float rstd = stats[((size_t)n * s.G + g) * 2 + 1];
+    a[i] = rstd * load_scalar<BF16>(w, c);
+    sh[i] = load_scalar<BF16>(b, c) - mean * a[i];
+  }
+  const int row0 = chunk * s.rows2, row1 = min(s.HW, row0 + s.rows2);
+  const size_t off = ((size_t)n * s.HW) * s.C + c0;
+  for (int row = row0 + r; row < row1; row += s.R) {
+    const size_t o = off + (size_t)row * s.C;
+    const uint4 v = *reinterpret_cast<const uint4*>(x + o);
+    float f[8];
+    unpack8<BF16>(v, f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float t = f[i] * a[i] + sh[i];
+      if constexpr (SILU) t = t / (1.f + __expf(-t));
+      f[i] = t;
+    }
+    *reinterpret_cast<uint4*>(y + o) = pack8<BF16>(f);
+  }
+}
+
+// GEGLU: x [M, 2D] -> out [M, D], out = h * gelu_erf(g), x = [h | g]
+template <bool BF16>
+__global__ void geglu_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ out, long M,
+                             int D) {
+  const int DV = D / 8;
+  const long total = M * DV;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long m = i / DV;
+    const int j = (int)(i - m * DV) * 8;
+    const uint16_t* row = x + m * 2L * D;
+    float h[8], g[8];
+    unpack8<BF16>(*reinterpret_cast<const uint4*>(row + j), h);
+    unpack8<BF16>(*reinterpret_cast<const uint4*>(row + D + j), g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] *= 0.5f * g[k] * (1.f + erff(g[k] * 0.70710678118654752f));
+    *reinterpret_cast<uint4*>(out + m * (long)D + j) = pack8<BF16>(h);
+  }
+}
+
+GnShape gn_shape(int N, int HW, int C, int G) {
+  GnShape s{};
+  s.N = N;
+  s.HW = HW;
+  s.C = C;
+  s.G = G;
+  s.Cg = C / G;
+  s.VC = C / 8;
+  s.R = s.VC >= 384 ? 1 : 384 / s.VC;
+  if (s.R > HW) s.R = HW;
+  // stats pass: ~1024 blocks overall, >= R rows per chunk, <= 64 chunks per image
+  int want1 = (1024 + N - 1) / N;
+  int maxc = (HW + s.R - 1) / s.R;
+  s.chunks1 = want1 < maxc ? want1 : maxc;
+  if (s.chunks1 > 64) s.chunks1 = 64;
+  if (s.chunks1 < 1) s.chunks1 = 1;
+  s.rows1 = (HW + s.chunks1 - 1) / s.chunks1;
+  s.chunks1 = (HW + s.rows1 - 1) / s.rows1;
+  int want2 = (2048 + N - 1) / N;
+  s.chunks2 = want2 < maxc ? want2 : maxc;
+  if (s.chunks2 < 1) s.chunks2 = 1;
+  s.rows2 = (HW + s.chunks2 - 1) / s.chunks2;
+  s.chunks2 = (HW + s.rows2 - 1) / s.rows2;
+  return s;
+}
+
+// Every 16-byte vector of 8 channels must touch at most two groups (the per-thread split).
+bool gn_supported(int C, int G) {
+  if (C <= 0 || G <= 0 || C % 8 != 0 || C % G != 0 || C / 8 > kMaxThreads) return false;
+  const int Cg = C / G;
+  for (int c0 = 0; c0 < C; c0 += 8)
+    if ((c0 + 7) / Cg - c0 / Cg > 1) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int amdk8s_groupnorm_supported(int C, int G) { return gn_supported(C, G) ? 1 : 0; }
+
+// Workspace floats needed by amdk8s_groupnorm_nhwc (partials + stats).
+long amdk8s_groupnorm_workspace(int N, int HW, int C, int G) {
+  GnShape s = gn_shape(N, HW, C, G);
+  return (long)N * s.chunks1 * G * 3 + (long)N * G * 2;
+}
+
+// y = GroupNorm(x) * w + b (optionally SiLU), x/y [N, HW, C] (channels-last), w/b [C].
+// dtype: 0 = fp16, 1 = bf16.  ticket: >= N zeroed ints, owned by the caller, left zeroed.
+int amdk8s_groupnorm_nhwc(const void* x, void* y, const void* w, const void* b, float* workspace,
+                          int* ticket, int N, int HW, int C, int G, float eps, int silu, int dtype,
+                          hipStream_t stream) {
+  if (N <= 0 || HW <= 0 || !gn_supported(C, G)) return -1;
+  GnShape s = gn_shape(N, HW, C, G);
+  float* part = workspace;
+  float* stats = workspace + (size_t)N * s.chunks1 * G * 3;
+  const int threads = s.VC * s.R;
+  const int nsub = threads / G > 0 ? threads / G : 1;
+  const size_t red_f = (size_t)s.R * s.VC * 4, mrg_f = (size_t)nsub * G * 3;
+  const size_t lds = (red_f > mrg_f ? red_f : mrg_f) * sizeof(float);
+  const auto* xi = static_cast<const uint16_t*>(x);
+  auto* yo = static_cast<uint16_t*>(y);
+  const auto* wi = static_cast<const uint16_t*>(w);
+  const auto* bi = static_cast<const uint16_t*>(b);
+  dim3 g1(s.chunks1, N), g2(s.chunks2, N);
+  if (dtype == 1) {
+    hipLaunchKernelGGL(gn_partial<true>, g1, dim3(threads), lds, stream, xi, part, stats, ticket, s, eps);
+    if (silu)
+      hipLaunchKernelGGL((gn_apply<true, true>), g2, dim3(threads), 0, stream, xi, yo, wi, bi, stats, s);
+    else
+      hipLaunchKernelGGL((gn_apply<true, false>), g2, dim3(threads), 0, stream, xi, yo, wi, bi, stats, s);
+  } else {
+    hipLaunchKernelGGL(gn_partial<false>, g1, dim3(threads), lds, stream, xi, part, stats, ticket, s, eps);
+    if (silu)
+      hipLaunchKernelGGL((gn_apply<false, true>), g2, dim3(threads), 0, stream, xi, yo, wi, bi, stats, s);
+    else
+      hipLaunchKernelGGL((gn_apply<false, false>), g2, dim3(threads), 0, stream, xi, yo, wi, bi, stats, s);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int amdk8s_geglu(const void* x, void* out, long M, int D, int dtype, hipStream_t stream) {
+  if (M <= 0 || D % 8 != 0) return -1;
+  const long vecs = M * (D / 8);
+  long blocks = (vecs + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  const auto* xi = static_cast<const uint16_t*>(x);
+  auto* o = static_cast<uint16_t*>(out);
+  if (dtype == 1)
+    hipLaunchKernelGGL(geglu_kernel<true>, dim3(blocks), dim3(256), 0, stream, xi, o, M, D);
+  else
+    hipLaunchKernelGGL(geglu_kernel<false>, dim3(blocks), dim3(256), 0, stream, xi, o, M, D);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // extern "C"

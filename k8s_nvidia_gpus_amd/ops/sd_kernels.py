@@ -1,0 +1,143 @@
+"""ctypes bindings of the SD1.5 hot-op kernels (``csrc/sd_norm.hip``, ``csrc/sd_attention.hip``).
+
+Same conventions as ``kernels.py``: raw device pointers, torch's current stream (so the kernels are
+captured by ``torch.cuda.graph``), no fallback when the library is missing on a GPU machine.
+Shapes a kernel does not cover are reported by the ``*_supported`` predicates; the model's dispatch
+(``models/sd15/functional.py``) routes only those to PyTorch.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from typing import Dict
+
+import torch
+
+from .kernels import library
+
+_DTYPE = {torch.float16: 0, torch.bfloat16: 1}
+_declared = False
+_lock = threading.Lock()
+_tickets: Dict[int, torch.Tensor] = {}
+
+
+def _lib():
+    global _declared
+    lib = library()
+    if not _declared:
+        with _lock:
+            vp, ci, cl, cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
+            lib.amdk8s_groupnorm_supported.argtypes = [ci, ci]
+            lib.amdk8s_groupnorm_supported.restype = ci
+            lib.amdk8s_groupnorm_workspace.argtypes = [ci, ci, ci, ci]
+            lib.amdk8s_groupnorm_workspace.restype = cl
+            lib.amdk8s_groupnorm_nhwc.argtypes = [vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, cf, ci,
+                                                  ci, vp]
+            lib.amdk8s_groupnorm_nhwc.restype = ci
+            lib.amdk8s_geglu.argtypes = [vp, vp, cl, ci, ci, vp]
+            lib.amdk8s_geglu.restype = ci
+            if hasattr(lib, "amdk8s_attention_fwd"):
+                lib.amdk8s_attention_supported.argtypes = [ci, ci, ci]
+                lib.amdk8s_attention_supported.restype = ci
+                lib.amdk8s_attention_fwd.argtypes = [vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, ci,
+                                                     ci, ci, ci, ci, cf, ci, vp]
+                lib.amdk8s_attention_fwd.restype = ci
+            _declared = True
+    return lib
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _ticket(device: torch.device) -> torch.Tensor:
+    """Per-device block-ticket array of the GroupNorm stats pass (self-resetting, zero at rest)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    t = _tickets.get(idx)
+    if t is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("group_norm_nhwc: first call must happen outside HIP-graph capture")
+        t = torch.zeros(4096, dtype=torch.int32, device=device)
+        torch.cuda.synchronize(device)
+        _tickets[idx] = t
+    return t
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (rc={rc})")
+
+
+def group_norm_supported(c: int, groups: int) -> bool:
+    return bool(_lib().amdk8s_groupnorm_supported(c, groups))
+
+
+def group_norm_nhwc(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, groups: int,
+                    eps: float, silu: bool = False) -> torch.Tensor:
+    """GroupNorm(+SiLU) of ``x`` ([N, C, H, W] channels-last, or [N, L, C] rows)."""
+    if x.dtype not in _DTYPE:
+        raise TypeError(f"group_norm_nhwc: {x.dtype} (fp16/bf16 only)")
+    lib = _lib()
+    if x.dim() == 4:
+        n, c, h, w = x.shape
+        hw = h * w
+        x = x.contiguous(memory_format=torch.channels_last)
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+    elif x.dim() == 3:
+        n, hw, c = x.shape
+        x = x.contiguous()
+        y = torch.empty_like(x)
+    else:
+        raise ValueError("group_norm_nhwc: 3-D or 4-D input")
+    if not lib.amdk8s_groupnorm_supported(c, groups):
+        raise ValueError(f"group_norm_nhwc: C={c}, groups={groups} not supported")
+    if n > 4096:
+        raise ValueError("group_norm_nhwc: batch > 4096")
+    w = weight.to(x.dtype).contiguous()
+    b = bias.to(x.dtype).contiguous()
+    ws = torch.empty(lib.amdk8s_groupnorm_workspace(n, hw, c, groups), dtype=torch.float32,
+                     device=x.device)
+    rc = lib.amdk8s_groupnorm_nhwc(x.data_ptr(), y.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                   ws.data_ptr(), _ticket(x.device).data_ptr(), n, hw, c, groups,
+                                   float(eps), int(silu), _DTYPE[x.dtype], _stream(x))
+    _check(rc, "amdk8s_groupnorm_nhwc")
+    return y
+
+
+def geglu(x: torch.Tensor) -> torch.Tensor:
+    """``h * gelu(g)`` for ``x = [h | g]`` along the last dim."""
+    if x.dtype not in _DTYPE:
+        raise TypeError(f"geglu: {x.dtype} (fp16/bf16 only)")
+    x = x.contiguous()
+    d2 = x.shape[-1]
+    d = d2 // 2
+    m = x.numel() // d2
+    out = torch.empty(x.shape[:-1] + (d,), dtype=x.dtype, device=x.device)
+    _check(_lib().amdk8s_geglu(x.data_ptr(), out.data_ptr(), m, d, _DTYPE[x.dtype], _stream(x)),
+           "amdk8s_geglu")
+    return out
+
+
+def attention_supported(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int) -> bool:
+    lib = _lib()
+    if not hasattr(lib, "amdk8s_attention_fwd") or q.dtype not in _DTYPE:
+        return False
+    if q.stride(-1) != 1 or k.stride(-1) != 1 or v.stride(-1) != 1:
+        return False
+    d = q.shape[-1] // heads
+    return bool(lib.amdk8s_attention_supported(d, q.shape[1], k.shape[1]))
+
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
+              scale: float) -> torch.Tensor:
+    """softmax(q kᵀ · scale) v per head; q/k/v ``[N, L, H*d]`` with unit inner stride."""
+    n, lq, c = q.shape
+    lk = k.shape[1]
+    d = c // heads
+    o = torch.empty((n, lq, c), dtype=q.dtype, device=q.device)
+    rc = _lib().amdk8s_attention_fwd(
+        q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), n, heads, lq, lk, d,
+        q.stride(0), q.stride(1), k.stride(0), k.stride(1), v.stride(0), v.stride(1), o.stride(1),
+        float(scale), _DTYPE[q.dtype], _stream(q))
+    _check(rc, "amdk8s_attention_fwd")
+    return o
