@@ -56,18 +56,30 @@ def _sd():
 
 # ---------------------------------------------------------------- GroupNorm (+SiLU)
 def group_norm_ref(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, groups: int,
-                   eps: float, silu: bool = False) -> torch.Tensor:
-    y = F.group_norm(x.float(), groups, weight.float(), bias.float(), eps).to(x.dtype)
+                   eps: float, silu: bool = False, add: Optional[torch.Tensor] = None) -> torch.Tensor:
+    xf = x.float()
+    if add is not None:
+        xf = xf + (add.float()[:, :, None, None] if x.dim() == 4 else add.float()[:, None, :])
+    y = F.group_norm(xf, groups, weight.float(), bias.float(), eps).to(x.dtype)
     return F.silu(y) if silu else y
 
 
 def group_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, groups: int,
-               eps: float, silu: bool = False) -> torch.Tensor:
-    """GroupNorm over a 4-D NCHW-shaped tensor (channels-last memory on the GPU path)."""
+               eps: float, silu: bool = False, add: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """GroupNorm of ``x (+ add[n, c])`` over a 4-D NCHW-shaped tensor (channels-last memory on the
+    GPU path); ``add`` is the ResNet block's time-embedding + conv-bias addend."""
     if _native(x) and _sd().group_norm_supported(x.shape[1] if x.dim() == 4 else x.shape[-1],
                                                  groups):
-        return _sd().group_norm_nhwc(x, weight, bias, groups, eps, silu)
-    return group_norm_ref(x, weight, bias, groups, eps, silu)
+        return _sd().group_norm_nhwc(x, weight, bias, groups, eps, silu, add)
+    return group_norm_ref(x, weight, bias, groups, eps, silu, add)
+
+
+def add3(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``a + b + bias[c]`` (NCHW-shaped): residual add with the convolution bias folded in."""
+    if _native(a) and a.shape == b.shape and a.shape[1] % 8 == 0:
+        return _sd().add3(a, b, bias)
+    out = a + b
+    return out + bias[:, None, None] if bias is not None else out
 
 
 # ---------------------------------------------------------------- attention

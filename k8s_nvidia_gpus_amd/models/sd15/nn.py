@@ -27,10 +27,12 @@ from . import functional as SF
 
 
 class GroupNorm(nn.GroupNorm):
-    """``nn.GroupNorm`` whose forward optionally fuses the following SiLU (native kernel)."""
+    """``nn.GroupNorm`` whose forward optionally fuses the following SiLU and a per-(n, c) addend
+    applied to its input (native kernel)."""
 
-    def forward(self, x: torch.Tensor, silu: bool = False) -> torch.Tensor:  # type: ignore[override]
-        return SF.group_norm(x, self.weight, self.bias, self.num_groups, self.eps, silu)
+    def forward(self, x: torch.Tensor, silu: bool = False,  # type: ignore[override]
+                add: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return SF.group_norm(x, self.weight, self.bias, self.num_groups, self.eps, silu, add)
 
 
 def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos: bool = True,
@@ -56,7 +58,21 @@ class TimestepEmbedding(nn.Module):
         return self.linear_2(F.silu(self.linear_1(x)))
 
 
+class TembAddends:
+    """All ResNet time-embedding addends of one UNet forward, from ONE GEMM (see UNet.prepare)."""
+
+    def __init__(self, all_: torch.Tensor):
+        self.all = all_
+
+
 class ResnetBlock2D(nn.Module):
+    """GroupNorm+SiLU → conv1 → (+ time embedding) GroupNorm+SiLU → conv2 → + shortcut.
+
+    Epilogues are folded instead of run as separate passes: conv1's bias and the time-embedding
+    projection form one per-(n, c) addend that the second GroupNorm applies to its input; conv2's
+    (and the 1×1 shortcut's) bias ride in the fused residual add.  Same maths as diffusers'
+    ``ResnetBlock2D`` (output_scale_factor 1)."""
+
     def __init__(self, cin: int, cout: int, temb: Optional[int], groups: int, eps: float):
         super().__init__()
         self.norm1 = GroupNorm(groups, cin, eps=eps)
@@ -65,16 +81,38 @@ class ResnetBlock2D(nn.Module):
         self.norm2 = GroupNorm(groups, cout, eps=eps)
         self.conv2 = nn.Conv2d(cout, cout, 3, padding=1)
         self.conv_shortcut = nn.Conv2d(cin, cout, 1) if cin != cout else None
+        self._temb_off = None          # (start, end) in TembAddends.all, set by UNet.prepare
+        self._out_bias: Optional[torch.Tensor] = None
 
-    def forward(self, x, temb_act=None):
-        """``temb_act`` is ``silu(temb)`` (computed once per UNet forward, shared by every block)."""
-        h = self.conv1(self.norm1(x, silu=True))
-        if self.time_emb_proj is not None and temb_act is not None:
-            h = h + self.time_emb_proj(temb_act)[:, :, None, None]
-        h = self.conv2(self.norm2(h, silu=True))
+    @torch.no_grad()
+    def fuse_biases(self) -> None:
+        b = self.conv2.bias
         if self.conv_shortcut is not None:
-            x = self.conv_shortcut(x)
-        return x + h
+            b = b + self.conv_shortcut.bias
+        self._out_bias = b.detach().clone()
+
+    def _addend(self, temb, n: int) -> torch.Tensor:
+        if isinstance(temb, TembAddends):
+            s, e = self._temb_off
+            return temb.all[:, s:e]
+        if temb is not None and self.time_emb_proj is not None:
+            return self.time_emb_proj(temb) + self.conv1.bias
+        return self.conv1.bias.expand(n, -1)
+
+    def forward(self, x, temb=None):
+        """``temb``: ``silu(temb)`` [N, 1280], a :class:`TembAddends`, or None (VAE)."""
+        h = F.conv2d(self.norm1(x, silu=True), self.conv1.weight, None, padding=1)
+        h = self.norm2(h, silu=True, add=self._addend(temb, x.shape[0]))
+        h = F.conv2d(h, self.conv2.weight, None, padding=1)
+        if self.conv_shortcut is not None:
+            sc = F.conv2d(x, self.conv_shortcut.weight, None)
+        else:
+            sc = x
+        bias = self._out_bias
+        if bias is None or bias.device != h.device or bias.dtype != h.dtype:
+            bias = self.conv2.bias if self.conv_shortcut is None \
+                else self.conv2.bias + self.conv_shortcut.bias
+        return SF.add3(sc, h, bias)
 
 
 class Attention(nn.Module):

@@ -18,8 +18,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .config import UNetConfig
-from .nn import (Downsample2D, GroupNorm, ResnetBlock2D, TimestepEmbedding, Transformer2DModel,
-                 Upsample2D, timestep_embedding)
+from .nn import (Downsample2D, GroupNorm, ResnetBlock2D, TembAddends, TimestepEmbedding,
+                 Transformer2DModel, Upsample2D, timestep_embedding)
 
 
 class DownBlock(nn.Module):
@@ -134,12 +134,28 @@ class UNet2DConditionModel(nn.Module):
 
         return [m for m in self.modules() if isinstance(m, Attention)]
 
+    def resnets(self) -> List[ResnetBlock2D]:
+        return [m for m in self.modules() if isinstance(m, ResnetBlock2D)]
+
+    @torch.no_grad()
     def prepare(self) -> "UNet2DConditionModel":
-        """Inference layout: channels-last parameters, fused q/k/v weights (call after .to())."""
+        """Inference layout (call after .to()): channels-last parameters, fused q/k/v weights,
+        folded ResNet biases, and the 22 ResNet time-embedding projections stacked into one
+        [ΣC, 1280] GEMM whose bias already holds each conv1 bias."""
         if next(self.parameters()).device.type == "cuda":
             self.to(memory_format=torch.channels_last)
         for a in self.attention_modules():
             a.fuse_qkv()
+        ws, bs, off = [], [], 0
+        for r in self.resnets():
+            r.fuse_biases()
+            c = r.conv1.out_channels
+            r._temb_off = (off, off + c)
+            off += c
+            ws.append(r.time_emb_proj.weight)
+            bs.append(r.time_emb_proj.bias + r.conv1.bias)
+        self._temb_w = torch.cat(ws, 0).contiguous()
+        self._temb_b = torch.cat(bs, 0).contiguous()
         return self
 
     def forward(self, sample: torch.Tensor, timestep: torch.Tensor,
@@ -150,6 +166,9 @@ class UNet2DConditionModel(nn.Module):
         t = timestep_embedding(timestep, self.cfg.block_out_channels[0],
                                self.cfg.flip_sin_to_cos, self.cfg.freq_shift).to(sample.dtype)
         temb_act = F.silu(self.time_embedding(t))
+        tw = getattr(self, "_temb_w", None)
+        if tw is not None and tw.dtype == temb_act.dtype and tw.device == temb_act.device:
+            temb_act = TembAddends(F.linear(temb_act, tw, self._temb_b))
         x = sample
         if x.device.type == "cuda":
             x = x.contiguous(memory_format=torch.channels_last)

@@ -74,9 +74,13 @@ class AutoencoderKLDecoder(nn.Module):
         self.post_quant_conv = nn.Conv2d(cfg.latent_channels, cfg.latent_channels, 1)
         self.decoder = Decoder(cfg)
 
+    @torch.no_grad()
     def prepare(self) -> "AutoencoderKLDecoder":
         if next(self.parameters()).device.type == "cuda":
             self.to(memory_format=torch.channels_last)
+        for m in self.modules():
+            if isinstance(m, ResnetBlock2D):
+                m.fuse_biases()
         return self
 
     def decode(self, latents: torch.Tensor) -> torch.Tensor:

@@ -87,8 +87,9 @@ struct GnShape {
 
 // Partial layout: part[((n * chunks1 + chunk) * G + g) * 3 + {count, mean, M2}]
 template <bool BF16>
-__global__ void gn_partial(const uint16_t* __restrict__ x, float* __restrict__ part,
-                           float* __restrict__ stats, int* __restrict__ ticket, GnShape s, float eps) {
+__global__ void gn_partial(const uint16_t* __restrict__ x, const uint16_t* __restrict__ add,
+                           long add_stride, float* __restrict__ part, float* __restrict__ stats,
+                           int* __restrict__ ticket, GnShape s, float eps) {
   const int tid = threadIdx.x;
   const int chunk = blockIdx.x, n = blockIdx.y;
   const int vc = tid % s.VC, r = tid / s.VC;
@@ -97,6 +98,9 @@ __global__ void gn_partial(const uint16_t* __restrict__ x, float* __restrict__ p
   const int split = min(8, (g_lo + 1) * s.Cg - c0);  // elements [0, split) are in g_lo
   const int row0 = chunk * s.rows1, row1 = min(s.HW, row0 + s.rows1);
   float s_lo = 0.f, q_lo = 0.f, s_hi = 0.f, q_hi = 0.f;
+  float ad[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ad[i] = add ? load_scalar<BF16>(add + n * add_stride, c0 + i) : 0.f;
   const uint16_t* base = x + ((size_t)n * s.HW) * s.C + c0;
   for (int row = row0 + r; row < row1; row += s.R) {
     const uint4 v = *reinterpret_cast<const uint4*>(base + (size_t)row * s.C);
@@ -104,6 +108,7 @@ __global__ void gn_partial(const uint16_t* __restrict__ x, float* __restrict__ p
     unpack8<BF16>(v, f);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+      f[i] += ad[i];
       if (i < split) {
         s_lo += f[i];
         q_lo += f[i] * f[i];
@@ -201,7 +206,8 @@ __global__ void gn_partial(const uint16_t* __restrict__ x, float* __restrict__ p
 }
 
 template <bool BF16, bool SILU>
-__global__ void gn_apply(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+__global__ void gn_apply(const uint16_t* __restrict__ x, const uint16_t* __restrict__ add,
+                         long add_stride, uint16_t* __restrict__ y,
                          const uint16_t* __restrict__ w, const uint16_t* __restrict__ b,
                          const float* __restrict__ stats, GnShape s) {
   const int tid = threadIdx.x;
@@ -216,7 +222,9 @@ __global__ void gn_apply(const uint16_t* __restrict__ x, uint16_t* __restrict__ 
     const float mean = stats[((size_t)n * s.G + g) * 2 + 0];
     const float rstd = stats[((size_t)n * s.G + g) * 2 + 1];
     a[i] = rstd * load_scalar<BF16>(w, c);
-    sh[i] = load_scalar<BF16>(b, c) - mean * a[i];
+    // (x + add) * a + b - mean * a: the per-(n, c) addend folds into the shift
+    const float ad = add ? load_scalar<BF16>(add + n * add_stride, c) : 0.f;
+    sh[i] = load_scalar<BF16>(b, c) - mean * a[i] + ad * a[i];
   }
   const int row0 = chunk * s.rows2, row1 = min(s.HW, row0 + s.rows2);
   const size_t off = ((size_t)n * s.HW) * s.C + c0;
@@ -252,6 +260,32 @@ __global__ void geglu_kernel(const uint16_t* __restrict__ x, uint16_t* __restric
 #pragma unroll
     for (int k = 0; k < 8; ++k) h[k] *= 0.5f * g[k] * (1.f + erff(g[k] * 0.70710678118654752f));
     *reinterpret_cast<uint4*>(out + m * (long)D + j) = pack8<BF16>(h);
+  }
+}
+
+// out[m, c] = a[m, c] + b[m, c] (+ bias[c]) over [M, C] rows (C % 8 == 0): the ResNet block's
+// residual add with the convolution bias folded in (one pass instead of bias kernel + add kernel)
+template <bool BF16>
+__global__ void add3_kernel(const uint16_t* __restrict__ a, const uint16_t* __restrict__ b,
+                            const uint16_t* __restrict__ bias, uint16_t* __restrict__ out, long M,
+                            int C) {
+  const int CV = C / 8;
+  const long total = M * CV;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % CV) * 8;
+    float fa[8], fb[8];
+    unpack8<BF16>(reinterpret_cast<const uint4*>(a)[i], fa);
+    unpack8<BF16>(reinterpret_cast<const uint4*>(b)[i], fb);
+    if (bias) {
+      float fc[8];
+      unpack8<BF16>(*reinterpret_cast<const uint4*>(bias + c0), fc);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) fa[k] += fc[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) fa[k] += fb[k];
+    reinterpret_cast<uint4*>(out)[i] = pack8<BF16>(fa);
   }
 }
 
@@ -304,9 +338,10 @@ long amdk8s_groupnorm_workspace(int N, int HW, int C, int G) {
 
 // y = GroupNorm(x) * w + b (optionally SiLU), x/y [N, HW, C] (channels-last), w/b [C].
 // dtype: 0 = fp16, 1 = bf16.  ticket: >= N zeroed ints, owned by the caller, left zeroed.
-int amdk8s_groupnorm_nhwc(const void* x, void* y, const void* w, const void* b, float* workspace,
-                          int* ticket, int N, int HW, int C, int G, float eps, int silu, int dtype,
-                          hipStream_t stream) {
+// add (nullable): per-(n, c) addend [N, C] with row stride add_stride: y = GroupNorm(x + add[n, c])
+int amdk8s_groupnorm_nhwc(const void* x, const void* add, long add_stride, void* y, const void* w,
+                          const void* b, float* workspace, int* ticket, int N, int HW, int C, int G,
+                          float eps, int silu, int dtype, hipStream_t stream) {
   if (N <= 0 || HW <= 0 || !gn_supported(C, G)) return -1;
   GnShape s = gn_shape(N, HW, C, G);
   float* part = workspace;
@@ -316,22 +351,23 @@ int amdk8s_groupnorm_nhwc(const void* x, void* y, const void* w, const void* b, 
   const size_t red_f = (size_t)s.R * s.VC * 4, mrg_f = (size_t)nsub * G * 3;
   const size_t lds = (red_f > mrg_f ? red_f : mrg_f) * sizeof(float);
   const auto* xi = static_cast<const uint16_t*>(x);
+  const auto* ai = static_cast<const uint16_t*>(add);
   auto* yo = static_cast<uint16_t*>(y);
   const auto* wi = static_cast<const uint16_t*>(w);
   const auto* bi = static_cast<const uint16_t*>(b);
   dim3 g1(s.chunks1, N), g2(s.chunks2, N);
   if (dtype == 1) {
-    hipLaunchKernelGGL(gn_partial<true>, g1, dim3(threads), lds, stream, xi, part, stats, ticket, s, eps);
+    hipLaunchKernelGGL(gn_partial<true>, g1, dim3(threads), lds, stream, xi, ai, add_stride, part, stats, ticket, s, eps);
     if (silu)
-      hipLaunchKernelGGL((gn_apply<true, true>), g2, dim3(threads), 0, stream, xi, yo, wi, bi, stats, s);
+      hipLaunchKernelGGL((gn_apply<true, true>), g2, dim3(threads), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s);
     else
-      hipLaunchKernelGGL((gn_apply<true, false>), g2, dim3(threads), 0, stream, xi, yo, wi, bi, stats, s);
+      hipLaunchKernelGGL((gn_apply<true, false>), g2, dim3(threads), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s);
   } else {
-    hipLaunchKernelGGL(gn_partial<false>, g1, dim3(threads), lds, stream, xi, part, stats, ticket, s, eps);
+    hipLaunchKernelGGL(gn_partial<false>, g1, dim3(threads), lds, stream, xi, ai, add_stride, part, stats, ticket, s, eps);
     if (silu)
-      hipLaunchKernelGGL((gn_apply<false, true>), g2, dim3(threads), 0, stream, xi, yo, wi, bi, stats, s);
+      hipLaunchKernelGGL((gn_apply<false, true>), g2, dim3(threads), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s);
     else
-      hipLaunchKernelGGL((gn_apply<false, false>), g2, dim3(threads), 0, stream, xi, yo, wi, bi, stats, s);
+      hipLaunchKernelGGL((gn_apply<false, false>), g2, dim3(threads), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s);
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
@@ -347,6 +383,22 @@ int amdk8s_geglu(const void* x, void* out, long M, int D, int dtype, hipStream_t
     hipLaunchKernelGGL(geglu_kernel<true>, dim3(blocks), dim3(256), 0, stream, xi, o, M, D);
   else
     hipLaunchKernelGGL(geglu_kernel<false>, dim3(blocks), dim3(256), 0, stream, xi, o, M, D);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int amdk8s_add3(const void* a, const void* b, const void* bias, void* out, long M, int C, int dtype,
+                hipStream_t stream) {
+  if (M <= 0 || C % 8 != 0) return -1;
+  long blocks = (M * (C / 8) + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  const auto* ai = static_cast<const uint16_t*>(a);
+  const auto* bi = static_cast<const uint16_t*>(b);
+  const auto* ci = static_cast<const uint16_t*>(bias);
+  auto* o = static_cast<uint16_t*>(out);
+  if (dtype == 1)
+    hipLaunchKernelGGL(add3_kernel<true>, dim3(blocks), dim3(256), 0, stream, ai, bi, ci, o, M, C);
+  else
+    hipLaunchKernelGGL(add3_kernel<false>, dim3(blocks), dim3(256), 0, stream, ai, bi, ci, o, M, C);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -31,11 +31,13 @@ def _lib():
             lib.amdk8s_groupnorm_supported.restype = ci
             lib.amdk8s_groupnorm_workspace.argtypes = [ci, ci, ci, ci]
             lib.amdk8s_groupnorm_workspace.restype = cl
-            lib.amdk8s_groupnorm_nhwc.argtypes = [vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, cf, ci,
-                                                  ci, vp]
+            lib.amdk8s_groupnorm_nhwc.argtypes = [vp, vp, cl, vp, vp, vp, vp, vp, ci, ci, ci, ci,
+                                                  cf, ci, ci, vp]
             lib.amdk8s_groupnorm_nhwc.restype = ci
             lib.amdk8s_geglu.argtypes = [vp, vp, cl, ci, ci, vp]
             lib.amdk8s_geglu.restype = ci
+            lib.amdk8s_add3.argtypes = [vp, vp, vp, vp, cl, ci, ci, vp]
+            lib.amdk8s_add3.restype = ci
             if hasattr(lib, "amdk8s_attention_fwd"):
                 lib.amdk8s_attention_supported.argtypes = [ci, ci, ci]
                 lib.amdk8s_attention_supported.restype = ci
@@ -73,8 +75,9 @@ def group_norm_supported(c: int, groups: int) -> bool:
 
 
 def group_norm_nhwc(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, groups: int,
-                    eps: float, silu: bool = False) -> torch.Tensor:
-    """GroupNorm(+SiLU) of ``x`` ([N, C, H, W] channels-last, or [N, L, C] rows)."""
+                    eps: float, silu: bool = False, add: torch.Tensor = None) -> torch.Tensor:
+    """GroupNorm(+SiLU) of ``x + add[n, c]`` (``x`` [N, C, H, W] channels-last or [N, L, C] rows;
+    ``add`` an optional [N, C] per-image channel addend, any row stride)."""
     if x.dtype not in _DTYPE:
         raise TypeError(f"group_norm_nhwc: {x.dtype} (fp16/bf16 only)")
     lib = _lib()
@@ -97,7 +100,14 @@ def group_norm_nhwc(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, g
     b = bias.to(x.dtype).contiguous()
     ws = torch.empty(lib.amdk8s_groupnorm_workspace(n, hw, c, groups), dtype=torch.float32,
                      device=x.device)
-    rc = lib.amdk8s_groupnorm_nhwc(x.data_ptr(), y.data_ptr(), w.data_ptr(), b.data_ptr(),
+    add_ptr, add_stride = None, 0
+    if add is not None:
+        if add.shape != (n, c) or add.stride(1) != 1:
+            raise ValueError(f"group_norm_nhwc: addend must be [N, C] with unit column stride")
+        add = add.to(x.dtype)
+        add_ptr, add_stride = add.data_ptr(), add.stride(0)
+    rc = lib.amdk8s_groupnorm_nhwc(x.data_ptr(), add_ptr, add_stride, y.data_ptr(), w.data_ptr(),
+                                   b.data_ptr(),
                                    ws.data_ptr(), _ticket(x.device).data_ptr(), n, hw, c, groups,
                                    float(eps), int(silu), _DTYPE[x.dtype], _stream(x))
     _check(rc, "amdk8s_groupnorm_nhwc")
@@ -115,6 +125,24 @@ def geglu(x: torch.Tensor) -> torch.Tensor:
     out = torch.empty(x.shape[:-1] + (d,), dtype=x.dtype, device=x.device)
     _check(_lib().amdk8s_geglu(x.data_ptr(), out.data_ptr(), m, d, _DTYPE[x.dtype], _stream(x)),
            "amdk8s_geglu")
+    return out
+
+
+def add3(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor = None) -> torch.Tensor:
+    """``a + b + bias[c]`` over channels-last [N, C, H, W] (or [..., C]) tensors of one dtype."""
+    if a.dtype not in _DTYPE or b.dtype != a.dtype:
+        raise TypeError("add3: fp16/bf16 operands of one dtype")
+    fmt = torch.channels_last if a.dim() == 4 else torch.contiguous_format
+    a = a.contiguous(memory_format=fmt)
+    b = b.contiguous(memory_format=fmt)
+    c = a.shape[1] if a.dim() == 4 else a.shape[-1]
+    out = torch.empty_like(a, memory_format=fmt)
+    bias_ptr = None
+    if bias is not None:
+        bias = bias.to(a.dtype).contiguous()
+        bias_ptr = bias.data_ptr()
+    _check(_lib().amdk8s_add3(a.data_ptr(), b.data_ptr(), bias_ptr, out.data_ptr(),
+                              a.numel() // c, c, _DTYPE[a.dtype], _stream(a)), "amdk8s_add3")
     return out
 
 

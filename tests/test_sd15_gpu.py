@@ -126,3 +126,78 @@ def test_tiny_pipeline_end_to_end_png(dev):
     solo = pipe(["b"], num_inference_steps=4, width=64, height=64,
                 generator=[torch.Generator(device=dev).manual_seed(1)], output_type="latent")
     torch.testing.assert_close(solo.latents[0], out.latents[1], rtol=2e-2, atol=2e-2)
+
+
+def _attn_ref(q, k, v, heads, scale):
+    n, lq, c = q.shape
+    d = c // heads
+
+    def split(t):
+        return t.float().reshape(n, t.shape[1], heads, d).transpose(1, 2)
+
+    o = torch.nn.functional.scaled_dot_product_attention(split(q), split(k), split(v), scale=scale)
+    return o.transpose(1, 2).reshape(n, lq, c)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("n,heads,lq,lk,d,fused", [
+    (2, 8, 4096, 4096, 40, True),     # 64x64 self-attention, q|k|v slices of one projection
+    (2, 8, 1024, 1024, 80, True),     # 32x32
+    (2, 8, 256, 256, 160, True),      # 16x16
+    (2, 8, 64, 64, 160, True),        # mid block 8x8
+    (2, 8, 4096, 77, 40, False),      # cross-attention over 77 text tokens
+    (2, 8, 1024, 77, 80, False),
+    (1, 3, 100, 33, 64, False),       # ragged query and key counts
+    (1, 2, 130, 200, 128, True),
+])
+def test_attention_vs_fp32(SK, dev, dtype, n, heads, lq, lk, d, fused):
+    g = torch.Generator(device=dev).manual_seed(lq + lk + d)
+    c = heads * d
+    if fused:
+        qkv = torch.randn(n, lq, 3 * c, generator=g, device=dev).to(dtype)
+        q, k, v = qkv[..., :c], qkv[..., c:2 * c], qkv[..., 2 * c:]
+    else:
+        q = torch.randn(n, lq, c, generator=g, device=dev).to(dtype)
+        kv = torch.randn(n, lk, 2 * c, generator=g, device=dev).to(dtype)
+        k, v = kv[..., :c], kv[..., c:]
+    q = q * 2   # sharper softmax than unit scores
+    assert SK.attention_supported(q, k, v, heads)
+    scale = d ** -0.5
+    o = SK.attention(q, k, v, heads, scale)
+    ref = _attn_ref(q, k, v, heads, scale)
+    tol = 2e-2 if dtype == torch.bfloat16 else 5e-3
+    torch.testing.assert_close(o.float(), ref, rtol=tol, atol=tol)
+
+
+def test_attention_extreme_scores_are_finite(SK, dev):
+    g = torch.Generator(device=dev).manual_seed(9)
+    q = (torch.randn(1, 256, 320, generator=g, device=dev) * 30).half()
+    k = (torch.randn(1, 256, 320, generator=g, device=dev) * 30).half()
+    v = torch.randn(1, 256, 320, generator=g, device=dev).half()
+    o = SK.attention(q, k, v, 8, 40 ** -0.5)
+    assert torch.isfinite(o).all()
+    torch.testing.assert_close(o.float(), _attn_ref(q, k, v, 8, 40 ** -0.5), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_group_norm_with_addend_and_add3(SK, dev, dtype):
+    g = torch.Generator(device=dev).manual_seed(11)
+    x = torch.randn(2, 640, 32, 32, generator=g, device=dev).to(dtype)
+    x = x.contiguous(memory_format=torch.channels_last)
+    w = (torch.rand(640, generator=g, device=dev) + 0.5).to(dtype)
+    b = torch.randn(640, generator=g, device=dev).to(dtype)
+    big = torch.randn(2, 3000, generator=g, device=dev).to(dtype) * 4
+    add = big[:, 1000:1640]                       # strided slice of the stacked temb GEMM output
+    y = SK.group_norm_nhwc(x, w, b, 32, 1e-5, True, add)
+    ref = _gn_ref(x.float() + add.float()[:, :, None, None], w, b, 32, 1e-5, True)
+    tol = 3e-2 if dtype == torch.bfloat16 else 6e-3
+    torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+    bias = torch.randn(640, generator=g, device=dev).to(dtype)
+    y0 = SK.group_norm_nhwc(x, w, b, 32, 1e-5, False, bias.expand(2, -1))   # row stride 0
+    torch.testing.assert_close(y0.float(), _gn_ref(x.float() + bias.float()[:, None, None], w, b, 32,
+                                                   1e-5, False), rtol=tol, atol=tol)
+    z = torch.randn(2, 640, 32, 32, generator=g, device=dev).to(dtype)
+    z = z.contiguous(memory_format=torch.channels_last)
+    s = SK.add3(x, z, bias)
+    torch.testing.assert_close(s.float(), x.float() + z.float() + bias.float()[:, None, None],
+                               rtol=tol, atol=tol)
