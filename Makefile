@@ -1,6 +1,6 @@
 # Convenience targets (everything also works with plain python/pytest commands).
 PY ?= python3
-.PHONY: build native kernels test test-gpu bench lint-manifests sync images clean
+.PHONY: build native kernels test test-gpu bench sd15-bench lint-manifests images clean
 build:            ## every HIP kernel (gfx950) + native tool, in-tree
 	$(PY) -c "import __graft_entry__ as g; g.build()"
 kernels:
@@ -17,8 +17,8 @@ bench:            ## headline benchmark on all local GPUs (one rank per GPU)
 	  --master-addr 127.0.0.1 bench.py --gpus $$n; else $(PY) bench.py; fi
 lint-manifests:
 	$(PY) -m pytest tests/test_static_manifests.py -q
-sync:             ## mirror in-package app sources into the Kustomize trees
-	$(PY) -m k8s_nvidia_gpus_amd.utils.sync_apps
+sd15-bench:       ## SD1.5 UNet pass / 512x512 30-step latency on one MI355X
+	$(PY) tools/sd15_bench.py
 images:
 	docker build -f images/operator/Dockerfile -t ghcr.io/example-org/amd-gpu-operator:0.1.0 .
 	docker build -f images/bench/Dockerfile -t ghcr.io/example-org/amd-gpu-bench:0.1.0 .

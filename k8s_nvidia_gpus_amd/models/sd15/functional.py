@@ -82,6 +82,18 @@ def add3(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None) 
     return out + bias[:, None, None] if bias is not None else out
 
 
+# ---------------------------------------------------------------- (residual add +) LayerNorm
+def add_layernorm(x: torch.Tensor, delta: Optional[torch.Tensor], weight: torch.Tensor,
+                  bias: torch.Tensor, eps: float):
+    """``LN(x)`` or, with ``delta``, ``(x + delta, LN(x + delta))`` — the transformer block's
+    residual add fused in front of the next LayerNorm."""
+    if _native(x) and _sd().layernorm_supported(x.shape[-1]):
+        return _sd().add_layernorm(x, delta, weight, bias, eps)
+    xs = x if delta is None else x + delta
+    y = F.layer_norm(xs, (x.shape[-1],), weight, bias, eps)
+    return y if delta is None else (xs, y)
+
+
 # ---------------------------------------------------------------- attention
 def attention_ref(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
                   scale: Optional[float] = None) -> torch.Tensor:

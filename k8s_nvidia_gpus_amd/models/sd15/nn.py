@@ -193,9 +193,11 @@ class BasicTransformerBlock(nn.Module):
         self.ff = FeedForward(dim)
 
     def forward(self, x, context):
-        x = x + self.attn1(self.norm1(x))
-        x = x + self.attn2(self.norm2(x), context)
-        return x + self.ff(self.norm3(x))
+        n1, n2, n3 = self.norm1, self.norm2, self.norm3
+        h = SF.add_layernorm(x, None, n1.weight, n1.bias, n1.eps)
+        x, h = SF.add_layernorm(x, self.attn1(h), n2.weight, n2.bias, n2.eps)
+        x, h = SF.add_layernorm(x, self.attn2(h, context), n3.weight, n3.bias, n3.eps)
+        return x + self.ff(h)
 
 
 class Transformer2DModel(nn.Module):

@@ -104,6 +104,8 @@ def _to_pil(images: torch.Tensor):
 class StableDiffusion:
     """SD1.5 text-to-image. ``model_dir`` (diffusers layout) or random-init weights (benchmarks)."""
 
+    native_pipeline = True   # the service skips torch.autocast and runs its warm-up for it
+
     def __init__(self, model_dir: Optional[str] = None, device: Union[str, torch.device] = "cuda",
                  dtype: torch.dtype = torch.float16, cfg: SD15Config = SD15,
                  scheduler: str = "pndm", use_graphs: bool = True, init_seed: int = 0):
@@ -203,15 +205,21 @@ class StableDiffusion:
 def load_native_pipeline(settings) -> StableDiffusion:
     """``sd15_api`` pipeline factory: the in-tree SD1.5 on the ROCm device.
 
-    ``MODEL_DIR`` (diffusers layout on the PVC) supplies weights; without it the service starts with
-    random-init weights and says so (useful for load tests; images are noise)."""
+    ``settings.model_dir`` (diffusers layout on the PVC) supplies weights; without it the service
+    starts with random-init weights and says so (load tests; the images are noise)."""
     import logging
+
+    from .config import tiny
 
     dtype = getattr(torch, settings.dtype)
     device = settings.device if torch.cuda.is_available() else "cpu"
-    model_dir = os.getenv("MODEL_DIR") or None
+    model_dir = getattr(settings, "model_dir", "") or None
     if model_dir is None:
         logging.getLogger("sd15-api").warning("MODEL_DIR unset: random-init SD1.5 weights")
-    return StableDiffusion(model_dir=model_dir, device=device, dtype=dtype,
-                           scheduler=os.getenv("SCHEDULER", "pndm"),
-                           use_graphs=os.getenv("HIP_GRAPHS", "1") != "0")
+    cfg = tiny() if getattr(settings, "model_config", "sd15") == "tiny" else SD15
+    pipe = StableDiffusion(model_dir=model_dir, device=device, dtype=dtype, cfg=cfg,
+                           scheduler=getattr(settings, "scheduler", "pndm"),
+                           use_graphs=getattr(settings, "hip_graphs", True))
+    if getattr(settings, "vae_slicing", False):
+        pipe.enable_vae_slicing()
+    return pipe

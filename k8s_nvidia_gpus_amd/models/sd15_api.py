@@ -20,8 +20,15 @@ with an ``X-Gen-Time`` header).  Redesigned for a 288 GB GPU shared by concurren
 * ``_LAST_IMAGE`` is read and written under one lock (the reference reads it unlocked).
 * ``/metrics``: Prometheus counters/histograms for requests, latency and batch size.
 
+* **In-tree model, no diffusers.**  The default pipeline is this repository's SD1.5
+  (``k8s_nvidia_gpus_amd/models/sd15``: HIP GroupNorm / attention / fused epilogues, the UNet pass
+  replayed from a HIP graph), loading the same checkpoint files from ``MODEL_DIR``.  Before the pod
+  reports ready it warms up every batch size in ``WARMUP_BATCHES`` (MIOpen solver search + graph
+  capture happen then, not on the first user request).  ``PIPELINE=diffusers`` keeps the upstream
+  library path for images that ship diffusers.
+
 ``create_app(pipeline_factory=...)`` takes the pipeline constructor so tests run the whole HTTP +
-batching path on CPU with a fake pipeline (diffusers is installed only in the serving image).
+batching path on CPU with a fake or a miniature in-tree pipeline.
 """
 from __future__ import annotations
 
@@ -37,7 +44,7 @@ from typing import Any, Callable, List, Optional
 
 logger = logging.getLogger("sd15-api")
 
-DEFAULT_MODEL_ID = "runwayml/stable-diffusion-v1-5"
+DEFAULT_MODEL_ID = "stable-diffusion-v1-5/stable-diffusion-v1-5"
 
 
 def _env_bool(name: str, default: bool) -> bool:
@@ -61,6 +68,12 @@ class Settings:
     max_side: int = 2048
     queue_limit: int = 256
     request_timeout_s: float = 600.0
+    pipeline: str = "native"          # native (in-tree SD1.5) | diffusers
+    model_dir: str = ""               # diffusers-layout checkpoint directory (native pipeline)
+    scheduler: str = "pndm"           # pndm | ddim | euler (native pipeline)
+    hip_graphs: bool = True
+    warmup_batches: str = "1"         # batch sizes captured before /readyz turns green
+    model_config: str = "sd15"        # sd15 | tiny (tests)
 
     @classmethod
     def from_env(cls) -> "Settings":
@@ -77,7 +90,28 @@ class Settings:
             max_side=int(os.getenv("MAX_SIDE", "2048")),
             queue_limit=int(os.getenv("QUEUE_LIMIT", "256")),
             request_timeout_s=float(os.getenv("REQUEST_TIMEOUT_S", "600")),
+            pipeline=os.getenv("PIPELINE", "native"),
+            model_dir=os.getenv("MODEL_DIR", ""),
+            scheduler=os.getenv("SCHEDULER", "pndm"),
+            hip_graphs=_env_bool("HIP_GRAPHS", True),
+            warmup_batches=os.getenv("WARMUP_BATCHES", "1"),
+            model_config=os.getenv("MODEL_CONFIG", "sd15"),
         )
+
+
+def load_native_pipeline(settings: Settings):
+    """In-tree SD1.5 (``models/sd15``) on the ROCm device; random-init weights without MODEL_DIR."""
+    from k8s_nvidia_gpus_amd.models.sd15.pipeline import load_native_pipeline as _load
+
+    return _load(settings)
+
+
+def load_pipeline(settings: Settings):
+    if settings.pipeline == "diffusers":
+        return load_diffusers_pipeline(settings)
+    if settings.pipeline != "native":
+        raise ValueError(f"PIPELINE={settings.pipeline!r} (native | diffusers)")
+    return load_native_pipeline(settings)
 
 
 def load_diffusers_pipeline(settings: Settings):
@@ -178,6 +212,7 @@ class GenerationWorker:
     def _run(self) -> None:
         try:
             self._pipe = self._factory(self.settings)
+            self._warmup()
         except BaseException as e:  # noqa: BLE001 - surfaced through /readyz
             logger.exception("pipeline load failed")
             self._load_error = e
@@ -204,6 +239,19 @@ class GenerationWorker:
             ids = {id(j) for j in batch}
             pending = [j for j in pending if id(j) not in ids]
             self._run_batch(batch)
+
+    def _warmup(self) -> None:
+        """Run each WARMUP_BATCHES size once at the default request shape (2 steps): the native
+        pipeline captures its HIP graph per batch size and MIOpen picks its solvers here, so the
+        first real request of that size runs at steady-state speed."""
+        sizes = [int(x) for x in str(self.settings.warmup_batches).split(",") if x.strip()]
+        if not sizes or not getattr(self._pipe, "native_pipeline", False):
+            return
+        for b in sizes:
+            t0 = time.time()
+            self._pipe(["warmup"] * b, num_inference_steps=2, guidance_scale=7.5, width=512,
+                       height=512, output_type="latent")
+            logger.info("warm-up batch %d: %.2fs", b, time.time() - t0)
 
     def _run_batch(self, batch: List[_Job]) -> None:
         import contextlib
@@ -232,7 +280,8 @@ class GenerationWorker:
                 import torch
 
                 if torch.cuda.is_available() and self.settings.device.startswith("cuda") \
-                        and self.settings.dtype != "float32":
+                        and self.settings.dtype != "float32" \
+                        and not getattr(self._pipe, "native_pipeline", False):
                     ctx = torch.autocast(device_type="cuda", dtype=getattr(torch, self.settings.dtype))
             except ImportError:  # pragma: no cover - torch is always in the serving image
                 pass
@@ -284,7 +333,7 @@ def create_app(settings: Optional[Settings] = None,
         prom = None
 
     settings = settings or Settings.from_env()
-    worker = GenerationWorker(settings, pipeline_factory or load_diffusers_pipeline)
+    worker = GenerationWorker(settings, pipeline_factory or load_pipeline)
     state = {"last": None}
     last_lock = threading.Lock()
 

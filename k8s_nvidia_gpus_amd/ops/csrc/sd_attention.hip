@@ -203,6 +203,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
   };
 
   const int ntiles = (a.Lk + kKeys - 1) / kKeys;
+  constexpr float kThr = 8.f;              // P <= 2^8 between rescales (exact in fp16 / bf16)
+  const float thr = kThr / a.c;            // the same margin in raw score units
   load_tile(0);
   for (int kt = 0; kt < ntiles; ++kt) {
     const int kbase = kt * kKeys;
@@ -231,15 +233,22 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
         for (int t = 0; t < 4; ++t)
           if (kbase + 16 * t + c16 >= a.Lk) sacc[t] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
       }
-      // online softmax; this lane's rows are q = 4g + i
+      // online softmax; this lane's rows are q = 4g + i.  Deferred max (T13): the row max and the
+      // O / l rescale run only when some score of the wave exceeds its row's running max by more
+      // than kThr (exp2 units), so P stays <= 2^kThr and exact; otherwise the old max is kept.
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float tmax = fmaxf(fmaxf(sacc[0][i], sacc[1][i]), fmaxf(sacc[2][i], sacc[3][i]));
-        tmax = row16_max(tmax);
-        const float mnew = fmaxf(m[qt][i], tmax);
-        const float alpha = __builtin_amdgcn_exp2f((m[qt][i] - mnew) * a.c);
-        m[qt][i] = mnew;
-        const float mc = mnew * a.c;
+        const float lmax = fmaxf(fmaxf(sacc[0][i], sacc[1][i]), fmaxf(sacc[2][i], sacc[3][i]));
+        if (__builtin_amdgcn_ballot_w64(lmax > m[qt][i] + thr) != 0) {  // wave-uniform branch
+          const float tmax = row16_max(lmax);
+          const float mnew = fmaxf(m[qt][i], tmax);
+          const float alpha = __builtin_amdgcn_exp2f((m[qt][i] - mnew) * a.c);
+          m[qt][i] = mnew;
+          l[qt][i] *= alpha;
+#pragma unroll
+          for (int t = 0; t < DT; ++t) o[qt][t][i] *= alpha;
+        }
+        const float mc = m[qt][i] * a.c;
         float rs = 0.f;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -247,9 +256,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
           sacc[t][i] = p;
           rs += p;
         }
-        l[qt][i] = l[qt][i] * alpha + rs;
-#pragma unroll
-        for (int t = 0; t < DT; ++t) o[qt][t][i] *= alpha;
+        l[qt][i] += rs;
       }
       // Pᵀ[key][q]: this lane holds keys 16t + c16, q = 4g .. 4g+3 of tile qt → one 8-byte store
 #pragma unroll

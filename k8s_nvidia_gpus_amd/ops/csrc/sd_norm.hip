@@ -19,6 +19,7 @@
 namespace {
 
 constexpr int kMaxThreads = 1024;
+constexpr int kMergeMax = 8;  // partials merged per thread by the last block (see gn_shape)
 
 __device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
 
@@ -80,7 +81,7 @@ __device__ __forceinline__ float load_scalar(const uint16_t* p, int i) {
 }
 
 struct GnShape {
-  int N, HW, C, G, Cg, VC, R;  // VC = C/8 vector columns, R = rows in flight per block
+  int N, HW, C, G, Cg, VC, R;  // VC = C/8 vector columns, R = rows in flight per block (per pass)
   int chunks1, rows1;          // stats pass: chunks per image, rows per chunk
   int chunks2, rows2;          // apply pass
 };
@@ -98,10 +99,10 @@ __global__ void gn_partial(const uint16_t* __restrict__ x, const uint16_t* __res
   const int split = min(8, (g_lo + 1) * s.Cg - c0);  // elements [0, split) are in g_lo
   const int row0 = chunk * s.rows1, row1 = min(s.HW, row0 + s.rows1);
   float s_lo = 0.f, q_lo = 0.f, s_hi = 0.f, q_hi = 0.f;
-  float ad[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) ad[i] = add ? load_scalar<BF16>(add + n * add_stride, c0 + i) : 0.f;
+  float ad[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (add) unpack8<BF16>(*reinterpret_cast<const uint4*>(add + n * add_stride + c0), ad);
   const uint16_t* base = x + ((size_t)n * s.HW) * s.C + c0;
+#pragma unroll 8
   for (int row = row0 + r; row < row1; row += s.R) {
     const uint4 v = *reinterpret_cast<const uint4*>(base + (size_t)row * s.C);
     float f[8];
@@ -126,13 +127,16 @@ __global__ void gn_partial(const uint16_t* __restrict__ x, const uint16_t* __res
   red[(r * s.VC + vc) * 4 + 2] = s_hi;
   red[(r * s.VC + vc) * 4 + 3] = q_hi;
   __syncthreads();
-  if (r == 0) {
-    for (int rr = 1; rr < s.R; ++rr) {
+  // tree over the R row-slots (log2 R dependent steps instead of R)
+  int span = 1;
+  while (span < s.R) span <<= 1;
+  for (int st = span >> 1; st > 0; st >>= 1) {
+    if (r < st && r + st < s.R) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) red[vc * 4 + k] += red[(rr * s.VC + vc) * 4 + k];
+      for (int k = 0; k < 4; ++k) red[(r * s.VC + vc) * 4 + k] += red[((r + st) * s.VC + vc) * 4 + k];
     }
+    __syncthreads();
   }
-  __syncthreads();
   const int rows_in_chunk = max(0, row1 - row0);
   for (int g = tid; g < s.G; g += blockDim.x) {
     const int cbeg = g * s.Cg, cend = cbeg + s.Cg;  // [cbeg, cend)
@@ -168,17 +172,28 @@ __global__ void gn_partial(const uint16_t* __restrict__ x, const uint16_t* __res
   float* mrg = lds;  // [nsub][G][3], reuses the reduction scratch (>= that size, see host)
   if (tid < nsub * s.G) {
     const int g = tid % s.G, sub = tid / s.G;
+    // all loads first (independent, in flight together), then the merge; plain loads: only this
+    // last block ever reads the partials, so no L1 line of them can be stale
+    float pc[kMergeMax], pm[kMergeMax], pq[kMergeMax];
+#pragma unroll
+    for (int j = 0; j < kMergeMax; ++j) {
+      const int k = sub + j * nsub;
+      pc[j] = pm[j] = pq[j] = 0.f;
+      if (k < s.chunks1) {
+        const float* p = part + (((size_t)n * s.chunks1 + k) * s.G + g) * 3;
+        pc[j] = p[0];
+        pm[j] = p[1];
+        pq[j] = p[2];
+      }
+    }
     float cnt = 0.f, mean = 0.f, m2 = 0.f;
-    for (int k = sub; k < s.chunks1; k += nsub) {
-      const float* p = part + (((size_t)n * s.chunks1 + k) * s.G + g) * 3;
-      const float cb = __hip_atomic_load(p + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const float mb = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const float m2b = __hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (cb <= 0.f) continue;
-      const float tot = cnt + cb;
-      const float d = mb - mean;
-      mean += d * (cb / tot);
-      m2 += m2b + d * d * (cnt * cb / tot);
+#pragma unroll
+    for (int j = 0; j < kMergeMax; ++j) {
+      const float tot = cnt + pc[j];
+      const float f = pc[j] > 0.f ? pc[j] / tot : 0.f;
+      const float d = pm[j] - mean;
+      mean += d * f;
+      m2 += pq[j] + d * d * cnt * f;
       cnt = tot;
     }
     mrg[(sub * s.G + g) * 3 + 0] = cnt;
@@ -214,20 +229,25 @@ __global__ void gn_apply(const uint16_t* __restrict__ x, const uint16_t* __restr
   const int chunk = blockIdx.x, n = blockIdx.y;
   const int vc = tid % s.VC, r = tid / s.VC;
   const int c0 = vc * 8;
-  float a[8], sh[8];
+  float a[8], sh[8], wv[8], bv[8], av[8];
+  unpack8<BF16>(*reinterpret_cast<const uint4*>(w + c0), wv);
+  unpack8<BF16>(*reinterpret_cast<const uint4*>(b + c0), bv);
+  if (add)
+    unpack8<BF16>(*reinterpret_cast<const uint4*>(add + n * add_stride + c0), av);
+  const int g_lo = c0 / s.Cg, g_hi = (c0 + 7) / s.Cg;  // at most two groups per vector
+  const float2 st_lo = reinterpret_cast<const float2*>(stats)[(size_t)n * s.G + g_lo];
+  const float2 st_hi = reinterpret_cast<const float2*>(stats)[(size_t)n * s.G + g_hi];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int c = c0 + i;
-    const int g = c / s.Cg;
-    const float mean = stats[((size_t)n * s.G + g) * 2 + 0];
-    const float rstd = stats[((size_t)n * s.G + g) * 2 + 1];
-    a[i] = rstd * load_scalar<BF16>(w, c);
+    const bool lo = (c0 + i) / s.Cg == g_lo;
+    const float mean = lo ? st_lo.x : st_hi.x, rstd = lo ? st_lo.y : st_hi.y;
+    a[i] = rstd * wv[i];
     // (x + add) * a + b - mean * a: the per-(n, c) addend folds into the shift
-    const float ad = add ? load_scalar<BF16>(add + n * add_stride, c) : 0.f;
-    sh[i] = load_scalar<BF16>(b, c) - mean * a[i] + ad * a[i];
+    sh[i] = bv[i] - mean * a[i] + (add ? av[i] * a[i] : 0.f);
   }
   const int row0 = chunk * s.rows2, row1 = min(s.HW, row0 + s.rows2);
   const size_t off = ((size_t)n * s.HW) * s.C + c0;
+#pragma unroll 8
   for (int row = row0 + r; row < row1; row += s.R) {
     const size_t o = off + (size_t)row * s.C;
     const uint4 v = *reinterpret_cast<const uint4*>(x + o);
@@ -289,7 +309,77 @@ __global__ void add3_kernel(const uint16_t* __restrict__ a, const uint16_t* __re
   }
 }
 
-GnShape gn_shape(int N, int HW, int C, int G) {
+// pass = 1: stats (big blocks: ~1024 threads, <= 64 chunks per image, so the last block's merge is
+// 1-2 partials per thread); pass = 2: apply (~384-thread blocks, ~2048 blocks overall)
+// LayerNorm over rows of C channels (C % 8 == 0, C <= 64*8*kLnVec), one wave per row, values held
+// in registers between the mean and the variance pass (exact two-pass variance).  With `delta`
+// it is the transformer block's residual add fused in front: xs = x + delta is written out (the
+// next residual) and y = LN(xs).
+constexpr int kLnVec = 4;  // 16-byte vectors per lane: C <= 2048
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <bool BF16, bool DELTA>
+__global__ __launch_bounds__(256) void add_layernorm_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ delta, uint16_t* __restrict__ xs,
+    uint16_t* __restrict__ y, const uint16_t* __restrict__ gamma, const uint16_t* __restrict__ beta,
+    long M, int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;  // whole waves only: the row is wave-uniform
+  const int CV = C / 8;
+  const size_t base = (size_t)row * C;
+  float v[kLnVec][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < kLnVec; ++k) {
+    const int vi = lane + 64 * k;
+    if (vi < CV) {
+      unpack8<BF16>(*reinterpret_cast<const uint4*>(x + base + vi * 8), v[k]);
+      if constexpr (DELTA) {
+        float dl[8];
+        unpack8<BF16>(*reinterpret_cast<const uint4*>(delta + base + vi * 8), dl);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[k][e] += dl[e];
+        *reinterpret_cast<uint4*>(xs + base + vi * 8) = pack8<BF16>(v[k]);
+        unpack8<BF16>(pack8<BF16>(v[k]), v[k]);  // normalise exactly what the residual stores
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sum += v[k][e];
+    }
+  }
+  const float mean = wave_sum(sum) / C;
+  float sq = 0.f;
+#pragma unroll
+  for (int k = 0; k < kLnVec; ++k) {
+    if (lane + 64 * k < CV) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dd = v[k][e] - mean;
+        sq += dd * dd;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(sq) / C + eps);
+#pragma unroll
+  for (int k = 0; k < kLnVec; ++k) {
+    const int vi = lane + 64 * k;
+    if (vi < CV) {
+      float gm[8], bt[8], o[8];
+      unpack8<BF16>(*reinterpret_cast<const uint4*>(gamma + vi * 8), gm);
+      unpack8<BF16>(*reinterpret_cast<const uint4*>(beta + vi * 8), bt);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (v[k][e] - mean) * rstd * gm[e] + bt[e];
+      *reinterpret_cast<uint4*>(y + base + vi * 8) = pack8<BF16>(o);
+    }
+  }
+}
+
+GnShape gn_shape(int N, int HW, int C, int G, int pass) {
   GnShape s{};
   s.N = N;
   s.HW = HW;
@@ -297,27 +387,32 @@ GnShape gn_shape(int N, int HW, int C, int G) {
   s.G = G;
   s.Cg = C / G;
   s.VC = C / 8;
-  s.R = s.VC >= 384 ? 1 : 384 / s.VC;
+  // ~256-thread blocks (VC channel vectors x R row slots), 8 rows per thread (unrolled loads)
+  s.R = s.VC >= 256 ? 1 : 256 / s.VC;
   if (s.R > HW) s.R = HW;
-  // stats pass: ~1024 blocks overall, >= R rows per chunk, <= 64 chunks per image
-  int want1 = (1024 + N - 1) / N;
-  int maxc = (HW + s.R - 1) / s.R;
-  s.chunks1 = want1 < maxc ? want1 : maxc;
-  if (s.chunks1 > 64) s.chunks1 = 64;
-  if (s.chunks1 < 1) s.chunks1 = 1;
-  s.rows1 = (HW + s.chunks1 - 1) / s.chunks1;
-  s.chunks1 = (HW + s.rows1 - 1) / s.rows1;
-  int want2 = (2048 + N - 1) / N;
-  s.chunks2 = want2 < maxc ? want2 : maxc;
-  if (s.chunks2 < 1) s.chunks2 = 1;
-  s.rows2 = (HW + s.chunks2 - 1) / s.chunks2;
-  s.chunks2 = (HW + s.rows2 - 1) / s.rows2;
+  int rows = s.R * 8;
+  int chunks = (HW + rows - 1) / rows;
+  if (pass == 1) {  // the last block merges <= kMergeMax partials per thread
+    const int nsub = (s.VC * s.R) / G > 0 ? (s.VC * s.R) / G : 1;
+    const int cap = kMergeMax * nsub;
+    if (chunks > cap) {
+      chunks = cap;
+      rows = (HW + chunks - 1) / chunks;
+    }
+  }
+  if (pass == 1) {
+    s.rows1 = rows;
+    s.chunks1 = (HW + rows - 1) / rows;
+  } else {
+    s.rows2 = rows;
+    s.chunks2 = (HW + rows - 1) / rows;
+  }
   return s;
 }
 
 // Every 16-byte vector of 8 channels must touch at most two groups (the per-thread split).
 bool gn_supported(int C, int G) {
-  if (C <= 0 || G <= 0 || C % 8 != 0 || C % G != 0 || C / 8 > kMaxThreads) return false;
+  if (C <= 0 || G <= 0 || G > 128 || C % 8 != 0 || C % G != 0 || C / 8 > kMaxThreads) return false;
   const int Cg = C / G;
   for (int c0 = 0; c0 < C; c0 += 8)
     if ((c0 + 7) / Cg - c0 / Cg > 1) return false;
@@ -332,8 +427,8 @@ int amdk8s_groupnorm_supported(int C, int G) { return gn_supported(C, G) ? 1 : 0
 
 // Workspace floats needed by amdk8s_groupnorm_nhwc (partials + stats).
 long amdk8s_groupnorm_workspace(int N, int HW, int C, int G) {
-  GnShape s = gn_shape(N, HW, C, G);
-  return (long)N * s.chunks1 * G * 3 + (long)N * G * 2;
+  GnShape s = gn_shape(N, HW, C, G, 1);
+  return ((long)N * s.chunks1 * G * 3 + 3) / 4 * 4 + (long)N * G * 2;
 }
 
 // y = GroupNorm(x) * w + b (optionally SiLU), x/y [N, HW, C] (channels-last), w/b [C].
@@ -343,10 +438,11 @@ int amdk8s_groupnorm_nhwc(const void* x, const void* add, long add_stride, void*
                           const void* b, float* workspace, int* ticket, int N, int HW, int C, int G,
                           float eps, int silu, int dtype, hipStream_t stream) {
   if (N <= 0 || HW <= 0 || !gn_supported(C, G)) return -1;
-  GnShape s = gn_shape(N, HW, C, G);
+  GnShape s = gn_shape(N, HW, C, G, 1);
+  GnShape s2 = gn_shape(N, HW, C, G, 2);
   float* part = workspace;
-  float* stats = workspace + (size_t)N * s.chunks1 * G * 3;
-  const int threads = s.VC * s.R;
+  float* stats = workspace + ((size_t)N * s.chunks1 * G * 3 + 3) / 4 * 4;  // float2-aligned
+  const int threads = s.VC * s.R, threads2 = s2.VC * s2.R;
   const int nsub = threads / G > 0 ? threads / G : 1;
   const size_t red_f = (size_t)s.R * s.VC * 4, mrg_f = (size_t)nsub * G * 3;
   const size_t lds = (red_f > mrg_f ? red_f : mrg_f) * sizeof(float);
@@ -355,19 +451,19 @@ int amdk8s_groupnorm_nhwc(const void* x, const void* add, long add_stride, void*
   auto* yo = static_cast<uint16_t*>(y);
   const auto* wi = static_cast<const uint16_t*>(w);
   const auto* bi = static_cast<const uint16_t*>(b);
-  dim3 g1(s.chunks1, N), g2(s.chunks2, N);
+  dim3 g1(s.chunks1, N), g2(s2.chunks2, N);
   if (dtype == 1) {
     hipLaunchKernelGGL(gn_partial<true>, g1, dim3(threads), lds, stream, xi, ai, add_stride, part, stats, ticket, s, eps);
     if (silu)
-      hipLaunchKernelGGL((gn_apply<true, true>), g2, dim3(threads), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s);
+      hipLaunchKernelGGL((gn_apply<true, true>), g2, dim3(threads2), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s2);
     else
-      hipLaunchKernelGGL((gn_apply<true, false>), g2, dim3(threads), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s);
+      hipLaunchKernelGGL((gn_apply<true, false>), g2, dim3(threads2), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s2);
   } else {
     hipLaunchKernelGGL(gn_partial<false>, g1, dim3(threads), lds, stream, xi, ai, add_stride, part, stats, ticket, s, eps);
     if (silu)
-      hipLaunchKernelGGL((gn_apply<false, true>), g2, dim3(threads), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s);
+      hipLaunchKernelGGL((gn_apply<false, true>), g2, dim3(threads2), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s2);
     else
-      hipLaunchKernelGGL((gn_apply<false, false>), g2, dim3(threads), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s);
+      hipLaunchKernelGGL((gn_apply<false, false>), g2, dim3(threads2), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s2);
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
@@ -383,6 +479,31 @@ int amdk8s_geglu(const void* x, void* out, long M, int D, int dtype, hipStream_t
     hipLaunchKernelGGL(geglu_kernel<true>, dim3(blocks), dim3(256), 0, stream, xi, o, M, D);
   else
     hipLaunchKernelGGL(geglu_kernel<false>, dim3(blocks), dim3(256), 0, stream, xi, o, M, D);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// y = LayerNorm(x (+ delta)) over [M, C] rows; with delta, xs = x + delta is stored too.
+int amdk8s_add_layernorm(const void* x, const void* delta, void* xs, void* y, const void* gamma,
+                         const void* beta, long M, int C, float eps, int dtype, hipStream_t stream) {
+  if (M <= 0 || C % 8 != 0 || C / 8 > 64 * kLnVec) return -1;
+  const dim3 grid((unsigned)((M + 3) / 4)), block(256);
+  const auto* xi = static_cast<const uint16_t*>(x);
+  const auto* di = static_cast<const uint16_t*>(delta);
+  auto* so = static_cast<uint16_t*>(xs);
+  auto* yo = static_cast<uint16_t*>(y);
+  const auto* gi = static_cast<const uint16_t*>(gamma);
+  const auto* bi = static_cast<const uint16_t*>(beta);
+  if (dtype == 1) {
+    if (delta)
+      hipLaunchKernelGGL((add_layernorm_kernel<true, true>), grid, block, 0, stream, xi, di, so, yo, gi, bi, M, C, eps);
+    else
+      hipLaunchKernelGGL((add_layernorm_kernel<true, false>), grid, block, 0, stream, xi, di, so, yo, gi, bi, M, C, eps);
+  } else {
+    if (delta)
+      hipLaunchKernelGGL((add_layernorm_kernel<false, true>), grid, block, 0, stream, xi, di, so, yo, gi, bi, M, C, eps);
+    else
+      hipLaunchKernelGGL((add_layernorm_kernel<false, false>), grid, block, 0, stream, xi, di, so, yo, gi, bi, M, C, eps);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

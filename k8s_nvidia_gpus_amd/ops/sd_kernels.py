@@ -38,6 +38,8 @@ def _lib():
             lib.amdk8s_geglu.restype = ci
             lib.amdk8s_add3.argtypes = [vp, vp, vp, vp, cl, ci, ci, vp]
             lib.amdk8s_add3.restype = ci
+            lib.amdk8s_add_layernorm.argtypes = [vp, vp, vp, vp, vp, vp, cl, ci, cf, ci, vp]
+            lib.amdk8s_add_layernorm.restype = ci
             if hasattr(lib, "amdk8s_attention_fwd"):
                 lib.amdk8s_attention_supported.argtypes = [ci, ci, ci]
                 lib.amdk8s_attention_supported.restype = ci
@@ -105,6 +107,8 @@ def group_norm_nhwc(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, g
         if add.shape != (n, c) or add.stride(1) != 1:
             raise ValueError(f"group_norm_nhwc: addend must be [N, C] with unit column stride")
         add = add.to(x.dtype)
+        if add.data_ptr() % 16 or add.stride(0) % 8:   # the kernels read 8-channel vectors
+            add = add.contiguous()
         add_ptr, add_stride = add.data_ptr(), add.stride(0)
     rc = lib.amdk8s_groupnorm_nhwc(x.data_ptr(), add_ptr, add_stride, y.data_ptr(), w.data_ptr(),
                                    b.data_ptr(),
@@ -144,6 +148,34 @@ def add3(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor = None) -> torch.T
     _check(_lib().amdk8s_add3(a.data_ptr(), b.data_ptr(), bias_ptr, out.data_ptr(),
                               a.numel() // c, c, _DTYPE[a.dtype], _stream(a)), "amdk8s_add3")
     return out
+
+
+def add_layernorm(x: torch.Tensor, delta, weight: torch.Tensor, bias: torch.Tensor,
+                  eps: float):
+    """LayerNorm over the last dim of ``x (+ delta)``.  Returns ``y`` (no delta) or ``(x + delta, y)``."""
+    if x.dtype not in _DTYPE:
+        raise TypeError(f"add_layernorm: {x.dtype} (fp16/bf16 only)")
+    x = x.contiguous()
+    c = x.shape[-1]
+    y = torch.empty_like(x)
+    xs = None
+    dptr = sptr = None
+    if delta is not None:
+        delta = delta.contiguous()
+        if delta.shape != x.shape or delta.dtype != x.dtype:
+            raise ValueError("add_layernorm: delta must match x")
+        xs = torch.empty_like(x)
+        dptr, sptr = delta.data_ptr(), xs.data_ptr()
+    w = weight.to(x.dtype).contiguous()
+    b = bias.to(x.dtype).contiguous()
+    _check(_lib().amdk8s_add_layernorm(x.data_ptr(), dptr, sptr, y.data_ptr(), w.data_ptr(),
+                                       b.data_ptr(), x.numel() // c, c, float(eps),
+                                       _DTYPE[x.dtype], _stream(x)), "amdk8s_add_layernorm")
+    return y if delta is None else (xs, y)
+
+
+def layernorm_supported(c: int) -> bool:
+    return c % 8 == 0 and c // 8 <= 256
 
 
 def attention_supported(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int) -> bool:

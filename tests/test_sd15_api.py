@@ -1,8 +1,9 @@
-"""SD1.5 REST service: HTTP surface, request coalescing, seeding, validation — with a fake pipeline.
+"""SD1.5 REST service: HTTP surface, request coalescing, seeding, validation.
 
-diffusers is only installed in the serving image, so the pipeline is a deterministic fake that
-records every batched call; the FastAPI app, the GPU worker and the batching logic are the real
-ones (k8s_nvidia_gpus_amd/models/sd15_api.py, shipped verbatim as the sd15-app ConfigMap).
+Most tests use a deterministic fake pipeline that records every batched call (fast, exact batch
+accounting); the FastAPI app, the GPU worker and the batching logic are the real ones
+(k8s_nvidia_gpus_amd/models/sd15_api.py).  The last tests serve the in-tree SD1.5 pipeline itself
+(miniature config on CPU).
 """
 import io
 import threading
@@ -147,3 +148,30 @@ def test_load_failure_surfaces_in_readyz():
         r = c.get("/readyz")
         assert r.status_code == 500 and "weights not found" in r.text
         assert c.post("/generate", json={"prompt": "x"}).status_code == 500
+
+
+def test_native_pipeline_serves_end_to_end_on_cpu():
+    """Default factory (PIPELINE=native): the in-tree SD1.5 (miniature config on CPU) behind the
+    real HTTP worker — warm-up runs before ready, seeded requests are reproducible PNGs."""
+    s = Settings(device="cpu", dtype="float32", model_config="tiny", warmup_batches="1,2",
+                 batch_window_ms=5)
+    app = create_app(s)
+    with TestClient(app) as c:
+        assert app.state.worker.wait_ready(120), app.state.worker.load_error
+        body = {"prompt": "a cozy cabin", "steps": 3, "width": 64, "height": 64, "seed": 7}
+        r1 = c.post("/generate", json=body)
+        r2 = c.post("/generate", json=body)
+        assert r1.status_code == 200 and r1.headers["content-type"] == "image/png"
+        assert Image.open(io.BytesIO(r1.content)).size == (64, 64)
+        assert r1.content == r2.content
+        assert c.get("/readyz").json()["ready"] is True
+
+
+def test_unknown_pipeline_kind_fails_readiness():
+    app = create_app(Settings(device="cpu", dtype="float32", pipeline="onnx"))
+    with TestClient(app) as c:
+        for _ in range(100):
+            if app.state.worker.load_error is not None:
+                break
+            time.sleep(0.02)
+        assert c.get("/readyz").status_code == 500

@@ -201,3 +201,37 @@ def test_group_norm_with_addend_and_add3(SK, dev, dtype):
     s = SK.add3(x, z, bias)
     torch.testing.assert_close(s.float(), x.float() + z.float() + bias.float()[:, None, None],
                                rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("c", [320, 640, 1280, 2048])
+def test_add_layernorm_vs_fp32(SK, dev, dtype, c):
+    g = torch.Generator(device=dev).manual_seed(c)
+    x = (torch.randn(2, 1000, c, generator=g, device=dev) * 2 + 1).to(dtype)
+    dl = torch.randn(2, 1000, c, generator=g, device=dev).to(dtype)
+    w = (torch.rand(c, generator=g, device=dev) + 0.5).to(dtype)
+    b = torch.randn(c, generator=g, device=dev).to(dtype)
+    tol = 3e-2 if dtype == torch.bfloat16 else 6e-3
+    y = SK.add_layernorm(x, None, w, b, 1e-5)
+    ref = torch.nn.functional.layer_norm(x.float(), (c,), w.float(), b.float(), 1e-5)
+    torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+    xs, y2 = SK.add_layernorm(x, dl, w, b, 1e-5)
+    assert torch.equal(xs, x + dl)
+    ref2 = torch.nn.functional.layer_norm((x + dl).float(), (c,), w.float(), b.float(), 1e-5)
+    torch.testing.assert_close(y2.float(), ref2, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("growing", [True, False])
+def test_attention_deferred_rescale_branch(SK, dev, growing):
+    """Scores whose row max grows tile after tile (rescale taken at many tiles) or only shrinks
+    (never taken after the first tile): both must match the fp32 reference."""
+    g = torch.Generator(device=dev).manual_seed(21)
+    lk = 1024
+    q = torch.randn(1, 512, 320, generator=g, device=dev)
+    k = torch.randn(1, lk, 320, generator=g, device=dev)
+    ramp = torch.linspace(0.2, 6.0, lk, device=dev)
+    k = k * (ramp if growing else ramp.flip(0))[None, :, None]
+    v = torch.randn(1, lk, 320, generator=g, device=dev)
+    q, k, v = q.half(), k.half(), v.half()
+    o = SK.attention(q, k, v, 8, 40 ** -0.5)
+    torch.testing.assert_close(o.float(), _attn_ref(q, k, v, 8, 40 ** -0.5), rtol=6e-3, atol=6e-3)

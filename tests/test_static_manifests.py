@@ -224,13 +224,24 @@ def test_operator_daemonsets_gate_on_markers_and_share_config():
     assert rc["handler"] == "amd" and rc["metadata"]["name"] == "amd"
 
 
-def test_sd15_app_source_in_sync_and_no_pypi_torch():
-    app = (CC / "apps/sd15-api/app/app.py").read_text()
-    assert app == (REPO / "k8s_nvidia_gpus_amd/models/sd15_api.py").read_text(), \
-        "run: python -m k8s_nvidia_gpus_amd.utils.sync_apps"
-    reqs = (CC / "apps/sd15-api/app/requirements.txt").read_text().splitlines()
-    pkgs = [r.split("==")[0].split("[")[0].strip().lower() for r in reqs if r.strip() and not r.startswith("#")]
-    assert "torch" not in pkgs and "torchvision" not in pkgs
+def test_sd15_runs_the_in_tree_pipeline_from_the_image():
+    """The service and the SD1.5 model ship prebuilt in the image: no pip install at pod start,
+    no diffusers; the init container fetches exactly the files the in-tree loader reads."""
+    dep = load_all(CC / "apps/sd15-api/deployment.yaml")[0]
+    spec = dep["spec"]["template"]["spec"]
+    api = spec["containers"][0]
+    assert api["command"] == ["python3", "-m", "k8s_nvidia_gpus_amd.models.sd15_api"]
+    env = {e["name"]: e["value"] for e in api["env"]}
+    assert env["PIPELINE"] == "native" and env["MODEL_DIR"] == "/models/sd15"
+    assert "pip install" not in yaml.safe_dump(dep)
+    fetch = spec["initContainers"][0]["args"][0]
+    files = re.findall(r"fetch (\S+) \d+", fetch)
+    for sub, stem in (("unet", "diffusion_pytorch_model"), ("vae", "diffusion_pytorch_model"),
+                      ("text_encoder", "model")):
+        assert f"{sub}/{stem}.fp16.safetensors" in files   # weights.find_file takes .fp16 too
+    assert {"tokenizer/vocab.json", "tokenizer/merges.txt"} <= set(files)
+    docker = (REPO / "images/bench/Dockerfile").read_text()
+    assert "fastapi" in docker and "diffusers" not in docker and "ops.build all" in docker
 
 
 def test_sd15_service_keeps_reference_nodeport():
