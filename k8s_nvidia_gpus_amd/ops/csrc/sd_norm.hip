@@ -6,20 +6,21 @@
 // Cg = 4..80).  Each thread owns ONE fixed 8-channel vector column (vc) and walks rows, so rows are
 // read fully coalesced (C*2 bytes contiguous per pixel) and the per-thread group split is a compile-
 // free constant.  Two launches:
-//   1. gn_partial: blocks = N x chunks.  Per (n, chunk, group): count / mean / M2 in fp32 (per-thread
-//      sums over a few hundred elements, then a deterministic in-block reduction).  The LAST block of
-//      each n to finish (atomic ticket) merges the chunks with Chan's parallel-variance formula into
-//      stats[n][g] = (mean, rstd) and re-arms the ticket (self-resetting: safe inside HIP graphs).
-//   2. gn_apply: y = x * a_c + b_c (a_c = rstd*w_c, b_c = bias_c - mean*a_c, per thread in
-//      registers), optional SiLU, 16-byte stores.
-// Deterministic: no float atomics anywhere; the ticket counts blocks only.
+//   1. gn_partial: blocks = N x (<= 16 chunks).  Per (n, chunk, group): count / mean / M2 in fp32
+//      (per-thread sums over a few rows, then a tree reduction over the block's row slots).
+//   2. gn_apply: every block first merges its image's chunk partials (LDS, Chan's parallel-variance
+//      formula) into (mean, rstd) per group — no block publishes stats to another, so there is no
+//      inter-block fence (on MI355X an agent-scope fence writes back L2 across the 8 XCDs) and
+//      nothing to reset between calls — then y = x * a_c + b_c (a_c = rstd*w_c, b_c = bias_c -
+//      mean*a_c, per thread in registers), optional SiLU, 16-byte stores.
+// Deterministic: no atomics anywhere.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace {
 
 constexpr int kMaxThreads = 1024;
-constexpr int kMergeMax = 8;  // partials merged per thread by the last block (see gn_shape)
+constexpr int kMaxChunks = 16;  // stats-pass chunks per image (merged by every apply block)
 
 __device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
 
@@ -89,8 +90,7 @@ struct GnShape {
 // Partial layout: part[((n * chunks1 + chunk) * G + g) * 3 + {count, mean, M2}]
 template <bool BF16>
 __global__ void gn_partial(const uint16_t* __restrict__ x, const uint16_t* __restrict__ add,
-                           long add_stride, float* __restrict__ part, float* __restrict__ stats,
-                           int* __restrict__ ticket, GnShape s, float eps) {
+                           long add_stride, float* __restrict__ part, GnShape s) {
   const int tid = threadIdx.x;
   const int chunk = blockIdx.x, n = blockIdx.y;
   const int vc = tid % s.VC, r = tid / s.VC;
@@ -159,73 +159,58 @@ __global__ void gn_partial(const uint16_t* __restrict__ x, const uint16_t* __res
     p[1] = mean;
     p[2] = m2;
   }
-  // last block of image n merges all chunks: nsub threads per group each merge a strided subset
-  // of the chunks (independent loads, pipelined), then one thread per group merges the nsub results
-  __shared__ int last;
-  __threadfence();
-  __syncthreads();
-  if (tid == 0) last = (atomicAdd(&ticket[n], 1) == s.chunks1 - 1);
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  const int nsub = max(1, (int)blockDim.x / s.G);
-  float* mrg = lds;  // [nsub][G][3], reuses the reduction scratch (>= that size, see host)
-  if (tid < nsub * s.G) {
-    const int g = tid % s.G, sub = tid / s.G;
-    // all loads first (independent, in flight together), then the merge; plain loads: only this
-    // last block ever reads the partials, so no L1 line of them can be stale
-    float pc[kMergeMax], pm[kMergeMax], pq[kMergeMax];
-#pragma unroll
-    for (int j = 0; j < kMergeMax; ++j) {
-      const int k = sub + j * nsub;
-      pc[j] = pm[j] = pq[j] = 0.f;
-      if (k < s.chunks1) {
-        const float* p = part + (((size_t)n * s.chunks1 + k) * s.G + g) * 3;
-        pc[j] = p[0];
-        pm[j] = p[1];
-        pq[j] = p[2];
-      }
-    }
-    float cnt = 0.f, mean = 0.f, m2 = 0.f;
-#pragma unroll
-    for (int j = 0; j < kMergeMax; ++j) {
-      const float tot = cnt + pc[j];
-      const float f = pc[j] > 0.f ? pc[j] / tot : 0.f;
-      const float d = pm[j] - mean;
-      mean += d * f;
-      m2 += pq[j] + d * d * cnt * f;
-      cnt = tot;
-    }
-    mrg[(sub * s.G + g) * 3 + 0] = cnt;
-    mrg[(sub * s.G + g) * 3 + 1] = mean;
-    mrg[(sub * s.G + g) * 3 + 2] = m2;
-  }
-  __syncthreads();
-  for (int g = tid; g < s.G; g += blockDim.x) {
-    float cnt = 0.f, mean = 0.f, m2 = 0.f;
-    for (int sub = 0; sub < nsub; ++sub) {
-      const float cb = mrg[(sub * s.G + g) * 3 + 0];
-      if (cb <= 0.f) continue;
-      const float mb = mrg[(sub * s.G + g) * 3 + 1], m2b = mrg[(sub * s.G + g) * 3 + 2];
-      const float tot = cnt + cb;
-      const float d = mb - mean;
-      mean += d * (cb / tot);
-      m2 += m2b + d * d * (cnt * cb / tot);
-      cnt = tot;
-    }
-    const float var = cnt > 0.f ? m2 / cnt : 0.f;
-    stats[((size_t)n * s.G + g) * 2 + 0] = mean;
-    stats[((size_t)n * s.G + g) * 2 + 1] = rsqrtf(var + eps);
-  }
-  if (tid == 0) atomicExch(&ticket[n], 0);
 }
 
 template <bool BF16, bool SILU>
 __global__ void gn_apply(const uint16_t* __restrict__ x, const uint16_t* __restrict__ add,
                          long add_stride, uint16_t* __restrict__ y,
                          const uint16_t* __restrict__ w, const uint16_t* __restrict__ b,
-                         const float* __restrict__ stats, GnShape s) {
+                         const float* __restrict__ part, int chunks1, float eps, GnShape s) {
   const int tid = threadIdx.x;
+  // prologue: this image's chunk partials → LDS (coalesced), then per-group Chan merge.  Every
+  // block redoes this small merge (chunks1 * G * 3 floats, L2-resident) instead of any block
+  // publishing stats to the others: no inter-block fences (cross-XCD L2 writeback) and no tickets.
+  extern __shared__ float lds[];
+  float* pl = lds;                           // [chunks1][G][3]
+  float2* st = reinterpret_cast<float2*>(lds + ((chunks1 * s.G * 3 + 1) & ~1));  // [G]
+  const float* pn = part + (size_t)blockIdx.y * chunks1 * s.G * 3;
+  for (int i = tid; i < chunks1 * s.G * 3; i += blockDim.x) pl[i] = pn[i];
+  __syncthreads();
+  // (group, sub) threads each merge a strided subset of the chunks, then one thread per group
+  // merges the nsub results: two short serial chains instead of one chunks1-long one
+  const int nsub = max(1, min((int)blockDim.x / s.G, chunks1));
+  float* mg = lds + ((chunks1 * s.G * 3 + 1) & ~1) + 2 * s.G;  // [nsub][G][3]
+  if (tid < nsub * s.G) {
+    const int g = tid % s.G, sub = tid / s.G;
+    float cnt = 0.f, mean = 0.f, m2 = 0.f;
+    for (int k = sub; k < chunks1; k += nsub) {
+      const float cb = pl[(k * s.G + g) * 3 + 0];
+      const float tot = cnt + cb;
+      const float f = cb > 0.f ? cb / tot : 0.f;
+      const float d = pl[(k * s.G + g) * 3 + 1] - mean;
+      mean += d * f;
+      m2 += pl[(k * s.G + g) * 3 + 2] + d * d * cnt * f;
+      cnt = tot;
+    }
+    mg[(sub * s.G + g) * 3 + 0] = cnt;
+    mg[(sub * s.G + g) * 3 + 1] = mean;
+    mg[(sub * s.G + g) * 3 + 2] = m2;
+  }
+  __syncthreads();
+  for (int g = tid; g < s.G; g += blockDim.x) {
+    float cnt = 0.f, mean = 0.f, m2 = 0.f;
+    for (int k = 0; k < nsub; ++k) {
+      const float cb = mg[(k * s.G + g) * 3 + 0];
+      const float tot = cnt + cb;
+      const float f = cb > 0.f ? cb / tot : 0.f;
+      const float d = mg[(k * s.G + g) * 3 + 1] - mean;
+      mean += d * f;
+      m2 += mg[(k * s.G + g) * 3 + 2] + d * d * cnt * f;
+      cnt = tot;
+    }
+    st[g] = make_float2(mean, rsqrtf((cnt > 0.f ? m2 / cnt : 0.f) + eps));
+  }
+  __syncthreads();
   const int chunk = blockIdx.x, n = blockIdx.y;
   const int vc = tid % s.VC, r = tid / s.VC;
   const int c0 = vc * 8;
@@ -235,8 +220,8 @@ __global__ void gn_apply(const uint16_t* __restrict__ x, const uint16_t* __restr
   if (add)
     unpack8<BF16>(*reinterpret_cast<const uint4*>(add + n * add_stride + c0), av);
   const int g_lo = c0 / s.Cg, g_hi = (c0 + 7) / s.Cg;  // at most two groups per vector
-  const float2 st_lo = reinterpret_cast<const float2*>(stats)[(size_t)n * s.G + g_lo];
-  const float2 st_hi = reinterpret_cast<const float2*>(stats)[(size_t)n * s.G + g_hi];
+  const float2 st_lo = st[g_lo];
+  const float2 st_hi = st[g_hi];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const bool lo = (c0 + i) / s.Cg == g_lo;
@@ -309,8 +294,6 @@ __global__ void add3_kernel(const uint16_t* __restrict__ a, const uint16_t* __re
   }
 }
 
-// pass = 1: stats (big blocks: ~1024 threads, <= 64 chunks per image, so the last block's merge is
-// 1-2 partials per thread); pass = 2: apply (~384-thread blocks, ~2048 blocks overall)
 // LayerNorm over rows of C channels (C % 8 == 0, C <= 64*8*kLnVec), one wave per row, values held
 // in registers between the mean and the variance pass (exact two-pass variance).  With `delta`
 // it is the transformer block's residual add fused in front: xs = x + delta is written out (the
@@ -379,6 +362,7 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(
   }
 }
 
+// pass = 1: stats pass shape; pass = 2: apply pass shape
 GnShape gn_shape(int N, int HW, int C, int G, int pass) {
   GnShape s{};
   s.N = N;
@@ -387,25 +371,20 @@ GnShape gn_shape(int N, int HW, int C, int G, int pass) {
   s.G = G;
   s.Cg = C / G;
   s.VC = C / 8;
-  // ~256-thread blocks (VC channel vectors x R row slots), 8 rows per thread (unrolled loads)
-  s.R = s.VC >= 256 ? 1 : 256 / s.VC;
-  if (s.R > HW) s.R = HW;
-  int rows = s.R * 8;
-  int chunks = (HW + rows - 1) / rows;
-  if (pass == 1) {  // the last block merges <= kMergeMax partials per thread
-    const int nsub = (s.VC * s.R) / G > 0 ? (s.VC * s.R) / G : 1;
-    const int cap = kMergeMax * nsub;
-    if (chunks > cap) {
-      chunks = cap;
-      rows = (HW + chunks - 1) / chunks;
-    }
-  }
   if (pass == 1) {
-    s.rows1 = rows;
-    s.chunks1 = (HW + rows - 1) / rows;
+    // stats: ~1024-thread blocks, <= kMaxChunks chunks per image (every apply block merges them)
+    s.R = s.VC >= 1024 ? 1 : 1024 / s.VC;
+    if (s.R > HW) s.R = HW;
+    int chunks = (HW + s.R - 1) / s.R;
+    if (chunks > kMaxChunks) chunks = kMaxChunks;
+    s.rows1 = (HW + chunks - 1) / chunks;
+    s.chunks1 = (HW + s.rows1 - 1) / s.rows1;
   } else {
-    s.rows2 = rows;
-    s.chunks2 = (HW + rows - 1) / rows;
+    // apply: ~256-thread blocks, 8 rows per thread (unrolled loads)
+    s.R = s.VC >= 256 ? 1 : 256 / s.VC;
+    if (s.R > HW) s.R = HW;
+    s.rows2 = s.R * 8;
+    s.chunks2 = (HW + s.rows2 - 1) / s.rows2;
   }
   return s;
 }
@@ -425,45 +404,45 @@ extern "C" {
 
 int amdk8s_groupnorm_supported(int C, int G) { return gn_supported(C, G) ? 1 : 0; }
 
-// Workspace floats needed by amdk8s_groupnorm_nhwc (partials + stats).
+// Workspace floats needed by amdk8s_groupnorm_nhwc (the stats pass's chunk partials).
 long amdk8s_groupnorm_workspace(int N, int HW, int C, int G) {
   GnShape s = gn_shape(N, HW, C, G, 1);
-  return ((long)N * s.chunks1 * G * 3 + 3) / 4 * 4 + (long)N * G * 2;
+  return (long)N * s.chunks1 * G * 3;
 }
 
 // y = GroupNorm(x) * w + b (optionally SiLU), x/y [N, HW, C] (channels-last), w/b [C].
-// dtype: 0 = fp16, 1 = bf16.  ticket: >= N zeroed ints, owned by the caller, left zeroed.
+// dtype: 0 = fp16, 1 = bf16.
 // add (nullable): per-(n, c) addend [N, C] with row stride add_stride: y = GroupNorm(x + add[n, c])
 int amdk8s_groupnorm_nhwc(const void* x, const void* add, long add_stride, void* y, const void* w,
-                          const void* b, float* workspace, int* ticket, int N, int HW, int C, int G,
-                          float eps, int silu, int dtype, hipStream_t stream) {
+                          const void* b, float* workspace, int N, int HW, int C, int G, float eps,
+                          int silu, int dtype, hipStream_t stream) {
   if (N <= 0 || HW <= 0 || !gn_supported(C, G)) return -1;
   GnShape s = gn_shape(N, HW, C, G, 1);
   GnShape s2 = gn_shape(N, HW, C, G, 2);
-  float* part = workspace;
-  float* stats = workspace + ((size_t)N * s.chunks1 * G * 3 + 3) / 4 * 4;  // float2-aligned
   const int threads = s.VC * s.R, threads2 = s2.VC * s2.R;
-  const int nsub = threads / G > 0 ? threads / G : 1;
-  const size_t red_f = (size_t)s.R * s.VC * 4, mrg_f = (size_t)nsub * G * 3;
-  const size_t lds = (red_f > mrg_f ? red_f : mrg_f) * sizeof(float);
+  const size_t lds1 = (size_t)s.R * s.VC * 4 * sizeof(float);
+  const int nsub2 = threads2 / G > 0 ? (threads2 / G < s.chunks1 ? threads2 / G : s.chunks1) : 1;
+  const size_t lds2 =
+      ((size_t)((s.chunks1 * G * 3 + 1) & ~1) + 2 * G + (size_t)nsub2 * G * 3) * sizeof(float);
   const auto* xi = static_cast<const uint16_t*>(x);
   const auto* ai = static_cast<const uint16_t*>(add);
   auto* yo = static_cast<uint16_t*>(y);
   const auto* wi = static_cast<const uint16_t*>(w);
   const auto* bi = static_cast<const uint16_t*>(b);
   dim3 g1(s.chunks1, N), g2(s2.chunks2, N);
+  const int c1 = s.chunks1;
   if (dtype == 1) {
-    hipLaunchKernelGGL(gn_partial<true>, g1, dim3(threads), lds, stream, xi, ai, add_stride, part, stats, ticket, s, eps);
+    hipLaunchKernelGGL(gn_partial<true>, g1, dim3(threads), lds1, stream, xi, ai, add_stride, workspace, s);
     if (silu)
-      hipLaunchKernelGGL((gn_apply<true, true>), g2, dim3(threads2), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s2);
+      hipLaunchKernelGGL((gn_apply<true, true>), g2, dim3(threads2), lds2, stream, xi, ai, add_stride, yo, wi, bi, workspace, c1, eps, s2);
     else
-      hipLaunchKernelGGL((gn_apply<true, false>), g2, dim3(threads2), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s2);
+      hipLaunchKernelGGL((gn_apply<true, false>), g2, dim3(threads2), lds2, stream, xi, ai, add_stride, yo, wi, bi, workspace, c1, eps, s2);
   } else {
-    hipLaunchKernelGGL(gn_partial<false>, g1, dim3(threads), lds, stream, xi, ai, add_stride, part, stats, ticket, s, eps);
+    hipLaunchKernelGGL(gn_partial<false>, g1, dim3(threads), lds1, stream, xi, ai, add_stride, workspace, s);
     if (silu)
-      hipLaunchKernelGGL((gn_apply<false, true>), g2, dim3(threads2), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s2);
+      hipLaunchKernelGGL((gn_apply<false, true>), g2, dim3(threads2), lds2, stream, xi, ai, add_stride, yo, wi, bi, workspace, c1, eps, s2);
     else
-      hipLaunchKernelGGL((gn_apply<false, false>), g2, dim3(threads2), 0, stream, xi, ai, add_stride, yo, wi, bi, stats, s2);
+      hipLaunchKernelGGL((gn_apply<false, false>), g2, dim3(threads2), lds2, stream, xi, ai, add_stride, yo, wi, bi, workspace, c1, eps, s2);
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

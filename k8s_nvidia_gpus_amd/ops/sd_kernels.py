@@ -9,7 +9,6 @@ from __future__ import annotations
 
 import ctypes
 import threading
-from typing import Dict
 
 import torch
 
@@ -18,7 +17,6 @@ from .kernels import library
 _DTYPE = {torch.float16: 0, torch.bfloat16: 1}
 _declared = False
 _lock = threading.Lock()
-_tickets: Dict[int, torch.Tensor] = {}
 
 
 def _lib():
@@ -31,8 +29,8 @@ def _lib():
             lib.amdk8s_groupnorm_supported.restype = ci
             lib.amdk8s_groupnorm_workspace.argtypes = [ci, ci, ci, ci]
             lib.amdk8s_groupnorm_workspace.restype = cl
-            lib.amdk8s_groupnorm_nhwc.argtypes = [vp, vp, cl, vp, vp, vp, vp, vp, ci, ci, ci, ci,
-                                                  cf, ci, ci, vp]
+            lib.amdk8s_groupnorm_nhwc.argtypes = [vp, vp, cl, vp, vp, vp, vp, ci, ci, ci, ci, cf,
+                                                  ci, ci, vp]
             lib.amdk8s_groupnorm_nhwc.restype = ci
             lib.amdk8s_geglu.argtypes = [vp, vp, cl, ci, ci, vp]
             lib.amdk8s_geglu.restype = ci
@@ -52,19 +50,6 @@ def _lib():
 
 def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
-
-
-def _ticket(device: torch.device) -> torch.Tensor:
-    """Per-device block-ticket array of the GroupNorm stats pass (self-resetting, zero at rest)."""
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    t = _tickets.get(idx)
-    if t is None:
-        if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("group_norm_nhwc: first call must happen outside HIP-graph capture")
-        t = torch.zeros(4096, dtype=torch.int32, device=device)
-        torch.cuda.synchronize(device)
-        _tickets[idx] = t
-    return t
 
 
 def _check(rc: int, what: str) -> None:
@@ -96,8 +81,6 @@ def group_norm_nhwc(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, g
         raise ValueError("group_norm_nhwc: 3-D or 4-D input")
     if not lib.amdk8s_groupnorm_supported(c, groups):
         raise ValueError(f"group_norm_nhwc: C={c}, groups={groups} not supported")
-    if n > 4096:
-        raise ValueError("group_norm_nhwc: batch > 4096")
     w = weight.to(x.dtype).contiguous()
     b = bias.to(x.dtype).contiguous()
     ws = torch.empty(lib.amdk8s_groupnorm_workspace(n, hw, c, groups), dtype=torch.float32,
@@ -112,7 +95,7 @@ def group_norm_nhwc(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, g
         add_ptr, add_stride = add.data_ptr(), add.stride(0)
     rc = lib.amdk8s_groupnorm_nhwc(x.data_ptr(), add_ptr, add_stride, y.data_ptr(), w.data_ptr(),
                                    b.data_ptr(),
-                                   ws.data_ptr(), _ticket(x.device).data_ptr(), n, hw, c, groups,
+                                   ws.data_ptr(), n, hw, c, groups,
                                    float(eps), int(silu), _DTYPE[x.dtype], _stream(x))
     _check(rc, "amdk8s_groupnorm_nhwc")
     return y

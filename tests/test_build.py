@@ -31,6 +31,17 @@ def test_kernel_library_exports(built):
         assert s in syms, s
 
 
+def test_sd_kernel_bindings_resolve_in_the_library(built):
+    """Every C symbol the SD1.5 bindings declare (ops/sd_kernels.py) is exported."""
+    import re
+
+    syms = _nm(B.KERNEL_LIB)
+    src = (B.PKG_DIR / "sd_kernels.py").read_text()
+    names = set(re.findall(r"lib\.(amdk8s_\w+)\.argtypes", src))
+    assert len(names) >= 8
+    assert names <= syms, names - syms
+
+
 def test_kernel_library_targets_gfx950_only(built):
     blob = B.KERNEL_LIB.read_bytes()
     assert b"gfx950" in blob
