@@ -1,0 +1,341 @@
+"""Qwen2 inference engine for one MI355X: K-quant GEMV decode on hand-written HIP kernels, replayed
+from HIP graphs; prompt processing on an fp16 copy of the weights; a slot-based KV cache.
+
+The reference runs ``llama-server -m <Q4_K_M gguf> --ctx-size 4096 --n-gpu-layers 35`` (reference
+cluster-config/apps/llm/deployment.yaml:61-84); this is the in-tree MI355X engine behind the same
+kind of server (``server.py``).  Design points:
+
+* **Decode (the hot loop)** is HBM-bound: per token every weight byte is read once.  Per layer:
+  RMSNorm+Q8-quantise → fused q|k|v GEMV (+bias) → RoPE + KV-cache write → split-context
+  attention + combine + Q8-quantise → o_proj GEMV (+= residual) → RMSNorm+Q8 → gate|up pair GEMV
+  (SwiGLU epilogue) → Q8 → ffn_down GEMV (+= residual); then the final norm and the lm_head.
+  ``T <= 4`` concurrent sequences share one weight pass (continuous batching).  Every step of a
+  given ``T`` is captured once into a ``torch.cuda.CUDAGraph`` (a HIP graph on ROCm) and replayed,
+  so the ~290 launches of a 28-layer step cost no host time.
+* **Prefill** is compute-bound: with ``dense=True`` the engine keeps an fp16 copy of every matrix
+  (HBM is plentiful: +15 GB for 7B) and runs the prompt through library GEMMs (hipBLASLt) and
+  SDPA, writing the KV cache.  Without it, prompts run through the decode kernels 4 tokens at a
+  time (causality comes from each token's own length).
+* **KV cache**: fp16 ``[layers, slots, kv_heads, max_ctx, 128]`` — one contiguous slab per
+  sequence slot; the server maps requests to slots.
+
+On a CPU (tests) the same API runs the fp32 reference maths (dequantised weights, PyTorch ops);
+the GPU path is compared against it.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.nn.functional as F
+
+from .config import LLMConfig
+from .weights import ModelWeights, QWeight
+
+
+def rope_tables(max_ctx: int, head_dim: int, theta: float, device) -> tuple:
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    ang = torch.arange(max_ctx, dtype=torch.float64)[:, None] * inv[None, :]
+    return ang.cos().float().to(device), ang.sin().float().to(device)
+
+
+def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """NeoX rotation (pairs i, i + d/2) — llama.cpp's rope type for qwen2.  x [..., P, d]."""
+    h = x.shape[-1] // 2
+    x0, x1 = x[..., :h], x[..., h:]
+    return torch.cat([x0 * cos - x1 * sin, x0 * sin + x1 * cos], -1)
+
+
+@dataclass
+class StepBuffers:
+    """Static tensors of one decode step size ``T`` (graph-captured)."""
+    T: int
+    tok: torch.Tensor
+    pos: torch.Tensor
+    slot: torch.Tensor
+    h: torch.Tensor
+    x8: torch.Tensor
+    dx: torch.Tensor
+    sx: torch.Tensor
+    qkv: torch.Tensor
+    qrot: torch.Tensor
+    po: torch.Tensor
+    pml: torch.Tensor
+    t: torch.Tensor
+    logits: torch.Tensor
+    graph: Optional[torch.cuda.CUDAGraph] = None
+
+
+class Engine:
+    def __init__(self, weights: ModelWeights, max_ctx: int = 4096, slots: int = 4,
+                 dense: Optional[bool] = None, use_graphs: bool = True):
+        self.w = weights
+        self.cfg: LLMConfig = weights.cfg
+        self.device = weights.out_norm.device
+        self.gpu = self.device.type == "cuda"
+        chunk = 256
+        self.max_ctx = (max_ctx + chunk - 1) // chunk * chunk
+        self.slots = slots
+        self.use_graphs = use_graphs and self.gpu
+        c = self.cfg
+        if c.head_dim != 128 and self.gpu:
+            raise ValueError(f"head_dim {c.head_dim}: the decode kernels are built for 128")
+        self.kv_dtype = torch.float16 if self.gpu else torch.float32
+        shape = (c.layers, slots, c.kv_heads, self.max_ctx, c.head_dim)
+        self.k_cache = torch.zeros(shape, dtype=self.kv_dtype, device=self.device)
+        self.v_cache = torch.zeros(shape, dtype=self.kv_dtype, device=self.device)
+        self.cos, self.sin = rope_tables(self.max_ctx, c.head_dim, c.rope_theta, self.device)
+        self.dense = self.gpu if dense is None else dense
+        self._dense_w: Optional[Dict[str, torch.Tensor]] = None
+        self._bufs: Dict[int, StepBuffers] = {}
+        self.rows_per_wg = int(os.environ.get("AMDK8S_LLM_ROWS_PER_WG", "0"))
+        if self.gpu:
+            from k8s_nvidia_gpus_amd.ops import llm_kernels as LK
+
+            self.LK = LK
+            self.max_T = LK.max_tokens()
+        else:
+            self.max_T = 4
+        self.stats = {"decode_steps": 0, "decode_tokens": 0, "prefill_tokens": 0,
+                      "graph_captures": 0}
+
+    # ------------------------------------------------------------------ dense weights (prefill / CPU)
+    def dense_weights(self) -> Dict[str, torch.Tensor]:
+        if self._dense_w is None:
+            dt = torch.float16 if self.gpu else torch.float32
+            d: Dict[str, torch.Tensor] = {}
+            for i, L in enumerate(self.w.layers):
+                d[f"{i}.qkv"] = torch.cat([w.dequant(dt) for w in L.wqkv], 0)
+                d[f"{i}.o"] = L.wo.dequant(dt)
+                d[f"{i}.gu"] = torch.cat([L.wg.dequant(dt), L.wu.dequant(dt)], 0)
+                d[f"{i}.down"] = L.wd.dequant(dt)
+            d["out"] = self.w.output.dequant(dt)
+            self._dense_w = d
+        return self._dense_w
+
+    def embed(self, tokens: torch.Tensor) -> torch.Tensor:
+        return self.w.tok_embd.dequant(torch.float32, rows=tokens.to(self.device))
+
+    # ------------------------------------------------------------------ dense forward
+    def _forward_dense(self, tokens: torch.Tensor, slot: int, start: int) -> torch.Tensor:
+        """Prompt tokens [P] of one sequence at positions start..start+P-1 → last-position logits
+        (fp32 [vocab]).  Writes the KV cache."""
+        c = self.cfg
+        W = self.dense_weights()
+        dt = torch.float16 if self.gpu else torch.float32
+        P = tokens.numel()
+        end = start + P
+        x = self.embed(tokens)                                  # fp32 [P, dim]
+        cos, sin = self.cos[start:end], self.sin[start:end]
+        mask = None
+        if P > 1:
+            qi = torch.arange(start, end, device=self.device)[:, None]
+            kj = torch.arange(end, device=self.device)[None, :]
+            mask = kj <= qi
+        for i, L in enumerate(self.w.layers):
+            xn = (x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + c.eps) * L.attn_norm).to(dt)
+            qkv = (xn @ W[f"{i}.qkv"].t()).float() + L.bqkv
+            q = qkv[:, :c.dim].view(P, c.heads, c.head_dim).transpose(0, 1)
+            k = qkv[:, c.dim:c.dim + c.kv_dim].view(P, c.kv_heads, c.head_dim).transpose(0, 1)
+            v = qkv[:, c.dim + c.kv_dim:].view(P, c.kv_heads, c.head_dim).transpose(0, 1)
+            q = apply_rope(q, cos, sin)
+            k = apply_rope(k, cos, sin)
+            self.k_cache[i, slot, :, start:end] = k.to(self.kv_dtype)
+            self.v_cache[i, slot, :, start:end] = v.to(self.kv_dtype)
+            kk = self.k_cache[i, slot, :, :end].to(dt).repeat_interleave(c.group, 0)
+            vv = self.v_cache[i, slot, :, :end].to(dt).repeat_interleave(c.group, 0)
+            o = F.scaled_dot_product_attention(q.to(dt)[None], kk[None], vv[None],
+                                               attn_mask=None if mask is None else mask[None, None])
+            o = o[0].transpose(0, 1).reshape(P, c.dim)
+            x = x + (o @ W[f"{i}.o"].t()).float()
+            xn = (x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + c.eps) * L.ffn_norm).to(dt)
+            gu = (xn @ W[f"{i}.gu"].t()).float()
+            t = F.silu(gu[:, :c.ffn]) * gu[:, c.ffn:]
+            x = x + (t.to(dt) @ W[f"{i}.down"].t()).float()
+        xl = x[-1:]
+        xn = (xl * torch.rsqrt(xl.pow(2).mean(-1, keepdim=True) + c.eps) * self.w.out_norm).to(dt)
+        return (xn @ W["out"].t()).float()[0]
+
+    # ------------------------------------------------------------------ native decode
+    def _buffers(self, T: int) -> StepBuffers:
+        b = self._bufs.get(T)
+        if b is None:
+            c, dev = self.cfg, self.device
+            kmax = max(c.dim, c.ffn)
+            nsplit = self.max_ctx // 256
+            f32 = dict(dtype=torch.float32, device=dev)
+            b = StepBuffers(
+                T=T, tok=torch.zeros(T, dtype=torch.int32, device=dev),
+                pos=torch.zeros(T, dtype=torch.int32, device=dev),
+                slot=torch.zeros(T, dtype=torch.int32, device=dev),
+                h=torch.zeros(T, c.dim, **f32),
+                x8=torch.zeros(T, kmax, dtype=torch.int8, device=dev),
+                dx=torch.zeros(T, kmax // 32, **f32), sx=torch.zeros(T, kmax // 16, **f32),
+                qkv=torch.zeros(T, c.dim + 2 * c.kv_dim, **f32), qrot=torch.zeros(T, c.dim, **f32),
+                po=torch.zeros(T, c.heads, nsplit, c.head_dim, **f32),
+                pml=torch.zeros(T, c.heads, nsplit, 2, **f32), t=torch.zeros(T, c.ffn, **f32),
+                logits=torch.zeros(T, c.vocab, **f32))
+            self._bufs[T] = b
+        return b
+
+    def _rpw(self, n: int) -> int:
+        if self.rows_per_wg > 0:
+            return self.rows_per_wg
+        # ~2 workgroups per CU of work, at least one row per wave
+        return max(4, -(-n // 512))
+
+    def _q8(self, b: StepBuffers, k: int):
+        """Views of the Q8 activation buffers for inner dimension ``k`` (contiguous [T, k])."""
+        T = b.T
+        return (b.x8.view(-1)[:T * k].view(T, k), b.dx.view(-1)[:T * k // 32].view(T, k // 32),
+                b.sx.view(-1)[:T * k // 16].view(T, k // 16))
+
+    def _step_kernels(self, b: StepBuffers) -> None:
+        LK, c = self.LK, self.cfg
+        LK.dequant(self.w.tok_embd, b.h, rows=b.tok)          # embedding rows → residual
+        qd = self._q8(b, c.dim)
+        qf = self._q8(b, c.ffn)
+        scale = 1.0 / math.sqrt(c.head_dim)
+        for i, L in enumerate(self.w.layers):
+            LK.rmsnorm_q8(b.h, L.attn_norm, c.eps, *qd)
+            off = 0
+            for w in L.wqkv:
+                LK.qgemv(w, *qd, b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:],
+                         ldo=b.qkv.stride(0), rows_per_wg=self._rpw(w.n))
+                off += w.n
+            LK.rope_kv(b.qkv, b.pos, b.slot, self.cos, self.sin, c.heads, c.kv_heads, c.head_dim,
+                       self.max_ctx, b.qrot, self.k_cache[i], self.v_cache[i])
+            LK.attn_decode(b.qrot, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
+                           c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd)
+            LK.qgemv(L.wo, *qd, b.h, LK.RESID, rows_per_wg=self._rpw(L.wo.n))
+            LK.rmsnorm_q8(b.h, L.ffn_norm, c.eps, *qd)
+            LK.qgemv(L.wg, *qd, b.t, LK.PAIR, w1=L.wu, rows_per_wg=self._rpw(L.wg.n))
+            LK.rmsnorm_q8(b.t, None, 0.0, *qf)
+            LK.qgemv(L.wd, *qf, b.h, LK.RESID, rows_per_wg=self._rpw(L.wd.n))
+        LK.rmsnorm_q8(b.h, self.w.out_norm, c.eps, *qd)
+        LK.qgemv(self.w.output, *qd, b.logits, LK.STORE, rows_per_wg=self._rpw(self.w.output.n))
+
+    def _decode_native(self, tokens: Sequence[int], positions: Sequence[int],
+                       slots: Sequence[int]) -> torch.Tensor:
+        T = len(tokens)
+        b = self._buffers(T)
+        host = torch.tensor([list(tokens), list(positions), list(slots)], dtype=torch.int32)
+        b.tok.copy_(host[0], non_blocking=False)
+        b.pos.copy_(host[1])
+        b.slot.copy_(host[2])
+        if self.use_graphs:
+            if b.graph is None:
+                s = torch.cuda.Stream(self.device)
+                s.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(s):
+                    self._step_kernels(b)       # warm-up outside capture
+                torch.cuda.current_stream(self.device).wait_stream(s)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._step_kernels(b)
+                b.graph = g
+                self.stats["graph_captures"] += 1
+            b.graph.replay()
+        else:
+            self._step_kernels(b)
+        return b.logits
+
+    # ------------------------------------------------------------------ public API
+    def decode(self, tokens: Sequence[int], positions: Sequence[int],
+               slots: Sequence[int]) -> torch.Tensor:
+        """One step for T sequences: token ``tokens[i]`` at ``positions[i]`` of slot ``slots[i]``.
+        Returns fp32 logits [T, vocab] (a view of a reused buffer on the GPU: copy to keep)."""
+        T = len(tokens)
+        if T == 0:
+            raise ValueError("decode: no tokens")
+        for p in positions:
+            if p >= self.max_ctx:
+                raise ValueError(f"position {p} beyond the context ({self.max_ctx})")
+        self.stats["decode_steps"] += 1
+        self.stats["decode_tokens"] += T
+        if self.gpu:
+            out = []
+            for i in range(0, T, self.max_T):
+                out.append(self._decode_native(tokens[i:i + self.max_T],
+                                               positions[i:i + self.max_T],
+                                               slots[i:i + self.max_T]))
+            return out[0] if len(out) == 1 else torch.cat(out, 0)
+        rows = [self._forward_dense(torch.tensor([t]), s, p)
+                for t, p, s in zip(tokens, positions, slots)]
+        return torch.stack(rows, 0)
+
+    def prefill(self, tokens: Sequence[int], slot: int, start: int = 0) -> torch.Tensor:
+        """Process prompt tokens of one sequence; returns the logits of its last token [vocab]."""
+        P = len(tokens)
+        if P == 0:
+            raise ValueError("prefill: empty prompt")
+        if start + P > self.max_ctx:
+            raise ValueError(f"prompt of {P} tokens at {start} exceeds the context ({self.max_ctx})")
+        self.stats["prefill_tokens"] += P
+        if self.dense or not self.gpu:
+            return self._forward_dense(torch.tensor(list(tokens), device=self.device), slot, start)
+        logits = None
+        for i in range(0, P, self.max_T):
+            chunk = list(tokens[i:i + self.max_T])
+            n = len(chunk)
+            logits = self._decode_native(chunk, list(range(start + i, start + i + n)), [slot] * n)
+            logits = logits[n - 1]
+        return logits.clone()
+
+    def capture(self, sizes: Sequence[int] = (1, 2, 3, 4)) -> None:
+        """Capture the decode graphs up front (server warm-up), writing into slot 0 only."""
+        if not self.gpu:
+            return
+        for T in sizes:
+            if T <= self.max_T:
+                self._decode_native([0] * T, [0] * T, [0] * T)
+        torch.cuda.synchronize(self.device)
+
+
+def sample(logits: torch.Tensor, temperature: float = 0.0, top_k: int = 0, top_p: float = 1.0,
+           generator: Optional[torch.Generator] = None) -> int:
+    """Greedy at temperature 0; otherwise temperature / top-k / top-p (nucleus) sampling."""
+    if temperature <= 0.0:
+        return int(torch.argmax(logits).item())
+    x = logits.float() / temperature
+    if top_k and top_k > 0:
+        kth = torch.topk(x, min(top_k, x.numel())).values[-1]
+        x = torch.where(x < kth, torch.full_like(x, -float("inf")), x)
+    if top_p < 1.0:
+        sx, idx = torch.sort(x, descending=True)
+        cp = torch.softmax(sx, -1).cumsum(-1)
+        drop = cp - torch.softmax(sx, -1) > top_p
+        sx = sx.masked_fill(drop, -float("inf"))
+        x = torch.full_like(x, -float("inf")).scatter(0, idx, sx)
+    p = torch.softmax(x, -1)
+    if generator is not None and generator.device != p.device:
+        p = p.to(generator.device)
+    return int(torch.multinomial(p, 1, generator=generator).item())
+
+
+def generate(engine: Engine, prompt: Sequence[int], max_new: int, slot: int = 0,
+             eos: Sequence[int] = (), temperature: float = 0.0, seed: Optional[int] = None) -> dict:
+    """Single-sequence generation (benchmarks, tests).  Returns tokens and timings."""
+    gen = None
+    if temperature > 0:
+        gen = torch.Generator(device=engine.device if engine.gpu else "cpu")
+        gen.manual_seed(seed if seed is not None else 0)
+    t0 = time.perf_counter()
+    logits = engine.prefill(prompt, slot)
+    tok = sample(logits, temperature, generator=gen)
+    t1 = time.perf_counter()
+    out = [tok]
+    pos = len(prompt)
+    while len(out) < max_new and tok not in eos and pos < engine.max_ctx - 1:
+        logits = engine.decode([tok], [pos], [slot])[0]
+        tok = sample(logits, temperature, generator=gen)
+        out.append(tok)
+        pos += 1
+    t2 = time.perf_counter()
+    n_dec = max(1, len(out) - 1)
+    return {"tokens": out, "prefill_s": t1 - t0, "decode_s": t2 - t1,
+            "decode_tok_s": n_dec / max(t2 - t1, 1e-9), "prompt_tokens": len(prompt)}

@@ -1,0 +1,122 @@
+"""ctypes bindings of the LLM decode kernels (``csrc/llm_decode.hip``).
+
+Same conventions as ``kernels.py`` / ``sd_kernels.py``: raw device pointers, torch's current stream
+(so a decode step captures into one HIP graph), and no fallback — a missing library on a GPU host
+raises ``KernelLibraryError`` from ``kernels.library()``.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import torch
+
+from .kernels import library
+
+Q4K, Q6K = 0, 1
+STORE, RESID, PAIR = 0, 1, 2
+
+_declared = False
+_lock = threading.Lock()
+
+
+def _lib():
+    global _declared
+    lib = library()
+    if not _declared:
+        with _lock:
+            vp, ci, cl, cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
+            lib.amdk8s_llm_max_tokens.restype = ci
+            lib.amdk8s_llm_attn_chunk.restype = ci
+            lib.amdk8s_llm_qgemv.argtypes = [ci, ci] + [vp] * 8 + [vp, vp, vp, vp, vp] \
+                + [ci, ci, ci, ci, ci, vp]
+            lib.amdk8s_llm_qgemv.restype = ci
+            lib.amdk8s_llm_rmsnorm_q8.argtypes = [vp, vp, cf, ci, ci, vp, vp, vp, vp]
+            lib.amdk8s_llm_rmsnorm_q8.restype = ci
+            lib.amdk8s_llm_rope_kv.argtypes = [vp, ci, vp, vp, vp, vp, ci, ci, ci, ci, vp, vp, vp,
+                                               ci, vp]
+            lib.amdk8s_llm_rope_kv.restype = ci
+            lib.amdk8s_llm_attn_decode.argtypes = [vp, vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, vp,
+                                                   vp, vp, vp, vp, ci, vp]
+            lib.amdk8s_llm_attn_decode.restype = ci
+            lib.amdk8s_llm_dequant.argtypes = [ci, vp, vp, vp, vp, vp, ci, ci, vp, ci, vp]
+            lib.amdk8s_llm_dequant.restype = ci
+            lib.amdk8s_llm_q6k_repack.argtypes = [vp, cl, vp, vp, vp, vp, vp]
+            lib.amdk8s_llm_q6k_repack.restype = ci
+            _declared = True
+    return lib
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (rc={rc})")
+
+
+def max_tokens() -> int:
+    return int(_lib().amdk8s_llm_max_tokens())
+
+
+def attn_chunk() -> int:
+    return int(_lib().amdk8s_llm_attn_chunk())
+
+
+def qgemv(w0, x8, dx, sx, out, mode: int = STORE, w1=None, bias=None, ldo: int = None,
+          rows_per_wg: int = 8) -> None:
+    """``w0``/``w1``: :class:`~k8s_nvidia_gpus_amd.models.llm.weights.QWeight` on the GPU;
+    activations [T, K] in Q8 form; ``out`` fp32 [T, ldo] (a view with row stride ``ldo``)."""
+    t = x8.shape[0]
+    ldo = out.stride(0) if ldo is None else ldo
+    a = w0.ptrs()
+    b = w1.ptrs() if w1 is not None else (None, None, None, None)
+    _check(_lib().amdk8s_llm_qgemv(w0.qtype, mode, *a, *b, x8.data_ptr(), dx.data_ptr(),
+                                   sx.data_ptr(), _p(bias), out.data_ptr(), ldo, w0.n, w0.k, t,
+                                   rows_per_wg, _stream(x8)), "amdk8s_llm_qgemv")
+
+
+def rmsnorm_q8(x, w, eps: float, x8, dx, sx) -> None:
+    t, k = x.shape
+    _check(_lib().amdk8s_llm_rmsnorm_q8(x.data_ptr(), _p(w), float(eps), k, t, x8.data_ptr(),
+                                        dx.data_ptr(), sx.data_ptr(), _stream(x)),
+           "amdk8s_llm_rmsnorm_q8")
+
+
+def rope_kv(qkv, pos, slot, cos_t, sin_t, heads: int, kv_heads: int, head_dim: int,
+            max_ctx: int, q_out, kc, vc) -> None:
+    _check(_lib().amdk8s_llm_rope_kv(qkv.data_ptr(), qkv.stride(0), pos.data_ptr(),
+                                     slot.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(), heads,
+                                     kv_heads, head_dim, max_ctx, q_out.data_ptr(), kc.data_ptr(),
+                                     vc.data_ptr(), qkv.shape[0], _stream(qkv)),
+           "amdk8s_llm_rope_kv")
+
+
+def attn_decode(q, pos, slot, kc, vc, heads: int, kv_heads: int, head_dim: int, max_ctx: int,
+                scale: float, po, pml, x8, dx, sx, out=None) -> None:
+    _check(_lib().amdk8s_llm_attn_decode(q.data_ptr(), pos.data_ptr(), slot.data_ptr(),
+                                         kc.data_ptr(), vc.data_ptr(), heads, kv_heads, head_dim,
+                                         max_ctx, float(scale), po.data_ptr(), pml.data_ptr(),
+                                         _p(out), x8.data_ptr(), dx.data_ptr(), sx.data_ptr(),
+                                         q.shape[0], _stream(q)), "amdk8s_llm_attn_decode")
+
+
+def dequant(w, out, rows=None) -> None:
+    """Rows of ``w`` (all, or the int32 indices ``rows``) → ``out`` (fp16 or fp32, [n, K])."""
+    n = w.n if rows is None else rows.numel()
+    if out.dtype not in (torch.float16, torch.float32) or tuple(out.shape) != (n, w.k):
+        raise ValueError("dequant: out must be fp16/fp32 [rows, K]")
+    _check(_lib().amdk8s_llm_dequant(w.qtype, *w.ptrs(), _p(rows), n, w.k, out.data_ptr(),
+                                     int(out.dtype == torch.float32), _stream(out)),
+           "amdk8s_llm_dequant")
+
+
+def q6k_repack(raw, ql, qh, sc, d) -> None:
+    _check(_lib().amdk8s_llm_q6k_repack(raw.data_ptr(), raw.numel() // 210, ql.data_ptr(),
+                                        qh.data_ptr(), sc.data_ptr(), d.data_ptr(), _stream(raw)),
+           "amdk8s_llm_q6k_repack")

@@ -1,0 +1,149 @@
+#!/usr/bin/env python3
+"""Qwen2.5-7B (Q4_K_M layout, random-init blocks) on one MI355X: decode tokens/s and prefill.
+
+The reference serves this model with llama.cpp at ``--ctx-size 4096`` and publishes no speed
+(reference cluster-config/apps/llm/deployment.yaml:61-84).  This measures the in-tree
+engine (``k8s_nvidia_gpus_amd/models/llm``) on the exact architecture and quantisation mix with
+random weights (no network for the checkpoint): bytes streamed per token are those of the real file.
+
+Reports, as one JSON line:
+  * weight bytes and the HBM-roofline decode time per step (bytes / 6.3 TB/s measured copy peak);
+  * decode ms/step and tokens/s for T = 1..4 concurrent sequences (HIP-graph replay, greedy
+    sampling of every step on the GPU, per-step host sync as a server does);
+  * prefill tokens/s for a ``--prompt``-token prompt (fp16 dense path);
+  * per-GEMV-shape achieved bandwidth (``--gemv``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from k8s_nvidia_gpus_amd.models.llm import QWEN25_7B  # noqa: E402
+from k8s_nvidia_gpus_amd.models.llm.engine import Engine  # noqa: E402
+from k8s_nvidia_gpus_amd.models.llm.weights import ModelWeights  # noqa: E402
+
+
+def heartbeat(period=30.0):
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(period)
+            print(f"[llm_bench] running ({time.time() - t0:.0f} s)", file=sys.stderr, flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
+
+
+def bench_gemv(eng: Engine, iters: int = 50) -> list:
+    LK = eng.LK
+    L = eng.w.layers[0]
+    rows = []
+    cases = [("qkv", L.wqkv[0], "store"), ("o_proj", L.wo, "resid"),
+             ("gate_up", L.wg, "pair"), ("down", L.wd, "resid"), ("lm_head", eng.w.output, "store")]
+    for name, w, mode in cases:
+        for T in (1, 4):
+            x8 = torch.randint(-127, 127, (T, w.k), dtype=torch.int8, device=eng.device)
+            dx = torch.full((T, w.k // 32), 0.01, device=eng.device)
+            sx = torch.zeros(T, w.k // 16, device=eng.device)
+            out = torch.zeros(T, w.n, device=eng.device)
+            m = {"store": LK.STORE, "resid": LK.RESID, "pair": LK.PAIR}[mode]
+            kw = dict(w1=L.wu if mode == "pair" else None, rows_per_wg=eng._rpw(w.n))
+            for _ in range(5):
+                LK.qgemv(w, x8, dx, sx, out, m, **kw)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+            e0.record()
+            for _ in range(iters):
+                LK.qgemv(w, x8, dx, sx, out, m, **kw)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) / iters * 1e3
+            nbytes = w.nbytes() * (2 if mode == "pair" else 1)
+            rows.append({"gemv": name, "T": T, "N": w.n, "K": w.k, "type": ["Q4_K", "Q6_K"][w.qtype],
+                         "us": round(us, 2), "GBps": round(nbytes / us / 1e3, 1)})
+    return rows
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--layers", type=int, default=QWEN25_7B.layers)
+    ap.add_argument("--steps", type=int, default=128, help="decode steps per T")
+    ap.add_argument("--ctx", type=int, default=4096, help="KV-cache context (reference --ctx-size)")
+    ap.add_argument("--prompt", type=int, default=512)
+    ap.add_argument("--tokens", default="1,2,3,4")
+    ap.add_argument("--gemv", action="store_true")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args(argv)
+    if not torch.cuda.is_available():
+        print("llm_bench needs an MI355X", file=sys.stderr)
+        return 2
+    heartbeat()
+    from dataclasses import replace
+
+    cfg = replace(QWEN25_7B, layers=args.layers)
+    dev = torch.device("cuda:0")
+    t0 = time.perf_counter()
+    w = ModelWeights.random(cfg, device=dev, seed=0)
+    torch.cuda.synchronize()
+    eng = Engine(w, max_ctx=args.ctx, slots=4, dense=True)
+    eng.dense_weights()
+    torch.cuda.synchronize()
+    load_s = time.perf_counter() - t0
+    wbytes = w.nbytes()
+    res = {"model": f"Qwen2.5-7B architecture, Q4_K_M type mix, random blocks ({cfg.layers} layers)",
+           "weight_bytes": wbytes, "roofline_ms_at_6.3TBps": round(wbytes / 6.3e12 * 1e3, 4),
+           "load_s": round(load_s, 2), "ctx": eng.max_ctx, "decode": [], "device":
+           torch.cuda.get_device_name(0)}
+    # prefill (dense fp16 path) — also fills the KV caches the decode steps attend over
+    prompt = list(range(100, 100 + args.prompt))
+    for s in range(4):
+        eng.prefill(prompt, slot=s)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    eng.prefill(prompt, slot=0)
+    torch.cuda.synchronize()
+    pf = time.perf_counter() - t
+    res["prefill"] = {"tokens": args.prompt, "s": round(pf, 4), "tok_s": round(args.prompt / pf, 1)}
+    print(f"prefill {args.prompt} tokens: {pf * 1e3:.1f} ms", file=sys.stderr, flush=True)
+    for T in [int(x) for x in args.tokens.split(",") if x]:
+        pos = [args.prompt] * T
+        toks = [11] * T
+        slots = list(range(T))
+        eng.decode(toks, pos, slots)                 # capture
+        for i in range(3):
+            eng.decode(toks, [p + 1 + i for p in pos], slots)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for i in range(args.steps):
+            lg = eng.decode(toks, [p + 4 + i for p in pos], slots)
+            nxt = torch.argmax(lg, -1).tolist()       # sample on the GPU, sync like a server
+            toks = [int(x) % cfg.vocab for x in nxt]
+        dt = time.perf_counter() - t
+        row = {"T": T, "ms_per_step": round(dt / args.steps * 1e3, 4),
+               "tok_s": round(T * args.steps / dt, 1),
+               "eff_GBps": round(wbytes / (dt / args.steps) / 1e9, 1)}
+        res["decode"].append(row)
+        print(f"decode T={T}: {row}", file=sys.stderr, flush=True)
+    if args.gemv:
+        res["gemv"] = bench_gemv(eng)
+        for r in res["gemv"]:
+            print(r, file=sys.stderr, flush=True)
+    res["graph_captures"] = eng.stats["graph_captures"]
+    line = json.dumps(res)
+    print(line, flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(line + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
