@@ -67,7 +67,7 @@ class StepBuffers:
     pml: torch.Tensor
     t: torch.Tensor
     logits: torch.Tensor
-    graph: Optional[torch.cuda.CUDAGraph] = None
+    graphs: Dict[int, torch.cuda.CUDAGraph] = None   # keyed by attention span
 
 
 class Engine:
@@ -92,7 +92,9 @@ class Engine:
         self.dense = self.gpu if dense is None else dense
         self._dense_w: Optional[Dict[str, torch.Tensor]] = None
         self._bufs: Dict[int, StepBuffers] = {}
-        self.rows_per_wg = int(os.environ.get("AMDK8S_LLM_ROWS_PER_WG", "0"))
+        # GEMV decomposition override "waves,ks,rows" (sweeps); default: the kernel's per-shape
+        self.gemv_cfg = dict(zip(("waves", "ks", "rows_per_wg"),
+                                 map(int, os.environ.get("AMDK8S_LLM_GEMV", "0,0,0").split(","))))
         if self.gpu:
             from k8s_nvidia_gpus_amd.ops import llm_kernels as LK
 
@@ -166,7 +168,7 @@ class Engine:
         if b is None:
             c, dev = self.cfg, self.device
             kmax = max(c.dim, c.ffn)
-            nsplit = self.max_ctx // 256
+            nsplit = self.max_ctx // self.LK.attn_chunk()
             f32 = dict(dtype=torch.float32, device=dev)
             b = StepBuffers(
                 T=T, tok=torch.zeros(T, dtype=torch.int32, device=dev),
@@ -182,19 +184,22 @@ class Engine:
             self._bufs[T] = b
         return b
 
-    def _rpw(self, n: int) -> int:
-        if self.rows_per_wg > 0:
-            return self.rows_per_wg
-        # ~2 workgroups per CU of work, at least one row per wave
-        return max(4, -(-n // 512))
-
     def _q8(self, b: StepBuffers, k: int):
         """Views of the Q8 activation buffers for inner dimension ``k`` (contiguous [T, k])."""
         T = b.T
         return (b.x8.view(-1)[:T * k].view(T, k), b.dx.view(-1)[:T * k // 32].view(T, k // 32),
                 b.sx.view(-1)[:T * k // 16].view(T, k // 16))
 
-    def _step_kernels(self, b: StepBuffers) -> None:
+    def _span(self, max_pos: int) -> int:
+        """Attention span bucket for a step whose furthest position is ``max_pos``: the next power
+        of two (>= 256), so a graph covers many steps and never launches chunks far past the
+        context in use."""
+        span = 256
+        while span <= max_pos:
+            span *= 2
+        return min(span, self.max_ctx)
+
+    def _step_kernels(self, b: StepBuffers, span: int) -> None:
         LK, c = self.LK, self.cfg
         LK.dequant(self.w.tok_embd, b.h, rows=b.tok)          # embedding rows → residual
         qd = self._q8(b, c.dim)
@@ -205,19 +210,20 @@ class Engine:
             off = 0
             for w in L.wqkv:
                 LK.qgemv(w, *qd, b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:],
-                         ldo=b.qkv.stride(0), rows_per_wg=self._rpw(w.n))
+                         ldo=b.qkv.stride(0), **self.gemv_cfg)
                 off += w.n
             LK.rope_kv(b.qkv, b.pos, b.slot, self.cos, self.sin, c.heads, c.kv_heads, c.head_dim,
                        self.max_ctx, b.qrot, self.k_cache[i], self.v_cache[i])
             LK.attn_decode(b.qrot, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
-                           c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd)
-            LK.qgemv(L.wo, *qd, b.h, LK.RESID, rows_per_wg=self._rpw(L.wo.n))
+                           c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
+                           span=span)
+            LK.qgemv(L.wo, *qd, b.h, LK.RESID, **self.gemv_cfg)
             LK.rmsnorm_q8(b.h, L.ffn_norm, c.eps, *qd)
-            LK.qgemv(L.wg, *qd, b.t, LK.PAIR, w1=L.wu, rows_per_wg=self._rpw(L.wg.n))
+            LK.qgemv(L.wg, *qd, b.t, LK.PAIR, w1=L.wu, **self.gemv_cfg)
             LK.rmsnorm_q8(b.t, None, 0.0, *qf)
-            LK.qgemv(L.wd, *qf, b.h, LK.RESID, rows_per_wg=self._rpw(L.wd.n))
+            LK.qgemv(L.wd, *qf, b.h, LK.RESID, **self.gemv_cfg)
         LK.rmsnorm_q8(b.h, self.w.out_norm, c.eps, *qd)
-        LK.qgemv(self.w.output, *qd, b.logits, LK.STORE, rows_per_wg=self._rpw(self.w.output.n))
+        LK.qgemv(self.w.output, *qd, b.logits, LK.STORE, **self.gemv_cfg)
 
     def _decode_native(self, tokens: Sequence[int], positions: Sequence[int],
                        slots: Sequence[int]) -> torch.Tensor:
@@ -227,21 +233,25 @@ class Engine:
         b.tok.copy_(host[0], non_blocking=False)
         b.pos.copy_(host[1])
         b.slot.copy_(host[2])
+        span = self._span(max(positions))
         if self.use_graphs:
-            if b.graph is None:
+            if b.graphs is None:
+                b.graphs = {}
+            g = b.graphs.get(span)
+            if g is None:
                 s = torch.cuda.Stream(self.device)
                 s.wait_stream(torch.cuda.current_stream(self.device))
                 with torch.cuda.stream(s):
-                    self._step_kernels(b)       # warm-up outside capture
+                    self._step_kernels(b, span)       # warm-up outside capture
                 torch.cuda.current_stream(self.device).wait_stream(s)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    self._step_kernels(b)
-                b.graph = g
+                    self._step_kernels(b, span)
+                b.graphs[span] = g
                 self.stats["graph_captures"] += 1
-            b.graph.replay()
+            g.replay()
         else:
-            self._step_kernels(b)
+            self._step_kernels(b, span)
         return b.logits
 
     # ------------------------------------------------------------------ public API
@@ -287,12 +297,21 @@ class Engine:
         return logits.clone()
 
     def capture(self, sizes: Sequence[int] = (1, 2, 3, 4)) -> None:
-        """Capture the decode graphs up front (server warm-up), writing into slot 0 only."""
+        """Capture every decode graph (batch sizes x attention-span buckets) up front — the server
+        does this before it reports ready.  Writes only position ``span-1`` of slot 0."""
         if not self.gpu:
             return
+        spans = []
+        s = 256
+        while True:
+            spans.append(min(s, self.max_ctx))
+            if s >= self.max_ctx:
+                break
+            s *= 2
         for T in sizes:
             if T <= self.max_T:
-                self._decode_native([0] * T, [0] * T, [0] * T)
+                for span in spans:
+                    self._decode_native([0] * T, [span - 1] * T, [0] * T)
         torch.cuda.synchronize(self.device)
 
 

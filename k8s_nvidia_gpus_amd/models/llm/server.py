@@ -1,0 +1,461 @@
+"""llama-server-compatible HTTP API over the in-tree Qwen2 engine, with continuous batching.
+
+The reference's LLM pod runs ``llama-server -m <gguf> --host 0.0.0.0 --port 8080 --ctx-size 4096
+--n-gpu-layers 35 --threads 6`` behind Service ``coder-llm`` and a Gateway (reference
+cluster-config/apps/llm/deployment.yaml:76-84, service.yaml, httproute.yaml).  This server accepts
+the same command line (``-m``, ``--ctx-size``, ``--n-gpu-layers`` / ``--threads`` accepted; every
+layer is on the GPU) and serves the endpoints clients of that pod use:
+
+* ``GET /health`` (503 while the model loads, like llama-server), ``GET /v1/models``;
+* ``POST /completion`` (llama.cpp native: ``prompt``, ``n_predict``, ``temperature``, ``top_k``,
+  ``top_p``, ``seed``, ``stop``, ``stream``) with llama.cpp's ``timings`` block;
+* ``POST /v1/completions`` and ``POST /v1/chat/completions`` (OpenAI; ChatML prompt format of
+  Qwen2.5-Instruct; ``stream`` as server-sent events);
+* ``POST /tokenize``, ``POST /detokenize``, ``GET /metrics`` (Prometheus text).
+
+One scheduler thread owns the GPU: new requests are prefilled into free KV-cache slots, then every
+active sequence advances by one token per decode step — up to 4 sequences share each pass over
+the weights (``--parallel``).  Request handlers only wait on per-request queues, so the GPU is never
+driven from two threads (the reference's SD15 app had that hazard).
+"""
+from __future__ import annotations
+
+import argparse
+import itertools
+import json
+import os
+import queue
+import threading
+import time
+import uuid
+from dataclasses import dataclass, field
+from typing import Any, Dict, Iterator, List, Optional
+
+import torch
+
+from .engine import Engine, sample
+from .tokenizer import Tokenizer, chatml
+
+
+@dataclass
+class Job:
+    ids: List[int]
+    max_new: int
+    temperature: float = 0.0
+    top_k: int = 0
+    top_p: float = 1.0
+    seed: Optional[int] = None
+    stop: List[str] = field(default_factory=list)
+    out: "queue.Queue" = field(default_factory=queue.Queue)
+    # scheduler state
+    slot: int = -1
+    pos: int = 0
+    last: int = 0
+    gen: List[int] = field(default_factory=list)
+    text: str = ""
+    emitted: int = 0
+    generator: Optional[torch.Generator] = None
+    t_submit: float = 0.0
+    t_first: float = 0.0
+    t_prefill: float = 0.0
+    finish: str = ""
+    cancelled: bool = False
+
+
+class Scheduler:
+    """Continuous batching over the engine's KV-cache slots."""
+
+    def __init__(self, engine: Engine, tok: Tokenizer, parallel: int = 4):
+        self.engine = engine
+        self.tok = tok
+        self.parallel = max(1, min(parallel, engine.slots))
+        self.pending: "queue.Queue[Job]" = queue.Queue()
+        self.active: Dict[int, Job] = {}
+        self.stop_ids = set(tok.stop_ids())
+        self.metrics = {"requests_total": 0, "prompt_tokens_total": 0, "tokens_predicted_total": 0,
+                        "decode_steps_total": 0, "decode_seconds_total": 0.0,
+                        "prefill_seconds_total": 0.0, "requests_processing": 0}
+        self._run = True
+        self._lock = threading.Lock()
+        self.thread = threading.Thread(target=self._loop, name="llm-scheduler", daemon=True)
+        self.thread.start()
+
+    def submit(self, job: Job) -> Job:
+        if len(job.ids) == 0:
+            raise ValueError("empty prompt")
+        if len(job.ids) + 1 >= self.engine.max_ctx:
+            raise ValueError(f"prompt of {len(job.ids)} tokens exceeds the context "
+                             f"({self.engine.max_ctx})")
+        job.max_new = max(1, min(job.max_new, self.engine.max_ctx - len(job.ids) - 1))
+        job.t_submit = time.perf_counter()
+        with self._lock:
+            self.metrics["requests_total"] += 1
+        self.pending.put(job)
+        return job
+
+    def close(self) -> None:
+        self._run = False
+        self.pending.put(None)  # type: ignore[arg-type]
+        self.thread.join(timeout=10)
+
+    # ---------------------------------------------------------------- scheduler thread
+    def _free_slot(self) -> int:
+        for s in range(self.parallel):
+            if s not in self.active:
+                return s
+        return -1
+
+    def _emit(self, job: Job, tok: int) -> bool:
+        """Record a sampled token; returns True when the job is finished."""
+        job.gen.append(tok)
+        job.last = tok
+        if tok in self.stop_ids:
+            job.finish = "stop"
+            self._flush(job, final=True)
+            return True
+        text = self.tok.decode(job.gen)
+        cut = None
+        for s in job.stop:
+            i = text.find(s)
+            if i >= 0 and (cut is None or i < cut):
+                cut = i
+        if cut is not None:
+            job.text = text[:cut]
+            job.finish = "stop"
+            self._flush(job, final=True)
+            return True
+        job.text = text
+        if len(job.gen) >= job.max_new:
+            job.finish = "length"
+            self._flush(job, final=True)
+            return True
+        self._flush(job, final=False)
+        return False
+
+    def _flush(self, job: Job, final: bool) -> None:
+        text = job.text
+        hold = 0
+        if not final:
+            if text.endswith("�"):          # an incomplete UTF-8 sequence: wait for more bytes
+                hold = 1
+            for s in job.stop:                    # a stop string may be starting: hold its prefix
+                for k in range(min(len(s) - 1, len(text)), 0, -1):
+                    if text.endswith(s[:k]):
+                        hold = max(hold, k)
+                        break
+        upto = len(text) - hold
+        if upto > job.emitted:
+            job.out.put(("text", text[job.emitted:upto]))
+            job.emitted = upto
+        if final:
+            job.out.put(("done", job))
+
+    def _admit(self) -> None:
+        while len(self.active) < self.parallel:
+            try:
+                job = self.pending.get_nowait() if self.active else self.pending.get(timeout=0.5)
+            except queue.Empty:
+                return
+            if job is None:
+                return
+            if job.cancelled:
+                continue
+            slot = self._free_slot()
+            job.slot = slot
+            if job.temperature > 0:
+                dev = self.engine.device if self.engine.gpu else "cpu"
+                job.generator = torch.Generator(device=dev)
+                job.generator.manual_seed(job.seed if job.seed is not None
+                                          else int.from_bytes(os.urandom(4), "little"))
+            t0 = time.perf_counter()
+            logits = self.engine.prefill(job.ids, slot)
+            tok = sample(logits, job.temperature, job.top_k, job.top_p, job.generator)
+            job.t_prefill = time.perf_counter() - t0
+            job.t_first = time.perf_counter()
+            with self._lock:
+                self.metrics["prompt_tokens_total"] += len(job.ids)
+                self.metrics["prefill_seconds_total"] += job.t_prefill
+                self.metrics["tokens_predicted_total"] += 1
+            job.pos = len(job.ids)
+            if not self._emit(job, tok):
+                self.active[slot] = job
+
+    def _step(self) -> None:
+        jobs = [j for j in self.active.values() if not j.cancelled]
+        for j in [j for j in self.active.values() if j.cancelled]:
+            del self.active[j.slot]
+        if not jobs:
+            return
+        t0 = time.perf_counter()
+        logits = self.engine.decode([j.last for j in jobs], [j.pos for j in jobs],
+                                    [j.slot for j in jobs])
+        greedy = [j.temperature <= 0 for j in jobs]
+        if all(greedy):
+            toks = torch.argmax(logits, -1).tolist()
+        else:
+            toks = [sample(logits[i], j.temperature, j.top_k, j.top_p, j.generator)
+                    for i, j in enumerate(jobs)]
+        dt = time.perf_counter() - t0
+        with self._lock:
+            self.metrics["decode_steps_total"] += 1
+            self.metrics["decode_seconds_total"] += dt
+            self.metrics["tokens_predicted_total"] += len(jobs)
+        for j, t in zip(jobs, toks):
+            j.pos += 1
+            if self._emit(j, int(t)):
+                del self.active[j.slot]
+
+    def _loop(self) -> None:
+        while self._run:
+            try:
+                self._admit()
+                self.metrics["requests_processing"] = len(self.active)
+                self._step()
+            except Exception as e:  # surface to every waiting request, keep serving
+                for j in list(self.active.values()):
+                    j.out.put(("error", repr(e)))
+                self.active.clear()
+
+
+# -------------------------------------------------------------------- HTTP layer
+def _job_from(body: Dict[str, Any], ids: List[int], default_max: int) -> Job:
+    stop = body.get("stop") or []
+    if isinstance(stop, str):
+        stop = [stop]
+    n = body.get("n_predict", body.get("max_tokens", body.get("max_completion_tokens")))
+    if n is None or int(n) < 0:
+        n = default_max
+    return Job(ids=ids, max_new=int(n), temperature=float(body.get("temperature", 0.8)),
+               top_k=int(body.get("top_k", 40)), top_p=float(body.get("top_p", 0.95)),
+               seed=None if body.get("seed") in (None, -1) else int(body["seed"]), stop=list(stop))
+
+
+def _collect(job: Job) -> Job:
+    while True:
+        kind, val = job.out.get()
+        if kind == "error":
+            raise RuntimeError(val)
+        if kind == "done":
+            return val
+
+
+def _stream(job: Job) -> Iterator[tuple]:
+    while True:
+        kind, val = job.out.get()
+        if kind == "error":
+            raise RuntimeError(val)
+        yield kind, val
+        if kind == "done":
+            return
+
+
+def _timings(job: Job) -> Dict[str, Any]:
+    now = time.perf_counter()
+    pred_ms = (now - job.t_first) * 1e3
+    n = len(job.gen)
+    return {"prompt_n": len(job.ids), "prompt_ms": round(job.t_prefill * 1e3, 3),
+            "prompt_per_second": round(len(job.ids) / max(job.t_prefill, 1e-9), 2),
+            "predicted_n": n, "predicted_ms": round(pred_ms, 3),
+            "predicted_per_second": round(max(n - 1, 0) / max(pred_ms / 1e3, 1e-9), 2)}
+
+
+def create_app(state: Dict[str, Any]):
+    """``state``: {"scheduler": Scheduler | None, "tok": Tokenizer | None, "model": name}; the
+    scheduler may be attached later (``/health`` answers 503 until then)."""
+    from fastapi import FastAPI, HTTPException
+    from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
+
+    app = FastAPI(title="amdk8s llm server")
+
+    def sched() -> Scheduler:
+        s = state.get("scheduler")
+        if s is None:
+            raise HTTPException(503, "Loading model")
+        return s
+
+    def encode_prompt(p) -> List[int]:
+        if isinstance(p, list) and all(isinstance(x, int) for x in p):
+            return list(p)
+        if isinstance(p, list):
+            p = "".join(str(x) for x in p)
+        return state["tok"].encode(str(p))
+
+    @app.get("/health")
+    def health():
+        if state.get("scheduler") is None:
+            return JSONResponse({"error": {"code": 503, "message": "Loading model",
+                                           "type": "unavailable_error"}}, status_code=503)
+        return {"status": "ok"}
+
+    @app.get("/v1/models")
+    def models():
+        return {"object": "list", "data": [{"id": state.get("model", "model"), "object": "model",
+                                            "created": int(state.get("created", 0)),
+                                            "owned_by": "amdk8s"}]}
+
+    @app.post("/tokenize")
+    def tokenize(body: Dict[str, Any]):
+        return {"tokens": encode_prompt(body.get("content", ""))}
+
+    @app.post("/detokenize")
+    def detokenize(body: Dict[str, Any]):
+        return {"content": state["tok"].decode(body.get("tokens", []))}
+
+    def submit(body, ids, default_max):
+        try:
+            return sched().submit(_job_from(body, ids, default_max))
+        except ValueError as e:
+            raise HTTPException(400, str(e))
+
+    @app.post("/completion")
+    def completion(body: Dict[str, Any]):
+        s = sched()
+        job = submit(body, encode_prompt(body.get("prompt", "")), s.engine.max_ctx)
+        if body.get("stream"):
+            def gen():
+                for kind, val in _stream(job):
+                    if kind == "text":
+                        yield "data: " + json.dumps({"content": val, "stop": False}) + "\n\n"
+                    else:
+                        yield "data: " + json.dumps({"content": "", "stop": True,
+                                                     "timings": _timings(val)}) + "\n\n"
+            return StreamingResponse(gen(), media_type="text/event-stream")
+        job = _collect(job)
+        return {"content": job.text, "stop": True, "model": state.get("model"),
+                "tokens_predicted": len(job.gen), "tokens_evaluated": len(job.ids),
+                "stopped_eos": job.finish == "stop" and job.gen[-1] in s.stop_ids,
+                "stopped_limit": job.finish == "length",
+                "stopped_word": job.finish == "stop" and job.gen[-1] not in s.stop_ids,
+                "timings": _timings(job)}
+
+    def openai(body, ids, chat: bool):
+        s = sched()
+        job = submit(body, ids, 16 if not chat else s.engine.max_ctx)
+        rid = ("chatcmpl-" if chat else "cmpl-") + uuid.uuid4().hex[:24]
+        created = int(time.time())
+        obj = "chat.completion" if chat else "text_completion"
+        if body.get("stream"):
+            def gen():
+                first = True
+                for kind, val in _stream(job):
+                    if kind == "text":
+                        if chat:
+                            delta = {"content": val}
+                            if first:
+                                delta["role"] = "assistant"
+                            ch = {"index": 0, "delta": delta, "finish_reason": None}
+                        else:
+                            ch = {"index": 0, "text": val, "finish_reason": None}
+                        first = False
+                        yield "data: " + json.dumps({"id": rid, "object": obj + ".chunk" if chat
+                                                     else obj, "created": created,
+                                                     "model": state.get("model"),
+                                                     "choices": [ch]}) + "\n\n"
+                    else:
+                        ch = {"index": 0, "finish_reason": val.finish}
+                        ch["delta" if chat else "text"] = {} if chat else ""
+                        yield "data: " + json.dumps({"id": rid, "object": obj + ".chunk" if chat
+                                                     else obj, "created": created,
+                                                     "model": state.get("model"),
+                                                     "choices": [ch]}) + "\n\n"
+                yield "data: [DONE]\n\n"
+            return StreamingResponse(gen(), media_type="text/event-stream")
+        job = _collect(job)
+        choice = {"index": 0, "finish_reason": job.finish, "logprobs": None}
+        if chat:
+            choice["message"] = {"role": "assistant", "content": job.text}
+        else:
+            choice["text"] = job.text
+        return {"id": rid, "object": obj, "created": created, "model": state.get("model"),
+                "choices": [choice],
+                "usage": {"prompt_tokens": len(job.ids), "completion_tokens": len(job.gen),
+                          "total_tokens": len(job.ids) + len(job.gen)},
+                "timings": _timings(job)}
+
+    @app.post("/v1/completions")
+    def v1_completions(body: Dict[str, Any]):
+        return openai(body, encode_prompt(body.get("prompt", "")), chat=False)
+
+    @app.post("/v1/chat/completions")
+    def v1_chat(body: Dict[str, Any]):
+        msgs = body.get("messages") or []
+        if not isinstance(msgs, list) or not msgs:
+            raise HTTPException(400, "messages must be a non-empty list")
+        return openai(body, state["tok"].encode(chatml(msgs)), chat=True)
+
+    @app.get("/metrics")
+    def metrics():
+        s = state.get("scheduler")
+        m = dict(s.metrics) if s else {}
+        lines = []
+        for k, v in sorted(m.items()):
+            name = f"llamacpp_amdk8s_{k}"
+            lines += [f"# TYPE {name} {'counter' if k.endswith('_total') else 'gauge'}",
+                      f"{name} {v}"]
+        if s and m.get("decode_seconds_total"):
+            tps = m["tokens_predicted_total"] / max(m["decode_seconds_total"] +
+                                                    m["prefill_seconds_total"], 1e-9)
+            lines += ["# TYPE llamacpp_amdk8s_predicted_tokens_seconds gauge",
+                      f"llamacpp_amdk8s_predicted_tokens_seconds {tps:.3f}"]
+        return PlainTextResponse("\n".join(lines) + "\n")
+
+    return app
+
+
+def build_engine(args) -> tuple:
+    """Load a GGUF (``-m``) or build a synthetic model (``--synthetic tiny|7b``)."""
+    device = "cuda" if torch.cuda.is_available() else "cpu"
+    if args.model:
+        from .synthetic import load
+
+        eng, tok = load(args.model, device=device, max_ctx=args.ctx_size, slots=args.parallel)
+        return eng, tok, os.path.basename(args.model)
+    from .config import QWEN25_7B, tiny
+    from .synthetic import write_synthetic_gguf, load
+    import tempfile
+
+    if args.synthetic == "7b":
+        from .tokenizer import Tokenizer, synthetic_vocab
+        from .weights import ModelWeights
+
+        w = ModelWeights.random(QWEN25_7B, device=device)
+        eng = Engine(w, max_ctx=args.ctx_size, slots=args.parallel)
+        return eng, Tokenizer.from_gguf(synthetic_vocab(QWEN25_7B.vocab)), "qwen2.5-7b-synthetic"
+    path = os.path.join(tempfile.mkdtemp(prefix="amdk8s-llm-"), "tiny.gguf")
+    write_synthetic_gguf(path, tiny())
+    eng, tok = load(path, device=device, max_ctx=args.ctx_size, slots=args.parallel)
+    return eng, tok, "tiny-qwen2-synthetic"
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="llama-server-compatible API on the in-tree engine")
+    ap.add_argument("-m", "--model", default=os.environ.get("MODEL_PATH"))
+    ap.add_argument("--synthetic", choices=["tiny", "7b"], default="tiny",
+                    help="random-weight model when no -m is given (offline)")
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=8080)
+    ap.add_argument("-c", "--ctx-size", type=int, default=4096)
+    ap.add_argument("-np", "--parallel", type=int, default=4)
+    ap.add_argument("-ngl", "--n-gpu-layers", type=int, default=999, help="accepted; all layers run on the GPU")
+    ap.add_argument("-t", "--threads", type=int, default=0, help="accepted; the GPU does the work")
+    args = ap.parse_args(argv)
+    import uvicorn
+
+    state: Dict[str, Any] = {"scheduler": None, "tok": None, "model": "loading",
+                             "created": time.time()}
+    app = create_app(state)
+
+    def load_bg():
+        eng, tok, name = build_engine(args)
+        if eng.gpu:
+            eng.capture(range(1, min(args.parallel, eng.max_T) + 1))   # HIP graphs before ready
+        state.update(tok=tok, model=name, scheduler=Scheduler(eng, tok, args.parallel))
+        print(f"model {name} ready (ctx {eng.max_ctx}, parallel {args.parallel})", flush=True)
+
+    threading.Thread(target=load_bg, daemon=True).start()
+    uvicorn.run(app, host=args.host, port=args.port, log_level="info")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -19,9 +19,10 @@
 //   then streams its rows against them.
 // * Epilogues are fused: bias add (q/k/v), residual add in place (o_proj, ffn_down), and the SwiGLU
 //   pair mode that runs ffn_gate and ffn_up rows in the same wave and writes silu(g)*u.
-// * Decode attention is split over the context (flash-decoding): per (kv head, 256-position chunk,
-//   token) one workgroup scores all q heads of the GQA group, and the combine kernel merges the
-//   chunks and emits the Q8 activations of the o_proj input directly.
+// * Decode attention is split over the context (flash-decoding): per (kv head, 64-position chunk,
+//   token) one workgroup scores all q heads of the GQA group with every K/V load of the chunk in
+//   flight at once, and the combine kernel merges the chunks and emits the Q8 activations of the
+//   o_proj input directly.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -30,7 +31,7 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kQ4KBytes = 144;
 constexpr int kMaxTok = 4;          // tokens per GEMV launch (activations staged in LDS)
-constexpr int kAttnChunk = 256;     // context positions per decode-attention workgroup
+constexpr int kAttnChunk = 64;      // context positions per decode-attention workgroup
 constexpr int kHeadDim = 128;
 constexpr int kMaxGroup = 8;        // q heads per kv head
 
@@ -83,128 +84,156 @@ struct GemvArgs {
   const float* sx;       // [T][K/16]  (dx * sum of the 16 int8 values)
   const float* bias;     // [N] or null (store mode)
   float* out;            // [T][ldo]
-  int ldo, N, K, T, rows_per_wg;
+  int ldo, N, K, T;
+  int ks;                // waves per row (split-K inside the workgroup): 1, 2, 4
+  int rows_per_wg;       // multiple of (waves per workgroup / ks)
 };
 
-// Partial dot products of one lane for one 256-weight super-block of a Q4_K row.
-template <int T>
-__device__ __forceinline__ void q4k_block(const uint8_t* __restrict__ row, int blk, int sub,
-                                          const int8_t* xs, const float* dxs, const float* sxs,
-                                          int xstride, int dstride, int sstride, float* acc) {
-  const uint8_t* b = row + (long)blk * kQ4KBytes;
-  const uint4 hdr = *reinterpret_cast<const uint4*>(b);
-  const uint4 qv = *reinterpret_cast<const uint4*>(b + 16 + sub * 16);
-  const int c = sub >> 1;                 // 64-weight chunk: sub-blocks 2c (low) and 2c+1 (high)
-  const float d = h2f(hdr.x & 0xffffu), dmin = h2f(hdr.x >> 16);
-  const uint32_t s[3] = {hdr.y, hdr.z, hdr.w};
-  auto sbyte = [&](int i) -> uint32_t { return (s[i >> 2] >> ((i & 3) * 8)) & 0xffu; };
-  const int j0 = 2 * c, j1 = 2 * c + 1;
-  uint32_t sc0, m0, sc1, m1;
-  if (c < 2) {
-    sc0 = sbyte(j0) & 63; m0 = sbyte(j0 + 4) & 63;
-    sc1 = sbyte(j1) & 63; m1 = sbyte(j1 + 4) & 63;
+// One lane's share of a 256-weight super-block: Q4_K = header + 16 B of nibbles; Q6_K = 16 B of
+// low bits + 16 B of high bits + the 16 scales + d.
+template <int TYPE> struct Blk;
+template <> struct Blk<kQ4K> { uint4 h, q; };
+template <> struct Blk<kQ6K> { uint4 l, hb, s; uint32_t d; };
+
+template <int TYPE>
+__device__ __forceinline__ void load_blk(const QMat& w, long rowblk, int blk, int sub,
+                                         Blk<TYPE>& r) {
+  if constexpr (TYPE == kQ4K) {
+    const uint8_t* b = w.q + (rowblk + blk) * kQ4KBytes;
+    r.h = *reinterpret_cast<const uint4*>(b);
+    r.q = *reinterpret_cast<const uint4*>(b + 16 + sub * 16);
   } else {
-    sc0 = (sbyte(j0 + 4) & 0xf) | ((sbyte(j0 - 4) >> 6) << 4);
-    m0 = (sbyte(j0 + 4) >> 4) | ((sbyte(j0) >> 6) << 4);
-    sc1 = (sbyte(j1 + 4) & 0xf) | ((sbyte(j1 - 4) >> 6) << 4);
-    m1 = (sbyte(j1 + 4) >> 4) | ((sbyte(j1) >> 6) << 4);
-  }
-  const uint32_t q[4] = {qv.x, qv.y, qv.z, qv.w};
-  const int p_lo = blk * 256 + c * 64 + (sub & 1) * 16;    // weight index of this lane's low run
-  const int g_lo = p_lo >> 4;                                // 16-group
-  const int d_lo = p_lo >> 5;                                // 32-block
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    const uint4 xl = *reinterpret_cast<const uint4*>(xs + t * xstride + xoff(p_lo));
-    const uint4 xh = *reinterpret_cast<const uint4*>(xs + t * xstride + xoff(p_lo + 32));
-    int il = 0, ih = 0;
-    il = dot4(q[0] & 0x0f0f0f0fu, xl.x, il);
-    il = dot4(q[1] & 0x0f0f0f0fu, xl.y, il);
-    il = dot4(q[2] & 0x0f0f0f0fu, xl.z, il);
-    il = dot4(q[3] & 0x0f0f0f0fu, xl.w, il);
-    ih = dot4((q[0] >> 4) & 0x0f0f0f0fu, xh.x, ih);
-    ih = dot4((q[1] >> 4) & 0x0f0f0f0fu, xh.y, ih);
-    ih = dot4((q[2] >> 4) & 0x0f0f0f0fu, xh.z, ih);
-    ih = dot4((q[3] >> 4) & 0x0f0f0f0fu, xh.w, ih);
-    const float dxl = dxs[t * dstride + d_lo], dxh = dxs[t * dstride + d_lo + 1];
-    const float sxl = sxs[t * sstride + g_lo], sxh = sxs[t * sstride + g_lo + 2];
-    acc[t] += d * ((float)sc0 * dxl * (float)il + (float)sc1 * dxh * (float)ih)
-              - dmin * ((float)m0 * sxl + (float)m1 * sxh);
+    const long rb = rowblk + blk;
+    r.l = *reinterpret_cast<const uint4*>(w.q + rb * 128 + sub * 16);
+    r.hb = *reinterpret_cast<const uint4*>(w.qh + rb * 64 + (sub >> 2) * 32 + (sub & 1) * 16);
+    r.s = *reinterpret_cast<const uint4*>(w.sc + rb * 16);
+    r.d = w.d[rb];
   }
 }
 
-template <int T>
-__device__ __forceinline__ void q6k_block(const QMat& w, long rowblk, int blk, int sub,
-                                          const int8_t* xs, const float* dxs, const float* sxs,
-                                          int xstride, int dstride, int sstride, float* acc) {
-  const long rb = rowblk + blk;                       // (row * nb + blk)
-  const int n = sub >> 2, h1 = sub & 1, klo = (sub & 3) >> 1;
-  const uint4 ql = *reinterpret_cast<const uint4*>(w.q + rb * 128 + sub * 16);
-  const uint4 qh = *reinterpret_cast<const uint4*>(w.qh + rb * 64 + n * 32 + h1 * 16);
-  const uint4 scv = *reinterpret_cast<const uint4*>(w.sc + rb * 16);
-  const float d = h2f(w.d[rb]);
-  const uint32_t scw[4] = {scv.x, scv.y, scv.z, scv.w};
-  const int i0 = 8 * n + h1 + 2 * klo, i1 = i0 + 4;
-  const float sc0 = (float)(int8_t)((scw[i0 >> 2] >> ((i0 & 3) * 8)) & 0xffu);
-  const float sc1 = (float)(int8_t)((scw[i1 >> 2] >> ((i1 & 3) * 8)) & 0xffu);
-  const uint32_t l[4] = {ql.x, ql.y, ql.z, ql.w};
-  const uint32_t hb[4] = {qh.x, qh.y, qh.z, qh.w};
-  const int sh = 2 * klo;
-  uint32_t qlo[4], qhi[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    qlo[i] = (l[i] & 0x0f0f0f0fu) | (((hb[i] >> sh) & 0x03030303u) << 4);
-    qhi[i] = ((l[i] >> 4) & 0x0f0f0f0fu) | (((hb[i] >> (sh + 4)) & 0x03030303u) << 4);
-  }
-  const int p_lo = blk * 256 + n * 128 + klo * 32 + h1 * 16;
-  const int g_lo = p_lo >> 4, d_lo = p_lo >> 5;
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    const uint4 xl = *reinterpret_cast<const uint4*>(xs + t * xstride + xoff(p_lo));
-    const uint4 xh = *reinterpret_cast<const uint4*>(xs + t * xstride + xoff(p_lo + 64));
-    int il = 0, ih = 0;
-    il = dot4(qlo[0], xl.x, il); il = dot4(qlo[1], xl.y, il);
-    il = dot4(qlo[2], xl.z, il); il = dot4(qlo[3], xl.w, il);
-    ih = dot4(qhi[0], xh.x, ih); ih = dot4(qhi[1], xh.y, ih);
-    ih = dot4(qhi[2], xh.z, ih); ih = dot4(qhi[3], xh.w, ih);
-    const float dxl = dxs[t * dstride + d_lo], dxh = dxs[t * dstride + d_lo + 2];
-    const float sxl = sxs[t * sstride + g_lo], sxh = sxs[t * sstride + g_lo + 4];
-    acc[t] += d * (sc0 * (dxl * (float)il - 32.f * sxl) + sc1 * (dxh * (float)ih - 32.f * sxh));
-  }
-}
+struct XView {           // the workgroup's staged activations
+  const int8_t* xs;
+  const float* dxs;
+  const float* sxs;
+  int xstride, dstride, sstride;
+};
 
 template <int TYPE, int T>
-__device__ __forceinline__ void row_dot(const QMat& w, int row, int nb, int lane,
-                                        const int8_t* xs, const float* dxs, const float* sxs,
-                                        int xstride, int dstride, int sstride, float* acc) {
-  const int sub = lane & 7;
-  const int bl = lane >> 3;
+__device__ __forceinline__ void dot_blk(const Blk<TYPE>& r, int blk, int sub, const XView& x,
+                                        float* acc) {
   if constexpr (TYPE == kQ4K) {
-    const uint8_t* r = w.q + (long)row * nb * kQ4KBytes;
-#pragma unroll 2
-    for (int b0 = 0; b0 < nb; b0 += 8) {
-      const int blk = b0 + bl;
-      if (blk < nb) q4k_block<T>(r, blk, sub, xs, dxs, sxs, xstride, dstride, sstride, acc);
+    const int c = sub >> 1;               // 64-weight chunk: sub-blocks 2c (low) and 2c+1 (high)
+    const float d = h2f(r.h.x & 0xffffu), dmin = h2f(r.h.x >> 16);
+    const uint32_t s[3] = {r.h.y, r.h.z, r.h.w};
+    auto sbyte = [&](int i) -> uint32_t { return (s[i >> 2] >> ((i & 3) * 8)) & 0xffu; };
+    const int j0 = 2 * c, j1 = 2 * c + 1;
+    uint32_t sc0, m0, sc1, m1;
+    if (c < 2) {
+      sc0 = sbyte(j0) & 63; m0 = sbyte(j0 + 4) & 63;
+      sc1 = sbyte(j1) & 63; m1 = sbyte(j1 + 4) & 63;
+    } else {
+      sc0 = (sbyte(j0 + 4) & 0xf) | ((sbyte(j0 - 4) >> 6) << 4);
+      m0 = (sbyte(j0 + 4) >> 4) | ((sbyte(j0) >> 6) << 4);
+      sc1 = (sbyte(j1 + 4) & 0xf) | ((sbyte(j1 - 4) >> 6) << 4);
+      m1 = (sbyte(j1 + 4) >> 4) | ((sbyte(j1) >> 6) << 4);
+    }
+    const uint32_t q[4] = {r.q.x, r.q.y, r.q.z, r.q.w};
+    const int p_lo = blk * 256 + c * 64 + (sub & 1) * 16;
+    const int g_lo = p_lo >> 4, d_lo = p_lo >> 5;
+    const float dsc0 = d * (float)sc0, dsc1 = d * (float)sc1;
+    const float dm0 = dmin * (float)m0, dm1 = dmin * (float)m1;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const uint4 xl = *reinterpret_cast<const uint4*>(x.xs + t * x.xstride + xoff(p_lo));
+      const uint4 xh = *reinterpret_cast<const uint4*>(x.xs + t * x.xstride + xoff(p_lo + 32));
+      int il = 0, ih = 0;
+      il = dot4(q[0] & 0x0f0f0f0fu, xl.x, il);
+      il = dot4(q[1] & 0x0f0f0f0fu, xl.y, il);
+      il = dot4(q[2] & 0x0f0f0f0fu, xl.z, il);
+      il = dot4(q[3] & 0x0f0f0f0fu, xl.w, il);
+      ih = dot4((q[0] >> 4) & 0x0f0f0f0fu, xh.x, ih);
+      ih = dot4((q[1] >> 4) & 0x0f0f0f0fu, xh.y, ih);
+      ih = dot4((q[2] >> 4) & 0x0f0f0f0fu, xh.z, ih);
+      ih = dot4((q[3] >> 4) & 0x0f0f0f0fu, xh.w, ih);
+      const float2 dxv = *reinterpret_cast<const float2*>(x.dxs + t * x.dstride + d_lo);
+      const float sxl = x.sxs[t * x.sstride + g_lo], sxh = x.sxs[t * x.sstride + g_lo + 2];
+      acc[t] += dsc0 * dxv.x * (float)il + dsc1 * dxv.y * (float)ih - dm0 * sxl - dm1 * sxh;
     }
   } else {
-    const long rowblk = (long)row * nb;
-#pragma unroll 2
-    for (int b0 = 0; b0 < nb; b0 += 8) {
-      const int blk = b0 + bl;
-      if (blk < nb) q6k_block<T>(w, rowblk, blk, sub, xs, dxs, sxs, xstride, dstride, sstride, acc);
+    const int n = sub >> 2, h1 = sub & 1, klo = (sub & 3) >> 1;
+    const float d = h2f(r.d & 0xffffu);
+    const uint32_t scw[4] = {r.s.x, r.s.y, r.s.z, r.s.w};
+    const int i0 = 8 * n + h1 + 2 * klo, i1 = i0 + 4;
+    const float sc0 = d * (float)(int8_t)((scw[i0 >> 2] >> ((i0 & 3) * 8)) & 0xffu);
+    const float sc1 = d * (float)(int8_t)((scw[i1 >> 2] >> ((i1 & 3) * 8)) & 0xffu);
+    const uint32_t l[4] = {r.l.x, r.l.y, r.l.z, r.l.w};
+    const uint32_t hb[4] = {r.hb.x, r.hb.y, r.hb.z, r.hb.w};
+    const int sh = 2 * klo;
+    uint32_t qlo[4], qhi[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      qlo[i] = (l[i] & 0x0f0f0f0fu) | (((hb[i] >> sh) & 0x03030303u) << 4);
+      qhi[i] = ((l[i] >> 4) & 0x0f0f0f0fu) | (((hb[i] >> (sh + 4)) & 0x03030303u) << 4);
+    }
+    const int p_lo = blk * 256 + n * 128 + klo * 32 + h1 * 16;
+    const int g_lo = p_lo >> 4, d_lo = p_lo >> 5;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const uint4 xl = *reinterpret_cast<const uint4*>(x.xs + t * x.xstride + xoff(p_lo));
+      const uint4 xh = *reinterpret_cast<const uint4*>(x.xs + t * x.xstride + xoff(p_lo + 64));
+      int il = 0, ih = 0;
+      il = dot4(qlo[0], xl.x, il); il = dot4(qlo[1], xl.y, il);
+      il = dot4(qlo[2], xl.z, il); il = dot4(qlo[3], xl.w, il);
+      ih = dot4(qhi[0], xh.x, ih); ih = dot4(qhi[1], xh.y, ih);
+      ih = dot4(qhi[2], xh.z, ih); ih = dot4(qhi[3], xh.w, ih);
+      const float dxl = x.dxs[t * x.dstride + d_lo], dxh = x.dxs[t * x.dstride + d_lo + 2];
+      const float sxl = x.sxs[t * x.sstride + g_lo], sxh = x.sxs[t * x.sstride + g_lo + 4];
+      acc[t] += sc0 * (dxl * (float)il - 32.f * sxl) + sc1 * (dxh * (float)ih - 32.f * sxh);
     }
   }
 }
 
+// Blocks in flight per lane per batch (all loads of a batch are issued before any is used).
+template <int TYPE, int MODE>
+constexpr int kBatch = TYPE == kQ4K ? (MODE == kPair ? 2 : 4) : (MODE == kPair ? 1 : 2);
+
+// Workgroup = W waves (blockDim/64); ks waves share one row (each walks 1/ks of the super-blocks,
+// partial sums meet in LDS); W/ks rows per workgroup iteration; rows_per_wg rows per workgroup.
+// The first batch of weight loads is issued before the activations are staged, so the staging
+// (L2 → LDS → barrier) overlaps the first HBM round trip.
 template <int TYPE, int T, int MODE>
-__global__ void __launch_bounds__(256) qgemv_kernel(GemvArgs a) {
+__global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
+  constexpr int U = kBatch<TYPE, MODE>;
   extern __shared__ __align__(16) uint8_t lds[];
   const int K = a.K, nb = K >> 8;
+  const int W = blockDim.x >> 6, KS = a.ks, rpi = W / KS;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane & 7, bl = lane >> 3;
+  const int kp = wave % KS, rw = wave / KS;
+  const int nbk = (nb + KS - 1) / KS;
+  const int kb0 = kp * nbk, kb1 = min(nb, kb0 + nbk);
+  const int r0 = blockIdx.x * a.rows_per_wg;
+  const int r1 = min(a.N, r0 + a.rows_per_wg);
+
+  Blk<TYPE> pre[U], pre1[U];
+  {
+    const int row = r0 + rw;
+    if (row < r1) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int blk = kb0 + 8 * u + bl;
+        if (blk < kb1) {
+          load_blk<TYPE>(a.w0, (long)row * nb, blk, sub, pre[u]);
+          if constexpr (MODE == kPair) load_blk<TYPE>(a.w1, (long)row * nb, blk, sub, pre1[u]);
+        }
+      }
+    }
+  }
   const int xstride = nb * 288;                      // padded bytes per token
   int8_t* xs = reinterpret_cast<int8_t*>(lds);
   float* dxs = reinterpret_cast<float*>(lds + T * xstride);
   float* sxs = dxs + T * (K >> 5);
-  // ---- stage the T tokens' activations (16-byte vectors) ----
+  float* red = sxs + T * (K >> 4);                   // [W][T][2]
   for (int i = threadIdx.x; i < T * (K >> 4); i += blockDim.x) {
     const int t = i / (K >> 4), p = (i - t * (K >> 4)) << 4;
     *reinterpret_cast<uint4*>(xs + t * xstride + xoff(p)) =
@@ -213,22 +242,70 @@ __global__ void __launch_bounds__(256) qgemv_kernel(GemvArgs a) {
   for (int i = threadIdx.x; i < T * (K >> 5); i += blockDim.x) dxs[i] = a.dx[i];
   for (int i = threadIdx.x; i < T * (K >> 4); i += blockDim.x) sxs[i] = a.sx[i];
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int r0 = blockIdx.x * a.rows_per_wg;
-  const int r1 = min(a.N, r0 + a.rows_per_wg);
-  for (int row = r0 + wave; row < r1; row += nw) {
+  const XView xv = {xs, dxs, sxs, xstride, K >> 5, K >> 4};
+
+  for (int rb = r0; rb < r1; rb += rpi) {
+    const int row = rb + rw;
+    const bool valid = row < r1;
     float acc[T], acc1[T];
 #pragma unroll
     for (int t = 0; t < T; ++t) acc[t] = acc1[t] = 0.f;
-    row_dot<TYPE, T>(a.w0, row, nb, lane, xs, dxs, sxs, xstride, K >> 5, K >> 4, acc);
-    if constexpr (MODE == kPair)
-      row_dot<TYPE, T>(a.w1, row, nb, lane, xs, dxs, sxs, xstride, K >> 5, K >> 4, acc1);
+    if (valid) {
+      const long rowblk = (long)row * nb;
+      for (int b0 = kb0; b0 < kb1; b0 += 8 * U) {
+        Blk<TYPE> cur[U], cur1[U];
+        if (rb == r0 && b0 == kb0) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) { cur[u] = pre[u]; cur1[u] = pre1[u]; }
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int blk = b0 + 8 * u + bl;
+            if (blk < kb1) {
+              load_blk<TYPE>(a.w0, rowblk, blk, sub, cur[u]);
+              if constexpr (MODE == kPair) load_blk<TYPE>(a.w1, rowblk, blk, sub, cur1[u]);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int blk = b0 + 8 * u + bl;
+          if (blk < kb1) {
+            dot_blk<TYPE, T>(cur[u], blk, sub, xv, acc);
+            if constexpr (MODE == kPair) dot_blk<TYPE, T>(cur1[u], blk, sub, xv, acc1);
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       acc[t] = wave_sum(acc[t]);
       if constexpr (MODE == kPair) acc1[t] = wave_sum(acc1[t]);
     }
-    if (lane < T) {
+    if (KS > 1) {
+      if (lane == 0) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          red[(wave * T + t) * 2] = acc[t];
+          red[(wave * T + t) * 2 + 1] = acc1[t];
+        }
+      }
+      __syncthreads();
+      if (kp == 0) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          float s = 0.f, s1 = 0.f;
+          for (int k = 0; k < KS; ++k) {
+            s += red[((wave + k) * T + t) * 2];
+            s1 += red[((wave + k) * T + t) * 2 + 1];
+          }
+          acc[t] = s;
+          acc1[t] = s1;
+        }
+      }
+      __syncthreads();
+    }
+    if (valid && kp == 0 && lane < T) {
       float v = 0.f, v1 = 0.f;
 #pragma unroll
       for (int t = 0; t < T; ++t)
@@ -242,15 +319,23 @@ __global__ void __launch_bounds__(256) qgemv_kernel(GemvArgs a) {
 }
 
 // ---------------------------------------------------------------- RMSNorm + Q8 activation quant
-// One workgroup per token.  x fp32 [T][K]; w fp32 [K] or null (quantise only).
+// grid (ceil(K/2048), T), 256 threads; thread = 8 consecutive values, 4 threads = one 32-block.
+// With a norm weight every workgroup first reduces the whole row's sum of squares (the row is
+// L2-resident: 14-74 KB), then scales its slice.  x fp32 [T][K]; w fp32 [K] or null.
 __global__ void __launch_bounds__(256) rmsnorm_q8_kernel(const float* __restrict__ x,
                                                          const float* __restrict__ w, float eps,
                                                          int K, int8_t* __restrict__ x8,
                                                          float* __restrict__ dx,
                                                          float* __restrict__ sx) {
   __shared__ float red[4];
-  const int t = blockIdx.x;
+  const int t = blockIdx.y;
   const float* xr = x + (long)t * K;
+  const int i0 = blockIdx.x * 2048 + threadIdx.x * 8;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  if (i0 < K) {
+    a = *reinterpret_cast<const float4*>(xr + i0);
+    b = *reinterpret_cast<const float4*>(xr + i0 + 4);
+  }
   float rs = 1.f;
   if (w) {
     float ss = 0.f;
@@ -261,45 +346,38 @@ __global__ void __launch_bounds__(256) rmsnorm_q8_kernel(const float* __restrict
     ss = wave_sum(ss);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
     __syncthreads();
-    ss = 0.f;
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) ss += red[i];
+    ss = red[0] + red[1] + red[2] + red[3];
     rs = rsqrtf(ss / (float)K + eps);
   }
-  for (int blk = threadIdx.x; blk < (K >> 5); blk += blockDim.x) {
-    float v[32];
+  if (i0 >= K) return;                       // K % 256 == 0: whole quads leave together
+  float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  if (w) {
+    const float4 wa = *reinterpret_cast<const float4*>(w + i0);
+    const float4 wb = *reinterpret_cast<const float4*>(w + i0 + 4);
+    const float ww[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float4 a = *reinterpret_cast<const float4*>(xr + blk * 32 + i * 4);
-      v[4 * i] = a.x; v[4 * i + 1] = a.y; v[4 * i + 2] = a.z; v[4 * i + 3] = a.w;
-    }
-    float amax = 0.f;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      v[i] *= rs * (w ? w[blk * 32 + i] : 1.f);
-      amax = fmaxf(amax, fabsf(v[i]));
-    }
-    const float d = amax / 127.f;
-    const float id = d > 0.f ? 1.f / d : 0.f;
-    uint32_t pk[8];
-    int s0 = 0, s1 = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      uint32_t word = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = (int)__builtin_rintf(v[4 * i + j] * id);
-        word |= ((uint32_t)(q & 0xff)) << (8 * j);
-        if (i < 4) s0 += q; else s1 += q;
-      }
-      pk[i] = word;
-    }
-    int8_t* o = x8 + (long)t * K + blk * 32;
-    reinterpret_cast<uint4*>(o)[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-    reinterpret_cast<uint4*>(o)[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
-    dx[(long)t * (K >> 5) + blk] = d;
-    sx[(long)t * (K >> 4) + 2 * blk] = d * (float)s0;
-    sx[(long)t * (K >> 4) + 2 * blk + 1] = d * (float)s1;
+    for (int i = 0; i < 8; ++i) v[i] *= rs * ww[i];
   }
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
+  amax = fmaxf(amax, __shfl_xor(amax, 1, kWave));
+  amax = fmaxf(amax, __shfl_xor(amax, 2, kWave));
+  const float d = amax / 127.f;
+  const float id = d > 0.f ? 1.f / d : 0.f;
+  uint32_t pk[2] = {0u, 0u};
+  int s = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int q = (int)__builtin_rintf(v[i] * id);
+    pk[i >> 2] |= ((uint32_t)(q & 0xff)) << (8 * (i & 3));
+    s += q;
+  }
+  s += __shfl_xor(s, 1, kWave);              // 16-value sums: lanes (0,1) and (2,3) of the quad
+  *reinterpret_cast<uint2*>(x8 + (long)t * K + i0) = make_uint2(pk[0], pk[1]);
+  const int q4 = threadIdx.x & 3;
+  if (q4 == 0) dx[(long)t * (K >> 5) + (i0 >> 5)] = d;
+  if ((q4 & 1) == 0) sx[(long)t * (K >> 4) + (i0 >> 4)] = d * (float)s;
 }
 
 // ---------------------------------------------------------------- RoPE (NeoX) + KV-cache write
@@ -342,8 +420,11 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------- split-context decode attention
-// grid (Hkv, nsplit, T); 256 threads.  Each workgroup: the G = H/Hkv q heads of one kv head over
-// positions [s*256, min(s*256+256, len)).  Writes unnormalised partial outputs + (max, sum).
+// grid (Hkv, max_ctx/64, T); 256 threads.  One workgroup: the G = H/Hkv q heads of one kv head
+// over the 64 positions [s*64, min(s*64+64, len)).  Scores: 4 lanes per position (32 dims each,
+// all four 16-byte K loads in flight), softmax by one wave (lane = position), P.V: wave w takes
+// 16 positions with all 16 V loads in flight, lane = 2 dims.  Writes the unnormalised partial
+// output and (max, sum) per head.
 __global__ void __launch_bounds__(256) attn_decode_kernel(const float* __restrict__ q,
                                                           const int* __restrict__ pos,
                                                           const int* __restrict__ slot,
@@ -354,7 +435,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(const float* __restric
                                                           float* __restrict__ pml) {
   __shared__ float qs[kMaxGroup][kHeadDim];
   __shared__ float ps[kMaxGroup][kAttnChunk];
-  __shared__ float red[kMaxGroup][4];
+  __shared__ float mls[kMaxGroup][2];
   __shared__ float opart[4][kMaxGroup][kHeadDim];
   const int kh = blockIdx.x, sp = blockIdx.y, t = blockIdx.z;
   const int G = H / Hkv;
@@ -369,24 +450,27 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(const float* __restric
     return;
   }
   const int n = min(kAttnChunk, len - p0);
+  const long cbase = ((long)slot[t] * Hkv + kh) * max_ctx * kHeadDim;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // K loads first (independent of q)
+  const int pi = threadIdx.x >> 2, qd = threadIdx.x & 3;
+  uint4 kv[4];
+  if (pi < n) {
+    const uint4* kr = reinterpret_cast<const uint4*>(kc + cbase + (long)(p0 + pi) * kHeadDim
+                                                     + qd * 32);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) kv[c] = kr[c];
+  }
   for (int i = threadIdx.x; i < G * kHeadDim; i += blockDim.x)
     qs[i / kHeadDim][i % kHeadDim] = q[(long)t * H * kHeadDim + (kh * G) * kHeadDim + i] * scale;
   __syncthreads();
-  const long cbase = ((long)slot[t] * Hkv + kh) * max_ctx * kHeadDim;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  // scores: one position per thread
   float sc[kMaxGroup];
-  const int pi = threadIdx.x;
 #pragma unroll
-  for (int g = 0; g < kMaxGroup; ++g) sc[g] = -INFINITY;
+  for (int g = 0; g < kMaxGroup; ++g) sc[g] = 0.f;
   if (pi < n) {
 #pragma unroll
-    for (int g = 0; g < kMaxGroup; ++g) sc[g] = 0.f;
-    const uint4* kr = reinterpret_cast<const uint4*>(kc + cbase + (long)(p0 + pi) * kHeadDim);
-#pragma unroll 4
-    for (int c = 0; c < kHeadDim / 8; ++c) {
-      const uint4 kv = kr[c];
-      const uint32_t kw[4] = {kv.x, kv.y, kv.z, kv.w};
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t kw[4] = {kv[c].x, kv[c].y, kv[c].z, kv[c].w};
       float kf[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -397,50 +481,62 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(const float* __restric
       for (int g = 0; g < kMaxGroup; ++g) {
         if (g < G) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) sc[g] += kf[e] * qs[g][c * 8 + e];
+          for (int e = 0; e < 8; ++e) sc[g] += kf[e] * qs[g][qd * 32 + c * 8 + e];
         }
       }
     }
   }
-  // row max / sum over the chunk, per head
-  float mx[kMaxGroup];
 #pragma unroll
   for (int g = 0; g < kMaxGroup; ++g) {
-    const float m = wave_max(sc[g]);
-    if (lane == 0) red[g][wave] = m;
+    sc[g] += __shfl_xor(sc[g], 1, kWave);
+    sc[g] += __shfl_xor(sc[g], 2, kWave);
+  }
+  if (qd == 0) {
+#pragma unroll
+    for (int g = 0; g < kMaxGroup; ++g)
+      if (g < G) ps[g][pi] = pi < n ? sc[g] : -INFINITY;
   }
   __syncthreads();
-#pragma unroll
-  for (int g = 0; g < kMaxGroup; ++g)
-    mx[g] = fmaxf(fmaxf(red[g][0], red[g][1]), fmaxf(red[g][2], red[g][3]));
-  __syncthreads();
-#pragma unroll
-  for (int g = 0; g < kMaxGroup; ++g) {
-    const float p = (pi < n && g < G) ? __expf(sc[g] - mx[g]) : 0.f;
-    ps[g][pi] = p;
-    const float s = wave_sum(p);
-    if (lane == 0) red[g][wave] = s;
+  if (wave == 0) {
+    for (int g = 0; g < G; ++g) {
+      const float s = ps[g][lane];
+      const float m = wave_max(s);
+      const float p = lane < n ? __expf(s - m) : 0.f;
+      ps[g][lane] = p;
+      const float l = wave_sum(p);
+      if (lane == 0) { mls[g][0] = m; mls[g][1] = l; }
+    }
   }
   __syncthreads();
-  // P.V: wave w takes positions w, w+4, ...; lane owns dims 2*lane, 2*lane+1
+  // P.V: wave w → positions w*16 .. w*16+15
+  uint32_t vv[16];
+  const uint32_t* vr = reinterpret_cast<const uint32_t*>(vc + cbase) + lane;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int p = wave * 16 + j;
+    vv[j] = p < n ? vr[(long)(p0 + p) * (kHeadDim / 2)] : 0u;
+  }
   float o[kMaxGroup][2];
 #pragma unroll
   for (int g = 0; g < kMaxGroup; ++g) o[g][0] = o[g][1] = 0.f;
-  const uint32_t* vr = reinterpret_cast<const uint32_t*>(vc + cbase) + lane;
-  for (int p = wave; p < n; p += 4) {
-    const uint32_t vv = vr[(long)(p0 + p) * (kHeadDim / 2)];
-    const float v0 = h2f(vv & 0xffffu), v1 = h2f(vv >> 16);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const float v0 = h2f(vv[j] & 0xffffu), v1 = h2f(vv[j] >> 16);
 #pragma unroll
     for (int g = 0; g < kMaxGroup; ++g) {
-      const float pw = ps[g][p];
-      o[g][0] += pw * v0;
-      o[g][1] += pw * v1;
+      if (g < G) {
+        const float pw = ps[g][wave * 16 + j];
+        o[g][0] += pw * v0;
+        o[g][1] += pw * v1;
+      }
     }
   }
 #pragma unroll
   for (int g = 0; g < kMaxGroup; ++g) {
-    opart[wave][g][2 * lane] = o[g][0];
-    opart[wave][g][2 * lane + 1] = o[g][1];
+    if (g < G) {
+      opart[wave][g][2 * lane] = o[g][0];
+      opart[wave][g][2 * lane + 1] = o[g][1];
+    }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < G * kHeadDim; i += blockDim.x) {
@@ -450,80 +546,47 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(const float* __restric
   }
   if (threadIdx.x < G) {
     const int g = threadIdx.x;
-    pml[(pidx + (long)g * nsplit) * 2] = mx[g];
-    pml[(pidx + (long)g * nsplit) * 2 + 1] = red[g][0] + red[g][1] + red[g][2] + red[g][3];
+    pml[(pidx + (long)g * nsplit) * 2] = mls[g][0];
+    pml[(pidx + (long)g * nsplit) * 2 + 1] = mls[g][1];
   }
 }
 
-// Merge the chunks of every head and quantise the attention output to Q8 (the o_proj input).
-// grid T; thread i < H*4 owns one 32-value block (head i/4, dims (i%4)*32..+32).
-__global__ void __launch_bounds__(256) attn_combine_q8_kernel(const float* __restrict__ po,
+// Merge the chunks of one head and quantise the attention output to Q8 (the o_proj input).
+// grid (H, T), 128 threads: thread = one output dim; a 32-dim block = half a wave.
+__global__ void __launch_bounds__(128) attn_combine_q8_kernel(const float* __restrict__ po,
                                                               const float* __restrict__ pml,
                                                               const int* __restrict__ pos, int H,
                                                               int nsplit, float* __restrict__ out,
                                                               int8_t* __restrict__ x8,
                                                               float* __restrict__ dx,
                                                               float* __restrict__ sx) {
-  const int t = blockIdx.x;
+  const int h = blockIdx.x, t = blockIdx.y, dd = threadIdx.x;
   const int ns = min(nsplit, (pos[t] + kAttnChunk) / kAttnChunk);
-  const int K = H * kHeadDim;
-  for (int blk = threadIdx.x; blk < H * (kHeadDim / 32); blk += blockDim.x) {
-    const int h = blk / (kHeadDim / 32), d0 = (blk % (kHeadDim / 32)) * 32;
-    const long hb = ((long)t * H + h) * nsplit;
-    float m = -INFINITY;
-    for (int s = 0; s < ns; ++s) m = fmaxf(m, pml[(hb + s) * 2]);
-    float den = 0.f;
-    float v[32];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) v[i] = 0.f;
-    for (int s = 0; s < ns; ++s) {
-      const float ms = pml[(hb + s) * 2];
-      if (ms == -INFINITY) continue;
-      const float wgt = __expf(ms - m);
-      den += wgt * pml[(hb + s) * 2 + 1];
-      const float4* src = reinterpret_cast<const float4*>(po + (hb + s) * kHeadDim + d0);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float4 a = src[i];
-        v[4 * i] += wgt * a.x; v[4 * i + 1] += wgt * a.y;
-        v[4 * i + 2] += wgt * a.z; v[4 * i + 3] += wgt * a.w;
-      }
-    }
-    const float inv = den > 0.f ? 1.f / den : 0.f;
-    float amax = 0.f;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      v[i] *= inv;
-      amax = fmaxf(amax, fabsf(v[i]));
-    }
-    if (out) {
-      float4* dst = reinterpret_cast<float4*>(out + (long)t * K + h * kHeadDim + d0);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) dst[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
-    }
-    const float d = amax / 127.f;
-    const float id = d > 0.f ? 1.f / d : 0.f;
-    uint32_t pk[8];
-    int s0 = 0, s1 = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      uint32_t word = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = (int)__builtin_rintf(v[4 * i + j] * id);
-        word |= ((uint32_t)(q & 0xff)) << (8 * j);
-        if (i < 4) s0 += q; else s1 += q;
-      }
-      pk[i] = word;
-    }
-    const int gb = h * (kHeadDim / 32) + d0 / 32;      // 32-block index within the row
-    int8_t* o = x8 + (long)t * K + gb * 32;
-    reinterpret_cast<uint4*>(o)[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-    reinterpret_cast<uint4*>(o)[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
-    dx[(long)t * (K >> 5) + gb] = d;
-    sx[(long)t * (K >> 4) + 2 * gb] = d * (float)s0;
-    sx[(long)t * (K >> 4) + 2 * gb + 1] = d * (float)s1;
+  const long hb = ((long)t * H + h) * nsplit;
+  float m = -INFINITY;
+  for (int s = 0; s < ns; ++s) m = fmaxf(m, pml[(hb + s) * 2]);
+  float den = 0.f, v = 0.f;
+#pragma unroll 8
+  for (int s = 0; s < ns; ++s) {
+    const float ms = pml[(hb + s) * 2];
+    const float wgt = ms == -INFINITY ? 0.f : __expf(ms - m);
+    den += wgt * pml[(hb + s) * 2 + 1];
+    v += wgt * po[(hb + s) * kHeadDim + dd];
   }
+  v = den > 0.f ? v / den : 0.f;
+  const int K = H * kHeadDim, col = h * kHeadDim + dd;
+  if (out) out[(long)t * K + col] = v;
+  float amax = fabsf(v);
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, kWave));
+  const float d = amax / 127.f;
+  const int qv = d > 0.f ? (int)__builtin_rintf(v / d) : 0;
+  x8[(long)t * K + col] = (int8_t)qv;
+  int s16 = qv;
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) s16 += __shfl_xor(s16, o, kWave);
+  if ((dd & 31) == 0) dx[(long)t * (K >> 5) + (col >> 5)] = d;
+  if ((dd & 15) == 0) sx[(long)t * (K >> 4) + (col >> 4)] = d * (float)s16;
 }
 
 // ---------------------------------------------------------------- dequantisation (rows → fp16/fp32)
@@ -602,24 +665,39 @@ __global__ void q6k_repack_kernel(const uint8_t* __restrict__ src, long nblocks,
 }
 
 template <int TYPE, int T, int MODE>
-int launch_gemv(const GemvArgs& a, hipStream_t st) {
+int launch_gemv(const GemvArgs& a, int waves, hipStream_t st) {
   const int nb = a.K >> 8;
-  const size_t lds = (size_t)T * (nb * 288 + (a.K >> 5) * 4 + (a.K >> 4) * 4);
+  const size_t lds = (size_t)T * (nb * 288 + (a.K >> 5) * 4 + (a.K >> 4) * 4)
+                     + (size_t)waves * T * 2 * 4;
   if (lds > 160 * 1024) return 3;
   const int grid = (a.N + a.rows_per_wg - 1) / a.rows_per_wg;
-  hipLaunchKernelGGL((qgemv_kernel<TYPE, T, MODE>), dim3(grid), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((qgemv_kernel<TYPE, T, MODE>), dim3(grid), dim3(waves * 64), lds, st, a);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
 template <int TYPE, int MODE>
-int dispatch_t(const GemvArgs& a, hipStream_t st) {
+int dispatch_t(const GemvArgs& a, int waves, hipStream_t st) {
   switch (a.T) {
-    case 1: return launch_gemv<TYPE, 1, MODE>(a, st);
-    case 2: return launch_gemv<TYPE, 2, MODE>(a, st);
-    case 3: return launch_gemv<TYPE, 3, MODE>(a, st);
-    case 4: return launch_gemv<TYPE, 4, MODE>(a, st);
+    case 1: return launch_gemv<TYPE, 1, MODE>(a, waves, st);
+    case 2: return launch_gemv<TYPE, 2, MODE>(a, waves, st);
+    case 3: return launch_gemv<TYPE, 3, MODE>(a, waves, st);
+    case 4: return launch_gemv<TYPE, 4, MODE>(a, waves, st);
     default: return 2;
   }
+}
+
+// Default decomposition: enough waves to keep ~32 per CU streaming (256 CUs), split-K inside the
+// workgroup for short matrices, bigger workgroups for long rows so the LDS-staged activations
+// (1.4 bytes per weight column per token) are shared by 8 rows.
+void gemv_shape(int N, int K, int& waves, int& ks, int& rows) {
+  const int nb = K >> 8;
+  if (ks <= 0) ks = N >= 8192 ? 1 : (N >= 2048 ? 2 : 4);
+  while (ks > 1 && nb / ks < 2) ks >>= 1;
+  if (waves <= 0) waves = 8;
+  if (waves < ks) waves = ks;
+  if (rows <= 0) rows = (waves / ks) * (K >= 8192 ? 1 : 2);
+  const int rpi = waves / ks;
+  rows = (rows + rpi - 1) / rpi * rpi;
 }
 
 }  // namespace
@@ -634,10 +712,12 @@ int amdk8s_llm_attn_chunk() { return kAttnChunk; }
 int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, const void* w0sc,
                      const void* w0d, const void* w1q, const void* w1qh, const void* w1sc,
                      const void* w1d, const void* x8, const void* dx, const void* sx,
-                     const void* bias, void* out, int ldo, int N, int K, int T, int rows_per_wg,
-                     void* stream) {
-  if (K % 256 || N <= 0 || T < 1 || T > kMaxTok || rows_per_wg < 1) return 2;
+                     const void* bias, void* out, int ldo, int N, int K, int T, int waves, int ks,
+                     int rows_per_wg, void* stream) {
+  if (K % 256 || N <= 0 || T < 1 || T > kMaxTok) return 2;
   if (mode == kPair && !w1q) return 2;
+  gemv_shape(N, K, waves, ks, rows_per_wg);
+  if (waves > 8 || waves % ks || (ks != 1 && ks != 2 && ks != 4)) return 2;
   GemvArgs a;
   a.w0 = {static_cast<const uint8_t*>(w0q), static_cast<const uint8_t*>(w0qh),
           static_cast<const int8_t*>(w0sc), static_cast<const uint16_t*>(w0d)};
@@ -648,16 +728,16 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
   a.sx = static_cast<const float*>(sx);
   a.bias = static_cast<const float*>(bias);
   a.out = static_cast<float*>(out);
-  a.ldo = ldo; a.N = N; a.K = K; a.T = T; a.rows_per_wg = rows_per_wg;
+  a.ldo = ldo; a.N = N; a.K = K; a.T = T; a.ks = ks; a.rows_per_wg = rows_per_wg;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (type == kQ4K) {
-    if (mode == kStore) return dispatch_t<kQ4K, kStore>(a, st);
-    if (mode == kResid) return dispatch_t<kQ4K, kResid>(a, st);
-    if (mode == kPair) return dispatch_t<kQ4K, kPair>(a, st);
+    if (mode == kStore) return dispatch_t<kQ4K, kStore>(a, waves, st);
+    if (mode == kResid) return dispatch_t<kQ4K, kResid>(a, waves, st);
+    if (mode == kPair) return dispatch_t<kQ4K, kPair>(a, waves, st);
   } else if (type == kQ6K) {
-    if (mode == kStore) return dispatch_t<kQ6K, kStore>(a, st);
-    if (mode == kResid) return dispatch_t<kQ6K, kResid>(a, st);
-    if (mode == kPair) return dispatch_t<kQ6K, kPair>(a, st);
+    if (mode == kStore) return dispatch_t<kQ6K, kStore>(a, waves, st);
+    if (mode == kResid) return dispatch_t<kQ6K, kResid>(a, waves, st);
+    if (mode == kPair) return dispatch_t<kQ6K, kPair>(a, waves, st);
   }
   return 2;
 }
@@ -665,7 +745,8 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
 int amdk8s_llm_rmsnorm_q8(const void* x, const void* w, float eps, int K, int T, void* x8,
                           void* dx, void* sx, void* stream) {
   if (K % 256 || T < 1) return 2;
-  hipLaunchKernelGGL(rmsnorm_q8_kernel, dim3(T), dim3(256), 0, static_cast<hipStream_t>(stream),
+  hipLaunchKernelGGL(rmsnorm_q8_kernel, dim3((K + 2047) / 2048, T), dim3(256), 0,
+                     static_cast<hipStream_t>(stream),
                      static_cast<const float*>(x), static_cast<const float*>(w), eps, K,
                      static_cast<int8_t*>(x8), static_cast<float*>(dx), static_cast<float*>(sx));
   return hipGetLastError() == hipSuccess ? 0 : 1;
@@ -686,13 +767,17 @@ int amdk8s_llm_rope_kv(const void* qkv, int ldq, const void* pos, const void* sl
 
 // Decode attention over the KV cache + combine + Q8 quantisation of the output.
 // po/pml: workspace [T][H][nsplit][128] / [T][H][nsplit][2]; out (nullable) fp32 [T][H*128].
+// span: positions covered by this launch (a multiple of 64, <= max_ctx, > every pos[t]); the
+// caller buckets it so a captured graph does not launch empty chunks up to max_ctx.
 int amdk8s_llm_attn_decode(const void* q, const void* pos, const void* slot, const void* kc,
-                           const void* vc, int H, int Hkv, int head_dim, int max_ctx, float scale,
-                           void* po, void* pml, void* out, void* x8, void* dx, void* sx, int T,
-                           void* stream) {
-  if (head_dim != kHeadDim || H % Hkv || H / Hkv > kMaxGroup || max_ctx % kAttnChunk || T < 1)
+                           const void* vc, int H, int Hkv, int head_dim, int max_ctx, int span,
+                           float scale, void* po, void* pml, void* out, void* x8, void* dx,
+                           void* sx, int T, void* stream) {
+  if (span <= 0) span = max_ctx;
+  if (head_dim != kHeadDim || H % Hkv || H / Hkv > kMaxGroup || max_ctx % kAttnChunk ||
+      span % kAttnChunk || span > max_ctx || T < 1)
     return 2;
-  const int nsplit = max_ctx / kAttnChunk;
+  const int nsplit = span / kAttnChunk;
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(attn_decode_kernel, dim3(Hkv, nsplit, T), dim3(256), 0, st,
                      static_cast<const float*>(q), static_cast<const int*>(pos),
@@ -700,7 +785,7 @@ int amdk8s_llm_attn_decode(const void* q, const void* pos, const void* slot, con
                      static_cast<const uint16_t*>(vc), H, Hkv, max_ctx, nsplit, scale,
                      static_cast<float*>(po), static_cast<float*>(pml));
   if (hipGetLastError() != hipSuccess) return 1;
-  hipLaunchKernelGGL(attn_combine_q8_kernel, dim3(T), dim3(256), 0, st,
+  hipLaunchKernelGGL(attn_combine_q8_kernel, dim3(H, T), dim3(128), 0, st,
                      static_cast<const float*>(po), static_cast<const float*>(pml),
                      static_cast<const int*>(pos), H, nsplit, static_cast<float*>(out),
                      static_cast<int8_t*>(x8), static_cast<float*>(dx), static_cast<float*>(sx));

@@ -29,15 +29,15 @@ def _lib():
             lib.amdk8s_llm_max_tokens.restype = ci
             lib.amdk8s_llm_attn_chunk.restype = ci
             lib.amdk8s_llm_qgemv.argtypes = [ci, ci] + [vp] * 8 + [vp, vp, vp, vp, vp] \
-                + [ci, ci, ci, ci, ci, vp]
+                + [ci, ci, ci, ci, ci, ci, ci, vp]
             lib.amdk8s_llm_qgemv.restype = ci
             lib.amdk8s_llm_rmsnorm_q8.argtypes = [vp, vp, cf, ci, ci, vp, vp, vp, vp]
             lib.amdk8s_llm_rmsnorm_q8.restype = ci
             lib.amdk8s_llm_rope_kv.argtypes = [vp, ci, vp, vp, vp, vp, ci, ci, ci, ci, vp, vp, vp,
                                                ci, vp]
             lib.amdk8s_llm_rope_kv.restype = ci
-            lib.amdk8s_llm_attn_decode.argtypes = [vp, vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, vp,
-                                                   vp, vp, vp, vp, ci, vp]
+            lib.amdk8s_llm_attn_decode.argtypes = [vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, cf, vp,
+                                                   vp, vp, vp, vp, vp, ci, vp]
             lib.amdk8s_llm_attn_decode.restype = ci
             lib.amdk8s_llm_dequant.argtypes = [ci, vp, vp, vp, vp, vp, ci, ci, vp, ci, vp]
             lib.amdk8s_llm_dequant.restype = ci
@@ -69,16 +69,18 @@ def attn_chunk() -> int:
 
 
 def qgemv(w0, x8, dx, sx, out, mode: int = STORE, w1=None, bias=None, ldo: int = None,
-          rows_per_wg: int = 8) -> None:
+          rows_per_wg: int = 0, waves: int = 0, ks: int = 0) -> None:
     """``w0``/``w1``: :class:`~k8s_nvidia_gpus_amd.models.llm.weights.QWeight` on the GPU;
-    activations [T, K] in Q8 form; ``out`` fp32 [T, ldo] (a view with row stride ``ldo``)."""
+    activations [T, K] in Q8 form; ``out`` fp32 [T, ldo] (a view with row stride ``ldo``).
+    ``waves`` per workgroup, ``ks`` waves per row and ``rows_per_wg``: 0 = the kernel's default
+    decomposition for this shape."""
     t = x8.shape[0]
     ldo = out.stride(0) if ldo is None else ldo
     a = w0.ptrs()
     b = w1.ptrs() if w1 is not None else (None, None, None, None)
     _check(_lib().amdk8s_llm_qgemv(w0.qtype, mode, *a, *b, x8.data_ptr(), dx.data_ptr(),
                                    sx.data_ptr(), _p(bias), out.data_ptr(), ldo, w0.n, w0.k, t,
-                                   rows_per_wg, _stream(x8)), "amdk8s_llm_qgemv")
+                                   waves, ks, rows_per_wg, _stream(x8)), "amdk8s_llm_qgemv")
 
 
 def rmsnorm_q8(x, w, eps: float, x8, dx, sx) -> None:
@@ -98,10 +100,12 @@ def rope_kv(qkv, pos, slot, cos_t, sin_t, heads: int, kv_heads: int, head_dim: i
 
 
 def attn_decode(q, pos, slot, kc, vc, heads: int, kv_heads: int, head_dim: int, max_ctx: int,
-                scale: float, po, pml, x8, dx, sx, out=None) -> None:
+                scale: float, po, pml, x8, dx, sx, out=None, span: int = 0) -> None:
+    """``span``: context positions this call covers (multiple of ``attn_chunk()``, above every
+    position; 0 = ``max_ctx``)."""
     _check(_lib().amdk8s_llm_attn_decode(q.data_ptr(), pos.data_ptr(), slot.data_ptr(),
                                          kc.data_ptr(), vc.data_ptr(), heads, kv_heads, head_dim,
-                                         max_ctx, float(scale), po.data_ptr(), pml.data_ptr(),
+                                         max_ctx, span, float(scale), po.data_ptr(), pml.data_ptr(),
                                          _p(out), x8.data_ptr(), dx.data_ptr(), sx.data_ptr(),
                                          q.shape[0], _stream(q)), "amdk8s_llm_attn_decode")
 

@@ -1,0 +1,296 @@
+"""CPU tests of the in-tree Qwen2 LLM family: GGUF container, K-quant codecs (against independent
+scalar decoders written from the format description), tokenizer / ChatML, the engine's reference
+path (incremental decode == full prefill), and the llama-server-compatible API with continuous
+batching (FastAPI TestClient, no GPU)."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from k8s_nvidia_gpus_amd.models.llm import gguf, quants, tiny
+from k8s_nvidia_gpus_amd.models.llm.config import from_gguf, to_gguf_metadata, use_more_bits
+
+
+# ----------------------------------------------------------------- scalar reference decoders
+def _f16(b):
+    return float(np.frombuffer(bytes(b), "<f2")[0])
+
+
+def scalar_q4_k(block: bytes) -> list:
+    d, dmin = _f16(block[0:2]), _f16(block[2:4])
+    sc = block[4:16]
+    qs = block[16:144]
+
+    def scale_min(j):
+        if j < 4:
+            return sc[j] & 63, sc[j + 4] & 63
+        return (sc[j + 4] & 0xF) | ((sc[j - 4] >> 6) << 4), (sc[j + 4] >> 4) | ((sc[j] >> 6) << 4)
+
+    out = []
+    for c in range(4):
+        s0, m0 = scale_min(2 * c)
+        s1, m1 = scale_min(2 * c + 1)
+        out += [d * s0 * (qs[32 * c + l] & 0xF) - dmin * m0 for l in range(32)]
+        out += [d * s1 * (qs[32 * c + l] >> 4) - dmin * m1 for l in range(32)]
+    return out
+
+
+def scalar_q6_k(block: bytes) -> list:
+    ql, qh = block[0:128], block[128:192]
+    sc = np.frombuffer(bytes(block[192:208]), np.int8)
+    d = _f16(block[208:210])
+    y = [0.0] * 256
+    for n in range(2):
+        for l in range(32):
+            is_ = l // 16
+            q1 = ((ql[64 * n + l] & 0xF) | (((qh[32 * n + l] >> 0) & 3) << 4)) - 32
+            q2 = ((ql[64 * n + l + 32] & 0xF) | (((qh[32 * n + l] >> 2) & 3) << 4)) - 32
+            q3 = ((ql[64 * n + l] >> 4) | (((qh[32 * n + l] >> 4) & 3) << 4)) - 32
+            q4 = ((ql[64 * n + l + 32] >> 4) | (((qh[32 * n + l] >> 6) & 3) << 4)) - 32
+            y[128 * n + l] = d * sc[8 * n + is_] * q1
+            y[128 * n + l + 32] = d * sc[8 * n + is_ + 2] * q2
+            y[128 * n + l + 64] = d * sc[8 * n + is_ + 4] * q3
+            y[128 * n + l + 96] = d * sc[8 * n + is_ + 6] * q4
+    return y
+
+
+@pytest.mark.parametrize("t,scalar,bs", [(gguf.Q4_K, scalar_q4_k, 144),
+                                          (gguf.Q6_K, scalar_q6_k, 210)])
+def test_vectorised_decoders_match_scalar_on_random_bytes(t, scalar, bs):
+    rng = np.random.default_rng(7)
+    raw = rng.integers(0, 256, (3, 2 * bs), dtype=np.uint8)
+    # sane f16 scales (random bytes can be inf/nan)
+    for r in range(3):
+        for b in range(2):
+            off = b * bs + (0 if t == gguf.Q4_K else 208)
+            vals = np.array([0.01, 0.003] if t == gguf.Q4_K else [0.02], np.float16)
+            raw[r, off:off + vals.nbytes] = vals.view(np.uint8)
+    v = quants.dequantize(raw, t)
+    for r in range(3):
+        for b in range(2):
+            ref = scalar(raw[r, b * bs:(b + 1) * bs].tobytes())
+            np.testing.assert_allclose(v[r, b * 256:(b + 1) * 256], ref, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("t,tol", [(gguf.Q4_K, 0.09), (gguf.Q6_K, 0.02), (gguf.Q8_0, 0.01)])
+def test_quantisers_round_trip(t, tol):
+    rng = np.random.default_rng(1)
+    w = rng.standard_normal((8, 512)).astype(np.float32)
+    back = quants.dequantize(quants.quantize(w, t), t)
+    rel = np.linalg.norm(back - w) / np.linalg.norm(w)
+    assert rel < tol, rel
+
+
+def test_gguf_write_read_round_trip(tmp_path):
+    p = str(tmp_path / "x.gguf")
+    w = quants.quant_q4_k(np.random.default_rng(0).standard_normal((4, 256)).astype(np.float32))
+    md = {"general.architecture": "qwen2", "a.f": 1.5, "a.s": "héllo", "a.b": True,
+          "a.arr": ["x", "y z"], "a.ints": np.array([1, -2, 3], np.int32), "a.neg": -7}
+    gguf.write_gguf(p, md, [("w", (256, 4), gguf.Q4_K, w),
+                            ("v", (5,), gguf.F32, np.arange(5, dtype=np.float32)),
+                            ("h", (2, 3), gguf.F16, np.ones((3, 2), np.float16))])
+    with gguf.GGUFFile(p) as g:
+        assert g.version == 3
+        assert g.metadata["a.s"] == "héllo" and g.metadata["a.b"] is True
+        assert g.metadata["a.arr"] == ["x", "y z"] and g.metadata["a.neg"] == -7
+        assert list(g.metadata["a.ints"]) == [1, -2, 3]
+        assert abs(g.metadata["a.f"] - 1.5) < 1e-6
+        assert np.array_equal(g.raw("w"), w)
+        assert np.array_equal(g.tensor("v"), np.arange(5, dtype=np.float32))
+        assert g.tensor("h").shape == (3, 2)
+        assert g.data_offset % 32 == 0
+        s = gguf.summary(g)
+        assert s["types"] == {"Q4_K": 1, "F32": 1, "F16": 1}
+
+
+def test_gguf_rejects_bad_files(tmp_path):
+    p = tmp_path / "bad.gguf"
+    p.write_bytes(b"NOPE" + b"\0" * 40)
+    with pytest.raises(gguf.GGUFError):
+        gguf.GGUFFile(str(p))
+    good = str(tmp_path / "t.gguf")
+    gguf.write_gguf(good, {"k": 1}, [("v", (64,), gguf.F32, np.zeros(64, np.float32))])
+    data = open(good, "rb").read()
+    (tmp_path / "trunc.gguf").write_bytes(data[:-100])
+    with pytest.raises(gguf.GGUFError):
+        gguf.GGUFFile(str(tmp_path / "trunc.gguf"))
+
+
+def test_config_round_trip_and_q4km_layers():
+    c = tiny(layers=3)
+    assert from_gguf(dict(to_gguf_metadata(c), **{"tokenizer.ggml.tokens": ["a"] * c.vocab})) \
+        .dim == c.dim
+    from k8s_nvidia_gpus_amd.models.llm import QWEN25_7B
+
+    assert QWEN25_7B.head_dim == 128 and QWEN25_7B.group == 7
+    assert 7.0e9 < QWEN25_7B.params() < 8.0e9
+    more = [i for i in range(28) if use_more_bits(i, 28)]
+    assert more[:3] == [0, 1, 2] and 27 in more and len(more) == 14
+
+
+@pytest.fixture(scope="module")
+def tiny_model(tmp_path_factory):
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load, write_synthetic_gguf
+
+    p = str(tmp_path_factory.mktemp("llm") / "tiny.gguf")
+    write_synthetic_gguf(p, tiny())
+    return p
+
+
+def test_tokenizer_round_trip_and_specials(tiny_model):
+    from k8s_nvidia_gpus_amd.models.llm.tokenizer import Tokenizer, chatml
+
+    with gguf.GGUFFile(tiny_model) as g:
+        tok = Tokenizer.from_gguf(g.metadata)
+    for s in ["hello world", "The quick brown fox!\n  indented\ttab", "naïve café 東京 🙂"]:
+        assert tok.decode(tok.encode(s)) == s
+    text = chatml([{"role": "user", "content": "hi"}])
+    ids = tok.encode(text)
+    assert ids.count(tok.token_id("<|im_start|>")) == 3        # system, user, assistant
+    assert tok.token_id("<|im_end|>") in tok.stop_ids()
+    assert text.endswith("<|im_start|>assistant\n")
+    assert "You are Qwen" in text
+    assert "You are Qwen" not in chatml([{"role": "system", "content": "x"},
+                                         {"role": "user", "content": "y"}])
+
+
+def test_engine_incremental_decode_equals_prefill(tiny_model):
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load
+
+    eng, tok = load(tiny_model, device="cpu", max_ctx=256)
+    ids = tok.encode("a cozy cabin in the woods, hello world")
+    full = eng.prefill(ids, slot=0)
+    eng.prefill(ids[:5], slot=1)
+    for i in range(5, len(ids)):
+        last = eng.decode([ids[i]], [i], [1])[0]
+    torch.testing.assert_close(full, last, rtol=1e-4, atol=1e-4)
+    # batched decode across slots equals per-slot decode
+    eng.prefill(ids[:3], slot=2)
+    b = eng.decode([ids[-1], ids[3]], [len(ids), 3], [0, 2])
+    eng2, _ = load(tiny_model, device="cpu", max_ctx=256)
+    eng2.prefill(ids, 0)
+    eng2.prefill(ids[:3], 2)
+    torch.testing.assert_close(b[0], eng2.decode([ids[-1]], [len(ids)], [0])[0])
+    torch.testing.assert_close(b[1], eng2.decode([ids[3]], [3], [2])[0])
+
+
+def test_prefill_rejects_overflow(tiny_model):
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load
+
+    eng, _ = load(tiny_model, device="cpu", max_ctx=256)
+    with pytest.raises(ValueError):
+        eng.prefill(list(range(300)), 0)
+
+
+def test_sampling_modes():
+    from k8s_nvidia_gpus_amd.models.llm.engine import sample
+
+    lg = torch.tensor([0.0, 5.0, 1.0, 4.9])
+    assert sample(lg) == 1
+    g = torch.Generator().manual_seed(0)
+    draws = {sample(lg, 1.0, top_k=2, generator=g) for _ in range(50)}
+    assert draws <= {1, 3} and len(draws) == 2
+    g = torch.Generator().manual_seed(0)
+    assert {sample(lg, 1.0, top_p=0.3, generator=g) for _ in range(20)} == {1}
+
+
+# ----------------------------------------------------------------- server
+@pytest.fixture(scope="module")
+def client(tiny_model):
+    from fastapi.testclient import TestClient
+
+    from k8s_nvidia_gpus_amd.models.llm.server import Scheduler, create_app
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load
+
+    eng, tok = load(tiny_model, device="cpu", max_ctx=256, slots=4)
+    state = {"scheduler": None, "tok": tok, "model": "tiny"}
+    app = create_app(state)
+    c = TestClient(app)
+    assert c.get("/health").status_code == 503              # llama-server: 503 while loading
+    state["scheduler"] = Scheduler(eng, tok, parallel=4)
+    yield c, eng, tok, state
+    state["scheduler"].close()
+
+
+def test_server_health_models_tokenize(client):
+    c, eng, tok, _ = client
+    assert c.get("/health").json() == {"status": "ok"}
+    assert c.get("/v1/models").json()["data"][0]["id"] == "tiny"
+    ids = c.post("/tokenize", json={"content": "hello world"}).json()["tokens"]
+    assert ids == tok.encode("hello world")
+    assert c.post("/detokenize", json={"tokens": ids}).json()["content"] == "hello world"
+
+
+def test_server_completion_greedy_matches_engine(client, tiny_model):
+    from k8s_nvidia_gpus_amd.models.llm.engine import generate
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load
+
+    c, eng, tok, _ = client
+    r = c.post("/completion", json={"prompt": "the quick brown", "n_predict": 6,
+                                    "temperature": 0}).json()
+    assert r["tokens_predicted"] <= 6 and r["tokens_evaluated"] == len(tok.encode("the quick brown"))
+    assert set(r["timings"]) >= {"prompt_n", "predicted_n", "predicted_per_second"}
+    ref, _ = load(tiny_model, device="cpu", max_ctx=256)      # the server's engine is busy
+    out = generate(ref, tok.encode("the quick brown"), 6, eos=tok.stop_ids())["tokens"]
+    assert r["content"] == tok.decode(out)
+
+
+def test_server_openai_chat_and_stream(client):
+    c, eng, tok, _ = client
+    body = {"model": "x", "messages": [{"role": "user", "content": "hello"}], "max_tokens": 5,
+            "temperature": 0}
+    r = c.post("/v1/chat/completions", json=body).json()
+    assert r["object"] == "chat.completion"
+    assert r["choices"][0]["message"]["role"] == "assistant"
+    assert r["usage"]["completion_tokens"] <= 5
+    assert r["choices"][0]["finish_reason"] in ("stop", "length")
+    with c.stream("POST", "/v1/chat/completions", json=dict(body, stream=True)) as s:
+        lines = [ln for ln in s.iter_lines() if ln]
+    assert lines[-1] == "data: [DONE]"
+    chunks = [json.loads(ln[6:]) for ln in lines[:-1]]
+    text = "".join(ch["choices"][0]["delta"].get("content", "") for ch in chunks)
+    assert text == r["choices"][0]["message"]["content"]
+    assert chunks[-1]["choices"][0]["finish_reason"] == r["choices"][0]["finish_reason"]
+    r2 = c.post("/v1/completions", json={"prompt": "hello", "max_tokens": 3, "temperature": 0})
+    assert r2.json()["object"] == "text_completion"
+
+
+def test_server_stop_strings_and_errors(client):
+    c, eng, tok, _ = client
+    r = c.post("/completion", json={"prompt": "hello", "n_predict": 20, "temperature": 0}).json()
+    if len(r["content"]) > 2:
+        stop = r["content"][1:3]
+        r2 = c.post("/completion", json={"prompt": "hello", "n_predict": 20, "temperature": 0,
+                                         "stop": [stop]}).json()
+        assert stop not in r2["content"] and r["content"].startswith(r2["content"])
+    assert c.post("/completion", json={"prompt": "x " * 400, "n_predict": 4}).status_code == 400
+    assert c.post("/v1/chat/completions", json={"messages": []}).status_code == 400
+
+
+def test_server_concurrent_requests_are_batched(client):
+    """8 concurrent greedy requests over 4 slots: every answer equals its sequential answer and
+    the scheduler ran multi-sequence decode steps."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    c, eng, tok, state = client
+    prompts = [f"hello world {i}" for i in range(8)]
+    seq = [c.post("/completion", json={"prompt": p, "n_predict": 8, "temperature": 0}).json()
+           ["content"] for p in prompts]
+    steps0 = state["scheduler"].metrics["decode_steps_total"]
+    toks0 = state["scheduler"].metrics["tokens_predicted_total"]
+    with ThreadPoolExecutor(8) as ex:
+        par = list(ex.map(lambda p: c.post("/completion", json={
+            "prompt": p, "n_predict": 8, "temperature": 0}).json()["content"], prompts))
+    assert par == seq
+    m = state["scheduler"].metrics
+    assert m["tokens_predicted_total"] - toks0 > m["decode_steps_total"] - steps0  # T > 1 steps
+    assert "llamacpp_amdk8s_tokens_predicted_total" in c.get("/metrics").text
+
+
+def test_server_seeded_sampling_is_reproducible(client):
+    c, *_ = client
+    body = {"prompt": "a cozy cabin", "n_predict": 8, "temperature": 1.0, "seed": 42}
+    a = c.post("/completion", json=body).json()["content"]
+    b = c.post("/completion", json=body).json()["content"]
+    assert a == b

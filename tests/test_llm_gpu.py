@@ -83,7 +83,8 @@ def test_quantise_kernel_and_rmsnorm(dev, LK):
 @pytest.mark.parametrize("qt", ["Q4_K", "Q6_K"])
 @pytest.mark.parametrize("T", [1, 2, 3, 4])
 @pytest.mark.parametrize("mode", ["store", "resid", "pair"])
-def test_qgemv_vs_fp32(dev, LK, qt, T, mode):
+@pytest.mark.parametrize("cfg", [(0, 0, 0), (4, 1, 7), (8, 2, 6), (8, 4, 4)])
+def test_qgemv_vs_fp32(dev, LK, qt, T, mode, cfg):
     from k8s_nvidia_gpus_amd.models.llm import gguf
 
     t = getattr(gguf, qt)
@@ -99,13 +100,13 @@ def test_qgemv_vs_fp32(dev, LK, qt, T, mode):
     out = torch.randn(T, N + 5, device=dev)[:, :N]      # strided output rows (ldo = N + 5)
     before = out.clone()
     if mode == "store":
-        LK.qgemv(w0, x8, dx, sx, out, LK.STORE, bias=bias, rows_per_wg=7)
+        LK.qgemv(w0, x8, dx, sx, out, LK.STORE, bias=bias, waves=cfg[0], ks=cfg[1], rows_per_wg=cfg[2])
         ref = a0 + bias.cpu()
     elif mode == "resid":
-        LK.qgemv(w0, x8, dx, sx, out, LK.RESID, rows_per_wg=7)
+        LK.qgemv(w0, x8, dx, sx, out, LK.RESID, waves=cfg[0], ks=cfg[1], rows_per_wg=cfg[2])
         ref = before.cpu() + a0
     else:
-        LK.qgemv(w0, x8, dx, sx, out, LK.PAIR, w1=w1, rows_per_wg=7)
+        LK.qgemv(w0, x8, dx, sx, out, LK.PAIR, w1=w1, waves=cfg[0], ks=cfg[1], rows_per_wg=cfg[2])
         ref = torch.nn.functional.silu(a0) * a1
     torch.testing.assert_close(out.cpu(), ref, rtol=2e-4, atol=2e-4)
     # and against the unquantised activations (int8 activation error only)
@@ -138,7 +139,7 @@ def test_rope_kv_and_decode_attention(dev, LK, H, Hkv):
     kc = (torch.randn(slots, Hkv, max_ctx, 128, device=dev) * 0.5).half()
     vc = torch.randn(slots, Hkv, max_ctx, 128, device=dev).half()
     cos, sin = rope_tables(max_ctx, 128, 1.0e6, dev)
-    pos = torch.tensor([0, 255, 256, 700], dtype=torch.int32, device=dev)
+    pos = torch.tensor([0, 63, 64, 700], dtype=torch.int32, device=dev)
     slot = torch.tensor([2, 0, 1, 2], dtype=torch.int32, device=dev)
     T = 4
     qkv = torch.randn(T, (H + 2 * Hkv) * 128, device=dev)
@@ -156,7 +157,7 @@ def test_rope_kv_and_decode_attention(dev, LK, H, Hkv):
         kc0[s, :, p] = apply_rope(k, cos[p:p + 1], sin[p:p + 1])[:, 0].half()
         vc0[s, :, p] = v.half()
     assert torch.equal(kc, kc0) and torch.equal(vc, vc0)
-    nsplit = max_ctx // 256
+    nsplit = max_ctx // LK.attn_chunk()
     po = torch.empty(T, H, nsplit, 128, device=dev)
     pml = torch.empty(T, H, nsplit, 2, device=dev)
     x8 = torch.empty(T, H * 128, dtype=torch.int8, device=dev)

@@ -43,11 +43,16 @@ def heartbeat(period=30.0):
 
 
 def bench_gemv(eng: Engine, iters: int = 50) -> list:
+    """Achieved bandwidth of every decode GEMV shape, default decomposition and a sweep."""
     LK = eng.LK
     L = eng.w.layers[0]
+    Lq6 = eng.w.layers[1] if len(eng.w.layers) > 1 else L     # layer 1: Q6_K attn_v / ffn_down
     rows = []
     cases = [("qkv", L.wqkv[0], "store"), ("o_proj", L.wo, "resid"),
-             ("gate_up", L.wg, "pair"), ("down", L.wd, "resid"), ("lm_head", eng.w.output, "store")]
+             ("gate_up", L.wg, "pair"), ("down_q4k", L.wd, "resid"),
+             ("down_q6k", Lq6.wd, "resid"), ("lm_head", eng.w.output, "store")]
+    cfgs = [(0, 0, 0), (4, 1, 4), (4, 1, 8), (8, 1, 8), (8, 1, 16), (8, 2, 4), (8, 2, 8),
+            (8, 4, 2), (8, 4, 4), (4, 2, 2), (4, 4, 1)]
     for name, w, mode in cases:
         for T in (1, 4):
             x8 = torch.randint(-127, 127, (T, w.k), dtype=torch.int8, device=eng.device)
@@ -55,20 +60,24 @@ def bench_gemv(eng: Engine, iters: int = 50) -> list:
             sx = torch.zeros(T, w.k // 16, device=eng.device)
             out = torch.zeros(T, w.n, device=eng.device)
             m = {"store": LK.STORE, "resid": LK.RESID, "pair": LK.PAIR}[mode]
-            kw = dict(w1=L.wu if mode == "pair" else None, rows_per_wg=eng._rpw(w.n))
-            for _ in range(5):
-                LK.qgemv(w, x8, dx, sx, out, m, **kw)
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
-            e0.record()
-            for _ in range(iters):
-                LK.qgemv(w, x8, dx, sx, out, m, **kw)
-            e1.record()
-            torch.cuda.synchronize()
-            us = e0.elapsed_time(e1) / iters * 1e3
-            nbytes = w.nbytes() * (2 if mode == "pair" else 1)
-            rows.append({"gemv": name, "T": T, "N": w.n, "K": w.k, "type": ["Q4_K", "Q6_K"][w.qtype],
-                         "us": round(us, 2), "GBps": round(nbytes / us / 1e3, 1)})
+            for waves, ks, rpw in (cfgs if T == 1 else cfgs[:1]):
+                kw = dict(w1=L.wu if mode == "pair" else None, waves=waves, ks=ks,
+                          rows_per_wg=rpw)
+                for _ in range(3):
+                    LK.qgemv(w, x8, dx, sx, out, m, **kw)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+                e0.record()
+                for _ in range(iters):
+                    LK.qgemv(w, x8, dx, sx, out, m, **kw)
+                e1.record()
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) / iters * 1e3
+                nbytes = w.nbytes() * (2 if mode == "pair" else 1)
+                r = {"gemv": name, "T": T, "N": w.n, "K": w.k, "type": ["Q4_K", "Q6_K"][w.qtype],
+                     "cfg": [waves, ks, rpw], "us": round(us, 2),
+                     "GBps": round(nbytes / us / 1e3, 1)}
+                rows.append(r)
     return rows
 
 
