@@ -92,9 +92,9 @@ class Engine:
         self.dense = self.gpu if dense is None else dense
         self._dense_w: Optional[Dict[str, torch.Tensor]] = None
         self._bufs: Dict[int, StepBuffers] = {}
-        # GEMV decomposition override "waves,ks,rows" (sweeps); default: the kernel's per-shape
-        self.gemv_cfg = dict(zip(("waves", "ks", "rows_per_wg"),
-                                 map(int, os.environ.get("AMDK8S_LLM_GEMV", "0,0,0").split(","))))
+        # GEMV decomposition override "waves,rows" (sweeps); default: the kernel's own
+        self.gemv_cfg = dict(zip(("waves", "rows_per_wg"),
+                                 map(int, os.environ.get("AMDK8S_LLM_GEMV", "0,0").split(","))))
         if self.gpu:
             from k8s_nvidia_gpus_amd.ops import llm_kernels as LK
 
@@ -203,27 +203,26 @@ class Engine:
         LK, c = self.LK, self.cfg
         LK.dequant(self.w.tok_embd, b.h, rows=b.tok)          # embedding rows → residual
         qd = self._q8(b, c.dim)
-        qf = self._q8(b, c.ffn)
         scale = 1.0 / math.sqrt(c.head_dim)
+        G = self.gemv_cfg
         for i, L in enumerate(self.w.layers):
-            LK.rmsnorm_q8(b.h, L.attn_norm, c.eps, *qd)
+            # RMSNorm + Q8 quantisation run in each GEMV's prologue (fp32 input + norm weight)
             off = 0
             for w in L.wqkv:
-                LK.qgemv(w, *qd, b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:],
-                         ldo=b.qkv.stride(0), **self.gemv_cfg)
+                LK.qgemv(w, None, None, None, b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:],
+                         ldo=b.qkv.stride(0), xf=b.h, norm_w=L.attn_norm, eps=c.eps, **G)
                 off += w.n
             LK.rope_kv(b.qkv, b.pos, b.slot, self.cos, self.sin, c.heads, c.kv_heads, c.head_dim,
                        self.max_ctx, b.qrot, self.k_cache[i], self.v_cache[i])
             LK.attn_decode(b.qrot, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
                            c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
                            span=span)
-            LK.qgemv(L.wo, *qd, b.h, LK.RESID, **self.gemv_cfg)
-            LK.rmsnorm_q8(b.h, L.ffn_norm, c.eps, *qd)
-            LK.qgemv(L.wg, *qd, b.t, LK.PAIR, w1=L.wu, **self.gemv_cfg)
-            LK.rmsnorm_q8(b.t, None, 0.0, *qf)
-            LK.qgemv(L.wd, *qf, b.h, LK.RESID, **self.gemv_cfg)
-        LK.rmsnorm_q8(b.h, self.w.out_norm, c.eps, *qd)
-        LK.qgemv(self.w.output, *qd, b.logits, LK.STORE, **self.gemv_cfg)
+            LK.qgemv(L.wo, *qd, b.h, LK.RESID, **G)
+            LK.qgemv(L.wg, None, None, None, b.t, LK.PAIR, w1=L.wu, xf=b.h, norm_w=L.ffn_norm,
+                     eps=c.eps, **G)
+            LK.qgemv(L.wd, None, None, None, b.h, LK.RESID, xf=b.t, **G)
+        LK.qgemv(self.w.output, None, None, None, b.logits, LK.STORE, xf=b.h,
+                 norm_w=self.w.out_norm, eps=c.eps, **G)
 
     def _decode_native(self, tokens: Sequence[int], positions: Sequence[int],
                        slots: Sequence[int]) -> torch.Tensor:

@@ -4,9 +4,9 @@ Decoding streams every weight once per token, so the engine keeps the file's 4/6
 (~4.4 GB for Qwen2.5-7B Q4_K_M) and reads them with the GEMV kernels; with 288 GB per MI355X it
 can also keep an fp16 copy for compute-bound prompt processing (``dense=True``, +15 GB).
 
-* ``QWeight`` — one [N, K] matrix: Q4_K rows as stored in the GGUF (144-byte blocks, 16-byte
-  aligned); Q6_K repacked on the GPU into four aligned planes (ql / qh / scales / d).  On the CPU
-  (tests, no GPU) it holds the raw rows and dequantises with the numpy codecs.
+* ``QWeight`` — one [N, K] matrix repacked on the GPU into aligned planes (Q4_K: nibbles + 16-byte
+  block headers; Q6_K: ql / qh / scales / d) — same bytes as the file.  On the CPU (tests, no GPU)
+  it holds the raw GGUF rows and dequantises with the numpy codecs.
 * ``ModelWeights.from_gguf`` — tensor names of llama.cpp's qwen2 GGUF layout
   (``token_embd``, ``blk.N.attn_q`` …, ``output``); matrices of other types (F16/F32/Q8_0) are
   re-encoded to Q6_K at load.
@@ -69,11 +69,14 @@ class QWeight:
         per, size = gguf.BLOCK[ggml_type]
         n = t.shape[0]
         k = t.shape[1] // size * per
-        if ggml_type == gguf.Q4_K:
-            return cls(0, n, k, t.contiguous())
         from k8s_nvidia_gpus_amd.ops import llm_kernels as LK
 
         nb = k // 256
+        if ggml_type == gguf.Q4_K:
+            qs = torch.empty((n, nb * 128), dtype=torch.uint8, device=t.device)
+            hdr = torch.empty((n, nb * 16), dtype=torch.int8, device=t.device)
+            LK.q4k_repack(t.contiguous(), qs, hdr)
+            return cls(0, n, k, qs, sc=hdr)
         ql = torch.empty((n, nb * 128), dtype=torch.uint8, device=t.device)
         qh = torch.empty((n, nb * 64), dtype=torch.uint8, device=t.device)
         sc = torch.empty((n, nb * 16), dtype=torch.int8, device=t.device)

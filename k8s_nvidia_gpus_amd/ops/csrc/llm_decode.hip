@@ -11,9 +11,12 @@
 //   then v_dot4_i32_i8 on nibbles masked straight out of the weight words: ~0.5 VALU op per
 //   weight, so the streaming load, not the ALU, is the bound.
 // * One wavefront walks one weight row: 8 lanes x 16 B cover a 256-weight super-block, so each
-//   wave-wide 16-byte load reads 8 consecutive super-blocks (1 KiB of quants) fully coalesced.
-//   Q4_K rows keep the GGUF block layout (144 B, 16-byte aligned); Q6_K (210 B, unaligned) is
-//   repacked at load time into four planes (ql / qh / scales / d) so every load is aligned.
+//   wave-wide 16-byte load reads 8 consecutive super-blocks (1 KiB of quants) fully coalesced; a
+//   wave's rows run as one software pipeline (next stage's loads in flight during this stage's
+//   maths).
+//   Both formats are repacked at load time into planes (Q4_K: nibbles + 16-byte block headers;
+//   Q6_K: ql / qh / scales / d) so every load is aligned and a wave's header load covers 8
+//   consecutive blocks in one 128-byte line.
 // * The activations of the (<= 4) tokens are staged once per workgroup in LDS (x8 padded 32 B per
 //   256 so the 16-lane groups of a ds_read_b128 hit disjoint banks); every wave of the workgroup
 //   then streams its rows against them.
@@ -70,27 +73,38 @@ __device__ __forceinline__ float wave_max(float v) {
 // LDS offset of activation byte p of one token (32-byte pad per 256 bytes)
 __device__ __forceinline__ int xoff(int p) { return (p >> 8) * 288 + (p & 255); }
 
-struct QMat {            // one quantised weight matrix [N, K]
-  const uint8_t* q;      // Q4_K: rows of nb*144 B;  Q6_K: ql plane [N][nb][128]
-  const uint8_t* qh;     // Q6_K: [N][nb][64]
-  const int8_t* sc;      // Q6_K: [N][nb][16]
+struct QMat {            // one quantised weight matrix [N, K], repacked at load into aligned planes
+  const uint8_t* q;      // Q4_K: nibbles [N][nb][128];  Q6_K: low bits [N][nb][128]
+  const uint8_t* qh;     // Q6_K: high bits [N][nb][64]
+  const int8_t* sc;      // Q4_K: block headers [N][nb][16] (d, dmin, scales);  Q6_K: scales [N][nb][16]
   const uint16_t* d;     // Q6_K: [N][nb]
 };
 
 struct GemvArgs {
   QMat w0, w1;           // w1: ffn_up in pair mode
-  const int8_t* x8;      // [T][K]
-  const float* dx;       // [T][K/32]
-  const float* sx;       // [T][K/16]  (dx * sum of the 16 int8 values)
+  const int8_t* x8;      // Q8 input: [T][K]
+  const float* dx;       //           [T][K/32]
+  const float* sx;       //           [T][K/16]  (dx * sum of the 16 int8 values)
+  const float* xf;       // fp32 input [T][ldx] (quantised in the prologue) — instead of x8/dx/sx
+  const float* norm_w;   //   optional RMSNorm weight [K] applied first
+  float eps;
+  int ldx;
   const float* bias;     // [N] or null (store mode)
   float* out;            // [T][ldo]
   int ldo, N, K, T;
-  int ks;                // waves per row (split-K inside the workgroup): 1, 2, 4
-  int rows_per_wg;       // multiple of (waves per workgroup / ks)
+  int rows_per_wg;
 };
 
-// One lane's share of a 256-weight super-block: Q4_K = header + 16 B of nibbles; Q6_K = 16 B of
-// low bits + 16 B of high bits + the 16 scales + d.
+// Weights are streamed exactly once per step: non-temporal loads keep them from evicting the
+// activations and KV cache from L2 / the Infinity Cache.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ldnt(const void* p) {
+  const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// One lane's share of a 256-weight super-block: Q4_K = the block header (d, dmin, 12 scale bytes)
+// + 16 B of nibbles; Q6_K = 16 B of low bits + 16 B of high bits + the 16 scales + d.
 template <int TYPE> struct Blk;
 template <> struct Blk<kQ4K> { uint4 h, q; };
 template <> struct Blk<kQ6K> { uint4 l, hb, s; uint32_t d; };
@@ -99,15 +113,15 @@ template <int TYPE>
 __device__ __forceinline__ void load_blk(const QMat& w, long rowblk, int blk, int sub,
                                          Blk<TYPE>& r) {
   if constexpr (TYPE == kQ4K) {
-    const uint8_t* b = w.q + (rowblk + blk) * kQ4KBytes;
-    r.h = *reinterpret_cast<const uint4*>(b);
-    r.q = *reinterpret_cast<const uint4*>(b + 16 + sub * 16);
+    const long rb = rowblk + blk;
+    r.h = ldnt(w.sc + rb * 16);                                 // header plane: 8 blocks = 128 B
+    r.q = ldnt(w.q + rb * 128 + sub * 16);
   } else {
     const long rb = rowblk + blk;
-    r.l = *reinterpret_cast<const uint4*>(w.q + rb * 128 + sub * 16);
-    r.hb = *reinterpret_cast<const uint4*>(w.qh + rb * 64 + (sub >> 2) * 32 + (sub & 1) * 16);
-    r.s = *reinterpret_cast<const uint4*>(w.sc + rb * 16);
-    r.d = w.d[rb];
+    r.l = ldnt(w.q + rb * 128 + sub * 16);
+    r.hb = ldnt(w.qh + rb * 64 + (sub >> 2) * 32 + (sub & 1) * 16);
+    r.s = ldnt(w.sc + rb * 16);
+    r.d = __builtin_nontemporal_load(w.d + rb);
   }
 }
 
@@ -140,8 +154,10 @@ __device__ __forceinline__ void dot_blk(const Blk<TYPE>& r, int blk, int sub, co
     const uint32_t q[4] = {r.q.x, r.q.y, r.q.z, r.q.w};
     const int p_lo = blk * 256 + c * 64 + (sub & 1) * 16;
     const int g_lo = p_lo >> 4, d_lo = p_lo >> 5;
-    const float dsc0 = d * (float)sc0, dsc1 = d * (float)sc1;
-    const float dm0 = dmin * (float)m0, dm1 = dmin * (float)m1;
+    // explicit roundings: the same instruction sequence for every T instantiation, so a token's
+    // result does not depend on how many sequences share the step (batch-invariant decode)
+    const float dsc0 = __fmul_rn(d, (float)sc0), dsc1 = __fmul_rn(d, (float)sc1);
+    const float dm0 = __fmul_rn(dmin, (float)m0), dm1 = __fmul_rn(dmin, (float)m1);
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       const uint4 xl = *reinterpret_cast<const uint4*>(x.xs + t * x.xstride + xoff(p_lo));
@@ -157,15 +173,18 @@ __device__ __forceinline__ void dot_blk(const Blk<TYPE>& r, int blk, int sub, co
       ih = dot4((q[3] >> 4) & 0x0f0f0f0fu, xh.w, ih);
       const float2 dxv = *reinterpret_cast<const float2*>(x.dxs + t * x.dstride + d_lo);
       const float sxl = x.sxs[t * x.sstride + g_lo], sxh = x.sxs[t * x.sstride + g_lo + 2];
-      acc[t] += dsc0 * dxv.x * (float)il + dsc1 * dxv.y * (float)ih - dm0 * sxl - dm1 * sxh;
+      float a = __fmaf_rn(__fmul_rn(dsc0, dxv.x), (float)il, acc[t]);
+      a = __fmaf_rn(__fmul_rn(dsc1, dxv.y), (float)ih, a);
+      a = __fmaf_rn(-dm0, sxl, a);
+      acc[t] = __fmaf_rn(-dm1, sxh, a);
     }
   } else {
     const int n = sub >> 2, h1 = sub & 1, klo = (sub & 3) >> 1;
     const float d = h2f(r.d & 0xffffu);
     const uint32_t scw[4] = {r.s.x, r.s.y, r.s.z, r.s.w};
     const int i0 = 8 * n + h1 + 2 * klo, i1 = i0 + 4;
-    const float sc0 = d * (float)(int8_t)((scw[i0 >> 2] >> ((i0 & 3) * 8)) & 0xffu);
-    const float sc1 = d * (float)(int8_t)((scw[i1 >> 2] >> ((i1 & 3) * 8)) & 0xffu);
+    const float sc0 = __fmul_rn(d, (float)(int8_t)((scw[i0 >> 2] >> ((i0 & 3) * 8)) & 0xffu));
+    const float sc1 = __fmul_rn(d, (float)(int8_t)((scw[i1 >> 2] >> ((i1 & 3) * 8)) & 0xffu));
     const uint32_t l[4] = {r.l.x, r.l.y, r.l.z, r.l.w};
     const uint32_t hb[4] = {r.hb.x, r.hb.y, r.hb.z, r.hb.w};
     const int sh = 2 * klo;
@@ -188,133 +207,193 @@ __device__ __forceinline__ void dot_blk(const Blk<TYPE>& r, int blk, int sub, co
       ih = dot4(qhi[2], xh.z, ih); ih = dot4(qhi[3], xh.w, ih);
       const float dxl = x.dxs[t * x.dstride + d_lo], dxh = x.dxs[t * x.dstride + d_lo + 2];
       const float sxl = x.sxs[t * x.sstride + g_lo], sxh = x.sxs[t * x.sstride + g_lo + 4];
-      acc[t] += sc0 * (dxl * (float)il - 32.f * sxl) + sc1 * (dxh * (float)ih - 32.f * sxh);
+      const float u0 = __fmaf_rn(dxl, (float)il, __fmul_rn(-32.f, sxl));
+      const float u1 = __fmaf_rn(dxh, (float)ih, __fmul_rn(-32.f, sxh));
+      acc[t] = __fmaf_rn(sc1, u1, __fmaf_rn(sc0, u0, acc[t]));
     }
   }
 }
 
-// Blocks in flight per lane per batch (all loads of a batch are issued before any is used).
+// Blocks per lane per pipeline stage (one stage = 8*U super-blocks of a row).
 template <int TYPE, int MODE>
 constexpr int kBatch = TYPE == kQ4K ? (MODE == kPair ? 2 : 4) : (MODE == kPair ? 1 : 2);
 
-// Workgroup = W waves (blockDim/64); ks waves share one row (each walks 1/ks of the super-blocks,
-// partial sums meet in LDS); W/ks rows per workgroup iteration; rows_per_wg rows per workgroup.
-// The first batch of weight loads is issued before the activations are staged, so the staging
-// (L2 → LDS → barrier) overlaps the first HBM round trip.
+template <int TYPE, int MODE, int U>
+__device__ __forceinline__ void load_stage(const GemvArgs& a, int row, int b0, int nb, int sub,
+                                           int bl, Blk<TYPE> (&c)[U], Blk<TYPE> (&c1)[U]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int blk = min(b0 + 8 * u + bl, nb - 1);  // unconditional (see attention): clamped
+    load_blk<TYPE>(a.w0, (long)row * nb, blk, sub, c[u]);
+    if constexpr (MODE == kPair) load_blk<TYPE>(a.w1, (long)row * nb, blk, sub, c1[u]);
+  }
+}
+
+template <int TYPE, int T, int MODE, int U>
+__device__ __forceinline__ void compute_stage(int b0, int nb, int sub, int bl, const XView& xv,
+                                              const Blk<TYPE> (&c)[U], const Blk<TYPE> (&c1)[U],
+                                              float (&acc)[T], float (&acc1)[T]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int blk = b0 + 8 * u + bl;
+    if (blk < nb) {
+      dot_blk<TYPE, T>(c[u], blk, sub, xv, acc);
+      if constexpr (MODE == kPair) dot_blk<TYPE, T>(c1[u], blk, sub, xv, acc1);
+    }
+  }
+}
+
+template <int T, int MODE>
+__device__ __forceinline__ void finish_row(const GemvArgs& a, int row, int lane, float (&acc)[T],
+                                           float (&acc1)[T]) {
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    acc[t] = wave_sum(acc[t]);
+    if constexpr (MODE == kPair) acc1[t] = wave_sum(acc1[t]);
+  }
+  if (lane < T) {
+    float v = 0.f, v1 = 0.f;
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+      if (t == lane) { v = acc[t]; v1 = acc1[t]; }
+    float* o = a.out + (long)lane * a.ldo + row;
+    if constexpr (MODE == kStore) *o = v + (a.bias ? a.bias[row] : 0.f);
+    else if constexpr (MODE == kResid) *o += v;
+    else *o = v / (1.f + __expf(-v)) * v1;
+  }
+#pragma unroll
+  for (int t = 0; t < T; ++t) acc[t] = acc1[t] = 0.f;
+}
+
+// Workgroup = W waves (blockDim/64) over rows_per_wg rows; wave w takes rows w, w+W, ...  Each
+// wave walks its (row, stage) items as one flat software pipeline with two register sets: the
+// loads of item i+1 are in flight while item i is computed, across row boundaries, so a wave
+// always has a stage of weights on the way.  Item 0's loads are issued before the activations
+// are staged, so the staging (L2 → LDS → barrier) overlaps the first HBM round trip.
 template <int TYPE, int T, int MODE>
 __global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
   constexpr int U = kBatch<TYPE, MODE>;
   extern __shared__ __align__(16) uint8_t lds[];
   const int K = a.K, nb = K >> 8;
-  const int W = blockDim.x >> 6, KS = a.ks, rpi = W / KS;
+  const int W = blockDim.x >> 6;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int sub = lane & 7, bl = lane >> 3;
-  const int kp = wave % KS, rw = wave / KS;
-  const int nbk = (nb + KS - 1) / KS;
-  const int kb0 = kp * nbk, kb1 = min(nb, kb0 + nbk);
-  const int r0 = blockIdx.x * a.rows_per_wg;
-  const int r1 = min(a.N, r0 + a.rows_per_wg);
+  const int nst = (nb + 8 * U - 1) / (8 * U);       // pipeline stages per row
+  const int r0 = blockIdx.x * a.rows_per_wg + wave;
+  const int r1 = min(a.N, blockIdx.x * a.rows_per_wg + a.rows_per_wg);
+  const int nrows = r0 < r1 ? (r1 - r0 + W - 1) / W : 0;
+  const int items = nrows * nst;
 
-  Blk<TYPE> pre[U], pre1[U];
-  {
-    const int row = r0 + rw;
-    if (row < r1) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int blk = kb0 + 8 * u + bl;
-        if (blk < kb1) {
-          load_blk<TYPE>(a.w0, (long)row * nb, blk, sub, pre[u]);
-          if constexpr (MODE == kPair) load_blk<TYPE>(a.w1, (long)row * nb, blk, sub, pre1[u]);
-        }
-      }
-    }
-  }
+  Blk<TYPE> A[U], A1[U], B[U], B1[U];
+  if (items > 0) load_stage<TYPE, MODE, U>(a, r0, 0, nb, sub, bl, A, A1);
+
   const int xstride = nb * 288;                      // padded bytes per token
   int8_t* xs = reinterpret_cast<int8_t*>(lds);
   float* dxs = reinterpret_cast<float*>(lds + T * xstride);
   float* sxs = dxs + T * (K >> 5);
-  float* red = sxs + T * (K >> 4);                   // [W][T][2]
-  for (int i = threadIdx.x; i < T * (K >> 4); i += blockDim.x) {
-    const int t = i / (K >> 4), p = (i - t * (K >> 4)) << 4;
-    *reinterpret_cast<uint4*>(xs + t * xstride + xoff(p)) =
-        *reinterpret_cast<const uint4*>(a.x8 + (long)t * K + p);
+  float* red = sxs + T * (K >> 4);                   // [W] block-reduction scratch
+  if (a.xf == nullptr) {                             // Q8 input: copy into LDS
+    for (int i = threadIdx.x; i < T * (K >> 4); i += blockDim.x) {
+      const int t = i / (K >> 4), p = (i - t * (K >> 4)) << 4;
+      *reinterpret_cast<uint4*>(xs + t * xstride + xoff(p)) =
+          *reinterpret_cast<const uint4*>(a.x8 + (long)t * K + p);
+    }
+    for (int i = threadIdx.x; i < T * (K >> 5); i += blockDim.x) dxs[i] = a.dx[i];
+    for (int i = threadIdx.x; i < T * (K >> 4); i += blockDim.x) sxs[i] = a.sx[i];
+  } else {
+    // fp32 input (+ RMSNorm): every workgroup normalises and quantises the (L2-resident) rows
+    // itself, which removes a launch and its boundary per matrix.  Per token the thread mapping
+    // does not depend on T, so results are batch-invariant.
+    for (int t = 0; t < T; ++t) {
+      const float* xr = a.xf + (long)t * a.ldx;
+      float rs = 1.f;
+      if (a.norm_w) {
+        float ss = 0.f;
+        for (int i0 = threadIdx.x * 4; i0 < K; i0 += blockDim.x * 16) {
+          float4 v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            v[u] = *reinterpret_cast<const float4*>(xr + min(i0 + u * (int)blockDim.x * 4, K - 4));
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (i0 + u * (int)blockDim.x * 4 < K)
+              ss += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
+        }
+        ss = wave_sum(ss);
+        if (lane == 0) red[wave] = ss;
+        __syncthreads();
+        ss = 0.f;
+        for (int w = 0; w < W; ++w) ss += red[w];
+        __syncthreads();
+        rs = rsqrtf(ss / (float)K + a.eps);
+      }
+      // chunk c = 8 values; 4 consecutive chunks (one lane quad) = one 32-value block
+      for (int c0 = threadIdx.x; c0 < (K >> 3); c0 += blockDim.x * 2) {
+        float v[2][8];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int c = min(c0 + u * (int)blockDim.x, (K >> 3) - 1);
+          const float4 x0 = *reinterpret_cast<const float4*>(xr + c * 8);
+          const float4 x1 = *reinterpret_cast<const float4*>(xr + c * 8 + 4);
+          v[u][0] = x0.x; v[u][1] = x0.y; v[u][2] = x0.z; v[u][3] = x0.w;
+          v[u][4] = x1.x; v[u][5] = x1.y; v[u][6] = x1.z; v[u][7] = x1.w;
+          if (a.norm_w) {
+            const float4 w0 = *reinterpret_cast<const float4*>(a.norm_w + c * 8);
+            const float4 w1 = *reinterpret_cast<const float4*>(a.norm_w + c * 8 + 4);
+            const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[u][i] *= rs * wv[i];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int c = c0 + u * (int)blockDim.x;
+          if (c >= (K >> 3)) break;                 // whole quads leave together (K % 256 == 0)
+          float amax = 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[u][i]));
+          amax = fmaxf(amax, __shfl_xor(amax, 1, kWave));
+          amax = fmaxf(amax, __shfl_xor(amax, 2, kWave));
+          const float d = amax / 127.f;
+          const float id = d > 0.f ? 1.f / d : 0.f;
+          uint32_t pk0 = 0u, pk1 = 0u;
+          int sq = 0;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int q = (int)__builtin_rintf(v[u][i] * id);
+            if (i < 4) pk0 |= ((uint32_t)(q & 0xff)) << (8 * i);
+            else pk1 |= ((uint32_t)(q & 0xff)) << (8 * (i - 4));
+            sq += q;
+          }
+          sq += __shfl_xor(sq, 1, kWave);
+          *reinterpret_cast<uint2*>(xs + t * xstride + xoff(c * 8)) = make_uint2(pk0, pk1);
+          if ((c & 3) == 0) dxs[t * (K >> 5) + (c >> 2)] = d;
+          if ((c & 1) == 0) sxs[t * (K >> 4) + (c >> 1)] = d * (float)sq;
+        }
+      }
+    }
   }
-  for (int i = threadIdx.x; i < T * (K >> 5); i += blockDim.x) dxs[i] = a.dx[i];
-  for (int i = threadIdx.x; i < T * (K >> 4); i += blockDim.x) sxs[i] = a.sx[i];
   __syncthreads();
   const XView xv = {xs, dxs, sxs, xstride, K >> 5, K >> 4};
 
-  for (int rb = r0; rb < r1; rb += rpi) {
-    const int row = rb + rw;
-    const bool valid = row < r1;
-    float acc[T], acc1[T];
+  float acc[T], acc1[T];
 #pragma unroll
-    for (int t = 0; t < T; ++t) acc[t] = acc1[t] = 0.f;
-    if (valid) {
-      const long rowblk = (long)row * nb;
-      for (int b0 = kb0; b0 < kb1; b0 += 8 * U) {
-        Blk<TYPE> cur[U], cur1[U];
-        if (rb == r0 && b0 == kb0) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) { cur[u] = pre[u]; cur1[u] = pre1[u]; }
-        } else {
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int blk = b0 + 8 * u + bl;
-            if (blk < kb1) {
-              load_blk<TYPE>(a.w0, rowblk, blk, sub, cur[u]);
-              if constexpr (MODE == kPair) load_blk<TYPE>(a.w1, rowblk, blk, sub, cur1[u]);
-            }
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int blk = b0 + 8 * u + bl;
-          if (blk < kb1) {
-            dot_blk<TYPE, T>(cur[u], blk, sub, xv, acc);
-            if constexpr (MODE == kPair) dot_blk<TYPE, T>(cur1[u], blk, sub, xv, acc1);
-          }
-        }
-      }
+  for (int t = 0; t < T; ++t) acc[t] = acc1[t] = 0.f;
+  for (int it = 0; it < items; it += 2) {
+    if (it + 1 < items) {
+      const int j = it + 1;
+      load_stage<TYPE, MODE, U>(a, r0 + (j / nst) * W, (j % nst) * 8 * U, nb, sub, bl, B, B1);
     }
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      acc[t] = wave_sum(acc[t]);
-      if constexpr (MODE == kPair) acc1[t] = wave_sum(acc1[t]);
+    compute_stage<TYPE, T, MODE, U>((it % nst) * 8 * U, nb, sub, bl, xv, A, A1, acc, acc1);
+    if (it % nst == nst - 1) finish_row<T, MODE>(a, r0 + (it / nst) * W, lane, acc, acc1);
+    if (it + 1 >= items) break;
+    if (it + 2 < items) {
+      const int j = it + 2;
+      load_stage<TYPE, MODE, U>(a, r0 + (j / nst) * W, (j % nst) * 8 * U, nb, sub, bl, A, A1);
     }
-    if (KS > 1) {
-      if (lane == 0) {
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-          red[(wave * T + t) * 2] = acc[t];
-          red[(wave * T + t) * 2 + 1] = acc1[t];
-        }
-      }
-      __syncthreads();
-      if (kp == 0) {
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-          float s = 0.f, s1 = 0.f;
-          for (int k = 0; k < KS; ++k) {
-            s += red[((wave + k) * T + t) * 2];
-            s1 += red[((wave + k) * T + t) * 2 + 1];
-          }
-          acc[t] = s;
-          acc1[t] = s1;
-        }
-      }
-      __syncthreads();
-    }
-    if (valid && kp == 0 && lane < T) {
-      float v = 0.f, v1 = 0.f;
-#pragma unroll
-      for (int t = 0; t < T; ++t)
-        if (t == lane) { v = acc[t]; v1 = acc1[t]; }
-      float* o = a.out + (long)lane * a.ldo + row;
-      if constexpr (MODE == kStore) *o = v + (a.bias ? a.bias[row] : 0.f);
-      else if constexpr (MODE == kResid) *o += v;
-      else *o = v / (1.f + __expf(-v)) * v1;
-    }
+    const int i1 = it + 1;
+    compute_stage<TYPE, T, MODE, U>((i1 % nst) * 8 * U, nb, sub, bl, xv, B, B1, acc, acc1);
+    if (i1 % nst == nst - 1) finish_row<T, MODE>(a, r0 + (i1 / nst) * W, lane, acc, acc1);
   }
 }
 
@@ -339,9 +418,15 @@ __global__ void __launch_bounds__(256) rmsnorm_q8_kernel(const float* __restrict
   float rs = 1.f;
   if (w) {
     float ss = 0.f;
-    for (int i = threadIdx.x * 4; i < K; i += blockDim.x * 4) {
-      const float4 v = *reinterpret_cast<const float4*>(xr + i);
-      ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    for (int i0 = threadIdx.x * 4; i0 < K; i0 += blockDim.x * 4 * 4) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)            // 4 loads in flight (clamped, masked below)
+        v[u] = *reinterpret_cast<const float4*>(xr + min(i0 + u * (int)blockDim.x * 4, K - 4));
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i0 + u * (int)blockDim.x * 4 < K)
+          ss += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
     }
     ss = wave_sum(ss);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
@@ -392,16 +477,16 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(const float* __restrict__ 
                                                       float* __restrict__ q_out,
                                                       uint16_t* __restrict__ kc,
                                                       uint16_t* __restrict__ vc) {
-  const int t = blockIdx.x;
+  // grid (ceil(((H + Hkv) * 64 + Hkv * 64) / 256), T): one thread per rotated pair or V pair
+  const int t = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int p = pos[t], s = slot[t];
   const float* row = qkv + (long)t * ldq;
-  const float* ct = cos_t + (long)p * (kHeadDim / 2);
-  const float* st = sin_t + (long)p * (kHeadDim / 2);
   const int pairs = (H + Hkv) * (kHeadDim / 2);
-  for (int i = threadIdx.x; i < pairs; i += blockDim.x) {
+  if (i < pairs) {
     const int h = i / (kHeadDim / 2), j = i % (kHeadDim / 2);
     const float x0 = row[h * kHeadDim + j], x1 = row[h * kHeadDim + j + kHeadDim / 2];
-    const float c = ct[j], sn = st[j];
+    const float c = cos_t[(long)p * (kHeadDim / 2) + j], sn = sin_t[(long)p * (kHeadDim / 2) + j];
     const float y0 = x0 * c - x1 * sn, y1 = x0 * sn + x1 * c;
     if (h < H) {
       q_out[(long)t * H * kHeadDim + h * kHeadDim + j] = y0;
@@ -411,11 +496,12 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(const float* __restrict__ 
       kc[base + j] = f2h(y0);
       kc[base + j + kHeadDim / 2] = f2h(y1);
     }
-  }
-  const float* vrow = row + (H + Hkv) * kHeadDim;
-  for (int i = threadIdx.x; i < Hkv * kHeadDim; i += blockDim.x) {
-    const int h = i / kHeadDim, j = i % kHeadDim;
-    vc[(((long)s * Hkv + h) * max_ctx + p) * kHeadDim + j] = f2h(vrow[i]);
+  } else if (i < pairs + Hkv * (kHeadDim / 2)) {
+    const int e = (i - pairs) * 2;                 // V: two values per thread
+    const int h = e / kHeadDim, j = e % kHeadDim;
+    const float2 v = *reinterpret_cast<const float2*>(row + (H + Hkv) * kHeadDim + e);
+    const uint32_t pk = f2h(v.x) | ((uint32_t)f2h(v.y) << 16);
+    *reinterpret_cast<uint32_t*>(vc + (((long)s * Hkv + h) * max_ctx + p) * kHeadDim + j) = pk;
   }
 }
 
@@ -425,6 +511,7 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(const float* __restrict__ 
 // all four 16-byte K loads in flight), softmax by one wave (lane = position), P.V: wave w takes
 // 16 positions with all 16 V loads in flight, lane = 2 dims.  Writes the unnormalised partial
 // output and (max, sum) per head.
+template <int G>
 __global__ void __launch_bounds__(256) attn_decode_kernel(const float* __restrict__ q,
                                                           const int* __restrict__ pos,
                                                           const int* __restrict__ slot,
@@ -433,12 +520,11 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(const float* __restric
                                                           int H, int Hkv, int max_ctx, int nsplit,
                                                           float scale, float* __restrict__ po,
                                                           float* __restrict__ pml) {
-  __shared__ float qs[kMaxGroup][kHeadDim];
-  __shared__ float ps[kMaxGroup][kAttnChunk];
-  __shared__ float mls[kMaxGroup][2];
-  __shared__ float opart[4][kMaxGroup][kHeadDim];
+  __shared__ float qs[G][kHeadDim];
+  __shared__ float ps[G][kAttnChunk];
+  __shared__ float mls[G][2];
+  __shared__ float opart[4][G][kHeadDim];
   const int kh = blockIdx.x, sp = blockIdx.y, t = blockIdx.z;
-  const int G = H / Hkv;
   const int len = pos[t] + 1;
   const int p0 = sp * kAttnChunk;
   const long pidx = ((long)t * H + kh * G) * nsplit + sp;   // + g * nsplit
@@ -454,20 +540,22 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(const float* __restric
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // K loads first (independent of q)
   const int pi = threadIdx.x >> 2, qd = threadIdx.x & 3;
+  // every load is unconditional (positions clamped into the chunk): a load under a branch ends
+  // its basic block and the join waits for it, which would serialise the HBM round trips
   uint4 kv[4];
-  if (pi < n) {
-    const uint4* kr = reinterpret_cast<const uint4*>(kc + cbase + (long)(p0 + pi) * kHeadDim
-                                                     + qd * 32);
+  {
+    const uint4* kr = reinterpret_cast<const uint4*>(kc + cbase + (long)(p0 + min(pi, n - 1))
+                                                     * kHeadDim + qd * 32);
 #pragma unroll
     for (int c = 0; c < 4; ++c) kv[c] = kr[c];
   }
   for (int i = threadIdx.x; i < G * kHeadDim; i += blockDim.x)
     qs[i / kHeadDim][i % kHeadDim] = q[(long)t * H * kHeadDim + (kh * G) * kHeadDim + i] * scale;
   __syncthreads();
-  float sc[kMaxGroup];
+  float sc[G];
 #pragma unroll
-  for (int g = 0; g < kMaxGroup; ++g) sc[g] = 0.f;
-  if (pi < n) {
+  for (int g = 0; g < G; ++g) sc[g] = 0.f;
+  {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const uint32_t kw[4] = {kv[c].x, kv[c].y, kv[c].z, kv[c].w};
@@ -478,26 +566,25 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(const float* __restric
         kf[2 * e + 1] = h2f(kw[e] >> 16);
       }
 #pragma unroll
-      for (int g = 0; g < kMaxGroup; ++g) {
-        if (g < G) {
+      for (int g = 0; g < G; ++g) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) sc[g] += kf[e] * qs[g][qd * 32 + c * 8 + e];
-        }
+        for (int e = 0; e < 8; ++e) sc[g] += kf[e] * qs[g][qd * 32 + c * 8 + e];
       }
     }
   }
 #pragma unroll
-  for (int g = 0; g < kMaxGroup; ++g) {
+  for (int g = 0; g < G; ++g) {
     sc[g] += __shfl_xor(sc[g], 1, kWave);
     sc[g] += __shfl_xor(sc[g], 2, kWave);
   }
   if (qd == 0) {
 #pragma unroll
-    for (int g = 0; g < kMaxGroup; ++g)
-      if (g < G) ps[g][pi] = pi < n ? sc[g] : -INFINITY;
+    for (int g = 0; g < G; ++g)
+      ps[g][pi] = pi < n ? sc[g] : -INFINITY;
   }
   __syncthreads();
   if (wave == 0) {
+#pragma unroll
     for (int g = 0; g < G; ++g) {
       const float s = ps[g][lane];
       const float m = wave_max(s);
@@ -513,30 +600,26 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(const float* __restric
   const uint32_t* vr = reinterpret_cast<const uint32_t*>(vc + cbase) + lane;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const int p = wave * 16 + j;
-    vv[j] = p < n ? vr[(long)(p0 + p) * (kHeadDim / 2)] : 0u;
+    const int p = min(wave * 16 + j, n - 1);        // ps[.][p >= n] == 0
+    vv[j] = vr[(long)(p0 + p) * (kHeadDim / 2)];
   }
-  float o[kMaxGroup][2];
+  float o[G][2];
 #pragma unroll
-  for (int g = 0; g < kMaxGroup; ++g) o[g][0] = o[g][1] = 0.f;
+  for (int g = 0; g < G; ++g) o[g][0] = o[g][1] = 0.f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const float v0 = h2f(vv[j] & 0xffffu), v1 = h2f(vv[j] >> 16);
 #pragma unroll
-    for (int g = 0; g < kMaxGroup; ++g) {
-      if (g < G) {
-        const float pw = ps[g][wave * 16 + j];
-        o[g][0] += pw * v0;
-        o[g][1] += pw * v1;
-      }
+    for (int g = 0; g < G; ++g) {
+      const float pw = ps[g][wave * 16 + j];
+      o[g][0] += pw * v0;
+      o[g][1] += pw * v1;
     }
   }
 #pragma unroll
-  for (int g = 0; g < kMaxGroup; ++g) {
-    if (g < G) {
-      opart[wave][g][2 * lane] = o[g][0];
-      opart[wave][g][2 * lane + 1] = o[g][1];
-    }
+  for (int g = 0; g < G; ++g) {
+    opart[wave][g][2 * lane] = o[g][0];
+    opart[wave][g][2 * lane + 1] = o[g][1];
   }
   __syncthreads();
   for (int i = threadIdx.x; i < G * kHeadDim; i += blockDim.x) {
@@ -563,15 +646,32 @@ __global__ void __launch_bounds__(128) attn_combine_q8_kernel(const float* __res
   const int h = blockIdx.x, t = blockIdx.y, dd = threadIdx.x;
   const int ns = min(nsplit, (pos[t] + kAttnChunk) / kAttnChunk);
   const long hb = ((long)t * H + h) * nsplit;
+  // chunk partials in groups of 8 with all loads in flight (indices clamped, extra terms masked)
   float m = -INFINITY;
-  for (int s = 0; s < ns; ++s) m = fmaxf(m, pml[(hb + s) * 2]);
+  for (int s0 = 0; s0 < ns; s0 += 8) {
+    float2 ml[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      ml[u] = *reinterpret_cast<const float2*>(pml + (hb + min(s0 + u, ns - 1)) * 2);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) m = fmaxf(m, ml[u].x);
+  }
   float den = 0.f, v = 0.f;
-#pragma unroll 8
-  for (int s = 0; s < ns; ++s) {
-    const float ms = pml[(hb + s) * 2];
-    const float wgt = ms == -INFINITY ? 0.f : __expf(ms - m);
-    den += wgt * pml[(hb + s) * 2 + 1];
-    v += wgt * po[(hb + s) * kHeadDim + dd];
+  for (int s0 = 0; s0 < ns; s0 += 8) {
+    float2 ml[8];
+    float ov[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long s = hb + min(s0 + u, ns - 1);
+      ml[u] = *reinterpret_cast<const float2*>(pml + s * 2);
+      ov[u] = po[s * kHeadDim + dd];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float wgt = (s0 + u < ns && ml[u].x != -INFINITY) ? __expf(ml[u].x - m) : 0.f;
+      den += wgt * ml[u].y;
+      v += wgt * ov[u];
+    }
   }
   v = den > 0.f ? v / den : 0.f;
   const int K = H * kHeadDim, col = h * kHeadDim + dd;
@@ -604,14 +704,15 @@ __global__ void __launch_bounds__(256) dequant_kernel(QMat w, const int* __restr
     const int blk = run >> 3, j = run & 7;            // super-block, 32-run within it
     float v[32];
     if constexpr (TYPE == kQ4K) {
-      const uint8_t* b = w.q + ((long)row * nb + blk) * kQ4KBytes;
+      const long rb = (long)row * nb + blk;
+      const uint8_t* b = reinterpret_cast<const uint8_t*>(w.sc) + rb * 16;
       const float d = h2f(*reinterpret_cast<const uint16_t*>(b));
       const float dmin = h2f(*reinterpret_cast<const uint16_t*>(b + 2));
       const uint8_t* s = b + 4;
       uint32_t sc, m;
       if (j < 4) { sc = s[j] & 63; m = s[j + 4] & 63; }
       else { sc = (s[j + 4] & 0xf) | ((s[j - 4] >> 6) << 4); m = (s[j + 4] >> 4) | ((s[j] >> 6) << 4); }
-      const uint8_t* qs = b + 16 + (j >> 1) * 32;
+      const uint8_t* qs = w.q + rb * 128 + (j >> 1) * 32;
 #pragma unroll
       for (int l = 0; l < 32; ++l) {
         const uint32_t q = (j & 1) ? (qs[l] >> 4) : (qs[l] & 0xf);
@@ -664,11 +765,23 @@ __global__ void q6k_repack_kernel(const uint8_t* __restrict__ src, long nblocks,
   }
 }
 
+// Q4_K GGUF blocks (144 B) → header plane [nb][16] + nibble plane [nb][128].
+__global__ void q4k_repack_kernel(const uint8_t* __restrict__ src, long nblocks,
+                                  uint8_t* __restrict__ qs, uint8_t* __restrict__ hdr) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nblocks * 9;
+       i += (long)gridDim.x * blockDim.x) {
+    const long b = i / 9;
+    const int c = (int)(i % 9);
+    const uint4 v = *reinterpret_cast<const uint4*>(src + b * kQ4KBytes + c * 16);
+    if (c == 0) *reinterpret_cast<uint4*>(hdr + b * 16) = v;
+    else *reinterpret_cast<uint4*>(qs + b * 128 + (c - 1) * 16) = v;
+  }
+}
+
 template <int TYPE, int T, int MODE>
 int launch_gemv(const GemvArgs& a, int waves, hipStream_t st) {
   const int nb = a.K >> 8;
-  const size_t lds = (size_t)T * (nb * 288 + (a.K >> 5) * 4 + (a.K >> 4) * 4)
-                     + (size_t)waves * T * 2 * 4;
+  const size_t lds = (size_t)T * (nb * 288 + (a.K >> 5) * 4 + (a.K >> 4) * 4) + 16 * 4;
   if (lds > 160 * 1024) return 3;
   const int grid = (a.N + a.rows_per_wg - 1) / a.rows_per_wg;
   hipLaunchKernelGGL((qgemv_kernel<TYPE, T, MODE>), dim3(grid), dim3(waves * 64), lds, st, a);
@@ -686,18 +799,12 @@ int dispatch_t(const GemvArgs& a, int waves, hipStream_t st) {
   }
 }
 
-// Default decomposition: enough waves to keep ~32 per CU streaming (256 CUs), split-K inside the
-// workgroup for short matrices, bigger workgroups for long rows so the LDS-staged activations
-// (1.4 bytes per weight column per token) are shared by 8 rows.
-void gemv_shape(int N, int K, int& waves, int& ks, int& rows) {
-  const int nb = K >> 8;
-  if (ks <= 0) ks = N >= 8192 ? 1 : (N >= 2048 ? 2 : 4);
-  while (ks > 1 && nb / ks < 2) ks >>= 1;
-  if (waves <= 0) waves = 8;
-  if (waves < ks) waves = ks;
-  if (rows <= 0) rows = (waves / ks) * (K >= 8192 ? 1 : 2);
-  const int rpi = waves / ks;
-  rows = (rows + rpi - 1) / rpi * rpi;
+// Default decomposition (measured on MI355X, tools/llm_bench.py --gemv): 4-wave workgroups of 8
+// rows — 2 rows per wave through the stage pipeline.
+void gemv_shape(int N, int K, int& waves, int& rows) {
+  (void)N; (void)K;
+  if (waves <= 0) waves = 4;
+  if (rows <= 0) rows = 2 * waves;
 }
 
 }  // namespace
@@ -708,16 +815,18 @@ int amdk8s_llm_max_tokens() { return kMaxTok; }
 int amdk8s_llm_attn_chunk() { return kAttnChunk; }
 
 // Quantised GEMV: out[t][n] (mode 0: = W.x + bias; 1: += W.x; 2: = silu(W0.x) * (W1.x)).
+// x: Q8 (x8/dx/sx) or fp32 rows xf [T][ldx] with an optional fused RMSNorm (norm_w, eps).
 // type 0 = Q4_K (w0q: GGUF rows), 1 = Q6_K (w0q/w0qh/w0sc/w0d planes).
 int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, const void* w0sc,
                      const void* w0d, const void* w1q, const void* w1qh, const void* w1sc,
                      const void* w1d, const void* x8, const void* dx, const void* sx,
-                     const void* bias, void* out, int ldo, int N, int K, int T, int waves, int ks,
+                     const void* xf, int ldx, const void* norm_w, float eps,
+                     const void* bias, void* out, int ldo, int N, int K, int T, int waves,
                      int rows_per_wg, void* stream) {
   if (K % 256 || N <= 0 || T < 1 || T > kMaxTok) return 2;
   if (mode == kPair && !w1q) return 2;
-  gemv_shape(N, K, waves, ks, rows_per_wg);
-  if (waves > 8 || waves % ks || (ks != 1 && ks != 2 && ks != 4)) return 2;
+  gemv_shape(N, K, waves, rows_per_wg);
+  if (waves < 1 || waves > 8 || rows_per_wg < 1) return 2;
   GemvArgs a;
   a.w0 = {static_cast<const uint8_t*>(w0q), static_cast<const uint8_t*>(w0qh),
           static_cast<const int8_t*>(w0sc), static_cast<const uint16_t*>(w0d)};
@@ -726,9 +835,15 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
   a.x8 = static_cast<const int8_t*>(x8);
   a.dx = static_cast<const float*>(dx);
   a.sx = static_cast<const float*>(sx);
+  a.xf = static_cast<const float*>(xf);
+  a.ldx = ldx;
+  a.norm_w = static_cast<const float*>(norm_w);
+  a.eps = eps;
+  if (!xf && !(x8 && dx && sx)) return 2;
+  if (xf && ldx % 4) return 2;
   a.bias = static_cast<const float*>(bias);
   a.out = static_cast<float*>(out);
-  a.ldo = ldo; a.N = N; a.K = K; a.T = T; a.ks = ks; a.rows_per_wg = rows_per_wg;
+  a.ldo = ldo; a.N = N; a.K = K; a.T = T; a.rows_per_wg = rows_per_wg;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (type == kQ4K) {
     if (mode == kStore) return dispatch_t<kQ4K, kStore>(a, waves, st);
@@ -756,7 +871,9 @@ int amdk8s_llm_rope_kv(const void* qkv, int ldq, const void* pos, const void* sl
                        const void* cos_t, const void* sin_t, int H, int Hkv, int head_dim,
                        int max_ctx, void* q_out, void* kc, void* vc, int T, void* stream) {
   if (head_dim != kHeadDim || T < 1) return 2;
-  hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, static_cast<hipStream_t>(stream),
+  const int threads = (H + 2 * Hkv) * (kHeadDim / 2);
+  hipLaunchKernelGGL(rope_kv_kernel, dim3((threads + 255) / 256, T), dim3(256), 0,
+                     static_cast<hipStream_t>(stream),
                      static_cast<const float*>(qkv), ldq, static_cast<const int*>(pos),
                      static_cast<const int*>(slot), static_cast<const float*>(cos_t),
                      static_cast<const float*>(sin_t), H, Hkv, max_ctx,
@@ -779,11 +896,25 @@ int amdk8s_llm_attn_decode(const void* q, const void* pos, const void* slot, con
     return 2;
   const int nsplit = span / kAttnChunk;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(attn_decode_kernel, dim3(Hkv, nsplit, T), dim3(256), 0, st,
-                     static_cast<const float*>(q), static_cast<const int*>(pos),
-                     static_cast<const int*>(slot), static_cast<const uint16_t*>(kc),
-                     static_cast<const uint16_t*>(vc), H, Hkv, max_ctx, nsplit, scale,
-                     static_cast<float*>(po), static_cast<float*>(pml));
+  // the GQA group size is a template parameter: fully unrolled head loops, no per-head branches
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(Hkv, nsplit, T), dim3(256), 0, st,
+                       static_cast<const float*>(q), static_cast<const int*>(pos),
+                       static_cast<const int*>(slot), static_cast<const uint16_t*>(kc),
+                       static_cast<const uint16_t*>(vc), H, Hkv, max_ctx, nsplit, scale,
+                       static_cast<float*>(po), static_cast<float*>(pml));
+  };
+  switch (H / Hkv) {
+    case 1: launch(attn_decode_kernel<1>); break;
+    case 2: launch(attn_decode_kernel<2>); break;
+    case 3: launch(attn_decode_kernel<3>); break;
+    case 4: launch(attn_decode_kernel<4>); break;
+    case 5: launch(attn_decode_kernel<5>); break;
+    case 6: launch(attn_decode_kernel<6>); break;
+    case 7: launch(attn_decode_kernel<7>); break;
+    case 8: launch(attn_decode_kernel<8>); break;
+    default: return 2;
+  }
   if (hipGetLastError() != hipSuccess) return 1;
   hipLaunchKernelGGL(attn_combine_q8_kernel, dim3(H, T), dim3(128), 0, st,
                      static_cast<const float*>(po), static_cast<const float*>(pml),
@@ -812,6 +943,16 @@ int amdk8s_llm_dequant(int type, const void* q, const void* qh, const void* sc, 
     hipLaunchKernelGGL((dequant_kernel<kQ6K, false>), dim3(grid), dim3(256), 0, st, w, r, nrows, K, out);
   else
     return 2;
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+int amdk8s_llm_q4k_repack(const void* src, long nblocks, void* qs, void* hdr, void* stream) {
+  if (nblocks < 1) return 2;
+  const long work = nblocks * 9;
+  const int grid = (int)((work + 255) / 256 < 65536 ? (work + 255) / 256 : 65536);
+  hipLaunchKernelGGL(q4k_repack_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint8_t*>(src), nblocks, static_cast<uint8_t*>(qs),
+                     static_cast<uint8_t*>(hdr));
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

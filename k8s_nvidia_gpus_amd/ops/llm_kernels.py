@@ -28,8 +28,8 @@ def _lib():
             vp, ci, cl, cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
             lib.amdk8s_llm_max_tokens.restype = ci
             lib.amdk8s_llm_attn_chunk.restype = ci
-            lib.amdk8s_llm_qgemv.argtypes = [ci, ci] + [vp] * 8 + [vp, vp, vp, vp, vp] \
-                + [ci, ci, ci, ci, ci, ci, ci, vp]
+            lib.amdk8s_llm_qgemv.argtypes = [ci, ci] + [vp] * 8 + [vp, vp, vp] \
+                + [vp, ci, vp, cf] + [vp, vp] + [ci, ci, ci, ci, ci, ci, vp]
             lib.amdk8s_llm_qgemv.restype = ci
             lib.amdk8s_llm_rmsnorm_q8.argtypes = [vp, vp, cf, ci, ci, vp, vp, vp, vp]
             lib.amdk8s_llm_rmsnorm_q8.restype = ci
@@ -42,6 +42,9 @@ def _lib():
             lib.amdk8s_llm_dequant.argtypes = [ci, vp, vp, vp, vp, vp, ci, ci, vp, ci, vp]
             lib.amdk8s_llm_dequant.restype = ci
             lib.amdk8s_llm_q6k_repack.argtypes = [vp, cl, vp, vp, vp, vp, vp]
+            lib.amdk8s_llm_q6k_repack.restype = ci
+            lib.amdk8s_llm_q4k_repack.argtypes = [vp, cl, vp, vp, vp]
+            lib.amdk8s_llm_q4k_repack.restype = ci
             lib.amdk8s_llm_q6k_repack.restype = ci
             _declared = True
     return lib
@@ -69,18 +72,21 @@ def attn_chunk() -> int:
 
 
 def qgemv(w0, x8, dx, sx, out, mode: int = STORE, w1=None, bias=None, ldo: int = None,
-          rows_per_wg: int = 0, waves: int = 0, ks: int = 0) -> None:
-    """``w0``/``w1``: :class:`~k8s_nvidia_gpus_amd.models.llm.weights.QWeight` on the GPU;
-    activations [T, K] in Q8 form; ``out`` fp32 [T, ldo] (a view with row stride ``ldo``).
-    ``waves`` per workgroup, ``ks`` waves per row and ``rows_per_wg``: 0 = the kernel's default
-    decomposition for this shape."""
-    t = x8.shape[0]
+          rows_per_wg: int = 0, waves: int = 0, xf=None, norm_w=None, eps: float = 1e-6) -> None:
+    """``w0``/``w1``: :class:`~k8s_nvidia_gpus_amd.models.llm.weights.QWeight` on the GPU.
+    Input: Q8 activations (``x8``/``dx``/``sx``, [T, K]) or fp32 rows ``xf`` [T, K] (pass
+    ``x8=dx=sx=None``) that the kernel quantises itself, after an RMSNorm when ``norm_w`` is given.
+    ``out`` fp32 [T, ldo] (a view with row stride ``ldo``).  ``waves`` per workgroup and
+    ``rows_per_wg``: 0 = the kernel's default decomposition."""
+    t = (xf if xf is not None else x8).shape[0]
     ldo = out.stride(0) if ldo is None else ldo
     a = w0.ptrs()
     b = w1.ptrs() if w1 is not None else (None, None, None, None)
-    _check(_lib().amdk8s_llm_qgemv(w0.qtype, mode, *a, *b, x8.data_ptr(), dx.data_ptr(),
-                                   sx.data_ptr(), _p(bias), out.data_ptr(), ldo, w0.n, w0.k, t,
-                                   waves, ks, rows_per_wg, _stream(x8)), "amdk8s_llm_qgemv")
+    ref = xf if xf is not None else x8
+    _check(_lib().amdk8s_llm_qgemv(w0.qtype, mode, *a, *b, _p(x8), _p(dx), _p(sx), _p(xf),
+                                   xf.stride(0) if xf is not None else 0, _p(norm_w), float(eps),
+                                   _p(bias), out.data_ptr(), ldo, w0.n, w0.k, t,
+                                   waves, rows_per_wg, _stream(ref)), "amdk8s_llm_qgemv")
 
 
 def rmsnorm_q8(x, w, eps: float, x8, dx, sx) -> None:
@@ -124,3 +130,8 @@ def q6k_repack(raw, ql, qh, sc, d) -> None:
     _check(_lib().amdk8s_llm_q6k_repack(raw.data_ptr(), raw.numel() // 210, ql.data_ptr(),
                                         qh.data_ptr(), sc.data_ptr(), d.data_ptr(), _stream(raw)),
            "amdk8s_llm_q6k_repack")
+
+
+def q4k_repack(raw, qs, hdr) -> None:
+    _check(_lib().amdk8s_llm_q4k_repack(raw.data_ptr(), raw.numel() // 144, qs.data_ptr(),
+                                        hdr.data_ptr(), _stream(raw)), "amdk8s_llm_q4k_repack")

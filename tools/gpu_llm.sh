@@ -9,7 +9,7 @@ echo "== pytest llm gpu"
 timeout -k 10 600 python -u -m pytest tests/test_llm_gpu.py -x -v -p no:warnings --timeout 200 --timeout-method thread > "$OUT/pytest_llm.log" 2>&1 || { tail -60 "$OUT/pytest_llm.log"; exit 1; }
 tail -3 "$OUT/pytest_llm.log"
 echo "== llm bench"
-timeout -k 10 600 python -u tools/llm_bench.py --gemv --out "$OUT/llm_bench.json" > "$OUT/llm_bench.log" 2>&1 || { tail -30 "$OUT/llm_bench.log"; exit 1; }
+timeout -k 10 600 python -u tools/llm_bench.py --gemv --kernels --out "$OUT/llm_bench.json" > "$OUT/llm_bench.log" 2>&1 || { tail -30 "$OUT/llm_bench.log"; exit 1; }
 grep -v '^{' "$OUT/llm_bench.log" | tail -20
 if [[ "${PROFILE:-1}" == 1 ]]; then
   echo "== rocprof llm"

@@ -51,8 +51,8 @@ def bench_gemv(eng: Engine, iters: int = 50) -> list:
     cases = [("qkv", L.wqkv[0], "store"), ("o_proj", L.wo, "resid"),
              ("gate_up", L.wg, "pair"), ("down_q4k", L.wd, "resid"),
              ("down_q6k", Lq6.wd, "resid"), ("lm_head", eng.w.output, "store")]
-    cfgs = [(0, 0, 0), (4, 1, 4), (4, 1, 8), (8, 1, 8), (8, 1, 16), (8, 2, 4), (8, 2, 8),
-            (8, 4, 2), (8, 4, 4), (4, 2, 2), (4, 4, 1)]
+    cfgs = [(0, 0), (4, 4), (4, 16), (4, 32), (8, 8), (8, 16), (8, 32), (2, 4), (2, 8),
+            (1, 2), (1, 4)]
     for name, w, mode in cases:
         for T in (1, 4):
             x8 = torch.randint(-127, 127, (T, w.k), dtype=torch.int8, device=eng.device)
@@ -60,9 +60,8 @@ def bench_gemv(eng: Engine, iters: int = 50) -> list:
             sx = torch.zeros(T, w.k // 16, device=eng.device)
             out = torch.zeros(T, w.n, device=eng.device)
             m = {"store": LK.STORE, "resid": LK.RESID, "pair": LK.PAIR}[mode]
-            for waves, ks, rpw in (cfgs if T == 1 else cfgs[:1]):
-                kw = dict(w1=L.wu if mode == "pair" else None, waves=waves, ks=ks,
-                          rows_per_wg=rpw)
+            for waves, rpw in (cfgs if T == 1 else cfgs[:1]):
+                kw = dict(w1=L.wu if mode == "pair" else None, waves=waves, rows_per_wg=rpw)
                 for _ in range(3):
                     LK.qgemv(w, x8, dx, sx, out, m, **kw)
                 torch.cuda.synchronize()
@@ -75,9 +74,52 @@ def bench_gemv(eng: Engine, iters: int = 50) -> list:
                 us = e0.elapsed_time(e1) / iters * 1e3
                 nbytes = w.nbytes() * (2 if mode == "pair" else 1)
                 r = {"gemv": name, "T": T, "N": w.n, "K": w.k, "type": ["Q4_K", "Q6_K"][w.qtype],
-                     "cfg": [waves, ks, rpw], "us": round(us, 2),
+                     "cfg": [waves, rpw], "us": round(us, 2),
                      "GBps": round(nbytes / us / 1e3, 1)}
                 rows.append(r)
+    return rows
+
+
+def bench_small_kernels(eng: Engine, iters: int = 100) -> list:
+    """Per-launch time of the non-GEMV decode kernels (T = 1), attention at several lengths."""
+    import math
+
+    LK, c = eng.LK, eng.cfg
+    b = eng._buffers(1)
+    qd = eng._q8(b, c.dim)
+    L = eng.w.layers[0]
+    rows = []
+
+    def timed(name, fn, **extra):
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        r = dict(kernel=name, us=round(e0.elapsed_time(e1) / iters * 1e3, 2), **extra)
+        rows.append(r)
+        print(r, file=sys.stderr, flush=True)
+
+    timed("rmsnorm_q8_dim", lambda: LK.rmsnorm_q8(b.h, L.attn_norm, c.eps, *qd))
+    qf = eng._q8(b, c.ffn)
+    timed("quant_ffn", lambda: LK.rmsnorm_q8(b.t, None, 0.0, *qf))
+    timed("rope_kv", lambda: LK.rope_kv(b.qkv, b.pos, b.slot, eng.cos, eng.sin, c.heads,
+                                        c.kv_heads, c.head_dim, eng.max_ctx, b.qrot,
+                                        eng.k_cache[0], eng.v_cache[0]))
+    for p in (100, 1000, 4000):
+        if p >= eng.max_ctx:
+            continue
+        b.pos.fill_(p)
+        span = eng._span(p)
+        timed("attn_decode+combine", lambda: LK.attn_decode(
+            b.qrot, b.pos, b.slot, eng.k_cache[0], eng.v_cache[0], c.heads, c.kv_heads,
+            c.head_dim, eng.max_ctx, 1 / math.sqrt(c.head_dim), b.po, b.pml, *qd, span=span),
+            pos=p, span=span)
+    timed("embed_dequant", lambda: LK.dequant(eng.w.tok_embd, b.h, rows=b.tok))
     return rows
 
 
@@ -89,6 +131,7 @@ def main(argv=None) -> int:
     ap.add_argument("--prompt", type=int, default=512)
     ap.add_argument("--tokens", default="1,2,3,4")
     ap.add_argument("--gemv", action="store_true")
+    ap.add_argument("--kernels", action="store_true", help="time the non-GEMV decode kernels")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
     if not torch.cuda.is_available():
@@ -145,6 +188,8 @@ def main(argv=None) -> int:
         res["gemv"] = bench_gemv(eng)
         for r in res["gemv"]:
             print(r, file=sys.stderr, flush=True)
+    if args.kernels:
+        res["kernels"] = bench_small_kernels(eng)
     res["graph_captures"] = eng.stats["graph_captures"]
     line = json.dumps(res)
     print(line, flush=True)
