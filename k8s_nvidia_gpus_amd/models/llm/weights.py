@@ -4,8 +4,9 @@ Decoding streams every weight once per token, so the engine keeps the file's 4/6
 (~4.4 GB for Qwen2.5-7B Q4_K_M) and reads them with the GEMV kernels; with 288 GB per MI355X it
 can also keep an fp16 copy for compute-bound prompt processing (``dense=True``, +15 GB).
 
-* ``QWeight`` — one [N, K] matrix repacked on the GPU into aligned planes (Q4_K: nibbles + 16-byte
-  block headers; Q6_K: ql / qh / scales / d) — same bytes as the file.  On the CPU (tests, no GPU)
+* ``QWeight`` — one [N, K] matrix repacked on the GPU into aligned planes (Q4_K: nibbles + the
+  6-bit scales/mins decoded to bytes + d/dmin; Q6_K: ql / qh / lane-ordered scales / d) — the
+  file's information, 148 instead of 144 bytes per Q4_K block.  On the CPU (tests, no GPU)
   it holds the raw GGUF rows and dequantises with the numpy codecs.
 * ``ModelWeights.from_gguf`` — tensor names of llama.cpp's qwen2 GGUF layout
   (``token_embd``, ``blk.N.attn_q`` …, ``output``); matrices of other types (F16/F32/Q8_0) are
@@ -74,9 +75,10 @@ class QWeight:
         nb = k // 256
         if ggml_type == gguf.Q4_K:
             qs = torch.empty((n, nb * 128), dtype=torch.uint8, device=t.device)
-            hdr = torch.empty((n, nb * 16), dtype=torch.int8, device=t.device)
-            LK.q4k_repack(t.contiguous(), qs, hdr)
-            return cls(0, n, k, qs, sc=hdr)
+            scm = torch.empty((n, nb * 16), dtype=torch.int8, device=t.device)
+            dm = torch.empty((n, nb), dtype=torch.int32, device=t.device)
+            LK.q4k_repack(t.contiguous(), qs, scm, dm)
+            return cls(0, n, k, qs, sc=scm, d=dm)
         ql = torch.empty((n, nb * 128), dtype=torch.uint8, device=t.device)
         qh = torch.empty((n, nb * 64), dtype=torch.uint8, device=t.device)
         sc = torch.empty((n, nb * 16), dtype=torch.int8, device=t.device)

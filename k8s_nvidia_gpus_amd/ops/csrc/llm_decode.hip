@@ -14,9 +14,10 @@
 //   wave-wide 16-byte load reads 8 consecutive super-blocks (1 KiB of quants) fully coalesced; a
 //   wave's rows run as one software pipeline (next stage's loads in flight during this stage's
 //   maths).
-//   Both formats are repacked at load time into planes (Q4_K: nibbles + 16-byte block headers;
-//   Q6_K: ql / qh / scales / d) so every load is aligned and a wave's header load covers 8
-//   consecutive blocks in one 128-byte line.
+//   Both formats are repacked at load time into planes (Q4_K: nibbles + the 6-bit scales/mins
+//   decoded to bytes, one dword per lane pair, + d/dmin; Q6_K: ql / qh / lane-ordered scales / d)
+//   so every load is aligned and the per-lane scale decode is a byte extract (the GGUF 6-bit
+//   unpacking cost more VALU than the dot products).  Same information, 148 vs 144 bytes/block.
 // * The activations of the (<= 4) tokens are staged once per workgroup in LDS (x8 padded 32 B per
 //   256 so the 16-lane groups of a ds_read_b128 hit disjoint banks); every wave of the workgroup
 //   then streams its rows against them.
@@ -76,9 +77,16 @@ __device__ __forceinline__ int xoff(int p) { return (p >> 8) * 288 + (p & 255); 
 struct QMat {            // one quantised weight matrix [N, K], repacked at load into aligned planes
   const uint8_t* q;      // Q4_K: nibbles [N][nb][128];  Q6_K: low bits [N][nb][128]
   const uint8_t* qh;     // Q6_K: high bits [N][nb][64]
-  const int8_t* sc;      // Q4_K: block headers [N][nb][16] (d, dmin, scales);  Q6_K: scales [N][nb][16]
-  const uint16_t* d;     // Q6_K: [N][nb]
+  const int8_t* sc;      // Q4_K: decoded 6-bit scales/mins [N][nb][4] dwords, dword c =
+                         //   sc[2c] | sc[2c+1] << 8 | m[2c] << 16 | m[2c+1] << 24;
+                         // Q6_K: scales [N][nb][16] ordered so lane `sub` reads bytes 2sub, 2sub+1
+  const uint16_t* d;     // Q4_K: [N][nb] dwords (d | dmin << 16);  Q6_K: [N][nb] f16
 };
+
+// Q6_K: stored scale position of GGUF scale index i (pairs (i, i+4) adjacent per lane).
+__host__ __device__ constexpr int q6_scale_pos(int i) {
+  return (i & 8) + 2 * (i & 3) + ((i >> 2) & 1);
+}
 
 struct GemvArgs {
   QMat w0, w1;           // w1: ffn_up in pair mode
@@ -106,21 +114,22 @@ __device__ __forceinline__ uint4 ldnt(const void* p) {
 // One lane's share of a 256-weight super-block: Q4_K = the block header (d, dmin, 12 scale bytes)
 // + 16 B of nibbles; Q6_K = 16 B of low bits + 16 B of high bits + the 16 scales + d.
 template <int TYPE> struct Blk;
-template <> struct Blk<kQ4K> { uint4 h, q; };
-template <> struct Blk<kQ6K> { uint4 l, hb, s; uint32_t d; };
+template <> struct Blk<kQ4K> { uint4 q; uint32_t sm, dd; };
+template <> struct Blk<kQ6K> { uint4 l, hb; uint32_t s2, d; };
 
 template <int TYPE>
 __device__ __forceinline__ void load_blk(const QMat& w, long rowblk, int blk, int sub,
                                          Blk<TYPE>& r) {
   if constexpr (TYPE == kQ4K) {
     const long rb = rowblk + blk;
-    r.h = ldnt(w.sc + rb * 16);                                 // header plane: 8 blocks = 128 B
     r.q = ldnt(w.q + rb * 128 + sub * 16);
+    r.sm = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(w.sc) + rb * 4 + (sub >> 1));
+    r.dd = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(w.d) + rb);
   } else {
     const long rb = rowblk + blk;
     r.l = ldnt(w.q + rb * 128 + sub * 16);
     r.hb = ldnt(w.qh + rb * 64 + (sub >> 2) * 32 + (sub & 1) * 16);
-    r.s = ldnt(w.sc + rb * 16);
+    r.s2 = __builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(w.sc) + rb * 8 + sub);
     r.d = __builtin_nontemporal_load(w.d + rb);
   }
 }
@@ -137,20 +146,10 @@ __device__ __forceinline__ void dot_blk(const Blk<TYPE>& r, int blk, int sub, co
                                         float* acc) {
   if constexpr (TYPE == kQ4K) {
     const int c = sub >> 1;               // 64-weight chunk: sub-blocks 2c (low) and 2c+1 (high)
-    const float d = h2f(r.h.x & 0xffffu), dmin = h2f(r.h.x >> 16);
-    const uint32_t s[3] = {r.h.y, r.h.z, r.h.w};
-    auto sbyte = [&](int i) -> uint32_t { return (s[i >> 2] >> ((i & 3) * 8)) & 0xffu; };
-    const int j0 = 2 * c, j1 = 2 * c + 1;
-    uint32_t sc0, m0, sc1, m1;
-    if (c < 2) {
-      sc0 = sbyte(j0) & 63; m0 = sbyte(j0 + 4) & 63;
-      sc1 = sbyte(j1) & 63; m1 = sbyte(j1 + 4) & 63;
-    } else {
-      sc0 = (sbyte(j0 + 4) & 0xf) | ((sbyte(j0 - 4) >> 6) << 4);
-      m0 = (sbyte(j0 + 4) >> 4) | ((sbyte(j0) >> 6) << 4);
-      sc1 = (sbyte(j1 + 4) & 0xf) | ((sbyte(j1 - 4) >> 6) << 4);
-      m1 = (sbyte(j1 + 4) >> 4) | ((sbyte(j1) >> 6) << 4);
-    }
+    const float d = h2f(r.dd & 0xffffu), dmin = h2f(r.dd >> 16);
+    // the lane's two scales and mins were decoded from the 6-bit packing at load time
+    const uint32_t sc0 = r.sm & 0xffu, sc1 = (r.sm >> 8) & 0xffu;
+    const uint32_t m0 = (r.sm >> 16) & 0xffu, m1 = r.sm >> 24;
     const uint32_t q[4] = {r.q.x, r.q.y, r.q.z, r.q.w};
     const int p_lo = blk * 256 + c * 64 + (sub & 1) * 16;
     const int g_lo = p_lo >> 4, d_lo = p_lo >> 5;
@@ -181,10 +180,9 @@ __device__ __forceinline__ void dot_blk(const Blk<TYPE>& r, int blk, int sub, co
   } else {
     const int n = sub >> 2, h1 = sub & 1, klo = (sub & 3) >> 1;
     const float d = h2f(r.d & 0xffffu);
-    const uint32_t scw[4] = {r.s.x, r.s.y, r.s.z, r.s.w};
-    const int i0 = 8 * n + h1 + 2 * klo, i1 = i0 + 4;
-    const float sc0 = __fmul_rn(d, (float)(int8_t)((scw[i0 >> 2] >> ((i0 & 3) * 8)) & 0xffu));
-    const float sc1 = __fmul_rn(d, (float)(int8_t)((scw[i1 >> 2] >> ((i1 & 3) * 8)) & 0xffu));
+    // scales 8n + h1 + 2klo and that + 4, stored adjacent for this lane (q6_scale_pos)
+    const float sc0 = __fmul_rn(d, (float)(int8_t)(r.s2 & 0xffu));
+    const float sc1 = __fmul_rn(d, (float)(int8_t)((r.s2 >> 8) & 0xffu));
     const uint32_t l[4] = {r.l.x, r.l.y, r.l.z, r.l.w};
     const uint32_t hb[4] = {r.hb.x, r.hb.y, r.hb.z, r.hb.w};
     const int sh = 2 * klo;
@@ -291,7 +289,7 @@ __global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
   int8_t* xs = reinterpret_cast<int8_t*>(lds);
   float* dxs = reinterpret_cast<float*>(lds + T * xstride);
   float* sxs = dxs + T * (K >> 5);
-  float* red = sxs + T * (K >> 4);                   // [W] block-reduction scratch
+  float* red = sxs + T * (K >> 4);                   // [W][T] block-reduction scratch
   if (a.xf == nullptr) {                             // Q8 input: copy into LDS
     for (int i = threadIdx.x; i < T * (K >> 4); i += blockDim.x) {
       const int t = i / (K >> 4), p = (i - t * (K >> 4)) << 4;
@@ -302,74 +300,87 @@ __global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
     for (int i = threadIdx.x; i < T * (K >> 4); i += blockDim.x) sxs[i] = a.sx[i];
   } else {
     // fp32 input (+ RMSNorm): every workgroup normalises and quantises the (L2-resident) rows
-    // itself, which removes a launch and its boundary per matrix.  Per token the thread mapping
-    // does not depend on T, so results are batch-invariant.
-    for (int t = 0; t < T; ++t) {
-      const float* xr = a.xf + (long)t * a.ldx;
-      float rs = 1.f;
-      if (a.norm_w) {
-        float ss = 0.f;
-        for (int i0 = threadIdx.x * 4; i0 < K; i0 += blockDim.x * 16) {
-          float4 v[4];
+    // itself, which removes a launch and its boundary per matrix.  All T tokens are processed
+    // together (their loads in flight at once); per token the thread mapping and reduction order
+    // do not depend on T, so results are batch-invariant.
+    float rs[T];
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
-            v[u] = *reinterpret_cast<const float4*>(xr + min(i0 + u * (int)blockDim.x * 4, K - 4));
+    for (int t = 0; t < T; ++t) rs[t] = 1.f;
+    if (a.norm_w) {
+      float ss[T];
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
+      for (int t = 0; t < T; ++t) ss[t] = 0.f;
+      for (int i0 = threadIdx.x * 4; i0 < K; i0 += blockDim.x * 8) {
+        float4 v[T][2];
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+            v[t][u] = *reinterpret_cast<const float4*>(
+                a.xf + (long)t * a.ldx + min(i0 + u * (int)blockDim.x * 4, K - 4));
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
             if (i0 + u * (int)blockDim.x * 4 < K)
-              ss += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
-        }
-        ss = wave_sum(ss);
-        if (lane == 0) red[wave] = ss;
-        __syncthreads();
-        ss = 0.f;
-        for (int w = 0; w < W; ++w) ss += red[w];
-        __syncthreads();
-        rs = rsqrtf(ss / (float)K + a.eps);
+              ss[t] += v[t][u].x * v[t][u].x + v[t][u].y * v[t][u].y + v[t][u].z * v[t][u].z +
+                       v[t][u].w * v[t][u].w;
       }
-      // chunk c = 8 values; 4 consecutive chunks (one lane quad) = one 32-value block
-      for (int c0 = threadIdx.x; c0 < (K >> 3); c0 += blockDim.x * 2) {
-        float v[2][8];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int c = min(c0 + u * (int)blockDim.x, (K >> 3) - 1);
-          const float4 x0 = *reinterpret_cast<const float4*>(xr + c * 8);
-          const float4 x1 = *reinterpret_cast<const float4*>(xr + c * 8 + 4);
-          v[u][0] = x0.x; v[u][1] = x0.y; v[u][2] = x0.z; v[u][3] = x0.w;
-          v[u][4] = x1.x; v[u][5] = x1.y; v[u][6] = x1.z; v[u][7] = x1.w;
-          if (a.norm_w) {
-            const float4 w0 = *reinterpret_cast<const float4*>(a.norm_w + c * 8);
-            const float4 w1 = *reinterpret_cast<const float4*>(a.norm_w + c * 8 + 4);
-            const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      for (int t = 0; t < T; ++t) {
+        ss[t] = wave_sum(ss[t]);
+        if (lane == 0) red[wave * T + t] = ss[t];
+      }
+      __syncthreads();
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[u][i] *= rs * wv[i];
-          }
+      for (int t = 0; t < T; ++t) {
+        float tot = 0.f;
+        for (int w = 0; w < W; ++w) tot += red[w * T + t];
+        rs[t] = rsqrtf(tot / (float)K + a.eps);
+      }
+    }
+    // chunk c = 8 values; 4 consecutive chunks (one lane quad) = one 32-value block
+    for (int c = threadIdx.x; c < (K >> 3); c += blockDim.x) {   // whole quads leave together
+      float v[T][8];
+      float4 w0 = make_float4(1.f, 1.f, 1.f, 1.f), w1 = w0;
+      if (a.norm_w) {
+        w0 = *reinterpret_cast<const float4*>(a.norm_w + c * 8);
+        w1 = *reinterpret_cast<const float4*>(a.norm_w + c * 8 + 4);
+      }
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const float4 x0 = *reinterpret_cast<const float4*>(a.xf + (long)t * a.ldx + c * 8);
+        const float4 x1 = *reinterpret_cast<const float4*>(a.xf + (long)t * a.ldx + c * 8 + 4);
+        v[t][0] = x0.x; v[t][1] = x0.y; v[t][2] = x0.z; v[t][3] = x0.w;
+        v[t][4] = x1.x; v[t][5] = x1.y; v[t][6] = x1.z; v[t][7] = x1.w;
+      }
+      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        if (a.norm_w) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[t][i] *= rs[t] * wv[i];
         }
+        float amax = 0.f;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int c = c0 + u * (int)blockDim.x;
-          if (c >= (K >> 3)) break;                 // whole quads leave together (K % 256 == 0)
-          float amax = 0.f;
+        for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[t][i]));
+        amax = fmaxf(amax, __shfl_xor(amax, 1, kWave));
+        amax = fmaxf(amax, __shfl_xor(amax, 2, kWave));
+        const float d = amax / 127.f;
+        const float id = d > 0.f ? 1.f / d : 0.f;
+        uint32_t pk0 = 0u, pk1 = 0u;
+        int sq = 0;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[u][i]));
-          amax = fmaxf(amax, __shfl_xor(amax, 1, kWave));
-          amax = fmaxf(amax, __shfl_xor(amax, 2, kWave));
-          const float d = amax / 127.f;
-          const float id = d > 0.f ? 1.f / d : 0.f;
-          uint32_t pk0 = 0u, pk1 = 0u;
-          int sq = 0;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const int q = (int)__builtin_rintf(v[u][i] * id);
-            if (i < 4) pk0 |= ((uint32_t)(q & 0xff)) << (8 * i);
-            else pk1 |= ((uint32_t)(q & 0xff)) << (8 * (i - 4));
-            sq += q;
-          }
-          sq += __shfl_xor(sq, 1, kWave);
-          *reinterpret_cast<uint2*>(xs + t * xstride + xoff(c * 8)) = make_uint2(pk0, pk1);
-          if ((c & 3) == 0) dxs[t * (K >> 5) + (c >> 2)] = d;
-          if ((c & 1) == 0) sxs[t * (K >> 4) + (c >> 1)] = d * (float)sq;
+        for (int i = 0; i < 8; ++i) {
+          const int q = (int)__builtin_rintf(v[t][i] * id);
+          if (i < 4) pk0 |= ((uint32_t)(q & 0xff)) << (8 * i);
+          else pk1 |= ((uint32_t)(q & 0xff)) << (8 * (i - 4));
+          sq += q;
         }
+        sq += __shfl_xor(sq, 1, kWave);
+        *reinterpret_cast<uint2*>(xs + t * xstride + xoff(c * 8)) = make_uint2(pk0, pk1);
+        if ((c & 3) == 0) dxs[t * (K >> 5) + (c >> 2)] = d;
+        if ((c & 1) == 0) sxs[t * (K >> 4) + (c >> 1)] = d * (float)sq;
       }
     }
   }
@@ -705,13 +716,10 @@ __global__ void __launch_bounds__(256) dequant_kernel(QMat w, const int* __restr
     float v[32];
     if constexpr (TYPE == kQ4K) {
       const long rb = (long)row * nb + blk;
-      const uint8_t* b = reinterpret_cast<const uint8_t*>(w.sc) + rb * 16;
-      const float d = h2f(*reinterpret_cast<const uint16_t*>(b));
-      const float dmin = h2f(*reinterpret_cast<const uint16_t*>(b + 2));
-      const uint8_t* s = b + 4;
-      uint32_t sc, m;
-      if (j < 4) { sc = s[j] & 63; m = s[j + 4] & 63; }
-      else { sc = (s[j + 4] & 0xf) | ((s[j - 4] >> 6) << 4); m = (s[j + 4] >> 4) | ((s[j] >> 6) << 4); }
+      const uint32_t dd = reinterpret_cast<const uint32_t*>(w.d)[rb];
+      const float d = h2f(dd & 0xffffu), dmin = h2f(dd >> 16);
+      const uint32_t smw = reinterpret_cast<const uint32_t*>(w.sc)[rb * 4 + (j >> 1)];
+      const uint32_t sc = (smw >> (8 * (j & 1))) & 0xffu, m = (smw >> (16 + 8 * (j & 1))) & 0xffu;
       const uint8_t* qs = w.q + rb * 128 + (j >> 1) * 32;
 #pragma unroll
       for (int l = 0; l < 32; ++l) {
@@ -723,13 +731,13 @@ __global__ void __launch_bounds__(256) dequant_kernel(QMat w, const int* __restr
       const int n = j >> 2, k = j & 3;                // half, 32-run within the half
       const uint8_t* ql = w.q + rb * 128 + n * 64 + (k & 1) * 32;
       const uint8_t* qh = w.qh + rb * 64 + n * 32;
-      const int8_t* sc = w.sc + rb * 16 + n * 8 + 2 * k;
+      const int8_t* sc = w.sc + rb * 16;
       const float d = h2f(w.d[rb]);
 #pragma unroll
       for (int l = 0; l < 32; ++l) {
         const uint32_t lo = (k < 2) ? (ql[l] & 0xf) : (ql[l] >> 4);
         const int q = (int)(lo | (((qh[l] >> (2 * k)) & 3) << 4)) - 32;
-        v[l] = d * (float)sc[l >> 4] * (float)q;
+        v[l] = d * (float)sc[q6_scale_pos(8 * n + 2 * k + (l >> 4))] * (float)q;
       }
     }
     if constexpr (F32OUT) {
@@ -760,28 +768,37 @@ __global__ void q6k_repack_kernel(const uint8_t* __restrict__ src, long nblocks,
     const uint8_t* s = src + b * 210;
     for (int i = 0; i < 128; ++i) ql[b * 128 + i] = s[i];
     for (int i = 0; i < 64; ++i) qh[b * 64 + i] = s[128 + i];
-    for (int i = 0; i < 16; ++i) sc[b * 16 + i] = (int8_t)s[192 + i];
+    for (int i = 0; i < 16; ++i) sc[b * 16 + q6_scale_pos(i)] = (int8_t)s[192 + i];
     d[b] = (uint16_t)(s[208] | (s[209] << 8));
   }
 }
 
-// Q4_K GGUF blocks (144 B) → header plane [nb][16] + nibble plane [nb][128].
+// Q4_K GGUF blocks (144 B) → nibbles [nb][128] + decoded scales/mins [nb][4 dwords] + d/dmin.
 __global__ void q4k_repack_kernel(const uint8_t* __restrict__ src, long nblocks,
-                                  uint8_t* __restrict__ qs, uint8_t* __restrict__ hdr) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nblocks * 9;
-       i += (long)gridDim.x * blockDim.x) {
-    const long b = i / 9;
-    const int c = (int)(i % 9);
-    const uint4 v = *reinterpret_cast<const uint4*>(src + b * kQ4KBytes + c * 16);
-    if (c == 0) *reinterpret_cast<uint4*>(hdr + b * 16) = v;
-    else *reinterpret_cast<uint4*>(qs + b * 128 + (c - 1) * 16) = v;
+                                  uint8_t* __restrict__ qs, uint32_t* __restrict__ scm,
+                                  uint32_t* __restrict__ dm) {
+  for (long b = blockIdx.x * (long)blockDim.x + threadIdx.x; b < nblocks;
+       b += (long)gridDim.x * blockDim.x) {
+    const uint8_t* s = src + b * kQ4KBytes;
+    dm[b] = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
+    const uint8_t* q = s + 4;
+    uint32_t sc[8], m[8];
+    for (int j = 0; j < 8; ++j) {
+      if (j < 4) { sc[j] = q[j] & 63; m[j] = q[j + 4] & 63; }
+      else { sc[j] = (q[j + 4] & 0xf) | ((q[j - 4] >> 6) << 4); m[j] = (q[j + 4] >> 4) | ((q[j] >> 6) << 4); }
+    }
+    for (int c = 0; c < 4; ++c)
+      scm[b * 4 + c] = sc[2 * c] | (sc[2 * c + 1] << 8) | (m[2 * c] << 16) | (m[2 * c + 1] << 24);
+    for (int c = 0; c < 8; ++c)
+      *reinterpret_cast<uint4*>(qs + b * 128 + c * 16) =
+          *reinterpret_cast<const uint4*>(s + 16 + c * 16);
   }
 }
 
 template <int TYPE, int T, int MODE>
 int launch_gemv(const GemvArgs& a, int waves, hipStream_t st) {
   const int nb = a.K >> 8;
-  const size_t lds = (size_t)T * (nb * 288 + (a.K >> 5) * 4 + (a.K >> 4) * 4) + 16 * 4;
+  const size_t lds = (size_t)T * (nb * 288 + (a.K >> 5) * 4 + (a.K >> 4) * 4) + 16 * T * 4;
   if (lds > 160 * 1024) return 3;
   const int grid = (a.N + a.rows_per_wg - 1) / a.rows_per_wg;
   hipLaunchKernelGGL((qgemv_kernel<TYPE, T, MODE>), dim3(grid), dim3(waves * 64), lds, st, a);
@@ -799,12 +816,12 @@ int dispatch_t(const GemvArgs& a, int waves, hipStream_t st) {
   }
 }
 
-// Default decomposition (measured on MI355X, tools/llm_bench.py --gemv): 4-wave workgroups of 8
-// rows — 2 rows per wave through the stage pipeline.
+// Default decomposition (measured on MI355X, tools/llm_bench.py --gemv, T = 1): 4-wave
+// workgroups of 8 rows for the 3584/4608/18944-row matrices, 8 waves for the 18944-long rows of
+// ffn_down, and 32 rows per workgroup for the 152064-row lm_head (longer per-wave pipelines).
 void gemv_shape(int N, int K, int& waves, int& rows) {
-  (void)N; (void)K;
-  if (waves <= 0) waves = 4;
-  if (rows <= 0) rows = 2 * waves;
+  if (waves <= 0) waves = K >= 8192 ? 8 : 4;
+  if (rows <= 0) rows = N >= 65536 ? 32 : 8;
 }
 
 }  // namespace
@@ -946,13 +963,13 @@ int amdk8s_llm_dequant(int type, const void* q, const void* qh, const void* sc, 
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
-int amdk8s_llm_q4k_repack(const void* src, long nblocks, void* qs, void* hdr, void* stream) {
+int amdk8s_llm_q4k_repack(const void* src, long nblocks, void* qs, void* scm, void* dm,
+                          void* stream) {
   if (nblocks < 1) return 2;
-  const long work = nblocks * 9;
-  const int grid = (int)((work + 255) / 256 < 65536 ? (work + 255) / 256 : 65536);
+  const int grid = (int)((nblocks + 255) / 256 < 65536 ? (nblocks + 255) / 256 : 65536);
   hipLaunchKernelGGL(q4k_repack_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
                      static_cast<const uint8_t*>(src), nblocks, static_cast<uint8_t*>(qs),
-                     static_cast<uint8_t*>(hdr));
+                     static_cast<uint32_t*>(scm), static_cast<uint32_t*>(dm));
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

@@ -43,7 +43,7 @@ def _lib():
             lib.amdk8s_llm_dequant.restype = ci
             lib.amdk8s_llm_q6k_repack.argtypes = [vp, cl, vp, vp, vp, vp, vp]
             lib.amdk8s_llm_q6k_repack.restype = ci
-            lib.amdk8s_llm_q4k_repack.argtypes = [vp, cl, vp, vp, vp]
+            lib.amdk8s_llm_q4k_repack.argtypes = [vp, cl, vp, vp, vp, vp]
             lib.amdk8s_llm_q4k_repack.restype = ci
             lib.amdk8s_llm_q6k_repack.restype = ci
             _declared = True
@@ -132,6 +132,7 @@ def q6k_repack(raw, ql, qh, sc, d) -> None:
            "amdk8s_llm_q6k_repack")
 
 
-def q4k_repack(raw, qs, hdr) -> None:
+def q4k_repack(raw, qs, scm, dm) -> None:
     _check(_lib().amdk8s_llm_q4k_repack(raw.data_ptr(), raw.numel() // 144, qs.data_ptr(),
-                                        hdr.data_ptr(), _stream(raw)), "amdk8s_llm_q4k_repack")
+                                        scm.data_ptr(), dm.data_ptr(), _stream(raw)),
+           "amdk8s_llm_q4k_repack")
