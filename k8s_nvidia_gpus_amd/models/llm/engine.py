@@ -6,9 +6,10 @@ cluster-config/apps/llm/deployment.yaml:61-84); this is the in-tree MI355X engin
 kind of server (``server.py``).  Design points:
 
 * **Decode (the hot loop)** is HBM-bound: per token every weight byte is read once.  Per layer:
-  RMSNorm+Q8-quantise → fused q|k|v GEMV (+bias) → RoPE + KV-cache write → split-context
-  attention + combine + Q8-quantise → o_proj GEMV (+= residual) → RMSNorm+Q8 → gate|up pair GEMV
-  (SwiGLU epilogue) → Q8 → ffn_down GEMV (+= residual); then the final norm and the lm_head.
+  fused q|k|v GEMV (RMSNorm + Q8 quantisation in its prologue, +bias) → split-context attention
+  (RoPE and the KV-cache write fused in) + combine + Q8 → o_proj GEMV (+= residual) → gate|up
+  pair GEMV (RMSNorm prologue, SwiGLU epilogue) → ffn_down GEMV (Q8 prologue, += residual); then
+  the final norm and the lm_head: 6 launches per layer.
   ``T <= 4`` concurrent sequences share one weight pass (continuous batching).  Every step of a
   given ``T`` is captured once into a ``torch.cuda.CUDAGraph`` (a HIP graph on ROCm) and replayed,
   so the ~290 launches of a 28-layer step cost no host time.
@@ -67,7 +68,7 @@ class StepBuffers:
     pml: torch.Tensor
     t: torch.Tensor
     logits: torch.Tensor
-    graphs: Dict[int, torch.cuda.CUDAGraph] = None   # keyed by attention span
+    graphs: Dict[tuple, torch.cuda.CUDAGraph] = None   # keyed by (attention span, fused rope)
 
 
 class Engine:
@@ -199,7 +200,9 @@ class Engine:
             span *= 2
         return min(span, self.max_ctx)
 
-    def _step_kernels(self, b: StepBuffers, span: int) -> None:
+    def _step_kernels(self, b: StepBuffers, span: int, fused: bool) -> None:
+        """One decode step.  ``fused``: every token in its own slot, so RoPE + the KV write run
+        inside the attention kernel (no rope_kv launch)."""
         LK, c = self.LK, self.cfg
         LK.dequant(self.w.tok_embd, b.h, rows=b.tok)          # embedding rows → residual
         qd = self._q8(b, c.dim)
@@ -212,11 +215,16 @@ class Engine:
                 LK.qgemv(w, None, None, None, b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:],
                          ldo=b.qkv.stride(0), xf=b.h, norm_w=L.attn_norm, eps=c.eps, **G)
                 off += w.n
-            LK.rope_kv(b.qkv, b.pos, b.slot, self.cos, self.sin, c.heads, c.kv_heads, c.head_dim,
-                       self.max_ctx, b.qrot, self.k_cache[i], self.v_cache[i])
-            LK.attn_decode(b.qrot, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
-                           c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
-                           span=span)
+            if fused:
+                LK.attn_decode(None, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
+                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
+                               span=span, qkv=b.qkv, cos_t=self.cos, sin_t=self.sin)
+            else:
+                LK.rope_kv(b.qkv, b.pos, b.slot, self.cos, self.sin, c.heads, c.kv_heads,
+                           c.head_dim, self.max_ctx, b.qrot, self.k_cache[i], self.v_cache[i])
+                LK.attn_decode(b.qrot, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
+                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
+                               span=span)
             LK.qgemv(L.wo, *qd, b.h, LK.RESID, **G)
             LK.qgemv(L.wg, None, None, None, b.t, LK.PAIR, w1=L.wu, xf=b.h, norm_w=L.ffn_norm,
                      eps=c.eps, **G)
@@ -233,24 +241,25 @@ class Engine:
         b.pos.copy_(host[1])
         b.slot.copy_(host[2])
         span = self._span(max(positions))
+        fused = len(set(slots)) == len(slots)
         if self.use_graphs:
             if b.graphs is None:
                 b.graphs = {}
-            g = b.graphs.get(span)
+            g = b.graphs.get((span, fused))
             if g is None:
                 s = torch.cuda.Stream(self.device)
                 s.wait_stream(torch.cuda.current_stream(self.device))
                 with torch.cuda.stream(s):
-                    self._step_kernels(b, span)       # warm-up outside capture
+                    self._step_kernels(b, span, fused)      # warm-up outside capture
                 torch.cuda.current_stream(self.device).wait_stream(s)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    self._step_kernels(b, span)
-                b.graphs[span] = g
+                    self._step_kernels(b, span, fused)
+                b.graphs[(span, fused)] = g
                 self.stats["graph_captures"] += 1
             g.replay()
         else:
-            self._step_kernels(b, span)
+            self._step_kernels(b, span, fused)
         return b.logits
 
     # ------------------------------------------------------------------ public API

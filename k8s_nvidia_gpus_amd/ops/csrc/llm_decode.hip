@@ -303,31 +303,62 @@ __global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
     // itself, which removes a launch and its boundary per matrix.  All T tokens are processed
     // together (their loads in flight at once); per token the thread mapping and reduction order
     // do not depend on T, so results are batch-invariant.
-    float rs[T];
+    // chunk c = 8 values; 4 consecutive chunks (one lane quad) = one 32-value block.  Whole
+    // quads leave the loops together (K % 256 == 0).
+    auto quantise = [&](int t, int c, float (&v)[8], float r, const float (&wv)[8]) {
+      if (a.norm_w) {
 #pragma unroll
-    for (int t = 0; t < T; ++t) rs[t] = 1.f;
-    if (a.norm_w) {
+        for (int i = 0; i < 8; ++i) v[i] *= r * wv[i];
+      }
+      float amax = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
+      amax = fmaxf(amax, __shfl_xor(amax, 1, kWave));
+      amax = fmaxf(amax, __shfl_xor(amax, 2, kWave));
+      const float d = amax / 127.f;
+      const float id = d > 0.f ? 1.f / d : 0.f;
+      uint32_t pk0 = 0u, pk1 = 0u;
+      int sq = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int q = (int)__builtin_rintf(v[i] * id);
+        if (i < 4) pk0 |= ((uint32_t)(q & 0xff)) << (8 * i);
+        else pk1 |= ((uint32_t)(q & 0xff)) << (8 * (i - 4));
+        sq += q;
+      }
+      sq += __shfl_xor(sq, 1, kWave);
+      *reinterpret_cast<uint2*>(xs + t * xstride + xoff(c * 8)) = make_uint2(pk0, pk1);
+      if ((c & 3) == 0) dxs[t * (K >> 5) + (c >> 2)] = d;
+      if ((c & 1) == 0) sxs[t * (K >> 4) + (c >> 1)] = d * (float)sq;
+    };
+    auto load8 = [&](const float* p, float (&v)[8]) {
+      const float4 x0 = *reinterpret_cast<const float4*>(p);
+      const float4 x1 = *reinterpret_cast<const float4*>(p + 4);
+      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
+      v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+    };
+    const int nch = K >> 3;
+    if (a.norm_w && nch <= 2 * (int)blockDim.x) {
+      // single pass: each thread keeps its (<= 2) chunks of every token in registers for the
+      // sum of squares and the quantisation — one L2 round trip instead of two
+      float v[T][2][8], wv[2][8];
       float ss[T];
 #pragma unroll
-      for (int t = 0; t < T; ++t) ss[t] = 0.f;
-      for (int i0 = threadIdx.x * 4; i0 < K; i0 += blockDim.x * 8) {
-        float4 v[T][2];
+      for (int u = 0; u < 2; ++u) {
+        const int c = min((int)threadIdx.x + u * (int)blockDim.x, nch - 1);
+        load8(a.norm_w + c * 8, wv[u]);
 #pragma unroll
-        for (int t = 0; t < T; ++t)
-#pragma unroll
-          for (int u = 0; u < 2; ++u)
-            v[t][u] = *reinterpret_cast<const float4*>(
-                a.xf + (long)t * a.ldx + min(i0 + u * (int)blockDim.x * 4, K - 4));
-#pragma unroll
-        for (int t = 0; t < T; ++t)
-#pragma unroll
-          for (int u = 0; u < 2; ++u)
-            if (i0 + u * (int)blockDim.x * 4 < K)
-              ss[t] += v[t][u].x * v[t][u].x + v[t][u].y * v[t][u].y + v[t][u].z * v[t][u].z +
-                       v[t][u].w * v[t][u].w;
+        for (int t = 0; t < T; ++t) load8(a.xf + (long)t * a.ldx + c * 8, v[t][u]);
       }
 #pragma unroll
       for (int t = 0; t < T; ++t) {
+        ss[t] = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          if ((int)threadIdx.x + u * (int)blockDim.x < nch) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ss[t] += v[t][u][i] * v[t][u][i];
+          }
         ss[t] = wave_sum(ss[t]);
         if (lane == 0) red[wave * T + t] = ss[t];
       }
@@ -336,51 +367,57 @@ __global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
       for (int t = 0; t < T; ++t) {
         float tot = 0.f;
         for (int w = 0; w < W; ++w) tot += red[w * T + t];
-        rs[t] = rsqrtf(tot / (float)K + a.eps);
+        const float r = rsqrtf(tot / (float)K + a.eps);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int c = (int)threadIdx.x + u * (int)blockDim.x;
+          if (c < nch) quantise(t, c, v[t][u], r, wv[u]);
+        }
       }
-    }
-    // chunk c = 8 values; 4 consecutive chunks (one lane quad) = one 32-value block
-    for (int c = threadIdx.x; c < (K >> 3); c += blockDim.x) {   // whole quads leave together
-      float v[T][8];
-      float4 w0 = make_float4(1.f, 1.f, 1.f, 1.f), w1 = w0;
+    } else {
+      float rs[T];
+#pragma unroll
+      for (int t = 0; t < T; ++t) rs[t] = 1.f;
       if (a.norm_w) {
-        w0 = *reinterpret_cast<const float4*>(a.norm_w + c * 8);
-        w1 = *reinterpret_cast<const float4*>(a.norm_w + c * 8 + 4);
-      }
+        float ss[T];
 #pragma unroll
-      for (int t = 0; t < T; ++t) {
-        const float4 x0 = *reinterpret_cast<const float4*>(a.xf + (long)t * a.ldx + c * 8);
-        const float4 x1 = *reinterpret_cast<const float4*>(a.xf + (long)t * a.ldx + c * 8 + 4);
-        v[t][0] = x0.x; v[t][1] = x0.y; v[t][2] = x0.z; v[t][3] = x0.w;
-        v[t][4] = x1.x; v[t][5] = x1.y; v[t][6] = x1.z; v[t][7] = x1.w;
-      }
-      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        for (int t = 0; t < T; ++t) ss[t] = 0.f;
+        for (int i0 = threadIdx.x * 4; i0 < K; i0 += blockDim.x * 8) {
+          float4 v[T][2];
 #pragma unroll
-      for (int t = 0; t < T; ++t) {
-        if (a.norm_w) {
+          for (int t = 0; t < T; ++t)
 #pragma unroll
-          for (int i = 0; i < 8; ++i) v[t][i] *= rs[t] * wv[i];
+            for (int u = 0; u < 2; ++u)
+              v[t][u] = *reinterpret_cast<const float4*>(
+                  a.xf + (long)t * a.ldx + min(i0 + u * (int)blockDim.x * 4, K - 4));
+#pragma unroll
+          for (int t = 0; t < T; ++t)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+              if (i0 + u * (int)blockDim.x * 4 < K)
+                ss[t] += v[t][u].x * v[t][u].x + v[t][u].y * v[t][u].y +
+                         v[t][u].z * v[t][u].z + v[t][u].w * v[t][u].w;
         }
-        float amax = 0.f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[t][i]));
-        amax = fmaxf(amax, __shfl_xor(amax, 1, kWave));
-        amax = fmaxf(amax, __shfl_xor(amax, 2, kWave));
-        const float d = amax / 127.f;
-        const float id = d > 0.f ? 1.f / d : 0.f;
-        uint32_t pk0 = 0u, pk1 = 0u;
-        int sq = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int q = (int)__builtin_rintf(v[t][i] * id);
-          if (i < 4) pk0 |= ((uint32_t)(q & 0xff)) << (8 * i);
-          else pk1 |= ((uint32_t)(q & 0xff)) << (8 * (i - 4));
-          sq += q;
+        for (int t = 0; t < T; ++t) {
+          ss[t] = wave_sum(ss[t]);
+          if (lane == 0) red[wave * T + t] = ss[t];
         }
-        sq += __shfl_xor(sq, 1, kWave);
-        *reinterpret_cast<uint2*>(xs + t * xstride + xoff(c * 8)) = make_uint2(pk0, pk1);
-        if ((c & 3) == 0) dxs[t * (K >> 5) + (c >> 2)] = d;
-        if ((c & 1) == 0) sxs[t * (K >> 4) + (c >> 1)] = d * (float)sq;
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          float tot = 0.f;
+          for (int w = 0; w < W; ++w) tot += red[w * T + t];
+          rs[t] = rsqrtf(tot / (float)K + a.eps);
+        }
+      }
+      for (int c = threadIdx.x; c < nch; c += blockDim.x) {
+        float v[T][8], wv[8];
+        if (a.norm_w) load8(a.norm_w + c * 8, wv);
+#pragma unroll
+        for (int t = 0; t < T; ++t) load8(a.xf + (long)t * a.ldx + c * 8, v[t]);
+#pragma unroll
+        for (int t = 0; t < T; ++t) quantise(t, c, v[t], rs[t], wv);
       }
     }
   }
@@ -522,16 +559,40 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(const float* __restrict__ 
 // all four 16-byte K loads in flight), softmax by one wave (lane = position), P.V: wave w takes
 // 16 positions with all 16 V loads in flight, lane = 2 dims.  Writes the unnormalised partial
 // output and (max, sum) per head.
+// Fused form (qkv != null): the workgroup rotates its q heads from the raw q|k|v projection
+// itself, and the one workgroup per (token, kv head) whose chunk holds the new position also
+// rotates k, writes K/V to the cache and uses them from LDS — which replaces rope_kv_kernel and its
+// launch.  Valid when every token of the step is in its own slot (decode); chunked prefill of one
+// sequence through this path keeps the separate rope_kv_kernel.
+struct AttnArgs {
+  const float* q;        // rotated q [T][H*128] (unfused)
+  const float* qkv;      // raw projection [T][ldq] (fused) or null
+  int ldq;
+  const float* cos_t;
+  const float* sin_t;
+  const int* pos;
+  const int* slot;
+  uint16_t* kc;
+  uint16_t* vc;
+  int H, Hkv, max_ctx, nsplit;
+  float scale;
+  float* po;
+  float* pml;
+};
+
 template <int G>
-__global__ void __launch_bounds__(256) attn_decode_kernel(const float* __restrict__ q,
-                                                          const int* __restrict__ pos,
-                                                          const int* __restrict__ slot,
-                                                          const uint16_t* __restrict__ kc,
-                                                          const uint16_t* __restrict__ vc,
-                                                          int H, int Hkv, int max_ctx, int nsplit,
-                                                          float scale, float* __restrict__ po,
-                                                          float* __restrict__ pml) {
+__global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
+  const float* __restrict__ q = a.q;
+  const int* __restrict__ pos = a.pos;
+  const int* __restrict__ slot = a.slot;
+  const uint16_t* __restrict__ kc = a.kc;
+  const uint16_t* __restrict__ vc = a.vc;
+  const int H = a.H, Hkv = a.Hkv, max_ctx = a.max_ctx, nsplit = a.nsplit;
+  const float scale = a.scale;
+  float* __restrict__ po = a.po;
+  float* __restrict__ pml = a.pml;
   __shared__ float qs[G][kHeadDim];
+  __shared__ __align__(16) uint16_t knew[kHeadDim];   // the new position's rotated K (fp16)
   __shared__ float ps[G][kAttnChunk];
   __shared__ float mls[G][2];
   __shared__ float opart[4][G][kHeadDim];
@@ -560,9 +621,46 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(const float* __restric
 #pragma unroll
     for (int c = 0; c < 4; ++c) kv[c] = kr[c];
   }
-  for (int i = threadIdx.x; i < G * kHeadDim; i += blockDim.x)
-    qs[i / kHeadDim][i % kHeadDim] = q[(long)t * H * kHeadDim + (kh * G) * kHeadDim + i] * scale;
+  const int pnew = len - 1;
+  const bool own = a.qkv != nullptr && pnew >= p0 && pnew < p0 + kAttnChunk;
+  if (a.qkv) {
+    const float* row = a.qkv + (long)t * a.ldq;
+    const float* ct = a.cos_t + (long)pnew * (kHeadDim / 2);
+    const float* st = a.sin_t + (long)pnew * (kHeadDim / 2);
+    for (int i = threadIdx.x; i < G * (kHeadDim / 2); i += blockDim.x) {
+      const int g = i / (kHeadDim / 2), j = i % (kHeadDim / 2);
+      const float x0 = row[(kh * G + g) * kHeadDim + j];
+      const float x1 = row[(kh * G + g) * kHeadDim + j + kHeadDim / 2];
+      const float c = ct[j], sn = st[j];
+      qs[g][j] = (x0 * c - x1 * sn) * scale;
+      qs[g][j + kHeadDim / 2] = (x0 * sn + x1 * c) * scale;
+    }
+    if (own) {
+      const long cpos = cbase + (long)pnew * kHeadDim;
+      if (threadIdx.x < kHeadDim / 2) {
+        const int j = threadIdx.x;
+        const float x0 = row[(H + kh) * kHeadDim + j];
+        const float x1 = row[(H + kh) * kHeadDim + j + kHeadDim / 2];
+        const float c = ct[j], sn = st[j];
+        const uint16_t h0 = f2h(x0 * c - x1 * sn), h1 = f2h(x0 * sn + x1 * c);
+        a.kc[cpos + j] = h0;
+        a.kc[cpos + j + kHeadDim / 2] = h1;
+        knew[j] = h0;
+        knew[j + kHeadDim / 2] = h1;
+      } else if (threadIdx.x < kHeadDim / 2 + kHeadDim) {
+        const int e = threadIdx.x - kHeadDim / 2;
+        a.vc[cpos + e] = f2h(row[(H + Hkv + kh) * kHeadDim + e]);
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < G * kHeadDim; i += blockDim.x)
+      qs[i / kHeadDim][i % kHeadDim] = q[(long)t * H * kHeadDim + (kh * G) * kHeadDim + i] * scale;
+  }
   __syncthreads();
+  if (own && p0 + pi == pnew) {   // the new position: its K row was loaded before it was written
+#pragma unroll
+    for (int c = 0; c < 4; ++c) kv[c] = reinterpret_cast<const uint4*>(knew)[qd * 4 + c];
+  }
   float sc[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) sc[g] = 0.f;
@@ -619,6 +717,8 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(const float* __restric
   for (int g = 0; g < G; ++g) o[g][0] = o[g][1] = 0.f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
+    // V rows are loaded after the barrier that follows this workgroup's own KV write, so the
+    // new position reads back what was just stored (workgroup-scope visibility)
     const float v0 = h2f(vv[j] & 0xffffu), v1 = h2f(vv[j] >> 16);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -903,8 +1003,11 @@ int amdk8s_llm_rope_kv(const void* qkv, int ldq, const void* pos, const void* sl
 // po/pml: workspace [T][H][nsplit][128] / [T][H][nsplit][2]; out (nullable) fp32 [T][H*128].
 // span: positions covered by this launch (a multiple of 64, <= max_ctx, > every pos[t]); the
 // caller buckets it so a captured graph does not launch empty chunks up to max_ctx.
-int amdk8s_llm_attn_decode(const void* q, const void* pos, const void* slot, const void* kc,
-                           const void* vc, int H, int Hkv, int head_dim, int max_ctx, int span,
+// qkv (nullable): the raw q|k|v projection [T][ldq] — fused RoPE + KV write (distinct slots
+// only, see attn_decode_kernel); q is then unused.
+int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* cos_t,
+                           const void* sin_t, const void* pos, const void* slot, void* kc,
+                           void* vc, int H, int Hkv, int head_dim, int max_ctx, int span,
                            float scale, void* po, void* pml, void* out, void* x8, void* dx,
                            void* sx, int T, void* stream) {
   if (span <= 0) span = max_ctx;
@@ -914,12 +1017,23 @@ int amdk8s_llm_attn_decode(const void* q, const void* pos, const void* slot, con
   const int nsplit = span / kAttnChunk;
   hipStream_t st = static_cast<hipStream_t>(stream);
   // the GQA group size is a template parameter: fully unrolled head loops, no per-head branches
+  AttnArgs aa;
+  aa.q = static_cast<const float*>(q);
+  aa.qkv = static_cast<const float*>(qkv);
+  aa.ldq = ldq;
+  aa.cos_t = static_cast<const float*>(cos_t);
+  aa.sin_t = static_cast<const float*>(sin_t);
+  aa.pos = static_cast<const int*>(pos);
+  aa.slot = static_cast<const int*>(slot);
+  aa.kc = static_cast<uint16_t*>(kc);
+  aa.vc = static_cast<uint16_t*>(vc);
+  aa.H = H; aa.Hkv = Hkv; aa.max_ctx = max_ctx; aa.nsplit = nsplit; aa.scale = scale;
+  aa.po = static_cast<float*>(po);
+  aa.pml = static_cast<float*>(pml);
+  if (!qkv && !q) return 2;
+  if (qkv && (!cos_t || !sin_t)) return 2;
   auto launch = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(Hkv, nsplit, T), dim3(256), 0, st,
-                       static_cast<const float*>(q), static_cast<const int*>(pos),
-                       static_cast<const int*>(slot), static_cast<const uint16_t*>(kc),
-                       static_cast<const uint16_t*>(vc), H, Hkv, max_ctx, nsplit, scale,
-                       static_cast<float*>(po), static_cast<float*>(pml));
+    hipLaunchKernelGGL(kern, dim3(Hkv, nsplit, T), dim3(256), 0, st, aa);
   };
   switch (H / Hkv) {
     case 1: launch(attn_decode_kernel<1>); break;

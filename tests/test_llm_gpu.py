@@ -200,6 +200,42 @@ def test_rope_kv_and_decode_attention(dev, LK, H, Hkv):
     assert ((xq - out).abs() <= dx.repeat_interleave(32, 1) * 0.5 + 1e-5).all()
 
 
+@pytest.mark.parametrize("H,Hkv", [(28, 4), (8, 8)])
+def test_fused_rope_attention_equals_separate_kernels(dev, LK, H, Hkv):
+    """Distinct slots: RoPE + KV write inside the attention kernel == rope_kv + attention."""
+    from k8s_nvidia_gpus_amd.models.llm.engine import rope_tables
+
+    torch.manual_seed(3)
+    max_ctx, slots, T = 1024, 4, 4
+    base_k = (torch.randn(slots, Hkv, max_ctx, 128, device=dev) * 0.5).half()
+    base_v = torch.randn(slots, Hkv, max_ctx, 128, device=dev).half()
+    cos, sin = rope_tables(max_ctx, 128, 1.0e6, dev)
+    pos = torch.tensor([0, 63, 64, 700], dtype=torch.int32, device=dev)
+    slot = torch.tensor([3, 0, 1, 2], dtype=torch.int32, device=dev)
+    qkv = torch.randn(T, (H + 2 * Hkv) * 128, device=dev)
+    outs = []
+    for fused in (False, True):
+        kc, vc = base_k.clone(), base_v.clone()
+        nsplit = max_ctx // LK.attn_chunk()
+        po = torch.empty(T, H, nsplit, 128, device=dev)
+        pml = torch.empty(T, H, nsplit, 2, device=dev)
+        x8 = torch.empty(T, H * 128, dtype=torch.int8, device=dev)
+        dx = torch.empty(T, H * 4, device=dev)
+        sx = torch.empty(T, H * 8, device=dev)
+        out = torch.empty(T, H * 128, device=dev)
+        if fused:
+            LK.attn_decode(None, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po,
+                           pml, x8, dx, sx, out=out, qkv=qkv, cos_t=cos, sin_t=sin)
+        else:
+            qrot = torch.empty(T, H * 128, device=dev)
+            LK.rope_kv(qkv, pos, slot, cos, sin, H, Hkv, 128, max_ctx, qrot, kc, vc)
+            LK.attn_decode(qrot, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po,
+                           pml, x8, dx, sx, out=out)
+        outs.append((kc, vc, out))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    torch.testing.assert_close(outs[1][2], outs[0][2], rtol=1e-5, atol=1e-5)
+
+
 @pytest.fixture(scope="module")
 def tiny_gguf(tmp_path_factory):
     from k8s_nvidia_gpus_amd.models.llm import tiny
