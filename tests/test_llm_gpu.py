@@ -315,3 +315,38 @@ def test_random_7b_layer_shapes_run(dev):
     assert torch.isfinite(ln).all() and torch.isfinite(ld).all()
     cos = torch.nn.functional.cosine_similarity(ln[None], ld[None]).item()
     assert cos > 0.98, cos
+
+
+def test_server_on_gpu_concurrent_answers_equal_sequential(dev, tiny_gguf):
+    """The llama-server-compatible API on the GPU engine: 6 concurrent greedy requests share
+    decode steps (continuous batching over 4 slots) and still return exactly their sequential
+    answers — the decode kernels are batch-invariant."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from fastapi.testclient import TestClient
+
+    from k8s_nvidia_gpus_amd.models.llm.server import Scheduler, create_app
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load
+
+    eng, tok = load(tiny_gguf, device=dev, max_ctx=512, slots=4)
+    eng.capture((1, 2, 3, 4))
+    state = {"scheduler": Scheduler(eng, tok, parallel=4), "tok": tok, "model": "tiny"}
+    c = TestClient(create_app(state))
+    try:
+        prompts = [f"a cozy cabin number {i} in the woods" for i in range(6)]
+        body = lambda p: {"prompt": p, "n_predict": 12, "temperature": 0}  # noqa: E731
+        seq = [c.post("/completion", json=body(p)).json()["content"] for p in prompts]
+        m0 = dict(state["scheduler"].metrics)
+        with ThreadPoolExecutor(6) as ex:
+            par = list(ex.map(lambda p: c.post("/completion", json=body(p)).json()["content"],
+                              prompts))
+        m1 = state["scheduler"].metrics
+        assert par == seq
+        assert m1["tokens_predicted_total"] - m0["tokens_predicted_total"] > \
+            m1["decode_steps_total"] - m0["decode_steps_total"]        # multi-sequence steps
+        r = c.post("/v1/chat/completions", json={
+            "messages": [{"role": "user", "content": "hello"}], "max_tokens": 8,
+            "temperature": 0}).json()
+        assert r["usage"]["completion_tokens"] <= 8
+    finally:
+        state["scheduler"].close()
