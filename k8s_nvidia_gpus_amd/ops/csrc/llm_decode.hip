@@ -141,44 +141,63 @@ struct XView {           // the workgroup's staged activations
   int xstride, dstride, sstride;
 };
 
-template <int TYPE, int T>
-__device__ __forceinline__ void dot_blk(const Blk<TYPE>& r, int blk, int sub, const XView& x,
-                                        float* acc) {
+// One lane's activations for one super-block and one token: 2 x 16 int8 + their scales / sums.
+struct XReg {
+  uint4 xl, xh;
+  float dxl, dxh, sxl, sxh;
+};
+
+template <int TYPE>
+__device__ __forceinline__ XReg load_x(const XView& x, int t, int blk, int sub) {
+  XReg r;
   if constexpr (TYPE == kQ4K) {
-    const int c = sub >> 1;               // 64-weight chunk: sub-blocks 2c (low) and 2c+1 (high)
+    const int p_lo = blk * 256 + (sub >> 1) * 64 + (sub & 1) * 16;   // low run; high = +32
+    const int g_lo = p_lo >> 4, d_lo = p_lo >> 5;
+    r.xl = *reinterpret_cast<const uint4*>(x.xs + t * x.xstride + xoff(p_lo));
+    r.xh = *reinterpret_cast<const uint4*>(x.xs + t * x.xstride + xoff(p_lo + 32));
+    const float2 dxv = *reinterpret_cast<const float2*>(x.dxs + t * x.dstride + d_lo);
+    r.dxl = dxv.x; r.dxh = dxv.y;
+    r.sxl = x.sxs[t * x.sstride + g_lo]; r.sxh = x.sxs[t * x.sstride + g_lo + 2];
+  } else {
+    const int n = sub >> 2, h1 = sub & 1, klo = (sub & 3) >> 1;
+    const int p_lo = blk * 256 + n * 128 + klo * 32 + h1 * 16;       // low run; high = +64
+    const int g_lo = p_lo >> 4, d_lo = p_lo >> 5;
+    r.xl = *reinterpret_cast<const uint4*>(x.xs + t * x.xstride + xoff(p_lo));
+    r.xh = *reinterpret_cast<const uint4*>(x.xs + t * x.xstride + xoff(p_lo + 64));
+    r.dxl = x.dxs[t * x.dstride + d_lo]; r.dxh = x.dxs[t * x.dstride + d_lo + 2];
+    r.sxl = x.sxs[t * x.sstride + g_lo]; r.sxh = x.sxs[t * x.sstride + g_lo + 4];
+  }
+  return r;
+}
+
+// acc += (this lane's part of) w . x for one super-block.  Explicit roundings: the same
+// instruction sequence for every T instantiation and activation source (LDS or registers), so a
+// token's result does not depend on how many sequences share the step (batch-invariant decode).
+template <int TYPE>
+__device__ __forceinline__ float dot_core(const Blk<TYPE>& r, int sub, const XReg& x, float acc) {
+  if constexpr (TYPE == kQ4K) {
     const float d = h2f(r.dd & 0xffffu), dmin = h2f(r.dd >> 16);
     // the lane's two scales and mins were decoded from the 6-bit packing at load time
     const uint32_t sc0 = r.sm & 0xffu, sc1 = (r.sm >> 8) & 0xffu;
     const uint32_t m0 = (r.sm >> 16) & 0xffu, m1 = r.sm >> 24;
-    const uint32_t q[4] = {r.q.x, r.q.y, r.q.z, r.q.w};
-    const int p_lo = blk * 256 + c * 64 + (sub & 1) * 16;
-    const int g_lo = p_lo >> 4, d_lo = p_lo >> 5;
-    // explicit roundings: the same instruction sequence for every T instantiation, so a token's
-    // result does not depend on how many sequences share the step (batch-invariant decode)
     const float dsc0 = __fmul_rn(d, (float)sc0), dsc1 = __fmul_rn(d, (float)sc1);
     const float dm0 = __fmul_rn(dmin, (float)m0), dm1 = __fmul_rn(dmin, (float)m1);
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const uint4 xl = *reinterpret_cast<const uint4*>(x.xs + t * x.xstride + xoff(p_lo));
-      const uint4 xh = *reinterpret_cast<const uint4*>(x.xs + t * x.xstride + xoff(p_lo + 32));
-      int il = 0, ih = 0;
-      il = dot4(q[0] & 0x0f0f0f0fu, xl.x, il);
-      il = dot4(q[1] & 0x0f0f0f0fu, xl.y, il);
-      il = dot4(q[2] & 0x0f0f0f0fu, xl.z, il);
-      il = dot4(q[3] & 0x0f0f0f0fu, xl.w, il);
-      ih = dot4((q[0] >> 4) & 0x0f0f0f0fu, xh.x, ih);
-      ih = dot4((q[1] >> 4) & 0x0f0f0f0fu, xh.y, ih);
-      ih = dot4((q[2] >> 4) & 0x0f0f0f0fu, xh.z, ih);
-      ih = dot4((q[3] >> 4) & 0x0f0f0f0fu, xh.w, ih);
-      const float2 dxv = *reinterpret_cast<const float2*>(x.dxs + t * x.dstride + d_lo);
-      const float sxl = x.sxs[t * x.sstride + g_lo], sxh = x.sxs[t * x.sstride + g_lo + 2];
-      float a = __fmaf_rn(__fmul_rn(dsc0, dxv.x), (float)il, acc[t]);
-      a = __fmaf_rn(__fmul_rn(dsc1, dxv.y), (float)ih, a);
-      a = __fmaf_rn(-dm0, sxl, a);
-      acc[t] = __fmaf_rn(-dm1, sxh, a);
-    }
+    const uint32_t q[4] = {r.q.x, r.q.y, r.q.z, r.q.w};
+    int il = 0, ih = 0;
+    il = dot4(q[0] & 0x0f0f0f0fu, x.xl.x, il);
+    il = dot4(q[1] & 0x0f0f0f0fu, x.xl.y, il);
+    il = dot4(q[2] & 0x0f0f0f0fu, x.xl.z, il);
+    il = dot4(q[3] & 0x0f0f0f0fu, x.xl.w, il);
+    ih = dot4((q[0] >> 4) & 0x0f0f0f0fu, x.xh.x, ih);
+    ih = dot4((q[1] >> 4) & 0x0f0f0f0fu, x.xh.y, ih);
+    ih = dot4((q[2] >> 4) & 0x0f0f0f0fu, x.xh.z, ih);
+    ih = dot4((q[3] >> 4) & 0x0f0f0f0fu, x.xh.w, ih);
+    float a = __fmaf_rn(__fmul_rn(dsc0, x.dxl), (float)il, acc);
+    a = __fmaf_rn(__fmul_rn(dsc1, x.dxh), (float)ih, a);
+    a = __fmaf_rn(-dm0, x.sxl, a);
+    return __fmaf_rn(-dm1, x.sxh, a);
   } else {
-    const int n = sub >> 2, h1 = sub & 1, klo = (sub & 3) >> 1;
+    const int klo = (sub & 3) >> 1;
     const float d = h2f(r.d & 0xffffu);
     // scales 8n + h1 + 2klo and that + 4, stored adjacent for this lane (q6_scale_pos)
     const float sc0 = __fmul_rn(d, (float)(int8_t)(r.s2 & 0xffu));
@@ -192,24 +211,22 @@ __device__ __forceinline__ void dot_blk(const Blk<TYPE>& r, int blk, int sub, co
       qlo[i] = (l[i] & 0x0f0f0f0fu) | (((hb[i] >> sh) & 0x03030303u) << 4);
       qhi[i] = ((l[i] >> 4) & 0x0f0f0f0fu) | (((hb[i] >> (sh + 4)) & 0x03030303u) << 4);
     }
-    const int p_lo = blk * 256 + n * 128 + klo * 32 + h1 * 16;
-    const int g_lo = p_lo >> 4, d_lo = p_lo >> 5;
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const uint4 xl = *reinterpret_cast<const uint4*>(x.xs + t * x.xstride + xoff(p_lo));
-      const uint4 xh = *reinterpret_cast<const uint4*>(x.xs + t * x.xstride + xoff(p_lo + 64));
-      int il = 0, ih = 0;
-      il = dot4(qlo[0], xl.x, il); il = dot4(qlo[1], xl.y, il);
-      il = dot4(qlo[2], xl.z, il); il = dot4(qlo[3], xl.w, il);
-      ih = dot4(qhi[0], xh.x, ih); ih = dot4(qhi[1], xh.y, ih);
-      ih = dot4(qhi[2], xh.z, ih); ih = dot4(qhi[3], xh.w, ih);
-      const float dxl = x.dxs[t * x.dstride + d_lo], dxh = x.dxs[t * x.dstride + d_lo + 2];
-      const float sxl = x.sxs[t * x.sstride + g_lo], sxh = x.sxs[t * x.sstride + g_lo + 4];
-      const float u0 = __fmaf_rn(dxl, (float)il, __fmul_rn(-32.f, sxl));
-      const float u1 = __fmaf_rn(dxh, (float)ih, __fmul_rn(-32.f, sxh));
-      acc[t] = __fmaf_rn(sc1, u1, __fmaf_rn(sc0, u0, acc[t]));
-    }
+    int il = 0, ih = 0;
+    il = dot4(qlo[0], x.xl.x, il); il = dot4(qlo[1], x.xl.y, il);
+    il = dot4(qlo[2], x.xl.z, il); il = dot4(qlo[3], x.xl.w, il);
+    ih = dot4(qhi[0], x.xh.x, ih); ih = dot4(qhi[1], x.xh.y, ih);
+    ih = dot4(qhi[2], x.xh.z, ih); ih = dot4(qhi[3], x.xh.w, ih);
+    const float u0 = __fmaf_rn(x.dxl, (float)il, __fmul_rn(-32.f, x.sxl));
+    const float u1 = __fmaf_rn(x.dxh, (float)ih, __fmul_rn(-32.f, x.sxh));
+    return __fmaf_rn(sc1, u1, __fmaf_rn(sc0, u0, acc));
   }
+}
+
+template <int TYPE, int T>
+__device__ __forceinline__ void dot_blk(const Blk<TYPE>& r, int blk, int sub, const XView& x,
+                                        float* acc) {
+#pragma unroll
+  for (int t = 0; t < T; ++t) acc[t] = dot_core<TYPE>(r, sub, load_x<TYPE>(x, t, blk, sub), acc[t]);
 }
 
 // Blocks per lane per pipeline stage (one stage = 8*U super-blocks of a row).
@@ -268,9 +285,28 @@ __device__ __forceinline__ void finish_row(const GemvArgs& a, int row, int lane,
 // loads of item i+1 are in flight while item i is computed, across row boundaries, so a wave
 // always has a stage of weights on the way.  Item 0's loads are issued before the activations
 // are staged, so the staging (L2 → LDS → barrier) overlaps the first HBM round trip.
-template <int TYPE, int T, int MODE>
+template <int TYPE, int T, int MODE, int U>
+__device__ __forceinline__ void compute_reg(int nb, int sub, int bl, const XReg (&xr)[U][T],
+                                            const Blk<TYPE> (&c)[U], const Blk<TYPE> (&c1)[U],
+                                            float (&acc)[T], float (&acc1)[T]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (8 * u + bl < nb) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) acc[t] = dot_core<TYPE>(c[u], sub, xr[u][t], acc[t]);
+      if constexpr (MODE == kPair) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) acc1[t] = dot_core<TYPE>(c1[u], sub, xr[u][t], acc1[t]);
+      }
+    }
+  }
+}
+
+// REGX (a whole row is one stage, nb <= 8U): each lane touches the same <= U super-block columns
+// in every row, so its activations are read from LDS once into registers and every row after
+// that is pure weight streaming + VALU (no per-row LDS traffic).
+template <int TYPE, int T, int MODE, int U, bool REGX>
 __global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
-  constexpr int U = kBatch<TYPE, MODE>;
   extern __shared__ __align__(16) uint8_t lds[];
   const int K = a.K, nb = K >> 8;
   const int W = blockDim.x >> 6;
@@ -427,6 +463,23 @@ __global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
   float acc[T], acc1[T];
 #pragma unroll
   for (int t = 0; t < T; ++t) acc[t] = acc1[t] = 0.f;
+  if constexpr (REGX) {
+    XReg xr[U][T];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int t = 0; t < T; ++t) xr[u][t] = load_x<TYPE>(xv, t, min(8 * u + bl, nb - 1), sub);
+    for (int it = 0; it < nrows; it += 2) {
+      if (it + 1 < nrows) load_stage<TYPE, MODE, U>(a, r0 + (it + 1) * W, 0, nb, sub, bl, B, B1);
+      compute_reg<TYPE, T, MODE, U>(nb, sub, bl, xr, A, A1, acc, acc1);
+      finish_row<T, MODE>(a, r0 + it * W, lane, acc, acc1);
+      if (it + 1 >= nrows) break;
+      if (it + 2 < nrows) load_stage<TYPE, MODE, U>(a, r0 + (it + 2) * W, 0, nb, sub, bl, A, A1);
+      compute_reg<TYPE, T, MODE, U>(nb, sub, bl, xr, B, B1, acc, acc1);
+      finish_row<T, MODE>(a, r0 + (it + 1) * W, lane, acc, acc1);
+    }
+    return;
+  }
   for (int it = 0; it < items; it += 2) {
     if (it + 1 < items) {
       const int j = it + 1;
@@ -895,14 +948,33 @@ __global__ void q4k_repack_kernel(const uint8_t* __restrict__ src, long nblocks,
   }
 }
 
-template <int TYPE, int T, int MODE>
-int launch_gemv(const GemvArgs& a, int waves, hipStream_t st) {
+template <int TYPE, int T, int MODE, int U, bool REGX>
+int launch_one(const GemvArgs& a, int waves, hipStream_t st) {
   const int nb = a.K >> 8;
   const size_t lds = (size_t)T * (nb * 288 + (a.K >> 5) * 4 + (a.K >> 4) * 4) + 16 * T * 4;
   if (lds > 160 * 1024) return 3;
   const int grid = (a.N + a.rows_per_wg - 1) / a.rows_per_wg;
-  hipLaunchKernelGGL((qgemv_kernel<TYPE, T, MODE>), dim3(grid), dim3(waves * 64), lds, st, a);
+  hipLaunchKernelGGL((qgemv_kernel<TYPE, T, MODE, U, REGX>), dim3(grid), dim3(waves * 64), lds, st,
+                     a);
   return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// Stage width U (super-blocks per lane per stage): the smallest that covers a row in one stage
+// (short rows), else the type/mode batch; register-resident activations when a row is one stage
+// and U*T <= 4 (VGPR budget).  Every variant runs the same dot_core, so the choice never changes
+// a result bit.
+template <int TYPE, int T, int MODE>
+int launch_gemv(const GemvArgs& a, int waves, hipStream_t st) {
+  constexpr int KB = kBatch<TYPE, MODE>;
+  const int nb = a.K >> 8;
+  if (nb <= 8) return launch_one<TYPE, T, MODE, 1, true>(a, waves, st);
+  if constexpr (KB >= 2) {
+    if (nb <= 16) {
+      if constexpr (T <= 2) return launch_one<TYPE, T, MODE, 2, true>(a, waves, st);
+      else return launch_one<TYPE, T, MODE, 2, false>(a, waves, st);
+    }
+  }
+  return launch_one<TYPE, T, MODE, KB, false>(a, waves, st);
 }
 
 template <int TYPE, int MODE>

@@ -144,6 +144,29 @@ def test_qgemv_fp32_input_fused_norm(dev, LK, qt, T, norm):
     assert ((out.cpu() - full).norm() / full.norm()) < 0.02
 
 
+@pytest.mark.parametrize("qt", ["Q4_K", "Q6_K"])
+@pytest.mark.parametrize("K", [1536, 2304, 3584, 18944])
+def test_qgemv_batch_invariant_across_variants(dev, LK, qt, K):
+    """Every T (and so every kernel variant: register- or LDS-resident activations, stage width)
+    gives each token bit-identical results."""
+    from k8s_nvidia_gpus_amd.models.llm import gguf
+
+    w0, _ = _qw(64, K, getattr(gguf, qt), 9, dev)
+    w1, _ = _qw(64, K, getattr(gguf, qt), 10, dev)
+    torch.manual_seed(K)
+    x = torch.randn(4, K, device=dev)
+    nw = torch.rand(K, device=dev) + 0.5
+    for mode in (LK.STORE, LK.PAIR):
+        full = torch.zeros(4, 64, device=dev)
+        LK.qgemv(w0, None, None, None, full, mode, w1=w1 if mode == LK.PAIR else None, xf=x,
+                 norm_w=nw)
+        for T in (1, 2, 3):
+            part = torch.zeros(T, 64, device=dev)
+            LK.qgemv(w0, None, None, None, part, mode, w1=w1 if mode == LK.PAIR else None,
+                     xf=x[:T], norm_w=nw)
+            assert torch.equal(part, full[:T]), (mode, T)
+
+
 def _attn_ref(q, kc, vc, pos, slot, H, Hkv):
     T = q.shape[0]
     G = H // Hkv
