@@ -1,0 +1,168 @@
+"""Wan2.1 model family on MI355X: the row kernels (csrc/wan_ops.hip) vs PyTorch fp32 references, the
+native bf16 DiT vs the upstream-semantics fp32 forward, the tap-stacked VAE vs the upstream chunked
+decode, and the whole pipeline on the GPU."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from k8s_nvidia_gpus_amd.ops import kernels
+
+    lib = kernels.library()  # the in-tree .so — no fallback
+    assert hasattr(lib, "amdk8s_wan_add_ln") and hasattr(lib, "amdk8s_wan_rmsnorm_rope")
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def WK(dev):
+    from k8s_nvidia_gpus_amd.ops import wan_kernels
+
+    return wan_kernels
+
+
+@pytest.mark.parametrize("c", [512, 1536, 2048, 5120])
+@pytest.mark.parametrize("mode", ["gate", "plain", "none", "affine"])
+def test_add_ln_vs_fp32(WK, dev, c, mode):
+    from k8s_nvidia_gpus_amd.models.wan import functional as WF
+
+    g = torch.Generator(device=dev).manual_seed(c)
+    b, l = 2, 333
+    x = torch.randn(b, l, c, generator=g, device=dev) * 2 + 0.5
+    y = (torch.randn(b, l, c, generator=g, device=dev)).bfloat16() if mode != "none" else None
+    mods = torch.randn(b, 6, c, generator=g, device=dev)          # strided rows like the DiT's
+    gate = mods[:, 2] if mode == "gate" else None
+    if mode == "affine":
+        mul = torch.rand(1, c, generator=g, device=dev) + 0.5
+        add = torch.randn(1, c, generator=g, device=dev) * 0.1
+    else:
+        mul, add = 1.0 + mods[:, 1], mods[:, 0]
+    xr = x.clone()
+    out = WK.add_ln(x, y, gate, mul, add, 1e-6)
+    ref = WF.add_ln_ref(xr, y, gate, mul, add, 1e-6)
+    torch.testing.assert_close(x, xr, rtol=1e-5, atol=1e-5)          # residual update in place
+    torch.testing.assert_close(out.float(), ref.float(), rtol=2e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("c,heads,rope", [(1536, 12, True), (1536, 12, False), (512, 4, True),
+                                          (5120, 40, True)])
+def test_rmsnorm_rope_vs_fp32(WK, dev, c, heads, rope):
+    from k8s_nvidia_gpus_amd.models.wan import functional as WF
+
+    g = torch.Generator(device=dev).manual_seed(heads)
+    grid = (3, 6, 10)
+    l = grid[0] * grid[1] * grid[2]
+    qkv = (torch.randn(2, l, 3 * c, generator=g, device=dev) * 3).bfloat16()
+    wq = (torch.rand(c, generator=g, device=dev) + 0.5).bfloat16()
+    wk = (torch.rand(c, generator=g, device=dev) + 0.5).bfloat16()
+    cos, sin = WF.rope_table(grid, c // heads, device=dev) if rope else (None, None)
+    ref = qkv.clone()
+    WF.rmsnorm_rope_ref(ref[..., :c], wq, cos, sin, heads, 1e-6)
+    WF.rmsnorm_rope_ref(ref[..., c:2 * c], wk, cos, sin, heads, 1e-6)
+    WK.rmsnorm_rope(qkv[..., :c], wq, cos, sin, heads, 1e-6, w2=wk)
+    torch.testing.assert_close(qkv[..., :2 * c].float(), ref[..., :2 * c].float(), rtol=2e-2, atol=3e-2)
+    assert torch.equal(qkv[..., 2 * c:], ref[..., 2 * c:])           # v untouched
+
+
+def _randomise(model, scale=0.02):
+    with torch.no_grad():
+        for p in model.parameters():
+            p.add_(torch.randn_like(p) * scale)
+
+
+def test_dit_native_bf16_vs_upstream_fp32(dev):
+    from k8s_nvidia_gpus_amd.models.wan.config import WanDiTConfig
+    from k8s_nvidia_gpus_amd.models.wan.dit import WanDiT, reference_forward
+
+    torch.manual_seed(0)
+    cfg = WanDiTConfig(dim=512, ffn_dim=1024, freq_dim=64, heads=4, layers=3, text_dim=256,
+                       text_len=64)
+    m = WanDiT(cfg)
+    _randomise(m)
+    x = torch.randn(2, 16, 3, 16, 24)
+    t = torch.tensor([700.0, 700.0])
+    ctx = torch.randn(2, 20, cfg.text_dim)
+    ref = reference_forward(m, x, t, ctx)
+    mg = m.to(dev, torch.bfloat16).fuse()
+    kv = mg.text_kv(mg.embed_text(ctx.to(dev)))
+    y = mg(x.to(dev, torch.bfloat16), t.to(dev), kv).float().cpu()
+    err = (y - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 3e-2, err
+
+
+def test_dit_native_matches_torch_backend(dev):
+    """The kernels change nothing but rounding: native and the PyTorch dispatch agree in bf16."""
+    from k8s_nvidia_gpus_amd.models.sd15 import functional as SF
+    from k8s_nvidia_gpus_amd.models.wan import functional as WF
+    from k8s_nvidia_gpus_amd.models.wan.config import WanDiTConfig
+    from k8s_nvidia_gpus_amd.models.wan.dit import WanDiT
+
+    torch.manual_seed(1)
+    cfg = WanDiTConfig(dim=1536, ffn_dim=2048, freq_dim=256, heads=12, layers=2, text_dim=512,
+                       text_len=128)
+    m = WanDiT(cfg)
+    _randomise(m)
+    m = m.to(dev, torch.bfloat16).fuse()
+    x = torch.randn(2, 16, 2, 20, 32, device=dev).bfloat16()
+    t = torch.tensor([500.0, 500.0], device=dev)
+    ctx = torch.randn(2, 30, cfg.text_dim, device=dev)
+    kv = m.text_kv(m.embed_text(ctx))
+    y_native = m(x, t, kv)
+    try:
+        WF.set_backend("torch")
+        SF.set_backend("torch")
+        kv_t = m.text_kv(m.embed_text(ctx))
+        y_torch = m(x, t, kv_t)
+    finally:
+        WF.set_backend("auto")
+        SF.set_backend("auto")
+    err = (y_native - y_torch).abs().max().item() / y_torch.abs().max().item()
+    assert err < 2e-2, err
+
+
+def test_vae_tap_stacked_vs_upstream_chunked(dev):
+    from k8s_nvidia_gpus_amd.models.wan.config import WanVAEConfig
+    from k8s_nvidia_gpus_amd.models.wan.vae import WanVAE, reference_decode
+
+    torch.manual_seed(2)
+    v = WanVAE(WanVAEConfig(dim=32))
+    with torch.no_grad():
+        for n, p in v.named_parameters():
+            if n.endswith("bias") or "gamma" in n:
+                p.add_(torch.randn_like(p) * 0.05)
+    z = torch.randn(1, 16, 3, 8, 12) * 0.5
+    ref = reference_decode(v, z)
+    out = v.to(dev, torch.bfloat16).decode(z.to(dev)).float().cpu()
+    assert out.shape == ref.shape == (1, 3, 9, 64, 96)
+    err = (out - ref).abs()
+    # bf16 activations through 15 residual blocks: a few LSB of bf16 at |x| ~ 1 worst case
+    assert err.max().item() < 0.1 and err.mean().item() < 1e-2, (err.max().item(), err.mean().item())
+
+
+def test_pipeline_generates_deterministic_video_on_gpu(dev):
+    from k8s_nvidia_gpus_amd.models.wan.config import UMT5Config, WanDiTConfig, WanVAEConfig
+    from k8s_nvidia_gpus_amd.models.wan.pipeline import WanPipeline
+
+    p = WanPipeline.synthetic(dev, WanDiTConfig(dim=512, ffn_dim=1024, freq_dim=64, heads=4,
+                                                layers=2, text_dim=256, text_len=64),
+                              UMT5Config(vocab=300, dim=256, ffn_dim=512, heads=4, head_dim=64,
+                                         layers=2), WanVAEConfig(dim=32))
+    p.generate("warm-up", "", width=128, height=96, frames=9, steps=1, cfg=6.0)
+    r1 = p.generate("a red panda on a motorbike", "blurry", width=128, height=96, frames=9,
+                    steps=3, cfg=6.0, seed=7)
+    r2 = p.generate("a red panda on a motorbike", "blurry", width=128, height=96, frames=9,
+                    steps=3, cfg=6.0, seed=7)
+    assert r1.frames.shape == (9, 96, 128, 3) and r1.frames.dtype == torch.uint8
+    # DiT path (hipBLASLt + row kernels + flash attention, no atomics) is bit-reproducible; the
+    # VAE's convolutions go through MIOpen (deterministic solvers requested); any residual
+    # run-to-run difference must stay at bf16 rounding level
+    assert torch.equal(r1.latent, r2.latent)
+    d = (r1.frames.int() - r2.frames.int()).abs().float()
+    print("vae run-to-run |diff| max/mean (LSB):", d.max().item(), d.mean().item())
+    assert d.max().item() <= 8 and d.mean().item() < 1.0, (d.max().item(), d.mean().item())
+    r3 = p.generate("a red panda on a motorbike", "blurry", width=128, height=96, frames=9,
+                    steps=3, cfg=6.0, seed=8)
+    assert not torch.equal(r1.latent, r3.latent)
