@@ -179,12 +179,7 @@ class WanVAE(nn.Module):
         dt = self.conv2.weight.dtype
         z = (z.float() * std + mean).to(dt)
         x = z.permute(0, 2, 1, 3, 4).reshape(b * t, c, h, w).contiguous(memory_format=torch.channels_last)
-        prev = torch.backends.cudnn.deterministic
-        torch.backends.cudnn.deterministic = True       # MIOpen: no atomic split-K solvers
-        try:
-            x = self.decoder(self.conv2(x, b), b)
-        finally:
-            torch.backends.cudnn.deterministic = prev
+        x = self.decoder(self.conv2(x, b), b)
         n, co, hh, ww = x.shape
         return x.reshape(b, n // b, co, hh, ww).permute(0, 2, 1, 3, 4).clamp_(-1, 1)
 

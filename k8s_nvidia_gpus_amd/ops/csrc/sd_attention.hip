@@ -326,11 +326,26 @@ int launch(const AttnArgs& a, int NH, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+int g_qt_override = 0;   // amdk8s_attention_set_qt(): 0 = heuristic, else 1 / 2 / 4
+
 template <bool BF16, int QK, int DT>
 int launch_qt(const AttnArgs& a, int NH, hipStream_t stream) {
-  // two query tiles per wave (K/V fragments reused twice) when that still gives >= 512 workgroups
+  // K/V fragments read from LDS are reused by QT query tiles of a wave: QT = 1 leaves the d >= 128
+  // kernels LDS-bound (one ds_read_b128 of K per MFMA), so take the largest QT that still puts at
+  // least one workgroup on every CU (256 on MI355X).  QT = 4 is instantiated for d = 128 only
+  // (Wan2.1's 2560-token self-attention: 240 workgroups x 256 rows).
   const long wg2 = (long)((a.Lq + 127) / 128) * NH;
-  if (wg2 >= 512) return launch<BF16, QK, DT, 2>(a, NH, stream);
+  const long wg4 = (long)((a.Lq + 255) / 256) * NH;
+  int qt = wg2 >= 256 ? 2 : 1;
+  if constexpr (DT == 8) {
+    if (wg4 >= 224) qt = 4;
+  }
+  if (g_qt_override == 1 || g_qt_override == 2) qt = g_qt_override;
+  if constexpr (DT == 8) {
+    if (g_qt_override == 4) qt = 4;
+    if (qt == 4) return launch<BF16, QK, DT, 4>(a, NH, stream);
+  }
+  if (qt == 2) return launch<BF16, QK, DT, 2>(a, NH, stream);
   return launch<BF16, QK, DT, 1>(a, NH, stream);
 }
 
@@ -349,6 +364,8 @@ int dispatch(const AttnArgs& a, int NH, hipStream_t stream) {
 }  // namespace
 
 extern "C" {
+
+void amdk8s_attention_set_qt(int qt) { g_qt_override = qt; }
 
 int amdk8s_attention_supported(int d, int Lq, int Lk) {
   if (Lq <= 0 || Lk <= 0) return 0;

@@ -161,6 +161,15 @@ def layernorm_supported(c: int) -> bool:
     return c % 8 == 0 and c // 8 <= 256
 
 
+def attention_set_qt(qt: int) -> None:
+    """Force the query tiles per wave of the attention kernel (0 = heuristic; 1 / 2 / 4) — for
+    tuning sweeps (tools/attn_probe.py)."""
+    lib = _lib()
+    lib.amdk8s_attention_set_qt.argtypes = [ctypes.c_int]
+    lib.amdk8s_attention_set_qt.restype = None
+    lib.amdk8s_attention_set_qt(int(qt))
+
+
 def attention_supported(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int) -> bool:
     lib = _lib()
     if not hasattr(lib, "amdk8s_attention_fwd") or q.dtype not in _DTYPE:

@@ -244,6 +244,24 @@ def test_sd15_runs_the_in_tree_pipeline_from_the_image():
     assert "fastapi" in docker and "diffusers" not in docker and "ops.build all" in docker
 
 
+def test_wan_server_runs_in_tree_engine_with_comfy_contract():
+    """wan-video-gen serves ComfyUI's API from the in-tree Wan2.1 engine in the bench image: no
+    git clone / pip at pod start, the client's port 8181 and the reference client's model names."""
+    dep = load_all(CC / "apps/comfyui/deployment.yaml")[0]
+    c = dep["spec"]["template"]["spec"]["containers"][0]
+    assert c["image"] == "amd-gpu-bench"
+    script = c["args"][0]
+    assert "k8s_nvidia_gpus_amd.models.wan.server" in script and "--port 8181" in script
+    text = yaml.safe_dump(dep)
+    assert "pip install" not in text and "git clone" not in text
+    assert c["ports"][0]["containerPort"] == 8181
+    assert dep["metadata"]["name"] == "wan-video-gen"
+    k = load_all(CC / "apps/comfyui/kustomization.yaml")[0]
+    assert k["images"][0]["name"] == "amd-gpu-bench"
+    from k8s_nvidia_gpus_amd.models.wan.server import MODEL_DIRS
+    assert MODEL_DIRS["unet"][0] == "diffusion_models" and MODEL_DIRS["clip"][0] == "text_encoders"
+
+
 def test_sd15_service_keeps_reference_nodeport():
     svc = load_all(CC / "apps/sd15-api/service.yaml")[0]
     assert svc["spec"]["ports"][0]["nodePort"] == 30800

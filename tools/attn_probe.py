@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Flash-attention kernel sweep over query tiles per wave (QT) at the Wan2.1 / SD1.5 shapes:
+time per call, TFLOPS, and max error against PyTorch SDPA (fp32 math)."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from k8s_nvidia_gpus_amd.ops import sd_kernels as SK  # noqa: E402
+
+dev = torch.device("cuda", 0)
+SHAPES = {  # name: (N, heads, Lq, Lk, d)
+    "wan_self": (2, 12, 2560, 2560, 128),
+    "wan_cross": (2, 12, 2560, 512, 128),
+    "sd_64x64": (2, 8, 4096, 4096, 40),
+    "sd_32x32": (2, 8, 1024, 1024, 80),
+}
+res = {}
+for name, (n, h, lq, lk, d) in SHAPES.items():
+    g = torch.Generator(device=dev).manual_seed(0)
+    q = torch.randn(n, lq, h * d, generator=g, device=dev).bfloat16()
+    k = torch.randn(n, lk, h * d, generator=g, device=dev).bfloat16()
+    v = torch.randn(n, lk, h * d, generator=g, device=dev).bfloat16()
+    ref = F.scaled_dot_product_attention(*(t.float().view(n, -1, h, d).transpose(1, 2) for t in (q, k, v)))
+    ref = ref.transpose(1, 2).reshape(n, lq, h * d)
+    flops = 4.0 * n * h * lq * lk * d
+    res[name] = {}
+    for qt in ((1, 2, 4) if d == 128 else (1, 2)):
+        SK.attention_set_qt(qt)
+        o = SK.attention(q, k, v, h, d ** -0.5)
+        err = (o.float() - ref).abs().max().item()
+        for _ in range(3):
+            SK.attention(q, k, v, h, d ** -0.5)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        it = 50
+        for _ in range(it):
+            SK.attention(q, k, v, h, d ** -0.5)
+        torch.cuda.synchronize()
+        us = (time.perf_counter() - t0) * 1e6 / it
+        res[name][f"qt{qt}"] = {"us": round(us, 1), "tflops": round(flops / us / 1e6, 1), "max_err": round(err, 4)}
+        print(name, qt, res[name][f"qt{qt}"], flush=True)
+    SK.attention_set_qt(0)
+    o = SK.attention(q, k, v, h, d ** -0.5)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(50):
+        SK.attention(q, k, v, h, d ** -0.5)
+    torch.cuda.synchronize()
+    res[name]["heuristic_us"] = round((time.perf_counter() - t0) * 1e6 / 50, 1)
+print(json.dumps(res))
