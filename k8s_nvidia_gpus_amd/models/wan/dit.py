@@ -210,7 +210,7 @@ class WanDiT(nn.Module):
             o = ca.o(WF.attention(qc, kc, vc, cfg.heads))
             h = WF.add_ln(res, o, None, 1.0 + m[:, 4], m[:, 3], cfg.eps, wdt)
             # feed-forward
-            f = WF.gelu_tanh(blk.ffn[0](h))
+            f = WF.linear_gelu(h, blk.ffn[0].weight, blk.ffn[0].bias)
             o = blk.ffn[2](f)
             if i + 1 < len(self.blocks):
                 nm = mods[i + 1]

@@ -146,3 +146,13 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int) -> 
 
 def gelu_tanh(x: torch.Tensor) -> torch.Tensor:
     return F.gelu(x, approximate="tanh")
+
+
+def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """``gelu_tanh(x·wᵀ + b)``.  On the GPU the bias and the tanh-GELU run in hipBLASLt's GEMM
+    epilogue (``torch._addmm_activation``): the [B·L, ffn] pre-activation is never written to and
+    re-read from HBM (Wan2.1-1.3B: 2 × 2560 × 8960 bf16 per block, 30 blocks per step)."""
+    if _native(x):
+        y = torch._addmm_activation(b, x.reshape(-1, x.shape[-1]), w.t(), use_gelu=True)
+        return y.view(*x.shape[:-1], w.shape[0])
+    return F.gelu(F.linear(x, w, b), approximate="tanh")

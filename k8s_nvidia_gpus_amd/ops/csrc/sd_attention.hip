@@ -51,10 +51,15 @@ __device__ __forceinline__ uint32_t f32_to_bf16(float f) {
   return u >> 16;
 }
 
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+
 template <bool BF16>
 __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
   if constexpr (BF16) {
-    return f32_to_bf16(lo) | (f32_to_bf16(hi) << 16);
+    // one v_cvt_pk_bf16_f32 (gfx950, round-to-nearest-even) instead of ~10 integer ops: P is
+    // packed for every score, and this conversion was ~40 % of the softmax VALU work
+    const bf16x2 v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(uint32_t, v);
   } else {
     _Float16 a = (_Float16)lo, b = (_Float16)hi;
     uint16_t ua, ub;
@@ -113,7 +118,7 @@ struct AttnArgs {
 };
 
 // QK_STEPS = ceil(d/32) (reduction steps of S), DT = ceil(d/16) (16-column tiles of O), QT = q tiles per wave
-template <bool BF16, int QK_STEPS, int DT, int QT>
+template <bool BF16, int QK_STEPS, int DT, int QT, int D>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
   constexpr int DK = QK_STEPS * 32;   // K row width in LDS (zero padded)
   constexpr int DV = DT * 16;         // V row width in LDS (zero padded)
@@ -130,7 +135,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
   const int g = lane >> 4, c16 = lane & 15;   // 16-lane group, lane in group
   const int nh = blockIdx.y, n = nh / a.H, head = nh % a.H;
   const int q0 = blockIdx.x * (kWaves * QW) + wave * QW;
-  const int d = a.d;
+  constexpr int d = D;                // head dim as a compile-time constant: the K/V tile loader's
+                                      // row/column split below is shifts, not integer divisions
   const uint16_t* qb = a.q + n * a.sqb + (long)head * d;
   const uint16_t* kb = a.k + n * a.skb + (long)head * d;
   const uint16_t* vb = a.v + n * a.svb + (long)head * d;
@@ -169,8 +175,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
   }
 
   // K/V tile loader: 16-byte chunks, CK = d/8 per row
-  const int CK = d / 8;
-  const int nchunks = kKeys * CK;
+  constexpr int CK = d / 8;
+  constexpr int nchunks = kKeys * CK;
   constexpr int kMaxPer = QK_STEPS;  // chunks per thread: 64 rows * d/8 <= 256 * QK_STEPS
   uint4 kreg[kMaxPer], vreg[kMaxPer];
   auto load_tile = [&](int kbase) {
@@ -214,20 +220,23 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
     if (kt + 1 < ntiles) load_tile(kbase + kKeys);  // in flight under this tile's MFMAs
     const bool partial = kbase + kKeys > a.Lk;
 
+    // S = Q Kᵀ for QT × (16 q × 64 keys): each K fragment is read from LDS once and feeds the
+    // MFMAs of all QT query tiles (the QT independent accumulators also hide MFMA latency)
+    f32x4 sall[QT][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) sall[qt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < QK_STEPS; ++s) {
+        const s16x8 kf = *reinterpret_cast<const s16x8*>(kl + (16 * t + c16) * KS + 32 * s + 8 * g);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) sall[qt][t] = mfma16<BF16>(qf[qt][s], kf, sall[qt][t]);
+      }
+    }
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
-      // S = Q Kᵀ for 16 q × 64 keys: four 16×16 tiles
-      f32x4 sacc[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        sacc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < QK_STEPS; ++s) {
-          const s16x8 kf =
-              *reinterpret_cast<const s16x8*>(kl + (16 * t + c16) * KS + 32 * s + 8 * g);
-          sacc[t] = mfma16<BF16>(qf[qt][s], kf, sacc[t]);
-        }
-      }
+      f32x4* sacc = sall[qt];
       if (partial) {
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -316,47 +325,44 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
   }
 }
 
-template <bool BF16, int QK, int DT, int QT>
+template <bool BF16, int QK, int DT, int QT, int D>
 int launch(const AttnArgs& a, int NH, hipStream_t stream) {
   constexpr int KS = QK * 32 + kPad, VS = DT * 16 + kPad, PS = QT * 16 + 4;
   const size_t lds = (size_t)(kKeys * KS + kKeys * VS + kWaves * kKeys * PS) * 2;
   const int rows = kWaves * QT * 16;
   dim3 grid((a.Lq + rows - 1) / rows, NH);
-  hipLaunchKernelGGL((attn_fwd_kernel<BF16, QK, DT, QT>), grid, dim3(256), lds, stream, a);
+  hipLaunchKernelGGL((attn_fwd_kernel<BF16, QK, DT, QT, D>), grid, dim3(256), lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 int g_qt_override = 0;   // amdk8s_attention_set_qt(): 0 = heuristic, else 1 / 2 / 4
 
-template <bool BF16, int QK, int DT>
+template <bool BF16, int QK, int DT, int D>
 int launch_qt(const AttnArgs& a, int NH, hipStream_t stream) {
-  // K/V fragments read from LDS are reused by QT query tiles of a wave: QT = 1 leaves the d >= 128
-  // kernels LDS-bound (one ds_read_b128 of K per MFMA), so take the largest QT that still puts at
-  // least one workgroup on every CU (256 on MI355X).  QT = 4 is instantiated for d = 128 only
-  // (Wan2.1's 2560-token self-attention: 240 workgroups x 256 rows).
+  // K fragments (one LDS read per 16x32 step) and V fragments are shared by the QT query tiles of
+  // a wave; QT = 2 wherever that still leaves >= 256 workgroups (one per CU), QT = 1 otherwise.
+  // QT = 4 (d = 128 only) is reachable through amdk8s_attention_set_qt for sweeps: at Wan2.1's
+  // 2560-token shape it is register-bound (256 VGPR + 256 AGPR, spills) and slower than QT = 2
+  // (tools/attn_probe.py: 207 vs 176 us).
   const long wg2 = (long)((a.Lq + 127) / 128) * NH;
-  const long wg4 = (long)((a.Lq + 255) / 256) * NH;
   int qt = wg2 >= 256 ? 2 : 1;
-  if constexpr (DT == 8) {
-    if (wg4 >= 224) qt = 4;
-  }
   if (g_qt_override == 1 || g_qt_override == 2) qt = g_qt_override;
   if constexpr (DT == 8) {
     if (g_qt_override == 4) qt = 4;
-    if (qt == 4) return launch<BF16, QK, DT, 4>(a, NH, stream);
+    if (qt == 4) return launch<BF16, QK, DT, 4, D>(a, NH, stream);
   }
-  if (qt == 2) return launch<BF16, QK, DT, 2>(a, NH, stream);
-  return launch<BF16, QK, DT, 1>(a, NH, stream);
+  if (qt == 2) return launch<BF16, QK, DT, 2, D>(a, NH, stream);
+  return launch<BF16, QK, DT, 1, D>(a, NH, stream);
 }
 
 template <bool BF16>
 int dispatch(const AttnArgs& a, int NH, hipStream_t stream) {
   switch (a.d) {
-    case 40: return launch_qt<BF16, 2, 3>(a, NH, stream);
-    case 64: return launch_qt<BF16, 2, 4>(a, NH, stream);
-    case 80: return launch_qt<BF16, 3, 5>(a, NH, stream);
-    case 128: return launch_qt<BF16, 4, 8>(a, NH, stream);
-    case 160: return launch_qt<BF16, 5, 10>(a, NH, stream);
+    case 40: return launch_qt<BF16, 2, 3, 40>(a, NH, stream);
+    case 64: return launch_qt<BF16, 2, 4, 64>(a, NH, stream);
+    case 80: return launch_qt<BF16, 3, 5, 80>(a, NH, stream);
+    case 128: return launch_qt<BF16, 4, 8, 128>(a, NH, stream);
+    case 160: return launch_qt<BF16, 5, 10, 160>(a, NH, stream);
     default: return -1;
   }
 }

@@ -67,6 +67,21 @@ def test_rmsnorm_rope_vs_fp32(WK, dev, c, heads, rope):
     assert torch.equal(qkv[..., 2 * c:], ref[..., 2 * c:])           # v untouched
 
 
+def test_linear_gelu_epilogue_is_tanh_gelu(dev):
+    """hipBLASLt's GELU epilogue must be the tanh form Wan was trained with."""
+    from k8s_nvidia_gpus_amd.models.wan import functional as WF
+
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(2, 300, 1536, generator=g, device=dev).bfloat16()
+    w = (torch.randn(8960, 1536, generator=g, device=dev) * 0.03).bfloat16()
+    b = (torch.randn(8960, generator=g, device=dev) * 0.5).bfloat16()
+    y = WF.linear_gelu(x, w, b)
+    pre = x.float() @ w.float().t() + b.float()
+    ref_tanh = torch.nn.functional.gelu(pre, approximate="tanh")
+    assert y.shape == (2, 300, 8960)
+    torch.testing.assert_close(y.float(), ref_tanh, rtol=2e-2, atol=2e-2)
+
+
 def _randomise(model, scale=0.02):
     with torch.no_grad():
         for p in model.parameters():

@@ -13,6 +13,8 @@ import torch.nn.functional as F  # noqa: E402
 from k8s_nvidia_gpus_amd.ops import sd_kernels as SK  # noqa: E402
 
 dev = torch.device("cuda", 0)
+ONLY = os.environ.get("ATTN_ONLY")          # e.g. wan_self (PMC passes)
+QTS = [int(x) for x in os.environ.get("ATTN_QTS", "").split(",") if x]
 SHAPES = {  # name: (N, heads, Lq, Lk, d)
     "wan_self": (2, 12, 2560, 2560, 128),
     "wan_cross": (2, 12, 2560, 512, 128),
@@ -21,6 +23,8 @@ SHAPES = {  # name: (N, heads, Lq, Lk, d)
 }
 res = {}
 for name, (n, h, lq, lk, d) in SHAPES.items():
+    if ONLY and name != ONLY:
+        continue
     g = torch.Generator(device=dev).manual_seed(0)
     q = torch.randn(n, lq, h * d, generator=g, device=dev).bfloat16()
     k = torch.randn(n, lk, h * d, generator=g, device=dev).bfloat16()
@@ -29,7 +33,7 @@ for name, (n, h, lq, lk, d) in SHAPES.items():
     ref = ref.transpose(1, 2).reshape(n, lq, h * d)
     flops = 4.0 * n * h * lq * lk * d
     res[name] = {}
-    for qt in ((1, 2, 4) if d == 128 else (1, 2)):
+    for qt in (QTS or ((1, 2, 4) if d == 128 else (1, 2))):
         SK.attention_set_qt(qt)
         o = SK.attention(q, k, v, h, d ** -0.5)
         err = (o.float() - ref).abs().max().item()
