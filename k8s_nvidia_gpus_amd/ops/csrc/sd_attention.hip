@@ -325,13 +325,218 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Transposed-score variant (default): S^T = K Q^T and O^T = V^T P^T on the same MFMA.  With the
+// operands swapped, a lane's S accumulator holds 4 keys (16t + 4g + i) of ONE query (c16), which
+// is exactly the B-operand layout P^T needs for the P·V MFMA (keys 4g..4g+3 of two 16-key tiles
+// per 32-key step, a consistent permutation of the reduction index shared with V^T).  P therefore
+// never leaves registers: no P store / transpose read through LDS and no wave barrier per tile,
+// and the per-query max / sum live in one register per query tile (a 4-lane shuffle on the rare
+// rescale and once in the epilogue).  V^T comes from the same ds_read_b64_tr_b16 column reads as
+// before, only with the key rows permuted to match.
+template <bool BF16, int QK_STEPS, int DT, int QT, int D>
+__global__ __launch_bounds__(256) void attn_fwd_t_kernel(const AttnArgs a) {
+  constexpr int DK = QK_STEPS * 32;
+  constexpr int DV = DT * 16;
+  constexpr int KS = DK + kPad;
+  constexpr int VS = DV + kPad;
+  constexpr int QW = QT * 16;
+  constexpr int d = D;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* kl = smem;                // [64][KS]
+  uint16_t* vl = kl + kKeys * KS;     // [64][VS]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int nh = blockIdx.y, n = nh / a.H, head = nh % a.H;
+  const int q0 = blockIdx.x * (kWaves * QW) + wave * QW;
+  const uint16_t* qb = a.q + n * a.sqb + (long)head * d;
+  const uint16_t* kb = a.k + n * a.skb + (long)head * d;
+  const uint16_t* vb = a.v + n * a.svb + (long)head * d;
+
+  for (int i = tid; i < kKeys * (KS + VS) / 8; i += 256)
+    reinterpret_cast<uint4*>(smem)[i] = make_uint4(0, 0, 0, 0);
+
+  // Q^T fragments (B operand): lane holds Q[q0 + 16qt + c16][32s + 8g .. +7]
+  s16x8 qf[QT][QK_STEPS];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    const int qrow = min(q0 + qt * 16 + c16, a.Lq - 1);
+#pragma unroll
+    for (int s = 0; s < QK_STEPS; ++s) {
+      const int col = 32 * s + 8 * g;
+      if (col < d)
+        qf[qt][s] = *reinterpret_cast<const s16x8*>(qb + qrow * a.sqr + col);
+      else
+        qf[qt][s] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+
+  f32x4 o[QT][DT];                    // O^T: lane holds O[q = c16][16t + 4g + i]
+  float m[QT], l[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+#pragma unroll
+    for (int t = 0; t < DT; ++t) o[qt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m[qt] = -INFINITY;
+    l[qt] = 0.f;
+  }
+
+  constexpr int CK = d / 8;
+  constexpr int nchunks = kKeys * CK;
+  constexpr int kMaxPer = QK_STEPS;
+  uint4 kreg[kMaxPer], vreg[kMaxPer];
+  auto load_tile = [&](int kbase) {
+#pragma unroll
+    for (int j = 0; j < kMaxPer; ++j) {
+      const int ch = tid + j * 256;
+      if (ch < nchunks) {
+        const int r = ch / CK, cc = (ch - r * CK) * 8;
+        const int key = kbase + r;
+        if (key < a.Lk) {
+          kreg[j] = *reinterpret_cast<const uint4*>(kb + key * a.skr + cc);
+          vreg[j] = *reinterpret_cast<const uint4*>(vb + key * a.svr + cc);
+        } else {
+          kreg[j] = make_uint4(0, 0, 0, 0);
+          vreg[j] = make_uint4(0, 0, 0, 0);
+        }
+      }
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int j = 0; j < kMaxPer; ++j) {
+      const int ch = tid + j * 256;
+      if (ch < nchunks) {
+        const int r = ch / CK, cc = (ch - r * CK) * 8;
+        *reinterpret_cast<uint4*>(kl + r * KS + cc) = kreg[j];
+        *reinterpret_cast<uint4*>(vl + r * VS + cc) = vreg[j];
+      }
+    }
+  };
+
+  const int ntiles = (a.Lk + kKeys - 1) / kKeys;
+  constexpr float kThr = 8.f;
+  const float thr = kThr / a.c;
+  const int qq = c16 >> 2, p4 = (c16 & 3) * 4;
+  load_tile(0);
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int kbase = kt * kKeys;
+    __syncthreads();
+    store_tile();
+    __syncthreads();
+    if (kt + 1 < ntiles) load_tile(kbase + kKeys);
+    const bool partial = kbase + kKeys > a.Lk;
+
+    // S^T tiles: sall[qt][t][i] = score(key 16t + 4g + i, query c16)
+    f32x4 sall[QT][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) sall[qt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < QK_STEPS; ++s) {
+        const s16x8 kf = *reinterpret_cast<const s16x8*>(kl + (16 * t + c16) * KS + 32 * s + 8 * g);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) sall[qt][t] = mfma16<BF16>(kf, qf[qt][s], sall[qt][t]);
+      }
+    }
+    s16x8 pf[QT][2];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      if (partial) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (kbase + 16 * t + 4 * g + i >= a.Lk) sall[qt][t][i] = -INFINITY;
+      }
+      float lmax = sall[qt][0][0];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) lmax = fmaxf(lmax, sall[qt][t][i]);
+      if (__builtin_amdgcn_ballot_w64(lmax > m[qt] + thr) != 0) {   // wave-uniform, rare
+        float tmax = fmaxf(lmax, __shfl_xor(lmax, 16, 64));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float mnew = fmaxf(m[qt], tmax);
+        const float alpha = __builtin_amdgcn_exp2f((m[qt] - mnew) * a.c);
+        m[qt] = mnew;
+        l[qt] *= alpha;
+#pragma unroll
+        for (int t = 0; t < DT; ++t) o[qt][t] *= alpha;
+      }
+      const float mc = m[qt] * a.c;
+      float rs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(sall[qt][t][i], a.c, -mc));
+          sall[qt][t][i] = p;
+          rs += p;
+        }
+      l[qt] += rs;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const f32x4 lo = sall[qt][2 * ks], hi = sall[qt][2 * ks + 1];
+        const uint32_t w0 = pack2<BF16>(lo[0], lo[1]), w1 = pack2<BF16>(lo[2], lo[3]);
+        const uint32_t w2 = pack2<BF16>(hi[0], hi[1]), w3 = pack2<BF16>(hi[2], hi[3]);
+        pf[qt][ks] = __builtin_bit_cast(s16x8, make_uint4(w0, w1, w2, w3));
+      }
+    }
+
+    // O^T += V^T P^T: reduction position 8g + j <-> key 32ks + 4g + j (j < 4), 32ks + 16 + 4g + j - 4
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int rlo = 32 * ks + 4 * g + qq;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4*)((lds_short*)vl + rlo * VS + 16 * t + p4));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4*)((lds_short*)vl + (rlo + 16) * VS + 16 * t + p4));
+        const s16x8 vf = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) o[qt][t] = mfma16<BF16>(vf, pf[qt][ks], o[qt][t]);
+      }
+    }
+  }
+
+  uint16_t* ob = a.o + n * a.sob + (long)head * d;
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    float lt = l[qt] + __shfl_xor(l[qt], 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const float inv = 1.f / lt;
+    const int q = q0 + qt * 16 + c16;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const int col = 16 * t + 4 * g;
+      if (q < a.Lq && col < d) {
+        uint2 w;
+        w.x = pack2<BF16>(o[qt][t][0] * inv, o[qt][t][1] * inv);
+        w.y = pack2<BF16>(o[qt][t][2] * inv, o[qt][t][3] * inv);
+        *reinterpret_cast<uint2*>(ob + q * a.sor + col) = w;
+      }
+    }
+  }
+}
+
+int g_variant = 0;   // amdk8s_attention_set_variant(): 0 = transposed (P in registers), 1 = P via LDS
+
 template <bool BF16, int QK, int DT, int QT, int D>
 int launch(const AttnArgs& a, int NH, hipStream_t stream) {
   constexpr int KS = QK * 32 + kPad, VS = DT * 16 + kPad, PS = QT * 16 + 4;
-  const size_t lds = (size_t)(kKeys * KS + kKeys * VS + kWaves * kKeys * PS) * 2;
   const int rows = kWaves * QT * 16;
   dim3 grid((a.Lq + rows - 1) / rows, NH);
-  hipLaunchKernelGGL((attn_fwd_kernel<BF16, QK, DT, QT, D>), grid, dim3(256), lds, stream, a);
+  if (g_variant == 0) {
+    const size_t lds = (size_t)(kKeys * KS + kKeys * VS) * 2;
+    hipLaunchKernelGGL((attn_fwd_t_kernel<BF16, QK, DT, QT, D>), grid, dim3(256), lds, stream, a);
+  } else {
+    const size_t lds = (size_t)(kKeys * KS + kKeys * VS + kWaves * kKeys * PS) * 2;
+    hipLaunchKernelGGL((attn_fwd_kernel<BF16, QK, DT, QT, D>), grid, dim3(256), lds, stream, a);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -341,11 +546,15 @@ template <bool BF16, int QK, int DT, int D>
 int launch_qt(const AttnArgs& a, int NH, hipStream_t stream) {
   // K fragments (one LDS read per 16x32 step) and V fragments are shared by the QT query tiles of
   // a wave; QT = 2 wherever that still leaves >= 256 workgroups (one per CU), QT = 1 otherwise.
-  // QT = 4 (d = 128 only) is reachable through amdk8s_attention_set_qt for sweeps: at Wan2.1's
-  // 2560-token shape it is register-bound (256 VGPR + 256 AGPR, spills) and slower than QT = 2
-  // (tools/attn_probe.py: 207 vs 176 us).
+  // d = 128 (Wan2.1) takes QT = 4 when that still covers ~all CUs: with P kept in registers the
+  // transposed kernel fits it without spills and reuses every K/V fragment 4x
+  // (tools/attn_probe.py at 2x12 heads x 2560 tokens: QT 1 / 2 / 4 = 182 / 164 / 132 us).
   const long wg2 = (long)((a.Lq + 127) / 128) * NH;
+  const long wg4 = (long)((a.Lq + 255) / 256) * NH;
   int qt = wg2 >= 256 ? 2 : 1;
+  if constexpr (DT == 8) {
+    if (g_variant == 0 && wg4 >= 224) qt = 4;
+  }
   if (g_qt_override == 1 || g_qt_override == 2) qt = g_qt_override;
   if constexpr (DT == 8) {
     if (g_qt_override == 4) qt = 4;
@@ -372,6 +581,7 @@ int dispatch(const AttnArgs& a, int NH, hipStream_t stream) {
 extern "C" {
 
 void amdk8s_attention_set_qt(int qt) { g_qt_override = qt; }
+void amdk8s_attention_set_variant(int v) { g_variant = v; }
 
 int amdk8s_attention_supported(int d, int Lq, int Lk) {
   if (Lq <= 0 || Lk <= 0) return 0;

@@ -170,6 +170,14 @@ def attention_set_qt(qt: int) -> None:
     lib.amdk8s_attention_set_qt(int(qt))
 
 
+def attention_set_variant(v: int) -> None:
+    """0 = transposed-score kernel (P stays in registers, default), 1 = P staged through LDS."""
+    lib = _lib()
+    lib.amdk8s_attention_set_variant.argtypes = [ctypes.c_int]
+    lib.amdk8s_attention_set_variant.restype = None
+    lib.amdk8s_attention_set_variant(int(v))
+
+
 def attention_supported(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int) -> bool:
     lib = _lib()
     if not hasattr(lib, "amdk8s_attention_fwd") or q.dtype not in _DTYPE:

@@ -181,3 +181,24 @@ def test_pipeline_generates_deterministic_video_on_gpu(dev):
     r3 = p.generate("a red panda on a motorbike", "blurry", width=128, height=96, frames=9,
                     steps=3, cfg=6.0, seed=8)
     assert not torch.equal(r1.latent, r3.latent)
+
+
+def test_comfy_server_runs_prompt_on_gpu(dev, tmp_path):
+    """The ComfyUI-compatible server executing a Wan graph on the GPU (miniature random-init
+    components under the reference's model file names)."""
+    from fastapi.testclient import TestClient
+
+    from k8s_nvidia_gpus_amd.models.comfy_client import ComfyClient, WanJob, build_wan_graph
+    from k8s_nvidia_gpus_amd.models.wan.server import create_app, synthetic_store
+
+    store = synthetic_store("cuda", tiny=True)
+    app = create_app(store, str(tmp_path / "out"), ffmpeg="")
+    job = WanJob(prompt="a panda", width=64, height=48, frames=5, steps=2, formats=("webp",))
+    with TestClient(app) as c:
+        pid = c.post("/prompt", json={"prompt": build_wan_graph(job)}).json()["prompt_id"]
+        assert app.state.queue.wait_idle(120)
+        h = c.get(f"/history/{pid}").json()[pid]
+        assert h["status"]["status_str"] == "success", h["status"]
+        f = ComfyClient.output_files(h)[0]
+        assert c.get("/view", params=f).content[8:12] == b"WEBP"
+        assert c.get("/system_stats").json()["devices"][0]["vram_total"] > 200e9

@@ -15,6 +15,7 @@ from k8s_nvidia_gpus_amd.ops import sd_kernels as SK  # noqa: E402
 dev = torch.device("cuda", 0)
 ONLY = os.environ.get("ATTN_ONLY")          # e.g. wan_self (PMC passes)
 QTS = [int(x) for x in os.environ.get("ATTN_QTS", "").split(",") if x]
+VARIANTS = [int(x) for x in os.environ.get("ATTN_VARIANTS", "0,1").split(",") if x]
 SHAPES = {  # name: (N, heads, Lq, Lk, d)
     "wan_self": (2, 12, 2560, 2560, 128),
     "wan_cross": (2, 12, 2560, 512, 128),
@@ -33,7 +34,8 @@ for name, (n, h, lq, lk, d) in SHAPES.items():
     ref = ref.transpose(1, 2).reshape(n, lq, h * d)
     flops = 4.0 * n * h * lq * lk * d
     res[name] = {}
-    for qt in (QTS or ((1, 2, 4) if d == 128 else (1, 2))):
+    for var, qt in [(vv, qq) for vv in VARIANTS for qq in (QTS or ((1, 2, 4) if d == 128 else (1, 2)))]:
+        SK.attention_set_variant(var)
         SK.attention_set_qt(qt)
         o = SK.attention(q, k, v, h, d ** -0.5)
         err = (o.float() - ref).abs().max().item()
@@ -46,9 +48,11 @@ for name, (n, h, lq, lk, d) in SHAPES.items():
             SK.attention(q, k, v, h, d ** -0.5)
         torch.cuda.synchronize()
         us = (time.perf_counter() - t0) * 1e6 / it
-        res[name][f"qt{qt}"] = {"us": round(us, 1), "tflops": round(flops / us / 1e6, 1), "max_err": round(err, 4)}
-        print(name, qt, res[name][f"qt{qt}"], flush=True)
+        key = f"v{var}_qt{qt}"
+        res[name][key] = {"us": round(us, 1), "tflops": round(flops / us / 1e6, 1), "max_err": round(err, 4)}
+        print(name, key, res[name][key], flush=True)
     SK.attention_set_qt(0)
+    SK.attention_set_variant(0)
     o = SK.attention(q, k, v, h, d ** -0.5)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
