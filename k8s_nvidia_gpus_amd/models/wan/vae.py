@@ -63,6 +63,10 @@ class CausalConv(nn.Module):
                 memory_format=torch.channels_last)
         return self._w2
 
+    def conv_stacked(self, xs: torch.Tensor) -> torch.Tensor:
+        """The convolution on an input whose temporal taps are already stacked on channels."""
+        return F.conv2d(xs, self.weight2d(), self.bias, padding=self.pad[1:])
+
     def forward(self, x: torch.Tensor, b: int) -> torch.Tensor:
         """x: [B·T, Cin, H, W] (frames of each sample consecutive) → [B·T, Cout, H, W]."""
         kt = self.weight.shape[2]
@@ -76,6 +80,17 @@ class CausalConv(nn.Module):
         return F.conv2d(x, self.weight2d(), self.bias, padding=self.pad[1:])
 
 
+def norm_silu_conv(norm: RMSNorm, conv: "CausalConv", x: torch.Tensor, b: int) -> torch.Tensor:
+    """``conv(silu(norm(x)))`` — on the GPU one fused normalise/activate/tap-stack kernel
+    (ops/csrc/wan_ops.hip) feeding one 2-D convolution."""
+    if x.is_cuda and conv.weight.shape[2] == 3:
+        from k8s_nvidia_gpus_amd.ops import wan_kernels as WK
+
+        if WK.vae_rms_silu_supported(x):
+            return conv.conv_stacked(WK.vae_rms_silu_stack(x, norm.gamma, x.shape[0] // b, 3))
+    return conv(F.silu(norm(x)), b)
+
+
 class ResidualBlock(nn.Module):
     def __init__(self, cin: int, cout: int):
         super().__init__()
@@ -86,8 +101,8 @@ class ResidualBlock(nn.Module):
 
     def forward(self, x, b):
         r = self.residual
-        h = r[2](F.silu(r[0](x)), b)
-        h = r[6](F.silu(r[3](h)), b)
+        h = norm_silu_conv(r[0], r[2], x, b)
+        h = norm_silu_conv(r[3], r[6], h, b)
         return h + (self.shortcut(x, b) if self.shortcut is not None else x)
 
 
@@ -157,7 +172,7 @@ class Decoder(nn.Module):
             x = m(x, b)
         for m in self.upsamples:
             x = m(x, b)
-        return self.head[2](F.silu(self.head[0](x)), b)
+        return norm_silu_conv(self.head[0], self.head[2], x, b)
 
 
 class WanVAE(nn.Module):

@@ -211,6 +211,84 @@ int launch_rms(uint16_t* t, long st, const float* w, const float* cs, const floa
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// amdk8s_wan_vae_rms_silu_stack — the Wan VAE's "RMS_norm → SiLU → causal 3×3×3 conv input" glue
+// in one pass over channels-last frames x [B·T, H·W, C] (C = 96 / 192 / 384):
+//     y = silu(x / max(‖x‖₂, 1e-12) · √C · γ)                       (per pixel, over channels)
+// written either plainly (kt = 1) or straight into the temporal-tap-stacked input of the next
+// causal convolution (kt = 3): out[t][p][j·C : (j+1)·C] = y[t − 2 + j] (zero before frame 0 of
+// each sample), so the convolution runs as ONE 2-D conv over 3·C input channels with no
+// separate normalise / activation / concatenate passes (each a full-resolution HBM round trip).
+// 4 lanes per pixel, each holding CPL 16-byte chunks; 16 pixels per wave, 64 per workgroup.
+template <int CPL, int KT>
+__global__ __launch_bounds__(256) void vae_rms_silu_stack_kernel(const uint16_t* __restrict__ x,
+                                                                 const float* __restrict__ gamma,
+                                                                 uint16_t* __restrict__ out,
+                                                                 long pixels, int hw, int T) {
+  constexpr int C = CPL * 32;
+  const int lane = threadIdx.x & 63, sub = lane & 3;
+  const long px = ((long)blockIdx.x * 256 + threadIdx.x) >> 2;     // global pixel row
+  if (px >= pixels) return;                                        // 4-lane groups exit together
+  const uint16_t* xr = x + px * C;
+  float v[CPL][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    unpack8(*reinterpret_cast<const uint4*>(xr + (j * 4 + sub) * 8), v[j]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ss = fmaf(v[j][e], v[j][e], ss);
+  }
+  ss += __shfl_xor(ss, 1, 64);
+  ss += __shfl_xor(ss, 2, 64);
+  const float sc = sqrtf((float)C) / fmaxf(sqrtf(ss), 1e-12f);
+  uint4 y[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    float g[8], o[8];
+    load8f(gamma + (j * 4 + sub) * 8, g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float t = v[j][e] * sc * g[e];
+      o[e] = t / (1.f + __expf(-t));
+    }
+    y[j] = pack8(o);
+  }
+  if constexpr (KT == 1) {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) *reinterpret_cast<uint4*>(out + px * C + (j * 4 + sub) * 8) = y[j];
+  } else {
+    const long n = px / hw, p = px - n * hw;       // frame index (b·T + t) and pixel in frame
+    const int t = (int)(n % T);
+    // y[t] feeds out[t + j'] at slot 2 − j'  (j' = 0, 1, 2 while t + j' < T)
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      if (t + jj < T) {
+        uint16_t* dst = out + ((n + jj) * hw + p) * (3 * C) + (2 - jj) * C;
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) *reinterpret_cast<uint4*>(dst + (j * 4 + sub) * 8) = y[j];
+      }
+    }
+    // slots of this frame that reach before frame 0 are zero
+    if (t < 2) {
+      uint16_t* dst = out + (n * hw + p) * (3 * C);
+      const uint4 z = make_uint4(0, 0, 0, 0);
+      for (int slot = 0; slot < 2 - t; ++slot)
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) *reinterpret_cast<uint4*>(dst + slot * C + (j * 4 + sub) * 8) = z;
+    }
+  }
+}
+
+template <int CPL>
+int launch_vae(const uint16_t* x, const float* g, uint16_t* out, long pixels, int hw, int T, int kt,
+               hipStream_t s) {
+  const unsigned blocks = (unsigned)((pixels * 4 + 255) / 256);
+  if (kt == 3)
+    vae_rms_silu_stack_kernel<CPL, 3><<<blocks, 256, 0, s>>>(x, g, out, pixels, hw, T);
+  else
+    vae_rms_silu_stack_kernel<CPL, 1><<<blocks, 256, 0, s>>>(x, g, out, pixels, hw, T);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 }  // namespace
 
 extern "C" {
@@ -262,6 +340,24 @@ int amdk8s_wan_rmsnorm_rope(void* t, long st, const float* w, const float* cs, c
     case 8: return launch_rms<8>(tp, st, w, cs, sn, rows, L, hd, nsec, eps, s);
     case 10: return launch_rms<10>(tp, st, w, cs, sn, rows, L, hd, nsec, eps, s);
     default: return -1;
+  }
+}
+
+int amdk8s_wan_vae_supported(int C) { return (C == 96 || C == 192 || C == 384) ? 1 : 0; }
+
+// x bf16 [pixels = B·T·hw, C] contiguous; gamma fp32 [C]; out bf16 [pixels, C] (kt 1) or
+// [pixels, 3C] (kt 3, every element written).
+int amdk8s_wan_vae_rms_silu_stack(const void* x, const float* gamma, void* out, long pixels, int hw,
+                                  int T, int C, int kt, hipStream_t s) {
+  if (!amdk8s_wan_vae_supported(C) || pixels <= 0 || hw <= 0 || T <= 0 || (kt != 1 && kt != 3) ||
+      pixels % ((long)hw * T) != 0)
+    return -1;
+  const uint16_t* xp = static_cast<const uint16_t*>(x);
+  uint16_t* op = static_cast<uint16_t*>(out);
+  switch (C) {
+    case 96: return launch_vae<3>(xp, gamma, op, pixels, hw, T, kt, s);
+    case 192: return launch_vae<6>(xp, gamma, op, pixels, hw, T, kt, s);
+    default: return launch_vae<12>(xp, gamma, op, pixels, hw, T, kt, s);
   }
 }
 

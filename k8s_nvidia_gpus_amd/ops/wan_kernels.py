@@ -33,6 +33,10 @@ def _lib():
             lib.amdk8s_wan_add_ln.restype = ci
             lib.amdk8s_wan_rmsnorm_rope.argtypes = [vp, cl, vp, vp, vp, cl, ci, ci, ci, ci, cf, vp]
             lib.amdk8s_wan_rmsnorm_rope.restype = ci
+            lib.amdk8s_wan_vae_supported.argtypes = [ci]
+            lib.amdk8s_wan_vae_supported.restype = ci
+            lib.amdk8s_wan_vae_rms_silu_stack.argtypes = [vp, vp, vp, cl, ci, ci, ci, ci, vp]
+            lib.amdk8s_wan_vae_rms_silu_stack.restype = ci
             _declared = True
     return lib
 
@@ -135,3 +139,22 @@ def rmsnorm_rope(t: torch.Tensor, w: torch.Tensor, cos: Optional[torch.Tensor],
                                         c // heads, nsec, float(eps), _stream(t))
     _check(rc, "amdk8s_wan_rmsnorm_rope")
     return t
+
+
+def vae_rms_silu_supported(x: torch.Tensor) -> bool:
+    return (x.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and bool(_lib().amdk8s_wan_vae_supported(x.shape[1])))
+
+
+def vae_rms_silu_stack(x: torch.Tensor, gamma: torch.Tensor, frames: int, kt: int = 3) -> torch.Tensor:
+    """``silu(RMS_norm(x))`` of channels-last frames ``x`` [B·T, C, H, W]; with ``kt = 3`` the
+    result is written as the temporal-tap-stacked [B·T, 3C, H, W] input of a causal 3×3×3 conv."""
+    n, c, h, w = x.shape
+    g32 = _weight32(gamma.reshape(-1))
+    out = torch.empty((n, kt * c, h, w), dtype=x.dtype, device=x.device,
+                      memory_format=torch.channels_last)
+    rc = _lib().amdk8s_wan_vae_rms_silu_stack(x.data_ptr(), g32.data_ptr(), out.data_ptr(), n * h * w,
+                                              h * w, frames, c, kt, _stream(x))
+    _check(rc, "amdk8s_wan_vae_rms_silu_stack")
+    return out

@@ -202,3 +202,26 @@ def test_comfy_server_runs_prompt_on_gpu(dev, tmp_path):
         f = ComfyClient.output_files(h)[0]
         assert c.get("/view", params=f).content[8:12] == b"WEBP"
         assert c.get("/system_stats").json()["devices"][0]["vram_total"] > 200e9
+
+
+@pytest.mark.parametrize("c", [96, 192, 384])
+def test_vae_rms_silu_stack_kernel(dev, c):
+    from k8s_nvidia_gpus_amd.ops import wan_kernels as WK
+
+    g = torch.Generator(device=dev).manual_seed(c)
+    b, t, h, w = 2, 3, 5, 7
+    x = (torch.randn(b * t, c, h, w, generator=g, device=dev) * 2).bfloat16()
+    x = x.contiguous(memory_format=torch.channels_last)
+    gamma = (torch.rand(c, 1, 1, 1, generator=g, device=dev) + 0.5).bfloat16()
+    y = torch.nn.functional.silu(torch.nn.functional.normalize(x.float(), dim=1) * c ** 0.5
+                                 * gamma.float().view(1, c, 1, 1))
+    plain = WK.vae_rms_silu_stack(x, gamma, t, kt=1)
+    torch.testing.assert_close(plain.float(), y, rtol=2e-2, atol=2e-2)
+    st = WK.vae_rms_silu_stack(x, gamma, t, kt=3).float().view(b, t, 3, c, h, w)
+    yy = y.view(b, t, c, h, w)
+    zero = torch.zeros_like(yy[:, 0])
+    for ti in range(t):
+        for j in range(3):
+            src = ti - 2 + j
+            ref = yy[:, src] if src >= 0 else zero
+            torch.testing.assert_close(st[:, ti, j], ref, rtol=2e-2, atol=2e-2)

@@ -104,7 +104,8 @@ def main(argv=None) -> int:
     SF.set_backend("auto")
     if not a.no_e2e:
         pipe.generate("warm-up", "blurry", a.width, a.height, a.frames, steps=2, cfg=6.0)
-        r = pipe.generate("a panda riding a motorbike through a neon city", "blurry", a.width,
+        # a prompt not seen before: encode_s is the umT5 cost of a new request (cached afterwards)
+        r = pipe.generate("a red fox running through fresh snow at dawn, cinematic", "low quality", a.width,
                           a.height, a.frames, steps=a.steps, cfg=6.0, sampler="uni_pc",
                           scheduler="simple", seed=0)
         res["e2e"] = {k: round(v, 3) for k, v in r.timings.items()}
