@@ -116,15 +116,85 @@ def load_vae(path: str) -> WanVAE:
     return v
 
 
+class DiTRunner:
+    """``x0 = x − σ·v_cfg`` of one sampling step, eager or replayed from a HIP graph.
+
+    The graph is captured once per (latent shape, CFG on/off) with static buffers for x, σ, the
+    guidance scale and the per-layer text K/V; a job copies its K/V in (30 × 2 × 3 MB for the
+    1.3B model) and every step is one ``hipGraphLaunch`` of the ~400 kernels of a DiT forward
+    instead of ~400 launches from Python."""
+
+    def __init__(self, dit: WanDiT, use_graphs: bool = True):
+        self.dit = dit
+        self.use_graphs = use_graphs
+        self._graphs: Dict[tuple, dict] = {}
+        self.captures = 0
+
+    def _body(self, x, sig, g, kv, two):
+        dtype = next(self.dit.parameters()).dtype
+        xin = torch.cat([x, x], 0) if two else x
+        t = (sig * 1000.0).reshape(1).expand(xin.shape[0])
+        v = self.dit(xin.to(dtype), t, kv, out_dtype=torch.float32)
+        if two:
+            v = v[1:2] + g * (v[0:1] - v[1:2])
+        return x - sig * v
+
+    def _capture(self, x, kv, two):
+        key = (tuple(x.shape), two)
+        st = {"x": torch.zeros_like(x), "sig": torch.zeros((), device=x.device),
+              "g": torch.zeros((), device=x.device),
+              "kv": [(torch.zeros_like(k), torch.zeros_like(v)) for k, v in kv]}
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):   # warm-up: hipBLASLt heuristics, lazy caches (RoPE table, fp32 weights)
+                self._body(st["x"], st["sig"], st["g"], st["kv"], two)
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            st["out"] = self._body(st["x"], st["sig"], st["g"], st["kv"], two)
+        st["graph"] = graph
+        st["kv_src"] = None
+        self._graphs[key] = st
+        self.captures += 1
+        return st
+
+    def model(self, kv, cfg: float, device) -> Callable[[torch.Tensor, float], torch.Tensor]:
+        two = len(kv) > 0 and kv[0][0].shape[0] == 2
+        if not (self.use_graphs and torch.device(device).type == "cuda"):
+            def eager(x, sigma):
+                sig = torch.tensor(float(sigma), device=x.device)
+                return self._body(x, sig, torch.tensor(float(cfg), device=x.device), kv, two)
+            return eager
+
+        def replay(x, sigma):
+            key = (tuple(x.shape), two)
+            st = self._graphs.get(key) or self._capture(x, kv, two)
+            if st["kv_src"] is not kv:               # new job: copy its text K/V in once
+                for (dk, dv), (k, v) in zip(st["kv"], kv):
+                    dk.copy_(k)
+                    dv.copy_(v)
+                st["kv_src"] = kv
+            st["x"].copy_(x)
+            st["sig"].fill_(float(sigma))
+            st["g"].fill_(float(cfg))
+            st["graph"].replay()
+            return st["out"].clone()
+
+        return replay
+
+    def reset(self):
+        self._graphs.clear()
+
+
 def ksample(dit: WanDiT, positive: torch.Tensor, negative: Optional[torch.Tensor],
             latent: torch.Tensor, seed: int, steps: int, cfg: float, sampler: str = "uni_pc",
             scheduler: str = "simple", denoise: float = 1.0, shift: float = 8.0,
-            callback=None) -> torch.Tensor:
+            callback=None, runner: Optional[DiTRunner] = None) -> torch.Tensor:
     """ComfyUI ``KSampler`` semantics on a flow model: noise from ``seed`` (CPU generator) mixed
     into ``latent`` at σ_0 (``x = σ₀·ε + (1−σ₀)·latent``), CFG ``uncond + cfg·(cond − uncond)``
     on the velocity, ``steps`` of ``sampler`` over the ``scheduler`` sigmas."""
     dev = next(dit.parameters()).device
-    dtype = next(dit.parameters()).dtype
     sig = S.schedule(scheduler, steps, shift, denoise)
     s0 = float(sig[0])
     lat = latent.to(dev, torch.float32)
@@ -135,15 +205,9 @@ def ksample(dit: WanDiT, positive: torch.Tensor, negative: Optional[torch.Tensor
         if use_cfg:
             ctxs.append(dit.embed_text(negative.to(dev)))
         kv = dit.text_kv(torch.cat(ctxs, 0))
-
-        def model(xx: torch.Tensor, sigma: float) -> torch.Tensor:
-            xin = torch.cat([xx, xx], 0) if use_cfg else xx
-            t = torch.full((xin.shape[0],), sigma * 1000.0, device=dev, dtype=torch.float32)
-            v = dit(xin.to(dtype), t, kv, out_dtype=torch.float32)
-            if use_cfg:
-                v = v[1:2] + cfg * (v[0:1] - v[1:2])
-            return xx - sigma * v
-
+        if runner is None:
+            runner = DiTRunner(dit, use_graphs=False)
+        model = runner.model(kv, cfg, dev)
         return S.sample(sampler, model, x, sig, callback)
 
 
@@ -170,6 +234,7 @@ class WanPipeline:
         self.tokenizer = tokenizer
         self.vae = vae.to(self.device, dtype).eval()
         self.shift = shift
+        self.runner = DiTRunner(self.dit, use_graphs=self.device.type == "cuda")
         self._text_cache: "OrderedDict[str, torch.Tensor]" = OrderedDict()
 
     # ------------------------------------------------------------------ construction
@@ -258,7 +323,7 @@ class WanPipeline:
                       scheduler: str = "simple", seed: int = 0, denoise: float = 1.0,
                       callback=None) -> torch.Tensor:
         return ksample(self.dit, positive, negative, self.empty_latent(width, height, frames), seed,
-                       steps, cfg, sampler, scheduler, denoise, self.shift, callback)
+                       steps, cfg, sampler, scheduler, denoise, self.shift, callback, self.runner)
 
     @torch.no_grad()
     def decode(self, latent: torch.Tensor) -> torch.Tensor:

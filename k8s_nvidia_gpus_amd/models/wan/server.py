@@ -270,6 +270,7 @@ class Executor:
         self.ffmpeg = ffmpeg if ffmpeg is not None else shutil.which("ffmpeg")
         self._counter_lock = threading.Lock()
         self.interrupt = threading.Event()
+        self._runners: Dict[int, Any] = {}     # id(DiT) -> DiTRunner (HIP-graph step per shape)
 
     # --------------------------------------------------------------------- graph walk
     def run(self, graph: dict, on_node: Optional[Callable[[str], None]] = None) -> Dict[str, dict]:
@@ -338,8 +339,12 @@ class Executor:
     # --------------------------------------------------------------------- sampling / decode
     def node_KSampler(self, model, seed, steps, cfg, sampler_name, scheduler, positive, negative,
                       latent_image, denoise=1.0):
-        from .pipeline import ksample
+        from .pipeline import DiTRunner, ksample
 
+        runner = self._runners.get(id(model))
+        if runner is None:
+            runner = DiTRunner(model, use_graphs=next(model.parameters()).is_cuda)
+            self._runners[id(model)] = runner
         lat = latent_image["samples"]
         total = int(steps)
 
@@ -349,7 +354,7 @@ class Executor:
             log.debug("step %d/%d", i + 1, total)
 
         out = ksample(model, positive, negative, lat, int(seed), total, float(cfg), sampler_name,
-                      scheduler, float(denoise), self.shift, cb)
+                      scheduler, float(denoise), self.shift, cb, runner)
         return ({"samples": out.float()},)
 
     @torch.no_grad()

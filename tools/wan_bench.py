@@ -8,8 +8,9 @@ exactly those defaults with random-init weights of the published architectures (
 checkpoints; the arithmetic per step is identical): the 1.3B DiT (30 blocks, 1536 wide, 12 heads),
 the Wan VAE decoder and, with ``--t5``, the umT5-xxl encoder (5.7 B parameters).
 
-Arms: ``native`` (HIP row kernels + flash attention) and ``torch`` (the same model through
-PyTorch ops) for one CFG step (batch 2, 2560 tokens); then the end-to-end job on the native path.
+Arms: ``native-graph`` (HIP row kernels + flash attention, the step replayed from a HIP graph —
+the serving path), ``native`` (same kernels launched eagerly) and ``torch`` (the same model through
+PyTorch ops) for one CFG step (batch 2, 2560 tokens); then the end-to-end job on the serving path.
 Prints one JSON object (``--out`` also writes it).
 """
 from __future__ import annotations
@@ -43,9 +44,9 @@ def heartbeat(period: float = 30.0) -> None:
     threading.Thread(target=run, daemon=True).start()
 
 
-def step_ms(pipe: WanPipeline, kv, shape, iters: int, warmup: int) -> float:
+def step_ms(pipe: WanPipeline, kv, shape, iters: int, warmup: int, graph: bool = False) -> float:
     x = torch.randn(shape, device=pipe.device)
-    model = pipe.denoiser(kv, 6.0)
+    model = pipe.runner.model(kv, 6.0, pipe.device) if graph else pipe.denoiser(kv, 6.0)
     for _ in range(warmup):
         model(x, 0.7)
     torch.cuda.synchronize()
@@ -71,7 +72,7 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=25)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--arms", default="native,torch")
+    ap.add_argument("--arms", default="native-graph,native,torch")
     ap.add_argument("--t5", action="store_true", help="include the umT5-xxl encoder (11 GB bf16)")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--out")
@@ -96,7 +97,7 @@ def main(argv=None) -> int:
         WF.set_backend("torch" if arm == "torch" else "auto")
         SF.set_backend("torch" if arm == "torch" else "auto")
         kv = pipe.text_kv(pos, neg)
-        ms = step_ms(pipe, kv, lat, a.iters, a.warmup)
+        ms = step_ms(pipe, kv, lat, a.iters, a.warmup, graph=arm == "native-graph")
         res["arms"][arm] = {"cfg_step_ms": round(ms, 3), "tflops": round(flops / ms / 1e9, 1)}
         print(f"[wan_bench] {arm}: CFG step {ms:.2f} ms ({flops / ms / 1e9:.0f} TFLOPS)", file=sys.stderr,
               flush=True)
