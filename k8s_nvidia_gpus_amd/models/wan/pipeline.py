@@ -124,10 +124,11 @@ class DiTRunner:
     1.3B model) and every step is one ``hipGraphLaunch`` of the ~400 kernels of a DiT forward
     instead of ~400 launches from Python."""
 
-    def __init__(self, dit: WanDiT, use_graphs: bool = True):
+    def __init__(self, dit: WanDiT, use_graphs: bool = True, max_graphs: int = 4):
         self.dit = dit
         self.use_graphs = use_graphs
-        self._graphs: Dict[tuple, dict] = {}
+        self.max_graphs = max_graphs          # each graph pins its activation pool (~0.5 GB at 1.3B)
+        self._graphs: "OrderedDict[tuple, dict]" = OrderedDict()
         self.captures = 0
 
     def _body(self, x, sig, g, kv, two):
@@ -156,6 +157,8 @@ class DiTRunner:
         st["graph"] = graph
         st["kv_src"] = None
         self._graphs[key] = st
+        while len(self._graphs) > self.max_graphs:
+            self._graphs.popitem(last=False)
         self.captures += 1
         return st
 
@@ -169,7 +172,11 @@ class DiTRunner:
 
         def replay(x, sigma):
             key = (tuple(x.shape), two)
-            st = self._graphs.get(key) or self._capture(x, kv, two)
+            st = self._graphs.get(key)
+            if st is None:
+                st = self._capture(x, kv, two)
+            else:
+                self._graphs.move_to_end(key)
             if st["kv_src"] is not kv:               # new job: copy its text K/V in once
                 for (dk, dv), (k, v) in zip(st["kv"], kv):
                     dk.copy_(k)
