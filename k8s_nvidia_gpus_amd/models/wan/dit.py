@@ -177,15 +177,26 @@ class WanDiT(nn.Module):
         e0 = self.time_projection(e).float().view(-1, 6, self.cfg.dim)
         return e.float(), e0
 
-    def forward(self, x: torch.Tensor, t: torch.Tensor, text_kv, out_dtype=torch.float32):
+    def forward(self, x: torch.Tensor, t: torch.Tensor, text_kv, out_dtype=torch.float32,
+                sp=None):
         """x: [B, C, F, H, W] latent; t: [B] timesteps (flow sigma × 1000); text_kv: from
-        :meth:`text_kv` (batch B).  Returns the velocity prediction [B, C, F, H, W]."""
+        :meth:`text_kv` (batch B).  Returns the velocity prediction [B, C, F, H, W].  With ``sp``
+        (:class:`parallel.SequenceParallel`) this rank runs 1/P of the tokens through the blocks
+        and self-attention exchanges heads↔tokens with its peers."""
         cfg = self.cfg
         grid = self.grid(x.shape)
         cos, sin = self.rope(grid, x.device)
         wdt = self.patch_embedding.weight.dtype
         pw = self.patch_embedding.weight.reshape(cfg.dim, -1)
         res = F.linear(self.patchify(x.to(wdt)), pw, self.patch_embedding.bias).float()  # fp32 stream
+        if sp is not None and sp.world > 1:
+            sp.check(res.shape[1], cfg.heads)
+            res, cos, sin = sp.shard(res), sp.shard(cos, 0), sp.shard(sin, 0)
+
+            def attend(q, k, v, heads):
+                return sp.attention(q, k, v, heads, WF.attention)
+        else:
+            attend = WF.attention
         b, l, d = res.shape
         e, e0 = self.time_mod(t)
         mods = [(blk.modulation.float() + e0) for blk in self.blocks]   # [B, 6, d] each
@@ -199,7 +210,7 @@ class WanDiT(nn.Module):
             q, k, v = qkv[..., :d], qkv[..., d:2 * d], qkv[..., 2 * d:]
             WF.rmsnorm_rope_qk(qkv, blk.self_attn.norm_q.weight, blk.self_attn.norm_k.weight,
                                cos, sin, cfg.heads, cfg.eps)
-            o = blk.self_attn.o(WF.attention(q, k, v, cfg.heads))
+            o = blk.self_attn.o(attend(q, k, v, cfg.heads))
             h = WF.add_ln(res, o, m[:, 2], blk.norm3.weight.float()[None], blk.norm3.bias.float()[None],
                           cfg.eps, wdt)
             # cross-attention over the cached text K/V
@@ -219,6 +230,8 @@ class WanDiT(nn.Module):
                 hm = self.head.modulation.float() + e[:, None, :]      # [B, 2, d]
                 h = WF.add_ln(res, o, m[:, 5], 1.0 + hm[:, 1], hm[:, 0], cfg.eps, wdt)
         y = self.head.head(h)
+        if sp is not None and sp.world > 1:
+            y = sp.gather(y)
         return self.unpatchify(y.to(out_dtype), grid)
 
 

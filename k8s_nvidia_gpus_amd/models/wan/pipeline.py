@@ -124,9 +124,11 @@ class DiTRunner:
     1.3B model) and every step is one ``hipGraphLaunch`` of the ~400 kernels of a DiT forward
     instead of ~400 launches from Python."""
 
-    def __init__(self, dit: WanDiT, use_graphs: bool = True, max_graphs: int = 4):
+    def __init__(self, dit: WanDiT, use_graphs: bool = True, max_graphs: int = 4, sp=None):
         self.dit = dit
-        self.use_graphs = use_graphs
+        self.sp = sp if sp is not None and sp.world > 1 else None
+        # collectives stay outside graphs: a sequence-parallel step runs eagerly
+        self.use_graphs = use_graphs and self.sp is None
         self.max_graphs = max_graphs          # each graph pins its activation pool (~0.5 GB at 1.3B)
         self._graphs: "OrderedDict[tuple, dict]" = OrderedDict()
         self.captures = 0
@@ -135,7 +137,7 @@ class DiTRunner:
         dtype = next(self.dit.parameters()).dtype
         xin = torch.cat([x, x], 0) if two else x
         t = (sig * 1000.0).reshape(1).expand(xin.shape[0])
-        v = self.dit(xin.to(dtype), t, kv, out_dtype=torch.float32)
+        v = self.dit(xin.to(dtype), t, kv, out_dtype=torch.float32, sp=self.sp)
         if two:
             v = v[1:2] + g * (v[0:1] - v[1:2])
         return x - sig * v
@@ -197,7 +199,7 @@ class DiTRunner:
 def ksample(dit: WanDiT, positive: torch.Tensor, negative: Optional[torch.Tensor],
             latent: torch.Tensor, seed: int, steps: int, cfg: float, sampler: str = "uni_pc",
             scheduler: str = "simple", denoise: float = 1.0, shift: float = 8.0,
-            callback=None, runner: Optional[DiTRunner] = None) -> torch.Tensor:
+            callback=None, runner: Optional[DiTRunner] = None, sp=None) -> torch.Tensor:
     """ComfyUI ``KSampler`` semantics on a flow model: noise from ``seed`` (CPU generator) mixed
     into ``latent`` at σ_0 (``x = σ₀·ε + (1−σ₀)·latent``), CFG ``uncond + cfg·(cond − uncond)``
     on the velocity, ``steps`` of ``sampler`` over the ``scheduler`` sigmas."""
@@ -213,7 +215,7 @@ def ksample(dit: WanDiT, positive: torch.Tensor, negative: Optional[torch.Tensor
             ctxs.append(dit.embed_text(negative.to(dev)))
         kv = dit.text_kv(torch.cat(ctxs, 0))
         if runner is None:
-            runner = DiTRunner(dit, use_graphs=False)
+            runner = DiTRunner(dit, use_graphs=False, sp=sp)
         model = runner.model(kv, cfg, dev)
         return S.sample(sampler, model, x, sig, callback)
 
@@ -233,7 +235,8 @@ class WanResult:
 
 class WanPipeline:
     def __init__(self, dit: WanDiT, t5: Optional[UMT5Encoder], tokenizer, vae: WanVAE,
-                 device: torch.device, dtype: torch.dtype = torch.bfloat16, shift: float = 8.0):
+                 device: torch.device, dtype: torch.dtype = torch.bfloat16, shift: float = 8.0,
+                 sp=None):
         self.device = torch.device(device)
         self.dtype = dtype
         self.dit = dit.to(self.device, dtype).eval().fuse()
@@ -241,7 +244,7 @@ class WanPipeline:
         self.tokenizer = tokenizer
         self.vae = vae.to(self.device, dtype).eval()
         self.shift = shift
-        self.runner = DiTRunner(self.dit, use_graphs=self.device.type == "cuda")
+        self.runner = DiTRunner(self.dit, use_graphs=self.device.type == "cuda", sp=sp)
         self._text_cache: "OrderedDict[str, torch.Tensor]" = OrderedDict()
 
     # ------------------------------------------------------------------ construction
