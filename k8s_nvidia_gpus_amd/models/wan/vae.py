@@ -194,7 +194,16 @@ class WanVAE(nn.Module):
         dt = self.conv2.weight.dtype
         z = (z.float() * std + mean).to(dt)
         x = z.permute(0, 2, 1, 3, 4).reshape(b * t, c, h, w).contiguous(memory_format=torch.channels_last)
-        x = self.decoder(self.conv2(x, b), b)
+        # MIOpen "find" per convolution shape (exhaustive solver search, cached in-process and in
+        # its find-db): the immediate-mode heuristic picks 256x32 igemm tiles for the 288->96
+        # full-resolution convs; the searched solvers halve the decode (87 -> 43 ms, 13 frames
+        # 512x320; tools/wan_vae_prof.py)
+        prev = torch.backends.cudnn.benchmark
+        torch.backends.cudnn.benchmark = True
+        try:
+            x = self.decoder(self.conv2(x, b), b)
+        finally:
+            torch.backends.cudnn.benchmark = prev
         n, co, hh, ww = x.shape
         return x.reshape(b, n // b, co, hh, ww).permute(0, 2, 1, 3, 4).clamp_(-1, 1)
 

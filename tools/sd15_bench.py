@@ -73,7 +73,11 @@ def main(argv=None) -> int:
     ap.add_argument("--batches", default="1,8", help="end-to-end batch sizes ('' = skip)")
     ap.add_argument("--tiny", action="store_true", help="miniature config (plumbing check only)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--miopen-find", action="store_true",
+                    help="torch.backends.cudnn.benchmark: MIOpen solver search per conv shape")
     args = ap.parse_args(argv)
+    if args.miopen_find:
+        torch.backends.cudnn.benchmark = True
     if not torch.cuda.is_available():
         print("sd15_bench needs an MI355X", file=sys.stderr)
         return 2
