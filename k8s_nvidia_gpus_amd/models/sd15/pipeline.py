@@ -108,9 +108,17 @@ class StableDiffusion:
 
     def __init__(self, model_dir: Optional[str] = None, device: Union[str, torch.device] = "cuda",
                  dtype: torch.dtype = torch.float16, cfg: SD15Config = SD15,
-                 scheduler: str = "pndm", use_graphs: bool = True, init_seed: int = 0):
+                 scheduler: str = "pndm", use_graphs: bool = True, init_seed: int = 0,
+                 miopen_find: bool = True):
         self.cfg = cfg
         self.device = torch.device(device)
+        if miopen_find and self.device.type == "cuda":
+            # MIOpen "find": exhaustive solver search per convolution shape (first call of a shape,
+            # cached in-process and in the find-db on the PVC) instead of the immediate-mode
+            # heuristic — UNet CFG pass 8.1 -> 7.8 ms, batch-8 images 7.7 -> 9.1 img/s
+            # (profiles/r02_session5/sd15_miopen_find.json).  Process-wide: the service owns its
+            # process.
+            torch.backends.cudnn.benchmark = True
         if self.device.type != "cuda":
             dtype = torch.float32
         self.dtype = dtype
