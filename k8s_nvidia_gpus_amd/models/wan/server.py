@@ -488,13 +488,11 @@ class PromptQueue:
                             e.class_type, e)
             dt = time.time() - t0
             self.stats["exec_seconds"] += dt
+            # "completed" marks the prompt as final (the client then reads status_str)
             entry = {"prompt": [job.number, job.prompt_id, job.graph, job.extra, []],
                      "outputs": outputs,
-                     "status": {"status_str": status, "completed": status == "success",
-                                "messages": msgs},
+                     "status": {"status_str": status, "completed": True, "messages": msgs},
                      "meta": {"execution_s": round(dt, 3)}}
-            # ComfyUI reports completed=True only for success; a failed prompt is still final
-            entry["status"]["completed"] = True if status == "success" else True
             with self._lock:
                 self._history[job.prompt_id] = entry
                 self._order.append(job.prompt_id)
@@ -546,7 +544,21 @@ class PromptQueue:
 
 
 # --------------------------------------------------------------------------------------------- app
-def create_app(store: ModelStore, out_dir: str, shift: float = 8.0, ffmpeg: Optional[str] = None):
+def warmup_graph(store: ModelStore, width: int = 512, height: int = 320, frames: int = 16) -> Optional[dict]:
+    """A one-step job at the default size with the reference client's model files, when all three
+    exist: loads the models and pays MIOpen's per-shape kernel compilation + solver search, the
+    hipBLASLt heuristics and the HIP-graph capture before the pod reports ready."""
+    from ..comfy_client import WanJob, build_wan_graph
+
+    job = WanJob(prompt="warm-up", negative="", width=width, height=height, frames=frames, steps=1,
+                 mode="video", formats=("webp",), prefix="_warmup/wan")
+    if any(job.models[k] not in store.names(k) for k in ("unet", "clip", "vae")):
+        return None
+    return build_wan_graph(job)
+
+
+def create_app(store: ModelStore, out_dir: str, shift: float = 8.0, ffmpeg: Optional[str] = None,
+               warmup: Optional[Tuple[int, int, int]] = None):
     from fastapi import FastAPI, HTTPException
     from fastapi.responses import JSONResponse, PlainTextResponse, Response
 
@@ -556,6 +568,26 @@ def create_app(store: ModelStore, out_dir: str, shift: float = 8.0, ffmpeg: Opti
     app = FastAPI(title="Wan2.1 ComfyUI-compatible API (MI355X)")
     app.state.queue = pq
     app.state.executor = ex
+    ready = threading.Event()
+    app.state.ready = ready
+    if warmup is not None:
+        graph = warmup_graph(store, *warmup)
+        if graph is None:
+            log.info("warm-up skipped: the reference model files are not all present")
+            ready.set()
+        else:
+            job = pq.submit(graph, "warmup")
+
+            def watch():
+                while pq.history(job.prompt_id) == {}:
+                    time.sleep(0.5)
+                st = pq.history(job.prompt_id)[job.prompt_id]["status"]["status_str"]
+                log.info("warm-up finished: %s", st)
+                ready.set()
+
+            threading.Thread(target=watch, daemon=True, name="wan-warmup").start()
+    else:
+        ready.set()
 
     @app.get("/health")
     def health():
@@ -563,6 +595,8 @@ def create_app(store: ModelStore, out_dir: str, shift: float = 8.0, ffmpeg: Opti
 
     @app.get("/queue")
     def get_queue():
+        if not ready.is_set():     # readiness: 503 until the start-up warm-up job has run
+            return JSONResponse({"status": "warming up"}, 503)
         return pq.queue_state()
 
     @app.post("/queue")
@@ -725,6 +759,8 @@ def main(argv=None) -> int:  # pragma: no cover - container entry point
     ap.add_argument("--base-directory", default=os.environ.get("COMFY_BASE", "/data"))
     ap.add_argument("--output-directory", default=None)
     ap.add_argument("--shift", type=float, default=8.0)
+    ap.add_argument("--warmup", default=os.environ.get("WAN_WARMUP", ""),
+                    help="WxHxF: run one 1-step job of that size before /queue reports ready")
     ap.add_argument("--synthetic", action="store_true",
                     help="random-init weights under the reference file names (no checkpoints)")
     a = ap.parse_args(argv)
@@ -732,7 +768,8 @@ def main(argv=None) -> int:  # pragma: no cover - container entry point
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     store = synthetic_store(dev) if a.synthetic else ModelStore(a.base_directory, dev)
     out = a.output_directory or os.path.join(a.base_directory, "output")
-    uvicorn.run(create_app(store, out, a.shift), host=a.listen, port=a.port)
+    warm = tuple(int(v) for v in a.warmup.lower().split("x")) if a.warmup else None
+    uvicorn.run(create_app(store, out, a.shift, warmup=warm), host=a.listen, port=a.port)
     return 0
 
 

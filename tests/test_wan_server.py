@@ -167,3 +167,12 @@ def test_reference_client_flow_against_live_server(app, tmp_path):
         th.join(10)
     assert os.path.isdir(tmp_path / "output")
     time.sleep(0)
+
+
+def test_startup_warmup_gates_readiness(store, tmp_path):
+    app = create_app(store, str(tmp_path / "out"), ffmpeg="", warmup=(64, 48, 5))
+    with TestClient(app) as c:
+        assert app.state.ready.wait(120)
+        assert c.get("/queue").status_code == 200
+        hist = c.get("/history").json()
+        assert len(hist) == 1 and next(iter(hist.values()))["status"]["status_str"] == "success"
