@@ -75,11 +75,12 @@ def main(argv=None) -> int:
     ap.add_argument("--arms", default="native-graph,native,torch")
     ap.add_argument("--t5", action="store_true", help="include the umT5-xxl encoder (11 GB bf16)")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--model", default="1.3b", choices=["1.3b", "14b"])
     ap.add_argument("--out")
     a = ap.parse_args(argv)
     heartbeat()
     dev = torch.device("cuda", 0)
-    dcfg = WanDiTConfig.wan21_t2v_1_3b()
+    dcfg = WanDiTConfig.wan21_t2v_14b() if a.model == "14b" else WanDiTConfig.wan21_t2v_1_3b()
     t0 = time.time()
     pipe = WanPipeline.synthetic(dev, dcfg, UMT5Config.umt5_xxl() if a.t5 else None,
                                  WanVAEConfig.wan21())
@@ -88,7 +89,7 @@ def main(argv=None) -> int:
     lat = (1, 16, latent_frames(a.frames), a.height // 8, a.width // 8)
     tokens = lat[2] * (lat[3] // 2) * (lat[4] // 2)
     pos, neg = pipe.encode("a panda riding a motorbike through a neon city"), pipe.encode("blurry")
-    res = {"model": "Wan2.1-T2V-1.3B (random-init weights of the published architecture)",
+    res = {"model": f"Wan2.1-T2V-{a.model.upper()} (random-init weights of the published architecture)",
            "video": {"width": a.width, "height": a.height, "frames_requested": a.frames,
                      "latent": list(lat), "tokens": tokens},
            "dtype": "bf16", "init_s": round(init_s, 2), "arms": {}}
