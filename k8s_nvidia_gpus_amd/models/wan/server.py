@@ -22,7 +22,6 @@ ComfyUI base directory, so the existing PVC layout (cluster-config/apps/comfyui)
 """
 from __future__ import annotations
 
-import io
 import itertools
 import json
 import logging
@@ -271,6 +270,19 @@ class Executor:
         self._counter_lock = threading.Lock()
         self.interrupt = threading.Event()
         self._runners: Dict[int, Any] = {}     # id(DiT) -> DiTRunner (HIP-graph step per shape)
+        # output encoding (PNG / WEBP / ffmpeg) runs off the GPU worker: the next prompt's
+        # sampling overlaps the previous prompt's CPU-side encode
+        from concurrent.futures import ThreadPoolExecutor
+
+        self.encode_pool = ThreadPoolExecutor(max_workers=2, thread_name_prefix="wan-encode")
+        self._writes: List[Tuple[str, str, Any]] = []
+
+    def _defer(self, node_class: str, fn, *args) -> None:
+        self._writes.append((node_class, fn.__name__, self.encode_pool.submit(fn, *args)))
+
+    def take_writes(self) -> List[Tuple[str, str, Any]]:
+        w, self._writes = self._writes, []
+        return w
 
     # --------------------------------------------------------------------- graph walk
     def run(self, graph: dict, on_node: Optional[Callable[[str], None]] = None) -> Dict[str, dict]:
@@ -382,25 +394,20 @@ class Executor:
                     return name, sub
 
     def node_SaveImage(self, images: Image, filename_prefix="ComfyUI"):
-        from PIL import Image as PILImage
-
         res = []
         for fr in images.frames:
             name, sub = self._next_name(filename_prefix, "png")
-            PILImage.fromarray(fr.numpy()).save(os.path.join(self.out_dir, sub, name), compress_level=4)
+            self._defer("SaveImage", _write_png, fr.numpy(), os.path.join(self.out_dir, sub, name))
             res.append({"filename": name, "subfolder": sub, "type": "output"})
         return {"ui": {"images": res}}
 
     def node_SaveAnimatedWEBP(self, images: Image, filename_prefix="ComfyUI", fps=6.0, lossless=True,
                               quality=80, method="default"):
-        from PIL import Image as PILImage
-
         meth = {"default": 4, "fastest": 0, "slowest": 6}.get(method, 4)
-        pil = [PILImage.fromarray(fr.numpy()) for fr in images.frames]
         name, sub = self._next_name(filename_prefix, "webp")
-        pil[0].save(os.path.join(self.out_dir, sub, name), save_all=True, append_images=pil[1:],
-                    duration=int(1000.0 / float(fps)), lossless=bool(lossless), quality=int(quality),
-                    method=meth, loop=0)
+        self._defer("SaveAnimatedWEBP", _write_webp, images.frames.numpy(),
+                    os.path.join(self.out_dir, sub, name), int(1000.0 / float(fps)), bool(lossless),
+                    int(quality), meth)
         return {"ui": {"images": [{"filename": name, "subfolder": sub, "type": "output"}],
                        "animated": [True]}}
 
@@ -415,12 +422,29 @@ class Executor:
         cmd = [self.ffmpeg, "-y", "-loglevel", "error", "-f", "rawvideo", "-pix_fmt", "rgb24",
                "-s", f"{w}x{h}", "-r", str(float(fps)), "-i", "-", "-c:v", enc, "-crf", str(int(crf)),
                "-b:v", "0", "-pix_fmt", "yuv420p", os.path.join(self.out_dir, sub, name)]
-        proc = subprocess.run(cmd, input=fr.numpy().tobytes(), stdout=subprocess.PIPE,
-                              stderr=subprocess.PIPE, timeout=600)
-        if proc.returncode != 0:
-            raise RuntimeError(f"ffmpeg failed: {proc.stderr.decode(errors='replace')[-300:]}")
+        self._defer("SaveWEBM", _run_ffmpeg, cmd, fr.numpy().tobytes())
         return {"ui": {"images": [{"filename": name, "subfolder": sub, "type": "output"}],
                        "animated": [True]}}
+
+
+def _write_png(arr, path: str) -> None:
+    from PIL import Image as PILImage
+
+    PILImage.fromarray(arr).save(path, compress_level=4)
+
+
+def _write_webp(frames, path: str, duration_ms: int, lossless: bool, quality: int, method: int) -> None:
+    from PIL import Image as PILImage
+
+    pil = [PILImage.fromarray(f) for f in frames]
+    pil[0].save(path, save_all=True, append_images=pil[1:], duration=duration_ms, lossless=lossless,
+                quality=quality, method=method, loop=0)
+
+
+def _run_ffmpeg(cmd: List[str], data: bytes) -> None:
+    proc = subprocess.run(cmd, input=data, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
+    if proc.returncode != 0:
+        raise RuntimeError(f"ffmpeg failed: {proc.stderr.decode(errors='replace')[-300:]}")
 
 
 # ------------------------------------------------------------------------------------------- queue
@@ -439,6 +463,7 @@ class PromptQueue:
         self._q: "queue.Queue[Optional[Job]]" = queue.Queue()
         self._pending: List[Job] = []
         self._running: Optional[Job] = None
+        self._finalizing = 0                   # prompts whose outputs are still being encoded
         self._history: Dict[str, dict] = {}
         self._order: List[str] = []
         self._lock = threading.Lock()
@@ -468,37 +493,61 @@ class PromptQueue:
             self.ex.interrupt.clear()
             t0 = time.time()
             msgs: List[list] = [["execution_start", {"prompt_id": job.prompt_id, "timestamp": int(t0 * 1000)}]]
-            status, outputs = "success", {}
+            status, outputs, kind = "success", {}, "completed"
             try:
                 outputs = self.ex.run(job.graph)
-                msgs.append(["execution_success", {"prompt_id": job.prompt_id,
-                                                   "timestamp": int(time.time() * 1000)}])
-                self.stats["completed"] += 1
             except Interrupted:
-                status = "error"
+                status, kind = "error", "interrupted"
                 msgs.append(["execution_interrupted", {"prompt_id": job.prompt_id}])
-                self.stats["interrupted"] += 1
             except NodeError as e:
-                status = "error"
+                status, kind = "error", "failed"
                 msgs.append(["execution_error", {"prompt_id": job.prompt_id, "node_id": e.node_id,
                                                  "node_type": e.class_type, "exception_message": str(e),
                                                  "exception_type": e.kind}])
-                self.stats["failed"] += 1
                 log.warning("prompt %s failed at node %s (%s): %s", job.prompt_id, e.node_id,
                             e.class_type, e)
-            dt = time.time() - t0
-            self.stats["exec_seconds"] += dt
-            # "completed" marks the prompt as final (the client then reads status_str)
-            entry = {"prompt": [job.number, job.prompt_id, job.graph, job.extra, []],
-                     "outputs": outputs,
-                     "status": {"status_str": status, "completed": True, "messages": msgs},
-                     "meta": {"execution_s": round(dt, 3)}}
+            gpu_s = time.time() - t0
+            writes = self.ex.take_writes()
             with self._lock:
-                self._history[job.prompt_id] = entry
-                self._order.append(job.prompt_id)
-                while len(self._order) > self.max_history:
-                    self._history.pop(self._order.pop(0), None)
                 self._running = None
+                self._finalizing += 1
+            if writes:
+                threading.Thread(target=self._finalize, name="wan-finalize", daemon=True,
+                                 args=(job, status, kind, outputs, msgs, t0, gpu_s, writes)).start()
+            else:
+                self._finalize(job, status, kind, outputs, msgs, t0, gpu_s, writes)
+
+    def _finalize(self, job: Job, status: str, kind: str, outputs: dict, msgs: List[list],
+                  t0: float, gpu_s: float, writes) -> None:
+        """Wait for the prompt's output files, then publish its history entry (a client polling
+        /history never sees a prompt as done before its files exist)."""
+        for node_class, what, fut in writes:
+            try:
+                fut.result()
+            except Exception as e:  # noqa: BLE001 - reported like a node failure
+                if status == "success":
+                    status, kind = "error", "failed"
+                    msgs.append(["execution_error", {"prompt_id": job.prompt_id, "node_id": "",
+                                                     "node_type": node_class,
+                                                     "exception_message": f"{what}: {e}",
+                                                     "exception_type": "execution_error"}])
+        if status == "success":
+            msgs.append(["execution_success", {"prompt_id": job.prompt_id,
+                                               "timestamp": int(time.time() * 1000)}])
+        dt = time.time() - t0
+        # "completed" marks the prompt as final (the client then reads status_str)
+        entry = {"prompt": [job.number, job.prompt_id, job.graph, job.extra, []],
+                 "outputs": outputs,
+                 "status": {"status_str": status, "completed": True, "messages": msgs},
+                 "meta": {"execution_s": round(dt, 3), "gpu_s": round(gpu_s, 3)}}
+        with self._lock:
+            self.stats[kind] += 1
+            self.stats["exec_seconds"] += dt
+            self._history[job.prompt_id] = entry
+            self._order.append(job.prompt_id)
+            while len(self._order) > self.max_history:
+                self._history.pop(self._order.pop(0), None)
+            self._finalizing -= 1
 
     def queue_state(self) -> dict:
         def row(j: Job):
@@ -532,7 +581,7 @@ class PromptQueue:
 
     def remaining(self) -> int:
         with self._lock:
-            return len(self._pending) + (1 if self._running else 0)
+            return len(self._pending) + (1 if self._running else 0) + self._finalizing
 
     def wait_idle(self, timeout: float = 60.0) -> bool:
         deadline = time.time() + timeout

@@ -115,6 +115,10 @@ def test_savewebm_drives_ffmpeg(store, tmp_path):
 
     frames = torch.randint(0, 255, (3, 16, 32, 3), dtype=torch.uint8)
     ui = ex.node_SaveWEBM(Image(frames), "clips/wan", "vp9", 24, 32)["ui"]
+    writes = ex.take_writes()                  # encoding runs on the encode pool
+    assert [w[0] for w in writes] == ["SaveWEBM"]
+    for _, _, fut in writes:
+        fut.result(timeout=60)
     f = ui["images"][0]
     assert f["subfolder"] == "clips" and f["filename"] == "wan_00001_.webm"
     path = tmp_path / "out" / "clips" / f["filename"]
@@ -176,3 +180,18 @@ def test_startup_warmup_gates_readiness(store, tmp_path):
         assert c.get("/queue").status_code == 200
         hist = c.get("/history").json()
         assert len(hist) == 1 and next(iter(hist.values()))["status"]["status_str"] == "success"
+
+
+def test_encode_failure_reported_after_gpu_part(store, tmp_path):
+    """A saver failing on the encode pool turns the prompt into an error entry naming the node."""
+    bad = tmp_path / "ffmpeg"
+    bad.write_text("#!/bin/sh\necho boom >&2\nexit 3\n")
+    bad.chmod(0o755)
+    app = create_app(store, str(tmp_path / "out"), ffmpeg=str(bad))
+    with TestClient(app) as c:
+        pid = c.post("/prompt", json={"prompt": build_wan_graph(_job(formats=("webm",)))}).json()["prompt_id"]
+        assert app.state.queue.wait_idle(120)
+        st = c.get(f"/history/{pid}").json()[pid]["status"]
+        assert st["status_str"] == "error" and st["completed"]
+        err = [m for m in st["messages"] if m[0] == "execution_error"][0][1]
+        assert err["node_type"] == "SaveWEBM" and "boom" in err["exception_message"]

@@ -52,6 +52,14 @@ def main():
             res.setdefault("files", []).append({"name": f["filename"], "bytes": size,
                                                 "exec_s": h["meta"]["execution_s"]})
         res["request_s"] = lat
+        # burst: 4 prompts queued at once — sampling of prompt i+1 overlaps the WEBP encode of i
+        t1 = time.perf_counter()
+        pids = [c.post("/prompt", json={"prompt": build_wan_graph(
+            WanJob(prompt=f"burst {i}", seed=10 + i, formats=("webp",)))}).json()["prompt_id"]
+            for i in range(4)]
+        assert app.state.queue.wait_idle(900)
+        assert all(c.get(f"/history/{p}").json()[p]["status"]["status_str"] == "success" for p in pids)
+        res["burst4_s"] = round(time.perf_counter() - t1, 3)
     res["job"] = "512x320, 16 frames (13 decoded), 25 uni_pc/simple steps, CFG 6, animated WEBP"
     print(json.dumps(res), flush=True)
 
