@@ -160,6 +160,7 @@ class _Job:
     negative_prompt: Optional[str] = None
     done: threading.Event = field(default_factory=threading.Event)
     png: Optional[bytes] = None
+    image: Any = None                 # PIL image from the GPU worker; PNG-encoded by the request thread
     error: Optional[BaseException] = None
     batch_size: int = 0
     t_enqueue: float = field(default_factory=time.time)
@@ -289,10 +290,10 @@ class GenerationWorker:
                 images = self._pipe(**kwargs).images
             if len(images) != len(batch):
                 raise RuntimeError(f"pipeline returned {len(images)} images for {len(batch)} prompts")
+            # PNG encoding (~25 ms per 512² image) happens in each request's own thread, not here:
+            # the GPU worker moves straight on to the next coalesced batch
             for j, img in zip(batch, images):
-                buf = io.BytesIO()
-                img.save(buf, format="PNG")
-                j.png = buf.getvalue()
+                j.image = img
                 j.batch_size = len(batch)
         except BaseException as e:  # noqa: BLE001 - delivered to every waiting request
             logger.exception("generation failed")
@@ -432,6 +433,11 @@ def create_app(settings: Optional[Settings] = None,
             if prom:
                 m_req.labels("error").inc()
             raise HTTPException(500, f"generation failed: {job.error}")
+        if job.png is None:
+            buf = io.BytesIO()
+            job.image.save(buf, format="PNG")
+            job.png = buf.getvalue()
+            job.image = None
         latency = time.time() - t0
         with last_lock:
             state["last"] = job.png
