@@ -278,7 +278,8 @@ class Executor:
         self._writes: List[Tuple[str, str, Any]] = []
 
     def _defer(self, node_class: str, fn, *args) -> None:
-        self._writes.append((node_class, fn.__name__, self.encode_pool.submit(fn, *args)))
+        self._writes.append((node_class, fn.__name__,
+                             self.encode_pool.submit(_removing_on_failure(fn), *args)))
 
     def take_writes(self) -> List[Tuple[str, str, Any]]:
         w, self._writes = self._writes, []
@@ -425,6 +426,23 @@ class Executor:
         self._defer("SaveWEBM", _run_ffmpeg, cmd, fr.numpy().tobytes())
         return {"ui": {"images": [{"filename": name, "subfolder": sub, "type": "output"}],
                        "animated": [True]}}
+
+
+def _removing_on_failure(fn):
+    """An encoder that fails leaves no truncated or placeholder file behind (the name was reserved
+    with an empty file by ``Executor._next_name``)."""
+    def wrapped(*args):
+        path = args[1] if fn is not _run_ffmpeg else args[0][-1]
+        try:
+            fn(*args)
+        except BaseException:
+            try:
+                os.remove(path)
+            except OSError:
+                pass
+            raise
+    wrapped.__name__ = fn.__name__
+    return wrapped
 
 
 def _write_png(arr, path: str) -> None:

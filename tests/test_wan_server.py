@@ -195,3 +195,4 @@ def test_encode_failure_reported_after_gpu_part(store, tmp_path):
         assert st["status_str"] == "error" and st["completed"]
         err = [m for m in st["messages"] if m[0] == "execution_error"][0][1]
         assert err["node_type"] == "SaveWEBM" and "boom" in err["exception_message"]
+    assert not list((tmp_path / "out").rglob("*.webm"))        # no empty placeholder left
