@@ -54,7 +54,7 @@ def add_ln_supported(c: int) -> bool:
     return bool(_lib().amdk8s_wan_row_supported(c))
 
 
-def _row_vec(t: torch.Tensor, c: int, what: str) -> Tuple[torch.Tensor, int]:
+def _row_vec(t: torch.Tensor, c: int) -> Tuple[torch.Tensor, int]:
     """fp32 [B, C] / [1, C] (any batch stride, unit inner stride, 16-byte aligned rows)."""
     if t.dtype != torch.float32 or t.stride(-1) != 1 or t.shape[-1] != c:
         t = t.float().contiguous()
@@ -79,14 +79,12 @@ def add_ln(x: torch.Tensor, y: Optional[torch.Tensor], gate: Optional[torch.Tens
             y = y.to(torch.bfloat16).contiguous()
         if (b > 1 and y.stride(0) != l * y.stride(1)) or y.stride(1) % 8 or y.data_ptr() % 16:
             y = y.contiguous()
-    keep = []
     g_ptr, sg = None, 0
     if y is not None and gate is not None:
-        gate, sg = _row_vec(gate, c, "gate")
-        keep.append(gate)
+        gate, sg = _row_vec(gate, c)          # the local name keeps a converted copy alive
         g_ptr = gate.data_ptr()
-    mul, sm = _row_vec(mul, c, "mul")
-    add, sa = _row_vec(add, c, "add")
+    mul, sm = _row_vec(mul, c)
+    add, sa = _row_vec(add, c)
     out = torch.empty((b, l, c), dtype=torch.bfloat16, device=x.device)
     rc = _lib().amdk8s_wan_add_ln(x.data_ptr(), y.data_ptr() if y is not None else None,
                                   y.stride(1) if y is not None else 0, g_ptr, sg, mul.data_ptr(), sm,
