@@ -624,6 +624,21 @@ def warmup_graph(store: ModelStore, width: int = 512, height: int = 320, frames:
     return build_wan_graph(job)
 
 
+def _freeze_tunableop() -> None:
+    """With PyTorch TunableOp enabled (the Deployment sets it), GEMM tuning runs only during the
+    warm-up job — the DiT's fixed shapes — and is then switched off and the table written: later
+    requests use the tuned solutions, and a new prompt length (the umT5 GEMMs' M) falls back to the
+    default heuristic instead of stalling the request on a tuning sweep."""
+    try:
+        tun = torch.cuda.tunable
+        if tun.is_enabled() and tun.tuning_is_enabled():
+            tun.tuning_enable(False)
+            tun.write_file()
+            log.info("TunableOp: tuning frozen after warm-up, results written")
+    except (AttributeError, RuntimeError) as e:  # torch without TunableOp / no GPU
+        log.debug("TunableOp not frozen: %s", e)
+
+
 def create_app(store: ModelStore, out_dir: str, shift: float = 8.0, ffmpeg: Optional[str] = None,
                warmup: Optional[Tuple[int, int, int]] = None):
     from fastapi import FastAPI, HTTPException
@@ -650,6 +665,7 @@ def create_app(store: ModelStore, out_dir: str, shift: float = 8.0, ffmpeg: Opti
                     time.sleep(0.5)
                 st = pq.history(job.prompt_id)[job.prompt_id]["status"]["status_str"]
                 log.info("warm-up finished: %s", st)
+                _freeze_tunableop()
                 ready.set()
 
             threading.Thread(target=watch, daemon=True, name="wan-warmup").start()
