@@ -523,14 +523,16 @@ __global__ __launch_bounds__(256) void attn_fwd_t_kernel(const AttnArgs a) {
   }
 }
 
-int g_variant = 0;   // amdk8s_attention_set_variant(): 0 = transposed (P in registers), 1 = P via LDS
+// amdk8s_attention_set_variant(): -1 = auto (d = 128 → attn_d128.hip's 32x32x16 kernel, every other
+// head dim → the transposed kernel), 0 = transposed (P in registers), 1 = P via LDS, 2 = attn_d128
+int g_variant = -1;
 
 template <bool BF16, int QK, int DT, int QT, int D>
 int launch(const AttnArgs& a, int NH, hipStream_t stream) {
   constexpr int KS = QK * 32 + kPad, VS = DT * 16 + kPad, PS = QT * 16 + 4;
   const int rows = kWaves * QT * 16;
   dim3 grid((a.Lq + rows - 1) / rows, NH);
-  if (g_variant == 0) {
+  if (g_variant <= 0 || g_variant == 2) {
     const size_t lds = (size_t)(kKeys * KS + kKeys * VS) * 2;
     hipLaunchKernelGGL((attn_fwd_t_kernel<BF16, QK, DT, QT, D>), grid, dim3(256), lds, stream, a);
   } else {
@@ -553,7 +555,7 @@ int launch_qt(const AttnArgs& a, int NH, hipStream_t stream) {
   const long wg4 = (long)((a.Lq + 255) / 256) * NH;
   int qt = wg2 >= 256 ? 2 : 1;
   if constexpr (DT == 8) {
-    if (g_variant == 0 && wg4 >= 224) qt = 4;
+    if (g_variant <= 0 && wg4 >= 224) qt = 4;
   }
   if (g_qt_override == 1 || g_qt_override == 2) qt = g_qt_override;
   if constexpr (DT == 8) {
@@ -578,6 +580,11 @@ int dispatch(const AttnArgs& a, int NH, hipStream_t stream) {
 
 }  // namespace
 
+extern "C" int amdk8s_attention_d128_fwd(const void* q, const void* k, const void* v, void* o, int N,
+                                         int H, int Lq, int Lk, int sqb, int sqr, int skb, int skr,
+                                         int svb, int svr, int sor, float scale, int dtype,
+                                         hipStream_t stream);
+
 extern "C" {
 
 void amdk8s_attention_set_qt(int qt) { g_qt_override = qt; }
@@ -595,6 +602,9 @@ int amdk8s_attention_fwd(const void* q, const void* k, const void* v, void* o, i
   if (!amdk8s_attention_supported(d, Lq, Lk) || N <= 0 || H <= 0) return -1;
   // 16-byte loads of 8 consecutive elements: every row start must stay 16-byte aligned
   if ((sqr | skr | svr | sqb | skb | svb | sor) % 8 != 0) return -3;
+  if (d == 128 && (g_variant == -1 || g_variant == 2))
+    return amdk8s_attention_d128_fwd(q, k, v, o, N, H, Lq, Lk, sqb, sqr, skb, skr, svb, svr, sor,
+                                     scale, dtype, stream);
   if ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v)) % 16 != 0)
     return -3;

@@ -171,11 +171,21 @@ def attention_set_qt(qt: int) -> None:
 
 
 def attention_set_variant(v: int) -> None:
-    """0 = transposed-score kernel (P stays in registers, default), 1 = P staged through LDS."""
+    """-1 = auto (default: head dim 128 → the 32x32x16 kernel of ``csrc/attn_d128.hip``, every other
+    head dim → the transposed-score kernel), 0 = transposed-score kernel (P stays in registers),
+    1 = P staged through LDS, 2 = ``attn_d128`` (d = 128 only)."""
     lib = _lib()
     lib.amdk8s_attention_set_variant.argtypes = [ctypes.c_int]
     lib.amdk8s_attention_set_variant.restype = None
     lib.amdk8s_attention_set_variant(int(v))
+
+
+def attention_d128_set_nw(nw: int) -> None:
+    """Waves per workgroup of the d = 128 kernel (0 = heuristic, 4 or 8) — for tuning sweeps."""
+    lib = _lib()
+    lib.amdk8s_attention_d128_set_nw.argtypes = [ctypes.c_int]
+    lib.amdk8s_attention_d128_set_nw.restype = None
+    lib.amdk8s_attention_d128_set_nw(int(nw))
 
 
 def attention_supported(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int) -> bool:

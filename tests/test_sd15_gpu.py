@@ -150,6 +150,9 @@ def _attn_ref(q, k, v, heads, scale):
     (2, 8, 1024, 77, 80, False),
     (1, 3, 100, 33, 64, False),       # ragged query and key counts
     (1, 2, 130, 200, 128, True),
+    (2, 12, 2560, 2560, 128, True),   # Wan2.1 self-attention (attn_d128.hip)
+    (2, 12, 2560, 512, 128, False),   # Wan2.1 cross-attention over the 512-token text context
+    (1, 3, 1000, 777, 128, False),    # ragged d = 128
 ])
 def test_attention_vs_fp32(SK, dev, dtype, n, heads, lq, lk, d, fused):
     g = torch.Generator(device=dev).manual_seed(lq + lk + d)
@@ -236,3 +239,38 @@ def test_attention_deferred_rescale_branch(SK, dev, growing):
     q, k, v = q.half(), k.half(), v.half()
     o = SK.attention(q, k, v, 8, 40 ** -0.5)
     torch.testing.assert_close(o.float(), _attn_ref(q, k, v, 8, 40 ** -0.5), rtol=6e-3, atol=6e-3)
+
+
+@pytest.mark.parametrize("variant,nw", [(0, 0), (2, 4), (2, 8)])
+@pytest.mark.parametrize("lq,lk", [(333, 1000), (2560, 2560)])
+def test_attention_d128_kernels_agree(SK, dev, variant, nw, lq, lk):
+    """The d = 128 kernels (legacy 16x16x32 transposed kernel, attn_d128 at 4 and 8 waves) against
+    fp32, on fused q|k|v column views with ragged lengths."""
+    g = torch.Generator(device=dev).manual_seed(lq * 7 + lk)
+    heads, d = 4, 128
+    c = heads * d
+    q = torch.randn(2, lq, c, generator=g, device=dev).bfloat16() * 2
+    kv = torch.randn(2, lk, 3 * c, generator=g, device=dev).bfloat16()
+    k, v = kv[..., c:2 * c], kv[..., 2 * c:]
+    SK.attention_set_variant(variant)
+    SK.attention_d128_set_nw(nw)
+    try:
+        o = SK.attention(q, k, v, heads, d ** -0.5)
+    finally:
+        SK.attention_set_variant(-1)
+        SK.attention_d128_set_nw(0)
+    torch.testing.assert_close(o.float(), _attn_ref(q, k, v, heads, d ** -0.5), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("growing", [True, False])
+def test_attention_d128_deferred_rescale_branch(SK, dev, growing):
+    g = torch.Generator(device=dev).manual_seed(23)
+    lk = 1024
+    q = torch.randn(1, 512, 256, generator=g, device=dev)
+    k = torch.randn(1, lk, 256, generator=g, device=dev)
+    ramp = torch.linspace(0.2, 6.0, lk, device=dev)
+    k = k * (ramp if growing else ramp.flip(0))[None, :, None]
+    v = torch.randn(1, lk, 256, generator=g, device=dev)
+    q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
+    o = SK.attention(q, k, v, 2, 128 ** -0.5)
+    torch.testing.assert_close(o.float(), _attn_ref(q, k, v, 2, 128 ** -0.5), rtol=2e-2, atol=2e-2)
