@@ -124,8 +124,10 @@ def main(argv=None) -> int:
 
     if c == "device-plugin":
         from .device_plugin import AmdGpuDevicePlugin
+        from .validator import DEVICE_ID_MAP
 
-        AmdGpuDevicePlugin(cfg, root=args.root, kubelet_dir=args.kubelet_dir).run()
+        AmdGpuDevicePlugin(cfg, root=args.root, kubelet_dir=args.kubelet_dir,
+                           id_map_path=DEVICE_ID_MAP).run()
         return 0
 
     if c == "labeller":

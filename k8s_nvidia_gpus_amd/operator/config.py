@@ -62,6 +62,15 @@ DEFAULTS: Dict[str, Any] = {
         "rccl": True,
         "rcclMinBusbwGBps": 100,
         "pluginTest": True,
+        # GPUs kubelet has allocated to pods are never loaded: gemm / bandwidth / stress / rccl run
+        # on the free ones only (kubelet PodResources API), and are deferred when none is free
+        "podResourcesSocket": "/var/lib/kubelet/pod-resources/kubelet.sock",
+        # a validator restart with the node's fingerprint (boot id, amdgpu version, operator image)
+        # unchanged since the last full pass re-uses that pass instead of re-running the load steps
+        "skipUnchangedNode": True,
+        # compute-partitioned GPUs (DPX/QPX/CPX): per-partition GEMM size; the TFLOPS / HBM floors
+        # are scaled by the partition's share of the ASIC (CUs / memory)
+        "gemmSizePartitioned": 4096,
     },
 }
 

@@ -29,6 +29,7 @@ Design (MI355X-first):
 """
 from __future__ import annotations
 
+import json
 import logging
 import os
 import threading
@@ -187,8 +188,12 @@ class AmdGpuDevicePlugin:
                  kubelet_dir: str = api.DEVICE_PLUGIN_PATH, socket_name: str = "amd-gpu.sock",
                  topology_fn: Optional[Callable[[], topo_mod.NodeTopology]] = None,
                  health_fn: Optional[HealthFn] = None, pause_marker: Optional[str] = PAUSE_MARKER,
-                 dev_prefix: str = "/dev", ecc_fn: Optional[Callable] = None):
+                 dev_prefix: str = "/dev", ecc_fn: Optional[Callable] = None,
+                 id_map_path: Optional[str] = None):
         self.config = config
+        # {kubelet device ID: device_uid} for the validator, which maps kubelet's PodResources
+        # answer to GPUs with it (needed with deviceIdStrategy: index)
+        self.id_map_path = id_map_path
         self.root = root
         self.kubelet_dir = kubelet_dir
         self.socket_path = os.path.join(kubelet_dir, socket_name)
@@ -257,9 +262,24 @@ class AmdGpuDevicePlugin:
                 self._version += 1
                 self._cond.notify_all()
         if changed:
+            self._write_id_map()
             log.info("advertising %d device(s) (%d healthy)%s", len(merged),
                      sum(1 for v in health.values() if v == api.HEALTHY), " [paused]" if paused else "")
         return changed
+
+    def _write_id_map(self) -> None:
+        if not self.id_map_path:
+            return
+        with self._cond:
+            m = {self._id(d): d.device_uid for d in self._devices}
+        try:
+            os.makedirs(os.path.dirname(self.id_map_path), exist_ok=True)
+            tmp = self.id_map_path + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump(m, f)
+            os.replace(tmp, self.id_map_path)
+        except OSError as e:
+            log.warning("cannot write %s: %s", self.id_map_path, e)
 
     def list_response(self):
         resp = api.ListAndWatchResponse()

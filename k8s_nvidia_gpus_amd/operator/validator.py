@@ -20,6 +20,16 @@ the previous one's marker under ``/run/amd/validations``:
   plugin    a pod requesting amd.com/gpu: 1 is scheduled THROUGH the device plugin and passes
   report    node label amd.com/gpu.validated=true|false, validator-ready marker
 
+The load steps (gemm, bandwidth, stress, rccl) never touch a GPU that kubelet has allocated to a
+pod: the kubelet PodResources API (``podresources_api.py``) lists the device IDs pods hold, and the
+native tools run with ``ROCR_VISIBLE_DEVICES`` narrowed to the free agents — or the step is
+recorded as *deferred* (passed, with the reason) when none is free.  A validator restart whose
+node fingerprint (boot id, amdgpu version, operator image, validator config) equals the one of
+the last full pass re-uses that pass instead of loading the GPUs again.  On compute-partitioned
+GPUs (DPX/QPX/CPX) the TFLOPS and HBM floors scale with the partition's share of the ASIC, the
+GEMM runs at ``gemmSizePartitioned``, xGMI pair copies are skipped and RCCL runs over one agent
+per ASIC.
+
 Each step writes ``<step>.json`` (the metrics exporter publishes TFLOPS / busbw / pass flags from
 them) and ``<step>-ready`` on success.  Command execution is injectable so the parsing and gating
 logic is tested on CPU against the real outputs the native tools produced on an MI355X
@@ -36,12 +46,17 @@ import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
+from . import podresources_api
 from .config import OperatorConfig
 
 log = logging.getLogger("amd-gpu-validator")
 
 STEPS = ("driver", "runtime", "vectoradd", "gemm", "bandwidth", "stress", "rccl", "plugin", "report")
+LOAD_STEPS = ("gemm", "bandwidth", "stress", "rccl")
 LABEL_VALIDATED = "amd.com/gpu.validated"
+FINGERPRINT = "fingerprint.json"
+# kubelet device ID -> device_uid, written by the device plugin (needed for deviceIdStrategy: index)
+DEVICE_ID_MAP = "/run/amd/device-plugin/ids.json"
 
 Runner = Callable[[Sequence[str], float], Tuple[int, str]]
 
@@ -155,6 +170,40 @@ def rocprof_counter_summary(prof_dir: str, cus: int, kernel_filter: str = "gemm"
 
 
 @dataclass
+class GpuScope:
+    """Which GPU agents the load steps may use.  ``devices`` are in ROCr enumeration order (KFD
+    node id), so a position in it is a ``ROCR_VISIBLE_DEVICES`` index."""
+    devices: List = field(default_factory=list)
+    free: List[int] = field(default_factory=list)
+    allocated: Dict[str, str] = field(default_factory=dict)   # device_uid -> namespace/pod
+    note: str = ""
+    split: int = 1                                            # partitions per ASIC (CPX: 8)
+
+    @property
+    def full(self) -> bool:
+        return len(self.free) == len(self.devices)
+
+    @property
+    def known(self) -> bool:
+        """False when the KFD topology is unreadable here (the tools then run unrestricted and
+        fail on their own if there really is no GPU)."""
+        return bool(self.devices)
+
+    def env_prefix(self, indices: Optional[Sequence[int]] = None) -> List[str]:
+        if not self.known:
+            return []
+        idx = list(self.free if indices is None else indices)
+        if indices is None and self.full:
+            return []
+        return ["env", "ROCR_VISIBLE_DEVICES=" + ",".join(str(i) for i in idx)]
+
+    def to_dict(self) -> Dict:
+        return {"full": self.full, "agents": len(self.devices), "split": self.split,
+                "validated": [self.devices[i].device_uid for i in self.free] if self.devices else [],
+                "allocated": dict(self.allocated), "note": self.note}
+
+
+@dataclass
 class StepResult:
     step: str
     passed: bool
@@ -171,8 +220,11 @@ class Validator:
     def __init__(self, config: OperatorConfig, marker_dir: str = "/run/amd/validations",
                  bin_dir: Optional[str] = None, runner: Runner = default_runner, root: str = "/",
                  kube=None, node_name: Optional[str] = None, driver_wait: float = 120,
-                 telemetry: Optional[Callable[[], List[Dict]]] = None):
+                 telemetry: Optional[Callable[[], List[Dict]]] = None,
+                 device_id_map: str = DEVICE_ID_MAP):
         self.cfg = config
+        self.device_id_map = device_id_map
+        self._scope: Optional[GpuScope] = None
         self.telemetry = telemetry  # per-GPU samples for the stress step (default: amd-smi)
         self.driver_wait = driver_wait  # kfd-probe --wait: how long the driver may take to appear
         self.vcfg = config.section("validator")
@@ -214,6 +266,107 @@ class Validator:
     def _bin(self, name: str) -> str:
         return os.path.join(self.bin_dir, name)
 
+    # ---------------------------------------------------------------- GPU scope / fingerprint
+    def _kubelet_id_map(self, devs) -> Dict[str, str]:
+        if self.cfg["deviceIdStrategy"] != "index":
+            return {g.device_uid: g.device_uid for g in devs}
+        try:
+            with open(self.device_id_map) as f:
+                return {str(k): str(v) for k, v in json.load(f).items()}
+        except (OSError, ValueError):
+            return {}
+
+    def gpu_scope(self) -> GpuScope:
+        """The free GPU agents: every agent minus what kubelet's PodResources API says pods hold.
+        Fails closed — an unreadable kubelet answer or an ID that cannot be mapped to a GPU leaves
+        no GPU free (the load steps are then deferred, never run on a tenant's GPU)."""
+        from ..utils import topology as topo_mod
+
+        try:
+            topo = topo_mod.read_topology(self.root, self.cfg.min_gfx)
+            devs = sorted(topo.gpus, key=lambda g: g.node_id)
+        except FileNotFoundError:
+            devs = []
+        split = max((g.partitions_on_asic for g in devs), default=1)
+        try:
+            alloc = podresources_api.allocated(self.cfg.resource_name,
+                                               str(self.vcfg["podResourcesSocket"]))
+        except Exception as e:  # noqa: BLE001 - kubelet unreachable: cannot prove a GPU is free
+            return GpuScope(devs, [], {}, f"PodResources List failed: {e}"[:300], split)
+        if alloc is None:
+            return GpuScope(devs, list(range(len(devs))), {},
+                            "no kubelet PodResources socket: all agents", split)
+        idmap = self._kubelet_id_map(devs)
+        busy: Dict[str, str] = {}
+        unknown = []
+        for kid, pod in sorted(alloc.items()):
+            uid = idmap.get(kid)
+            if uid is None:
+                unknown.append(kid)
+            else:
+                busy[uid] = pod
+        if unknown:
+            return GpuScope(devs, [], busy, "cannot map allocated device id(s) " + ",".join(unknown), split)
+        free = [i for i, g in enumerate(devs) if g.device_uid not in busy]
+        return GpuScope(devs, free, busy, "", split)
+
+    def scope(self) -> GpuScope:
+        if self._scope is None:
+            self._scope = self.gpu_scope()
+        return self._scope
+
+    def _cmd(self, argv: List[str], indices: Optional[Sequence[int]] = None) -> List[str]:
+        """argv narrowed to the free agents (or to ``indices``) with ROCR_VISIBLE_DEVICES."""
+        if self._scope is None:
+            return list(argv)
+        return self._scope.env_prefix(indices) + list(argv)
+
+    def fingerprint(self) -> Dict[str, str]:
+        from .labeller import driver_version
+
+        fp: Dict[str, str] = {}
+        try:
+            with open(os.path.join(self.root, "proc/sys/kernel/random/boot_id")) as f:
+                fp["boot_id"] = f.read().strip()
+        except OSError:
+            fp["boot_id"] = ""
+        fp["amdgpu"] = driver_version(self.root) or ""
+        fp["image"] = os.environ.get("VALIDATOR_IMAGE_ID") or self._own_image_id()
+        fp["config"] = json.dumps(self.vcfg, sort_keys=True, default=str)
+        return fp
+
+    def _own_image_id(self) -> str:
+        pod_name = os.environ.get("POD_NAME")
+        if not pod_name or self.kube is None:
+            return ""
+        try:
+            pod = self.kube.get_pod(os.environ.get("POD_NAMESPACE", "amd-gpu-operator"), pod_name)
+        except Exception as e:  # noqa: BLE001
+            log.warning("cannot read own pod: %s", e)
+            return ""
+        st = pod.get("status", {})
+        for c in st.get("initContainerStatuses", []) + st.get("containerStatuses", []):
+            if c.get("imageID"):
+                return c["imageID"]
+        return ""
+
+    def _unchanged_pass(self, step: str) -> Optional[Dict]:
+        """The previous result of ``step`` when the node has not changed since a FULL pass."""
+        if not self.vcfg.get("skipUnchangedNode") or not self.ready(step):
+            return None
+        try:
+            with open(self._path(FINGERPRINT)) as f:
+                saved = json.load(f)
+            with open(self._path(f"{step}.json")) as f:
+                prev = json.load(f)
+        except (OSError, ValueError):
+            return None
+        if not saved.get("full") or saved.get("fingerprint") != self.fingerprint() or not prev.get("passed"):
+            return None
+        keep = {k: prev[k] for k in ("aggregate_tflops", "min_by_test_gbps", "peak_busbw_gbps", "time",
+                                     "deferred") if k in prev}
+        return {"since": saved.get("time"), **keep}
+
     # ---------------------------------------------------------------- steps
     def step_driver(self) -> StepResult:
         n = int(self.cfg["expectedGpusPerNode"])
@@ -251,7 +404,7 @@ class Validator:
             prof_dir = self._path("gemm-rocprof" if dtype == "bf16" else f"gemm-{dtype}-rocprof")
             argv = ["rocprofv3", "--kernel-trace", "--stats", "-d", prof_dir, "-o", "gemm",
                     "--output-format", "csv", "--"] + argv
-        rc, out = self.run_cmd(argv, 900)
+        rc, out = self.run_cmd(self._cmd(argv), 900)
         devs = [d for d in json_lines(out) if d.get("check") == f"gemm_{dtype}"]
         slow = [d for d in devs if float(d.get("tflops", 0)) < floor]
         bad = [d for d in devs if not d.get("passed")]
@@ -274,7 +427,7 @@ class Validator:
         argv = ["rocprofv3", "--kernel-trace", "--pmc", *GEMM_COUNTERS, "-d", prof_dir, "-o", "pmc",
                 "--output-format", "csv", "--", self._bin("amd-gemm-validator"), "--size", str(size),
                 "--iters", "10", "--settle-ms", "50", "--json"]
-        rc, out = self.run_cmd(argv, 300)
+        rc, out = self.run_cmd(self._cmd(argv), 300)
         summary = rocprof_counter_summary(prof_dir, cus) if rc == 0 else {}
         if rc != 0:
             summary["error"] = f"rocprofv3 --pmc rc={rc}: {out.strip()[-200:]}"
@@ -284,24 +437,38 @@ class Validator:
         return summary
 
     def step_gemm(self) -> StepResult:
-        size = int(self.vcfg["gemmSize"])
+        split = self._scope.split if self._scope else 1
+        # a compute partition owns 1/split of the ASIC's CUs: per-partition floor and a GEMM sized
+        # for 32 CUs (CPX) rather than the whole chip
+        size = int(self.vcfg["gemmSize"] if split == 1 else self.vcfg["gemmSizePartitioned"])
         rocprof = bool(self.vcfg.get("rocprof"))
-        ok, detail, reason = self._gemm_run("bf16", size, float(self.vcfg["gemmMinTflops"]), rocprof)
+        ok, detail, reason = self._gemm_run("bf16", size, float(self.vcfg["gemmMinTflops"]) / split,
+                                            rocprof)
+        detail["partition_split"] = split
         if self.vcfg.get("rocprofCounters") and ok:
             cus = min((int(d.get("cus", 256)) for d in detail["devices"]), default=256)
             detail["rocprof_counters"] = self._gemm_counters(size, cus)
         if self.vcfg.get("gemmFp8"):
-            ok8, detail8, reason8 = self._gemm_run("fp8", size, float(self.vcfg["gemmFp8MinTflops"]),
-                                                   rocprof)
+            ok8, detail8, reason8 = self._gemm_run("fp8", size,
+                                                   float(self.vcfg["gemmFp8MinTflops"]) / split, rocprof)
             detail["fp8"] = detail8
             ok = ok and ok8
             reason = "; ".join(r for r in (reason, reason8) if r)
         return StepResult("gemm", bool(ok), detail, reason)
 
     def step_bandwidth(self) -> StepResult:
-        floors = {"hbm-copy": float(self.vcfg["hbmMinGBps"]), "pcie-h2d": float(self.vcfg["pcieMinGBps"]),
+        split = self._scope.split if self._scope else 1
+        floors = {"hbm-copy": float(self.vcfg["hbmMinGBps"]) / split,
+                  "pcie-h2d": float(self.vcfg["pcieMinGBps"]),
                   "pcie-d2h": float(self.vcfg["pcieMinGBps"]), "xgmi": float(self.vcfg["xgmiMinGBps"])}
-        rc, out = self.run_cmd([self._bin("amd-proftester"), "-t", ",".join(floors), "--json"], 900)
+        extra: Dict[str, str] = {}
+        if split > 1:
+            # partitions of one ASIC share its HBM and talk over the on-package fabric, not xGMI; the
+            # ASIC-to-ASIC links are exercised by the RCCL step (one agent per ASIC)
+            del floors["xgmi"]
+            extra["xgmi_skipped"] = f"compute-partitioned ({split} agents per ASIC)"
+        rc, out = self.run_cmd(self._cmd([self._bin("amd-proftester"), "-t", ",".join(floors), "--json"]),
+                               900)
         docs = [d for d in json_lines(out) if d.get("check") == "proftester" and d.get("test") in floors]
         # pairs: SDMA copies are gated; the copy-kernel pulls and the all-peer aggregate are reported
         gated = [d for d in docs if not d.get("skipped")
@@ -327,7 +494,7 @@ class Validator:
                 f"no result for {','.join(missing)}" if missing else "",
                 f"rc={rc}" if rc else ""]))
         return StepResult("bandwidth", bool(ok), {"results": docs, "min_by_test_gbps": summary,
-                                                  "floors_gbps": floors}, reason)
+                                                  "floors_gbps": floors, **extra}, reason)
 
     def _telemetry_fn(self) -> Optional[Callable[[], List[Dict]]]:
         if self.telemetry is not None:
@@ -362,8 +529,8 @@ class Validator:
         if th:
             th.start()
         try:
-            rc, out = self.run_cmd([self._bin("amd-proftester"), "-t", "tensor", "--duration",
-                                    str(secs), "--json"], secs + 300)
+            rc, out = self.run_cmd(self._cmd([self._bin("amd-proftester"), "-t", "tensor", "--duration",
+                                              str(secs), "--json"]), secs + 300)
         finally:
             stop.set()
             if th:
@@ -419,8 +586,17 @@ class Validator:
         if ngpus is not None and ngpus < 2:
             return StepResult("rccl", True, {"ngpus": ngpus, "skipped": "single GPU"})
         floor = float(self.vcfg["rcclMinBusbwGBps"])
-        rc, out = self.run_cmd([self._bin("rccl-allreduce-bench"), "-b", "1M", "-e", "1G", "-f", "4",
-                                "-n", "20", "--json"], 900)
+        indices = None
+        sc = self._scope
+        if sc is not None and sc.devices and (sc.split > 1 or not sc.full):
+            # one agent per ASIC (partition 0): RCCL measures the xGMI links between ASICs, not 64
+            # partitions contending for eight sets of links
+            indices = [i for i in sc.free if sc.devices[i].partition_index == 0] if sc.split > 1 else sc.free
+            if len(indices) < 2:
+                return StepResult("rccl", True, {"ngpus": len(indices),
+                                                 "skipped": "fewer than 2 free ASICs"})
+        rc, out = self.run_cmd(self._cmd([self._bin("rccl-allreduce-bench"), "-b", "1M", "-e", "1G",
+                                          "-f", "4", "-n", "20", "--json"], indices), 900)
         docs = [d for d in json_lines(out) if d.get("check") == "rccl_allreduce"]
         d = docs[-1] if docs else {}
         n = d.get("ngpus", ngpus)
@@ -517,6 +693,26 @@ class Validator:
                                       "chain_seconds": round(sum(durations.values()), 3),
                                       "chain_complete": not no_duration},
                        "" if ok else "failed/missing: " + ",".join(missing))
+        full = True
+        for st in LOAD_STEPS:
+            if st not in required:
+                continue
+            try:
+                with open(self._path(f"{st}.json")) as f:
+                    d = json.load(f)
+            except (OSError, ValueError):
+                full = False
+                continue
+            if d.get("deferred") and "previous" not in d:
+                full = False     # deferred for allocation: not a full validation
+            elif not d.get("deferred") and not d.get("skipped") and not (d.get("gpu_scope") or {}).get("full", True):
+                full = False     # ran on a subset of the GPUs
+        r.detail["full_validation"] = full
+        if ok and full:
+            tmp = self._path(f".{FINGERPRINT}.tmp")
+            with open(tmp, "w") as f:
+                json.dump({"full": True, "time": time.time(), "fingerprint": self.fingerprint()}, f)
+            os.replace(tmp, self._path(FINGERPRINT))
         if ok:
             with open(self._path("validator-ready"), "w") as f:
                 f.write(f"{time.time()}\n")
@@ -545,6 +741,26 @@ class Validator:
         return r
 
     def _run_step(self, step: str) -> StepResult:
+        if step in LOAD_STEPS and self._enabled(step):
+            prev = self._unchanged_pass(step)
+            if prev is not None:
+                return StepResult(step, True, {"deferred": "node fingerprint unchanged since the last "
+                                                           "full validation", "previous": prev})
+            sc = self.scope()
+            if sc.known and not sc.free:
+                return StepResult(step, True, {
+                    "deferred": sc.note or f"all {len(sc.devices)} GPU agent(s) allocated to pods",
+                    "gpu_scope": sc.to_dict()})
+            r = self._run_load_step(step)
+            r.detail["gpu_scope"] = sc.to_dict()
+            return r
+        return self._run_load_step(step)
+
+    def _enabled(self, step: str) -> bool:
+        return bool(self.vcfg[{"gemm": "gemm", "bandwidth": "bandwidth", "stress": "stress",
+                               "rccl": "rccl"}[step]])
+
+    def _run_load_step(self, step: str) -> StepResult:
         if step == "driver":
             r = self.step_driver()
         elif step == "runtime":

@@ -1,4 +1,5 @@
 """amd.com/gpu device plugin against a fake MI355X sysfs tree and a fake kubelet (CPU-only)."""
+import json
 import os
 import tempfile
 import threading
@@ -268,3 +269,18 @@ def test_grpc_register_listandwatch_allocate_and_kubelet_restart(node, sockdir):
         stop.set()
         t.join(10)
         kubelet.stop()
+
+
+def test_index_id_map_file_for_the_validator(tmp_path, sockdir):
+    """The plugin publishes {kubelet ID: device_uid}; the validator maps PodResources answers with it."""
+    from k8s_nvidia_gpus_amd.operator.config import load_config
+    from k8s_nvidia_gpus_amd.operator.device_plugin import AmdGpuDevicePlugin
+
+    root = fake_sysfs.build_node(tmp_path / "r")
+    path = tmp_path / "run/device-plugin/ids.json"
+    cfg = load_config(text="deviceIdStrategy: index\n")
+    p = AmdGpuDevicePlugin(cfg, root=str(root), kubelet_dir=str(sockdir), pause_marker=None,
+                           health_fn=lambda devs: {d.device_uid: api.HEALTHY for d in devs},
+                           id_map_path=str(path))
+    m = json.loads(path.read_text())
+    assert m == {i: d.device_uid for i, d in p._id_map().items()} and set(m) == {str(i) for i in range(8)}

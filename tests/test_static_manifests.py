@@ -436,3 +436,43 @@ def test_default_runtime_goes_through_rke2_config_not_a_table():
     assert drop and "default-runtime:" in drop[0]["ansible.builtin.copy"]["content"]
     tmpl = (ANS / "roles/amd-host-prep/templates/config-v3.toml.tmpl.j2").read_text()
     assert "default_runtime_name" not in tmpl.split("---", 1)[1].split("\n[", 1)[1]
+
+
+# ---------------------------------------------------------------- bootstrap --registry / --git-url
+def test_retarget_leaves_no_placeholders(tmp_path):
+    """hack/retarget.py (what hack/bootstrap.sh --registry/--git-url runs) rewrites every image,
+    the Flux Git URL, Renovate's autodiscover filter and the validator's fallback image."""
+    import shutil
+    import subprocess
+    import sys
+
+    for d in ("cluster-config", "images", "hack"):
+        shutil.copytree(REPO / d, tmp_path / d)
+    (tmp_path / "k8s_nvidia_gpus_amd/operator").mkdir(parents=True)
+    shutil.copy(REPO / "k8s_nvidia_gpus_amd/operator/validator.py", tmp_path / "k8s_nvidia_gpus_amd/operator/")
+    (tmp_path / "tools").mkdir()
+    shutil.copy(REPO / "tools/time_to_first_gpu_pod.py", tmp_path / "tools/")
+    tool = [sys.executable, str(tmp_path / "hack/retarget.py"), "--root", str(tmp_path)]
+    assert subprocess.run(tool + ["--check"]).returncode == 1      # placeholders before
+    subprocess.run(tool + ["--registry", "ghcr.io/acme", "--git-url",
+                           "https://github.com/acme/k8s-amd.git"], check=True)
+    assert subprocess.run(tool + ["--check"]).returncode == 0
+    ks = yaml.safe_load((tmp_path / "cluster-config/apps/amd-gpu-operator/kustomization.yaml").read_text())
+    assert ks["images"][0]["newName"] == "ghcr.io/acme/amd-gpu-operator"
+    sync = load_all(tmp_path / "cluster-config/cluster/flux-system/gotk-sync.yaml")
+    assert sync[0]["spec"]["url"] == "https://github.com/acme/k8s-amd.git"
+    cron = (tmp_path / "cluster-config/apps/renovate/cronjob.yaml").read_text()
+    assert '"acme/k8s-amd"' in cron
+    assert "ghcr.io/acme/amd-gpu-operator" in (tmp_path / "k8s_nvidia_gpus_amd/operator/validator.py").read_text()
+    for kf in (tmp_path / "cluster-config/apps").glob("*/kustomization.yaml"):
+        for img in yaml.safe_load(kf.read_text()).get("images", []):
+            assert img["newName"].startswith("ghcr.io/acme/"), (kf, img)
+    # re-runnable: a second registry replaces the first
+    subprocess.run(tool + ["--registry", "registry.example.net/gpu"], check=True)
+    ks = yaml.safe_load((tmp_path / "cluster-config/apps/amd-gpu-operator/kustomization.yaml").read_text())
+    assert ks["images"][0]["newName"] == "registry.example.net/gpu/amd-gpu-operator"
+
+
+def test_bootstrap_refuses_placeholder_images():
+    text = (REPO / "hack/bootstrap.sh").read_text()
+    assert "--registry" in text and "retarget.py --check" in text

@@ -44,6 +44,10 @@ class Runner:
 
     def __call__(self, argv, timeout):
         self.calls.append(list(argv))
+        if argv and argv[0] == "env":   # ROCR_VISIBLE_DEVICES=... narrowing (GPU scope)
+            argv = argv[1:]
+            while argv and "=" in argv[0]:
+                argv = argv[1:]
         name = os.path.basename(argv[0])
         if "--dtype" in argv:  # e.g. "amd-gemm-validator:fp8"
             name += ":" + argv[argv.index("--dtype") + 1]
