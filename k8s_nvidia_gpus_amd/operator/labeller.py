@@ -12,6 +12,11 @@ sysfs topology, so workloads select on product, architecture, partition mode or 
     amd.com/gpu.driver-version=...     amd.com/gpu.numa-nodes=2
 
 ``amd.com/gpu.present`` is what schedules the rest of the operator's DaemonSets onto the node.
+``amd.com/gpu.pci-present=true`` comes from the PCI bus alone (vendor 0x1002, class 0x12xxxx
+processing accelerator or 0x03xxxx display), so it is set before amdgpu is loaded: it schedules the
+driver DaemonSet, which therefore never lands on a CPU-only worker (whose never-ready pod would
+block the operator Kustomization's ``wait: true``).  The partition labels read every ASIC and
+say ``mixed`` when they disagree (a partition change that stopped half-way), never the head GPU's.
 Labels this component owns are removed again when the GPUs go away; labels owned by other
 components (``amd.com/gpu.validated``, ``amd.com/gpu.compute-partition.desired``) are left alone.
 """
@@ -27,7 +32,7 @@ from ..utils import topology as topo_mod
 log = logging.getLogger("amd-node-labeller")
 
 PREFIX = "amd.com/gpu"
-OWNED = ("present", "count", "asic-count", "product", "family", "device-id", "cu-count", "vram",
+OWNED = ("present", "pci-present", "count", "asic-count", "product", "family", "device-id", "cu-count", "vram",
          "compute-partition", "memory-partition", "xgmi-links", "driver-version", "numa-nodes")
 _LABEL_VALUE = re.compile(r"^(([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9])?$")
 
@@ -50,9 +55,35 @@ def driver_version(root: str = "/") -> Optional[str]:
     return None
 
 
+AMD_VENDOR = "0x1002"
+
+
+def amd_accelerators_on_pci(root: str = "/") -> int:
+    """AMD GPUs / accelerators on the PCI bus (needs no driver)."""
+    base = os.path.join(root, "sys/bus/pci/devices")
+    try:
+        names = os.listdir(base)
+    except OSError:
+        return 0
+    n = 0
+    for name in names:
+        try:
+            with open(os.path.join(base, name, "vendor")) as f:
+                vendor = f.read().strip().lower()
+            with open(os.path.join(base, name, "class")) as f:
+                cls = int(f.read().strip(), 16)
+        except (OSError, ValueError):
+            continue
+        if vendor == AMD_VENDOR and (cls >> 16) in (0x12, 0x03):
+            n += 1
+    return n
+
+
 def compute_labels(root: str = "/", min_gfx: int = topo_mod.GFX950) -> Dict[str, Optional[str]]:
     """Desired values for every owned label (None = remove)."""
     labels: Dict[str, Optional[str]] = {f"{PREFIX}.{k}": None for k in OWNED}
+    if amd_accelerators_on_pci(root):
+        labels[f"{PREFIX}.pci-present"] = "true"
     try:
         topo = topo_mod.read_topology(root, min_gfx)
     except FileNotFoundError:
@@ -62,6 +93,9 @@ def compute_labels(root: str = "/", min_gfx: int = topo_mod.GFX950) -> Dict[str,
         return labels
     asics = topo.asics()
     head = gpus[0]
+    from .partition import asic_modes, node_mode
+
+    compute_mode, memory_mode = node_mode(asic_modes(topo))
     vram_gib = round(sum(g.vram_bytes for g in asics[head.unique_id]) / (1 << 30))
     labels.update({
         f"{PREFIX}.present": "true",
@@ -72,8 +106,8 @@ def compute_labels(root: str = "/", min_gfx: int = topo_mod.GFX950) -> Dict[str,
         f"{PREFIX}.device-id": "%04x" % head.device_id,
         f"{PREFIX}.cu-count": str(head.cu_count),
         f"{PREFIX}.vram": f"{vram_gib}G",
-        f"{PREFIX}.compute-partition": head.compute_partition,
-        f"{PREFIX}.memory-partition": head.memory_partition,
+        f"{PREFIX}.compute-partition": compute_mode,
+        f"{PREFIX}.memory-partition": memory_mode,
         f"{PREFIX}.xgmi-links": str(len({p for p in head.xgmi_peers
                                          if p not in {g.node_id for g in asics[head.unique_id]}})
                                     if head.partitions_on_asic == 1 else

@@ -13,13 +13,17 @@ KFD agents, new render minors, different device IDs.  The manager drives that sa
 The desired mode comes from the node label ``amd.com/gpu.compute-partition.desired`` (and
 ``…memory-partition.desired``), else from operator.yaml.  The state is published as the node
 annotation ``amd.com/gpu.partition-state`` so it survives agent restarts and is visible with kubectl.
+
+Convergence is per ASIC: every ASIC's current mode is read (a node whose change stopped half-way —
+``set_compute`` raising on ASIC 3 after ASICs 0-2 switched — reads as ``mixed``, never as the head
+GPU's mode), and a reconcile re-applies the desired mode only to the ASICs that are off target.
 """
 from __future__ import annotations
 
 import logging
 import os
 import time
-from typing import Callable, Optional
+from typing import Callable, Dict, List, Optional, Tuple
 
 from ..utils import kube as kube_mod
 from ..utils import topology as topo_mod
@@ -33,8 +37,24 @@ TAINT_KEY = "amd.com/gpu-partitioning"
 PAUSE_MARKER = "/run/amd/partition-in-progress"
 
 
+MIXED = "mixed"
+
+
 class PartitionError(RuntimeError):
     pass
+
+
+def asic_modes(topo: topo_mod.NodeTopology) -> Dict[int, Tuple[str, str]]:
+    """{ASIC unique id: (compute mode, memory mode)} from each ASIC's own PCI attributes."""
+    return {uid: (members[0].compute_partition, members[0].memory_partition)
+            for uid, members in topo.asics().items()}
+
+
+def node_mode(modes: Dict[int, Tuple[str, str]]) -> Tuple[str, str]:
+    """The node's (compute, memory) mode, ``mixed`` where its ASICs disagree."""
+    cs = {c for c, _ in modes.values()}
+    ms = {m for _, m in modes.values()}
+    return (cs.pop() if len(cs) == 1 else MIXED), (ms.pop() if len(ms) == 1 else MIXED)
 
 
 class SysfsPartitionBackend:
@@ -94,11 +114,12 @@ class PartitionManager:
                 labels.get(LABEL_MEM_DESIRED, self.default_memory).upper())
 
     def current(self) -> tuple:
+        """(compute, memory, topology) of the node; a mode is ``mixed`` when the ASICs disagree."""
         topo = topo_mod.read_topology(self.root, self.min_gfx)
         if not topo.gpus:
             raise PartitionError("no GPUs in the KFD topology")
-        head = topo.gpus[0]
-        return head.compute_partition, head.memory_partition, topo
+        c, m = node_mode(asic_modes(topo))
+        return c, m, topo
 
     def gpu_pods(self) -> list:
         pods = self.client.list_pods(field_selector=f"spec.nodeName={self.node}")
@@ -113,18 +134,22 @@ class PartitionManager:
             self._state("failed", f"unknown compute partition {want_c}")
             return "failed"
         cur_c, cur_m, topo = self.current()
-        if (cur_c, cur_m) == (want_c, want_m):
+        modes = asic_modes(topo)
+        asics = topo.asics()
+        # PCI order (ASIC 0 = lowest bus), so a partial failure is reported and resumed predictably
+        off = sorted((uid for uid, cm in modes.items() if cm != (want_c, want_m)),
+                     key=lambda u: asics[u][0].pci_bdf)
+        if not off:
             self._pause(False)
             self.client.set_taint(self.node, TAINT_KEY, "", present=False)
             self._state("idle")
             return "idle"
-        avail = topo_mod.available_partitions(self.root, topo.gpus[0])
+        avail = topo_mod.available_partitions(self.root, asics[off[0]][0])
         if want_c not in avail:
             self._state("failed", f"{want_c} not in available {','.join(avail)}")
             return "failed"
-        asics = topo.asics()
-        log.info("node %s: %s/%s -> %s/%s on %d ASIC(s)", self.node, cur_c, cur_m, want_c, want_m,
-                 len(asics))
+        log.info("node %s: %s/%s -> %s/%s on %d of %d ASIC(s)", self.node, cur_c, cur_m, want_c,
+                 want_m, len(off), len(asics))
         # 1. stop new GPU work landing here; hide devices from kubelet
         self.client.set_taint(self.node, TAINT_KEY, want_c, present=True)
         self._pause(True)
@@ -139,19 +164,24 @@ class PartitionManager:
                 self._abort(f"drain timeout: GPU pods still running ({names})")
                 return "failed"
             self.sleep(self.poll)
-        # 2. apply, memory partition first (the compute split must fit the memory layout)
-        self._state("applying", f"{want_c}/{want_m}")
-        try:
-            for members in asics.values():
-                head = members[0]
-                if cur_m != want_m:
+        # 2. apply to the off-target ASICs only, memory partition first (the compute split must
+        #    fit the memory layout)
+        self._state("applying", f"{want_c}/{want_m} on {len(off)} ASIC(s)")
+        done: List[str] = []
+        for uid in off:
+            head = asics[uid][0]
+            c_i, m_i = modes[uid]
+            try:
+                if m_i != want_m:
                     self.backend.set_memory(head, want_m)
-                if cur_c != want_c:
+                if c_i != want_c:
                     self.backend.set_compute(head, want_c)
-        except Exception as e:  # noqa: BLE001
-            self._abort(f"apply failed: {e}")
-            return "failed"
-        # 3. wait for the driver to re-enumerate N × split agents
+            except Exception as e:  # noqa: BLE001
+                self._abort(f"apply failed on {head.pci_bdf} after {len(done)} of {len(off)} "
+                            f"ASIC(s) switched: {e}")
+                return "failed"
+            done.append(head.pci_bdf)
+        # 3. wait for the driver to re-enumerate every ASIC in the new mode
         self._state("reenumerating")
         expect = len(asics) * topo_mod.PARTITION_SPLIT[want_c]
         deadline = time.monotonic() + self.reenum_timeout
@@ -171,7 +201,7 @@ class PartitionManager:
         self.client.set_taint(self.node, TAINT_KEY, "", present=False)
         self.client.set_node_labels(self.node, {"amd.com/gpu.compute-partition": want_c,
                                                 "amd.com/gpu.memory-partition": want_m})
-        self._state("idle", f"applied {want_c}/{want_m}")
+        self._state("idle", f"applied {want_c}/{want_m} on {len(off)} ASIC(s)")
         return "applied"
 
     def _abort(self, reason: str) -> None:

@@ -11,7 +11,7 @@ from __future__ import annotations
 import json
 import os
 from pathlib import Path
-from typing import Iterable, Optional
+from typing import Iterable, Optional, Sequence, Union
 
 FIX = Path(__file__).resolve().parent.parent / "fixtures"
 LAYOUT = json.loads((FIX / "mi355x_node_layout.json").read_text())
@@ -51,16 +51,19 @@ def bdf_to_location(bdf: str) -> int:
     return (int(bus, 16) << 8) | (int(dev, 16) << 3) | int(fn)
 
 
-def build_node(root, n_gpus: int = 8, compute_partition: str = "SPX",
-               memory_partition: str = "NPS1", hidden: Iterable[int] = (),
+def build_node(root, n_gpus: int = 8, compute_partition: Union[str, Sequence[str]] = "SPX",
+               memory_partition: Union[str, Sequence[str]] = "NPS1", hidden: Iterable[int] = (),
                gfx_target_version: int = 90500, with_dev: bool = True) -> Path:
     """Create ``root``/sys/... and ``root``/dev/...; returns ``root`` as a Path.
 
-    ``hidden``: ASIC indices whose agents have an empty ``properties`` (what a container that was
-    not allocated those GPUs sees).
+    ``compute_partition`` / ``memory_partition``: one mode for every ASIC, or one per ASIC (a node
+    whose partition change stopped half-way).  ``hidden``: ASIC indices whose agents have an empty
+    ``properties`` (what a container that was not allocated those GPUs sees).
     """
     root = Path(root)
-    split = SPLIT[compute_partition]
+    modes = ([compute_partition] * n_gpus if isinstance(compute_partition, str)
+             else list(compute_partition))
+    mems = [memory_partition] * n_gpus if isinstance(memory_partition, str) else list(memory_partition)
     topo = root / "sys/class/kfd/kfd/topology"
     drm = root / "sys/class/drm"
     devices = root / "sys/devices"
@@ -78,24 +81,30 @@ def build_node(root, n_gpus: int = 8, compute_partition: str = "SPX",
     node_id = 2
     for a, _g in enumerate(gpus):
         ids = []
-        for _p in range(split):
+        for _p in range(SPLIT[modes[a]]):
             ids.append(node_id)
             node_id += 1
         agent_ids.append(ids)
     all_agents = [i for ids in agent_ids for i in ids]
     for a, g in enumerate(gpus):
+        split = SPLIT[modes[a]]
         loc = bdf_to_location(g["bdf"])
         uid = int(g["unique_id_hex"], 16)
         pci_dir = devices / "pci0000:00" / g["bdf"]
         # PCI device attributes (shared by the card/render node of the ASIC)
         _w(pci_dir / "numa_node", f"{g['numa_node']}\n")
         _w(pci_dir / "unique_id", g["unique_id_hex"] + "\n")
-        _w(pci_dir / "current_compute_partition", compute_partition + "\n")
+        _w(pci_dir / "current_compute_partition", modes[a] + "\n")
         _w(pci_dir / "available_compute_partition", "SPX, DPX, QPX, CPX\n")
-        _w(pci_dir / "current_memory_partition", memory_partition + "\n")
+        _w(pci_dir / "current_memory_partition", mems[a] + "\n")
         _w(pci_dir / "available_memory_partition", "NPS1, NPS2\n")
         _w(pci_dir / "vendor", "0x1002\n")
         _w(pci_dir / "device", "0x75a3\n")
+        _w(pci_dir / "class", "0x120000\n")          # processing accelerator
+        bus = root / "sys/bus/pci/devices"
+        bus.mkdir(parents=True, exist_ok=True)
+        if not (bus / g["bdf"]).exists():
+            os.symlink(os.path.relpath(pci_dir, bus), bus / g["bdf"])
         _w(pci_dir / "mem_info_vram_total", f"{VRAM_BYTES}\n")
         _w(pci_dir / "mem_info_vram_used", f"{(a + 1) * 1024 ** 3}\n")
         _w(pci_dir / "gpu_busy_percent", f"{10 * a}\n")
@@ -142,6 +151,18 @@ def build_node(root, n_gpus: int = 8, compute_partition: str = "SPX",
     return root
 
 
+def add_cpu_only_pci(root, bdf: str = "0000:c1:00.0", vendor: str = "0x1a03",
+                     cls: str = "0x030000") -> None:
+    """A non-AMD PCI device (e.g. the BMC's VGA) on the node."""
+    root = Path(root)
+    d = root / "sys/devices/pci0000:c0" / bdf
+    _w(d / "vendor", vendor + "\n")
+    _w(d / "class", cls + "\n")
+    bus = root / "sys/bus/pci/devices"
+    bus.mkdir(parents=True, exist_ok=True)
+    os.symlink(os.path.relpath(d, bus), bus / bdf)
+
+
 def remove_gpu(root, asic_index: int, compute_partition: str = "SPX") -> None:
     """Fault injection: make one ASIC's agents disappear (driver reset / fell off the bus)."""
     root = Path(root)
@@ -154,7 +175,8 @@ def remove_gpu(root, asic_index: int, compute_partition: str = "SPX") -> None:
             p.write_text("")
 
 
-def set_partition(root, n_gpus: int, compute_partition: str, memory_partition: str = "NPS1",
+def set_partition(root, n_gpus: int, compute_partition: Union[str, Sequence[str]],
+                  memory_partition: Union[str, Sequence[str]] = "NPS1",
                   tmp_parent: Optional[Path] = None) -> Path:
     """Re-enumerate the node in another compute partition mode (what a mode switch does)."""
     import shutil

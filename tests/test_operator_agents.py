@@ -15,6 +15,7 @@ from fakes.kubeapi import FakeKubeAPI
 from k8s_nvidia_gpus_amd.operator import exporter as ex
 from k8s_nvidia_gpus_amd.operator import labeller as lb
 from k8s_nvidia_gpus_amd.operator import partition as pm
+from k8s_nvidia_gpus_amd.operator.labeller import compute_labels
 from k8s_nvidia_gpus_amd.operator import runtime as rt
 from k8s_nvidia_gpus_amd.operator.config import ConfigError, load_config
 from k8s_nvidia_gpus_amd.utils.kube import KubeClient, pod_gpu_request
@@ -368,3 +369,62 @@ def test_validator_gemm_step_under_rocprof(tmp_path):
     assert r.passed and seen[0][:3] == ["rocprofv3", "--kernel-trace", "--stats"]
     assert r.detail["rocprof_kernels"][0]["name"] == "amdk8s_gemm_bf16_nt_256x256"
     assert r.detail["fp8"]["rocprof_kernels"][0]["name"] == "amdk8s_gemm_fp8_nt_256x256"
+
+
+class PerAsicPartitionBackend:
+    """Switches ONE ASIC per call (what the driver does per PCI device); can fail on one ASIC."""
+
+    def __init__(self, root, n_gpus=8, fail_on=None):
+        self.root, self.n, self.fail_on = root, n_gpus, fail_on
+        self.applied = []
+        self.bdfs = [g["bdf"] for g in fake_sysfs.LAYOUT["gpus"][:n_gpus]]
+        self.fail_bdf = sorted(self.bdfs)[fail_on] if fail_on is not None else None
+        topo = read_topology(str(root), 90500)
+        by_bdf = {m[0].pci_bdf: m[0] for m in topo.asics().values()}
+        self.modes = [by_bdf[b].compute_partition for b in self.bdfs]
+        self.mems = [by_bdf[b].memory_partition for b in self.bdfs]
+
+    def set_memory(self, dev, mode):
+        self.mems[self.bdfs.index(dev.pci_bdf)] = mode
+        self.applied.append(("memory", dev.pci_bdf, mode))
+
+    def set_compute(self, dev, mode):
+        a = self.bdfs.index(dev.pci_bdf)
+        if dev.pci_bdf == self.fail_bdf:    # "ASIC 3" = 4th by PCI bus
+            raise OSError(f"amdsmi: device {dev.pci_bdf} busy")
+        self.modes[a] = mode
+        self.applied.append(("compute", dev.pci_bdf, mode))
+        fake_sysfs.set_partition(self.root, self.n, list(self.modes), list(self.mems))
+
+
+def test_partition_failure_mid_node_is_mixed_and_reconverges_per_asic(tmp_path, api, client):
+    root = fake_sysfs.build_node(tmp_path / "r")
+    api.nodes["gpu-node-1"]["metadata"]["labels"][pm.LABEL_DESIRED] = "CPX"
+    kw = dict(poll=0.01, pause_marker=str(tmp_path / "p"), sleep=lambda s: None, reenum_timeout=0.2)
+    bad = PerAsicPartitionBackend(root, fail_on=3)
+    assert pm.PartitionManager(client, "gpu-node-1", bad, str(root), **kw).reconcile() == "failed"
+    state = api.nodes["gpu-node-1"]["metadata"]["annotations"][pm.ANNOT_STATE]
+    assert "after 3 of 8 ASIC(s) switched" in state
+    # the node is half CPX, half SPX: reported as mixed, not as the head GPU's CPX
+    mgr = pm.PartitionManager(client, "gpu-node-1", PerAsicPartitionBackend(root), str(root), **kw)
+    c, m, topo = mgr.current()
+    assert (c, m) == ("mixed", "NPS1") and len(topo.gpus) == 3 * 8 + 5
+    assert compute_labels(str(root))["amd.com/gpu.compute-partition"] == "mixed"
+    # the next reconcile switches only the 5 ASICs still in SPX
+    assert mgr.reconcile() == "applied"
+    assert len([a for a in mgr.backend.applied if a[0] == "compute"]) == 5
+    assert len(read_topology(str(root), 90500).gpus) == 64
+    assert compute_labels(str(root))["amd.com/gpu.compute-partition"] == "CPX"
+    assert mgr.reconcile() == "idle"
+
+
+def test_labeller_pci_present_without_driver_and_not_on_cpu_nodes(tmp_path):
+    import shutil
+
+    root = fake_sysfs.build_node(tmp_path / "gpu")
+    shutil.rmtree(root / "sys/class/kfd")          # amdgpu not loaded yet: no KFD topology
+    labels = compute_labels(str(root))
+    assert labels["amd.com/gpu.pci-present"] == "true" and labels["amd.com/gpu.present"] is None
+    cpu = tmp_path / "cpu"
+    fake_sysfs.add_cpu_only_pci(cpu)                # BMC VGA (ASPEED), no AMD device
+    assert all(v is None for v in compute_labels(str(cpu)).values())

@@ -476,3 +476,13 @@ def test_retarget_leaves_no_placeholders(tmp_path):
 def test_bootstrap_refuses_placeholder_images():
     text = (REPO / "hack/bootstrap.sh").read_text()
     assert "--registry" in text and "retarget.py --check" in text
+
+
+def test_driver_daemonset_only_on_nodes_with_an_amd_accelerator():
+    """A CPU-only worker must not get a driver pod that never turns ready (it would hold the
+    operator Kustomization's wait: true and every app that dependsOn it)."""
+    ds = load_all(REPO / "cluster-config/apps/amd-gpu-operator/driver-daemonset.yaml")[0]
+    sel = ds["spec"]["template"]["spec"]["nodeSelector"]
+    assert sel.get("amd.com/gpu.pci-present") == "true"
+    lab = load_all(REPO / "cluster-config/apps/amd-gpu-operator/node-labeller-daemonset.yaml")[0]
+    assert "amd.com/gpu.pci-present" not in lab["spec"]["template"]["spec"]["nodeSelector"]
