@@ -16,11 +16,15 @@ layer is on the GPU) and serves the endpoints clients of that pod use:
 One scheduler thread owns the GPU: new requests are prefilled into free KV-cache slots, then every
 active sequence advances by one token per decode step — up to 4 sequences share each pass over
 the weights (``--parallel``).  Request handlers only wait on per-request queues, so the GPU is never
-driven from two threads (the reference's SD15 app had that hazard).
+driven from two threads (the reference's SD15 app had that hazard).  A request
+whose client goes away (stream closed, or the connection dropped while a blocking request waits)
+is cancelled and frees its KV slot at the next decode step; a request whose prefill or first
+sample fails gets that error, and no handler waits longer than ``--timeout`` seconds.
 """
 from __future__ import annotations
 
 import argparse
+import asyncio
 import itertools
 import json
 import os
@@ -35,6 +39,11 @@ import torch
 
 from .engine import Engine, sample
 from .tokenizer import Tokenizer, chatml
+
+try:   # module level: FastAPI resolves the handlers' (postponed) annotations in this namespace
+    from fastapi import Request
+except ImportError:  # pragma: no cover - the engine/scheduler work without the HTTP layer
+    Request = None
 
 
 @dataclass
@@ -162,22 +171,29 @@ class Scheduler:
                 continue
             slot = self._free_slot()
             job.slot = slot
-            if job.temperature > 0:
-                dev = self.engine.device if self.engine.gpu else "cpu"
-                job.generator = torch.Generator(device=dev)
-                job.generator.manual_seed(job.seed if job.seed is not None
-                                          else int.from_bytes(os.urandom(4), "little"))
-            t0 = time.perf_counter()
-            logits = self.engine.prefill(job.ids, slot)
-            tok = sample(logits, job.temperature, job.top_k, job.top_p, job.generator)
-            job.t_prefill = time.perf_counter() - t0
-            job.t_first = time.perf_counter()
-            with self._lock:
-                self.metrics["prompt_tokens_total"] += len(job.ids)
-                self.metrics["prefill_seconds_total"] += job.t_prefill
-                self.metrics["tokens_predicted_total"] += 1
-            job.pos = len(job.ids)
-            if not self._emit(job, tok):
+            try:
+                if job.temperature > 0:
+                    dev = self.engine.device if self.engine.gpu else "cpu"
+                    job.generator = torch.Generator(device=dev)
+                    job.generator.manual_seed(job.seed if job.seed is not None
+                                              else int.from_bytes(os.urandom(4), "little"))
+                t0 = time.perf_counter()
+                logits = self.engine.prefill(job.ids, slot)
+                tok = sample(logits, job.temperature, job.top_k, job.top_p, job.generator)
+                job.t_prefill = time.perf_counter() - t0
+                job.t_first = time.perf_counter()
+                with self._lock:
+                    self.metrics["prompt_tokens_total"] += len(job.ids)
+                    self.metrics["prefill_seconds_total"] += job.t_prefill
+                    self.metrics["tokens_predicted_total"] += 1
+                job.pos = len(job.ids)
+                finished = self._emit(job, tok)
+            except Exception as e:  # noqa: BLE001 - this job fails; the others keep decoding
+                with self._lock:
+                    self.metrics["requests_failed_total"] = self.metrics.get("requests_failed_total", 0) + 1
+                job.out.put(("error", repr(e)))
+                continue
+            if not finished:
                 self.active[slot] = job
 
     def _step(self) -> None:
@@ -230,23 +246,58 @@ def _job_from(body: Dict[str, Any], ids: List[int], default_max: int) -> Job:
                seed=None if body.get("seed") in (None, -1) else int(body["seed"]), stop=list(stop))
 
 
-def _collect(job: Job) -> Job:
+class RequestTimeout(RuntimeError):
+    pass
+
+
+def _get(job: Job, deadline: float, poll: Optional[float] = None):
+    """Next (kind, value) of ``job``; raises RequestTimeout past ``deadline`` (perf_counter)."""
+    left = deadline - time.perf_counter()
+    if left <= 0:
+        job.cancelled = True
+        raise RequestTimeout("request timed out")
+    return job.out.get(timeout=left if poll is None else min(left, poll))
+
+
+async def _collect(job: Job, timeout: float, disconnected=None) -> Job:
+    """Wait for ``job`` without holding a worker thread; cancels it when ``disconnected()`` (the
+    client went away) or past ``timeout``."""
+    deadline = time.perf_counter() + timeout
+    loop = asyncio.get_running_loop()
     while True:
-        kind, val = job.out.get()
+        try:
+            kind, val = await loop.run_in_executor(None, _get, job, deadline, 0.5)
+        except queue.Empty:
+            if disconnected is not None and await disconnected():
+                job.cancelled = True
+                raise ConnectionAbortedError("client disconnected")
+            continue
         if kind == "error":
             raise RuntimeError(val)
         if kind == "done":
             return val
 
 
-def _stream(job: Job) -> Iterator[tuple]:
-    while True:
-        kind, val = job.out.get()
-        if kind == "error":
-            raise RuntimeError(val)
-        yield kind, val
-        if kind == "done":
-            return
+def _stream(job: Job, timeout: float) -> Iterator[tuple]:
+    """Events of ``job`` for a streaming response.  When the client disconnects the server closes
+    this generator (GeneratorExit): the job is cancelled and its KV slot freed."""
+    deadline = time.perf_counter() + timeout
+    finished = False
+    try:
+        while True:
+            try:
+                kind, val = _get(job, deadline)
+            except queue.Empty:
+                continue
+            if kind == "error":
+                raise RuntimeError(val)
+            yield kind, val
+            if kind == "done":
+                finished = True
+                return
+    finally:
+        if not finished:
+            job.cancelled = True
 
 
 def _timings(job: Job) -> Dict[str, Any]:
@@ -259,7 +310,7 @@ def _timings(job: Job) -> Dict[str, Any]:
             "predicted_per_second": round(max(n - 1, 0) / max(pred_ms / 1e3, 1e-9), 2)}
 
 
-def create_app(state: Dict[str, Any]):
+def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
     """``state``: {"scheduler": Scheduler | None, "tok": Tokenizer | None, "model": name}; the
     scheduler may be attached later (``/health`` answers 503 until then)."""
     from fastapi import FastAPI, HTTPException
@@ -307,20 +358,30 @@ def create_app(state: Dict[str, Any]):
         except ValueError as e:
             raise HTTPException(400, str(e))
 
+    async def wait(job: Job, request: Request) -> Job:
+        try:
+            return await _collect(job, request_timeout, request.is_disconnected)
+        except RequestTimeout as e:
+            raise HTTPException(504, str(e))
+        except ConnectionAbortedError as e:
+            raise HTTPException(499, str(e))
+        except RuntimeError as e:
+            raise HTTPException(500, str(e))
+
     @app.post("/completion")
-    def completion(body: Dict[str, Any]):
+    async def completion(body: Dict[str, Any], request: Request):
         s = sched()
         job = submit(body, encode_prompt(body.get("prompt", "")), s.engine.max_ctx)
         if body.get("stream"):
             def gen():
-                for kind, val in _stream(job):
+                for kind, val in _stream(job, request_timeout):
                     if kind == "text":
                         yield "data: " + json.dumps({"content": val, "stop": False}) + "\n\n"
                     else:
                         yield "data: " + json.dumps({"content": "", "stop": True,
                                                      "timings": _timings(val)}) + "\n\n"
             return StreamingResponse(gen(), media_type="text/event-stream")
-        job = _collect(job)
+        job = await wait(job, request)
         return {"content": job.text, "stop": True, "model": state.get("model"),
                 "tokens_predicted": len(job.gen), "tokens_evaluated": len(job.ids),
                 "stopped_eos": job.finish == "stop" and job.gen[-1] in s.stop_ids,
@@ -328,7 +389,7 @@ def create_app(state: Dict[str, Any]):
                 "stopped_word": job.finish == "stop" and job.gen[-1] not in s.stop_ids,
                 "timings": _timings(job)}
 
-    def openai(body, ids, chat: bool):
+    async def openai(body, ids, chat: bool, request: Request):
         s = sched()
         job = submit(body, ids, 16 if not chat else s.engine.max_ctx)
         rid = ("chatcmpl-" if chat else "cmpl-") + uuid.uuid4().hex[:24]
@@ -337,7 +398,7 @@ def create_app(state: Dict[str, Any]):
         if body.get("stream"):
             def gen():
                 first = True
-                for kind, val in _stream(job):
+                for kind, val in _stream(job, request_timeout):
                     if kind == "text":
                         if chat:
                             delta = {"content": val}
@@ -360,7 +421,7 @@ def create_app(state: Dict[str, Any]):
                                                      "choices": [ch]}) + "\n\n"
                 yield "data: [DONE]\n\n"
             return StreamingResponse(gen(), media_type="text/event-stream")
-        job = _collect(job)
+        job = await wait(job, request)
         choice = {"index": 0, "finish_reason": job.finish, "logprobs": None}
         if chat:
             choice["message"] = {"role": "assistant", "content": job.text}
@@ -373,15 +434,15 @@ def create_app(state: Dict[str, Any]):
                 "timings": _timings(job)}
 
     @app.post("/v1/completions")
-    def v1_completions(body: Dict[str, Any]):
-        return openai(body, encode_prompt(body.get("prompt", "")), chat=False)
+    async def v1_completions(body: Dict[str, Any], request: Request):
+        return await openai(body, encode_prompt(body.get("prompt", "")), False, request)
 
     @app.post("/v1/chat/completions")
-    def v1_chat(body: Dict[str, Any]):
+    async def v1_chat(body: Dict[str, Any], request: Request):
         msgs = body.get("messages") or []
         if not isinstance(msgs, list) or not msgs:
             raise HTTPException(400, "messages must be a non-empty list")
-        return openai(body, state["tok"].encode(chatml(msgs)), chat=True)
+        return await openai(body, state["tok"].encode(chatml(msgs)), True, request)
 
     @app.get("/metrics")
     def metrics():
@@ -438,12 +499,14 @@ def main(argv=None) -> int:
     ap.add_argument("-np", "--parallel", type=int, default=4)
     ap.add_argument("-ngl", "--n-gpu-layers", type=int, default=999, help="accepted; all layers run on the GPU")
     ap.add_argument("-t", "--threads", type=int, default=0, help="accepted; the GPU does the work")
+    ap.add_argument("-to", "--timeout", type=float, default=600.0,
+                    help="seconds a request may wait for its result (then 504 and cancelled)")
     args = ap.parse_args(argv)
     import uvicorn
 
     state: Dict[str, Any] = {"scheduler": None, "tok": None, "model": "loading",
                              "created": time.time()}
-    app = create_app(state)
+    app = create_app(state, request_timeout=args.timeout)
 
     def load_bg():
         eng, tok, name = build_engine(args)

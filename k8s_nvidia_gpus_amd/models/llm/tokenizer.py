@@ -11,6 +11,8 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional, Sequence
 
+from ...utils.bpe import bytes_to_unicode
+
 import numpy as np
 
 QWEN2_PATTERN = (r"(?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}|"
@@ -102,18 +104,6 @@ def chatml(messages: Sequence[Dict[str, str]], default_system: Optional[str] = D
     return "".join(out)
 
 
-def bytes_to_unicode() -> Dict[int, str]:
-    """GPT-2's byte → printable-unicode table (the alphabet of byte-level BPE vocabularies)."""
-    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("¡"), ord("¬") + 1)) \
-        + list(range(ord("®"), ord("ÿ") + 1))
-    cs = bs[:]
-    n = 0
-    for b in range(256):
-        if b not in bs:
-            bs.append(b)
-            cs.append(256 + n)
-            n += 1
-    return dict(zip(bs, map(chr, cs)))
 
 
 def synthetic_vocab(size: int, corpus: str = "") -> Dict:

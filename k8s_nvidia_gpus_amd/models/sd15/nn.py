@@ -242,8 +242,14 @@ class Upsample2D(nn.Module):
         super().__init__()
         self.conv = nn.Conv2d(channels, channels, 3, padding=1)
 
-    def forward(self, x):
-        x = F.interpolate(x, scale_factor=2.0, mode="nearest")
+    def forward(self, x, size=None):
+        """Nearest 2x, or to ``size`` — the next skip's spatial size, which differs from 2x when a
+        latent side is not a multiple of 8 (e.g. 520 px → latent 65 → 33 → 17 → 9 → back up to 17),
+        as diffusers' ``forward_upsample_size`` does."""
+        if size is None:
+            x = F.interpolate(x, scale_factor=2.0, mode="nearest")
+        else:
+            x = F.interpolate(x, size=tuple(size), mode="nearest")
         if x.device.type == "cuda":
             x = x.contiguous(memory_format=torch.channels_last)
         return self.conv(x)

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import os
 import time
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple, Union
 
@@ -42,10 +43,14 @@ class PipelineOutput:
 class UNetRunner:
     """``eps_cfg = uncond + g·(cond − uncond)`` of one UNet pass, eager or replayed from a HIP graph."""
 
-    def __init__(self, unet: UNet2DConditionModel, dtype: torch.dtype, use_graphs: bool):
+    def __init__(self, unet: UNet2DConditionModel, dtype: torch.dtype, use_graphs: bool,
+                 max_graphs: int = 4):
         self.unet, self.dtype = unet, dtype
         self.use_graphs = use_graphs
-        self._graphs: Dict[Tuple[int, int, int], dict] = {}
+        # (batch, h, w) → captured graph, least recently used first; each graph pins its memory
+        # pool, and the key is client-chosen (batch, width, height), so the cache is bounded
+        self.max_graphs = max_graphs
+        self._graphs: "OrderedDict[Tuple[int, int, int], dict]" = OrderedDict()
         self.captures = 0
 
     def _body(self, lat, t, ctx, g):
@@ -75,13 +80,23 @@ class UNetRunner:
         st["graph"] = graph
         self._graphs[key] = st
         self.captures += 1
+        self._evict()
         return st
+
+    def _evict(self) -> None:
+        while len(self._graphs) > self.max_graphs:
+            _, old = self._graphs.popitem(last=False)
+            old["graph"].reset()                 # release the evicted graph's memory pool
 
     def __call__(self, lat, t: int, ctx, guidance: float):
         if not (self.use_graphs and lat.device.type == "cuda"):
             return self.eager(lat, t, ctx, guidance)
         key = (lat.shape[0], lat.shape[2], lat.shape[3])
-        st = self._graphs.get(key) or self._capture(lat, ctx)
+        st = self._graphs.get(key)
+        if st is None:
+            st = self._capture(lat, ctx)
+        else:
+            self._graphs.move_to_end(key)
         st["lat"].copy_(lat)
         st["ctx"].copy_(ctx)
         st["t"].fill_(float(t))

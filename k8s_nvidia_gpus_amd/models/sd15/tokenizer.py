@@ -14,6 +14,8 @@ import os
 import zlib
 from typing import Dict, List, Sequence, Tuple
 
+from ...utils.bpe import bytes_to_unicode
+
 import regex
 
 _PAT = regex.compile(
@@ -22,17 +24,6 @@ _PAT = regex.compile(
 
 
 @functools.lru_cache()
-def bytes_to_unicode() -> Dict[int, str]:
-    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("¡"), ord("¬") + 1)) \
-        + list(range(ord("®"), ord("ÿ") + 1))
-    cs = bs[:]
-    n = 0
-    for b in range(256):
-        if b not in bs:
-            bs.append(b)
-            cs.append(256 + n)
-            n += 1
-    return dict(zip(bs, map(chr, cs)))
 
 
 def _pairs(word: Tuple[str, ...]):

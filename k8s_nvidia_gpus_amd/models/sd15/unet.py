@@ -81,7 +81,7 @@ class UpBlock(nn.Module):
             if self.attentions is not None:
                 x = self.attentions[i](x, context)
         if self.upsamplers is not None:
-            x = self.upsamplers[0](x)
+            x = self.upsamplers[0](x, skips[-1].shape[-2:] if skips else None)
         return x
 
 

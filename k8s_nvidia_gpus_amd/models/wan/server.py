@@ -524,6 +524,13 @@ class PromptQueue:
                                                  "exception_type": e.kind}])
                 log.warning("prompt %s failed at node %s (%s): %s", job.prompt_id, e.node_id,
                             e.class_type, e)
+            except Exception as e:  # noqa: BLE001 - outside any node: still one failed prompt,
+                # never a dead worker thread that leaves every later prompt pending forever
+                status, kind = "error", "failed"
+                msgs.append(["execution_error", {"prompt_id": job.prompt_id, "node_id": "",
+                                                 "node_type": "", "exception_message": repr(e),
+                                                 "exception_type": type(e).__name__}])
+                log.exception("prompt %s failed", job.prompt_id)
             gpu_s = time.time() - t0
             writes = self.ex.take_writes()
             with self._lock:
@@ -652,10 +659,12 @@ def create_app(store: ModelStore, out_dir: str, shift: float = 8.0, ffmpeg: Opti
     app.state.executor = ex
     ready = threading.Event()
     app.state.ready = ready
+    app.state.warmup_error = None
     if warmup is not None:
         graph = warmup_graph(store, *warmup)
         if graph is None:
             log.info("warm-up skipped: the reference model files are not all present")
+            _freeze_tunableop()          # no request may start a tuning sweep
             ready.set()
         else:
             job = pq.submit(graph, "warmup")
@@ -664,12 +673,19 @@ def create_app(store: ModelStore, out_dir: str, shift: float = 8.0, ffmpeg: Opti
                 while pq.history(job.prompt_id) == {}:
                     time.sleep(0.5)
                 st = pq.history(job.prompt_id)[job.prompt_id]["status"]["status_str"]
-                log.info("warm-up finished: %s", st)
                 _freeze_tunableop()
+                if st != "success":
+                    # the models did not load / run: stay NOT ready (readiness 503) rather than
+                    # take traffic that would fail
+                    app.state.warmup_error = st
+                    log.error("warm-up job failed (%s): the pod stays unready", st)
+                    return
+                log.info("warm-up finished: %s", st)
                 ready.set()
 
             threading.Thread(target=watch, daemon=True, name="wan-warmup").start()
     else:
+        _freeze_tunableop()
         ready.set()
 
     @app.get("/health")
@@ -679,7 +695,8 @@ def create_app(store: ModelStore, out_dir: str, shift: float = 8.0, ffmpeg: Opti
     @app.get("/queue")
     def get_queue():
         if not ready.is_set():     # readiness: 503 until the start-up warm-up job has run
-            return JSONResponse({"status": "warming up"}, 503)
+            err = app.state.warmup_error
+            return JSONResponse({"status": f"warm-up failed: {err}" if err else "warming up"}, 503)
         return pq.queue_state()
 
     @app.post("/queue")

@@ -9,7 +9,8 @@ Two kinds of output, both built IN-TREE so they travel with the repository snaps
 * ``native/bin/*`` — standalone executables used by the operator DaemonSets / validator pods:
   ``amd-vectoradd`` (reference-compatible stdout protocol), ``amd-gemm-validator``,
   ``amd-proftester`` (per-pipe load generator: tensor / HBM / fp32 / fp64 / PCIe / xGMI),
-  ``rccl-allreduce-bench``, ``kfd-probe`` and the containerd OCI hook ``amd-oci-hook``.
+  ``rccl-allreduce-bench``, ``kfd-probe`` and ``amd-container-runtime`` (the runc wrapper containerd
+  runs for RuntimeClass ``amd``; it injects the allocated /dev/kfd + render nodes as an OCI hook would).
 
 The reference has no in-tree native code at all (its GPU code lives in pulled images
 such as ``nvcr.io/nvidia/k8s/cuda-sample:vectoradd`` — reference README.md:283); these are the

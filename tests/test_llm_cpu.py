@@ -294,3 +294,75 @@ def test_server_seeded_sampling_is_reproducible(client):
     a = c.post("/completion", json=body).json()["content"]
     b = c.post("/completion", json=body).json()["content"]
     assert a == b
+
+
+def test_server_prefill_error_reaches_its_request_and_serving_continues(tiny_model):
+    """a job whose prefill raises (before it is active) gets a 500, not a hung worker."""
+    from fastapi.testclient import TestClient
+
+    from k8s_nvidia_gpus_amd.models.llm.server import Scheduler, create_app
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load
+
+    eng, tok = load(tiny_model, device="cpu", max_ctx=256, slots=2)
+    real = eng.prefill
+    calls = {"n": 0}
+
+    def flaky(ids, slot):
+        calls["n"] += 1
+        if calls["n"] == 1:
+            raise RuntimeError("probabilities contain inf")
+        return real(ids, slot)
+
+    eng.prefill = flaky
+    state = {"scheduler": Scheduler(eng, tok, parallel=2), "tok": tok, "model": "tiny"}
+    c = TestClient(create_app(state, request_timeout=30))
+    try:
+        r = c.post("/completion", json={"prompt": "hello", "n_predict": 3, "temperature": 0})
+        assert r.status_code == 500 and "inf" in r.text
+        ok = c.post("/completion", json={"prompt": "hello", "n_predict": 3, "temperature": 0})
+        assert ok.status_code == 200 and ok.json()["tokens_predicted"] >= 1
+        assert state["scheduler"].metrics["requests_failed_total"] == 1
+    finally:
+        state["scheduler"].close()
+
+
+def test_server_cancels_abandoned_requests_and_times_out(tiny_model):
+    """a stream the client closes is cancelled (its slot is freed before n_predict) and a
+    blocking request never waits past the timeout."""
+    import time as _t
+
+    from fastapi.testclient import TestClient
+
+    from k8s_nvidia_gpus_amd.models.llm import server as S
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load
+
+    eng, tok = load(tiny_model, device="cpu", max_ctx=256, slots=1)
+    real_decode = eng.decode
+
+    def slow_decode(*a, **k):
+        _t.sleep(0.02)
+        return real_decode(*a, **k)
+
+    eng.decode = slow_decode
+    sched = S.Scheduler(eng, tok, parallel=1)
+    state = {"scheduler": sched, "tok": tok, "model": "tiny"}
+    try:
+        job = sched.submit(S.Job(ids=tok.encode("hello"), max_new=200, temperature=0.0))
+        gen = S._stream(job, timeout=30)
+        next(gen)                                  # first token arrived: job is decoding
+        gen.close()                                # client went away
+        assert job.cancelled
+        t0 = _t.time()
+        while sched.active and _t.time() - t0 < 5:
+            _t.sleep(0.01)
+        assert not sched.active and len(job.gen) < 200
+        # blocking request with a short timeout: 504, and the job is cancelled
+        c = TestClient(S.create_app(state, request_timeout=0.3))
+        r = c.post("/completion", json={"prompt": "hello", "n_predict": 200, "temperature": 0})
+        assert r.status_code == 504
+        t0 = _t.time()
+        while sched.active and _t.time() - t0 < 5:
+            _t.sleep(0.01)
+        assert not sched.active
+    finally:
+        sched.close()

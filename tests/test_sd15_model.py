@@ -223,3 +223,40 @@ def test_functional_reference_ops_match_torch():
     torch.testing.assert_close(o, ref, rtol=1e-5, atol=1e-5)
     x = torch.randn(3, 5, 8)
     torch.testing.assert_close(SF.geglu(x), x[..., :4] * torch.nn.functional.gelu(x[..., 4:]))
+
+
+def test_unet_handles_sizes_that_are_not_multiples_of_64():
+    """a 520x512 request (latent 65x64) — the upsamplers follow the skips' sizes
+    (65 → 33 → 17 → 9 and back), as diffusers' forward_upsample_size does."""
+    cfg = tiny()
+    torch.manual_seed(0)
+    unet = UNet2DConditionModel(cfg.unet).eval()
+    ctx = torch.randn(1, 77, cfg.unet.cross_attention_dim)
+    for h, w in ((65, 64), (17, 23), (9, 40)):
+        x = torch.randn(1, 4, h, w)
+        with torch.no_grad():
+            y = unet(x, torch.tensor([10]), ctx)
+        assert y.shape == x.shape and torch.isfinite(y).all()
+    pipe = _tiny_pipe()
+    out = pipe("a cabin", num_inference_steps=1, width=72, height=520 // 4 // 2 * 8,
+               generator=[torch.Generator().manual_seed(1)])
+    assert out.images[0].size == (72, 520 // 4 // 2 * 8)
+
+
+def test_unet_graph_cache_is_bounded():
+    from k8s_nvidia_gpus_amd.models.sd15.pipeline import UNetRunner
+
+    class _G:
+        was_reset = False
+
+        def reset(self):
+            self.was_reset = True
+
+    r = UNetRunner(UNet2DConditionModel(tiny().unet), torch.float32, use_graphs=True, max_graphs=2)
+    graphs = {}
+    for key in [(1, 64, 64), (1, 64, 72), (2, 64, 64)]:
+        graphs[key] = _G()
+        r._graphs[key] = {"graph": graphs[key]}
+        r._evict()
+    assert list(r._graphs) == [(1, 64, 72), (2, 64, 64)]
+    assert graphs[(1, 64, 64)].was_reset and not graphs[(2, 64, 64)].was_reset

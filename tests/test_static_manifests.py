@@ -486,3 +486,23 @@ def test_driver_daemonset_only_on_nodes_with_an_amd_accelerator():
     assert sel.get("amd.com/gpu.pci-present") == "true"
     lab = load_all(REPO / "cluster-config/apps/amd-gpu-operator/node-labeller-daemonset.yaml")[0]
     assert "amd.com/gpu.pci-present" not in lab["spec"]["template"]["spec"]["nodeSelector"]
+
+
+def test_renovate_bumps_dockerfile_base_images():
+    """ROCm userspace bumps (the dashboard footer's warning) reach the images' FROM / ARG pins."""
+    import json
+
+    cfg = json.loads((REPO / "renovate.json").read_text())
+    mgr = next(m for m in cfg["customManagers"] if "Dockerfile" in m["managerFilePatterns"][0])
+    rx = re.compile(_py_regex(mgr["matchStrings"][0]))
+    fp = re.compile(mgr["managerFilePatterns"][0].strip("/"))
+    seen = {}
+    for df in sorted((REPO / "images").glob("*/Dockerfile")):
+        rel = str(df.relative_to(REPO))
+        assert fp.search(rel), rel
+        text = df.read_text()
+        hits = [m.groupdict() for m in rx.finditer(text)]
+        assert len(hits) == text.count("# renovate:"), rel
+        seen.update({h["depName"]: h["currentValue"] for h in hits})
+    assert seen["rocm/dev-ubuntu-22.04"] == "7.2"
+    assert seen["rocm/pytorch"].startswith("rocm7.2_")

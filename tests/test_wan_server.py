@@ -196,3 +196,21 @@ def test_encode_failure_reported_after_gpu_part(store, tmp_path):
         err = [m for m in st["messages"] if m[0] == "execution_error"][0][1]
         assert err["node_type"] == "SaveWEBM" and "boom" in err["exception_message"]
     assert not list((tmp_path / "out").rglob("*.webm"))        # no empty placeholder left
+
+
+def test_failed_warmup_keeps_the_pod_unready(store, tmp_path, monkeypatch):
+    """a warm-up job that fails (models that do not load) must not turn the pod ready."""
+    from k8s_nvidia_gpus_amd.models.wan import server as WS
+
+    def boom(self, graph, on_node=None):
+        raise RuntimeError("cannot load wan2.1_t2v_1.3B_bf16.safetensors")
+
+    monkeypatch.setattr(WS.Executor, "run", boom)
+    app = create_app(store, str(tmp_path / "out"), ffmpeg="", warmup=(64, 48, 5))
+    with TestClient(app) as c:
+        t0 = time.time()
+        while app.state.warmup_error is None and time.time() - t0 < 60:
+            time.sleep(0.05)
+        assert not app.state.ready.is_set()
+        r = c.get("/queue")
+        assert r.status_code == 503 and "warm-up failed" in r.json()["status"]
