@@ -22,7 +22,11 @@ Outside the timed region it also reports:
   ``import torch``); ``time_to_first_gpu_result_native_s`` — the same check as the validator pod
   runs it (native ``amd-vectoradd``, a child process started before torch loads, this rank's GPU);
 * ``numerics_max_rel_err`` — sampled error of the timed kernel against an fp32 on-device reference;
-* ``allreduce_busbw_gbps`` — RCCL all-reduce bus bandwidth over xGMI across the N ranks (N > 1);
+* ``allreduce_busbw_gbps`` — peak RCCL all-reduce bus bandwidth over xGMI across the N ranks, from
+  ``allreduce_sweep`` (1 MiB … 1 GiB, ×4; N > 1);
+* ``telemetry_per_rank`` — each rank's gfx clock (mean / min), socket power and hotspot temperature
+  sampled through amd-smi during the timed window, so a flat weak-scaling curve can be told apart
+  into a power-capped clock vs a slow rank from one run (parallel/telemetry.py);
 * ``fp8_tflops`` — the validator's second precision: the same GEMM shape in OCP fp8 e4m3 through
   the hand-written ``v_mfma_scale_f32_16x16x128_f8f6f4`` kernel, whole-job aggregate, timed the
   same way (extra field; the headline ``value`` stays bf16).
@@ -83,8 +87,9 @@ def parse_args(argv=None):
                          "has left its load-step transient (see settle())")
     ap.add_argument("--size", type=int, default=8192, help="M = N = K of the validator GEMM")
     ap.add_argument("--variant", default=None, help="GEMM variant (auto | w8 | w4)")
-    ap.add_argument("--allreduce-mib", type=int, default=256,
-                    help="message size of the post-run RCCL all-reduce probe (N > 1)")
+    ap.add_argument("--allreduce-mib", type=int, default=1024,
+                    help="largest message of the post-run RCCL all-reduce sweep (1 MiB .. this, x4; N > 1)")
+    ap.add_argument("--no-telemetry", action="store_true", help="no amd-smi sampling")
     ap.add_argument("--no-allreduce", action="store_true")
     ap.add_argument("--no-fp8", action="store_true", help="skip the fp8 GEMM extra measurement")
     ap.add_argument("--cpu-smoke", action="store_true", help=argparse.SUPPRESS)
@@ -156,7 +161,7 @@ def main(argv=None) -> int:
     if not smoke and not torch.cuda.is_available():
         print("bench.py needs an MI355X (no GPU visible)", file=sys.stderr)
         return 2
-    from k8s_nvidia_gpus_amd.parallel.collectives import init_distributed, measure
+    from k8s_nvidia_gpus_amd.parallel.collectives import init_distributed, sweep
 
     if distributed:
         device = init_distributed("gloo" if smoke else "nccl")
@@ -205,9 +210,15 @@ def main(argv=None) -> int:
     for _ in range(args.warmup):
         step()
     sync()
+    from k8s_nvidia_gpus_amd.parallel import telemetry
+
+    sampler = (telemetry.timed(device_index=device.index if device.index is not None else 0)
+               if not smoke and not args.no_telemetry else None)
     if distributed:
         dist.barrier()
     sync()
+    if sampler is not None:
+        sampler.__enter__()     # a sleeping thread; one amd-smi read per 20 ms
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -216,6 +227,10 @@ def main(argv=None) -> int:
         dist.barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    tel = None
+    if sampler is not None:
+        sampler.__exit__(None, None, None)
+        tel = sampler.summary()
 
     flop_per_gpu = 2.0 * s * s * s * args.steps
     per_rank = [round(flop_per_gpu / elapsed / 1e12, 2)]
@@ -228,6 +243,10 @@ def main(argv=None) -> int:
         gathered = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(gathered, mine)
         per_rank = [round(float(x.item()), 2) for x in gathered]
+        tels = [None] * world
+        dist.all_gather_object(tels, tel)
+    else:
+        tels = [tel]
     fp8_tflops = None
     if not smoke and not args.no_fp8 and K.gemm_fp8_shape_supported(s, s, s):
         del a, b
@@ -260,12 +279,18 @@ def main(argv=None) -> int:
         del a8, b8
 
     busbw = None
+    ar_sweep = None
     if distributed and not args.no_allreduce:
-        r = measure("all_reduce", (1 if smoke else args.allreduce_mib) << 20, iters=3 if smoke else 10,
-                    warmup=1 if smoke else 3, device=device)
-        if r.wrong:
-            raise RuntimeError(f"all-reduce returned {r.wrong} wrong elements")
-        busbw = r.busbw_gbps
+        top = (4 if smoke else args.allreduce_mib) << 20
+        rows = sweep("all_reduce", 1 << 20, top, factor=4, iters=3 if smoke else 10,
+                     warmup=1 if smoke else 3, device=device)
+        bad = sum(r.wrong for r in rows)
+        if bad:
+            raise RuntimeError(f"all-reduce returned {bad} wrong elements")
+        ar_sweep = [{"bytes": r.bytes, "time_us": round(r.time_us, 1),
+                     "algbw_gbps": round(r.algbw_gbps, 2), "busbw_gbps": round(r.busbw_gbps, 2)}
+                    for r in rows]
+        busbw = max(r.busbw_gbps for r in rows)
 
     value = flop_per_gpu * world / elapsed / 1e12
     if rank == 0:
@@ -299,6 +324,8 @@ def main(argv=None) -> int:
             "time_to_first_gpu_result_native_s": _NATIVE_TTFR,
             "numerics_max_rel_err": max_rel_err,
             "allreduce_busbw_gbps": (round(busbw, 2) if busbw is not None else None),
+            "allreduce_sweep": ar_sweep,
+            "telemetry_per_rank": tels,
             "fp8_tflops": (round(fp8_tflops, 2) if fp8_tflops is not None else None),
             "device": torch.cuda.get_device_name(device) if device.type == "cuda" else "cpu",
         }

@@ -7,6 +7,13 @@
 //
 //   size  count  type  time(us)  algbw(GB/s)  busbw(GB/s)  #wrong
 //
+// With --mp it runs as ONE RANK of a one-process-per-GPU job instead — the topology bench.py and
+// every torch.distributed job use — launched as
+//   torchrun --nproc-per-node N --no-python rccl-allreduce-bench --mp [...]
+// (RANK / WORLD_SIZE / LOCAL_RANK from the launcher; rank 0 publishes the ncclUniqueId through a file
+// that the other ranks poll, then ncclCommInitRank); times are the MAX over ranks and rank 0 prints.
+// --plan prints the resolved launch (mode, rank, world, device, id file) and exits before any HIP call.
+//
 // busbw = algbw · 2(n−1)/n (ring all-reduce traffic per rank).  On MI355X each GPU has 7 xGMI links
 // of ~153 GB/s; a ring uses one outgoing link per hop, so RCCL reaches beyond one link only by
 // spreading channels over several rings — report what is measured, not the aggregate link rate.
@@ -15,12 +22,15 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <unistd.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "amdk8s_native.h"
@@ -59,7 +69,38 @@ struct Options {
   int warmup = 5;
   int ngpus = 0;  // 0 = all visible
   bool json = false;
+  bool mp = false;    // one rank of a one-process-per-GPU job
+  bool plan = false;  // print the resolved launch and exit
+  std::string id_file;
+  int id_timeout_s = 300;
 };
+
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+
+// rank 0 → file (atomic rename); others poll for it
+bool exchange_id(ncclUniqueId* id, int rank, const std::string& path, int timeout_s) {
+  if (rank == 0) {
+    const std::string tmp = path + ".tmp";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f || std::fwrite(id, sizeof(*id), 1, f) != 1) return false;
+    std::fclose(f);
+    return std::rename(tmp.c_str(), path.c_str()) == 0;
+  }
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(timeout_s);
+  while (std::chrono::steady_clock::now() < deadline) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (f) {
+      const bool ok = std::fread(id, sizeof(*id), 1, f) == 1;
+      std::fclose(f);
+      if (ok) return true;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  }
+  return false;
+}
 
 size_t parse_size(const char* s) {
   char* end = nullptr;
@@ -69,6 +110,99 @@ size_t parse_size(const char* s) {
   else if (suf == "M" || suf == "m") v *= 1024 * 1024;
   else if (suf == "G" || suf == "g") v *= 1024.0 * 1024 * 1024;
   return (size_t)v;
+}
+
+int run_mp(const Options& o, int rank, int world, int local) {
+  AMDK8S_HIP_CHECK(hipSetDevice(local));
+  ncclUniqueId id;
+  if (rank == 0) RCCL_CHECK(ncclGetUniqueId(&id));
+  if (!exchange_id(&id, rank, o.id_file, o.id_timeout_s)) {
+    std::fprintf(stderr, "rank %d: no ncclUniqueId at %s after %d s\n", rank, o.id_file.c_str(),
+                 o.id_timeout_s);
+    return 3;
+  }
+  ncclComm_t comm;
+  RCCL_CHECK(ncclCommInitRank(&comm, world, id, rank));
+  if (rank == 0) std::remove(o.id_file.c_str());   // every rank has read it by now
+  int ver = 0;
+  ncclGetVersion(&ver);
+  hipStream_t st;
+  AMDK8S_HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  const size_t max_count = std::max<size_t>(1, o.max_bytes / sizeof(float));
+  float* buf = nullptr;
+  double* scal = nullptr;   // [0] time (max over ranks), [1] wrong count (sum)
+  unsigned long long* dbad = nullptr;
+  AMDK8S_HIP_CHECK(hipMalloc(&buf, max_count * sizeof(float)));
+  AMDK8S_HIP_CHECK(hipMalloc(&scal, 2 * sizeof(double)));
+  AMDK8S_HIP_CHECK(hipMalloc(&dbad, sizeof(unsigned long long)));
+  if (rank == 0) {
+    std::printf("# rccl-allreduce-bench --mp: %d rank(s), one GPU each, RCCL %d, in-place float "
+                "sum, %d iters\n", world, ver, o.iters);
+    std::printf("# %12s %12s %6s %10s %12s %12s %8s\n", "size(B)", "count", "type", "time(us)",
+                "algbw(GB/s)", "busbw(GB/s)", "#wrong");
+  }
+  auto barrier = [&]() {
+    RCCL_CHECK(ncclAllReduce(scal, scal, 1, ncclFloat64, ncclMax, comm, st));
+    AMDK8S_HIP_CHECK(hipStreamSynchronize(st));
+  };
+  double peak_bus = 0, peak_alg = 0;
+  size_t peak_size = 0;
+  unsigned long long total_bad = 0;
+  const float expect = (float)world * (world + 1) / 2.0f;
+  for (size_t bytes = o.min_bytes; bytes <= o.max_bytes; bytes *= (size_t)o.factor) {
+    const size_t count = std::max<size_t>(1, bytes / sizeof(float));
+    hipLaunchKernelGGL(fill_f32, dim3(1024), dim3(256), 0, st, buf, count, (float)(rank + 1));
+    AMDK8S_HIP_CHECK(hipMemsetAsync(dbad, 0, sizeof(unsigned long long), st));
+    RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat, ncclSum, comm, st));
+    hipLaunchKernelGGL(count_wrong_f32, dim3(1024), dim3(256), 0, st, buf, count, expect, dbad);
+    unsigned long long b = 0;
+    AMDK8S_HIP_CHECK(hipMemcpyAsync(&b, dbad, sizeof(b), hipMemcpyDeviceToHost, st));
+    AMDK8S_HIP_CHECK(hipStreamSynchronize(st));
+    for (int w = 0; w < o.warmup; ++w)
+      RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat, ncclSum, comm, st));
+    barrier();
+    auto t0 = std::chrono::steady_clock::now();
+    for (int it = 0; it < o.iters; ++it)
+      RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat, ncclSum, comm, st));
+    AMDK8S_HIP_CHECK(hipStreamSynchronize(st));
+    double h[2] = {std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0)
+                       .count() / o.iters, (double)b};
+    AMDK8S_HIP_CHECK(hipMemcpyAsync(scal, h, sizeof(h), hipMemcpyHostToDevice, st));
+    RCCL_CHECK(ncclAllReduce(scal, scal, 1, ncclFloat64, ncclMax, comm, st));
+    RCCL_CHECK(ncclAllReduce(scal + 1, scal + 1, 1, ncclFloat64, ncclSum, comm, st));
+    AMDK8S_HIP_CHECK(hipMemcpyAsync(h, scal, sizeof(h), hipMemcpyDeviceToHost, st));
+    AMDK8S_HIP_CHECK(hipStreamSynchronize(st));
+    const double us = h[0];
+    const unsigned long long bad = (unsigned long long)h[1];
+    total_bad += bad;
+    const double algbw = (double)count * sizeof(float) / (us * 1e-6) / 1e9;
+    const double busbw = world > 1 ? algbw * 2.0 * (world - 1) / world : algbw;
+    if (busbw > peak_bus) {
+      peak_bus = busbw;
+      peak_alg = algbw;
+      peak_size = count * sizeof(float);
+    }
+    if (rank == 0)
+      std::printf("  %12zu %12zu %6s %10.1f %12.2f %12.2f %8llu\n", count * sizeof(float), count,
+                  "float", us, algbw, busbw, bad);
+    if (bytes > o.max_bytes / (size_t)o.factor) break;
+  }
+  if (rank == 0) {
+    std::printf("# peak busbw %.2f GB/s (algbw %.2f GB/s) at %zu bytes on %d rank(s)\n", peak_bus,
+                peak_alg, peak_size, world);
+    if (o.json)
+      std::printf("{\"check\": \"rccl_allreduce\", \"mode\": \"mp\", \"ngpus\": %d, "
+                  "\"peak_busbw_gbps\": %.2f, \"peak_algbw_gbps\": %.2f, \"peak_bytes\": %zu, "
+                  "\"wrong\": %llu, \"passed\": %s}\n", world, peak_bus, peak_alg, peak_size, total_bad,
+                  total_bad == 0 ? "true" : "false");
+    std::printf(total_bad ? "Test FAILED\n" : "Test PASSED\nDone\n");
+  }
+  ncclCommDestroy(comm);
+  hipFree(buf);
+  hipFree(scal);
+  hipFree(dbad);
+  hipStreamDestroy(st);
+  return total_bad ? 1 : 0;
 }
 
 }  // namespace
@@ -88,11 +222,40 @@ int main(int argc, char** argv) {
     else if (a == "-w" || a == "--warmup") o.warmup = std::atoi(next());
     else if (a == "-g" || a == "--ngpus") o.ngpus = std::atoi(next());
     else if (a == "--json") o.json = true;
+    else if (a == "--mp") o.mp = true;
+    else if (a == "--plan") o.plan = true;
+    else if (a == "--id-file") o.id_file = next();
+    else if (a == "--id-timeout") o.id_timeout_s = std::atoi(next());
     else {
       std::printf("usage: rccl-allreduce-bench [-b MIN] [-e MAX] [-f FACTOR] [-n ITERS] "
-                  "[-w WARMUP] [-g NGPUS] [--json]\n");
+                  "[-w WARMUP] [-g NGPUS] [--json] [--mp [--id-file PATH] [--id-timeout S]] "
+                  "[--plan]\n");
       return a == "-h" || a == "--help" ? 0 : 2;
     }
+  }
+  if (o.mp) {
+    const int rank = env_int("RANK", -1), world = env_int("WORLD_SIZE", -1);
+    const int local = env_int("LOCAL_RANK", rank);
+    if (rank < 0 || world < 1 || rank >= world) {
+      std::fprintf(stderr, "--mp needs RANK and WORLD_SIZE (launch with torchrun --no-python)\n");
+      return 2;
+    }
+    if (o.id_file.empty()) {
+      const char* run = std::getenv("TORCHELASTIC_RUN_ID");
+      const char* port = std::getenv("MASTER_PORT");
+      o.id_file = std::string("/tmp/rccl-allreduce-bench.") + (run ? run : "none") + "." +
+                  (port ? port : "0") + ".id";
+    }
+    if (o.plan) {
+      std::printf("{\"mode\": \"mp\", \"rank\": %d, \"world\": %d, \"device\": %d, "
+                  "\"id_file\": \"%s\"}\n", rank, world, local, o.id_file.c_str());
+      return 0;
+    }
+    return run_mp(o, rank, world, local);
+  }
+  if (o.plan) {
+    std::printf("{\"mode\": \"single\", \"ngpus\": %d}\n", o.ngpus);
+    return 0;
   }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {

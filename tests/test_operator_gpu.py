@@ -94,6 +94,26 @@ def test_rccl_bench_single_gpu_passes(native):
     assert "Test PASSED" in p.stdout
 
 
+def test_rccl_bench_multiprocess_mode_one_rank(native):
+    """The one-process-per-GPU launch of the gpu-bench Job (torchrun --no-python ... --mp): the
+    ncclUniqueId file exchange, ncclCommInitRank and the MAX-over-ranks timing on the real GPU."""
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=1", "--master-addr=127.0.0.1", f"--master-port={port}",
+                        "--no-python", str(native / "rccl-allreduce-bench"), "--mp", "-b", "1M",
+                        "-e", "16M", "-n", "5", "--json"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    doc = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert doc["mode"] == "mp" and doc["ngpus"] == 1 and doc["passed"] and doc["wrong"] == 0
+    assert "Test PASSED" in p.stdout
+
+
 def test_bench_py_rccl_path_under_torchrun_one_rank():
     """bench.py under torchrun with one rank takes the N>1 code path (RCCL process group, MAX over
     ranks, all_gather of per-rank TFLOPS, post-run all-reduce probe) on the real GPU."""
@@ -119,6 +139,9 @@ def test_bench_py_rccl_path_under_torchrun_one_rank():
     assert doc["n_gpus"] == 1 and doc["steps"] == 5 and doc["value"] > 0
     assert doc["allreduce_busbw_gbps"] is not None and len(doc["tflops_per_rank"]) == 1
     assert doc["settle"]["launches"] > 0
+    assert len(doc["allreduce_sweep"]) == 3          # 1, 4, 16 MiB
+    tel = doc["telemetry_per_rank"][0]
+    assert tel is None or "error" in tel or tel["samples"] >= 1
 
 
 def test_node_bringup_rehearsal_on_real_hardware(tmp_path, native):

@@ -106,6 +106,10 @@ def test_bench_py_distributed_contract_on_cpu(world):
     assert doc["config"]["parallelism"] == f"dp{world}" and doc["config"]["global_batch"] == world
     assert len(doc["tflops_per_rank"]) == world
     assert doc["allreduce_busbw_gbps"] is not None
+    sw = doc["allreduce_sweep"]
+    assert [r["bytes"] for r in sw] == [1 << 20, 4 << 20]            # 1 MiB .. top, x4
+    assert doc["allreduce_busbw_gbps"] == pytest.approx(max(r["busbw_gbps"] for r in sw), abs=0.01)
+    assert len(doc["telemetry_per_rank"]) == world                    # None on CPU (no GPU)
     assert doc["value"] == pytest.approx(sum(doc["tflops_per_rank"]), rel=0.6)
 
 
@@ -130,3 +134,61 @@ def test_bench_settle_phase_bounds():
     assert n == len(calls) and n % 4 == 0 and len(syncs) == n // 4
     calls.clear()
     assert bench.settle(step, lambda: None, 1e6, chunk=4, max_launches=12) == 12 == len(calls)
+
+
+def test_rccl_bench_multiprocess_plan_under_torchrun():
+    """rccl-allreduce-bench --mp takes its rank/world/device from torchrun (--no-python) — the
+    launch the gpu-bench Job uses; --plan stops before any HIP call so this runs on CPU."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    import yaml
+
+    repo = Path(__file__).resolve().parent.parent
+    exe = repo / "native/bin/rccl-allreduce-bench"
+    if not exe.exists():
+        from k8s_nvidia_gpus_amd.ops import build as B
+
+        B.build_native(only=["rccl-allreduce-bench"])
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=3", "--master-addr=127.0.0.1", f"--master-port={port}",
+                        "--no-python", str(exe), "--mp", "--plan"],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    plans = sorted((json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")),
+                   key=lambda d: d["rank"])
+    assert [(d["rank"], d["world"], d["device"]) for d in plans] == [(0, 3, 0), (1, 3, 1), (2, 3, 2)]
+    assert len({d["id_file"] for d in plans}) == 1 and str(port) in plans[0]["id_file"]
+    job = yaml.safe_load((repo / "cluster-config/apps/gpu-bench/job-rccl-allreduce.yaml").read_text())
+    c = job["spec"]["template"]["spec"]["containers"][0]
+    assert c["command"][-1] == "torch.distributed.run" and "--no-python" in c["args"] and "--mp" in c["args"]
+    nproc = next(a for a in c["args"] if a.startswith("--nproc-per-node=")).split("=")[1]
+    assert int(nproc) == int(c["resources"]["limits"]["amd.com/gpu"])
+
+
+def test_telemetry_sampler_matches_gpu_by_pci_address():
+    """The sampler picks the amd-smi handle of THIS rank's GPU by BDF, summarises clock / power /
+    hotspot, and degrades to an error record without amd-smi."""
+    import time
+
+    from fakes.amdsmi import FakeAmdSmi
+    from k8s_nvidia_gpus_amd.parallel.telemetry import Sampler
+
+    fake = FakeAmdSmi()
+    bdf = fake.amdsmi_get_gpu_device_bdf(fake.amdsmi_get_processor_handles()[5])
+    with Sampler(bdf, period=0.005, amdsmi_module=fake) as s:
+        time.sleep(0.05)
+    summ = s.summary()
+    assert s.handle is not None and int(s.handle) == 5
+    assert summ["samples"] >= 2 and summ["bdf"] == bdf.lower()
+    assert summ["gfxclk_mhz_mean"] and summ["power_w_mean"] and summ["temp_hotspot_c_max"]
+    missing = Sampler("0000:ff:00.0", amdsmi_module=FakeAmdSmi())
+    with missing:
+        pass
+    assert missing.summary() == {"error": "no amd-smi handle for 0000:ff:00.0"}
