@@ -14,6 +14,9 @@ Ops (all activations are channels-last, i.e. NHWC memory = ``[N, H*W, C]`` token
   80 / 160 (UNet) and 64 (CLIP-free paths); q/k/v may be strided column views of one fused
   projection output.
 * ``geglu(x)`` — ``h * gelu(g)`` for ``x = [h | g]`` (the transformer feed-forward's gate).
+* ``linear(x, w, b)`` — the transformer projections (fused q|k|v, cross k|v, out, GEGLU in / out,
+  the 1×1 proj_in / proj_out convolutions as token GEMMs) on the hand-written 256×128-tile gfx950
+  GEMM (``ops/csrc/gemm_bf16_epi.hip``, fp16 operands, bias in the epilogue).
 """
 from __future__ import annotations
 
@@ -52,6 +55,19 @@ def _sd():
     from k8s_nvidia_gpus_amd.ops import sd_kernels
 
     return sd_kernels
+
+
+# ---------------------------------------------------------------- projections
+_GEMM = os.environ.get("AMDK8S_SD_GEMM", "native")   # native | torch (A/B against hipBLASLt)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if _GEMM != "torch" and _native(x):
+        from k8s_nvidia_gpus_amd.ops import gemm_epi
+
+        if gemm_epi.supported(x, w):
+            return gemm_epi.linear(x, w, b)
+    return F.linear(x, w, b)
 
 
 # ---------------------------------------------------------------- GroupNorm (+SiLU)

@@ -150,17 +150,18 @@ class Attention(nn.Module):
         if self._w_qkv is not None and self._w_qkv.device == x.device \
                 and self._w_qkv.dtype == x.dtype:
             if self.is_cross:
-                q = self.to_q(x)
-                kv = F.linear(context, self._w_qkv, self._b_qkv)
+                q = SF.linear(x, self.to_q.weight, self.to_q.bias)
+                kv = SF.linear(context, self._w_qkv, self._b_qkv)
                 k, v = kv[..., :c], kv[..., c:]
             else:
-                qkv = F.linear(x, self._w_qkv, self._b_qkv)
+                qkv = SF.linear(x, self._w_qkv, self._b_qkv)
                 q, k, v = qkv[..., :c], qkv[..., c:2 * c], qkv[..., 2 * c:]
         else:
             ctx = context if self.is_cross else x
             q, k, v = self.to_q(x), self.to_k(ctx), self.to_v(ctx)
         o = SF.attention(q, k, v, self.heads)
-        return self.to_out[0](o)
+        out = self.to_out[0]
+        return SF.linear(o, out.weight, out.bias)
 
 
 class GEGLU(nn.Module):
@@ -169,7 +170,7 @@ class GEGLU(nn.Module):
         self.proj = nn.Linear(dim, inner * 2)
 
     def forward(self, x):
-        return SF.geglu(self.proj(x))
+        return SF.geglu(SF.linear(x, self.proj.weight, self.proj.bias))
 
 
 class FeedForward(nn.Module):
@@ -179,7 +180,8 @@ class FeedForward(nn.Module):
         self.net = nn.ModuleList([GEGLU(dim, inner), nn.Dropout(0.0), nn.Linear(inner, dim)])
 
     def forward(self, x):
-        return self.net[2](self.net[0](x))
+        out = self.net[2]
+        return SF.linear(self.net[0](x), out.weight, out.bias)
 
 
 class BasicTransformerBlock(nn.Module):
@@ -212,7 +214,7 @@ class Transformer2DModel(nn.Module):
 
     @staticmethod
     def _as_linear(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
-        return F.linear(x, conv.weight.view(conv.out_channels, conv.in_channels), conv.bias)
+        return SF.linear(x, conv.weight.view(conv.out_channels, conv.in_channels), conv.bias)
 
     def forward(self, x, context):
         n, c, h, w = x.shape

@@ -11,9 +11,11 @@ rather than a transcription of the upstream module graph:
 * one fused q|k|v GEMM per self-attention (weights concatenated once, :meth:`WanDiT.fuse`), q/k
   RMSNorm + 3-D RoPE in place on that output (``functional.rmsnorm_rope``), attention reading q/k/v
   as strided column views — no head split/permute copies;
-* the residual stream is one fp32 ``[B, L, C]`` buffer; every residual update is fused with the
-  LayerNorm (+ AdaLN modulation) that follows it (``functional.add_ln``) — 3 kernels of glue per
-  block besides the GEMMs and attention;
+* every projection runs on the hand-written gfx950 GEMM (``ops/csrc/gemm_bf16_epi.hip``) with its
+  epilogue fused: bias everywhere, tanh-GELU on the FFN input, and the gated residual update
+  ``x += gate · (y + b)`` of the o-projections and the FFN output straight from the fp32
+  accumulators into the fp32 ``[B, L, C]`` residual stream; the LayerNorm (+ AdaLN modulation)
+  that follows each update is one row kernel (``functional.add_ln``);
 * cross-attention K/V of the text context are computed ONCE per prompt for all layers
   (:meth:`WanDiT.text_kv`) and reused by every sampling step — the 512-token context never changes
   during denoising;
@@ -89,7 +91,7 @@ class Block(nn.Module):
         w = self.self_attn.q.weight
         if self._wqkv is None or self._wqkv.dtype != w.dtype or self._wqkv.device != w.device:
             self.fuse()
-        return F.linear(h, self._wqkv, self._bqkv)
+        return WF.linear(h, self._wqkv, self._bqkv)
 
 
 class Head(nn.Module):
@@ -158,17 +160,18 @@ class WanDiT(nn.Module):
         b, l, c = context.shape
         if l < self.cfg.text_len:
             context = torch.cat([context, context.new_zeros(b, self.cfg.text_len - l, c)], 1)
-        w = self.text_embedding[0].weight
-        return self.text_embedding(context.to(w.dtype))
+        t0, t2 = self.text_embedding[0], self.text_embedding[2]
+        h = WF.linear_gelu(context.to(t0.weight.dtype), t0.weight, t0.bias)
+        return WF.linear(h, t2.weight, t2.bias)
 
     def text_kv(self, ctx: torch.Tensor) -> List[Tuple[torch.Tensor, torch.Tensor]]:
         """Per-layer cross-attention (K, V) of the embedded context, K already RMS-normalised."""
         out = []
         for blk in self.blocks:
             ca = blk.cross_attn
-            k = ca.k(ctx)
+            k = WF.linear(ctx, ca.k.weight, ca.k.bias)
             WF.rmsnorm_rope(k, ca.norm_k.weight, None, None, self.cfg.heads, self.cfg.eps)
-            out.append((k, ca.v(ctx)))
+            out.append((k, WF.linear(ctx, ca.v.weight, ca.v.bias)))
         return out
 
     # ------------------------------------------------------------------ forward
@@ -188,7 +191,7 @@ class WanDiT(nn.Module):
         cos, sin = self.rope(grid, x.device)
         wdt = self.patch_embedding.weight.dtype
         pw = self.patch_embedding.weight.reshape(cfg.dim, -1)
-        res = F.linear(self.patchify(x.to(wdt)), pw, self.patch_embedding.bias).float()  # fp32 stream
+        res = WF.linear(self.patchify(x.to(wdt)), pw, self.patch_embedding.bias).float()  # fp32 stream
         if sp is not None and sp.world > 1:
             sp.check(res.shape[1], cfg.heads)
             res, cos, sin = sp.shard(res), sp.shard(cos, 0), sp.shard(sin, 0)
@@ -205,30 +208,31 @@ class WanDiT(nn.Module):
         h = WF.add_ln(res, None, None, 1.0 + m[:, 1], m[:, 0], cfg.eps, wdt)
         for i, blk in enumerate(self.blocks):
             m = mods[i]
-            # self-attention
+            # self-attention; x += gate1 · o_proj(attn) fused into the o-projection
             qkv = blk.qkv(h)
             q, k, v = qkv[..., :d], qkv[..., d:2 * d], qkv[..., 2 * d:]
             WF.rmsnorm_rope_qk(qkv, blk.self_attn.norm_q.weight, blk.self_attn.norm_k.weight,
                                cos, sin, cfg.heads, cfg.eps)
-            o = blk.self_attn.o(attend(q, k, v, cfg.heads))
-            h = WF.add_ln(res, o, m[:, 2], blk.norm3.weight.float()[None], blk.norm3.bias.float()[None],
+            so = blk.self_attn.o
+            WF.linear_residual_(res, attend(q, k, v, cfg.heads), so.weight, so.bias, m[:, 2])
+            h = WF.add_ln(res, None, None, blk.norm3.weight.float()[None], blk.norm3.bias.float()[None],
                           cfg.eps, wdt)
-            # cross-attention over the cached text K/V
+            # cross-attention over the cached text K/V; x += o_proj(attn)
             ca = blk.cross_attn
-            qc = ca.q(h)
+            qc = WF.linear(h, ca.q.weight, ca.q.bias)
             WF.rmsnorm_rope(qc, ca.norm_q.weight, None, None, cfg.heads, cfg.eps)
             kc, vc = text_kv[i]
-            o = ca.o(WF.attention(qc, kc, vc, cfg.heads))
-            h = WF.add_ln(res, o, None, 1.0 + m[:, 4], m[:, 3], cfg.eps, wdt)
-            # feed-forward
+            WF.linear_residual_(res, WF.attention(qc, kc, vc, cfg.heads), ca.o.weight, ca.o.bias, None)
+            h = WF.add_ln(res, None, None, 1.0 + m[:, 4], m[:, 3], cfg.eps, wdt)
+            # feed-forward; x += gate2 · ffn(h)
             f = WF.linear_gelu(h, blk.ffn[0].weight, blk.ffn[0].bias)
-            o = blk.ffn[2](f)
+            WF.linear_residual_(res, f, blk.ffn[2].weight, blk.ffn[2].bias, m[:, 5])
             if i + 1 < len(self.blocks):
                 nm = mods[i + 1]
-                h = WF.add_ln(res, o, m[:, 5], 1.0 + nm[:, 1], nm[:, 0], cfg.eps, wdt)
+                h = WF.add_ln(res, None, None, 1.0 + nm[:, 1], nm[:, 0], cfg.eps, wdt)
             else:
                 hm = self.head.modulation.float() + e[:, None, :]      # [B, 2, d]
-                h = WF.add_ln(res, o, m[:, 5], 1.0 + hm[:, 1], hm[:, 0], cfg.eps, wdt)
+                h = WF.add_ln(res, None, None, 1.0 + hm[:, 1], hm[:, 0], cfg.eps, wdt)
         y = self.head.head(h)
         if sp is not None and sp.world > 1:
             y = sp.gather(y)

@@ -59,15 +59,19 @@ def _wk():
 
 # ---------------------------------------------------------------- residual add + LayerNorm
 def add_ln_ref(x: torch.Tensor, y: Optional[torch.Tensor], gate: Optional[torch.Tensor],
-               mul: torch.Tensor, add: torch.Tensor, eps: float) -> torch.Tensor:
-    """Reference of :func:`add_ln`: updates ``x`` (fp32 [B, L, C]) in place, returns bf16/``y``
-    dtype LN output.  ``gate``/``mul``/``add`` are [B, C] or [1, C] fp32."""
+               mul: torch.Tensor, add: torch.Tensor, eps: float,
+               out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """Reference of :func:`add_ln`: updates ``x`` (fp32 [B, L, C]) in place, returns the LN output
+    in ``out_dtype`` (default: bf16, or ``y``'s dtype).  ``gate``/``mul``/``add`` are [B, C] or
+    [1, C] fp32."""
     if y is not None:
         upd = y.float() if gate is None else y.float() * gate.float()[:, None, :]
         x.add_(upd)
     n = F.layer_norm(x.float(), (x.shape[-1],), eps=eps)
     out = n * mul.float()[:, None, :] + add.float()[:, None, :]
-    return out.to(torch.bfloat16 if y is None else y.dtype)
+    if out_dtype is None:
+        out_dtype = torch.bfloat16 if y is None else y.dtype
+    return out.to(out_dtype)
 
 
 def add_ln(x: torch.Tensor, y: Optional[torch.Tensor], gate: Optional[torch.Tensor],
@@ -75,8 +79,7 @@ def add_ln(x: torch.Tensor, y: Optional[torch.Tensor], gate: Optional[torch.Tens
            out_dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
     if _native(x) and _wk().add_ln_supported(x.shape[-1]):
         return _wk().add_ln(x, y, gate, mul, add, eps, out_dtype)
-    out = add_ln_ref(x, y, gate, mul, add, eps)
-    return out.to(out_dtype)
+    return add_ln_ref(x, y, gate, mul, add, eps, out_dtype)
 
 
 # ---------------------------------------------------------------- RMSNorm (+ RoPE), in place
@@ -148,11 +151,44 @@ def gelu_tanh(x: torch.Tensor) -> torch.Tensor:
     return F.gelu(x, approximate="tanh")
 
 
+# ---------------------------------------------------------------- projections (hand-written GEMM)
+def _ge():
+    from k8s_nvidia_gpus_amd.ops import gemm_epi
+
+    return gemm_epi
+
+
+_GEMM = os.environ.get("AMDK8S_WAN_GEMM", "native")   # native | torch (A/B against hipBLASLt)
+
+
+def _gemm_native(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return _GEMM != "torch" and _native(x) and _ge().supported(x, w)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> torch.Tensor:
+    """``x·wᵀ + b``: the gfx950 256×128-tile GEMM (``csrc/gemm_bf16_epi.hip``) on the GPU."""
+    if _gemm_native(x, w):
+        return _ge().linear(x, w, b)
+    return F.linear(x, w, b)
+
+
 def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """``gelu_tanh(x·wᵀ + b)``.  On the GPU the bias and the tanh-GELU run in hipBLASLt's GEMM
-    epilogue (``torch._addmm_activation``): the [B·L, ffn] pre-activation is never written to and
-    re-read from HBM (Wan2.1-1.3B: 2 × 2560 × 8960 bf16 per block, 30 blocks per step)."""
-    if _native(x):
-        y = torch._addmm_activation(b, x.reshape(-1, x.shape[-1]), w.t(), use_gelu=True)
-        return y.view(*x.shape[:-1], w.shape[0])
+    """``gelu_tanh(x·wᵀ + b)``, bias and tanh-GELU in the GEMM's epilogue: the [B·L, ffn]
+    pre-activation is never written to and re-read from HBM (Wan2.1-1.3B: 2 × 2560 × 8960 bf16 per
+    block, 30 blocks per step)."""
+    if _gemm_native(x, w):
+        return _ge().linear_gelu(x, w, b)
     return F.gelu(F.linear(x, w, b), approximate="tanh")
+
+
+def linear_residual_(res: torch.Tensor, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor],
+                     gate: Optional[torch.Tensor]) -> torch.Tensor:
+    """``res += gate · (x·wᵀ + b)`` on the fp32 residual stream, in place (``gate`` [B, C] per
+    sample or None): the projection's output goes straight into the residual from the GEMM's
+    fp32 accumulators instead of a bf16 round trip through HBM."""
+    if _gemm_native(x, w) and res.is_contiguous():
+        return _ge().linear_residual_(res, x, w, b, gate)
+    y = F.linear(x, w, b).float()
+    if gate is not None:
+        y = y * gate.float()[:, None, :]
+    return res.add_(y)

@@ -1,0 +1,356 @@
+// bf16 MFMA GEMM with fused epilogues for the diffusion-transformer / UNet projections (gfx950).
+//
+//   Y = A · Bᵀ (+ bias)            A [M, K] bf16 activations (row-major, lda)
+//                                  B [N, K] bf16 nn.Linear weight (row-major, ldb)
+//   epilogue (fp32 accumulators, one pass, no extra kernel):
+//     EPI_STORE   out[m, n] = bf16(Y)
+//     EPI_GELU    out[m, n] = bf16(gelu_tanh(Y))                      (DiT / text-embedding FFN-in)
+//     EPI_RESID   x[m, n]  += Y · gate[m / rows_per_gate, n]          (fp32 residual stream, in place;
+//                                                                      gate = AdaLN gate or none)
+//
+// The validator GEMMs (gemm_bf16_gfx950*.hip) use 256×256 tiles; the Wan2.1 DiT at the reference
+// defaults (512×320×16 frames → 2×2560 token rows with CFG, generate_wan_t2v.py:305-312) has
+// N = 1536 for four of its six projections, where 256×256 tiles make only 120 workgroups for 256
+// CUs.  This kernel uses 256×128 tiles (240 workgroups there, 1400 for the 8960-wide FFN):
+//
+//   * 512 threads = 8 waves, 4 (M) × 2 (N), each wave a 64×64 output block = 4×4 tiles of
+//     v_mfma_f32_16x16x32_bf16 (weight fragment as the A operand, so a lane's 4 accumulators are 4
+//     consecutive output columns of one row);
+//   * A and B K-tiles (BK = 64) staged HBM→LDS by LDS-DMA (global_load_lds_dwordx4, 6 per thread per
+//     K-tile) into a 3-deep ring of 48 KiB stages: one barrier per K-tile, the DMA of K-tile t+2
+//     issued right after it and retired by a counted `s_waitcnt vmcnt(6)` two iterations later —
+//     the loop never drains the DMA queue;
+//   * XOR-swizzled 128-B LDS rows (16-B chunk c of row r at c ^ ((r >> 1) & 7)), applied to the DMA
+//     SOURCE address (LDS-DMA writes lane-linearly), so every ds_read_b128 fragment read is
+//     conflict-free;
+//   * M / N tails: rows ≥ M (columns ≥ N) are loaded as clamped copies of row M−1 (weight row N−1)
+//     and never stored, so any token count and any N % 8 == 0 runs unpadded (K % 64 == 0);
+//   * bf16 (Wan DiT) or fp16 (the SD1.5 service) operands and output, fp32 accumulation;
+//   * epilogue through the idle LDS ring: fp32 (residual) or bf16 rows staged, then 16-B coalesced
+//     loads/stores of whole rows; bias and tanh-GELU in fp32 registers before the conversion;
+//   * XCD-aware bijective block remap + GROUP_M tile order (neighbouring tiles share A / B panels in
+//     one XCD's L2).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int BM = 256, BN = 128, BK = 64;
+constexpr int NT = 512;
+constexpr int A_STAGE = BM * BK * 2;               // 32 KiB
+constexpr int B_STAGE = BN * BK * 2;               // 16 KiB
+constexpr int STAGE = A_STAGE + B_STAGE;           // 48 KiB
+constexpr int NSTAGE = 3;
+constexpr int RING = NSTAGE * STAGE;               // 144 KiB
+constexpr int CF_STRIDE = BN * 4 + 16;             // fp32 epilogue row (528 B)
+constexpr int CB_STRIDE = BN * 2 + 16;             // bf16 epilogue row (272 B)
+static_assert(BM * CF_STRIDE <= RING, "fp32 epilogue image must fit the ring");
+constexpr int GROUP_M = 8;
+
+enum Epi { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID = 2 };
+
+struct Args {
+  const uint16_t* A;
+  const uint16_t* B;
+  const uint16_t* bias;   // [N] bf16 / fp16 (operand dtype) or null
+  uint16_t* out;          // bf16 / fp16 output (STORE / GELU)
+  float* x;               // fp32 residual stream (RESID)
+  const float* gate;      // [M / rows_per_gate][gate_stride] fp32 or null (RESID)
+  int M, N, K, lda, ldb, ldo, ldx, rows_per_gate, gate_stride;
+};
+
+__device__ __forceinline__ void barrier_raw() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ bf16x8 lds_read16(const char* p) {
+  return *reinterpret_cast<const bf16x8*>(__builtin_assume_aligned(p, 16));
+}
+
+template <bool F16>
+__device__ __forceinline__ f32x4 mfma16(const bf16x8 a, const bf16x8 b, const f32x4 c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <bool F16>
+__device__ __forceinline__ float h2f(uint16_t v) {
+  if constexpr (F16) return (float)__builtin_bit_cast(_Float16, v);
+  else return __uint_as_float((uint32_t)v << 16);
+}
+
+template <bool F16>
+__device__ __forceinline__ uint2 pack4(f32x4 v) {
+  if constexpr (F16) return __builtin_bit_cast(uint2, __builtin_convertvector(v, f16x4));
+  else return __builtin_bit_cast(uint2, __builtin_convertvector(v, bf16x4));
+}
+
+__device__ __forceinline__ float gelu_tanh(float v) {
+  // 0.5 v (1 + tanh(√(2/π)(v + 0.044715 v³))) = v · sigmoid(2u) = v / (1 + exp(−2u))
+  const float u = 0.7978845608028654f * fmaf(0.044715f * v, v * v, v);
+  return v / (1.f + __expf(-2.f * u));
+}
+
+template <int EPI, bool F16>
+__global__ void __launch_bounds__(NT, 1) gemm_bf16_epi_256x128(const Args a) {
+  __shared__ __attribute__((aligned(16))) char lds[RING];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1;  // 0..3: 64-row block
+  const int wn = wave & 1;   // 0..1: 64-column block
+
+  // ---- block → tile: bijective XCD remap, then GROUP_M order ----
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int tiles_n = (a.N + BN - 1) / BN;
+  const int nwg = tiles_m * tiles_n;
+  int wgid;
+  {
+    const int bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int group = wgid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid - group * GROUP_M * tiles_n;
+  const int m0 = (first_m + in_group % gsz) * BM;
+  const int n0 = (in_group / gsz) * BN;
+
+  // ---- LDS-DMA sources: wave-instruction q covers 8 rows; lane → row q*8 + lane/8, physical chunk
+  //      lane%8 holds logical chunk (lane%8) ^ ((row >> 1) & 7) ----
+  const size_t lda_b = (size_t)a.lda * 2, ldb_b = (size_t)a.ldb * 2;
+  const char* a_src[4];
+  const char* b_src[2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = j * 8 + wave, row = q * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    const int grow = min(m0 + row, a.M - 1);     // M tail: clamped rows, never stored
+    a_src[j] = reinterpret_cast<const char*>(a.A) + (size_t)grow * lda_b + c * 16;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int q = j * 8 + wave, row = q * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    const int gn = min(n0 + row, a.N - 1);       // N tail: clamped weight rows, never stored
+    b_src[j] = reinterpret_cast<const char*>(a.B) + (size_t)gn * ldb_b + c * 16;
+  }
+  auto stage = [&](int t) {
+    char* sa = lds + (t % NSTAGE) * STAGE;
+    char* sb = sa + A_STAGE;
+    const size_t kb = (size_t)t * BK * 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(a_src[j] + kb),
+                                       (lds_void*)(sa + (j * 8 + wave) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + kb),
+                                       (lds_void*)(sb + (j * 8 + wave) * 1024), 16, 0, 0);
+  };
+
+  // ---- fragment read offsets: row (lane & 15) of a 16-row block, logical chunk 4·kk + lane/16 ----
+  const int fr = lane & 15, fq = lane >> 4;
+  const int sw = fr >> 1;
+  const int foff0 = fr * 128 + (((0 + fq) ^ sw) << 4);
+  const int foff1 = fr * 128 + (((4 + fq) ^ sw) << 4);
+  const int a_wave = wm * 64 * 128;
+  const int b_wave = wn * 64 * 128;
+
+  f32x4 acc[4][4];   // [m 16-block][n 16-block]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int T = a.K / BK;
+  stage(0);
+  if (T > 1) stage(1);
+  for (int t = 0; t < T; ++t) {
+    if (t + 1 < T) wait_vmcnt<6>(); else wait_vmcnt<0>();
+    barrier_raw();                       // K-tile t landed for every wave; t−1's reads are done
+    if (t + 2 < T) stage(t + 2);         // into the buffer K-tile t−1 used
+    const char* sa = lds + (t % NSTAGE) * STAGE + a_wave;
+    const char* sb = lds + (t % NSTAGE) * STAGE + A_STAGE + b_wave;
+    // all 16 fragment reads of the K-tile up front (64 VGPRs): the second half's reads are in
+    // flight under the first half's 16 MFMAs
+    bf16x8 af[2][4], bw[2][4];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int fo = kk ? foff1 : foff0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bw[kk][j] = lds_read16(sb + j * 2048 + fo);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[kk][i] = lds_read16(sa + i * 2048 + fo);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = mfma16<F16>(bw[kk][j], af[kk][i], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  barrier_raw();                         // every wave is done with the ring: reuse it for C
+
+  // ---- epilogue: lane holds C[m0 + wm·64 + 16i + fr][n0 + wn·64 + 16j + 4fq + 0..3] ----
+  float bias[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias[j][e] = 0.f;
+  if (a.bias) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + 16 * j + 4 * fq;
+      if (n < a.N) {                    // N % 4 == 0: a lane's 4 columns are all in or all out
+        const uint2 bv = *reinterpret_cast<const uint2*>(a.bias + n);
+        bias[j][0] = h2f<F16>((uint16_t)(bv.x & 0xffffu));
+        bias[j][1] = h2f<F16>((uint16_t)(bv.x >> 16));
+        bias[j][2] = h2f<F16>((uint16_t)(bv.y & 0xffffu));
+        bias[j][3] = h2f<F16>((uint16_t)(bv.y >> 16));
+      }
+    }
+  }
+  if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = wm * 64 + 16 * i + fr, n = wn * 64 + 16 * j + 4 * fq;
+        f32x4 v = acc[i][j];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += bias[j][e];
+        *reinterpret_cast<f32x4*>(lds + m * CF_STRIDE + n * 4) = v;
+      }
+    __syncthreads();
+    // 256 rows × 128 fp32: 32 threads per row (16 B each), 16 rows per pass
+#pragma unroll 4
+    for (int it = 0; it < BM / 16; ++it) {
+      const int row = it * 16 + (tid >> 5), col = (tid & 31) * 4;
+      const int gm = m0 + row;
+      if (gm < a.M && n0 + col < a.N) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(lds + row * CF_STRIDE + col * 4);
+        f32x4* xp = reinterpret_cast<f32x4*>(a.x + (size_t)gm * a.ldx + n0 + col);
+        f32x4 xv = *xp;
+        if (a.gate) {
+          const f32x4 g = *reinterpret_cast<const f32x4*>(
+              a.gate + (size_t)(gm / a.rows_per_gate) * a.gate_stride + n0 + col);
+          xv += v * g;
+        } else {
+          xv += v;
+        }
+        *xp = xv;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = wm * 64 + 16 * i + fr, n = wn * 64 + 16 * j + 4 * fq;
+        f32x4 v = acc[i][j];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] += bias[j][e];
+          if constexpr (EPI == EPI_GELU) v[e] = gelu_tanh(v[e]);
+        }
+        *reinterpret_cast<uint2*>(lds + m * CB_STRIDE + n * 2) = pack4<F16>(v);
+      }
+    __syncthreads();
+    // 256 rows × 256 B: 16 threads per row (16 B each), 32 rows per pass
+    char* obase = reinterpret_cast<char*>(a.out) + ((size_t)m0 * a.ldo + n0) * 2;
+    const size_t ldo_b = (size_t)a.ldo * 2;
+#pragma unroll 4
+    for (int it = 0; it < BM / 32; ++it) {
+      const int row = it * 32 + (tid >> 4), ch = tid & 15;
+      if (m0 + row < a.M && n0 + ch * 8 < a.N)
+        *reinterpret_cast<uint4*>(obase + row * ldo_b + ch * 16) =
+            *reinterpret_cast<const uint4*>(lds + row * CB_STRIDE + ch * 16);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Shape contract: N % 8 == 0, K % 64 == 0, lda/ldb/ldo % 8 == 0, ldx % 4 == 0, 16-B aligned
+// operand bases (bias 8-B aligned), gate_stride % 4 == 0; any M ≥ 1.  dtype 1 = bf16, 0 = fp16.
+int amdk8s_gemm_epi_supported(int M, int N, int K) {
+  return M > 0 && N > 0 && K > 0 && N % 8 == 0 && K % BK == 0;
+}
+
+int amdk8s_gemm_epi(int epi, int dtype, const void* A, const void* B, const void* bias, void* out,
+                    float* x, const float* gate, int M, int N, int K, int lda, int ldb, int ldo,
+                    int ldx, int rows_per_gate, int gate_stride, hipStream_t stream) {
+  if (!amdk8s_gemm_epi_supported(M, N, K)) return (int)hipErrorInvalidValue;
+  if (lda % 8 || ldb % 8 || lda < K || ldb < K) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)A | (uintptr_t)B) & 15 || ((uintptr_t)bias & 7)) return (int)hipErrorInvalidValue;
+  if (epi == EPI_RESID) {
+    if (!x || ldx % 4 || ldx < N || ((uintptr_t)x & 15)) return (int)hipErrorInvalidValue;
+    if (gate && (rows_per_gate <= 0 || gate_stride % 4 || ((uintptr_t)gate & 15)))
+      return (int)hipErrorInvalidValue;
+  } else {
+    if (!out || ldo % 8 || ldo < N || ((uintptr_t)out & 15)) return (int)hipErrorInvalidValue;
+  }
+  // 32-bit row offsets inside one panel are never formed; the full extent must stay addressable
+  Args a;
+  a.A = (const uint16_t*)A;
+  a.B = (const uint16_t*)B;
+  a.bias = (const uint16_t*)bias;
+  a.out = (uint16_t*)out;
+  a.x = x;
+  a.gate = gate;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldo = ldo;
+  a.ldx = ldx;
+  a.rows_per_gate = rows_per_gate > 0 ? rows_per_gate : M;
+  a.gate_stride = gate_stride;
+  const long nwg = (long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
+#define AMDK8S_EPI_LAUNCH(E, F)                                                                  \
+  hipLaunchKernelGGL((gemm_bf16_epi_256x128<E, F>), dim3(nwg), dim3(NT), 0, stream, a)
+  const bool f16 = dtype == 0;
+  switch (epi) {
+    case EPI_STORE:
+      if (f16) AMDK8S_EPI_LAUNCH(EPI_STORE, true); else AMDK8S_EPI_LAUNCH(EPI_STORE, false);
+      break;
+    case EPI_GELU:
+      if (f16) AMDK8S_EPI_LAUNCH(EPI_GELU, true); else AMDK8S_EPI_LAUNCH(EPI_GELU, false);
+      break;
+    case EPI_RESID:
+      if (f16) AMDK8S_EPI_LAUNCH(EPI_RESID, true); else AMDK8S_EPI_LAUNCH(EPI_RESID, false);
+      break;
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+#undef AMDK8S_EPI_LAUNCH
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

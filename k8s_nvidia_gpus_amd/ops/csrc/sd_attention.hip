@@ -523,8 +523,9 @@ __global__ __launch_bounds__(256) void attn_fwd_t_kernel(const AttnArgs a) {
   }
 }
 
-// amdk8s_attention_set_variant(): -1 = auto (d = 128 → attn_d128.hip's 32x32x16 kernel, every other
-// head dim → the transposed kernel), 0 = transposed (P in registers), 1 = P via LDS, 2 = attn_d128
+// amdk8s_attention_set_variant(): -1 = auto (head dims 40 / 64 / 80 / 128 / 160 → attn_d128.hip's
+// 32x32x16 kernel, any other → the transposed kernel), 0 = transposed (P in registers),
+// 1 = P via LDS, 2 = the 32x32x16 kernel
 int g_variant = -1;
 
 template <bool BF16, int QK, int DT, int QT, int D>
@@ -580,10 +581,11 @@ int dispatch(const AttnArgs& a, int NH, hipStream_t stream) {
 
 }  // namespace
 
-extern "C" int amdk8s_attention_d128_fwd(const void* q, const void* k, const void* v, void* o, int N,
-                                         int H, int Lq, int Lk, int sqb, int sqr, int skb, int skr,
-                                         int svb, int svr, int sor, float scale, int dtype,
-                                         hipStream_t stream);
+extern "C" int amdk8s_attention_m32_supported(int d);
+extern "C" int amdk8s_attention_m32_fwd(const void* q, const void* k, const void* v, void* o, int N,
+                                        int H, int Lq, int Lk, int d, int sqb, int sqr, int skb,
+                                        int skr, int svb, int svr, int sor, float scale, int dtype,
+                                        hipStream_t stream);
 
 extern "C" {
 
@@ -602,9 +604,9 @@ int amdk8s_attention_fwd(const void* q, const void* k, const void* v, void* o, i
   if (!amdk8s_attention_supported(d, Lq, Lk) || N <= 0 || H <= 0) return -1;
   // 16-byte loads of 8 consecutive elements: every row start must stay 16-byte aligned
   if ((sqr | skr | svr | sqb | skb | svb | sor) % 8 != 0) return -3;
-  if (d == 128 && (g_variant == -1 || g_variant == 2))
-    return amdk8s_attention_d128_fwd(q, k, v, o, N, H, Lq, Lk, sqb, sqr, skb, skr, svb, svr, sor,
-                                     scale, dtype, stream);
+  if ((g_variant == -1 || g_variant == 2) && amdk8s_attention_m32_supported(d))
+    return amdk8s_attention_m32_fwd(q, k, v, o, N, H, Lq, Lk, d, sqb, sqr, skb, skr, svb, svr, sor,
+                                    scale, dtype, stream);
   if ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v)) % 16 != 0)
     return -3;

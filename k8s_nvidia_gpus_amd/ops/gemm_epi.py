@@ -1,0 +1,121 @@
+"""ctypes bindings of the fused-epilogue bf16 GEMM (``csrc/gemm_bf16_epi.hip``).
+
+``linear(x, w, b)`` / ``linear_gelu(x, w, b)`` are ``F.linear`` (+ tanh-GELU) on the hand-written
+256×128-tile gfx950 kernel (bf16 or fp16 operands); ``linear_residual_(res, x, w, b, gate)`` folds the
+DiT's gated residual update ``res += gate · (x·wᵀ + b)`` into the GEMM's epilogue, so the
+projection output never round-trips through HBM in bf16.  Same conventions as the other binding
+modules: raw device pointers, torch's current stream, ``supported(...)`` predicates for what the
+kernel covers (N % 8, K % 64), and no silent fallback once a caller has chosen the kernel.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from typing import Optional
+
+import torch
+
+from .kernels import library
+
+EPI_STORE, EPI_GELU, EPI_RESID = 0, 1, 2
+_declared = False
+_lock = threading.Lock()
+
+
+def _lib():
+    global _declared
+    lib = library()
+    if not _declared:
+        with _lock:
+            vp, ci = ctypes.c_void_p, ctypes.c_int
+            lib.amdk8s_gemm_epi_supported.argtypes = [ci, ci, ci]
+            lib.amdk8s_gemm_epi_supported.restype = ci
+            lib.amdk8s_gemm_epi.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci,
+                                            ci, ci, ci, vp]
+            lib.amdk8s_gemm_epi.restype = ci
+            _declared = True
+    return lib
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _rows(x: torch.Tensor) -> torch.Tensor:
+    """[.., K] → a 2-D [M, K] view with unit inner stride and 16-B aligned rows (copy if needed)."""
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.stride(-1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    return x2
+
+
+_DT = {torch.bfloat16: 1, torch.float16: 0}
+
+
+def supported(x: torch.Tensor, w: torch.Tensor) -> bool:
+    if x.device.type != "cuda" or x.dtype not in _DT or w.dtype != x.dtype:
+        return False
+    n, k = w.shape
+    if x.shape[-1] != k or w.stride(-1) != 1 or w.stride(0) % 8 or w.data_ptr() % 16:
+        return False
+    m = x.numel() // k
+    return m > 0 and bool(_lib().amdk8s_gemm_epi_supported(m, n, k))
+
+
+def _bias(b: Optional[torch.Tensor], n: int, dtype: torch.dtype) -> Optional[torch.Tensor]:
+    if b is None:
+        return None
+    if b.dtype != dtype or not b.is_contiguous() or b.numel() != n or b.data_ptr() % 8:
+        b = b.to(dtype).contiguous().clone()
+    return b
+
+
+def _run(epi, x2, w, b, out, res, gate, rows_per_gate, gate_stride, ldo, ldx):
+    m, k = x2.shape
+    n = w.shape[0]
+    rc = _lib().amdk8s_gemm_epi(
+        epi, _DT[x2.dtype], x2.data_ptr(), w.data_ptr(), b.data_ptr() if b is not None else None,
+        out.data_ptr() if out is not None else None, res.data_ptr() if res is not None else None,
+        gate.data_ptr() if gate is not None else None, m, n, k, x2.stride(0), w.stride(0), ldo, ldx,
+        rows_per_gate, gate_stride, _stream(x2))
+    if rc != 0:
+        raise RuntimeError(f"amdk8s_gemm_epi failed (rc={rc}, M={m} N={n} K={k}, epi={epi})")
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
+           gelu: bool = False) -> torch.Tensor:
+    """``x·wᵀ + b`` (tanh-GELU with ``gelu``) in x's dtype: ``x`` [..., K], ``w`` [N, K]."""
+    x2 = _rows(x)
+    n = w.shape[0]
+    out = torch.empty((x2.shape[0], n), dtype=x.dtype, device=x.device)
+    _run(EPI_GELU if gelu else EPI_STORE, x2, w, _bias(b, n, x.dtype), out, None, None, 0, 0, n, 0)
+    return out.view(*x.shape[:-1], n)
+
+
+def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    return linear(x, w, b, gelu=True)
+
+
+def linear_residual_(res: torch.Tensor, x: torch.Tensor, w: torch.Tensor,
+                     b: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``res += gate · (x·wᵀ + b)`` in place.  ``res`` fp32 [B, L, N] contiguous, ``x`` [B, L, K],
+    ``gate`` fp32 [B, N] (per sample, e.g. an AdaLN gate; any batch stride) or None."""
+    if res.dtype != torch.float32 or not res.is_contiguous():
+        raise TypeError("linear_residual_: res must be a contiguous fp32 tensor")
+    n = w.shape[0]
+    if res.shape[-1] != n or res.numel() != x.numel() // x.shape[-1] * n:
+        raise ValueError(f"residual {tuple(res.shape)} does not match x {tuple(x.shape)} · w {tuple(w.shape)}")
+    x2 = _rows(x)
+    rows_per_gate, gstride = 0, 0
+    if gate is not None:
+        gate = gate.reshape(-1, n)
+        if gate.dtype != torch.float32 or gate.stride(-1) != 1:
+            gate = gate.float().contiguous()
+        if gate.data_ptr() % 16 or (gate.shape[0] > 1 and gate.stride(0) % 4):
+            gate = gate.contiguous()
+        if x2.shape[0] % gate.shape[0]:
+            raise ValueError("rows are not a whole number of gate rows")
+        rows_per_gate = x2.shape[0] // gate.shape[0]
+        gstride = gate.stride(0) if gate.shape[0] > 1 else 0
+    _run(EPI_RESID, x2, w, _bias(b, n, x.dtype), None, res, gate, rows_per_gate, gstride, 0, n)
+    return res

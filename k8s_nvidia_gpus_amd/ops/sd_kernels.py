@@ -171,9 +171,9 @@ def attention_set_qt(qt: int) -> None:
 
 
 def attention_set_variant(v: int) -> None:
-    """-1 = auto (default: head dim 128 → the 32x32x16 kernel of ``csrc/attn_d128.hip``, every other
-    head dim → the transposed-score kernel), 0 = transposed-score kernel (P stays in registers),
-    1 = P staged through LDS, 2 = ``attn_d128`` (d = 128 only)."""
+    """-1 = auto (default: head dims 40 / 64 / 80 / 128 / 160 → the 32x32x16 kernel of
+    ``csrc/attn_d128.hip``, any other → the transposed-score kernel), 0 = transposed-score kernel
+    (P stays in registers), 1 = P staged through LDS, 2 = the 32x32x16 kernel."""
     lib = _lib()
     lib.amdk8s_attention_set_variant.argtypes = [ctypes.c_int]
     lib.amdk8s_attention_set_variant.restype = None
@@ -181,7 +181,7 @@ def attention_set_variant(v: int) -> None:
 
 
 def attention_d128_set_nw(nw: int) -> None:
-    """Waves per workgroup of the d = 128 kernel (0 = heuristic, 4 or 8) — for tuning sweeps."""
+    """Waves per workgroup of the 32x32x16 kernel (0 = heuristic, 4 or 8) — for tuning sweeps."""
     lib = _lib()
     lib.amdk8s_attention_d128_set_nw.argtypes = [ctypes.c_int]
     lib.amdk8s_attention_d128_set_nw.restype = None

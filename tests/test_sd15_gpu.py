@@ -243,11 +243,12 @@ def test_attention_deferred_rescale_branch(SK, dev, growing):
 
 @pytest.mark.parametrize("variant,nw", [(0, 0), (2, 4), (2, 8)])
 @pytest.mark.parametrize("lq,lk", [(333, 1000), (2560, 2560)])
-def test_attention_d128_kernels_agree(SK, dev, variant, nw, lq, lk):
-    """The d = 128 kernels (legacy 16x16x32 transposed kernel, attn_d128 at 4 and 8 waves) against
-    fp32, on fused q|k|v column views with ragged lengths."""
-    g = torch.Generator(device=dev).manual_seed(lq * 7 + lk)
-    heads, d = 4, 128
+@pytest.mark.parametrize("d", [40, 64, 80, 128, 160])
+def test_attention_m32_kernels_agree(SK, dev, variant, nw, lq, lk, d):
+    """Every head dim of the 32x32x16 kernel (4 and 8 waves) and the legacy transposed kernel
+    against fp32, on fused q|k|v column views with ragged lengths."""
+    g = torch.Generator(device=dev).manual_seed(lq * 7 + lk + d)
+    heads = 4
     c = heads * d
     q = torch.randn(2, lq, c, generator=g, device=dev).bfloat16() * 2
     kv = torch.randn(2, lk, 3 * c, generator=g, device=dev).bfloat16()
@@ -260,6 +261,18 @@ def test_attention_d128_kernels_agree(SK, dev, variant, nw, lq, lk):
         SK.attention_set_variant(-1)
         SK.attention_d128_set_nw(0)
     torch.testing.assert_close(o.float(), _attn_ref(q, k, v, heads, d ** -0.5), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("d", [40, 80, 160])
+def test_attention_m32_fp16_sd_shapes(SK, dev, d):
+    """fp16 (the SD1.5 service's dtype) through the 32x32x16 kernel at the UNet head dims."""
+    g = torch.Generator(device=dev).manual_seed(d)
+    heads, lq = 8, {40: 4096, 80: 1024, 160: 256}[d]
+    qkv = torch.randn(2, lq, 3 * heads * d, generator=g, device=dev).half()
+    c = heads * d
+    q, k, v = qkv[..., :c] * 2, qkv[..., c:2 * c], qkv[..., 2 * c:]
+    o = SK.attention(q, k, v, heads, d ** -0.5)
+    torch.testing.assert_close(o.float(), _attn_ref(q, k, v, heads, d ** -0.5), rtol=6e-3, atol=6e-3)
 
 
 @pytest.mark.parametrize("growing", [True, False])

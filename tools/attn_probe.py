@@ -22,6 +22,7 @@ SHAPES = {  # name: (N, heads, Lq, Lk, d)
     "wan_long": (2, 12, 32760, 32760, 128),
     "sd_64x64": (2, 8, 4096, 4096, 40),
     "sd_32x32": (2, 8, 1024, 1024, 80),
+    "sd_16x16": (2, 8, 256, 256, 160),
 }
 res = {}
 for name, (n, h, lq, lk, d) in SHAPES.items():
@@ -40,7 +41,7 @@ for name, (n, h, lq, lk, d) in SHAPES.items():
     combos = []
     for vv in VARIANTS:
         if vv == 2:
-            combos += [(2, nw) for nw in (4, 8)] if d == 128 else []
+            combos += [(2, nw) for nw in (4, 8)]
         else:
             combos += [(vv, qq) for qq in (QTS or ((1, 2, 4) if d == 128 else (1, 2)))]
     for var, qt in combos:
