@@ -190,25 +190,32 @@ __global__ void __launch_bounds__(NT, 1) gemm_bf16_epi_256x128(const Args a) {
     if (t + 2 < T) stage(t + 2);         // into the buffer K-tile t−1 used
     const char* sa = lds + (t % NSTAGE) * STAGE + a_wave;
     const char* sb = lds + (t % NSTAGE) * STAGE + A_STAGE + b_wave;
-    // all 16 fragment reads of the K-tile up front (64 VGPRs): the second half's reads are in
-    // flight under the first half's 16 MFMAs
+    // the first half's 8 fragment reads, then the second half's 8 issued between the first half's
+    // MFMAs (explicit order, pinned by sched_barrier: the reads' latency hides under MFMAs)
     bf16x8 af[2][4], bw[2][4];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int fo = kk ? foff1 : foff0;
+    for (int j = 0; j < 4; ++j) bw[0][j] = lds_read16(sb + j * 2048 + foff0);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bw[kk][j] = lds_read16(sb + j * 2048 + fo);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[kk][i] = lds_read16(sa + i * 2048 + fo);
-    }
+    for (int i = 0; i < 4; ++i) af[0][i] = lds_read16(sa + i * 2048 + foff0);
+    __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int j = 0; j < 4; ++j) acc[0][j] = mfma16<F16>(bw[0][j], af[0][0], acc[0][j]);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) bw[1][j] = lds_read16(sb + j * 2048 + foff1);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = mfma16<F16>(bw[kk][j], af[kk][i], acc[i][j]);
+    for (int i = 0; i < 4; ++i) af[1][i] = lds_read16(sa + i * 2048 + foff1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16<F16>(bw[0][j], af[0][i], acc[i][j]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16<F16>(bw[1][j], af[1][i], acc[i][j]);
     __builtin_amdgcn_s_setprio(0);
   }
   barrier_raw();                         // every wave is done with the ring: reuse it for C

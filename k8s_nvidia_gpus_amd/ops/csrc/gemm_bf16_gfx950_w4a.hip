@@ -16,6 +16,11 @@
 //
 // Shape contract (host-checked): M % 256 == 0, N % 256 == 0, K % 64 == 0, lda/ldb/ldc % 8 == 0,
 // 16-B aligned base pointers, 256·lda·2 and 256·ldb·2 < 2³¹ (32-bit panel offsets).
+//
+// Epilogue variants (amdk8s_gemm_bf16_nt_w4a_epi, the DiT / UNet projections): any M — the last
+// row panel's buffer descriptor covers only its valid rows, so the DMA reads zeros past M and those
+// rows are not stored — and the 16-B store pass adds a bf16 bias and optionally applies tanh-GELU
+// to each bf16 C value (fp32 maths on the bf16-rounded product).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -45,11 +50,19 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 // (v_mfma_f32_16x16x32_f16, fp16 C) — same fragment layout, LDS image and cycles as bf16.
 constexpr int kF16 = 16;
 
-template <int SCHED>
+constexpr int kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2;
+
+__device__ __forceinline__ float w4a_gelu_tanh(float v) {
+  const float u = 0.7978845608028654f * fmaf(0.044715f * v, v * v, v);
+  return v / (1.f + __expf(-2.f * u));
+}
+
+template <int SCHED, int EPI = kEpiNone>
 __global__ void __launch_bounds__(NT, 1)
 amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                 uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
-                                int ldc, int order, int nt_store) {
+                                int ldc, int order, int nt_store,
+                                const uint16_t* __restrict__ bias = nullptr) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
 
   const int tid = threadIdx.x;
@@ -59,7 +72,7 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
   const int wc = wave & 1;   // B half
 
   // ---- block → tile: per-partition XCD corners of super-blocks, or GROUP_M order (tile_order.h) ----
-  const int tiles_m = M / BM;
+  const int tiles_m = (M + BM - 1) / BM;
   const int tiles_n = N / BN;
   const int nwg = tiles_m * tiles_n;
   const int bid = blockIdx.x;
@@ -92,7 +105,8 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
   const uint64_t b_addr = (uint64_t)(uintptr_t)B + (uint64_t)n0 * ldb_b;
   const uint32_t a_lo = (uint32_t)a_addr, a_hi = (uint32_t)(a_addr >> 32);
   const uint32_t b_lo = (uint32_t)b_addr, b_hi = (uint32_t)(b_addr >> 32);
-  const uint32_t nrec_a = 256u * lda_b, nrec_b = 256u * ldb_b;
+  // the last row panel's descriptor ends at row M: the DMA reads zeros past it (M tail)
+  const uint32_t nrec_a = (uint32_t)min(BM, M - m0) * lda_b, nrec_b = 256u * ldb_b;
   const int T = K / BK;
 
 #define AMDK8S_W4A_OPERANDS                                                                \
@@ -111,11 +125,35 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
   // ---- 16-B coalesced stores of the 256×256 bf16 tile ----
   char* cbase_g = reinterpret_cast<char*>(C) + ((size_t)m0 * ldc + n0) * 2;
   const size_t ldc_b = (size_t)ldc * 2;
+  float bv[8];
+  if constexpr (EPI != kEpiNone) {   // this thread's 8 columns are the same in every row it stores
+    const u32x4 braw = *reinterpret_cast<const u32x4*>(bias + n0 + (tid & 31) * 8);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bv[2 * e] = __uint_as_float(braw[e] << 16);
+      bv[2 * e + 1] = __uint_as_float(braw[e] & 0xffff0000u);
+    }
+  }
+  const int rows_valid = min(BM, M - m0);
 #pragma unroll 4
   for (int it = 0; it < BM * BN * 2 / (NT * 16); ++it) {
     const int row = it * 8 + (tid >> 5);
     const int ch = tid & 31;
-    const u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * C_STRIDE + ch * 16);
+    u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * C_STRIDE + ch * 16);
+    if (row >= rows_valid) continue;
+    if constexpr (EPI != kEpiNone) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float lo = __uint_as_float(v[e] << 16) + bv[2 * e];
+        float hi = __uint_as_float(v[e] & 0xffff0000u) + bv[2 * e + 1];
+        if constexpr (EPI == kEpiBiasGelu) {
+          lo = w4a_gelu_tanh(lo);
+          hi = w4a_gelu_tanh(hi);
+        }
+        const __attribute__((ext_vector_type(2))) __bf16 p = {(__bf16)lo, (__bf16)hi};
+        v[e] = __builtin_bit_cast(uint32_t, p);
+      }
+    }
     u32x4* dst = reinterpret_cast<u32x4*>(cbase_g + row * ldc_b + ch * 16);
     if (nt_store)  // C streams out (nt: no L2/MALL retention) — the caches stay with A and B
       asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(dst), "v"(v) : "memory");
@@ -166,6 +204,36 @@ int launch_w4a(const void* A, const void* B, void* C, int M, int N, int K, int l
   return (int)hipGetLastError();
 }
 }  // namespace
+
+// Any M >= 1 (N % 256 == 0, K % 64 == 0); epi 0 = plain, 1 = + bias, 2 = gelu_tanh(+ bias).
+extern "C" int amdk8s_gemm_bf16_nt_w4a_epi(const void* A, const void* B, void* C, const void* bias,
+                                           int epi, int M, int N, int K, int lda, int ldb, int ldc,
+                                           hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || N % BN || K % BK) return (int)hipErrorInvalidValue;
+  if (lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)bias) & 15)
+    return (int)hipErrorInvalidValue;
+  if (epi != kEpiNone && !bias) return (int)hipErrorInvalidValue;
+  if (256ull * (unsigned long long)(lda > ldb ? lda : ldb) * 2 >= (1ull << 31))
+    return (int)hipErrorInvalidValue;
+  const int tm = (M + BM - 1) / BM, tn = N / BN;
+  const int sb = amdk8s::tile_order_arg(tm, tn);
+  const uint16_t* a = (const uint16_t*)A;
+  const uint16_t* b = (const uint16_t*)B;
+  const uint16_t* bs = (const uint16_t*)bias;
+  uint16_t* c = (uint16_t*)C;
+  constexpr int S = AMDK8S_W4A_DEFAULT_SCHEDULE;
+  if (epi == kEpiBias)
+    hipLaunchKernelGGL((amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiBias>), dim3(tm * tn), dim3(NT), 0,
+                       stream, a, b, c, M, N, K, lda, ldb, ldc, sb, 0, bs);
+  else if (epi == kEpiBiasGelu)
+    hipLaunchKernelGGL((amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiBiasGelu>), dim3(tm * tn), dim3(NT),
+                       0, stream, a, b, c, M, N, K, lda, ldb, ldc, sb, 0, bs);
+  else
+    hipLaunchKernelGGL((amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiNone>), dim3(tm * tn), dim3(NT), 0,
+                       stream, a, b, c, M, N, K, lda, ldb, ldc, sb, 0, bs);
+  return (int)hipGetLastError();
+}
 
 extern "C" int amdk8s_gemm_bf16_nt_w4a(const void* A, const void* B, void* C, int M, int N, int K,
                                        int lda, int ldb, int ldc, hipStream_t stream) {

@@ -604,7 +604,12 @@ int amdk8s_attention_fwd(const void* q, const void* k, const void* v, void* o, i
   if (!amdk8s_attention_supported(d, Lq, Lk) || N <= 0 || H <= 0) return -1;
   // 16-byte loads of 8 consecutive elements: every row start must stay 16-byte aligned
   if ((sqr | skr | svr | sqb | skb | svb | sor) % 8 != 0) return -3;
-  if ((g_variant == -1 || g_variant == 2) && amdk8s_attention_m32_supported(d))
+  // auto: the 32x32x16 kernel wherever its 128-row workgroups still fill the chip; tiny problems
+  // (SD1.5 16² latents: 256 tokens) keep the 64-row legacy kernel (10.6 vs 16.2 us at d = 160,
+  // profiles/r03/b/attn_probe.log)
+  const bool m32 = g_variant == 2 ||
+                   (g_variant == -1 && (long)((Lq + 127) / 128) * N * H >= 128);
+  if (m32 && amdk8s_attention_m32_supported(d))
     return amdk8s_attention_m32_fwd(q, k, v, o, N, H, Lq, Lk, d, sqb, sqr, skb, skr, svb, svr, sor,
                                     scale, dtype, stream);
   if ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |

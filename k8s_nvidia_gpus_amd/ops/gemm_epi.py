@@ -10,6 +10,7 @@ kernel covers (N % 8, K % 64), and no silent fallback once a caller has chosen t
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from typing import Optional
 
@@ -33,6 +34,8 @@ def _lib():
             lib.amdk8s_gemm_epi.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci,
                                             ci, ci, ci, vp]
             lib.amdk8s_gemm_epi.restype = ci
+            lib.amdk8s_gemm_bf16_nt_w4a_epi.argtypes = [vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, vp]
+            lib.amdk8s_gemm_bf16_nt_w4a_epi.restype = ci
             _declared = True
     return lib
 
@@ -82,13 +85,43 @@ def _run(epi, x2, w, b, out, res, gate, rows_per_gate, gate_stride, ldo, ldx):
         raise RuntimeError(f"amdk8s_gemm_epi failed (rc={rc}, M={m} N={n} K={k}, epi={epi})")
 
 
+# Wide bf16 projections (N % 256 == 0, enough 256×256 tiles to fill the chip) run on the
+# validator's 256x256 kernel (w4a: generated-assembly K-loop) with its bias / GELU store epilogue;
+# everything else on the 256×128 kernel.  AMDK8S_GEMM_WIDE=epi forces the latter (A/B runs).
+_WIDE = os.environ.get("AMDK8S_GEMM_WIDE", "w4a")
+
+
+def use_w4a(m: int, n: int, k: int, dtype: torch.dtype) -> bool:
+    return (_WIDE == "w4a" and dtype == torch.bfloat16 and n % 256 == 0 and k % 64 == 0
+            and ((m + 255) // 256) * (n // 256) >= 256)
+
+
+def _w4a(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu: bool,
+         out: torch.Tensor) -> None:
+    m, k = x2.shape
+    n = w.shape[0]
+    if b is None:
+        b = torch.zeros(n, dtype=torch.bfloat16, device=x2.device) if gelu else None
+    epi = 0 if b is None else (2 if gelu else 1)
+    rc = _lib().amdk8s_gemm_bf16_nt_w4a_epi(x2.data_ptr(), w.data_ptr(), out.data_ptr(),
+                                            b.data_ptr() if b is not None else None, epi, m, n, k,
+                                            x2.stride(0), w.stride(0), out.stride(0), _stream(x2))
+    if rc != 0:
+        raise RuntimeError(f"amdk8s_gemm_bf16_nt_w4a_epi failed (rc={rc}, M={m} N={n} K={k})")
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
            gelu: bool = False) -> torch.Tensor:
     """``x·wᵀ + b`` (tanh-GELU with ``gelu``) in x's dtype: ``x`` [..., K], ``w`` [N, K]."""
     x2 = _rows(x)
     n = w.shape[0]
     out = torch.empty((x2.shape[0], n), dtype=x.dtype, device=x.device)
-    _run(EPI_GELU if gelu else EPI_STORE, x2, w, _bias(b, n, x.dtype), out, None, None, 0, 0, n, 0)
+    bb = _bias(b, n, x.dtype)
+    if use_w4a(x2.shape[0], n, x2.shape[1], x.dtype) and w.data_ptr() % 16 == 0 \
+            and (bb is None or bb.data_ptr() % 16 == 0):
+        _w4a(x2, w, bb, gelu, out)
+    else:
+        _run(EPI_GELU if gelu else EPI_STORE, x2, w, bb, out, None, None, 0, 0, n, 0)
     return out.view(*x.shape[:-1], n)
 
 

@@ -75,3 +75,25 @@ def test_strided_input_rows(GE):
     x = big[:, 1536:3072]
     w = (torch.randn(1536, 1536, device=dev) / 40).bfloat16()
     torch.testing.assert_close(GE.linear(x, w).float(), _ref(x, w, None), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("m", [5120, 5000, 65520])
+@pytest.mark.parametrize("gelu", [False, True])
+def test_wide_projection_on_w4a(GE, m, gelu):
+    """Wide bf16 projections take the 256x256 w4a kernel (bias / GELU store epilogue, M tail)."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(m)
+    n, k = 4608, 1536
+    assert GE.use_w4a(m, n, k, torch.bfloat16)
+    x = torch.randn(m, k, generator=g, device=dev).bfloat16()
+    w = (torch.randn(n, k, generator=g, device=dev) / 40).bfloat16()
+    b = torch.randn(n, generator=g, device=dev).bfloat16()
+    y = GE.linear(x, w, b, gelu=gelu)
+    ref = _ref(x, w, b)
+    if gelu:
+        ref = F.gelu(ref, approximate="tanh")
+    torch.testing.assert_close(y.float(), ref, rtol=3e-2, atol=3e-2)
+    # w4a wrote only rows < M: the row after the output is untouched
+    big = torch.full((m + 256, n), 7.0, device=dev).bfloat16()
+    GE._w4a(x, w, b, gelu, big[:m])
+    assert bool((big[m:] == 7.0).all())

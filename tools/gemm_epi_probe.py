@@ -11,6 +11,7 @@ import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
 from k8s_nvidia_gpus_amd.ops import gemm_epi as GE  # noqa: E402
+from k8s_nvidia_gpus_amd.ops import kernels as K  # noqa: E402
 
 dev = torch.device("cuda", 0)
 ITERS = int(os.environ.get("ITERS", "50"))
@@ -28,7 +29,7 @@ def bench(fn, iters=ITERS):
 
 
 res = {}
-for tokens in [int(t) for t in os.environ.get("TOKENS", "2560,32760").split(",")]:
+for tokens in [int(t) for t in os.environ.get("TOKENS", "2560,32768").split(",")]:
     M = 2 * tokens
     for name, n, k in [("qkv", 4608, 1536), ("o", 1536, 1536), ("ffn0", 8960, 1536), ("ffn2", 1536, 8960)]:
         x = torch.randn(M, k, device=dev).bfloat16()
@@ -50,9 +51,13 @@ for tokens in [int(t) for t in os.environ.get("TOKENS", "2560,32760").split(",")
         else:
             row["ours_us"] = bench(lambda: GE.linear(x, w, b))
             row["torch_us"] = bench(lambda: F.linear(x, w, b))
+        if M % 256 == 0 and n % 256 == 0:          # the validator's 256x256 w4a kernel, plain store
+            row["w4a_us"] = bench(lambda: K.gemm_bf16_nt(x, w))
         for key in list(row):
             row[key] = round(row[key], 1)
         row["ours_tflops"] = round(fl / row["ours_us"] / 1e6, 1)
+        if "w4a_us" in row:
+            row["w4a_tflops"] = round(fl / row["w4a_us"] / 1e6, 1)
         row["torch_tflops"] = round(fl / row["torch_us"] / 1e6, 1)
         res[f"{tokens}_{name}"] = row
         print(tokens, name, row, flush=True)

@@ -11,10 +11,25 @@ import sqlite3
 import sys
 
 
-def summarize(db_path: str, window_ms: float = 0.0, per: int = 1, top: int = 30) -> str:
+def last_gap_start(db, gap_ms: float) -> int:
+    """Start time of the first dispatch after the LAST idle gap longer than ``gap_ms`` (a benchmark
+    sleeps before its steady-state loop, so everything after the gap is steady state)."""
+    rows = db.execute("select start, end from kernels order by start").fetchall()
+    cut, prev_end = rows[0][0], None
+    for st, en in rows:
+        if prev_end is not None and st - prev_end > gap_ms * 1e6:
+            cut = st
+        prev_end = en if prev_end is None else max(prev_end, en)
+    return cut
+
+
+def summarize(db_path: str, window_ms: float = 0.0, per: int = 1, top: int = 30,
+              after_gap_ms: float = 0.0) -> str:
     db = sqlite3.connect(db_path)
     emax = db.execute("select max(end) from kernels").fetchone()[0]
     where = f"where start > {emax - window_ms * 1e6}" if window_ms > 0 else ""
+    if after_gap_ms > 0:
+        where = f"where start >= {last_gap_start(db, after_gap_ms)}"
     tot_ns, count, span = db.execute(
         f"select sum(end-start), count(*), max(end)-min(start) from kernels {where}").fetchone()
     rows = db.execute(
@@ -36,8 +51,10 @@ def main(argv=None) -> int:
     ap.add_argument("--window-ms", type=float, default=0.0)
     ap.add_argument("--per", type=int, default=1, help="iterations inside the window")
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--after-gap-ms", type=float, default=0.0,
+                    help="only dispatches after the last idle gap longer than this (steady state)")
     a = ap.parse_args(argv)
-    print(summarize(a.db, a.window_ms, a.per, a.top))
+    print(summarize(a.db, a.window_ms, a.per, a.top, a.after_gap_ms))
     return 0
 
 
