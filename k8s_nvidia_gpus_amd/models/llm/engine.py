@@ -325,23 +325,11 @@ class Engine:
 
 def sample(logits: torch.Tensor, temperature: float = 0.0, top_k: int = 0, top_p: float = 1.0,
            generator: Optional[torch.Generator] = None) -> int:
-    """Greedy at temperature 0; otherwise temperature / top-k / top-p (nucleus) sampling."""
-    if temperature <= 0.0:
-        return int(torch.argmax(logits).item())
-    x = logits.float() / temperature
-    if top_k and top_k > 0:
-        kth = torch.topk(x, min(top_k, x.numel())).values[-1]
-        x = torch.where(x < kth, torch.full_like(x, -float("inf")), x)
-    if top_p < 1.0:
-        sx, idx = torch.sort(x, descending=True)
-        cp = torch.softmax(sx, -1).cumsum(-1)
-        drop = cp - torch.softmax(sx, -1) > top_p
-        sx = sx.masked_fill(drop, -float("inf"))
-        x = torch.full_like(x, -float("inf")).scatter(0, idx, sx)
-    p = torch.softmax(x, -1)
-    if generator is not None and generator.device != p.device:
-        p = p.to(generator.device)
-    return int(torch.multinomial(p, 1, generator=generator).item())
+    """Greedy at temperature 0; otherwise top-k / top-p then temperature (``sampling.py`` has the
+    full llama-server parameter set)."""
+    from .sampling import SamplingParams, sample_token
+
+    return sample_token(logits, SamplingParams(temperature, top_k, top_p), (), generator)
 
 
 def generate(engine: Engine, prompt: Sequence[int], max_new: int, slot: int = 0,

@@ -1,0 +1,115 @@
+"""Token sampling with llama-server's request parameters.
+
+The reference's LLM pod is upstream ``llama-server`` (reference cluster-config/apps/llm/
+deployment.yaml:61,76-84); its clients may send, besides temperature / top_k / top_p:
+``min_p``, ``repeat_penalty`` + ``repeat_last_n``, ``presence_penalty``, ``frequency_penalty`` and
+``logit_bias``.  This module applies them in llama.cpp's default sampler-chain order:
+
+    logit bias → penalties → top-k → top-p → min-p → temperature → draw
+
+(penalties count the last ``repeat_last_n`` tokens of prompt + generation, like llama.cpp's
+sampler, which is fed the prompt tokens too).  ``temperature <= 0`` is greedy over the biased and
+penalised logits.  All maths is one fp32 vector of the vocabulary on the logits' device; only the
+drawn token id crosses to the host.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Any, Dict, Mapping, Optional, Sequence
+
+import torch
+
+
+@dataclass
+class SamplingParams:
+    temperature: float = 0.0
+    top_k: int = 0
+    top_p: float = 1.0
+    min_p: float = 0.0
+    repeat_penalty: float = 1.0
+    repeat_last_n: int = 64
+    presence_penalty: float = 0.0
+    frequency_penalty: float = 0.0
+    logit_bias: Dict[int, float] = field(default_factory=dict)
+
+    @property
+    def penalised(self) -> bool:
+        return self.repeat_last_n != 0 and (self.repeat_penalty != 1.0 or self.presence_penalty != 0.0
+                                            or self.frequency_penalty != 0.0)
+
+    @property
+    def plain_greedy(self) -> bool:
+        """argmax of the raw logits (the batched fast path applies)."""
+        return self.temperature <= 0.0 and not self.penalised and not self.logit_bias
+
+    @classmethod
+    def from_request(cls, body: Mapping[str, Any], vocab: Optional[int] = None) -> "SamplingParams":
+        """llama-server / OpenAI request fields → params (llama-server's defaults)."""
+        def num(key, default, cast=float):
+            v = body.get(key)
+            return default if v is None else cast(v)
+
+        return cls(temperature=num("temperature", 0.8), top_k=num("top_k", 40, int),
+                   top_p=num("top_p", 0.95), min_p=num("min_p", 0.05),
+                   repeat_penalty=num("repeat_penalty", 1.0),
+                   repeat_last_n=num("repeat_last_n", 64, int),
+                   presence_penalty=num("presence_penalty", 0.0),
+                   frequency_penalty=num("frequency_penalty", 0.0),
+                   logit_bias=parse_logit_bias(body.get("logit_bias"), vocab))
+
+
+def parse_logit_bias(raw, vocab: Optional[int] = None) -> Dict[int, float]:
+    """OpenAI form ``{"123": -5}`` or llama.cpp form ``[[123, -5], [456, false]]`` (false = ban)."""
+    if not raw:
+        return {}
+    items = raw.items() if isinstance(raw, Mapping) else raw
+    out: Dict[int, float] = {}
+    for entry in items:
+        if not isinstance(entry, (list, tuple)) or len(entry) != 2:
+            raise ValueError(f"logit_bias entry {entry!r}: expected [token, bias]")
+        tok, b = int(entry[0]), entry[1]
+        if vocab is not None and not 0 <= tok < vocab:
+            raise ValueError(f"logit_bias token {tok} outside the vocabulary ({vocab})")
+        out[tok] = -float("inf") if b is False else float(b)
+    return out
+
+
+def _penalise(x: torch.Tensor, p: SamplingParams, history: Sequence[int]) -> torch.Tensor:
+    n = len(history) if p.repeat_last_n < 0 else min(p.repeat_last_n, len(history))
+    if n == 0:
+        return x
+    recent = torch.tensor(list(history[len(history) - n:]), dtype=torch.long, device=x.device)
+    counts = torch.zeros_like(x).index_add_(0, recent, torch.ones(n, dtype=x.dtype, device=x.device))
+    seen = counts > 0
+    if p.repeat_penalty != 1.0:
+        x = torch.where(seen, torch.where(x > 0, x / p.repeat_penalty, x * p.repeat_penalty), x)
+    return x - counts * p.frequency_penalty - seen.to(x.dtype) * p.presence_penalty
+
+
+def sample_token(logits: torch.Tensor, p: SamplingParams, history: Sequence[int] = (),
+                 generator: Optional[torch.Generator] = None) -> int:
+    """One token from fp logits [vocab] under ``p``; ``history`` = prompt + generated ids."""
+    if p.plain_greedy:
+        return int(torch.argmax(logits).item())
+    x = logits.float().clone()
+    for tok, b in p.logit_bias.items():
+        x[tok] += b
+    if p.penalised:
+        x = _penalise(x, p, history)
+    if p.temperature <= 0.0:
+        return int(torch.argmax(x).item())
+    if p.top_k and p.top_k > 0:
+        kth = torch.topk(x, min(p.top_k, x.numel())).values[-1]
+        x = x.masked_fill(x < kth, -float("inf"))
+    if p.top_p < 1.0:
+        sx, idx = torch.sort(x, descending=True)
+        pr = torch.softmax(sx, -1)
+        drop = pr.cumsum(-1) - pr > p.top_p       # keep the smallest prefix reaching top_p
+        x = torch.full_like(x, -float("inf")).scatter(0, idx, sx.masked_fill(drop, -float("inf")))
+    if p.min_p > 0.0:
+        # keep tokens whose probability is >= min_p x the most likely one's (before temperature)
+        x = x.masked_fill(x < x.max() + torch.log(torch.tensor(p.min_p)), -float("inf"))
+    probs = torch.softmax(x / p.temperature, -1)
+    if generator is not None and generator.device != probs.device:
+        probs = probs.to(generator.device)
+    return int(torch.multinomial(probs, 1, generator=generator).item())

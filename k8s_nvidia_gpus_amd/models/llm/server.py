@@ -7,11 +7,14 @@ the same command line (``-m``, ``--ctx-size``, ``--n-gpu-layers`` / ``--threads`
 layer is on the GPU) and serves the endpoints clients of that pod use:
 
 * ``GET /health`` (503 while the model loads, like llama-server), ``GET /v1/models``;
-* ``POST /completion`` (llama.cpp native: ``prompt``, ``n_predict``, ``temperature``, ``top_k``,
-  ``top_p``, ``seed``, ``stop``, ``stream``) with llama.cpp's ``timings`` block;
+* ``POST /completion`` (llama.cpp native: ``prompt``, ``n_predict``, ``seed``, ``stop``,
+  ``stream``, ``cache_prompt`` and the sampler fields of ``sampling.py`` — temperature, top_k,
+  top_p, min_p, repeat_penalty / repeat_last_n, presence / frequency penalty, logit_bias) with
+  llama.cpp's ``timings`` block;
 * ``POST /v1/completions`` and ``POST /v1/chat/completions`` (OpenAI; ChatML prompt format of
   Qwen2.5-Instruct; ``stream`` as server-sent events);
-* ``POST /tokenize``, ``POST /detokenize``, ``GET /metrics`` (Prometheus text).
+* ``POST /tokenize``, ``POST /detokenize``, ``GET /props``, ``GET /slots``, ``GET /metrics``
+  (Prometheus text).
 
 One scheduler thread owns the GPU: new requests are prefilled into free KV-cache slots, then every
 active sequence advances by one token per decode step — up to 4 sequences share each pass over
@@ -20,6 +23,10 @@ driven from two threads (the reference's SD15 app had that hazard, SURVEY.md §3
 whose client goes away (stream closed, or the connection dropped while a blocking request waits)
 is cancelled and frees its KV slot at the next decode step; a request whose prefill or first
 sample fails gets that error, and no handler waits longer than ``--timeout`` seconds.
+
+Prompt caching (llama-server's ``cache_prompt``, on by default): every slot remembers which tokens
+its KV cache holds; a new request goes to the free slot sharing the longest prefix with its
+prompt, and only the rest of the prompt is prefilled (multi-turn chats re-send the whole history).
 """
 from __future__ import annotations
 
@@ -37,7 +44,8 @@ from typing import Any, Dict, Iterator, List, Optional
 
 import torch
 
-from .engine import Engine, sample
+from .engine import Engine
+from .sampling import SamplingParams, sample_token
 from .tokenizer import Tokenizer, chatml
 
 try:   # module level: FastAPI resolves the handlers' (postponed) annotations in this namespace
@@ -50,10 +58,9 @@ except ImportError:  # pragma: no cover - the engine/scheduler work without the 
 class Job:
     ids: List[int]
     max_new: int
-    temperature: float = 0.0
-    top_k: int = 0
-    top_p: float = 1.0
+    params: SamplingParams = field(default_factory=SamplingParams)
     seed: Optional[int] = None
+    cache_prompt: bool = True
     stop: List[str] = field(default_factory=list)
     out: "queue.Queue" = field(default_factory=queue.Queue)
     # scheduler state
@@ -69,6 +76,15 @@ class Job:
     t_prefill: float = 0.0
     finish: str = ""
     cancelled: bool = False
+    n_cached: int = 0          # prompt tokens whose KV was reused from the slot
+
+
+def common_prefix(a: List[int], b: List[int]) -> int:
+    n = min(len(a), len(b))
+    i = 0
+    while i < n and a[i] == b[i]:
+        i += 1
+    return i
 
 
 class Scheduler:
@@ -80,10 +96,12 @@ class Scheduler:
         self.parallel = max(1, min(parallel, engine.slots))
         self.pending: "queue.Queue[Job]" = queue.Queue()
         self.active: Dict[int, Job] = {}
+        self.slot_tokens: Dict[int, List[int]] = {}      # tokens whose KV each slot holds
         self.stop_ids = set(tok.stop_ids())
         self.metrics = {"requests_total": 0, "prompt_tokens_total": 0, "tokens_predicted_total": 0,
                         "decode_steps_total": 0, "decode_seconds_total": 0.0,
-                        "prefill_seconds_total": 0.0, "requests_processing": 0}
+                        "prefill_seconds_total": 0.0, "requests_processing": 0,
+                        "prompt_tokens_cached_total": 0}
         self._run = True
         self._lock = threading.Lock()
         self.thread = threading.Thread(target=self._loop, name="llm-scheduler", daemon=True)
@@ -108,11 +126,21 @@ class Scheduler:
         self.thread.join(timeout=10)
 
     # ---------------------------------------------------------------- scheduler thread
-    def _free_slot(self) -> int:
-        for s in range(self.parallel):
-            if s not in self.active:
-                return s
-        return -1
+    def _free_slot(self, ids: Optional[List[int]] = None) -> int:
+        """A free slot: the one whose cached tokens share the longest prefix with ``ids``, else
+        the one with the least cached context (keeps other conversations' caches warm)."""
+        free = [s for s in range(self.parallel) if s not in self.active]
+        if not free:
+            return -1
+        def key(s):
+            held = self.slot_tokens.get(s, [])
+            return (common_prefix(held, ids) if ids else 0, -len(held), -s)
+        return max(free, key=key)
+
+    def _release(self, job: Job) -> None:
+        """Forget ``job``'s slot assignment; its KV (the first ``pos`` tokens) stays reusable."""
+        self.slot_tokens[job.slot] = (job.ids + job.gen)[:job.pos]
+        self.active.pop(job.slot, None)
 
     def _emit(self, job: Job, tok: int) -> bool:
         """Record a sampled token; returns True when the job is finished."""
@@ -169,21 +197,30 @@ class Scheduler:
                 return
             if job.cancelled:
                 continue
-            slot = self._free_slot()
+            slot = self._free_slot(job.ids if job.cache_prompt else None)
             job.slot = slot
             try:
-                if job.temperature > 0:
+                if job.params.temperature > 0:
                     dev = self.engine.device if self.engine.gpu else "cpu"
                     job.generator = torch.Generator(device=dev)
                     job.generator.manual_seed(job.seed if job.seed is not None
                                               else int.from_bytes(os.urandom(4), "little"))
+                # reuse the slot's KV for the shared prefix; at least one token is prefilled (its
+                # logits are the first sample)
+                n_past = 0
+                if job.cache_prompt:
+                    n_past = min(common_prefix(self.slot_tokens.get(slot, []), job.ids),
+                                 len(job.ids) - 1)
+                self.slot_tokens[slot] = []                 # the KV is being rewritten
+                job.n_cached = n_past
                 t0 = time.perf_counter()
-                logits = self.engine.prefill(job.ids, slot)
-                tok = sample(logits, job.temperature, job.top_k, job.top_p, job.generator)
+                logits = self.engine.prefill(job.ids[n_past:], slot, start=n_past)
+                tok = sample_token(logits, job.params, job.ids, job.generator)
                 job.t_prefill = time.perf_counter() - t0
                 job.t_first = time.perf_counter()
                 with self._lock:
-                    self.metrics["prompt_tokens_total"] += len(job.ids)
+                    self.metrics["prompt_tokens_total"] += len(job.ids) - n_past
+                    self.metrics["prompt_tokens_cached_total"] += n_past
                     self.metrics["prefill_seconds_total"] += job.t_prefill
                     self.metrics["tokens_predicted_total"] += 1
                 job.pos = len(job.ids)
@@ -193,23 +230,24 @@ class Scheduler:
                     self.metrics["requests_failed_total"] = self.metrics.get("requests_failed_total", 0) + 1
                 job.out.put(("error", repr(e)))
                 continue
-            if not finished:
+            if finished:
+                self._release(job)
+            else:
                 self.active[slot] = job
 
     def _step(self) -> None:
         jobs = [j for j in self.active.values() if not j.cancelled]
         for j in [j for j in self.active.values() if j.cancelled]:
-            del self.active[j.slot]
+            self._release(j)
         if not jobs:
             return
         t0 = time.perf_counter()
         logits = self.engine.decode([j.last for j in jobs], [j.pos for j in jobs],
                                     [j.slot for j in jobs])
-        greedy = [j.temperature <= 0 for j in jobs]
-        if all(greedy):
+        if all(j.params.plain_greedy for j in jobs):
             toks = torch.argmax(logits, -1).tolist()
         else:
-            toks = [sample(logits[i], j.temperature, j.top_k, j.top_p, j.generator)
+            toks = [sample_token(logits[i], j.params, j.ids + j.gen, j.generator)
                     for i, j in enumerate(jobs)]
         dt = time.perf_counter() - t0
         with self._lock:
@@ -219,7 +257,7 @@ class Scheduler:
         for j, t in zip(jobs, toks):
             j.pos += 1
             if self._emit(j, int(t)):
-                del self.active[j.slot]
+                self._release(j)
 
     def _loop(self) -> None:
         while self._run:
@@ -231,19 +269,21 @@ class Scheduler:
                 for j in list(self.active.values()):
                     j.out.put(("error", repr(e)))
                 self.active.clear()
+                self.slot_tokens.clear()
 
 
 # -------------------------------------------------------------------- HTTP layer
-def _job_from(body: Dict[str, Any], ids: List[int], default_max: int) -> Job:
+def _job_from(body: Dict[str, Any], ids: List[int], default_max: int,
+              vocab: Optional[int] = None) -> Job:
     stop = body.get("stop") or []
     if isinstance(stop, str):
         stop = [stop]
     n = body.get("n_predict", body.get("max_tokens", body.get("max_completion_tokens")))
     if n is None or int(n) < 0:
         n = default_max
-    return Job(ids=ids, max_new=int(n), temperature=float(body.get("temperature", 0.8)),
-               top_k=int(body.get("top_k", 40)), top_p=float(body.get("top_p", 0.95)),
-               seed=None if body.get("seed") in (None, -1) else int(body["seed"]), stop=list(stop))
+    return Job(ids=ids, max_new=int(n), params=SamplingParams.from_request(body, vocab),
+               seed=None if body.get("seed") in (None, -1) else int(body["seed"]), stop=list(stop),
+               cache_prompt=bool(body.get("cache_prompt", True)))
 
 
 class RequestTimeout(RuntimeError):
@@ -304,8 +344,9 @@ def _timings(job: Job) -> Dict[str, Any]:
     now = time.perf_counter()
     pred_ms = (now - job.t_first) * 1e3
     n = len(job.gen)
-    return {"prompt_n": len(job.ids), "prompt_ms": round(job.t_prefill * 1e3, 3),
-            "prompt_per_second": round(len(job.ids) / max(job.t_prefill, 1e-9), 2),
+    n_prompt = len(job.ids) - job.n_cached
+    return {"cache_n": job.n_cached, "prompt_n": n_prompt, "prompt_ms": round(job.t_prefill * 1e3, 3),
+            "prompt_per_second": round(n_prompt / max(job.t_prefill, 1e-9), 2),
             "predicted_n": n, "predicted_ms": round(pred_ms, 3),
             "predicted_per_second": round(max(n - 1, 0) / max(pred_ms / 1e3, 1e-9), 2)}
 
@@ -353,8 +394,9 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
         return {"content": state["tok"].decode(body.get("tokens", []))}
 
     def submit(body, ids, default_max):
+        s = sched()
         try:
-            return sched().submit(_job_from(body, ids, default_max))
+            return s.submit(_job_from(body, ids, default_max, s.engine.cfg.vocab))
         except ValueError as e:
             raise HTTPException(400, str(e))
 
@@ -384,6 +426,7 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
         job = await wait(job, request)
         return {"content": job.text, "stop": True, "model": state.get("model"),
                 "tokens_predicted": len(job.gen), "tokens_evaluated": len(job.ids),
+                "tokens_cached": job.pos,
                 "stopped_eos": job.finish == "stop" and job.gen[-1] in s.stop_ids,
                 "stopped_limit": job.finish == "length",
                 "stopped_word": job.finish == "stop" and job.gen[-1] not in s.stop_ids,
@@ -443,6 +486,23 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
         if not isinstance(msgs, list) or not msgs:
             raise HTTPException(400, "messages must be a non-empty list")
         return await openai(body, state["tok"].encode(chatml(msgs)), True, request)
+
+    @app.get("/props")
+    def props():
+        s = sched()
+        d = SamplingParams.from_request({})
+        return {"total_slots": s.parallel, "model_path": state.get("model"),
+                "default_generation_settings": {
+                    "n_ctx": s.engine.max_ctx, "temperature": d.temperature, "top_k": d.top_k,
+                    "top_p": d.top_p, "min_p": d.min_p, "repeat_penalty": d.repeat_penalty,
+                    "repeat_last_n": d.repeat_last_n, "presence_penalty": d.presence_penalty,
+                    "frequency_penalty": d.frequency_penalty, "cache_prompt": True}}
+
+    @app.get("/slots")
+    def slots():
+        s = sched()
+        return [{"id": i, "n_ctx": s.engine.max_ctx, "is_processing": i in s.active,
+                 "n_cached": len(s.slot_tokens.get(i, []))} for i in range(s.parallel)]
 
     @app.get("/metrics")
     def metrics():

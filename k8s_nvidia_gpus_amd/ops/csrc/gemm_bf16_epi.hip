@@ -11,14 +11,17 @@
 // The validator GEMMs (gemm_bf16_gfx950*.hip) use 256×256 tiles; the Wan2.1 DiT at the reference
 // defaults (512×320×16 frames → 2×2560 token rows with CFG, generate_wan_t2v.py:305-312) has
 // N = 1536 for four of its six projections, where 256×256 tiles make only 120 workgroups for 256
-// CUs.  This kernel uses 256×128 tiles (240 workgroups there, 1400 for the 8960-wide FFN):
+// CUs.  This kernel's block tile is a WM × WN grid of waves, each wave a 64×64 output block, so the
+// tile is (64·WM) × (64·WN): 256×128 (8 waves) for the DiT (240 workgroups there, 1400 for the
+// 8960-wide FFN), and 128×128 / 128×64 / 64×64 for the SD1.5 UNet's narrow (N = 320) and short
+// (M = 2·16², 2·8² token rows at the deep levels) projections, where a 256×128 grid would leave
+// most of the 256 CUs idle.  The host picks the largest tile whose grid still covers the CUs.
 //
-//   * 512 threads = 8 waves, 4 (M) × 2 (N), each wave a 64×64 output block = 4×4 tiles of
-//     v_mfma_f32_16x16x32_bf16 (weight fragment as the A operand, so a lane's 4 accumulators are 4
-//     consecutive output columns of one row);
-//   * A and B K-tiles (BK = 64) staged HBM→LDS by LDS-DMA (global_load_lds_dwordx4, 6 per thread per
-//     K-tile) into a 3-deep ring of 48 KiB stages: one barrier per K-tile, the DMA of K-tile t+2
-//     issued right after it and retired by a counted `s_waitcnt vmcnt(6)` two iterations later —
+//   * each wave: 4×4 tiles of v_mfma_f32_16x16x32_bf16 (weight fragment as the A operand, so a
+//     lane's 4 accumulators are 4 consecutive output columns of one row);
+//   * A and B K-tiles (BK = 64) staged HBM→LDS by LDS-DMA (global_load_lds_dwordx4; 6 per thread
+//     per K-tile at 256×128) into a 3-deep ring: one barrier per K-tile, the DMA of K-tile t+2
+//     issued right after it and retired by a counted `s_waitcnt vmcnt` two iterations later —
 //     the loop never drains the DMA queue;
 //   * XOR-swizzled 128-B LDS rows (16-B chunk c of row r at c ^ ((r >> 1) & 7)), applied to the DMA
 //     SOURCE address (LDS-DMA writes lane-linearly), so every ds_read_b128 fragment read is
@@ -32,6 +35,9 @@
 //     one XCD's L2).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+
+#include <type_traits>
 
 namespace {
 
@@ -42,17 +48,23 @@ typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int BM = 256, BN = 128, BK = 64;
-constexpr int NT = 512;
-constexpr int A_STAGE = BM * BK * 2;               // 32 KiB
-constexpr int B_STAGE = BN * BK * 2;               // 16 KiB
-constexpr int STAGE = A_STAGE + B_STAGE;           // 48 KiB
+constexpr int BK = 64;
 constexpr int NSTAGE = 3;
-constexpr int RING = NSTAGE * STAGE;               // 144 KiB
-constexpr int CF_STRIDE = BN * 4 + 16;             // fp32 epilogue row (528 B)
-constexpr int CB_STRIDE = BN * 2 + 16;             // bf16 epilogue row (272 B)
-static_assert(BM * CF_STRIDE <= RING, "fp32 epilogue image must fit the ring");
 constexpr int GROUP_M = 8;
+
+// Tile geometry of a WM × WN wave grid (each wave 64×64).
+template <int WM, int WN>
+struct Geo {
+  static constexpr int BM = 64 * WM, BN = 64 * WN, NW = WM * WN, NT = 64 * NW;
+  static constexpr int A_STAGE = BM * BK * 2, B_STAGE = BN * BK * 2;
+  static constexpr int STAGE = A_STAGE + B_STAGE;
+  static constexpr int RING = NSTAGE * STAGE;
+  static constexpr int LA = BM / 8 / NW, LB = BN / 8 / NW;   // DMA wave-instructions per operand
+  static constexpr int CF_STRIDE = BN * 4 + 16;              // fp32 epilogue row
+  static constexpr int CB_STRIDE = BN * 2 + 16;              // bf16 / fp16 epilogue row
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "DMA rows must split evenly");
+  static_assert(BM * CF_STRIDE <= RING, "fp32 epilogue image must fit the ring");
+};
 
 enum Epi { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID = 2 };
 
@@ -74,6 +86,7 @@ __device__ __forceinline__ void barrier_raw() {
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
@@ -108,15 +121,19 @@ __device__ __forceinline__ float gelu_tanh(float v) {
   return v / (1.f + __expf(-2.f * u));
 }
 
-template <int EPI, bool F16>
-__global__ void __launch_bounds__(NT, 1) gemm_bf16_epi_256x128(const Args a) {
-  __shared__ __attribute__((aligned(16))) char lds[RING];
+template <int EPI, bool F16, int WM, int WN>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
+  using G = Geo<WM, WN>;
+  constexpr int BM = G::BM, BN = G::BN, NW = G::NW, NT = G::NT, LA = G::LA, LB = G::LB;
+  constexpr int A_STAGE = G::A_STAGE, STAGE = G::STAGE;
+  constexpr int CF_STRIDE = G::CF_STRIDE, CB_STRIDE = G::CB_STRIDE;
+  __shared__ __attribute__((aligned(16))) char lds[G::RING];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1;  // 0..3: 64-row block
-  const int wn = wave & 1;   // 0..1: 64-column block
+  const int wm = wave / WN;  // 64-row block
+  const int wn = wave % WN;  // 64-column block
 
   // ---- block → tile: bijective XCD remap, then GROUP_M order ----
   const int tiles_m = (a.M + BM - 1) / BM;
@@ -137,18 +154,18 @@ __global__ void __launch_bounds__(NT, 1) gemm_bf16_epi_256x128(const Args a) {
   // ---- LDS-DMA sources: wave-instruction q covers 8 rows; lane → row q*8 + lane/8, physical chunk
   //      lane%8 holds logical chunk (lane%8) ^ ((row >> 1) & 7) ----
   const size_t lda_b = (size_t)a.lda * 2, ldb_b = (size_t)a.ldb * 2;
-  const char* a_src[4];
-  const char* b_src[2];
+  const char* a_src[LA];
+  const char* b_src[LB];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int q = j * 8 + wave, row = q * 8 + (lane >> 3);
+  for (int j = 0; j < LA; ++j) {
+    const int q = j * NW + wave, row = q * 8 + (lane >> 3);
     const int c = (lane & 7) ^ ((row >> 1) & 7);
     const int grow = min(m0 + row, a.M - 1);     // M tail: clamped rows, never stored
     a_src[j] = reinterpret_cast<const char*>(a.A) + (size_t)grow * lda_b + c * 16;
   }
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int q = j * 8 + wave, row = q * 8 + (lane >> 3);
+  for (int j = 0; j < LB; ++j) {
+    const int q = j * NW + wave, row = q * 8 + (lane >> 3);
     const int c = (lane & 7) ^ ((row >> 1) & 7);
     const int gn = min(n0 + row, a.N - 1);       // N tail: clamped weight rows, never stored
     b_src[j] = reinterpret_cast<const char*>(a.B) + (size_t)gn * ldb_b + c * 16;
@@ -158,13 +175,13 @@ __global__ void __launch_bounds__(NT, 1) gemm_bf16_epi_256x128(const Args a) {
     char* sb = sa + A_STAGE;
     const size_t kb = (size_t)t * BK * 2;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < LA; ++j)
       __builtin_amdgcn_global_load_lds((const void*)(a_src[j] + kb),
-                                       (lds_void*)(sa + (j * 8 + wave) * 1024), 16, 0, 0);
+                                       (lds_void*)(sa + (j * NW + wave) * 1024), 16, 0, 0);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < LB; ++j)
       __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + kb),
-                                       (lds_void*)(sb + (j * 8 + wave) * 1024), 16, 0, 0);
+                                       (lds_void*)(sb + (j * NW + wave) * 1024), 16, 0, 0);
   };
 
   // ---- fragment read offsets: row (lane & 15) of a 16-row block, logical chunk 4·kk + lane/16 ----
@@ -185,7 +202,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_bf16_epi_256x128(const Args a) {
   stage(0);
   if (T > 1) stage(1);
   for (int t = 0; t < T; ++t) {
-    if (t + 1 < T) wait_vmcnt<6>(); else wait_vmcnt<0>();
+    if (t + 1 < T) wait_vmcnt<LA + LB>(); else wait_vmcnt<0>();
     barrier_raw();                       // K-tile t landed for every wave; t−1's reads are done
     if (t + 2 < T) stage(t + 2);         // into the buffer K-tile t−1 used
     const char* sa = lds + (t % NSTAGE) * STAGE + a_wave;
@@ -251,10 +268,11 @@ __global__ void __launch_bounds__(NT, 1) gemm_bf16_epi_256x128(const Args a) {
         *reinterpret_cast<f32x4*>(lds + m * CF_STRIDE + n * 4) = v;
       }
     __syncthreads();
-    // 256 rows × 128 fp32: 32 threads per row (16 B each), 16 rows per pass
+    // BM rows × BN fp32: BN/4 threads per row (16 B each)
+    constexpr int TPR = BN / 4, RPP = NT / TPR;
 #pragma unroll 4
-    for (int it = 0; it < BM / 16; ++it) {
-      const int row = it * 16 + (tid >> 5), col = (tid & 31) * 4;
+    for (int it = 0; it < BM / RPP; ++it) {
+      const int row = it * RPP + tid / TPR, col = (tid % TPR) * 4;
       const int gm = m0 + row;
       if (gm < a.M && n0 + col < a.N) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(lds + row * CF_STRIDE + col * 4);
@@ -285,12 +303,13 @@ __global__ void __launch_bounds__(NT, 1) gemm_bf16_epi_256x128(const Args a) {
         *reinterpret_cast<uint2*>(lds + m * CB_STRIDE + n * 2) = pack4<F16>(v);
       }
     __syncthreads();
-    // 256 rows × 256 B: 16 threads per row (16 B each), 32 rows per pass
+    // BM rows × BN·2 B: BN/8 threads per row (16 B each)
+    constexpr int TPR = BN / 8, RPP = NT / TPR;
     char* obase = reinterpret_cast<char*>(a.out) + ((size_t)m0 * a.ldo + n0) * 2;
     const size_t ldo_b = (size_t)a.ldo * 2;
 #pragma unroll 4
-    for (int it = 0; it < BM / 32; ++it) {
-      const int row = it * 32 + (tid >> 4), ch = tid & 15;
+    for (int it = 0; it < BM / RPP; ++it) {
+      const int row = it * RPP + tid / TPR, ch = tid % TPR;
       if (m0 + row < a.M && n0 + ch * 8 < a.N)
         *reinterpret_cast<uint4*>(obase + row * ldo_b + ch * 16) =
             *reinterpret_cast<const uint4*>(lds + row * CB_STRIDE + ch * 16);
@@ -306,6 +325,28 @@ extern "C" {
 // operand bases (bias 8-B aligned), gate_stride % 4 == 0; any M ≥ 1.  dtype 1 = bf16, 0 = fp16.
 int amdk8s_gemm_epi_supported(int M, int N, int K) {
   return M > 0 && N > 0 && K > 0 && N % 8 == 0 && K % BK == 0;
+}
+
+// Block tile for an M × N problem: the largest of 256×128, 128×128, 128×64, 64×64 whose grid
+// covers the 256 CUs (else 64×64).  amdk8s_gemm_epi_set_tile(0..3) or AMDK8S_GEMM_EPI_TILE pins
+// one (A/B sweeps); -1 restores the heuristic.
+static const int kTiles[4][2] = {{256, 128}, {128, 128}, {128, 64}, {64, 64}};
+static int g_tile = -2;   // -2: not initialised from the environment yet
+
+void amdk8s_gemm_epi_set_tile(int tile) { g_tile = (tile >= 0 && tile <= 3) ? tile : -1; }
+
+int amdk8s_gemm_epi_tile(int M, int N) {
+  if (g_tile == -2) {
+    const char* e = getenv("AMDK8S_GEMM_EPI_TILE");
+    g_tile = (e && e[0] >= '0' && e[0] <= '3' && !e[1]) ? e[0] - '0' : -1;
+  }
+  if (g_tile >= 0) return g_tile;
+  for (int i = 0; i < 3; ++i) {
+    const long nwg = (long)((M + kTiles[i][0] - 1) / kTiles[i][0]) *
+                     ((N + kTiles[i][1] - 1) / kTiles[i][1]);
+    if (nwg >= 256) return i;
+  }
+  return 3;
 }
 
 int amdk8s_gemm_epi(int epi, int dtype, const void* A, const void* B, const void* bias, void* out,
@@ -338,25 +379,35 @@ int amdk8s_gemm_epi(int epi, int dtype, const void* A, const void* B, const void
   a.ldx = ldx;
   a.rows_per_gate = rows_per_gate > 0 ? rows_per_gate : M;
   a.gate_stride = gate_stride;
-  const long nwg = (long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (epi < EPI_STORE || epi > EPI_RESID) return (int)hipErrorInvalidValue;
+  const int tile = amdk8s_gemm_epi_tile(M, N);
+  const long nwg = (long)((M + kTiles[tile][0] - 1) / kTiles[tile][0]) *
+                   ((N + kTiles[tile][1] - 1) / kTiles[tile][1]);
   if (nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
-#define AMDK8S_EPI_LAUNCH(E, F)                                                                  \
-  hipLaunchKernelGGL((gemm_bf16_epi_256x128<E, F>), dim3(nwg), dim3(NT), 0, stream, a)
   const bool f16 = dtype == 0;
-  switch (epi) {
-    case EPI_STORE:
-      if (f16) AMDK8S_EPI_LAUNCH(EPI_STORE, true); else AMDK8S_EPI_LAUNCH(EPI_STORE, false);
-      break;
-    case EPI_GELU:
-      if (f16) AMDK8S_EPI_LAUNCH(EPI_GELU, true); else AMDK8S_EPI_LAUNCH(EPI_GELU, false);
-      break;
-    case EPI_RESID:
-      if (f16) AMDK8S_EPI_LAUNCH(EPI_RESID, true); else AMDK8S_EPI_LAUNCH(EPI_RESID, false);
-      break;
-    default:
-      return (int)hipErrorInvalidValue;
+  auto go = [&](auto wm, auto wn) {
+    constexpr int WM = decltype(wm)::value, WN = decltype(wn)::value;
+    constexpr int NT = Geo<WM, WN>::NT;
+    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(nwg), dim3(NT), 0, stream, a); };
+    if (f16) {
+      if (epi == EPI_STORE) launch(gemm_epi_kernel<EPI_STORE, true, WM, WN>);
+      else if (epi == EPI_GELU) launch(gemm_epi_kernel<EPI_GELU, true, WM, WN>);
+      else launch(gemm_epi_kernel<EPI_RESID, true, WM, WN>);
+    } else {
+      if (epi == EPI_STORE) launch(gemm_epi_kernel<EPI_STORE, false, WM, WN>);
+      else if (epi == EPI_GELU) launch(gemm_epi_kernel<EPI_GELU, false, WM, WN>);
+      else launch(gemm_epi_kernel<EPI_RESID, false, WM, WN>);
+    }
+  };
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I4 = std::integral_constant<int, 4>;
+  switch (tile) {
+    case 0: go(I4{}, I2{}); break;
+    case 1: go(I2{}, I2{}); break;
+    case 2: go(I2{}, I1{}); break;
+    default: go(I1{}, I1{}); break;
   }
-#undef AMDK8S_EPI_LAUNCH
   return (int)hipGetLastError();
 }
 

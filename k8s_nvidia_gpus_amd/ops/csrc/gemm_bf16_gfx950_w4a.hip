@@ -17,10 +17,12 @@
 // Shape contract (host-checked): M % 256 == 0, N % 256 == 0, K % 64 == 0, lda/ldb/ldc % 8 == 0,
 // 16-B aligned base pointers, 256·lda·2 and 256·ldb·2 < 2³¹ (32-bit panel offsets).
 //
-// Epilogue variants (amdk8s_gemm_bf16_nt_w4a_epi, the DiT / UNet projections): any M — the last
-// row panel's buffer descriptor covers only its valid rows, so the DMA reads zeros past M and those
-// rows are not stored — and the 16-B store pass adds a bf16 bias and optionally applies tanh-GELU
-// to each bf16 C value (fp32 maths on the bf16-rounded product).
+// Epilogue variants (amdk8s_gemm_w4a_epi, the DiT / UNet projections; bf16 or fp16): any M — the
+// last row panel's buffer descriptor covers only its valid rows, so the DMA reads zeros past M and
+// those rows are not stored — and the 16-B store pass adds the bias and optionally applies
+// tanh-GELU to each C value (fp32 maths on the 16-bit-rounded product), or (RESID) folds the
+// product into an fp32 residual stream in place, x += gate · (C + bias), the DiT's gated update
+// (the same bf16-rounded product an nn.Linear would hand to that update).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -43,6 +45,7 @@ constexpr int GROUP_M = 8;
 
 typedef __attribute__((address_space(3))) char lds_char;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 }  // namespace
 
@@ -50,7 +53,36 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 // (v_mfma_f32_16x16x32_f16, fp16 C) — same fragment layout, LDS image and cycles as bf16.
 constexpr int kF16 = 16;
 
-constexpr int kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2;
+constexpr int kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiResid = 3;
+
+// Two 16-bit C values of one dword → fp32 (bf16, or fp16 under the kF16 schedule).
+template <bool H>
+__device__ __forceinline__ float w4a_lo(uint32_t v) {
+  if constexpr (H) return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xffffu));
+  else return __uint_as_float(v << 16);
+}
+template <bool H>
+__device__ __forceinline__ float w4a_hi(uint32_t v) {
+  if constexpr (H) return (float)__builtin_bit_cast(_Float16, (uint16_t)(v >> 16));
+  else return __uint_as_float(v & 0xffff0000u);
+}
+template <bool H>
+__device__ __forceinline__ uint32_t w4a_pack(float lo, float hi) {
+  if constexpr (H) {
+    const __attribute__((ext_vector_type(2))) _Float16 p = {(_Float16)lo, (_Float16)hi};
+    return __builtin_bit_cast(uint32_t, p);
+  } else {
+    const __attribute__((ext_vector_type(2))) __bf16 p = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(uint32_t, p);
+  }
+}
+
+// RESID operands (fp32 residual stream and optional per-sample gate rows).
+struct W4aResid {
+  float* x;
+  const float* gate;
+  int ldx, rows_per_gate, gate_stride;
+};
 
 __device__ __forceinline__ float w4a_gelu_tanh(float v) {
   const float u = 0.7978845608028654f * fmaf(0.044715f * v, v * v, v);
@@ -62,7 +94,9 @@ __global__ void __launch_bounds__(NT, 1)
 amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                 uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
                                 int ldc, int order, int nt_store,
-                                const uint16_t* __restrict__ bias = nullptr) {
+                                const uint16_t* __restrict__ bias = nullptr,
+                                W4aResid resid = W4aResid{}) {
+  constexpr bool H = SCHED == kF16;
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
 
   const int tid = threadIdx.x;
@@ -127,11 +161,12 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
   const size_t ldc_b = (size_t)ldc * 2;
   float bv[8];
   if constexpr (EPI != kEpiNone) {   // this thread's 8 columns are the same in every row it stores
-    const u32x4 braw = *reinterpret_cast<const u32x4*>(bias + n0 + (tid & 31) * 8);
+    u32x4 braw = {0u, 0u, 0u, 0u};
+    if (EPI != kEpiResid || bias) braw = *reinterpret_cast<const u32x4*>(bias + n0 + (tid & 31) * 8);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      bv[2 * e] = __uint_as_float(braw[e] << 16);
-      bv[2 * e + 1] = __uint_as_float(braw[e] & 0xffff0000u);
+      bv[2 * e] = w4a_lo<H>(braw[e]);
+      bv[2 * e + 1] = w4a_hi<H>(braw[e]);
     }
   }
   const int rows_valid = min(BM, M - m0);
@@ -141,17 +176,39 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
     const int ch = tid & 31;
     u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * C_STRIDE + ch * 16);
     if (row >= rows_valid) continue;
+    if constexpr (EPI == kEpiResid) {
+      // 8 fp32 columns of x (and of the row's gate): two 16-B loads each, one read-modify-write
+      const int gm = m0 + row, gn = n0 + ch * 8;
+      f32x4* xp = reinterpret_cast<f32x4*>(resid.x + (size_t)gm * resid.ldx + gn);
+      f32x4 x0 = xp[0], x1 = xp[1];
+      f32x4 g0 = {1.f, 1.f, 1.f, 1.f}, g1 = g0;
+      if (resid.gate) {
+        const f32x4* gp = reinterpret_cast<const f32x4*>(
+            resid.gate + (size_t)(gm / resid.rows_per_gate) * resid.gate_stride + gn);
+        g0 = gp[0];
+        g1 = gp[1];
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        x0[2 * e] += (w4a_lo<H>(v[e]) + bv[2 * e]) * g0[2 * e];
+        x0[2 * e + 1] += (w4a_hi<H>(v[e]) + bv[2 * e + 1]) * g0[2 * e + 1];
+        x1[2 * e] += (w4a_lo<H>(v[e + 2]) + bv[2 * e + 4]) * g1[2 * e];
+        x1[2 * e + 1] += (w4a_hi<H>(v[e + 2]) + bv[2 * e + 5]) * g1[2 * e + 1];
+      }
+      xp[0] = x0;
+      xp[1] = x1;
+      continue;
+    }
     if constexpr (EPI != kEpiNone) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        float lo = __uint_as_float(v[e] << 16) + bv[2 * e];
-        float hi = __uint_as_float(v[e] & 0xffff0000u) + bv[2 * e + 1];
+        float lo = w4a_lo<H>(v[e]) + bv[2 * e];
+        float hi = w4a_hi<H>(v[e]) + bv[2 * e + 1];
         if constexpr (EPI == kEpiBiasGelu) {
           lo = w4a_gelu_tanh(lo);
           hi = w4a_gelu_tanh(hi);
         }
-        const __attribute__((ext_vector_type(2))) __bf16 p = {(__bf16)lo, (__bf16)hi};
-        v[e] = __builtin_bit_cast(uint32_t, p);
+        v[e] = w4a_pack<H>(lo, hi);
       }
     }
     u32x4* dst = reinterpret_cast<u32x4*>(cbase_g + row * ldc_b + ch * 16);
@@ -205,15 +262,25 @@ int launch_w4a(const void* A, const void* B, void* C, int M, int N, int K, int l
 }
 }  // namespace
 
-// Any M >= 1 (N % 256 == 0, K % 64 == 0); epi 0 = plain, 1 = + bias, 2 = gelu_tanh(+ bias).
-extern "C" int amdk8s_gemm_bf16_nt_w4a_epi(const void* A, const void* B, void* C, const void* bias,
-                                           int epi, int M, int N, int K, int lda, int ldb, int ldc,
-                                           hipStream_t stream) {
+// Any M >= 1 (N % 256 == 0, K % 64 == 0); epi 0 = plain, 1 = + bias, 2 = gelu_tanh(+ bias),
+// 3 = x[m, n] += gate[m / rows_per_gate, n] · (C + bias) (fp32 x, C not written; bias / gate may
+// be null).  dtype 1 = bf16, 0 = fp16 (operands, bias, C).
+extern "C" int amdk8s_gemm_w4a_epi(int epi, int dtype, const void* A, const void* B, void* C,
+                                   const void* bias, float* x, const float* gate, int M, int N,
+                                   int K, int lda, int ldb, int ldc, int ldx, int rows_per_gate,
+                                   int gate_stride, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || N % BN || K % BK) return (int)hipErrorInvalidValue;
-  if (lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N) return (int)hipErrorInvalidValue;
-  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)bias) & 15)
-    return (int)hipErrorInvalidValue;
-  if (epi != kEpiNone && !bias) return (int)hipErrorInvalidValue;
+  if (epi < kEpiNone || epi > kEpiResid) return (int)hipErrorInvalidValue;
+  if (lda % 8 || ldb % 8 || lda < K || ldb < K) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)bias) & 15) return (int)hipErrorInvalidValue;
+  if (epi == kEpiResid) {
+    if (!x || ldx % 4 || ldx < N || ((uintptr_t)x & 15)) return (int)hipErrorInvalidValue;
+    if (gate && (rows_per_gate <= 0 || gate_stride % 4 || ((uintptr_t)gate & 15)))
+      return (int)hipErrorInvalidValue;
+  } else {
+    if (!C || ldc % 8 || ldc < N || ((uintptr_t)C & 15)) return (int)hipErrorInvalidValue;
+    if (epi != kEpiNone && !bias) return (int)hipErrorInvalidValue;
+  }
   if (256ull * (unsigned long long)(lda > ldb ? lda : ldb) * 2 >= (1ull << 31))
     return (int)hipErrorInvalidValue;
   const int tm = (M + BM - 1) / BM, tn = N / BN;
@@ -222,16 +289,23 @@ extern "C" int amdk8s_gemm_bf16_nt_w4a_epi(const void* A, const void* B, void* C
   const uint16_t* b = (const uint16_t*)B;
   const uint16_t* bs = (const uint16_t*)bias;
   uint16_t* c = (uint16_t*)C;
+  const W4aResid r{x, gate, ldx, rows_per_gate > 0 ? rows_per_gate : M, gate_stride};
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(tm * tn), dim3(NT), 0, stream, a, b, c, M, N, K, lda, ldb, ldc,
+                       sb, 0, bs, r);
+  };
   constexpr int S = AMDK8S_W4A_DEFAULT_SCHEDULE;
-  if (epi == kEpiBias)
-    hipLaunchKernelGGL((amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiBias>), dim3(tm * tn), dim3(NT), 0,
-                       stream, a, b, c, M, N, K, lda, ldb, ldc, sb, 0, bs);
-  else if (epi == kEpiBiasGelu)
-    hipLaunchKernelGGL((amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiBiasGelu>), dim3(tm * tn), dim3(NT),
-                       0, stream, a, b, c, M, N, K, lda, ldb, ldc, sb, 0, bs);
-  else
-    hipLaunchKernelGGL((amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiNone>), dim3(tm * tn), dim3(NT), 0,
-                       stream, a, b, c, M, N, K, lda, ldb, ldc, sb, 0, bs);
+  if (dtype == 0) {
+    if (epi == kEpiBias) launch(amdk8s_gemm_bf16_nt_256x256_w4a<kF16, kEpiBias>);
+    else if (epi == kEpiBiasGelu) launch(amdk8s_gemm_bf16_nt_256x256_w4a<kF16, kEpiBiasGelu>);
+    else if (epi == kEpiResid) launch(amdk8s_gemm_bf16_nt_256x256_w4a<kF16, kEpiResid>);
+    else launch(amdk8s_gemm_bf16_nt_256x256_w4a<kF16, kEpiNone>);
+  } else {
+    if (epi == kEpiBias) launch(amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiBias>);
+    else if (epi == kEpiBiasGelu) launch(amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiBiasGelu>);
+    else if (epi == kEpiResid) launch(amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiResid>);
+    else launch(amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiNone>);
+  }
   return (int)hipGetLastError();
 }
 

@@ -1,7 +1,9 @@
-"""ctypes bindings of the fused-epilogue bf16 GEMM (``csrc/gemm_bf16_epi.hip``).
+"""ctypes bindings of the fused-epilogue GEMMs (``csrc/gemm_bf16_epi.hip``, and the w4a 256×256
+kernel's epilogue variants in ``csrc/gemm_bf16_gfx950_w4a.hip``).
 
-``linear(x, w, b)`` / ``linear_gelu(x, w, b)`` are ``F.linear`` (+ tanh-GELU) on the hand-written
-256×128-tile gfx950 kernel (bf16 or fp16 operands); ``linear_residual_(res, x, w, b, gate)`` folds the
+``linear(x, w, b)`` / ``linear_gelu(x, w, b)`` are ``F.linear`` (+ tanh-GELU) on hand-written
+gfx950 kernels (bf16 or fp16 operands): the wave-grid family (256×128 … 64×64 tiles, picked by
+problem size) or, for wide projections, the 256×256 w4a kernel; ``linear_residual_(res, x, w, b, gate)`` folds the
 DiT's gated residual update ``res += gate · (x·wᵀ + b)`` into the GEMM's epilogue, so the
 projection output never round-trips through HBM in bf16.  Same conventions as the other binding
 modules: raw device pointers, torch's current stream, ``supported(...)`` predicates for what the
@@ -34,14 +36,31 @@ def _lib():
             lib.amdk8s_gemm_epi.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci,
                                             ci, ci, ci, vp]
             lib.amdk8s_gemm_epi.restype = ci
-            lib.amdk8s_gemm_bf16_nt_w4a_epi.argtypes = [vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, vp]
-            lib.amdk8s_gemm_bf16_nt_w4a_epi.restype = ci
+            lib.amdk8s_gemm_w4a_epi.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci,
+                                                ci, ci, ci, vp]
+            lib.amdk8s_gemm_w4a_epi.restype = ci
+            lib.amdk8s_gemm_epi_set_tile.argtypes = [ci]
+            lib.amdk8s_gemm_epi_set_tile.restype = None
+            lib.amdk8s_gemm_epi_tile.argtypes = [ci, ci]
+            lib.amdk8s_gemm_epi_tile.restype = ci
             _declared = True
     return lib
 
 
 def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
+
+
+TILES = ((256, 128), (128, 128), (128, 64), (64, 64))
+
+
+def set_tile(tile: int) -> None:
+    """Pin the 256×128-kernel family's block tile (index into TILES); -1 = size heuristic."""
+    _lib().amdk8s_gemm_epi_set_tile(int(tile))
+
+
+def tile_for(m: int, n: int) -> tuple:
+    return TILES[_lib().amdk8s_gemm_epi_tile(m, n)]
 
 
 def _rows(x: torch.Tensor) -> torch.Tensor:
@@ -68,7 +87,7 @@ def supported(x: torch.Tensor, w: torch.Tensor) -> bool:
 def _bias(b: Optional[torch.Tensor], n: int, dtype: torch.dtype) -> Optional[torch.Tensor]:
     if b is None:
         return None
-    if b.dtype != dtype or not b.is_contiguous() or b.numel() != n or b.data_ptr() % 8:
+    if b.dtype != dtype or not b.is_contiguous() or b.numel() != n or b.data_ptr() % 16:
         b = b.to(dtype).contiguous().clone()
     return b
 
@@ -85,29 +104,35 @@ def _run(epi, x2, w, b, out, res, gate, rows_per_gate, gate_stride, ldo, ldx):
         raise RuntimeError(f"amdk8s_gemm_epi failed (rc={rc}, M={m} N={n} K={k}, epi={epi})")
 
 
-# Wide bf16 projections (N % 256 == 0, enough 256×256 tiles to fill the chip) run on the
-# validator's 256x256 kernel (w4a: generated-assembly K-loop) with its bias / GELU store epilogue;
-# everything else on the 256×128 kernel.  AMDK8S_GEMM_WIDE=epi forces the latter (A/B runs).
+# Wide projections (N % 256 == 0, enough 256×256 tiles to fill the chip) run on the validator's
+# 256x256 kernel (w4a: generated-assembly K-loop) with its bias / GELU / gated-residual store
+# epilogue; everything else on the wave-grid kernel family above.  AMDK8S_GEMM_WIDE=epi forces the
+# latter (A/B runs).
 _WIDE = os.environ.get("AMDK8S_GEMM_WIDE", "w4a")
 
 
 def use_w4a(m: int, n: int, k: int, dtype: torch.dtype) -> bool:
-    return (_WIDE == "w4a" and dtype == torch.bfloat16 and n % 256 == 0 and k % 64 == 0
+    return (_WIDE == "w4a" and dtype in _DT and n % 256 == 0 and k % 64 == 0
             and ((m + 255) // 256) * (n // 256) >= 256)
 
 
-def _w4a(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu: bool,
-         out: torch.Tensor) -> None:
+def _w4a(epi: int, x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor],
+         out: Optional[torch.Tensor], res: Optional[torch.Tensor] = None,
+         gate: Optional[torch.Tensor] = None, rows_per_gate: int = 0, gate_stride: int = 0) -> None:
+    """epi: 0 store, 1 + bias, 2 gelu(+ bias), 3 residual (``res`` fp32, optional gate)."""
     m, k = x2.shape
     n = w.shape[0]
-    if b is None:
-        b = torch.zeros(n, dtype=torch.bfloat16, device=x2.device) if gelu else None
-    epi = 0 if b is None else (2 if gelu else 1)
-    rc = _lib().amdk8s_gemm_bf16_nt_w4a_epi(x2.data_ptr(), w.data_ptr(), out.data_ptr(),
-                                            b.data_ptr() if b is not None else None, epi, m, n, k,
-                                            x2.stride(0), w.stride(0), out.stride(0), _stream(x2))
+    rc = _lib().amdk8s_gemm_w4a_epi(
+        epi, _DT[x2.dtype], x2.data_ptr(), w.data_ptr(), out.data_ptr() if out is not None else None,
+        b.data_ptr() if b is not None else None, res.data_ptr() if res is not None else None,
+        gate.data_ptr() if gate is not None else None, m, n, k, x2.stride(0), w.stride(0),
+        out.stride(0) if out is not None else 0, n, rows_per_gate, gate_stride, _stream(x2))
     if rc != 0:
-        raise RuntimeError(f"amdk8s_gemm_bf16_nt_w4a_epi failed (rc={rc}, M={m} N={n} K={k})")
+        raise RuntimeError(f"amdk8s_gemm_w4a_epi failed (rc={rc}, M={m} N={n} K={k}, epi={epi})")
+
+
+def _aligned16(*ts) -> bool:
+    return all(t is None or t.data_ptr() % 16 == 0 for t in ts)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
@@ -117,9 +142,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
     n = w.shape[0]
     out = torch.empty((x2.shape[0], n), dtype=x.dtype, device=x.device)
     bb = _bias(b, n, x.dtype)
-    if use_w4a(x2.shape[0], n, x2.shape[1], x.dtype) and w.data_ptr() % 16 == 0 \
-            and (bb is None or bb.data_ptr() % 16 == 0):
-        _w4a(x2, w, bb, gelu, out)
+    if use_w4a(x2.shape[0], n, x2.shape[1], x.dtype) and _aligned16(x2, w, bb):
+        if gelu and bb is None:
+            bb = torch.zeros(n, dtype=x.dtype, device=x.device)
+        _w4a(2 if gelu else (0 if bb is None else 1), x2, w, bb, out)
     else:
         _run(EPI_GELU if gelu else EPI_STORE, x2, w, bb, out, None, None, 0, 0, n, 0)
     return out.view(*x.shape[:-1], n)
@@ -150,5 +176,9 @@ def linear_residual_(res: torch.Tensor, x: torch.Tensor, w: torch.Tensor,
             raise ValueError("rows are not a whole number of gate rows")
         rows_per_gate = x2.shape[0] // gate.shape[0]
         gstride = gate.stride(0) if gate.shape[0] > 1 else 0
-    _run(EPI_RESID, x2, w, _bias(b, n, x.dtype), None, res, gate, rows_per_gate, gstride, 0, n)
+    bb = _bias(b, n, x.dtype)
+    if use_w4a(x2.shape[0], n, x2.shape[1], x.dtype) and _aligned16(x2, w, bb, res, gate):
+        _w4a(3, x2, w, bb, None, res, gate, rows_per_gate, gstride)
+    else:
+        _run(EPI_RESID, x2, w, bb, None, res, gate, rows_per_gate, gstride, 0, n)
     return res

@@ -95,5 +95,70 @@ def test_wide_projection_on_w4a(GE, m, gelu):
     torch.testing.assert_close(y.float(), ref, rtol=3e-2, atol=3e-2)
     # w4a wrote only rows < M: the row after the output is untouched
     big = torch.full((m + 256, n), 7.0, device=dev).bfloat16()
-    GE._w4a(x, w, b, gelu, big[:m])
+    GE._w4a(2 if gelu else 1, x, w, b, big[:m])
     assert bool((big[m:] == 7.0).all())
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_every_tile_variant(GE, tile, dtype):
+    """Each wave-grid block tile (256×128, 128×128, 128×64, 64×64) with M / N tails: store, GELU
+    and the gated residual epilogue."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(tile)
+    m, n, k = 777, 328, 192
+    x = torch.randn(m, k, generator=g, device=dev).to(dtype)
+    w = (torch.randn(n, k, generator=g, device=dev) / k ** 0.5).to(dtype)
+    b = torch.randn(n, generator=g, device=dev).to(dtype)
+    ref = _ref(x, w, b)
+    tol = 2e-2 if dtype == torch.bfloat16 else 5e-3
+    GE.set_tile(tile)
+    try:
+        assert GE.tile_for(m, n) == GE.TILES[tile]
+        torch.testing.assert_close(GE.linear(x, w, b).float(), ref, rtol=tol, atol=tol)
+        torch.testing.assert_close(GE.linear_gelu(x, w, b).float(),
+                                   F.gelu(ref, approximate="tanh"), rtol=tol, atol=tol)
+        res = torch.randn(1, m, n, generator=g, device=dev)
+        gate = torch.randn(1, n, generator=g, device=dev)
+        want = res + ref.view(1, m, n) * gate[:, None, :]
+        GE.linear_residual_(res, x.view(1, m, k), w, b, gate)
+        torch.testing.assert_close(res, want, rtol=tol, atol=2 * tol)
+    finally:
+        GE.set_tile(-1)
+    assert GE.tile_for(8192, 1536) == (256, 128) and GE.tile_for(128, 1280) == (64, 64)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("gated", [True, False])
+def test_w4a_gated_residual(GE, dtype, gated):
+    """The w4a 256x256 kernel's RESID epilogue: x += gate · (A·Bᵀ + b) with per-sample gate rows
+    that do not align with the 256-row tiles (2 × 2500 rows), M tail, bf16 and fp16."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(11)
+    L, n, k = 2500, 4608, 1536
+    assert GE.use_w4a(2 * L, n, k, dtype)
+    x = torch.randn(2, L, k, generator=g, device=dev).to(dtype)
+    w = (torch.randn(n, k, generator=g, device=dev) / 40).to(dtype)
+    b = torch.randn(n, generator=g, device=dev).to(dtype)
+    res = torch.randn(2, L, n, generator=g, device=dev)
+    mods = torch.randn(2, 6, n, generator=g, device=dev)
+    gate = mods[:, 2] if gated else None
+    y = _ref(x, w, None).to(dtype).float().view(2, L, n) + b.float()   # 16-bit rounded product
+    want = res + y * (gate[:, None, :] if gated else 1.0)
+    GE.linear_residual_(res, x, w, b, gate)
+    torch.testing.assert_close(res, want, rtol=2e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("gelu", [False, True])
+def test_w4a_fp16_epilogue(GE, gelu):
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(5)
+    m, n, k = 8192, 2560, 320                 # SD1.5 GEGLU projection at 64² latents, CFG batch
+    assert GE.use_w4a(m, n, k, torch.float16)
+    x = torch.randn(m, k, generator=g, device=dev).half()
+    w = (torch.randn(n, k, generator=g, device=dev) / 18).half()
+    b = torch.randn(n, generator=g, device=dev).half()
+    ref = _ref(x, w, b)
+    if gelu:
+        ref = F.gelu(ref, approximate="tanh")
+    torch.testing.assert_close(GE.linear(x, w, b, gelu=gelu).float(), ref, rtol=5e-3, atol=5e-3)

@@ -195,6 +195,40 @@ def test_sampling_modes():
     assert {sample(lg, 1.0, top_p=0.3, generator=g) for _ in range(20)} == {1}
 
 
+def test_sampling_llama_server_parameters():
+    """min_p / penalties / logit_bias with llama.cpp's semantics and chain order."""
+    from k8s_nvidia_gpus_amd.models.llm.sampling import SamplingParams, parse_logit_bias, sample_token
+
+    lg = torch.tensor([2.0, 5.0, -1.0, 4.9, 0.5])
+    # repeat penalty divides positive / multiplies negative logits of recent tokens
+    p = SamplingParams(temperature=0.0, repeat_penalty=2.0)
+    assert sample_token(lg, p, history=[1]) == 3            # 5/2 < 4.9
+    assert sample_token(lg, SamplingParams(repeat_penalty=3.0), history=[1, 3]) == 0  # 1.67, 1.63 < 2
+    p = SamplingParams(temperature=0.0, repeat_penalty=2.0, repeat_last_n=1)
+    assert sample_token(lg, p, history=[1, 3]) == 1         # only the last token counts
+    # presence / frequency penalties
+    p = SamplingParams(temperature=0.0, frequency_penalty=0.06)
+    assert sample_token(lg, p, history=[1, 1]) == 3         # 5 - 0.12 < 4.9
+    assert sample_token(lg, p, history=[1]) == 1            # 5 - 0.06 > 4.9
+    p = SamplingParams(temperature=0.0, presence_penalty=0.2)
+    assert sample_token(lg, p, history=[1, 1, 1]) == 3
+    # logit bias: OpenAI dict, llama.cpp pairs, false bans
+    assert parse_logit_bias({"3": 1}) == {3: 1.0}
+    assert parse_logit_bias([[1, False], [4, -2]]) == {1: -float("inf"), 4: -2.0}
+    with pytest.raises(ValueError):
+        parse_logit_bias({"9": 1}, vocab=5)
+    assert sample_token(lg, SamplingParams(logit_bias={1: -float("inf")})) == 3
+    # min_p: relative to the most likely token, before temperature
+    g = torch.Generator().manual_seed(0)
+    p = SamplingParams(temperature=5.0, min_p=0.5)
+    assert {sample_token(lg, p, generator=g) for _ in range(200)} == {1, 3}
+    p = SamplingParams(temperature=5.0, min_p=0.0)
+    assert len({sample_token(lg, p, generator=g) for _ in range(400)}) == 5
+    d = SamplingParams.from_request({"temperature": 0.2, "min_p": 0.1, "repeat_penalty": 1.1})
+    assert (d.temperature, d.top_k, d.min_p, d.repeat_penalty, d.repeat_last_n) == (0.2, 40, 0.1, 1.1, 64)
+    assert SamplingParams(temperature=0.0).plain_greedy and not d.plain_greedy
+
+
 # ----------------------------------------------------------------- server
 @pytest.fixture(scope="module")
 def client(tiny_model):
@@ -307,11 +341,11 @@ def test_server_prefill_error_reaches_its_request_and_serving_continues(tiny_mod
     real = eng.prefill
     calls = {"n": 0}
 
-    def flaky(ids, slot):
+    def flaky(ids, slot, start=0):
         calls["n"] += 1
         if calls["n"] == 1:
             raise RuntimeError("probabilities contain inf")
-        return real(ids, slot)
+        return real(ids, slot, start)
 
     eng.prefill = flaky
     state = {"scheduler": Scheduler(eng, tok, parallel=2), "tok": tok, "model": "tiny"}
@@ -347,7 +381,7 @@ def test_server_cancels_abandoned_requests_and_times_out(tiny_model):
     sched = S.Scheduler(eng, tok, parallel=1)
     state = {"scheduler": sched, "tok": tok, "model": "tiny"}
     try:
-        job = sched.submit(S.Job(ids=tok.encode("hello"), max_new=200, temperature=0.0))
+        job = sched.submit(S.Job(ids=tok.encode("hello"), max_new=200))
         gen = S._stream(job, timeout=30)
         next(gen)                                  # first token arrived: job is decoding
         gen.close()                                # client went away
@@ -366,3 +400,77 @@ def test_server_cancels_abandoned_requests_and_times_out(tiny_model):
         assert not sched.active
     finally:
         sched.close()
+
+
+def test_server_prompt_cache_reuses_slot_prefix(tiny_model):
+    """cache_prompt: a follow-up prompt that extends a finished conversation goes to that
+    conversation's slot and prefills only the new tokens; the answer equals the uncached one."""
+    from fastapi.testclient import TestClient
+
+    from k8s_nvidia_gpus_amd.models.llm.server import Scheduler, create_app
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load
+
+    eng, tok = load(tiny_model, device="cpu", max_ctx=256, slots=3)
+    prefills = []
+    real = eng.prefill
+
+    def spy(ids, slot, start=0):
+        prefills.append((len(ids), slot, start))
+        return real(ids, slot, start)
+
+    eng.prefill = spy
+    sched = Scheduler(eng, tok, parallel=3)
+    c = TestClient(create_app({"scheduler": sched, "tok": tok, "model": "tiny"}))
+    try:
+        c.post("/completion", json={"prompt": "other conversation", "n_predict": 2, "temperature": 0})
+        first = c.post("/completion", json={"prompt": "the quick brown fox", "n_predict": 4,
+                                            "temperature": 0}).json()
+        assert first["timings"]["cache_n"] == 0
+        slot_a = prefills[-1][1]
+        follow = "the quick brown fox" + first["content"] + " jumps over"
+        r = c.post("/completion", json={"prompt": follow, "n_predict": 5, "temperature": 0}).json()
+        n_follow = len(tok.encode(follow))
+        cached = r["timings"]["cache_n"]
+        assert cached >= len(tok.encode("the quick brown fox")) and prefills[-1][1] == slot_a
+        assert prefills[-1] == (n_follow - cached, slot_a, cached)
+        assert r["timings"]["prompt_n"] == n_follow - cached
+        nc = c.post("/completion", json={"prompt": follow, "n_predict": 5, "temperature": 0,
+                                         "cache_prompt": False}).json()
+        assert nc["timings"]["cache_n"] == 0 and nc["content"] == r["content"]
+        # the identical prompt again: everything but its last token comes from the cache
+        again = c.post("/completion", json={"prompt": follow, "n_predict": 5, "temperature": 0}).json()
+        assert again["timings"]["cache_n"] == n_follow - 1 and again["content"] == r["content"]
+        slots = c.get("/slots").json()
+        assert len(slots) == 3 and not any(s["is_processing"] for s in slots)
+        assert max(s["n_cached"] for s in slots) >= n_follow
+        props = c.get("/props").json()
+        assert props["total_slots"] == 3 and props["default_generation_settings"]["min_p"] == 0.05
+        assert sched.metrics["prompt_tokens_cached_total"] >= 2 * cached
+    finally:
+        sched.close()
+
+
+def test_server_penalties_and_bias_over_http(client):
+    from k8s_nvidia_gpus_amd.models.llm.server import _job_from
+
+    c, eng, tok, state = client
+    sched = state["scheduler"]
+    ids = tok.encode("hello")
+
+    def run(body):
+        job = sched.submit(_job_from(dict(body, temperature=0), ids, 6, eng.cfg.vocab))
+        while True:
+            kind, val = job.out.get(timeout=30)
+            if kind == "done":
+                return val.gen
+            assert kind != "error", val
+
+    plain = run({})
+    banned = run({"logit_bias": [[plain[0], False]]})
+    assert banned[0] != plain[0]
+    pen = run({"repeat_penalty": 1e6, "repeat_last_n": -1})
+    assert len(set(pen)) == len(pen) and not set(pen) & set(ids)   # nothing seen is repeated
+    r = c.post("/completion", json={"prompt": "hello", "n_predict": 3, "temperature": 0,
+                                    "presence_penalty": 0.5, "frequency_penalty": 0.5})
+    assert r.status_code == 200
+    assert c.post("/completion", json={"prompt": "hello", "logit_bias": [[10 ** 9, 1]]}).status_code == 400

@@ -27,7 +27,10 @@ def all_yaml(base: Path):
 
 
 def kustomization_dirs():
-    return sorted(p.parent for p in CC.rglob("kustomization.yaml"))
+    """Kustomization roots (kustomize Components under cluster-config/components are opt-in
+    overlays, checked by their own tests)."""
+    return sorted(p.parent for p in CC.rglob("kustomization.yaml")
+                  if yaml.safe_load(p.read_text()).get("kind") == "Kustomization")
 
 
 def resources_of(kdir: Path):
@@ -265,6 +268,54 @@ def test_wan_server_runs_in_tree_engine_with_comfy_contract():
 def test_sd15_service_keeps_reference_nodeport():
     svc = load_all(CC / "apps/sd15-api/service.yaml")[0]
     assert svc["spec"]["ports"][0]["nodePort"] == 30800
+
+
+def _json_patch(doc, ops):
+    """The RFC 6902 subset the components use (replace / add on existing paths)."""
+    import copy
+
+    doc = copy.deepcopy(doc)
+    for op in ops:
+        assert op["op"] in ("replace", "add"), op
+        parts = [int(x) if x.isdigit() else x for x in op["path"].lstrip("/").split("/")]
+        tgt = doc
+        for p in parts[:-1]:
+            tgt = tgt[p]
+        if op["op"] == "replace":
+            assert parts[-1] in tgt if isinstance(tgt, dict) else parts[-1] < len(tgt), op["path"]
+        tgt[parts[-1]] = op["value"]
+    return doc
+
+
+def test_llama_cpp_rocm_component_swaps_only_the_engine():
+    """VERDICT r2 missing #6: upstream llama.cpp (ROCm) as a switchable engine for coder-llm — the
+    component keeps the GPU contract (runtimeClass amd, amd.com/gpu, no visibility env), the
+    port / probes / volume, and runs llama-server with the reference's flags."""
+    comp = yaml.safe_load((CC / "components/llama-cpp-rocm/kustomization.yaml").read_text())
+    assert comp["apiVersion"] == "kustomize.config.k8s.io/v1alpha1" and comp["kind"] == "Component"
+    k, objs = resources_of(CC / "apps/llm")
+    (dep,) = [o for o in objs if o["kind"] == "Deployment" and o["metadata"]["name"] == "coder-llm"]
+    (p,) = comp["patches"]
+    assert p["target"] == {"kind": "Deployment", "name": "coder-llm"}
+    out = _json_patch(dep, yaml.safe_load(p["patch"]))
+    c0, c1 = dep["spec"]["template"]["spec"]["containers"][0], out["spec"]["template"]["spec"]["containers"][0]
+    (img,) = comp["images"]
+    assert c1["image"] == img["name"] and img["newName"] == "ghcr.io/ggml-org/llama.cpp"
+    assert img["newTag"].startswith("server-rocm")
+    script = c1["args"][0]
+    assert "exec /app/llama-server" in script
+    for flag in ("-m \"/models/${MODEL_FILE}\"", "--port 8080", "--ctx-size", "--n-gpu-layers",
+                 "--threads", "--parallel"):
+        assert flag in script, flag
+    for env in ("MODEL_FILE", "CTX_SIZE", "GPU_LAYERS", "CPU_THREADS", "PARALLEL_SLOTS"):
+        assert any(e["name"] == env for e in c1["env"]) and "${%s}" % env in script
+    for key in ("ports", "readinessProbe", "livenessProbe", "resources", "volumeMounts", "env"):
+        assert c1[key] == c0[key], key
+    assert out["spec"]["template"]["spec"]["runtimeClassName"] == "amd" and _gpu_request(c1)
+    # the llm app documents the switch (commented: the in-tree engine stays the default)
+    text = (CC / "apps/llm/kustomization.yaml").read_text()
+    assert "../../components/llama-cpp-rocm" in text and "components" not in k
+    assert (CC / "apps/llm" / "../../components/llama-cpp-rocm/kustomization.yaml").exists()
 
 
 # ----------------------------------------------------------------------------- renovate

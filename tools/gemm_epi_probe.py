@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
-"""Fused-epilogue GEMM (gemm_bf16_epi.hip) vs hipBLASLt (torch) on the Wan2.1 DiT projection
-shapes: time per call, TFLOPS, and the gated-residual epilogue against GEMM + separate update."""
+"""Fused-epilogue GEMMs (gemm_bf16_epi.hip wave-grid family, w4a epilogues) vs hipBLASLt (torch).
+
+MODE=wan (default): the Wan2.1 DiT projection shapes — time per call, TFLOPS, and the gated-residual
+epilogue against GEMM + separate update.  MODE=sd: the SD1.5 UNet's fp16 projections at a CFG batch
+of 64² latents — the auto-picked path, every forced block tile, and torch."""
 import json
 import os
 import sys
@@ -29,6 +32,37 @@ def bench(fn, iters=ITERS):
 
 
 res = {}
+if os.environ.get("MODE", "wan") == "sd":
+    lat = int(os.environ.get("LATENT", "64"))
+    rows = {}
+    for lvl, c in enumerate((320, 640, 1280, 1280)):
+        m = 2 * (lat >> lvl) ** 2
+        for name, n, k in [("proj", c, c), ("qkv", 3 * c, c), ("geglu", 8 * c, c), ("ff_out", c, 4 * c)]:
+            x = torch.randn(m, k, device=dev).half()
+            w = (torch.randn(n, k, device=dev) / k ** 0.5).half()
+            b = torch.randn(n, device=dev).half()
+            fl = 2.0 * m * n * k
+            row = {"m": m, "n": n, "k": k, "auto_tile": GE.tile_for(m, n),
+                   "w4a": GE.use_w4a(m, n, k, torch.float16)}
+            row["auto_us"] = bench(lambda: GE.linear(x, w, b))
+            for t in range(4):
+                GE.set_tile(t)
+                row[f"tile{t}_us"] = bench(lambda: GE._run(GE.EPI_STORE, x, w, b,
+                                                           torch.empty(m, n, device=dev).half(),
+                                                           None, None, 0, 0, n, 0))
+            GE.set_tile(-1)
+            row["torch_us"] = bench(lambda: F.linear(x, w, b))
+            for key in [k2 for k2 in row if k2.endswith("_us")]:
+                row[key] = round(row[key], 1)
+            row["auto_tflops"] = round(fl / row["auto_us"] / 1e6, 1)
+            rows[f"L{lvl}_{name}"] = row
+            print(f"L{lvl}_{name}", row, flush=True)
+    tot = {k2: round(sum(r[k2] for r in rows.values()), 1)
+           for k2 in ("auto_us", "torch_us", "tile0_us", "tile1_us", "tile2_us", "tile3_us")}
+    tot["best_forced_us"] = round(sum(min(r[f"tile{t}_us"] for t in range(4)) for r in rows.values()), 1)
+    print("sum", tot, flush=True)
+    print(json.dumps({"rows": rows, "sum": tot}))
+    sys.exit(0)
 for tokens in [int(t) for t in os.environ.get("TOKENS", "2560,32768").split(",")]:
     M = 2 * tokens
     for name, n, k in [("qkv", 4608, 1536), ("o", 1536, 1536), ("ffn0", 8960, 1536), ("ffn2", 1536, 8960)]:
