@@ -116,9 +116,10 @@ __device__ __forceinline__ uint2 pack4(f32x4 v) {
 }
 
 __device__ __forceinline__ float gelu_tanh(float v) {
-  // 0.5 v (1 + tanh(√(2/π)(v + 0.044715 v³))) = v · sigmoid(2u) = v / (1 + exp(−2u))
-  const float u = 0.7978845608028654f * fmaf(0.044715f * v, v * v, v);
-  return v / (1.f + __expf(-2.f * u));
+  // 0.5 v (1 + tanh(√(2/π)(v + 0.044715 v³))) = v · sigmoid(2u) = v / (1 + 2^t), t = −2u·log2 e:
+  // one v_exp_f32 and one v_rcp_f32 (no IEEE division sequence — the epilogue is VALU-bound)
+  const float t = v * fmaf(-0.10294324f, v * v, -2.3022082f);
+  return v * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(t));
 }
 
 template <int EPI, bool F16, int WM, int WN>
@@ -328,7 +329,9 @@ int amdk8s_gemm_epi_supported(int M, int N, int K) {
 }
 
 // Block tile for an M × N problem: the largest of 256×128, 128×128, 128×64, 64×64 whose grid
-// covers the 256 CUs (else 64×64).  amdk8s_gemm_epi_set_tile(0..3) or AMDK8S_GEMM_EPI_TILE pins
+// nearly covers the 256 CUs (>= 224 workgroups; else 64×64).  Measured (profiles/r03/e): the Wan
+// o / ffn2 projections at 2 × 2560 rows run 240 256×128 tiles 20-30 % faster than 480 128×128 ones,
+// while the SD1.5 deep-level projections (M = 128 … 2048) want the small tiles.  amdk8s_gemm_epi_set_tile(0..3) or AMDK8S_GEMM_EPI_TILE pins
 // one (A/B sweeps); -1 restores the heuristic.
 static const int kTiles[4][2] = {{256, 128}, {128, 128}, {128, 64}, {64, 64}};
 static int g_tile = -2;   // -2: not initialised from the environment yet
@@ -344,7 +347,7 @@ int amdk8s_gemm_epi_tile(int M, int N) {
   for (int i = 0; i < 3; ++i) {
     const long nwg = (long)((M + kTiles[i][0] - 1) / kTiles[i][0]) *
                      ((N + kTiles[i][1] - 1) / kTiles[i][1]);
-    if (nwg >= 256) return i;
+    if (nwg >= 224) return i;
   }
   return 3;
 }

@@ -85,8 +85,10 @@ struct W4aResid {
 };
 
 __device__ __forceinline__ float w4a_gelu_tanh(float v) {
-  const float u = 0.7978845608028654f * fmaf(0.044715f * v, v * v, v);
-  return v / (1.f + __expf(-2.f * u));
+  // 0.5 v (1 + tanh(√(2/π)(v + 0.044715 v³))) = v · sigmoid(2u) = v / (1 + 2^t), t = −2u·log2 e:
+  // one v_exp_f32 and one v_rcp_f32 (no IEEE division sequence — the epilogue is VALU-bound)
+  const float t = v * fmaf(-0.10294324f, v * v, -2.3022082f);
+  return v * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(t));
 }
 
 template <int SCHED, int EPI = kEpiNone>

@@ -646,6 +646,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   float* __restrict__ pml = a.pml;
   __shared__ float qs[G][kHeadDim];
   __shared__ __align__(16) uint16_t knew[kHeadDim];   // the new position's rotated K (fp16)
+  __shared__ __align__(16) uint16_t vnew[kHeadDim];   // and its V
   __shared__ float ps[G][kAttnChunk];
   __shared__ float mls[G][2];
   __shared__ float opart[4][G][kHeadDim];
@@ -673,6 +674,17 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
                                                      * kHeadDim + qd * 32);
 #pragma unroll
     for (int c = 0; c < 4; ++c) kv[c] = kr[c];
+  }
+  // V rows too (P.V: wave w → positions w*16 .. w*16+15, lane = 2 dims): independent of the
+  // scores, so their HBM round trip overlaps the K one instead of following the softmax
+  uint32_t vv[16];
+  {
+    const uint32_t* vr = reinterpret_cast<const uint32_t*>(vc + cbase) + lane;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int p = min(wave * 16 + j, n - 1);        // ps[.][p >= n] == 0
+      vv[j] = vr[(long)(p0 + p) * (kHeadDim / 2)];
+    }
   }
   const int pnew = len - 1;
   const bool own = a.qkv != nullptr && pnew >= p0 && pnew < p0 + kAttnChunk;
@@ -702,7 +714,9 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
         knew[j + kHeadDim / 2] = h1;
       } else if (threadIdx.x < kHeadDim / 2 + kHeadDim) {
         const int e = threadIdx.x - kHeadDim / 2;
-        a.vc[cpos + e] = f2h(row[(H + Hkv + kh) * kHeadDim + e]);
+        const uint16_t hv = f2h(row[(H + Hkv + kh) * kHeadDim + e]);
+        a.vc[cpos + e] = hv;
+        vnew[e] = hv;
       }
     }
   } else {
@@ -713,6 +727,12 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   if (own && p0 + pi == pnew) {   // the new position: its K row was loaded before it was written
 #pragma unroll
     for (int c = 0; c < 4; ++c) kv[c] = reinterpret_cast<const uint4*>(knew)[qd * 4 + c];
+  }
+  if (own) {                      // ... and so was its V row
+    const int jn = pnew - p0 - wave * 16;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j == jn) vv[j] = reinterpret_cast<const uint32_t*>(vnew)[lane];
   }
   float sc[G];
 #pragma unroll
@@ -757,21 +777,12 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
     }
   }
   __syncthreads();
-  // P.V: wave w → positions w*16 .. w*16+15
-  uint32_t vv[16];
-  const uint32_t* vr = reinterpret_cast<const uint32_t*>(vc + cbase) + lane;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int p = min(wave * 16 + j, n - 1);        // ps[.][p >= n] == 0
-    vv[j] = vr[(long)(p0 + p) * (kHeadDim / 2)];
-  }
+  // P.V: wave w → positions w*16 .. w*16+15 (rows loaded at the top)
   float o[G][2];
 #pragma unroll
   for (int g = 0; g < G; ++g) o[g][0] = o[g][1] = 0.f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    // V rows are loaded after the barrier that follows this workgroup's own KV write, so the
-    // new position reads back what was just stored (workgroup-scope visibility)
     const float v0 = h2f(vv[j] & 0xffffu), v1 = h2f(vv[j] >> 16);
 #pragma unroll
     for (int g = 0; g < G; ++g) {

@@ -45,10 +45,10 @@ if os.environ.get("MODE", "wan") == "sd":
             row = {"m": m, "n": n, "k": k, "auto_tile": GE.tile_for(m, n),
                    "w4a": GE.use_w4a(m, n, k, torch.float16)}
             row["auto_us"] = bench(lambda: GE.linear(x, w, b))
+            out = torch.empty(m, n, device=dev).half()
             for t in range(4):
                 GE.set_tile(t)
-                row[f"tile{t}_us"] = bench(lambda: GE._run(GE.EPI_STORE, x, w, b,
-                                                           torch.empty(m, n, device=dev).half(),
+                row[f"tile{t}_us"] = bench(lambda: GE._run(GE.EPI_STORE, x, w, b, out,
                                                            None, None, 0, 0, n, 0))
             GE.set_tile(-1)
             row["torch_us"] = bench(lambda: F.linear(x, w, b))
