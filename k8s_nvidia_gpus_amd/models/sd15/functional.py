@@ -15,8 +15,13 @@ Ops (all activations are channels-last, i.e. NHWC memory = ``[N, H*W, C]`` token
   projection output.
 * ``geglu(x)`` — ``h * gelu(g)`` for ``x = [h | g]`` (the transformer feed-forward's gate).
 * ``linear(x, w, b)`` — the transformer projections (fused q|k|v, cross k|v, out, GEGLU in / out,
-  the 1×1 proj_in / proj_out convolutions as token GEMMs) on the hand-written 256×128-tile gfx950
-  GEMM (``ops/csrc/gemm_bf16_epi.hip``, fp16 operands, bias in the epilogue).
+  the 1×1 proj_in / proj_out convolutions as token GEMMs) on the hand-written gfx950 GEMMs
+  (``ops/csrc/gemm_bf16_epi.hip``: tile picked by problem size; fp16 operands, bias in the
+  epilogue).
+* ``conv3x3(x, conv, bias, stride, up, residual)`` — the 3×3 convolutions (ResNet conv1 / conv2,
+  down- and up-samplers) as implicit GEMMs on the same kernel family: padding taps read a zero row,
+  the nearest-2× upsample is folded into the input addressing, and conv2's bias + the block's
+  residual (or 1×1-shortcut output) ride in the epilogue — no MIOpen, no separate add pass.
 """
 from __future__ import annotations
 
@@ -68,6 +73,51 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -
         if gemm_epi.supported(x, w):
             return gemm_epi.linear(x, w, b)
     return F.linear(x, w, b)
+
+
+_CONV = os.environ.get("AMDK8S_SD_CONV", "native")   # native | torch (A/B against MIOpen)
+
+
+def _conv_weight(conv: torch.nn.Conv2d, dtype: torch.dtype) -> torch.Tensor:
+    """The kernel's [Cout, 9·Cin] weight, packed once per (weight version, dtype)."""
+    from k8s_nvidia_gpus_amd.ops import gemm_epi
+
+    w = conv.weight
+    key = (w.data_ptr(), w._version, dtype)
+    cached = getattr(conv, "_amdk8s_wk", None)
+    if cached is None or cached[0] != key:
+        cached = (key, gemm_epi.conv_weight(w.detach().to(dtype)))
+        conv._amdk8s_wk = cached
+    return cached[1]
+
+
+def conv3x3(x: torch.Tensor, conv: torch.nn.Conv2d, bias: Optional[torch.Tensor] = None,
+            stride: int = 1, up: bool = False, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``conv2d(up2(x) if up else x, conv.weight, bias, stride, padding=1) (+ residual)``."""
+    if _CONV != "torch" and _native(x):
+        from k8s_nvidia_gpus_amd.ops import gemm_epi as GE
+
+        if GE.conv3x3_supported(x, conv.out_channels) and stride in (1, 2) and not (up and stride != 1) \
+                and (residual is None or (residual.dtype == x.dtype and residual.is_contiguous(
+                    memory_format=torch.channels_last))):
+            mode = GE.CONV_UP2 if up else (GE.CONV_S2 if stride == 2 else GE.CONV_S1)
+            return GE.conv3x3(x, _conv_weight(conv, x.dtype), bias, mode, residual)
+    if up:
+        x = F.interpolate(x, scale_factor=2.0, mode="nearest")
+        if x.device.type == "cuda":
+            x = x.contiguous(memory_format=torch.channels_last)
+    y = F.conv2d(x, conv.weight, bias, stride=stride, padding=1)
+    return y if residual is None else add3(residual, y, None)
+
+
+def conv1x1(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """1×1 convolution of a channels-last NCHW tensor as a token-row GEMM (no copies)."""
+    n, c, h, wd = x.shape
+    if _native(x) and x.is_contiguous(memory_format=torch.channels_last):
+        rows = x.permute(0, 2, 3, 1).reshape(-1, c)
+        out = linear(rows, w.view(w.shape[0], c), bias)
+        return out.view(n, h, wd, -1).permute(0, 3, 1, 2)
+    return F.conv2d(x, w, bias)
 
 
 # ---------------------------------------------------------------- GroupNorm (+SiLU)

@@ -5,7 +5,7 @@ Module and parameter names follow the diffusers SD1.5 state dict (``down_blocks.
 safetensors files with no renaming table.  The compute is laid out for MI355X instead of mirroring
 diffusers' module graph:
 
-* activations stay channels-last (NHWC memory) end to end: MIOpen's NHWC convolutions, and the
+* activations stay channels-last (NHWC memory) end to end: implicit-GEMM 3×3 conv kernels, and the
   transformer's token rows ``[N, H*W, C]`` are a free view of the same memory (no permute copies
   around every Transformer2D);
 * GroupNorm + SiLU is one kernel (``functional.group_norm(..., silu=True)``);
@@ -101,18 +101,17 @@ class ResnetBlock2D(nn.Module):
 
     def forward(self, x, temb=None):
         """``temb``: ``silu(temb)`` [N, 1280], a :class:`TembAddends`, or None (VAE)."""
-        h = F.conv2d(self.norm1(x, silu=True), self.conv1.weight, None, padding=1)
+        h = SF.conv3x3(self.norm1(x, silu=True), self.conv1)
         h = self.norm2(h, silu=True, add=self._addend(temb, x.shape[0]))
-        h = F.conv2d(h, self.conv2.weight, None, padding=1)
         if self.conv_shortcut is not None:
-            sc = F.conv2d(x, self.conv_shortcut.weight, None)
+            sc = SF.conv1x1(x, self.conv_shortcut.weight)
         else:
             sc = x
         bias = self._out_bias
         if bias is None or bias.device != h.device or bias.dtype != h.dtype:
             bias = self.conv2.bias if self.conv_shortcut is None \
                 else self.conv2.bias + self.conv_shortcut.bias
-        return SF.add3(sc, h, bias)
+        return SF.conv3x3(h, self.conv2, bias, residual=sc)   # conv2 + biases + shortcut, one pass
 
 
 class Attention(nn.Module):
@@ -236,7 +235,7 @@ class Downsample2D(nn.Module):
         self.conv = nn.Conv2d(channels, channels, 3, stride=2, padding=1)
 
     def forward(self, x):
-        return self.conv(x)
+        return SF.conv3x3(x, self.conv, self.conv.bias, stride=2)
 
 
 class Upsample2D(nn.Module):
@@ -248,13 +247,12 @@ class Upsample2D(nn.Module):
         """Nearest 2x, or to ``size`` — the next skip's spatial size, which differs from 2x when a
         latent side is not a multiple of 8 (e.g. 520 px → latent 65 → 33 → 17 → 9 → back up to 17),
         as diffusers' ``forward_upsample_size`` does."""
-        if size is None:
-            x = F.interpolate(x, scale_factor=2.0, mode="nearest")
-        else:
-            x = F.interpolate(x, size=tuple(size), mode="nearest")
+        if size is None or tuple(size) == (2 * x.shape[-2], 2 * x.shape[-1]):
+            return SF.conv3x3(x, self.conv, self.conv.bias, up=True)   # upsample folded in
+        x = F.interpolate(x, size=tuple(size), mode="nearest")
         if x.device.type == "cuda":
             x = x.contiguous(memory_format=torch.channels_last)
-        return self.conv(x)
+        return SF.conv3x3(x, self.conv, self.conv.bias)
 
 
 class VAEAttention(nn.Module):

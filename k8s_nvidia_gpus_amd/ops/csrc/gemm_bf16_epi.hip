@@ -66,17 +66,31 @@ struct Geo {
   static_assert(BM * CF_STRIDE <= RING, "fp32 epilogue image must fit the ring");
 };
 
-enum Epi { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID = 2 };
+enum Epi { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_ADD = 3,
+           EPI_PARTIAL = 4 };   // split-K: fp32 atomic accumulation into a zeroed workspace
+
+// Implicit-GEMM 3×3 convolution (pad 1) over NHWC activations: the A "row" of output pixel m at
+// K-tile t is the 64-channel slice t % (Cin/64) of input pixel (tap t / (Cin/64)) — a 128-B run
+// of the NHWC tensor, or a zero row where the tap falls in the padding.
+enum ConvMode { CONV_NONE = 0, CONV_S1 = 1, CONV_S2 = 2, CONV_UP2 = 3 };
 
 struct Args {
   const uint16_t* A;
   const uint16_t* B;
   const uint16_t* bias;   // [N] bf16 / fp16 (operand dtype) or null
-  uint16_t* out;          // bf16 / fp16 output (STORE / GELU)
+  uint16_t* out;          // bf16 / fp16 output (STORE / GELU / ADD)
   float* x;               // fp32 residual stream (RESID)
   const float* gate;      // [M / rows_per_gate][gate_stride] fp32 or null (RESID)
-  int M, N, K, lda, ldb, ldo, ldx, rows_per_gate, gate_stride;
+  const uint16_t* r;      // [M][ldr] 16-bit addend (ADD: out = Y + bias + r; may alias out)
+  int M, N, K, lda, ldb, ldo, ldx, rows_per_gate, gate_stride, ldr;
+  int splits;             // K split across `splits` workgroups per tile (EPI_PARTIAL), else 1
+  float* ws;              // [M][N] fp32 split-K workspace (EPI_PARTIAL)
+  // convolution geometry (CONV != CONV_NONE): input [batch][Hin][Win][Cin], output Hout × Wout
+  int Hin, Win, Hout, Wout, Cin;
 };
+
+// 128 B of zeros: the LDS-DMA source of padding rows.
+__device__ __attribute__((aligned(16))) uint4 g_zero_row[8];
 
 __device__ __forceinline__ void barrier_raw() {
   __builtin_amdgcn_sched_barrier(0);
@@ -122,7 +136,7 @@ __device__ __forceinline__ float gelu_tanh(float v) {
   return v * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(t));
 }
 
-template <int EPI, bool F16, int WM, int WN>
+template <int EPI, bool F16, int WM, int WN, int CONV = CONV_NONE>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
   using G = Geo<WM, WN>;
   constexpr int BM = G::BM, BN = G::BN, NW = G::NW, NT = G::NT, LA = G::LA, LB = G::LB;
@@ -140,10 +154,15 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
   const int tiles_m = (a.M + BM - 1) / BM;
   const int tiles_n = (a.N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n;
-  int wgid;
+  int wgid, split = 0;
   {
-    const int bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int tot = nwg * a.splits;
+    const int bid = blockIdx.x, xcd = bid & 7, q = tot >> 3, r = tot & 7;
     wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    if (EPI == EPI_PARTIAL) {
+      split = wgid / nwg;
+      wgid -= split * nwg;
+    }
   }
   const int group = wgid / (GROUP_M * tiles_n);
   const int first_m = group * GROUP_M;
@@ -157,13 +176,41 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
   const size_t lda_b = (size_t)a.lda * 2, ldb_b = (size_t)a.ldb * 2;
   const char* a_src[LA];
   const char* b_src[LB];
+  // convolution: per A row, the output pixel's coordinates and (stride 1 / 2) the taps that land
+  // inside the input; a_src = input pixel (y·s, x·s) (or the image base for UP2) + this lane's chunk
+  int cv_yx[CONV ? LA : 1], cv_mask[CONV ? LA : 1];
+  const char* zsrc = reinterpret_cast<const char*>(g_zero_row) + (lane & 7) * 16;
+  const size_t cin_b = (size_t)a.Cin * 2;
 #pragma unroll
   for (int j = 0; j < LA; ++j) {
     const int q = j * NW + wave, row = q * 8 + (lane >> 3);
     const int c = (lane & 7) ^ ((row >> 1) & 7);
     const int grow = min(m0 + row, a.M - 1);     // M tail: clamped rows, never stored
-    a_src[j] = reinterpret_cast<const char*>(a.A) + (size_t)grow * lda_b + c * 16;
+    if constexpr (CONV == CONV_NONE) {
+      a_src[j] = reinterpret_cast<const char*>(a.A) + (size_t)grow * lda_b + c * 16;
+    } else {
+      const int hw = a.Hout * a.Wout;
+      const int img = grow / hw, rem = grow - img * hw;
+      const int y = rem / a.Wout, x = rem - y * a.Wout;
+      cv_yx[j] = (y << 16) | x;
+      if constexpr (CONV == CONV_UP2) {
+        a_src[j] = reinterpret_cast<const char*>(a.A) + (size_t)img * a.Hin * a.Win * cin_b + c * 16;
+        cv_mask[j] = 0;
+      } else {
+        constexpr int S = CONV == CONV_S2 ? 2 : 1;
+        int mask = 0;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          const int iy = y * S + tap / 3 - 1, ix = x * S + tap % 3 - 1;
+          if ((unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win) mask |= 1 << tap;
+        }
+        cv_mask[j] = mask;
+        a_src[j] = reinterpret_cast<const char*>(a.A) +
+                   ((size_t)(img * a.Hin + y * S) * a.Win + x * S) * cin_b + c * 16;
+      }
+    }
   }
+  const int cpt = a.Cin >> 6;                    // K-tiles per tap
 #pragma unroll
   for (int j = 0; j < LB; ++j) {
     const int q = j * NW + wave, row = q * 8 + (lane >> 3);
@@ -171,14 +218,38 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
     const int gn = min(n0 + row, a.N - 1);       // N tail: clamped weight rows, never stored
     b_src[j] = reinterpret_cast<const char*>(a.B) + (size_t)gn * ldb_b + c * 16;
   }
-  auto stage = [&](int t) {
-    char* sa = lds + (t % NSTAGE) * STAGE;
+  // K-tiles [t0, t0 + T) of this workgroup (all of K unless split)
+  const int Ttot = a.K / BK;
+  const int t0 = (int)((long)Ttot * split / a.splits);
+  const int T = (int)((long)Ttot * (split + 1) / a.splits) - t0;
+  auto stage = [&](int i) {                      // ring slot i % NSTAGE ← absolute K-tile t0 + i
+    const int t = t0 + i;
+    char* sa = lds + (i % NSTAGE) * STAGE;
     char* sb = sa + A_STAGE;
     const size_t kb = (size_t)t * BK * 2;
+    if constexpr (CONV == CONV_NONE) {
 #pragma unroll
-    for (int j = 0; j < LA; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(a_src[j] + kb),
-                                       (lds_void*)(sa + (j * NW + wave) * 1024), 16, 0, 0);
+      for (int j = 0; j < LA; ++j)
+        __builtin_amdgcn_global_load_lds((const void*)(a_src[j] + kb),
+                                         (lds_void*)(sa + (j * NW + wave) * 1024), 16, 0, 0);
+    } else {
+      const int tap = t / cpt, cc = t - tap * cpt;  // uniform
+      const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+      const long toff = (long)(dy * a.Win + dx) * (long)cin_b + cc * 128;
+#pragma unroll
+      for (int j = 0; j < LA; ++j) {
+        const char* src;
+        if constexpr (CONV == CONV_UP2) {       // nearest 2× upsample folded into the addressing
+          const int iy = (cv_yx[j] >> 16) + dy, ix = (cv_yx[j] & 0xffff) + dx;
+          const bool ok = (unsigned)iy < (unsigned)a.Hout && (unsigned)ix < (unsigned)a.Wout;
+          src = ok ? a_src[j] + ((long)(iy >> 1) * a.Win + (ix >> 1)) * (long)cin_b + cc * 128 : zsrc;
+        } else {
+          src = ((cv_mask[j] >> tap) & 1) ? a_src[j] + toff : zsrc;
+        }
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (lds_void*)(sa + (j * NW + wave) * 1024), 16, 0, 0);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < LB; ++j)
       __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + kb),
@@ -199,7 +270,6 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int T = a.K / BK;
   stage(0);
   if (T > 1) stage(1);
   for (int t = 0; t < T; ++t) {
@@ -235,6 +305,20 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = mfma16<F16>(bw[1][j], af[1][i], acc[i][j]);
     __builtin_amdgcn_s_setprio(0);
+  }
+  if constexpr (EPI == EPI_PARTIAL) {     // split-K: fp32 atomics straight from the accumulators
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wm * 64 + 16 * i + fr, n = n0 + wn * 64 + 16 * j + 4 * fq;
+        if (m < a.M && n < a.N) {
+          float* w = a.ws + (size_t)m * a.N + n;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) atomicAdd(w + e, acc[i][j][e]);
+        }
+      }
+    return;
   }
   barrier_raw();                         // every wave is done with the ring: reuse it for C
 
@@ -311,11 +395,71 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
 #pragma unroll 4
     for (int it = 0; it < BM / RPP; ++it) {
       const int row = it * RPP + tid / TPR, ch = tid % TPR;
-      if (m0 + row < a.M && n0 + ch * 8 < a.N)
-        *reinterpret_cast<uint4*>(obase + row * ldo_b + ch * 16) =
-            *reinterpret_cast<const uint4*>(lds + row * CB_STRIDE + ch * 16);
+      if (m0 + row < a.M && n0 + ch * 8 < a.N) {
+        uint4 v = *reinterpret_cast<const uint4*>(lds + row * CB_STRIDE + ch * 16);
+        if constexpr (EPI == EPI_ADD) {         // + the 16-bit addend (residual / shortcut)
+          const uint4 rv = *reinterpret_cast<const uint4*>(
+              a.r + (size_t)(m0 + row) * a.ldr + n0 + ch * 8);
+          const uint32_t* pv = reinterpret_cast<const uint32_t*>(&v);
+          const uint32_t* pr = reinterpret_cast<const uint32_t*>(&rv);
+          uint32_t o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const f32x4 s4 = {h2f<F16>((uint16_t)(pv[e] & 0xffffu)) + h2f<F16>((uint16_t)(pr[e] & 0xffffu)),
+                              h2f<F16>((uint16_t)(pv[e] >> 16)) + h2f<F16>((uint16_t)(pr[e] >> 16)),
+                              0.f, 0.f};
+            o[e] = pack4<F16>(s4).x;
+          }
+          v = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        *reinterpret_cast<uint4*>(obase + row * ldo_b + ch * 16) = v;
+      }
     }
   }
+}
+
+// Split-K finalize: out = epi(ws + bias) (+ r), 8 columns per thread (N % 8 == 0).
+template <int EPI, bool F16>
+__global__ void __launch_bounds__(256) splitk_finalize(const Args a) {
+  const long i8 = (long)blockIdx.x * 256 + threadIdx.x;   // 8-column group index
+  const int groups = a.N >> 3;
+  if (i8 >= (long)a.M * groups) return;
+  const int m = (int)(i8 / groups), n = (int)(i8 - (long)m * groups) * 8;
+  const f32x4* w = reinterpret_cast<const f32x4*>(a.ws + (size_t)m * a.N + n);
+  f32x4 v0 = w[0], v1 = w[1];
+  if (a.bias) {
+    const uint4 bv = *reinterpret_cast<const uint4*>(a.bias + n);
+    const uint32_t b32[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      v0[2 * e] += h2f<F16>((uint16_t)(b32[e] & 0xffffu));
+      v0[2 * e + 1] += h2f<F16>((uint16_t)(b32[e] >> 16));
+      v1[2 * e] += h2f<F16>((uint16_t)(b32[e + 2] & 0xffffu));
+      v1[2 * e + 1] += h2f<F16>((uint16_t)(b32[e + 2] >> 16));
+    }
+  }
+  if constexpr (EPI == EPI_GELU) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v0[e] = gelu_tanh(v0[e]);
+      v1[e] = gelu_tanh(v1[e]);
+    }
+  }
+  uint2 p0 = pack4<F16>(v0), p1 = pack4<F16>(v1);
+  if constexpr (EPI == EPI_ADD) {      // round like the fused path: Y to 16 bit, then + r
+    const uint4 rv = *reinterpret_cast<const uint4*>(a.r + (size_t)m * a.ldr + n);
+    const uint32_t pv[4] = {p0.x, p0.y, p1.x, p1.y}, pr[4] = {rv.x, rv.y, rv.z, rv.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f32x4 s4 = {h2f<F16>((uint16_t)(pv[e] & 0xffffu)) + h2f<F16>((uint16_t)(pr[e] & 0xffffu)),
+                        h2f<F16>((uint16_t)(pv[e] >> 16)) + h2f<F16>((uint16_t)(pr[e] >> 16)), 0.f, 0.f};
+      o[e] = pack4<F16>(s4).x;
+    }
+    p0 = make_uint2(o[0], o[1]);
+    p1 = make_uint2(o[2], o[3]);
+  }
+  *reinterpret_cast<uint4*>(a.out + (size_t)m * a.ldo + n) = make_uint4(p0.x, p0.y, p1.x, p1.y);
 }
 
 }  // namespace
@@ -338,6 +482,29 @@ static int g_tile = -2;   // -2: not initialised from the environment yet
 
 void amdk8s_gemm_epi_set_tile(int tile) { g_tile = (tile >= 0 && tile <= 3) ? tile : -1; }
 
+int amdk8s_gemm_epi_tile(int M, int N);
+
+// Split-K factor for a problem whose tile grid cannot fill the chip: enough splits for ~512
+// workgroups, each keeping >= 8 K-tiles (the ring's pipeline depth), at most 16.  1 = no split.
+// AMDK8S_GEMM_SPLITK=0 disables it.
+int amdk8s_gemm_epi_splits(int M, int N, int K) {
+  static int enabled = -1;
+  if (enabled < 0) {
+    const char* e = getenv("AMDK8S_GEMM_SPLITK");
+    enabled = !(e && e[0] == '0' && !e[1]);
+  }
+  if (!enabled) return 1;
+  const int tile = amdk8s_gemm_epi_tile(M, N);
+  const long nwg = (long)((M + kTiles[tile][0] - 1) / kTiles[tile][0]) *
+                   ((N + kTiles[tile][1] - 1) / kTiles[tile][1]);
+  const int T = K / BK;
+  if (nwg >= 224 || T < 16) return 1;
+  int s = (int)((512 + nwg - 1) / nwg);
+  s = s < T / 8 ? s : T / 8;
+  s = s < 16 ? s : 16;
+  return s > 1 ? s : 1;
+}
+
 int amdk8s_gemm_epi_tile(int M, int N) {
   if (g_tile == -2) {
     const char* e = getenv("AMDK8S_GEMM_EPI_TILE");
@@ -352,54 +519,44 @@ int amdk8s_gemm_epi_tile(int M, int N) {
   return 3;
 }
 
-int amdk8s_gemm_epi(int epi, int dtype, const void* A, const void* B, const void* bias, void* out,
-                    float* x, const float* gate, int M, int N, int K, int lda, int ldb, int ldo,
-                    int ldx, int rows_per_gate, int gate_stride, hipStream_t stream) {
-  if (!amdk8s_gemm_epi_supported(M, N, K)) return (int)hipErrorInvalidValue;
-  if (lda % 8 || ldb % 8 || lda < K || ldb < K) return (int)hipErrorInvalidValue;
-  if (((uintptr_t)A | (uintptr_t)B) & 15 || ((uintptr_t)bias & 7)) return (int)hipErrorInvalidValue;
-  if (epi == EPI_RESID) {
-    if (!x || ldx % 4 || ldx < N || ((uintptr_t)x & 15)) return (int)hipErrorInvalidValue;
-    if (gate && (rows_per_gate <= 0 || gate_stride % 4 || ((uintptr_t)gate & 15)))
-      return (int)hipErrorInvalidValue;
-  } else {
-    if (!out || ldo % 8 || ldo < N || ((uintptr_t)out & 15)) return (int)hipErrorInvalidValue;
+}  // extern "C"
+
+namespace {
+
+template <int CONV>
+int launch_epi(Args a, int epi, bool f16, hipStream_t stream) {
+  const int tile = amdk8s_gemm_epi_tile(a.M, a.N);
+  const long nwg = (long)((a.M + kTiles[tile][0] - 1) / kTiles[tile][0]) *
+                   ((a.N + kTiles[tile][1] - 1) / kTiles[tile][1]);
+  const int splits = a.ws && epi != EPI_RESID ? amdk8s_gemm_epi_splits(a.M, a.N, a.K) : 1;
+  if (nwg * splits > 0x7fffffff) return (int)hipErrorInvalidValue;
+  a.splits = splits;
+  if (splits > 1) {
+    const hipError_t e = hipMemsetAsync(a.ws, 0, (size_t)a.M * a.N * sizeof(float), stream);
+    if (e != hipSuccess) return (int)e;
   }
-  // 32-bit row offsets inside one panel are never formed; the full extent must stay addressable
-  Args a;
-  a.A = (const uint16_t*)A;
-  a.B = (const uint16_t*)B;
-  a.bias = (const uint16_t*)bias;
-  a.out = (uint16_t*)out;
-  a.x = x;
-  a.gate = gate;
-  a.M = M;
-  a.N = N;
-  a.K = K;
-  a.lda = lda;
-  a.ldb = ldb;
-  a.ldo = ldo;
-  a.ldx = ldx;
-  a.rows_per_gate = rows_per_gate > 0 ? rows_per_gate : M;
-  a.gate_stride = gate_stride;
-  if (epi < EPI_STORE || epi > EPI_RESID) return (int)hipErrorInvalidValue;
-  const int tile = amdk8s_gemm_epi_tile(M, N);
-  const long nwg = (long)((M + kTiles[tile][0] - 1) / kTiles[tile][0]) *
-                   ((N + kTiles[tile][1] - 1) / kTiles[tile][1]);
-  if (nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
-  const bool f16 = dtype == 0;
   auto go = [&](auto wm, auto wn) {
     constexpr int WM = decltype(wm)::value, WN = decltype(wn)::value;
     constexpr int NT = Geo<WM, WN>::NT;
-    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(nwg), dim3(NT), 0, stream, a); };
-    if (f16) {
+    auto launch = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(nwg * splits), dim3(NT), 0, stream, a);
+    };
+    if (splits > 1) {                          // partial sums; epilogue in splitk_finalize
+      if (f16) launch(gemm_epi_kernel<EPI_PARTIAL, true, WM, WN, CONV>);
+      else launch(gemm_epi_kernel<EPI_PARTIAL, false, WM, WN, CONV>);
+    } else if constexpr (CONV != CONV_NONE) {  // convolutions: fp16 (the SD1.5 UNet / VAE)
+      if (epi == EPI_ADD) launch(gemm_epi_kernel<EPI_ADD, true, WM, WN, CONV>);
+      else launch(gemm_epi_kernel<EPI_STORE, true, WM, WN, CONV>);
+    } else if (f16) {
       if (epi == EPI_STORE) launch(gemm_epi_kernel<EPI_STORE, true, WM, WN>);
       else if (epi == EPI_GELU) launch(gemm_epi_kernel<EPI_GELU, true, WM, WN>);
-      else launch(gemm_epi_kernel<EPI_RESID, true, WM, WN>);
+      else if (epi == EPI_RESID) launch(gemm_epi_kernel<EPI_RESID, true, WM, WN>);
+      else launch(gemm_epi_kernel<EPI_ADD, true, WM, WN>);
     } else {
       if (epi == EPI_STORE) launch(gemm_epi_kernel<EPI_STORE, false, WM, WN>);
       else if (epi == EPI_GELU) launch(gemm_epi_kernel<EPI_GELU, false, WM, WN>);
-      else launch(gemm_epi_kernel<EPI_RESID, false, WM, WN>);
+      else if (epi == EPI_RESID) launch(gemm_epi_kernel<EPI_RESID, false, WM, WN>);
+      else launch(gemm_epi_kernel<EPI_ADD, false, WM, WN>);
     }
   };
   using I1 = std::integral_constant<int, 1>;
@@ -411,7 +568,117 @@ int amdk8s_gemm_epi(int epi, int dtype, const void* A, const void* B, const void
     case 2: go(I2{}, I1{}); break;
     default: go(I1{}, I1{}); break;
   }
+  if (splits > 1) {
+    const long groups = (long)a.M * (a.N / 8);
+    const dim3 grid((unsigned)((groups + 255) / 256));
+    auto fin = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, a); };
+    if (f16) {
+      if (epi == EPI_GELU) fin(splitk_finalize<EPI_GELU, true>);
+      else if (epi == EPI_ADD) fin(splitk_finalize<EPI_ADD, true>);
+      else fin(splitk_finalize<EPI_STORE, true>);
+    } else {
+      if (epi == EPI_GELU) fin(splitk_finalize<EPI_GELU, false>);
+      else if (epi == EPI_ADD) fin(splitk_finalize<EPI_ADD, false>);
+      else fin(splitk_finalize<EPI_STORE, false>);
+    }
+  }
   return (int)hipGetLastError();
+}
+
+int check_out(int epi, int N, const void* out, int ldo, const void* r, int ldr) {
+  if (!out || ldo % 8 || ldo < N || ((uintptr_t)out & 15)) return (int)hipErrorInvalidValue;
+  if (epi == EPI_ADD && (!r || ldr % 8 || ldr < N || ((uintptr_t)r & 15)))
+    return (int)hipErrorInvalidValue;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// epi: 0 store, 1 GELU, 2 fp32 gated residual (x, gate), 3 add (out = Y + bias + r, 16-bit r).
+// ws: optional [M][N] fp32 workspace; when given (and the epilogue is not RESID), problems that
+// cannot fill the chip run split-K (amdk8s_gemm_epi_splits) + a finalize pass.
+int amdk8s_gemm_epi(int epi, int dtype, const void* A, const void* B, const void* bias, void* out,
+                    float* x, const float* gate, const void* r, int M, int N, int K, int lda,
+                    int ldb, int ldo, int ldx, int ldr, int rows_per_gate, int gate_stride,
+                    float* ws, hipStream_t stream) {
+  if (!amdk8s_gemm_epi_supported(M, N, K)) return (int)hipErrorInvalidValue;
+  if (epi < EPI_STORE || epi > EPI_ADD) return (int)hipErrorInvalidValue;
+  if (lda % 8 || ldb % 8 || lda < K || ldb < K) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)A | (uintptr_t)B) & 15 || ((uintptr_t)bias & 7)) return (int)hipErrorInvalidValue;
+  if (epi == EPI_RESID) {
+    if (!x || ldx % 4 || ldx < N || ((uintptr_t)x & 15)) return (int)hipErrorInvalidValue;
+    if (gate && (rows_per_gate <= 0 || gate_stride % 4 || ((uintptr_t)gate & 15)))
+      return (int)hipErrorInvalidValue;
+  } else if (int rc = check_out(epi, N, out, ldo, r, ldr)) {
+    return rc;
+  }
+  Args a{};
+  a.A = (const uint16_t*)A;
+  a.B = (const uint16_t*)B;
+  a.bias = (const uint16_t*)bias;
+  a.out = (uint16_t*)out;
+  a.x = x;
+  a.gate = gate;
+  a.r = (const uint16_t*)r;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldo = ldo;
+  a.ldx = ldx;
+  a.ldr = ldr;
+  a.rows_per_gate = rows_per_gate > 0 ? rows_per_gate : M;
+  a.gate_stride = gate_stride;
+  a.splits = 1;
+  a.ws = ((uintptr_t)ws & 15) ? nullptr : ws;
+  return launch_epi<CONV_NONE>(a, epi, dtype == 0, stream);
+}
+
+// 3×3 convolution, padding 1, fp16 NHWC: x [batch][Hin][Win][Cin] (channels-last, contiguous),
+// w [Cout][3][3][Cin] (the OIHW weight permuted once), out [batch·Hout·Wout][ldo] (NHWC when
+// ldo == Cout).  mode 1: stride 1 (Hout = Hin); 2: stride 2 (Hout = ceil(Hin/2)); 3: nearest 2×
+// upsample then stride 1 (Hout = 2·Hin).  epi 0: out = conv + bias; 3: out = conv + bias + r.
+// Cin % 64 == 0, Cout % 8 == 0.
+int amdk8s_conv3x3_epi(int epi, int mode, const void* X, const void* W, const void* bias,
+                       void* out, const void* r, int batch, int Hin, int Win, int Cin, int Cout,
+                       int ldo, int ldr, float* ws, hipStream_t stream) {
+  if (epi != EPI_STORE && epi != EPI_ADD) return (int)hipErrorInvalidValue;
+  if (mode < CONV_S1 || mode > CONV_UP2 || batch <= 0 || Hin <= 0 || Win <= 0) return (int)hipErrorInvalidValue;
+  if (Cin % 64 || Cout % 8 || Cout <= 0) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)X | (uintptr_t)W) & 15 || ((uintptr_t)bias & 7)) return (int)hipErrorInvalidValue;
+  if (int rc = check_out(epi, Cout, out, ldo, r, ldr)) return rc;
+  const int Hout = mode == CONV_S1 ? Hin : mode == CONV_S2 ? (Hin + 1) / 2 : 2 * Hin;
+  const int Wout = mode == CONV_S1 ? Win : mode == CONV_S2 ? (Win + 1) / 2 : 2 * Win;
+  if (Hout >= 32768 || Wout >= 32768) return (int)hipErrorInvalidValue;   // packed (y, x)
+  const long M = (long)batch * Hout * Wout;
+  if (M > 0x7fffffff) return (int)hipErrorInvalidValue;
+  Args a{};
+  a.A = (const uint16_t*)X;
+  a.B = (const uint16_t*)W;
+  a.bias = (const uint16_t*)bias;
+  a.out = (uint16_t*)out;
+  a.r = (const uint16_t*)r;
+  a.M = (int)M;
+  a.N = Cout;
+  a.K = 9 * Cin;
+  a.lda = Cin;
+  a.ldb = 9 * Cin;
+  a.ldo = ldo;
+  a.ldr = ldr;
+  a.rows_per_gate = a.M;
+  a.Hin = Hin;
+  a.Win = Win;
+  a.Hout = Hout;
+  a.Wout = Wout;
+  a.Cin = Cin;
+  a.splits = 1;
+  a.ws = ((uintptr_t)ws & 15) ? nullptr : ws;
+  if (mode == CONV_S1) return launch_epi<CONV_S1>(a, epi, true, stream);
+  if (mode == CONV_S2) return launch_epi<CONV_S2>(a, epi, true, stream);
+  return launch_epi<CONV_UP2>(a, epi, true, stream);
 }
 
 }  // extern "C"

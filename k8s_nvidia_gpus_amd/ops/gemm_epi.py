@@ -20,7 +20,8 @@ import torch
 
 from .kernels import library
 
-EPI_STORE, EPI_GELU, EPI_RESID = 0, 1, 2
+EPI_STORE, EPI_GELU, EPI_RESID, EPI_ADD = 0, 1, 2, 3
+CONV_S1, CONV_S2, CONV_UP2 = 1, 2, 3
 _declared = False
 _lock = threading.Lock()
 
@@ -33,8 +34,13 @@ def _lib():
             vp, ci = ctypes.c_void_p, ctypes.c_int
             lib.amdk8s_gemm_epi_supported.argtypes = [ci, ci, ci]
             lib.amdk8s_gemm_epi_supported.restype = ci
-            lib.amdk8s_gemm_epi.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci,
-                                            ci, ci, ci, vp]
+            lib.amdk8s_gemm_epi.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci,
+                                            ci, ci, ci, ci, ci, vp, vp]
+            lib.amdk8s_conv3x3_epi.argtypes = [ci, ci, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci,
+                                               ci, vp, vp]
+            lib.amdk8s_gemm_epi_splits.argtypes = [ci, ci, ci]
+            lib.amdk8s_gemm_epi_splits.restype = ci
+            lib.amdk8s_conv3x3_epi.restype = ci
             lib.amdk8s_gemm_epi.restype = ci
             lib.amdk8s_gemm_w4a_epi.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci,
                                                 ci, ci, ci, vp]
@@ -92,14 +98,29 @@ def _bias(b: Optional[torch.Tensor], n: int, dtype: torch.dtype) -> Optional[tor
     return b
 
 
-def _run(epi, x2, w, b, out, res, gate, rows_per_gate, gate_stride, ldo, ldx):
+def _ptr(t: Optional[torch.Tensor]):
+    return t.data_ptr() if t is not None else None
+
+
+def splits(m: int, n: int, k: int) -> int:
+    """Split-K factor the kernels use for an m × n × k problem (1 = none)."""
+    return _lib().amdk8s_gemm_epi_splits(m, n, k)
+
+
+def _workspace(epi: int, m: int, n: int, k: int, dev) -> Optional[torch.Tensor]:
+    if epi == EPI_RESID or splits(m, n, k) <= 1:
+        return None
+    return torch.empty(m * n, dtype=torch.float32, device=dev)
+
+
+def _run(epi, x2, w, b, out, res, gate, rows_per_gate, gate_stride, ldo, ldx, r=None, ldr=0):
     m, k = x2.shape
     n = w.shape[0]
+    ws = _workspace(epi, m, n, k, x2.device)
     rc = _lib().amdk8s_gemm_epi(
-        epi, _DT[x2.dtype], x2.data_ptr(), w.data_ptr(), b.data_ptr() if b is not None else None,
-        out.data_ptr() if out is not None else None, res.data_ptr() if res is not None else None,
-        gate.data_ptr() if gate is not None else None, m, n, k, x2.stride(0), w.stride(0), ldo, ldx,
-        rows_per_gate, gate_stride, _stream(x2))
+        epi, _DT[x2.dtype], x2.data_ptr(), w.data_ptr(), _ptr(b), _ptr(out), _ptr(res), _ptr(gate),
+        _ptr(r), m, n, k, x2.stride(0), w.stride(0), ldo, ldx, ldr, rows_per_gate, gate_stride,
+        _ptr(ws), _stream(x2))
     if rc != 0:
         raise RuntimeError(f"amdk8s_gemm_epi failed (rc={rc}, M={m} N={n} K={k}, epi={epi})")
 
@@ -182,3 +203,56 @@ def linear_residual_(res: torch.Tensor, x: torch.Tensor, w: torch.Tensor,
     else:
         _run(EPI_RESID, x2, w, bb, None, res, gate, rows_per_gate, gstride, 0, n)
     return res
+
+
+def linear_add(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], r: torch.Tensor,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``x·wᵀ + b + r`` in x's dtype (``r`` [..., N] same dtype, unit inner stride); ``out`` may be
+    ``r`` itself (in-place residual add)."""
+    x2 = _rows(x)
+    n = w.shape[0]
+    r2 = r.reshape(-1, n)
+    if r2.stride(-1) != 1 or r2.dtype != x.dtype or r2.shape[0] != x2.shape[0]:
+        raise ValueError("linear_add: r must be [rows, N] in x's dtype with unit inner stride")
+    if out is None:
+        out = torch.empty((x2.shape[0], n), dtype=x.dtype, device=x.device)
+    o2 = out.reshape(-1, n)
+    _run(EPI_ADD, x2, w, _bias(b, n, x.dtype), o2, None, None, 0, 0, o2.stride(0), 0, r2, r2.stride(0))
+    return out.view(*x.shape[:-1], n)
+
+
+def conv_weight(w: torch.Tensor) -> torch.Tensor:
+    """OIHW 3×3 conv weight → the kernel's [Cout, 3·3·Cin] (tap-major) layout."""
+    return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1).contiguous()
+
+
+def conv3x3_supported(x: torch.Tensor, cout: int) -> bool:
+    return (x.device.type == "cuda" and x.dtype == torch.float16 and x.dim() == 4
+            and x.shape[1] % 64 == 0 and cout % 8 == 0
+            and x.is_contiguous(memory_format=torch.channels_last))
+
+
+def conv3x3(x: torch.Tensor, wk: torch.Tensor, b: Optional[torch.Tensor] = None,
+            mode: int = CONV_S1, r: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """3×3 convolution (padding 1) of a channels-last fp16 NCHW tensor on the implicit-GEMM
+    kernel: ``mode`` CONV_S1 (stride 1), CONV_S2 (stride 2), CONV_UP2 (nearest 2× upsample, then
+    stride 1).  ``wk`` = :func:`conv_weight`; ``r`` (same shape as the output, channels-last) is
+    added in the epilogue.  Returns a channels-last [N, Cout, Hout, Wout] tensor."""
+    n, cin, h, w = x.shape
+    cout = wk.shape[0]
+    if not conv3x3_supported(x, cout) or wk.shape[1] != 9 * cin or wk.dtype != x.dtype:
+        raise ValueError(f"conv3x3: unsupported input {tuple(x.shape)} {x.dtype} / weight {tuple(wk.shape)}")
+    ho, wo = {CONV_S1: (h, w), CONV_S2: ((h + 1) // 2, (w + 1) // 2), CONV_UP2: (2 * h, 2 * w)}[mode]
+    out = torch.empty((n, cout, ho, wo), dtype=x.dtype, device=x.device,
+                      memory_format=torch.channels_last)
+    if r is not None:
+        if r.shape != out.shape or r.dtype != x.dtype or not r.is_contiguous(memory_format=torch.channels_last):
+            raise ValueError("conv3x3: r must match the output (channels-last, same dtype)")
+    bb = _bias(b, cout, x.dtype)
+    epi = EPI_ADD if r is not None else EPI_STORE
+    ws = _workspace(epi, n * ho * wo, cout, 9 * cin, x.device)
+    rc = _lib().amdk8s_conv3x3_epi(epi, mode, x.data_ptr(), wk.data_ptr(), _ptr(bb), out.data_ptr(),
+                                   _ptr(r), n, h, w, cin, cout, cout, cout, _ptr(ws), _stream(x))
+    if rc != 0:
+        raise RuntimeError(f"amdk8s_conv3x3_epi failed (rc={rc}, x={tuple(x.shape)}, Cout={cout}, mode={mode})")
+    return out

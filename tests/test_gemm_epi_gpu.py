@@ -162,3 +162,69 @@ def test_w4a_fp16_epilogue(GE, gelu):
     if gelu:
         ref = F.gelu(ref, approximate="tanh")
     torch.testing.assert_close(GE.linear(x, w, b, gelu=gelu).float(), ref, rtol=5e-3, atol=5e-3)
+
+
+@pytest.mark.parametrize("mode", ["s1", "s2", "up2"])
+@pytest.mark.parametrize("shape", [(2, 64, 9, 13, 40), (2, 320, 64, 64, 320), (1, 128, 17, 6, 264),
+                                   (3, 640, 8, 8, 1280)])
+@pytest.mark.parametrize("add", [False, True])
+def test_conv3x3_implicit_gemm_vs_fp32(GE, mode, shape, add):
+    """Implicit-GEMM 3×3 conv (pad 1) on channels-last fp16 against F.conv2d in fp32: stride 1,
+    stride 2 (odd sizes), nearest-2× upsample folded into the addressing, bias, residual add."""
+    dev = torch.device("cuda")
+    n, cin, h, w, cout = shape
+    g = torch.Generator(device=dev).manual_seed(cin + h + w)
+    x = torch.randn(n, cin, h, w, generator=g, device=dev).half().contiguous(memory_format=torch.channels_last)
+    wt = (torch.randn(cout, cin, 3, 3, generator=g, device=dev) / (3 * cin ** 0.5)).half()
+    b = torch.randn(cout, generator=g, device=dev).half()
+    xin = x.float()
+    if mode == "up2":
+        xin = F.interpolate(xin, scale_factor=2.0, mode="nearest")
+    ref = F.conv2d(xin, wt.float(), b.float(), stride=2 if mode == "s2" else 1, padding=1)
+    r = None
+    if add:
+        r = torch.randn(ref.shape, generator=g, device=dev).half().contiguous(memory_format=torch.channels_last)
+        ref = ref + r.float()
+    m = {"s1": GE.CONV_S1, "s2": GE.CONV_S2, "up2": GE.CONV_UP2}[mode]
+    y = GE.conv3x3(x, GE.conv_weight(wt), b, mode=m, r=r)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+
+
+def test_linear_add_in_place(GE):
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(2)
+    x = torch.randn(3000, 640, generator=g, device=dev).half()
+    w = (torch.randn(320, 640, generator=g, device=dev) / 25).half()
+    b = torch.randn(320, generator=g, device=dev).half()
+    r = torch.randn(3000, 320, generator=g, device=dev).half()
+    want = _ref(x, w, b) + r.float()
+    out = GE.linear_add(x, w, b, r, out=r)
+    assert out.data_ptr() == r.data_ptr()
+    torch.testing.assert_close(r.float(), want, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("epi", ["store", "gelu", "add"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_split_k_small_grid(GE, epi, dtype):
+    """Problems whose tile grid cannot fill the chip (SD1.5 deep levels: M = 128, K = 5120) run
+    split-K: fp32 atomics into a workspace + a finalize pass with the same epilogue."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(7)
+    m, n, k = 128, 1280, 5120
+    assert GE.splits(m, n, k) > 1
+    x = torch.randn(m, k, generator=g, device=dev).to(dtype)
+    w = (torch.randn(n, k, generator=g, device=dev) / k ** 0.5).to(dtype)
+    b = torch.randn(n, generator=g, device=dev).to(dtype)
+    ref = _ref(x, w, b)
+    tol = 2e-2 if dtype == torch.bfloat16 else 5e-3
+    if epi == "store":
+        y = GE.linear(x, w, b)
+    elif epi == "gelu":
+        y = GE.linear_gelu(x, w, b)
+        ref = F.gelu(ref, approximate="tanh")
+    else:
+        r = torch.randn(m, n, generator=g, device=dev).to(dtype)
+        ref = ref.to(dtype).float() + r.float()
+        y = GE.linear_add(x, w, b, r)
+    torch.testing.assert_close(y.float(), ref, rtol=tol, atol=2 * tol)
