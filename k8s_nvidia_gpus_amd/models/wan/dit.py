@@ -114,12 +114,31 @@ class WanDiT(nn.Module):
         self.blocks = nn.ModuleList([Block(cfg) for _ in range(cfg.layers)])
         self.head = Head(cfg)
         self._rope_cache = {}
+        self._f32 = None        # (key, tensors) of :meth:`_fp32_params`
 
     # ------------------------------------------------------------------ helpers
     def fuse(self) -> "WanDiT":
         for b in self.blocks:
             b.fuse()
         return self
+
+    def _fp32_params(self):
+        """fp32 copies of the small per-block parameters the step reads, stacked once: AdaLN
+        modulations with the ``1 +`` of both scale slots folded in ([blocks, 6, d]), norm3
+        weight / bias, the head modulation — one add per step instead of ~150 tiny kernels."""
+        ps = [b.modulation for b in self.blocks] + [self.head.modulation]
+        key = tuple((p.data_ptr(), p._version, str(p.device)) for p in ps)
+        if self._f32 is None or self._f32[0] != key:
+            with torch.no_grad():
+                mod = torch.stack([b.modulation.float()[0] for b in self.blocks])   # [n, 6, d]
+                mod[:, 1] += 1.0
+                mod[:, 4] += 1.0
+                n3w = torch.stack([b.norm3.weight.float() for b in self.blocks])[:, None]
+                n3b = torch.stack([b.norm3.bias.float() for b in self.blocks])[:, None]
+                head = self.head.modulation.float()[0].clone()                    # [2, d]
+                head[1] += 1.0
+            self._f32 = (key, (mod, n3w, n3b, head))
+        return self._f32[1]
 
     def grid(self, latent_shape: Sequence[int]) -> Tuple[int, int, int]:
         _, _, f, h, w = latent_shape
@@ -176,8 +195,10 @@ class WanDiT(nn.Module):
 
     # ------------------------------------------------------------------ forward
     def time_mod(self, t: torch.Tensor):
-        e = self.time_embedding(sinusoidal(self.cfg.freq_dim, t).to(self.time_embedding[0].weight.dtype))
-        e0 = self.time_projection(e).float().view(-1, 6, self.cfg.dim)
+        t0, t2, tp = self.time_embedding[0], self.time_embedding[2], self.time_projection[1]
+        s = sinusoidal(self.cfg.freq_dim, t).to(t0.weight.dtype)
+        e = WF.linear(F.silu(WF.linear(s, t0.weight, t0.bias)), t2.weight, t2.bias)
+        e0 = WF.linear(F.silu(e), tp.weight, tp.bias).float().view(-1, 6, self.cfg.dim)
         return e.float(), e0
 
     def forward(self, x: torch.Tensor, t: torch.Tensor, text_kv, out_dtype=torch.float32,
@@ -202,10 +223,11 @@ class WanDiT(nn.Module):
             attend = WF.attention
         b, l, d = res.shape
         e, e0 = self.time_mod(t)
-        mods = [(blk.modulation.float() + e0) for blk in self.blocks]   # [B, 6, d] each
+        mod1, n3w, n3b, head1 = self._fp32_params()
+        mods = mod1[:, None] + e0[None]               # [blocks, B, 6, d]; slots 1, 4 hold 1 + scale
 
         m = mods[0]
-        h = WF.add_ln(res, None, None, 1.0 + m[:, 1], m[:, 0], cfg.eps, wdt)
+        h = WF.add_ln(res, None, None, m[:, 1], m[:, 0], cfg.eps, wdt)
         for i, blk in enumerate(self.blocks):
             m = mods[i]
             # self-attention; x += gate1 · o_proj(attn) fused into the o-projection
@@ -215,25 +237,24 @@ class WanDiT(nn.Module):
                                cos, sin, cfg.heads, cfg.eps)
             so = blk.self_attn.o
             WF.linear_residual_(res, attend(q, k, v, cfg.heads), so.weight, so.bias, m[:, 2])
-            h = WF.add_ln(res, None, None, blk.norm3.weight.float()[None], blk.norm3.bias.float()[None],
-                          cfg.eps, wdt)
+            h = WF.add_ln(res, None, None, n3w[i], n3b[i], cfg.eps, wdt)
             # cross-attention over the cached text K/V; x += o_proj(attn)
             ca = blk.cross_attn
             qc = WF.linear(h, ca.q.weight, ca.q.bias)
             WF.rmsnorm_rope(qc, ca.norm_q.weight, None, None, cfg.heads, cfg.eps)
             kc, vc = text_kv[i]
             WF.linear_residual_(res, WF.attention(qc, kc, vc, cfg.heads), ca.o.weight, ca.o.bias, None)
-            h = WF.add_ln(res, None, None, 1.0 + m[:, 4], m[:, 3], cfg.eps, wdt)
+            h = WF.add_ln(res, None, None, m[:, 4], m[:, 3], cfg.eps, wdt)
             # feed-forward; x += gate2 · ffn(h)
             f = WF.linear_gelu(h, blk.ffn[0].weight, blk.ffn[0].bias)
             WF.linear_residual_(res, f, blk.ffn[2].weight, blk.ffn[2].bias, m[:, 5])
             if i + 1 < len(self.blocks):
                 nm = mods[i + 1]
-                h = WF.add_ln(res, None, None, 1.0 + nm[:, 1], nm[:, 0], cfg.eps, wdt)
+                h = WF.add_ln(res, None, None, nm[:, 1], nm[:, 0], cfg.eps, wdt)
             else:
-                hm = self.head.modulation.float() + e[:, None, :]      # [B, 2, d]
-                h = WF.add_ln(res, None, None, 1.0 + hm[:, 1], hm[:, 0], cfg.eps, wdt)
-        y = self.head.head(h)
+                hm = head1 + e[:, None, :]                             # [B, 2, d]
+                h = WF.add_ln(res, None, None, hm[:, 1], hm[:, 0], cfg.eps, wdt)
+        y = WF.linear(h, self.head.head.weight, self.head.head.bias)
         if sp is not None and sp.world > 1:
             y = sp.gather(y)
         return self.unpatchify(y.to(out_dtype), grid)

@@ -67,7 +67,7 @@ struct Geo {
 };
 
 enum Epi { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_ADD = 3,
-           EPI_PARTIAL = 4 };   // split-K: fp32 atomic accumulation into a zeroed workspace
+           EPI_PARTIAL = 4 };   // split-K: this split's fp32 partial tile into its workspace slice
 
 // Implicit-GEMM 3×3 convolution (pad 1) over NHWC activations: the A "row" of output pixel m at
 // K-tile t is the 64-channel slice t % (Cin/64) of input pixel (tap t / (Cin/64)) — a 128-B run
@@ -84,7 +84,7 @@ struct Args {
   const uint16_t* r;      // [M][ldr] 16-bit addend (ADD: out = Y + bias + r; may alias out)
   int M, N, K, lda, ldb, ldo, ldx, rows_per_gate, gate_stride, ldr;
   int splits;             // K split across `splits` workgroups per tile (EPI_PARTIAL), else 1
-  float* ws;              // [M][N] fp32 split-K workspace (EPI_PARTIAL)
+  float* ws;              // [splits][M][N] fp32 split-K workspace (EPI_PARTIAL)
   // convolution geometry (CONV != CONV_NONE): input [batch][Hin][Win][Cin], output Hout × Wout
   int Hin, Win, Hout, Wout, Cin;
 };
@@ -306,17 +306,15 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
       for (int j = 0; j < 4; ++j) acc[i][j] = mfma16<F16>(bw[1][j], af[1][i], acc[i][j]);
     __builtin_amdgcn_s_setprio(0);
   }
-  if constexpr (EPI == EPI_PARTIAL) {     // split-K: fp32 atomics straight from the accumulators
+  if constexpr (EPI == EPI_PARTIAL) {     // split-K: plain 16-B stores of the fp32 partial tile
+    float* slice = a.ws + (size_t)split * a.M * a.N;   // (no atomics, no zeroing: deterministic)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = m0 + wm * 64 + 16 * i + fr, n = n0 + wn * 64 + 16 * j + 4 * fq;
-        if (m < a.M && n < a.N) {
-          float* w = a.ws + (size_t)m * a.N + n;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) atomicAdd(w + e, acc[i][j][e]);
-        }
+        if (m < a.M && n < a.N)                 // N % 8 == 0: a lane's 4 columns all in or out
+          *reinterpret_cast<f32x4*>(slice + (size_t)m * a.N + n) = acc[i][j];
       }
     return;
   }
@@ -427,6 +425,11 @@ __global__ void __launch_bounds__(256) splitk_finalize(const Args a) {
   const int m = (int)(i8 / groups), n = (int)(i8 - (long)m * groups) * 8;
   const f32x4* w = reinterpret_cast<const f32x4*>(a.ws + (size_t)m * a.N + n);
   f32x4 v0 = w[0], v1 = w[1];
+  const size_t slice = (size_t)a.M * a.N / 4;      // in f32x4
+  for (int sp = 1; sp < a.splits; ++sp) {          // fixed order: bitwise reproducible
+    v0 += w[sp * slice];
+    v1 += w[sp * slice + 1];
+  }
   if (a.bias) {
     const uint4 bv = *reinterpret_cast<const uint4*>(a.bias + n);
     const uint32_t b32[4] = {bv.x, bv.y, bv.z, bv.w};
@@ -472,51 +475,71 @@ int amdk8s_gemm_epi_supported(int M, int N, int K) {
   return M > 0 && N > 0 && K > 0 && N % 8 == 0 && K % BK == 0;
 }
 
-// Block tile for an M × N problem: the largest of 256×128, 128×128, 128×64, 64×64 whose grid
-// nearly covers the 256 CUs (>= 224 workgroups; else 64×64).  Measured (profiles/r03/e): the Wan
-// o / ffn2 projections at 2 × 2560 rows run 240 256×128 tiles 20-30 % faster than 480 128×128 ones,
-// while the SD1.5 deep-level projections (M = 128 … 2048) want the small tiles.  amdk8s_gemm_epi_set_tile(0..3) or AMDK8S_GEMM_EPI_TILE pins
-// one (A/B sweeps); -1 restores the heuristic.
+// Launch plan of an M × N × K problem: block tile (index into kTiles: 256×128, 128×128, 128×64,
+// 64×64) and split-K factor.  The largest tile whose grid covers the CUs (>= 224 workgroups; the
+// Wan o / ffn2 projections at 2 × 2560 rows run 240 256×128 tiles 20-30 % faster than 480
+// 128×128 ones — profiles/r03/e) runs unsplit; otherwise the largest tile that reaches 224
+// workgroups with K split into parts of >= 8 K-tiles (the ring's pipeline depth), else 64×64 with
+// as many such splits as K allows (at most 16).  Overrides for A/B sweeps:
+// amdk8s_gemm_epi_set_tile(0..3) / AMDK8S_GEMM_EPI_TILE pin the tile, AMDK8S_GEMM_SPLITK=<n> pins
+// the split factor (1 = never split); -1 / unset = the plan above.
 static const int kTiles[4][2] = {{256, 128}, {128, 128}, {128, 64}, {64, 64}};
-static int g_tile = -2;   // -2: not initialised from the environment yet
+static int g_tile = -2;     // -2: not initialised from the environment yet
+static int g_splits = -2;
 
 void amdk8s_gemm_epi_set_tile(int tile) { g_tile = (tile >= 0 && tile <= 3) ? tile : -1; }
+void amdk8s_gemm_epi_set_splits(int s) { g_splits = (s >= 1 && s <= 64) ? s : -1; }
 
-int amdk8s_gemm_epi_tile(int M, int N);
-
-// Split-K factor for a problem whose tile grid cannot fill the chip: enough splits for ~512
-// workgroups, each keeping >= 8 K-tiles (the ring's pipeline depth), at most 16.  1 = no split.
-// AMDK8S_GEMM_SPLITK=0 disables it.
-int amdk8s_gemm_epi_splits(int M, int N, int K) {
-  static int enabled = -1;
-  if (enabled < 0) {
-    const char* e = getenv("AMDK8S_GEMM_SPLITK");
-    enabled = !(e && e[0] == '0' && !e[1]);
-  }
-  if (!enabled) return 1;
-  const int tile = amdk8s_gemm_epi_tile(M, N);
-  const long nwg = (long)((M + kTiles[tile][0] - 1) / kTiles[tile][0]) *
-                   ((N + kTiles[tile][1] - 1) / kTiles[tile][1]);
-  const int T = K / BK;
-  if (nwg >= 224 || T < 16) return 1;
-  int s = (int)((512 + nwg - 1) / nwg);
-  s = s < T / 8 ? s : T / 8;
-  s = s < 16 ? s : 16;
-  return s > 1 ? s : 1;
+static long tile_grid(int tile, int M, int N) {
+  return (long)((M + kTiles[tile][0] - 1) / kTiles[tile][0]) * ((N + kTiles[tile][1] - 1) / kTiles[tile][1]);
 }
 
-int amdk8s_gemm_epi_tile(int M, int N) {
+void amdk8s_gemm_epi_plan(int M, int N, int K, int* tile_out, int* splits_out) {
   if (g_tile == -2) {
     const char* e = getenv("AMDK8S_GEMM_EPI_TILE");
     g_tile = (e && e[0] >= '0' && e[0] <= '3' && !e[1]) ? e[0] - '0' : -1;
   }
-  if (g_tile >= 0) return g_tile;
-  for (int i = 0; i < 3; ++i) {
-    const long nwg = (long)((M + kTiles[i][0] - 1) / kTiles[i][0]) *
-                     ((N + kTiles[i][1] - 1) / kTiles[i][1]);
-    if (nwg >= 224) return i;
+  if (g_splits == -2) {
+    const char* e = getenv("AMDK8S_GEMM_SPLITK");
+    const int v = e ? atoi(e) : 0;
+    g_splits = (v >= 1 && v <= 64) ? v : -1;
   }
-  return 3;
+  const int T = K / BK;
+  auto max_splits = [&](int want) { int s = want < T / 8 ? want : T / 8; s = s < 16 ? s : 16; return s > 1 ? s : 1; };
+  int tile = 3, splits = 1;
+  if (g_tile >= 0) {
+    tile = g_tile;
+    const long nwg = tile_grid(tile, M, N);
+    splits = nwg >= 224 ? 1 : max_splits((int)((224 + nwg - 1) / nwg));
+  } else {
+    bool done = false;
+    for (int i = 0; i < 4 && !done; ++i) {
+      const long nwg = tile_grid(i, M, N);
+      if (nwg >= 224) { tile = i; splits = 1; done = true; break; }
+      const int need = (int)((224 + nwg - 1) / nwg);
+      if (need <= 16 && T / need >= 8) { tile = i; splits = need; done = true; }
+    }
+    if (!done) {
+      tile = 3;
+      const long nwg = tile_grid(3, M, N);
+      splits = max_splits((int)((224 + nwg - 1) / nwg));
+    }
+  }
+  if (g_splits >= 1) splits = g_splits < T ? g_splits : (T > 0 ? T : 1);
+  *tile_out = tile;
+  *splits_out = splits;
+}
+
+int amdk8s_gemm_epi_tile(int M, int N) {     // the tile the plan picks for a deep K (reporting)
+  int t, s;
+  amdk8s_gemm_epi_plan(M, N, 1 << 20, &t, &s);
+  return t;
+}
+
+int amdk8s_gemm_epi_splits(int M, int N, int K) {
+  int t, s;
+  amdk8s_gemm_epi_plan(M, N, K, &t, &s);
+  return s;
 }
 
 }  // extern "C"
@@ -525,16 +548,12 @@ namespace {
 
 template <int CONV>
 int launch_epi(Args a, int epi, bool f16, hipStream_t stream) {
-  const int tile = amdk8s_gemm_epi_tile(a.M, a.N);
-  const long nwg = (long)((a.M + kTiles[tile][0] - 1) / kTiles[tile][0]) *
-                   ((a.N + kTiles[tile][1] - 1) / kTiles[tile][1]);
-  const int splits = a.ws && epi != EPI_RESID ? amdk8s_gemm_epi_splits(a.M, a.N, a.K) : 1;
+  int tile, splits;
+  amdk8s_gemm_epi_plan(a.M, a.N, a.K, &tile, &splits);
+  if (!a.ws || epi == EPI_RESID) splits = 1;         // no workspace: one pass over K
+  const long nwg = tile_grid(tile, a.M, a.N);
   if (nwg * splits > 0x7fffffff) return (int)hipErrorInvalidValue;
   a.splits = splits;
-  if (splits > 1) {
-    const hipError_t e = hipMemsetAsync(a.ws, 0, (size_t)a.M * a.N * sizeof(float), stream);
-    if (e != hipSuccess) return (int)e;
-  }
   auto go = [&](auto wm, auto wn) {
     constexpr int WM = decltype(wm)::value, WN = decltype(wn)::value;
     constexpr int NT = Geo<WM, WN>::NT;
@@ -597,8 +616,9 @@ int check_out(int epi, int N, const void* out, int ldo, const void* r, int ldr) 
 extern "C" {
 
 // epi: 0 store, 1 GELU, 2 fp32 gated residual (x, gate), 3 add (out = Y + bias + r, 16-bit r).
-// ws: optional [M][N] fp32 workspace; when given (and the epilogue is not RESID), problems that
-// cannot fill the chip run split-K (amdk8s_gemm_epi_splits) + a finalize pass.
+// ws: optional fp32 workspace of amdk8s_gemm_epi_splits(M, N, K) × M × N floats; when given (and
+// the epilogue is not RESID), problems that cannot fill the chip run split-K (each split stores
+// its partial tile to its own slice) + a finalize pass that sums the slices in a fixed order.
 int amdk8s_gemm_epi(int epi, int dtype, const void* A, const void* B, const void* bias, void* out,
                     float* x, const float* gate, const void* r, int M, int N, int K, int lda,
                     int ldb, int ldo, int ldx, int ldr, int rows_per_gate, int gate_stride,

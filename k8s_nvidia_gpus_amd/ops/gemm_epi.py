@@ -47,8 +47,10 @@ def _lib():
             lib.amdk8s_gemm_w4a_epi.restype = ci
             lib.amdk8s_gemm_epi_set_tile.argtypes = [ci]
             lib.amdk8s_gemm_epi_set_tile.restype = None
-            lib.amdk8s_gemm_epi_tile.argtypes = [ci, ci]
-            lib.amdk8s_gemm_epi_tile.restype = ci
+            lib.amdk8s_gemm_epi_set_splits.argtypes = [ci]
+            lib.amdk8s_gemm_epi_set_splits.restype = None
+            lib.amdk8s_gemm_epi_plan.argtypes = [ci, ci, ci, ctypes.POINTER(ci), ctypes.POINTER(ci)]
+            lib.amdk8s_gemm_epi_plan.restype = None
             _declared = True
     return lib
 
@@ -61,12 +63,20 @@ TILES = ((256, 128), (128, 128), (128, 64), (64, 64))
 
 
 def set_tile(tile: int) -> None:
-    """Pin the 256×128-kernel family's block tile (index into TILES); -1 = size heuristic."""
+    """Pin the wave-grid kernel family's block tile (index into TILES); -1 = the planner."""
     _lib().amdk8s_gemm_epi_set_tile(int(tile))
 
 
-def tile_for(m: int, n: int) -> tuple:
-    return TILES[_lib().amdk8s_gemm_epi_tile(m, n)]
+def set_splits(s: int) -> None:
+    """Pin the split-K factor (1 = never split); -1 = the planner."""
+    _lib().amdk8s_gemm_epi_set_splits(int(s))
+
+
+def plan(m: int, n: int, k: int) -> tuple:
+    """(block tile, split-K factor) the kernels use for an m × n × k problem."""
+    t, sp = ctypes.c_int(), ctypes.c_int()
+    _lib().amdk8s_gemm_epi_plan(m, n, k, ctypes.byref(t), ctypes.byref(sp))
+    return TILES[t.value], sp.value
 
 
 def _rows(x: torch.Tensor) -> torch.Tensor:
@@ -104,13 +114,14 @@ def _ptr(t: Optional[torch.Tensor]):
 
 def splits(m: int, n: int, k: int) -> int:
     """Split-K factor the kernels use for an m × n × k problem (1 = none)."""
-    return _lib().amdk8s_gemm_epi_splits(m, n, k)
+    return plan(m, n, k)[1]
 
 
 def _workspace(epi: int, m: int, n: int, k: int, dev) -> Optional[torch.Tensor]:
-    if epi == EPI_RESID or splits(m, n, k) <= 1:
+    sp = 1 if epi == EPI_RESID else splits(m, n, k)
+    if sp <= 1:
         return None
-    return torch.empty(m * n, dtype=torch.float32, device=dev)
+    return torch.empty(sp * m * n, dtype=torch.float32, device=dev)
 
 
 def _run(epi, x2, w, b, out, res, gate, rows_per_gate, gate_stride, ldo, ldx, r=None, ldr=0):

@@ -114,7 +114,7 @@ def test_every_tile_variant(GE, tile, dtype):
     tol = 2e-2 if dtype == torch.bfloat16 else 5e-3
     GE.set_tile(tile)
     try:
-        assert GE.tile_for(m, n) == GE.TILES[tile]
+        assert GE.plan(m, n, k) == (GE.TILES[tile], 1)
         torch.testing.assert_close(GE.linear(x, w, b).float(), ref, rtol=tol, atol=tol)
         torch.testing.assert_close(GE.linear_gelu(x, w, b).float(),
                                    F.gelu(ref, approximate="tanh"), rtol=tol, atol=tol)
@@ -125,7 +125,8 @@ def test_every_tile_variant(GE, tile, dtype):
         torch.testing.assert_close(res, want, rtol=tol, atol=2 * tol)
     finally:
         GE.set_tile(-1)
-    assert GE.tile_for(8192, 1536) == (256, 128) and GE.tile_for(128, 1280) == (64, 64)
+    assert GE.plan(8192, 1536, 1536) == ((256, 128), 1) and GE.plan(128, 1280, 1280) == ((64, 64), 2)
+    assert GE.plan(8192, 320, 2880) == ((256, 128), 3)       # SD 64² conv: 96 tiles x 3 splits
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])

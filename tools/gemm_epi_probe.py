@@ -42,7 +42,7 @@ if os.environ.get("MODE", "wan") == "sd":
             w = (torch.randn(n, k, device=dev) / k ** 0.5).half()
             b = torch.randn(n, device=dev).half()
             fl = 2.0 * m * n * k
-            row = {"m": m, "n": n, "k": k, "auto_tile": GE.tile_for(m, n),
+            row = {"m": m, "n": n, "k": k, "auto_plan": GE.plan(m, n, k),
                    "w4a": GE.use_w4a(m, n, k, torch.float16)}
             row["auto_us"] = bench(lambda: GE.linear(x, w, b))
             out = torch.empty(m, n, device=dev).half()
