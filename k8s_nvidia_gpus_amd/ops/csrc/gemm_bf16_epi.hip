@@ -476,11 +476,11 @@ int amdk8s_gemm_epi_supported(int M, int N, int K) {
 }
 
 // Launch plan of an M × N × K problem: block tile (index into kTiles: 256×128, 128×128, 128×64,
-// 64×64) and split-K factor.  The largest tile whose grid covers the CUs (>= 224 workgroups; the
-// Wan o / ffn2 projections at 2 × 2560 rows run 240 256×128 tiles 20-30 % faster than 480
-// 128×128 ones — profiles/r03/e) runs unsplit; otherwise the largest tile that reaches 224
-// workgroups with K split into parts of >= 8 K-tiles (the ring's pipeline depth), else 64×64 with
-// as many such splits as K allows (at most 16).  Overrides for A/B sweeps:
+// 64×64) and split-K factor.  A 256×128 / 128×128 grid of >= 160 workgroups runs unsplit (the Wan
+// o / ffn2 projections at 2 × 2560 rows run 240 256×128 tiles 20-30 % faster than 480 128×128
+// ones — profiles/r03/e); otherwise the largest tile that reaches 192 workgroups with K split
+// into parts of >= 8 K-tiles (the ring's pipeline depth), else 64×64 with as many such splits as
+// K allows (at most 16).  Overrides for A/B sweeps:
 // amdk8s_gemm_epi_set_tile(0..3) / AMDK8S_GEMM_EPI_TILE pin the tile, AMDK8S_GEMM_SPLITK=<n> pins
 // the split factor (1 = never split); -1 / unset = the plan above.
 static const int kTiles[4][2] = {{256, 128}, {128, 128}, {128, 64}, {64, 64}};
@@ -513,18 +513,21 @@ void amdk8s_gemm_epi_plan(int M, int N, int K, int* tile_out, int* splits_out) {
     splits = nwg >= 224 ? 1 : max_splits((int)((224 + nwg - 1) / nwg));
   } else {
     bool done = false;
+    // a 4- or 8-wave tile whose grid nearly fills the chip runs unsplit: the split's finalize
+    // pass (S × M × N fp32 through L2 / HBM) costs more than the idle CUs (SD 64² convs: 128×128
+    // × 192 tiles 35.6 µs vs 256×128 × 96 tiles × 3 splits 50.3 µs — profiles/r03/h/conv_probe.log)
+    for (int i = 0; i < 2 && !done; ++i)
+      if (tile_grid(i, M, N) >= 160) { tile = i; splits = 1; done = true; }
     for (int i = 0; i < 4 && !done; ++i) {
       const long nwg = tile_grid(i, M, N);
-      if (nwg >= 224) { tile = i; splits = 1; done = true; break; }
-      const int need = (int)((224 + nwg - 1) / nwg);
+      const int need = (int)((192 + nwg - 1) / nwg);
       if (need <= 16 && T / need >= 8) { tile = i; splits = need; done = true; }
     }
     if (!done) {
       tile = 3;
       const long nwg = tile_grid(3, M, N);
-      splits = max_splits((int)((224 + nwg - 1) / nwg));
+      splits = max_splits((int)((192 + nwg - 1) / nwg));
     }
-  }
   if (g_splits >= 1) splits = g_splits < T ? g_splits : (T > 0 ? T : 1);
   *tile_out = tile;
   *splits_out = splits;

@@ -126,7 +126,8 @@ def test_every_tile_variant(GE, tile, dtype):
     finally:
         GE.set_tile(-1)
     assert GE.plan(8192, 1536, 1536) == ((256, 128), 1) and GE.plan(128, 1280, 1280) == ((64, 64), 2)
-    assert GE.plan(8192, 320, 2880) == ((256, 128), 3)       # SD 64² conv: 96 tiles x 3 splits
+    assert GE.plan(8192, 320, 2880) == ((128, 128), 1)       # SD 64² conv: 192 tiles, unsplit
+    assert GE.plan(2048, 640, 5760) == ((256, 128), 5)       # 40 tiles x 5 splits
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
