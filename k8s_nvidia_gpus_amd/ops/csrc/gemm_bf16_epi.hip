@@ -528,6 +528,7 @@ void amdk8s_gemm_epi_plan(int M, int N, int K, int* tile_out, int* splits_out) {
       const long nwg = tile_grid(3, M, N);
       splits = max_splits((int)((192 + nwg - 1) / nwg));
     }
+  }
   if (g_splits >= 1) splits = g_splits < T ? g_splits : (T > 0 ? T : 1);
   *tile_out = tile;
   *splits_out = splits;
