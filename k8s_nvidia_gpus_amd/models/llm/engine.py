@@ -139,9 +139,10 @@ class Engine:
             qi = torch.arange(start, end, device=self.device)[:, None]
             kj = torch.arange(end, device=self.device)[None, :]
             mask = kj <= qi
+        mm, mm_res = self._dense_ops()
         for i, L in enumerate(self.w.layers):
             xn = (x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + c.eps) * L.attn_norm).to(dt)
-            qkv = (xn @ W[f"{i}.qkv"].t()).float() + L.bqkv
+            qkv = mm(xn, W[f"{i}.qkv"]).float() + L.bqkv
             q = qkv[:, :c.dim].view(P, c.heads, c.head_dim).transpose(0, 1)
             k = qkv[:, c.dim:c.dim + c.kv_dim].view(P, c.kv_heads, c.head_dim).transpose(0, 1)
             v = qkv[:, c.dim + c.kv_dim:].view(P, c.kv_heads, c.head_dim).transpose(0, 1)
@@ -154,14 +155,31 @@ class Engine:
             o = F.scaled_dot_product_attention(q.to(dt)[None], kk[None], vv[None],
                                                attn_mask=None if mask is None else mask[None, None])
             o = o[0].transpose(0, 1).reshape(P, c.dim)
-            x = x + (o @ W[f"{i}.o"].t()).float()
+            x = mm_res(x, o, W[f"{i}.o"])
             xn = (x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + c.eps) * L.ffn_norm).to(dt)
-            gu = (xn @ W[f"{i}.gu"].t()).float()
+            gu = mm(xn, W[f"{i}.gu"]).float()
             t = F.silu(gu[:, :c.ffn]) * gu[:, c.ffn:]
-            x = x + (t.to(dt) @ W[f"{i}.down"].t()).float()
+            x = mm_res(x, t.to(dt), W[f"{i}.down"])
         xl = x[-1:]
         xn = (xl * torch.rsqrt(xl.pow(2).mean(-1, keepdim=True) + c.eps) * self.w.out_norm).to(dt)
-        return (xn @ W["out"].t()).float()[0]
+        return mm(xn, W["out"]).float()[0]
+
+    def _dense_ops(self):
+        """Prompt-processing GEMMs: on the GPU the hand-written fp16 MFMA GEMMs
+        (``ops/gemm_epi.py``: tile / split-K planned per shape, the residual add of o_proj and
+        ffn_down fused into the epilogue straight into the fp32 stream); PyTorch on the CPU."""
+        if self.gpu and os.environ.get("AMDK8S_LLM_PREFILL_GEMM", "native") != "torch":
+            from k8s_nvidia_gpus_amd.ops import gemm_epi as GE
+
+            def mm(a, w):
+                return GE.linear(a, w) if GE.supported(a, w) else a @ w.t()
+
+            def mm_res(x, a, w):
+                if GE.supported(a, w) and x.is_contiguous():
+                    return GE.linear_residual_(x, a, w)
+                return x + (a @ w.t()).float()
+            return mm, mm_res
+        return (lambda a, w: a @ w.t()), (lambda x, a, w: x + (a @ w.t()).float())
 
     # ------------------------------------------------------------------ native decode
     def _buffers(self, T: int) -> StepBuffers:

@@ -170,63 +170,81 @@ __device__ __forceinline__ XReg load_x(const XView& x, int t, int blk, int sub) 
   return r;
 }
 
-// acc += (this lane's part of) w . x for one super-block.  Explicit roundings: the same
-// instruction sequence for every T instantiation and activation source (LDS or registers), so a
-// token's result does not depend on how many sequences share the step (batch-invariant decode).
+// acc += (this lane's part of) w . x for one super-block, in two halves: prep_blk decodes the
+// lane's weights (nibbles / 6-bit values, block scales) once, dot_apply runs the per-token part —
+// so with T tokens the decode is not repeated T times.  Explicit roundings: the same instruction
+// sequence for every T instantiation and activation source (LDS or registers), so a token's
+// result does not depend on how many sequences share the step (batch-invariant decode).
+template <int TYPE> struct Prep;
+template <> struct Prep<kQ4K> { uint32_t ql[4], qh[4]; float dsc0, dsc1, dm0, dm1; };
+template <> struct Prep<kQ6K> { uint32_t ql[4], qh[4]; float sc0, sc1; };
+
 template <int TYPE>
-__device__ __forceinline__ float dot_core(const Blk<TYPE>& r, int sub, const XReg& x, float acc) {
+__device__ __forceinline__ Prep<TYPE> prep_blk(const Blk<TYPE>& r, int sub) {
+  Prep<TYPE> p;
   if constexpr (TYPE == kQ4K) {
     const float d = h2f(r.dd & 0xffffu), dmin = h2f(r.dd >> 16);
     // the lane's two scales and mins were decoded from the 6-bit packing at load time
     const uint32_t sc0 = r.sm & 0xffu, sc1 = (r.sm >> 8) & 0xffu;
     const uint32_t m0 = (r.sm >> 16) & 0xffu, m1 = r.sm >> 24;
-    const float dsc0 = __fmul_rn(d, (float)sc0), dsc1 = __fmul_rn(d, (float)sc1);
-    const float dm0 = __fmul_rn(dmin, (float)m0), dm1 = __fmul_rn(dmin, (float)m1);
+    p.dsc0 = __fmul_rn(d, (float)sc0);
+    p.dsc1 = __fmul_rn(d, (float)sc1);
+    p.dm0 = __fmul_rn(dmin, (float)m0);
+    p.dm1 = __fmul_rn(dmin, (float)m1);
     const uint32_t q[4] = {r.q.x, r.q.y, r.q.z, r.q.w};
-    int il = 0, ih = 0;
-    il = dot4(q[0] & 0x0f0f0f0fu, x.xl.x, il);
-    il = dot4(q[1] & 0x0f0f0f0fu, x.xl.y, il);
-    il = dot4(q[2] & 0x0f0f0f0fu, x.xl.z, il);
-    il = dot4(q[3] & 0x0f0f0f0fu, x.xl.w, il);
-    ih = dot4((q[0] >> 4) & 0x0f0f0f0fu, x.xh.x, ih);
-    ih = dot4((q[1] >> 4) & 0x0f0f0f0fu, x.xh.y, ih);
-    ih = dot4((q[2] >> 4) & 0x0f0f0f0fu, x.xh.z, ih);
-    ih = dot4((q[3] >> 4) & 0x0f0f0f0fu, x.xh.w, ih);
-    float a = __fmaf_rn(__fmul_rn(dsc0, x.dxl), (float)il, acc);
-    a = __fmaf_rn(__fmul_rn(dsc1, x.dxh), (float)ih, a);
-    a = __fmaf_rn(-dm0, x.sxl, a);
-    return __fmaf_rn(-dm1, x.sxh, a);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      p.ql[i] = q[i] & 0x0f0f0f0fu;
+      p.qh[i] = (q[i] >> 4) & 0x0f0f0f0fu;
+    }
   } else {
     const int klo = (sub & 3) >> 1;
     const float d = h2f(r.d & 0xffffu);
     // scales 8n + h1 + 2klo and that + 4, stored adjacent for this lane (q6_scale_pos)
-    const float sc0 = __fmul_rn(d, (float)(int8_t)(r.s2 & 0xffu));
-    const float sc1 = __fmul_rn(d, (float)(int8_t)((r.s2 >> 8) & 0xffu));
+    p.sc0 = __fmul_rn(d, (float)(int8_t)(r.s2 & 0xffu));
+    p.sc1 = __fmul_rn(d, (float)(int8_t)((r.s2 >> 8) & 0xffu));
     const uint32_t l[4] = {r.l.x, r.l.y, r.l.z, r.l.w};
     const uint32_t hb[4] = {r.hb.x, r.hb.y, r.hb.z, r.hb.w};
     const int sh = 2 * klo;
-    uint32_t qlo[4], qhi[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      qlo[i] = (l[i] & 0x0f0f0f0fu) | (((hb[i] >> sh) & 0x03030303u) << 4);
-      qhi[i] = ((l[i] >> 4) & 0x0f0f0f0fu) | (((hb[i] >> (sh + 4)) & 0x03030303u) << 4);
+      p.ql[i] = (l[i] & 0x0f0f0f0fu) | (((hb[i] >> sh) & 0x03030303u) << 4);
+      p.qh[i] = ((l[i] >> 4) & 0x0f0f0f0fu) | (((hb[i] >> (sh + 4)) & 0x03030303u) << 4);
     }
-    int il = 0, ih = 0;
-    il = dot4(qlo[0], x.xl.x, il); il = dot4(qlo[1], x.xl.y, il);
-    il = dot4(qlo[2], x.xl.z, il); il = dot4(qlo[3], x.xl.w, il);
-    ih = dot4(qhi[0], x.xh.x, ih); ih = dot4(qhi[1], x.xh.y, ih);
-    ih = dot4(qhi[2], x.xh.z, ih); ih = dot4(qhi[3], x.xh.w, ih);
+  }
+  return p;
+}
+
+template <int TYPE>
+__device__ __forceinline__ float dot_apply(const Prep<TYPE>& p, const XReg& x, float acc) {
+  int il = 0, ih = 0;
+  il = dot4(p.ql[0], x.xl.x, il); il = dot4(p.ql[1], x.xl.y, il);
+  il = dot4(p.ql[2], x.xl.z, il); il = dot4(p.ql[3], x.xl.w, il);
+  ih = dot4(p.qh[0], x.xh.x, ih); ih = dot4(p.qh[1], x.xh.y, ih);
+  ih = dot4(p.qh[2], x.xh.z, ih); ih = dot4(p.qh[3], x.xh.w, ih);
+  if constexpr (TYPE == kQ4K) {
+    float a = __fmaf_rn(__fmul_rn(p.dsc0, x.dxl), (float)il, acc);
+    a = __fmaf_rn(__fmul_rn(p.dsc1, x.dxh), (float)ih, a);
+    a = __fmaf_rn(-p.dm0, x.sxl, a);
+    return __fmaf_rn(-p.dm1, x.sxh, a);
+  } else {
     const float u0 = __fmaf_rn(x.dxl, (float)il, __fmul_rn(-32.f, x.sxl));
     const float u1 = __fmaf_rn(x.dxh, (float)ih, __fmul_rn(-32.f, x.sxh));
-    return __fmaf_rn(sc1, u1, __fmaf_rn(sc0, u0, acc));
+    return __fmaf_rn(p.sc1, u1, __fmaf_rn(p.sc0, u0, acc));
   }
+}
+
+template <int TYPE>
+__device__ __forceinline__ float dot_core(const Blk<TYPE>& r, int sub, const XReg& x, float acc) {
+  return dot_apply<TYPE>(prep_blk<TYPE>(r, sub), x, acc);
 }
 
 template <int TYPE, int T>
 __device__ __forceinline__ void dot_blk(const Blk<TYPE>& r, int blk, int sub, const XView& x,
                                         float* acc) {
+  const Prep<TYPE> p = prep_blk<TYPE>(r, sub);
 #pragma unroll
-  for (int t = 0; t < T; ++t) acc[t] = dot_core<TYPE>(r, sub, load_x<TYPE>(x, t, blk, sub), acc[t]);
+  for (int t = 0; t < T; ++t) acc[t] = dot_apply<TYPE>(p, load_x<TYPE>(x, t, blk, sub), acc[t]);
 }
 
 // Blocks per lane per pipeline stage (one stage = 8*U super-blocks of a row).
@@ -292,11 +310,13 @@ __device__ __forceinline__ void compute_reg(int nb, int sub, int bl, const XReg 
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (8 * u + bl < nb) {
+      const Prep<TYPE> p = prep_blk<TYPE>(c[u], sub);
 #pragma unroll
-      for (int t = 0; t < T; ++t) acc[t] = dot_core<TYPE>(c[u], sub, xr[u][t], acc[t]);
+      for (int t = 0; t < T; ++t) acc[t] = dot_apply<TYPE>(p, xr[u][t], acc[t]);
       if constexpr (MODE == kPair) {
+        const Prep<TYPE> p1 = prep_blk<TYPE>(c1[u], sub);
 #pragma unroll
-        for (int t = 0; t < T; ++t) acc1[t] = dot_core<TYPE>(c1[u], sub, xr[u][t], acc1[t]);
+        for (int t = 0; t < T; ++t) acc1[t] = dot_apply<TYPE>(p1, xr[u][t], acc1[t]);
       }
     }
   }

@@ -9,7 +9,14 @@ import sys
 from collections import defaultdict
 
 
+_MATCH = os.environ.get("PMC_MATCH")      # regex over kernel names (default: GEMM kernels)
+
+
 def _is_gemm(name):
+    if _MATCH:
+        import re
+
+        return re.search(_MATCH, name) is not None
     return "gemm" in name.lower() or "Cijk" in name
 
 
@@ -40,6 +47,11 @@ def main(paths):
         means = {c: sum(v) / len(v) for c, v in ctrs.items()}
         for c, v in sorted(ctrs.items()):
             print(f"   {c:28s} {means[c]:16.1f}  (n={len(v)})")
+        if "SQ_INSTS_MFMA" in means and means["SQ_INSTS_MFMA"]:
+            if "SQ_INSTS_VALU" in means:
+                print(f"   {'VALU insts per MFMA':28s} {means['SQ_INSTS_VALU'] / means['SQ_INSTS_MFMA']:16.2f}")
+        if means.get("SQ_INSTS_LDS") and "SQ_LDS_BANK_CONFLICT" in means:
+            print(f"   {'bank conflicts per LDS inst':28s} {means['SQ_LDS_BANK_CONFLICT'] / means['SQ_INSTS_LDS']:16.2f}")
         if durs.get(name):
             d = sorted(durs[name])[len(durs[name]) // 2]
             print(f"   {'duration_ns (median)':28s} {d:16.1f}")
