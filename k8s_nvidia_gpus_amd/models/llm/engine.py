@@ -96,6 +96,10 @@ class Engine:
         # GEMV decomposition override "waves,rows" (sweeps); default: the kernel's own
         self.gemv_cfg = dict(zip(("waves", "rows_per_wg"),
                                  map(int, os.environ.get("AMDK8S_LLM_GEMV", "0,0").split(","))))
+        # Infinity-Cache prefetch of each layer's gate|up weights on a side stream while the
+        # latency-bound q|k|v / attention / o_proj kernels run (AMDK8S_LLM_PREFETCH=<workgroups>)
+        self.prefetch_wgs = int(os.environ.get("AMDK8S_LLM_PREFETCH", "0"))
+        self._side = None
         if self.gpu:
             from k8s_nvidia_gpus_amd.ops import llm_kernels as LK
 
@@ -226,7 +230,16 @@ class Engine:
         qd = self._q8(b, c.dim)
         scale = 1.0 / math.sqrt(c.head_dim)
         G = self.gemv_cfg
+        pf = self.prefetch_wgs > 0
+        if pf:
+            main = torch.cuda.current_stream(self.device)
+            if self._side is None:
+                self._side = torch.cuda.Stream(self.device)
         for i, L in enumerate(self.w.layers):
+            if pf:                     # fork: the side stream streams gate|up into the MALL
+                self._side.wait_stream(main)
+                planes = [L.wg.q, L.wg.qh, L.wg.sc, L.wg.d, L.wu.q, L.wu.qh, L.wu.sc, L.wu.d]
+                self.LK.prefetch(planes, self.prefetch_wgs, self._side)
             # RMSNorm + Q8 quantisation run in each GEMV's prologue (fp32 input + norm weight)
             off = 0
             for w in L.wqkv:
@@ -249,6 +262,8 @@ class Engine:
             LK.qgemv(L.wd, None, None, None, b.h, LK.RESID, xf=b.t, **G)
         LK.qgemv(self.w.output, None, None, None, b.logits, LK.STORE, xf=b.h,
                  norm_w=self.w.out_norm, eps=c.eps, **G)
+        if pf:
+            main.wait_stream(self._side)   # join (graph capture needs every fork joined)
 
     def _decode_native(self, tokens: Sequence[int], positions: Sequence[int],
                        slots: Sequence[int]) -> torch.Tensor:

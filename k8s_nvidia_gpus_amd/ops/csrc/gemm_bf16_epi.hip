@@ -1,12 +1,18 @@
-// bf16 MFMA GEMM with fused epilogues for the diffusion-transformer / UNet projections (gfx950).
+// bf16 / fp16 MFMA GEMM + implicit-GEMM 3×3 convolution with fused epilogues, for the diffusion
+// transformer / UNet projections and the UNet / VAE convolutions (gfx950).
 //
-//   Y = A · Bᵀ (+ bias)            A [M, K] bf16 activations (row-major, lda)
-//                                  B [N, K] bf16 nn.Linear weight (row-major, ldb)
+//   Y = A · Bᵀ (+ bias)            A [M, K] activations (row-major, lda) — or, for a convolution,
+//                                  the NHWC input gathered per 3×3 tap (zero rows for padding,
+//                                  stride 2, or a nearest-2× upsample folded into the addressing)
+//                                  B [N, K] nn.Linear weight / [Cout, 3·3·Cin] packed conv weight
 //   epilogue (fp32 accumulators, one pass, no extra kernel):
-//     EPI_STORE   out[m, n] = bf16(Y)
-//     EPI_GELU    out[m, n] = bf16(gelu_tanh(Y))                      (DiT / text-embedding FFN-in)
+//     EPI_STORE   out[m, n] = 16bit(Y)
+//     EPI_GELU    out[m, n] = 16bit(gelu_tanh(Y))                     (DiT / text-embedding FFN-in)
 //     EPI_RESID   x[m, n]  += Y · gate[m / rows_per_gate, n]          (fp32 residual stream, in place;
 //                                                                      gate = AdaLN gate or none)
+//     EPI_ADD     out[m, n] = 16bit(Y) + r[m, n]                      (UNet conv2 + shortcut)
+//   split-K (grids that cannot fill the chip): each split writes its fp32 partial tile to its own
+//   workspace slice; splitk_finalize sums the slices in a fixed order and applies the epilogue.
 //
 // The validator GEMMs (gemm_bf16_gfx950*.hip) use 256×256 tiles; the Wan2.1 DiT at the reference
 // defaults (512×320×16 frames → 2×2560 token rows with CFG, generate_wan_t2v.py:305-312) has
@@ -441,6 +447,22 @@ __global__ void __launch_bounds__(256) splitk_finalize(const Args a) {
       v1[2 * e + 1] += h2f<F16>((uint16_t)(b32[e + 2] >> 16));
     }
   }
+  if constexpr (EPI == EPI_RESID) {     // x += gate · (Y + bias), fp32 in place
+    f32x4* xp = reinterpret_cast<f32x4*>(a.x + (size_t)m * a.ldx + n);
+    f32x4 x0 = xp[0], x1 = xp[1];
+    if (a.gate) {
+      const f32x4* g = reinterpret_cast<const f32x4*>(
+          a.gate + (size_t)(m / a.rows_per_gate) * a.gate_stride + n);
+      x0 += v0 * g[0];
+      x1 += v1 * g[1];
+    } else {
+      x0 += v0;
+      x1 += v1;
+    }
+    xp[0] = x0;
+    xp[1] = x1;
+    return;
+  }
   if constexpr (EPI == EPI_GELU) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -554,7 +576,7 @@ template <int CONV>
 int launch_epi(Args a, int epi, bool f16, hipStream_t stream) {
   int tile, splits;
   amdk8s_gemm_epi_plan(a.M, a.N, a.K, &tile, &splits);
-  if (!a.ws || epi == EPI_RESID) splits = 1;         // no workspace: one pass over K
+  if (!a.ws) splits = 1;                             // no workspace: one pass over K
   const long nwg = tile_grid(tile, a.M, a.N);
   if (nwg * splits > 0x7fffffff) return (int)hipErrorInvalidValue;
   a.splits = splits;
@@ -598,10 +620,12 @@ int launch_epi(Args a, int epi, bool f16, hipStream_t stream) {
     if (f16) {
       if (epi == EPI_GELU) fin(splitk_finalize<EPI_GELU, true>);
       else if (epi == EPI_ADD) fin(splitk_finalize<EPI_ADD, true>);
+      else if (epi == EPI_RESID) fin(splitk_finalize<EPI_RESID, true>);
       else fin(splitk_finalize<EPI_STORE, true>);
     } else {
       if (epi == EPI_GELU) fin(splitk_finalize<EPI_GELU, false>);
       else if (epi == EPI_ADD) fin(splitk_finalize<EPI_ADD, false>);
+      else if (epi == EPI_RESID) fin(splitk_finalize<EPI_RESID, false>);
       else fin(splitk_finalize<EPI_STORE, false>);
     }
   }
@@ -620,9 +644,9 @@ int check_out(int epi, int N, const void* out, int ldo, const void* r, int ldr) 
 extern "C" {
 
 // epi: 0 store, 1 GELU, 2 fp32 gated residual (x, gate), 3 add (out = Y + bias + r, 16-bit r).
-// ws: optional fp32 workspace of amdk8s_gemm_epi_splits(M, N, K) × M × N floats; when given (and
-// the epilogue is not RESID), problems that cannot fill the chip run split-K (each split stores
-// its partial tile to its own slice) + a finalize pass that sums the slices in a fixed order.
+// ws: optional fp32 workspace of amdk8s_gemm_epi_splits(M, N, K) × M × N floats; when given,
+// problems that cannot fill the chip run split-K (each split stores its partial tile to its own
+// slice) + a finalize pass that sums the slices in a fixed order and applies the epilogue.
 int amdk8s_gemm_epi(int epi, int dtype, const void* A, const void* B, const void* bias, void* out,
                     float* x, const float* gate, const void* r, int M, int N, int K, int lda,
                     int ldb, int ldo, int ldx, int ldr, int rows_per_gate, int gate_stride,

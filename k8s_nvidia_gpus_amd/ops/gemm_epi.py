@@ -118,7 +118,7 @@ def splits(m: int, n: int, k: int) -> int:
 
 
 def _workspace(epi: int, m: int, n: int, k: int, dev) -> Optional[torch.Tensor]:
-    sp = 1 if epi == EPI_RESID else splits(m, n, k)
+    sp = splits(m, n, k)
     if sp <= 1:
         return None
     return torch.empty(sp * m * n, dtype=torch.float32, device=dev)

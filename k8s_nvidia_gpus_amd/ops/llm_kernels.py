@@ -46,6 +46,8 @@ def _lib():
             lib.amdk8s_llm_q4k_repack.argtypes = [vp, cl, vp, vp, vp, vp]
             lib.amdk8s_llm_q4k_repack.restype = ci
             lib.amdk8s_llm_q6k_repack.restype = ci
+            lib.amdk8s_llm_prefetch.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(cl), ci, ci, vp]
+            lib.amdk8s_llm_prefetch.restype = ci
             _declared = True
     return lib
 
@@ -143,3 +145,17 @@ def q4k_repack(raw, qs, scm, dm) -> None:
     _check(_lib().amdk8s_llm_q4k_repack(raw.data_ptr(), raw.numel() // 144, qs.data_ptr(),
                                         scm.data_ptr(), dm.data_ptr(), _stream(raw)),
            "amdk8s_llm_q4k_repack")
+
+
+def prefetch(tensors, wgs: int = 32, stream=None) -> None:
+    """Read ``tensors`` (16-B aligned, sizes % 16 == 0; at most 8) through the cache hierarchy on
+    ``stream`` (default: current) so a following kernel finds them in the Infinity Cache."""
+    ts = [t for t in tensors if t is not None]
+    if not ts:
+        return
+    if len(ts) > 8:
+        raise ValueError("prefetch: at most 8 ranges")
+    ptrs = (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+    sizes = (ctypes.c_long * len(ts))(*[(t.numel() * t.element_size()) // 16 * 16 for t in ts])
+    st = (stream or torch.cuda.current_stream(ts[0].device)).cuda_stream
+    _check(_lib().amdk8s_llm_prefetch(ptrs, sizes, len(ts), wgs, st), "amdk8s_llm_prefetch")

@@ -230,3 +230,20 @@ def test_split_k_small_grid(GE, epi, dtype):
         ref = ref.to(dtype).float() + r.float()
         y = GE.linear_add(x, w, b, r)
     torch.testing.assert_close(y.float(), ref, rtol=tol, atol=2 * tol)
+
+
+@pytest.mark.parametrize("gated", [False, True])
+def test_split_k_gated_residual(GE, gated):
+    """The LLM prefill's ffn_down shape (512 tokens, N 3584, K 18944): split-K with the fp32
+    (gated) residual update in the finalize pass."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(9)
+    m, n, k = 512, 3584, 18944
+    assert GE.splits(m, n, k) > 1
+    x = torch.randn(1, m, k, generator=g, device=dev).half()
+    w = (torch.randn(n, k, generator=g, device=dev) / k ** 0.5).half()
+    res = torch.randn(1, m, n, generator=g, device=dev)
+    gate = torch.randn(1, n, generator=g, device=dev) if gated else None
+    want = res + _ref(x, w, None).view(1, m, n) * (gate[:, None, :] if gated else 1.0)
+    GE.linear_residual_(res, x, w, None, gate)
+    torch.testing.assert_close(res, want, rtol=5e-3, atol=5e-3)
