@@ -98,7 +98,14 @@ class Engine:
                                  map(int, os.environ.get("AMDK8S_LLM_GEMV", "0,0").split(","))))
         # Infinity-Cache prefetch of each layer's gate|up weights on a side stream while the
         # latency-bound q|k|v / attention / o_proj kernels run (AMDK8S_LLM_PREFETCH=<workgroups>)
+        # measured and rejected (profiles/r03/k: 2.11 -> 3.08-3.50 ms per T=1 step): the prefetch
+        # competes with the GEMVs for HBM and its 2 GB per step is slower than the step itself
         self.prefetch_wgs = int(os.environ.get("AMDK8S_LLM_PREFETCH", "0"))
+        # from this many tokens per step on, each GEMV input is RMS-normalised + quantised ONCE by
+        # rmsnorm_q8 instead of redundantly in every GEMV workgroup's prologue.  One threshold for
+        # every T keeps decode batch-invariant only if it is 1 or never reached (the two paths
+        # reduce the sum of squares in different orders): 1 = always, 0 = never.
+        self.q8_split_T = int(os.environ.get("AMDK8S_LLM_Q8SPLIT", "0")) or (1 << 30)
         self._side = None
         if self.gpu:
             from k8s_nvidia_gpus_amd.ops import llm_kernels as LK
@@ -230,6 +237,16 @@ class Engine:
         qd = self._q8(b, c.dim)
         scale = 1.0 / math.sqrt(c.head_dim)
         G = self.gemv_cfg
+
+        def act(xf, norm_w, k):
+            """GEMV input: ((x8, dx, sx), {}) quantised here, or ((None,) * 3, fused-prologue
+            kwargs)."""
+            if b.T >= self.q8_split_T:
+                q = self._q8(b, k)
+                LK.rmsnorm_q8(xf, norm_w, c.eps, *q)
+                return q, {}
+            return (None, None, None), dict(xf=xf, norm_w=norm_w, eps=c.eps)
+
         pf = self.prefetch_wgs > 0
         if pf:
             main = torch.cuda.current_stream(self.device)
@@ -240,11 +257,13 @@ class Engine:
                 self._side.wait_stream(main)
                 planes = [L.wg.q, L.wg.qh, L.wg.sc, L.wg.d, L.wu.q, L.wu.qh, L.wu.sc, L.wu.d]
                 self.LK.prefetch(planes, self.prefetch_wgs, self._side)
-            # RMSNorm + Q8 quantisation run in each GEMV's prologue (fp32 input + norm weight)
+            # RMSNorm + Q8 quantisation: in each GEMV's prologue (fp32 input + norm weight), or once
+            # per input for larger T (act())
             off = 0
+            xin = act(b.h, L.attn_norm, c.dim)
             for w in L.wqkv:
-                LK.qgemv(w, None, None, None, b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:],
-                         ldo=b.qkv.stride(0), xf=b.h, norm_w=L.attn_norm, eps=c.eps, **G)
+                LK.qgemv(w, *xin[0], b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:],
+                         ldo=b.qkv.stride(0), **xin[1], **G)
                 off += w.n
             if fused:
                 LK.attn_decode(None, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
@@ -257,11 +276,12 @@ class Engine:
                                c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
                                span=span)
             LK.qgemv(L.wo, *qd, b.h, LK.RESID, **G)
-            LK.qgemv(L.wg, None, None, None, b.t, LK.PAIR, w1=L.wu, xf=b.h, norm_w=L.ffn_norm,
-                     eps=c.eps, **G)
-            LK.qgemv(L.wd, None, None, None, b.h, LK.RESID, xf=b.t, **G)
-        LK.qgemv(self.w.output, None, None, None, b.logits, LK.STORE, xf=b.h,
-                 norm_w=self.w.out_norm, eps=c.eps, **G)
+            xin = act(b.h, L.ffn_norm, c.dim)
+            LK.qgemv(L.wg, *xin[0], b.t, LK.PAIR, w1=L.wu, **xin[1], **G)
+            xin = act(b.t, None, c.ffn)
+            LK.qgemv(L.wd, *xin[0], b.h, LK.RESID, **xin[1], **G)
+        xin = act(b.h, self.w.out_norm, c.dim)
+        LK.qgemv(self.w.output, *xin[0], b.logits, LK.STORE, **xin[1], **G)
         if pf:
             main.wait_stream(self._side)   # join (graph capture needs every fork joined)
 
