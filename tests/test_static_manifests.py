@@ -529,6 +529,37 @@ def test_bootstrap_refuses_placeholder_images():
     assert "--registry" in text and "retarget.py --check" in text
 
 
+def test_build_images_script_builds_every_image_and_pushes_only_on_request(tmp_path):
+    """hack/build-images.sh: one image per images/<name>/Dockerfile under the given registry,
+    `docker push` only with --push, the placeholder registry refused; CI builds without pushing."""
+    import os
+    import subprocess
+
+    calls = tmp_path / "calls"
+    fake = tmp_path / "bin"
+    fake.mkdir()
+    (fake / "docker").write_text(f"#!/bin/sh\necho \"$@\" >> {calls}\n")
+    (fake / "docker").chmod(0o755)
+    env = dict(os.environ, PATH=f"{fake}:{os.environ['PATH']}")
+    sh = REPO / "hack/build-images.sh"
+    p = subprocess.run([str(sh), "--registry", "ghcr.io/me", "--tag", "1.2.3"], env=env,
+                       capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+    lines = calls.read_text().splitlines()
+    images = sorted(d.name for d in (REPO / "images").iterdir() if (d / "Dockerfile").exists())
+    assert [ln.split()[0] for ln in lines] == ["build"] * len(images)
+    for name in images:
+        assert any(f"ghcr.io/me/amd-gpu-{name}:1.2.3" in ln for ln in lines)
+    calls.unlink()
+    p = subprocess.run([str(sh), "--registry", "ghcr.io/me", "--push"], env=env, capture_output=True, text=True)
+    assert p.returncode == 0 and sum(ln.startswith("push ") for ln in calls.read_text().splitlines()) == len(images)
+    assert subprocess.run([str(sh), "--registry", "ghcr.io/example-org"], env=env,
+                          capture_output=True).returncode == 2
+    ci = yaml.safe_load((REPO / ".github/workflows/ci.yaml").read_text())
+    run = " ".join(st.get("run", "") for st in ci["jobs"]["images"]["steps"])
+    assert "hack/build-images.sh" in run and "--push" not in run
+
+
 def test_driver_daemonset_only_on_nodes_with_an_amd_accelerator():
     """A CPU-only worker must not get a driver pod that never turns ready (it would hold the
     operator Kustomization's wait: true and every app that dependsOn it)."""
