@@ -29,6 +29,7 @@
 //   o_proj input directly.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace {
 
@@ -994,6 +995,17 @@ int launch_one(const GemvArgs& a, int waves, hipStream_t st) {
 // (short rows), else the type/mode batch; register-resident activations when a row is one stage
 // and U*T <= 4 (VGPR budget).  Every variant runs the same dot_core, so the choice never changes
 // a result bit.
+// AMDK8S_LLM_REGX_T: largest T whose 2-block rows keep their activations in registers (default 2;
+// 4 trades ~50 VGPRs for no per-row LDS activation reads — A/B knob).
+static int regx_max_t() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("AMDK8S_LLM_REGX_T");
+    v = e ? atoi(e) : 2;
+  }
+  return v;
+}
+
 template <int TYPE, int T, int MODE>
 int launch_gemv(const GemvArgs& a, int waves, hipStream_t st) {
   constexpr int KB = kBatch<TYPE, MODE>;
@@ -1002,6 +1014,7 @@ int launch_gemv(const GemvArgs& a, int waves, hipStream_t st) {
   if constexpr (KB >= 2) {
     if (nb <= 16) {
       if constexpr (T <= 2) return launch_one<TYPE, T, MODE, 2, true>(a, waves, st);
+      else if (T <= regx_max_t()) return launch_one<TYPE, T, MODE, 2, true>(a, waves, st);
       else return launch_one<TYPE, T, MODE, 2, false>(a, waves, st);
     }
   }

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 3 session M: LLM decode, register-resident activations for T = 3, 4 (AMDK8S_LLM_REGX_T A/B)
+# on top of the once-per-input Q8 pass; tests with the new default.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+OUT=gpurun_out/r03/m
+mkdir -p $OUT
+for r in 2 4; do
+  AMDK8S_LLM_REGX_T=$r timeout -k 10 400 python -u tools/llm_bench.py --gemv --out $OUT/llm_bench_regx$r.json \
+    > $OUT/llm_bench_regx$r.log 2>&1 || { tail -30 $OUT/llm_bench_regx$r.log; exit 1; }
+  echo "regx_t=$r"; grep -v '^{' $OUT/llm_bench_regx$r.log | grep -E "decode|prefill"
+done
+AMDK8S_LLM_REGX_T=4 timeout -k 10 600 python -u -m pytest tests/test_llm_gpu.py -x -q -p no:warnings --timeout 200 \
+  --timeout-method thread > $OUT/pytest_llm.log 2>&1 || { tail -60 $OUT/pytest_llm.log; exit 1; }
+tail -2 $OUT/pytest_llm.log
