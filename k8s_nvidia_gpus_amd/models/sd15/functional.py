@@ -75,6 +75,19 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -
     return F.linear(x, w, b)
 
 
+def linear_add(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor],
+               r: torch.Tensor) -> torch.Tensor:
+    """``x·wᵀ + b + r`` with the residual add in the GEMM epilogue (``r`` [..., N], x's dtype)."""
+    if _GEMM != "torch" and _native(x) and r.dtype == x.dtype and r.stride(-1) == 1:
+        from k8s_nvidia_gpus_amd.ops import gemm_epi
+
+        if gemm_epi.supported(x, w):
+            rr = r.reshape(-1, r.shape[-1])
+            if rr.data_ptr() % 16 == 0 and rr.stride(0) % 8 == 0:
+                return gemm_epi.linear_add(x, w, b, rr).view(r.shape)
+    return F.linear(x, w, b) + r
+
+
 _CONV = os.environ.get("AMDK8S_SD_CONV", "native")   # native | torch (A/B against MIOpen)
 
 

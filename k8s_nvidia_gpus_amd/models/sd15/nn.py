@@ -178,8 +178,10 @@ class FeedForward(nn.Module):
         inner = dim * mult
         self.net = nn.ModuleList([GEGLU(dim, inner), nn.Dropout(0.0), nn.Linear(inner, dim)])
 
-    def forward(self, x):
+    def forward(self, x, residual: Optional[torch.Tensor] = None):
         out = self.net[2]
+        if residual is not None:       # residual + FF(x): the add rides in the GEMM epilogue
+            return SF.linear_add(self.net[0](x), out.weight, out.bias, residual)
         return SF.linear(self.net[0](x), out.weight, out.bias)
 
 
@@ -198,7 +200,7 @@ class BasicTransformerBlock(nn.Module):
         h = SF.add_layernorm(x, None, n1.weight, n1.bias, n1.eps)
         x, h = SF.add_layernorm(x, self.attn1(h), n2.weight, n2.bias, n2.eps)
         x, h = SF.add_layernorm(x, self.attn2(h, context), n3.weight, n3.bias, n3.eps)
-        return x + self.ff(h)
+        return self.ff(h, residual=x)
 
 
 class Transformer2DModel(nn.Module):
@@ -224,9 +226,11 @@ class Transformer2DModel(nn.Module):
         tokens = self._as_linear(self.proj_in, tokens)
         for blk in self.transformer_blocks:
             tokens = blk(tokens, context)
-        tokens = self._as_linear(self.proj_out, tokens)
-        out = tokens.reshape(n, h, w, c).permute(0, 3, 1, 2)
-        return out + residual
+        po = self.proj_out                # proj_out + the block's residual in one GEMM epilogue
+        res_tokens = residual.permute(0, 2, 3, 1).reshape(n, h * w, c)
+        tokens = SF.linear_add(tokens, po.weight.view(po.out_channels, po.in_channels), po.bias,
+                               res_tokens)
+        return tokens.reshape(n, h, w, c).permute(0, 3, 1, 2)
 
 
 class Downsample2D(nn.Module):

@@ -14,3 +14,9 @@ done
 AMDK8S_LLM_REGX_T=4 timeout -k 10 600 python -u -m pytest tests/test_llm_gpu.py -x -q -p no:warnings --timeout 200 \
   --timeout-method thread > $OUT/pytest_llm.log 2>&1 || { tail -60 $OUT/pytest_llm.log; exit 1; }
 tail -2 $OUT/pytest_llm.log
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
+  tests/test_sd15_gpu.py > $OUT/pytest_sd15.log 2>&1 || { tail -40 $OUT/pytest_sd15.log; exit 1; }
+tail -2 $OUT/pytest_sd15.log
+timeout -k 10 500 python -u tools/sd15_bench.py --arms native-graph --batches 1,8 --miopen-find \
+  --out $OUT/sd15_bench.json > $OUT/sd15_bench.log 2>&1 || { tail -20 $OUT/sd15_bench.log; exit 1; }
+grep -E "unet|e2e" $OUT/sd15_bench.log
