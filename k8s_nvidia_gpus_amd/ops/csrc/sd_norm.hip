@@ -16,11 +16,23 @@
 // Deterministic: no atomics anywhere.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace {
 
 constexpr int kMaxThreads = 1024;
 constexpr int kMaxChunks = 16;  // stats-pass chunks per image (merged by every apply block)
+
+// AMDK8S_GN_CHUNKS overrides kMaxChunks (A/B: more, shorter stats blocks vs a longer merge).
+int max_chunks() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("AMDK8S_GN_CHUNKS");
+    const int c = e ? atoi(e) : 0;
+    v = (c >= 1 && c <= 256) ? c : kMaxChunks;
+  }
+  return v;
+}
 
 __device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
 
@@ -376,7 +388,7 @@ GnShape gn_shape(int N, int HW, int C, int G, int pass) {
     s.R = s.VC >= 1024 ? 1 : 1024 / s.VC;
     if (s.R > HW) s.R = HW;
     int chunks = (HW + s.R - 1) / s.R;
-    if (chunks > kMaxChunks) chunks = kMaxChunks;
+    if (chunks > max_chunks()) chunks = max_chunks();
     s.rows1 = (HW + chunks - 1) / chunks;
     s.chunks1 = (HW + s.rows1 - 1) / s.rows1;
   } else {

@@ -20,3 +20,9 @@ tail -2 $OUT/pytest_sd15.log
 timeout -k 10 500 python -u tools/sd15_bench.py --arms native-graph --batches 1,8 --miopen-find \
   --out $OUT/sd15_bench.json > $OUT/sd15_bench.log 2>&1 || { tail -20 $OUT/sd15_bench.log; exit 1; }
 grep -E "unet|e2e" $OUT/sd15_bench.log
+AMDK8S_GEMM_SPLITK=1 timeout -k 10 400 python -u tools/sd15_bench.py --arms native-graph --batches "" --miopen-find \
+  --out $OUT/sd15_bench_nosplit.json > $OUT/sd15_bench_nosplit.log 2>&1 || { tail -20 $OUT/sd15_bench_nosplit.log; exit 1; }
+echo "no split-K:"; grep -E "unet" $OUT/sd15_bench_nosplit.log
+AMDK8S_GN_CHUNKS=64 timeout -k 10 400 python -u tools/sd15_bench.py --arms native-graph --batches "" --miopen-find \
+  --out $OUT/sd15_bench_gn64.json > $OUT/sd15_bench_gn64.log 2>&1 || { tail -20 $OUT/sd15_bench_gn64.log; exit 1; }
+echo "GN 64 chunks:"; grep -E "unet" $OUT/sd15_bench_gn64.log
