@@ -107,6 +107,10 @@ class Engine:
         # reduce the sum of squares in different orders): 1 = always (default: T = 1 unchanged,
         # T = 4 3.98 -> 3.44 ms, profiles/r03/l), 0 = never.
         self.q8_split_T = int(os.environ.get("AMDK8S_LLM_Q8SPLIT", "1")) or (1 << 30)
+        # decode attention's chunk merge inside the attention kernel (last-arriving workgroup of a
+        # (token, kv head) combines; arrival counters stay zero between launches)
+        self.fused_combine = os.environ.get("AMDK8S_LLM_FUSED_COMBINE", "1") != "0"
+        self._attn_cnt = None
         self._side = None
         if self.gpu:
             from k8s_nvidia_gpus_amd.ops import llm_kernels as LK
@@ -238,6 +242,12 @@ class Engine:
         qd = self._q8(b, c.dim)
         scale = 1.0 / math.sqrt(c.head_dim)
         G = self.gemv_cfg
+        cnt = None
+        if self.fused_combine:
+            if self._attn_cnt is None:
+                self._attn_cnt = torch.zeros(self.max_T * c.kv_heads, dtype=torch.int32,
+                                             device=self.device)
+            cnt = self._attn_cnt
 
         def act(xf, norm_w, k):
             """GEMV input: ((x8, dx, sx), {}) quantised here, or ((None,) * 3, fused-prologue
@@ -269,13 +279,13 @@ class Engine:
             if fused:
                 LK.attn_decode(None, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
                                c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
-                               span=span, qkv=b.qkv, cos_t=self.cos, sin_t=self.sin)
+                               span=span, qkv=b.qkv, cos_t=self.cos, sin_t=self.sin, cnt=cnt)
             else:
                 LK.rope_kv(b.qkv, b.pos, b.slot, self.cos, self.sin, c.heads, c.kv_heads,
                            c.head_dim, self.max_ctx, b.qrot, self.k_cache[i], self.v_cache[i])
                 LK.attn_decode(b.qrot, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
                                c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
-                               span=span)
+                               span=span, cnt=cnt)
             LK.qgemv(L.wo, *qd, b.h, LK.RESID, **G)
             xin = act(b.h, L.ffn_norm, c.dim)
             LK.qgemv(L.wg, *xin[0], b.t, LK.PAIR, w1=L.wu, **xin[1], **G)

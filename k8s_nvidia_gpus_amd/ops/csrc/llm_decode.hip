@@ -652,7 +652,93 @@ struct AttnArgs {
   float scale;
   float* po;
   float* pml;
+  // fused combine (cnt != null): the last of a (token, kv head)'s nsplit workgroups merges its G
+  // heads' chunks and writes the Q8 o_proj input (and the fp32 output when out != null)
+  int* cnt;               // [T][Hkv] arrival counters, zero between launches (the last resets)
+  float* out;
+  int8_t* x8;
+  float* dx;
+  float* sx;
 };
+
+// Arrival of one (token, kv head) workgroup: publishes its partials, counts in, and tells whether
+// it was the last of the nsplit (then the others' partials are visible to it).
+__device__ __forceinline__ bool arrive_last(int* cnt, int nsplit) {
+  __shared__ int last;
+  __threadfence();                       // release this workgroup's po / pml device-wide
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    last = atomicAdd(cnt, 1) == nsplit - 1;
+    if (last) atomicExch(cnt, 0);        // every split has arrived: ready for the next launch
+  }
+  __syncthreads();
+  if (last) __threadfence();             // acquire the other workgroups' partials
+  return last;
+}
+
+// Merge the chunks of head h of token t and quantise the attention output to Q8 (the o_proj
+// input): thread dd = one output dim; a 32-dim block = half a wave (dd & 31 within a wave).
+__device__ __forceinline__ void combine_head(const float* __restrict__ po,
+                                             const float* __restrict__ pml,
+                                             const int* __restrict__ pos, int H, int nsplit,
+                                             int h, int t, int dd, float* __restrict__ out,
+                                             int8_t* __restrict__ x8, float* __restrict__ dx,
+                                             float* __restrict__ sx) {
+  const int ns = min(nsplit, (pos[t] + kAttnChunk) / kAttnChunk);
+  const long hb = ((long)t * H + h) * nsplit;
+  // chunk partials in groups of 8 with all loads in flight (indices clamped, extra terms masked)
+  float m = -INFINITY;
+  for (int s0 = 0; s0 < ns; s0 += 8) {
+    float2 ml[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      ml[u] = *reinterpret_cast<const float2*>(pml + (hb + min(s0 + u, ns - 1)) * 2);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) m = fmaxf(m, ml[u].x);
+  }
+  float den = 0.f, v = 0.f;
+  for (int s0 = 0; s0 < ns; s0 += 8) {
+    float2 ml[8];
+    float ov[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long s = hb + min(s0 + u, ns - 1);
+      ml[u] = *reinterpret_cast<const float2*>(pml + s * 2);
+      ov[u] = po[s * kHeadDim + dd];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float wgt = (s0 + u < ns && ml[u].x != -INFINITY) ? __expf(ml[u].x - m) : 0.f;
+      den += wgt * ml[u].y;
+      v += wgt * ov[u];
+    }
+  }
+  v = den > 0.f ? v / den : 0.f;
+  const int K = H * kHeadDim, col = h * kHeadDim + dd;
+  if (out) out[(long)t * K + col] = v;
+  float amax = fabsf(v);
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, kWave));
+  const float d = amax / 127.f;
+  const int qv = d > 0.f ? (int)__builtin_rintf(v / d) : 0;
+  x8[(long)t * K + col] = (int8_t)qv;
+  int s16 = qv;
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) s16 += __shfl_xor(s16, o, kWave);
+  if ((dd & 31) == 0) dx[(long)t * (K >> 5) + (col >> 5)] = d;
+  if ((dd & 15) == 0) sx[(long)t * (K >> 4) + (col >> 4)] = d * (float)s16;
+}
+
+// grid (H, T), 128 threads.
+__global__ void __launch_bounds__(128) attn_combine_q8_kernel(const float* __restrict__ po,
+                                                              const float* __restrict__ pml,
+                                                              const int* __restrict__ pos, int H,
+                                                              int nsplit, float* __restrict__ out,
+                                                              int8_t* __restrict__ x8,
+                                                              float* __restrict__ dx,
+                                                              float* __restrict__ sx) {
+  combine_head(po, pml, pos, H, nsplit, blockIdx.x, blockIdx.y, threadIdx.x, out, x8, dx, sx);
+}
 
 template <int G>
 __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
@@ -675,11 +761,22 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   const int len = pos[t] + 1;
   const int p0 = sp * kAttnChunk;
   const long pidx = ((long)t * H + kh * G) * nsplit + sp;   // + g * nsplit
+  auto merge = [&]() {                   // fused combine by the last-arriving workgroup
+    if (a.cnt && arrive_last(a.cnt + t * Hkv + kh, nsplit)) {
+      for (int g0 = 0; g0 < G; g0 += 2) {
+        const int g = g0 + (threadIdx.x >> 7);
+        if (g < G)
+          combine_head(po, pml, pos, H, nsplit, kh * G + g, t, threadIdx.x & 127, a.out, a.x8,
+                       a.dx, a.sx);
+      }
+    }
+  };
   if (p0 >= len) {
     if (threadIdx.x < G) {
       pml[(pidx + (long)threadIdx.x * nsplit) * 2] = -INFINITY;
       pml[(pidx + (long)threadIdx.x * nsplit) * 2 + 1] = 0.f;
     }
+    merge();
     return;
   }
   const int n = min(kAttnChunk, len - p0);
@@ -828,61 +925,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
     pml[(pidx + (long)g * nsplit) * 2] = mls[g][0];
     pml[(pidx + (long)g * nsplit) * 2 + 1] = mls[g][1];
   }
-}
-
-// Merge the chunks of one head and quantise the attention output to Q8 (the o_proj input).
-// grid (H, T), 128 threads: thread = one output dim; a 32-dim block = half a wave.
-__global__ void __launch_bounds__(128) attn_combine_q8_kernel(const float* __restrict__ po,
-                                                              const float* __restrict__ pml,
-                                                              const int* __restrict__ pos, int H,
-                                                              int nsplit, float* __restrict__ out,
-                                                              int8_t* __restrict__ x8,
-                                                              float* __restrict__ dx,
-                                                              float* __restrict__ sx) {
-  const int h = blockIdx.x, t = blockIdx.y, dd = threadIdx.x;
-  const int ns = min(nsplit, (pos[t] + kAttnChunk) / kAttnChunk);
-  const long hb = ((long)t * H + h) * nsplit;
-  // chunk partials in groups of 8 with all loads in flight (indices clamped, extra terms masked)
-  float m = -INFINITY;
-  for (int s0 = 0; s0 < ns; s0 += 8) {
-    float2 ml[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      ml[u] = *reinterpret_cast<const float2*>(pml + (hb + min(s0 + u, ns - 1)) * 2);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) m = fmaxf(m, ml[u].x);
-  }
-  float den = 0.f, v = 0.f;
-  for (int s0 = 0; s0 < ns; s0 += 8) {
-    float2 ml[8];
-    float ov[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const long s = hb + min(s0 + u, ns - 1);
-      ml[u] = *reinterpret_cast<const float2*>(pml + s * 2);
-      ov[u] = po[s * kHeadDim + dd];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float wgt = (s0 + u < ns && ml[u].x != -INFINITY) ? __expf(ml[u].x - m) : 0.f;
-      den += wgt * ml[u].y;
-      v += wgt * ov[u];
-    }
-  }
-  v = den > 0.f ? v / den : 0.f;
-  const int K = H * kHeadDim, col = h * kHeadDim + dd;
-  if (out) out[(long)t * K + col] = v;
-  float amax = fabsf(v);
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, kWave));
-  const float d = amax / 127.f;
-  const int qv = d > 0.f ? (int)__builtin_rintf(v / d) : 0;
-  x8[(long)t * K + col] = (int8_t)qv;
-  int s16 = qv;
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) s16 += __shfl_xor(s16, o, kWave);
-  if ((dd & 31) == 0) dx[(long)t * (K >> 5) + (col >> 5)] = d;
-  if ((dd & 15) == 0) sx[(long)t * (K >> 4) + (col >> 4)] = d * (float)s16;
+  merge();
 }
 
 // ---------------------------------------------------------------- dequantisation (rows → fp16/fp32)
@@ -1149,11 +1192,13 @@ int amdk8s_llm_rope_kv(const void* qkv, int ldq, const void* pos, const void* sl
 // caller buckets it so a captured graph does not launch empty chunks up to max_ctx.
 // qkv (nullable): the raw q|k|v projection [T][ldq] — fused RoPE + KV write (distinct slots
 // only, see attn_decode_kernel); q is then unused.
+// cnt (nullable): [T][Hkv] int32 arrival counters, zero-initialised once by the caller and left
+// zero by every launch: the combine runs inside the attention kernel (no second launch).
 int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* cos_t,
                            const void* sin_t, const void* pos, const void* slot, void* kc,
                            void* vc, int H, int Hkv, int head_dim, int max_ctx, int span,
                            float scale, void* po, void* pml, void* out, void* x8, void* dx,
-                           void* sx, int T, void* stream) {
+                           void* sx, int T, void* cnt, void* stream) {
   if (span <= 0) span = max_ctx;
   if (head_dim != kHeadDim || H % Hkv || H / Hkv > kMaxGroup || max_ctx % kAttnChunk ||
       span % kAttnChunk || span > max_ctx || T < 1)
@@ -1174,6 +1219,11 @@ int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* 
   aa.H = H; aa.Hkv = Hkv; aa.max_ctx = max_ctx; aa.nsplit = nsplit; aa.scale = scale;
   aa.po = static_cast<float*>(po);
   aa.pml = static_cast<float*>(pml);
+  aa.cnt = static_cast<int*>(cnt);
+  aa.out = static_cast<float*>(out);
+  aa.x8 = static_cast<int8_t*>(x8);
+  aa.dx = static_cast<float*>(dx);
+  aa.sx = static_cast<float*>(sx);
   if (!qkv && !q) return 2;
   if (qkv && (!cos_t || !sin_t)) return 2;
   auto launch = [&](auto kern) {
@@ -1191,6 +1241,7 @@ int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* 
     default: return 2;
   }
   if (hipGetLastError() != hipSuccess) return 1;
+  if (cnt) return 0;                     // combined in-kernel
   hipLaunchKernelGGL(attn_combine_q8_kernel, dim3(H, T), dim3(128), 0, st,
                      static_cast<const float*>(po), static_cast<const float*>(pml),
                      static_cast<const int*>(pos), H, nsplit, static_cast<float*>(out),

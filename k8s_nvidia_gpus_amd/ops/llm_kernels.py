@@ -37,7 +37,7 @@ def _lib():
                                                ci, vp]
             lib.amdk8s_llm_rope_kv.restype = ci
             lib.amdk8s_llm_attn_decode.argtypes = [vp, vp, ci, vp, vp, vp, vp, vp, vp, ci, ci, ci,
-                                                   ci, ci, cf, vp, vp, vp, vp, vp, vp, ci, vp]
+                                                   ci, ci, cf, vp, vp, vp, vp, vp, vp, ci, vp, vp]
             lib.amdk8s_llm_attn_decode.restype = ci
             lib.amdk8s_llm_dequant.argtypes = [ci, vp, vp, vp, vp, vp, ci, ci, vp, ci, vp]
             lib.amdk8s_llm_dequant.restype = ci
@@ -109,20 +109,21 @@ def rope_kv(qkv, pos, slot, cos_t, sin_t, heads: int, kv_heads: int, head_dim: i
 
 def attn_decode(q, pos, slot, kc, vc, heads: int, kv_heads: int, head_dim: int, max_ctx: int,
                 scale: float, po, pml, x8, dx, sx, out=None, span: int = 0, qkv=None,
-                cos_t=None, sin_t=None) -> None:
+                cos_t=None, sin_t=None, cnt=None) -> None:
     """Split-context decode attention + combine + Q8 quantisation of the output.
 
     ``span``: context positions this call covers (multiple of ``attn_chunk()``, above every
     position; 0 = ``max_ctx``).  With ``qkv`` (the raw q|k|v projection) and the RoPE tables, the
     kernel also rotates q/k and writes the new K/V itself (``q`` unused, pass None) — only when
-    every token of the step is in a distinct slot."""
+    every token of the step is in a distinct slot.  ``cnt``: int32 [T, kv_heads] zeros (kept zero
+    by every call) — the combine then runs inside the attention kernel, one launch instead of two."""
     ref = qkv if qkv is not None else q
     _check(_lib().amdk8s_llm_attn_decode(_p(q), _p(qkv), qkv.stride(0) if qkv is not None else 0,
                                          _p(cos_t), _p(sin_t), pos.data_ptr(), slot.data_ptr(),
                                          kc.data_ptr(), vc.data_ptr(), heads, kv_heads, head_dim,
                                          max_ctx, span, float(scale), po.data_ptr(), pml.data_ptr(),
                                          _p(out), x8.data_ptr(), dx.data_ptr(), sx.data_ptr(),
-                                         ref.shape[0], _stream(ref)), "amdk8s_llm_attn_decode")
+                                         ref.shape[0], _p(cnt), _stream(ref)), "amdk8s_llm_attn_decode")
 
 
 def dequant(w, out, rows=None) -> None:

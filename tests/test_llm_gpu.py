@@ -259,6 +259,38 @@ def test_fused_rope_attention_equals_separate_kernels(dev, LK, H, Hkv):
     torch.testing.assert_close(outs[1][2], outs[0][2], rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("H,Hkv", [(28, 4), (8, 8), (6, 2)])
+def test_in_kernel_combine_equals_combine_kernel(dev, LK, H, Hkv):
+    """The last-arriving workgroup's chunk merge (cnt given) is bit-identical to the separate
+    combine kernel, leaves the arrival counters at zero, and stays so over repeated launches."""
+    torch.manual_seed(5)
+    max_ctx, slots, T = 1024, 4, 4
+    kc = (torch.randn(slots, Hkv, max_ctx, 128, device=dev) * 0.5).half()
+    vc = torch.randn(slots, Hkv, max_ctx, 128, device=dev).half()
+    pos = torch.tensor([0, 63, 64, 1000], dtype=torch.int32, device=dev)
+    slot = torch.tensor([3, 0, 1, 2], dtype=torch.int32, device=dev)
+    q = torch.randn(T, H * 128, device=dev)
+    nsplit = max_ctx // LK.attn_chunk()
+    cnt = torch.zeros(T * Hkv, dtype=torch.int32, device=dev)
+    res = []
+    for use_cnt in (False, True, True):
+        po = torch.empty(T, H, nsplit, 128, device=dev)
+        pml = torch.empty(T, H, nsplit, 2, device=dev)
+        x8 = torch.empty(T, H * 128, dtype=torch.int8, device=dev)
+        dx = torch.empty(T, H * 4, device=dev)
+        sx = torch.empty(T, H * 8, device=dev)
+        out = torch.empty(T, H * 128, device=dev)
+        LK.attn_decode(q, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po, pml,
+                       x8, dx, sx, out=out, cnt=cnt if use_cnt else None)
+        torch.cuda.synchronize()
+        res.append((x8, dx, sx, out))
+        assert int(cnt.abs().sum()) == 0
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
+    for a, b in zip(res[1], res[2]):
+        assert torch.equal(a, b)
+
+
 @pytest.fixture(scope="module")
 def tiny_gguf(tmp_path_factory):
     from k8s_nvidia_gpus_amd.models.llm import tiny
