@@ -108,8 +108,11 @@ class Engine:
         # T = 4 3.98 -> 3.44 ms, profiles/r03/l), 0 = never.
         self.q8_split_T = int(os.environ.get("AMDK8S_LLM_Q8SPLIT", "1")) or (1 << 30)
         # decode attention's chunk merge inside the attention kernel (last-arriving workgroup of a
-        # (token, kv head) combines; arrival counters stay zero between launches)
-        self.fused_combine = os.environ.get("AMDK8S_LLM_FUSED_COMBINE", "1") != "0"
+        # (token, kv head) combines; arrival counters stay zero between launches).  Correct but
+        # measured slower (profiles/r03/n: T=1 2.10 -> 2.43 ms): the agent-scope release / acquire
+        # fences around the arrival counter write back / invalidate L2 across the XCDs, which
+        # costs more than the separate combine launch.  Off by default.
+        self.fused_combine = os.environ.get("AMDK8S_LLM_FUSED_COMBINE", "0") != "0"
         self._attn_cnt = None
         self._side = None
         if self.gpu:
