@@ -58,10 +58,10 @@ constexpr int BK = 64;
 constexpr int NSTAGE = 3;
 constexpr int GROUP_M = 8;
 
-// Tile geometry of a WM × WN wave grid (each wave 64×64).
-template <int WM, int WN>
+// Tile geometry of a WM × WN wave grid, each wave a (64·TM) × (64·TN) block.
+template <int WM, int WN, int TM = 1, int TN = 1>
 struct Geo {
-  static constexpr int BM = 64 * WM, BN = 64 * WN, NW = WM * WN, NT = 64 * NW;
+  static constexpr int BM = 64 * WM * TM, BN = 64 * WN * TN, NW = WM * WN, NT = 64 * NW;
   static constexpr int A_STAGE = BM * BK * 2, B_STAGE = BN * BK * 2;
   static constexpr int STAGE = A_STAGE + B_STAGE;
   static constexpr int RING = NSTAGE * STAGE;
@@ -142,9 +142,10 @@ __device__ __forceinline__ float gelu_tanh(float v) {
   return v * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(t));
 }
 
-template <int EPI, bool F16, int WM, int WN, int CONV = CONV_NONE>
+template <int EPI, bool F16, int WM, int WN, int CONV = CONV_NONE, int TM = 1, int TN = 1>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
-  using G = Geo<WM, WN>;
+  using G = Geo<WM, WN, TM, TN>;
+  constexpr int MI = 4 * TM, NJ = 4 * TN;       // 16×16 accumulator blocks per wave
   constexpr int BM = G::BM, BN = G::BN, NW = G::NW, NT = G::NT, LA = G::LA, LB = G::LB;
   constexpr int A_STAGE = G::A_STAGE, STAGE = G::STAGE;
   constexpr int CF_STRIDE = G::CF_STRIDE, CB_STRIDE = G::CB_STRIDE;
@@ -153,8 +154,8 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN;  // 64-row block
-  const int wn = wave % WN;  // 64-column block
+  const int wm = wave / WN;  // (64·TM)-row block
+  const int wn = wave % WN;  // (64·TN)-column block
 
   // ---- block → tile: bijective XCD remap, then GROUP_M order ----
   const int tiles_m = (a.M + BM - 1) / BM;
@@ -267,14 +268,14 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
   const int sw = fr >> 1;
   const int foff0 = fr * 128 + (((0 + fq) ^ sw) << 4);
   const int foff1 = fr * 128 + (((4 + fq) ^ sw) << 4);
-  const int a_wave = wm * 64 * 128;
-  const int b_wave = wn * 64 * 128;
+  const int a_wave = wm * 64 * TM * 128;
+  const int b_wave = wn * 64 * TN * 128;
 
-  f32x4 acc[4][4];   // [m 16-block][n 16-block]
+  f32x4 acc[MI][NJ];   // [m 16-block][n 16-block]
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   stage(0);
   if (T > 1) stage(1);
@@ -286,39 +287,39 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
     const char* sb = lds + (t % NSTAGE) * STAGE + A_STAGE + b_wave;
     // the first half's 8 fragment reads, then the second half's 8 issued between the first half's
     // MFMAs (explicit order, pinned by sched_barrier: the reads' latency hides under MFMAs)
-    bf16x8 af[2][4], bw[2][4];
+    bf16x8 af[2][MI], bw[2][NJ];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bw[0][j] = lds_read16(sb + j * 2048 + foff0);
+    for (int j = 0; j < NJ; ++j) bw[0][j] = lds_read16(sb + j * 2048 + foff0);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[0][i] = lds_read16(sa + i * 2048 + foff0);
+    for (int i = 0; i < MI; ++i) af[0][i] = lds_read16(sa + i * 2048 + foff0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[0][j] = mfma16<F16>(bw[0][j], af[0][0], acc[0][j]);
+    for (int j = 0; j < NJ; ++j) acc[0][j] = mfma16<F16>(bw[0][j], af[0][0], acc[0][j]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bw[1][j] = lds_read16(sb + j * 2048 + foff1);
+    for (int j = 0; j < NJ; ++j) bw[1][j] = lds_read16(sb + j * 2048 + foff1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[1][i] = lds_read16(sa + i * 2048 + foff1);
+    for (int i = 0; i < MI; ++i) af[1][i] = lds_read16(sa + i * 2048 + foff1);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 1; i < 4; ++i)
+    for (int i = 1; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16<F16>(bw[0][j], af[0][i], acc[i][j]);
+      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16<F16>(bw[0][j], af[0][i], acc[i][j]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16<F16>(bw[1][j], af[1][i], acc[i][j]);
+      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16<F16>(bw[1][j], af[1][i], acc[i][j]);
     __builtin_amdgcn_s_setprio(0);
   }
   if constexpr (EPI == EPI_PARTIAL) {     // split-K: plain 16-B stores of the fp32 partial tile
     float* slice = a.ws + (size_t)split * a.M * a.N;   // (no atomics, no zeroing: deterministic)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = m0 + wm * 64 + 16 * i + fr, n = n0 + wn * 64 + 16 * j + 4 * fq;
+      for (int j = 0; j < NJ; ++j) {
+        const int m = m0 + wm * 64 * TM + 16 * i + fr, n = n0 + wn * 64 * TN + 16 * j + 4 * fq;
         if (m < a.M && n < a.N)                 // N % 8 == 0: a lane's 4 columns all in or out
           *reinterpret_cast<f32x4*>(slice + (size_t)m * a.N + n) = acc[i][j];
       }
@@ -326,16 +327,16 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
   }
   barrier_raw();                         // every wave is done with the ring: reuse it for C
 
-  // ---- epilogue: lane holds C[m0 + wm·64 + 16i + fr][n0 + wn·64 + 16j + 4fq + 0..3] ----
-  float bias[4][4];
+  // ---- epilogue: lane holds C[m0 + wm·64TM + 16i + fr][n0 + wn·64TN + 16j + 4fq + 0..3] ----
+  float bias[NJ][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) bias[j][e] = 0.f;
   if (a.bias) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + 16 * j + 4 * fq;
+    for (int j = 0; j < NJ; ++j) {
+      const int n = n0 + wn * 64 * TN + 16 * j + 4 * fq;
       if (n < a.N) {                    // N % 4 == 0: a lane's 4 columns are all in or all out
         const uint2 bv = *reinterpret_cast<const uint2*>(a.bias + n);
         bias[j][0] = h2f<F16>((uint16_t)(bv.x & 0xffffu));
@@ -347,10 +348,10 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
   }
   if constexpr (EPI == EPI_RESID) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = wm * 64 + 16 * i + fr, n = wn * 64 + 16 * j + 4 * fq;
+      for (int j = 0; j < NJ; ++j) {
+        const int m = wm * 64 * TM + 16 * i + fr, n = wn * 64 * TN + 16 * j + 4 * fq;
         f32x4 v = acc[i][j];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] += bias[j][e];
@@ -379,10 +380,10 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_epi_kernel(const Args a) {
     }
   } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = wm * 64 + 16 * i + fr, n = wn * 64 + 16 * j + 4 * fq;
+      for (int j = 0; j < NJ; ++j) {
+        const int m = wm * 64 * TM + 16 * i + fr, n = wn * 64 * TN + 16 * j + 4 * fq;
         f32x4 v = acc[i][j];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -505,11 +506,13 @@ int amdk8s_gemm_epi_supported(int M, int N, int K) {
 // K allows (at most 16).  Overrides for A/B sweeps:
 // amdk8s_gemm_epi_set_tile(0..3) / AMDK8S_GEMM_EPI_TILE pin the tile, AMDK8S_GEMM_SPLITK=<n> pins
 // the split factor (1 = never split); -1 / unset = the plan above.
-static const int kTiles[4][2] = {{256, 128}, {128, 128}, {128, 64}, {64, 64}};
+// (tile 4: 256×128 on 4 waves of 128×64 — a quarter less LDS traffic per MFMA than tile 0's 8
+// waves of 64×64, half the waves to hide latency; A/B via AMDK8S_GEMM_EPI_TILE=4)
+static const int kTiles[5][2] = {{256, 128}, {128, 128}, {128, 64}, {64, 64}, {256, 128}};
 static int g_tile = -2;     // -2: not initialised from the environment yet
 static int g_splits = -2;
 
-void amdk8s_gemm_epi_set_tile(int tile) { g_tile = (tile >= 0 && tile <= 3) ? tile : -1; }
+void amdk8s_gemm_epi_set_tile(int tile) { g_tile = (tile >= 0 && tile <= 4) ? tile : -1; }
 void amdk8s_gemm_epi_set_splits(int s) { g_splits = (s >= 1 && s <= 64) ? s : -1; }
 
 static long tile_grid(int tile, int M, int N) {
@@ -519,7 +522,7 @@ static long tile_grid(int tile, int M, int N) {
 void amdk8s_gemm_epi_plan(int M, int N, int K, int* tile_out, int* splits_out) {
   if (g_tile == -2) {
     const char* e = getenv("AMDK8S_GEMM_EPI_TILE");
-    g_tile = (e && e[0] >= '0' && e[0] <= '3' && !e[1]) ? e[0] - '0' : -1;
+    g_tile = (e && e[0] >= '0' && e[0] <= '4' && !e[1]) ? e[0] - '0' : -1;
   }
   if (g_splits == -2) {
     const char* e = getenv("AMDK8S_GEMM_SPLITK");
@@ -580,38 +583,39 @@ int launch_epi(Args a, int epi, bool f16, hipStream_t stream) {
   const long nwg = tile_grid(tile, a.M, a.N);
   if (nwg * splits > 0x7fffffff) return (int)hipErrorInvalidValue;
   a.splits = splits;
-  auto go = [&](auto wm, auto wn) {
-    constexpr int WM = decltype(wm)::value, WN = decltype(wn)::value;
-    constexpr int NT = Geo<WM, WN>::NT;
+  auto go = [&](auto wm, auto wn, auto tm) {
+    constexpr int WM = decltype(wm)::value, WN = decltype(wn)::value, TM = decltype(tm)::value;
+    constexpr int NT = Geo<WM, WN, TM>::NT;
     auto launch = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(nwg * splits), dim3(NT), 0, stream, a);
     };
     if (splits > 1) {                          // partial sums; epilogue in splitk_finalize
-      if (f16) launch(gemm_epi_kernel<EPI_PARTIAL, true, WM, WN, CONV>);
-      else launch(gemm_epi_kernel<EPI_PARTIAL, false, WM, WN, CONV>);
+      if (f16) launch(gemm_epi_kernel<EPI_PARTIAL, true, WM, WN, CONV, TM>);
+      else launch(gemm_epi_kernel<EPI_PARTIAL, false, WM, WN, CONV, TM>);
     } else if constexpr (CONV != CONV_NONE) {  // convolutions: fp16 (the SD1.5 UNet / VAE)
-      if (epi == EPI_ADD) launch(gemm_epi_kernel<EPI_ADD, true, WM, WN, CONV>);
-      else launch(gemm_epi_kernel<EPI_STORE, true, WM, WN, CONV>);
+      if (epi == EPI_ADD) launch(gemm_epi_kernel<EPI_ADD, true, WM, WN, CONV, TM>);
+      else launch(gemm_epi_kernel<EPI_STORE, true, WM, WN, CONV, TM>);
     } else if (f16) {
-      if (epi == EPI_STORE) launch(gemm_epi_kernel<EPI_STORE, true, WM, WN>);
-      else if (epi == EPI_GELU) launch(gemm_epi_kernel<EPI_GELU, true, WM, WN>);
-      else if (epi == EPI_RESID) launch(gemm_epi_kernel<EPI_RESID, true, WM, WN>);
-      else launch(gemm_epi_kernel<EPI_ADD, true, WM, WN>);
+      if (epi == EPI_STORE) launch(gemm_epi_kernel<EPI_STORE, true, WM, WN, CONV, TM>);
+      else if (epi == EPI_GELU) launch(gemm_epi_kernel<EPI_GELU, true, WM, WN, CONV, TM>);
+      else if (epi == EPI_RESID) launch(gemm_epi_kernel<EPI_RESID, true, WM, WN, CONV, TM>);
+      else launch(gemm_epi_kernel<EPI_ADD, true, WM, WN, CONV, TM>);
     } else {
-      if (epi == EPI_STORE) launch(gemm_epi_kernel<EPI_STORE, false, WM, WN>);
-      else if (epi == EPI_GELU) launch(gemm_epi_kernel<EPI_GELU, false, WM, WN>);
-      else if (epi == EPI_RESID) launch(gemm_epi_kernel<EPI_RESID, false, WM, WN>);
-      else launch(gemm_epi_kernel<EPI_ADD, false, WM, WN>);
+      if (epi == EPI_STORE) launch(gemm_epi_kernel<EPI_STORE, false, WM, WN, CONV, TM>);
+      else if (epi == EPI_GELU) launch(gemm_epi_kernel<EPI_GELU, false, WM, WN, CONV, TM>);
+      else if (epi == EPI_RESID) launch(gemm_epi_kernel<EPI_RESID, false, WM, WN, CONV, TM>);
+      else launch(gemm_epi_kernel<EPI_ADD, false, WM, WN, CONV, TM>);
     }
   };
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   using I4 = std::integral_constant<int, 4>;
   switch (tile) {
-    case 0: go(I4{}, I2{}); break;
-    case 1: go(I2{}, I2{}); break;
-    case 2: go(I2{}, I1{}); break;
-    default: go(I1{}, I1{}); break;
+    case 0: go(I4{}, I2{}, I1{}); break;
+    case 1: go(I2{}, I2{}, I1{}); break;
+    case 2: go(I2{}, I1{}, I1{}); break;
+    case 4: go(I2{}, I2{}, I2{}); break;
+    default: go(I1{}, I1{}, I1{}); break;
   }
   if (splits > 1) {
     const long groups = (long)a.M * (a.N / 8);

@@ -87,6 +87,19 @@ for tokens in [int(t) for t in os.environ.get("TOKENS", "2560,32768").split(",")
             row["torch_us"] = bench(lambda: F.linear(x, w, b))
         if M % 256 == 0 and n % 256 == 0:          # the validator's 256x256 w4a kernel, plain store
             row["w4a_us"] = bench(lambda: K.gemm_bf16_nt(x, w))
+        # the wave-grid kernel's 256x128 tiles: 8 waves of 64x64 (tile 0) vs 4 of 128x64 (tile 4)
+        out = torch.empty(M, n, device=dev).bfloat16()
+        for t in (0, 4):
+            GE.set_tile(t)
+            if name in ("o", "ffn2"):
+                r2 = torch.randn(2, tokens, n, device=dev)
+                g2 = torch.randn(2, n, device=dev)
+                row[f"resid_t{t}_us"] = bench(lambda: GE._run(GE.EPI_RESID, x, w, b, None, r2.view(-1, n),
+                                                              g2, tokens, n, 0, n))
+            else:
+                epi = GE.EPI_GELU if name == "ffn0" else GE.EPI_STORE
+                row[f"epi_t{t}_us"] = bench(lambda: GE._run(epi, x, w, b, out, None, None, 0, 0, n, 0))
+        GE.set_tile(-1)
         for key in list(row):
             row[key] = round(row[key], 1)
         row["ours_tflops"] = round(fl / row["ours_us"] / 1e6, 1)

@@ -1,11 +1,16 @@
 #!/bin/bash
-# Round 3 session O: attention loop without per-tile masking / index maths, packed exp-argument FMAs
+# Round 3 session O: 4-wave 256x128 GEMM tile (tests, Wan probe); attention loop without per-tile masking / index maths, packed exp-argument FMAs
 # and row sums — tests, probe, PMC, SD1.5 + Wan benches.
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=gpurun_out/r03/o
 mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+  tests/test_gemm_epi_gpu.py > $OUT/gemm_epi_tests.log 2>&1 || { tail -40 $OUT/gemm_epi_tests.log; exit 1; }
+tail -2 $OUT/gemm_epi_tests.log
+TOKENS=2560 timeout -k 10 300 python -u tools/gemm_epi_probe.py > $OUT/gemm_probe_wan.log 2>&1 || { tail -20 $OUT/gemm_probe_wan.log; exit 1; }
+grep -v '^{' $OUT/gemm_probe_wan.log | grep -v amdgpu.ids
 timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
   tests/test_sd15_gpu.py tests/test_wan_gpu.py > $OUT/pytest_models.log 2>&1 || { tail -40 $OUT/pytest_models.log; exit 1; }
 tail -2 $OUT/pytest_models.log
