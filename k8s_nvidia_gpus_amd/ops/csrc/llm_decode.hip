@@ -1049,6 +1049,16 @@ static int regx_max_t() {
   return v;
 }
 
+// AMDK8S_LLM_LONGROW=0: long rows keep the type/mode batch as stage width (A/B knob).
+static bool longrow_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("AMDK8S_LLM_LONGROW");
+    v = !(e && e[0] == '0');
+  }
+  return v != 0;
+}
+
 template <int TYPE, int T, int MODE>
 int launch_gemv(const GemvArgs& a, int waves, hipStream_t st) {
   constexpr int KB = kBatch<TYPE, MODE>;
@@ -1059,6 +1069,15 @@ int launch_gemv(const GemvArgs& a, int waves, hipStream_t st) {
       if constexpr (T <= 2) return launch_one<TYPE, T, MODE, 2, true>(a, waves, st);
       else if (T <= regx_max_t()) return launch_one<TYPE, T, MODE, 2, true>(a, waves, st);
       else return launch_one<TYPE, T, MODE, 2, false>(a, waves, st);
+    }
+  }
+  if constexpr (MODE != kPair) {
+    // long rows (ffn_down: 74 super-blocks): two stages per row with U = ceil(nb / 16) instead of
+    // KB-wide stages whose last one is mostly clamped lanes (74 = 32 + 32 + 10 at U = 4)
+    if (longrow_enabled()) {
+      const int u2 = (nb + 15) / 16;
+      if (u2 == 5) return launch_one<TYPE, T, MODE, 5, false>(a, waves, st);
+      if (u2 == 6) return launch_one<TYPE, T, MODE, 6, false>(a, waves, st);
     }
   }
   return launch_one<TYPE, T, MODE, KB, false>(a, waves, st);
