@@ -62,6 +62,9 @@ class StepBuffers:
     x8: torch.Tensor
     dx: torch.Tensor
     sx: torch.Tensor
+    x8f: torch.Tensor       # second Q8 set: the ffn_down input written by the gate|up GEMV while
+    dxf: torch.Tensor       # its own input (x8/dx/sx) is still being read
+    sxf: torch.Tensor
     qkv: torch.Tensor
     qrot: torch.Tensor
     po: torch.Tensor
@@ -113,6 +116,9 @@ class Engine:
         # fences around the arrival counter write back / invalidate L2 across the XCDs, which
         # costs more than the separate combine launch.  Off by default.
         self.fused_combine = os.environ.get("AMDK8S_LLM_FUSED_COMBINE", "0") != "0"
+        # with the once-per-input Q8 path: the gate|up pair GEMV quantises silu(g)·u itself (its
+        # workgroups own whole 32-row blocks), so ffn_down needs no separate quantisation launch
+        self.pair_q8 = os.environ.get("AMDK8S_LLM_PAIR_Q8", "1") != "0"
         self._attn_cnt = None
         self._side = None
         if self.gpu:
@@ -215,6 +221,8 @@ class Engine:
                 h=torch.zeros(T, c.dim, **f32),
                 x8=torch.zeros(T, kmax, dtype=torch.int8, device=dev),
                 dx=torch.zeros(T, kmax // 32, **f32), sx=torch.zeros(T, kmax // 16, **f32),
+                x8f=torch.zeros(T, c.ffn, dtype=torch.int8, device=dev),
+                dxf=torch.zeros(T, c.ffn // 32, **f32), sxf=torch.zeros(T, c.ffn // 16, **f32),
                 qkv=torch.zeros(T, c.dim + 2 * c.kv_dim, **f32), qrot=torch.zeros(T, c.dim, **f32),
                 po=torch.zeros(T, c.heads, nsplit, c.head_dim, **f32),
                 pml=torch.zeros(T, c.heads, nsplit, 2, **f32), t=torch.zeros(T, c.ffn, **f32),
@@ -291,9 +299,14 @@ class Engine:
                                span=span, cnt=cnt)
             LK.qgemv(L.wo, *qd, b.h, LK.RESID, **G)
             xin = act(b.h, L.ffn_norm, c.dim)
-            LK.qgemv(L.wg, *xin[0], b.t, LK.PAIR, w1=L.wu, **xin[1], **G)
-            xin = act(b.t, None, c.ffn)
-            LK.qgemv(L.wd, *xin[0], b.h, LK.RESID, **xin[1], **G)
+            if self.pair_q8 and b.T >= self.q8_split_T and c.ffn % 32 == 0:
+                qf = (b.x8f, b.dxf, b.sxf)
+                LK.qgemv(L.wg, *xin[0], b.t, LK.PAIR, w1=L.wu, **xin[1], **G, q8_out=qf)
+                LK.qgemv(L.wd, *qf, b.h, LK.RESID, **G)
+            else:
+                LK.qgemv(L.wg, *xin[0], b.t, LK.PAIR, w1=L.wu, **xin[1], **G)
+                xin = act(b.t, None, c.ffn)
+                LK.qgemv(L.wd, *xin[0], b.h, LK.RESID, **xin[1], **G)
         xin = act(b.h, self.w.out_norm, c.dim)
         LK.qgemv(self.w.output, *xin[0], b.logits, LK.STORE, **xin[1], **G)
         if pf:

@@ -506,13 +506,14 @@ int amdk8s_gemm_epi_supported(int M, int N, int K) {
 // K allows (at most 16).  Overrides for A/B sweeps:
 // amdk8s_gemm_epi_set_tile(0..3) / AMDK8S_GEMM_EPI_TILE pin the tile, AMDK8S_GEMM_SPLITK=<n> pins
 // the split factor (1 = never split); -1 / unset = the plan above.
-// (tile 4: 256×128 on 4 waves of 128×64 — a quarter less LDS traffic per MFMA than tile 0's 8
-// waves of 64×64, half the waves to hide latency; A/B via AMDK8S_GEMM_EPI_TILE=4)
-static const int kTiles[5][2] = {{256, 128}, {128, 128}, {128, 64}, {64, 64}, {256, 128}};
+// (Measured and dropped: 256×128 on 4 waves of 128×64 — a quarter less LDS traffic per MFMA but
+// half the waves to hide latency: 20-25 % slower than tile 0 on the Wan shapes, profiles/r03/o.
+// The kernel template keeps the (TM, TN) wave-tile parameters.)
+static const int kTiles[4][2] = {{256, 128}, {128, 128}, {128, 64}, {64, 64}};
 static int g_tile = -2;     // -2: not initialised from the environment yet
 static int g_splits = -2;
 
-void amdk8s_gemm_epi_set_tile(int tile) { g_tile = (tile >= 0 && tile <= 4) ? tile : -1; }
+void amdk8s_gemm_epi_set_tile(int tile) { g_tile = (tile >= 0 && tile <= 3) ? tile : -1; }
 void amdk8s_gemm_epi_set_splits(int s) { g_splits = (s >= 1 && s <= 64) ? s : -1; }
 
 static long tile_grid(int tile, int M, int N) {
@@ -522,7 +523,7 @@ static long tile_grid(int tile, int M, int N) {
 void amdk8s_gemm_epi_plan(int M, int N, int K, int* tile_out, int* splits_out) {
   if (g_tile == -2) {
     const char* e = getenv("AMDK8S_GEMM_EPI_TILE");
-    g_tile = (e && e[0] >= '0' && e[0] <= '4' && !e[1]) ? e[0] - '0' : -1;
+    g_tile = (e && e[0] >= '0' && e[0] <= '3' && !e[1]) ? e[0] - '0' : -1;
   }
   if (g_splits == -2) {
     const char* e = getenv("AMDK8S_GEMM_SPLITK");
@@ -614,7 +615,6 @@ int launch_epi(Args a, int epi, bool f16, hipStream_t stream) {
     case 0: go(I4{}, I2{}, I1{}); break;
     case 1: go(I2{}, I2{}, I1{}); break;
     case 2: go(I2{}, I1{}, I1{}); break;
-    case 4: go(I2{}, I2{}, I2{}); break;
     default: go(I1{}, I1{}, I1{}); break;
   }
   if (splits > 1) {

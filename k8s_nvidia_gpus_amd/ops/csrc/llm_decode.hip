@@ -102,6 +102,11 @@ struct GemvArgs {
   float* out;            // [T][ldo]
   int ldo, N, K, T;
   int rows_per_wg;
+  // pair mode: emit silu(g)·u quantised to Q8 (the ffn_down input) instead of fp32 — needs
+  // rows_per_wg == 32 so a workgroup owns whole 32-value blocks
+  int8_t* ox8;           // [T][N]
+  float* odx;            // [T][N/32]
+  float* osx;            // [T][N/16]
 };
 
 // Weights are streamed exactly once per step: non-temporal loads keep them from evicting the
@@ -279,7 +284,7 @@ __device__ __forceinline__ void compute_stage(int b0, int nb, int sub, int bl, c
 
 template <int T, int MODE>
 __device__ __forceinline__ void finish_row(const GemvArgs& a, int row, int lane, float (&acc)[T],
-                                           float (&acc1)[T]) {
+                                           float (&acc1)[T], float* q8s = nullptr, int wrow0 = 0) {
 #pragma unroll
   for (int t = 0; t < T; ++t) {
     acc[t] = wave_sum(acc[t]);
@@ -293,7 +298,11 @@ __device__ __forceinline__ void finish_row(const GemvArgs& a, int row, int lane,
     float* o = a.out + (long)lane * a.ldo + row;
     if constexpr (MODE == kStore) *o = v + (a.bias ? a.bias[row] : 0.f);
     else if constexpr (MODE == kResid) *o += v;
-    else *o = v / (1.f + __expf(-v)) * v1;
+    else {
+      const float y = v / (1.f + __expf(-v)) * v1;
+      if (q8s) q8s[lane * 32 + (row - wrow0)] = y;   // quantised at the end of the workgroup
+      else *o = y;
+    }
   }
 #pragma unroll
   for (int t = 0; t < T; ++t) acc[t] = acc1[t] = 0.f;
@@ -484,6 +493,9 @@ __global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
   float acc[T], acc1[T];
 #pragma unroll
   for (int t = 0; t < T; ++t) acc[t] = acc1[t] = 0.f;
+  // pair → Q8: the workgroup's 32 outputs per token collect in LDS (after the [W][T] scratch)
+  float* q8s = (MODE == kPair && a.ox8) ? red + W * T : nullptr;
+  const int wrow0 = blockIdx.x * a.rows_per_wg;
   if constexpr (REGX) {
     XReg xr[U][T];
 #pragma unroll
@@ -493,21 +505,20 @@ __global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
     for (int it = 0; it < nrows; it += 2) {
       if (it + 1 < nrows) load_stage<TYPE, MODE, U>(a, r0 + (it + 1) * W, 0, nb, sub, bl, B, B1);
       compute_reg<TYPE, T, MODE, U>(nb, sub, bl, xr, A, A1, acc, acc1);
-      finish_row<T, MODE>(a, r0 + it * W, lane, acc, acc1);
+      finish_row<T, MODE>(a, r0 + it * W, lane, acc, acc1, q8s, wrow0);
       if (it + 1 >= nrows) break;
       if (it + 2 < nrows) load_stage<TYPE, MODE, U>(a, r0 + (it + 2) * W, 0, nb, sub, bl, A, A1);
       compute_reg<TYPE, T, MODE, U>(nb, sub, bl, xr, B, B1, acc, acc1);
-      finish_row<T, MODE>(a, r0 + (it + 1) * W, lane, acc, acc1);
+      finish_row<T, MODE>(a, r0 + (it + 1) * W, lane, acc, acc1, q8s, wrow0);
     }
-    return;
-  }
+  } else {
   for (int it = 0; it < items; it += 2) {
     if (it + 1 < items) {
       const int j = it + 1;
       load_stage<TYPE, MODE, U>(a, r0 + (j / nst) * W, (j % nst) * 8 * U, nb, sub, bl, B, B1);
     }
     compute_stage<TYPE, T, MODE, U>((it % nst) * 8 * U, nb, sub, bl, xv, A, A1, acc, acc1);
-    if (it % nst == nst - 1) finish_row<T, MODE>(a, r0 + (it / nst) * W, lane, acc, acc1);
+    if (it % nst == nst - 1) finish_row<T, MODE>(a, r0 + (it / nst) * W, lane, acc, acc1, q8s, wrow0);
     if (it + 1 >= items) break;
     if (it + 2 < items) {
       const int j = it + 2;
@@ -515,7 +526,31 @@ __global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
     }
     const int i1 = it + 1;
     compute_stage<TYPE, T, MODE, U>((i1 % nst) * 8 * U, nb, sub, bl, xv, B, B1, acc, acc1);
-    if (i1 % nst == nst - 1) finish_row<T, MODE>(a, r0 + (i1 / nst) * W, lane, acc, acc1);
+    if (i1 % nst == nst - 1) finish_row<T, MODE>(a, r0 + (i1 / nst) * W, lane, acc, acc1, q8s, wrow0);
+  }
+  }
+  if constexpr (MODE == kPair) {
+    if (q8s) {       // quantise the 32-row block per token: half a wave per token (lane & 31 = row)
+      __syncthreads();
+      const int t = threadIdx.x >> 5, i = threadIdx.x & 31;
+      if (t < T) {
+        const int row = wrow0 + i;
+        const float v = row < a.N ? q8s[t * 32 + i] : 0.f;
+        float amax = fabsf(v);
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, kWave));
+        const float d = amax / 127.f;
+        const int qv = d > 0.f ? (int)__builtin_rintf(v / d) : 0;
+        int s16 = qv;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) s16 += __shfl_xor(s16, o, kWave);
+        if (row < a.N) {
+          a.ox8[(long)t * a.N + row] = (int8_t)qv;
+          if (i == 0) a.odx[(long)t * (a.N >> 5) + (row >> 5)] = d;
+          if ((i & 15) == 0) a.osx[(long)t * (a.N >> 4) + (row >> 4)] = d * (float)s16;
+        }
+      }
+    }
   }
 }
 
@@ -1026,7 +1061,8 @@ __global__ void q4k_repack_kernel(const uint8_t* __restrict__ src, long nblocks,
 template <int TYPE, int T, int MODE, int U, bool REGX>
 int launch_one(const GemvArgs& a, int waves, hipStream_t st) {
   const int nb = a.K >> 8;
-  const size_t lds = (size_t)T * (nb * 288 + (a.K >> 5) * 4 + (a.K >> 4) * 4) + 16 * T * 4;
+  const size_t lds = (size_t)T * (nb * 288 + (a.K >> 5) * 4 + (a.K >> 4) * 4) + 16 * T * 4 +
+                     (a.ox8 ? (size_t)T * 32 * 4 : 0);
   if (lds > 160 * 1024) return 3;
   const int grid = (a.N + a.rows_per_wg - 1) / a.rows_per_wg;
   hipLaunchKernelGGL((qgemv_kernel<TYPE, T, MODE, U, REGX>), dim3(grid), dim3(waves * 64), lds, st,
@@ -1145,10 +1181,15 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
                      const void* w1d, const void* x8, const void* dx, const void* sx,
                      const void* xf, int ldx, const void* norm_w, float eps,
                      const void* bias, void* out, int ldo, int N, int K, int T, int waves,
-                     int rows_per_wg, void* stream) {
+                     int rows_per_wg, void* ox8, void* odx, void* osx, void* stream) {
   if (K % 256 || N <= 0 || T < 1 || T > kMaxTok) return 2;
   if (mode == kPair && !w1q) return 2;
+  if (ox8) {                                  // pair → Q8 output: whole 32-row blocks per workgroup
+    if (mode != kPair || N % 32 || !odx || !osx) return 2;
+    rows_per_wg = 32;
+  }
   gemv_shape(N, K, waves, rows_per_wg);
+  if (ox8 && waves * 64 < 32 * T) return 2;
   if (waves < 1 || waves > 8 || rows_per_wg < 1) return 2;
   GemvArgs a;
   a.w0 = {static_cast<const uint8_t*>(w0q), static_cast<const uint8_t*>(w0qh),
@@ -1167,6 +1208,9 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
   a.bias = static_cast<const float*>(bias);
   a.out = static_cast<float*>(out);
   a.ldo = ldo; a.N = N; a.K = K; a.T = T; a.rows_per_wg = rows_per_wg;
+  a.ox8 = static_cast<int8_t*>(ox8);
+  a.odx = static_cast<float*>(odx);
+  a.osx = static_cast<float*>(osx);
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (type == kQ4K) {
     if (mode == kStore) return dispatch_t<kQ4K, kStore>(a, waves, st);

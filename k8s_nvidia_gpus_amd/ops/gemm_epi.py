@@ -59,7 +59,7 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
-TILES = ((256, 128), (128, 128), (128, 64), (64, 64), (256, 128))   # 4: 4 waves of 128×64
+TILES = ((256, 128), (128, 128), (128, 64), (64, 64))
 
 
 def set_tile(tile: int) -> None:

@@ -247,33 +247,3 @@ def test_split_k_gated_residual(GE, gated):
     want = res + _ref(x, w, None).view(1, m, n) * (gate[:, None, :] if gated else 1.0)
     GE.linear_residual_(res, x, w, None, gate)
     torch.testing.assert_close(res, want, rtol=5e-3, atol=5e-3)
-
-
-@pytest.mark.parametrize("m", [1000, 8000])
-@pytest.mark.parametrize("epi", ["store", "gelu", "resid"])
-def test_four_wave_256x128_tile(GE, epi, m):
-    """Tile 4: 256×128 on 4 waves of 128×64 (two 64-row accumulator halves per wave), M/N tails;
-    m = 1000 runs split-K (52 tiles), m = 8000 the in-kernel epilogues."""
-    dev = torch.device("cuda")
-    g = torch.Generator(device=dev).manual_seed(4)
-    n, k = 1544, 1536
-    x = torch.randn(m, k, generator=g, device=dev).bfloat16()
-    w = (torch.randn(n, k, generator=g, device=dev) / 40).bfloat16()
-    b = torch.randn(n, generator=g, device=dev).bfloat16()
-    ref = _ref(x, w, b)
-    GE.set_tile(4)
-    try:
-        assert GE.plan(m, n, k)[0] == (256, 128)
-        if epi == "store":
-            torch.testing.assert_close(GE.linear(x, w, b).float(), ref, rtol=2e-2, atol=2e-2)
-        elif epi == "gelu":
-            torch.testing.assert_close(GE.linear_gelu(x, w, b).float(),
-                                       F.gelu(ref, approximate="tanh"), rtol=2e-2, atol=2e-2)
-        else:
-            res = torch.randn(1, m, n, generator=g, device=dev)
-            gate = torch.randn(1, n, generator=g, device=dev)
-            want = res + ref.view(1, m, n) * gate[:, None, :]
-            GE.linear_residual_(res, x.view(1, m, k), w, b, gate)
-            torch.testing.assert_close(res, want, rtol=1e-2, atol=2e-2)
-    finally:
-        GE.set_tile(-1)
