@@ -1085,12 +1085,13 @@ static int regx_max_t() {
   return v;
 }
 
-// AMDK8S_LLM_LONGROW=0: long rows keep the type/mode batch as stage width (A/B knob).
+// AMDK8S_LLM_LONGROW=1: long rows in two balanced stages instead of KB-wide ones (A/B knob;
+// measured neutral to slightly slower on MI355X — profiles/r03/q — so off by default).
 static bool longrow_enabled() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("AMDK8S_LLM_LONGROW");
-    v = !(e && e[0] == '0');
+    v = (e && e[0] == '1');
   }
   return v != 0;
 }
