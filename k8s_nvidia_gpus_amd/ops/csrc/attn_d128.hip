@@ -35,9 +35,6 @@
 // (reference workload: the Wan2.1 T2V DiT the reference's ComfyUI client drives,
 // generate_wan_t2v.py:305-312, 347).
 #include <hip/hip_runtime.h>
-#include <stdlib.h>
-
-#include <type_traits>
 #include <stdint.h>
 
 namespace {
@@ -48,7 +45,6 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(8))) short s16x8;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-typedef __attribute__((ext_vector_type(2))) float f32x2;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int kKeys = 64;                    // keys per tile
@@ -110,9 +106,7 @@ struct Args {
   float c;                                       // scale * log2(e)
 };
 
-// VER 1: per-tile index maths, runtime tail check, scalar softmax arithmetic; VER 2: unmasked full
-// tiles with pointer-advanced loads, packed fp32 exp arguments / row sums (fewer VALU per MFMA).
-template <bool BF16, int NW, int D, int VER = 1>
+template <bool BF16, int NW, int D>
 __global__ __launch_bounds__(NW * 64, 2) void attn_m32_kernel(const Args a) {
   using G = Geo<D>;
   constexpr int NT = NW * 64;
@@ -159,41 +153,14 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_m32_kernel(const Args a) {
   float m = -INFINITY, l = 0.f;
 
   uint4 kr[CH], vr[CH];
-  // per-thread chunk pointers of tile 0, advanced by whole tiles (no per-tile index maths)
-  const uint16_t* kp[CH];
-  const uint16_t* vp[CH];
-  int krow[CH];
-#pragma unroll
-  for (int j = 0; j < CH; ++j) {
-    const int c = min(tid + j * NT, NCH - 1), row = c / G::CR, ch = c - row * G::CR;
-    krow[j] = row;
-    kp[j] = kb + (long)row * a.skr + ch * 8;
-    vp[j] = vb + (long)row * a.svr + ch * 8;
-  }
-  // MASKED: the tile may run past Lk (the last one) — rows >= Lk load as zeros
-  auto load_tile = [&](int kbase, auto masked) {
-    if constexpr (VER == 1) {
-#pragma unroll
-      for (int j = 0; j < CH; ++j) {
-        const int c = tid + j * NT, row = c / G::CR, ch = c - row * G::CR;
-        const int key = kbase + row;
-        if (c < NCH && key < a.Lk) {
-          kr[j] = *reinterpret_cast<const uint4*>(kb + key * a.skr + ch * 8);
-          vr[j] = *reinterpret_cast<const uint4*>(vb + key * a.svr + ch * 8);
-        } else {
-          kr[j] = make_uint4(0, 0, 0, 0);
-          vr[j] = make_uint4(0, 0, 0, 0);
-        }
-      }
-      return;
-    }
+  auto load_tile = [&](int kbase) {
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-      const bool live = (NCH % NT == 0 || tid + j * NT < NCH) &&
-                        (!decltype(masked)::value || kbase + krow[j] < a.Lk);
-      if (live) {
-        kr[j] = *reinterpret_cast<const uint4*>(kp[j] + (long)kbase * a.skr);
-        vr[j] = *reinterpret_cast<const uint4*>(vp[j] + (long)kbase * a.svr);
+      const int c = tid + j * NT, row = c / G::CR, ch = c - row * G::CR;
+      const int key = kbase + row;
+      if (c < NCH && key < a.Lk) {
+        kr[j] = *reinterpret_cast<const uint4*>(kb + key * a.skr + ch * 8);
+        vr[j] = *reinterpret_cast<const uint4*>(vb + key * a.svr + ch * 8);
       } else {
         kr[j] = make_uint4(0, 0, 0, 0);
         vr[j] = make_uint4(0, 0, 0, 0);
@@ -222,27 +189,19 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_m32_kernel(const Args a) {
   const int vrow = 4 * h + qq;
 
   const int ntiles = (a.Lk + kKeys - 1) / kKeys;
-  const int nfull = a.Lk / kKeys;                // tiles with every key < Lk
   const float thr = 8.f / a.c;                   // deferred-max margin in raw score units
-  using kMasked = std::integral_constant<bool, true>;
-  using kFull = std::integral_constant<bool, false>;
-  if (nfull > 0) load_tile(0, kFull{}); else load_tile(0, kMasked{});
+  load_tile(0);
   if constexpr (G::PAD) {      // pad columns of both buffers read as zeros for the whole kernel
     for (int i = tid; i < G::LDS / 16; i += NT) reinterpret_cast<uint4*>(lds)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
   }
   store_tile(0);
   __syncthreads();
-  // one K/V tile; TAIL: keys past Lk in this tile (the last one only)
-  auto tile_step = [&](int kt, auto tail) {
-    constexpr bool TAIL = decltype(tail)::value;
+  for (int kt = 0; kt < ntiles; ++kt) {
     const int kbase = kt * kKeys;
     const char* kl = lds + (kt & 1) * G::BUF;
     const char* vl = kl + G::TILE;
-    if (kt + 1 < ntiles) {                           // in flight under this tile's MFMAs
-      if (kt + 1 < nfull) load_tile(kbase + kKeys, kFull{});
-      else load_tile(kbase + kKeys, kMasked{});
-    }
+    if (kt + 1 < ntiles) load_tile(kbase + kKeys);   // in flight under this tile's MFMAs
 
     // ---- Sᵀ = K Qᵀ: two 32-key blocks × KSTEPS k-steps over d
     f32x16 s[2];
@@ -258,7 +217,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_m32_kernel(const Args a) {
       }
     }
     // keys past Lk (zero rows in the image) score -inf
-    if (VER == 1 ? kbase + kKeys > a.Lk : TAIL) {
+    if (kbase + kKeys > a.Lk) {
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -283,43 +242,20 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_m32_kernel(const Args a) {
     }
     const float mc = m * a.c;
     s16x8 pf[4];                                 // Pᵀ B fragments of the 4 16-key steps
-    if constexpr (VER == 1) {
-      float rs0 = 0.f, rs1 = 0.f;
+    float rs0 = 0.f, rs1 = 0.f;
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int b = ks >> 1, base = 8 * (ks & 1);
-        float e[8];
+    for (int ks = 0; ks < 4; ++ks) {
+      const int b = ks >> 1, base = 8 * (ks & 1);
+      float e[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) e[j] = __builtin_amdgcn_exp2f(fmaf(s[b][base + j], a.c, -mc));
-        rs0 += (e[0] + e[1]) + (e[2] + e[3]);
-        rs1 += (e[4] + e[5]) + (e[6] + e[7]);
-        pf[ks] = __builtin_bit_cast(
-            s16x8, make_uint4(pack2<BF16>(e[0], e[1]), pack2<BF16>(e[2], e[3]),
-                              pack2<BF16>(e[4], e[5]), pack2<BF16>(e[6], e[7])));
-      }
-      l += rs0 + rs1;
-    } else {
-      // exponent arguments and row sums two at a time (v_pk_fma_f32 / v_pk_add_f32)
-      const f32x2 c2 = {a.c, a.c}, nmc2 = {-mc, -mc};
-      f32x2 rs = {0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int b = ks >> 1, base = 8 * (ks & 1);
-        float e[8];
-#pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-          const f32x2 sv = {s[b][base + j], s[b][base + j + 1]};
-          const f32x2 t = __builtin_elementwise_fma(sv, c2, nmc2);
-          e[j] = __builtin_amdgcn_exp2f(t[0]);
-          e[j + 1] = __builtin_amdgcn_exp2f(t[1]);
-          rs += f32x2{e[j], e[j + 1]};
-        }
-        pf[ks] = __builtin_bit_cast(
-            s16x8, make_uint4(pack2<BF16>(e[0], e[1]), pack2<BF16>(e[2], e[3]),
-                              pack2<BF16>(e[4], e[5]), pack2<BF16>(e[6], e[7])));
-      }
-      l += rs[0] + rs[1];
+      for (int j = 0; j < 8; ++j) e[j] = __builtin_amdgcn_exp2f(fmaf(s[b][base + j], a.c, -mc));
+      rs0 += (e[0] + e[1]) + (e[2] + e[3]);
+      rs1 += (e[4] + e[5]) + (e[6] + e[7]);
+      pf[ks] = __builtin_bit_cast(
+          s16x8, make_uint4(pack2<BF16>(e[0], e[1]), pack2<BF16>(e[2], e[3]),
+                            pack2<BF16>(e[4], e[5]), pack2<BF16>(e[6], e[7])));
     }
+    l += rs0 + rs1;
 
     // ---- Oᵀ += Vᵀ Pᵀ: k-step ks covers keys 16ks + {4h + 0..3, 8 + 4h + 0..3} for lane half h
 #pragma unroll
@@ -339,12 +275,6 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_m32_kernel(const Args a) {
 
     if (kt + 1 < ntiles) store_tile((kt + 1) & 1);   // other buffer: its last reads were a barrier ago
     __syncthreads();
-  };
-  if constexpr (VER == 1) {
-    for (int kt = 0; kt < ntiles; ++kt) tile_step(kt, kMasked{});   // runtime tail check per tile
-  } else {
-    for (int kt = 0; kt < nfull; ++kt) tile_step(kt, kFull{});
-    if (nfull < ntiles) tile_step(nfull, kMasked{});
   }
 
   // ---- epilogue: lane holds O[q0 + r][32db + 8(i>>2) + 4h + (i&3)]
@@ -366,26 +296,13 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_m32_kernel(const Args a) {
   }
 }
 
-// AMDK8S_ATTN_VER=2 selects the VER 2 loop (A/B on one box; box-to-box spread is ~5-8 %).
-int loop_version() {
-  static int v = 0;
-  if (!v) {
-    const char* e = getenv("AMDK8S_ATTN_VER");
-    v = (e && e[0] == '2') ? 2 : 1;
-  }
-  return v;
-}
-
 template <bool BF16, int NW, int D>
 int launch(const Args& a0, int NH, hipStream_t stream) {
   Args a = a0;
   a.nqb = (a.Lq + NW * 32 - 1) / (NW * 32);
   const long nwg = (long)a.nqb * NH;
   if (nwg <= 0 || nwg > 0x7fffffff) return -1;
-  if (loop_version() == 2)
-    hipLaunchKernelGGL((attn_m32_kernel<BF16, NW, D, 2>), dim3((unsigned)nwg), dim3(NW * 64), 0, stream, a);
-  else
-    hipLaunchKernelGGL((attn_m32_kernel<BF16, NW, D, 1>), dim3((unsigned)nwg), dim3(NW * 64), 0, stream, a);
+  hipLaunchKernelGGL((attn_m32_kernel<BF16, NW, D>), dim3((unsigned)nwg), dim3(NW * 64), 0, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

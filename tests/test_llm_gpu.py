@@ -81,6 +81,35 @@ def test_quantise_kernel_and_rmsnorm(dev, LK):
 
 
 @pytest.mark.parametrize("qt", ["Q4_K", "Q6_K"])
+@pytest.mark.parametrize("T", [1, 4])
+def test_pair_gemv_q8_output(dev, LK, qt, T):
+    """gate|up pair GEMV emitting silu(g)·u as Q8 (the ffn_down input): matches the fp32 output
+    quantised by rmsnorm_q8 (same per-32 scale, values within one quantisation step) and the
+    pre-multiplied 16-sums are consistent with the int8 values."""
+    from k8s_nvidia_gpus_amd.models.llm import gguf
+
+    t = getattr(gguf, qt)
+    N, K = 320, 1536                 # 10 whole 32-row blocks per token
+    w0, _ = _qw(N, K, t, 4, dev)
+    w1, _ = _qw(N, K, t, 5, dev)
+    x = torch.randn(T, K, device=dev)
+    x8, dx, sx, _ = _q8(x, LK)
+    out = torch.empty(T, N, device=dev)
+    LK.qgemv(w0, x8, dx, sx, out, LK.PAIR, w1=w1)
+    r8, rdx, rsx, rq = _q8(out, LK)
+    o8 = torch.empty(T, N, dtype=torch.int8, device=dev)
+    odx = torch.empty(T, N // 32, device=dev)
+    osx = torch.empty(T, N // 16, device=dev)
+    junk = torch.full((T, N), 7.0, device=dev)
+    LK.qgemv(w0, x8, dx, sx, junk, LK.PAIR, w1=w1, q8_out=(o8, odx, osx))
+    torch.testing.assert_close(odx, rdx, rtol=1e-6, atol=0)
+    assert int((o8.int() - r8.int()).abs().max()) <= 1
+    sums = (o8.float().view(T, N // 16, 16).sum(-1)) * odx.repeat_interleave(2, -1)
+    torch.testing.assert_close(osx, sums, rtol=1e-5, atol=1e-5)
+    assert bool((junk == 7.0).all())              # fp32 output untouched in Q8 mode
+
+
+@pytest.mark.parametrize("qt", ["Q4_K", "Q6_K"])
 @pytest.mark.parametrize("T", [1, 2, 3, 4])
 @pytest.mark.parametrize("mode", ["store", "resid", "pair"])
 @pytest.mark.parametrize("cfg", [(0, 0), (4, 7), (8, 6), (2, 1), (1, 3)])
