@@ -16,10 +16,10 @@ from k8s_nvidia_gpus_amd.operator.validator import default_runner
 
 REPO = Path(__file__).resolve().parent.parent
 LOGS = {
-    "amd-vectoradd": (REPO / "profiles/r01_vectoradd.log").read_text(),
-    "amd-gemm-validator": (REPO / "profiles/r01_gemm_validator.log").read_text(),
-    "amd-gemm-validator:fp8": (REPO / "profiles/r01_gemm_validator_fp8.log").read_text(),
-    "amd-proftester": (REPO / "profiles/r02_session1/proftester_all.log").read_text(),
+    "amd-vectoradd": (REPO / "tests/fixtures/native_logs/r01_vectoradd.log").read_text(),
+    "amd-gemm-validator": (REPO / "tests/fixtures/native_logs/r01_gemm_validator.log").read_text(),
+    "amd-gemm-validator:fp8": (REPO / "tests/fixtures/native_logs/r01_gemm_validator_fp8.log").read_text(),
+    "amd-proftester": (REPO / "tests/fixtures/native_logs/proftester_all.log").read_text(),
     "rccl-allreduce-bench": '{"check": "rccl_allreduce", "ngpus": 8, "peak_busbw_gbps": 301.2, '
                             '"wrong": 0, "passed": true}\nTest PASSED\nDone\n',
 }

@@ -1,6 +1,7 @@
 """Validator chain: gating logic on the REAL outputs the native tools produced on an MI355X.
 
-profiles/r01_vectoradd.log and profiles/r01_gemm_validator.log are the stdout of native/bin/
+tests/fixtures/native_logs/ (copies of profiles/r01_vectoradd.log, r01_gemm_validator*.log and
+profiles/r02_session1/proftester_all.log) are the stdout of native/bin/
 amd-vectoradd and amd-gemm-validator from the first gpurun session; the driver step runs the real
 kfd-probe binary (host C++, built here) against a fabricated MI355X sysfs tree.
 """
@@ -19,11 +20,11 @@ from k8s_nvidia_gpus_amd.operator.validator import (Validator, json_lines, proto
 from k8s_nvidia_gpus_amd.utils.kube import KubeClient
 
 REPO = Path(__file__).resolve().parent.parent
-VECTORADD_LOG = (REPO / "profiles/r01_vectoradd.log").read_text()
-GEMM_LOG = (REPO / "profiles/r01_gemm_validator.log").read_text()
-GEMM_FP8_LOG = (REPO / "profiles/r01_gemm_validator_fp8.log").read_text()
+VECTORADD_LOG = (REPO / "tests/fixtures/native_logs/r01_vectoradd.log").read_text()
+GEMM_LOG = (REPO / "tests/fixtures/native_logs/r01_gemm_validator.log").read_text()
+GEMM_FP8_LOG = (REPO / "tests/fixtures/native_logs/r01_gemm_validator_fp8.log").read_text()
 # stdout of native/bin/amd-proftester --json on one MI355X (round 2, session 1)
-PROFTESTER_LOG = (REPO / "profiles/r02_session1/proftester_all.log").read_text()
+PROFTESTER_LOG = (REPO / "tests/fixtures/native_logs/proftester_all.log").read_text()
 
 
 def _pt_line(test, device, value, peer=-1, engine="", passed=True, skipped=False):
@@ -366,7 +367,7 @@ def test_exporter_publishes_bandwidth_results(tmp_path, cfg):
 
 
 # ----------------------------------------------------------------------------- rocprof counters
-PMC_DIR = REPO / "profiles/r02_session2/pmc_validator"
+PMC_DIR = REPO / "tests/fixtures/pmc_validator"   # copy of profiles/r02_session2/pmc_validator
 
 
 def test_rocprof_counter_summary_on_real_mi355x_csv():
