@@ -89,7 +89,7 @@ def test_pair_gemv_q8_output(dev, LK, qt, T):
     from k8s_nvidia_gpus_amd.models.llm import gguf
 
     t = getattr(gguf, qt)
-    N, K = 320, 1536                 # 10 whole 32-row blocks per token
+    N, K = 512, 1536                 # 16 whole 32-row blocks per token (rmsnorm_q8: N % 256)
     w0, _ = _qw(N, K, t, 4, dev)
     w1, _ = _qw(N, K, t, 5, dev)
     x = torch.randn(T, K, device=dev)
