@@ -59,6 +59,7 @@ class StepBuffers:
     pos: torch.Tensor
     slot: torch.Tensor
     h: torch.Tensor
+    h2: torch.Tensor        # the other residual buffer of the fused-norm path (ping-pong)
     x8: torch.Tensor
     dx: torch.Tensor
     sx: torch.Tensor
@@ -72,6 +73,9 @@ class StepBuffers:
     t: torch.Tensor
     logits: torch.Tensor
     graphs: Dict[tuple, torch.cuda.CUDAGraph] = None   # keyed by (attention span, fused rope)
+    meta: torch.Tensor = None        # int32 [3, T] on the GPU: tok / pos / slot are its rows
+    host: torch.Tensor = None        # pinned staging copy of meta
+    host_evt: torch.cuda.Event = None
 
 
 class Engine:
@@ -119,6 +123,11 @@ class Engine:
         # with the once-per-input Q8 path: the gate|up pair GEMV quantises silu(g)·u itself (its
         # workgroups own whole 32-row blocks), so ffn_down needs no separate quantisation launch
         self.pair_q8 = os.environ.get("AMDK8S_LLM_PAIR_Q8", "1") != "0"   # T=1 2.13 -> 2.07 ms (r03/q)
+        # with the once-per-input Q8 path: o_proj and ffn_down write the new residual to the other
+        # of two buffers and their last workgroup RMS-normalises + quantises it for the next GEMV
+        # (LK.qgemv(..., cnt=)), so no rmsnorm_q8 launch is left inside the layer loop
+        self.resid_norm = os.environ.get("AMDK8S_LLM_RESID_NORM", "0") != "0"
+        self._norm_cnt = None
         self._attn_cnt = None
         self._side = None
         if self.gpu:
@@ -214,11 +223,11 @@ class Engine:
             kmax = max(c.dim, c.ffn)
             nsplit = self.max_ctx // self.LK.attn_chunk()
             f32 = dict(dtype=torch.float32, device=dev)
+            meta = torch.zeros(3, T, dtype=torch.int32, device=dev)
             b = StepBuffers(
-                T=T, tok=torch.zeros(T, dtype=torch.int32, device=dev),
-                pos=torch.zeros(T, dtype=torch.int32, device=dev),
-                slot=torch.zeros(T, dtype=torch.int32, device=dev),
-                h=torch.zeros(T, c.dim, **f32),
+                T=T, tok=meta[0], pos=meta[1], slot=meta[2], meta=meta,
+                host=torch.zeros(3, T, dtype=torch.int32).pin_memory(),
+                h=torch.zeros(T, c.dim, **f32), h2=torch.zeros(T, c.dim, **f32),
                 x8=torch.zeros(T, kmax, dtype=torch.int8, device=dev),
                 dx=torch.zeros(T, kmax // 32, **f32), sx=torch.zeros(T, kmax // 16, **f32),
                 x8f=torch.zeros(T, c.ffn, dtype=torch.int8, device=dev),
@@ -269,6 +278,10 @@ class Engine:
                 return q, {}
             return (None, None, None), dict(xf=xf, norm_w=norm_w, eps=c.eps)
 
+        if (self.resid_norm and b.T >= self.q8_split_T and self.pair_q8 and c.ffn % 32 == 0
+                and c.dim % 256 == 0 and c.dim <= 4096):
+            self._step_fused_norm(b, span, fused, cnt)
+            return
         pf = self.prefetch_wgs > 0
         if pf:
             main = torch.cuda.current_stream(self.device)
@@ -312,14 +325,58 @@ class Engine:
         if pf:
             main.wait_stream(self._side)   # join (graph capture needs every fork joined)
 
+    def _step_fused_norm(self, b: StepBuffers, span: int, fused: bool, cnt) -> None:
+        """The decode step with the norms fused into the residual GEMVs: per layer q|k|v,
+        attention (+ combine), o_proj (h -> h2, + ffn_norm Q8), gate|up (-> Q8), ffn_down (h2 -> h,
+        + the next layer's attn_norm / out_norm Q8) — one rmsnorm_q8 launch per step."""
+        LK, c = self.LK, self.cfg
+        if self._norm_cnt is None:
+            self._norm_cnt = torch.zeros(4, dtype=torch.int32, device=self.device)
+        nc = self._norm_cnt[:1]
+        G = self.gemv_cfg
+        qd = self._q8(b, c.dim)
+        qf = (b.x8f, b.dxf, b.sxf)
+        scale = 1.0 / math.sqrt(c.head_dim)
+        layers = self.w.layers
+        LK.rmsnorm_q8(b.h, layers[0].attn_norm, c.eps, *qd)
+        for i, L in enumerate(layers):
+            off = 0
+            for w in L.wqkv:
+                LK.qgemv(w, *qd, b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:], ldo=b.qkv.stride(0),
+                         **G)
+                off += w.n
+            if fused:
+                LK.attn_decode(None, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
+                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
+                               span=span, qkv=b.qkv, cos_t=self.cos, sin_t=self.sin, cnt=cnt)
+            else:
+                LK.rope_kv(b.qkv, b.pos, b.slot, self.cos, self.sin, c.heads, c.kv_heads,
+                           c.head_dim, self.max_ctx, b.qrot, self.k_cache[i], self.v_cache[i])
+                LK.attn_decode(b.qrot, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
+                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
+                               span=span, cnt=cnt)
+            LK.qgemv(L.wo, *qd, b.h2, LK.RESID, res=b.h, norm_out=L.ffn_norm, q8_out=qd, cnt=nc,
+                     eps=c.eps, **G)
+            LK.qgemv(L.wg, *qd, b.t, LK.PAIR, w1=L.wu, **G, q8_out=qf)
+            nxt = layers[i + 1].attn_norm if i + 1 < len(layers) else self.w.out_norm
+            LK.qgemv(L.wd, *qf, b.h, LK.RESID, res=b.h2, norm_out=nxt, q8_out=qd, cnt=nc,
+                     eps=c.eps, **G)
+        LK.qgemv(self.w.output, *qd, b.logits, LK.STORE, **G)
+
     def _decode_native(self, tokens: Sequence[int], positions: Sequence[int],
                        slots: Sequence[int]) -> torch.Tensor:
         T = len(tokens)
         b = self._buffers(T)
-        host = torch.tensor([list(tokens), list(positions), list(slots)], dtype=torch.int32)
-        b.tok.copy_(host[0], non_blocking=False)
-        b.pos.copy_(host[1])
-        b.slot.copy_(host[2])
+        # one H2D copy per step from a pinned staging row (three synchronous pageable copies cost
+        # ~3 x 10 us of idle GPU per token); the event guards the row against being rewritten
+        # before the previous step's copy has read it
+        if b.host_evt is not None:
+            b.host_evt.synchronize()
+        b.host.copy_(torch.tensor([list(tokens), list(positions), list(slots)], dtype=torch.int32))
+        b.meta.copy_(b.host, non_blocking=True)
+        if b.host_evt is None:
+            b.host_evt = torch.cuda.Event()
+        b.host_evt.record()
         span = self._span(max(positions))
         fused = len(set(slots)) == len(slots)
         if self.use_graphs:

@@ -72,6 +72,16 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Write-through (sc1) store / sc1 load: relaxed agent-scope atomics.  Data handed to another
+// workgroup INSIDE a launch goes through these on both sides (per-XCD L2s are not coherent; see
+// arrive_last).
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // LDS offset of activation byte p of one token (32-byte pad per 256 bytes)
 __device__ __forceinline__ int xoff(int p) { return (p >> 8) * 288 + (p & 255); }
 
@@ -107,6 +117,12 @@ struct GemvArgs {
   int8_t* ox8;           // [T][N]
   float* odx;            // [T][N/32]
   float* osx;            // [T][N/16]
+  // resid mode with a fused RMSNorm of the updated residual (cnt != null): out = res + W.x is
+  // stored write-through, and the last workgroup to finish RMS-normalises out with onorm_w and
+  // quantises it into ox8 / odx / osx (the next GEMV's input) — no separate norm launch
+  const float* res;      // [T][ldo] residual input (out must be a different buffer)
+  const float* onorm_w;  // [N]
+  int* cnt;              // arrival counter, zero between launches (the last arriver resets it)
 };
 
 // Weights are streamed exactly once per step: non-temporal loads keep them from evicting the
@@ -297,7 +313,10 @@ __device__ __forceinline__ void finish_row(const GemvArgs& a, int row, int lane,
       if (t == lane) { v = acc[t]; v1 = acc1[t]; }
     float* o = a.out + (long)lane * a.ldo + row;
     if constexpr (MODE == kStore) *o = v + (a.bias ? a.bias[row] : 0.f);
-    else if constexpr (MODE == kResid) *o += v;
+    else if constexpr (MODE == kResid) {
+      if (a.res) st_wt(o, a.res[(long)lane * a.ldo + row] + v);   // fused-norm form
+      else *o += v;
+    }
     else {
       const float y = v / (1.f + __expf(-v)) * v1;
       if (q8s) q8s[lane * 32 + (row - wrow0)] = y;   // quantised at the end of the workgroup
@@ -328,6 +347,91 @@ __device__ __forceinline__ void compute_reg(int nb, int sub, int bl, const XReg 
 #pragma unroll
         for (int t = 0; t < T; ++t) acc1[t] = dot_apply<TYPE>(p1, xr[u][t], acc1[t]);
       }
+    }
+  }
+}
+
+
+// Fused RMSNorm + Q8 of the updated residual (resid mode, cnt != null), run by the LAST workgroup
+// of the launch.  Every workgroup's out stores were write-through (st_wt); each wave drains them,
+// the workgroup meets at a barrier, one lane counts in, and the workgroup that draws gridDim - 1
+// reads out back with sc1 loads (ld_wt) — the arrive_last hand-off at launch scope.  The first 256
+// threads normalise: thread = 8-value chunks tid + 256 j, a lane quad = one 32-value Q8 block (the
+// rmsnorm_q8_kernel mapping); the per-token arithmetic does not depend on T.  N % 256 == 0,
+// N <= 4096 (checked by the host; larger models keep the rmsnorm_q8 launch).
+constexpr int kNormCh = 2;          // 8-value chunks per thread and token: N <= 4096
+template <int T>
+__device__ __forceinline__ void resid_norm_tail(const GemvArgs& a, float* red) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave: its sc1 stores landed
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(red);
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(a.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (int)gridDim.x - 1;
+    if (last) __hip_atomic_store(a.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  if (*flag == 0) return;
+  const int N = a.N, nch = N >> 3, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  float* part = red + 4;                             // [T][4] per-wave sums (red[0] = the flag)
+  // every token's rows in flight at once (one memory round trip), then per token the same maths
+  float v[T][kNormCh][8];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int j = 0; j < kNormCh; ++j) {
+      const int c = tid + 256 * j;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        v[t][j][i] = (tid < 256 && c < nch) ? ld_wt(a.out + (long)t * a.ldo + c * 8 + i) : 0.f;
+    }
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < kNormCh; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss = __fmaf_rn(v[t][j][i], v[t][j][i], ss);
+    ss = wave_sum(ss);
+    if (lane == 0 && wave < 4) part[t * 4 + wave] = ss;
+  }
+  __syncthreads();
+  if (tid >= 256) return;
+#pragma unroll
+  for (int j = 0; j < kNormCh; ++j) {
+    const int c = tid + 256 * j;
+    if (c >= nch) break;                             // whole quads (nch % 32 == 0)
+    const float4 wa = *reinterpret_cast<const float4*>(a.onorm_w + c * 8);
+    const float4 wb = *reinterpret_cast<const float4*>(a.onorm_w + c * 8 + 4);
+    const float ww[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const float r = rsqrtf((part[t * 4] + part[t * 4 + 1] + part[t * 4 + 2] + part[t * 4 + 3]) /
+                             (float)N + a.eps);
+      float q[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) q[i] = v[t][j][i] * (r * ww[i]);
+      float amax = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(q[i]));
+      amax = fmaxf(amax, __shfl_xor(amax, 1, kWave));
+      amax = fmaxf(amax, __shfl_xor(amax, 2, kWave));
+      const float d = amax / 127.f;
+      const float id = d > 0.f ? 1.f / d : 0.f;
+      uint32_t pk[2] = {0u, 0u};
+      int sq = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int qi = (int)__builtin_rintf(q[i] * id);
+        pk[i >> 2] |= ((uint32_t)(qi & 0xff)) << (8 * (i & 3));
+        sq += qi;
+      }
+      sq += __shfl_xor(sq, 1, kWave);
+      *reinterpret_cast<uint2*>(a.ox8 + (long)t * N + c * 8) = make_uint2(pk[0], pk[1]);
+      if ((tid & 3) == 0) a.odx[(long)t * (N >> 5) + (c >> 2)] = d;
+      if ((tid & 1) == 0) a.osx[(long)t * (N >> 4) + (c >> 1)] = d * (float)sq;
     }
   }
 }
@@ -552,6 +656,9 @@ __global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
       }
     }
   }
+  if constexpr (MODE == kResid) {
+    if (a.cnt) resid_norm_tail<T>(a, red);
+  }
 }
 
 // ---------------------------------------------------------------- RMSNorm + Q8 activation quant
@@ -696,72 +803,97 @@ struct AttnArgs {
   float* sx;
 };
 
-// Arrival of one (token, kv head) workgroup: publishes its partials, counts in, and tells whether
-// it was the last of the nsplit (then the others' partials are visible to it).
+// In-launch hand-off of the chunk partials (MI355X: per-XCD L2s are not coherent): every partial is
+// stored write-through (sc1: relaxed agent-scope atomic store) and read back with sc1 loads, so no
+// release / acquire fence (buffer_wbl2 / buffer_inv: several us each) is needed — each storing wave
+// drains its stores (vmcnt(0)), the workgroup meets at a barrier, then ONE lane counts in with an
+// agent-scope add; the workgroup whose add returns nsplit - 1 is last and merges (the hand-off form
+// of the MI355X visibility table: sc1 stores + drain + counter add, sc1 loads by the last arriver).
+// Arrival of one (token, kv head) workgroup after its write-through partial stores; true for the
+// last of the nsplit (which then reads every partial with ld_wt).  The counter is left at zero.
 __device__ __forceinline__ bool arrive_last(int* cnt, int nsplit) {
   __shared__ int last;
-  __threadfence();                       // release this workgroup's po / pml device-wide
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave: its sc1 stores landed
   __syncthreads();
   if (threadIdx.x == 0) {
-    last = atomicAdd(cnt, 1) == nsplit - 1;
-    if (last) atomicExch(cnt, 0);        // every split has arrived: ready for the next launch
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == nsplit - 1;
+    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  if (last) __threadfence();             // acquire the other workgroups' partials
   return last;
 }
 
-// Merge the chunks of head h of token t and quantise the attention output to Q8 (the o_proj
-// input): thread dd = one output dim; a 32-dim block = half a wave (dd & 31 within a wave).
-__device__ __forceinline__ void combine_head(const float* __restrict__ po,
-                                             const float* __restrict__ pml,
-                                             const int* __restrict__ pos, int H, int nsplit,
-                                             int h, int t, int dd, float* __restrict__ out,
-                                             int8_t* __restrict__ x8, float* __restrict__ dx,
-                                             float* __restrict__ sx) {
+// Merge the chunks of NH heads (h0, h0 + hstep, ...; those >= hend are skipped) of token t and
+// quantise the attention output to Q8 (the o_proj input): thread dd = one output dim of each of its
+// heads; a 32-dim block = half a wave (dd & 31 within a wave).  One pass over the chunks in groups
+// of 8 with every partial of the group (all NH heads) loaded before any maths (online max: one
+// memory round trip per 8 chunks); per head the arithmetic does not depend on NH, so the separate
+// combine kernel (NH = 1) and the in-launch merge (NH = ceil(G / 2)) give identical bits.
+template <int NH>
+__device__ __forceinline__ void combine_heads(const float* __restrict__ po,
+                                              const float* __restrict__ pml,
+                                              const int* __restrict__ pos, int H, int nsplit,
+                                              int h0, int hstep, int hend, int t, int dd,
+                                              float* __restrict__ out, int8_t* __restrict__ x8,
+                                              float* __restrict__ dx, float* __restrict__ sx) {
   const int ns = min(nsplit, (pos[t] + kAttnChunk) / kAttnChunk);
-  const long hb = ((long)t * H + h) * nsplit;
-  // chunk partials in groups of 8 with all loads in flight (indices clamped, extra terms masked)
-  float m = -INFINITY;
+  long hb[NH];
+#pragma unroll
+  for (int k = 0; k < NH; ++k) hb[k] = ((long)t * H + min(h0 + k * hstep, hend - 1)) * nsplit;
+  float m[NH], den[NH], v[NH];
+#pragma unroll
+  for (int k = 0; k < NH; ++k) { m[k] = -INFINITY; den[k] = 0.f; v[k] = 0.f; }
   for (int s0 = 0; s0 < ns; s0 += 8) {
-    float2 ml[8];
+    float mx[NH][8], l[NH][8], ov[NH][8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      ml[u] = *reinterpret_cast<const float2*>(pml + (hb + min(s0 + u, ns - 1)) * 2);
+    for (int k = 0; k < NH; ++k)
 #pragma unroll
-    for (int u = 0; u < 8; ++u) m = fmaxf(m, ml[u].x);
-  }
-  float den = 0.f, v = 0.f;
-  for (int s0 = 0; s0 < ns; s0 += 8) {
-    float2 ml[8];
-    float ov[8];
+      for (int u = 0; u < 8; ++u) {                  // indices clamped, extra terms masked below
+        const long sidx = hb[k] + min(s0 + u, ns - 1);
+        mx[k][u] = ld_wt(pml + sidx * 2);
+        l[k][u] = ld_wt(pml + sidx * 2 + 1);
+        ov[k][u] = ld_wt(po + sidx * kHeadDim + dd);
+      }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const long s = hb + min(s0 + u, ns - 1);
-      ml[u] = *reinterpret_cast<const float2*>(pml + s * 2);
-      ov[u] = po[s * kHeadDim + dd];
+    for (int k = 0; k < NH; ++k) {
+      float mn = m[k];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (s0 + u < ns) mn = fmaxf(mn, mx[k][u]);
+      if (mn == -INFINITY) continue;                 // nothing attended yet
+      const float sc = m[k] == -INFINITY ? 0.f : __expf(m[k] - mn);
+      den[k] *= sc;
+      v[k] *= sc;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float wgt = (s0 + u < ns && mx[k][u] != -INFINITY) ? __expf(mx[k][u] - mn) : 0.f;
+        den[k] += wgt * l[k][u];
+        v[k] += wgt * ov[k][u];
+      }
+      m[k] = mn;
     }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float wgt = (s0 + u < ns && ml[u].x != -INFINITY) ? __expf(ml[u].x - m) : 0.f;
-      den += wgt * ml[u].y;
-      v += wgt * ov[u];
-    }
   }
-  v = den > 0.f ? v / den : 0.f;
-  const int K = H * kHeadDim, col = h * kHeadDim + dd;
-  if (out) out[(long)t * K + col] = v;
-  float amax = fabsf(v);
+  const int K = H * kHeadDim;
 #pragma unroll
-  for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, kWave));
-  const float d = amax / 127.f;
-  const int qv = d > 0.f ? (int)__builtin_rintf(v / d) : 0;
-  x8[(long)t * K + col] = (int8_t)qv;
-  int s16 = qv;
+  for (int k = 0; k < NH; ++k) {
+    const int h = h0 + k * hstep;
+    if (h >= hend) break;                            // uniform per wave (hstep multiple of waves)
+    const float y = den[k] > 0.f ? v[k] / den[k] : 0.f;
+    const int col = h * kHeadDim + dd;
+    if (out) out[(long)t * K + col] = y;
+    float amax = fabsf(y);
 #pragma unroll
-  for (int o = 8; o > 0; o >>= 1) s16 += __shfl_xor(s16, o, kWave);
-  if ((dd & 31) == 0) dx[(long)t * (K >> 5) + (col >> 5)] = d;
-  if ((dd & 15) == 0) sx[(long)t * (K >> 4) + (col >> 4)] = d * (float)s16;
+    for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, kWave));
+    const float d = amax / 127.f;
+    const int qv = d > 0.f ? (int)__builtin_rintf(y / d) : 0;
+    x8[(long)t * K + col] = (int8_t)qv;
+    int s16 = qv;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) s16 += __shfl_xor(s16, o, kWave);
+    if ((dd & 31) == 0) dx[(long)t * (K >> 5) + (col >> 5)] = d;
+    if ((dd & 15) == 0) sx[(long)t * (K >> 4) + (col >> 4)] = d * (float)s16;
+  }
 }
 
 // grid (H, T), 128 threads.
@@ -772,7 +904,8 @@ __global__ void __launch_bounds__(128) attn_combine_q8_kernel(const float* __res
                                                               int8_t* __restrict__ x8,
                                                               float* __restrict__ dx,
                                                               float* __restrict__ sx) {
-  combine_head(po, pml, pos, H, nsplit, blockIdx.x, blockIdx.y, threadIdx.x, out, x8, dx, sx);
+  combine_heads<1>(po, pml, pos, H, nsplit, blockIdx.x, 1, H, blockIdx.y, threadIdx.x, out, x8,
+                   dx, sx);
 }
 
 template <int G>
@@ -797,19 +930,14 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   const int p0 = sp * kAttnChunk;
   const long pidx = ((long)t * H + kh * G) * nsplit + sp;   // + g * nsplit
   auto merge = [&]() {                   // fused combine by the last-arriving workgroup
-    if (a.cnt && arrive_last(a.cnt + t * Hkv + kh, nsplit)) {
-      for (int g0 = 0; g0 < G; g0 += 2) {
-        const int g = g0 + (threadIdx.x >> 7);
-        if (g < G)
-          combine_head(po, pml, pos, H, nsplit, kh * G + g, t, threadIdx.x & 127, a.out, a.x8,
-                       a.dx, a.sx);
-      }
-    }
+    if (a.cnt && arrive_last(a.cnt + t * Hkv + kh, nsplit))   // 2 heads per pass, all at once
+      combine_heads<(G + 1) / 2>(po, pml, pos, H, nsplit, kh * G + (threadIdx.x >> 7), 2,
+                                 kh * G + G, t, threadIdx.x & 127, a.out, a.x8, a.dx, a.sx);
   };
   if (p0 >= len) {
     if (threadIdx.x < G) {
-      pml[(pidx + (long)threadIdx.x * nsplit) * 2] = -INFINITY;
-      pml[(pidx + (long)threadIdx.x * nsplit) * 2 + 1] = 0.f;
+      st_wt(pml + (pidx + (long)threadIdx.x * nsplit) * 2, -INFINITY);
+      st_wt(pml + (pidx + (long)threadIdx.x * nsplit) * 2 + 1, 0.f);
     }
     merge();
     return;
@@ -953,12 +1081,12 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   for (int i = threadIdx.x; i < G * kHeadDim; i += blockDim.x) {
     const int g = i / kHeadDim, dd = i % kHeadDim;
     const float v = opart[0][g][dd] + opart[1][g][dd] + opart[2][g][dd] + opart[3][g][dd];
-    po[(pidx + (long)g * nsplit) * kHeadDim + dd] = v;
+    st_wt(po + (pidx + (long)g * nsplit) * kHeadDim + dd, v);
   }
   if (threadIdx.x < G) {
     const int g = threadIdx.x;
-    pml[(pidx + (long)g * nsplit) * 2] = mls[g][0];
-    pml[(pidx + (long)g * nsplit) * 2 + 1] = mls[g][1];
+    st_wt(pml + (pidx + (long)g * nsplit) * 2, mls[g][0]);
+    st_wt(pml + (pidx + (long)g * nsplit) * 2 + 1, mls[g][1]);
   }
   merge();
 }
@@ -1182,10 +1310,14 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
                      const void* w1d, const void* x8, const void* dx, const void* sx,
                      const void* xf, int ldx, const void* norm_w, float eps,
                      const void* bias, void* out, int ldo, int N, int K, int T, int waves,
-                     int rows_per_wg, void* ox8, void* odx, void* osx, void* stream) {
+                     int rows_per_wg, void* ox8, void* odx, void* osx, const void* res,
+                     const void* onorm_w, void* cnt, void* stream) {
   if (K % 256 || N <= 0 || T < 1 || T > kMaxTok) return 2;
   if (mode == kPair && !w1q) return 2;
-  if (ox8) {                                  // pair → Q8 output: whole 32-row blocks per workgroup
+  if (cnt) {                                  // resid + fused RMSNorm/Q8 of the new residual
+    if (mode != kResid || !res || res == out || !onorm_w || !ox8 || !odx || !osx) return 2;
+    if (N % 256 || N > kNormCh * 256 * 8 || ldo < N) return 2;
+  } else if (ox8) {                           // pair → Q8 output: whole 32-row blocks per workgroup
     if (mode != kPair || N % 32 || !odx || !osx) return 2;
     rows_per_wg = 32;
   }
@@ -1212,6 +1344,9 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
   a.ox8 = static_cast<int8_t*>(ox8);
   a.odx = static_cast<float*>(odx);
   a.osx = static_cast<float*>(osx);
+  a.res = static_cast<const float*>(res);
+  a.onorm_w = static_cast<const float*>(onorm_w);
+  a.cnt = static_cast<int*>(cnt);
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (type == kQ4K) {
     if (mode == kStore) return dispatch_t<kQ4K, kStore>(a, waves, st);

@@ -29,7 +29,8 @@ def _lib():
             lib.amdk8s_llm_max_tokens.restype = ci
             lib.amdk8s_llm_attn_chunk.restype = ci
             lib.amdk8s_llm_qgemv.argtypes = [ci, ci] + [vp] * 8 + [vp, vp, vp] \
-                + [vp, ci, vp, cf] + [vp, vp] + [ci, ci, ci, ci, ci, ci] + [vp, vp, vp, vp]
+                + [vp, ci, vp, cf] + [vp, vp] + [ci, ci, ci, ci, ci, ci] + [vp, vp, vp] \
+                + [vp, vp, vp] + [vp]
             lib.amdk8s_llm_qgemv.restype = ci
             lib.amdk8s_llm_rmsnorm_q8.argtypes = [vp, vp, cf, ci, ci, vp, vp, vp, vp]
             lib.amdk8s_llm_rmsnorm_q8.restype = ci
@@ -75,13 +76,16 @@ def attn_chunk() -> int:
 
 def qgemv(w0, x8, dx, sx, out, mode: int = STORE, w1=None, bias=None, ldo: int = None,
           rows_per_wg: int = 0, waves: int = 0, xf=None, norm_w=None, eps: float = 1e-6,
-          q8_out=None) -> None:
+          q8_out=None, res=None, norm_out=None, cnt=None) -> None:
     """``w0``/``w1``: :class:`~k8s_nvidia_gpus_amd.models.llm.weights.QWeight` on the GPU.
     Input: Q8 activations (``x8``/``dx``/``sx``, [T, K]) or fp32 rows ``xf`` [T, K] (pass
     ``x8=dx=sx=None``) that the kernel quantises itself, after an RMSNorm when ``norm_w`` is given.
     ``out`` fp32 [T, ldo] (a view with row stride ``ldo``).  ``waves`` per workgroup and
     ``rows_per_wg``: 0 = the kernel's default decomposition.  ``q8_out`` = (x8, dx, sx) [T, N]
-    (pair mode only): write silu(g)·u quantised to Q8 — the ffn_down input — instead of ``out``."""
+    (pair mode only): write silu(g)·u quantised to Q8 — the ffn_down input — instead of ``out``.
+    Resid mode with ``cnt`` (int32 [1] zeros, left zero): ``out = res + W.x`` (``out`` a different
+    buffer than ``res``), and the launch's last workgroup RMS-normalises ``out`` with ``norm_out``
+    and writes it as Q8 into ``q8_out`` — the next GEMV's input, without a norm launch."""
     t = (xf if xf is not None else x8).shape[0]
     ldo = out.stride(0) if ldo is None else ldo
     a = w0.ptrs()
@@ -91,7 +95,7 @@ def qgemv(w0, x8, dx, sx, out, mode: int = STORE, w1=None, bias=None, ldo: int =
                                    xf.stride(0) if xf is not None else 0, _p(norm_w), float(eps),
                                    _p(bias), out.data_ptr(), ldo, w0.n, w0.k, t,
                                    waves, rows_per_wg, *((_p(t) for t in q8_out) if q8_out else (None,) * 3),
-                                   _stream(ref)), "amdk8s_llm_qgemv")
+                                   _p(res), _p(norm_out), _p(cnt), _stream(ref)), "amdk8s_llm_qgemv")
 
 
 def rmsnorm_q8(x, w, eps: float, x8, dx, sx) -> None:

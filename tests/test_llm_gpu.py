@@ -320,6 +320,46 @@ def test_in_kernel_combine_equals_combine_kernel(dev, LK, H, Hkv):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("qt", ["Q4_K", "Q6_K"])
+@pytest.mark.parametrize("T", [1, 3, 4])
+def test_resid_gemv_fused_norm_tail(dev, LK, qt, T):
+    """Resid GEMV with the fused RMSNorm tail (cnt given): out = res + W.x bit-identical to the
+    in-place resid GEMV; the last workgroup's Q8 of RMSNorm(out) matches rmsnorm_q8 of the same
+    rows (same scales, int8 within one step); the arrival counter is left at zero, launch after
+    launch (448 workgroups arriving on one counter)."""
+    from k8s_nvidia_gpus_amd.models.llm import gguf
+
+    t = getattr(gguf, qt)
+    N, K = 3584, 1536
+    w, _ = _qw(N, K, t, 6, dev)
+    torch.manual_seed(10 + T)
+    x = torch.randn(T, K, device=dev)
+    x8, dx, sx, _ = _q8(x, LK)
+    res = torch.randn(T, N, device=dev)
+    nw = torch.rand(N, device=dev) + 0.5
+    ref = res.clone()
+    LK.qgemv(w, x8, dx, sx, ref, LK.RESID)
+    r8 = torch.empty(T, N, dtype=torch.int8, device=dev)
+    rdx = torch.empty(T, N // 32, device=dev)
+    rsx = torch.empty(T, N // 16, device=dev)
+    LK.rmsnorm_q8(ref, nw, 1e-6, r8, rdx, rsx)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    for _ in range(3):
+        out = torch.full((T, N), float("nan"), device=dev)
+        o8 = torch.empty(T, N, dtype=torch.int8, device=dev)
+        odx = torch.empty(T, N // 32, device=dev)
+        osx = torch.empty(T, N // 16, device=dev)
+        LK.qgemv(w, x8, dx, sx, out, LK.RESID, res=res, norm_out=nw, q8_out=(o8, odx, osx),
+                 cnt=cnt, eps=1e-6)
+        torch.cuda.synchronize()
+        assert int(cnt.item()) == 0
+        assert torch.equal(out, ref)
+        torch.testing.assert_close(odx, rdx, rtol=1e-5, atol=0)
+        assert int((o8.int() - r8.int()).abs().max()) <= 1
+        sums = o8.float().view(T, N // 16, 16).sum(-1) * odx.repeat_interleave(2, -1)
+        torch.testing.assert_close(osx, sums, rtol=1e-5, atol=1e-5)
+
+
 @pytest.fixture(scope="module")
 def tiny_gguf(tmp_path_factory):
     from k8s_nvidia_gpus_amd.models.llm import tiny
@@ -330,10 +370,12 @@ def tiny_gguf(tmp_path_factory):
     return write_synthetic_gguf(str(p), tiny(layers=4, dim=512, heads=4, kv_heads=2, ffn=1024))
 
 
-def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf):
+@pytest.mark.parametrize("resid_norm", [False, True])
+def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf, resid_norm):
     from k8s_nvidia_gpus_amd.models.llm.synthetic import load
 
     gpu, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=False)
+    gpu.resid_norm = resid_norm
     cpu, _ = load(tiny_gguf, device="cpu", max_ctx=512)
     prompt = tok.encode("<|im_start|>user\nhello world, a cozy cabin<|im_end|>\n")
     lg = gpu.prefill(prompt, slot=1)            # native kernels, 4 tokens per step
@@ -352,13 +394,16 @@ def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf):
     assert gpu.stats["graph_captures"] >= 1
 
 
-def test_engine_batched_decode_equals_single(dev, tiny_gguf):
+@pytest.mark.parametrize("resid_norm,fused_combine", [(False, False), (True, False), (True, True)])
+def test_engine_batched_decode_equals_single(dev, tiny_gguf, resid_norm, fused_combine):
     """T sequences in one step give the same logits as each alone: slots are independent and the
     GEMV's roundings are pinned, so the int8 activation quantisation never flips between a batched
-    and a single step (batch-invariant serving)."""
+    and a single step (batch-invariant serving) — also with the norms fused into the residual
+    GEMVs and the attention combine inside the attention launch."""
     from k8s_nvidia_gpus_amd.models.llm.synthetic import load
 
     eng, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=True)
+    eng.resid_norm, eng.fused_combine = resid_norm, fused_combine
     prompts = [tok.encode(s) for s in ("hello", "the quick brown fox", "a cozy cabin in", "you")]
     last = []
     for s, p in enumerate(prompts):

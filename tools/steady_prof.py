@@ -5,6 +5,8 @@ lazy kernel loads), sleep 300 ms, then run N iterations — tools/rocpd_summary.
 
     python tools/steady_prof.py sd15-unet  [--iters 20]   # one SD1.5 UNet CFG pass (512², fp16)
     python tools/steady_prof.py wan-step   [--iters 5]    # one Wan2.1-1.3B CFG DiT step (2560 tokens)
+    python tools/steady_prof.py llm-decode [--iters 64]   # one Qwen2.5-7B Q4_K_M decode step, T=1
+                                                          #   (position 512, host sync per token)
 """
 import argparse
 import os
@@ -37,13 +39,35 @@ def wan_step():
     return lambda: model(x, 0.7)
 
 
+def llm_decode(T: int = 1):
+    from k8s_nvidia_gpus_amd.models.llm.config import QWEN25_7B
+    from k8s_nvidia_gpus_amd.models.llm.engine import Engine
+    from k8s_nvidia_gpus_amd.models.llm.weights import ModelWeights
+
+    w = ModelWeights.random(QWEN25_7B, device=torch.device("cuda", 0), seed=0)
+    eng = Engine(w, max_ctx=4096, slots=4, dense=True)
+    prompt = list(range(100, 612))
+    for s in range(T):
+        eng.prefill(prompt, slot=s)
+    state = {"pos": len(prompt), "tok": [11] * T}
+
+    def step():
+        p = state["pos"]
+        lg = eng.decode(state["tok"], [p] * T, list(range(T)))
+        state["tok"] = [int(x) % QWEN25_7B.vocab for x in torch.argmax(lg, -1).tolist()]
+        state["pos"] = p + 1 if p + 1 < 1000 else len(prompt)
+    return step
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["sd15-unet", "wan-step"])
+    ap.add_argument("what", choices=["sd15-unet", "wan-step", "llm-decode"])
+    ap.add_argument("--tokens", type=int, default=1, help="llm-decode: concurrent sequences")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     a = ap.parse_args()
-    fn = {"sd15-unet": sd15_unet, "wan-step": wan_step}[a.what]()
+    fn = (llm_decode(a.tokens) if a.what == "llm-decode"
+          else {"sd15-unet": sd15_unet, "wan-step": wan_step}[a.what]())
     for _ in range(a.warmup):
         fn()
     torch.cuda.synchronize()
