@@ -116,17 +116,24 @@ class Engine:
         self.q8_split_T = int(os.environ.get("AMDK8S_LLM_Q8SPLIT", "1")) or (1 << 30)
         # decode attention's chunk merge inside the attention kernel (last-arriving workgroup of a
         # (token, kv head) combines; arrival counters stay zero between launches).  Correct but
-        # measured slower (profiles/r03/n: T=1 2.10 -> 2.43 ms): the agent-scope release / acquire
-        # fences around the arrival counter write back / invalidate L2 across the XCDs, which
-        # costs more than the separate combine launch.  Off by default.
+        # measured slower: with agent-scope release / acquire fences T=1 2.10 -> 2.43 ms
+        # (profiles/r03/n); with write-through (sc1) partials, no fences and a one-pass merge of
+        # all heads 1.94 -> 2.06 ms (profiles/r03/w: the attention launch grows 8.7 -> 15.3 us,
+        # more than the 4.6 us combine launch it replaces).  Off by default.
         self.fused_combine = os.environ.get("AMDK8S_LLM_FUSED_COMBINE", "0") != "0"
         # with the once-per-input Q8 path: the gate|up pair GEMV quantises silu(g)·u itself (its
         # workgroups own whole 32-row blocks), so ffn_down needs no separate quantisation launch
         self.pair_q8 = os.environ.get("AMDK8S_LLM_PAIR_Q8", "1") != "0"   # T=1 2.13 -> 2.07 ms (r03/q)
         # with the once-per-input Q8 path: o_proj and ffn_down write the new residual to the other
         # of two buffers and their last workgroup RMS-normalises + quantises it for the next GEMV
-        # (LK.qgemv(..., cnt=)), so no rmsnorm_q8 launch is left inside the layer loop
+        # (LK.qgemv(..., cnt=)), so no rmsnorm_q8 launch is left inside the layer loop.  Correct
+        # (tests) but measured slower (profiles/r03/w: T=1 1.94 -> 2.17 ms; o_proj 5.8 -> 14.2 us:
+        # write-through drain + a 448-way arrival counter + the last workgroup's reload cost more
+        # than a boundary and the 4.5 us norm launch).  Off by default.
         self.resid_norm = os.environ.get("AMDK8S_LLM_RESID_NORM", "0") != "0"
+        # q|k (Q4_K) and v (Q6_K in about half the Q4_K_M layers) in one two-matrix launch:
+        # T=1 2.00 -> 1.94 ms, T=4 3.36 -> 3.27 ms (profiles/r03/w)
+        self.qkv2 = os.environ.get("AMDK8S_LLM_QKV2", "1") != "0"
         self._norm_cnt = None
         self._attn_cnt = None
         self._side = None
@@ -294,12 +301,15 @@ class Engine:
                 self.LK.prefetch(planes, self.prefetch_wgs, self._side)
             # RMSNorm + Q8 quantisation: in each GEMV's prologue (fp32 input + norm weight), or once
             # per input for larger T (act())
-            off = 0
             xin = act(b.h, L.attn_norm, c.dim)
-            for w in L.wqkv:
-                LK.qgemv(w, *xin[0], b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:],
-                         ldo=b.qkv.stride(0), **xin[1], **G)
-                off += w.n
+            if xin[0][0] is not None:
+                self._qkv(b, L, xin[0])
+            else:
+                off = 0
+                for w in L.wqkv:
+                    LK.qgemv(w, *xin[0], b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:],
+                             ldo=b.qkv.stride(0), **xin[1], **G)
+                    off += w.n
             if fused:
                 LK.attn_decode(None, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
                                c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
@@ -325,6 +335,20 @@ class Engine:
         if pf:
             main.wait_stream(self._side)   # join (graph capture needs every fork joined)
 
+    def _qkv(self, b: StepBuffers, L, q8) -> None:
+        """q|k|v projections from the Q8 input: one launch, also when q|k and v are stored in
+        different quantisation types (two-matrix GEMV; AMDK8S_LLM_QKV2=0 launches them apart)."""
+        LK, G = self.LK, self.gemv_cfg
+        if len(L.wqkv) == 2 and self.qkv2:
+            w0, w1 = L.wqkv
+            if LK.qgemv2(w0, w1, *q8, b.qkv[:, :w0.n], b.qkv[:, w0.n:], bias0=L.bqkv[:w0.n],
+                         bias1=L.bqkv[w0.n:], **G):
+                return
+        off = 0
+        for w in L.wqkv:
+            LK.qgemv(w, *q8, b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:], ldo=b.qkv.stride(0), **G)
+            off += w.n
+
     def _step_fused_norm(self, b: StepBuffers, span: int, fused: bool, cnt) -> None:
         """The decode step with the norms fused into the residual GEMVs: per layer q|k|v,
         attention (+ combine), o_proj (h -> h2, + ffn_norm Q8), gate|up (-> Q8), ffn_down (h2 -> h,
@@ -340,11 +364,7 @@ class Engine:
         layers = self.w.layers
         LK.rmsnorm_q8(b.h, layers[0].attn_norm, c.eps, *qd)
         for i, L in enumerate(layers):
-            off = 0
-            for w in L.wqkv:
-                LK.qgemv(w, *qd, b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:], ldo=b.qkv.stride(0),
-                         **G)
-                off += w.n
+            self._qkv(b, L, qd)
             if fused:
                 LK.attn_decode(None, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
                                c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,

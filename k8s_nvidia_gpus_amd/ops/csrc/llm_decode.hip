@@ -439,16 +439,17 @@ __device__ __forceinline__ void resid_norm_tail(const GemvArgs& a, float* red) {
 // REGX (a whole row is one stage, nb <= 8U): each lane touches the same <= U super-block columns
 // in every row, so its activations are read from LDS once into registers and every row after
 // that is pure weight streaming + VALU (no per-row LDS traffic).
+// bid = the workgroup's index within this matrix's grid.
 template <int TYPE, int T, int MODE, int U, bool REGX>
-__global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
+__device__ __forceinline__ void qgemv_body(const GemvArgs& a, const int bid) {
   extern __shared__ __align__(16) uint8_t lds[];
   const int K = a.K, nb = K >> 8;
   const int W = blockDim.x >> 6;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int sub = lane & 7, bl = lane >> 3;
   const int nst = (nb + 8 * U - 1) / (8 * U);       // pipeline stages per row
-  const int r0 = blockIdx.x * a.rows_per_wg + wave;
-  const int r1 = min(a.N, blockIdx.x * a.rows_per_wg + a.rows_per_wg);
+  const int r0 = bid * a.rows_per_wg + wave;
+  const int r1 = min(a.N, bid * a.rows_per_wg + a.rows_per_wg);
   const int nrows = r0 < r1 ? (r1 - r0 + W - 1) / W : 0;
   const int items = nrows * nst;
 
@@ -599,7 +600,7 @@ __global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
   for (int t = 0; t < T; ++t) acc[t] = acc1[t] = 0.f;
   // pair → Q8: the workgroup's 32 outputs per token collect in LDS (after the [W][T] scratch)
   float* q8s = (MODE == kPair && a.ox8) ? red + W * T : nullptr;
-  const int wrow0 = blockIdx.x * a.rows_per_wg;
+  const int wrow0 = bid * a.rows_per_wg;
   if constexpr (REGX) {
     XReg xr[U][T];
 #pragma unroll
@@ -659,6 +660,20 @@ __global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
   if constexpr (MODE == kResid) {
     if (a.cnt) resid_norm_tail<T>(a, red);
   }
+}
+
+template <int TYPE, int T, int MODE, int U, bool REGX>
+__global__ void __launch_bounds__(512) qgemv_kernel(GemvArgs a) {
+  qgemv_body<TYPE, T, MODE, U, REGX>(a, blockIdx.x);
+}
+
+// Two matrices of different quantisation types that read the same input, in ONE launch (store
+// mode): Q4_K_M keeps attn_q|attn_k in Q4_K and attn_v in Q6_K in about half the layers, which
+// would otherwise cost the short v GEMV a launch of its own.  Workgroups [0, grid0) run a0.
+template <int TYPE0, int TYPE1, int T, int U, bool REGX>
+__global__ void __launch_bounds__(512) qgemv2_kernel(GemvArgs a0, GemvArgs a1, int grid0) {
+  if ((int)blockIdx.x < grid0) qgemv_body<TYPE0, T, kStore, U, REGX>(a0, blockIdx.x);
+  else qgemv_body<TYPE1, T, kStore, U, REGX>(a1, blockIdx.x - grid0);
 }
 
 // ---------------------------------------------------------------- RMSNorm + Q8 activation quant
@@ -862,14 +877,16 @@ __device__ __forceinline__ void combine_heads(const float* __restrict__ po,
       for (int u = 0; u < 8; ++u)
         if (s0 + u < ns) mn = fmaxf(mn, mx[k][u]);
       if (mn == -INFINITY) continue;                 // nothing attended yet
-      const float sc = m[k] == -INFINITY ? 0.f : __expf(m[k] - mn);
-      den[k] *= sc;
-      v[k] *= sc;
+      // explicit roundings (no fp-contract choice left to the compiler): the same bits for any NH
+      const float sc = m[k] == -INFINITY ? 0.f : __expf(__fsub_rn(m[k], mn));
+      den[k] = __fmul_rn(den[k], sc);
+      v[k] = __fmul_rn(v[k], sc);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const float wgt = (s0 + u < ns && mx[k][u] != -INFINITY) ? __expf(mx[k][u] - mn) : 0.f;
-        den[k] += wgt * l[k][u];
-        v[k] += wgt * ov[k][u];
+        const float wgt =
+            (s0 + u < ns && mx[k][u] != -INFINITY) ? __expf(__fsub_rn(mx[k][u], mn)) : 0.f;
+        den[k] = __fmaf_rn(wgt, l[k][u], den[k]);
+        v[k] = __fmaf_rn(wgt, ov[k][u], v[k]);
       }
       m[k] = mn;
     }
@@ -879,7 +896,7 @@ __device__ __forceinline__ void combine_heads(const float* __restrict__ po,
   for (int k = 0; k < NH; ++k) {
     const int h = h0 + k * hstep;
     if (h >= hend) break;                            // uniform per wave (hstep multiple of waves)
-    const float y = den[k] > 0.f ? v[k] / den[k] : 0.f;
+    const float y = den[k] > 0.f ? __fdiv_rn(v[k], den[k]) : 0.f;
     const int col = h * kHeadDim + dd;
     if (out) out[(long)t * K + col] = y;
     float amax = fabsf(y);
@@ -1259,6 +1276,38 @@ int dispatch_t(const GemvArgs& a, int waves, hipStream_t st) {
   }
 }
 
+// Two matrices in one launch (qgemv2_kernel): rows of one pipeline stage only (nb <= 16, the
+// q|k|v shapes), with the stage width each type takes alone; 4 = not supported here (the caller
+// launches the two matrices separately).
+template <int TYPE0, int TYPE1, int T>
+int launch_gemv2(const GemvArgs& a0, const GemvArgs& a1, int waves, hipStream_t st) {
+  const int nb = a0.K >> 8;
+  const size_t lds = (size_t)T * (nb * 288 + (a0.K >> 5) * 4 + (a0.K >> 4) * 4) + 16 * T * 4;
+  const int g0 = (a0.N + a0.rows_per_wg - 1) / a0.rows_per_wg;
+  const int g1 = (a1.N + a1.rows_per_wg - 1) / a1.rows_per_wg;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(g0 + g1), dim3(waves * 64), lds, st, a0, a1, g0);
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+  };
+  if (nb <= 8) return go(qgemv2_kernel<TYPE0, TYPE1, T, 1, true>);
+  if (nb <= 16) {
+    if (T <= 2 || T <= regx_max_t()) return go(qgemv2_kernel<TYPE0, TYPE1, T, 2, true>);
+    return go(qgemv2_kernel<TYPE0, TYPE1, T, 2, false>);
+  }
+  return 4;
+}
+
+template <int TYPE0, int TYPE1>
+int dispatch2_t(const GemvArgs& a0, const GemvArgs& a1, int waves, hipStream_t st) {
+  switch (a0.T) {
+    case 1: return launch_gemv2<TYPE0, TYPE1, 1>(a0, a1, waves, st);
+    case 2: return launch_gemv2<TYPE0, TYPE1, 2>(a0, a1, waves, st);
+    case 3: return launch_gemv2<TYPE0, TYPE1, 3>(a0, a1, waves, st);
+    case 4: return launch_gemv2<TYPE0, TYPE1, 4>(a0, a1, waves, st);
+    default: return 2;
+  }
+}
+
 // Default decomposition (measured on MI355X, tools/llm_bench.py --gemv, T = 1): 4-wave
 // workgroups of 8 rows for the 3584/4608/18944-row matrices, 8 waves for the 18944-long rows of
 // ffn_down, and 32 rows per workgroup for the 152064-row lm_head (longer per-wave pipelines).
@@ -1358,6 +1407,43 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
     if (mode == kPair) return dispatch_t<kQ6K, kPair>(a, waves, st);
   }
   return 2;
+}
+
+// Two store-mode GEMVs over the same Q8 input in one launch: out_i[t][n] = W_i.x + bias_i (the
+// q|k and v projections when their quantisation types differ).  Returns 4 when the shape is not
+// covered (K > 4096): launch the two with amdk8s_llm_qgemv instead.
+int amdk8s_llm_qgemv2(int type0, const void* w0q, const void* w0qh, const void* w0sc,
+                      const void* w0d, int N0, const void* bias0, void* out0, int type1,
+                      const void* w1q, const void* w1qh, const void* w1sc, const void* w1d, int N1,
+                      const void* bias1, void* out1, int ldo, const void* x8, const void* dx,
+                      const void* sx, int K, int T, int waves, int rows_per_wg, void* stream) {
+  if (K % 256 || N0 <= 0 || N1 <= 0 || T < 1 || T > kMaxTok || !x8 || !dx || !sx) return 2;
+  if ((type0 != kQ4K && type0 != kQ6K) || (type1 != kQ4K && type1 != kQ6K)) return 2;
+  int rows = rows_per_wg;
+  gemv_shape(N0 + N1, K, waves, rows);
+  if (waves < 1 || waves > 8 || rows < 1) return 2;
+  GemvArgs a[2];
+  const int N[2] = {N0, N1};
+  const void* q[2][4] = {{w0q, w0qh, w0sc, w0d}, {w1q, w1qh, w1sc, w1d}};
+  const void* bias[2] = {bias0, bias1};
+  void* out[2] = {out0, out1};
+  for (int i = 0; i < 2; ++i) {
+    GemvArgs& g = a[i];
+    g = GemvArgs{};
+    g.w0 = {static_cast<const uint8_t*>(q[i][0]), static_cast<const uint8_t*>(q[i][1]),
+            static_cast<const int8_t*>(q[i][2]), static_cast<const uint16_t*>(q[i][3])};
+    g.x8 = static_cast<const int8_t*>(x8);
+    g.dx = static_cast<const float*>(dx);
+    g.sx = static_cast<const float*>(sx);
+    g.bias = static_cast<const float*>(bias[i]);
+    g.out = static_cast<float*>(out[i]);
+    g.ldo = ldo; g.N = N[i]; g.K = K; g.T = T; g.rows_per_wg = rows;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (type0 == kQ4K && type1 == kQ6K) return dispatch2_t<kQ4K, kQ6K>(a[0], a[1], waves, st);
+  if (type0 == kQ6K && type1 == kQ4K) return dispatch2_t<kQ6K, kQ4K>(a[0], a[1], waves, st);
+  if (type0 == kQ4K) return dispatch2_t<kQ4K, kQ4K>(a[0], a[1], waves, st);
+  return dispatch2_t<kQ6K, kQ6K>(a[0], a[1], waves, st);
 }
 
 int amdk8s_llm_rmsnorm_q8(const void* x, const void* w, float eps, int K, int T, void* x8,

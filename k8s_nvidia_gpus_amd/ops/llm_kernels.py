@@ -32,6 +32,9 @@ def _lib():
                 + [vp, ci, vp, cf] + [vp, vp] + [ci, ci, ci, ci, ci, ci] + [vp, vp, vp] \
                 + [vp, vp, vp] + [vp]
             lib.amdk8s_llm_qgemv.restype = ci
+            lib.amdk8s_llm_qgemv2.argtypes = [ci] + [vp] * 4 + [ci, vp, vp] + [ci] + [vp] * 4 \
+                + [ci, vp, vp] + [ci, vp, vp, vp, ci, ci, ci, ci, vp]
+            lib.amdk8s_llm_qgemv2.restype = ci
             lib.amdk8s_llm_rmsnorm_q8.argtypes = [vp, vp, cf, ci, ci, vp, vp, vp, vp]
             lib.amdk8s_llm_rmsnorm_q8.restype = ci
             lib.amdk8s_llm_rope_kv.argtypes = [vp, ci, vp, vp, vp, vp, ci, ci, ci, ci, vp, vp, vp,
@@ -96,6 +99,24 @@ def qgemv(w0, x8, dx, sx, out, mode: int = STORE, w1=None, bias=None, ldo: int =
                                    _p(bias), out.data_ptr(), ldo, w0.n, w0.k, t,
                                    waves, rows_per_wg, *((_p(t) for t in q8_out) if q8_out else (None,) * 3),
                                    _p(res), _p(norm_out), _p(cnt), _stream(ref)), "amdk8s_llm_qgemv")
+
+
+def qgemv2(w0, w1, x8, dx, sx, out0, out1, bias0=None, bias1=None, rows_per_wg: int = 0,
+           waves: int = 0) -> bool:
+    """Two store-mode GEMVs over the same Q8 input [T, K] in ONE launch (``out_i = W_i.x +
+    bias_i``; ``out0``/``out1`` views with the same row stride) — q|k and v when their
+    quantisation types differ.  Returns False when the shape is not covered (K > 4096): the
+    caller launches them with :func:`qgemv`."""
+    if out0.stride(0) != out1.stride(0) or w0.k != w1.k:
+        raise ValueError("qgemv2: both outputs need one row stride and both matrices one K")
+    rc = _lib().amdk8s_llm_qgemv2(w0.qtype, *w0.ptrs(), w0.n, _p(bias0), out0.data_ptr(),
+                                  w1.qtype, *w1.ptrs(), w1.n, _p(bias1), out1.data_ptr(),
+                                  out0.stride(0), x8.data_ptr(), dx.data_ptr(), sx.data_ptr(),
+                                  w0.k, x8.shape[0], waves, rows_per_wg, _stream(x8))
+    if rc == 4:
+        return False
+    _check(rc, "amdk8s_llm_qgemv2")
+    return True
 
 
 def rmsnorm_q8(x, w, eps: float, x8, dx, sx) -> None:

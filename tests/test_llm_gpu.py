@@ -360,6 +360,28 @@ def test_resid_gemv_fused_norm_tail(dev, LK, qt, T):
         torch.testing.assert_close(osx, sums, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("types", [("Q4_K", "Q6_K"), ("Q6_K", "Q4_K")])
+@pytest.mark.parametrize("T", [1, 2, 3, 4])
+@pytest.mark.parametrize("K", [1536, 3584])
+def test_two_matrix_gemv_equals_two_launches(dev, LK, types, T, K):
+    """q|k (one type) and v (the other) in one launch: bit-identical to the two GEMVs alone, bias
+    included, rows written into one strided [T, N0 + N1] output."""
+    from k8s_nvidia_gpus_amd.models.llm import gguf
+
+    w0, _ = _qw(640, K, getattr(gguf, types[0]), 7, dev)
+    w1, _ = _qw(128, K, getattr(gguf, types[1]), 8, dev)
+    x8, dx, sx, _ = _q8(torch.randn(T, K, device=dev), LK)
+    bias = torch.randn(768, device=dev)
+    ref = torch.zeros(T, 770, device=dev)
+    LK.qgemv(w0, x8, dx, sx, ref[:, :640], LK.STORE, bias=bias[:640], ldo=770)
+    LK.qgemv(w1, x8, dx, sx, ref[:, 640:], LK.STORE, bias=bias[640:], ldo=770)
+    out = torch.full((T, 770), 3.0, device=dev)
+    assert LK.qgemv2(w0, w1, x8, dx, sx, out[:, :640], out[:, 640:768], bias0=bias[:640],
+                     bias1=bias[640:])
+    torch.testing.assert_close(out[:, :768], ref[:, :768], rtol=0, atol=0)
+    assert bool((out[:, 768:] == 3.0).all())
+
+
 @pytest.fixture(scope="module")
 def tiny_gguf(tmp_path_factory):
     from k8s_nvidia_gpus_amd.models.llm import tiny
