@@ -60,6 +60,14 @@ __device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c) {
   return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
 }
 
+// a . b with a zero accumulator as the VOP3P form's inline constant (the builtin always selects
+// v_dot4c with a v_mov of 0 into the accumulator first: 2 extra VALU per 8 dot products)
+__device__ __forceinline__ int dot4z(uint32_t a, uint32_t b) {
+  int r;
+  asm("v_dot4_i32_i8 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
@@ -239,10 +247,10 @@ __device__ __forceinline__ Prep<TYPE> prep_blk(const Blk<TYPE>& r, int sub) {
 
 template <int TYPE>
 __device__ __forceinline__ float dot_apply(const Prep<TYPE>& p, const XReg& x, float acc) {
-  int il = 0, ih = 0;
-  il = dot4(p.ql[0], x.xl.x, il); il = dot4(p.ql[1], x.xl.y, il);
+  int il = dot4z(p.ql[0], x.xl.x), ih = dot4z(p.qh[0], x.xh.x);
+  il = dot4(p.ql[1], x.xl.y, il);
   il = dot4(p.ql[2], x.xl.z, il); il = dot4(p.ql[3], x.xl.w, il);
-  ih = dot4(p.qh[0], x.xh.x, ih); ih = dot4(p.qh[1], x.xh.y, ih);
+  ih = dot4(p.qh[1], x.xh.y, ih);
   ih = dot4(p.qh[2], x.xh.z, ih); ih = dot4(p.qh[3], x.xh.w, ih);
   if constexpr (TYPE == kQ4K) {
     float a = __fmaf_rn(__fmul_rn(p.dsc0, x.dxl), (float)il, acc);
@@ -298,33 +306,126 @@ __device__ __forceinline__ void compute_stage(int b0, int nb, int sub, int bl, c
   }
 }
 
+// Cross-lane sums without the LDS unit (gfx950): v_permlane32_swap / v_permlane16_swap exchange
+// 32- / 16-lane halves between two registers, DPP row_mirror / row_half_mirror / quad_perm pair
+// the remaining lanes.  Every step pairs lanes symmetrically (a + b in one lane, b + a in its
+// partner: the same bits), so after a full reduction every lane of a group holds identical bits.
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppMirror = 0x140, kDppHalfMirror = 0x141;
+
+// lanes < 32: a[l] + a[l + 32];  lanes >= 32: b[l - 32] + b[l]
+__device__ __forceinline__ float swap_sum32(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false,
+                                                   false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// within each 32-lane half: rows of 16 — row 0: a[l] + a[l + 16];  row 1: b[l - 16] + b[l]
+__device__ __forceinline__ float swap_sum16(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false,
+                                                   false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// Sum NV values (1, 2, 4 or 8) over the wave in 6 steps: at each of the first log2(NV) steps a
+// lane keeps half of its values and hands the other half to its partner (lane bit 5, 4, then 3
+// decides which half), then one value finishes.  Every lane of group l / (64 / NV) ends with the
+// full sum of value l / (64 / NV).  Each value is reduced over the same lane pairings in the same
+// order for any NV (bit 5, bit 4, mirror, half mirror, xor 2, xor 1), so its bits do not depend on
+// how many values share the reduction: decode stays batch-invariant.
+template <int NV>
+__device__ __forceinline__ float wave_sum_multi(float (&x)[NV], int lane) {
+  static_assert(NV == 1 || NV == 2 || NV == 4 || NV == 8, "NV must be 1, 2, 4 or 8");
+  if constexpr (NV >= 2) {
+#pragma unroll
+    for (int i = 0; i < NV / 2; ++i) x[i] = swap_sum32(x[i], x[NV / 2 + i]);
+  } else {
+    x[0] = swap_sum32(x[0], x[0]);
+  }
+  constexpr int C1 = NV >= 2 ? NV / 2 : 1;
+  if constexpr (C1 >= 2) {
+#pragma unroll
+    for (int i = 0; i < C1 / 2; ++i) x[i] = swap_sum16(x[i], x[C1 / 2 + i]);
+  } else {
+    x[0] = swap_sum16(x[0], x[0]);
+  }
+  constexpr int C2 = C1 >= 2 ? C1 / 2 : 1;
+  float v;
+  if constexpr (C2 == 2) {
+    const bool hi = (lane & 8) != 0;                 // the row_mirror partner has the other bit 3
+    const float keep = hi ? x[1] : x[0], give = hi ? x[0] : x[1];
+    v = keep + dppf<kDppMirror>(give);
+  } else {
+    v = x[0] + dppf<kDppMirror>(x[0]);
+  }
+  v = v + dppf<kDppHalfMirror>(v);
+  v = v + dppf<kDppXor2>(v);
+  return v + dppf<kDppXor1>(v);
+}
+
+// Single-value full-wave max / sum without the LDS unit (same pairings as wave_sum_multi<1>).
+__device__ __forceinline__ float wave_max_fast(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  v = fmaxf(v, dppf<kDppMirror>(v));
+  v = fmaxf(v, dppf<kDppHalfMirror>(v));
+  v = fmaxf(v, dppf<kDppXor2>(v));
+  return fmaxf(v, dppf<kDppXor1>(v));
+}
+__device__ __forceinline__ float wave_sum_fast(float v) {
+  float x[1] = {v};
+  return wave_sum_multi<1>(x, 0);
+}
+
 template <int T, int MODE>
 __device__ __forceinline__ void finish_row(const GemvArgs& a, int row, int lane, float (&acc)[T],
                                            float (&acc1)[T], float* q8s = nullptr, int wrow0 = 0) {
+  // values: token t's acc (and, in pair mode, acc1 right after it), padded to a power of two
+  constexpr int NV0 = MODE == kPair ? 2 * T : T;
+  constexpr int NV = NV0 <= 1 ? 1 : NV0 <= 2 ? 2 : NV0 <= 4 ? 4 : 8;
+  constexpr int SP = 64 / NV;                        // lanes holding each value
+  constexpr int PER = MODE == kPair ? 2 : 1;
+  float x[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) x[i] = 0.f;
 #pragma unroll
   for (int t = 0; t < T; ++t) {
-    acc[t] = wave_sum(acc[t]);
-    if constexpr (MODE == kPair) acc1[t] = wave_sum(acc1[t]);
+    x[PER * t] = acc[t];
+    if constexpr (MODE == kPair) x[2 * t + 1] = acc1[t];
   }
-  if (lane < T) {
-    float v = 0.f, v1 = 0.f;
-#pragma unroll
-    for (int t = 0; t < T; ++t)
-      if (t == lane) { v = acc[t]; v1 = acc1[t]; }
-    float* o = a.out + (long)lane * a.ldo + row;
+  const float v = wave_sum_multi<NV>(x, lane);
+  float v1 = 0.f;                                    // pair: acc1 of the same token (next group)
+  if constexpr (MODE == kPair) {
+    if constexpr (SP == 32) {
+      v1 = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v),
+                                                            false, false)[1]);
+    } else if constexpr (SP == 16) {
+      v1 = __uint_as_float(__builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v),
+                                                            false, false)[1]);
+    } else {
+      v1 = dppf<kDppMirror>(v);                      // SP == 8: lane 15 of the row = the next group
+    }
+  }
+  const int t = lane / (SP * PER);
+  if (lane % (SP * PER) == 0 && t < T) {
+    float* o = a.out + (long)t * a.ldo + row;
     if constexpr (MODE == kStore) *o = v + (a.bias ? a.bias[row] : 0.f);
     else if constexpr (MODE == kResid) {
-      if (a.res) st_wt(o, a.res[(long)lane * a.ldo + row] + v);   // fused-norm form
+      if (a.res) st_wt(o, a.res[(long)t * a.ldo + row] + v);      // fused-norm form
       else *o += v;
     }
     else {
       const float y = v / (1.f + __expf(-v)) * v1;
-      if (q8s) q8s[lane * 32 + (row - wrow0)] = y;   // quantised at the end of the workgroup
+      if (q8s) q8s[t * 32 + (row - wrow0)] = y;      // quantised at the end of the workgroup
       else *o = y;
     }
   }
 #pragma unroll
-  for (int t = 0; t < T; ++t) acc[t] = acc1[t] = 0.f;
+  for (int i = 0; i < T; ++i) acc[i] = acc1[i] = 0.f;
 }
 
 // Workgroup = W waves (blockDim/64) over rows_per_wg rows; wave w takes rows w, w+W, ...  Each
@@ -461,14 +562,33 @@ __device__ __forceinline__ void qgemv_body(const GemvArgs& a, const int bid) {
   float* dxs = reinterpret_cast<float*>(lds + T * xstride);
   float* sxs = dxs + T * (K >> 5);
   float* red = sxs + T * (K >> 4);                   // [W][T] block-reduction scratch
-  if (a.xf == nullptr) {                             // Q8 input: copy into LDS
-    for (int i = threadIdx.x; i < T * (K >> 4); i += blockDim.x) {
-      const int t = i / (K >> 4), p = (i - t * (K >> 4)) << 4;
-      *reinterpret_cast<uint4*>(xs + t * xstride + xoff(p)) =
-          *reinterpret_cast<const uint4*>(a.x8 + (long)t * K + p);
+  if (a.xf == nullptr) {
+    // Q8 input: copy into LDS.  x8 [T][K], dx [T][K/32] and sx [T][K/16] are read as flat arrays
+    // (index i = one 16-byte x8 unit = one sx value; dx for i < T*K/32), four units per thread
+    // per round with every load of the round issued before any LDS store (clamped indices, no
+    // load under a branch): one L2 round trip per round instead of one per loop iteration.
+    const int nx = T * (K >> 4), nd = T * (K >> 5);
+    for (int i0 = threadIdx.x; i0 < nx; i0 += 4 * (int)blockDim.x) {
+      uint4 xv[4];
+      float dv[4], sv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = min(i0 + u * (int)blockDim.x, nx - 1);
+        xv[u] = *reinterpret_cast<const uint4*>(a.x8 + (long)i * 16);
+        sv[u] = a.sx[i];
+        dv[u] = a.dx[min(i, nd - 1)];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * (int)blockDim.x;
+        if (i < nx) {
+          const int t = i / (K >> 4), p = (i - t * (K >> 4)) << 4;
+          *reinterpret_cast<uint4*>(xs + t * xstride + xoff(p)) = xv[u];
+          sxs[i] = sv[u];
+          if (i < nd) dxs[i] = dv[u];
+        }
+      }
     }
-    for (int i = threadIdx.x; i < T * (K >> 5); i += blockDim.x) dxs[i] = a.dx[i];
-    for (int i = threadIdx.x; i < T * (K >> 4); i += blockDim.x) sxs[i] = a.sx[i];
   } else {
     // fp32 input (+ RMSNorm): every workgroup normalises and quantises the (L2-resident) rows
     // itself, which removes a launch and its boundary per matrix.  All T tokens are processed
@@ -689,11 +809,13 @@ __global__ void __launch_bounds__(256) rmsnorm_q8_kernel(const float* __restrict
   const int t = blockIdx.y;
   const float* xr = x + (long)t * K;
   const int i0 = blockIdx.x * 2048 + threadIdx.x * 8;
-  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-  if (i0 < K) {
-    a = *reinterpret_cast<const float4*>(xr + i0);
-    b = *reinterpret_cast<const float4*>(xr + i0 + 4);
-  }
+  // unconditional (clamped) loads: in flight together with the sum-of-squares loads below
+  const int ic = min(i0, K - 8);
+  const float4 a = *reinterpret_cast<const float4*>(xr + ic);
+  const float4 b = *reinterpret_cast<const float4*>(xr + ic + 4);
+  const float* wp = w ? w : xr;              // the norm weight loads are issued up front too
+  const float4 wa = *reinterpret_cast<const float4*>(wp + ic);
+  const float4 wb = *reinterpret_cast<const float4*>(wp + ic + 4);
   float rs = 1.f;
   if (w) {
     float ss = 0.f;
@@ -707,7 +829,7 @@ __global__ void __launch_bounds__(256) rmsnorm_q8_kernel(const float* __restrict
         if (i0 + u * (int)blockDim.x * 4 < K)
           ss += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
     }
-    ss = wave_sum(ss);
+    ss = wave_sum_fast(ss);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
     __syncthreads();
     ss = red[0] + red[1] + red[2] + red[3];
@@ -716,8 +838,6 @@ __global__ void __launch_bounds__(256) rmsnorm_q8_kernel(const float* __restrict
   if (i0 >= K) return;                       // K % 256 == 0: whole quads leave together
   float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
   if (w) {
-    const float4 wa = *reinterpret_cast<const float4*>(w + i0);
-    const float4 wb = *reinterpret_cast<const float4*>(w + i0 + 4);
     const float ww[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] *= rs * ww[i];
@@ -725,8 +845,8 @@ __global__ void __launch_bounds__(256) rmsnorm_q8_kernel(const float* __restrict
   float amax = 0.f;
 #pragma unroll
   for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
-  amax = fmaxf(amax, __shfl_xor(amax, 1, kWave));
-  amax = fmaxf(amax, __shfl_xor(amax, 2, kWave));
+  amax = fmaxf(amax, dppf<kDppXor1>(amax));
+  amax = fmaxf(amax, dppf<kDppXor2>(amax));
   const float d = amax / 127.f;
   const float id = d > 0.f ? 1.f / d : 0.f;
   uint32_t pk[2] = {0u, 0u};
@@ -737,7 +857,7 @@ __global__ void __launch_bounds__(256) rmsnorm_q8_kernel(const float* __restrict
     pk[i >> 2] |= ((uint32_t)(q & 0xff)) << (8 * (i & 3));
     s += q;
   }
-  s += __shfl_xor(s, 1, kWave);              // 16-value sums: lanes (0,1) and (2,3) of the quad
+  s += __float_as_int(dppf<kDppXor1>(__int_as_float(s)));   // 16-value sums: lanes (0,1), (2,3)
   *reinterpret_cast<uint2*>(x8 + (long)t * K + i0) = make_uint2(pk[0], pk[1]);
   const int q4 = threadIdx.x & 3;
   if (q4 == 0) dx[(long)t * (K >> 5) + (i0 >> 5)] = d;
@@ -953,8 +1073,9 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   };
   if (p0 >= len) {
     if (threadIdx.x < G) {
-      st_wt(pml + (pidx + (long)threadIdx.x * nsplit) * 2, -INFINITY);
-      st_wt(pml + (pidx + (long)threadIdx.x * nsplit) * 2 + 1, 0.f);
+      float* dst = pml + (pidx + (long)threadIdx.x * nsplit) * 2;
+      if (a.cnt) { st_wt(dst, -INFINITY); st_wt(dst + 1, 0.f); }
+      else { dst[0] = -INFINITY; dst[1] = 0.f; }
     }
     merge();
     return;
@@ -990,31 +1111,45 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
     const float* row = a.qkv + (long)t * a.ldq;
     const float* ct = a.cos_t + (long)pnew * (kHeadDim / 2);
     const float* st = a.sin_t + (long)pnew * (kHeadDim / 2);
-    for (int i = threadIdx.x; i < G * (kHeadDim / 2); i += blockDim.x) {
+    // every load of the q rotation and of the new k / v row in flight at once (indices clamped,
+    // no load under a branch), then the maths and the stores
+    constexpr int QR = (G * (kHeadDim / 2) + 255) / 256;   // rotation pairs per thread
+    float qx0[QR], qx1[QR], qc[QR], qsn[QR];
+#pragma unroll
+    for (int u = 0; u < QR; ++u) {
+      const int i = min((int)threadIdx.x + 256 * u, G * (kHeadDim / 2) - 1);
       const int g = i / (kHeadDim / 2), j = i % (kHeadDim / 2);
-      const float x0 = row[(kh * G + g) * kHeadDim + j];
-      const float x1 = row[(kh * G + g) * kHeadDim + j + kHeadDim / 2];
-      const float c = ct[j], sn = st[j];
-      qs[g][j] = (x0 * c - x1 * sn) * scale;
-      qs[g][j + kHeadDim / 2] = (x0 * sn + x1 * c) * scale;
+      qx0[u] = row[(kh * G + g) * kHeadDim + j];
+      qx1[u] = row[(kh * G + g) * kHeadDim + j + kHeadDim / 2];
+      qc[u] = ct[j];
+      qsn[u] = st[j];
+    }
+    const int jk = threadIdx.x & (kHeadDim / 2 - 1), ev = threadIdx.x & (kHeadDim - 1);
+    const float k0 = row[(H + kh) * kHeadDim + jk], k1 = row[(H + kh) * kHeadDim + jk + kHeadDim / 2];
+    const float vn = row[(H + Hkv + kh) * kHeadDim + ev];
+#pragma unroll
+    for (int u = 0; u < QR; ++u) {
+      const int i = (int)threadIdx.x + 256 * u;
+      if (i < G * (kHeadDim / 2)) {
+        const int g = i / (kHeadDim / 2), j = i % (kHeadDim / 2);
+        qs[g][j] = (qx0[u] * qc[u] - qx1[u] * qsn[u]) * scale;
+        qs[g][j + kHeadDim / 2] = (qx0[u] * qsn[u] + qx1[u] * qc[u]) * scale;
+      }
     }
     if (own) {
       const long cpos = cbase + (long)pnew * kHeadDim;
       if (threadIdx.x < kHeadDim / 2) {
-        const int j = threadIdx.x;
-        const float x0 = row[(H + kh) * kHeadDim + j];
-        const float x1 = row[(H + kh) * kHeadDim + j + kHeadDim / 2];
-        const float c = ct[j], sn = st[j];
-        const uint16_t h0 = f2h(x0 * c - x1 * sn), h1 = f2h(x0 * sn + x1 * c);
-        a.kc[cpos + j] = h0;
-        a.kc[cpos + j + kHeadDim / 2] = h1;
-        knew[j] = h0;
-        knew[j + kHeadDim / 2] = h1;
-      } else if (threadIdx.x < kHeadDim / 2 + kHeadDim) {
-        const int e = threadIdx.x - kHeadDim / 2;
-        const uint16_t hv = f2h(row[(H + Hkv + kh) * kHeadDim + e]);
-        a.vc[cpos + e] = hv;
-        vnew[e] = hv;
+        const float c = qc[0], sn = qsn[0];          // thread j < 64 loaded ct[j] / st[j] at u = 0
+        const uint16_t h0 = f2h(k0 * c - k1 * sn), h1 = f2h(k0 * sn + k1 * c);
+        a.kc[cpos + jk] = h0;
+        a.kc[cpos + jk + kHeadDim / 2] = h1;
+        knew[jk] = h0;
+        knew[jk + kHeadDim / 2] = h1;
+      }
+      if (threadIdx.x < kHeadDim) {
+        const uint16_t hv = f2h(vn);
+        a.vc[cpos + ev] = hv;
+        vnew[ev] = hv;
       }
     }
   } else {
@@ -1063,14 +1198,16 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
       ps[g][pi] = pi < n ? sc[g] : -INFINITY;
   }
   __syncthreads();
-  if (wave == 0) {
+  // softmax: head g on wave g % 4 (lane = position), LDS-free cross-lane max / sum
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
+  for (int g0 = 0; g0 < G; g0 += 4) {
+    const int g = g0 + wave;
+    if (g < G) {
       const float s = ps[g][lane];
-      const float m = wave_max(s);
+      const float m = wave_max_fast(s);
       const float p = lane < n ? __expf(s - m) : 0.f;
       ps[g][lane] = p;
-      const float l = wave_sum(p);
+      const float l = wave_sum_fast(p);
       if (lane == 0) { mls[g][0] = m; mls[g][1] = l; }
     }
   }
@@ -1098,12 +1235,15 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   for (int i = threadIdx.x; i < G * kHeadDim; i += blockDim.x) {
     const int g = i / kHeadDim, dd = i % kHeadDim;
     const float v = opart[0][g][dd] + opart[1][g][dd] + opart[2][g][dd] + opart[3][g][dd];
-    st_wt(po + (pidx + (long)g * nsplit) * kHeadDim + dd, v);
+    float* dst = po + (pidx + (long)g * nsplit) * kHeadDim + dd;
+    if (a.cnt) st_wt(dst, v);                        // read back inside this launch
+    else *dst = v;
   }
   if (threadIdx.x < G) {
     const int g = threadIdx.x;
-    st_wt(pml + (pidx + (long)g * nsplit) * 2, mls[g][0]);
-    st_wt(pml + (pidx + (long)g * nsplit) * 2 + 1, mls[g][1]);
+    float* dst = pml + (pidx + (long)g * nsplit) * 2;
+    if (a.cnt) { st_wt(dst, mls[g][0]); st_wt(dst + 1, mls[g][1]); }
+    else { dst[0] = mls[g][0]; dst[1] = mls[g][1]; }
   }
   merge();
 }

@@ -42,15 +42,20 @@ def heartbeat(period=30.0):
     threading.Thread(target=run, daemon=True).start()
 
 
-def bench_gemv(eng: Engine, iters: int = 50) -> list:
+GEMV_CASES = ("qkv", "o_proj", "gate_up", "down_q4k", "down_q6k", "lm_head")
+
+
+def bench_gemv(eng: Engine, iters: int = 50, sweep4: bool = False) -> list:
     """Achieved bandwidth of every decode GEMV shape, default decomposition and a sweep."""
     LK = eng.LK
     L = eng.w.layers[0]
-    Lq6 = eng.w.layers[1] if len(eng.w.layers) > 1 else L     # layer 1: Q6_K attn_v / ffn_down
+    Lq4 = next((x for x in eng.w.layers if x.wd.qtype == 0), L)   # a Q4_K ffn_down layer
+    Lq6 = next((x for x in eng.w.layers if x.wd.qtype == 1), L)   # a Q6_K ffn_down layer
     rows = []
     cases = [("qkv", L.wqkv[0], "store"), ("o_proj", L.wo, "resid"),
-             ("gate_up", L.wg, "pair"), ("down_q4k", L.wd, "resid"),
+             ("gate_up", L.wg, "pair"), ("down_q4k", Lq4.wd, "resid"),
              ("down_q6k", Lq6.wd, "resid"), ("lm_head", eng.w.output, "store")]
+    cases = [(n, w, m) for n, w, m in cases if n in GEMV_CASES]
     cfgs = [(0, 0), (4, 4), (4, 16), (4, 32), (8, 8), (8, 16), (8, 32), (2, 4), (2, 8),
             (1, 2), (1, 4)]
     for name, w, mode in cases:
@@ -60,7 +65,7 @@ def bench_gemv(eng: Engine, iters: int = 50) -> list:
             sx = torch.zeros(T, w.k // 16, device=eng.device)
             out = torch.zeros(T, w.n, device=eng.device)
             m = {"store": LK.STORE, "resid": LK.RESID, "pair": LK.PAIR}[mode]
-            for waves, rpw in (cfgs if T == 1 else cfgs[:1]):
+            for waves, rpw in (cfgs if T == 1 or sweep4 else cfgs[:1]):
                 kw = dict(w1=L.wu if mode == "pair" else None, waves=waves, rows_per_wg=rpw)
                 for _ in range(3):
                     LK.qgemv(w, x8, dx, sx, out, m, **kw)
@@ -131,6 +136,7 @@ def main(argv=None) -> int:
     ap.add_argument("--prompt", type=int, default=512)
     ap.add_argument("--tokens", default="1,2,3,4")
     ap.add_argument("--gemv", action="store_true")
+    ap.add_argument("--gemv-sweep4", action="store_true", help="also sweep the decomposition at T=4")
     ap.add_argument("--kernels", action="store_true", help="time the non-GEMV decode kernels")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
@@ -185,7 +191,7 @@ def main(argv=None) -> int:
         res["decode"].append(row)
         print(f"decode T={T}: {row}", file=sys.stderr, flush=True)
     if args.gemv:
-        res["gemv"] = bench_gemv(eng)
+        res["gemv"] = bench_gemv(eng, sweep4=args.gemv_sweep4)
         for r in res["gemv"]:
             print(r, file=sys.stderr, flush=True)
     if args.kernels:
