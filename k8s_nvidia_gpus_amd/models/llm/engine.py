@@ -134,6 +134,10 @@ class Engine:
         # q|k (Q4_K) and v (Q6_K in about half the Q4_K_M layers) in one two-matrix launch:
         # T=1 2.00 -> 1.94 ms, T=4 3.36 -> 3.27 ms (profiles/r03/w)
         self.qkv2 = os.environ.get("AMDK8S_LLM_QKV2", "1") != "0"
+        # attn_norm / ffn_norm inside the q|k|v and gate|up GEMV prologues (each workgroup
+        # normalises the L2-resident fp32 row itself) instead of two rmsnorm_q8 launches per
+        # layer; the gate|up -> Q8 hand-off to ffn_down and the final norm stay as they are
+        self.norm_prologue = os.environ.get("AMDK8S_LLM_NORM_PROLOGUE", "0") != "0"
         self._norm_cnt = None
         self._attn_cnt = None
         self._side = None
@@ -276,9 +280,11 @@ class Engine:
                                              device=self.device)
             cnt = self._attn_cnt
 
-        def act(xf, norm_w, k):
+        def act(xf, norm_w, k, prologue=False):
             """GEMV input: ((x8, dx, sx), {}) quantised here, or ((None,) * 3, fused-prologue
             kwargs)."""
+            if prologue or b.T < self.q8_split_T:
+                return (None, None, None), dict(xf=xf, norm_w=norm_w, eps=c.eps)
             if b.T >= self.q8_split_T:
                 q = self._q8(b, k)
                 LK.rmsnorm_q8(xf, norm_w, c.eps, *q)
@@ -301,9 +307,9 @@ class Engine:
                 self.LK.prefetch(planes, self.prefetch_wgs, self._side)
             # RMSNorm + Q8 quantisation: in each GEMV's prologue (fp32 input + norm weight), or once
             # per input for larger T (act())
-            xin = act(b.h, L.attn_norm, c.dim)
-            if xin[0][0] is not None:
-                self._qkv(b, L, xin[0])
+            xin = act(b.h, L.attn_norm, c.dim, self.norm_prologue)
+            if xin[0][0] is not None or self.norm_prologue:
+                self._qkv(b, L, xin[0], xin[1])
             else:
                 off = 0
                 for w in L.wqkv:
@@ -321,7 +327,7 @@ class Engine:
                                c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
                                span=span, cnt=cnt)
             LK.qgemv(L.wo, *qd, b.h, LK.RESID, **G)
-            xin = act(b.h, L.ffn_norm, c.dim)
+            xin = act(b.h, L.ffn_norm, c.dim, self.norm_prologue)
             if self.pair_q8 and b.T >= self.q8_split_T and c.ffn % 32 == 0:
                 qf = (b.x8f, b.dxf, b.sxf)
                 LK.qgemv(L.wg, *xin[0], b.t, LK.PAIR, w1=L.wu, **xin[1], **G, q8_out=qf)
@@ -335,18 +341,21 @@ class Engine:
         if pf:
             main.wait_stream(self._side)   # join (graph capture needs every fork joined)
 
-    def _qkv(self, b: StepBuffers, L, q8) -> None:
-        """q|k|v projections from the Q8 input: one launch, also when q|k and v are stored in
-        different quantisation types (two-matrix GEMV; AMDK8S_LLM_QKV2=0 launches them apart)."""
+    def _qkv(self, b: StepBuffers, L, q8, pro=None) -> None:
+        """q|k|v projections from the Q8 input (or, with ``pro``, from fp32 rows normalised in the
+        GEMV prologue): one launch, also when q|k and v are stored in different quantisation
+        types (two-matrix GEMV; AMDK8S_LLM_QKV2=0 launches them apart)."""
         LK, G = self.LK, self.gemv_cfg
+        pro = pro or {}
         if len(L.wqkv) == 2 and self.qkv2:
             w0, w1 = L.wqkv
             if LK.qgemv2(w0, w1, *q8, b.qkv[:, :w0.n], b.qkv[:, w0.n:], bias0=L.bqkv[:w0.n],
-                         bias1=L.bqkv[w0.n:], **G):
+                         bias1=L.bqkv[w0.n:], **pro, **G):
                 return
         off = 0
         for w in L.wqkv:
-            LK.qgemv(w, *q8, b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:], ldo=b.qkv.stride(0), **G)
+            LK.qgemv(w, *q8, b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:], ldo=b.qkv.stride(0),
+                     **pro, **G)
             off += w.n
 
     def _step_fused_norm(self, b: StepBuffers, span: int, fused: bool, cnt) -> None:

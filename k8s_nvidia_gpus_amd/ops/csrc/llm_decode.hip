@@ -31,6 +31,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 namespace {
 
 constexpr int kWave = 64;
@@ -54,6 +56,15 @@ __device__ __forceinline__ uint16_t f2h(float f) {
   uint16_t h;
   __builtin_memcpy(&h, &v, 2);
   return h;
+}
+
+// NeoX RoPE of one pair with explicit roundings: every kernel that rotates (rope_kv, the fused
+// attention kernels) produces the same bits.
+__device__ __forceinline__ float rope_lo(float x0, float x1, float c, float sn) {
+  return __fmaf_rn(x0, c, -__fmul_rn(x1, sn));
+}
+__device__ __forceinline__ float rope_hi(float x0, float x1, float c, float sn) {
+  return __fmaf_rn(x0, sn, __fmul_rn(x1, c));
 }
 
 __device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c) {
@@ -886,7 +897,7 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(const float* __restrict__ 
     const int h = i / (kHeadDim / 2), j = i % (kHeadDim / 2);
     const float x0 = row[h * kHeadDim + j], x1 = row[h * kHeadDim + j + kHeadDim / 2];
     const float c = cos_t[(long)p * (kHeadDim / 2) + j], sn = sin_t[(long)p * (kHeadDim / 2) + j];
-    const float y0 = x0 * c - x1 * sn, y1 = x0 * sn + x1 * c;
+    const float y0 = rope_lo(x0, x1, c, sn), y1 = rope_hi(x0, x1, c, sn);
     if (h < H) {
       q_out[(long)t * H * kHeadDim + h * kHeadDim + j] = y0;
       q_out[(long)t * H * kHeadDim + h * kHeadDim + j + kHeadDim / 2] = y1;
@@ -969,10 +980,10 @@ template <int NH>
 __device__ __forceinline__ void combine_heads(const float* __restrict__ po,
                                               const float* __restrict__ pml,
                                               const int* __restrict__ pos, int H, int nsplit,
-                                              int h0, int hstep, int hend, int t, int dd,
+                                              int chunk, int h0, int hstep, int hend, int t, int dd,
                                               float* __restrict__ out, int8_t* __restrict__ x8,
                                               float* __restrict__ dx, float* __restrict__ sx) {
-  const int ns = min(nsplit, (pos[t] + kAttnChunk) / kAttnChunk);
+  const int ns = min(nsplit, (pos[t] + chunk) / chunk);
   long hb[NH];
 #pragma unroll
   for (int k = 0; k < NH; ++k) hb[k] = ((long)t * H + min(h0 + k * hstep, hend - 1)) * nsplit;
@@ -1037,12 +1048,13 @@ __device__ __forceinline__ void combine_heads(const float* __restrict__ po,
 __global__ void __launch_bounds__(128) attn_combine_q8_kernel(const float* __restrict__ po,
                                                               const float* __restrict__ pml,
                                                               const int* __restrict__ pos, int H,
-                                                              int nsplit, float* __restrict__ out,
+                                                              int nsplit, int chunk,
+                                                              float* __restrict__ out,
                                                               int8_t* __restrict__ x8,
                                                               float* __restrict__ dx,
                                                               float* __restrict__ sx) {
-  combine_heads<1>(po, pml, pos, H, nsplit, blockIdx.x, 1, H, blockIdx.y, threadIdx.x, out, x8,
-                   dx, sx);
+  combine_heads<1>(po, pml, pos, H, nsplit, chunk, blockIdx.x, 1, H, blockIdx.y, threadIdx.x, out,
+                   x8, dx, sx);
 }
 
 template <int G>
@@ -1068,7 +1080,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   const long pidx = ((long)t * H + kh * G) * nsplit + sp;   // + g * nsplit
   auto merge = [&]() {                   // fused combine by the last-arriving workgroup
     if (a.cnt && arrive_last(a.cnt + t * Hkv + kh, nsplit))   // 2 heads per pass, all at once
-      combine_heads<(G + 1) / 2>(po, pml, pos, H, nsplit, kh * G + (threadIdx.x >> 7), 2,
+      combine_heads<(G + 1) / 2>(po, pml, pos, H, nsplit, kAttnChunk, kh * G + (threadIdx.x >> 7), 2,
                                  kh * G + G, t, threadIdx.x & 127, a.out, a.x8, a.dx, a.sx);
   };
   if (p0 >= len) {
@@ -1132,15 +1144,15 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
       const int i = (int)threadIdx.x + 256 * u;
       if (i < G * (kHeadDim / 2)) {
         const int g = i / (kHeadDim / 2), j = i % (kHeadDim / 2);
-        qs[g][j] = (qx0[u] * qc[u] - qx1[u] * qsn[u]) * scale;
-        qs[g][j + kHeadDim / 2] = (qx0[u] * qsn[u] + qx1[u] * qc[u]) * scale;
+        qs[g][j] = rope_lo(qx0[u], qx1[u], qc[u], qsn[u]) * scale;
+        qs[g][j + kHeadDim / 2] = rope_hi(qx0[u], qx1[u], qc[u], qsn[u]) * scale;
       }
     }
     if (own) {
       const long cpos = cbase + (long)pnew * kHeadDim;
       if (threadIdx.x < kHeadDim / 2) {
         const float c = qc[0], sn = qsn[0];          // thread j < 64 loaded ct[j] / st[j] at u = 0
-        const uint16_t h0 = f2h(k0 * c - k1 * sn), h1 = f2h(k0 * sn + k1 * c);
+        const uint16_t h0 = f2h(rope_lo(k0, k1, c, sn)), h1 = f2h(rope_hi(k0, k1, c, sn));
         a.kc[cpos + jk] = h0;
         a.kc[cpos + jk + kHeadDim / 2] = h1;
         knew[jk] = h0;
@@ -1246,6 +1258,290 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
     else { dst[0] = mls[g][0]; dst[1] = mls[g][1]; }
   }
   merge();
+}
+
+// ---------------------------------------------------------------- MFMA decode attention
+// One workgroup per (kv head, token, context split of up to kMChunk positions): 8 waves, each
+// walking 32-position tiles (tiles w, w + 8, ... of the split) with its own online softmax, then a
+// merge of the 8 waves' states in LDS.  Both products run on v_mfma_f32_16x16x32_f16 with the GQA
+// group as the 16-wide dimension (G <= 8 heads, the rest zero):
+//   S^T [32 pos x 16 heads] = K [pos][128] . Q^T — A = K rows straight from the cache (16 B per
+//       lane: row lane % 16, dims 8 (lane / 16) + 32 kk), B = Q^T held in registers;
+//       C: lane holds S^T[4 (lane / 16) + r + 16 pb][head lane % 16] — 8 positions of ONE head,
+//       so the softmax is lane-local but for a max over the 4 lanes of the head (permlane swaps)
+//       and the running sum stays per lane until the end.
+//   O^T [128 dims x 16 heads] += V^T . P^T — B = P^T straight from the S^T accumulators (the
+//       32 k-slots of the MFMA are mapped to positions so that lane (lane / 16 = q) supplies its own
+//       8 values: slot 8q + j <-> position 4q + j (j < 4), 16 + 4q + j - 4 (j >= 4)); A = V^T, read
+//       from the wave's V tile staged in LDS (8 ds_read_u16 per 16-dim block, rows padded).
+// With one split (contexts up to kMChunk) the workgroup writes the normalised output as Q8 (the
+// o_proj input) itself: no partials, no combine launch.  Longer contexts write per-split partials
+// (unnormalised O, natural-log max, sum) for attn_combine_q8_kernel.  Fused RoPE / KV write as in
+// attn_decode_kernel (distinct slots).  Scores use exp2 with log2(e) folded into the q scale.
+constexpr int kMChunk = 1024;
+constexpr int kMTile = 32;
+constexpr int kMWaves = 8;
+constexpr int kVRow = kHeadDim + 8;      // padded V-tile row (halves): lanes of a ds_read_u16 group
+                                         // hit different banks
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4_t mfma16h(const uint4 a, const uint4 b, const f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a),
+                                                __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float max4lanes(float v) {   // max over lanes l, l^16, l^32, l^48
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float sum4lanes(float v) {
+  v = swap_sum32(v, v);
+  return swap_sum16(v, v);
+}
+
+struct MAttnShared {
+  uint16_t qs[16][kHeadDim];                 // q (f16, scaled), heads >= G zero
+  uint16_t ql[16][kHeadDim];                 // q - f16(q): the low part (q ~ fp32 in two MFMAs)
+  uint16_t knew[kHeadDim];
+  uint16_t vnew[kHeadDim];
+  union {
+    uint16_t vt[kMWaves][kMTile][kVRow];     // per-wave V tiles
+    struct {
+      float m[kMWaves][16], l[kMWaves][16];
+      float o[kMWaves][8][kHeadDim];         // [wave][head < 8][dim]
+    } mg;
+  };
+};
+
+template <int G>
+__global__ void __launch_bounds__(512) attn_mfma_kernel(AttnArgs a, int chunk) {
+  __shared__ MAttnShared sh;
+  const int kh = blockIdx.x, sp = blockIdx.y, t = blockIdx.z;
+  const int H = a.H, Hkv = a.Hkv, nsplit = a.nsplit;
+  const int len = a.pos[t] + 1;
+  const int p0 = sp * chunk, p1 = min(p0 + chunk, len);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q4 = lane >> 4, c16 = lane & 15;
+  const long pidx = ((long)t * H + kh * G) * nsplit + sp;    // + g * nsplit
+  if (p0 >= len) {                                           // split past the context
+    if (tid < G) {
+      a.pml[(pidx + (long)tid * nsplit) * 2] = -INFINITY;
+      a.pml[(pidx + (long)tid * nsplit) * 2 + 1] = 0.f;
+    }
+    return;
+  }
+  const long cbase = ((long)a.slot[t] * Hkv + kh) * a.max_ctx * kHeadDim;
+  const float qscale = a.scale * 1.4426950408889634f;        // exp2 domain
+  const int pnew = len - 1;
+  const bool own = a.qkv != nullptr && pnew >= p0 && pnew < p1;
+  // ---- q (rotated here when fused) -> LDS f16; the new K / V row when this split holds it
+  {
+    const int g = tid >> 6, j = tid & 63;                    // 8 heads x 64 rotation pairs
+    float y0 = 0.f, y1 = 0.f;
+    if (a.qkv) {
+      const float* row = a.qkv + (long)t * a.ldq;
+      const float c = a.cos_t[(long)pnew * (kHeadDim / 2) + j];
+      const float sn = a.sin_t[(long)pnew * (kHeadDim / 2) + j];
+      const int gg = min(g, G - 1);
+      const float x0 = row[(kh * G + gg) * kHeadDim + j];
+      const float x1 = row[(kh * G + gg) * kHeadDim + j + kHeadDim / 2];
+      const float k0 = row[(H + kh) * kHeadDim + j], k1 = row[(H + kh) * kHeadDim + j + kHeadDim / 2];
+      const float v0 = row[(H + Hkv + kh) * kHeadDim + j];
+      const float v1 = row[(H + Hkv + kh) * kHeadDim + j + kHeadDim / 2];
+      y0 = rope_lo(x0, x1, c, sn) * qscale;
+      y1 = rope_hi(x0, x1, c, sn) * qscale;
+      if (own && g == 0) {
+        const long cpos = cbase + (long)pnew * kHeadDim;
+        const uint16_t h0 = f2h(rope_lo(k0, k1, c, sn)), h1 = f2h(rope_hi(k0, k1, c, sn));
+        const uint16_t e0 = f2h(v0), e1 = f2h(v1);
+        a.kc[cpos + j] = h0;
+        a.kc[cpos + j + kHeadDim / 2] = h1;
+        a.vc[cpos + j] = e0;
+        a.vc[cpos + j + kHeadDim / 2] = e1;
+        sh.knew[j] = h0;
+        sh.knew[j + kHeadDim / 2] = h1;
+        sh.vnew[j] = e0;
+        sh.vnew[j + kHeadDim / 2] = e1;
+      }
+    } else {
+      const int gg = min(g, G - 1);
+      const float* qr = a.q + (long)t * H * kHeadDim + (kh * G + gg) * kHeadDim;
+      y0 = qr[j] * qscale;
+      y1 = qr[j + kHeadDim / 2] * qscale;
+    }
+    if (g >= G) y0 = y1 = 0.f;
+    const uint16_t h0 = f2h(y0), h1 = f2h(y1);
+    sh.qs[g][j] = h0;
+    sh.qs[g][j + kHeadDim / 2] = h1;
+    sh.ql[g][j] = f2h(y0 - h2f(h0));
+    sh.ql[g][j + kHeadDim / 2] = f2h(y1 - h2f(h1));
+    sh.qs[g + 8][j] = sh.ql[g + 8][j] = 0;                   // heads 8..15: zero
+    sh.qs[g + 8][j + kHeadDim / 2] = sh.ql[g + 8][j + kHeadDim / 2] = 0;
+  }
+  __syncthreads();
+  uint4 qb[4], qlb[4];                                       // B = Q^T: head c16, dims 32kk+8q4
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    qb[kk] = *reinterpret_cast<const uint4*>(&sh.qs[c16][32 * kk + 8 * q4]);
+    qlb[kk] = *reinterpret_cast<const uint4*>(&sh.ql[c16][32 * kk + 8 * q4]);
+  }
+
+  float m = -INFINITY, l = 0.f;
+  f32x4_t o[8];
+#pragma unroll
+  for (int db = 0; db < 8; ++db) o[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  uint16_t (*vt)[kVRow] = sh.vt[wave];
+  const uint16_t* kcp = a.kc + cbase;
+  const uint16_t* vcp = a.vc + cbase;
+  auto load_tile = [&](int tb, uint4 (&kr)[2][4], uint4 (&vr)[8]) {
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb) {
+      const int pp = min(tb + 16 * pb + c16, p1 - 1);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        kr[pb][kk] = *reinterpret_cast<const uint4*>(kcp + (long)pp * kHeadDim + 32 * kk + 8 * q4);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {                            // V tile: row q4 + 4i, 16-B column c16
+      const int pp = min(tb + q4 + 4 * i, p1 - 1);
+      vr[i] = *reinterpret_cast<const uint4*>(vcp + (long)pp * kHeadDim + 8 * c16);
+    }
+  };
+  uint4 kA[2][4], vA[8], kB[2][4], vB[8];
+  const int tstep = kMWaves * kMTile;
+  int tb = p0 + wave * kMTile;
+  if (tb < p1) load_tile(tb, kA, vA);
+  auto tile = [&](int tb, uint4 (&kr)[2][4], uint4 (&vr)[8]) {
+    if (own && pnew >= tb && pnew < tb + kMTile) {           // loaded before it was written
+#pragma unroll
+      for (int pb = 0; pb < 2; ++pb)
+        if (tb + 16 * pb + c16 == pnew) {
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk)
+            kr[pb][kk] = *reinterpret_cast<const uint4*>(&sh.knew[32 * kk + 8 * q4]);
+        }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (tb + q4 + 4 * i == pnew) vr[i] = *reinterpret_cast<const uint4*>(&sh.vnew[8 * c16]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) *reinterpret_cast<uint4*>(&vt[q4 + 4 * i][8 * c16]) = vr[i];
+    f32x4_t st[2];
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb) {
+      st[pb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        st[pb] = mfma16h(kr[pb][kk], qlb[kk], st[pb]);       // low part first (smaller terms)
+        st[pb] = mfma16h(kr[pb][kk], qb[kk], st[pb]);
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (tb + 16 * pb + 4 * q4 + r >= p1) st[pb][r] = -INFINITY;
+        mx = fmaxf(mx, st[pb][r]);
+      }
+    const float mn = fmaxf(m, max4lanes(mx));                // > -inf: every tile has a position
+    const float alpha = exp2f(m - mn);
+    float pr[8];
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pr[4 * pb + r] = exp2f(st[pb][r] - mn);
+    float ps = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ps += pr[i];
+    l = l * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int db = 0; db < 8; ++db) o[db] *= alpha;
+    uint4 pb8;                                               // B = P^T: slots 8q4 + j
+    pb8.x = (uint32_t)f2h(pr[0]) | ((uint32_t)f2h(pr[1]) << 16);
+    pb8.y = (uint32_t)f2h(pr[2]) | ((uint32_t)f2h(pr[3]) << 16);
+    pb8.z = (uint32_t)f2h(pr[4]) | ((uint32_t)f2h(pr[5]) << 16);
+    pb8.w = (uint32_t)f2h(pr[6]) | ((uint32_t)f2h(pr[7]) << 16);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // this wave's V-tile stores landed
+#pragma unroll
+    for (int db = 0; db < 8; ++db) {                         // A = V^T: dim 16db + c16, slot 8q4+j
+      const int dcol = 16 * db + c16;
+      uint16_t h[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) h[j] = vt[(j < 4 ? 4 * q4 + j : 16 + 4 * q4 + j - 4)][dcol];
+      uint4 va;
+      va.x = h[0] | ((uint32_t)h[1] << 16);
+      va.y = h[2] | ((uint32_t)h[3] << 16);
+      va.z = h[4] | ((uint32_t)h[5] << 16);
+      va.w = h[6] | ((uint32_t)h[7] << 16);
+      o[db] = mfma16h(va, pb8, o[db]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // V-tile reads done before reuse
+  };
+  while (tb < p1) {
+    const int tn = tb + tstep;
+    if (tn < p1) load_tile(tn, kB, vB);
+    tile(tb, kA, vA);
+    if (tn >= p1) break;
+    const int tn2 = tn + tstep;
+    if (tn2 < p1) load_tile(tn2, kA, vA);
+    tile(tn, kB, vB);
+    tb = tn2;
+  }
+  // ---- merge the 8 waves: per wave (m, sum, O^T) -> LDS, then one output per (head, dim)
+  l = sum4lanes(l);
+  __syncthreads();                                           // V tiles dead: reuse as merge area
+  if (q4 == 0 && c16 < 16) {
+    sh.mg.m[wave][c16] = m;
+    sh.mg.l[wave][c16] = l;
+  }
+  if (c16 < 8) {
+#pragma unroll
+    for (int db = 0; db < 8; ++db)
+      *reinterpret_cast<float4*>(&sh.mg.o[wave][c16][16 * db + 4 * q4]) =
+          make_float4(o[db][0], o[db][1], o[db][2], o[db][3]);
+  }
+  __syncthreads();
+  const int K = H * kHeadDim;
+  for (int idx = tid; idx < G * kHeadDim; idx += blockDim.x) {   // whole 32-dim groups per wave
+    const int g = idx >> 7, dd = idx & (kHeadDim - 1);
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < kMWaves; ++w) M = fmaxf(M, sh.mg.m[w][g]);
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int w = 0; w < kMWaves; ++w) {
+      const float e = sh.mg.m[w][g] == -INFINITY ? 0.f : exp2f(sh.mg.m[w][g] - M);
+      L += sh.mg.l[w][g] * e;
+      O += sh.mg.o[w][g][dd] * e;
+    }
+    const int h = kh * G + g;
+    if (nsplit > 1) {                                        // partials for the combine kernel
+      a.po[(pidx + (long)g * nsplit) * kHeadDim + dd] = O;
+      if (dd == 0) {
+        a.pml[(pidx + (long)g * nsplit) * 2] = M * 0.6931471805599453f;   // natural-log units
+        a.pml[(pidx + (long)g * nsplit) * 2 + 1] = L;
+      }
+      continue;
+    }
+    const float y = L > 0.f ? O / L : 0.f;
+    const int col = h * kHeadDim + dd;
+    if (a.out) a.out[(long)t * K + col] = y;
+    float amax = fabsf(y);
+#pragma unroll
+    for (int o2 = 16; o2 > 0; o2 >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o2, kWave));
+    const float d = amax / 127.f;
+    const int qv = d > 0.f ? (int)__builtin_rintf(y / d) : 0;
+    a.x8[(long)t * K + col] = (int8_t)qv;
+    int s16 = qv;
+#pragma unroll
+    for (int o2 = 8; o2 > 0; o2 >>= 1) s16 += __shfl_xor(s16, o2, kWave);
+    if ((dd & 31) == 0) a.dx[(long)t * (K >> 5) + (col >> 5)] = d;
+    if ((dd & 15) == 0) a.sx[(long)t * (K >> 4) + (col >> 4)] = d * (float)s16;
+  }
 }
 
 // ---------------------------------------------------------------- dequantisation (rows → fp16/fp32)
@@ -1370,6 +1666,17 @@ static int regx_max_t() {
   return v;
 }
 
+// Decode attention implementation: AMDK8S_LLM_ATTN=split (64-position chunks on the VALU + a
+// combine launch) or mfma (default: attn_mfma_kernel, no combine launch up to kMChunk positions).
+static int attn_impl_default() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("AMDK8S_LLM_ATTN");
+    v = (e && e[0] == 's') ? 1 : 2;
+  }
+  return v;
+}
+
 // AMDK8S_LLM_LONGROW=1: long rows in two balanced stages instead of KB-wide ones (A/B knob;
 // measured neutral to slightly slower on MI355X — profiles/r03/q — so off by default).
 static bool longrow_enabled() {
@@ -1451,9 +1758,12 @@ int dispatch2_t(const GemvArgs& a0, const GemvArgs& a1, int waves, hipStream_t s
 // Default decomposition (measured on MI355X, tools/llm_bench.py --gemv, T = 1): 4-wave
 // workgroups of 8 rows for the 3584/4608/18944-row matrices, 8 waves for the 18944-long rows of
 // ffn_down, and 32 rows per workgroup for the 152064-row lm_head (longer per-wave pipelines).
-void gemv_shape(int N, int K, int& waves, int& rows) {
+// From T = 3 on, the 18944-long ffn_down rows run 16 per workgroup (2 per wave: the staged
+// activations serve twice the weights; 20.8 / 24.2 vs 24.4 / 26.6 us for Q4_K / Q6_K at T = 4,
+// profiles/r03/y — at T = 1 the 8-row grid is faster).
+void gemv_shape(int N, int K, int T, int& waves, int& rows) {
   if (waves <= 0) waves = K >= 8192 ? 8 : 4;
-  if (rows <= 0) rows = N >= 65536 ? 32 : 8;
+  if (rows <= 0) rows = N >= 65536 ? 32 : (K >= 8192 && T >= 3 && waves == 8) ? 16 : 8;
 }
 
 }  // namespace
@@ -1510,7 +1820,7 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
     if (mode != kPair || N % 32 || !odx || !osx) return 2;
     rows_per_wg = 32;
   }
-  gemv_shape(N, K, waves, rows_per_wg);
+  gemv_shape(N, K, T, waves, rows_per_wg);
   if (ox8 && waves * 64 < 32 * T) return 2;
   if (waves < 1 || waves > 8 || rows_per_wg < 1) return 2;
   GemvArgs a;
@@ -1549,18 +1859,22 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
   return 2;
 }
 
-// Two store-mode GEMVs over the same Q8 input in one launch: out_i[t][n] = W_i.x + bias_i (the
-// q|k and v projections when their quantisation types differ).  Returns 4 when the shape is not
+// Two store-mode GEMVs over the same input in one launch: out_i[t][n] = W_i.x + bias_i (the
+// q|k and v projections when their quantisation types differ); Q8 input, or fp32 rows xf
+// (+ RMSNorm norm_w) quantised in each workgroup's prologue.  Returns 4 when the shape is not
 // covered (K > 4096): launch the two with amdk8s_llm_qgemv instead.
 int amdk8s_llm_qgemv2(int type0, const void* w0q, const void* w0qh, const void* w0sc,
                       const void* w0d, int N0, const void* bias0, void* out0, int type1,
                       const void* w1q, const void* w1qh, const void* w1sc, const void* w1d, int N1,
                       const void* bias1, void* out1, int ldo, const void* x8, const void* dx,
-                      const void* sx, int K, int T, int waves, int rows_per_wg, void* stream) {
-  if (K % 256 || N0 <= 0 || N1 <= 0 || T < 1 || T > kMaxTok || !x8 || !dx || !sx) return 2;
+                      const void* sx, const void* xf, int ldx, const void* norm_w, float eps,
+                      int K, int T, int waves, int rows_per_wg, void* stream) {
+  if (K % 256 || N0 <= 0 || N1 <= 0 || T < 1 || T > kMaxTok) return 2;
+  if (!xf && !(x8 && dx && sx)) return 2;
+  if (xf && ldx % 4) return 2;
   if ((type0 != kQ4K && type0 != kQ6K) || (type1 != kQ4K && type1 != kQ6K)) return 2;
   int rows = rows_per_wg;
-  gemv_shape(N0 + N1, K, waves, rows);
+  gemv_shape(N0 + N1, K, T, waves, rows);
   if (waves < 1 || waves > 8 || rows < 1) return 2;
   GemvArgs a[2];
   const int N[2] = {N0, N1};
@@ -1575,6 +1889,10 @@ int amdk8s_llm_qgemv2(int type0, const void* w0q, const void* w0qh, const void* 
     g.x8 = static_cast<const int8_t*>(x8);
     g.dx = static_cast<const float*>(dx);
     g.sx = static_cast<const float*>(sx);
+    g.xf = static_cast<const float*>(xf);
+    g.ldx = ldx;
+    g.norm_w = static_cast<const float*>(norm_w);
+    g.eps = eps;
     g.bias = static_cast<const float*>(bias[i]);
     g.out = static_cast<float*>(out[i]);
     g.ldo = ldo; g.N = N[i]; g.K = K; g.T = T; g.rows_per_wg = rows;
@@ -1623,14 +1941,16 @@ int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* 
                            const void* sin_t, const void* pos, const void* slot, void* kc,
                            void* vc, int H, int Hkv, int head_dim, int max_ctx, int span,
                            float scale, void* po, void* pml, void* out, void* x8, void* dx,
-                           void* sx, int T, void* cnt, void* stream) {
+                           void* sx, int T, void* cnt, int impl, void* stream) {
   if (span <= 0) span = max_ctx;
   if (head_dim != kHeadDim || H % Hkv || H / Hkv > kMaxGroup || max_ctx % kAttnChunk ||
       span % kAttnChunk || span > max_ctx || T < 1)
     return 2;
-  const int nsplit = span / kAttnChunk;
+  if (!qkv && !q) return 2;
+  if (qkv && (!cos_t || !sin_t)) return 2;
+  if (impl == 0) impl = attn_impl_default();
+  if (impl == 2 && cnt) return 2;        // the in-launch combine is a split-kernel form only
   hipStream_t st = static_cast<hipStream_t>(stream);
-  // the GQA group size is a template parameter: fully unrolled head loops, no per-head branches
   AttnArgs aa;
   aa.q = static_cast<const float*>(q);
   aa.qkv = static_cast<const float*>(qkv);
@@ -1641,7 +1961,7 @@ int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* 
   aa.slot = static_cast<const int*>(slot);
   aa.kc = static_cast<uint16_t*>(kc);
   aa.vc = static_cast<uint16_t*>(vc);
-  aa.H = H; aa.Hkv = Hkv; aa.max_ctx = max_ctx; aa.nsplit = nsplit; aa.scale = scale;
+  aa.H = H; aa.Hkv = Hkv; aa.max_ctx = max_ctx; aa.scale = scale;
   aa.po = static_cast<float*>(po);
   aa.pml = static_cast<float*>(pml);
   aa.cnt = static_cast<int*>(cnt);
@@ -1649,27 +1969,41 @@ int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* 
   aa.x8 = static_cast<int8_t*>(x8);
   aa.dx = static_cast<float*>(dx);
   aa.sx = static_cast<float*>(sx);
-  if (!qkv && !q) return 2;
-  if (qkv && (!cos_t || !sin_t)) return 2;
-  auto launch = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(Hkv, nsplit, T), dim3(256), 0, st, aa);
+  // the GQA group size is a template parameter: fully unrolled head loops, no per-head branches
+  auto by_group = [&](auto launch) -> int {
+    switch (H / Hkv) {
+      case 1: launch(std::integral_constant<int, 1>{}); break;
+      case 2: launch(std::integral_constant<int, 2>{}); break;
+      case 3: launch(std::integral_constant<int, 3>{}); break;
+      case 4: launch(std::integral_constant<int, 4>{}); break;
+      case 5: launch(std::integral_constant<int, 5>{}); break;
+      case 6: launch(std::integral_constant<int, 6>{}); break;
+      case 7: launch(std::integral_constant<int, 7>{}); break;
+      case 8: launch(std::integral_constant<int, 8>{}); break;
+      default: return 2;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : 1;
   };
-  switch (H / Hkv) {
-    case 1: launch(attn_decode_kernel<1>); break;
-    case 2: launch(attn_decode_kernel<2>); break;
-    case 3: launch(attn_decode_kernel<3>); break;
-    case 4: launch(attn_decode_kernel<4>); break;
-    case 5: launch(attn_decode_kernel<5>); break;
-    case 6: launch(attn_decode_kernel<6>); break;
-    case 7: launch(attn_decode_kernel<7>); break;
-    case 8: launch(attn_decode_kernel<8>); break;
-    default: return 2;
+  int chunk = kAttnChunk;
+  if (impl == 2) {                       // MFMA: one workgroup per kMChunk positions
+    chunk = span <= kMChunk ? span : kMChunk;
+    aa.nsplit = (span + chunk - 1) / chunk;
+    const int rc = by_group([&](auto g) {
+      hipLaunchKernelGGL(attn_mfma_kernel<decltype(g)::value>, dim3(Hkv, aa.nsplit, T), dim3(512),
+                         0, st, aa, chunk);
+    });
+    if (rc || aa.nsplit == 1) return rc;   // one split: normalised Q8 output written in-kernel
+  } else {
+    aa.nsplit = span / kAttnChunk;
+    const int rc = by_group([&](auto g) {
+      hipLaunchKernelGGL(attn_decode_kernel<decltype(g)::value>, dim3(Hkv, aa.nsplit, T),
+                         dim3(256), 0, st, aa);
+    });
+    if (rc || cnt) return rc;            // in-kernel combine
   }
-  if (hipGetLastError() != hipSuccess) return 1;
-  if (cnt) return 0;                     // combined in-kernel
   hipLaunchKernelGGL(attn_combine_q8_kernel, dim3(H, T), dim3(128), 0, st,
                      static_cast<const float*>(po), static_cast<const float*>(pml),
-                     static_cast<const int*>(pos), H, nsplit, static_cast<float*>(out),
+                     static_cast<const int*>(pos), H, aa.nsplit, chunk, static_cast<float*>(out),
                      static_cast<int8_t*>(x8), static_cast<float*>(dx), static_cast<float*>(sx));
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

@@ -33,7 +33,7 @@ def _lib():
                 + [vp, vp, vp] + [vp]
             lib.amdk8s_llm_qgemv.restype = ci
             lib.amdk8s_llm_qgemv2.argtypes = [ci] + [vp] * 4 + [ci, vp, vp] + [ci] + [vp] * 4 \
-                + [ci, vp, vp] + [ci, vp, vp, vp, ci, ci, ci, ci, vp]
+                + [ci, vp, vp] + [ci, vp, vp, vp, vp, ci, vp, cf, ci, ci, ci, ci, vp]
             lib.amdk8s_llm_qgemv2.restype = ci
             lib.amdk8s_llm_rmsnorm_q8.argtypes = [vp, vp, cf, ci, ci, vp, vp, vp, vp]
             lib.amdk8s_llm_rmsnorm_q8.restype = ci
@@ -41,7 +41,8 @@ def _lib():
                                                ci, vp]
             lib.amdk8s_llm_rope_kv.restype = ci
             lib.amdk8s_llm_attn_decode.argtypes = [vp, vp, ci, vp, vp, vp, vp, vp, vp, ci, ci, ci,
-                                                   ci, ci, cf, vp, vp, vp, vp, vp, vp, ci, vp, vp]
+                                                   ci, ci, cf, vp, vp, vp, vp, vp, vp, ci, vp, ci,
+                                                   vp]
             lib.amdk8s_llm_attn_decode.restype = ci
             lib.amdk8s_llm_dequant.argtypes = [ci, vp, vp, vp, vp, vp, ci, ci, vp, ci, vp]
             lib.amdk8s_llm_dequant.restype = ci
@@ -102,17 +103,20 @@ def qgemv(w0, x8, dx, sx, out, mode: int = STORE, w1=None, bias=None, ldo: int =
 
 
 def qgemv2(w0, w1, x8, dx, sx, out0, out1, bias0=None, bias1=None, rows_per_wg: int = 0,
-           waves: int = 0) -> bool:
+           waves: int = 0, xf=None, norm_w=None, eps: float = 1e-6) -> bool:
     """Two store-mode GEMVs over the same Q8 input [T, K] in ONE launch (``out_i = W_i.x +
     bias_i``; ``out0``/``out1`` views with the same row stride) — q|k and v when their
-    quantisation types differ.  Returns False when the shape is not covered (K > 4096): the
-    caller launches them with :func:`qgemv`."""
+    quantisation types differ.  Input as for :func:`qgemv`: Q8 (``x8``/``dx``/``sx``) or fp32
+    rows ``xf`` (+ RMSNorm ``norm_w``) quantised in the prologue.  Returns False when the shape
+    is not covered (K > 4096): the caller launches them with :func:`qgemv`."""
     if out0.stride(0) != out1.stride(0) or w0.k != w1.k:
         raise ValueError("qgemv2: both outputs need one row stride and both matrices one K")
+    ref = xf if xf is not None else x8
     rc = _lib().amdk8s_llm_qgemv2(w0.qtype, *w0.ptrs(), w0.n, _p(bias0), out0.data_ptr(),
                                   w1.qtype, *w1.ptrs(), w1.n, _p(bias1), out1.data_ptr(),
-                                  out0.stride(0), x8.data_ptr(), dx.data_ptr(), sx.data_ptr(),
-                                  w0.k, x8.shape[0], waves, rows_per_wg, _stream(x8))
+                                  out0.stride(0), _p(x8), _p(dx), _p(sx), _p(xf),
+                                  xf.stride(0) if xf is not None else 0, _p(norm_w), float(eps),
+                                  w0.k, ref.shape[0], waves, rows_per_wg, _stream(ref))
     if rc == 4:
         return False
     _check(rc, "amdk8s_llm_qgemv2")
@@ -135,23 +139,32 @@ def rope_kv(qkv, pos, slot, cos_t, sin_t, heads: int, kv_heads: int, head_dim: i
            "amdk8s_llm_rope_kv")
 
 
+ATTN_DEFAULT, ATTN_SPLIT, ATTN_MFMA = 0, 1, 2
+
+
 def attn_decode(q, pos, slot, kc, vc, heads: int, kv_heads: int, head_dim: int, max_ctx: int,
                 scale: float, po, pml, x8, dx, sx, out=None, span: int = 0, qkv=None,
-                cos_t=None, sin_t=None, cnt=None) -> None:
+                cos_t=None, sin_t=None, cnt=None, impl: int = ATTN_DEFAULT) -> None:
     """Split-context decode attention + combine + Q8 quantisation of the output.
 
     ``span``: context positions this call covers (multiple of ``attn_chunk()``, above every
     position; 0 = ``max_ctx``).  With ``qkv`` (the raw q|k|v projection) and the RoPE tables, the
     kernel also rotates q/k and writes the new K/V itself (``q`` unused, pass None) — only when
     every token of the step is in a distinct slot.  ``cnt``: int32 [T, kv_heads] zeros (kept zero
-    by every call) — the combine then runs inside the attention kernel, one launch instead of two."""
+    by every call) — the combine then runs inside the attention kernel, one launch instead of two
+    (split kernel only).  ``impl``: ATTN_SPLIT (64-position chunks + combine), ATTN_MFMA (one
+    workgroup per 1024 positions on MFMA, no combine launch up to 1024) or ATTN_DEFAULT
+    (AMDK8S_LLM_ATTN, MFMA unless it says ``split``)."""
+    if cnt is not None and impl == ATTN_DEFAULT:
+        impl = ATTN_SPLIT
     ref = qkv if qkv is not None else q
     _check(_lib().amdk8s_llm_attn_decode(_p(q), _p(qkv), qkv.stride(0) if qkv is not None else 0,
                                          _p(cos_t), _p(sin_t), pos.data_ptr(), slot.data_ptr(),
                                          kc.data_ptr(), vc.data_ptr(), heads, kv_heads, head_dim,
                                          max_ctx, span, float(scale), po.data_ptr(), pml.data_ptr(),
                                          _p(out), x8.data_ptr(), dx.data_ptr(), sx.data_ptr(),
-                                         ref.shape[0], _p(cnt), _stream(ref)), "amdk8s_llm_attn_decode")
+                                         ref.shape[0], _p(cnt), int(impl), _stream(ref)),
+           "amdk8s_llm_attn_decode")
 
 
 def dequant(w, out, rows=None) -> None:

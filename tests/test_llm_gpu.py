@@ -210,8 +210,9 @@ def _attn_ref(q, kc, vc, pos, slot, H, Hkv):
     return torch.stack(outs)
 
 
+@pytest.mark.parametrize("impl", [1, 2])             # split (VALU + combine) / MFMA
 @pytest.mark.parametrize("H,Hkv", [(28, 4), (8, 8), (16, 2)])
-def test_rope_kv_and_decode_attention(dev, LK, H, Hkv):
+def test_rope_kv_and_decode_attention(dev, LK, H, Hkv, impl):
     from k8s_nvidia_gpus_amd.models.llm.engine import apply_rope, rope_tables
 
     torch.manual_seed(H + Hkv)
@@ -245,15 +246,16 @@ def test_rope_kv_and_decode_attention(dev, LK, H, Hkv):
     sx = torch.empty(T, H * 8, device=dev)
     out = torch.empty(T, H * 128, device=dev)
     LK.attn_decode(qrot, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po, pml,
-                   x8, dx, sx, out=out)
+                   x8, dx, sx, out=out, impl=impl)
     ref = _attn_ref(qrot, kc, vc, pos, slot, H, Hkv)
-    torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-3 if impl == 1 else 2e-3)
     xq = (x8.float().view(T, -1, 32) * dx[..., None]).view(T, -1)
     assert ((xq - out).abs() <= dx.repeat_interleave(32, 1) * 0.5 + 1e-5).all()
 
 
+@pytest.mark.parametrize("impl", [1, 2])
 @pytest.mark.parametrize("H,Hkv", [(28, 4), (8, 8)])
-def test_fused_rope_attention_equals_separate_kernels(dev, LK, H, Hkv):
+def test_fused_rope_attention_equals_separate_kernels(dev, LK, H, Hkv, impl):
     """Distinct slots: RoPE + KV write inside the attention kernel == rope_kv + attention."""
     from k8s_nvidia_gpus_amd.models.llm.engine import rope_tables
 
@@ -277,15 +279,69 @@ def test_fused_rope_attention_equals_separate_kernels(dev, LK, H, Hkv):
         out = torch.empty(T, H * 128, device=dev)
         if fused:
             LK.attn_decode(None, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po,
-                           pml, x8, dx, sx, out=out, qkv=qkv, cos_t=cos, sin_t=sin)
+                           pml, x8, dx, sx, out=out, qkv=qkv, cos_t=cos, sin_t=sin, impl=impl)
         else:
             qrot = torch.empty(T, H * 128, device=dev)
             LK.rope_kv(qkv, pos, slot, cos, sin, H, Hkv, 128, max_ctx, qrot, kc, vc)
             LK.attn_decode(qrot, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po,
-                           pml, x8, dx, sx, out=out)
+                           pml, x8, dx, sx, out=out, impl=impl)
         outs.append((kc, vc, out))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     torch.testing.assert_close(outs[1][2], outs[0][2], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("span", [2048, 4096])
+def test_mfma_attention_long_context_splits(dev, LK, span):
+    """MFMA decode attention past one 1024-position workgroup: per-split partials + the combine
+    kernel (chunk 1024) against the fp32 reference, fused RoPE / KV write included; positions
+    on both sides of split boundaries."""
+    from k8s_nvidia_gpus_amd.models.llm.engine import apply_rope, rope_tables
+
+    torch.manual_seed(11)
+    H, Hkv, max_ctx, slots, T = 28, 4, 4096, 4, 4
+    kc = (torch.randn(slots, Hkv, max_ctx, 128, device=dev) * 0.5).half()
+    vc = torch.randn(slots, Hkv, max_ctx, 128, device=dev).half()
+    cos, sin = rope_tables(max_ctx, 128, 1.0e6, dev)
+    top = span - 1
+    pos = torch.tensor([1023, 1024, 1500, top], dtype=torch.int32, device=dev)
+    slot = torch.tensor([1, 3, 0, 2], dtype=torch.int32, device=dev)
+    qkv = torch.randn(T, (H + 2 * Hkv) * 128, device=dev)
+    nsplit = max_ctx // LK.attn_chunk()
+    po = torch.empty(T, H, nsplit, 128, device=dev)
+    pml = torch.empty(T, H, nsplit, 2, device=dev)
+    x8 = torch.empty(T, H * 128, dtype=torch.int8, device=dev)
+    dx = torch.empty(T, H * 4, device=dev)
+    sx = torch.empty(T, H * 8, device=dev)
+    out = torch.empty(T, H * 128, device=dev)
+    kref, vref = kc.clone(), vc.clone()
+    LK.attn_decode(None, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po, pml,
+                   x8, dx, sx, out=out, span=span, qkv=qkv, cos_t=cos, sin_t=sin, impl=2)
+    qrot = torch.empty(T, H * 128, device=dev)
+    LK.rope_kv(qkv, pos, slot, cos, sin, H, Hkv, 128, max_ctx, qrot, kref, vref)
+    assert torch.equal(kc, kref) and torch.equal(vc, vref)
+    ref = _attn_ref(qrot, kref, vref, pos, slot, H, Hkv)
+    torch.testing.assert_close(out, ref, rtol=1e-3, atol=2e-3)
+    xq = (x8.float().view(T, -1, 32) * dx[..., None]).view(T, -1)
+    assert ((xq - out).abs() <= dx.repeat_interleave(32, 1) * 0.5 + 1e-5).all()
+
+
+@pytest.mark.parametrize("T", [1, 4])
+def test_two_matrix_gemv_fp32_prologue(dev, LK, T):
+    """The two-matrix GEMV with the RMSNorm + Q8 prologue (fp32 input) equals the two GEMVs
+    with the same prologue, bit for bit."""
+    from k8s_nvidia_gpus_amd.models.llm import gguf
+
+    K = 3584
+    w0, _ = _qw(640, K, gguf.Q4_K, 12, dev)
+    w1, _ = _qw(128, K, gguf.Q6_K, 13, dev)
+    xf = torch.randn(T, K, device=dev) * 2
+    nw = torch.rand(K, device=dev) + 0.5
+    ref = torch.zeros(T, 768, device=dev)
+    LK.qgemv(w0, None, None, None, ref[:, :640], LK.STORE, ldo=768, xf=xf, norm_w=nw)
+    LK.qgemv(w1, None, None, None, ref[:, 640:], LK.STORE, ldo=768, xf=xf, norm_w=nw)
+    out = torch.zeros(T, 768, device=dev)
+    assert LK.qgemv2(w0, w1, None, None, None, out[:, :640], out[:, 640:], xf=xf, norm_w=nw)
+    torch.testing.assert_close(out, ref, rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("H,Hkv", [(28, 4), (8, 8), (6, 2)])
@@ -392,12 +448,13 @@ def tiny_gguf(tmp_path_factory):
     return write_synthetic_gguf(str(p), tiny(layers=4, dim=512, heads=4, kv_heads=2, ffn=1024))
 
 
-@pytest.mark.parametrize("resid_norm", [False, True])
-def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf, resid_norm):
+@pytest.mark.parametrize("resid_norm,norm_prologue", [(False, False), (True, False),
+                                                      (False, True)])
+def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf, resid_norm, norm_prologue):
     from k8s_nvidia_gpus_amd.models.llm.synthetic import load
 
     gpu, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=False)
-    gpu.resid_norm = resid_norm
+    gpu.resid_norm, gpu.norm_prologue = resid_norm, norm_prologue
     cpu, _ = load(tiny_gguf, device="cpu", max_ctx=512)
     prompt = tok.encode("<|im_start|>user\nhello world, a cozy cabin<|im_end|>\n")
     lg = gpu.prefill(prompt, slot=1)            # native kernels, 4 tokens per step
@@ -416,8 +473,11 @@ def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf, resid_norm)
     assert gpu.stats["graph_captures"] >= 1
 
 
-@pytest.mark.parametrize("resid_norm,fused_combine", [(False, False), (True, False), (True, True)])
-def test_engine_batched_decode_equals_single(dev, tiny_gguf, resid_norm, fused_combine):
+@pytest.mark.parametrize("resid_norm,fused_combine,norm_prologue",
+                         [(False, False, False), (True, False, False), (True, True, False),
+                          (False, False, True)])
+def test_engine_batched_decode_equals_single(dev, tiny_gguf, resid_norm, fused_combine,
+                                             norm_prologue):
     """T sequences in one step give the same logits as each alone: slots are independent and the
     GEMV's roundings are pinned, so the int8 activation quantisation never flips between a batched
     and a single step (batch-invariant serving) — also with the norms fused into the residual
@@ -426,6 +486,7 @@ def test_engine_batched_decode_equals_single(dev, tiny_gguf, resid_norm, fused_c
 
     eng, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=True)
     eng.resid_norm, eng.fused_combine = resid_norm, fused_combine
+    eng.norm_prologue = norm_prologue
     prompts = [tok.encode(s) for s in ("hello", "the quick brown fox", "a cozy cabin in", "you")]
     last = []
     for s, p in enumerate(prompts):
