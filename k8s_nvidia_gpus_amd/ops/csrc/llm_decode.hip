@@ -1275,7 +1275,8 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
 //       8 values: slot 8q + j <-> position 4q + j (j < 4), 16 + 4q + j - 4 (j >= 4)); A = V^T, read
 //       from the wave's V tile staged in LDS (8 ds_read_u16 per 16-dim block, rows padded).
 // With one split (contexts up to kMChunk) the workgroup writes the normalised output as Q8 (the
-// o_proj input) itself: no partials, no combine launch.  Longer contexts write per-split partials
+// o_proj input) itself: no partials, no combine launch.  Not the default (attn_impl_default): with
+// 4 kv heads a decode token keeps only 4 CUs busy.  Longer contexts write per-split partials
 // (unnormalised O, natural-log max, sum) for attn_combine_q8_kernel.  Fused RoPE / KV write as in
 // attn_decode_kernel (distinct slots).  Scores use exp2 with log2(e) folded into the q scale.
 constexpr int kMChunk = 1024;
@@ -1666,13 +1667,15 @@ static int regx_max_t() {
   return v;
 }
 
-// Decode attention implementation: AMDK8S_LLM_ATTN=split (64-position chunks on the VALU + a
-// combine launch) or mfma (default: attn_mfma_kernel, no combine launch up to kMChunk positions).
+// Decode attention implementation: AMDK8S_LLM_ATTN=split (default: 64-position chunks on the VALU
+// + a combine launch) or mfma (attn_mfma_kernel: no combine launch up to kMChunk positions, but
+// one workgroup per kv head and token streams the whole context through one CU — 20.3 us against
+// 6.2 + 4.8 us for split + combine at 4 kv heads and ~600 positions, profiles/r03/aa).
 static int attn_impl_default() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("AMDK8S_LLM_ATTN");
-    v = (e && e[0] == 's') ? 1 : 2;
+    v = (e && e[0] == 'm') ? 2 : 1;
   }
   return v;
 }

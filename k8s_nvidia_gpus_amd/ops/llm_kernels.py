@@ -154,7 +154,7 @@ def attn_decode(q, pos, slot, kc, vc, heads: int, kv_heads: int, head_dim: int, 
     by every call) — the combine then runs inside the attention kernel, one launch instead of two
     (split kernel only).  ``impl``: ATTN_SPLIT (64-position chunks + combine), ATTN_MFMA (one
     workgroup per 1024 positions on MFMA, no combine launch up to 1024) or ATTN_DEFAULT
-    (AMDK8S_LLM_ATTN, MFMA unless it says ``split``)."""
+    (AMDK8S_LLM_ATTN: split unless it says ``mfma``)."""
     if cnt is not None and impl == ATTN_DEFAULT:
         impl = ATTN_SPLIT
     ref = qkv if qkv is not None else q

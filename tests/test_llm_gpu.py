@@ -366,7 +366,8 @@ def test_in_kernel_combine_equals_combine_kernel(dev, LK, H, Hkv):
         sx = torch.empty(T, H * 8, device=dev)
         out = torch.empty(T, H * 128, device=dev)
         LK.attn_decode(q, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po, pml,
-                       x8, dx, sx, out=out, cnt=cnt if use_cnt else None)
+                       x8, dx, sx, out=out, cnt=cnt if use_cnt else None,
+                       impl=LK.ATTN_SPLIT)
         torch.cuda.synchronize()
         res.append((x8, dx, sx, out))
         assert int(cnt.abs().sum()) == 0

@@ -45,7 +45,7 @@ def heartbeat(period=30.0):
 GEMV_CASES = ("qkv", "o_proj", "gate_up", "down_q4k", "down_q6k", "lm_head")
 
 
-def bench_gemv(eng: Engine, iters: int = 50, sweep4: bool = False) -> list:
+def bench_gemv(eng: Engine, iters: int = 50, sweep4: bool = False, only=GEMV_CASES) -> list:
     """Achieved bandwidth of every decode GEMV shape, default decomposition and a sweep."""
     LK = eng.LK
     L = eng.w.layers[0]
@@ -55,9 +55,9 @@ def bench_gemv(eng: Engine, iters: int = 50, sweep4: bool = False) -> list:
     cases = [("qkv", L.wqkv[0], "store"), ("o_proj", L.wo, "resid"),
              ("gate_up", L.wg, "pair"), ("down_q4k", Lq4.wd, "resid"),
              ("down_q6k", Lq6.wd, "resid"), ("lm_head", eng.w.output, "store")]
-    cases = [(n, w, m) for n, w, m in cases if n in GEMV_CASES]
+    cases = [(n, w, m) for n, w, m in cases if n in only]
     cfgs = [(0, 0), (4, 4), (4, 16), (4, 32), (8, 8), (8, 16), (8, 32), (2, 4), (2, 8),
-            (1, 2), (1, 4)]
+            (1, 2), (1, 4), (8, 7), (4, 7), (8, 14), (4, 37), (8, 37)]
     for name, w, mode in cases:
         for T in (1, 4):
             x8 = torch.randint(-127, 127, (T, w.k), dtype=torch.int8, device=eng.device)
@@ -137,6 +137,7 @@ def main(argv=None) -> int:
     ap.add_argument("--tokens", default="1,2,3,4")
     ap.add_argument("--gemv", action="store_true")
     ap.add_argument("--gemv-sweep4", action="store_true", help="also sweep the decomposition at T=4")
+    ap.add_argument("--gemv-cases", default=",".join(GEMV_CASES), help="GEMV shapes to time")
     ap.add_argument("--kernels", action="store_true", help="time the non-GEMV decode kernels")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
@@ -191,7 +192,7 @@ def main(argv=None) -> int:
         res["decode"].append(row)
         print(f"decode T={T}: {row}", file=sys.stderr, flush=True)
     if args.gemv:
-        res["gemv"] = bench_gemv(eng, sweep4=args.gemv_sweep4)
+        res["gemv"] = bench_gemv(eng, sweep4=args.gemv_sweep4, only=args.gemv_cases.split(","))
         for r in res["gemv"]:
             print(r, file=sys.stderr, flush=True)
     if args.kernels:
