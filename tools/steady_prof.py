@@ -7,6 +7,7 @@ lazy kernel loads), sleep 300 ms, then run N iterations — tools/rocpd_summary.
     python tools/steady_prof.py wan-step   [--iters 5]    # one Wan2.1-1.3B CFG DiT step (2560 tokens)
     python tools/steady_prof.py llm-decode [--iters 64]   # one Qwen2.5-7B Q4_K_M decode step, T=1
                                                           #   (position 512, host sync per token)
+    python tools/steady_prof.py llm-prefill [--iters 10]  # one 512-token prompt prefill (fp16 path)
 """
 import argparse
 import os
@@ -59,14 +60,26 @@ def llm_decode(T: int = 1):
     return step
 
 
+def llm_prefill(P: int = 512):
+    from k8s_nvidia_gpus_amd.models.llm.config import QWEN25_7B
+    from k8s_nvidia_gpus_amd.models.llm.engine import Engine
+    from k8s_nvidia_gpus_amd.models.llm.weights import ModelWeights
+
+    w = ModelWeights.random(QWEN25_7B, device=torch.device("cuda", 0), seed=0)
+    eng = Engine(w, max_ctx=4096, slots=4, dense=True)
+    eng.dense_weights()
+    prompt = list(range(100, 100 + P))
+    return lambda: eng.prefill(prompt, slot=0)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["sd15-unet", "wan-step", "llm-decode"])
+    ap.add_argument("what", choices=["sd15-unet", "wan-step", "llm-decode", "llm-prefill"])
     ap.add_argument("--tokens", type=int, default=1, help="llm-decode: concurrent sequences")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     a = ap.parse_args()
-    fn = (llm_decode(a.tokens) if a.what == "llm-decode"
+    fn = (llm_decode(a.tokens) if a.what == "llm-decode" else llm_prefill() if a.what == "llm-prefill"
           else {"sd15-unet": sd15_unet, "wan-step": wan_step}[a.what]())
     for _ in range(a.warmup):
         fn()
