@@ -134,12 +134,17 @@ class Engine:
         # q|k (Q4_K) and v (Q6_K in about half the Q4_K_M layers) in one two-matrix launch:
         # T=1 2.00 -> 1.94 ms, T=4 3.36 -> 3.27 ms (profiles/r03/w)
         self.qkv2 = os.environ.get("AMDK8S_LLM_QKV2", "1") != "0"
+        # dense prefill on the fused glue kernels (llm_prefill.hip); 0 = the PyTorch formulation
+        self.prefill_native = os.environ.get("AMDK8S_LLM_PREFILL_NATIVE", "1") != "0"
         # attn_norm / ffn_norm inside the q|k|v and gate|up GEMV prologues (each workgroup
         # normalises the L2-resident fp32 row itself) instead of two rmsnorm_q8 launches per
         # layer; the gate|up -> Q8 hand-off to ffn_down and the final norm stay as they are.
-        # T=1 1.81 -> 1.74 ms, T=4 2.73 -> 2.75 ms (profiles/r03/aa); one setting for every T
-        # keeps decode batch-invariant
+        # T=1 1.81 -> 1.74 ms, T=4 2.73 -> 2.75 ms (profiles/r03/aa), so only steps of up to
+        # AMDK8S_LLM_NORM_PROLOGUE_T tokens use it.  rmsnorm_q8 sums the squares in the 4-wave
+        # prologue's order, so both paths give the same bits and decode stays batch-invariant
+        # (models with dim >= 8192 run 8-wave GEMVs there: one path for every T)
         self.norm_prologue = os.environ.get("AMDK8S_LLM_NORM_PROLOGUE", "1") != "0"
+        self.norm_prologue_T = int(os.environ.get("AMDK8S_LLM_NORM_PROLOGUE_T", "2"))
         self._norm_cnt = None
         self._attn_cnt = None
         self._side = None
@@ -160,6 +165,7 @@ class Engine:
             d: Dict[str, torch.Tensor] = {}
             for i, L in enumerate(self.w.layers):
                 d[f"{i}.qkv"] = torch.cat([w.dequant(dt) for w in L.wqkv], 0)
+                d[f"{i}.bqkv"] = L.bqkv.to(dt)
                 d[f"{i}.o"] = L.wo.dequant(dt)
                 d[f"{i}.gu"] = torch.cat([L.wg.dequant(dt), L.wu.dequant(dt)], 0)
                 d[f"{i}.down"] = L.wd.dequant(dt)
@@ -174,6 +180,8 @@ class Engine:
     def _forward_dense(self, tokens: torch.Tensor, slot: int, start: int) -> torch.Tensor:
         """Prompt tokens [P] of one sequence at positions start..start+P-1 → last-position logits
         (fp32 [vocab]).  Writes the KV cache."""
+        if self.gpu and self.prefill_native and self.cfg.head_dim == 128:
+            return self._forward_dense_native(tokens, slot, start)
         c = self.cfg
         W = self.dense_weights()
         dt = torch.float16 if self.gpu else torch.float32
@@ -211,6 +219,43 @@ class Engine:
         xn = (xl * torch.rsqrt(xl.pow(2).mean(-1, keepdim=True) + c.eps) * self.w.out_norm).to(dt)
         return mm(xn, W["out"]).float()[0]
 
+    def _forward_dense_native(self, tokens: torch.Tensor, slot: int, start: int) -> torch.Tensor:
+        """The GPU prefill: hand-written fp16 GEMMs (bias in the q|k|v epilogue, residual adds
+        in the o_proj / ffn_down epilogues) and three glue kernels per layer use
+        (ops/csrc/llm_prefill.hip: RMSNorm -> fp16, RoPE + KV-cache write, SwiGLU) instead of
+        ~35 PyTorch elementwise launches (profiles/r03/ac)."""
+        c, LK = self.cfg, self.LK
+        W = self.dense_weights()
+        dt = torch.float16
+        P = tokens.numel()
+        end = start + P
+        x = self.embed(tokens)                                  # fp32 [P, dim]
+        mask = None
+        if P > 1:
+            qi = torch.arange(start, end, device=self.device)[:, None]
+            kj = torch.arange(end, device=self.device)[None, :]
+            mask = kj <= qi
+        mm, mm_res = self._dense_ops()
+        xn = torch.empty(P, c.dim, dtype=dt, device=self.device)
+        qh = torch.empty(c.heads, P, c.head_dim, dtype=dt, device=self.device)
+        t = torch.empty(P, c.ffn, dtype=dt, device=self.device)
+        for i, L in enumerate(self.w.layers):
+            LK.rmsnorm_f16(x, L.attn_norm, c.eps, xn)
+            qkv = mm(xn, W[f"{i}.qkv"], W[f"{i}.bqkv"])
+            LK.rope_kv_f16(qkv, self.cos, self.sin, start, c.heads, c.kv_heads, self.max_ctx, qh,
+                           self.k_cache[i, slot], self.v_cache[i, slot])
+            kk = self.k_cache[i, slot, :, :end].repeat_interleave(c.group, 0)
+            vv = self.v_cache[i, slot, :, :end].repeat_interleave(c.group, 0)
+            o = F.scaled_dot_product_attention(qh[None], kk[None], vv[None],
+                                               attn_mask=None if mask is None else mask[None, None])
+            o = o[0].transpose(0, 1).reshape(P, c.dim)
+            x = mm_res(x, o, W[f"{i}.o"])
+            LK.rmsnorm_f16(x, L.ffn_norm, c.eps, xn)
+            LK.swiglu_f16(mm(xn, W[f"{i}.gu"]), t)
+            x = mm_res(x, t, W[f"{i}.down"])
+        LK.rmsnorm_f16(x[-1:], self.w.out_norm, c.eps, xn[:1])
+        return mm(xn[:1], W["out"]).float()[0]
+
     def _dense_ops(self):
         """Prompt-processing GEMMs: on the GPU the hand-written fp16 MFMA GEMMs
         (``ops/gemm_epi.py``: tile / split-K planned per shape, the residual add of o_proj and
@@ -218,15 +263,19 @@ class Engine:
         if self.gpu and os.environ.get("AMDK8S_LLM_PREFILL_GEMM", "native") != "torch":
             from k8s_nvidia_gpus_amd.ops import gemm_epi as GE
 
-            def mm(a, w):
-                return GE.linear(a, w) if GE.supported(a, w) else a @ w.t()
+            def mm(a, w, b=None):
+                if GE.supported(a, w):
+                    return GE.linear(a, w, b)
+                y = a @ w.t()
+                return y if b is None else y + b
 
             def mm_res(x, a, w):
                 if GE.supported(a, w) and x.is_contiguous():
                     return GE.linear_residual_(x, a, w)
                 return x + (a @ w.t()).float()
             return mm, mm_res
-        return (lambda a, w: a @ w.t()), (lambda x, a, w: x + (a @ w.t()).float())
+        return ((lambda a, w, b=None: a @ w.t() if b is None else a @ w.t() + b),
+                (lambda x, a, w: x + (a @ w.t()).float()))
 
     # ------------------------------------------------------------------ native decode
     def _buffers(self, T: int) -> StepBuffers:
@@ -293,6 +342,7 @@ class Engine:
                 return q, {}
             return (None, None, None), dict(xf=xf, norm_w=norm_w, eps=c.eps)
 
+        pro = self.norm_prologue and (c.dim >= 8192 or b.T <= self.norm_prologue_T)
         if (self.resid_norm and b.T >= self.q8_split_T and self.pair_q8 and c.ffn % 32 == 0
                 and c.dim % 256 == 0 and c.dim <= 4096):
             self._step_fused_norm(b, span, fused, cnt)
@@ -309,8 +359,8 @@ class Engine:
                 self.LK.prefetch(planes, self.prefetch_wgs, self._side)
             # RMSNorm + Q8 quantisation: in each GEMV's prologue (fp32 input + norm weight), or once
             # per input for larger T (act())
-            xin = act(b.h, L.attn_norm, c.dim, self.norm_prologue)
-            if xin[0][0] is not None or self.norm_prologue:
+            xin = act(b.h, L.attn_norm, c.dim, pro)
+            if xin[0][0] is not None or pro:
                 self._qkv(b, L, xin[0], xin[1])
             else:
                 off = 0
@@ -329,7 +379,7 @@ class Engine:
                                c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
                                span=span, cnt=cnt)
             LK.qgemv(L.wo, *qd, b.h, LK.RESID, **G)
-            xin = act(b.h, L.ffn_norm, c.dim, self.norm_prologue)
+            xin = act(b.h, L.ffn_norm, c.dim, pro)
             if self.pair_q8 and b.T >= self.q8_split_T and c.ffn % 32 == 0:
                 qf = (b.x8f, b.dxf, b.sxf)
                 LK.qgemv(L.wg, *xin[0], b.t, LK.PAIR, w1=L.wu, **xin[1], **G, q8_out=qf)

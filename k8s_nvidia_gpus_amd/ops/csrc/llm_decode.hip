@@ -659,9 +659,9 @@ __device__ __forceinline__ void qgemv_body(const GemvArgs& a, const int bid) {
         for (int u = 0; u < 2; ++u)
           if ((int)threadIdx.x + u * (int)blockDim.x < nch) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) ss[t] += v[t][u][i] * v[t][u][i];
+            for (int i = 0; i < 8; ++i) ss[t] = __fmaf_rn(v[t][u][i], v[t][u][i], ss[t]);
           }
-        ss[t] = wave_sum(ss[t]);
+        ss[t] = wave_sum_fast(ss[t]);     // = rmsnorm_q8_kernel's sum bit for bit at 256 threads
         if (lane == 0) red[wave * T + t] = ss[t];
       }
       __syncthreads();
@@ -829,16 +829,28 @@ __global__ void __launch_bounds__(256) rmsnorm_q8_kernel(const float* __restrict
   const float4 wb = *reinterpret_cast<const float4*>(wp + ic + 4);
   float rs = 1.f;
   if (w) {
+    // sum of squares in the order of the qgemv prologue at 256 threads (8-value chunks tid + 256u,
+    // explicit fma, wave_sum_fast, waves in order), so a row normalised here and one normalised
+    // in a 4-wave GEMV prologue quantise to the same bits (decode stays batch-invariant when
+    // small steps normalise in the prologue and large ones here)
+    const int nch = K >> 3;
     float ss = 0.f;
-    for (int i0 = threadIdx.x * 4; i0 < K; i0 += blockDim.x * 4 * 4) {
-      float4 v[4];
+    for (int u0 = 0; u0 * 256 < nch; u0 += 4) {
+      float4 v[4][2];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)            // 4 loads in flight (clamped, masked below)
-        v[u] = *reinterpret_cast<const float4*>(xr + min(i0 + u * (int)blockDim.x * 4, K - 4));
+      for (int u = 0; u < 4; ++u) {          // 4 chunks in flight (clamped, masked below)
+        const int c = min((int)threadIdx.x + 256 * (u0 + u), nch - 1);
+        v[u][0] = *reinterpret_cast<const float4*>(xr + c * 8);
+        v[u][1] = *reinterpret_cast<const float4*>(xr + c * 8 + 4);
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (i0 + u * (int)blockDim.x * 4 < K)
-          ss += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
+        if ((int)threadIdx.x + 256 * (u0 + u) < nch) {
+          const float e[8] = {v[u][0].x, v[u][0].y, v[u][0].z, v[u][0].w,
+                              v[u][1].x, v[u][1].y, v[u][1].z, v[u][1].w};
+#pragma unroll
+          for (int i = 0; i < 8; ++i) ss = __fmaf_rn(e[i], e[i], ss);
+        }
     }
     ss = wave_sum_fast(ss);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;

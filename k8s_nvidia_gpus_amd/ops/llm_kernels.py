@@ -51,6 +51,13 @@ def _lib():
             lib.amdk8s_llm_q4k_repack.argtypes = [vp, cl, vp, vp, vp, vp]
             lib.amdk8s_llm_q4k_repack.restype = ci
             lib.amdk8s_llm_q6k_repack.restype = ci
+            lib.amdk8s_llm_rmsnorm_f16.argtypes = [vp, ci, vp, cf, ci, ci, vp, ci, vp]
+            lib.amdk8s_llm_rmsnorm_f16.restype = ci
+            lib.amdk8s_llm_rope_kv_f16.argtypes = [vp, ci, vp, vp, ci, ci, ci, ci, ci, ci, vp, vp,
+                                                   vp, vp]
+            lib.amdk8s_llm_rope_kv_f16.restype = ci
+            lib.amdk8s_llm_swiglu_f16.argtypes = [vp, ci, ci, vp, vp]
+            lib.amdk8s_llm_swiglu_f16.restype = ci
             lib.amdk8s_llm_prefetch.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(cl), ci, ci, vp]
             lib.amdk8s_llm_prefetch.restype = ci
             _declared = True
@@ -201,3 +208,31 @@ def prefetch(tensors, wgs: int = 32, stream=None) -> None:
     sizes = (ctypes.c_long * len(ts))(*[(t.numel() * t.element_size()) // 16 * 16 for t in ts])
     st = (stream or torch.cuda.current_stream(ts[0].device)).cuda_stream
     _check(_lib().amdk8s_llm_prefetch(ptrs, sizes, len(ts), wgs, st), "amdk8s_llm_prefetch")
+
+
+# ---------------------------------------------------------------------- prompt prefill (llm_prefill.hip)
+def rmsnorm_f16(x, w, eps: float, y) -> None:
+    """y (fp16 [P, K]) = RMSNorm(x fp32 [P, K]) * w — one launch (row stride of x / y free)."""
+    p, k = x.shape
+    _check(_lib().amdk8s_llm_rmsnorm_f16(x.data_ptr(), x.stride(0), w.data_ptr(), float(eps), p, k,
+                                         y.data_ptr(), y.stride(0), _stream(x)),
+           "amdk8s_llm_rmsnorm_f16")
+
+
+def rope_kv_f16(qkv, cos_t, sin_t, start: int, heads: int, kv_heads: int, max_ctx: int, q_out,
+                kc, vc) -> None:
+    """q|k|v fp16 [P, (H + 2 Hkv) * 128] (bias included) -> rotated q fp16 [H, P, 128] and the
+    rotated k / v written into one slot's fp16 cache slabs ``kc`` / ``vc`` [Hkv, max_ctx, 128] at
+    positions start .. start + P - 1."""
+    p = qkv.shape[0]
+    _check(_lib().amdk8s_llm_rope_kv_f16(qkv.data_ptr(), qkv.stride(0), cos_t.data_ptr(),
+                                         sin_t.data_ptr(), start, p, heads, kv_heads, 128, max_ctx,
+                                         q_out.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+                                         _stream(qkv)), "amdk8s_llm_rope_kv_f16")
+
+
+def swiglu_f16(gu, t) -> None:
+    """t (fp16 [P, F]) = silu(gu[:, :F]) * gu[:, F:] for gu fp16 [P, 2F] (both contiguous)."""
+    p, f = t.shape
+    _check(_lib().amdk8s_llm_swiglu_f16(gu.data_ptr(), p, f, t.data_ptr(), _stream(gu)),
+           "amdk8s_llm_swiglu_f16")

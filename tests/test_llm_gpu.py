@@ -344,6 +344,29 @@ def test_two_matrix_gemv_fp32_prologue(dev, LK, T):
     torch.testing.assert_close(out, ref, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("K", [512, 3584])
+@pytest.mark.parametrize("T", [1, 2, 3, 4])
+def test_prologue_norm_equals_rmsnorm_kernel(dev, LK, K, T):
+    """RMSNorm + Q8 inside a 4-wave GEMV prologue and rmsnorm_q8 followed by the Q8-input GEMV
+    give the same bits (the engine normalises small steps in the prologue and large ones with
+    rmsnorm_q8: batch invariance rests on this)."""
+    from k8s_nvidia_gpus_amd.models.llm import gguf
+
+    w, _ = _qw(512, K, gguf.Q4_K, 14, dev)
+    torch.manual_seed(20 + T)
+    xf = torch.randn(T, K, device=dev) * 3
+    nw = torch.rand(K, device=dev) + 0.5
+    a = torch.zeros(T, 512, device=dev)
+    LK.qgemv(w, None, None, None, a, LK.STORE, xf=xf, norm_w=nw, eps=1e-6)
+    x8 = torch.empty(T, K, dtype=torch.int8, device=dev)
+    dx = torch.empty(T, K // 32, device=dev)
+    sx = torch.empty(T, K // 16, device=dev)
+    LK.rmsnorm_q8(xf, nw, 1e-6, x8, dx, sx)
+    b = torch.zeros(T, 512, device=dev)
+    LK.qgemv(w, x8, dx, sx, b, LK.STORE)
+    torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
 @pytest.mark.parametrize("H,Hkv", [(28, 4), (8, 8), (6, 2)])
 def test_in_kernel_combine_equals_combine_kernel(dev, LK, H, Hkv):
     """The last-arriving workgroup's chunk merge (cnt given) is bit-identical to the separate
@@ -508,6 +531,27 @@ def test_dense_prefill_matches_native_prefill(dev, tiny_gguf):
     p = tok.encode("the lazy dog jumps over a helpful assistant " * 3)
     la, lb = a.prefill(p, 0).cpu(), b.prefill(p, 0).cpu()
     assert torch.nn.functional.cosine_similarity(la[None], lb[None]).item() > 0.99
+
+
+def test_native_prefill_equals_torch_prefill(dev, tiny_gguf):
+    """The fused prefill glue (RMSNorm -> fp16, RoPE + KV write, SwiGLU kernels) against the
+    PyTorch formulation of the same dense fp16 forward: logits and the written KV cache agree,
+    for a prompt from position 0 and a continuation at position > 0."""
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load
+
+    a, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=True)
+    b, _ = load(tiny_gguf, device=dev, max_ctx=512, dense=True)
+    b.prefill_native = False
+    p = tok.encode("the lazy dog jumps over a helpful assistant " * 3)
+    for start, chunk in ((0, p[:20]), (20, p[20:])):
+        la, lb = a.prefill(chunk, 1, start).cpu(), b.prefill(chunk, 1, start).cpu()
+        assert torch.nn.functional.cosine_similarity(la[None], lb[None]).item() > 0.9995
+        torch.testing.assert_close(la, lb, rtol=2e-2, atol=5e-2)
+    n = len(p)
+    torch.testing.assert_close(a.k_cache[:, 1, :, :n].float(), b.k_cache[:, 1, :, :n].float(),
+                               rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(a.v_cache[:, 1, :, :n].float(), b.v_cache[:, 1, :, :n].float(),
+                               rtol=1e-2, atol=1e-2)
 
 
 def test_random_7b_layer_shapes_run(dev):
