@@ -134,6 +134,12 @@ class Engine:
         # q|k (Q4_K) and v (Q6_K in about half the Q4_K_M layers) in one two-matrix launch:
         # T=1 2.00 -> 1.94 ms, T=4 3.36 -> 3.27 ms (profiles/r03/w)
         self.qkv2 = os.environ.get("AMDK8S_LLM_QKV2", "1") != "0"
+        # the attention combine inside the o_proj GEMV prologue (LK.qgemv_attn: each o_proj
+        # workgroup merges the chunk partials of every head itself) instead of its own launch;
+        # "waves,rows" of that GEMV in AMDK8S_LLM_ATTN_OPROJ
+        self.attn_prologue = os.environ.get("AMDK8S_LLM_ATTN_PROLOGUE", "0") != "0"
+        self.attn_oproj_cfg = dict(zip(("waves", "rows_per_wg"), map(int, os.environ.get(
+            "AMDK8S_LLM_ATTN_OPROJ", "8,16").split(","))))
         # dense prefill on the fused glue kernels (llm_prefill.hip); 0 = the PyTorch formulation
         self.prefill_native = os.environ.get("AMDK8S_LLM_PREFILL_NATIVE", "1") != "0"
         # attn_norm / ffn_norm inside the q|k|v and gate|up GEMV prologues (each workgroup
@@ -343,6 +349,8 @@ class Engine:
             return (None, None, None), dict(xf=xf, norm_w=norm_w, eps=c.eps)
 
         pro = self.norm_prologue and (c.dim >= 8192 or b.T <= self.norm_prologue_T)
+        ap = self.attn_prologue and cnt is None      # combine merged in the o_proj prologue
+        ak = {"impl": LK.ATTN_SPLIT} if ap else {}
         if (self.resid_norm and b.T >= self.q8_split_T and self.pair_q8 and c.ffn % 32 == 0
                 and c.dim % 256 == 0 and c.dim <= 4096):
             self._step_fused_norm(b, span, fused, cnt)
@@ -368,17 +376,25 @@ class Engine:
                     LK.qgemv(w, *xin[0], b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:],
                              ldo=b.qkv.stride(0), **xin[1], **G)
                     off += w.n
+            # attention: the o_proj prologue merges the chunk partials (no combine launch), or
+            # the combine writes the Q8 o_proj input
+            aq = (None, None, None) if ap else qd
             if fused:
                 LK.attn_decode(None, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
-                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
-                               span=span, qkv=b.qkv, cos_t=self.cos, sin_t=self.sin, cnt=cnt)
+                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *aq,
+                               span=span, qkv=b.qkv, cos_t=self.cos, sin_t=self.sin, cnt=cnt,
+                               **ak)
             else:
                 LK.rope_kv(b.qkv, b.pos, b.slot, self.cos, self.sin, c.heads, c.kv_heads,
                            c.head_dim, self.max_ctx, b.qrot, self.k_cache[i], self.v_cache[i])
                 LK.attn_decode(b.qrot, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
-                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
-                               span=span, cnt=cnt)
-            LK.qgemv(L.wo, *qd, b.h, LK.RESID, **G)
+                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *aq,
+                               span=span, cnt=cnt, **ak)
+            if ap:
+                LK.qgemv_attn(L.wo, b.po, b.pml, b.pos, span // LK.attn_chunk(), b.h,
+                              **self.attn_oproj_cfg)
+            else:
+                LK.qgemv(L.wo, *qd, b.h, LK.RESID, **G)
             xin = act(b.h, L.ffn_norm, c.dim, pro)
             if self.pair_q8 and b.T >= self.q8_split_T and c.ffn % 32 == 0:
                 qf = (b.x8f, b.dxf, b.sxf)

@@ -142,6 +142,12 @@ struct GemvArgs {
   const float* res;      // [T][ldo] residual input (out must be a different buffer)
   const float* onorm_w;  // [N]
   int* cnt;              // arrival counter, zero between launches (the last arriver resets it)
+  // input = decode-attention partials (po != null): the prologue merges the context chunks of
+  // every head (the attention combine) and quantises the result into the staged Q8 activations
+  const float* po;       // [T][heads][nsplit][128] unnormalised chunk outputs
+  const float* pml;      // [T][heads][nsplit][2] (max, sum) per chunk
+  const int* apos;       // [T] positions (chunks past pos[t] are not read)
+  int nsplit, chunk;
 };
 
 // Weights are streamed exactly once per step: non-temporal loads keep them from evicting the
@@ -548,6 +554,51 @@ __device__ __forceinline__ void resid_norm_tail(const GemvArgs& a, float* red) {
   }
 }
 
+// The attention combine for 8 consecutive output dims (chunk c = head c / 16, dims (c % 16) * 8
+// ..) of token t: one pass over the context chunks in groups of 8 with every load of the group in
+// flight (online max), explicit roundings.  Used by the o_proj GEMV prologue (GemvArgs.po).
+__device__ __forceinline__ void merge_chunk8(const GemvArgs& a, int t, int c, float (&v)[8]) {
+  const int h = c >> 4, d4 = (c & 15) * 2;                    // float4 index within the head row
+  const int ns = min(a.nsplit, (a.apos[t] + a.chunk) / a.chunk);
+  const long hb = ((long)t * (a.K >> 7) + h) * a.nsplit;
+  float m = -INFINITY, den = 0.f, acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  for (int s0 = 0; s0 < ns; s0 += 8) {
+    float mx[8], l[8];
+    float4 lo[8], hi[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long sidx = hb + min(s0 + u, ns - 1);
+      const float2 ml = *reinterpret_cast<const float2*>(a.pml + sidx * 2);
+      mx[u] = ml.x;
+      l[u] = ml.y;
+      lo[u] = reinterpret_cast<const float4*>(a.po + sidx * kHeadDim)[d4];
+      hi[u] = reinterpret_cast<const float4*>(a.po + sidx * kHeadDim)[d4 + 1];
+    }
+    float mn = m;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (s0 + u < ns) mn = fmaxf(mn, mx[u]);
+    if (mn == -INFINITY) continue;
+    const float sc = m == -INFINITY ? 0.f : __expf(__fsub_rn(m, mn));
+    den = __fmul_rn(den, sc);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = __fmul_rn(acc[i], sc);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float w = (s0 + u < ns && mx[u] != -INFINITY) ? __expf(__fsub_rn(mx[u], mn)) : 0.f;
+      den = __fmaf_rn(w, l[u], den);
+      const float e[8] = {lo[u].x, lo[u].y, lo[u].z, lo[u].w, hi[u].x, hi[u].y, hi[u].z, hi[u].w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = __fmaf_rn(w, e[i], acc[i]);
+    }
+    m = mn;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = den > 0.f ? __fdiv_rn(acc[i], den) : 0.f;
+}
+
 // REGX (a whole row is one stage, nb <= 8U): each lane touches the same <= U super-block columns
 // in every row, so its activations are read from LDS once into registers and every row after
 // that is pure weight streaming + VALU (no per-row LDS traffic).
@@ -573,7 +624,36 @@ __device__ __forceinline__ void qgemv_body(const GemvArgs& a, const int bid) {
   float* dxs = reinterpret_cast<float*>(lds + T * xstride);
   float* sxs = dxs + T * (K >> 5);
   float* red = sxs + T * (K >> 4);                   // [W][T] block-reduction scratch
-  if (a.xf == nullptr) {
+  if (a.po) {
+    // attention partials: merge each head's context chunks and quantise to Q8 (per token the
+    // thread mapping does not depend on T); lane quads = 32-value blocks (K % 256 == 0)
+    const int nch = K >> 3;
+    for (int i = threadIdx.x; i < T * nch; i += blockDim.x) {
+      const int t = i / nch, c = i - t * nch;
+      float v[8];
+      merge_chunk8(a, t, c, v);
+      float amax = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) amax = fmaxf(amax, fabsf(v[k]));
+      amax = fmaxf(amax, dppf<kDppXor1>(amax));
+      amax = fmaxf(amax, dppf<kDppXor2>(amax));
+      const float d = amax / 127.f;
+      const float id = d > 0.f ? 1.f / d : 0.f;
+      uint32_t pk0 = 0u, pk1 = 0u;
+      int sq = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int q = (int)__builtin_rintf(v[k] * id);
+        if (k < 4) pk0 |= ((uint32_t)(q & 0xff)) << (8 * k);
+        else pk1 |= ((uint32_t)(q & 0xff)) << (8 * (k - 4));
+        sq += q;
+      }
+      sq += __float_as_int(dppf<kDppXor1>(__int_as_float(sq)));
+      *reinterpret_cast<uint2*>(xs + t * xstride + xoff(c * 8)) = make_uint2(pk0, pk1);
+      if ((c & 3) == 0) dxs[t * (K >> 5) + (c >> 2)] = d;
+      if ((c & 1) == 0) sxs[t * (K >> 4) + (c >> 1)] = d * (float)sq;
+    }
+  } else if (a.xf == nullptr) {
     // Q8 input: copy into LDS.  x8 [T][K], dx [T][K/32] and sx [T][K/16] are read as flat arrays
     // (index i = one 16-byte x8 unit = one sx value; dx for i < T*K/32), four units per thread
     // per round with every load of the round issued before any LDS store (clamped indices, no
@@ -1838,7 +1918,7 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
   gemv_shape(N, K, T, waves, rows_per_wg);
   if (ox8 && waves * 64 < 32 * T) return 2;
   if (waves < 1 || waves > 8 || rows_per_wg < 1) return 2;
-  GemvArgs a;
+  GemvArgs a{};                               // every field not set below stays null / 0
   a.w0 = {static_cast<const uint8_t*>(w0q), static_cast<const uint8_t*>(w0qh),
           static_cast<const int8_t*>(w0sc), static_cast<const uint16_t*>(w0d)};
   a.w1 = {static_cast<const uint8_t*>(w1q), static_cast<const uint8_t*>(w1qh),
@@ -1919,6 +1999,35 @@ int amdk8s_llm_qgemv2(int type0, const void* w0q, const void* w0qh, const void* 
   return dispatch2_t<kQ6K, kQ6K>(a[0], a[1], waves, st);
 }
 
+// o_proj with the attention combine in its prologue: out[t][n] += W.y_t where y_t is merged from
+// the decode-attention partials po / pml (written by amdk8s_llm_attn_decode with x8 = null, split
+// kernel) — the combine launch disappears.  K = heads * 128.
+int amdk8s_llm_qgemv_attn(int type, const void* wq, const void* wqh, const void* wsc,
+                          const void* wd, const void* po, const void* pml, const void* pos,
+                          int nsplit, int chunk, void* out, int ldo, int N, int K, int T,
+                          int waves, int rows_per_wg, void* stream) {
+  if (K % 256 || N <= 0 || T < 1 || T > kMaxTok || !po || !pml || !pos || nsplit < 1 ||
+      chunk < 1)
+    return 2;
+  if (waves <= 0) waves = 8;
+  if (rows_per_wg <= 0) rows_per_wg = 16;
+  if (waves > 8 || rows_per_wg < 1) return 2;
+  GemvArgs a = GemvArgs{};
+  a.w0 = {static_cast<const uint8_t*>(wq), static_cast<const uint8_t*>(wqh),
+          static_cast<const int8_t*>(wsc), static_cast<const uint16_t*>(wd)};
+  a.out = static_cast<float*>(out);
+  a.ldo = ldo; a.N = N; a.K = K; a.T = T; a.rows_per_wg = rows_per_wg;
+  a.po = static_cast<const float*>(po);
+  a.pml = static_cast<const float*>(pml);
+  a.apos = static_cast<const int*>(pos);
+  a.nsplit = nsplit;
+  a.chunk = chunk;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (type == kQ4K) return dispatch_t<kQ4K, kResid>(a, waves, st);
+  if (type == kQ6K) return dispatch_t<kQ6K, kResid>(a, waves, st);
+  return 2;
+}
+
 int amdk8s_llm_rmsnorm_q8(const void* x, const void* w, float eps, int K, int T, void* x8,
                           void* dx, void* sx, void* stream) {
   if (K % 256 || T < 1) return 2;
@@ -1965,8 +2074,10 @@ int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* 
   if (qkv && (!cos_t || !sin_t)) return 2;
   if (impl == 0) impl = attn_impl_default();
   if (impl == 2 && cnt) return 2;        // the in-launch combine is a split-kernel form only
+  if (impl == 2 && !(x8 && dx && sx)) return 2;   // MFMA: writes the Q8 output itself
+  if (cnt && !(x8 && dx && sx)) return 2;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  AttnArgs aa;
+  AttnArgs aa{};
   aa.q = static_cast<const float*>(q);
   aa.qkv = static_cast<const float*>(qkv);
   aa.ldq = ldq;
@@ -2015,6 +2126,7 @@ int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* 
                          dim3(256), 0, st, aa);
     });
     if (rc || cnt) return rc;            // in-kernel combine
+    if (!x8) return rc;                  // partials only: the o_proj prologue merges them
   }
   hipLaunchKernelGGL(attn_combine_q8_kernel, dim3(H, T), dim3(128), 0, st,
                      static_cast<const float*>(po), static_cast<const float*>(pml),

@@ -35,6 +35,9 @@ def _lib():
             lib.amdk8s_llm_qgemv2.argtypes = [ci] + [vp] * 4 + [ci, vp, vp] + [ci] + [vp] * 4 \
                 + [ci, vp, vp] + [ci, vp, vp, vp, vp, ci, vp, cf, ci, ci, ci, ci, vp]
             lib.amdk8s_llm_qgemv2.restype = ci
+            lib.amdk8s_llm_qgemv_attn.argtypes = [ci] + [vp] * 4 + [vp, vp, vp, ci, ci, vp, ci, ci,
+                                                                  ci, ci, ci, ci, vp]
+            lib.amdk8s_llm_qgemv_attn.restype = ci
             lib.amdk8s_llm_rmsnorm_q8.argtypes = [vp, vp, cf, ci, ci, vp, vp, vp, vp]
             lib.amdk8s_llm_rmsnorm_q8.restype = ci
             lib.amdk8s_llm_rope_kv.argtypes = [vp, ci, vp, vp, vp, vp, ci, ci, ci, ci, vp, vp, vp,
@@ -130,6 +133,19 @@ def qgemv2(w0, w1, x8, dx, sx, out0, out1, bias0=None, bias1=None, rows_per_wg: 
     return True
 
 
+def qgemv_attn(w, po, pml, pos, nsplit: int, out, rows_per_wg: int = 0, waves: int = 0,
+               chunk: int = 0) -> None:
+    """``out[t] += W . y_t`` (resid mode) where y_t, the decode-attention output of token t, is
+    merged from the per-chunk partials ``po`` [T, H, >= nsplit, 128] / ``pml`` [T, H, >= nsplit, 2]
+    (row stride ``nsplit``, as written by :func:`attn_decode` without Q8 outputs) in the GEMV's
+    prologue: no combine launch.  ``chunk``: context positions per partial (0 = attn_chunk())."""
+    t = pos.shape[0]
+    _check(_lib().amdk8s_llm_qgemv_attn(w.qtype, *w.ptrs(), po.data_ptr(), pml.data_ptr(),
+                                        pos.data_ptr(), nsplit, chunk or attn_chunk(),
+                                        out.data_ptr(), out.stride(0), w.n, w.k, t, waves,
+                                        rows_per_wg, _stream(out)), "amdk8s_llm_qgemv_attn")
+
+
 def rmsnorm_q8(x, w, eps: float, x8, dx, sx) -> None:
     t, k = x.shape
     _check(_lib().amdk8s_llm_rmsnorm_q8(x.data_ptr(), _p(w), float(eps), k, t, x8.data_ptr(),
@@ -161,7 +177,8 @@ def attn_decode(q, pos, slot, kc, vc, heads: int, kv_heads: int, head_dim: int, 
     by every call) — the combine then runs inside the attention kernel, one launch instead of two
     (split kernel only).  ``impl``: ATTN_SPLIT (64-position chunks + combine), ATTN_MFMA (one
     workgroup per 1024 positions on MFMA, no combine launch up to 1024) or ATTN_DEFAULT
-    (AMDK8S_LLM_ATTN: split unless it says ``mfma``)."""
+    (AMDK8S_LLM_ATTN: split unless it says ``mfma``).  ``x8 = dx = sx = None`` (split kernel):
+    only the per-chunk partials ``po`` / ``pml`` are written — :func:`qgemv_attn` merges them."""
     if cnt is not None and impl == ATTN_DEFAULT:
         impl = ATTN_SPLIT
     ref = qkv if qkv is not None else q
@@ -169,7 +186,7 @@ def attn_decode(q, pos, slot, kc, vc, heads: int, kv_heads: int, head_dim: int, 
                                          _p(cos_t), _p(sin_t), pos.data_ptr(), slot.data_ptr(),
                                          kc.data_ptr(), vc.data_ptr(), heads, kv_heads, head_dim,
                                          max_ctx, span, float(scale), po.data_ptr(), pml.data_ptr(),
-                                         _p(out), x8.data_ptr(), dx.data_ptr(), sx.data_ptr(),
+                                         _p(out), _p(x8), _p(dx), _p(sx),
                                          ref.shape[0], _p(cnt), int(impl), _stream(ref)),
            "amdk8s_llm_attn_decode")
 

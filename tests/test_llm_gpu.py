@@ -367,6 +367,45 @@ def test_prologue_norm_equals_rmsnorm_kernel(dev, LK, K, T):
     torch.testing.assert_close(a, b, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("T", [1, 4])
+def test_oproj_prologue_combine(dev, LK, T):
+    """o_proj with the attention combine in its prologue (qgemv_attn over the split kernel's
+    partials) against the combine kernel's Q8 output fed to the plain resid GEMV: the same
+    result up to single int8 roundings of the activations."""
+    from k8s_nvidia_gpus_amd.models.llm import gguf
+
+    torch.manual_seed(30 + T)
+    H, Hkv, max_ctx, slots = 28, 4, 1024, 4
+    kc = (torch.randn(slots, Hkv, max_ctx, 128, device=dev) * 0.5).half()
+    vc = torch.randn(slots, Hkv, max_ctx, 128, device=dev).half()
+    pos = torch.tensor([600, 63, 64, 1000][:T], dtype=torch.int32, device=dev)
+    slot = torch.tensor([1, 0, 3, 2][:T], dtype=torch.int32, device=dev)
+    q = torch.randn(T, H * 128, device=dev)
+    nsplit = max_ctx // LK.attn_chunk()
+    po = torch.empty(T, H, nsplit, 128, device=dev)
+    pml = torch.empty(T, H, nsplit, 2, device=dev)
+    x8 = torch.empty(T, H * 128, dtype=torch.int8, device=dev)
+    dx = torch.empty(T, H * 4, device=dev)
+    sx = torch.empty(T, H * 8, device=dev)
+    w, wref = _qw(3584, H * 128, gguf.Q4_K, 15, dev)
+    res = torch.randn(T, 3584, device=dev)
+    LK.attn_decode(q, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po, pml,
+                   x8, dx, sx, impl=LK.ATTN_SPLIT)
+    ref = res.clone()
+    LK.qgemv(w, x8, dx, sx, ref, LK.RESID)
+    po2 = torch.empty_like(po)
+    pml2 = torch.empty_like(pml)
+    LK.attn_decode(q, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po2, pml2,
+                   None, None, None, impl=LK.ATTN_SPLIT)
+    out = res.clone()
+    LK.qgemv_attn(w, po2, pml2, pos, nsplit, out)
+    scale = (ref - res).abs().max().item()
+    torch.testing.assert_close(out, ref, rtol=0, atol=2e-2 * scale)
+    y = _attn_ref(q, kc, vc, pos, slot, H, Hkv)
+    full = res + (y.cpu() @ wref.t()).to(dev)
+    torch.testing.assert_close(out, full, rtol=0, atol=5e-2 * scale)
+
+
 @pytest.mark.parametrize("H,Hkv", [(28, 4), (8, 8), (6, 2)])
 def test_in_kernel_combine_equals_combine_kernel(dev, LK, H, Hkv):
     """The last-arriving workgroup's chunk merge (cnt given) is bit-identical to the separate
@@ -472,13 +511,16 @@ def tiny_gguf(tmp_path_factory):
     return write_synthetic_gguf(str(p), tiny(layers=4, dim=512, heads=4, kv_heads=2, ffn=1024))
 
 
-@pytest.mark.parametrize("resid_norm,norm_prologue", [(False, False), (True, False),
-                                                      (False, True)])
-def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf, resid_norm, norm_prologue):
+@pytest.mark.parametrize("resid_norm,norm_prologue,attn_prologue",
+                         [(False, False, False), (True, False, False), (False, True, False),
+                          (False, True, True)])
+def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf, resid_norm, norm_prologue,
+                                                     attn_prologue):
     from k8s_nvidia_gpus_amd.models.llm.synthetic import load
 
     gpu, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=False)
     gpu.resid_norm, gpu.norm_prologue = resid_norm, norm_prologue
+    gpu.attn_prologue = attn_prologue
     cpu, _ = load(tiny_gguf, device="cpu", max_ctx=512)
     prompt = tok.encode("<|im_start|>user\nhello world, a cozy cabin<|im_end|>\n")
     lg = gpu.prefill(prompt, slot=1)            # native kernels, 4 tokens per step
@@ -497,11 +539,12 @@ def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf, resid_norm,
     assert gpu.stats["graph_captures"] >= 1
 
 
-@pytest.mark.parametrize("resid_norm,fused_combine,norm_prologue",
-                         [(False, False, False), (True, False, False), (True, True, False),
-                          (False, False, True)])
+@pytest.mark.parametrize("resid_norm,fused_combine,norm_prologue,attn_prologue",
+                         [(False, False, False, False), (True, False, False, False),
+                          (True, True, False, False), (False, False, True, False),
+                          (False, False, True, True)])
 def test_engine_batched_decode_equals_single(dev, tiny_gguf, resid_norm, fused_combine,
-                                             norm_prologue):
+                                             norm_prologue, attn_prologue):
     """T sequences in one step give the same logits as each alone: slots are independent and the
     GEMV's roundings are pinned, so the int8 activation quantisation never flips between a batched
     and a single step (batch-invariant serving) — also with the norms fused into the residual
@@ -510,7 +553,7 @@ def test_engine_batched_decode_equals_single(dev, tiny_gguf, resid_norm, fused_c
 
     eng, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=True)
     eng.resid_norm, eng.fused_combine = resid_norm, fused_combine
-    eng.norm_prologue = norm_prologue
+    eng.norm_prologue, eng.attn_prologue = norm_prologue, attn_prologue
     prompts = [tok.encode(s) for s in ("hello", "the quick brown fox", "a cozy cabin in", "you")]
     last = []
     for s, p in enumerate(prompts):
