@@ -136,7 +136,8 @@ class Engine:
         self.qkv2 = os.environ.get("AMDK8S_LLM_QKV2", "1") != "0"
         # the attention combine inside the o_proj GEMV prologue (LK.qgemv_attn: each o_proj
         # workgroup merges the chunk partials of every head itself) instead of its own launch;
-        # "waves,rows" of that GEMV in AMDK8S_LLM_ATTN_OPROJ
+        # "waves,rows" of that GEMV in AMDK8S_LLM_ATTN_OPROJ.  Measured neutral at T=1 and slower
+        # from T=2 (1.758 / 2.65 -> 1.758 / 2.87 ms at T=1 / 4, profiles/r03/af): off by default
         self.attn_prologue = os.environ.get("AMDK8S_LLM_ATTN_PROLOGUE", "0") != "0"
         self.attn_oproj_cfg = dict(zip(("waves", "rows_per_wg"), map(int, os.environ.get(
             "AMDK8S_LLM_ATTN_OPROJ", "8,16").split(","))))
