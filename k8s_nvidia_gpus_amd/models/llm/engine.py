@@ -143,6 +143,8 @@ class Engine:
             "AMDK8S_LLM_ATTN_OPROJ", "8,16").split(","))))
         # dense prefill on the fused glue kernels (llm_prefill.hip); 0 = the PyTorch formulation
         self.prefill_native = os.environ.get("AMDK8S_LLM_PREFILL_NATIVE", "1") != "0"
+        # native prefill: SDPA with enable_gqa on the cache slabs (no repeat_interleave copies)
+        self.prefill_gqa = os.environ.get("AMDK8S_LLM_PREFILL_GQA", "0") != "0"
         # attn_norm / ffn_norm inside the q|k|v and gate|up GEMV prologues (each workgroup
         # normalises the L2-resident fp32 row itself) instead of two rmsnorm_q8 launches per
         # layer; the gate|up -> Q8 hand-off to ffn_down and the final norm stay as they are.
@@ -251,10 +253,18 @@ class Engine:
             qkv = mm(xn, W[f"{i}.qkv"], W[f"{i}.bqkv"])
             LK.rope_kv_f16(qkv, self.cos, self.sin, start, c.heads, c.kv_heads, self.max_ctx, qh,
                            self.k_cache[i, slot], self.v_cache[i, slot])
-            kk = self.k_cache[i, slot, :, :end].repeat_interleave(c.group, 0)
-            vv = self.v_cache[i, slot, :, :end].repeat_interleave(c.group, 0)
-            o = F.scaled_dot_product_attention(qh[None], kk[None], vv[None],
-                                               attn_mask=None if mask is None else mask[None, None])
+            if self.prefill_gqa:       # K/V read in place by SDPA's GQA path; causal flag from 0
+                o = F.scaled_dot_product_attention(
+                    qh[None], self.k_cache[i, slot, :, :end][None],
+                    self.v_cache[i, slot, :, :end][None],
+                    attn_mask=None if (mask is None or start == 0) else mask[None, None],
+                    is_causal=mask is not None and start == 0, enable_gqa=True)
+            else:
+                kk = self.k_cache[i, slot, :, :end].repeat_interleave(c.group, 0)
+                vv = self.v_cache[i, slot, :, :end].repeat_interleave(c.group, 0)
+                o = F.scaled_dot_product_attention(
+                    qh[None], kk[None], vv[None],
+                    attn_mask=None if mask is None else mask[None, None])
             o = o[0].transpose(0, 1).reshape(P, c.dim)
             x = mm_res(x, o, W[f"{i}.o"])
             LK.rmsnorm_f16(x, L.ffn_norm, c.eps, xn)
