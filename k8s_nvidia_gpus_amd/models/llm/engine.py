@@ -189,7 +189,8 @@ class Engine:
     def _forward_dense(self, tokens: torch.Tensor, slot: int, start: int) -> torch.Tensor:
         """Prompt tokens [P] of one sequence at positions start..start+P-1 → last-position logits
         (fp32 [vocab]).  Writes the KV cache."""
-        if self.gpu and self.prefill_native and self.cfg.head_dim == 128:
+        if (self.gpu and self.prefill_native and self.cfg.head_dim == 128
+                and self.cfg.dim <= 8192 and self.cfg.dim % 8 == 0 and self.cfg.ffn % 8 == 0):
             return self._forward_dense_native(tokens, slot, start)
         c = self.cfg
         W = self.dense_weights()

@@ -26,3 +26,12 @@ timeout -k 10 300 rocprofv3 --kernel-trace --output-format rocpd -d $OUT/prof_t1
   || { tail -20 $OUT/prof_t1.log; exit 1; }
 python3 tools/rocpd_summary.py $(find $OUT/prof_t1 -name '*.db' | head -1) --after-gap-ms 200 \
   --per 64 --top 30 > $OUT/llm_decode_t1_kernels.txt && head -12 $OUT/llm_decode_t1_kernels.txt | cut -c1-150
+# older GEMV knobs re-measured on the current kernels (tools/gpu_r03_ah.sh)
+OUT=gpurun_out/r03/ah
+mkdir -p $OUT
+for cfg in "2 0" "4 0" "2 1" "4 1"; do
+  set -- $cfg
+  AMDK8S_LLM_REGX_T=$1 AMDK8S_LLM_LONGROW=$2 timeout -k 10 300 python -u tools/llm_bench.py --steps 96 \
+    --out $OUT/llm_bench_rx$1_lr$2.json > $OUT/llm_bench_rx$1_lr$2.log 2>&1 || { tail -30 $OUT/llm_bench_rx$1_lr$2.log; exit 1; }
+  echo "regx_t=$1 longrow=$2"; grep -E "decode" $OUT/llm_bench_rx$1_lr$2.log | grep -v '^{'
+done
