@@ -1772,15 +1772,17 @@ static int attn_impl_default() {
   return v;
 }
 
-// AMDK8S_LLM_LONGROW=1: long rows in two balanced stages instead of KB-wide ones (A/B knob;
-// measured neutral to slightly slower on MI355X — profiles/r03/q — so off by default).
-static bool longrow_enabled() {
-  static int v = -1;
-  if (v < 0) {
+// Long rows (ffn_down: 74 super-blocks) in two balanced stages (U = ceil(nb / 16)) instead of
+// KB-wide ones: measured slower at T = 1 (1.754 -> 1.787 ms) and faster from T = 3 (T=3 / T=4
+// 2.43 / 2.64 -> 2.39 / 2.60 ms, profiles/r03/ag), so on from T = 3.  AMDK8S_LLM_LONGROW=0 / 1
+// forces it off / on for every T.  The stage width never changes a result bit.
+static bool longrow_enabled(int T) {
+  static int v = -2;
+  if (v == -2) {
     const char* e = getenv("AMDK8S_LLM_LONGROW");
-    v = (e && e[0] == '1');
+    v = e ? (e[0] == '1') : -1;
   }
-  return v != 0;
+  return v < 0 ? T >= 3 : v != 0;
 }
 
 template <int TYPE, int T, int MODE>
@@ -1798,7 +1800,7 @@ int launch_gemv(const GemvArgs& a, int waves, hipStream_t st) {
   if constexpr (MODE != kPair) {
     // long rows (ffn_down: 74 super-blocks): two stages per row with U = ceil(nb / 16) instead of
     // KB-wide stages whose last one is mostly clamped lanes (74 = 32 + 32 + 10 at U = 4)
-    if (longrow_enabled()) {
+    if (longrow_enabled(T)) {
       const int u2 = (nb + 15) / 16;
       if (u2 == 5) return launch_one<TYPE, T, MODE, 5, false>(a, waves, st);
       if (u2 == 6) return launch_one<TYPE, T, MODE, 6, false>(a, waves, st);

@@ -26,6 +26,13 @@ timeout -k 10 300 rocprofv3 --kernel-trace --output-format rocpd -d $OUT/prof_t1
   || { tail -20 $OUT/prof_t1.log; exit 1; }
 python3 tools/rocpd_summary.py $(find $OUT/prof_t1 -name '*.db' | head -1) --after-gap-ms 200 \
   --per 64 --top 30 > $OUT/llm_decode_t1_kernels.txt && head -12 $OUT/llm_decode_t1_kernels.txt | cut -c1-150
+# kernel arguments in device memory (HIP_FORCE_DEV_KERNARG=1): does the per-kernel floor move?
+for k in 0 1; do
+  HIP_FORCE_DEV_KERNARG=$k timeout -k 10 300 python -u tools/llm_bench.py --steps 96 \
+    --out gpurun_out/r03/ag/llm_bench_devkernarg$k.json > gpurun_out/r03/ag/llm_bench_devkernarg$k.log 2>&1 \
+    || { tail -30 gpurun_out/r03/ag/llm_bench_devkernarg$k.log; exit 1; }
+  echo "HIP_FORCE_DEV_KERNARG=$k"; grep -E "decode|prefill" gpurun_out/r03/ag/llm_bench_devkernarg$k.log | grep -v '^{'
+done
 # older GEMV knobs re-measured on the current kernels (tools/gpu_r03_ah.sh)
 OUT=gpurun_out/r03/ah
 mkdir -p $OUT
