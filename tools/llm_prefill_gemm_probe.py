@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""The LLM prompt-prefill GEMMs (Qwen2.5-7B layout, fp16, M = prompt tokens): every path of
+ops/gemm_epi.py against hipBLASLt (torch) — the planner's pick, the 256x256 w4a kernel, the
+wave-grid family with each block tile and split-K factor.
+
+    python tools/llm_prefill_gemm_probe.py [--m 512] [--out probe.json]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from k8s_nvidia_gpus_amd.ops import gemm_epi as GE  # noqa: E402
+
+SHAPES = (("qkv", 4608, 3584, "store"), ("o", 3584, 3584, "resid"),
+          ("gate_up", 37888, 3584, "store"), ("down", 3584, 18944, "resid"))
+
+
+def bench(fn, iters=30):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters * 1e6
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, default=512)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    rows = []
+    for name, n, k, kind in SHAPES:
+        m = a.m
+        x = torch.randn(m, k, device=dev, dtype=torch.float16)
+        w = torch.randn(n, k, device=dev, dtype=torch.float16) / k ** 0.5
+        res = torch.zeros(m, n, device=dev)
+        flop = 2.0 * m * n * k
+
+        def run():
+            return GE.linear(x, w) if kind == "store" else GE.linear_residual_(res, x, w)
+
+        def rec(variant, us):
+            r = {"gemm": name, "m": m, "n": n, "k": k, "variant": variant, "us": round(us, 1),
+                 "tflops": round(flop / us / 1e6, 1)}
+            rows.append(r)
+            print(r, flush=True)
+
+        rec(f"auto plan={GE.plan(m, n, k)} w4a={GE.use_w4a(m, n, k, x.dtype)}", bench(run))
+        rec("torch", bench(lambda: F.linear(x, w)))
+        wide = GE._WIDE
+        GE._WIDE = "epi"
+        for tile in range(len(GE.TILES)):
+            for sp in (1, 2, 4):
+                GE.set_tile(tile)
+                GE.set_splits(sp)
+                try:
+                    rec(f"epi tile={GE.TILES[tile]} splits={sp}", bench(run))
+                except RuntimeError as e:
+                    print(f"{name} tile {tile} splits {sp}: {e}", flush=True)
+        GE.set_tile(-1)
+        GE.set_splits(-1)
+        GE._WIDE = wide
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(rows, f)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
