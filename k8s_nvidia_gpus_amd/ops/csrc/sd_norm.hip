@@ -374,6 +374,155 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(
   }
 }
 
+// ---- single-launch GroupNorm for small images --------------------------------------------------
+// Every launch of this stack costs ~4.5 us of device time whatever it does (profiles/r03/z), so
+// the two-launch form above spends most of its ~17 us on two floors at the UNet's sizes.  Here a
+// block owns a GROUP SET — lcm(Cg, 8) channels, i.e. whole groups AND whole 16-byte vectors — of one
+// image, so no block needs another's statistics: it walks the set's rows once for the sums (same
+// per-thread vector-column scheme and in-block tree as gn_partial), turns them into (mean, rstd)
+// per group in LDS, and walks the rows again for the apply (L1 / L2-warm).  Used when a set's rows
+// are small (gn_fused_ok); the VAE's 512² activations keep the two-launch form.
+struct GnSet {
+  int N, HW, C, G, Cg, VS, GS, R;   // VS vectors / GS groups per set, R row slots per block
+};
+
+template <bool BF16, bool SILU>
+__global__ void gn_fused(const uint16_t* __restrict__ x, const uint16_t* __restrict__ add,
+                         long add_stride, uint16_t* __restrict__ y, const uint16_t* __restrict__ w,
+                         const uint16_t* __restrict__ b, float eps, GnSet s) {
+  const int set = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
+  const int vs = tid % s.VS, r = tid / s.VS;
+  const int c0 = (set * s.VS + vs) * 8;
+  const int g_lo = c0 / s.Cg, g_hi = (c0 + 7) / s.Cg;
+  const int split = min(8, (g_lo + 1) * s.Cg - c0);  // elements [0, split) are in g_lo
+  float ad[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (add) unpack8<BF16>(*reinterpret_cast<const uint4*>(add + n * add_stride + c0), ad);
+  const size_t off = ((size_t)n * s.HW) * s.C + c0;
+  float s_lo = 0.f, q_lo = 0.f, s_hi = 0.f, q_hi = 0.f;
+  if (r < s.R) {
+#pragma unroll 8
+    for (int row = r; row < s.HW; row += s.R) {
+      const uint4 v = *reinterpret_cast<const uint4*>(x + off + (size_t)row * s.C);
+      float f[8];
+      unpack8<BF16>(v, f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        f[i] += ad[i];
+        if (i < split) {
+          s_lo += f[i];
+          q_lo += f[i] * f[i];
+        } else {
+          s_hi += f[i];
+          q_hi += f[i] * f[i];
+        }
+      }
+    }
+  }
+  // per thread (count, mean, M2) for its lo / hi group part, then Chan merges over the row slots
+  // and the set's vectors: no sum-of-squares cancellation at large means (a group's sum of squares
+  // over a whole 64x64 image would lose the variance in fp32)
+  extern __shared__ float lds[];
+  float* red = lds;                                    // [R][VS][6]: lo (n, mean, m2), hi (...)
+  float2* st = reinterpret_cast<float2*>(lds + ((s.R * s.VS * 6 + 1) & ~1));   // [GS]
+  {
+    const int rows_t = r < s.R ? (s.HW - r + s.R - 1) / s.R : 0;
+    const float n_lo = (float)(rows_t * split), n_hi = (float)(rows_t * (8 - split));
+    const float m_lo = n_lo > 0.f ? s_lo / n_lo : 0.f, m_hi = n_hi > 0.f ? s_hi / n_hi : 0.f;
+    float* e = red + (r * s.VS + vs) * 6;
+    e[0] = n_lo; e[1] = m_lo; e[2] = fmaxf(q_lo - s_lo * m_lo, 0.f);
+    e[3] = n_hi; e[4] = m_hi; e[5] = fmaxf(q_hi - s_hi * m_hi, 0.f);
+  }
+  __syncthreads();
+  auto chan = [](float* a, const float* b) {           // a <- merge(a, b) for (n, mean, m2)
+    const float n = a[0] + b[0];
+    if (b[0] > 0.f) {
+      const float d = b[1] - a[1], f = b[0] / n;
+      a[1] += d * f;
+      a[2] += b[2] + d * d * a[0] * f;
+      a[0] = n;
+    }
+  };
+  int span = 1;
+  while (span < s.R) span <<= 1;
+  for (int stp = span >> 1; stp > 0; stp >>= 1) {     // tree over the row slots
+    if (r < stp && r + stp < s.R) {
+      float* e = red + (r * s.VS + vs) * 6;
+      const float* o = red + ((r + stp) * s.VS + vs) * 6;
+      chan(e, o);
+      chan(e + 3, o + 3);
+    }
+    __syncthreads();
+  }
+  for (int gg = tid; gg < s.GS; gg += blockDim.x) {
+    const int g = set * s.GS + gg;
+    const int cbeg = g * s.Cg, cend = cbeg + s.Cg;
+    float acc[3] = {0.f, 0.f, 0.f};
+    for (int v = cbeg / 8; v <= (cend - 1) / 8; ++v) {
+      const int lv = v - set * s.VS;
+      chan(acc, red + lv * 6 + (v * 8 / s.Cg == g ? 0 : 3));
+    }
+    st[gg] = make_float2(acc[1], rsqrtf((acc[0] > 0.f ? acc[2] / acc[0] : 0.f) + eps));
+  }
+  __syncthreads();
+  if (r >= s.R) return;
+  float a[8], sh[8], wv[8], bv[8];
+  unpack8<BF16>(*reinterpret_cast<const uint4*>(w + c0), wv);
+  unpack8<BF16>(*reinterpret_cast<const uint4*>(b + c0), bv);
+  const float2 st_lo = st[g_lo - set * s.GS];
+  const float2 st_hi = st[g_hi - set * s.GS];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const bool lo = (c0 + i) / s.Cg == g_lo;
+    const float mean = lo ? st_lo.x : st_hi.x, rstd = lo ? st_lo.y : st_hi.y;
+    a[i] = rstd * wv[i];
+    sh[i] = bv[i] - mean * a[i] + (add ? ad[i] * a[i] : 0.f);
+  }
+#pragma unroll 8
+  for (int row = r; row < s.HW; row += s.R) {
+    const size_t o = off + (size_t)row * s.C;
+    const uint4 v = *reinterpret_cast<const uint4*>(x + o);
+    float f[8];
+    unpack8<BF16>(v, f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float t = f[i] * a[i] + sh[i];
+      if constexpr (SILU) t = t / (1.f + __expf(-t));
+      f[i] = t;
+    }
+    *reinterpret_cast<uint4*>(y + o) = pack8<BF16>(f);
+  }
+}
+
+int gcd_int(int a, int b) { return b == 0 ? a : gcd_int(b, a % b); }
+
+GnSet gn_set_shape(int N, int HW, int C, int G) {
+  GnSet s{};
+  s.N = N; s.HW = HW; s.C = C; s.G = G; s.Cg = C / G;
+  const int set = s.Cg / gcd_int(s.Cg, 8) * 8;       // lcm(Cg, 8) channels
+  s.VS = set / 8;
+  s.GS = set / s.Cg;
+  s.R = 1024 / s.VS;
+  if (s.R > HW) s.R = HW;
+  return s;
+}
+
+// AMDK8S_GN_FUSED=0 keeps the two-launch form everywhere (A/B); otherwise a set's rows up to
+// 384 KB (every SD1.5 UNet GroupNorm at 512², none of the VAE decoder's full-resolution ones) and
+// at least 8 blocks use gn_fused.
+int g_gn_fused_force = -1;                  // amdk8s_groupnorm_set_fused (tests / A/B)
+
+bool gn_fused_ok(int N, int HW, int C, int G) {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("AMDK8S_GN_FUSED");
+    v = e ? atoi(e) : 1;
+  }
+  if (!(g_gn_fused_force >= 0 ? g_gn_fused_force : v)) return false;
+  const GnSet s = gn_set_shape(N, HW, C, G);
+  if (C % (s.VS * 8) || s.VS > 64) return false;
+  return (long)HW * s.VS * 16 <= 384 * 1024 && N * (C / (s.VS * 8)) >= 8;
+}
+
 // pass = 1: stats pass shape; pass = 2: apply pass shape
 GnShape gn_shape(int N, int HW, int C, int G, int pass) {
   GnShape s{};
@@ -416,6 +565,9 @@ extern "C" {
 
 int amdk8s_groupnorm_supported(int C, int G) { return gn_supported(C, G) ? 1 : 0; }
 
+// 1 / 0: single-launch GroupNorm where it applies / never; -1: AMDK8S_GN_FUSED (default on).
+void amdk8s_groupnorm_set_fused(int v) { g_gn_fused_force = v; }
+
 // Workspace floats needed by amdk8s_groupnorm_nhwc (the stats pass's chunk partials).
 long amdk8s_groupnorm_workspace(int N, int HW, int C, int G) {
   GnShape s = gn_shape(N, HW, C, G, 1);
@@ -429,6 +581,25 @@ int amdk8s_groupnorm_nhwc(const void* x, const void* add, long add_stride, void*
                           const void* b, float* workspace, int N, int HW, int C, int G, float eps,
                           int silu, int dtype, hipStream_t stream) {
   if (N <= 0 || HW <= 0 || !gn_supported(C, G)) return -1;
+  if (gn_fused_ok(N, HW, C, G)) {
+    const GnSet fs = gn_set_shape(N, HW, C, G);
+    const dim3 grid(C / (fs.VS * 8), N), block(fs.VS * fs.R);
+    const size_t lds = ((size_t)((fs.R * fs.VS * 6 + 1) & ~1) + 2 * fs.GS) * sizeof(float);
+    const auto* xi = static_cast<const uint16_t*>(x);
+    const auto* ai = static_cast<const uint16_t*>(add);
+    auto* yo = static_cast<uint16_t*>(y);
+    const auto* wi = static_cast<const uint16_t*>(w);
+    const auto* bi = static_cast<const uint16_t*>(b);
+    if (dtype == 1 && silu)
+      hipLaunchKernelGGL((gn_fused<true, true>), grid, block, lds, stream, xi, ai, add_stride, yo, wi, bi, eps, fs);
+    else if (dtype == 1)
+      hipLaunchKernelGGL((gn_fused<true, false>), grid, block, lds, stream, xi, ai, add_stride, yo, wi, bi, eps, fs);
+    else if (silu)
+      hipLaunchKernelGGL((gn_fused<false, true>), grid, block, lds, stream, xi, ai, add_stride, yo, wi, bi, eps, fs);
+    else
+      hipLaunchKernelGGL((gn_fused<false, false>), grid, block, lds, stream, xi, ai, add_stride, yo, wi, bi, eps, fs);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+  }
   GnShape s = gn_shape(N, HW, C, G, 1);
   GnShape s2 = gn_shape(N, HW, C, G, 2);
   const int threads = s.VC * s.R, threads2 = s2.VC * s2.R;

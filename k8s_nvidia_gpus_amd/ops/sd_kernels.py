@@ -27,6 +27,8 @@ def _lib():
             vp, ci, cl, cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
             lib.amdk8s_groupnorm_supported.argtypes = [ci, ci]
             lib.amdk8s_groupnorm_supported.restype = ci
+            lib.amdk8s_groupnorm_set_fused.argtypes = [ci]
+            lib.amdk8s_groupnorm_set_fused.restype = None
             lib.amdk8s_groupnorm_workspace.argtypes = [ci, ci, ci, ci]
             lib.amdk8s_groupnorm_workspace.restype = cl
             lib.amdk8s_groupnorm_nhwc.argtypes = [vp, vp, cl, vp, vp, vp, vp, ci, ci, ci, ci, cf,
@@ -59,6 +61,12 @@ def _check(rc: int, what: str) -> None:
 
 def group_norm_supported(c: int, groups: int) -> bool:
     return bool(_lib().amdk8s_groupnorm_supported(c, groups))
+
+
+def set_group_norm_fused(v: int) -> None:
+    """1: the single-launch GroupNorm wherever it applies, 0: always the two-launch form,
+    -1: AMDK8S_GN_FUSED (default on)."""
+    _lib().amdk8s_groupnorm_set_fused(int(v))
 
 
 def group_norm_nhwc(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, groups: int,

@@ -32,7 +32,9 @@ def _gn_ref(x, w, b, g, eps, silu):
                                           ((4, 960, 32, 32), 32), ((1, 128, 128, 128), 32),
                                           ((3, 32, 5, 7), 8)])
 @pytest.mark.parametrize("silu", [False, True])
-def test_group_norm_nhwc_vs_fp32(SK, dev, dtype, shape, groups, silu):
+@pytest.mark.parametrize("fused", [1, 0])           # single-launch group-set form / two launches
+def test_group_norm_nhwc_vs_fp32(SK, dev, dtype, shape, groups, silu, fused):
+    SK.set_group_norm_fused(fused)
     g = torch.Generator(device=dev).manual_seed(0)
     x = (torch.randn(shape, generator=g, device=dev) * 3 + 1.5).to(dtype)
     x = x.contiguous(memory_format=torch.channels_last)
@@ -42,7 +44,23 @@ def test_group_norm_nhwc_vs_fp32(SK, dev, dtype, shape, groups, silu):
     assert y.is_contiguous(memory_format=torch.channels_last)
     ref = _gn_ref(x, w, b, groups, 1e-5, silu)
     tol = 2e-2 if dtype == torch.bfloat16 else 4e-3
+    SK.set_group_norm_fused(-1)
     torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("fused", [1, 0])
+def test_group_norm_large_mean_both_forms(SK, dev, fused):
+    """Mean 200, unit variance: the single-launch form's per-thread (n, mean, M2) + Chan merges keep
+    the variance that a whole-image sum of squares would lose in fp32."""
+    SK.set_group_norm_fused(fused)
+    g = torch.Generator(device=dev).manual_seed(4)
+    x = (torch.randn(2, 640, 32, 32, generator=g, device=dev) + 200.0).half()
+    x = x.contiguous(memory_format=torch.channels_last)
+    w = torch.ones(640, device=dev).half()
+    b = torch.zeros(640, device=dev).half()
+    y = SK.group_norm_nhwc(x, w, b, 32, 1e-5, True)
+    SK.set_group_norm_fused(-1)
+    torch.testing.assert_close(y.float(), _gn_ref(x, w, b, 32, 1e-5, True), rtol=2e-2, atol=2e-2)
 
 
 def test_group_norm_rows_layout_and_determinism(SK, dev):
