@@ -507,8 +507,9 @@ GnSet gn_set_shape(int N, int HW, int C, int G) {
 }
 
 // AMDK8S_GN_FUSED=0 keeps the two-launch form everywhere (A/B); otherwise a set's rows up to
-// 384 KB (every SD1.5 UNet GroupNorm at 512², none of the VAE decoder's full-resolution ones) and
-// at least 8 blocks use gn_fused.
+// AMDK8S_GN_FUSED_KB (default 64 KB: the UNet's 16² and 8² levels) and at least 8 blocks use
+// gn_fused.  At 384 KB (every UNet GroupNorm at 512²) the 64² ones ran on 16 blocks and the pass
+// got slower (6.74 -> 6.94 ms, profiles/r03/ak): one CU cannot stream a set's rows fast enough.
 int g_gn_fused_force = -1;                  // amdk8s_groupnorm_set_fused (tests / A/B)
 
 bool gn_fused_ok(int N, int HW, int C, int G) {
@@ -518,9 +519,15 @@ bool gn_fused_ok(int N, int HW, int C, int G) {
     v = e ? atoi(e) : 1;
   }
   if (!(g_gn_fused_force >= 0 ? g_gn_fused_force : v)) return false;
+  static long kb = -1;
+  if (kb < 0) {
+    const char* e = getenv("AMDK8S_GN_FUSED_KB");
+    kb = e ? atol(e) : 64;
+  }
   const GnSet s = gn_set_shape(N, HW, C, G);
   if (C % (s.VS * 8) || s.VS > 64) return false;
-  return (long)HW * s.VS * 16 <= 384 * 1024 && N * (C / (s.VS * 8)) >= 8;
+  if (g_gn_fused_force == 2) return true;            // every supported shape (tests)
+  return (long)HW * s.VS * 16 <= kb * 1024 && N * (C / (s.VS * 8)) >= 8;
 }
 
 // pass = 1: stats pass shape; pass = 2: apply pass shape
@@ -565,7 +572,8 @@ extern "C" {
 
 int amdk8s_groupnorm_supported(int C, int G) { return gn_supported(C, G) ? 1 : 0; }
 
-// 1 / 0: single-launch GroupNorm where it applies / never; -1: AMDK8S_GN_FUSED (default on).
+// 1 / 0: single-launch GroupNorm where it applies / never; 2: wherever the shape allows (tests);
+// -1: AMDK8S_GN_FUSED (default on).
 void amdk8s_groupnorm_set_fused(int v) { g_gn_fused_force = v; }
 
 // Workspace floats needed by amdk8s_groupnorm_nhwc (the stats pass's chunk partials).

@@ -64,8 +64,8 @@ def group_norm_supported(c: int, groups: int) -> bool:
 
 
 def set_group_norm_fused(v: int) -> None:
-    """1: the single-launch GroupNorm wherever it applies, 0: always the two-launch form,
-    -1: AMDK8S_GN_FUSED (default on)."""
+    """1: the single-launch GroupNorm where it pays (small images), 2: for every supported shape
+    (tests), 0: always the two-launch form, -1: AMDK8S_GN_FUSED (default on)."""
     _lib().amdk8s_groupnorm_set_fused(int(v))
 
 

@@ -32,7 +32,7 @@ def _gn_ref(x, w, b, g, eps, silu):
                                           ((4, 960, 32, 32), 32), ((1, 128, 128, 128), 32),
                                           ((3, 32, 5, 7), 8)])
 @pytest.mark.parametrize("silu", [False, True])
-@pytest.mark.parametrize("fused", [1, 0])           # single-launch group-set form / two launches
+@pytest.mark.parametrize("fused", [2, 0])           # single-launch group-set form / two launches
 def test_group_norm_nhwc_vs_fp32(SK, dev, dtype, shape, groups, silu, fused):
     SK.set_group_norm_fused(fused)
     g = torch.Generator(device=dev).manual_seed(0)
@@ -48,7 +48,7 @@ def test_group_norm_nhwc_vs_fp32(SK, dev, dtype, shape, groups, silu, fused):
     torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
 
 
-@pytest.mark.parametrize("fused", [1, 0])
+@pytest.mark.parametrize("fused", [2, 0])
 def test_group_norm_large_mean_both_forms(SK, dev, fused):
     """Mean 200, unit variance: the single-launch form's per-thread (n, mean, M2) + Chan merges keep
     the variance that a whole-image sum of squares would lose in fp32."""
