@@ -507,7 +507,8 @@ GnSet gn_set_shape(int N, int HW, int C, int G) {
 }
 
 // AMDK8S_GN_FUSED=0 keeps the two-launch form everywhere (A/B); otherwise a set's rows up to
-// AMDK8S_GN_FUSED_KB (default 64 KB: the UNet's 16² and 8² levels) and at least 8 blocks use
+// AMDK8S_GN_FUSED_KB (default 128 KB: the UNet levels up to 32², 6.58 -> 6.55 ms against 64 KB,
+// profiles/r03/am) and at least 8 blocks use
 // gn_fused.  At 384 KB (every UNet GroupNorm at 512²) the 64² ones ran on 16 blocks and the pass
 // got slower (6.74 -> 6.94 ms, profiles/r03/ak): one CU cannot stream a set's rows fast enough.
 int g_gn_fused_force = -1;                  // amdk8s_groupnorm_set_fused (tests / A/B)
@@ -522,7 +523,7 @@ bool gn_fused_ok(int N, int HW, int C, int G) {
   static long kb = -1;
   if (kb < 0) {
     const char* e = getenv("AMDK8S_GN_FUSED_KB");
-    kb = e ? atol(e) : 64;
+    kb = e ? atol(e) : 128;
   }
   const GnSet s = gn_set_shape(N, HW, C, G);
   if (C % (s.VS * 8) || s.VS > 64) return false;
