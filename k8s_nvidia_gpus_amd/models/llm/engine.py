@@ -73,6 +73,7 @@ class StepBuffers:
     t: torch.Tensor
     logits: torch.Tensor
     graphs: Dict[tuple, torch.cuda.CUDAGraph] = None   # keyed by (attention span, fused rope)
+    ids: torch.Tensor = None         # int32 [T]: greedy next tokens (decode_greedy)
     meta: torch.Tensor = None        # int32 [3, T] on the GPU: tok / pos / slot are its rows
     host: torch.Tensor = None        # pinned staging copy of meta
     host_evt: torch.cuda.Event = None
@@ -308,6 +309,7 @@ class Engine:
             b = StepBuffers(
                 T=T, tok=meta[0], pos=meta[1], slot=meta[2], meta=meta,
                 host=torch.zeros(3, T, dtype=torch.int32).pin_memory(),
+                ids=torch.zeros(T, dtype=torch.int32, device=dev),
                 h=torch.zeros(T, c.dim, **f32), h2=torch.zeros(T, c.dim, **f32),
                 x8=torch.zeros(T, kmax, dtype=torch.int8, device=dev),
                 dx=torch.zeros(T, kmax // 32, **f32), sx=torch.zeros(T, kmax // 16, **f32),
@@ -474,7 +476,7 @@ class Engine:
         LK.qgemv(self.w.output, *qd, b.logits, LK.STORE, **G)
 
     def _decode_native(self, tokens: Sequence[int], positions: Sequence[int],
-                       slots: Sequence[int]) -> torch.Tensor:
+                       slots: Sequence[int], greedy: bool = False) -> torch.Tensor:
         T = len(tokens)
         b = self._buffers(T)
         # one H2D copy per step from a pinned staging row (three synchronous pageable copies cost
@@ -489,25 +491,31 @@ class Engine:
         b.host_evt.record()
         span = self._span(max(positions))
         fused = len(set(slots)) == len(slots)
+
+        def step():
+            self._step_kernels(b, span, fused)
+            if greedy:                 # the argmax inside the graph: one small copy per step
+                self.LK.argmax_rows(b.logits, b.ids)
+
         if self.use_graphs:
             if b.graphs is None:
                 b.graphs = {}
-            g = b.graphs.get((span, fused))
+            g = b.graphs.get((span, fused, greedy))
             if g is None:
                 s = torch.cuda.Stream(self.device)
                 s.wait_stream(torch.cuda.current_stream(self.device))
                 with torch.cuda.stream(s):
-                    self._step_kernels(b, span, fused)      # warm-up outside capture
+                    step()                                  # warm-up outside capture
                 torch.cuda.current_stream(self.device).wait_stream(s)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    self._step_kernels(b, span, fused)
-                b.graphs[(span, fused)] = g
+                    step()
+                b.graphs[(span, fused, greedy)] = g
                 self.stats["graph_captures"] += 1
             g.replay()
         else:
-            self._step_kernels(b, span, fused)
-        return b.logits
+            step()
+        return b.ids if greedy else b.logits
 
     # ------------------------------------------------------------------ public API
     def decode(self, tokens: Sequence[int], positions: Sequence[int],
@@ -533,6 +541,27 @@ class Engine:
                 for t, p, s in zip(tokens, positions, slots)]
         return torch.stack(rows, 0)
 
+    def decode_greedy(self, tokens: Sequence[int], positions: Sequence[int],
+                      slots: Sequence[int]) -> List[int]:
+        """:meth:`decode` + argmax of each row (the first index of the maximum, as torch.argmax),
+        on the GPU inside the step's HIP graph: the host receives T token ids, not T x vocab
+        logits, and no separate argmax launch follows the step."""
+        T = len(tokens)
+        if T == 0:
+            raise ValueError("decode: no tokens")
+        if not self.gpu:
+            return torch.argmax(self.decode(tokens, positions, slots), -1).tolist()
+        for p in positions:
+            if p >= self.max_ctx:
+                raise ValueError(f"position {p} beyond the context ({self.max_ctx})")
+        self.stats["decode_steps"] += 1
+        self.stats["decode_tokens"] += T
+        out: List[int] = []
+        for i in range(0, T, self.max_T):
+            out += self._decode_native(tokens[i:i + self.max_T], positions[i:i + self.max_T],
+                                       slots[i:i + self.max_T], greedy=True).tolist()
+        return out
+
     def prefill(self, tokens: Sequence[int], slot: int, start: int = 0) -> torch.Tensor:
         """Process prompt tokens of one sequence; returns the logits of its last token [vocab]."""
         P = len(tokens)
@@ -552,8 +581,9 @@ class Engine:
         return logits.clone()
 
     def capture(self, sizes: Sequence[int] = (1, 2, 3, 4)) -> None:
-        """Capture every decode graph (batch sizes x attention-span buckets) up front — the server
-        does this before it reports ready.  Writes only position ``span-1`` of slot 0."""
+        """Capture every decode graph (batch sizes x attention-span buckets, sampled and greedy
+        steps, one sequence per slot as the server runs them) up front — the server does this
+        before it reports ready.  Writes only position ``span-1`` of the slots it uses."""
         if not self.gpu:
             return
         spans = []
@@ -565,8 +595,10 @@ class Engine:
             s *= 2
         for T in sizes:
             if T <= self.max_T:
+                slots = list(range(T)) if T <= self.slots else [0] * T
                 for span in spans:
-                    self._decode_native([0] * T, [span - 1] * T, [0] * T)
+                    for greedy in (False, True):
+                        self._decode_native([0] * T, [span - 1] * T, slots, greedy=greedy)
         torch.cuda.synchronize(self.device)
 
 

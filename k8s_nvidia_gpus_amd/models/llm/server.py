@@ -242,11 +242,11 @@ class Scheduler:
         if not jobs:
             return
         t0 = time.perf_counter()
-        logits = self.engine.decode([j.last for j in jobs], [j.pos for j in jobs],
-                                    [j.slot for j in jobs])
-        if all(j.params.plain_greedy for j in jobs):
-            toks = torch.argmax(logits, -1).tolist()
+        args = ([j.last for j in jobs], [j.pos for j in jobs], [j.slot for j in jobs])
+        if all(j.params.plain_greedy for j in jobs) and hasattr(self.engine, "decode_greedy"):
+            toks = self.engine.decode_greedy(*args)       # argmax inside the step's graph
         else:
+            logits = self.engine.decode(*args)
             toks = [sample_token(logits[i], j.params, j.ids + j.gen, j.generator)
                     for i, j in enumerate(jobs)]
         dt = time.perf_counter() - t0

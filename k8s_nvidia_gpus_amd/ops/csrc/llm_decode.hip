@@ -1637,6 +1637,43 @@ __global__ void __launch_bounds__(512) attn_mfma_kernel(AttnArgs a, int chunk) {
   }
 }
 
+// ---------------------------------------------------------------- greedy sampling
+// out[t] = argmax of logits row t (the first index of the maximum, as torch.argmax): one 1024-thread
+// workgroup per row, 16-byte loads, (value, index) reductions.  Captured into the decode step's HIP
+// graph so a greedy step ends with one 4-byte-per-token copy instead of a separate argmax launch.
+__global__ void __launch_bounds__(1024) argmax_rows_kernel(const float* __restrict__ x, int V,
+                                                           long ld, int* __restrict__ out) {
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  const float* row = x + blockIdx.x * ld;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  const int nv4 = V >> 2;
+  for (int i = threadIdx.x; i < nv4; i += blockDim.x) {       // increasing indices per thread:
+    const float4 v = reinterpret_cast<const float4*>(row)[i]; //   strict '>' keeps the first
+    const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (e[k] > best) { best = e[k]; bi = 4 * i + k; }
+  }
+  for (int i = (nv4 << 2) + threadIdx.x; i < V; i += blockDim.x)
+    if (row[i] > best) { best = row[i]; bi = i; }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, kWave);
+    const int oi = __shfl_xor(bi, o, kWave);
+    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) { sv[wave] = best; si[wave] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+      if (sv[w] > best || (sv[w] == best && si[w] < bi)) { best = sv[w]; bi = si[w]; }
+    out[blockIdx.x] = bi == 0x7fffffff ? 0 : bi;
+  }
+}
+
 // ---------------------------------------------------------------- dequantisation (rows → fp16/fp32)
 // One thread per 32-weight run.  rows: optional row indices (embedding gather).
 template <int TYPE, bool F32OUT>
@@ -2028,6 +2065,13 @@ int amdk8s_llm_qgemv_attn(int type, const void* wq, const void* wqh, const void*
   if (type == kQ4K) return dispatch_t<kQ4K, kResid>(a, waves, st);
   if (type == kQ6K) return dispatch_t<kQ6K, kResid>(a, waves, st);
   return 2;
+}
+
+int amdk8s_llm_argmax_rows(const void* x, int V, long ld, int T, void* out, void* stream) {
+  if (V < 1 || T < 1 || ld < V || ((uintptr_t)x & 15) || (ld & 3)) return 2;
+  hipLaunchKernelGGL(argmax_rows_kernel, dim3(T), dim3(1024), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const float*>(x), V, ld, static_cast<int*>(out));
+  return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
 int amdk8s_llm_rmsnorm_q8(const void* x, const void* w, float eps, int K, int T, void* x8,

@@ -38,6 +38,8 @@ def _lib():
             lib.amdk8s_llm_qgemv_attn.argtypes = [ci] + [vp] * 4 + [vp, vp, vp, ci, ci, vp, ci, ci,
                                                                   ci, ci, ci, ci, vp]
             lib.amdk8s_llm_qgemv_attn.restype = ci
+            lib.amdk8s_llm_argmax_rows.argtypes = [vp, ci, cl, ci, vp, vp]
+            lib.amdk8s_llm_argmax_rows.restype = ci
             lib.amdk8s_llm_rmsnorm_q8.argtypes = [vp, vp, cf, ci, ci, vp, vp, vp, vp]
             lib.amdk8s_llm_rmsnorm_q8.restype = ci
             lib.amdk8s_llm_rope_kv.argtypes = [vp, ci, vp, vp, vp, vp, ci, ci, ci, ci, vp, vp, vp,
@@ -144,6 +146,13 @@ def qgemv_attn(w, po, pml, pos, nsplit: int, out, rows_per_wg: int = 0, waves: i
                                         pos.data_ptr(), nsplit, chunk or attn_chunk(),
                                         out.data_ptr(), out.stride(0), w.n, w.k, t, waves,
                                         rows_per_wg, _stream(out)), "amdk8s_llm_qgemv_attn")
+
+
+def argmax_rows(x, out) -> None:
+    """out (int32 [T]) = the first index of each row's maximum of x (fp32 [T, V], 16-B aligned)."""
+    t, v = x.shape
+    _check(_lib().amdk8s_llm_argmax_rows(x.data_ptr(), v, x.stride(0), t, out.data_ptr(),
+                                         _stream(x)), "amdk8s_llm_argmax_rows")
 
 
 def rmsnorm_q8(x, w, eps: float, x8, dx, sx) -> None:

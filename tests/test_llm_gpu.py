@@ -599,6 +599,25 @@ def test_native_prefill_equals_torch_prefill(dev, tiny_gguf, gqa):
                                rtol=1e-2, atol=1e-2)
 
 
+def test_argmax_rows_and_decode_greedy(dev, LK, tiny_gguf):
+    """The in-graph greedy step returns torch.argmax of the logits (first index on ties)."""
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load
+
+    x = torch.randn(3, 152064, device=dev)
+    x[1, 5] = x[1, 70000] = 1e4                      # tie: the first index wins
+    out = torch.empty(3, dtype=torch.int32, device=dev)
+    LK.argmax_rows(x, out)
+    assert out.tolist() == torch.argmax(x, -1).tolist()
+    assert int(out[1]) == 5
+    eng, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=True)
+    p = tok.encode("a cozy cabin in the woods")
+    for s in range(2):
+        eng.prefill(p, slot=s)
+    lg = eng.decode([7, 9], [len(p), len(p)], [0, 1]).clone()
+    ids = eng.decode_greedy([7, 9], [len(p), len(p)], [0, 1])
+    assert ids == torch.argmax(lg, -1).tolist()
+
+
 def test_random_7b_layer_shapes_run(dev):
     """The exact Qwen2.5-7B matrix shapes (K = 3584 / 18944, N up to 152064) on random blocks:
     one native decode step is finite and matches the fp16 dense path's logits direction."""

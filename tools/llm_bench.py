@@ -182,8 +182,8 @@ def main(argv=None) -> int:
         torch.cuda.synchronize()
         t = time.perf_counter()
         for i in range(args.steps):
-            lg = eng.decode(toks, [p + 4 + i for p in pos], slots)
-            nxt = torch.argmax(lg, -1).tolist()       # sample on the GPU, sync like a server
+            # greedy on the GPU inside the step's graph, host sync per step like a server
+            nxt = eng.decode_greedy(toks, [p + 4 + i for p in pos], slots)
             toks = [int(x) % cfg.vocab for x in nxt]
         dt = time.perf_counter() - t
         row = {"T": T, "ms_per_step": round(dt / args.steps * 1e3, 4),

@@ -54,8 +54,8 @@ def llm_decode(T: int = 1):
 
     def step():
         p = state["pos"]
-        lg = eng.decode(state["tok"], [p] * T, list(range(T)))
-        state["tok"] = [int(x) % QWEN25_7B.vocab for x in torch.argmax(lg, -1).tolist()]
+        nxt = eng.decode_greedy(state["tok"], [p] * T, list(range(T)))
+        state["tok"] = [int(x) % QWEN25_7B.vocab for x in nxt]
         state["pos"] = p + 1 if p + 1 < 1000 else len(prompt)
     return step
 
