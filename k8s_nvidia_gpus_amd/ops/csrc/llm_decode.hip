@@ -1649,12 +1649,22 @@ __global__ void __launch_bounds__(1024) argmax_rows_kernel(const float* __restri
   float best = -INFINITY;
   int bi = 0x7fffffff;
   const int nv4 = V >> 2;
-  for (int i = threadIdx.x; i < nv4; i += blockDim.x) {       // increasing indices per thread:
-    const float4 v = reinterpret_cast<const float4*>(row)[i]; //   strict '>' keeps the first
-    const float e[4] = {v.x, v.y, v.z, v.w};
+  // 8 loads in flight per thread per round (a 152k-entry row is 5 rounds, not 38 dependent trips);
+  // indices increase per thread, so strict '>' keeps the first maximum
+  constexpr int kU = 8;
+  for (int i0 = threadIdx.x; i0 < nv4; i0 += kU * blockDim.x) {
+    float4 v[kU];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (e[k] > best) { best = e[k]; bi = 4 * i + k; }
+    for (int u = 0; u < kU; ++u)
+      v[u] = reinterpret_cast<const float4*>(row)[min(i0 + u * (int)blockDim.x, nv4 - 1)];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * (int)blockDim.x;
+      const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (i < nv4 && e[k] > best) { best = e[k]; bi = 4 * i + k; }
+    }
   }
   for (int i = (nv4 << 2) + threadIdx.x; i < V; i += blockDim.x)
     if (row[i] > best) { best = row[i]; bi = i; }
@@ -1812,13 +1822,15 @@ static int attn_impl_default() {
 // Long rows (ffn_down: 74 super-blocks) in two balanced stages (U = ceil(nb / 16)) instead of
 // KB-wide ones: measured slower at T = 1 (1.754 -> 1.787 ms) and faster from T = 3 (T=3 / T=4
 // 2.43 / 2.64 -> 2.39 / 2.60 ms, profiles/r03/ag), so on from T = 3.  AMDK8S_LLM_LONGROW=0 / 1
-// forces it off / on for every T.  The stage width never changes a result bit.
-static bool longrow_enabled(int T) {
+// forces it off / on for every T; q4 / q6 force it on for that type only (the other keeps the
+// default).  The stage width never changes a result bit.
+static bool longrow_enabled(int type, int T) {
   static int v = -2;
   if (v == -2) {
     const char* e = getenv("AMDK8S_LLM_LONGROW");
-    v = e ? (e[0] == '1') : -1;
+    v = !e ? -1 : e[0] == 'q' ? (e[1] == '4' ? 10 : 11) : (e[0] == '1');
   }
+  if (v >= 10) return v - 10 == type || T >= 3;
   return v < 0 ? T >= 3 : v != 0;
 }
 
@@ -1837,7 +1849,7 @@ int launch_gemv(const GemvArgs& a, int waves, hipStream_t st) {
   if constexpr (MODE != kPair) {
     // long rows (ffn_down: 74 super-blocks): two stages per row with U = ceil(nb / 16) instead of
     // KB-wide stages whose last one is mostly clamped lanes (74 = 32 + 32 + 10 at U = 4)
-    if (longrow_enabled(T)) {
+    if (longrow_enabled(TYPE, T)) {
       const int u2 = (nb + 15) / 16;
       if (u2 == 5) return launch_one<TYPE, T, MODE, 5, false>(a, waves, st);
       if (u2 == 6) return launch_one<TYPE, T, MODE, 6, false>(a, waves, st);
