@@ -1820,8 +1820,10 @@ static int attn_impl_default() {
 }
 
 // Long rows (ffn_down: 74 super-blocks) in two balanced stages (U = ceil(nb / 16)) instead of
-// KB-wide ones: measured slower at T = 1 (1.754 -> 1.787 ms) and faster from T = 3 (T=3 / T=4
-// 2.43 / 2.64 -> 2.39 / 2.60 ms, profiles/r03/ag), so on from T = 3.  AMDK8S_LLM_LONGROW=0 / 1
+// KB-wide ones: faster from T = 3 (T=3 / T=4 2.43 / 2.64 -> 2.39 / 2.60 ms, profiles/r03/ag); at
+// T = 1 faster for Q4_K rows (14.5 -> 13.5 us) and slower for Q6_K ones (13.8 -> 17.1 us; step
+// 1.740 -> 1.721 ms with Q4_K only, profiles/r03/ap), so Q4_K always, Q6_K from T = 3.
+// AMDK8S_LLM_LONGROW=0 / 1
 // forces it off / on for every T; q4 / q6 force it on for that type only (the other keeps the
 // default).  The stage width never changes a result bit.
 static bool longrow_enabled(int type, int T) {
@@ -1831,7 +1833,7 @@ static bool longrow_enabled(int type, int T) {
     v = !e ? -1 : e[0] == 'q' ? (e[1] == '4' ? 10 : 11) : (e[0] == '1');
   }
   if (v >= 10) return v - 10 == type || T >= 3;
-  return v < 0 ? T >= 3 : v != 0;
+  return v < 0 ? (type == 0 || T >= 3) : v != 0;
 }
 
 template <int TYPE, int T, int MODE>
@@ -1907,9 +1909,14 @@ int dispatch2_t(const GemvArgs& a0, const GemvArgs& a1, int waves, hipStream_t s
 // From T = 3 on, the 18944-long ffn_down rows run 16 per workgroup (2 per wave: the staged
 // activations serve twice the weights; 20.8 / 24.2 vs 24.4 / 26.6 us for Q4_K / Q6_K at T = 4,
 // profiles/r03/y — at T = 1 the 8-row grid is faster).
-void gemv_shape(int N, int K, int T, int& waves, int& rows) {
+// Q4_K ffn_down rows (long-row stages at every T) take 16 rows per workgroup at T = 1 too:
+// 13.6 -> 12.2 us (profiles/r03/aq); Q6_K ones stay at 8 (13.8 vs 17.2 us).
+void gemv_shape(int type, int N, int K, int T, int& waves, int& rows) {
   if (waves <= 0) waves = K >= 8192 ? 8 : 4;
-  if (rows <= 0) rows = N >= 65536 ? 32 : (K >= 8192 && T >= 3 && waves == 8) ? 16 : 8;
+  if (rows <= 0)
+    rows = N >= 65536 ? 32
+           : (K >= 8192 && waves == 8 && (T >= 3 || (type == kQ4K && longrow_enabled(type, T))))
+               ? 16 : 8;
 }
 
 }  // namespace
@@ -1966,7 +1973,7 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
     if (mode != kPair || N % 32 || !odx || !osx) return 2;
     rows_per_wg = 32;
   }
-  gemv_shape(N, K, T, waves, rows_per_wg);
+  gemv_shape(type, N, K, T, waves, rows_per_wg);
   if (ox8 && waves * 64 < 32 * T) return 2;
   if (waves < 1 || waves > 8 || rows_per_wg < 1) return 2;
   GemvArgs a{};                               // every field not set below stays null / 0
@@ -2020,7 +2027,7 @@ int amdk8s_llm_qgemv2(int type0, const void* w0q, const void* w0qh, const void* 
   if (xf && ldx % 4) return 2;
   if ((type0 != kQ4K && type0 != kQ6K) || (type1 != kQ4K && type1 != kQ6K)) return 2;
   int rows = rows_per_wg;
-  gemv_shape(N0 + N1, K, T, waves, rows);
+  gemv_shape(type0, N0 + N1, K, T, waves, rows);
   if (waves < 1 || waves > 8 || rows < 1) return 2;
   GemvArgs a[2];
   const int N[2] = {N0, N1};
