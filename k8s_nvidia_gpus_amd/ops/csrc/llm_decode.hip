@@ -1972,6 +1972,14 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
   } else if (ox8) {                           // pair → Q8 output: whole 32-row blocks per workgroup
     if (mode != kPair || N % 32 || !odx || !osx) return 2;
     rows_per_wg = 32;
+    if (waves <= 0) {                         // AMDK8S_LLM_PAIR_WAVES: waves sharing the 32 rows
+      static int pw = -1;
+      if (pw < 0) {
+        const char* e = getenv("AMDK8S_LLM_PAIR_WAVES");
+        pw = e ? atoi(e) : 0;
+      }
+      waves = pw;
+    }
   }
   gemv_shape(type, N, K, T, waves, rows_per_wg);
   if (ox8 && waves * 64 < 32 * T) return 2;
