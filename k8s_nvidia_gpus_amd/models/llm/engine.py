@@ -155,6 +155,9 @@ class Engine:
         # prologue's order, so both paths give the same bits and decode stays batch-invariant
         # (models with dim >= 8192 run 8-wave GEMVs there: one path for every T)
         self.norm_prologue = os.environ.get("AMDK8S_LLM_NORM_PROLOGUE", "1") != "0"
+        # prefill q stored token-major for SDPA (AMDK8S_LLM_PREFILL_QTOK): the attention output
+        # then needs no transpose copy before o_proj (tools/debug/sdpa_layout_probe.py)
+        self.prefill_qtok = os.environ.get("AMDK8S_LLM_PREFILL_QTOK", "1") != "0"
         self.norm_prologue_T = int(os.environ.get("AMDK8S_LLM_NORM_PROLOGUE_T", "2"))
         self._norm_cnt = None
         self._attn_cnt = None
@@ -249,7 +252,11 @@ class Engine:
             mask = kj <= qi
         mm, mm_res = self._dense_ops()
         xn = torch.empty(P, c.dim, dtype=dt, device=self.device)
-        qh = torch.empty(c.heads, P, c.head_dim, dtype=dt, device=self.device)
+        if self.prefill_qtok:          # [H][P][128] view of token-major storage: SDPA's output
+            qh = torch.empty(P, c.heads, c.head_dim, dtype=dt,      # comes back token-major and
+                             device=self.device).transpose(0, 1)    # the o reshape is a view
+        else:
+            qh = torch.empty(c.heads, P, c.head_dim, dtype=dt, device=self.device)
         t = torch.empty(P, c.ffn, dtype=dt, device=self.device)
         for i, L in enumerate(self.w.layers):
             LK.rmsnorm_f16(x, L.attn_norm, c.eps, xn)

@@ -9,8 +9,9 @@
 // them (one launch each per layer and use):
 //   rmsnorm_f16   x fp32 [P][K] -> y fp16 = x * rsqrt(mean(x^2) + eps) * w   (one workgroup per row)
 //   rope_kv_f16   q|k|v fp16 [P][ldq] (bias already added by the GEMM epilogue) -> rotated q fp16
-//                 [H][P][128] (SDPA layout) and rotated k / v written to the fp16 KV cache at
-//                 positions start .. start + P - 1
+//                 [H][P][128] for SDPA (any head / position strides: the engine stores it as
+//                 [P][H][128], so SDPA's output comes back in token-major order) and rotated k / v
+//                 written to the fp16 KV cache at positions start .. start + P - 1
 //   swiglu_f16    gate|up fp16 [P][2F] -> silu(gate) * up fp16 [P][F]
 // The arithmetic is fp32 in registers; the RoPE uses the same explicit roundings as the decode
 // kernels (llm_decode.hip).
@@ -102,7 +103,8 @@ __global__ void __launch_bounds__(256) rope_kv_f16_kernel(const uint16_t* __rest
                                                           int ldq, const float* __restrict__ cos_t,
                                                           const float* __restrict__ sin_t,
                                                           int start, int P, int H, int Hkv,
-                                                          int max_ctx, uint16_t* __restrict__ q_out,
+                                                          int max_ctx, long qsh, long qsp,
+                                                          uint16_t* __restrict__ q_out,
                                                           uint16_t* __restrict__ kc,
                                                           uint16_t* __restrict__ vc) {
   const int p = blockIdx.y;
@@ -116,7 +118,7 @@ __global__ void __launch_bounds__(256) rope_kv_f16_kernel(const uint16_t* __rest
     const float c = cos_t[(long)pos * (kHeadDim / 2) + j];
     const float sn = sin_t[(long)pos * (kHeadDim / 2) + j];
     const uint16_t y0 = f2h(rope_lo(x0, x1, c, sn)), y1 = f2h(rope_hi(x0, x1, c, sn));
-    uint16_t* dst = h < H ? q_out + ((long)h * P + p) * kHeadDim
+    uint16_t* dst = h < H ? q_out + (long)h * qsh + (long)p * qsp
                           : kc + ((long)(h - H) * max_ctx + pos) * kHeadDim;
     dst[j] = y0;
     dst[j + kHeadDim / 2] = y1;
@@ -165,13 +167,15 @@ int amdk8s_llm_rmsnorm_f16(const void* x, int ldx, const void* w, float eps, int
 
 int amdk8s_llm_rope_kv_f16(const void* qkv, int ldq, const void* cos_t, const void* sin_t,
                            int start, int P, int H, int Hkv, int head_dim, int max_ctx,
-                           void* q_out, void* kc, void* vc, void* stream) {
+                           long qsh, long qsp, void* q_out, void* kc, void* vc, void* stream) {
   if (head_dim != kHeadDim || P < 1 || start < 0 || start + P > max_ctx || ldq % 2) return 2;
+  if (qsh < kHeadDim || qsp < kHeadDim) return 2;
   const int threads = (H + 2 * Hkv) * (kHeadDim / 2);
   hipLaunchKernelGGL(rope_kv_f16_kernel, dim3((threads + 255) / 256, P), dim3(256), 0,
                      static_cast<hipStream_t>(stream), static_cast<const uint16_t*>(qkv), ldq,
                      static_cast<const float*>(cos_t), static_cast<const float*>(sin_t), start, P,
-                     H, Hkv, max_ctx, static_cast<uint16_t*>(q_out), static_cast<uint16_t*>(kc),
+                     H, Hkv, max_ctx, qsh, qsp, static_cast<uint16_t*>(q_out),
+                     static_cast<uint16_t*>(kc),
                      static_cast<uint16_t*>(vc));
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

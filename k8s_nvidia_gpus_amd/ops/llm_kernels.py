@@ -58,8 +58,8 @@ def _lib():
             lib.amdk8s_llm_q6k_repack.restype = ci
             lib.amdk8s_llm_rmsnorm_f16.argtypes = [vp, ci, vp, cf, ci, ci, vp, ci, vp]
             lib.amdk8s_llm_rmsnorm_f16.restype = ci
-            lib.amdk8s_llm_rope_kv_f16.argtypes = [vp, ci, vp, vp, ci, ci, ci, ci, ci, ci, vp, vp,
-                                                   vp, vp]
+            lib.amdk8s_llm_rope_kv_f16.argtypes = [vp, ci, vp, vp, ci, ci, ci, ci, ci, ci, cl, cl,
+                                                   vp, vp, vp, vp]
             lib.amdk8s_llm_rope_kv_f16.restype = ci
             lib.amdk8s_llm_swiglu_f16.argtypes = [vp, ci, ci, vp, vp]
             lib.amdk8s_llm_swiglu_f16.restype = ci
@@ -247,12 +247,16 @@ def rmsnorm_f16(x, w, eps: float, y) -> None:
 
 def rope_kv_f16(qkv, cos_t, sin_t, start: int, heads: int, kv_heads: int, max_ctx: int, q_out,
                 kc, vc) -> None:
-    """q|k|v fp16 [P, (H + 2 Hkv) * 128] (bias included) -> rotated q fp16 [H, P, 128] and the
-    rotated k / v written into one slot's fp16 cache slabs ``kc`` / ``vc`` [Hkv, max_ctx, 128] at
-    positions start .. start + P - 1."""
+    """q|k|v fp16 [P, (H + 2 Hkv) * 128] (bias included) -> rotated q fp16 [H, P, 128] (any head /
+    position strides, unit inner stride) and the rotated k / v written into one slot's fp16 cache
+    slabs ``kc`` / ``vc`` [Hkv, max_ctx, 128] at positions start .. start + P - 1."""
     p = qkv.shape[0]
+    if tuple(q_out.shape) != (heads, p, 128) or q_out.stride(2) != 1:
+        raise ValueError(f"rope_kv_f16: q_out {tuple(q_out.shape)} / {q_out.stride()} is not "
+                         f"[{heads}, {p}, 128] with a unit inner stride")
     _check(_lib().amdk8s_llm_rope_kv_f16(qkv.data_ptr(), qkv.stride(0), cos_t.data_ptr(),
                                          sin_t.data_ptr(), start, p, heads, kv_heads, 128, max_ctx,
+                                         q_out.stride(0), q_out.stride(1),
                                          q_out.data_ptr(), kc.data_ptr(), vc.data_ptr(),
                                          _stream(qkv)), "amdk8s_llm_rope_kv_f16")
 

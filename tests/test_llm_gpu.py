@@ -576,15 +576,17 @@ def test_dense_prefill_matches_native_prefill(dev, tiny_gguf):
     assert torch.nn.functional.cosine_similarity(la[None], lb[None]).item() > 0.99
 
 
-@pytest.mark.parametrize("gqa", [False, True])
-def test_native_prefill_equals_torch_prefill(dev, tiny_gguf, gqa):
+@pytest.mark.parametrize("gqa,qtok", [(False, False), (True, False), (True, True)])
+def test_native_prefill_equals_torch_prefill(dev, tiny_gguf, gqa, qtok):
     """The fused prefill glue (RMSNorm -> fp16, RoPE + KV write, SwiGLU kernels) against the
     PyTorch formulation of the same dense fp16 forward: logits and the written KV cache agree,
-    for a prompt from position 0 and a continuation at position > 0."""
+    for a prompt from position 0 and a continuation at position > 0 (q head-major or
+    token-major)."""
     from k8s_nvidia_gpus_amd.models.llm.synthetic import load
 
     a, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=True)
     a.prefill_gqa = gqa
+    a.prefill_qtok = qtok
     b, _ = load(tiny_gguf, device=dev, max_ctx=512, dense=True)
     b.prefill_native = False
     p = tok.encode("the lazy dog jumps over a helpful assistant " * 3)
