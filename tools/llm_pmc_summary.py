@@ -14,7 +14,8 @@ def main(pattern):
             name = r["Kernel_Name"]
             if "qgemv" not in name and "attn" not in name and "rope" not in name:
                 continue
-            key = name.split("(")[0].replace("void (anonymous namespace)::", "")[:40] + \
+            short = name.replace("void ", "").replace("(anonymous namespace)::", "")
+            key = short.split("(")[0][:40] + \
                 f" grid={r.get('Grid_Size', r.get('Grid_Size_X', ''))}"
             acc[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
             d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
