@@ -122,6 +122,48 @@ def settle(step, sync, settle_ms: float, chunk: int = 8, max_launches: int = 400
     return n
 
 
+def timed_window(step, sync, barrier, steps: int, warmup: int, settle_ms: float, sampler=None):
+    """settle → warmup → [sync, barrier, sync] → t0 → K steps → [sync, barrier, sync] → t1.
+
+    Returns ``(elapsed_s, settle_launches)``.  The sampler (already constructed: ``amdsmi_init``
+    and the handle scan are the slow part) starts its thread *before* the settle phase; inside the
+    bracket it is only told the clock (``mark_start``/``mark_end``) and is held quiet while the K
+    steps are launched (``hold`` … ``mark_launched``: no GIL contention with the launches).
+    Nothing but synchronisation
+    may sit between the last warmup step and ``t0``: any idle gap — r03's amd-smi init there cost
+    the driver's K=20/W=5 run 14 % — puts the chip back into the load-step DVFS transient that the
+    settle phase exists to skip (tests/test_parallel_gloo.py::test_bench_timed_window_order).
+    """
+    if sampler is not None:
+        sampler.__enter__()
+    try:
+        launches = settle(step, sync, settle_ms)
+        for _ in range(warmup):
+            step()
+        if sampler is not None:
+            sampler.hold()      # quiet from here to the last timed launch (waits under warmup work)
+        sync()
+        barrier()
+        sync()
+        if sampler is not None:
+            sampler.mark_start()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        if sampler is not None:
+            sampler.mark_launched()     # sample while the enqueued steps run, not between launches
+        sync()
+        barrier()
+        sync()
+        elapsed = time.perf_counter() - t0
+        if sampler is not None:
+            sampler.mark_end()
+    finally:
+        if sampler is not None:
+            sampler.__exit__(None, None, None)
+    return elapsed, launches
+
+
 def first_gpu_result(K, device: torch.device) -> float:
     """Reference-protocol vectorAdd (50 000 fp32, 196×256) — returns seconds since process start."""
     n = 50000
@@ -206,31 +248,19 @@ def main(argv=None) -> int:
         def step():
             K.gemm_bf16_nt(a, b, out=c, variant=variant)
 
-    settle_launches = settle(step, sync, 0.0 if smoke else args.settle_ms)
-    for _ in range(args.warmup):
-        step()
-    sync()
     from k8s_nvidia_gpus_amd.parallel import telemetry
 
-    sampler = (telemetry.timed(device_index=device.index if device.index is not None else 0)
+    def barrier():
+        if distributed:
+            dist.barrier()
+
+    # amd-smi init + handle scan happen here, before the settle phase (see timed_window)
+    sampler = (telemetry.timed(period=0.005,
+                               device_index=device.index if device.index is not None else 0)
                if not smoke and not args.no_telemetry else None)
-    if distributed:
-        dist.barrier()
-    sync()
-    if sampler is not None:
-        sampler.__enter__()     # a sleeping thread; one amd-smi read per 20 ms
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    sync()
-    if distributed:
-        dist.barrier()
-    sync()
-    elapsed = time.perf_counter() - t0
-    tel = None
-    if sampler is not None:
-        sampler.__exit__(None, None, None)
-        tel = sampler.summary()
+    elapsed, settle_launches = timed_window(step, sync, barrier, args.steps, args.warmup,
+                                            0.0 if smoke else args.settle_ms, sampler)
+    tel = sampler.summary() if sampler is not None else None
 
     flop_per_gpu = 2.0 * s * s * s * args.steps
     per_rank = [round(flop_per_gpu / elapsed / 1e12, 2)]
@@ -256,21 +286,7 @@ def main(argv=None) -> int:
         def step8():
             K.gemm_fp8_nt(a8, b8, out=c)
 
-        settle(step8, sync, args.settle_ms)
-        for _ in range(args.warmup):
-            step8()
-        sync()
-        if distributed:
-            dist.barrier()
-        sync()
-        t8 = time.perf_counter()
-        for _ in range(args.steps):
-            step8()
-        sync()
-        if distributed:
-            dist.barrier()
-        sync()
-        e8 = time.perf_counter() - t8
+        e8, _ = timed_window(step8, sync, barrier, args.steps, args.warmup, args.settle_ms)
         if distributed:
             t = torch.tensor([e8], device=device, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -123,11 +123,13 @@ def main(argv=None) -> int:
                             args.root, cfg.min_gfx)
 
     if c == "device-plugin":
-        from .device_plugin import AmdGpuDevicePlugin
+        from .device_plugin import AmdGpuDevicePlugin, ValidationGate
         from .validator import DEVICE_ID_MAP
 
+        gate = ValidationGate(args.marker_dir, root=args.root,
+                              gate=bool(cfg.section("validator")["gateOnValidation"]))
         AmdGpuDevicePlugin(cfg, root=args.root, kubelet_dir=args.kubelet_dir,
-                           id_map_path=DEVICE_ID_MAP).run()
+                           id_map_path=DEVICE_ID_MAP, gate=gate).run()
         return 0
 
     if c == "labeller":
@@ -168,8 +170,6 @@ def main(argv=None) -> int:
         return bringup.main(args, cfg, _bin_dir())
 
     if c == "validator":
-        import time
-
         from .validator import STEPS, Validator
 
         v = Validator(cfg, args.marker_dir, root=args.root, kube=_kube(), node_name=node)
@@ -178,15 +178,15 @@ def main(argv=None) -> int:
         for s in steps:
             r = v.run_step(s)
             print(json.dumps(r.to_json()), flush=True)
-            ok = ok and r.passed
-            if not r.passed:
+            # a deferred step (no free GPU) is not a pass, but the chain goes on: the report
+            # labels the node "deferred" and the hold loop below re-runs the chain later
+            ok = ok and r.proceed
+            if not r.proceed:
                 break
         if args.hold:
-            # re-validate when the driver is withdrawn (driver restart / GPU reset): exit so the
-            # DaemonSet restarts the whole init chain
-            while os.path.exists(os.path.join(args.marker_dir, "driver-ready")):
-                time.sleep(args.interval or 30)
-            return 3
+            from .validator import hold_loop
+
+            return hold_loop(v, args.marker_dir, interval=args.interval or 30)
         return 0 if ok else 1
 
     ap.error(f"unknown component {c!r}")

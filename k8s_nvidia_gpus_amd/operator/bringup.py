@@ -115,6 +115,8 @@ def rehearse(cfg: OperatorConfig, bin_dir: str, workdir: Optional[str] = None, r
     # the plugin-pod step needs an API server; everything else in the chain is node-local
     vraw = copy.deepcopy(cfg.raw)
     vraw["validator"]["pluginTest"] = False
+    # a bare box has no kubelet: every agent is free (in a cluster an absent socket fails the step)
+    vraw["validator"]["podResourcesRequired"] = False
     v = Validator(OperatorConfig(vraw), markers, bin_dir=bin_dir, runner=runner, root=root,
                   driver_wait=driver_wait)
     state: Dict = {}

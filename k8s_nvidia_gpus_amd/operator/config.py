@@ -65,6 +65,18 @@ DEFAULTS: Dict[str, Any] = {
         # GPUs kubelet has allocated to pods are never loaded: gemm / bandwidth / stress / rccl run
         # on the free ones only (kubelet PodResources API), and are deferred when none is free
         "podResourcesSocket": "/var/lib/kubelet/pod-resources/kubelet.sock",
+        # an absent socket fails the load steps (a node cannot prove a GPU is free); false only for
+        # runs outside Kubernetes (bring-up rehearsal on a bare box), where every agent is free
+        "podResourcesRequired": True,
+        # device plugin advertises a GPU Healthy only once every enabled load step has passed on it
+        # this boot (validated-devices.json), so pods cannot take GPUs before the first validation
+        "gateOnValidation": True,
+        # load steps reserve their GPUs (in-test.json → the plugin reports them Unhealthy) and wait
+        # this long for the plugin's ack before re-reading PodResources
+        "reserveAckSeconds": 15,
+        # the report container re-runs the chain when a deferred/partial node gets a free,
+        # not-yet-validated GPU; PodResources is polled at this period
+        "retryDeferredSeconds": 300,
         # a validator restart with the node's fingerprint (boot id, amdgpu version, operator image)
         # unchanged since the last full pass re-uses that pass instead of re-running the load steps
         "skipUnchangedNode": True,
@@ -129,6 +141,8 @@ class OperatorConfig:
             raise ConfigError(f"partition.memory must be one of {MEMORY_PARTITIONS}")
         if not 1 <= int(r["exporter"]["port"]) <= 65535:
             raise ConfigError("exporter.port out of range")
+        if float(r["validator"]["reserveAckSeconds"]) < 0 or float(r["validator"]["retryDeferredSeconds"]) <= 0:
+            raise ConfigError("validator.reserveAckSeconds must be >= 0, retryDeferredSeconds > 0")
         if int(r["validator"]["gemmSize"]) % 256:
             raise ConfigError("validator.gemmSize must be a multiple of 256 (MFMA block tile)")
         return self

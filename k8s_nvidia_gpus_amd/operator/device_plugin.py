@@ -26,6 +26,9 @@ Design (MI355X-first):
   ``kubelet.sock`` and its own socket and re-serves + re-registers.
 * **Partition changes**: while ``/run/amd/partition-in-progress`` exists (the partition manager's
   drain marker) the plugin advertises no devices, then re-enumerates.
+* **Validation gate** (:class:`ValidationGate`): with ``validator.gateOnValidation`` a device is
+  Healthy only after the validator's load steps passed on it this boot, and the devices a load
+  step is about to load are reported Unhealthy for its duration (the validator's TOCTOU guard).
 """
 from __future__ import annotations
 
@@ -141,6 +144,72 @@ def default_ecc_fn(threshold: int) -> Optional[Callable]:
         return None
 
 
+class ValidationGate:
+    """The validator's say in what the plugin advertises (files in ``/run/amd/validations``).
+
+    * ``validated-devices.json`` ``{boot_id, device_uids}`` — with ``gate`` on, a device is reported
+      Healthy only once every enabled validator load step has passed on it this boot: on first boot
+      no pod can be handed a GPU before the validator has loaded it (else a fully allocated node
+      would be labelled validated with zero GEMMs run).
+    * ``in-test.json`` ``{nonce, device_uids, expires}`` — the agents a load step is about to load;
+      reported Unhealthy (kubelet stops allocating them) until the file is removed or expires.
+      After publishing that state the plugin writes the nonce to ``in-test.ack``; the validator
+      then re-reads PodResources and drops any agent a pod took in between.
+    """
+
+    def __init__(self, marker_dir: str, root: str = "/", gate: bool = True,
+                 clock: Callable[[], float] = time.time):
+        self.marker_dir = marker_dir
+        self.root = root
+        self.gate = gate
+        self.clock = clock
+
+    def _json(self, name: str):
+        try:
+            with open(os.path.join(self.marker_dir, name)) as f:
+                return json.load(f)
+        except (OSError, ValueError):
+            return None
+
+    def boot_id(self) -> str:
+        try:
+            with open(os.path.join(self.root, "proc/sys/kernel/random/boot_id")) as f:
+                return f.read().strip()
+        except OSError:
+            return ""
+
+    def stamp(self) -> Tuple:
+        """Changes whenever either file does (cheap: polled every plugin loop iteration)."""
+        out = []
+        for name in ("validated-devices.json", "in-test.json"):
+            try:
+                st = os.stat(os.path.join(self.marker_dir, name))
+                out.append((st.st_mtime_ns, st.st_ino, st.st_size))
+            except OSError:
+                out.append(None)
+        return tuple(out)
+
+    def state(self) -> Tuple[Optional[set], set, Optional[str]]:
+        """(validated uids or None when not gating, reserved uids, reservation nonce)."""
+        validated = None
+        if self.gate:
+            doc = self._json("validated-devices.json") or {}
+            validated = set(doc.get("device_uids") or []) if doc.get("boot_id") == self.boot_id() else set()
+        res = self._json("in-test.json") or {}
+        if res and float(res.get("expires", 0)) > self.clock():
+            return validated, set(res.get("device_uids") or []), str(res.get("nonce", ""))
+        return validated, set(), None
+
+    def ack(self, nonce: str) -> None:
+        path = os.path.join(self.marker_dir, "in-test.ack")
+        try:
+            with open(path + ".tmp", "w") as f:
+                f.write(nonce + "\n")
+            os.replace(path + ".tmp", path)
+        except OSError as e:
+            log.warning("cannot ack reservation %s: %s", nonce, e)
+
+
 def preferred_allocation(available: Sequence[topo_mod.GpuDevice],
                          must_include: Sequence[topo_mod.GpuDevice], size: int) -> List[topo_mod.GpuDevice]:
     """Pick ``size`` devices: must_include first, then pack by ASIC, then NUMA node (best fit)."""
@@ -189,8 +258,10 @@ class AmdGpuDevicePlugin:
                  topology_fn: Optional[Callable[[], topo_mod.NodeTopology]] = None,
                  health_fn: Optional[HealthFn] = None, pause_marker: Optional[str] = PAUSE_MARKER,
                  dev_prefix: str = "/dev", ecc_fn: Optional[Callable] = None,
-                 id_map_path: Optional[str] = None):
+                 id_map_path: Optional[str] = None, gate: Optional[ValidationGate] = None):
         self.config = config
+        self.gate = gate
+        self._gate_stamp = None
         # {kubelet device ID: device_uid} for the validator, which maps kubelet's PodResources
         # answer to GPUs with it (needed with deviceIdStrategy: index)
         self.id_map_path = id_map_path
@@ -252,6 +323,13 @@ class AmdGpuDevicePlugin:
         for uid in list(health):
             if uid not in present:
                 health[uid] = api.UNHEALTHY
+        nonce = None
+        if self.gate is not None:
+            self._gate_stamp = self.gate.stamp()
+            validated, reserved, nonce = self.gate.state()
+            for uid in health:
+                if (validated is not None and uid not in validated) or uid in reserved:
+                    health[uid] = api.UNHEALTHY
         with self._cond:
             changed = (paused != self._paused or health != self._health
                        or [d.device_uid for d in merged] != [d.device_uid for d in self._devices])
@@ -265,6 +343,9 @@ class AmdGpuDevicePlugin:
             self._write_id_map()
             log.info("advertising %d device(s) (%d healthy)%s", len(merged),
                      sum(1 for v in health.values() if v == api.HEALTHY), " [paused]" if paused else "")
+        if nonce:
+            # the reserved devices' Unhealthy state is published (ListAndWatch woken above)
+            self.gate.ack(nonce)
         return changed
 
     def _write_id_map(self) -> None:
@@ -435,6 +516,8 @@ class AmdGpuDevicePlugin:
             if now - last_health >= health_interval:
                 self.refresh()
                 last_health = now
+            elif self.gate is not None and self.gate.stamp() != self._gate_stamp:
+                self.refresh()      # a reservation / validation result: apply it within one poll
             stop_event.wait(poll)
         self.stop()
 

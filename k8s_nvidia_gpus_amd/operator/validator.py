@@ -18,14 +18,25 @@ the previous one's marker under ``/run/amd/validations``:
             100 ms window below stressMinFraction of the mean rate, hotspot ≤ stressMaxHotspotC
   rccl      RCCL all-reduce over xGMI across all GPUs of the node: exact sums + bus bandwidth floor
   plugin    a pod requesting amd.com/gpu: 1 is scheduled THROUGH the device plugin and passes
-  report    node label amd.com/gpu.validated=true|false, validator-ready marker
+  report    node label amd.com/gpu.validated=true|partial|deferred|false, validator-ready marker
 
 The load steps (gemm, bandwidth, stress, rccl) never touch a GPU that kubelet has allocated to a
 pod: the kubelet PodResources API (``podresources_api.py``) lists the device IDs pods hold, and the
-native tools run with ``ROCR_VISIBLE_DEVICES`` narrowed to the free agents — or the step is
-recorded as *deferred* (passed, with the reason) when none is free.  A validator restart whose
-node fingerprint (boot id, amdgpu version, operator image, validator config) equals the one of
-the last full pass re-uses that pass instead of loading the GPUs again.  On compute-partitioned
+native tools run with ``ROCR_VISIBLE_DEVICES`` narrowed to the free agents.  Closing the window
+between that answer and the launch: the step first *reserves* its agents (``in-test.json``; the
+device plugin reports them Unhealthy and acks with ``in-test.ack``), then re-reads PodResources
+and drops any agent a pod took in between — that agent is never loaded.  When no agent is free
+the step is *deferred*: no ``-ready`` marker, the init chain continues, and the node label says
+``deferred`` (never ``true``) until a full pass exists.  A kubelet that cannot be asked (socket
+absent or List failing) or an allocated ID that cannot be mapped *fails* the step: "nothing was
+validated" is never reported as validated.  Every agent a load step passed on is recorded per
+fingerprint (``device-passes.json``); the agents on which every enabled load step passed this
+boot are published in ``validated-devices.json``, which the device plugin gates on
+(``gateOnValidation``).
+
+A validator restart whose node fingerprint (boot id, amdgpu version, operator image, validator
+config, partition modes, agent set) equals the one of the last full pass re-uses that pass instead
+of loading the GPUs again.  On compute-partitioned
 GPUs (DPX/QPX/CPX) the TFLOPS and HBM floors scale with the partition's share of the ASIC, the
 GEMM runs at ``gemmSizePartitioned``, xGMI pair copies are skipped and RCCL runs over one agent
 per ASIC.
@@ -55,6 +66,14 @@ STEPS = ("driver", "runtime", "vectoradd", "gemm", "bandwidth", "stress", "rccl"
 LOAD_STEPS = ("gemm", "bandwidth", "stress", "rccl")
 LABEL_VALIDATED = "amd.com/gpu.validated"
 FINGERPRINT = "fingerprint.json"
+IN_TEST = "in-test.json"                  # {nonce, step, device_uids, expires}: plugin → Unhealthy
+IN_TEST_ACK = "in-test.ack"               # the plugin's ack: the nonce it has published
+DEVICE_PASSES = "device-passes.json"      # {fingerprint, steps: {step: [device_uid]}}
+VALIDATED_DEVICES = "validated-devices.json"  # {boot_id, device_uids}: the plugin's gate
+LABEL_TRUE, LABEL_PARTIAL, LABEL_DEFERRED, LABEL_FALSE = "true", "partial", "deferred", "false"
+# upper bound of a load step's run time, for the reservation's expiry (a crashed validator must not
+# leave GPUs reported Unhealthy forever)
+STEP_TIMEOUT = {"gemm": 2400.0, "bandwidth": 900.0, "rccl": 900.0}
 # kubelet device ID -> device_uid, written by the device plugin (needed for deviceIdStrategy: index)
 DEVICE_ID_MAP = "/run/amd/device-plugin/ids.json"
 
@@ -178,10 +197,16 @@ class GpuScope:
     allocated: Dict[str, str] = field(default_factory=dict)   # device_uid -> namespace/pod
     note: str = ""
     split: int = 1                                            # partitions per ASIC (CPX: 8)
+    error: str = ""                                           # kubelet could not be asked
+    from_kubelet: bool = False                                # free set came from PodResources
 
     @property
     def full(self) -> bool:
         return len(self.free) == len(self.devices)
+
+    @property
+    def free_uids(self) -> List[str]:
+        return [self.devices[i].device_uid for i in self.free]
 
     @property
     def known(self) -> bool:
@@ -199,19 +224,29 @@ class GpuScope:
 
     def to_dict(self) -> Dict:
         return {"full": self.full, "agents": len(self.devices), "split": self.split,
-                "validated": [self.devices[i].device_uid for i in self.free] if self.devices else [],
+                "validated": self.free_uids if self.devices else [],
                 "allocated": dict(self.allocated), "note": self.note}
 
 
 @dataclass
 class StepResult:
+    """``passed`` → ``<step>-ready``.  ``deferred`` steps did not run (no free GPU): not a pass
+    (no marker, the report never says ``true`` for them) but not a failure either (the init chain
+    continues)."""
     step: str
     passed: bool
     detail: Dict = field(default_factory=dict)
     reason: str = ""
+    deferred: bool = False
+
+    @property
+    def proceed(self) -> bool:
+        return self.passed or self.deferred
 
     def to_json(self) -> dict:
         d = {"step": self.step, "passed": self.passed, "reason": self.reason, "time": time.time()}
+        if self.deferred:
+            d["deferred_step"] = True
         d.update(self.detail)
         return d
 
@@ -225,6 +260,7 @@ class Validator:
         self.cfg = config
         self.device_id_map = device_id_map
         self._scope: Optional[GpuScope] = None
+        self._fp: Optional[Dict[str, str]] = None
         self.telemetry = telemetry  # per-GPU samples for the stress step (default: amd-smi)
         self.driver_wait = driver_wait  # kfd-probe --wait: how long the driver may take to appear
         self.vcfg = config.section("validator")
@@ -276,26 +312,27 @@ class Validator:
         except (OSError, ValueError):
             return {}
 
-    def gpu_scope(self) -> GpuScope:
-        """The free GPU agents: every agent minus what kubelet's PodResources API says pods hold.
-        Fails closed — an unreadable kubelet answer or an ID that cannot be mapped to a GPU leaves
-        no GPU free (the load steps are then deferred, never run on a tenant's GPU)."""
+    def _devices(self) -> List:
         from ..utils import topology as topo_mod
 
         try:
             topo = topo_mod.read_topology(self.root, self.cfg.min_gfx)
-            devs = sorted(topo.gpus, key=lambda g: g.node_id)
+            return sorted(topo.gpus, key=lambda g: g.node_id)
         except FileNotFoundError:
-            devs = []
-        split = max((g.partitions_on_asic for g in devs), default=1)
+            return []
+
+    def _allocated(self, devs) -> Tuple[Optional[Dict[str, str]], str]:
+        """({device_uid: "ns/pod"} held by pods, error).  ``None`` with no error: no kubelet here
+        and ``podResourcesRequired: false``."""
+        sock = str(self.vcfg["podResourcesSocket"])
         try:
-            alloc = podresources_api.allocated(self.cfg.resource_name,
-                                               str(self.vcfg["podResourcesSocket"]))
+            alloc = podresources_api.allocated(self.cfg.resource_name, sock)
         except Exception as e:  # noqa: BLE001 - kubelet unreachable: cannot prove a GPU is free
-            return GpuScope(devs, [], {}, f"PodResources List failed: {e}"[:300], split)
+            return None, f"kubelet PodResources List failed: {e}"[:300]
         if alloc is None:
-            return GpuScope(devs, list(range(len(devs))), {},
-                            "no kubelet PodResources socket: all agents", split)
+            if self.vcfg.get("podResourcesRequired", True):
+                return None, f"kubelet PodResources socket {sock} absent: cannot prove any GPU is free"
+            return None, ""
         idmap = self._kubelet_id_map(devs)
         busy: Dict[str, str] = {}
         unknown = []
@@ -306,14 +343,120 @@ class Validator:
             else:
                 busy[uid] = pod
         if unknown:
-            return GpuScope(devs, [], busy, "cannot map allocated device id(s) " + ",".join(unknown), split)
+            return busy, "cannot map allocated device id(s) " + ",".join(unknown) + \
+                " to GPUs (device plugin id map missing or stale)"
+        return busy, ""
+
+    def gpu_scope(self) -> GpuScope:
+        """The free GPU agents: every agent minus what kubelet's PodResources API says pods hold.
+        Fails closed — an unreadable kubelet answer or an ID that cannot be mapped to a GPU sets
+        ``error`` and leaves no GPU free (the load step then fails, never runs on a tenant's GPU)."""
+        devs = self._devices()
+        split = max((g.partitions_on_asic for g in devs), default=1)
+        busy, err = self._allocated(devs)
+        if err:
+            return GpuScope(devs, [], busy or {}, "", split, error=err)
+        if busy is None:
+            return GpuScope(devs, list(range(len(devs))), {},
+                            "no kubelet PodResources socket (podResourcesRequired: false): all agents",
+                            split)
         free = [i for i, g in enumerate(devs) if g.device_uid not in busy]
-        return GpuScope(devs, free, busy, "", split)
+        return GpuScope(devs, free, busy, "", split, from_kubelet=True)
 
     def scope(self) -> GpuScope:
         if self._scope is None:
             self._scope = self.gpu_scope()
         return self._scope
+
+    # ---------------------------------------------------------------- reservation (TOCTOU)
+    def _write_json(self, name: str, doc) -> None:
+        os.makedirs(self.marker_dir, exist_ok=True)
+        tmp = self._path(f".{name}.tmp")
+        with open(tmp, "w") as f:
+            json.dump(doc, f)
+        os.replace(tmp, self._path(name))
+
+    def _read_json(self, name: str):
+        try:
+            with open(self._path(name)) as f:
+                return json.load(f)
+        except (OSError, ValueError):
+            return None
+
+    def reserve(self, step: str, sc: GpuScope) -> Tuple[GpuScope, Dict]:
+        """Reserve ``sc``'s free agents for ``step`` and re-check them against kubelet.
+
+        1. ``in-test.json`` names the agents; the device plugin reports them Unhealthy (kubelet
+           stops handing them out) and writes the nonce to ``in-test.ack``.
+        2. After the ack (or ``reserveAckSeconds`` without one: no plugin is serving, so nothing
+           can be allocated through it) PodResources is read again; an agent a pod took since the
+           first answer is dropped from the scope and never loaded.
+        Returns the narrowed scope (``error`` set when the second answer cannot be had) and a
+        detail dict."""
+        secs = float(self.vcfg.get("reserveAckSeconds", 15))
+        nonce = f"{step}-{os.getpid()}-{time.time_ns()}"
+        timeout = STEP_TIMEOUT.get(step, float(self.vcfg.get("stressSeconds", 30)) + 300.0)
+        self._write_json(IN_TEST, {"nonce": nonce, "step": step, "device_uids": sc.free_uids,
+                                   "expires": time.time() + timeout})
+        deadline = time.monotonic() + secs
+        acked = False
+        while True:
+            try:
+                with open(self._path(IN_TEST_ACK)) as f:
+                    acked = f.read().strip() == nonce
+            except OSError:
+                acked = False
+            if acked or time.monotonic() >= deadline:
+                break
+            time.sleep(0.05)
+        busy, err = self._allocated(sc.devices)
+        info: Dict = {"nonce": nonce, "acked": acked}
+        if err:
+            return GpuScope(sc.devices, [], busy or {}, "", sc.split, error=err), info
+        busy = busy or {}
+        taken = {u: busy[u] for u in sc.free_uids if u in busy}
+        if taken:
+            info["taken_while_reserving"] = taken
+            log.warning("%s: %d GPU(s) allocated to pods while being reserved, left untouched: %s",
+                        step, len(taken), taken)
+        free = [i for i in sc.free if sc.devices[i].device_uid not in busy]
+        narrowed = GpuScope(sc.devices, free, busy, sc.note, sc.split, from_kubelet=True)
+        if taken:   # keep only the agents actually under test reported Unhealthy
+            self._write_json(IN_TEST, {"nonce": nonce, "step": step, "device_uids": narrowed.free_uids,
+                                       "expires": time.time() + timeout})
+        return narrowed, info
+
+    def release(self) -> None:
+        for name in (IN_TEST,):
+            try:
+                os.unlink(self._path(name))
+            except FileNotFoundError:
+                pass
+
+    # ---------------------------------------------------------------- per-device passes (gate)
+    def _gating_steps(self) -> List[str]:
+        return [s for s in LOAD_STEPS if self._enabled(s)] or ["driver"]
+
+    def record_pass(self, step: str, uids: Sequence[str]) -> List[str]:
+        """Add ``uids`` to ``step``'s passes for the current fingerprint; republish the agents on
+        which every gating step has passed (``validated-devices.json``).  Returns that list."""
+        fp = self.fingerprint()
+        doc = self._read_json(DEVICE_PASSES) or {}
+        if doc.get("fingerprint") != fp:
+            doc = {"fingerprint": fp, "steps": {}}
+        doc["steps"][step] = sorted(set(doc["steps"].get(step, [])) | set(uids))
+        self._write_json(DEVICE_PASSES, doc)
+        sets = [set(doc["steps"].get(s, [])) for s in self._gating_steps()]
+        validated = sorted(set.intersection(*sets)) if sets else []
+        self._write_json(VALIDATED_DEVICES, {"boot_id": fp.get("boot_id", ""), "device_uids": validated,
+                                             "time": time.time()})
+        return validated
+
+    def validated_devices(self) -> List[str]:
+        doc = self._read_json(VALIDATED_DEVICES) or {}
+        if doc.get("boot_id") != self.fingerprint().get("boot_id"):
+            return []
+        return list(doc.get("device_uids") or [])
 
     def _cmd(self, argv: List[str], indices: Optional[Sequence[int]] = None) -> List[str]:
         """argv narrowed to the free agents (or to ``indices``) with ROCR_VISIBLE_DEVICES."""
@@ -322,6 +465,15 @@ class Validator:
         return self._scope.env_prefix(indices) + list(argv)
 
     def fingerprint(self) -> Dict[str, str]:
+        """What a full pass is valid for.  Besides boot / driver / image / config it covers the GPU
+        topology: a compute/memory partition switch re-enumerates the agents without a reboot, so
+        the partition modes, the agent count and the sorted device UIDs are part of it (an SPX pass
+        must not stand in for the CPX agents after a switch)."""
+        if self._fp is None:
+            self._fp = self._fingerprint()
+        return self._fp
+
+    def _fingerprint(self) -> Dict[str, str]:
         from .labeller import driver_version
 
         fp: Dict[str, str] = {}
@@ -333,6 +485,10 @@ class Validator:
         fp["amdgpu"] = driver_version(self.root) or ""
         fp["image"] = os.environ.get("VALIDATOR_IMAGE_ID") or self._own_image_id()
         fp["config"] = json.dumps(self.vcfg, sort_keys=True, default=str)
+        devs = self._devices()
+        fp["partition"] = ",".join(sorted({f"{g.compute_partition}/{g.memory_partition}" for g in devs}))
+        fp["agents"] = str(len(devs))
+        fp["device_uids"] = ",".join(sorted(g.device_uid for g in devs))
         return fp
 
     def _own_image_id(self) -> str:
@@ -364,7 +520,7 @@ class Validator:
         if not saved.get("full") or saved.get("fingerprint") != self.fingerprint() or not prev.get("passed"):
             return None
         keep = {k: prev[k] for k in ("aggregate_tflops", "min_by_test_gbps", "peak_busbw_gbps", "time",
-                                     "deferred") if k in prev}
+                                     "reused") if k in prev}
         return {"since": saved.get("time"), **keep}
 
     # ---------------------------------------------------------------- steps
@@ -652,7 +808,7 @@ class Validator:
                 log.warning("cannot read own pod image: %s", e)
         return os.environ.get("VALIDATOR_IMAGE", "ghcr.io/example-org/amd-gpu-operator:0.1.0")
 
-    def step_report(self) -> StepResult:
+    def required_steps(self) -> List[str]:
         required = ["driver", "runtime"]
         if self.vcfg["vectorAdd"]:
             required.append("vectoradd")
@@ -666,59 +822,101 @@ class Validator:
             required.append("rccl")
         if self.vcfg["pluginTest"]:
             required.append("plugin")
-        missing = [s for s in required if not self.ready(s)]
-        ok = not missing
+        return required
+
+    def _has_full_pass(self) -> bool:
+        saved = self._read_json(FINGERPRINT) or {}
+        return bool(saved.get("full")) and saved.get("fingerprint") == self.fingerprint()
+
+    def node_label(self) -> Tuple[str, Dict]:
+        """(label value, detail) from the recorded step results.
+
+        ``false``    a required step failed or never recorded a result
+        ``deferred`` a load step could not run (every GPU allocated) and no full pass exists for
+                     the current fingerprint
+        ``partial``  every step passed, but a load step ran on a subset of the GPUs, and no full
+                     pass exists for the current fingerprint
+        ``true``     every step passed on every GPU — now, or in a full pass for this fingerprint
+        """
+        required = self.required_steps()
+        failed, deferred, subset, docs = [], [], [], {}
+        for st in required:
+            d = self._read_json(f"{st}.json")
+            docs[st] = d
+            if d is None:
+                if not self.ready(st):      # a marker another agent published counts as a pass
+                    failed.append(st)
+            elif d.get("deferred_step"):
+                deferred.append(st)
+            elif not d.get("passed") or not self.ready(st):
+                failed.append(st)
+            elif st in LOAD_STEPS and "previous" not in d and not d.get("skipped") \
+                    and not (d.get("gpu_scope") or {}).get("full", True):
+                subset.append(st)
+        full = not failed and not deferred and not subset
+        prior = self._has_full_pass()
+        if failed:
+            label = LABEL_FALSE
+        elif full or prior:
+            label = LABEL_TRUE
+        else:
+            label = LABEL_DEFERRED if deferred else LABEL_PARTIAL
+        return label, {"required": required, "failed": failed, "deferred": deferred,
+                       "subset": subset, "full_validation": full, "prior_full_pass": prior,
+                       "docs": docs}
+
+    def step_report(self) -> StepResult:
+        label, info = self.node_label()
+        docs = info.pop("docs")
+        ok = label == LABEL_TRUE
         if self.kube is not None and self.node:
             try:
-                self.kube.set_node_labels(self.node, {LABEL_VALIDATED: "true" if ok else "false"})
+                self.kube.set_node_labels(self.node, {LABEL_VALIDATED: label})
             except Exception as e:  # noqa: BLE001
                 log.warning("cannot label node: %s", e)
         durations = {}
         no_duration = []
-        for st in required:
-            try:
-                with open(self._path(f"{st}.json")) as f:
-                    d = json.load(f).get("duration_s")
-            except (OSError, ValueError):
-                d = None
+        for st in info["required"]:
+            d = (docs.get(st) or {}).get("duration_s")
             if d is not None:
                 durations[st] = d
             else:
                 no_duration.append(st)
         # chain_seconds is only a complete time-to-validated when every required step is timed;
         # the untimed ones are listed instead of being silently counted as zero
-        r = StepResult("report", ok, {"required": required, "missing": missing,
+        missing = info["failed"] + info["deferred"]
+        reason = ""
+        if info["failed"]:
+            reason = "failed/missing: " + ",".join(info["failed"])
+        elif not ok:
+            reason = (f"deferred: {','.join(info['deferred'])}" if info["deferred"] else
+                      f"ran on a subset of the GPUs: {','.join(info['subset'])}") + \
+                " (no full pass for this boot/topology yet)"
+        r = StepResult("report", ok, {**info, "label": label, "missing": missing,
+                                      "validated_devices": self.validated_devices(),
                                       "step_seconds": durations,
                                       "step_seconds_missing": no_duration,
                                       "chain_seconds": round(sum(durations.values()), 3),
                                       "chain_complete": not no_duration},
-                       "" if ok else "failed/missing: " + ",".join(missing))
-        full = True
-        for st in LOAD_STEPS:
-            if st not in required:
-                continue
-            try:
-                with open(self._path(f"{st}.json")) as f:
-                    d = json.load(f)
-            except (OSError, ValueError):
-                full = False
-                continue
-            if d.get("deferred") and "previous" not in d:
-                full = False     # deferred for allocation: not a full validation
-            elif not d.get("deferred") and not d.get("skipped") and not (d.get("gpu_scope") or {}).get("full", True):
-                full = False     # ran on a subset of the GPUs
-        r.detail["full_validation"] = full
-        if ok and full:
-            tmp = self._path(f".{FINGERPRINT}.tmp")
-            with open(tmp, "w") as f:
-                json.dump({"full": True, "time": time.time(), "fingerprint": self.fingerprint()}, f)
-            os.replace(tmp, self._path(FINGERPRINT))
+                       reason, deferred=label in (LABEL_DEFERRED, LABEL_PARTIAL))
+        if info["full_validation"]:
+            self._write_json(FINGERPRINT, {"full": True, "time": time.time(),
+                                           "fingerprint": self.fingerprint()})
         if ok:
             with open(self._path("validator-ready"), "w") as f:
                 f.write(f"{time.time()}\n")
         elif os.path.exists(self._path("validator-ready")):
             os.unlink(self._path("validator-ready"))
         return r
+
+    def pending_devices(self) -> List[str]:
+        """Free agents (per kubelet, now) not yet validated this boot — what a re-run of the chain
+        would validate.  Empty when kubelet cannot be asked."""
+        sc = self.gpu_scope()
+        if sc.error:
+            return []
+        done = set(self.validated_devices())
+        return [u for u in sc.free_uids if u not in done]
 
     # ---------------------------------------------------------------- driver
     def run_step(self, step: str) -> StepResult:
@@ -737,24 +935,56 @@ class Validator:
         # per-step wall time: the report sums them into the node's time-to-validated breakdown
         r.detail.setdefault("duration_s", round(time.monotonic() - t0, 3))
         self.write_result(r)
-        log.info("step %s: %s %s", step, "PASSED" if r.passed else "FAILED", r.reason)
+        log.info("step %s: %s %s", step,
+                 "PASSED" if r.passed else "DEFERRED" if r.deferred else "FAILED", r.reason)
         return r
 
     def _run_step(self, step: str) -> StepResult:
         if step in LOAD_STEPS and self._enabled(step):
             prev = self._unchanged_pass(step)
             if prev is not None:
-                return StepResult(step, True, {"deferred": "node fingerprint unchanged since the last "
-                                                           "full validation", "previous": prev})
-            sc = self.scope()
+                return StepResult(step, True, {"reused": "node fingerprint unchanged since the last "
+                                                         "full validation", "previous": prev})
+            # a fresh kubelet answer per load step (steps run minutes apart)
+            sc = self._scope = self.gpu_scope()
+            if sc.error:
+                return StepResult(step, False, {"gpu_scope": sc.to_dict()}, sc.error)
             if sc.known and not sc.free:
-                return StepResult(step, True, {
-                    "deferred": sc.note or f"all {len(sc.devices)} GPU agent(s) allocated to pods",
-                    "gpu_scope": sc.to_dict()})
-            r = self._run_load_step(step)
+                return self._deferred(step, sc, f"all {len(sc.devices)} GPU agent(s) allocated to pods")
+            reservation = None
+            try:
+                if sc.known and sc.from_kubelet:
+                    sc, reservation = self.reserve(step, sc)
+                    self._scope = sc
+                    if sc.error:
+                        return StepResult(step, False, {"gpu_scope": sc.to_dict(),
+                                                        "reservation": reservation}, sc.error)
+                    if not sc.free:
+                        return self._deferred(step, sc, "every free GPU was allocated to a pod "
+                                                        "while being reserved", reservation)
+                r = self._run_load_step(step)
+            finally:
+                if reservation is not None:
+                    self.release()
             r.detail["gpu_scope"] = sc.to_dict()
+            if reservation is not None:
+                r.detail["reservation"] = reservation
+            if r.passed and sc.known:
+                r.detail["validated_devices"] = self.record_pass(step, sc.free_uids)
             return r
-        return self._run_load_step(step)
+        r = self._run_load_step(step)
+        if r.passed and step == "driver" and self._gating_steps() == ["driver"]:
+            # no load step enabled: the gate opens on the driver check alone
+            devs = self._devices()
+            if devs:
+                r.detail["validated_devices"] = self.record_pass("driver", [g.device_uid for g in devs])
+        return r
+
+    def _deferred(self, step: str, sc: GpuScope, why: str, reservation=None) -> StepResult:
+        detail = {"deferred": why, "gpu_scope": sc.to_dict()}
+        if reservation is not None:
+            detail["reservation"] = reservation
+        return StepResult(step, False, detail, f"deferred: {why}", deferred=True)
 
     def _enabled(self, step: str) -> bool:
         return bool(self.vcfg[{"gemm": "gemm", "bandwidth": "bandwidth", "stress": "stress",
@@ -791,3 +1021,47 @@ class Validator:
         else:
             raise ValueError(f"unknown step {step!r}; steps: {STEPS}")
         return r
+
+
+def hold_loop(v: "Validator", marker_dir: str, interval: float = 30.0,
+              stop: Optional[Callable[[], bool]] = None, sleep: Callable[[float], None] = time.sleep) -> int:
+    """The report container's life after the chain: restart the chain when it has to run again.
+
+    * the driver marker is withdrawn (driver restart / GPU reset), or
+    * the node is ``deferred`` / ``partial`` and kubelet now shows a free GPU that has not been
+      validated this boot (polled every ``retryDeferredSeconds``).
+    A container restart would not re-run init containers, so the chain is restarted by deleting
+    this pod (the DaemonSet recreates it); without API access the container exits (code 3).
+    Returns the exit code."""
+    retry = float(v.vcfg.get("retryDeferredSeconds", 300))
+    last_check = time.monotonic()
+    why = ""
+    while not (stop and stop()):
+        if not os.path.exists(os.path.join(marker_dir, "driver-ready")):
+            why = "driver-ready withdrawn"
+            break
+        if time.monotonic() - last_check >= retry:
+            last_check = time.monotonic()
+            label, _ = v.node_label()
+            if label in (LABEL_DEFERRED, LABEL_PARTIAL):
+                pending = v.pending_devices()
+                if pending:
+                    why = f"node {label}: {len(pending)} free GPU(s) not yet validated this boot"
+                    break
+        sleep(interval)
+    else:
+        return 0
+    log.info("re-running the validation chain: %s", why)
+    return 3 if not restart_own_pod(v) else 0
+
+
+def restart_own_pod(v: "Validator") -> bool:
+    pod, ns = os.environ.get("POD_NAME"), os.environ.get("POD_NAMESPACE", "amd-gpu-operator")
+    if v.kube is None or not pod:
+        return False
+    try:
+        v.kube.delete_pod(ns, pod)
+        return True
+    except Exception as e:  # noqa: BLE001 - fall back to exiting
+        log.warning("cannot delete own pod %s/%s: %s", ns, pod, e)
+        return False

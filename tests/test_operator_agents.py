@@ -364,7 +364,7 @@ def test_validator_gemm_step_under_rocprof(tmp_path):
             f'"{kernels[dtype]}",60,47700000,795000.0,98.9,782807,1030849,66849.2\n')
         return 0, logs[dtype]
 
-    cfg = load_config(text="validator: {rocprof: true}\n")
+    cfg = load_config(text="validator: {rocprof: true, podResourcesRequired: false}\n")
     r = Validator(cfg, str(tmp_path), bin_dir="/b", runner=runner).run_step("gemm")
     assert r.passed and seen[0][:3] == ["rocprofv3", "--kernel-trace", "--stats"]
     assert r.detail["rocprof_kernels"][0]["name"] == "amdk8s_gemm_bf16_nt_256x256"

@@ -64,7 +64,7 @@ def test_exporter_on_real_amdsmi():
 
 
 def test_validator_chain_with_native_binaries(tmp_path, native):
-    cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {gemmSize: 4096, gemmMinTflops: 600, "
+    cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {podResourcesRequired: false, gemmSize: 4096, gemmMinTflops: 600, "
                            "rccl: false, pluginTest: false, rocprofCounters: true}\n")
     v = Validator(cfg, str(tmp_path), bin_dir=str(native))
     for step in ("driver", "vectoradd", "gemm", "bandwidth"):
@@ -168,7 +168,7 @@ def test_node_bringup_rehearsal_on_real_hardware(tmp_path, native):
 
 def test_validator_stress_step_on_real_hardware(tmp_path, native):
     """5 s of sustained MFMA load with real amd-smi telemetry: steady rate, no ECC, sane temperatures."""
-    cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {stress: true, stressSeconds: 5}\n")
+    cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {podResourcesRequired: false, stress: true, stressSeconds: 5}\n")
     v = Validator(cfg, str(tmp_path), bin_dir=str(native))
     r = v.run_step("stress")
     assert r.passed, r.reason

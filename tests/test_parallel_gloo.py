@@ -136,6 +136,102 @@ def test_bench_settle_phase_bounds():
     assert bench.settle(step, lambda: None, 1e6, chunk=4, max_launches=12) == 12 == len(calls)
 
 
+def test_bench_timed_window_order():
+    """Sampler init → thread start → settle → warmup → t0 → K steps: between the last warmup step
+    and the first timed step only sync/barrier and the sampler's clock marks may run (r03's
+    amd-smi init in that gap cost the driver's K=20/W=5 headline 14 %)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", REPO / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    log = []
+
+    class FakeSampler:
+        def __init__(self):
+            log.append("init")                       # amdsmi_init + handle scan
+
+        def __enter__(self):
+            log.append("thread")
+            return self
+
+        def hold(self):
+            log.append("hold")
+
+        def mark_start(self):
+            log.append("mark_start")
+
+        def mark_launched(self):
+            log.append("mark_launched")
+
+        def mark_end(self):
+            log.append("mark_end")
+
+        def __exit__(self, *exc):
+            log.append("exit")
+
+    sampler = FakeSampler()
+    elapsed, launches = bench.timed_window(lambda: log.append("step"), lambda: log.append("sync"),
+                                           lambda: log.append("barrier"), steps=20, warmup=5,
+                                           settle_ms=0.5, sampler=sampler)
+    assert elapsed > 0 and launches >= 8
+    assert log[:2] == ["init", "thread"]
+    i_start = log.index("mark_start")
+    # exactly K steps inside the marks, and they are the last K steps issued
+    inside = log[i_start:log.index("mark_end")]
+    assert inside.count("step") == 20
+    assert log.count("step") == launches + 5 + 20
+    # the gap between the last untimed step and the first timed one holds no real work
+    last_warm = max(i for i, e in enumerate(log[:i_start]) if e == "step")
+    assert set(log[last_warm + 1:i_start + 1]) <= {"sync", "barrier", "hold", "mark_start"}
+    assert log[last_warm + 1] == "hold"             # quiet before the GPU drains the warmup
+    assert log[i_start + 1] == "step" and log[-1] == "exit"
+    # held quiet while the K steps are launched, sampling again while they execute
+    i_launched = log.index("mark_launched")
+    assert log.index("hold") < i_start and log[i_start:i_launched].count("step") == 20 and "sync" not in log[i_start:i_launched]
+    # the real Sampler does its amd-smi setup in the constructor, not in __enter__/mark_start
+    from k8s_nvidia_gpus_amd.parallel.telemetry import Sampler
+
+    calls = []
+
+    class FakeSmi:
+        def amdsmi_init(self):
+            calls.append("init")
+
+        def amdsmi_get_processor_handles(self):
+            calls.append("handles")
+            return ["h0"]
+
+        def amdsmi_get_gpu_device_bdf(self, h):
+            return "0000:05:00.0"
+
+        def amdsmi_get_gpu_metrics_info(self, h):
+            return {"current_gfxclk": 2100, "current_socket_power": 900, "temperature_hotspot": 70}
+
+        def amdsmi_shut_down(self):
+            calls.append("shutdown")
+
+    s = Sampler("0000:05:00.0", period=0.001, amdsmi_module=FakeSmi())
+    assert calls == ["init", "handles"]
+    before = len(calls)
+    with s:
+        import time as _t
+
+        _t.sleep(0.01)
+        s.hold()
+        s.mark_start()
+        n_held = len(s.rows)
+        _t.sleep(0.01)
+        assert len(s.rows) == n_held          # quiet while launching
+        s.mark_launched()
+        _t.sleep(0.01)
+        s.mark_end()
+        assert len(calls) == before
+    summ = s.summary()
+    assert summ["gfxclk_mhz_mean"] == 2100 and 1 <= summ["samples"] < len(s.rows)
+    assert calls[-1] == "shutdown"
+
+
 def test_rccl_bench_multiprocess_plan_under_torchrun():
     """rccl-allreduce-bench --mp takes its rank/world/device from torchrun (--no-python) — the
     launch the gpu-bench Job uses; --plan stops before any HIP call so this runs on CPU."""

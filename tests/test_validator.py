@@ -58,7 +58,7 @@ class Runner:
 
 @pytest.fixture
 def cfg():
-    return load_config(text="expectedGpusPerNode: 1\nvalidator: {gemmMinTflops: 900, rcclMinBusbwGBps: 100}\n")
+    return load_config(text="expectedGpusPerNode: 1\nvalidator: {podResourcesRequired: false, gemmMinTflops: 900, rcclMinBusbwGBps: 100}\n")
 
 
 def test_protocol_parser():
@@ -84,7 +84,7 @@ def test_vectoradd_and_gemm_steps_on_real_outputs(tmp_path, cfg):
 
 def test_report_carries_per_step_durations(tmp_path):
     """Every step records its wall time; the report sums the required ones (time-to-validated)."""
-    cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {gemmMinTflops: 900, rccl: false, "
+    cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {podResourcesRequired: false, gemmMinTflops: 900, rccl: false, "
                            "pluginTest: false}\n")
     r = Runner({"amd-vectoradd": (0, VECTORADD_LOG), "amd-gemm-validator": (0, GEMM_LOG),
                 "amd-gemm-validator:fp8": (0, GEMM_FP8_LOG), "amd-proftester": (0, PROFTESTER_LOG)})
@@ -104,7 +104,7 @@ def test_report_carries_per_step_durations(tmp_path):
 
 
 def test_gemm_step_enforces_tflops_floor(tmp_path):
-    cfg = load_config(text="validator: {gemmMinTflops: 2000}\n")
+    cfg = load_config(text="validator: {podResourcesRequired: false, gemmMinTflops: 2000}\n")
     v = Validator(cfg, str(tmp_path), bin_dir="/x",
                   runner=Runner({"amd-gemm-validator": (0, GEMM_LOG),
                                  "amd-gemm-validator:fp8": (0, GEMM_FP8_LOG)}))
@@ -228,14 +228,14 @@ def test_gemm_step_runs_fp8_on_real_output(tmp_path, cfg):
     assert d["fp8"]["aggregate_tflops"] > 2 * 1300
     assert d["fp8"]["devices"][0]["check"] == "gemm_fp8"
 
-    strict = load_config(text="validator: {gemmFp8MinTflops: 10000}\n")
+    strict = load_config(text="validator: {podResourcesRequired: false, gemmFp8MinTflops: 10000}\n")
     v2 = Validator(strict, str(tmp_path / "s"), bin_dir="/x", runner=r)
     g2 = v2.run_step("gemm")
     assert not g2.passed and "fp8" in g2.reason
 
 
 def test_gemm_step_fp8_can_be_disabled(tmp_path):
-    cfg = load_config(text="validator: {gemmFp8: false}\n")
+    cfg = load_config(text="validator: {podResourcesRequired: false, gemmFp8: false}\n")
     r = Runner({"amd-gemm-validator": (0, GEMM_LOG)})  # no fp8 output available: must not be run
     v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=r)
     assert v.run_step("gemm").passed
@@ -295,7 +295,7 @@ def test_unknown_step_still_raises(tmp_path, cfg):
 
 def test_report_lists_required_steps_without_duration(tmp_path):
     """chain_seconds must not silently treat an untimed required step as 0 s."""
-    cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {rccl: false, pluginTest: false, "
+    cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {podResourcesRequired: false, rccl: false, pluginTest: false, "
                            "gemm: false, vectorAdd: false, bandwidth: false}\n")
     v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=Runner({}))
     (tmp_path / "driver.json").write_text(json.dumps({"step": "driver", "passed": True, "duration_s": 2.0}))
@@ -324,7 +324,7 @@ def test_bandwidth_step_on_real_mi355x_output(tmp_path, cfg):
 
 
 def test_bandwidth_step_enforces_floors(tmp_path):
-    cfg = load_config(text="validator: {hbmMinGBps: 9000}\n")
+    cfg = load_config(text="validator: {podResourcesRequired: false, hbmMinGBps: 9000}\n")
     v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=Runner({"amd-proftester": (0, PROFTESTER_LOG)}))
     b = v.run_step("bandwidth")
     assert not b.passed and "hbm-copy dev 0" in b.reason and "< 9000" in b.reason
@@ -383,7 +383,7 @@ def test_rocprof_counter_summary_on_real_mi355x_csv():
 def test_gemm_step_runs_a_counter_pass(tmp_path):
     import shutil
 
-    cfg = load_config(text="validator: {gemmMinTflops: 900, rocprofCounters: true, gemmFp8: false}\n")
+    cfg = load_config(text="validator: {podResourcesRequired: false, gemmMinTflops: 900, rocprofCounters: true, gemmFp8: false}\n")
     gemm_log = GEMM_LOG.replace('"arch": "gfx950:sramecc+:xnack-", ', '"arch": "gfx950:sramecc+:xnack-", "cus": 256, ')
     calls = []
 
@@ -437,7 +437,7 @@ class Telemetry:
 
 
 def _stress_validator(tmp_path, out, tel, rc=0):
-    cfg = load_config(text="validator: {stress: true, stressSeconds: 0.3}\n")
+    cfg = load_config(text="validator: {podResourcesRequired: false, stress: true, stressSeconds: 0.3}\n")
 
     def runner(argv, timeout):
         import time as _t

@@ -1,18 +1,23 @@
 """Validator GPU scope: GPUs that kubelet allocated to pods are never loaded, a fully allocated node
-defers the load steps without failing, an unchanged node re-uses its last full pass, and
-compute-partitioned (CPX) nodes validate against per-partition floors.
+defers the load steps (label ``deferred``, never ``true``), an unreachable kubelet fails them, a GPU
+allocated between the PodResources answer and the launch is left untouched (reservation + re-read),
+the device plugin gates GPUs on this boot's validation, an unchanged node re-uses its last full
+pass (but a partition switch does not), and compute-partitioned (CPX) nodes validate against
+per-partition floors.
 
 kubelet's PodResources API is served by tests/fakes/podresources.py over a real unix socket; the
 node is the fake MI355X sysfs tree (tests/fakes/sysfs.py) with 8 ASICs (64 CPX agents)."""
 import json
 import os
+import time
 
 import pytest
 
 from fakes import sysfs as fake_sysfs
 from fakes.podresources import FakePodResources
 from k8s_nvidia_gpus_amd.operator.config import load_config
-from k8s_nvidia_gpus_amd.operator.validator import FINGERPRINT, Validator
+from k8s_nvidia_gpus_amd.operator.validator import (FINGERPRINT, IN_TEST, VALIDATED_DEVICES,
+                                                    Validator, hold_loop)
 from k8s_nvidia_gpus_amd.utils.topology import read_topology
 from test_validator import GEMM_FP8_LOG, RCCL_8GPU, Runner
 
@@ -41,7 +46,7 @@ def _node(tmp_path, mode="SPX", boot="boot-1"):
 def _cfg(tmp_path, extra=""):
     sock = tmp_path / "pod-resources/kubelet.sock"
     text = (f"expectedGpusPerNode: 8\nvalidator: {{gemmMinTflops: 900, gemmFp8: false, "
-            f"podResourcesSocket: {sock}, rccl: true, bandwidth: false{extra}}}\n")
+            f"podResourcesSocket: {sock}, rccl: true, bandwidth: false, reserveAckSeconds: 0.2{extra}}}\n")
     return load_config(text=text), str(sock)
 
 
@@ -72,37 +77,245 @@ def test_allocated_gpus_are_excluded(tmp_path):
     sc = g.detail["gpu_scope"]
     assert not sc["full"] and sc["allocated"] == {uids[2]: "llm/coder-llm-0", uids[5]: "llm/coder-llm-0"}
     assert uids[2] not in sc["validated"] and len(sc["validated"]) == 6
-    # a partial validation never becomes the node's fingerprint
-    v.run_step("report")
+    # a partial validation never becomes the node's fingerprint, and the node is not "validated"
+    for st in ("driver", "runtime", "vectoradd", "plugin", "bandwidth", "stress"):
+        (tmp_path / "m" / f"{st}-ready").write_text("1\n")
+    rep = v.run_step("report")
+    assert not rep.passed and rep.detail["label"] == "partial" and rep.proceed
     assert not os.path.exists(tmp_path / "m" / FINGERPRINT)
+    assert not os.path.exists(tmp_path / "m" / "validator-ready")
+    # only the GPUs the load steps actually ran on are validated for the plugin's gate
+    assert sorted(rep.detail["validated_devices"]) == sorted(sc["validated"])
 
 
-def test_fully_allocated_node_defers_without_failure(tmp_path):
+class _Kube:
+    def __init__(self):
+        self.labels = {}
+        self.deleted = []
+
+    def set_node_labels(self, node, labels):
+        self.labels.update(labels)
+
+    def delete_pod(self, ns, name):
+        self.deleted.append((ns, name))
+
+
+def _chain_markers(marker, steps=("driver", "runtime", "vectoradd", "plugin")):
+    marker.mkdir(exist_ok=True)
+    for st in steps:
+        (marker / f"{st}-ready").write_text("1\n")
+
+
+def test_fully_allocated_node_defers_and_is_not_labelled_validated(tmp_path):
+    """First boot, every GPU already taken: nothing is loaded, no load step gets a -ready marker,
+    the chain goes on (proceed), and the node label says "deferred" — not "true"."""
     root = _node(tmp_path)
     cfg, sock = _cfg(tmp_path)
     pods = {("train", f"job-{i}"): [("amd.com/gpu", [u])] for i, u in enumerate(_uids(root))}
     r = Runner({})
+    kube = _Kube()
+    _chain_markers(tmp_path / "m")
     with FakePodResources(sock, pods):
-        v = Validator(cfg, str(tmp_path / "m"), bin_dir="/x", runner=r, root=str(root))
-        for step in ("gemm", "rccl", "stress", "bandwidth"):
+        v = Validator(cfg, str(tmp_path / "m"), bin_dir="/x", runner=r, root=str(root), kube=kube,
+                      node_name="n1")
+        for step in ("gemm", "rccl"):
             res = v.run_step(step)
-            assert res.passed, step
+            assert not res.passed and res.deferred and res.proceed, step
+        for step in ("stress", "bandwidth"):                # disabled in this config
+            assert v.run_step(step).detail.get("skipped")
+        rep = v.run_step("report")
     assert r.calls == []                                   # no GPU was touched
     d = json.loads((tmp_path / "m/gemm.json").read_text())
     assert "allocated" in d["deferred"] and d["gpu_scope"]["validated"] == []
-    assert (tmp_path / "m/gemm-ready").exists()
+    assert not (tmp_path / "m/gemm-ready").exists()
+    assert not rep.passed and rep.detail["label"] == "deferred"
+    assert kube.labels == {"amd.com/gpu.validated": "deferred"}
+    assert rep.detail["validated_devices"] == []
+    assert not (tmp_path / "m/validator-ready").exists()
 
 
-def test_unreadable_kubelet_answer_fails_closed(tmp_path):
+def test_unreachable_kubelet_fails_the_step_and_the_node(tmp_path):
     root = _node(tmp_path)
     cfg, sock = _cfg(tmp_path)
     os.makedirs(os.path.dirname(sock))
     with open(sock, "w") as f:                              # a socket path nobody serves
         f.write("")
     r = Runner({})
-    v = Validator(cfg, str(tmp_path / "m"), bin_dir="/x", runner=r, root=str(root))
+    kube = _Kube()
+    _chain_markers(tmp_path / "m")
+    v = Validator(cfg, str(tmp_path / "m"), bin_dir="/x", runner=r, root=str(root), kube=kube,
+                  node_name="n1")
     res = v.run_step("gemm")
-    assert res.passed and "PodResources" in res.detail["deferred"] and r.calls == []
+    assert not res.passed and not res.deferred and "PodResources" in res.reason and r.calls == []
+    assert not res.proceed                                  # the init container fails
+    v.run_step("rccl")
+    rep = v.run_step("report")
+    assert rep.detail["label"] == "false" and kube.labels["amd.com/gpu.validated"] == "false"
+    assert "gemm" in rep.detail["failed"]
+
+
+def test_absent_kubelet_socket_fails_unless_not_required(tmp_path):
+    root = _node(tmp_path)
+    cfg, sock = _cfg(tmp_path)                              # socket path never created
+    r = Runner({"amd-gemm-validator": (0, _gemm_log(8, 1500.0))})
+    res = Validator(cfg, str(tmp_path / "m"), bin_dir="/x", runner=r, root=str(root)).run_step("gemm")
+    assert not res.passed and "absent" in res.reason and r.calls == []
+    cfg.raw["validator"]["podResourcesRequired"] = False    # bare box (bring-up rehearsal)
+    res = Validator(cfg, str(tmp_path / "m2"), bin_dir="/x", runner=r, root=str(root)).run_step("gemm")
+    assert res.passed and r.calls and r.calls[0][0] != "env"
+
+
+class _RacingPodResources(FakePodResources):
+    """The second List answer (after the validator's reservation) shows a pod that took a GPU in
+    between the first answer and the launch."""
+
+    def __init__(self, sock, pods, late):
+        super().__init__(sock, pods)
+        self.late = late
+
+    def List(self, request, context):  # noqa: N802
+        if self.calls == 1:
+            self.pods.update(self.late)
+        return super().List(request, context)
+
+
+def test_gpu_allocated_between_list_and_launch_is_left_untouched(tmp_path):
+    root = _node(tmp_path)
+    cfg, sock = _cfg(tmp_path)
+    uids = _uids(root)
+    seen_reservation = []
+
+    class R(Runner):
+        def __call__(self, argv, timeout):
+            seen_reservation.append(json.loads((tmp_path / "m" / IN_TEST).read_text()))
+            return super().__call__(argv, timeout)
+
+    r = R({"amd-gemm-validator": (0, _gemm_log(7, 1500.0))})
+    late = {("llm", "coder-llm-0"): [("amd.com/gpu", [uids[3]])]}
+    with _RacingPodResources(sock, {}, late) as fake:
+        v = Validator(cfg, str(tmp_path / "m"), bin_dir="/x", runner=r, root=str(root))
+        g = v.run_step("gemm")
+    assert fake.calls == 2                                  # answer, reserve, re-read
+    assert g.passed
+    assert g.detail["reservation"]["taken_while_reserving"] == {uids[3]: "llm/coder-llm-0"}
+    assert _narrowed(r.calls[0]) == ["0", "1", "2", "4", "5", "6", "7"]   # GPU 3 never loaded
+    # while the GEMM ran, the reservation named exactly the GPUs under test
+    assert uids[3] not in seen_reservation[0]["device_uids"] and len(seen_reservation[0]["device_uids"]) == 7
+    assert not (tmp_path / "m" / IN_TEST).exists()          # released afterwards
+    assert uids[3] not in g.detail["validated_devices"]
+
+
+def test_plugin_gates_on_validation_and_reports_reserved_gpus_unhealthy(tmp_path):
+    """First boot: the plugin advertises every GPU Unhealthy until the validator's load steps passed
+    on it; during a load step the GPUs under test are Unhealthy and the plugin acks the
+    reservation; after the pass exactly the validated GPUs turn Healthy."""
+    import threading
+
+    from k8s_nvidia_gpus_amd.operator import deviceplugin_api as api
+    from k8s_nvidia_gpus_amd.operator.device_plugin import AmdGpuDevicePlugin, ValidationGate
+
+    root = _node(tmp_path)
+    cfg, sock = _cfg(tmp_path, ", rccl: false, reserveAckSeconds: 5")
+    uids = _uids(root)
+    marker = tmp_path / "m"
+    marker.mkdir()
+    gate = ValidationGate(str(marker), root=str(root), gate=True)
+    plugin = AmdGpuDevicePlugin(cfg, root=str(root), kubelet_dir=str(tmp_path / "kd"), pause_marker=None,
+                                dev_prefix=str(root / "dev"), gate=gate, ecc_fn=lambda d: 0)
+    health = lambda: {d.ID: d.health for d in plugin.list_response().devices}  # noqa: E731
+    assert set(health().values()) == {api.UNHEALTHY}        # nothing validated this boot yet
+    stop = threading.Event()
+    loop = threading.Thread(target=plugin.run, kwargs={"poll": 0.02, "stop_event": stop,
+                                                        "health_interval": 60}, daemon=True)
+    during = []
+
+    class R(Runner):
+        def __call__(self, argv, timeout):
+            during.append(health())
+            return super().__call__(argv, timeout)
+
+    busy = {("llm", "coder-llm-0"): [("amd.com/gpu", [uids[0]])]}
+    r = R({"amd-gemm-validator": (0, _gemm_log(7, 1500.0))})
+    loop.start()
+    try:
+        with FakePodResources(sock, busy):
+            v = Validator(cfg, str(marker), bin_dir="/x", runner=r, root=str(root))
+            g = v.run_step("gemm")
+        time.sleep(0.2)
+        after = health()
+    finally:
+        stop.set()
+        loop.join(5)
+    assert g.passed and g.detail["reservation"]["acked"]
+    assert all(during[0][u] == api.UNHEALTHY for u in uids[1:])
+    doc = json.loads((marker / VALIDATED_DEVICES).read_text())
+    assert doc["boot_id"] == "boot-1" and sorted(doc["device_uids"]) == sorted(uids[1:])
+    assert after[uids[0]] == api.UNHEALTHY                   # held by a pod, never validated
+    assert all(after[u] == api.HEALTHY for u in uids[1:])
+    # a reboot (new boot id) closes the gate again
+    (root / "proc/sys/kernel/random/boot_id").write_text("boot-2\n")
+    plugin.refresh()
+    assert set(health().values()) == {api.UNHEALTHY}
+    # a reservation past its expiry (a crashed validator) is ignored
+    (root / "proc/sys/kernel/random/boot_id").write_text("boot-1\n")
+    (marker / IN_TEST).write_text(json.dumps({"nonce": "x", "device_uids": uids, "expires": time.time() - 1}))
+    plugin.refresh()
+    assert all(health()[u] == api.HEALTHY for u in uids[1:])
+
+
+def test_hold_loop_reruns_the_chain_when_a_deferred_node_gets_a_free_gpu(tmp_path, monkeypatch):
+    root = _node(tmp_path)
+    cfg, sock = _cfg(tmp_path, ", retryDeferredSeconds: 0.01")
+    uids = _uids(root)
+    marker = tmp_path / "m"
+    _chain_markers(marker)
+    pods = {("train", f"job-{i}"): [("amd.com/gpu", [u])] for i, u in enumerate(uids)}
+    kube = _Kube()
+    monkeypatch.setenv("POD_NAME", "amd-gpu-validator-abc")
+    monkeypatch.setenv("POD_NAMESPACE", "amd-gpu-operator")
+    with FakePodResources(sock, pods):
+        v = Validator(cfg, str(marker), bin_dir="/x", runner=Runner({}), root=str(root), kube=kube,
+                      node_name="n1")
+        for st in ("gemm", "rccl", "stress", "bandwidth"):
+            v.run_step(st)
+        assert v.run_step("report").detail["label"] == "deferred"
+        ticks = []
+
+        def sleep(_):
+            time.sleep(0.012)                                # > retryDeferredSeconds per tick
+            ticks.append(1)
+            if len(ticks) == 3:                              # a job finishes: GPU 5 is free
+                del pods[("train", "job-5")]
+        rc = hold_loop(v, str(marker), interval=0.0, stop=lambda: len(ticks) > 10, sleep=sleep)
+    assert rc == 0 and kube.deleted == [("amd-gpu-operator", "amd-gpu-validator-abc")]
+    assert 3 <= len(ticks) <= 5
+
+
+def test_partition_switch_invalidates_the_fingerprint(tmp_path):
+    """SPX → CPX changes no boot/driver/image/config field; the agent set and partition
+    mode are part of the fingerprint, so a validator restart after a switch re-runs the load steps."""
+    root = _node(tmp_path)
+    cfg, sock = _cfg(tmp_path, ", pluginTest: false, vectorAdd: false, rccl: false")
+    marker = tmp_path / "m"
+    _chain_markers(marker, ("driver", "runtime"))
+    with FakePodResources(sock, {}):
+        r1 = Runner({"amd-gemm-validator": (0, _gemm_log(8, 1600.0))})
+        v = Validator(cfg, str(marker), bin_dir="/x", runner=r1, root=str(root))
+        assert v.run_step("gemm").passed and v.run_step("report").detail["full_validation"]
+        fp_spx = v.fingerprint()
+        # the partition manager switches every ASIC to CPX (same boot)
+        import shutil
+
+        shutil.rmtree(root / "sys")
+        fake_sysfs.build_node(root, compute_partition="CPX")
+        r2 = Runner({"amd-gemm-validator": (0, _gemm_log(64, 190.0, size=4096))})
+        v2 = Validator(cfg, str(marker), bin_dir="/x", runner=r2, root=str(root))
+        fp_cpx = v2.fingerprint()
+        assert fp_cpx["boot_id"] == fp_spx["boot_id"] and fp_cpx["partition"] != fp_spx["partition"]
+        assert fp_cpx["agents"] == "64" and fp_spx["agents"] == "8"
+        g = v2.run_step("gemm")
+        assert g.passed and "reused" not in g.detail and len(r2.calls) == 1
+        assert len(g.detail["validated_devices"]) == 64
 
 
 def test_unchanged_node_reuses_full_pass_and_changed_fingerprint_reruns(tmp_path):
@@ -126,7 +339,7 @@ def test_unchanged_node_reuses_full_pass_and_changed_fingerprint_reruns(tmp_path
         r2 = Runner(outputs)
         v2 = Validator(cfg, str(marker), bin_dir="/x", runner=r2, root=str(root))
         g = v2.run_step("gemm")
-        assert g.passed and "unchanged" in g.detail["deferred"] and r2.calls == []
+        assert g.passed and "unchanged" in g.detail["reused"] and r2.calls == []
         assert g.detail["previous"]["aggregate_tflops"] == pytest.approx(12800.0)
         assert v2.run_step("report").detail["full_validation"]
 
@@ -135,12 +348,12 @@ def test_unchanged_node_reuses_full_pass_and_changed_fingerprint_reruns(tmp_path
         r3 = Runner(outputs)
         v3 = Validator(cfg, str(marker), bin_dir="/x", runner=r3, root=str(root))
         g3 = v3.run_step("gemm")
-        assert g3.passed and "deferred" not in g3.detail and len(r3.calls) == 1
+        assert g3.passed and "reused" not in g3.detail and len(r3.calls) == 1
         os.environ["VALIDATOR_IMAGE_ID"] = "sha256:new"
         try:
             r4 = Runner(outputs)
             g4 = Validator(cfg, str(marker), bin_dir="/x", runner=r4, root=str(root)).run_step("gemm")
-            assert "deferred" not in g4.detail and len(r4.calls) == 1
+            assert "reused" not in g4.detail and len(r4.calls) == 1
         finally:
             del os.environ["VALIDATOR_IMAGE_ID"]
 
@@ -196,4 +409,4 @@ def test_index_device_ids_map_through_the_plugin_file(tmp_path):
     with FakePodResources(sock, {("a", "p"): [("amd.com/gpu", ["3"])]}):
         res = Validator(cfg, str(tmp_path / "m3"), bin_dir="/x", runner=r2, root=str(root),
                         device_id_map=str(tmp_path / "missing.json")).run_step("gemm")
-    assert res.passed and "cannot map" in res.detail["deferred"] and r2.calls == []
+    assert not res.passed and "cannot map" in res.reason and r2.calls == []

@@ -1,0 +1,101 @@
+#!/usr/bin/env bash
+# The one GPU-box session runner (replaces the per-session gpu_r0*_*.sh scripts).
+#
+#   tools/gpu_run.sh <name> <step> [<step> ...]     → writes gpurun_out/<name>/...
+#
+# Steps (run in order; each GPU step has its own time limit; the first failure ends the call):
+#   tests            pytest -m gpu (what the driver runs at round end)
+#   tests:<expr>     pytest -m gpu -k <expr>
+#   smoke            __graft_entry__.smoke()
+#   driver           python3 bench.py --gpus 1 --steps 20 --warmup 5   (the driver's exact command)
+#   driver-notel     the same with --no-telemetry
+#   bench            bench.py defaults (K=200 / W=20)
+#   native           amd-vectoradd, amd-gemm-validator (bf16 + fp8), amd-proftester
+#   llm[:<tokens>]   tools/llm_bench.py (decode T list, default 1,2,4,8) + prefill
+#   prof-bench       rocprofv3 --kernel-trace --stats of the driver's bench command
+#   prof-llm         rocprofv3 kernel trace of steady LLM decode → per-kernel summary
+#   sd15 / wan       tools/sd15_bench.py / tools/wan_bench.py
+#   env:VAR=VALUE    export VAR for the following steps (A/B knobs)
+#
+# Usage from the container:  gpurun --timeout 900 -- tools/gpu_run.sh r04a tests smoke driver bench
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+NAME="${1:?usage: tools/gpu_run.sh <name> <step>...}"
+shift
+OUT="gpurun_out/$NAME"
+mkdir -p "$OUT"
+
+fail() { echo "!! step '$1' failed (exit $2); log tail:"; tail -40 "$3"; exit 1; }
+jsonline() { grep '^{' "$1" | tail -1 | cut -c1-"${2:-400}"; }
+
+for step in "$@"; do
+  echo "== $step ($(date +%T))"
+  case "$step" in
+    tests)
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1 || fail "$step" $? "$OUT/pytest_gpu.log"
+      tail -1 "$OUT/pytest_gpu.log" ;;
+    tests:*)
+      expr="${step#tests:}"
+      log="$OUT/pytest_gpu_${expr//[^A-Za-z0-9_]/_}.log"
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -k "$expr" --timeout 300 \
+        --timeout-method thread -p no:cacheprovider > "$log" 2>&1 || fail "$step" $? "$log"
+      tail -1 "$log" ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+        || fail "$step" $? "$OUT/smoke.log"
+      tail -1 "$OUT/smoke.log" ;;
+    driver|driver-notel)
+      extra=""; [[ "$step" == driver-notel ]] && extra="--no-telemetry"
+      n=$(ls "$OUT"/"$step"_*.log 2>/dev/null | wc -l)
+      log="$OUT/${step}_$n.log"
+      timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 $extra > "$log" 2>&1 \
+        || fail "$step" $? "$log"
+      jsonline "$log" 600 ;;
+    bench)
+      n=$(ls "$OUT"/bench_*.log 2>/dev/null | wc -l)
+      timeout -k 10 400 python3 bench.py > "$OUT/bench_$n.log" 2>&1 || fail "$step" $? "$OUT/bench_$n.log"
+      jsonline "$OUT/bench_$n.log" 600 ;;
+    native)
+      timeout -k 10 120 native/bin/amd-vectoradd > "$OUT/vectoradd.log" 2>&1 || fail "$step" $? "$OUT/vectoradd.log"
+      tail -2 "$OUT/vectoradd.log"
+      timeout -k 10 300 native/bin/amd-gemm-validator --size 8192 --iters 50 --json \
+        > "$OUT/gemm_validator_bf16.log" 2>&1 || fail "$step" $? "$OUT/gemm_validator_bf16.log"
+      timeout -k 10 300 native/bin/amd-gemm-validator --dtype fp8 --size 8192 --iters 50 --json \
+        > "$OUT/gemm_validator_fp8.log" 2>&1 || fail "$step" $? "$OUT/gemm_validator_fp8.log"
+      grep -h '"check"' "$OUT"/gemm_validator_*.log | cut -c1-300
+      timeout -k 10 300 native/bin/amd-proftester --json > "$OUT/proftester.log" 2>&1 \
+        || fail "$step" $? "$OUT/proftester.log"
+      grep -v '^{' "$OUT/proftester.log" | tail -8 ;;
+    llm|llm:*)
+      toks="1,2,4,8"; [[ "$step" == llm:* ]] && toks="${step#llm:}"
+      n=$(ls "$OUT"/llm_bench_*.json 2>/dev/null | wc -l)
+      timeout -k 10 500 python -u tools/llm_bench.py --tokens "$toks" --out "$OUT/llm_bench_$n.json" \
+        > "$OUT/llm_bench_$n.log" 2>&1 || fail "$step" $? "$OUT/llm_bench_$n.log"
+      grep -E "decode|prefill" "$OUT/llm_bench_$n.log" | grep -v '^{' ;;
+    prof-bench)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bench" -o bench --output-format csv \
+        -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/prof_bench.log" 2>&1 \
+        || fail "$step" $? "$OUT/prof_bench.log"
+      find "$OUT/prof_bench" -name "*kernel_stats.csv" -exec head -6 {} \; | cut -c1-200 ;;
+    prof-llm)
+      timeout -k 10 400 rocprofv3 --kernel-trace --output-format rocpd -d "$OUT/prof_llm" -o llm \
+        -- python3 tools/steady_prof.py llm-decode --iters 20 --warmup 5 > "$OUT/prof_llm.log" 2>&1 \
+        || fail "$step" $? "$OUT/prof_llm.log"
+      db=$(find "$OUT/prof_llm" -name '*.db' | head -1)
+      python3 tools/rocpd_summary.py "$db" --after-gap-ms 200 --per 20 --top 30 > "$OUT/llm_decode_kernels.txt" \
+        && head -24 "$OUT/llm_decode_kernels.txt" | cut -c1-170 ;;
+    sd15)
+      timeout -k 10 600 python -u tools/sd15_bench.py > "$OUT/sd15.log" 2>&1 || fail "$step" $? "$OUT/sd15.log"
+      tail -5 "$OUT/sd15.log" ;;
+    wan)
+      timeout -k 10 900 python -u tools/wan_bench.py > "$OUT/wan.log" 2>&1 || fail "$step" $? "$OUT/wan.log"
+      tail -5 "$OUT/wan.log" ;;
+    env:*)
+      kv="${step#env:}"; export "${kv?}"; echo "   export $kv" ;;
+    *)
+      echo "unknown step '$step'"; exit 2 ;;
+  esac
+done
+echo "== done ($(date +%T))"
