@@ -101,10 +101,13 @@ def main(argv=None) -> int:
             extra = ["--sysfs-root", os.path.join(args.root, "sys/class/kfd/kfd/topology"),
                      "--dev-root", os.path.join(args.root, "dev"), "--no-open"]
         drv = cfg.section("driver")
+        from .pause import PauseGuard
+
         driver_ready_loop(os.path.join(_bin_dir(), "kfd-probe"), int(cfg["expectedGpusPerNode"]),
                           cfg.min_gfx, args.marker_dir, args.interval or 30.0, extra=extra,
                           load_module=bool(drv["loadModule"]),
-                          dev_root=os.path.join(args.root, "dev"), host_root=drv["hostRoot"])
+                          dev_root=os.path.join(args.root, "dev"), host_root=drv["hostRoot"],
+                          guard=PauseGuard("driver"))
         return 0
 
     if c == "runtime-install":
@@ -126,10 +129,13 @@ def main(argv=None) -> int:
         from .device_plugin import AmdGpuDevicePlugin, ValidationGate
         from .validator import DEVICE_ID_MAP
 
+        from .pause import PauseGuard
+
         gate = ValidationGate(args.marker_dir, root=args.root,
                               gate=bool(cfg.section("validator")["gateOnValidation"]))
         AmdGpuDevicePlugin(cfg, root=args.root, kubelet_dir=args.kubelet_dir,
-                           id_map_path=DEVICE_ID_MAP, gate=gate).run()
+                           id_map_path=DEVICE_ID_MAP, gate=gate,
+                           pause_guard=PauseGuard("device-plugin")).run()
         return 0
 
     if c == "labeller":
@@ -139,15 +145,15 @@ def main(argv=None) -> int:
         return 0
 
     if c == "exporter":
-        import threading
-
         from .exporter import ExporterServer, GpuCollector, make_backend
+        from .pause import PauseGuard
 
-        srv = ExporterServer(GpuCollector(make_backend(args.root), node, args.marker_dir),
+        srv = ExporterServer(GpuCollector(make_backend(args.root), node, args.marker_dir,
+                                          guard=PauseGuard("exporter")),
                              port=args.port or int(cfg.section("exporter")["port"]))
         logging.getLogger("amd-gpu-exporter").info("listening on :%d", srv.port)
-        srv.serve_background().join()
-        threading.Event().wait()
+        srv.serve_background()
+        srv.watch_pause()
         return 0
 
     if c == "partition-manager":
@@ -161,7 +167,11 @@ def main(argv=None) -> int:
             backend = SysfsPartitionBackend(args.root)
         p = cfg.section("partition")
         PartitionManager(_kube(optional=False), node, backend, args.root, p["compute"], p["memory"],
-                         float(p["drainTimeoutSeconds"])).run(args.interval or 30)
+                         float(p["drainTimeoutSeconds"]), drain_policy=p["drainPolicy"],
+                         pause_ack_timeout=float(p["pauseAckSeconds"]),
+                         apply_retries=int(p["applyRetries"]),
+                         reservation=os.path.join(args.marker_dir, "in-test.json"),
+                         resource=cfg.resource_name).run(args.interval or 30)
         return 0
 
     if c == "bringup":

@@ -37,6 +37,13 @@ DEFAULTS: Dict[str, Any] = {
         "compute": "SPX",
         "memory": "NPS1",
         "drainTimeoutSeconds": 600,
+        # evict: GPU pods are evicted through the Eviction API (PodDisruptionBudgets honoured);
+        # wait: only wait for them to finish
+        "drainPolicy": "evict",
+        # how long to wait for the exporter / driver probe / device plugin to release the GPUs
+        "pauseAckSeconds": 60,
+        # sysfs / amd-smi writes that find the device busy (EBUSY): retries, 1 s doubling backoff
+        "applyRetries": 5,
     },
     "exporter": {
         "port": 9400,
@@ -139,6 +146,8 @@ class OperatorConfig:
             raise ConfigError(f"partition.compute must be one of {COMPUTE_PARTITIONS}")
         if r["partition"]["memory"] not in MEMORY_PARTITIONS:
             raise ConfigError(f"partition.memory must be one of {MEMORY_PARTITIONS}")
+        if r["partition"]["drainPolicy"] not in ("evict", "wait"):
+            raise ConfigError("partition.drainPolicy must be 'evict' or 'wait'")
         if not 1 <= int(r["exporter"]["port"]) <= 65535:
             raise ConfigError("exporter.port out of range")
         if float(r["validator"]["reserveAckSeconds"]) < 0 or float(r["validator"]["retryDeferredSeconds"]) <= 0:

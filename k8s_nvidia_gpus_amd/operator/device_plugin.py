@@ -25,7 +25,8 @@ Design (MI355X-first):
 * **Kubelet restarts**: kubelet deletes every plugin socket when it restarts; the plugin watches
   ``kubelet.sock`` and its own socket and re-serves + re-registers.
 * **Partition changes**: while ``/run/amd/partition-in-progress`` exists (the partition manager's
-  drain marker) the plugin advertises no devices, then re-enumerates.
+  drain marker) the plugin advertises no devices, releases its amd-smi (ECC) session and acks the
+  pause (:mod:`.pause`), then re-enumerates and re-opens when the marker goes away.
 * **Validation gate** (:class:`ValidationGate`): with ``validator.gateOnValidation`` a device is
   Healthy only after the validator's load steps passed on it this boot, and the devices a load
   step is about to load are reported Unhealthy for its duration (the validator's TOCTOU guard).
@@ -93,7 +94,20 @@ class AmdSmiEccReader:
             import amdsmi as amdsmi_module  # noqa: N813 - optional dependency
         self.S = amdsmi_module
         self.S.amdsmi_init()
+        self.active = True
         self._by_bdf: Dict[str, object] = {}
+
+    def suspend(self) -> None:
+        """Release the amd-smi session for a partition change (pause.py); handles go stale."""
+        if self.active:
+            self.close()
+            self.active = False
+            self._by_bdf = {}
+
+    def resume(self) -> None:
+        if not self.active:
+            self.S.amdsmi_init()
+            self.active = True
 
     def _rebuild(self) -> None:
         self._by_bdf = {}
@@ -116,6 +130,8 @@ class AmdSmiEccReader:
         raise LookupError(f"no amd-smi handle for {bdf}")
 
     def __call__(self, d: topo_mod.GpuDevice) -> int:
+        if not self.active:
+            raise LookupError("amd-smi session released (partition change in progress)")
         counts = []
         for h in self._handles(d.pci_bdf.lower()):
             ecc = self.S.amdsmi_get_gpu_total_ecc_count(h) or {}
@@ -258,10 +274,15 @@ class AmdGpuDevicePlugin:
                  topology_fn: Optional[Callable[[], topo_mod.NodeTopology]] = None,
                  health_fn: Optional[HealthFn] = None, pause_marker: Optional[str] = PAUSE_MARKER,
                  dev_prefix: str = "/dev", ecc_fn: Optional[Callable] = None,
-                 id_map_path: Optional[str] = None, gate: Optional[ValidationGate] = None):
+                 id_map_path: Optional[str] = None, gate: Optional[ValidationGate] = None,
+                 pause_guard=None):
         self.config = config
         self.gate = gate
         self._gate_stamp = None
+        # pause.PauseGuard("device-plugin"): release the ECC reader's amd-smi session while the
+        # partition manager switches modes (the pause marker is the same file as pause_marker)
+        self.pause_guard = pause_guard
+        self._ecc = None
         # {kubelet device ID: device_uid} for the validator, which maps kubelet's PodResources
         # answer to GPUs with it (needed with deviceIdStrategy: index)
         self.id_map_path = id_map_path
@@ -272,8 +293,8 @@ class AmdGpuDevicePlugin:
         self.topology_fn = topology_fn or (lambda: topo_mod.read_topology(root, config.min_gfx))
         if health_fn is None:
             threshold = int(config.section("health")["eccUncorrectableThreshold"])
-            health_fn = PresenceHealth(root, ecc_fn=ecc_fn or default_ecc_fn(threshold),
-                                       ecc_threshold=threshold)
+            self._ecc = ecc_fn or default_ecc_fn(threshold)
+            health_fn = PresenceHealth(root, ecc_fn=self._ecc, ecc_threshold=threshold)
         self.health_fn = health_fn
         self.pause_marker = pause_marker
         self.dev_prefix = dev_prefix
@@ -306,6 +327,11 @@ class AmdGpuDevicePlugin:
     def refresh(self) -> bool:
         """Re-enumerate + re-check health; returns True (and wakes ListAndWatch) on any change."""
         paused = bool(self.pause_marker and os.path.exists(self.pause_marker))
+        if not paused and self._ecc is not None and not getattr(self._ecc, "active", True):
+            try:
+                self._ecc.resume()          # partition change over: re-open on the new handles
+            except Exception as e:  # noqa: BLE001 - ECC criterion off until the next refresh
+                log.warning("cannot re-open amd-smi after the partition change: %s", e)
         try:
             devices = [] if paused else list(self.topology_fn().gpus)
         except FileNotFoundError as e:
@@ -346,6 +372,13 @@ class AmdGpuDevicePlugin:
         if nonce:
             # the reserved devices' Unhealthy state is published (ListAndWatch woken above)
             self.gate.ack(nonce)
+        if paused and self.pause_guard is not None:
+            # zero devices are published; drop the amd-smi session, then tell the manager
+            if self._ecc is not None and hasattr(self._ecc, "suspend"):
+                self._ecc.suspend()
+            self.pause_guard.ack()
+        elif self.pause_guard is not None:
+            self.pause_guard.clear()
         return changed
 
     def _write_id_map(self) -> None:
@@ -518,6 +551,8 @@ class AmdGpuDevicePlugin:
                 last_health = now
             elif self.gate is not None and self.gate.stamp() != self._gate_stamp:
                 self.refresh()      # a reservation / validation result: apply it within one poll
+            elif self.pause_marker and os.path.exists(self.pause_marker) != self._paused:
+                self.refresh()      # a partition change starts / ends: follow it within one poll
             stop_event.wait(poll)
         self.stop()
 

@@ -52,6 +52,7 @@ class AmdSmiBackend:
             import amdsmi as amdsmi_module  # noqa: N813 - optional dependency
         self.S = amdsmi_module
         self.S.amdsmi_init()
+        self.active = True
         self._static: Dict[Any, Dict[str, Any]] = {}
 
     def close(self) -> None:
@@ -59,6 +60,18 @@ class AmdSmiBackend:
             self.S.amdsmi_shut_down()
         except Exception:  # noqa: BLE001
             pass
+
+    def suspend(self) -> None:
+        """Release the amd-smi session (partition change in progress, see pause.py)."""
+        if self.active:
+            self.close()
+            self.active = False
+            self._static.clear()      # handles / identities change with the re-enumeration
+
+    def resume(self) -> None:
+        if not self.active:
+            self.S.amdsmi_init()
+            self.active = True
 
     def _call(self, name: str, *args):
         fn = getattr(self.S, name, None)
@@ -93,6 +106,8 @@ class AmdSmiBackend:
         return ident
 
     def samples(self) -> List[GpuSample]:
+        if not self.active:
+            raise RuntimeError("amd-smi session released (partition change in progress)")
         out = []
         handles = self._call("amdsmi_get_processor_handles") or []
         for idx, h in enumerate(handles):
@@ -198,12 +213,34 @@ def read_validations(marker_dir: str) -> Dict[str, Any]:
 class GpuCollector:
     """prometheus_client collector; ``collect`` samples the backend at scrape time."""
 
-    def __init__(self, backend, node_name: str = "", marker_dir: str = "/run/amd/validations"):
+    def __init__(self, backend, node_name: str = "", marker_dir: str = "/run/amd/validations",
+                 guard=None):
         self.backend = backend
         self.node = node_name
         self.marker_dir = marker_dir
         self.last_error: Optional[str] = None
         self.scrapes = 0
+        self.guard = guard            # pause.PauseGuard("exporter"): partition-change pause
+        self.paused = False
+
+    def check_pause(self) -> bool:
+        """Release / re-open the backend's GPU session around a partition change; returns paused.
+        Called by the exporter's watcher loop (every second) and at every scrape."""
+        if self.guard is None:
+            return False
+        if self.guard.paused():
+            if not self.paused:
+                getattr(self.backend, "suspend", lambda: None)()
+                self.paused = True
+            self.guard.ack()
+        elif self.paused:
+            try:
+                getattr(self.backend, "resume", lambda: None)()
+                self.paused = False
+                self.guard.clear()
+            except Exception as e:  # noqa: BLE001 - retried at the next check
+                log.warning("cannot re-open the GPU session after the partition change: %s", e)
+        return self.paused
 
     def describe(self):
         return []
@@ -214,15 +251,24 @@ class GpuCollector:
         self.scrapes += 1
         t0 = time.perf_counter()
         base = ["gpu", "uuid", "pci", "node"]
-        try:
-            samples = self.backend.samples()
-            self.last_error = None
-        except Exception as e:  # noqa: BLE001 - report through the up metric
-            log.warning("sampling failed: %s", e)
-            samples, self.last_error = [], str(e)
+        paused = self.check_pause()
+        if paused:
+            # stale on purpose: no GPU handle is open while the partition manager switches modes
+            samples, self.last_error = [], "paused: partition change in progress"
+        else:
+            try:
+                samples = self.backend.samples()
+                self.last_error = None
+            except Exception as e:  # noqa: BLE001 - report through the up metric
+                log.warning("sampling failed: %s", e)
+                samples, self.last_error = [], str(e)
         up = GaugeMetricFamily("amd_gpu_exporter_up", "1 if the last sample succeeded")
         up.add_metric([], 0.0 if self.last_error else 1.0)
         yield up
+        pz = GaugeMetricFamily("amd_gpu_exporter_paused",
+                               "1 while GPU sampling is paused for a partition change (metrics stale)")
+        pz.add_metric([], 1.0 if paused else 0.0)
+        yield pz
         info = GaugeMetricFamily("amd_gpu_info", "static GPU identity (value 1)",
                                  labels=base + ["product", "gfx", "driver", "compute_partition",
                                                 "memory_partition", "render_minor"])
@@ -380,7 +426,8 @@ class ExporterServer:
         from prometheus_client import CONTENT_TYPE_LATEST, generate_latest
 
         registry = make_registry(collector)
-        lock = threading.Lock()
+        self.collector = collector
+        self.lock = lock = threading.Lock()
 
         class H(BaseHTTPRequestHandler):
             def log_message(self, *a):
@@ -417,6 +464,14 @@ class ExporterServer:
     def shutdown(self) -> None:
         self.httpd.shutdown()
         self.httpd.server_close()
+
+    def watch_pause(self, interval: float = 1.0, stop_event=None) -> None:
+        """Release the GPU session within ``interval`` of a partition pause even without scrapes."""
+        stop_event = stop_event or threading.Event()
+        while not stop_event.is_set():
+            with self.lock:
+                self.collector.check_pause()
+            stop_event.wait(interval)
 
 
 def make_backend(root: str = "/"):

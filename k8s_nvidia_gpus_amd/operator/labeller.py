@@ -12,10 +12,12 @@ sysfs topology, so workloads select on product, architecture, partition mode or 
     amd.com/gpu.driver-version=...     amd.com/gpu.numa-nodes=2
 
 ``amd.com/gpu.present`` is what schedules the rest of the operator's DaemonSets onto the node.
-``amd.com/gpu.pci-present=true`` comes from the PCI bus alone (vendor 0x1002, class 0x12xxxx
-processing accelerator or 0x03xxxx display), so it is set before amdgpu is loaded: it schedules the
-driver DaemonSet, which therefore never lands on a CPU-only worker (whose never-ready pod would
-block the operator Kustomization's ``wait: true``).  The partition labels read every ASIC and
+``amd.com/gpu.pci-present=true`` comes from the PCI bus alone, so it is set before amdgpu is
+loaded: vendor 0x1002, class 0x12 (processing accelerator) and a device ID of an Instinct part the
+operator's ``minGfxTargetVersion`` accepts (:data:`INSTINCT_PCI_IDS`).  It schedules the driver
+DaemonSet, whose ``kfd-probe --min-gfx`` can only turn ready on such a part; a CPU worker with an
+AMD Radeon (display class 0x03) or an older Instinct never gets it, so no never-ready driver pod
+blocks the operator Kustomization's ``wait: true``.  The partition labels read every ASIC and
 say ``mixed`` when they disagree (a partition change that stopped half-way), never the head GPU's.
 Labels this component owns are removed again when the GPUs go away; labels owned by other
 components (``amd.com/gpu.validated``, ``amd.com/gpu.compute-partition.desired``) are left alone.
@@ -56,10 +58,19 @@ def driver_version(root: str = "/") -> Optional[str]:
 
 
 AMD_VENDOR = "0x1002"
+PCI_CLASS_ACCELERATOR = 0x12
+# Instinct PCI device IDs (PF and SR-IOV VF) → gfx target version; only parts >= minGfxTargetVersion
+# count.  MI300A/X/MI308X/MI325X are gfx942; MI350X/MI355X are gfx950 (the target of this operator).
+INSTINCT_PCI_IDS = {
+    0x74a0: 90402, 0x74a1: 90402, 0x74a2: 90402, 0x74a5: 90402, 0x74a9: 90402,   # MI300 series
+    0x74b5: 90402, 0x74b9: 90402, 0x74bd: 90402,                                 # MI300 VFs
+    0x75a0: 90500, 0x75a3: 90500,                                                # MI350X, MI355X
+    0x75b0: 90500, 0x75b3: 90500,                                                # MI350X/MI355X VFs
+}
 
 
-def amd_accelerators_on_pci(root: str = "/") -> int:
-    """AMD GPUs / accelerators on the PCI bus (needs no driver)."""
+def amd_accelerators_on_pci(root: str = "/", min_gfx: int = topo_mod.GFX950) -> int:
+    """Instinct accelerators on the PCI bus that this operator can drive (needs no driver)."""
     base = os.path.join(root, "sys/bus/pci/devices")
     try:
         names = os.listdir(base)
@@ -72,9 +83,12 @@ def amd_accelerators_on_pci(root: str = "/") -> int:
                 vendor = f.read().strip().lower()
             with open(os.path.join(base, name, "class")) as f:
                 cls = int(f.read().strip(), 16)
+            with open(os.path.join(base, name, "device")) as f:
+                device = int(f.read().strip(), 16)
         except (OSError, ValueError):
             continue
-        if vendor == AMD_VENDOR and (cls >> 16) in (0x12, 0x03):
+        if (vendor == AMD_VENDOR and (cls >> 16) == PCI_CLASS_ACCELERATOR
+                and INSTINCT_PCI_IDS.get(device, 0) >= min_gfx):
             n += 1
     return n
 
@@ -82,7 +96,7 @@ def amd_accelerators_on_pci(root: str = "/") -> int:
 def compute_labels(root: str = "/", min_gfx: int = topo_mod.GFX950) -> Dict[str, Optional[str]]:
     """Desired values for every owned label (None = remove)."""
     labels: Dict[str, Optional[str]] = {f"{PREFIX}.{k}": None for k in OWNED}
-    if amd_accelerators_on_pci(root):
+    if amd_accelerators_on_pci(root, min_gfx):
         labels[f"{PREFIX}.pci-present"] = "true"
     try:
         topo = topo_mod.read_topology(root, min_gfx)

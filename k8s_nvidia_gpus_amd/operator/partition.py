@@ -5,10 +5,24 @@ partitions (DPX/QPX/CPX; CPX = 8 GPUs of 1 XCD / 32 CUs each), with the HBM as o
 (NPS1) or two (NPS2).  Changing mode needs the GPU idle, and the driver then re-enumerates: new
 KFD agents, new render minors, different device IDs.  The manager drives that safely:
 
-    IDLE ──desired≠current──▶ DRAINING ──no amd.com/gpu pods left──▶ APPLYING ──▶ REENUMERATING ──▶ IDLE
-                                  │ taint NoSchedule + pause marker           │ amd-smi / sysfs   │ KFD shows
-                                  │ (device plugin advertises 0 devices)      │ per ASIC          │ N × split agents
-                                  └──timeout──▶ FAILED (taint and marker removed, reason annotated)
+    IDLE ─desired≠current─▶ DRAINING ─no GPU pods─▶ QUIESCING ─acks─▶ APPLYING ─▶ REENUMERATING ─▶ IDLE
+                              │ taint NoSchedule +        │ operator GPU      │ amd-smi /   │ KFD shows
+                              │ pause marker; evict GPU   │ clients release   │ sysfs per   │ N × split
+                              │ pods (Eviction API, PDBs) │ their handles     │ ASIC, EBUSY │ agents
+                              └─timeout / PDB-blocked─▶ FAILED (taint + marker removed, reason annotated)
+
+Draining (``partition.drainPolicy``): ``evict`` (default) evicts every pod on the node that holds
+``amd.com/gpu`` through the Eviction API, so PodDisruptionBudgets are honoured — a refused (429)
+eviction is retried until the drain timeout and then fails the change with the PDB's message; the
+reference's GPU workloads are long-lived Deployments (reference llm/deployment.yaml:8-12,
+sd15-api/deployment.yaml:8-9) whose pods a NoSchedule taint alone never removes.  ``wait`` only
+waits for them to finish.  A validator load step in flight (its ``in-test.json`` reservation)
+also holds the drain.
+
+Quiescing (:mod:`.pause`): the operator's own GPU clients — exporter, driver-readiness probe, device
+plugin — see the pause marker's nonce, close their amd-smi sessions / stop opening ``/dev/kfd`` and
+ack; the mode is applied after every ack (or ``pauseAckSeconds``).  A write that still finds the
+device busy (EBUSY) is retried with exponential backoff (``applyRetries``) before the change fails.
 
 The desired mode comes from the node label ``amd.com/gpu.compute-partition.desired`` (and
 ``…memory-partition.desired``), else from operator.yaml.  The state is published as the node
@@ -20,13 +34,16 @@ GPU's mode), and a reconcile re-applies the desired mode only to the ASICs that 
 """
 from __future__ import annotations
 
+import errno
+import json
 import logging
 import os
 import time
-from typing import Callable, Dict, List, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 from ..utils import kube as kube_mod
 from ..utils import topology as topo_mod
+from . import pause as pause_mod
 
 log = logging.getLogger("amd-partition-manager")
 
@@ -34,7 +51,16 @@ LABEL_DESIRED = "amd.com/gpu.compute-partition.desired"
 LABEL_MEM_DESIRED = "amd.com/gpu.memory-partition.desired"
 ANNOT_STATE = "amd.com/gpu.partition-state"
 TAINT_KEY = "amd.com/gpu-partitioning"
-PAUSE_MARKER = "/run/amd/partition-in-progress"
+PAUSE_MARKER = pause_mod.PAUSE_MARKER
+DRAIN_POLICIES = ("evict", "wait")
+
+
+def is_busy(e: BaseException) -> bool:
+    """The device refused the mode change because it is in use (retryable)."""
+    if isinstance(e, OSError) and e.errno == errno.EBUSY:
+        return True
+    text = str(e).lower()
+    return "ebusy" in text or "device or resource busy" in text or "amdsmi_status_busy" in text
 
 
 MIXED = "mixed"
@@ -80,7 +106,14 @@ class PartitionManager:
                  default_compute: str = "SPX", default_memory: str = "NPS1",
                  drain_timeout: float = 600.0, reenum_timeout: float = 300.0, poll: float = 2.0,
                  pause_marker: str = PAUSE_MARKER, min_gfx: int = topo_mod.GFX950,
-                 resource: str = "amd.com/gpu", sleep: Callable[[float], None] = time.sleep):
+                 resource: str = "amd.com/gpu", sleep: Callable[[float], None] = time.sleep,
+                 drain_policy: str = "evict", pause_ack_timeout: float = 60.0,
+                 apply_retries: int = 5, retry_backoff: float = 1.0,
+                 ack_dir: str = pause_mod.ACK_DIR,
+                 ack_components: Sequence[str] = pause_mod.COMPONENTS,
+                 reservation: Optional[str] = "/run/amd/validations/in-test.json"):
+        if drain_policy not in DRAIN_POLICIES:
+            raise ValueError(f"drainPolicy must be one of {DRAIN_POLICIES}")
         self.client = client
         self.node = node_name
         self.backend = backend
@@ -94,19 +127,24 @@ class PartitionManager:
         self.min_gfx = min_gfx
         self.resource = resource
         self.sleep = sleep
+        self.drain_policy = drain_policy
+        self.pause_ack_timeout = pause_ack_timeout
+        self.apply_retries = apply_retries
+        self.retry_backoff = retry_backoff
+        self.ack_dir = ack_dir
+        self.ack_components = tuple(ack_components)
+        self.reservation = reservation
 
     # ---------------------------------------------------------------- helpers
     def _state(self, state: str, reason: str = "") -> None:
         self.client.set_node_annotations(self.node, {ANNOT_STATE: f"{state}{': ' + reason if reason else ''}"})
         log.info("partition state %s %s", state, reason)
 
-    def _pause(self, on: bool) -> None:
+    def _pause(self, on: bool) -> Optional[str]:
         if on:
-            os.makedirs(os.path.dirname(self.pause_marker), exist_ok=True)
-            with open(self.pause_marker, "w") as f:
-                f.write(f"{time.time()}\n")
-        elif os.path.exists(self.pause_marker):
-            os.unlink(self.pause_marker)
+            return pause_mod.start_pause(self.pause_marker, self.ack_dir)
+        pause_mod.end_pause(self.pause_marker)
+        return None
 
     def desired(self) -> tuple:
         labels = self.client.get_node(self.node).get("metadata", {}).get("labels", {}) or {}
@@ -150,21 +188,22 @@ class PartitionManager:
             return "failed"
         log.info("node %s: %s/%s -> %s/%s on %d of %d ASIC(s)", self.node, cur_c, cur_m, want_c,
                  want_m, len(off), len(asics))
-        # 1. stop new GPU work landing here; hide devices from kubelet
+        # 1. stop new GPU work landing here; hide devices from kubelet; pause the operator's own
+        #    GPU clients; move the GPU pods off (Eviction API, PDBs honoured)
         self.client.set_taint(self.node, TAINT_KEY, want_c, present=True)
-        self._pause(True)
-        self._state("draining", f"{cur_c}->{want_c}")
-        deadline = time.monotonic() + self.drain_timeout
-        while True:
-            busy = self.gpu_pods()
-            if not busy:
-                break
-            if time.monotonic() >= deadline:
-                names = ",".join(p["metadata"]["name"] for p in busy[:5])
-                self._abort(f"drain timeout: GPU pods still running ({names})")
-                return "failed"
-            self.sleep(self.poll)
-        # 2. apply to the off-target ASICs only, memory partition first (the compute split must
+        nonce = self._pause(True)
+        self._state("draining", f"{cur_c}->{want_c} (drainPolicy {self.drain_policy})")
+        err = self.drain(time.monotonic() + self.drain_timeout)
+        if err:
+            self._abort(err)
+            return "failed"
+        # 2. the operator's GPU clients have closed their handles
+        self._state("quiescing", "waiting for exporter / driver probe / device plugin to release the GPUs")
+        missing = self.wait_acks(nonce)
+        if missing:
+            log.warning("no pause ack from %s after %.0f s; applying anyway (EBUSY is retried)",
+                        ",".join(missing), self.pause_ack_timeout)
+        # 3. apply to the off-target ASICs only, memory partition first (the compute split must
         #    fit the memory layout)
         self._state("applying", f"{want_c}/{want_m} on {len(off)} ASIC(s)")
         done: List[str] = []
@@ -173,15 +212,15 @@ class PartitionManager:
             c_i, m_i = modes[uid]
             try:
                 if m_i != want_m:
-                    self.backend.set_memory(head, want_m)
+                    self._apply(self.backend.set_memory, head, want_m)
                 if c_i != want_c:
-                    self.backend.set_compute(head, want_c)
+                    self._apply(self.backend.set_compute, head, want_c)
             except Exception as e:  # noqa: BLE001
                 self._abort(f"apply failed on {head.pci_bdf} after {len(done)} of {len(off)} "
                             f"ASIC(s) switched: {e}")
                 return "failed"
             done.append(head.pci_bdf)
-        # 3. wait for the driver to re-enumerate every ASIC in the new mode
+        # 4. wait for the driver to re-enumerate every ASIC in the new mode
         self._state("reenumerating")
         expect = len(asics) * topo_mod.PARTITION_SPLIT[want_c]
         deadline = time.monotonic() + self.reenum_timeout
@@ -196,13 +235,83 @@ class PartitionManager:
                 self._abort(f"re-enumeration timeout (expected {expect} agents)")
                 return "failed"
             self.sleep(self.poll)
-        # 4. resume
+        # 5. resume (the paused clients re-open re-enumerated handles)
         self._pause(False)
         self.client.set_taint(self.node, TAINT_KEY, "", present=False)
         self.client.set_node_labels(self.node, {"amd.com/gpu.compute-partition": want_c,
                                                 "amd.com/gpu.memory-partition": want_m})
         self._state("idle", f"applied {want_c}/{want_m} on {len(off)} ASIC(s)")
         return "applied"
+
+    def _validator_busy(self) -> bool:
+        """A validator load step holds a live reservation (it is loading the GPUs right now)."""
+        if not self.reservation:
+            return False
+        try:
+            with open(self.reservation) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            return False
+        return float(doc.get("expires", 0)) > time.time()
+
+    def drain(self, deadline: float) -> Optional[str]:
+        """Empty the node of GPU pods; returns None when drained, else the failure reason."""
+        blocked: Dict[str, str] = {}
+        while True:
+            busy = self.gpu_pods()
+            validating = self._validator_busy()
+            if not busy and not validating:
+                return None
+            if self.drain_policy == "evict":
+                for p in busy:
+                    md = p.get("metadata", {})
+                    if md.get("deletionTimestamp"):
+                        continue          # already terminating
+                    key = f"{md.get('namespace')}/{md.get('name')}"
+                    try:
+                        self.client.evict_pod(md.get("namespace"), md.get("name"))
+                        blocked.pop(key, None)
+                        log.info("evicted GPU pod %s", key)
+                    except kube_mod.KubeError as e:
+                        # 429: the eviction would violate a PodDisruptionBudget — retry later
+                        blocked[key] = (e.message if e.status == 429
+                                        else f"HTTP {e.status}: {e.message}")[:200]
+            if time.monotonic() >= deadline:
+                names = ",".join(p["metadata"]["name"] for p in busy[:5])
+                if blocked:
+                    return "drain timeout: eviction refused for " + "; ".join(
+                        f"{k} ({v})" for k, v in sorted(blocked.items())[:5])
+                if not busy:
+                    return "drain timeout: a validator load step is still running"
+                return f"drain timeout: GPU pods still running ({names})" + \
+                    (" [drainPolicy wait]" if self.drain_policy == "wait" else "")
+            self.sleep(self.poll)
+
+    def wait_acks(self, nonce: Optional[str]) -> List[str]:
+        """Wait for every paused component's ack; returns those that never acked."""
+        if not nonce or not self.ack_components:
+            return []
+        deadline = time.monotonic() + self.pause_ack_timeout
+        while True:
+            got = pause_mod.acks(nonce, self.ack_dir, self.ack_components)
+            missing = [c for c, ok in got.items() if not ok]
+            if not missing or time.monotonic() >= deadline:
+                return missing
+            self.sleep(min(self.poll, 1.0))
+
+    def _apply(self, fn, head: topo_mod.GpuDevice, mode: str) -> None:
+        """One sysfs / amd-smi write, retried with exponential backoff while the device is busy."""
+        for attempt in range(self.apply_retries + 1):
+            try:
+                fn(head, mode)
+                return
+            except Exception as e:  # noqa: BLE001
+                if not is_busy(e) or attempt == self.apply_retries:
+                    raise
+                delay = self.retry_backoff * (2 ** attempt)
+                log.warning("%s busy (%s); retry %d/%d in %.1f s", head.pci_bdf, e, attempt + 1,
+                            self.apply_retries, delay)
+                self.sleep(delay)
 
     def _abort(self, reason: str) -> None:
         self._pause(False)

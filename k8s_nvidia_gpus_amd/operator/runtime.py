@@ -145,7 +145,10 @@ def ensure_module(dev_root: str = "/dev", host_root: str = "/host", runner=None)
 def driver_ready_loop(bin_path: str, expect: int, min_gfx: int, marker_dir: str,
                       interval: float = 30.0, stop_event=None, extra: Optional[List[str]] = None,
                       load_module: bool = False, dev_root: str = "/dev",
-                      host_root: str = "/host") -> None:
+                      host_root: str = "/host", guard=None, pause_poll: float = 1.0) -> None:
+    """Re-probe every ``interval``.  While a partition change is in progress (``guard``, see
+    pause.py) the probe — which opens /dev/kfd and every render node — is not run, the marker is
+    left as it is, and the pause is acked; probing resumes when the pause ends."""
     import threading
 
     stop_event = stop_event or threading.Event()
@@ -154,6 +157,12 @@ def driver_ready_loop(bin_path: str, expect: int, min_gfx: int, marker_dir: str,
     was_ready = None
     tried_modprobe = False
     while not stop_event.is_set():
+        if guard is not None and guard.paused():
+            guard.ack()
+            stop_event.wait(pause_poll)
+            continue
+        if guard is not None:
+            guard.clear()
         if load_module and not tried_modprobe:
             tried_modprobe = ensure_module(dev_root, host_root) is not None
         p = run_kfd_probe(bin_path, expect, min_gfx, marker, extra)
@@ -162,7 +171,14 @@ def driver_ready_loop(bin_path: str, expect: int, min_gfx: int, marker_dir: str,
             log.info("driver %s%s", "READY" if ready else "NOT READY",
                      "" if ready else f": {p.stderr.strip()}")
             was_ready = ready
-        stop_event.wait(interval)
+        # wake early for a pause: sleep in short slices while no pause is pending
+        waited = 0.0
+        while waited < interval and not stop_event.is_set():
+            if guard is not None and guard.paused():
+                break
+            step = min(pause_poll, interval - waited)
+            stop_event.wait(step)
+            waited += step
 
 
 def host_binary_present(path: str) -> bool:

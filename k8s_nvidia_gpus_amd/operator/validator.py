@@ -256,9 +256,14 @@ class Validator:
                  bin_dir: Optional[str] = None, runner: Runner = default_runner, root: str = "/",
                  kube=None, node_name: Optional[str] = None, driver_wait: float = 120,
                  telemetry: Optional[Callable[[], List[Dict]]] = None,
-                 device_id_map: str = DEVICE_ID_MAP):
+                 device_id_map: str = DEVICE_ID_MAP, pause_marker: Optional[str] = None):
+        from .pause import PAUSE_MARKER
+
         self.cfg = config
         self.device_id_map = device_id_map
+        # no load step starts while the partition manager switches modes
+        self.pause_marker = pause_marker if pause_marker is not None else (
+            PAUSE_MARKER if root == "/" else os.path.join(root, PAUSE_MARKER.lstrip("/")))
         self._scope: Optional[GpuScope] = None
         self._fp: Optional[Dict[str, str]] = None
         self.telemetry = telemetry  # per-GPU samples for the stress step (default: amd-smi)
@@ -947,6 +952,8 @@ class Validator:
                                                          "full validation", "previous": prev})
             # a fresh kubelet answer per load step (steps run minutes apart)
             sc = self._scope = self.gpu_scope()
+            if os.path.exists(self.pause_marker):
+                return self._deferred(step, sc, "partition change in progress")
             if sc.error:
                 return StepResult(step, False, {"gpu_scope": sc.to_dict()}, sc.error)
             if sc.known and not sc.free:
@@ -1027,7 +1034,8 @@ def hold_loop(v: "Validator", marker_dir: str, interval: float = 30.0,
               stop: Optional[Callable[[], bool]] = None, sleep: Callable[[float], None] = time.sleep) -> int:
     """The report container's life after the chain: restart the chain when it has to run again.
 
-    * the driver marker is withdrawn (driver restart / GPU reset), or
+    * the driver marker is withdrawn (driver restart / GPU reset),
+    * the GPU topology changed under it (a partition switch re-enumerated the agents), or
     * the node is ``deferred`` / ``partial`` and kubelet now shows a free GPU that has not been
       validated this boot (polled every ``retryDeferredSeconds``).
     A container restart would not re-run init containers, so the chain is restarted by deleting
@@ -1042,6 +1050,10 @@ def hold_loop(v: "Validator", marker_dir: str, interval: float = 30.0,
             break
         if time.monotonic() - last_check >= retry:
             last_check = time.monotonic()
+            now = v._fingerprint()
+            if any(now.get(k) != v.fingerprint().get(k) for k in ("partition", "agents", "device_uids")):
+                why = "GPU topology changed (partition switch / GPU lost): re-validate"
+                break
             label, _ = v.node_label()
             if label in (LABEL_DEFERRED, LABEL_PARTIAL):
                 pending = v.pending_devices()

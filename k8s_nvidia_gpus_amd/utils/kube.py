@@ -24,6 +24,7 @@ class KubeError(RuntimeError):
     def __init__(self, status: int, message: str):
         super().__init__(f"HTTP {status}: {message}")
         self.status = status
+        self.message = message
 
 
 class KubeClient:
@@ -68,6 +69,10 @@ class KubeClient:
                 payload = resp.read()
         except urllib.error.HTTPError as e:
             msg = e.read().decode(errors="replace")
+            try:   # a Status object: keep its human-readable message
+                msg = json.loads(msg).get("message") or msg
+            except (ValueError, AttributeError):
+                pass
             raise KubeError(e.code, msg) from None
         except urllib.error.URLError as e:
             raise KubeError(0, str(e.reason)) from None
@@ -119,6 +124,17 @@ class KubeClient:
     def delete_pod(self, namespace: str, name: str) -> None:
         try:
             self.request("DELETE", f"/api/v1/namespaces/{namespace}/pods/{name}")
+        except KubeError as e:
+            if e.status != 404:
+                raise
+
+    def evict_pod(self, namespace: str, name: str) -> None:
+        """Eviction API (policy/v1): the API server refuses with 429 while the eviction would
+        violate a PodDisruptionBudget.  404 (already gone) is success."""
+        body = {"apiVersion": "policy/v1", "kind": "Eviction",
+                "metadata": {"name": name, "namespace": namespace}}
+        try:
+            self.request("POST", f"/api/v1/namespaces/{namespace}/pods/{name}/eviction", body)
         except KubeError as e:
             if e.status != 404:
                 raise

@@ -2,7 +2,7 @@
 
 Enough of the API for the node agents: GET/PATCH /api/v1/nodes/<n> (JSON merge patch, RFC 7386),
 GET/POST/DELETE pods (namespaced and cluster-wide list with spec.nodeName / status.phase field
-selectors), GET pod logs.  ``on_pod_created`` lets a test play kubelet (e.g. mark the validator's
+selectors), GET pod logs, POST pods/<n>/eviction (429 for pods in ``pdb_blocked``).  ``on_pod_created`` lets a test play kubelet (e.g. mark the validator's
 plugin-test pod Succeeded with a log).
 """
 from __future__ import annotations
@@ -34,6 +34,9 @@ class FakeKubeAPI:
         self.logs: Dict[tuple, str] = {}
         self.requests = []
         self.on_pod_created: Optional[Callable[["FakeKubeAPI", dict], None]] = None
+        # (namespace, name) -> message: evictions of these pods are refused (PDB, HTTP 429)
+        self.pdb_blocked: Dict[tuple, str] = {}
+        self.evictions = []
         self._lock = threading.Lock()
         self._server = None
 
@@ -145,6 +148,14 @@ class FakeKubeAPI:
                 return 404, {"message": "pod not found"}, None
             if len(parts) == 7 and parts[6] == "log":
                 return 200, None, self.logs.get(key, "")
+            if len(parts) == 7 and parts[6] == "eviction" and method == "POST":
+                if body.get("kind") != "Eviction" or body.get("metadata", {}).get("name") != name:
+                    return 400, {"message": "bad Eviction body"}, None
+                if key in self.pdb_blocked:
+                    return 429, {"message": self.pdb_blocked[key]}, None
+                self.evictions.append(key)
+                self.pods.pop(key)
+                return 201, {"status": "Success"}, None
             if method == "GET":
                 return 200, self.pods[key], None
             if method == "DELETE":

@@ -152,12 +152,13 @@ def build_node(root, n_gpus: int = 8, compute_partition: Union[str, Sequence[str
 
 
 def add_cpu_only_pci(root, bdf: str = "0000:c1:00.0", vendor: str = "0x1a03",
-                     cls: str = "0x030000") -> None:
-    """A non-AMD PCI device (e.g. the BMC's VGA) on the node."""
+                     cls: str = "0x030000", device: str = "0x2000") -> None:
+    """A PCI device that is not an MI355X (default: the BMC's ASPEED VGA) on the node."""
     root = Path(root)
     d = root / "sys/devices/pci0000:c0" / bdf
     _w(d / "vendor", vendor + "\n")
     _w(d / "class", cls + "\n")
+    _w(d / "device", device + "\n")
     bus = root / "sys/bus/pci/devices"
     bus.mkdir(parents=True, exist_ok=True)
     os.symlink(os.path.relpath(d, bus), bus / bdf)

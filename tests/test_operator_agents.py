@@ -229,7 +229,7 @@ def test_partition_manager_spx_to_cpx(tmp_path, api, client):
     backend = FakeSysfsPartitionBackend(root)
     marker = tmp_path / "run/partition-in-progress"
     mgr = pm.PartitionManager(client, "gpu-node-1", backend, str(root), poll=0.01,
-                              pause_marker=str(marker), sleep=lambda s: None)
+                              pause_marker=str(marker), sleep=lambda s: None, ack_components=())
     assert mgr.reconcile() == "applied"
     assert len(read_topology(str(root), 90500).gpus) == 64
     assert not marker.exists()
@@ -256,7 +256,7 @@ def test_partition_manager_waits_for_gpu_pods_then_times_out(tmp_path, api, clie
 
     mgr = pm.PartitionManager(client, "gpu-node-1", FakeSysfsPartitionBackend(root), str(root),
                               drain_timeout=0.05, poll=0.01, pause_marker=str(tmp_path / "pause"),
-                              sleep=sleep)
+                              sleep=sleep, drain_policy="wait", ack_components=())
     assert mgr.reconcile() == "failed"
     assert seen["taint"] and seen["marker"]  # drained with taint + device-plugin pause
     node = api.nodes["gpu-node-1"]
@@ -270,7 +270,7 @@ def test_partition_manager_rejects_unavailable_mode(tmp_path, api, client):
     root = fake_sysfs.build_node(tmp_path / "r")
     api.nodes["gpu-node-1"]["metadata"]["labels"][pm.LABEL_DESIRED] = "XPX"
     mgr = pm.PartitionManager(client, "gpu-node-1", FakeSysfsPartitionBackend(root), str(root),
-                              pause_marker=str(tmp_path / "p"), sleep=lambda s: None)
+                              pause_marker=str(tmp_path / "p"), sleep=lambda s: None, ack_components=())
     assert mgr.reconcile() == "failed"
 
 
@@ -400,7 +400,8 @@ class PerAsicPartitionBackend:
 def test_partition_failure_mid_node_is_mixed_and_reconverges_per_asic(tmp_path, api, client):
     root = fake_sysfs.build_node(tmp_path / "r")
     api.nodes["gpu-node-1"]["metadata"]["labels"][pm.LABEL_DESIRED] = "CPX"
-    kw = dict(poll=0.01, pause_marker=str(tmp_path / "p"), sleep=lambda s: None, reenum_timeout=0.2)
+    kw = dict(poll=0.01, pause_marker=str(tmp_path / "p"), sleep=lambda s: None, reenum_timeout=0.2,
+              ack_components=())
     bad = PerAsicPartitionBackend(root, fail_on=3)
     assert pm.PartitionManager(client, "gpu-node-1", bad, str(root), **kw).reconcile() == "failed"
     state = api.nodes["gpu-node-1"]["metadata"]["annotations"][pm.ANNOT_STATE]
@@ -428,3 +429,19 @@ def test_labeller_pci_present_without_driver_and_not_on_cpu_nodes(tmp_path):
     cpu = tmp_path / "cpu"
     fake_sysfs.add_cpu_only_pci(cpu)                # BMC VGA (ASPEED), no AMD device
     assert all(v is None for v in compute_labels(str(cpu)).values())
+    # a CPU worker with an AMD Radeon (display class) must not get the driver DaemonSet
+    radeon = tmp_path / "radeon"
+    fake_sysfs.add_cpu_only_pci(radeon, bdf="0000:03:00.0", vendor="0x1002", cls="0x030000",
+                                device="0x744c")   # Radeon RX 7900 XTX
+    assert compute_labels(str(radeon))["amd.com/gpu.pci-present"] is None
+    # an older Instinct (MI300X, gfx942: class 0x12) is below minGfxTargetVersion gfx950
+    mi300 = tmp_path / "mi300"
+    fake_sysfs.add_cpu_only_pci(mi300, bdf="0000:05:00.0", vendor="0x1002", cls="0x120000",
+                                device="0x74a1")
+    assert compute_labels(str(mi300))["amd.com/gpu.pci-present"] is None
+    assert compute_labels(str(mi300), min_gfx=90402)["amd.com/gpu.pci-present"] == "true"
+    # an MI355X (0x75a3) on the bus, driver not loaded yet
+    mi355 = tmp_path / "mi355"
+    fake_sysfs.add_cpu_only_pci(mi355, bdf="0000:05:00.0", vendor="0x1002", cls="0x120000",
+                                device="0x75a3")
+    assert compute_labels(str(mi355))["amd.com/gpu.pci-present"] == "true"

@@ -110,7 +110,9 @@ def test_bench_py_distributed_contract_on_cpu(world):
     assert [r["bytes"] for r in sw] == [1 << 20, 4 << 20]            # 1 MiB .. top, x4
     assert doc["allreduce_busbw_gbps"] == pytest.approx(max(r["busbw_gbps"] for r in sw), abs=0.01)
     assert len(doc["telemetry_per_rank"]) == world                    # None on CPU (no GPU)
-    assert doc["value"] == pytest.approx(sum(doc["tflops_per_rank"]), rel=0.6)
+    # world x flop / MAX elapsed <= sum of per-rank rates (equal only when every rank is as slow as
+    # the slowest; CPU ranks under a loaded test runner are not)
+    assert 0 < doc["value"] <= sum(doc["tflops_per_rank"]) * 1.01 + 0.01 * world
 
 
 def test_bench_settle_phase_bounds():
