@@ -58,8 +58,11 @@ def tiny(**kw) -> LLMConfig:
 
 def from_gguf(meta: Dict[str, Any]) -> LLMConfig:
     arch = meta.get("general.architecture", "qwen2")
-    if arch not in ("qwen2", "llama"):
-        raise ValueError(f"unsupported architecture {arch!r} (this engine runs Qwen2/Llama decoders)")
+    if arch != "qwen2":
+        # e.g. llama: GGML_ROPE_TYPE_NORM (adjacent-pair rotation over permuted Q/K) and no QKV
+        # bias — loading it through the Qwen2 (NeoX-rope, biased) kernels would run silently wrong
+        raise ValueError(f"unsupported architecture {arch!r}: this engine implements the Qwen2 "
+                         f"decoder (NeoX RoPE, QKV bias) of the reference's Qwen2.5 model only")
 
     def g(key, default=None):
         v = meta.get(f"{arch}.{key}", default)
@@ -80,7 +83,7 @@ def from_gguf(meta: Dict[str, Any]) -> LLMConfig:
         ffn=int(g("feed_forward_length")), ctx=int(g("context_length", 4096)),
         rope_theta=float(g("rope.freq_base", 10000.0)),
         eps=float(g("attention.layer_norm_rms_epsilon", 1e-6)),
-        qkv_bias=(arch == "qwen2"), name=str(meta.get("general.name", arch)))
+        qkv_bias=True, name=str(meta.get("general.name", arch)))
 
 
 def to_gguf_metadata(cfg: LLMConfig) -> Dict[str, Any]:

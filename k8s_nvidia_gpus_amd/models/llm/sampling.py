@@ -14,6 +14,7 @@ drawn token id crosses to the host.
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass, field
 from typing import Any, Dict, Mapping, Optional, Sequence
 
@@ -45,14 +46,30 @@ class SamplingParams:
     @classmethod
     def from_request(cls, body: Mapping[str, Any], vocab: Optional[int] = None) -> "SamplingParams":
         """llama-server / OpenAI request fields → params (llama-server's defaults)."""
-        def num(key, default, cast=float):
+        def num(key, default, cast=float, lo=None, hi=None, lo_open=False):
             v = body.get(key)
-            return default if v is None else cast(v)
+            if v is None:
+                return default
+            if isinstance(v, bool) or not isinstance(v, (int, float, str)):
+                raise ValueError(f"{key} must be a number")
+            try:
+                x = cast(v)
+            except (TypeError, ValueError):
+                raise ValueError(f"{key} must be a number, got {v!r}") from None
+            if not math.isfinite(x):
+                raise ValueError(f"{key} must be finite")
+            if lo is not None and (x <= lo if lo_open else x < lo):
+                raise ValueError(f"{key} = {x} must be {'>' if lo_open else '>='} {lo}")
+            if hi is not None and x > hi:
+                raise ValueError(f"{key} = {x} must be <= {hi}")
+            return x
 
+        # out-of-range values are rejected here (HTTP 400) instead of turning logits into inf/NaN
+        # inside the shared decode loop (ADVICE r3)
         return cls(temperature=num("temperature", 0.8), top_k=num("top_k", 40, int),
-                   top_p=num("top_p", 0.95), min_p=num("min_p", 0.05),
-                   repeat_penalty=num("repeat_penalty", 1.0),
-                   repeat_last_n=num("repeat_last_n", 64, int),
+                   top_p=num("top_p", 0.95, lo=0.0, hi=1.0), min_p=num("min_p", 0.05, lo=0.0, hi=1.0),
+                   repeat_penalty=num("repeat_penalty", 1.0, lo=0.0, lo_open=True),
+                   repeat_last_n=num("repeat_last_n", 64, int, lo=-1),
                    presence_penalty=num("presence_penalty", 0.0),
                    frequency_penalty=num("frequency_penalty", 0.0),
                    logit_bias=parse_logit_bias(body.get("logit_bias"), vocab))
@@ -70,8 +87,20 @@ def parse_logit_bias(raw, vocab: Optional[int] = None) -> Dict[int, float]:
         tok, b = int(entry[0]), entry[1]
         if vocab is not None and not 0 <= tok < vocab:
             raise ValueError(f"logit_bias token {tok} outside the vocabulary ({vocab})")
-        out[tok] = -float("inf") if b is False else float(b)
+        if b is False:
+            out[tok] = -float("inf")
+            continue
+        bias = float(b)
+        if math.isnan(bias) or bias == float("inf"):
+            raise ValueError(f"logit_bias for token {tok} must be finite (or false to ban it)")
+        out[tok] = bias
+    if vocab is not None and sum(1 for v in out.values() if v == -float("inf")) >= vocab:
+        raise ValueError("logit_bias bans every token of the vocabulary")
     return out
+
+
+class NoTokenLeft(ValueError):
+    """Every token was filtered out (e.g. the request's biases ban all that remain)."""
 
 
 def _penalise(x: torch.Tensor, p: SamplingParams, history: Sequence[int]) -> torch.Tensor:
@@ -96,7 +125,11 @@ def sample_token(logits: torch.Tensor, p: SamplingParams, history: Sequence[int]
         x[tok] += b
     if p.penalised:
         x = _penalise(x, p, history)
+        # extreme (valid) penalties may overflow: keep the order, never produce inf/NaN logits
+        x = torch.nan_to_num(x, nan=-float("inf"), posinf=torch.finfo(x.dtype).max)
     if p.temperature <= 0.0:
+        if not torch.isfinite(x.max()):
+            raise NoTokenLeft("no token left to sample (every candidate was banned)")
         return int(torch.argmax(x).item())
     if p.top_k and p.top_k > 0:
         kth = torch.topk(x, min(p.top_k, x.numel())).values[-1]
@@ -109,7 +142,11 @@ def sample_token(logits: torch.Tensor, p: SamplingParams, history: Sequence[int]
     if p.min_p > 0.0:
         # keep tokens whose probability is >= min_p x the most likely one's (before temperature)
         x = x.masked_fill(x < x.max() + torch.log(torch.tensor(p.min_p)), -float("inf"))
-    probs = torch.softmax(x / p.temperature, -1)
+    top = x.max()
+    if not torch.isfinite(top):
+        raise NoTokenLeft("no token left to sample (every candidate was banned or filtered)")
+    # shift before scaling: a tiny temperature sends the others to -inf, never the maximum to +inf
+    probs = torch.softmax((x - top) / p.temperature, -1)
     if generator is not None and generator.device != probs.device:
         probs = probs.to(generator.device)
     return int(torch.multinomial(probs, 1, generator=generator).item())

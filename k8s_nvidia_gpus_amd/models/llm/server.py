@@ -11,10 +11,16 @@ layer is on the GPU) and serves the endpoints clients of that pod use:
   ``stream``, ``cache_prompt`` and the sampler fields of ``sampling.py`` — temperature, top_k,
   top_p, min_p, repeat_penalty / repeat_last_n, presence / frequency penalty, logit_bias) with
   llama.cpp's ``timings`` block;
-* ``POST /v1/completions`` and ``POST /v1/chat/completions`` (OpenAI; ChatML prompt format of
-  Qwen2.5-Instruct; ``stream`` as server-sent events);
-* ``POST /tokenize``, ``POST /detokenize``, ``GET /props``, ``GET /slots``, ``GET /metrics``
-  (Prometheus text).
+* ``POST /v1/completions`` and ``POST /v1/chat/completions`` (OpenAI; the prompt is rendered with
+  the model file's own ``tokenizer.chat_template`` — chat_template.py — ChatML when it has none;
+  ``tools`` are passed to the template; ``stream`` as server-sent events);
+* ``POST /apply-template``, ``POST /tokenize``, ``POST /detokenize``, ``GET /props``, ``GET /slots``,
+  ``GET /metrics`` (Prometheus text).
+
+Request sampler fields are range-checked (400 on a non-finite temperature, ``repeat_penalty <= 0``,
+``top_p`` / ``min_p`` outside [0, 1], a bias that bans the whole vocabulary …); a sampler failure
+at decode time ends only the request it belongs to.  Prompt tokenisation and template rendering
+run in the thread pool, never on the event loop.
 
 One scheduler thread owns the GPU: new requests are prefilled into free KV-cache slots, then every
 active sequence advances by one token per decode step — up to 4 sequences share each pass over
@@ -40,13 +46,13 @@ import threading
 import time
 import uuid
 from dataclasses import dataclass, field
-from typing import Any, Dict, Iterator, List, Optional
+from typing import Any, Dict, List, Optional
 
 import torch
 
 from .engine import Engine
 from .sampling import SamplingParams, sample_token
-from .tokenizer import Tokenizer, chatml
+from .tokenizer import Tokenizer
 
 try:   # module level: FastAPI resolves the handlers' (postponed) annotations in this namespace
     from fastapi import Request
@@ -247,16 +253,25 @@ class Scheduler:
             toks = self.engine.decode_greedy(*args)       # argmax inside the step's graph
         else:
             logits = self.engine.decode(*args)
-            toks = [sample_token(logits[i], j.params, j.ids + j.gen, j.generator)
-                    for i, j in enumerate(jobs)]
+            toks = []
+            for i, j in enumerate(jobs):
+                try:   # a request's own sampler failure ends that request only
+                    toks.append(sample_token(logits[i], j.params, j.ids + j.gen, j.generator))
+                except Exception as e:  # noqa: BLE001
+                    toks.append(e)
         dt = time.perf_counter() - t0
         with self._lock:
             self.metrics["decode_steps_total"] += 1
             self.metrics["decode_seconds_total"] += dt
-            self.metrics["tokens_predicted_total"] += len(jobs)
+            self.metrics["tokens_predicted_total"] += sum(1 for t in toks if not isinstance(t, Exception))
         for j, t in zip(jobs, toks):
-            j.pos += 1
-            if self._emit(j, int(t)):
+            j.pos += 1          # the step wrote this job's KV either way
+            if isinstance(t, Exception):
+                with self._lock:
+                    self.metrics["requests_failed_total"] = self.metrics.get("requests_failed_total", 0) + 1
+                j.out.put(("error", repr(t)))
+                self._release(j)
+            elif self._emit(j, int(t)):
                 self._release(j)
 
     def _loop(self) -> None:
@@ -318,16 +333,21 @@ async def _collect(job: Job, timeout: float, disconnected=None) -> Job:
             return val
 
 
-def _stream(job: Job, timeout: float) -> Iterator[tuple]:
-    """Events of ``job`` for a streaming response.  When the client disconnects the server closes
-    this generator (GeneratorExit): the job is cancelled and its KV slot freed."""
+async def _astream(job: Job, timeout: float, disconnected=None):
+    """Async events of ``job`` for a streaming response.  Polls every 0.5 s, so a client that goes
+    away while the job still waits in the pending queue (or between tokens) is noticed through
+    ``disconnected()`` and the job cancelled — its slot is freed at the next decode step instead of
+    after the whole ``timeout``."""
     deadline = time.perf_counter() + timeout
+    loop = asyncio.get_running_loop()
     finished = False
     try:
         while True:
             try:
-                kind, val = _get(job, deadline)
+                kind, val = await loop.run_in_executor(None, _get, job, deadline, 0.5)
             except queue.Empty:
+                if disconnected is not None and await disconnected():
+                    return
                 continue
             if kind == "error":
                 raise RuntimeError(val)
@@ -356,6 +376,9 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
     scheduler may be attached later (``/health`` answers 503 until then)."""
     from fastapi import FastAPI, HTTPException
     from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
+    from starlette.concurrency import run_in_threadpool
+
+    from .chat_template import TemplateError
 
     app = FastAPI(title="amdk8s llm server")
 
@@ -371,6 +394,25 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
         if isinstance(p, list):
             p = "".join(str(x) for x in p)
         return state["tok"].encode(str(p))
+
+    async def aencode(p) -> List[int]:
+        """BPE of a long prompt off the event loop (it would stall /health and every stream)."""
+        return await run_in_threadpool(encode_prompt, p)
+
+    def chat_prompt(body: Dict[str, Any]) -> str:
+        msgs = body.get("messages") or []
+        if not isinstance(msgs, list) or not msgs:
+            raise HTTPException(400, "messages must be a non-empty list")
+        tools = body.get("tools") or None
+        try:
+            return state["tok"].formatter.render(msgs, add_generation_prompt=True, tools=tools)
+        except TemplateError as e:
+            raise HTTPException(400, str(e))
+
+    async def achat_ids(body: Dict[str, Any]) -> List[int]:
+        def work():
+            return state["tok"].encode(chat_prompt(body))
+        return await run_in_threadpool(work)
 
     @app.get("/health")
     def health():
@@ -413,10 +455,10 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
     @app.post("/completion")
     async def completion(body: Dict[str, Any], request: Request):
         s = sched()
-        job = submit(body, encode_prompt(body.get("prompt", "")), s.engine.max_ctx)
+        job = submit(body, await aencode(body.get("prompt", "")), s.engine.max_ctx)
         if body.get("stream"):
-            def gen():
-                for kind, val in _stream(job, request_timeout):
+            async def gen():
+                async for kind, val in _astream(job, request_timeout, request.is_disconnected):
                     if kind == "text":
                         yield "data: " + json.dumps({"content": val, "stop": False}) + "\n\n"
                     else:
@@ -439,9 +481,9 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
         created = int(time.time())
         obj = "chat.completion" if chat else "text_completion"
         if body.get("stream"):
-            def gen():
+            async def gen():
                 first = True
-                for kind, val in _stream(job, request_timeout):
+                async for kind, val in _astream(job, request_timeout, request.is_disconnected):
                     if kind == "text":
                         if chat:
                             delta = {"content": val}
@@ -478,20 +520,26 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
 
     @app.post("/v1/completions")
     async def v1_completions(body: Dict[str, Any], request: Request):
-        return await openai(body, encode_prompt(body.get("prompt", "")), False, request)
+        return await openai(body, await aencode(body.get("prompt", "")), False, request)
 
     @app.post("/v1/chat/completions")
     async def v1_chat(body: Dict[str, Any], request: Request):
-        msgs = body.get("messages") or []
-        if not isinstance(msgs, list) or not msgs:
-            raise HTTPException(400, "messages must be a non-empty list")
-        return await openai(body, state["tok"].encode(chatml(msgs)), True, request)
+        sched()
+        return await openai(body, await achat_ids(body), True, request)
+
+    @app.post("/apply-template")
+    def apply_template(body: Dict[str, Any]):
+        """llama-server's endpoint: the prompt the chat template makes of ``messages``."""
+        sched()
+        return {"prompt": chat_prompt(body)}
 
     @app.get("/props")
     def props():
         s = sched()
         d = SamplingParams.from_request({})
+        fmt = state["tok"].formatter
         return {"total_slots": s.parallel, "model_path": state.get("model"),
+                "chat_template": fmt.source or "", "chat_template_source": fmt.kind,
                 "default_generation_settings": {
                     "n_ctx": s.engine.max_ctx, "temperature": d.temperature, "top_k": d.top_k,
                     "top_p": d.top_p, "min_p": d.min_p, "repeat_penalty": d.repeat_penalty,

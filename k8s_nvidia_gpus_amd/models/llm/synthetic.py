@@ -8,7 +8,7 @@ Q4_K_M type mix (``config.use_more_bits``), F32 norms/biases, and a byte-level B
 """
 from __future__ import annotations
 
-from typing import Optional
+from typing import Any, Dict, Optional
 
 import numpy as np
 
@@ -18,10 +18,13 @@ from .tokenizer import synthetic_vocab
 
 
 def write_synthetic_gguf(path: str, cfg: LLMConfig, seed: int = 0,
-                         tied: bool = False, f16_output: bool = False) -> str:
+                         tied: bool = False, f16_output: bool = False,
+                         extra_metadata: Optional[Dict[str, Any]] = None) -> str:
+    """``extra_metadata`` overrides / adds GGUF keys (e.g. another ``tokenizer.chat_template``)."""
     rng = np.random.default_rng(seed)
     md = to_gguf_metadata(cfg)
     md.update(synthetic_vocab(cfg.vocab))
+    md.update(extra_metadata or {})
     md["general.file_type"] = 15          # LLAMA_FTYPE_MOSTLY_Q4_K_M
     tensors = []
     Q4, Q6 = gguf.Q4_K, gguf.Q6_K
@@ -70,6 +73,6 @@ def load(path: str, device="cuda", max_ctx: int = 4096, slots: int = 4,
     from .weights import ModelWeights
 
     with gguf.GGUFFile(path) as g:
+        tok = Tokenizer.from_gguf(g.metadata)      # refuses unknown pre-tokenisers / bad templates
         w = ModelWeights.from_gguf(g, device=device)
-        tok = Tokenizer.from_gguf(g.metadata)
     return Engine(w, max_ctx=max_ctx, slots=slots, dense=dense), tok

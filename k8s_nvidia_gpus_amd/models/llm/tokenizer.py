@@ -1,9 +1,10 @@
-"""Qwen2 byte-level BPE tokenizer built from a GGUF file's ``tokenizer.ggml.*`` metadata, and the
-ChatML prompt format of Qwen2.5-Instruct.
+"""Byte-level BPE tokenizer built from a GGUF file's ``tokenizer.ggml.*`` metadata, and the
+ChatML prompt format of Qwen2.5-Instruct (the fallback when a file carries no chat template).
 
 llama.cpp reads the vocabulary from the model file (``tokenizer.ggml.model = gpt2``, ``tokens``,
-``merges``, ``token_type``); so does this engine, through the ``tokenizers`` library's BPE model with
-Qwen2's pre-tokenisation regex and a byte-level decoder.  Control tokens (``token_type == 3``:
+``merges``, ``token_type``, ``pre``); so does this engine, through the ``tokenizers`` library's BPE
+model with the pre-tokenisation regex ``tokenizer.ggml.pre`` names (chat_template.py; unknown
+pre-types are refused) and a byte-level decoder.  Control tokens (``token_type == 3``:
 ``<|im_start|>``, ``<|im_end|>``, ``<|endoftext|>`` …) are registered as special tokens so they are
 matched whole in prompts.
 """
@@ -15,8 +16,7 @@ from ...utils.bpe import bytes_to_unicode
 
 import numpy as np
 
-QWEN2_PATTERN = (r"(?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}|"
-                 r" ?[^\s\p{L}\p{N}]+[\r\n]*|\s*[\r\n]+|\s+(?!\S)|\s+")
+from .chat_template import QWEN2 as QWEN2_PATTERN, QWEN25_TEMPLATE, pre_tokenizer_pattern
 CONTROL = 3
 DEFAULT_SYSTEM = "You are Qwen, created by Alibaba Cloud. You are a helpful assistant."
 
@@ -24,7 +24,7 @@ DEFAULT_SYSTEM = "You are Qwen, created by Alibaba Cloud. You are a helpful assi
 class Tokenizer:
     def __init__(self, tokens: Sequence[str], merges: Sequence[str],
                  token_types: Optional[Sequence[int]] = None, eos_id: Optional[int] = None,
-                 bos_id: Optional[int] = None, add_bos: bool = False):
+                 bos_id: Optional[int] = None, add_bos: bool = False, pattern: str = QWEN2_PATTERN):
         from tokenizers import AddedToken, Regex, decoders, models, pre_tokenizers
         from tokenizers import Tokenizer as HFTokenizer
 
@@ -37,7 +37,7 @@ class Tokenizer:
         bpe = models.BPE(vocab=vocab, merges=pairs, ignore_merges=False)
         tk = HFTokenizer(bpe)
         tk.pre_tokenizer = pre_tokenizers.Sequence([
-            pre_tokenizers.Split(Regex(QWEN2_PATTERN), behavior="isolated", invert=False),
+            pre_tokenizers.Split(Regex(pattern), behavior="isolated", invert=False),
             pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=False)])
         tk.decoder = decoders.ByteLevel()
         types = list(token_types) if token_types is not None else [1] * len(tokens)
@@ -52,18 +52,28 @@ class Tokenizer:
         self.bos_id = bos_id
         self.add_bos = add_bos
         self.vocab = vocab
+        from .chat_template import ChatFormatter
+
+        # prompt format of /v1/chat/completions: the file's own template once from_gguf ran
+        self.formatter = ChatFormatter(None, default_system=DEFAULT_SYSTEM)
 
     @classmethod
     def from_gguf(cls, meta: Dict) -> "Tokenizer":
         model = meta.get("tokenizer.ggml.model", "gpt2")
         if model != "gpt2":
             raise ValueError(f"tokenizer model {model!r}: only byte-level BPE (gpt2) is supported")
+        from .chat_template import ChatFormatter
+
+        pattern = pre_tokenizer_pattern(meta)
+        formatter = ChatFormatter.from_gguf(meta, meta["tokenizer.ggml.tokens"])  # parses or raises
         types = meta.get("tokenizer.ggml.token_type")
-        return cls(list(meta["tokenizer.ggml.tokens"]), list(meta.get("tokenizer.ggml.merges", [])),
+        t = cls(list(meta["tokenizer.ggml.tokens"]), list(meta.get("tokenizer.ggml.merges", [])),
                    None if types is None else [int(x) for x in np.asarray(types)],
                    eos_id=meta.get("tokenizer.ggml.eos_token_id"),
                    bos_id=meta.get("tokenizer.ggml.bos_token_id"),
-                   add_bos=bool(meta.get("tokenizer.ggml.add_bos_token", False)))
+                   add_bos=bool(meta.get("tokenizer.ggml.add_bos_token", False)), pattern=pattern)
+        t.formatter = formatter
+        return t
 
     def encode(self, text: str) -> List[int]:
         ids = self._tk.encode(text, add_special_tokens=False).ids
@@ -91,19 +101,16 @@ class Tokenizer:
 def chatml(messages: Sequence[Dict[str, str]], default_system: Optional[str] = DEFAULT_SYSTEM,
            add_generation_prompt: bool = True) -> str:
     """Qwen2.5-Instruct's chat template (ChatML)."""
+    from .chat_template import message_text
+
     out = []
     if default_system and (not messages or messages[0].get("role") != "system"):
         out.append(f"<|im_start|>system\n{default_system}<|im_end|>\n")
     for m in messages:
-        content = m.get("content", "")
-        if isinstance(content, list):   # OpenAI content parts
-            content = "".join(p.get("text", "") for p in content if isinstance(p, dict))
-        out.append(f"<|im_start|>{m.get('role', 'user')}\n{content}<|im_end|>\n")
+        out.append(f"<|im_start|>{m.get('role', 'user')}\n{message_text(m.get('content', ''))}<|im_end|>\n")
     if add_generation_prompt:
         out.append("<|im_start|>assistant\n")
     return "".join(out)
-
-
 
 
 def synthetic_vocab(size: int, corpus: str = "") -> Dict:
@@ -150,4 +157,5 @@ def synthetic_vocab(size: int, corpus: str = "") -> Dict:
             "tokenizer.ggml.eos_token_id": tokens.index("<|im_end|>"),
             "tokenizer.ggml.padding_token_id": tokens.index("<|endoftext|>"),
             "tokenizer.ggml.bos_token_id": tokens.index("<|endoftext|>"),
-            "tokenizer.ggml.add_bos_token": False}
+            "tokenizer.ggml.add_bos_token": False,
+            "tokenizer.chat_template": QWEN25_TEMPLATE}

@@ -382,9 +382,15 @@ def test_server_cancels_abandoned_requests_and_times_out(tiny_model):
     state = {"scheduler": sched, "tok": tok, "model": "tiny"}
     try:
         job = sched.submit(S.Job(ids=tok.encode("hello"), max_new=200))
-        gen = S._stream(job, timeout=30)
-        next(gen)                                  # first token arrived: job is decoding
-        gen.close()                                # client went away
+
+        async def first_then_close():
+            agen = S._astream(job, timeout=30)
+            await agen.__anext__()                 # first token arrived: job is decoding
+            await agen.aclose()                    # client went away
+
+        import asyncio
+
+        asyncio.run(first_then_close())
         assert job.cancelled
         t0 = _t.time()
         while sched.active and _t.time() - t0 < 5:
@@ -474,3 +480,146 @@ def test_server_penalties_and_bias_over_http(client):
                                     "presence_penalty": 0.5, "frequency_penalty": 0.5})
     assert r.status_code == 200
     assert c.post("/completion", json={"prompt": "hello", "logit_bias": [[10 ** 9, 1]]}).status_code == 400
+
+
+def test_stream_client_gone_while_pending_is_cancelled_before_admission(tiny_model):
+    """a streaming client that disconnects while its job still waits for a slot is
+    noticed within a poll period; the job never gets a slot or a prefill."""
+    import asyncio
+    import time as _t
+
+    from k8s_nvidia_gpus_amd.models.llm import server as S
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load
+
+    eng, tok = load(tiny_model, device="cpu", max_ctx=256, slots=1)
+    real_decode = eng.decode
+    eng.decode = lambda *a, **k: (_t.sleep(0.02), real_decode(*a, **k))[1]
+    sched = S.Scheduler(eng, tok, parallel=1)
+    try:
+        busy = sched.submit(S.Job(ids=tok.encode("hello"), max_new=150))
+        waiting = sched.submit(S.Job(ids=tok.encode("world"), max_new=5))
+
+        async def gone():
+            return True
+
+        async def consume():
+            out = [ev async for ev in S._astream(waiting, timeout=60, disconnected=gone)]
+            return out
+
+        t0 = _t.time()
+        assert asyncio.run(consume()) == [] and _t.time() - t0 < 5
+        assert waiting.cancelled and waiting.slot == -1 and waiting.gen == []
+        busy.cancelled = True
+    finally:
+        sched.close()
+
+
+def test_bad_sampler_fields_are_400_and_a_failing_sampler_ends_only_its_job(client, monkeypatch):
+    """repeat_penalty=0, a non-finite temperature, top_p/min_p outside [0,1] or a bias
+    banning the whole vocabulary are rejected up front; a sampler error at decode time fails only
+    the job it belongs to — the request decoding next to it completes."""
+    from k8s_nvidia_gpus_amd.models.llm import server as S
+
+    c, eng, tok, state = client
+    sched = state["scheduler"]
+    for bad in ({"repeat_penalty": 0}, {"repeat_penalty": -1}, {"temperature": "nan"},
+                {"temperature": "inf"}, {"top_p": 1.5}, {"min_p": -0.1}, {"top_k": True},
+                {"logit_bias": [[i, False] for i in range(eng.cfg.vocab)]},
+                {"logit_bias": [[1, "inf"]]}, {"repeat_last_n": -2}):
+        r = c.post("/completion", json=dict({"prompt": "hello", "n_predict": 2}, **bad))
+        assert r.status_code == 400, bad
+    # a tiny temperature no longer overflows the softmax
+    r = c.post("/completion", json={"prompt": "hello", "n_predict": 3, "temperature": 1e-30})
+    assert r.status_code == 200
+    real = S.sample_token
+
+    def flaky(logits, p, history=(), generator=None):
+        if p.top_k == 7 and len(history) > len(tok.encode("boom")):   # the doomed job, in _step
+            raise RuntimeError("sampler exploded")
+        return real(logits, p, history, generator)
+
+    monkeypatch.setattr(S, "sample_token", flaky)
+    ids_a, ids_b = tok.encode("hello"), tok.encode("boom")
+    a = sched.submit(S._job_from({"temperature": 0, "repeat_penalty": 1.1}, ids_a, 8, eng.cfg.vocab))
+    b = sched.submit(S._job_from({"temperature": 0.7, "top_k": 7, "seed": 1}, ids_b, 8, eng.cfg.vocab))
+
+    def result(job):
+        while True:
+            kind, val = job.out.get(timeout=30)
+            if kind in ("done", "error"):
+                return kind, val
+
+    ka, va = result(a)
+    kb, vb = result(b)
+    assert ka == "done" and len(va.gen) == 8
+    assert kb == "error" and "sampler exploded" in vb
+    assert sched.metrics.get("requests_failed_total", 0) >= 1
+    # the scheduler keeps serving
+    r = c.post("/completion", json={"prompt": "again", "n_predict": 2, "temperature": 0})
+    assert r.status_code == 200
+
+
+def test_qwen25_embedded_template_matches_chatml_byte_for_byte():
+    """the GGUF's own template renders exactly today's chatml() output."""
+    from k8s_nvidia_gpus_amd.models.llm.chat_template import QWEN25_TEMPLATE, ChatFormatter
+    from k8s_nvidia_gpus_amd.models.llm.tokenizer import DEFAULT_SYSTEM, chatml
+
+    fmt = ChatFormatter(QWEN25_TEMPLATE, default_system=DEFAULT_SYSTEM)
+    cases = [
+        [{"role": "user", "content": "hi"}],
+        [{"role": "system", "content": "Be terse."}, {"role": "user", "content": "2+2?"}],
+        [{"role": "user", "content": "a"}, {"role": "assistant", "content": "b"},
+         {"role": "user", "content": "c\nd"}],
+        [{"role": "system", "content": "S"}, {"role": "user", "content": "u1"},
+         {"role": "assistant", "content": "a1"}, {"role": "system", "content": "late system"},
+         {"role": "user", "content": [{"type": "text", "text": "parts "}, {"type": "text", "text": "joined"}]}],
+    ]
+    for msgs in cases:
+        for gen in (True, False):
+            assert fmt.render(msgs, add_generation_prompt=gen) == chatml(msgs, add_generation_prompt=gen)
+    # tools go through the template (the ChatML fallback has no tool format)
+    out = fmt.render(cases[0], tools=[{"type": "function", "function": {"name": "f", "parameters": {}}}])
+    assert "# Tools" in out and '"name": "f"' in out and out.endswith("<|im_start|>assistant\n")
+
+
+LLAMA3_STYLE = ("{{- bos_token }}{% for m in messages %}<|start_header_id|>{{ m['role'] }}"
+                "<|end_header_id|>\n\n{{ m['content'] | trim }}<|eot_id|>{% endfor %}"
+                "{% if add_generation_prompt %}<|start_header_id|>assistant<|end_header_id|>\n\n{% endif %}")
+
+
+def test_file_template_drives_chat_prompts_and_unsupported_files_are_refused(tmp_path):
+    """A non-ChatML template in the file is what /v1/chat/completions uses; a Llama-architecture
+    file, an unknown pre-tokeniser or a template that does not parse are refused at load."""
+    from fastapi.testclient import TestClient
+
+    from k8s_nvidia_gpus_amd.models.llm.server import Scheduler, create_app
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load, write_synthetic_gguf
+
+    p = str(tmp_path / "custom.gguf")
+    write_synthetic_gguf(p, tiny(), extra_metadata={"tokenizer.chat_template": LLAMA3_STYLE})
+    eng, tok = load(p, device="cpu", max_ctx=256, slots=1)
+    assert tok.formatter.kind == "gguf"
+    sched = Scheduler(eng, tok, parallel=1)
+    try:
+        c = TestClient(create_app({"scheduler": sched, "tok": tok, "model": "custom"}))
+        msgs = [{"role": "user", "content": "  hello  "}]
+        prompt = c.post("/apply-template", json={"messages": msgs}).json()["prompt"]
+        assert prompt == ("<|endoftext|><|start_header_id|>user<|end_header_id|>\n\nhello<|eot_id|>"
+                          "<|start_header_id|>assistant<|end_header_id|>\n\n")
+        r = c.post("/v1/chat/completions", json={"messages": msgs, "max_tokens": 2, "temperature": 0})
+        assert r.status_code == 200 and r.json()["usage"]["prompt_tokens"] == len(tok.encode(prompt))
+        assert c.get("/props").json()["chat_template"] == LLAMA3_STYLE
+        bad = c.post("/v1/chat/completions", json={"messages": [1, 2]})
+        assert bad.status_code == 400
+    finally:
+        sched.close()
+    for extra, needle in (({"general.architecture": "llama", "llama.block_count": 2,
+                            "llama.context_length": 512, "llama.embedding_length": 256,
+                            "llama.feed_forward_length": 512, "llama.attention.head_count": 2},
+                           "unsupported architecture 'llama'"),
+                          ({"tokenizer.ggml.pre": "deepseek-llm"}, "deepseek-llm"),
+                          ({"tokenizer.chat_template": "{% for m in messages %}"}, "does not parse")):
+        q = str(tmp_path / "bad.gguf")
+        write_synthetic_gguf(q, tiny(), extra_metadata=extra)
+        with pytest.raises(ValueError, match=needle):
+            load(q, device="cpu", max_ctx=256, slots=1)
