@@ -14,6 +14,12 @@
 // that the other ranks poll, then ncclCommInitRank); times are the MAX over ranks and rank 0 prints.
 // --plan prints the resolved launch (mode, rank, world, device, id file) and exits before any HIP call.
 //
+// The id file is keyed per launch, never just per port: <run id>.<launcher pid>.<restart>.<port>.
+// Every rank of one torchrun launch shares its parent (the elastic agent), whose pid is unique among
+// live processes; the Job also sets --rdzv-id to the pod UID.  A reader only accepts a file written
+// after the launcher started (mtime >= the agent's start time from /proc), so a stale file left in a
+// reused /tmp by a crashed earlier launch is ignored (rank 0 also removes it before publishing).
+//
 // busbw = algbw · 2(n−1)/n (ring all-reduce traffic per rank).  On MI355X each GPU has 7 xGMI links
 // of ~153 GB/s; a ring uses one outgoing link per hop, so RCCL reaches beyond one link only by
 // spreading channels over several rings — report what is measured, not the aggregate link rate.
@@ -22,6 +28,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -80,10 +87,59 @@ int env_int(const char* name, int dflt) {
   return v && *v ? std::atoi(v) : dflt;
 }
 
-// rank 0 → file (atomic rename); others poll for it
-bool exchange_id(ncclUniqueId* id, int rank, const std::string& path, int timeout_s) {
+// Wall-clock start time (s since the epoch) of process `pid`: /proc/<pid>/stat field 22 (clock
+// ticks after boot) + btime of /proc/stat.  -1 when unreadable.
+double process_start_time(pid_t pid) {
+  char path[64];
+  std::snprintf(path, sizeof(path), "/proc/%d/stat", (int)pid);
+  FILE* f = std::fopen(path, "r");
+  if (!f) return -1;
+  char buf[4096];
+  const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+  std::fclose(f);
+  buf[n] = 0;
+  const char* p = std::strrchr(buf, ')');   // comm may contain spaces
+  if (!p) return -1;
+  unsigned long long start = 0;
+  int field = 2;
+  for (const char* q = p + 1; *q && field < 22; ++q)
+    if (*q == ' ' && ++field == 22) start = std::strtoull(q + 1, nullptr, 10);
+  FILE* st = std::fopen("/proc/stat", "r");
+  if (!st) return -1;
+  char line[256];
+  double btime = -1;
+  while (std::fgets(line, sizeof(line), st))
+    if (std::strncmp(line, "btime ", 6) == 0) btime = std::strtod(line + 6, nullptr);
+  std::fclose(st);
+  if (btime < 0 || start == 0) return -1;
+  return btime + (double)start / (double)sysconf(_SC_CLK_TCK);
+}
+
+// Launch key shared by every rank of one torchrun launch (see the header comment).
+std::string launch_key() {
+  const char* run = std::getenv("TORCHELASTIC_RUN_ID");
+  const char* restart = std::getenv("TORCHELASTIC_RESTART_COUNT");
+  const char* port = std::getenv("MASTER_PORT");
+  return std::string(run && *run ? run : "none") + "." + std::to_string((long)getppid()) + "." +
+         (restart && *restart ? restart : "0") + "." + (port ? port : "0");
+}
+
+// A file at `path` that this launch may read: written no earlier than the launcher's start
+// (1 s slack for mtime granularity).  Without /proc the check is skipped (fresh = true).
+bool id_file_fresh(const std::string& path, double not_before) {
+  struct stat sb;
+  if (stat(path.c_str(), &sb) != 0) return false;
+  if (not_before < 0) return true;
+  const double mtime = (double)sb.st_mtim.tv_sec + 1e-9 * (double)sb.st_mtim.tv_nsec;
+  return mtime >= not_before - 1.0;
+}
+
+// rank 0 → file (stale copy removed first, then atomic rename); others poll for a FRESH file
+bool exchange_id(ncclUniqueId* id, int rank, const std::string& path, int timeout_s,
+                 double not_before) {
   if (rank == 0) {
-    const std::string tmp = path + ".tmp";
+    std::remove(path.c_str());
+    const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
     FILE* f = std::fopen(tmp.c_str(), "wb");
     if (!f || std::fwrite(id, sizeof(*id), 1, f) != 1) return false;
     std::fclose(f);
@@ -91,11 +147,13 @@ bool exchange_id(ncclUniqueId* id, int rank, const std::string& path, int timeou
   }
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(timeout_s);
   while (std::chrono::steady_clock::now() < deadline) {
-    FILE* f = std::fopen(path.c_str(), "rb");
-    if (f) {
-      const bool ok = std::fread(id, sizeof(*id), 1, f) == 1;
-      std::fclose(f);
-      if (ok) return true;
+    if (id_file_fresh(path, not_before)) {
+      FILE* f = std::fopen(path.c_str(), "rb");
+      if (f) {
+        const bool ok = std::fread(id, sizeof(*id), 1, f) == 1;
+        std::fclose(f);
+        if (ok) return true;
+      }
     }
     std::this_thread::sleep_for(std::chrono::milliseconds(20));
   }
@@ -116,7 +174,7 @@ int run_mp(const Options& o, int rank, int world, int local) {
   AMDK8S_HIP_CHECK(hipSetDevice(local));
   ncclUniqueId id;
   if (rank == 0) RCCL_CHECK(ncclGetUniqueId(&id));
-  if (!exchange_id(&id, rank, o.id_file, o.id_timeout_s)) {
+  if (!exchange_id(&id, rank, o.id_file, o.id_timeout_s, process_start_time(getppid()))) {
     std::fprintf(stderr, "rank %d: no ncclUniqueId at %s after %d s\n", rank, o.id_file.c_str(),
                  o.id_timeout_s);
     return 3;
@@ -241,14 +299,16 @@ int main(int argc, char** argv) {
       return 2;
     }
     if (o.id_file.empty()) {
-      const char* run = std::getenv("TORCHELASTIC_RUN_ID");
-      const char* port = std::getenv("MASTER_PORT");
-      o.id_file = std::string("/tmp/rccl-allreduce-bench.") + (run ? run : "none") + "." +
-                  (port ? port : "0") + ".id";
+      const char* tmpdir = std::getenv("TMPDIR");
+      o.id_file = std::string(tmpdir && *tmpdir ? tmpdir : "/tmp") + "/rccl-allreduce-bench." +
+                  launch_key() + ".id";
     }
     if (o.plan) {
+      const double not_before = process_start_time(getppid());
       std::printf("{\"mode\": \"mp\", \"rank\": %d, \"world\": %d, \"device\": %d, "
-                  "\"id_file\": \"%s\"}\n", rank, world, local, o.id_file.c_str());
+                  "\"id_file\": \"%s\", \"launcher_start\": %.3f, \"existing_id_file_fresh\": %s}\n",
+                  rank, world, local, o.id_file.c_str(), not_before,
+                  id_file_fresh(o.id_file, not_before) ? "true" : "false");
       return 0;
     }
     return run_mp(o, rank, world, local);

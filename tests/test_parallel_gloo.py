@@ -263,11 +263,40 @@ def test_rccl_bench_multiprocess_plan_under_torchrun():
                    key=lambda d: d["rank"])
     assert [(d["rank"], d["world"], d["device"]) for d in plans] == [(0, 3, 0), (1, 3, 1), (2, 3, 2)]
     assert len({d["id_file"] for d in plans}) == 1 and str(port) in plans[0]["id_file"]
+    # a second launch on the SAME port gets a different id file (launcher pid in
+    # the key) ...
+    p2 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                         "--nproc-per-node=2", "--master-addr=127.0.0.1", f"--master-port={port}",
+                         "--no-python", str(exe), "--mp", "--plan"],
+                        capture_output=True, text=True, timeout=120)
+    assert p2.returncode == 0, p2.stderr[-2000:]
+    second = [json.loads(ln) for ln in p2.stdout.splitlines() if ln.startswith("{")]
+    assert second[0]["id_file"] != plans[0]["id_file"] and str(port) in second[0]["id_file"]
+    # ... and a stale file at the launch's path (crashed earlier run, reused /tmp) is not accepted
+    import os
+    import tempfile
+    import time
+
+    stale = Path(tempfile.mkdtemp()) / "rccl.id"
+    stale.write_bytes(b"\0" * 128)
+    old = time.time() - 3600
+    os.utime(stale, (old, old))
+    p3 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                         "--nproc-per-node=2", "--master-addr=127.0.0.1", f"--master-port={port}",
+                         "--no-python", str(exe), "--mp", "--plan", "--id-file", str(stale)],
+                        capture_output=True, text=True, timeout=120)
+    third = [json.loads(ln) for ln in p3.stdout.splitlines() if ln.startswith("{")]
+    assert third and all(d["existing_id_file_fresh"] is False for d in third)
+    assert all(d["launcher_start"] > old for d in third)
     job = yaml.safe_load((repo / "cluster-config/apps/gpu-bench/job-rccl-allreduce.yaml").read_text())
     c = job["spec"]["template"]["spec"]["containers"][0]
     assert c["command"][-1] == "torch.distributed.run" and "--no-python" in c["args"] and "--mp" in c["args"]
     nproc = next(a for a in c["args"] if a.startswith("--nproc-per-node=")).split("=")[1]
     assert int(nproc) == int(c["resources"]["limits"]["amd.com/gpu"])
+    # the rendezvous id is the pod UID (downward API), unique per Job pod
+    assert "--rdzv-id=$(POD_UID)" in c["args"]
+    env = {e["name"]: e for e in c["env"]}
+    assert env["POD_UID"]["valueFrom"]["fieldRef"]["fieldPath"] == "metadata.uid"
 
 
 def test_telemetry_sampler_matches_gpu_by_pci_address():

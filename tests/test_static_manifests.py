@@ -41,7 +41,7 @@ def resources_of(kdir: Path):
             continue
         p = kdir / r
         if p.is_dir():
-            out.extend(resources_of(p))
+            out.extend(resources_of(p)[1])
         else:
             out.extend(load_all(p))
     return k, out
@@ -60,7 +60,7 @@ def test_kustomization_resources_resolve_and_are_pure_kustomize(kdir):
     k = yaml.safe_load((kdir / "kustomization.yaml").read_text())
     assert k["apiVersion"] == "kustomize.config.k8s.io/v1beta1" and k["kind"] == "Kustomization"
     allowed = {"apiVersion", "kind", "namespace", "resources", "labels", "images",
-               "configMapGenerator", "patches", "commonAnnotations", "generatorOptions"}
+               "configMapGenerator", "patches", "commonAnnotations", "generatorOptions", "nameSuffix"}
     extra = set(k) - allowed
     assert not extra, f"non-kustomize fields (Flux-only?) in {kdir}: {extra}"
     for r in k.get("resources", []):
@@ -137,6 +137,25 @@ def pod_specs(objs):
             yield o, o["spec"]
 
 
+def kustomize_bases(kdir: Path):
+    """Kustomization directories ``kdir`` pulls in as resources (recursively)."""
+    k = yaml.safe_load((kdir / "kustomization.yaml").read_text())
+    out = []
+    for r in k.get("resources", []):
+        p = (kdir / r).resolve()
+        if not r.startswith("https://") and p.is_dir():
+            out += [p] + kustomize_bases(p)
+    return out
+
+
+def is_base_or_overlay(kdir: Path) -> bool:
+    """A base another kustomization includes, or an overlay over one: the namespace object and the
+    image rewrite live in the including / included kustomization."""
+    if kustomize_bases(kdir):
+        return True
+    return any(kdir.resolve() in kustomize_bases(other) for other in kustomization_dirs() if other != kdir)
+
+
 def all_objects():
     for kdir in kustomization_dirs():
         if kdir.name in ("flux-system", "gotk-components"):
@@ -184,7 +203,10 @@ def test_images_are_pinned():
                 img = c["image"]
                 assert not img.endswith(":latest"), img
                 if img in ("amd-gpu-operator", "amd-gpu-bench"):
-                    assert any(i["name"] == img for i in k.get("images", [])), f"{kdir}: {img} not rewritten"
+                    imgs = list(k.get("images", []))
+                    for b in kustomize_bases(kdir):
+                        imgs += yaml.safe_load((b / "kustomization.yaml").read_text()).get("images", [])
+                    assert any(i["name"] == img for i in imgs), f"{kdir}: {img} not rewritten"
                 else:
                     assert ":" in img, f"unpinned image {img}"
 
@@ -199,7 +221,8 @@ def test_namespaced_objects_match_kustomization_namespace():
                 continue
             got = o["metadata"].get("namespace", ns)
             assert got == ns, f"{kdir}: {o['kind']}/{o['metadata']['name']} in {got} != {ns}"
-            assert ns in declared or kdir.name == "gateway-api", f"{kdir}: namespace {ns} not declared"
+            assert ns in declared or kdir.name == "gateway-api" or is_base_or_overlay(kdir), \
+                f"{kdir}: namespace {ns} not declared"
 
 
 def test_operator_daemonsets_gate_on_markers_and_share_config():
@@ -588,3 +611,27 @@ def test_renovate_bumps_dockerfile_base_images():
         seen.update({h["depName"]: h["currentValue"] for h in hits})
     assert seen["rocm/dev-ubuntu-22.04"] == "7.2"
     assert seen["rocm/pytorch"].startswith("rocm7.2_")
+
+
+def test_gemm_bench_overlays_are_one_apply_per_scaling_point():
+    """gpu-bench/gemm-n{1,2,4,8} — each overlay's GPUS (torchrun --nproc-per-node)
+    equals its amd.com/gpu limit and its N, so a curve point is one `kubectl apply -k`."""
+    base = CC / "apps/gpu-bench/gemm-base"
+    (job,) = [o for o in load_all(base / "job-gemm-bench.yaml") if o["kind"] == "Job"]
+    c0 = job["spec"]["template"]["spec"]["containers"][0]
+    assert c0["env"][0]["name"] == "GPUS"                       # the overlays patch env[0]
+    assert "--nproc-per-node \"${GPUS}\"" in c0["args"][0] and "--gpus \"${GPUS}\"" in c0["args"][0]
+    names = set()
+    for n in (1, 2, 4, 8):
+        k = yaml.safe_load((CC / f"apps/gpu-bench/gemm-n{n}/kustomization.yaml").read_text())
+        assert k["resources"] == ["../gemm-base"] and k["namespace"] == "gpu-bench"
+        (p,) = k["patches"]
+        assert p["target"]["kind"] == "Job" and p["target"]["name"] == job["metadata"]["name"]
+        out = _json_patch(job, yaml.safe_load(p["patch"]))
+        c = out["spec"]["template"]["spec"]["containers"][0]
+        gpus = int(c["env"][0]["value"])
+        assert gpus == n == int(c["resources"]["limits"]["amd.com/gpu"])
+        names.add(job["metadata"]["name"] + k["nameSuffix"])
+    assert len(names) == 4                                      # the points can run side by side
+    top = yaml.safe_load((CC / "apps/gpu-bench/kustomization.yaml").read_text())
+    assert "gemm-n8" in top["resources"]
