@@ -300,7 +300,8 @@ def _json_patch(doc, ops):
     doc = copy.deepcopy(doc)
     for op in ops:
         assert op["op"] in ("replace", "add"), op
-        parts = [int(x) if x.isdigit() else x for x in op["path"].lstrip("/").split("/")]
+        parts = [int(x) if x.isdigit() else x.replace("~1", "/").replace("~0", "~")
+                 for x in op["path"].lstrip("/").split("/")]
         tgt = doc
         for p in parts[:-1]:
             tgt = tgt[p]
