@@ -6,8 +6,9 @@ The tree ships with placeholders (``ghcr.io/example-org/amd-gpu-{operator,bench}
 because every image it names is public (GPU Operator chart, ``cuda-sample:vectoradd``,
 ``llama.cpp:server-cuda``, ``pytorch/pytorch`` — reference helmrelease.yaml:9-16, README.md:283,
 llm/deployment.yaml:61, sd15-api/deployment.yaml:21); here the operator and workload images are
-built from this repo by CI (.github/workflows/ci.yaml ``images`` job, pushed to
-``ghcr.io/<owner>``), so a fresh cluster can only pull them once the manifests name that registry.
+built from this repo and pushed by you (``hack/build-images.sh --registry <yours> --push``; CI's
+``images`` job only checks that they build and pushes nothing), so a fresh cluster can only pull
+them once the manifests name that registry.
 
 Rewrites, idempotently and re-runnably (the CURRENT values are read from the tree, so running it
 again with another registry works):

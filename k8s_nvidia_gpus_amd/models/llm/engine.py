@@ -26,7 +26,6 @@ the GPU path is compared against it.
 from __future__ import annotations
 
 import math
-import os
 import time
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
@@ -35,6 +34,8 @@ import torch
 import torch.nn.functional as F
 
 from .config import LLMConfig
+
+NORM_PROLOGUE_T = 2     # steps of up to this many tokens normalise in the GEMV prologues
 from .weights import ModelWeights, QWeight
 
 
@@ -59,7 +60,6 @@ class StepBuffers:
     pos: torch.Tensor
     slot: torch.Tensor
     h: torch.Tensor
-    h2: torch.Tensor        # the other residual buffer of the fused-norm path (ping-pong)
     x8: torch.Tensor
     dx: torch.Tensor
     sx: torch.Tensor
@@ -101,67 +101,22 @@ class Engine:
         self.dense = self.gpu if dense is None else dense
         self._dense_w: Optional[Dict[str, torch.Tensor]] = None
         self._bufs: Dict[int, StepBuffers] = {}
-        # GEMV decomposition override "waves,rows" (sweeps); default: the kernel's own
-        self.gemv_cfg = dict(zip(("waves", "rows_per_wg"),
-                                 map(int, os.environ.get("AMDK8S_LLM_GEMV", "0,0").split(","))))
-        # Infinity-Cache prefetch of each layer's gate|up weights on a side stream while the
-        # latency-bound q|k|v / attention / o_proj kernels run (AMDK8S_LLM_PREFETCH=<workgroups>)
-        # measured and rejected (profiles/r03/k: 2.11 -> 3.08-3.50 ms per T=1 step): the prefetch
-        # competes with the GEMVs for HBM and its 2 GB per step is slower than the step itself
-        self.prefetch_wgs = int(os.environ.get("AMDK8S_LLM_PREFETCH", "0"))
-        # from this many tokens per step on, each GEMV input is RMS-normalised + quantised ONCE by
-        # rmsnorm_q8 instead of redundantly in every GEMV workgroup's prologue.  One threshold for
-        # every T keeps decode batch-invariant only if it is 1 or never reached (the two paths
-        # reduce the sum of squares in different orders): 1 = always (default: T = 1 unchanged,
-        # T = 4 3.98 -> 3.44 ms, profiles/r03/l), 0 = never.
-        self.q8_split_T = int(os.environ.get("AMDK8S_LLM_Q8SPLIT", "1")) or (1 << 30)
-        # decode attention's chunk merge inside the attention kernel (last-arriving workgroup of a
-        # (token, kv head) combines; arrival counters stay zero between launches).  Correct but
-        # measured slower: with agent-scope release / acquire fences T=1 2.10 -> 2.43 ms
-        # (profiles/r03/n); with write-through (sc1) partials, no fences and a one-pass merge of
-        # all heads 1.94 -> 2.06 ms (profiles/r03/w: the attention launch grows 8.7 -> 15.3 us,
-        # more than the 4.6 us combine launch it replaces).  Off by default.
-        self.fused_combine = os.environ.get("AMDK8S_LLM_FUSED_COMBINE", "0") != "0"
-        # with the once-per-input Q8 path: the gate|up pair GEMV quantises silu(g)·u itself (its
-        # workgroups own whole 32-row blocks), so ffn_down needs no separate quantisation launch
-        self.pair_q8 = os.environ.get("AMDK8S_LLM_PAIR_Q8", "1") != "0"   # T=1 2.13 -> 2.07 ms (r03/q)
-        # with the once-per-input Q8 path: o_proj and ffn_down write the new residual to the other
-        # of two buffers and their last workgroup RMS-normalises + quantises it for the next GEMV
-        # (LK.qgemv(..., cnt=)), so no rmsnorm_q8 launch is left inside the layer loop.  Correct
-        # (tests) but measured slower (profiles/r03/w: T=1 1.94 -> 2.17 ms; o_proj 5.8 -> 14.2 us:
-        # write-through drain + a 448-way arrival counter + the last workgroup's reload cost more
-        # than a boundary and the 4.5 us norm launch).  Off by default.
-        self.resid_norm = os.environ.get("AMDK8S_LLM_RESID_NORM", "0") != "0"
-        # q|k (Q4_K) and v (Q6_K in about half the Q4_K_M layers) in one two-matrix launch:
-        # T=1 2.00 -> 1.94 ms, T=4 3.36 -> 3.27 ms (profiles/r03/w)
-        self.qkv2 = os.environ.get("AMDK8S_LLM_QKV2", "1") != "0"
-        # the attention combine inside the o_proj GEMV prologue (LK.qgemv_attn: each o_proj
-        # workgroup merges the chunk partials of every head itself) instead of its own launch;
-        # "waves,rows" of that GEMV in AMDK8S_LLM_ATTN_OPROJ.  Measured neutral at T=1 and slower
-        # from T=2 (1.758 / 2.65 -> 1.758 / 2.87 ms at T=1 / 4, profiles/r03/af): off by default
-        self.attn_prologue = os.environ.get("AMDK8S_LLM_ATTN_PROLOGUE", "0") != "0"
-        self.attn_oproj_cfg = dict(zip(("waves", "rows_per_wg"), map(int, os.environ.get(
-            "AMDK8S_LLM_ATTN_OPROJ", "8,16").split(","))))
-        # dense prefill on the fused glue kernels (llm_prefill.hip); 0 = the PyTorch formulation
-        self.prefill_native = os.environ.get("AMDK8S_LLM_PREFILL_NATIVE", "1") != "0"
-        # native prefill: SDPA with enable_gqa on the cache slabs (no repeat_interleave copies;
-        # 11.4 -> 10.8 ms for 512 tokens, profiles/r03/ag)
-        self.prefill_gqa = os.environ.get("AMDK8S_LLM_PREFILL_GQA", "1") != "0"
         # attn_norm / ffn_norm inside the q|k|v and gate|up GEMV prologues (each workgroup
-        # normalises the L2-resident fp32 row itself) instead of two rmsnorm_q8 launches per
-        # layer; the gate|up -> Q8 hand-off to ffn_down and the final norm stay as they are.
-        # T=1 1.81 -> 1.74 ms, T=4 2.73 -> 2.75 ms (profiles/r03/aa), so only steps of up to
-        # AMDK8S_LLM_NORM_PROLOGUE_T tokens use it.  rmsnorm_q8 sums the squares in the 4-wave
-        # prologue's order, so both paths give the same bits and decode stays batch-invariant
-        # (models with dim >= 8192 run 8-wave GEMVs there: one path for every T)
-        self.norm_prologue = os.environ.get("AMDK8S_LLM_NORM_PROLOGUE", "1") != "0"
-        # prefill q stored token-major for SDPA (AMDK8S_LLM_PREFILL_QTOK): the attention output
-        # then needs no transpose copy before o_proj (tools/debug/sdpa_layout_probe.py)
-        self.prefill_qtok = os.environ.get("AMDK8S_LLM_PREFILL_QTOK", "1") != "0"
-        self.norm_prologue_T = int(os.environ.get("AMDK8S_LLM_NORM_PROLOGUE_T", "2"))
-        self._norm_cnt = None
-        self._attn_cnt = None
-        self._side = None
+        # normalises the L2-resident fp32 row itself) for steps of up to NORM_PROLOGUE_T tokens;
+        # larger steps normalise + quantise once per input (rmsnorm_q8).  T=1 1.81 -> 1.74 ms
+        # (profiles/r03/aa); from T = 3 the shared launch is faster (session AX).  rmsnorm_q8 sums
+        # the squares in the 4-wave prologue's order, so both paths give the same bits and decode
+        # stays batch-invariant (models with dim >= 8192 run 8-wave GEMVs there: one path for every
+        # T).  Attribute, not a knob: the batch-invariance test runs both paths.
+        self.norm_prologue = True
+        # dense prefill on the fused glue kernels (llm_prefill.hip), SDPA's GQA path on the cache
+        # slabs and q stored token-major (no transpose copy before o_proj); the PyTorch formulation
+        # (prefill_native = False) is the oracle of test_native_prefill_equals_torch_prefill
+        self.prefill_native = True
+        self.prefill_gqa = True
+        self.prefill_qtok = True
+        # rejected variants (in-launch attention combine, fused residual norm, combine in the o_proj
+        # prologue, MFMA attention, Infinity-Cache prefetch, ...): docs/experiments/llm_decode_rejected.md
         if self.gpu:
             from k8s_nvidia_gpus_amd.ops import llm_kernels as LK
 
@@ -287,7 +242,7 @@ class Engine:
         """Prompt-processing GEMMs: on the GPU the hand-written fp16 MFMA GEMMs
         (``ops/gemm_epi.py``: tile / split-K planned per shape, the residual add of o_proj and
         ffn_down fused into the epilogue straight into the fp32 stream); PyTorch on the CPU."""
-        if self.gpu and os.environ.get("AMDK8S_LLM_PREFILL_GEMM", "native") != "torch":
+        if self.gpu:
             from k8s_nvidia_gpus_amd.ops import gemm_epi as GE
 
             def mm(a, w, b=None):
@@ -317,7 +272,7 @@ class Engine:
                 T=T, tok=meta[0], pos=meta[1], slot=meta[2], meta=meta,
                 host=torch.zeros(3, T, dtype=torch.int32).pin_memory(),
                 ids=torch.zeros(T, dtype=torch.int32, device=dev),
-                h=torch.zeros(T, c.dim, **f32), h2=torch.zeros(T, c.dim, **f32),
+                h=torch.zeros(T, c.dim, **f32),
                 x8=torch.zeros(T, kmax, dtype=torch.int8, device=dev),
                 dx=torch.zeros(T, kmax // 32, **f32), sx=torch.zeros(T, kmax // 16, **f32),
                 x8f=torch.zeros(T, c.ffn, dtype=torch.int8, device=dev),
@@ -345,142 +300,65 @@ class Engine:
         return min(span, self.max_ctx)
 
     def _step_kernels(self, b: StepBuffers, span: int, fused: bool) -> None:
-        """One decode step.  ``fused``: every token in its own slot, so RoPE + the KV write run
-        inside the attention kernel (no rope_kv launch)."""
+        """One decode step, per layer: q|k|v (one two-matrix launch when q|k and v have different
+        quantisation types) → attention (+ its combine, which writes the Q8 o_proj input) → o_proj
+        (+= residual) → gate|up (SwiGLU, Q8 out) → ffn_down (+= residual).  ``fused``: every token
+        in its own slot, so RoPE + the KV write run inside the attention kernel (no rope_kv launch).
+        Steps of up to NORM_PROLOGUE_T tokens normalise in the GEMV prologues, larger ones once per
+        input with rmsnorm_q8."""
         LK, c = self.LK, self.cfg
         LK.dequant(self.w.tok_embd, b.h, rows=b.tok)          # embedding rows → residual
         qd = self._q8(b, c.dim)
+        qf = (b.x8f, b.dxf, b.sxf)
         scale = 1.0 / math.sqrt(c.head_dim)
-        G = self.gemv_cfg
-        cnt = None
-        if self.fused_combine:
-            if self._attn_cnt is None:
-                self._attn_cnt = torch.zeros(self.max_T * c.kv_heads, dtype=torch.int32,
-                                             device=self.device)
-            cnt = self._attn_cnt
+        pro = self.norm_prologue and (c.dim >= 8192 or b.T <= NORM_PROLOGUE_T)
 
-        def act(xf, norm_w, k, prologue=False):
-            """GEMV input: ((x8, dx, sx), {}) quantised here, or ((None,) * 3, fused-prologue
-            kwargs)."""
-            if prologue or b.T < self.q8_split_T:
+        def act(xf, norm_w):
+            """GEMV input: (Q8 views, {}) quantised here, or ((None,) * 3, prologue kwargs)."""
+            if pro:
                 return (None, None, None), dict(xf=xf, norm_w=norm_w, eps=c.eps)
-            if b.T >= self.q8_split_T:
-                q = self._q8(b, k)
-                LK.rmsnorm_q8(xf, norm_w, c.eps, *q)
-                return q, {}
-            return (None, None, None), dict(xf=xf, norm_w=norm_w, eps=c.eps)
+            LK.rmsnorm_q8(xf, norm_w, c.eps, *qd)
+            return qd, {}
 
-        pro = self.norm_prologue and (c.dim >= 8192 or b.T <= self.norm_prologue_T)
-        ap = self.attn_prologue and cnt is None      # combine merged in the o_proj prologue
-        ak = {"impl": LK.ATTN_SPLIT} if ap else {}
-        if (self.resid_norm and b.T >= self.q8_split_T and self.pair_q8 and c.ffn % 32 == 0
-                and c.dim % 256 == 0 and c.dim <= 4096):
-            self._step_fused_norm(b, span, fused, cnt)
-            return
-        pf = self.prefetch_wgs > 0
-        if pf:
-            main = torch.cuda.current_stream(self.device)
-            if self._side is None:
-                self._side = torch.cuda.Stream(self.device)
         for i, L in enumerate(self.w.layers):
-            if pf:                     # fork: the side stream streams gate|up into the MALL
-                self._side.wait_stream(main)
-                planes = [L.wg.q, L.wg.qh, L.wg.sc, L.wg.d, L.wu.q, L.wu.qh, L.wu.sc, L.wu.d]
-                self.LK.prefetch(planes, self.prefetch_wgs, self._side)
-            # RMSNorm + Q8 quantisation: in each GEMV's prologue (fp32 input + norm weight), or once
-            # per input for larger T (act())
-            xin = act(b.h, L.attn_norm, c.dim, pro)
-            if xin[0][0] is not None or pro:
-                self._qkv(b, L, xin[0], xin[1])
-            else:
-                off = 0
-                for w in L.wqkv:
-                    LK.qgemv(w, *xin[0], b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:],
-                             ldo=b.qkv.stride(0), **xin[1], **G)
-                    off += w.n
-            # attention: the o_proj prologue merges the chunk partials (no combine launch), or
-            # the combine writes the Q8 o_proj input
-            aq = (None, None, None) if ap else qd
+            self._qkv(b, L, *act(b.h, L.attn_norm))
             if fused:
                 LK.attn_decode(None, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
-                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *aq,
-                               span=span, qkv=b.qkv, cos_t=self.cos, sin_t=self.sin, cnt=cnt,
-                               **ak)
+                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
+                               span=span, qkv=b.qkv, cos_t=self.cos, sin_t=self.sin)
             else:
                 LK.rope_kv(b.qkv, b.pos, b.slot, self.cos, self.sin, c.heads, c.kv_heads,
                            c.head_dim, self.max_ctx, b.qrot, self.k_cache[i], self.v_cache[i])
                 LK.attn_decode(b.qrot, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
-                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *aq,
-                               span=span, cnt=cnt, **ak)
-            if ap:
-                LK.qgemv_attn(L.wo, b.po, b.pml, b.pos, span // LK.attn_chunk(), b.h,
-                              **self.attn_oproj_cfg)
+                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
+                               span=span)
+            LK.qgemv(L.wo, *qd, b.h, LK.RESID)
+            xin = act(b.h, L.ffn_norm)
+            if c.ffn % 32 == 0:      # the pair GEMV quantises silu(g)·u (the ffn_down input) itself
+                LK.qgemv(L.wg, *xin[0], b.t, LK.PAIR, w1=L.wu, **xin[1], q8_out=qf)
+                LK.qgemv(L.wd, *qf, b.h, LK.RESID)
             else:
-                LK.qgemv(L.wo, *qd, b.h, LK.RESID, **G)
-            xin = act(b.h, L.ffn_norm, c.dim, pro)
-            if self.pair_q8 and b.T >= self.q8_split_T and c.ffn % 32 == 0:
-                qf = (b.x8f, b.dxf, b.sxf)
-                LK.qgemv(L.wg, *xin[0], b.t, LK.PAIR, w1=L.wu, **xin[1], **G, q8_out=qf)
-                LK.qgemv(L.wd, *qf, b.h, LK.RESID, **G)
-            else:
-                LK.qgemv(L.wg, *xin[0], b.t, LK.PAIR, w1=L.wu, **xin[1], **G)
-                xin = act(b.t, None, c.ffn)
-                LK.qgemv(L.wd, *xin[0], b.h, LK.RESID, **xin[1], **G)
-        xin = act(b.h, self.w.out_norm, c.dim)
-        LK.qgemv(self.w.output, *xin[0], b.logits, LK.STORE, **xin[1], **G)
-        if pf:
-            main.wait_stream(self._side)   # join (graph capture needs every fork joined)
+                LK.qgemv(L.wg, *xin[0], b.t, LK.PAIR, w1=L.wu, **xin[1])
+                LK.rmsnorm_q8(b.t, None, c.eps, *self._q8(b, c.ffn))
+                LK.qgemv(L.wd, *self._q8(b, c.ffn), b.h, LK.RESID)
+        LK.rmsnorm_q8(b.h, self.w.out_norm, c.eps, *qd)
+        LK.qgemv(self.w.output, *qd, b.logits, LK.STORE)
 
-    def _qkv(self, b: StepBuffers, L, q8, pro=None) -> None:
+    def _qkv(self, b: StepBuffers, L, q8, pro) -> None:
         """q|k|v projections from the Q8 input (or, with ``pro``, from fp32 rows normalised in the
         GEMV prologue): one launch, also when q|k and v are stored in different quantisation
-        types (two-matrix GEMV; AMDK8S_LLM_QKV2=0 launches them apart)."""
-        LK, G = self.LK, self.gemv_cfg
-        pro = pro or {}
-        if len(L.wqkv) == 2 and self.qkv2:
+        types (two-matrix GEMV)."""
+        LK = self.LK
+        if len(L.wqkv) == 2:
             w0, w1 = L.wqkv
             if LK.qgemv2(w0, w1, *q8, b.qkv[:, :w0.n], b.qkv[:, w0.n:], bias0=L.bqkv[:w0.n],
-                         bias1=L.bqkv[w0.n:], **pro, **G):
+                         bias1=L.bqkv[w0.n:], **pro):
                 return
         off = 0
         for w in L.wqkv:
             LK.qgemv(w, *q8, b.qkv[:, off:], LK.STORE, bias=L.bqkv[off:], ldo=b.qkv.stride(0),
-                     **pro, **G)
+                     **pro)
             off += w.n
-
-    def _step_fused_norm(self, b: StepBuffers, span: int, fused: bool, cnt) -> None:
-        """The decode step with the norms fused into the residual GEMVs: per layer q|k|v,
-        attention (+ combine), o_proj (h -> h2, + ffn_norm Q8), gate|up (-> Q8), ffn_down (h2 -> h,
-        + the next layer's attn_norm / out_norm Q8) — one rmsnorm_q8 launch per step."""
-        LK, c = self.LK, self.cfg
-        if self._norm_cnt is None:
-            self._norm_cnt = torch.zeros(4, dtype=torch.int32, device=self.device)
-        nc = self._norm_cnt[:1]
-        G = self.gemv_cfg
-        qd = self._q8(b, c.dim)
-        qf = (b.x8f, b.dxf, b.sxf)
-        scale = 1.0 / math.sqrt(c.head_dim)
-        layers = self.w.layers
-        LK.rmsnorm_q8(b.h, layers[0].attn_norm, c.eps, *qd)
-        for i, L in enumerate(layers):
-            self._qkv(b, L, qd)
-            if fused:
-                LK.attn_decode(None, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
-                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
-                               span=span, qkv=b.qkv, cos_t=self.cos, sin_t=self.sin, cnt=cnt)
-            else:
-                LK.rope_kv(b.qkv, b.pos, b.slot, self.cos, self.sin, c.heads, c.kv_heads,
-                           c.head_dim, self.max_ctx, b.qrot, self.k_cache[i], self.v_cache[i])
-                LK.attn_decode(b.qrot, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
-                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
-                               span=span, cnt=cnt)
-            LK.qgemv(L.wo, *qd, b.h2, LK.RESID, res=b.h, norm_out=L.ffn_norm, q8_out=qd, cnt=nc,
-                     eps=c.eps, **G)
-            LK.qgemv(L.wg, *qd, b.t, LK.PAIR, w1=L.wu, **G, q8_out=qf)
-            nxt = layers[i + 1].attn_norm if i + 1 < len(layers) else self.w.out_norm
-            LK.qgemv(L.wd, *qf, b.h, LK.RESID, res=b.h2, norm_out=nxt, q8_out=qd, cnt=nc,
-                     eps=c.eps, **G)
-        LK.qgemv(self.w.output, *qd, b.logits, LK.STORE, **G)
 
     def _decode_native(self, tokens: Sequence[int], positions: Sequence[int],
                        slots: Sequence[int], greedy: bool = False) -> torch.Tensor:

@@ -48,26 +48,6 @@ constexpr int GROUP_M = 8;
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-// Timing-only ablations of the INTERLEAVED schedule (tools/gemm_w4_ablate.hip; results are WRONG):
-// bit 0 drops the in-loop tile staging, bit 1 the in-loop fragment reads, bit 2 the per-K-tile
-// barrier, bit 3 the per-K-tile vmcnt(0).
-#ifndef AMDK8S_W4_ABLATE
-#define AMDK8S_W4_ABLATE 0
-#endif
-
-#ifdef AMDK8S_W4_STAMPS
-// Diagnostic build only (tools/gemm_w4_stamps.hip): s_memtime of wave 0 at 4 points of every
-// INTERLEAVED K-tile (0 start, 1 K-half 0 done, 2 past the barrier, 3 K-half 1 done).
-__device__ unsigned long long* g_w4_stamps;
-__device__ int g_w4_stamp_stride;
-#define AMDK8S_W4_STAMP(T, SLOT)                                                            \
-  if (tid == 0 && (T) * 4 + (SLOT) < g_w4_stamp_stride)                                     \
-    g_w4_stamps[(size_t)blockIdx.x * g_w4_stamp_stride + (T) * 4 + (SLOT)] =                \
-        __builtin_amdgcn_s_memtime();
-#else
-#define AMDK8S_W4_STAMP(T, SLOT)
-#endif
-
 __device__ __forceinline__ void barrier_raw() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_barrier" ::: "memory");
@@ -285,11 +265,11 @@ amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* _
 #define AMDK8S_W4_PHASE(FA, FB, NB, BUF, FO, READ, DMA, TD)                             \
   _Pragma("unroll") for (int g = 0; g < 16; ++g) {                                      \
     AMDK8S_W4_MFMA4(g, FA, FB);                                                         \
-    if ((READ) && !(AMDK8S_W4_ABLATE & 2)) {                                            \
+    if (READ) {                                                                         \
       if (g & 1) FA[g >> 1] = lds_read16((BUF) + a_off + (g >> 1) * 2048 + (FO));      \
       else NB[g >> 1] = lds_read16((BUF) + b_off + (g >> 1) * 2048 + (FO));             \
     }                                                                                   \
-    if ((DMA) && !(AMDK8S_W4_ABLATE & 1)) dma_piece(TD, g);                             \
+    if (DMA) dma_piece(TD, g);                                                          \
   }
 
     // ---- prologue: tiles 0 (and 1) in flight; K-half 0 of tile 0 into registers ----
@@ -316,18 +296,13 @@ amdk8s_gemm_bf16_nt_256x256_w4(const uint16_t* __restrict__ A, const uint16_t* _
   {                                                                                     \
     const char* cur = lds + (t & 1) * TILE_BYTES;                                       \
     const char* nxt = lds + ((t + 1) & 1) * TILE_BYTES;                                 \
-    AMDK8S_W4_STAMP(t, 0)                                                               \
     AMDK8S_W4_PHASE(fa, fb0, fb1, cur, fo1, true, false, t)                             \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                  \
-    AMDK8S_W4_STAMP(t, 1)                                                               \
     if (NEXT) {                                                                         \
-      if (!(AMDK8S_W4_ABLATE & 8))                                                      \
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* tile t+1 landed */          \
-      if (!(AMDK8S_W4_ABLATE & 4)) barrier_raw();                                       \
-      AMDK8S_W4_STAMP(t, 2)                                                             \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* tile t+1 landed */            \
+      barrier_raw();                                                                    \
       AMDK8S_W4_PHASE(fa, fb1, fb0, nxt, fo0, true, DMA, t + 2)                         \
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                \
-      AMDK8S_W4_STAMP(t, 3)                                                             \
     } else {                                                                            \
       AMDK8S_W4_PHASE(fa, fb1, fb0, nxt, fo0, false, false, t)                          \
     }                                                                                   \

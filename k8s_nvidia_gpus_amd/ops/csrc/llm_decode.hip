@@ -91,16 +91,6 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Write-through (sc1) store / sc1 load: relaxed agent-scope atomics.  Data handed to another
-// workgroup INSIDE a launch goes through these on both sides (per-XCD L2s are not coherent; see
-// arrive_last).
-__device__ __forceinline__ void st_wt(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_wt(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // LDS offset of activation byte p of one token (32-byte pad per 256 bytes)
 __device__ __forceinline__ int xoff(int p) { return (p >> 8) * 288 + (p & 255); }
 
@@ -136,18 +126,6 @@ struct GemvArgs {
   int8_t* ox8;           // [T][N]
   float* odx;            // [T][N/32]
   float* osx;            // [T][N/16]
-  // resid mode with a fused RMSNorm of the updated residual (cnt != null): out = res + W.x is
-  // stored write-through, and the last workgroup to finish RMS-normalises out with onorm_w and
-  // quantises it into ox8 / odx / osx (the next GEMV's input) — no separate norm launch
-  const float* res;      // [T][ldo] residual input (out must be a different buffer)
-  const float* onorm_w;  // [N]
-  int* cnt;              // arrival counter, zero between launches (the last arriver resets it)
-  // input = decode-attention partials (po != null): the prologue merges the context chunks of
-  // every head (the attention combine) and quantises the result into the staged Q8 activations
-  const float* po;       // [T][heads][nsplit][128] unnormalised chunk outputs
-  const float* pml;      // [T][heads][nsplit][2] (max, sum) per chunk
-  const int* apos;       // [T] positions (chunks past pos[t] are not read)
-  int nsplit, chunk;
 };
 
 // Weights are streamed exactly once per step: non-temporal loads keep them from evicting the
@@ -431,10 +409,7 @@ __device__ __forceinline__ void finish_row(const GemvArgs& a, int row, int lane,
   if (lane % (SP * PER) == 0 && t < T) {
     float* o = a.out + (long)t * a.ldo + row;
     if constexpr (MODE == kStore) *o = v + (a.bias ? a.bias[row] : 0.f);
-    else if constexpr (MODE == kResid) {
-      if (a.res) st_wt(o, a.res[(long)t * a.ldo + row] + v);      // fused-norm form
-      else *o += v;
-    }
+    else if constexpr (MODE == kResid) *o += v;
     else {
       const float y = v / (1.f + __expf(-v)) * v1;
       if (q8s) q8s[t * 32 + (row - wrow0)] = y;      // quantised at the end of the workgroup
@@ -470,135 +445,6 @@ __device__ __forceinline__ void compute_reg(int nb, int sub, int bl, const XReg 
 }
 
 
-// Fused RMSNorm + Q8 of the updated residual (resid mode, cnt != null), run by the LAST workgroup
-// of the launch.  Every workgroup's out stores were write-through (st_wt); each wave drains them,
-// the workgroup meets at a barrier, one lane counts in, and the workgroup that draws gridDim - 1
-// reads out back with sc1 loads (ld_wt) — the arrive_last hand-off at launch scope.  The first 256
-// threads normalise: thread = 8-value chunks tid + 256 j, a lane quad = one 32-value Q8 block (the
-// rmsnorm_q8_kernel mapping); the per-token arithmetic does not depend on T.  N % 256 == 0,
-// N <= 4096 (checked by the host; larger models keep the rmsnorm_q8 launch).
-constexpr int kNormCh = 2;          // 8-value chunks per thread and token: N <= 4096
-template <int T>
-__device__ __forceinline__ void resid_norm_tail(const GemvArgs& a, float* red) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave: its sc1 stores landed
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(red);
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(a.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == (int)gridDim.x - 1;
-    if (last) __hip_atomic_store(a.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last;
-  }
-  __syncthreads();
-  if (*flag == 0) return;
-  const int N = a.N, nch = N >> 3, tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  float* part = red + 4;                             // [T][4] per-wave sums (red[0] = the flag)
-  // every token's rows in flight at once (one memory round trip), then per token the same maths
-  float v[T][kNormCh][8];
-#pragma unroll
-  for (int t = 0; t < T; ++t)
-#pragma unroll
-    for (int j = 0; j < kNormCh; ++j) {
-      const int c = tid + 256 * j;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        v[t][j][i] = (tid < 256 && c < nch) ? ld_wt(a.out + (long)t * a.ldo + c * 8 + i) : 0.f;
-    }
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    float ss = 0.f;
-#pragma unroll
-    for (int j = 0; j < kNormCh; ++j)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) ss = __fmaf_rn(v[t][j][i], v[t][j][i], ss);
-    ss = wave_sum(ss);
-    if (lane == 0 && wave < 4) part[t * 4 + wave] = ss;
-  }
-  __syncthreads();
-  if (tid >= 256) return;
-#pragma unroll
-  for (int j = 0; j < kNormCh; ++j) {
-    const int c = tid + 256 * j;
-    if (c >= nch) break;                             // whole quads (nch % 32 == 0)
-    const float4 wa = *reinterpret_cast<const float4*>(a.onorm_w + c * 8);
-    const float4 wb = *reinterpret_cast<const float4*>(a.onorm_w + c * 8 + 4);
-    const float ww[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const float r = rsqrtf((part[t * 4] + part[t * 4 + 1] + part[t * 4 + 2] + part[t * 4 + 3]) /
-                             (float)N + a.eps);
-      float q[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) q[i] = v[t][j][i] * (r * ww[i]);
-      float amax = 0.f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(q[i]));
-      amax = fmaxf(amax, __shfl_xor(amax, 1, kWave));
-      amax = fmaxf(amax, __shfl_xor(amax, 2, kWave));
-      const float d = amax / 127.f;
-      const float id = d > 0.f ? 1.f / d : 0.f;
-      uint32_t pk[2] = {0u, 0u};
-      int sq = 0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int qi = (int)__builtin_rintf(q[i] * id);
-        pk[i >> 2] |= ((uint32_t)(qi & 0xff)) << (8 * (i & 3));
-        sq += qi;
-      }
-      sq += __shfl_xor(sq, 1, kWave);
-      *reinterpret_cast<uint2*>(a.ox8 + (long)t * N + c * 8) = make_uint2(pk[0], pk[1]);
-      if ((tid & 3) == 0) a.odx[(long)t * (N >> 5) + (c >> 2)] = d;
-      if ((tid & 1) == 0) a.osx[(long)t * (N >> 4) + (c >> 1)] = d * (float)sq;
-    }
-  }
-}
-
-// The attention combine for 8 consecutive output dims (chunk c = head c / 16, dims (c % 16) * 8
-// ..) of token t: one pass over the context chunks in groups of 8 with every load of the group in
-// flight (online max), explicit roundings.  Used by the o_proj GEMV prologue (GemvArgs.po).
-__device__ __forceinline__ void merge_chunk8(const GemvArgs& a, int t, int c, float (&v)[8]) {
-  const int h = c >> 4, d4 = (c & 15) * 2;                    // float4 index within the head row
-  const int ns = min(a.nsplit, (a.apos[t] + a.chunk) / a.chunk);
-  const long hb = ((long)t * (a.K >> 7) + h) * a.nsplit;
-  float m = -INFINITY, den = 0.f, acc[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
-  for (int s0 = 0; s0 < ns; s0 += 8) {
-    float mx[8], l[8];
-    float4 lo[8], hi[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const long sidx = hb + min(s0 + u, ns - 1);
-      const float2 ml = *reinterpret_cast<const float2*>(a.pml + sidx * 2);
-      mx[u] = ml.x;
-      l[u] = ml.y;
-      lo[u] = reinterpret_cast<const float4*>(a.po + sidx * kHeadDim)[d4];
-      hi[u] = reinterpret_cast<const float4*>(a.po + sidx * kHeadDim)[d4 + 1];
-    }
-    float mn = m;
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (s0 + u < ns) mn = fmaxf(mn, mx[u]);
-    if (mn == -INFINITY) continue;
-    const float sc = m == -INFINITY ? 0.f : __expf(__fsub_rn(m, mn));
-    den = __fmul_rn(den, sc);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = __fmul_rn(acc[i], sc);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float w = (s0 + u < ns && mx[u] != -INFINITY) ? __expf(__fsub_rn(mx[u], mn)) : 0.f;
-      den = __fmaf_rn(w, l[u], den);
-      const float e[8] = {lo[u].x, lo[u].y, lo[u].z, lo[u].w, hi[u].x, hi[u].y, hi[u].z, hi[u].w};
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] = __fmaf_rn(w, e[i], acc[i]);
-    }
-    m = mn;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = den > 0.f ? __fdiv_rn(acc[i], den) : 0.f;
-}
-
 // REGX (a whole row is one stage, nb <= 8U): each lane touches the same <= U super-block columns
 // in every row, so its activations are read from LDS once into registers and every row after
 // that is pure weight streaming + VALU (no per-row LDS traffic).
@@ -624,36 +470,7 @@ __device__ __forceinline__ void qgemv_body(const GemvArgs& a, const int bid) {
   float* dxs = reinterpret_cast<float*>(lds + T * xstride);
   float* sxs = dxs + T * (K >> 5);
   float* red = sxs + T * (K >> 4);                   // [W][T] block-reduction scratch
-  if (a.po) {
-    // attention partials: merge each head's context chunks and quantise to Q8 (per token the
-    // thread mapping does not depend on T); lane quads = 32-value blocks (K % 256 == 0)
-    const int nch = K >> 3;
-    for (int i = threadIdx.x; i < T * nch; i += blockDim.x) {
-      const int t = i / nch, c = i - t * nch;
-      float v[8];
-      merge_chunk8(a, t, c, v);
-      float amax = 0.f;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) amax = fmaxf(amax, fabsf(v[k]));
-      amax = fmaxf(amax, dppf<kDppXor1>(amax));
-      amax = fmaxf(amax, dppf<kDppXor2>(amax));
-      const float d = amax / 127.f;
-      const float id = d > 0.f ? 1.f / d : 0.f;
-      uint32_t pk0 = 0u, pk1 = 0u;
-      int sq = 0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int q = (int)__builtin_rintf(v[k] * id);
-        if (k < 4) pk0 |= ((uint32_t)(q & 0xff)) << (8 * k);
-        else pk1 |= ((uint32_t)(q & 0xff)) << (8 * (k - 4));
-        sq += q;
-      }
-      sq += __float_as_int(dppf<kDppXor1>(__int_as_float(sq)));
-      *reinterpret_cast<uint2*>(xs + t * xstride + xoff(c * 8)) = make_uint2(pk0, pk1);
-      if ((c & 3) == 0) dxs[t * (K >> 5) + (c >> 2)] = d;
-      if ((c & 1) == 0) sxs[t * (K >> 4) + (c >> 1)] = d * (float)sq;
-    }
-  } else if (a.xf == nullptr) {
+  if (a.xf == nullptr) {
     // Q8 input: copy into LDS.  x8 [T][K], dx [T][K/32] and sx [T][K/16] are read as flat arrays
     // (index i = one 16-byte x8 unit = one sx value; dx for i < T*K/32), four units per thread
     // per round with every load of the round issued before any LDS store (clamped indices, no
@@ -868,9 +685,6 @@ __device__ __forceinline__ void qgemv_body(const GemvArgs& a, const int bid) {
       }
     }
   }
-  if constexpr (MODE == kResid) {
-    if (a.cnt) resid_norm_tail<T>(a, red);
-  }
 }
 
 template <int TYPE, int T, int MODE, int U, bool REGX>
@@ -1032,42 +846,12 @@ struct AttnArgs {
   float scale;
   float* po;
   float* pml;
-  // fused combine (cnt != null): the last of a (token, kv head)'s nsplit workgroups merges its G
-  // heads' chunks and writes the Q8 o_proj input (and the fp32 output when out != null)
-  int* cnt;               // [T][Hkv] arrival counters, zero between launches (the last resets)
-  float* out;
-  int8_t* x8;
-  float* dx;
-  float* sx;
 };
 
-// In-launch hand-off of the chunk partials (MI355X: per-XCD L2s are not coherent): every partial is
-// stored write-through (sc1: relaxed agent-scope atomic store) and read back with sc1 loads, so no
-// release / acquire fence (buffer_wbl2 / buffer_inv: several us each) is needed — each storing wave
-// drains its stores (vmcnt(0)), the workgroup meets at a barrier, then ONE lane counts in with an
-// agent-scope add; the workgroup whose add returns nsplit - 1 is last and merges (the hand-off form
-// of the MI355X visibility table: sc1 stores + drain + counter add, sc1 loads by the last arriver).
-// Arrival of one (token, kv head) workgroup after its write-through partial stores; true for the
-// last of the nsplit (which then reads every partial with ld_wt).  The counter is left at zero.
-__device__ __forceinline__ bool arrive_last(int* cnt, int nsplit) {
-  __shared__ int last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave: its sc1 stores landed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = old == nsplit - 1;
-    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  return last;
-}
-
-// Merge the chunks of NH heads (h0, h0 + hstep, ...; those >= hend are skipped) of token t and
-// quantise the attention output to Q8 (the o_proj input): thread dd = one output dim of each of its
-// heads; a 32-dim block = half a wave (dd & 31 within a wave).  One pass over the chunks in groups
-// of 8 with every partial of the group (all NH heads) loaded before any maths (online max: one
-// memory round trip per 8 chunks); per head the arithmetic does not depend on NH, so the separate
-// combine kernel (NH = 1) and the in-launch merge (NH = ceil(G / 2)) give identical bits.
+// Merge the context chunks of head h of token t and quantise the attention output to Q8 (the o_proj
+// input): thread dd = one output dim; a 32-dim block = half a wave (dd & 31 within a wave).  One
+// pass over the chunks in groups of 8 with every partial of the group loaded before any maths
+// (online max: one memory round trip per 8 chunks), explicit roundings.
 template <int NH>
 __device__ __forceinline__ void combine_heads(const float* __restrict__ po,
                                               const float* __restrict__ pml,
@@ -1089,9 +873,9 @@ __device__ __forceinline__ void combine_heads(const float* __restrict__ po,
 #pragma unroll
       for (int u = 0; u < 8; ++u) {                  // indices clamped, extra terms masked below
         const long sidx = hb[k] + min(s0 + u, ns - 1);
-        mx[k][u] = ld_wt(pml + sidx * 2);
-        l[k][u] = ld_wt(pml + sidx * 2 + 1);
-        ov[k][u] = ld_wt(po + sidx * kHeadDim + dd);
+        mx[k][u] = pml[sidx * 2];
+        l[k][u] = pml[sidx * 2 + 1];
+        ov[k][u] = po[sidx * kHeadDim + dd];
       }
 #pragma unroll
     for (int k = 0; k < NH; ++k) {
@@ -1170,18 +954,12 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   const int len = pos[t] + 1;
   const int p0 = sp * kAttnChunk;
   const long pidx = ((long)t * H + kh * G) * nsplit + sp;   // + g * nsplit
-  auto merge = [&]() {                   // fused combine by the last-arriving workgroup
-    if (a.cnt && arrive_last(a.cnt + t * Hkv + kh, nsplit))   // 2 heads per pass, all at once
-      combine_heads<(G + 1) / 2>(po, pml, pos, H, nsplit, kAttnChunk, kh * G + (threadIdx.x >> 7), 2,
-                                 kh * G + G, t, threadIdx.x & 127, a.out, a.x8, a.dx, a.sx);
-  };
   if (p0 >= len) {
     if (threadIdx.x < G) {
       float* dst = pml + (pidx + (long)threadIdx.x * nsplit) * 2;
-      if (a.cnt) { st_wt(dst, -INFINITY); st_wt(dst + 1, 0.f); }
-      else { dst[0] = -INFINITY; dst[1] = 0.f; }
+      dst[0] = -INFINITY;
+      dst[1] = 0.f;
     }
-    merge();
     return;
   }
   const int n = min(kAttnChunk, len - p0);
@@ -1339,301 +1117,13 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   for (int i = threadIdx.x; i < G * kHeadDim; i += blockDim.x) {
     const int g = i / kHeadDim, dd = i % kHeadDim;
     const float v = opart[0][g][dd] + opart[1][g][dd] + opart[2][g][dd] + opart[3][g][dd];
-    float* dst = po + (pidx + (long)g * nsplit) * kHeadDim + dd;
-    if (a.cnt) st_wt(dst, v);                        // read back inside this launch
-    else *dst = v;
+    po[(pidx + (long)g * nsplit) * kHeadDim + dd] = v;
   }
   if (threadIdx.x < G) {
     const int g = threadIdx.x;
     float* dst = pml + (pidx + (long)g * nsplit) * 2;
-    if (a.cnt) { st_wt(dst, mls[g][0]); st_wt(dst + 1, mls[g][1]); }
-    else { dst[0] = mls[g][0]; dst[1] = mls[g][1]; }
-  }
-  merge();
-}
-
-// ---------------------------------------------------------------- MFMA decode attention
-// One workgroup per (kv head, token, context split of up to kMChunk positions): 8 waves, each
-// walking 32-position tiles (tiles w, w + 8, ... of the split) with its own online softmax, then a
-// merge of the 8 waves' states in LDS.  Both products run on v_mfma_f32_16x16x32_f16 with the GQA
-// group as the 16-wide dimension (G <= 8 heads, the rest zero):
-//   S^T [32 pos x 16 heads] = K [pos][128] . Q^T — A = K rows straight from the cache (16 B per
-//       lane: row lane % 16, dims 8 (lane / 16) + 32 kk), B = Q^T held in registers;
-//       C: lane holds S^T[4 (lane / 16) + r + 16 pb][head lane % 16] — 8 positions of ONE head,
-//       so the softmax is lane-local but for a max over the 4 lanes of the head (permlane swaps)
-//       and the running sum stays per lane until the end.
-//   O^T [128 dims x 16 heads] += V^T . P^T — B = P^T straight from the S^T accumulators (the
-//       32 k-slots of the MFMA are mapped to positions so that lane (lane / 16 = q) supplies its own
-//       8 values: slot 8q + j <-> position 4q + j (j < 4), 16 + 4q + j - 4 (j >= 4)); A = V^T, read
-//       from the wave's V tile staged in LDS (8 ds_read_u16 per 16-dim block, rows padded).
-// With one split (contexts up to kMChunk) the workgroup writes the normalised output as Q8 (the
-// o_proj input) itself: no partials, no combine launch.  Not the default (attn_impl_default): with
-// 4 kv heads a decode token keeps only 4 CUs busy.  Longer contexts write per-split partials
-// (unnormalised O, natural-log max, sum) for attn_combine_q8_kernel.  Fused RoPE / KV write as in
-// attn_decode_kernel (distinct slots).  Scores use exp2 with log2(e) folded into the q scale.
-constexpr int kMChunk = 1024;
-constexpr int kMTile = 32;
-constexpr int kMWaves = 8;
-constexpr int kVRow = kHeadDim + 8;      // padded V-tile row (halves): lanes of a ds_read_u16 group
-                                         // hit different banks
-typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ f32x4_t mfma16h(const uint4 a, const uint4 b, const f32x4_t c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a),
-                                                __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
-}
-
-__device__ __forceinline__ float max4lanes(float v) {   // max over lanes l, l^16, l^32, l^48
-  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-  r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-__device__ __forceinline__ float sum4lanes(float v) {
-  v = swap_sum32(v, v);
-  return swap_sum16(v, v);
-}
-
-struct MAttnShared {
-  uint16_t qs[16][kHeadDim];                 // q (f16, scaled), heads >= G zero
-  uint16_t ql[16][kHeadDim];                 // q - f16(q): the low part (q ~ fp32 in two MFMAs)
-  uint16_t knew[kHeadDim];
-  uint16_t vnew[kHeadDim];
-  union {
-    uint16_t vt[kMWaves][kMTile][kVRow];     // per-wave V tiles
-    struct {
-      float m[kMWaves][16], l[kMWaves][16];
-      float o[kMWaves][8][kHeadDim];         // [wave][head < 8][dim]
-    } mg;
-  };
-};
-
-template <int G>
-__global__ void __launch_bounds__(512) attn_mfma_kernel(AttnArgs a, int chunk) {
-  __shared__ MAttnShared sh;
-  const int kh = blockIdx.x, sp = blockIdx.y, t = blockIdx.z;
-  const int H = a.H, Hkv = a.Hkv, nsplit = a.nsplit;
-  const int len = a.pos[t] + 1;
-  const int p0 = sp * chunk, p1 = min(p0 + chunk, len);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q4 = lane >> 4, c16 = lane & 15;
-  const long pidx = ((long)t * H + kh * G) * nsplit + sp;    // + g * nsplit
-  if (p0 >= len) {                                           // split past the context
-    if (tid < G) {
-      a.pml[(pidx + (long)tid * nsplit) * 2] = -INFINITY;
-      a.pml[(pidx + (long)tid * nsplit) * 2 + 1] = 0.f;
-    }
-    return;
-  }
-  const long cbase = ((long)a.slot[t] * Hkv + kh) * a.max_ctx * kHeadDim;
-  const float qscale = a.scale * 1.4426950408889634f;        // exp2 domain
-  const int pnew = len - 1;
-  const bool own = a.qkv != nullptr && pnew >= p0 && pnew < p1;
-  // ---- q (rotated here when fused) -> LDS f16; the new K / V row when this split holds it
-  {
-    const int g = tid >> 6, j = tid & 63;                    // 8 heads x 64 rotation pairs
-    float y0 = 0.f, y1 = 0.f;
-    if (a.qkv) {
-      const float* row = a.qkv + (long)t * a.ldq;
-      const float c = a.cos_t[(long)pnew * (kHeadDim / 2) + j];
-      const float sn = a.sin_t[(long)pnew * (kHeadDim / 2) + j];
-      const int gg = min(g, G - 1);
-      const float x0 = row[(kh * G + gg) * kHeadDim + j];
-      const float x1 = row[(kh * G + gg) * kHeadDim + j + kHeadDim / 2];
-      const float k0 = row[(H + kh) * kHeadDim + j], k1 = row[(H + kh) * kHeadDim + j + kHeadDim / 2];
-      const float v0 = row[(H + Hkv + kh) * kHeadDim + j];
-      const float v1 = row[(H + Hkv + kh) * kHeadDim + j + kHeadDim / 2];
-      y0 = rope_lo(x0, x1, c, sn) * qscale;
-      y1 = rope_hi(x0, x1, c, sn) * qscale;
-      if (own && g == 0) {
-        const long cpos = cbase + (long)pnew * kHeadDim;
-        const uint16_t h0 = f2h(rope_lo(k0, k1, c, sn)), h1 = f2h(rope_hi(k0, k1, c, sn));
-        const uint16_t e0 = f2h(v0), e1 = f2h(v1);
-        a.kc[cpos + j] = h0;
-        a.kc[cpos + j + kHeadDim / 2] = h1;
-        a.vc[cpos + j] = e0;
-        a.vc[cpos + j + kHeadDim / 2] = e1;
-        sh.knew[j] = h0;
-        sh.knew[j + kHeadDim / 2] = h1;
-        sh.vnew[j] = e0;
-        sh.vnew[j + kHeadDim / 2] = e1;
-      }
-    } else {
-      const int gg = min(g, G - 1);
-      const float* qr = a.q + (long)t * H * kHeadDim + (kh * G + gg) * kHeadDim;
-      y0 = qr[j] * qscale;
-      y1 = qr[j + kHeadDim / 2] * qscale;
-    }
-    if (g >= G) y0 = y1 = 0.f;
-    const uint16_t h0 = f2h(y0), h1 = f2h(y1);
-    sh.qs[g][j] = h0;
-    sh.qs[g][j + kHeadDim / 2] = h1;
-    sh.ql[g][j] = f2h(y0 - h2f(h0));
-    sh.ql[g][j + kHeadDim / 2] = f2h(y1 - h2f(h1));
-    sh.qs[g + 8][j] = sh.ql[g + 8][j] = 0;                   // heads 8..15: zero
-    sh.qs[g + 8][j + kHeadDim / 2] = sh.ql[g + 8][j + kHeadDim / 2] = 0;
-  }
-  __syncthreads();
-  uint4 qb[4], qlb[4];                                       // B = Q^T: head c16, dims 32kk+8q4
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) {
-    qb[kk] = *reinterpret_cast<const uint4*>(&sh.qs[c16][32 * kk + 8 * q4]);
-    qlb[kk] = *reinterpret_cast<const uint4*>(&sh.ql[c16][32 * kk + 8 * q4]);
-  }
-
-  float m = -INFINITY, l = 0.f;
-  f32x4_t o[8];
-#pragma unroll
-  for (int db = 0; db < 8; ++db) o[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  uint16_t (*vt)[kVRow] = sh.vt[wave];
-  const uint16_t* kcp = a.kc + cbase;
-  const uint16_t* vcp = a.vc + cbase;
-  auto load_tile = [&](int tb, uint4 (&kr)[2][4], uint4 (&vr)[8]) {
-#pragma unroll
-    for (int pb = 0; pb < 2; ++pb) {
-      const int pp = min(tb + 16 * pb + c16, p1 - 1);
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-        kr[pb][kk] = *reinterpret_cast<const uint4*>(kcp + (long)pp * kHeadDim + 32 * kk + 8 * q4);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {                            // V tile: row q4 + 4i, 16-B column c16
-      const int pp = min(tb + q4 + 4 * i, p1 - 1);
-      vr[i] = *reinterpret_cast<const uint4*>(vcp + (long)pp * kHeadDim + 8 * c16);
-    }
-  };
-  uint4 kA[2][4], vA[8], kB[2][4], vB[8];
-  const int tstep = kMWaves * kMTile;
-  int tb = p0 + wave * kMTile;
-  if (tb < p1) load_tile(tb, kA, vA);
-  auto tile = [&](int tb, uint4 (&kr)[2][4], uint4 (&vr)[8]) {
-    if (own && pnew >= tb && pnew < tb + kMTile) {           // loaded before it was written
-#pragma unroll
-      for (int pb = 0; pb < 2; ++pb)
-        if (tb + 16 * pb + c16 == pnew) {
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk)
-            kr[pb][kk] = *reinterpret_cast<const uint4*>(&sh.knew[32 * kk + 8 * q4]);
-        }
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (tb + q4 + 4 * i == pnew) vr[i] = *reinterpret_cast<const uint4*>(&sh.vnew[8 * c16]);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) *reinterpret_cast<uint4*>(&vt[q4 + 4 * i][8 * c16]) = vr[i];
-    f32x4_t st[2];
-#pragma unroll
-    for (int pb = 0; pb < 2; ++pb) {
-      st[pb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        st[pb] = mfma16h(kr[pb][kk], qlb[kk], st[pb]);       // low part first (smaller terms)
-        st[pb] = mfma16h(kr[pb][kk], qb[kk], st[pb]);
-      }
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int pb = 0; pb < 2; ++pb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (tb + 16 * pb + 4 * q4 + r >= p1) st[pb][r] = -INFINITY;
-        mx = fmaxf(mx, st[pb][r]);
-      }
-    const float mn = fmaxf(m, max4lanes(mx));                // > -inf: every tile has a position
-    const float alpha = exp2f(m - mn);
-    float pr[8];
-#pragma unroll
-    for (int pb = 0; pb < 2; ++pb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) pr[4 * pb + r] = exp2f(st[pb][r] - mn);
-    float ps = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) ps += pr[i];
-    l = l * alpha + ps;
-    m = mn;
-#pragma unroll
-    for (int db = 0; db < 8; ++db) o[db] *= alpha;
-    uint4 pb8;                                               // B = P^T: slots 8q4 + j
-    pb8.x = (uint32_t)f2h(pr[0]) | ((uint32_t)f2h(pr[1]) << 16);
-    pb8.y = (uint32_t)f2h(pr[2]) | ((uint32_t)f2h(pr[3]) << 16);
-    pb8.z = (uint32_t)f2h(pr[4]) | ((uint32_t)f2h(pr[5]) << 16);
-    pb8.w = (uint32_t)f2h(pr[6]) | ((uint32_t)f2h(pr[7]) << 16);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // this wave's V-tile stores landed
-#pragma unroll
-    for (int db = 0; db < 8; ++db) {                         // A = V^T: dim 16db + c16, slot 8q4+j
-      const int dcol = 16 * db + c16;
-      uint16_t h[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) h[j] = vt[(j < 4 ? 4 * q4 + j : 16 + 4 * q4 + j - 4)][dcol];
-      uint4 va;
-      va.x = h[0] | ((uint32_t)h[1] << 16);
-      va.y = h[2] | ((uint32_t)h[3] << 16);
-      va.z = h[4] | ((uint32_t)h[5] << 16);
-      va.w = h[6] | ((uint32_t)h[7] << 16);
-      o[db] = mfma16h(va, pb8, o[db]);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // V-tile reads done before reuse
-  };
-  while (tb < p1) {
-    const int tn = tb + tstep;
-    if (tn < p1) load_tile(tn, kB, vB);
-    tile(tb, kA, vA);
-    if (tn >= p1) break;
-    const int tn2 = tn + tstep;
-    if (tn2 < p1) load_tile(tn2, kA, vA);
-    tile(tn, kB, vB);
-    tb = tn2;
-  }
-  // ---- merge the 8 waves: per wave (m, sum, O^T) -> LDS, then one output per (head, dim)
-  l = sum4lanes(l);
-  __syncthreads();                                           // V tiles dead: reuse as merge area
-  if (q4 == 0 && c16 < 16) {
-    sh.mg.m[wave][c16] = m;
-    sh.mg.l[wave][c16] = l;
-  }
-  if (c16 < 8) {
-#pragma unroll
-    for (int db = 0; db < 8; ++db)
-      *reinterpret_cast<float4*>(&sh.mg.o[wave][c16][16 * db + 4 * q4]) =
-          make_float4(o[db][0], o[db][1], o[db][2], o[db][3]);
-  }
-  __syncthreads();
-  const int K = H * kHeadDim;
-  for (int idx = tid; idx < G * kHeadDim; idx += blockDim.x) {   // whole 32-dim groups per wave
-    const int g = idx >> 7, dd = idx & (kHeadDim - 1);
-    float M = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < kMWaves; ++w) M = fmaxf(M, sh.mg.m[w][g]);
-    float L = 0.f, O = 0.f;
-#pragma unroll
-    for (int w = 0; w < kMWaves; ++w) {
-      const float e = sh.mg.m[w][g] == -INFINITY ? 0.f : exp2f(sh.mg.m[w][g] - M);
-      L += sh.mg.l[w][g] * e;
-      O += sh.mg.o[w][g][dd] * e;
-    }
-    const int h = kh * G + g;
-    if (nsplit > 1) {                                        // partials for the combine kernel
-      a.po[(pidx + (long)g * nsplit) * kHeadDim + dd] = O;
-      if (dd == 0) {
-        a.pml[(pidx + (long)g * nsplit) * 2] = M * 0.6931471805599453f;   // natural-log units
-        a.pml[(pidx + (long)g * nsplit) * 2 + 1] = L;
-      }
-      continue;
-    }
-    const float y = L > 0.f ? O / L : 0.f;
-    const int col = h * kHeadDim + dd;
-    if (a.out) a.out[(long)t * K + col] = y;
-    float amax = fabsf(y);
-#pragma unroll
-    for (int o2 = 16; o2 > 0; o2 >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o2, kWave));
-    const float d = amax / 127.f;
-    const int qv = d > 0.f ? (int)__builtin_rintf(y / d) : 0;
-    a.x8[(long)t * K + col] = (int8_t)qv;
-    int s16 = qv;
-#pragma unroll
-    for (int o2 = 8; o2 > 0; o2 >>= 1) s16 += __shfl_xor(s16, o2, kWave);
-    if ((dd & 31) == 0) a.dx[(long)t * (K >> 5) + (col >> 5)] = d;
-    if ((dd & 15) == 0) a.sx[(long)t * (K >> 4) + (col >> 4)] = d * (float)s16;
+    dst[0] = mls[g][0];
+    dst[1] = mls[g][1];
   }
 }
 
@@ -1793,48 +1283,16 @@ int launch_one(const GemvArgs& a, int waves, hipStream_t st) {
 
 // Stage width U (super-blocks per lane per stage): the smallest that covers a row in one stage
 // (short rows), else the type/mode batch; register-resident activations when a row is one stage
-// and U*T <= 4 (VGPR budget).  Every variant runs the same dot_core, so the choice never changes
-// a result bit.
-// AMDK8S_LLM_REGX_T: largest T whose 2-block rows keep their activations in registers (default 2;
-// 4 trades ~50 VGPRs for no per-row LDS activation reads — A/B knob).
-static int regx_max_t() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("AMDK8S_LLM_REGX_T");
-    v = e ? atoi(e) : 2;
-  }
-  return v;
-}
-
-// Decode attention implementation: AMDK8S_LLM_ATTN=split (default: 64-position chunks on the VALU
-// + a combine launch) or mfma (attn_mfma_kernel: no combine launch up to kMChunk positions, but
-// one workgroup per kv head and token streams the whole context through one CU — 20.3 us against
-// 6.2 + 4.8 us for split + combine at 4 kv heads and ~600 positions, profiles/r03/aa).
-static int attn_impl_default() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("AMDK8S_LLM_ATTN");
-    v = (e && e[0] == 'm') ? 2 : 1;
-  }
-  return v;
-}
+// and T <= kRegxMaxT (VGPR budget; 4 measured slower, docs/experiments/llm_decode_rejected.md).
+// Every variant runs the same dot_core, so the choice never changes a result bit.
+constexpr int kRegxMaxT = 2;
 
 // Long rows (ffn_down: 74 super-blocks) in two balanced stages (U = ceil(nb / 16)) instead of
 // KB-wide ones: faster from T = 3 (T=3 / T=4 2.43 / 2.64 -> 2.39 / 2.60 ms, profiles/r03/ag); at
 // T = 1 faster for Q4_K rows (14.5 -> 13.5 us) and slower for Q6_K ones (13.8 -> 17.1 us; step
-// 1.740 -> 1.721 ms with Q4_K only, profiles/r03/ap), so Q4_K always, Q6_K from T = 3.
-// AMDK8S_LLM_LONGROW=0 / 1
-// forces it off / on for every T; q4 / q6 force it on for that type only (the other keeps the
-// default).  The stage width never changes a result bit.
-static bool longrow_enabled(int type, int T) {
-  static int v = -2;
-  if (v == -2) {
-    const char* e = getenv("AMDK8S_LLM_LONGROW");
-    v = !e ? -1 : e[0] == 'q' ? (e[1] == '4' ? 10 : 11) : (e[0] == '1');
-  }
-  if (v >= 10) return v - 10 == type || T >= 3;
-  return v < 0 ? (type == 0 || T >= 3) : v != 0;
-}
+// 1.740 -> 1.721 ms with Q4_K only, profiles/r03/ap), so Q4_K always, Q6_K from T = 3.  The stage
+// width never changes a result bit.
+static bool longrow_enabled(int type, int T) { return type == kQ4K || T >= 3; }
 
 template <int TYPE, int T, int MODE>
 int launch_gemv(const GemvArgs& a, int waves, hipStream_t st) {
@@ -1844,7 +1302,7 @@ int launch_gemv(const GemvArgs& a, int waves, hipStream_t st) {
   if constexpr (KB >= 2) {
     if (nb <= 16) {
       if constexpr (T <= 2) return launch_one<TYPE, T, MODE, 2, true>(a, waves, st);
-      else if (T <= regx_max_t()) return launch_one<TYPE, T, MODE, 2, true>(a, waves, st);
+      else if (T <= kRegxMaxT) return launch_one<TYPE, T, MODE, 2, true>(a, waves, st);
       else return launch_one<TYPE, T, MODE, 2, false>(a, waves, st);
     }
   }
@@ -1886,7 +1344,7 @@ int launch_gemv2(const GemvArgs& a0, const GemvArgs& a1, int waves, hipStream_t 
   };
   if (nb <= 8) return go(qgemv2_kernel<TYPE0, TYPE1, T, 1, true>);
   if (nb <= 16) {
-    if (T <= 2 || T <= regx_max_t()) return go(qgemv2_kernel<TYPE0, TYPE1, T, 2, true>);
+    if (T <= kRegxMaxT) return go(qgemv2_kernel<TYPE0, TYPE1, T, 2, true>);
     return go(qgemv2_kernel<TYPE0, TYPE1, T, 2, false>);
   }
   return 4;
@@ -1921,34 +1379,6 @@ void gemv_shape(int type, int N, int K, int T, int& waves, int& rows) {
 
 }  // namespace
 
-// ---------------------------------------------------------------- Infinity-Cache prefetch
-// Streams up to 8 byte ranges through the memory hierarchy with ordinary (allocating) loads so the
-// next GEMV finds its weights in the 256 MB MALL: launched on a side stream while the latency-bound
-// small kernels (q|k|v, attention, combine, o_proj) leave HBM idle.  The loaded values feed a
-// never-true store condition (the loads cannot be dropped); nothing is written.
-struct PrefetchArgs {
-  const uint4* p[8];
-  long n16[8];              // 16-B units per range
-  int nr;
-  int* sink;
-};
-
-__global__ void __launch_bounds__(256) prefetch_kernel(PrefetchArgs a) {
-  uint32_t acc = 0;
-  const long stride = (long)gridDim.x * blockDim.x;
-  for (int r = 0; r < a.nr; ++r) {
-    const uint4* p = a.p[r];
-    const long n = a.n16[r];
-    long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n; i += 4 * stride) {      // 4 loads in flight per thread
-      const uint4 v0 = p[i], v1 = p[i + stride], v2 = p[i + 2 * stride], v3 = p[i + 3 * stride];
-      acc ^= v0.x ^ v1.y ^ v2.z ^ v3.w;
-    }
-    for (; i < n; i += stride) acc ^= p[i].x;
-  }
-  if (acc == 0x9e3779b9u && a.sink) a.sink[threadIdx.x] = (int)acc;
-}
-
 extern "C" {
 
 int amdk8s_llm_max_tokens() { return kMaxTok; }
@@ -1962,24 +1392,12 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
                      const void* w1d, const void* x8, const void* dx, const void* sx,
                      const void* xf, int ldx, const void* norm_w, float eps,
                      const void* bias, void* out, int ldo, int N, int K, int T, int waves,
-                     int rows_per_wg, void* ox8, void* odx, void* osx, const void* res,
-                     const void* onorm_w, void* cnt, void* stream) {
+                     int rows_per_wg, void* ox8, void* odx, void* osx, void* stream) {
   if (K % 256 || N <= 0 || T < 1 || T > kMaxTok) return 2;
   if (mode == kPair && !w1q) return 2;
-  if (cnt) {                                  // resid + fused RMSNorm/Q8 of the new residual
-    if (mode != kResid || !res || res == out || !onorm_w || !ox8 || !odx || !osx) return 2;
-    if (N % 256 || N > kNormCh * 256 * 8 || ldo < N) return 2;
-  } else if (ox8) {                           // pair → Q8 output: whole 32-row blocks per workgroup
+  if (ox8) {                                  // pair → Q8 output: whole 32-row blocks per workgroup
     if (mode != kPair || N % 32 || !odx || !osx) return 2;
-    rows_per_wg = 32;
-    if (waves <= 0) {                         // AMDK8S_LLM_PAIR_WAVES: waves sharing the 32 rows
-      static int pw = -1;
-      if (pw < 0) {
-        const char* e = getenv("AMDK8S_LLM_PAIR_WAVES");
-        pw = e ? atoi(e) : 0;
-      }
-      waves = pw;
-    }
+    rows_per_wg = 32;                         // 4 waves share them (8 and 2 measured slower)
   }
   gemv_shape(type, N, K, T, waves, rows_per_wg);
   if (ox8 && waves * 64 < 32 * T) return 2;
@@ -2004,9 +1422,6 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
   a.ox8 = static_cast<int8_t*>(ox8);
   a.odx = static_cast<float*>(odx);
   a.osx = static_cast<float*>(osx);
-  a.res = static_cast<const float*>(res);
-  a.onorm_w = static_cast<const float*>(onorm_w);
-  a.cnt = static_cast<int*>(cnt);
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (type == kQ4K) {
     if (mode == kStore) return dispatch_t<kQ4K, kStore>(a, waves, st);
@@ -2065,35 +1480,6 @@ int amdk8s_llm_qgemv2(int type0, const void* w0q, const void* w0qh, const void* 
   return dispatch2_t<kQ6K, kQ6K>(a[0], a[1], waves, st);
 }
 
-// o_proj with the attention combine in its prologue: out[t][n] += W.y_t where y_t is merged from
-// the decode-attention partials po / pml (written by amdk8s_llm_attn_decode with x8 = null, split
-// kernel) — the combine launch disappears.  K = heads * 128.
-int amdk8s_llm_qgemv_attn(int type, const void* wq, const void* wqh, const void* wsc,
-                          const void* wd, const void* po, const void* pml, const void* pos,
-                          int nsplit, int chunk, void* out, int ldo, int N, int K, int T,
-                          int waves, int rows_per_wg, void* stream) {
-  if (K % 256 || N <= 0 || T < 1 || T > kMaxTok || !po || !pml || !pos || nsplit < 1 ||
-      chunk < 1)
-    return 2;
-  if (waves <= 0) waves = 8;
-  if (rows_per_wg <= 0) rows_per_wg = 16;
-  if (waves > 8 || rows_per_wg < 1) return 2;
-  GemvArgs a = GemvArgs{};
-  a.w0 = {static_cast<const uint8_t*>(wq), static_cast<const uint8_t*>(wqh),
-          static_cast<const int8_t*>(wsc), static_cast<const uint16_t*>(wd)};
-  a.out = static_cast<float*>(out);
-  a.ldo = ldo; a.N = N; a.K = K; a.T = T; a.rows_per_wg = rows_per_wg;
-  a.po = static_cast<const float*>(po);
-  a.pml = static_cast<const float*>(pml);
-  a.apos = static_cast<const int*>(pos);
-  a.nsplit = nsplit;
-  a.chunk = chunk;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  if (type == kQ4K) return dispatch_t<kQ4K, kResid>(a, waves, st);
-  if (type == kQ6K) return dispatch_t<kQ6K, kResid>(a, waves, st);
-  return 2;
-}
-
 int amdk8s_llm_argmax_rows(const void* x, int V, long ld, int T, void* out, void* stream) {
   if (V < 1 || T < 1 || ld < V || ((uintptr_t)x & 15) || (ld & 3)) return 2;
   hipLaunchKernelGGL(argmax_rows_kernel, dim3(T), dim3(1024), 0, static_cast<hipStream_t>(stream),
@@ -2132,23 +1518,18 @@ int amdk8s_llm_rope_kv(const void* qkv, int ldq, const void* pos, const void* sl
 // caller buckets it so a captured graph does not launch empty chunks up to max_ctx.
 // qkv (nullable): the raw q|k|v projection [T][ldq] — fused RoPE + KV write (distinct slots
 // only, see attn_decode_kernel); q is then unused.
-// cnt (nullable): [T][Hkv] int32 arrival counters, zero-initialised once by the caller and left
-// zero by every launch: the combine runs inside the attention kernel (no second launch).
 int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* cos_t,
                            const void* sin_t, const void* pos, const void* slot, void* kc,
                            void* vc, int H, int Hkv, int head_dim, int max_ctx, int span,
                            float scale, void* po, void* pml, void* out, void* x8, void* dx,
-                           void* sx, int T, void* cnt, int impl, void* stream) {
+                           void* sx, int T, void* stream) {
   if (span <= 0) span = max_ctx;
   if (head_dim != kHeadDim || H % Hkv || H / Hkv > kMaxGroup || max_ctx % kAttnChunk ||
       span % kAttnChunk || span > max_ctx || T < 1)
     return 2;
   if (!qkv && !q) return 2;
   if (qkv && (!cos_t || !sin_t)) return 2;
-  if (impl == 0) impl = attn_impl_default();
-  if (impl == 2 && cnt) return 2;        // the in-launch combine is a split-kernel form only
-  if (impl == 2 && !(x8 && dx && sx)) return 2;   // MFMA: writes the Q8 output itself
-  if (cnt && !(x8 && dx && sx)) return 2;
+  if (!(x8 && dx && sx)) return 2;
   hipStream_t st = static_cast<hipStream_t>(stream);
   AttnArgs aa{};
   aa.q = static_cast<const float*>(q);
@@ -2163,11 +1544,6 @@ int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* 
   aa.H = H; aa.Hkv = Hkv; aa.max_ctx = max_ctx; aa.scale = scale;
   aa.po = static_cast<float*>(po);
   aa.pml = static_cast<float*>(pml);
-  aa.cnt = static_cast<int*>(cnt);
-  aa.out = static_cast<float*>(out);
-  aa.x8 = static_cast<int8_t*>(x8);
-  aa.dx = static_cast<float*>(dx);
-  aa.sx = static_cast<float*>(sx);
   // the GQA group size is a template parameter: fully unrolled head loops, no per-head branches
   auto by_group = [&](auto launch) -> int {
     switch (H / Hkv) {
@@ -2183,27 +1559,15 @@ int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* 
     }
     return hipGetLastError() == hipSuccess ? 0 : 1;
   };
-  int chunk = kAttnChunk;
-  if (impl == 2) {                       // MFMA: one workgroup per kMChunk positions
-    chunk = span <= kMChunk ? span : kMChunk;
-    aa.nsplit = (span + chunk - 1) / chunk;
-    const int rc = by_group([&](auto g) {
-      hipLaunchKernelGGL(attn_mfma_kernel<decltype(g)::value>, dim3(Hkv, aa.nsplit, T), dim3(512),
-                         0, st, aa, chunk);
-    });
-    if (rc || aa.nsplit == 1) return rc;   // one split: normalised Q8 output written in-kernel
-  } else {
-    aa.nsplit = span / kAttnChunk;
-    const int rc = by_group([&](auto g) {
-      hipLaunchKernelGGL(attn_decode_kernel<decltype(g)::value>, dim3(Hkv, aa.nsplit, T),
-                         dim3(256), 0, st, aa);
-    });
-    if (rc || cnt) return rc;            // in-kernel combine
-    if (!x8) return rc;                  // partials only: the o_proj prologue merges them
-  }
+  aa.nsplit = span / kAttnChunk;
+  const int rc = by_group([&](auto g) {
+    hipLaunchKernelGGL(attn_decode_kernel<decltype(g)::value>, dim3(Hkv, aa.nsplit, T), dim3(256), 0,
+                       st, aa);
+  });
+  if (rc) return rc;
   hipLaunchKernelGGL(attn_combine_q8_kernel, dim3(H, T), dim3(128), 0, st,
                      static_cast<const float*>(po), static_cast<const float*>(pml),
-                     static_cast<const int*>(pos), H, aa.nsplit, chunk, static_cast<float*>(out),
+                     static_cast<const int*>(pos), H, aa.nsplit, kAttnChunk, static_cast<float*>(out),
                      static_cast<int8_t*>(x8), static_cast<float*>(dx), static_cast<float*>(sx));
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
@@ -2252,21 +1616,5 @@ int amdk8s_llm_q6k_repack(const void* src, long nblocks, void* ql, void* qh, voi
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
-
-// Prefetch up to 8 ranges (ptrs[i], bytes[i]; 16-B aligned, bytes % 16 == 0) with `wgs`
-// workgroups on `stream`.
-int amdk8s_llm_prefetch(const void* const* ptrs, const long* bytes, int n, int wgs, void* stream) {
-  if (n < 0 || n > 8 || wgs <= 0) return 2;
-  PrefetchArgs a{};
-  for (int i = 0; i < n; ++i) {
-    if (((uintptr_t)ptrs[i] & 15) || (bytes[i] & 15)) return 2;
-    a.p[i] = static_cast<const uint4*>(ptrs[i]);
-    a.n16[i] = bytes[i] / 16;
-  }
-  a.nr = n;
-  a.sink = nullptr;
-  hipLaunchKernelGGL(prefetch_kernel, dim3(wgs), dim3(256), 0, static_cast<hipStream_t>(stream), a);
-  return hipGetLastError() == hipSuccess ? 0 : 1;
-}
 
 }  // extern "C"

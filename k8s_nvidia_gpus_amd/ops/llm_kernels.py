@@ -29,15 +29,11 @@ def _lib():
             lib.amdk8s_llm_max_tokens.restype = ci
             lib.amdk8s_llm_attn_chunk.restype = ci
             lib.amdk8s_llm_qgemv.argtypes = [ci, ci] + [vp] * 8 + [vp, vp, vp] \
-                + [vp, ci, vp, cf] + [vp, vp] + [ci, ci, ci, ci, ci, ci] + [vp, vp, vp] \
-                + [vp, vp, vp] + [vp]
+                + [vp, ci, vp, cf] + [vp, vp] + [ci, ci, ci, ci, ci, ci] + [vp, vp, vp] + [vp]
             lib.amdk8s_llm_qgemv.restype = ci
             lib.amdk8s_llm_qgemv2.argtypes = [ci] + [vp] * 4 + [ci, vp, vp] + [ci] + [vp] * 4 \
                 + [ci, vp, vp] + [ci, vp, vp, vp, vp, ci, vp, cf, ci, ci, ci, ci, vp]
             lib.amdk8s_llm_qgemv2.restype = ci
-            lib.amdk8s_llm_qgemv_attn.argtypes = [ci] + [vp] * 4 + [vp, vp, vp, ci, ci, vp, ci, ci,
-                                                                  ci, ci, ci, ci, vp]
-            lib.amdk8s_llm_qgemv_attn.restype = ci
             lib.amdk8s_llm_argmax_rows.argtypes = [vp, ci, cl, ci, vp, vp]
             lib.amdk8s_llm_argmax_rows.restype = ci
             lib.amdk8s_llm_rmsnorm_q8.argtypes = [vp, vp, cf, ci, ci, vp, vp, vp, vp]
@@ -46,8 +42,7 @@ def _lib():
                                                ci, vp]
             lib.amdk8s_llm_rope_kv.restype = ci
             lib.amdk8s_llm_attn_decode.argtypes = [vp, vp, ci, vp, vp, vp, vp, vp, vp, ci, ci, ci,
-                                                   ci, ci, cf, vp, vp, vp, vp, vp, vp, ci, vp, ci,
-                                                   vp]
+                                                   ci, ci, cf, vp, vp, vp, vp, vp, vp, ci, vp]
             lib.amdk8s_llm_attn_decode.restype = ci
             lib.amdk8s_llm_dequant.argtypes = [ci, vp, vp, vp, vp, vp, ci, ci, vp, ci, vp]
             lib.amdk8s_llm_dequant.restype = ci
@@ -63,8 +58,6 @@ def _lib():
             lib.amdk8s_llm_rope_kv_f16.restype = ci
             lib.amdk8s_llm_swiglu_f16.argtypes = [vp, ci, ci, vp, vp]
             lib.amdk8s_llm_swiglu_f16.restype = ci
-            lib.amdk8s_llm_prefetch.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(cl), ci, ci, vp]
-            lib.amdk8s_llm_prefetch.restype = ci
             _declared = True
     return lib
 
@@ -92,16 +85,13 @@ def attn_chunk() -> int:
 
 def qgemv(w0, x8, dx, sx, out, mode: int = STORE, w1=None, bias=None, ldo: int = None,
           rows_per_wg: int = 0, waves: int = 0, xf=None, norm_w=None, eps: float = 1e-6,
-          q8_out=None, res=None, norm_out=None, cnt=None) -> None:
+          q8_out=None) -> None:
     """``w0``/``w1``: :class:`~k8s_nvidia_gpus_amd.models.llm.weights.QWeight` on the GPU.
     Input: Q8 activations (``x8``/``dx``/``sx``, [T, K]) or fp32 rows ``xf`` [T, K] (pass
     ``x8=dx=sx=None``) that the kernel quantises itself, after an RMSNorm when ``norm_w`` is given.
     ``out`` fp32 [T, ldo] (a view with row stride ``ldo``).  ``waves`` per workgroup and
     ``rows_per_wg``: 0 = the kernel's default decomposition.  ``q8_out`` = (x8, dx, sx) [T, N]
-    (pair mode only): write silu(g)·u quantised to Q8 — the ffn_down input — instead of ``out``.
-    Resid mode with ``cnt`` (int32 [1] zeros, left zero): ``out = res + W.x`` (``out`` a different
-    buffer than ``res``), and the launch's last workgroup RMS-normalises ``out`` with ``norm_out``
-    and writes it as Q8 into ``q8_out`` — the next GEMV's input, without a norm launch."""
+    (pair mode only): write silu(g)·u quantised to Q8 — the ffn_down input — instead of ``out``."""
     t = (xf if xf is not None else x8).shape[0]
     ldo = out.stride(0) if ldo is None else ldo
     a = w0.ptrs()
@@ -111,7 +101,7 @@ def qgemv(w0, x8, dx, sx, out, mode: int = STORE, w1=None, bias=None, ldo: int =
                                    xf.stride(0) if xf is not None else 0, _p(norm_w), float(eps),
                                    _p(bias), out.data_ptr(), ldo, w0.n, w0.k, t,
                                    waves, rows_per_wg, *((_p(t) for t in q8_out) if q8_out else (None,) * 3),
-                                   _p(res), _p(norm_out), _p(cnt), _stream(ref)), "amdk8s_llm_qgemv")
+                                   _stream(ref)), "amdk8s_llm_qgemv")
 
 
 def qgemv2(w0, w1, x8, dx, sx, out0, out1, bias0=None, bias1=None, rows_per_wg: int = 0,
@@ -133,19 +123,6 @@ def qgemv2(w0, w1, x8, dx, sx, out0, out1, bias0=None, bias1=None, rows_per_wg: 
         return False
     _check(rc, "amdk8s_llm_qgemv2")
     return True
-
-
-def qgemv_attn(w, po, pml, pos, nsplit: int, out, rows_per_wg: int = 0, waves: int = 0,
-               chunk: int = 0) -> None:
-    """``out[t] += W . y_t`` (resid mode) where y_t, the decode-attention output of token t, is
-    merged from the per-chunk partials ``po`` [T, H, >= nsplit, 128] / ``pml`` [T, H, >= nsplit, 2]
-    (row stride ``nsplit``, as written by :func:`attn_decode` without Q8 outputs) in the GEMV's
-    prologue: no combine launch.  ``chunk``: context positions per partial (0 = attn_chunk())."""
-    t = pos.shape[0]
-    _check(_lib().amdk8s_llm_qgemv_attn(w.qtype, *w.ptrs(), po.data_ptr(), pml.data_ptr(),
-                                        pos.data_ptr(), nsplit, chunk or attn_chunk(),
-                                        out.data_ptr(), out.stride(0), w.n, w.k, t, waves,
-                                        rows_per_wg, _stream(out)), "amdk8s_llm_qgemv_attn")
 
 
 def argmax_rows(x, out) -> None:
@@ -171,32 +148,23 @@ def rope_kv(qkv, pos, slot, cos_t, sin_t, heads: int, kv_heads: int, head_dim: i
            "amdk8s_llm_rope_kv")
 
 
-ATTN_DEFAULT, ATTN_SPLIT, ATTN_MFMA = 0, 1, 2
-
-
 def attn_decode(q, pos, slot, kc, vc, heads: int, kv_heads: int, head_dim: int, max_ctx: int,
                 scale: float, po, pml, x8, dx, sx, out=None, span: int = 0, qkv=None,
-                cos_t=None, sin_t=None, cnt=None, impl: int = ATTN_DEFAULT) -> None:
+                cos_t=None, sin_t=None) -> None:
     """Split-context decode attention + combine + Q8 quantisation of the output.
 
     ``span``: context positions this call covers (multiple of ``attn_chunk()``, above every
     position; 0 = ``max_ctx``).  With ``qkv`` (the raw q|k|v projection) and the RoPE tables, the
     kernel also rotates q/k and writes the new K/V itself (``q`` unused, pass None) — only when
-    every token of the step is in a distinct slot.  ``cnt``: int32 [T, kv_heads] zeros (kept zero
-    by every call) — the combine then runs inside the attention kernel, one launch instead of two
-    (split kernel only).  ``impl``: ATTN_SPLIT (64-position chunks + combine), ATTN_MFMA (one
-    workgroup per 1024 positions on MFMA, no combine launch up to 1024) or ATTN_DEFAULT
-    (AMDK8S_LLM_ATTN: split unless it says ``mfma``).  ``x8 = dx = sx = None`` (split kernel):
-    only the per-chunk partials ``po`` / ``pml`` are written — :func:`qgemv_attn` merges them."""
-    if cnt is not None and impl == ATTN_DEFAULT:
-        impl = ATTN_SPLIT
+    every token of the step is in a distinct slot.  ``po`` / ``pml``: per-chunk partials
+    (workspace); the combine launch merges them and writes the Q8 o_proj input x8 / dx / sx."""
     ref = qkv if qkv is not None else q
     _check(_lib().amdk8s_llm_attn_decode(_p(q), _p(qkv), qkv.stride(0) if qkv is not None else 0,
                                          _p(cos_t), _p(sin_t), pos.data_ptr(), slot.data_ptr(),
                                          kc.data_ptr(), vc.data_ptr(), heads, kv_heads, head_dim,
                                          max_ctx, span, float(scale), po.data_ptr(), pml.data_ptr(),
                                          _p(out), _p(x8), _p(dx), _p(sx),
-                                         ref.shape[0], _p(cnt), int(impl), _stream(ref)),
+                                         ref.shape[0], _stream(ref)),
            "amdk8s_llm_attn_decode")
 
 
@@ -220,20 +188,6 @@ def q4k_repack(raw, qs, scm, dm) -> None:
     _check(_lib().amdk8s_llm_q4k_repack(raw.data_ptr(), raw.numel() // 144, qs.data_ptr(),
                                         scm.data_ptr(), dm.data_ptr(), _stream(raw)),
            "amdk8s_llm_q4k_repack")
-
-
-def prefetch(tensors, wgs: int = 32, stream=None) -> None:
-    """Read ``tensors`` (16-B aligned, sizes % 16 == 0; at most 8) through the cache hierarchy on
-    ``stream`` (default: current) so a following kernel finds them in the Infinity Cache."""
-    ts = [t for t in tensors if t is not None]
-    if not ts:
-        return
-    if len(ts) > 8:
-        raise ValueError("prefetch: at most 8 ranges")
-    ptrs = (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
-    sizes = (ctypes.c_long * len(ts))(*[(t.numel() * t.element_size()) // 16 * 16 for t in ts])
-    st = (stream or torch.cuda.current_stream(ts[0].device)).cuda_stream
-    _check(_lib().amdk8s_llm_prefetch(ptrs, sizes, len(ts), wgs, st), "amdk8s_llm_prefetch")
 
 
 # ---------------------------------------------------------------------- prompt prefill (llm_prefill.hip)

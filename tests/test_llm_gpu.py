@@ -210,9 +210,8 @@ def _attn_ref(q, kc, vc, pos, slot, H, Hkv):
     return torch.stack(outs)
 
 
-@pytest.mark.parametrize("impl", [1, 2])             # split (VALU + combine) / MFMA
 @pytest.mark.parametrize("H,Hkv", [(28, 4), (8, 8), (16, 2)])
-def test_rope_kv_and_decode_attention(dev, LK, H, Hkv, impl):
+def test_rope_kv_and_decode_attention(dev, LK, H, Hkv):
     from k8s_nvidia_gpus_amd.models.llm.engine import apply_rope, rope_tables
 
     torch.manual_seed(H + Hkv)
@@ -246,16 +245,15 @@ def test_rope_kv_and_decode_attention(dev, LK, H, Hkv, impl):
     sx = torch.empty(T, H * 8, device=dev)
     out = torch.empty(T, H * 128, device=dev)
     LK.attn_decode(qrot, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po, pml,
-                   x8, dx, sx, out=out, impl=impl)
+                   x8, dx, sx, out=out)
     ref = _attn_ref(qrot, kc, vc, pos, slot, H, Hkv)
-    torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-3 if impl == 1 else 2e-3)
+    torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-3)
     xq = (x8.float().view(T, -1, 32) * dx[..., None]).view(T, -1)
     assert ((xq - out).abs() <= dx.repeat_interleave(32, 1) * 0.5 + 1e-5).all()
 
 
-@pytest.mark.parametrize("impl", [1, 2])
 @pytest.mark.parametrize("H,Hkv", [(28, 4), (8, 8)])
-def test_fused_rope_attention_equals_separate_kernels(dev, LK, H, Hkv, impl):
+def test_fused_rope_attention_equals_separate_kernels(dev, LK, H, Hkv):
     """Distinct slots: RoPE + KV write inside the attention kernel == rope_kv + attention."""
     from k8s_nvidia_gpus_amd.models.llm.engine import rope_tables
 
@@ -279,50 +277,15 @@ def test_fused_rope_attention_equals_separate_kernels(dev, LK, H, Hkv, impl):
         out = torch.empty(T, H * 128, device=dev)
         if fused:
             LK.attn_decode(None, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po,
-                           pml, x8, dx, sx, out=out, qkv=qkv, cos_t=cos, sin_t=sin, impl=impl)
+                           pml, x8, dx, sx, out=out, qkv=qkv, cos_t=cos, sin_t=sin)
         else:
             qrot = torch.empty(T, H * 128, device=dev)
             LK.rope_kv(qkv, pos, slot, cos, sin, H, Hkv, 128, max_ctx, qrot, kc, vc)
             LK.attn_decode(qrot, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po,
-                           pml, x8, dx, sx, out=out, impl=impl)
+                           pml, x8, dx, sx, out=out)
         outs.append((kc, vc, out))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     torch.testing.assert_close(outs[1][2], outs[0][2], rtol=1e-5, atol=1e-5)
-
-
-@pytest.mark.parametrize("span", [2048, 4096])
-def test_mfma_attention_long_context_splits(dev, LK, span):
-    """MFMA decode attention past one 1024-position workgroup: per-split partials + the combine
-    kernel (chunk 1024) against the fp32 reference, fused RoPE / KV write included; positions
-    on both sides of split boundaries."""
-    from k8s_nvidia_gpus_amd.models.llm.engine import apply_rope, rope_tables
-
-    torch.manual_seed(11)
-    H, Hkv, max_ctx, slots, T = 28, 4, 4096, 4, 4
-    kc = (torch.randn(slots, Hkv, max_ctx, 128, device=dev) * 0.5).half()
-    vc = torch.randn(slots, Hkv, max_ctx, 128, device=dev).half()
-    cos, sin = rope_tables(max_ctx, 128, 1.0e6, dev)
-    top = span - 1
-    pos = torch.tensor([1023, 1024, 1500, top], dtype=torch.int32, device=dev)
-    slot = torch.tensor([1, 3, 0, 2], dtype=torch.int32, device=dev)
-    qkv = torch.randn(T, (H + 2 * Hkv) * 128, device=dev)
-    nsplit = max_ctx // LK.attn_chunk()
-    po = torch.empty(T, H, nsplit, 128, device=dev)
-    pml = torch.empty(T, H, nsplit, 2, device=dev)
-    x8 = torch.empty(T, H * 128, dtype=torch.int8, device=dev)
-    dx = torch.empty(T, H * 4, device=dev)
-    sx = torch.empty(T, H * 8, device=dev)
-    out = torch.empty(T, H * 128, device=dev)
-    kref, vref = kc.clone(), vc.clone()
-    LK.attn_decode(None, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po, pml,
-                   x8, dx, sx, out=out, span=span, qkv=qkv, cos_t=cos, sin_t=sin, impl=2)
-    qrot = torch.empty(T, H * 128, device=dev)
-    LK.rope_kv(qkv, pos, slot, cos, sin, H, Hkv, 128, max_ctx, qrot, kref, vref)
-    assert torch.equal(kc, kref) and torch.equal(vc, vref)
-    ref = _attn_ref(qrot, kref, vref, pos, slot, H, Hkv)
-    torch.testing.assert_close(out, ref, rtol=1e-3, atol=2e-3)
-    xq = (x8.float().view(T, -1, 32) * dx[..., None]).view(T, -1)
-    assert ((xq - out).abs() <= dx.repeat_interleave(32, 1) * 0.5 + 1e-5).all()
 
 
 @pytest.mark.parametrize("T", [1, 4])
@@ -367,118 +330,6 @@ def test_prologue_norm_equals_rmsnorm_kernel(dev, LK, K, T):
     torch.testing.assert_close(a, b, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("T", [1, 4])
-def test_oproj_prologue_combine(dev, LK, T):
-    """o_proj with the attention combine in its prologue (qgemv_attn over the split kernel's
-    partials) against the combine kernel's Q8 output fed to the plain resid GEMV: the same
-    result up to single int8 roundings of the activations."""
-    from k8s_nvidia_gpus_amd.models.llm import gguf
-
-    torch.manual_seed(30 + T)
-    H, Hkv, max_ctx, slots = 28, 4, 1024, 4
-    kc = (torch.randn(slots, Hkv, max_ctx, 128, device=dev) * 0.5).half()
-    vc = torch.randn(slots, Hkv, max_ctx, 128, device=dev).half()
-    pos = torch.tensor([600, 63, 64, 1000][:T], dtype=torch.int32, device=dev)
-    slot = torch.tensor([1, 0, 3, 2][:T], dtype=torch.int32, device=dev)
-    q = torch.randn(T, H * 128, device=dev)
-    nsplit = max_ctx // LK.attn_chunk()
-    po = torch.empty(T, H, nsplit, 128, device=dev)
-    pml = torch.empty(T, H, nsplit, 2, device=dev)
-    x8 = torch.empty(T, H * 128, dtype=torch.int8, device=dev)
-    dx = torch.empty(T, H * 4, device=dev)
-    sx = torch.empty(T, H * 8, device=dev)
-    w, wref = _qw(3584, H * 128, gguf.Q4_K, 15, dev)
-    res = torch.randn(T, 3584, device=dev)
-    LK.attn_decode(q, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po, pml,
-                   x8, dx, sx, impl=LK.ATTN_SPLIT)
-    ref = res.clone()
-    LK.qgemv(w, x8, dx, sx, ref, LK.RESID)
-    po2 = torch.empty_like(po)
-    pml2 = torch.empty_like(pml)
-    LK.attn_decode(q, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po2, pml2,
-                   None, None, None, impl=LK.ATTN_SPLIT)
-    out = res.clone()
-    LK.qgemv_attn(w, po2, pml2, pos, nsplit, out)
-    scale = (ref - res).abs().max().item()
-    torch.testing.assert_close(out, ref, rtol=0, atol=2e-2 * scale)
-    y = _attn_ref(q, kc, vc, pos, slot, H, Hkv)
-    full = res + (y.cpu() @ wref.t()).to(dev)
-    torch.testing.assert_close(out, full, rtol=0, atol=5e-2 * scale)
-
-
-@pytest.mark.parametrize("H,Hkv", [(28, 4), (8, 8), (6, 2)])
-def test_in_kernel_combine_equals_combine_kernel(dev, LK, H, Hkv):
-    """The last-arriving workgroup's chunk merge (cnt given) is bit-identical to the separate
-    combine kernel, leaves the arrival counters at zero, and stays so over repeated launches."""
-    torch.manual_seed(5)
-    max_ctx, slots, T = 1024, 4, 4
-    kc = (torch.randn(slots, Hkv, max_ctx, 128, device=dev) * 0.5).half()
-    vc = torch.randn(slots, Hkv, max_ctx, 128, device=dev).half()
-    pos = torch.tensor([0, 63, 64, 1000], dtype=torch.int32, device=dev)
-    slot = torch.tensor([3, 0, 1, 2], dtype=torch.int32, device=dev)
-    q = torch.randn(T, H * 128, device=dev)
-    nsplit = max_ctx // LK.attn_chunk()
-    cnt = torch.zeros(T * Hkv, dtype=torch.int32, device=dev)
-    res = []
-    for use_cnt in (False, True, True):
-        po = torch.empty(T, H, nsplit, 128, device=dev)
-        pml = torch.empty(T, H, nsplit, 2, device=dev)
-        x8 = torch.empty(T, H * 128, dtype=torch.int8, device=dev)
-        dx = torch.empty(T, H * 4, device=dev)
-        sx = torch.empty(T, H * 8, device=dev)
-        out = torch.empty(T, H * 128, device=dev)
-        LK.attn_decode(q, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po, pml,
-                       x8, dx, sx, out=out, cnt=cnt if use_cnt else None,
-                       impl=LK.ATTN_SPLIT)
-        torch.cuda.synchronize()
-        res.append((x8, dx, sx, out))
-        assert int(cnt.abs().sum()) == 0
-    for a, b in zip(res[0], res[1]):
-        assert torch.equal(a, b)
-    for a, b in zip(res[1], res[2]):
-        assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("qt", ["Q4_K", "Q6_K"])
-@pytest.mark.parametrize("T", [1, 3, 4])
-def test_resid_gemv_fused_norm_tail(dev, LK, qt, T):
-    """Resid GEMV with the fused RMSNorm tail (cnt given): out = res + W.x bit-identical to the
-    in-place resid GEMV; the last workgroup's Q8 of RMSNorm(out) matches rmsnorm_q8 of the same
-    rows (same scales, int8 within one step); the arrival counter is left at zero, launch after
-    launch (448 workgroups arriving on one counter)."""
-    from k8s_nvidia_gpus_amd.models.llm import gguf
-
-    t = getattr(gguf, qt)
-    N, K = 3584, 1536
-    w, _ = _qw(N, K, t, 6, dev)
-    torch.manual_seed(10 + T)
-    x = torch.randn(T, K, device=dev)
-    x8, dx, sx, _ = _q8(x, LK)
-    res = torch.randn(T, N, device=dev)
-    nw = torch.rand(N, device=dev) + 0.5
-    ref = res.clone()
-    LK.qgemv(w, x8, dx, sx, ref, LK.RESID)
-    r8 = torch.empty(T, N, dtype=torch.int8, device=dev)
-    rdx = torch.empty(T, N // 32, device=dev)
-    rsx = torch.empty(T, N // 16, device=dev)
-    LK.rmsnorm_q8(ref, nw, 1e-6, r8, rdx, rsx)
-    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-    for _ in range(3):
-        out = torch.full((T, N), float("nan"), device=dev)
-        o8 = torch.empty(T, N, dtype=torch.int8, device=dev)
-        odx = torch.empty(T, N // 32, device=dev)
-        osx = torch.empty(T, N // 16, device=dev)
-        LK.qgemv(w, x8, dx, sx, out, LK.RESID, res=res, norm_out=nw, q8_out=(o8, odx, osx),
-                 cnt=cnt, eps=1e-6)
-        torch.cuda.synchronize()
-        assert int(cnt.item()) == 0
-        assert torch.equal(out, ref)
-        torch.testing.assert_close(odx, rdx, rtol=1e-5, atol=0)
-        assert int((o8.int() - r8.int()).abs().max()) <= 1
-        sums = o8.float().view(T, N // 16, 16).sum(-1) * odx.repeat_interleave(2, -1)
-        torch.testing.assert_close(osx, sums, rtol=1e-5, atol=1e-5)
-
-
 @pytest.mark.parametrize("types", [("Q4_K", "Q6_K"), ("Q6_K", "Q4_K")])
 @pytest.mark.parametrize("T", [1, 2, 3, 4])
 @pytest.mark.parametrize("K", [1536, 3584])
@@ -511,16 +362,12 @@ def tiny_gguf(tmp_path_factory):
     return write_synthetic_gguf(str(p), tiny(layers=4, dim=512, heads=4, kv_heads=2, ffn=1024))
 
 
-@pytest.mark.parametrize("resid_norm,norm_prologue,attn_prologue",
-                         [(False, False, False), (True, False, False), (False, True, False),
-                          (False, True, True)])
-def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf, resid_norm, norm_prologue,
-                                                     attn_prologue):
+@pytest.mark.parametrize("norm_prologue", [False, True])
+def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf, norm_prologue):
     from k8s_nvidia_gpus_amd.models.llm.synthetic import load
 
     gpu, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=False)
-    gpu.resid_norm, gpu.norm_prologue = resid_norm, norm_prologue
-    gpu.attn_prologue = attn_prologue
+    gpu.norm_prologue = norm_prologue
     cpu, _ = load(tiny_gguf, device="cpu", max_ctx=512)
     prompt = tok.encode("<|im_start|>user\nhello world, a cozy cabin<|im_end|>\n")
     lg = gpu.prefill(prompt, slot=1)            # native kernels, 4 tokens per step
@@ -539,21 +386,16 @@ def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf, resid_norm,
     assert gpu.stats["graph_captures"] >= 1
 
 
-@pytest.mark.parametrize("resid_norm,fused_combine,norm_prologue,attn_prologue",
-                         [(False, False, False, False), (True, False, False, False),
-                          (True, True, False, False), (False, False, True, False),
-                          (False, False, True, True)])
-def test_engine_batched_decode_equals_single(dev, tiny_gguf, resid_norm, fused_combine,
-                                             norm_prologue, attn_prologue):
+@pytest.mark.parametrize("norm_prologue", [False, True])
+def test_engine_batched_decode_equals_single(dev, tiny_gguf, norm_prologue):
     """T sequences in one step give the same logits as each alone: slots are independent and the
     GEMV's roundings are pinned, so the int8 activation quantisation never flips between a batched
-    and a single step (batch-invariant serving) — also with the norms fused into the residual
-    GEMVs and the attention combine inside the attention launch."""
+    and a single step (batch-invariant serving) — the batched step normalises with rmsnorm_q8, the
+    single one (with norm_prologue) in the GEMV prologues."""
     from k8s_nvidia_gpus_amd.models.llm.synthetic import load
 
     eng, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=True)
-    eng.resid_norm, eng.fused_combine = resid_norm, fused_combine
-    eng.norm_prologue, eng.attn_prologue = norm_prologue, attn_prologue
+    eng.norm_prologue = norm_prologue
     prompts = [tok.encode(s) for s in ("hello", "the quick brown fox", "a cozy cabin in", "you")]
     last = []
     for s, p in enumerate(prompts):
