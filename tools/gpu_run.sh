@@ -11,7 +11,8 @@
 #   driver-notel     the same with --no-telemetry
 #   bench            bench.py defaults (K=200 / W=20)
 #   native           amd-vectoradd, amd-gemm-validator (bf16 + fp8), amd-proftester
-#   llm[:<tokens>]   tools/llm_bench.py (decode T list, default 1,2,4,8) + prefill
+#   llm[:<tokens>]   tools/llm_bench.py (decode T list, default 1,2,3,4) + prefill
+#   gemv[:<cases>]   tools/llm_bench.py --gemv: cold-weight GEMV decomposition sweep, T = 1 and 4
 #   prof-bench       rocprofv3 --kernel-trace --stats of the driver's bench command
 #   prof-llm         rocprofv3 kernel trace of steady LLM decode → per-kernel summary
 #   sd15 / wan       tools/sd15_bench.py / tools/wan_bench.py
@@ -69,11 +70,17 @@ for step in "$@"; do
         || fail "$step" $? "$OUT/proftester.log"
       grep -v '^{' "$OUT/proftester.log" | tail -8 ;;
     llm|llm:*)
-      toks="1,2,4,8"; [[ "$step" == llm:* ]] && toks="${step#llm:}"
+      toks="1,2,3,4"; [[ "$step" == llm:* ]] && toks="${step#llm:}"
       n=$(ls "$OUT"/llm_bench_*.json 2>/dev/null | wc -l)
       timeout -k 10 500 python -u tools/llm_bench.py --tokens "$toks" --out "$OUT/llm_bench_$n.json" \
         > "$OUT/llm_bench_$n.log" 2>&1 || fail "$step" $? "$OUT/llm_bench_$n.log"
       grep -E "decode|prefill" "$OUT/llm_bench_$n.log" | grep -v '^{' ;;
+    gemv|gemv:*)
+      cases="qkv,o_proj,gate_up,gate_up_q8,down_q4k,down_q6k,lm_head"; [[ "$step" == gemv:* ]] && cases="${step#gemv:}"
+      n=$(ls "$OUT"/gemv_*.json 2>/dev/null | wc -l)
+      timeout -k 10 600 python -u tools/llm_bench.py --tokens "" --prompt 64 --gemv --gemv-sweep4 \
+        --gemv-cases "$cases" --out "$OUT/gemv_$n.json" > "$OUT/gemv_$n.log" 2>&1 || fail "$step" $? "$OUT/gemv_$n.log"
+      grep "'gemv'" "$OUT/gemv_$n.log" | sort -t: -k8 | tail -40 | cut -c1-200 ;;
     prof-bench)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bench" -o bench --output-format csv \
         -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/prof_bench.log" 2>&1 \

@@ -42,46 +42,76 @@ def heartbeat(period=30.0):
     threading.Thread(target=run, daemon=True).start()
 
 
-GEMV_CASES = ("qkv", "o_proj", "gate_up", "down_q4k", "down_q6k", "lm_head")
+GEMV_CASES = ("qkv", "o_proj", "gate_up", "gate_up_q8", "down_q4k", "down_q6k", "lm_head")
+GEMV_CFGS = [(0, 0), (4, 4), (4, 16), (4, 32), (8, 8), (8, 16), (8, 32), (2, 4), (2, 8),
+             (1, 2), (1, 4), (8, 7), (4, 7), (8, 14), (4, 37), (8, 37), (8, 74), (4, 74)]
 
 
-def bench_gemv(eng: Engine, iters: int = 50, sweep4: bool = False, only=GEMV_CASES) -> list:
-    """Achieved bandwidth of every decode GEMV shape, default decomposition and a sweep."""
+def bench_gemv(eng: Engine, iters: int = 56, sweep4: bool = False, only=GEMV_CASES,
+               cfgs=GEMV_CFGS) -> list:
+    """Achieved bandwidth of every decode GEMV shape, default decomposition and a sweep.
+
+    Each timed launch reads ANOTHER layer's copy of the matrix (cycling over every layer that has
+    it in the same quantisation type): 28 × 76 MB of gate|up does not fit the 256 MB Infinity
+    Cache, so the numbers are the cold-weight rates of a real decode step, not MALL re-reads."""
     LK = eng.LK
-    L = eng.w.layers[0]
-    Lq4 = next((x for x in eng.w.layers if x.wd.qtype == 0), L)   # a Q4_K ffn_down layer
-    Lq6 = next((x for x in eng.w.layers if x.wd.qtype == 1), L)   # a Q6_K ffn_down layer
+    layers = eng.w.layers
+    per_case = {
+        "qkv": [(x.wqkv[0], None) for x in layers],
+        "o_proj": [(x.wo, None) for x in layers],
+        "gate_up": [(x.wg, x.wu) for x in layers],
+        "gate_up_q8": [(x.wg, x.wu) for x in layers],
+        "down_q4k": [(x.wd, None) for x in layers if x.wd.qtype == 0],
+        "down_q6k": [(x.wd, None) for x in layers if x.wd.qtype == 1],
+        "lm_head": [(eng.w.output, None)],
+    }
+    modes = {"qkv": "store", "o_proj": "resid", "gate_up": "pair", "gate_up_q8": "pair",
+             "down_q4k": "resid", "down_q6k": "resid", "lm_head": "store"}
     rows = []
-    cases = [("qkv", L.wqkv[0], "store"), ("o_proj", L.wo, "resid"),
-             ("gate_up", L.wg, "pair"), ("down_q4k", Lq4.wd, "resid"),
-             ("down_q6k", Lq6.wd, "resid"), ("lm_head", eng.w.output, "store")]
-    cases = [(n, w, m) for n, w, m in cases if n in only]
-    cfgs = [(0, 0), (4, 4), (4, 16), (4, 32), (8, 8), (8, 16), (8, 32), (2, 4), (2, 8),
-            (1, 2), (1, 4), (8, 7), (4, 7), (8, 14), (4, 37), (8, 37)]
-    for name, w, mode in cases:
+    for name in [c for c in GEMV_CASES if c in only]:
+        mats = per_case[name]
+        if not mats:
+            continue
+        mode = modes[name]
+        w = mats[0][0]
         for T in (1, 4):
             x8 = torch.randint(-127, 127, (T, w.k), dtype=torch.int8, device=eng.device)
             dx = torch.full((T, w.k // 32), 0.01, device=eng.device)
             sx = torch.zeros(T, w.k // 16, device=eng.device)
             out = torch.zeros(T, w.n, device=eng.device)
+            q8o = None
+            if name == "gate_up_q8":
+                q8o = (torch.zeros(T, w.n, dtype=torch.int8, device=eng.device),
+                       torch.zeros(T, w.n // 32, device=eng.device),
+                       torch.zeros(T, w.n // 16, device=eng.device))
             m = {"store": LK.STORE, "resid": LK.RESID, "pair": LK.PAIR}[mode]
-            for waves, rpw in (cfgs if T == 1 or sweep4 else cfgs[:1]):
-                kw = dict(w1=L.wu if mode == "pair" else None, waves=waves, rows_per_wg=rpw)
-                for _ in range(3):
-                    LK.qgemv(w, x8, dx, sx, out, m, **kw)
+            todo = cfgs if (T == 1 or sweep4) else cfgs[:1]
+            if name == "gate_up_q8":          # 32 rows per workgroup are fixed there
+                todo = [(wv, 0) for wv in (0, 2, 4, 8)]
+            for waves, rpw in todo:
+                def launch(i):
+                    w0, w1 = mats[i % len(mats)]
+                    LK.qgemv(w0, x8, dx, sx, out, m, w1=w1, waves=waves, rows_per_wg=rpw,
+                             q8_out=q8o)
+                try:
+                    for i in range(3):
+                        launch(i)
+                except RuntimeError:          # decomposition not supported for this shape
+                    continue
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
                 e0.record()
-                for _ in range(iters):
-                    LK.qgemv(w, x8, dx, sx, out, m, **kw)
+                for i in range(iters):
+                    launch(i)
                 e1.record()
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) / iters * 1e3
                 nbytes = w.nbytes() * (2 if mode == "pair" else 1)
                 r = {"gemv": name, "T": T, "N": w.n, "K": w.k, "type": ["Q4_K", "Q6_K"][w.qtype],
-                     "cfg": [waves, rpw], "us": round(us, 2),
+                     "cfg": [waves, rpw], "copies": len(mats), "us": round(us, 2),
                      "GBps": round(nbytes / us / 1e3, 1)}
                 rows.append(r)
+                print(r, file=sys.stderr, flush=True)
     return rows
 
 
@@ -134,7 +164,7 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=128, help="decode steps per T")
     ap.add_argument("--ctx", type=int, default=4096, help="KV-cache context (reference --ctx-size)")
     ap.add_argument("--prompt", type=int, default=512)
-    ap.add_argument("--tokens", default="1,2,3,4")
+    ap.add_argument("--tokens", default="1,2,3,4", help="decode T list ('' = no decode timing)")
     ap.add_argument("--gemv", action="store_true")
     ap.add_argument("--gemv-sweep4", action="store_true", help="also sweep the decomposition at T=4")
     ap.add_argument("--gemv-cases", default=",".join(GEMV_CASES), help="GEMV shapes to time")
@@ -193,8 +223,6 @@ def main(argv=None) -> int:
         print(f"decode T={T}: {row}", file=sys.stderr, flush=True)
     if args.gemv:
         res["gemv"] = bench_gemv(eng, sweep4=args.gemv_sweep4, only=args.gemv_cases.split(","))
-        for r in res["gemv"]:
-            print(r, file=sys.stderr, flush=True)
     if args.kernels:
         res["kernels"] = bench_small_kernels(eng)
     res["graph_captures"] = eng.stats["graph_captures"]
