@@ -73,7 +73,6 @@ class StepBuffers:
     t: torch.Tensor
     logits: torch.Tensor
     graphs: Dict[tuple, torch.cuda.CUDAGraph] = None   # keyed by (attention span, fused rope)
-    sync: torch.Tensor = None        # int32 [layers, 64]: in-launch hand-off counters (zeroed per step)
     ids: torch.Tensor = None         # int32 [T]: greedy next tokens (decode_greedy)
     meta: torch.Tensor = None        # int32 [3, T] on the GPU: tok / pos / slot are its rows
     host: torch.Tensor = None        # pinned staging copy of meta
@@ -116,9 +115,6 @@ class Engine:
         self.prefill_native = True
         self.prefill_gqa = True
         self.prefill_qtok = True
-        # attention → combine → o_proj as one launch with in-launch hand-offs
-        # (LK.attn_oproj; bit-identical to the three launches, which stay the fallback)
-        self.fused_attn_oproj = True
         # rejected variants (in-launch attention combine, fused residual norm, combine in the o_proj
         # prologue, MFMA attention, Infinity-Cache prefetch, ...): docs/experiments/llm_decode_rejected.md
         if self.gpu:
@@ -284,8 +280,7 @@ class Engine:
                 qkv=torch.zeros(T, c.dim + 2 * c.kv_dim, **f32), qrot=torch.zeros(T, c.dim, **f32),
                 po=torch.zeros(T, c.heads, nsplit, c.head_dim, **f32),
                 pml=torch.zeros(T, c.heads, nsplit, 2, **f32), t=torch.zeros(T, c.ffn, **f32),
-                logits=torch.zeros(T, c.vocab, **f32),
-                sync=torch.zeros(c.layers, 64, dtype=torch.int32, device=dev))
+                logits=torch.zeros(T, c.vocab, **f32))
             self._bufs[T] = b
         return b
 
@@ -306,9 +301,8 @@ class Engine:
 
     def _step_kernels(self, b: StepBuffers, span: int, fused: bool) -> None:
         """One decode step, per layer: q|k|v (one two-matrix launch when q|k and v have different
-        quantisation types) → attention → combine → o_proj (+= residual), as ONE launch with
-        in-launch hand-offs (LK.attn_oproj) or three → gate|up (SwiGLU, Q8 out) → ffn_down
-        (+= residual).  ``fused``: every token
+        quantisation types) → attention (+ its combine, which writes the Q8 o_proj input) → o_proj
+        (+= residual) → gate|up (SwiGLU, Q8 out) → ffn_down (+= residual).  ``fused``: every token
         in its own slot, so RoPE + the KV write run inside the attention kernel (no rope_kv launch).
         Steps of up to NORM_PROLOGUE_T tokens normalise in the GEMV prologues, larger ones once per
         input with rmsnorm_q8."""
@@ -326,25 +320,19 @@ class Engine:
             LK.rmsnorm_q8(xf, norm_w, c.eps, *qd)
             return qd, {}
 
-        fuse = self.fused_attn_oproj and c.kv_heads * b.T + b.T + 1 <= b.sync.shape[1]
-        if fuse:
-            b.sync.zero_()                  # one clear per step: every layer owns a row
         for i, L in enumerate(self.w.layers):
             self._qkv(b, L, *act(b.h, L.attn_norm))
-            kc, vc = self.k_cache[i], self.v_cache[i]
-            if fused:                       # RoPE + KV write inside the attention kernel
-                q, rope = None, dict(qkv=b.qkv, cos_t=self.cos, sin_t=self.sin)
+            if fused:
+                LK.attn_decode(None, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
+                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
+                               span=span, qkv=b.qkv, cos_t=self.cos, sin_t=self.sin)
             else:
                 LK.rope_kv(b.qkv, b.pos, b.slot, self.cos, self.sin, c.heads, c.kv_heads,
-                           c.head_dim, self.max_ctx, b.qrot, kc, vc)
-                q, rope = b.qrot, {}
-            # attention → combine → o_proj (+= residual): one launch, or three
-            if not (fuse and LK.attn_oproj(q, b.pos, b.slot, kc, vc, c.heads, c.kv_heads,
-                                           self.max_ctx, scale, b.po, b.pml, *qd, L.wo, b.h,
-                                           b.sync[i], span=span, **rope)):
-                LK.attn_decode(q, b.pos, b.slot, kc, vc, c.heads, c.kv_heads, c.head_dim,
-                               self.max_ctx, scale, b.po, b.pml, *qd, span=span, **rope)
-                LK.qgemv(L.wo, *qd, b.h, LK.RESID)
+                           c.head_dim, self.max_ctx, b.qrot, self.k_cache[i], self.v_cache[i])
+                LK.attn_decode(b.qrot, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
+                               c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
+                               span=span)
+            LK.qgemv(L.wo, *qd, b.h, LK.RESID)
             xin = act(b.h, L.ffn_norm)
             if c.ffn % 32 == 0:      # the pair GEMV quantises silu(g)·u (the ffn_down input) itself
                 LK.qgemv(L.wg, *xin[0], b.t, LK.PAIR, w1=L.wu, **xin[1], q8_out=qf)
@@ -355,15 +343,6 @@ class Engine:
                 LK.qgemv(L.wd, *self._q8(b, c.ffn), b.h, LK.RESID)
         LK.rmsnorm_q8(b.h, self.w.out_norm, c.eps, *qd)
         LK.qgemv(self.w.output, *qd, b.logits, LK.STORE)
-
-    def fused_wait_errors(self) -> int:
-        """Layers whose fused attention → o_proj launch gave up a bounded wait in the last step of
-        any batch size (0 = every hand-off completed; a non-zero count means invalid logits)."""
-        n = 0
-        for b in self._bufs.values():
-            if b.sync is not None:
-                n += int((b.sync[:, b.T * self.cfg.kv_heads + b.T] != 0).sum().item())
-        return n
 
     def _qkv(self, b: StepBuffers, L, q8, pro) -> None:
         """q|k|v projections from the Q8 input (or, with ``pro``, from fp32 rows normalised in the

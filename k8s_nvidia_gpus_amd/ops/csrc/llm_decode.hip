@@ -933,28 +933,8 @@ __global__ void __launch_bounds__(128) attn_combine_q8_kernel(const float* __res
                    x8, dx, sx);
 }
 
-// Write-through (sc1) store / sc1 load: relaxed agent-scope atomics.  Data handed to another
-// workgroup INSIDE a launch goes through these on both sides (per-XCD L2s are not coherent, a CU's
-// L1 is never refreshed by other CUs' stores): every handed-off word is stored sc1 and drained
-// (s_waitcnt vmcnt(0) in every storing wave) before the arrival counter is bumped, and read with
-// sc1 loads — no release / acquire fence needed (cdna_hip_programming.md §6 Guideline 16, R1).
-__device__ __forceinline__ void st_wt(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_wt(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_wt(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_wt(const uint32_t* p) {
-  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// One (kv head kh, 64-position chunk sp, token t) work item; WT: partials stored write-through
-// (the fused attention → combine → o_proj launch reads them back inside the launch).
-template <int G, bool WT>
-__device__ __forceinline__ void attn_item(const AttnArgs& a, const int kh, const int sp, const int t) {
+template <int G>
+__global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   const float* __restrict__ q = a.q;
   const int* __restrict__ pos = a.pos;
   const int* __restrict__ slot = a.slot;
@@ -970,14 +950,15 @@ __device__ __forceinline__ void attn_item(const AttnArgs& a, const int kh, const
   __shared__ float ps[G][kAttnChunk];
   __shared__ float mls[G][2];
   __shared__ float opart[4][G][kHeadDim];
+  const int kh = blockIdx.x, sp = blockIdx.y, t = blockIdx.z;
   const int len = pos[t] + 1;
   const int p0 = sp * kAttnChunk;
   const long pidx = ((long)t * H + kh * G) * nsplit + sp;   // + g * nsplit
   if (p0 >= len) {
     if (threadIdx.x < G) {
       float* dst = pml + (pidx + (long)threadIdx.x * nsplit) * 2;
-      if constexpr (WT) { st_wt(dst, -INFINITY); st_wt(dst + 1, 0.f); }
-      else { dst[0] = -INFINITY; dst[1] = 0.f; }
+      dst[0] = -INFINITY;
+      dst[1] = 0.f;
     }
     return;
   }
@@ -1136,222 +1117,13 @@ __device__ __forceinline__ void attn_item(const AttnArgs& a, const int kh, const
   for (int i = threadIdx.x; i < G * kHeadDim; i += blockDim.x) {
     const int g = i / kHeadDim, dd = i % kHeadDim;
     const float v = opart[0][g][dd] + opart[1][g][dd] + opart[2][g][dd] + opart[3][g][dd];
-    float* dst = po + (pidx + (long)g * nsplit) * kHeadDim + dd;
-    if constexpr (WT) st_wt(dst, v);
-    else *dst = v;
+    po[(pidx + (long)g * nsplit) * kHeadDim + dd] = v;
   }
   if (threadIdx.x < G) {
     const int g = threadIdx.x;
     float* dst = pml + (pidx + (long)g * nsplit) * 2;
-    if constexpr (WT) { st_wt(dst, mls[g][0]); st_wt(dst + 1, mls[g][1]); }
-    else { dst[0] = mls[g][0]; dst[1] = mls[g][1]; }
-  }
-  if constexpr (WT) __syncthreads();      // opart / ps / mls are reused by the next item
-}
-
-template <int G>
-__global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
-  attn_item<G, false>(a, blockIdx.x, blockIdx.y, blockIdx.z);
-}
-
-// ---------------------------------------------------------------- attention → combine → o_proj
-// The latency-bound middle of a decode layer as ONE launch (VERDICT r3 "LLM decode: build the
-// persistent decode layer"): as three launches it costs attention 6.2 + combine 4.8 + o_proj 7.1 µs
-// plus two boundaries at T = 1 while moving ~11 MB (profiles/r03/ar) — each kernel's floor is its
-// dispatch ramp and dependent load chain, not bytes.  Here every workgroup (one per CU) stays
-// resident through three phases separated by in-launch hand-offs instead of kernel boundaries:
-//
-//   1. attention work items (kv head, 64-position chunk, token), strided over the grid; partials
-//      stored write-through, then one arrival per item on the (token, kv head) counter;
-//   2. its o_proj rows' weights are loaded into registers — before any wait, so the weight stream
-//      overlaps the hand-offs (the weight loads do not depend on the attention output);
-//   3. workgroup h + H t (< H T) waits for the nsplit arrivals of head h's kv head, merges the
-//      chunks and stores head h's Q8 o_proj input write-through, then counts the head done;
-//   4. every workgroup waits until all H heads of every token are done, stages the Q8 input in
-//      LDS (sc1 loads) and finishes its rows: out += Wo · y.
-//
-// Hand-offs follow cdna_hip_programming.md §6 Guideline 16, R1: sc1 payload stores drained by
-// every storing wave (s_waitcnt vmcnt(0)) → barrier → one relaxed agent-scope atomic add; the
-// consumer polls ONE word with ONE lane (relaxed, s_sleep between polls) and reads the payload with
-// sc1 loads.  Every wait is bounded: past spin_ticks the launch's error word is set and the
-// workgroup leaves (garbage results, never a hang); the counters are zeroed before every launch
-// (the engine clears one block per step).  The host launches it only when the whole grid can be
-// co-resident (one workgroup per CU here) — a waiting workgroup never holds a slot a producer needs.
-// The arithmetic is the three kernels' own (attn_item, the combine's merge, compute_reg /
-// finish_row), so results are bit-identical to the three-launch path.
-constexpr int kAOMaxNb = 16;          // o_proj K <= 4096: one REGX stage per row
-constexpr int kAORowsPerWave = 4;     // o_proj rows preloaded per wave (<= 16 rows per workgroup)
-constexpr int kAOThreads = 256;
-
-struct AOArgs {
-  AttnArgs at;
-  int8_t* x8;            // Q8 o_proj input [T][H*128], handed over inside the launch
-  float* dx;             //                [T][H*4]
-  float* sx;             //                [T][H*8]
-  QMat wo;
-  float* out;            // residual [T][ldo]: out += Wo . y
-  int ldo, N, rows_per_wg;
-  uint32_t* sync;        // [T*Hkv] attention arrivals | [T] heads done | [1] error; zero at launch
-  long long spin_ticks;  // bound of every wait, wall_clock64 ticks
-};
-
-// ONE lane polls ONE word until it reaches `target` (relaxed agent-scope loads, s_sleep between
-// polls); the workgroup then continues together.  False (uniform) after spin_ticks or when another
-// workgroup already gave up: the error word is set.
-__device__ __forceinline__ bool ao_wait(const uint32_t* w, uint32_t target, uint32_t* err,
-                                        long long ticks) {
-  __shared__ int ok;
-  if (threadIdx.x == 0) {
-    const long long t0 = wall_clock64();
-    int good = 1;
-    for (unsigned spins = 0; ld_wt(w) < target; ++spins) {
-      if ((spins & 63) == 63 && (ld_wt(err) != 0u || wall_clock64() - t0 > ticks)) {
-        st_wt(err, 1u);
-        good = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    ok = good;
-  }
-  __syncthreads();
-  return ok != 0;
-}
-
-// combine_heads<1> of head h, token t, output dim dd (threads 0..127) for the fused launch: the
-// partials are read with sc1 loads and the Q8 result stored write-through (4 int8 per dword) — the
-// arithmetic of attn_combine_q8_kernel, so the same bits.
-__device__ __forceinline__ void combine_head_wt(const AttnArgs& at, int h, int t, int dd,
-                                                int8_t* x8, float* dx, float* sx) {
-  const int H = at.H, nsplit = at.nsplit;
-  const int ns = min(nsplit, (at.pos[t] + kAttnChunk) / kAttnChunk);
-  const long hb = ((long)t * H + h) * nsplit;
-  float m = -INFINITY, den = 0.f, v = 0.f;
-  for (int s0 = 0; s0 < ns; s0 += 8) {
-    float mx[8], l[8], ov[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const long sidx = hb + min(s0 + u, ns - 1);
-      mx[u] = ld_wt(at.pml + sidx * 2);
-      l[u] = ld_wt(at.pml + sidx * 2 + 1);
-      ov[u] = ld_wt(at.po + sidx * kHeadDim + dd);
-    }
-    float mn = m;
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (s0 + u < ns) mn = fmaxf(mn, mx[u]);
-    if (mn == -INFINITY) continue;
-    const float sc = m == -INFINITY ? 0.f : __expf(__fsub_rn(m, mn));
-    den = __fmul_rn(den, sc);
-    v = __fmul_rn(v, sc);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float wgt = (s0 + u < ns && mx[u] != -INFINITY) ? __expf(__fsub_rn(mx[u], mn)) : 0.f;
-      den = __fmaf_rn(wgt, l[u], den);
-      v = __fmaf_rn(wgt, ov[u], v);
-    }
-    m = mn;
-  }
-  const int K = H * kHeadDim;
-  const float y = den > 0.f ? __fdiv_rn(v, den) : 0.f;
-  const int col = h * kHeadDim + dd;
-  float amax = fabsf(y);
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, kWave));
-  const float d = amax / 127.f;
-  const int qv = d > 0.f ? (int)__builtin_rintf(y / d) : 0;
-  int s16 = qv;
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) s16 += __shfl_xor(s16, o, kWave);
-  // 4 consecutive int8 into one dword: lanes dd .. dd + 3 of the same wave
-  const uint32_t b = (uint32_t)(qv & 0xff);
-  const uint32_t w4 = b | ((uint32_t)__shfl_down((int)b, 1, kWave) << 8) |
-                      ((uint32_t)__shfl_down((int)b, 2, kWave) << 16) |
-                      ((uint32_t)__shfl_down((int)b, 3, kWave) << 24);
-  if ((dd & 3) == 0) st_wt(reinterpret_cast<uint32_t*>(x8 + (long)t * K + col), w4);
-  if ((dd & 31) == 0) st_wt(dx + (long)t * (K >> 5) + (col >> 5), d);
-  if ((dd & 15) == 0) st_wt(sx + (long)t * (K >> 4) + (col >> 4), d * (float)s16);
-}
-
-template <int G, int T>
-__global__ void __launch_bounds__(kAOThreads) attn_oproj_kernel(AOArgs a) {
-  constexpr int TYPE = kQ4K;
-  __shared__ __align__(16) int8_t xs[T * kAOMaxNb * 288];
-  __shared__ float dxs[T * kAOMaxNb * 8];
-  __shared__ float sxs[T * kAOMaxNb * 16];
-  const AttnArgs& at = a.at;
-  const int H = at.H, Hkv = at.Hkv, nsplit = at.nsplit;
-  const int K = H * kHeadDim, nb = K >> 8;
-  const int bid = blockIdx.x, nwg = gridDim.x;
-  uint32_t* arrive = a.sync;
-  uint32_t* heads = a.sync + T * Hkv;
-  uint32_t* err = heads + T;
-  // 1. attention items, strided over the grid (consecutive workgroups: different kv heads)
-  const int items = Hkv * nsplit * T;
-  for (int i = bid; i < items; i += nwg) {
-    const int kh = i % Hkv, sp = (i / Hkv) % nsplit, t = i / (Hkv * nsplit);
-    attn_item<G, true>(at, kh, sp, t);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // EVERY storing wave drains (R1)
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_fetch_add(arrive + t * Hkv + kh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // 2. this workgroup's o_proj rows into registers (wave w: rows row0 + w + 4 j)
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int sub = lane & 7, bl = lane >> 3;
-  const int row0 = bid * a.rows_per_wg, rend = min(a.N, row0 + a.rows_per_wg);
-  GemvArgs ga{};
-  ga.w0 = a.wo;
-  ga.out = a.out;
-  ga.ldo = a.ldo; ga.N = a.N; ga.K = K; ga.T = T; ga.rows_per_wg = a.rows_per_wg;
-  Blk<TYPE> wr[kAORowsPerWave][2], wdummy[2];
-#pragma unroll
-  for (int j = 0; j < kAORowsPerWave; ++j) {
-    const int r = min(row0 + wave + 4 * j, a.N - 1);    // clamped: no load under a branch
-    load_stage<TYPE, kResid, 2>(ga, r, 0, nb, sub, bl, wr[j], wdummy);
-  }
-  // 3. combine: workgroup h + H t merges head h of token t
-  if (bid < H * T) {
-    const int h = bid % H, t = bid / H;
-    if (!ao_wait(arrive + t * Hkv + h / G, (uint32_t)nsplit, err, a.spin_ticks)) return;
-    if (threadIdx.x < kHeadDim) combine_head_wt(at, h, t, threadIdx.x, a.x8, a.dx, a.sx);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_fetch_add(heads + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // 4. o_proj: every head of every token combined → stage the Q8 input (sc1 loads) → rows
-#pragma unroll
-  for (int t = 0; t < T; ++t)
-    if (!ao_wait(heads + t, (uint32_t)H, err, a.spin_ticks)) return;
-  const int xstride = nb * 288;
-  {
-    const int nw = K >> 2;                                  // dwords of x8 per token
-    for (int i = threadIdx.x; i < T * nw; i += kAOThreads) {
-      const int t = i / nw, p = (i - t * nw) << 2;
-      *reinterpret_cast<uint32_t*>(xs + t * xstride + xoff(p)) =
-          ld_wt(reinterpret_cast<const uint32_t*>(a.x8 + (long)t * K + p));
-    }
-    for (int i = threadIdx.x; i < T * (K >> 5); i += kAOThreads) dxs[i] = ld_wt(a.dx + i);
-    for (int i = threadIdx.x; i < T * (K >> 4); i += kAOThreads) sxs[i] = ld_wt(a.sx + i);
-  }
-  __syncthreads();
-  const XView xv = {xs, dxs, sxs, xstride, K >> 5, K >> 4};
-  XReg xr[2][T];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int t = 0; t < T; ++t) xr[u][t] = load_x<TYPE>(xv, t, min(8 * u + bl, nb - 1), sub);
-  float acc[T], acc1[T];
-#pragma unroll
-  for (int t = 0; t < T; ++t) acc[t] = acc1[t] = 0.f;
-#pragma unroll
-  for (int j = 0; j < kAORowsPerWave; ++j) {
-    const int r = row0 + wave + 4 * j;
-    if (r < rend) {
-      compute_reg<TYPE, T, kResid, 2>(nb, sub, bl, xr, wr[j], wdummy, acc, acc1);
-      finish_row<T, kResid>(ga, r, lane, acc, acc1);
-    }
+    dst[0] = mls[g][0];
+    dst[1] = mls[g][1];
   }
 }
 
@@ -1797,97 +1569,6 @@ int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* 
                      static_cast<const float*>(po), static_cast<const float*>(pml),
                      static_cast<const int*>(pos), H, aa.nsplit, kAttnChunk, static_cast<float*>(out),
                      static_cast<int8_t*>(x8), static_cast<float*>(dx), static_cast<float*>(sx));
-  return hipGetLastError() == hipSuccess ? 0 : 1;
-}
-
-// Attention (+ fused RoPE / KV write when qkv != null) → combine → o_proj (out += Wo . y) as ONE
-// launch (attn_oproj_kernel).  Returns 4 when the shape / device does not fit it (o_proj type not
-// Q4_K, K = H*128 > 4096, more than 16 rows per workgroup on this device, fewer workgroups than
-// H*T, or the grid would not be co-resident): the caller then runs the three-launch path.
-// sync: uint32 [>= T*Hkv + T + 1], ZERO at the launch (the engine clears one block per step);
-// sync[T*Hkv + T] != 0 afterwards = a bounded wait gave up (results invalid).
-int amdk8s_llm_attn_oproj(const void* q, const void* qkv, int ldq, const void* cos_t,
-                          const void* sin_t, const void* pos, const void* slot, void* kc, void* vc,
-                          int H, int Hkv, int max_ctx, int span, float scale, void* po, void* pml,
-                          void* x8, void* dx, void* sx, int wtype, const void* wq, const void* wqh,
-                          const void* wsc, const void* wd, void* out, int ldo, int N, void* sync,
-                          int T, void* stream) {
-  if (span <= 0) span = max_ctx;
-  if (H % Hkv || H / Hkv > kMaxGroup || max_ctx % kAttnChunk || span % kAttnChunk ||
-      span > max_ctx || T < 1 || T > kMaxTok || !sync || !(x8 && dx && sx) || !out || N < 1)
-    return 2;
-  if (!qkv && !q) return 2;
-  if (qkv && (!cos_t || !sin_t)) return 2;
-  const int K = H * kHeadDim;
-  if (wtype != kQ4K || K % 256 || (K >> 8) > kAOMaxNb) return 4;
-  static int cus = 0, occ = 0;
-  static long long ticks = 0;
-  if (cus == 0) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    int khz = 0;
-    hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
-    ticks = (long long)(khz > 0 ? khz : 100000) * 200;     // 200 ms: µs-scale waits, never a hang
-    // co-residency: the smallest per-CU occupancy over the instantiations (same LDS / VGPR shape)
-    int o = 0;
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, attn_oproj_kernel<7, 4>, kAOThreads, 0);
-    occ = o;
-  }
-  if (cus <= 0 || occ <= 0) return 4;
-  // one workgroup per CU: rows per workgroup so the grid is <= the CU count
-  int rows = (N + cus - 1) / cus;
-  if (rows > 4 * kAORowsPerWave) return 4;
-  const int nwg = (N + rows - 1) / rows;
-  if (nwg < H * T || nwg > cus * occ) return 4;
-  AOArgs a{};
-  AttnArgs& aa = a.at;
-  aa.q = static_cast<const float*>(q);
-  aa.qkv = static_cast<const float*>(qkv);
-  aa.ldq = ldq;
-  aa.cos_t = static_cast<const float*>(cos_t);
-  aa.sin_t = static_cast<const float*>(sin_t);
-  aa.pos = static_cast<const int*>(pos);
-  aa.slot = static_cast<const int*>(slot);
-  aa.kc = static_cast<uint16_t*>(kc);
-  aa.vc = static_cast<uint16_t*>(vc);
-  aa.H = H; aa.Hkv = Hkv; aa.max_ctx = max_ctx; aa.scale = scale;
-  aa.nsplit = span / kAttnChunk;
-  aa.po = static_cast<float*>(po);
-  aa.pml = static_cast<float*>(pml);
-  a.x8 = static_cast<int8_t*>(x8);
-  a.dx = static_cast<float*>(dx);
-  a.sx = static_cast<float*>(sx);
-  a.wo = {static_cast<const uint8_t*>(wq), static_cast<const uint8_t*>(wqh),
-          static_cast<const int8_t*>(wsc), static_cast<const uint16_t*>(wd)};
-  a.out = static_cast<float*>(out);
-  a.ldo = ldo; a.N = N; a.rows_per_wg = rows;
-  a.sync = static_cast<uint32_t*>(sync);
-  a.spin_ticks = ticks;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  auto go = [&](auto g, auto t) {
-    hipLaunchKernelGGL((attn_oproj_kernel<decltype(g)::value, decltype(t)::value>), dim3(nwg),
-                       dim3(kAOThreads), 0, st, a);
-  };
-  auto by_t = [&](auto g) {
-    switch (T) {
-      case 1: go(g, std::integral_constant<int, 1>{}); break;
-      case 2: go(g, std::integral_constant<int, 2>{}); break;
-      case 3: go(g, std::integral_constant<int, 3>{}); break;
-      default: go(g, std::integral_constant<int, 4>{}); break;
-    }
-  };
-  switch (H / Hkv) {
-    case 1: by_t(std::integral_constant<int, 1>{}); break;
-    case 2: by_t(std::integral_constant<int, 2>{}); break;
-    case 3: by_t(std::integral_constant<int, 3>{}); break;
-    case 4: by_t(std::integral_constant<int, 4>{}); break;
-    case 5: by_t(std::integral_constant<int, 5>{}); break;
-    case 6: by_t(std::integral_constant<int, 6>{}); break;
-    case 7: by_t(std::integral_constant<int, 7>{}); break;
-    case 8: by_t(std::integral_constant<int, 8>{}); break;
-    default: return 2;
-  }
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

@@ -44,10 +44,6 @@ def _lib():
             lib.amdk8s_llm_attn_decode.argtypes = [vp, vp, ci, vp, vp, vp, vp, vp, vp, ci, ci, ci,
                                                    ci, ci, cf, vp, vp, vp, vp, vp, vp, ci, vp]
             lib.amdk8s_llm_attn_decode.restype = ci
-            lib.amdk8s_llm_attn_oproj.argtypes = [vp, vp, ci, vp, vp, vp, vp, vp, vp, ci, ci, ci,
-                                                  ci, cf, vp, vp, vp, vp, vp, ci, vp, vp, vp, vp,
-                                                  vp, ci, ci, vp, ci, vp]
-            lib.amdk8s_llm_attn_oproj.restype = ci
             lib.amdk8s_llm_dequant.argtypes = [ci, vp, vp, vp, vp, vp, ci, ci, vp, ci, vp]
             lib.amdk8s_llm_dequant.restype = ci
             lib.amdk8s_llm_q6k_repack.argtypes = [vp, cl, vp, vp, vp, vp, vp]
@@ -170,28 +166,6 @@ def attn_decode(q, pos, slot, kc, vc, heads: int, kv_heads: int, head_dim: int, 
                                          _p(out), _p(x8), _p(dx), _p(sx),
                                          ref.shape[0], _stream(ref)),
            "amdk8s_llm_attn_decode")
-
-
-def attn_oproj(q, pos, slot, kc, vc, heads: int, kv_heads: int, max_ctx: int, scale: float, po,
-               pml, x8, dx, sx, wo, out, sync, span: int = 0, qkv=None, cos_t=None,
-               sin_t=None) -> bool:
-    """Decode attention → chunk combine → o_proj (``out += Wo · y``) as ONE launch (the three
-    kernels' arithmetic, bit-identical to :func:`attn_decode` + :func:`qgemv` RESID).  ``sync``:
-    int32 [>= T*kv_heads + T + 1], zero at the call; afterwards ``sync[T*kv_heads + T] != 0`` means
-    a bounded in-launch wait gave up.  Returns False (nothing launched) when the shape or the
-    device does not fit the fused form: run the three-launch path then."""
-    ref = qkv if qkv is not None else q
-    rc = _lib().amdk8s_llm_attn_oproj(_p(q), _p(qkv), qkv.stride(0) if qkv is not None else 0,
-                                      _p(cos_t), _p(sin_t), pos.data_ptr(), slot.data_ptr(),
-                                      kc.data_ptr(), vc.data_ptr(), heads, kv_heads, max_ctx, span,
-                                      float(scale), po.data_ptr(), pml.data_ptr(), x8.data_ptr(),
-                                      dx.data_ptr(), sx.data_ptr(), wo.qtype, *wo.ptrs(),
-                                      out.data_ptr(), out.stride(0), wo.n, sync.data_ptr(),
-                                      ref.shape[0], _stream(ref))
-    if rc == 4:
-        return False
-    _check(rc, "amdk8s_llm_attn_oproj")
-    return True
 
 
 def dequant(w, out, rows=None) -> None:

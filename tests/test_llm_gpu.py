@@ -330,64 +330,6 @@ def test_prologue_norm_equals_rmsnorm_kernel(dev, LK, K, T):
     torch.testing.assert_close(a, b, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("fused_rope", [False, True])
-@pytest.mark.parametrize("T", [1, 2, 3, 4])
-@pytest.mark.parametrize("H,Hkv,span", [(28, 4, 1024), (8, 8, 512), (4, 2, 2048)])
-def test_fused_attn_oproj_equals_three_launches(dev, LK, H, Hkv, span, T, fused_rope):
-    """Attention → combine → o_proj as ONE launch with in-launch hand-offs: bit-identical to
-    attn_decode + the resid GEMV (residual, Q8 o_proj input, K/V cache writes), over repeated
-    launches on one zeroed-per-call sync block, no bounded wait giving up."""
-    from k8s_nvidia_gpus_amd.models.llm import gguf
-    from k8s_nvidia_gpus_amd.models.llm.engine import rope_tables
-
-    torch.manual_seed(40 + H + T)
-    K, slots, max_ctx = H * 128, 4, 2048
-    base_k = (torch.randn(slots, Hkv, max_ctx, 128, device=dev) * 0.5).half()
-    base_v = torch.randn(slots, Hkv, max_ctx, 128, device=dev).half()
-    cos, sin = rope_tables(max_ctx, 128, 1.0e6, dev)
-    pos = torch.tensor([span - 1, 63, 64, span // 2 + 5][:T], dtype=torch.int32, device=dev)
-    slot = torch.tensor([1, 0, 3, 2][:T], dtype=torch.int32, device=dev)
-    qkv = torch.randn(T, (H + 2 * Hkv) * 128, device=dev)
-    w, _ = _qw(K, K, gguf.Q4_K, 41, dev)
-    res0 = torch.randn(T, K, device=dev)
-    nsplit = max_ctx // LK.attn_chunk()
-
-    def run(fused_launch):
-        kc, vc = base_k.clone(), base_v.clone()
-        po = torch.full((T, H, nsplit, 128), float("nan"), device=dev)
-        pml = torch.full((T, H, nsplit, 2), float("nan"), device=dev)
-        x8 = torch.zeros(T, K, dtype=torch.int8, device=dev)
-        dx = torch.zeros(T, K // 32, device=dev)
-        sx = torch.zeros(T, K // 16, device=dev)
-        out = res0.clone()
-        if fused_rope:
-            q, rope = None, dict(qkv=qkv, cos_t=cos, sin_t=sin)
-        else:
-            q = torch.empty(T, H * 128, device=dev)
-            LK.rope_kv(qkv, pos, slot, cos, sin, H, Hkv, 128, max_ctx, q, kc, vc)
-            rope = {}
-        if fused_launch:
-            sync = torch.zeros(64, dtype=torch.int32, device=dev)
-            assert LK.attn_oproj(q, pos, slot, kc, vc, H, Hkv, max_ctx, 1 / math.sqrt(128), po, pml,
-                                 x8, dx, sx, w, out, sync, span=span, **rope)
-            torch.cuda.synchronize()
-            assert int(sync[T * Hkv + T]) == 0                         # no wait gave up
-            assert sync[:T * Hkv].tolist() == [span // LK.attn_chunk()] * (T * Hkv)
-            assert sync[T * Hkv:T * Hkv + T].tolist() == [H] * T
-        else:
-            LK.attn_decode(q, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po, pml,
-                           x8, dx, sx, span=span, **rope)
-            LK.qgemv(w, x8, dx, sx, out, LK.RESID)
-        torch.cuda.synchronize()
-        return kc, vc, x8, dx, sx, out
-
-    ref = run(False)
-    for _ in range(3):
-        got = run(True)
-        for a, b in zip(got, ref):
-            assert torch.equal(a, b)
-
-
 @pytest.mark.parametrize("types", [("Q4_K", "Q6_K"), ("Q6_K", "Q4_K")])
 @pytest.mark.parametrize("T", [1, 2, 3, 4])
 @pytest.mark.parametrize("K", [1536, 3584])
@@ -444,8 +386,8 @@ def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf, norm_prolog
     assert gpu.stats["graph_captures"] >= 1
 
 
-@pytest.mark.parametrize("norm_prologue,fused_attn_oproj", [(False, True), (True, True), (True, False)])
-def test_engine_batched_decode_equals_single(dev, tiny_gguf, norm_prologue, fused_attn_oproj):
+@pytest.mark.parametrize("norm_prologue", [False, True])
+def test_engine_batched_decode_equals_single(dev, tiny_gguf, norm_prologue):
     """T sequences in one step give the same logits as each alone: slots are independent and the
     GEMV's roundings are pinned, so the int8 activation quantisation never flips between a batched
     and a single step (batch-invariant serving) — the batched step normalises with rmsnorm_q8, the
@@ -454,7 +396,6 @@ def test_engine_batched_decode_equals_single(dev, tiny_gguf, norm_prologue, fuse
 
     eng, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=True)
     eng.norm_prologue = norm_prologue
-    eng.fused_attn_oproj = fused_attn_oproj
     prompts = [tok.encode(s) for s in ("hello", "the quick brown fox", "a cozy cabin in", "you")]
     last = []
     for s, p in enumerate(prompts):
@@ -465,30 +406,6 @@ def test_engine_batched_decode_equals_single(dev, tiny_gguf, norm_prologue, fuse
     for s in range(4):
         single = eng.decode([toks[s]], [last[s][1]], [s])[0]
         torch.testing.assert_close(batch[s], single, rtol=0, atol=0)
-    assert eng.fused_wait_errors() == 0
-
-
-def test_engine_fused_attn_oproj_equals_three_launches(dev, tiny_gguf):
-    """Whole decode steps (HIP graphs, T = 1 and 4) with the fused attention → o_proj launch give
-    the same logits, bit for bit, as with the three launches."""
-    from k8s_nvidia_gpus_amd.models.llm.synthetic import load
-
-    outs = []
-    for fused in (False, True):
-        eng, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=True)
-        eng.fused_attn_oproj = fused
-        prompts = [tok.encode(s) for s in ("hello", "the quick brown fox", "a cozy cabin in", "you")]
-        for s, p in enumerate(prompts):
-            eng.prefill(p, slot=s)
-        lens = [len(p) for p in prompts]
-        steps = []
-        for k in range(3):
-            steps.append(eng.decode([7, 8, 9, 10], [n + k for n in lens], [0, 1, 2, 3]).clone())
-            steps.append(eng.decode([11], [lens[0] + 3 + k], [0]).clone())
-        assert eng.fused_wait_errors() == 0
-        outs.append(steps)
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
 
 
 def test_dense_prefill_matches_native_prefill(dev, tiny_gguf):

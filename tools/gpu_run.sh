@@ -12,7 +12,6 @@
 #   bench            bench.py defaults (K=200 / W=20)
 #   native           amd-vectoradd, amd-gemm-validator (bf16 + fp8), amd-proftester
 #   llm[:<tokens>]   tools/llm_bench.py (decode T list, default 1,2,3,4) + prefill
-#   llm3[:<tokens>]  the same with attention / combine / o_proj as three launches (A/B)
 #   gemv[:<cases>]   tools/llm_bench.py --gemv: cold-weight GEMV decomposition sweep, T = 1 and 4
 #   prof-bench       rocprofv3 --kernel-trace --stats of the driver's bench command
 #   prof-llm         rocprofv3 kernel trace of steady LLM decode → per-kernel summary
@@ -70,11 +69,10 @@ for step in "$@"; do
       timeout -k 10 300 native/bin/amd-proftester --json > "$OUT/proftester.log" 2>&1 \
         || fail "$step" $? "$OUT/proftester.log"
       grep -v '^{' "$OUT/proftester.log" | tail -8 ;;
-    llm|llm:*|llm3|llm3:*)
-      toks="1,2,3,4"; [[ "$step" == llm*:* ]] && toks="${step#*:}"
-      extra=""; [[ "$step" == llm3* ]] && extra="--three-launch"
+    llm|llm:*)
+      toks="1,2,3,4"; [[ "$step" == llm:* ]] && toks="${step#llm:}"
       n=$(ls "$OUT"/llm_bench_*.json 2>/dev/null | wc -l)
-      timeout -k 10 500 python -u tools/llm_bench.py --tokens "$toks" $extra --out "$OUT/llm_bench_$n.json" \
+      timeout -k 10 500 python -u tools/llm_bench.py --tokens "$toks" --out "$OUT/llm_bench_$n.json" \
         > "$OUT/llm_bench_$n.log" 2>&1 || fail "$step" $? "$OUT/llm_bench_$n.log"
       grep -E "decode|prefill" "$OUT/llm_bench_$n.log" | grep -v '^{' ;;
     gemv|gemv:*)

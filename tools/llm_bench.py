@@ -169,8 +169,6 @@ def main(argv=None) -> int:
     ap.add_argument("--gemv-sweep4", action="store_true", help="also sweep the decomposition at T=4")
     ap.add_argument("--gemv-cases", default=",".join(GEMV_CASES), help="GEMV shapes to time")
     ap.add_argument("--kernels", action="store_true", help="time the non-GEMV decode kernels")
-    ap.add_argument("--three-launch", action="store_true",
-                    help="attention, combine and o_proj as three launches (A/B vs the fused launch)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
     if not torch.cuda.is_available():
@@ -185,7 +183,6 @@ def main(argv=None) -> int:
     w = ModelWeights.random(cfg, device=dev, seed=0)
     torch.cuda.synchronize()
     eng = Engine(w, max_ctx=args.ctx, slots=4, dense=True)
-    eng.fused_attn_oproj = not args.three_launch
     eng.dense_weights()
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t0
@@ -229,8 +226,6 @@ def main(argv=None) -> int:
     if args.kernels:
         res["kernels"] = bench_small_kernels(eng)
     res["graph_captures"] = eng.stats["graph_captures"]
-    res["fused_attn_oproj"] = eng.fused_attn_oproj
-    res["fused_wait_errors"] = eng.fused_wait_errors()
     line = json.dumps(res)
     print(line, flush=True)
     if args.out:
