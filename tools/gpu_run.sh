@@ -14,7 +14,8 @@
 #   llm[:<tokens>]   tools/llm_bench.py (decode T list, default 1,2,3,4) + prefill
 #   gemv[:<cases>]   tools/llm_bench.py --gemv: cold-weight GEMV decomposition sweep, T = 1 and 4
 #   prof-bench       rocprofv3 --kernel-trace --stats of the driver's bench command
-#   prof-llm         rocprofv3 kernel trace of steady LLM decode → per-kernel summary
+#   prof-llm[:<T>]   rocprofv3 kernel trace of steady LLM decode at T tokens → per-kernel summary
+#   pmc-llm[:<T>]    tools/llm_pmc.sh: PMC passes (busy / VALU / wait shares, HBM bytes) at T tokens
 #   sd15 / wan       tools/sd15_bench.py / tools/wan_bench.py
 #   env:VAR=VALUE    export VAR for the following steps (A/B knobs)
 #
@@ -86,13 +87,19 @@ for step in "$@"; do
         -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/prof_bench.log" 2>&1 \
         || fail "$step" $? "$OUT/prof_bench.log"
       find "$OUT/prof_bench" -name "*kernel_stats.csv" -exec head -6 {} \; | cut -c1-200 ;;
-    prof-llm)
-      timeout -k 10 400 rocprofv3 --kernel-trace --output-format rocpd -d "$OUT/prof_llm" -o llm \
-        -- python3 tools/steady_prof.py llm-decode --iters 20 --warmup 5 > "$OUT/prof_llm.log" 2>&1 \
-        || fail "$step" $? "$OUT/prof_llm.log"
-      db=$(find "$OUT/prof_llm" -name '*.db' | head -1)
-      python3 tools/rocpd_summary.py "$db" --after-gap-ms 200 --per 20 --top 30 > "$OUT/llm_decode_kernels.txt" \
-        && head -24 "$OUT/llm_decode_kernels.txt" | cut -c1-170 ;;
+    prof-llm|prof-llm:*)
+      t=1; [[ "$step" == prof-llm:* ]] && t="${step#prof-llm:}"
+      timeout -k 10 400 rocprofv3 --kernel-trace --output-format rocpd -d "$OUT/prof_llm_t$t" -o llm \
+        -- python3 tools/steady_prof.py llm-decode --tokens "$t" --iters 20 --warmup 5 > "$OUT/prof_llm_t$t.log" 2>&1 \
+        || fail "$step" $? "$OUT/prof_llm_t$t.log"
+      db=$(find "$OUT/prof_llm_t$t" -name '*.db' | head -1)
+      python3 tools/rocpd_summary.py "$db" --after-gap-ms 200 --per 20 --top 30 > "$OUT/llm_decode_t${t}_kernels.txt" \
+        && head -24 "$OUT/llm_decode_t${t}_kernels.txt" | cut -c1-170 ;;
+    pmc-llm|pmc-llm:*)
+      t=1; [[ "$step" == pmc-llm:* ]] && t="${step#pmc-llm:}"
+      OUT="$OUT/llm_pmc_t$t" TOKENS=$t timeout -k 10 400 tools/llm_pmc.sh > "$OUT/llm_pmc_t$t.txt" 2>&1 \
+        || fail "$step" $? "$OUT/llm_pmc_t$t.txt"
+      cut -c1-200 "$OUT/llm_pmc_t$t.txt" | tail -14 ;;
     sd15)
       timeout -k 10 600 python -u tools/sd15_bench.py > "$OUT/sd15.log" 2>&1 || fail "$step" $? "$OUT/sd15.log"
       tail -5 "$OUT/sd15.log" ;;
