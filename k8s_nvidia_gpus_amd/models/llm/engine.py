@@ -122,6 +122,13 @@ class Engine:
 
             self.LK = LK
             self.max_T = LK.max_tokens()
+            if LK.gemv_impl() == LK.GEMV_MFMA:
+                # Q4_K GEMVs on the int8 matrix cores: every qualifying matrix gets its packed copy
+                # (the VALU kernel keeps the others, and the two-matrix q|k|v launch)
+                for L in self.w.layers:
+                    for w in [L.wo, L.wg, L.wu, L.wd] + list(L.wqkv):
+                        w.mfma_pack()
+                self.w.output.mfma_pack()
         else:
             self.max_T = 4
         self.stats = {"decode_steps": 0, "decode_tokens": 0, "prefill_tokens": 0,

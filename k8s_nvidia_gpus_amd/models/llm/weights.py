@@ -36,6 +36,21 @@ class QWeight:
         self.qtype, self.n, self.k = qtype, n, k
         self.q, self.qh, self.sc, self.d = q, qh, sc, d
         self.raw = raw          # CPU only: GGUF rows for the numpy decoder
+        self.mfma = None        # on the GPU: MFMA-packed planes (mq, mqh, msc, md), see mfma_pack
+
+    def mfma_pack(self) -> bool:
+        """Add the MFMA-packed copy of the planes (the int8 matrix-core GEMV reads it); False
+        when the matrix does not qualify (CPU, N % 16)."""
+        if self.q.device.type != "cuda" or self.n % 16:
+            return False
+        if self.mfma is None:
+            from k8s_nvidia_gpus_amd.ops import llm_kernels as LK
+
+            self.mfma = LK.mfma_pack(self)
+        return True
+
+    def mfma_ptrs(self):
+        return tuple(None if t is None else t.data_ptr() for t in self.mfma)
 
     @property
     def ggml_type(self) -> int:

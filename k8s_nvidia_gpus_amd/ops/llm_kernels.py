@@ -28,6 +28,12 @@ def _lib():
             vp, ci, cl, cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
             lib.amdk8s_llm_max_tokens.restype = ci
             lib.amdk8s_llm_attn_chunk.restype = ci
+            lib.amdk8s_llm_qgemv_mfma.argtypes = [ci, ci] + [vp] * 8 + [vp, vp, vp, vp, ci, vp, cf,
+                                                                       vp, vp, ci, ci, ci, ci, ci,
+                                                                       ci, vp, vp, vp, vp]
+            lib.amdk8s_llm_qgemv_mfma.restype = ci
+            lib.amdk8s_llm_mfma_pack.argtypes = [ci, vp, vp, vp, vp, ci, ci, vp, vp, vp, vp, vp]
+            lib.amdk8s_llm_mfma_pack.restype = ci
             lib.amdk8s_llm_qgemv.argtypes = [ci, ci] + [vp] * 8 + [vp, vp, vp] \
                 + [vp, ci, vp, cf] + [vp, vp] + [ci, ci, ci, ci, ci, ci] + [vp, vp, vp] + [vp]
             lib.amdk8s_llm_qgemv.restype = ci
@@ -83,25 +89,67 @@ def attn_chunk() -> int:
     return int(_lib().amdk8s_llm_attn_chunk())
 
 
+GEMV_VALU, GEMV_MFMA = 0, 1
+_GEMV = [GEMV_VALU]
+
+
+def gemv_impl(impl: int = None) -> int:
+    """Process-wide quantised-GEMV implementation (GEMV_VALU / GEMV_MFMA); returns the previous one.
+    Called with no argument it only queries.  The MFMA kernel needs the weights' MFMA-packed copy
+    (:meth:`QWeight.mfma_pack`); without it a matrix stays on the VALU kernel at every T, so each
+    matrix keeps one arithmetic (batch-invariant decode)."""
+    prev = _GEMV[0]
+    if impl is not None:
+        _GEMV[0] = int(impl)
+    return prev
+
+
+def mfma_pack(w) -> tuple:
+    """MFMA-packed copy (mq, mqh, msc, md) of a QWeight's planes (N % 16 == 0; mqh None for Q4_K)."""
+    nb = w.k // 256
+    dev = w.q.device
+    mq = torch.empty(w.n * nb * 128, dtype=torch.uint8, device=dev)
+    mqh = torch.empty(w.n * nb * 64, dtype=torch.uint8, device=dev) if w.qtype == 1 else None
+    msc = torch.empty(w.n * nb * 16, dtype=torch.uint8, device=dev)
+    md = torch.empty(w.n * nb, dtype=torch.int32, device=dev)
+    _check(_lib().amdk8s_llm_mfma_pack(w.qtype, *w.ptrs(), w.n, nb, mq.data_ptr(), _p(mqh),
+                                       msc.data_ptr(), md.data_ptr(), _stream(w.q)),
+           "amdk8s_llm_mfma_pack")
+    return mq, mqh, msc, md
+
+
 def qgemv(w0, x8, dx, sx, out, mode: int = STORE, w1=None, bias=None, ldo: int = None,
           rows_per_wg: int = 0, waves: int = 0, xf=None, norm_w=None, eps: float = 1e-6,
-          q8_out=None) -> None:
+          q8_out=None) -> str:
     """``w0``/``w1``: :class:`~k8s_nvidia_gpus_amd.models.llm.weights.QWeight` on the GPU.
     Input: Q8 activations (``x8``/``dx``/``sx``, [T, K]) or fp32 rows ``xf`` [T, K] (pass
     ``x8=dx=sx=None``) that the kernel quantises itself, after an RMSNorm when ``norm_w`` is given.
     ``out`` fp32 [T, ldo] (a view with row stride ``ldo``).  ``waves`` per workgroup and
     ``rows_per_wg``: 0 = the kernel's default decomposition.  ``q8_out`` = (x8, dx, sx) [T, N]
-    (pair mode only): write silu(g)·u quantised to Q8 — the ffn_down input — instead of ``out``."""
+    (pair mode only): write silu(g)·u quantised to Q8 — the ffn_down input — instead of ``out``.
+    Returns the kernel that ran: "mfma" (:func:`gemv_impl` MFMA and packed weights) or "valu"."""
     t = (xf if xf is not None else x8).shape[0]
     ldo = out.stride(0) if ldo is None else ldo
+    q8 = tuple(_p(t) for t in q8_out) if q8_out else (None,) * 3
+    if (_GEMV[0] == GEMV_MFMA and w0.mfma is not None
+            and (w1 is None or w1.mfma is not None)):
+        b = w1.mfma_ptrs() if w1 is not None else (None,) * 4
+        rc = _lib().amdk8s_llm_qgemv_mfma(
+            w0.qtype, mode, *w0.mfma_ptrs(), *b, _p(x8), _p(dx), _p(sx), _p(xf),
+            xf.stride(0) if xf is not None else 0, _p(norm_w), float(eps), _p(bias),
+            out.data_ptr(), ldo, w0.n, w0.k, t, waves, rows_per_wg, *q8,
+            _stream(xf if xf is not None else x8))
+        if rc != 4:
+            _check(rc, "amdk8s_llm_qgemv_mfma")
+            return "mfma"
     a = w0.ptrs()
     b = w1.ptrs() if w1 is not None else (None, None, None, None)
     ref = xf if xf is not None else x8
     _check(_lib().amdk8s_llm_qgemv(w0.qtype, mode, *a, *b, _p(x8), _p(dx), _p(sx), _p(xf),
                                    xf.stride(0) if xf is not None else 0, _p(norm_w), float(eps),
                                    _p(bias), out.data_ptr(), ldo, w0.n, w0.k, t,
-                                   waves, rows_per_wg, *((_p(t) for t in q8_out) if q8_out else (None,) * 3),
-                                   _stream(ref)), "amdk8s_llm_qgemv")
+                                   waves, rows_per_wg, *q8, _stream(ref)), "amdk8s_llm_qgemv")
+    return "valu"
 
 
 def qgemv2(w0, w1, x8, dx, sx, out0, out1, bias0=None, bias1=None, rows_per_wg: int = 0,

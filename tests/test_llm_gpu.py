@@ -196,6 +196,113 @@ def test_qgemv_batch_invariant_across_variants(dev, LK, qt, K):
             assert torch.equal(part, full[:T]), (mode, T)
 
 
+@pytest.fixture
+def mfma(LK):
+    """Q4_K GEMVs on the MFMA kernel for the test (process-wide switch), restored afterwards."""
+    prev = LK.gemv_impl(LK.GEMV_MFMA)
+    yield LK
+    LK.gemv_impl(prev)
+
+
+@pytest.mark.parametrize("qt", ["Q4_K", "Q6_K"])
+@pytest.mark.parametrize("T", [1, 2, 3, 4])
+@pytest.mark.parametrize("mode", ["store", "resid", "pair"])
+@pytest.mark.parametrize("N,K", [(320, 1536), (256, 3584), (96, 18944), (65536, 512)])
+def test_mfma_gemv_vs_fp32(dev, mfma, qt, T, mode, N, K):
+    """qgemv_mfma_kernel (int8 MFMA sub-block sums + per-lane scaling) against the fp32 product of
+    the dequantised weights and activations, on each launch shape: 2x2 pair, 1x2, 1x8 long rows,
+    4x1 tall."""
+    from k8s_nvidia_gpus_amd.models.llm import gguf
+
+    LK = mfma
+    w0, r0 = _qw(N, K, getattr(gguf, qt), 21, dev)
+    w1, r1 = _qw(N, K, getattr(gguf, qt), 22, dev)
+    assert w0.mfma_pack() and w1.mfma_pack()
+    torch.manual_seed(100 + T)
+    x = torch.randn(T, K, device=dev)
+    x8, dx, sx, xq = _q8(x, LK)
+    bias = torch.randn(N, device=dev)
+    a0 = xq.cpu() @ r0.t()
+    out = torch.randn(T, N + 3, device=dev)[:, :N]      # strided rows
+    before = out.clone()
+    if mode == "store":
+        ran = LK.qgemv(w0, x8, dx, sx, out, LK.STORE, bias=bias)
+        ref = a0 + bias.cpu()
+    elif mode == "resid":
+        ran = LK.qgemv(w0, x8, dx, sx, out, LK.RESID)
+        ref = before.cpu() + a0
+    else:
+        ran = LK.qgemv(w0, x8, dx, sx, out, LK.PAIR, w1=w1)
+        ref = torch.nn.functional.silu(a0) * (xq.cpu() @ r1.t())
+    assert ran == "mfma"
+    torch.testing.assert_close(out.cpu(), ref, rtol=2e-4, atol=2e-4)
+
+
+@pytest.mark.parametrize("qt", ["Q4_K", "Q6_K"])
+@pytest.mark.parametrize("K", [1536, 3584, 18944])
+def test_mfma_gemv_batch_invariant(dev, mfma, qt, K):
+    """Each token's MFMA GEMV result is bit-identical for every T, with Q8 and with fp32 (+ fused
+    RMSNorm) input."""
+    from k8s_nvidia_gpus_amd.models.llm import gguf
+
+    LK = mfma
+    w0, _ = _qw(64, K, getattr(gguf, qt), 31, dev)
+    w1, _ = _qw(64, K, getattr(gguf, qt), 32, dev)
+    assert w0.mfma_pack() and w1.mfma_pack()
+    torch.manual_seed(K + 1)
+    x = torch.randn(4, K, device=dev)
+    nw = torch.rand(K, device=dev) + 0.5
+    x8, dx, sx, _ = _q8(x, LK)
+    for mode in (LK.STORE, LK.RESID, LK.PAIR):
+        pw = w1 if mode == LK.PAIR else None
+        full = torch.ones(4, 64, device=dev)
+        assert LK.qgemv(w0, x8, dx, sx, full, mode, w1=pw) == "mfma"
+        fullf = torch.ones(4, 64, device=dev)
+        LK.qgemv(w0, None, None, None, fullf, mode, w1=pw, xf=x, norm_w=nw)
+        for T in (1, 2, 3):
+            part = torch.ones(T, 64, device=dev)
+            LK.qgemv(w0, x8[:T], dx[:T], sx[:T], part, mode, w1=pw)
+            assert torch.equal(part, full[:T]), (mode, T)
+            partf = torch.ones(T, 64, device=dev)
+            LK.qgemv(w0, None, None, None, partf, mode, w1=pw, xf=x[:T], norm_w=nw)
+            assert torch.equal(partf, fullf[:T]), (mode, T, "xf")
+
+
+@pytest.mark.parametrize("T", [1, 4])
+def test_mfma_pair_q8_output_and_valu_agreement(dev, LK, T):
+    """MFMA pair GEMV with Q8 output: same contract as the VALU kernel's (scales match the fp32
+    output quantised separately, int8 within one step), and MFMA vs VALU fp32 outputs agree to
+    rounding."""
+    from k8s_nvidia_gpus_amd.models.llm import gguf
+
+    N, K = 512, 3584
+    w0, _ = _qw(N, K, gguf.Q4_K, 41, dev)
+    w1, _ = _qw(N, K, gguf.Q4_K, 42, dev)
+    assert w0.mfma_pack() and w1.mfma_pack()
+    x = torch.randn(T, K, device=dev)
+    x8, dx, sx, _ = _q8(x, LK)
+    valu = torch.empty(T, N, device=dev)
+    assert LK.qgemv(w0, x8, dx, sx, valu, LK.PAIR, w1=w1) == "valu"
+    prev = LK.gemv_impl(LK.GEMV_MFMA)
+    try:
+        out = torch.empty(T, N, device=dev)
+        assert LK.qgemv(w0, x8, dx, sx, out, LK.PAIR, w1=w1) == "mfma"
+        o8 = torch.empty(T, N, dtype=torch.int8, device=dev)
+        odx = torch.empty(T, N // 32, device=dev)
+        osx = torch.empty(T, N // 16, device=dev)
+        junk = torch.full((T, N), 7.0, device=dev)
+        LK.qgemv(w0, x8, dx, sx, junk, LK.PAIR, w1=w1, q8_out=(o8, odx, osx))
+    finally:
+        LK.gemv_impl(prev)
+    torch.testing.assert_close(out, valu, rtol=1e-4, atol=1e-5)
+    r8, rdx, _, _ = _q8(out, LK)
+    torch.testing.assert_close(odx, rdx, rtol=1e-6, atol=0)
+    assert int((o8.int() - r8.int()).abs().max()) <= 1
+    sums = (o8.float().view(T, N // 16, 16).sum(-1)) * odx.repeat_interleave(2, -1)
+    torch.testing.assert_close(osx, sums, rtol=1e-5, atol=1e-5)
+    assert bool((junk == 7.0).all())
+
+
 def _attn_ref(q, kc, vc, pos, slot, H, Hkv):
     T = q.shape[0]
     G = H // Hkv

@@ -29,6 +29,7 @@ import torch  # noqa: E402
 from k8s_nvidia_gpus_amd.models.llm import QWEN25_7B  # noqa: E402
 from k8s_nvidia_gpus_amd.models.llm.engine import Engine  # noqa: E402
 from k8s_nvidia_gpus_amd.models.llm.weights import ModelWeights  # noqa: E402
+from k8s_nvidia_gpus_amd.ops import llm_kernels as LK  # noqa: E402
 
 
 def heartbeat(period=30.0):
@@ -45,6 +46,8 @@ def heartbeat(period=30.0):
 GEMV_CASES = ("qkv", "o_proj", "gate_up", "gate_up_q8", "down_q4k", "down_q6k", "lm_head")
 GEMV_CFGS = [(0, 0), (4, 4), (4, 16), (4, 32), (8, 8), (8, 16), (8, 32), (2, 4), (2, 8),
              (1, 2), (1, 4), (8, 7), (4, 7), (8, 14), (4, 37), (8, 37), (8, 74), (4, 74)]
+# MFMA GEMV: (K-waves, rows per workgroup = 16 x row groups)
+MFMA_CFGS = [(0, 0), (1, 64), (2, 16), (2, 32), (4, 16), (4, 32), (8, 16)]
 
 
 def bench_gemv(eng: Engine, iters: int = 56, sweep4: bool = False, only=GEMV_CASES,
@@ -88,6 +91,8 @@ def bench_gemv(eng: Engine, iters: int = 56, sweep4: bool = False, only=GEMV_CAS
             todo = cfgs if (T == 1 or sweep4) else cfgs[:1]
             if name == "gate_up_q8":          # 32 rows per workgroup are fixed there
                 todo = [(wv, 0) for wv in (0, 2, 4, 8)]
+            if LK.gemv_impl() == LK.GEMV_MFMA and w.mfma is not None:
+                todo = MFMA_CFGS if name != "gate_up_q8" else [(0, 0), (2, 32), (4, 32), (8, 32)]
             for waves, rpw in todo:
                 def launch(i):
                     w0, w1 = mats[i % len(mats)]
@@ -169,8 +174,12 @@ def main(argv=None) -> int:
     ap.add_argument("--gemv-sweep4", action="store_true", help="also sweep the decomposition at T=4")
     ap.add_argument("--gemv-cases", default=",".join(GEMV_CASES), help="GEMV shapes to time")
     ap.add_argument("--kernels", action="store_true", help="time the non-GEMV decode kernels")
+    ap.add_argument("--gemv-impl", choices=["valu", "mfma"],
+                    default=os.environ.get("AMDK8S_LLM_GEMV_IMPL", "valu"),
+                    help="Q4_K GEMV kernel (A/B; env AMDK8S_LLM_GEMV_IMPL)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
+    LK.gemv_impl(LK.GEMV_MFMA if args.gemv_impl == "mfma" else LK.GEMV_VALU)
     if not torch.cuda.is_available():
         print("llm_bench needs an MI355X", file=sys.stderr)
         return 2
@@ -226,6 +235,7 @@ def main(argv=None) -> int:
     if args.kernels:
         res["kernels"] = bench_small_kernels(eng)
     res["graph_captures"] = eng.stats["graph_captures"]
+    res["gemv_impl"] = args.gemv_impl
     line = json.dumps(res)
     print(line, flush=True)
     if args.out:
