@@ -109,6 +109,7 @@ class Engine:
         # stays batch-invariant (models with dim >= 8192 run 8-wave GEMVs there: one path for every
         # T).  Attribute, not a knob: the batch-invariance test runs both paths.
         self.norm_prologue = True
+        self.norm_prologue_t = NORM_PROLOGUE_T
         # dense prefill on the fused glue kernels (llm_prefill.hip), SDPA's GQA path on the cache
         # slabs and q stored token-major (no transpose copy before o_proj); the PyTorch formulation
         # (prefill_native = False) is the oracle of test_native_prefill_equals_torch_prefill
@@ -318,7 +319,7 @@ class Engine:
         qd = self._q8(b, c.dim)
         qf = (b.x8f, b.dxf, b.sxf)
         scale = 1.0 / math.sqrt(c.head_dim)
-        pro = self.norm_prologue and (c.dim >= 8192 or b.T <= NORM_PROLOGUE_T)
+        pro = self.norm_prologue and (c.dim >= 8192 or b.T <= self.norm_prologue_t)
 
         def act(xf, norm_w):
             """GEMV input: (Q8 views, {}) quantised here, or ((None,) * 3, prologue kwargs)."""

@@ -1722,9 +1722,9 @@ void gemv_shape(int type, int N, int K, int T, int& waves, int& rows) {
                ? 16 : 8;
 }
 
-// MFMA GEMV launch shapes: pair (gate|up) 2 row groups x 2 K-waves (a whole 32-row Q8 block per
-// workgroup); long rows (K >= 8192: ffn_down) 1 x 8; very tall matrices (lm_head) 4 x 1; the rest
-// 1 x 2.  4 = shape not covered (N % 16, fewer super-blocks than K-waves, LDS): use qgemv_kernel.
+// MFMA GEMV launch shapes (K-waves x row groups, swept with tools/llm_bench.py --gemv, profiles/r04/l):
+// pair (gate|up) 2 x 2 (a whole 32-row Q8 block per workgroup); long rows (K >= 8192: ffn_down)
+// 8 x 1; very tall matrices (lm_head) 2 x 2; the rest 2 x 1 (4 x 1 with the fp32 prologue).  4 = shape not covered (N % 16, fewer super-blocks than K-waves, LDS): use qgemv_kernel.
 template <int TYPE, int T, int MODE, int KW, int RG>
 int launch_mfma_one(const GemvArgs& a, hipStream_t st) {
   constexpr int D = 3;
@@ -1741,8 +1741,11 @@ template <int TYPE, int T, int MODE>
 int launch_mfma(const GemvArgs& a, int kw, int rg, hipStream_t st) {
   if (a.N % 16) return 4;
   if (kw <= 0) {                                     // default shape
-    kw = MODE == kPair ? 2 : a.K >= 8192 ? 8 : a.N >= 65536 ? 1 : 2;
-    rg = MODE == kPair ? 2 : kw == 1 ? 4 : 1;
+    kw = MODE == kPair ? 2 : a.K >= 8192 ? 8 : 2;
+    rg = MODE == kPair || a.N >= 65536 ? 2 : 1;      // lm_head: 75.0 / 80.2 us at T = 1 / 4
+    // fp32 input: the RMSNorm prologue reduces over 4 waves in rmsnorm_q8's order (stage_x), so
+    // a prologue-normalised row quantises to the same bits as a rmsnorm_q8 one (batch invariance)
+    if (a.xf && kw * rg != 4 && a.K < 8192) kw = 4, rg = 1;
   }
   if (MODE == kPair && a.ox8 && rg != 2) return 2;   // a whole 32-row Q8 block per workgroup
   switch (kw * 8 + rg) {

@@ -90,7 +90,7 @@ def attn_chunk() -> int:
 
 
 GEMV_VALU, GEMV_MFMA = 0, 1
-_GEMV = [GEMV_VALU]
+_GEMV = [GEMV_MFMA]
 
 
 def gemv_impl(impl: int = None) -> int:

@@ -414,20 +414,24 @@ def test_two_matrix_gemv_fp32_prologue(dev, LK, T):
     torch.testing.assert_close(out, ref, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("packed", [False, True])
 @pytest.mark.parametrize("K", [512, 3584])
 @pytest.mark.parametrize("T", [1, 2, 3, 4])
-def test_prologue_norm_equals_rmsnorm_kernel(dev, LK, K, T):
+def test_prologue_norm_equals_rmsnorm_kernel(dev, LK, K, T, packed):
     """RMSNorm + Q8 inside a 4-wave GEMV prologue and rmsnorm_q8 followed by the Q8-input GEMV
     give the same bits (the engine normalises small steps in the prologue and large ones with
     rmsnorm_q8: batch invariance rests on this)."""
     from k8s_nvidia_gpus_amd.models.llm import gguf
 
     w, _ = _qw(512, K, gguf.Q4_K, 14, dev)
+    if packed:                       # the MFMA kernel (default implementation) reads this copy
+        assert w.mfma_pack()
     torch.manual_seed(20 + T)
     xf = torch.randn(T, K, device=dev) * 3
     nw = torch.rand(K, device=dev) + 0.5
     a = torch.zeros(T, 512, device=dev)
-    LK.qgemv(w, None, None, None, a, LK.STORE, xf=xf, norm_w=nw, eps=1e-6)
+    ran = LK.qgemv(w, None, None, None, a, LK.STORE, xf=xf, norm_w=nw, eps=1e-6)
+    assert ran == ("mfma" if packed and LK.gemv_impl() == LK.GEMV_MFMA else "valu")
     x8 = torch.empty(T, K, dtype=torch.int8, device=dev)
     dx = torch.empty(T, K // 32, device=dev)
     sx = torch.empty(T, K // 16, device=dev)
@@ -470,7 +474,7 @@ def tiny_gguf(tmp_path_factory):
 
 
 @pytest.mark.parametrize("norm_prologue", [False, True])
-def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf, norm_prologue):
+def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf, norm_prologue, gemv):
     from k8s_nvidia_gpus_amd.models.llm.synthetic import load
 
     gpu, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=False)
@@ -493,8 +497,18 @@ def test_engine_native_decode_matches_fp32_reference(dev, tiny_gguf, norm_prolog
     assert gpu.stats["graph_captures"] >= 1
 
 
+@pytest.fixture(params=["mfma", "valu"])
+def gemv(request, dev):
+    """Engine GEMV implementation for the test (set before the engine packs its weights)."""
+    from k8s_nvidia_gpus_amd.ops import llm_kernels as LK
+
+    prev = LK.gemv_impl(LK.GEMV_MFMA if request.param == "mfma" else LK.GEMV_VALU)
+    yield request.param
+    LK.gemv_impl(prev)
+
+
 @pytest.mark.parametrize("norm_prologue", [False, True])
-def test_engine_batched_decode_equals_single(dev, tiny_gguf, norm_prologue):
+def test_engine_batched_decode_equals_single(dev, tiny_gguf, norm_prologue, gemv):
     """T sequences in one step give the same logits as each alone: slots are independent and the
     GEMV's roundings are pinned, so the int8 activation quantisation never flips between a batched
     and a single step (batch-invariant serving) — the batched step normalises with rmsnorm_q8, the

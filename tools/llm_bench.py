@@ -175,8 +175,12 @@ def main(argv=None) -> int:
     ap.add_argument("--gemv-cases", default=",".join(GEMV_CASES), help="GEMV shapes to time")
     ap.add_argument("--kernels", action="store_true", help="time the non-GEMV decode kernels")
     ap.add_argument("--gemv-impl", choices=["valu", "mfma"],
-                    default=os.environ.get("AMDK8S_LLM_GEMV_IMPL", "valu"),
+                    default=os.environ.get("AMDK8S_LLM_GEMV_IMPL", "mfma"),
                     help="Q4_K GEMV kernel (A/B; env AMDK8S_LLM_GEMV_IMPL)")
+    ap.add_argument("--norm-prologue-t", type=int,
+                    default=int(os.environ.get("AMDK8S_LLM_NORM_PROLOGUE_T", "0")),
+                    help="A/B: steps of up to this many tokens normalise in the GEMV prologues "
+                         "(0 = the engine default; env AMDK8S_LLM_NORM_PROLOGUE_T)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
     LK.gemv_impl(LK.GEMV_MFMA if args.gemv_impl == "mfma" else LK.GEMV_VALU)
@@ -192,6 +196,8 @@ def main(argv=None) -> int:
     w = ModelWeights.random(cfg, device=dev, seed=0)
     torch.cuda.synchronize()
     eng = Engine(w, max_ctx=args.ctx, slots=4, dense=True)
+    if args.norm_prologue_t:
+        eng.norm_prologue_t = args.norm_prologue_t
     eng.dense_weights()
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t0
@@ -236,6 +242,7 @@ def main(argv=None) -> int:
         res["kernels"] = bench_small_kernels(eng)
     res["graph_captures"] = eng.stats["graph_captures"]
     res["gemv_impl"] = args.gemv_impl
+    res["norm_prologue_t"] = eng.norm_prologue_t
     line = json.dumps(res)
     print(line, flush=True)
     if args.out:
