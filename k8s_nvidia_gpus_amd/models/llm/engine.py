@@ -124,12 +124,13 @@ class Engine:
             self.LK = LK
             self.max_T = LK.max_tokens()
             if LK.gemv_impl() == LK.GEMV_MFMA:
-                # Q4_K GEMVs on the int8 matrix cores: every qualifying matrix gets its packed copy
-                # (the VALU kernel keeps the others, and the two-matrix q|k|v launch)
-                for L in self.w.layers:
-                    for w in [L.wo, L.wg, L.wu, L.wd] + list(L.wqkv):
-                        w.mfma_pack()
-                self.w.output.mfma_pack()
+                # GEMVs on the int8 matrix cores: every matrix gets its MFMA-packed copy (the VALU
+                # kernel keeps the two-type q|k + v launch up to 4 tokens, and any matrix with
+                # N % 16 — steps then stay at the VALU kernel's 4 tokens)
+                mats = [self.w.output] + [w for L in self.w.layers
+                                          for w in [L.wo, L.wg, L.wu, L.wd] + list(L.wqkv)]
+                if not all([w.mfma_pack() for w in mats]):
+                    self.max_T = min(self.max_T, 4)
         else:
             self.max_T = 4
         self.stats = {"decode_steps": 0, "decode_tokens": 0, "prefill_tokens": 0,

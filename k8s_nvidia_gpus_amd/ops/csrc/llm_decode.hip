@@ -37,7 +37,8 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kQ4KBytes = 144;
-constexpr int kMaxTok = 4;          // tokens per GEMV launch (activations staged in LDS)
+constexpr int kMaxTok = 8;          // tokens per decode step (MFMA GEMV: two quads of 4 per wave)
+constexpr int kValuMaxTok = 4;      // tokens per VALU GEMV launch (activations staged in LDS)
 constexpr int kAttnChunk = 64;      // context positions per decode-attention workgroup
 constexpr int kHeadDim = 128;
 constexpr int kMaxGroup = 8;        // q heads per kv head
@@ -485,7 +486,7 @@ __device__ __forceinline__ XView stage_x(const GemvArgs& a, uint8_t* lds) {
         }
       }
     }
-  } else {
+  } else if constexpr (T <= kValuMaxTok) {
     // fp32 input (+ RMSNorm): every workgroup normalises and quantises the (L2-resident) rows
     // itself, which removes a launch and its boundary per matrix.  All T tokens are processed
     // together (their loads in flight at once); per token the thread mapping and reduction order
@@ -860,7 +861,7 @@ __device__ __forceinline__ float mfma_block(const MBlk<TYPE>& w, const i32x4 (&x
 
 // LDS after stage_x's arrays: [W][T] prologue scratch (rounded to 16 B), the per-type activation
 // sums (Q4_K sxp float [T][K/32], Q6_K X int [T][K/16]), 256 zero bytes (the A operand of
-// inactive lanes), the K-split partials [waves][P][64], q8s [T][32].
+// inactive lanes), the K-split partials [waves][token quads][P][64], q8s [T][32].
 struct MfmaLds { int aux, zero, kred, q8s, total; };
 __host__ __device__ inline MfmaLds mfma_lds(int type, int T, int K, int waves, int P) {
   MfmaLds L;
@@ -870,16 +871,20 @@ __host__ __device__ inline MfmaLds mfma_lds(int type, int T, int K, int waves, i
   L.aux = base + red;
   L.zero = L.aux + T * (type == kQ6K ? K >> 4 : K >> 5) * 4;
   L.kred = L.zero + 256;
-  L.q8s = L.kred + waves * P * 64 * 4;
+  L.q8s = L.kred + waves * ((T + 3) / 4) * P * 64 * 4;
   L.total = L.q8s + T * 32 * 4;
   return L;
 }
 
+// gate|up (pair, <= 4 tokens): 592 4-wave workgroups need 3 waves per SIMD to be co-resident
 template <int TYPE, int T, int MODE, int KW, int RG, int D>
-__global__ void __launch_bounds__(KW * RG * 64) qgemv_mfma_kernel(GemvArgs a) {
+__global__ void __launch_bounds__(KW * RG * 64)
+__attribute__((amdgpu_waves_per_eu(MODE == kPair && T <= 4 ? 3 : 1, 8)))
+qgemv_mfma_kernel(GemvArgs a) {
   extern __shared__ __align__(16) uint8_t lds[];
   constexpr int P = MODE == kPair ? 2 : 1;
   constexpr int NA = TYPE == kQ6K ? 4 : 2;          // uint4 of activation sums per block
+  constexpr int NQ = (T + 3) / 4;                   // token quads: MFMA M = 4 tokens x 4 K-groups
   const int K = a.K, nb = K >> 8;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int rg = wave / KW, kw = wave % KW;
@@ -914,39 +919,50 @@ __global__ void __launch_bounds__(KW * RG * 64) qgemv_mfma_kernel(GemvArgs a) {
   }
   if (threadIdx.x < 16) reinterpret_cast<uint4*>(lds + L.zero)[threadIdx.x] = make_uint4(0, 0, 0, 0);
   __syncthreads();
-  // A operand: lane l is row (t, s) = ((l & 15) >> 2, l & 3) of K-group g; live only for s == g.
-  // MFMA m's 16 activations: Q4_K +0 / +32 / +128 / +160 from 64 (g >> 1) + 16 (g & 1);
-  // Q6_K +0 / +64 / +128 / +192 from 16 g (zero lanes: the zero bytes)
-  const int at = (lane & 15) >> 2;
-  const bool live = (lane & 3) == g && at < T;
+  // A operand of quad q: lane l is row (t, s) = (4q + ((l & 15) >> 2), l & 3) of K-group g; live
+  // only for s == g.  MFMA m's 16 activations: Q4_K +0 / +32 / +128 / +160 from
+  // 64 (g >> 1) + 16 (g & 1); Q6_K +0 / +64 / +128 / +192 from 16 g (zero lanes: the zero bytes)
   const int xb = TYPE == kQ6K ? 16 * g : 64 * (g >> 1) + 16 * (g & 1);
-  const int xa0 = live ? at * xv.xstride + xb : L.zero;
-  const int xstep = live ? 288 : 0;
-  const int xo1 = live ? (TYPE == kQ6K ? 64 : 32) : 0;
-  const int xo2 = live ? 128 : 0;
-  const int xo3 = live ? (TYPE == kQ6K ? 192 : 160) : 0;
-  const int tt = min(g, T - 1);                      // this lane's output token
-  const float* dxb = xv.dxs + tt * (K >> 5);
-  const uint4* axb = reinterpret_cast<const uint4*>(lds + L.aux) + tt * nb * NA;
-  float acc = 0.f, acc1 = 0.f;
+  int xa0[NQ], xstep[NQ], xo1[NQ], xo2[NQ], xo3[NQ];
+  const float* dxb[NQ];
+  const uint4* axb[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int at = 4 * q + ((lane & 15) >> 2);
+    const bool live = (lane & 3) == g && at < T;
+    xa0[q] = live ? at * xv.xstride + xb : L.zero;
+    xstep[q] = live ? 288 : 0;
+    xo1[q] = live ? (TYPE == kQ6K ? 64 : 32) : 0;
+    xo2[q] = live ? 128 : 0;
+    xo3[q] = live ? (TYPE == kQ6K ? 192 : 160) : 0;
+    const int tt = min(4 * q + g, T - 1);            // this lane's output token in quad q
+    dxb[q] = xv.dxs + tt * (K >> 5);
+    axb[q] = reinterpret_cast<const uint4*>(lds + L.aux) + tt * nb * NA;
+  }
+  float acc[NQ], acc1[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) acc[q] = acc1[q] = 0.f;
   auto compute = [&](const MBlk<TYPE>& q0, const MBlk<TYPE>& q1, int i) {
     const int kb = kb0 + i;
-    const uint8_t* xp = lds + xa0 + kb * xstep;
-    i32x4 xa[4];
-    xa[0] = *reinterpret_cast<const i32x4*>(xp);
-    xa[1] = *reinterpret_cast<const i32x4*>(xp + xo1);
-    xa[2] = *reinterpret_cast<const i32x4*>(xp + xo2);
-    xa[3] = *reinterpret_cast<const i32x4*>(xp + xo3);
-    float dxv[8];
-    const float4 d0 = *reinterpret_cast<const float4*>(dxb + kb * 8);
-    const float4 d1 = *reinterpret_cast<const float4*>(dxb + kb * 8 + 4);
-    dxv[0] = d0.x; dxv[1] = d0.y; dxv[2] = d0.z; dxv[3] = d0.w;
-    dxv[4] = d1.x; dxv[5] = d1.y; dxv[6] = d1.z; dxv[7] = d1.w;
-    uint4 aux[4];
 #pragma unroll
-    for (int u = 0; u < NA; ++u) aux[u] = axb[kb * NA + u];
-    acc = mfma_block<TYPE>(q0, xa, dxv, aux, g, acc);
-    if constexpr (P == 2) acc1 = mfma_block<TYPE>(q1, xa, dxv, aux, g, acc1);
+    for (int q = 0; q < NQ; ++q) {
+      const uint8_t* xp = lds + xa0[q] + kb * xstep[q];
+      i32x4 xa[4];
+      xa[0] = *reinterpret_cast<const i32x4*>(xp);
+      xa[1] = *reinterpret_cast<const i32x4*>(xp + xo1[q]);
+      xa[2] = *reinterpret_cast<const i32x4*>(xp + xo2[q]);
+      xa[3] = *reinterpret_cast<const i32x4*>(xp + xo3[q]);
+      float dxv[8];
+      const float4 d0 = *reinterpret_cast<const float4*>(dxb[q] + kb * 8);
+      const float4 d1 = *reinterpret_cast<const float4*>(dxb[q] + kb * 8 + 4);
+      dxv[0] = d0.x; dxv[1] = d0.y; dxv[2] = d0.z; dxv[3] = d0.w;
+      dxv[4] = d1.x; dxv[5] = d1.y; dxv[6] = d1.z; dxv[7] = d1.w;
+      uint4 aux[4];
+#pragma unroll
+      for (int u = 0; u < NA; ++u) aux[u] = axb[q][kb * NA + u];
+      acc[q] = mfma_block<TYPE>(q0, xa, dxv, aux, g, acc[q]);
+      if constexpr (P == 2) acc1[q] = mfma_block<TYPE>(q1, xa, dxv, aux, g, acc1[q]);
+    }
   };
   // Whole groups of D steps: every step first refills the slot consumed one step ago with block
   // i + D - 1 (clamped: the last group re-reads the final block from L2), then computes slot d.
@@ -972,31 +988,43 @@ __global__ void __launch_bounds__(KW * RG * 64) qgemv_mfma_kernel(GemvArgs a) {
   for (int d = 0; d < D - 1; ++d)
     if (i0 + d < n) compute(w0[d], w1[d], i0 + d);
   // K-split partials: wave kw = 0 of each row group adds its group's in wave order
-  float v = acc, v1 = acc1;
+  float v[NQ], v1[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) v[q] = acc[q], v1[q] = acc1[q];
   if constexpr (KW > 1) {
-    float* kred = reinterpret_cast<float*>(lds + L.kred);
-    kred[(wave * P) * 64 + lane] = acc;
-    if constexpr (P == 2) kred[(wave * P + 1) * 64 + lane] = acc1;
+    float* kred = reinterpret_cast<float*>(lds + L.kred);      // [waves][NQ][P][64]
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      kred[((wave * NQ + q) * P) * 64 + lane] = acc[q];
+      if constexpr (P == 2) kred[((wave * NQ + q) * P + 1) * 64 + lane] = acc1[q];
+    }
     __syncthreads();
     if (kw == 0) {
-      v = 0.f; v1 = 0.f;
 #pragma unroll
-      for (int k = 0; k < KW; ++k) {
-        v += kred[((rg * KW + k) * P) * 64 + lane];
-        if constexpr (P == 2) v1 += kred[((rg * KW + k) * P + 1) * 64 + lane];
+      for (int q = 0; q < NQ; ++q) {
+        v[q] = 0.f; v1[q] = 0.f;
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+          v[q] += kred[(((rg * KW + k) * NQ + q) * P) * 64 + lane];
+          if constexpr (P == 2) v1[q] += kred[(((rg * KW + k) * NQ + q) * P + 1) * 64 + lane];
+        }
       }
     }
   }
   float* q8s = (MODE == kPair && a.ox8) ? reinterpret_cast<float*>(lds + L.q8s) : nullptr;
   const int orow = wrow0 + rg * 16 + r;
-  if (kw == 0 && g < T && orow < a.N) {
-    float* o = a.out + (long)g * a.ldo + orow;
-    if constexpr (MODE == kStore) *o = v + (a.bias ? a.bias[orow] : 0.f);
-    else if constexpr (MODE == kResid) *o += v;
-    else {
-      const float y = v / (1.f + __expf(-v)) * v1;
-      if (q8s) q8s[g * 32 + rg * 16 + r] = y;
-      else *o = y;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int t = 4 * q + g;
+    if (kw == 0 && t < T && orow < a.N) {
+      float* o = a.out + (long)t * a.ldo + orow;
+      if constexpr (MODE == kStore) *o = v[q] + (a.bias ? a.bias[orow] : 0.f);
+      else if constexpr (MODE == kResid) *o += v[q];
+      else {
+        const float y = v[q] / (1.f + __expf(-v[q])) * v1[q];
+        if (q8s) q8s[t * 32 + rg * 16 + r] = y;
+        else *o = y;
+      }
     }
   }
   if constexpr (MODE == kPair && RG == 2) {
@@ -1727,7 +1755,7 @@ void gemv_shape(int type, int N, int K, int T, int& waves, int& rows) {
 // 8 x 1; very tall matrices (lm_head) 2 x 2; the rest 2 x 1 (4 x 1 with the fp32 prologue).  4 = shape not covered (N % 16, fewer super-blocks than K-waves, LDS): use qgemv_kernel.
 template <int TYPE, int T, int MODE, int KW, int RG>
 int launch_mfma_one(const GemvArgs& a, hipStream_t st) {
-  constexpr int D = 3;
+  constexpr int D = MODE == kPair ? 2 : 3;          // pair: two matrices per slot (VGPR budget)
   if ((a.K >> 8) < KW) return 4;
   const MfmaLds L = mfma_lds(TYPE, T, a.K, KW * RG, MODE == kPair ? 2 : 1);
   if (L.total > 160 * 1024) return 4;
@@ -1767,8 +1795,31 @@ int dispatch_mfma(const GemvArgs& a, int kw, int rg, hipStream_t st) {
     case 2: return launch_mfma<TYPE, 2, MODE>(a, kw, rg, st);
     case 3: return launch_mfma<TYPE, 3, MODE>(a, kw, rg, st);
     case 4: return launch_mfma<TYPE, 4, MODE>(a, kw, rg, st);
+    case 5: return launch_mfma<TYPE, 5, MODE>(a, kw, rg, st);
+    case 6: return launch_mfma<TYPE, 6, MODE>(a, kw, rg, st);
+    case 7: return launch_mfma<TYPE, 7, MODE>(a, kw, rg, st);
+    case 8: return launch_mfma<TYPE, 8, MODE>(a, kw, rg, st);
     default: return 2;
   }
+}
+
+// More than 4 tokens whose activations do not fit the LDS with T (ffn_down's K = 18944 at T > 4):
+// tokens [0, 4) and [4, T) as two launches.  Every token's arithmetic is the same in either form.
+template <int TYPE, int MODE>
+int dispatch_mfma_split(const GemvArgs& a, int kw, int rg, hipStream_t st) {
+  const int rc = dispatch_mfma<TYPE, MODE>(a, kw, rg, st);
+  if (rc != 4 || a.T <= 4) return rc;
+  GemvArgs lo = a, hi = a;
+  lo.T = 4;
+  hi.T = a.T - 4;
+  const long K = a.K;
+  if (hi.x8) { hi.x8 += 4 * K; hi.dx += 4 * (K >> 5); hi.sx += 4 * (K >> 4); }
+  if (hi.xf) hi.xf += 4L * a.ldx;
+  hi.out += 4L * a.ldo;
+  if (hi.ox8) { hi.ox8 += 4L * a.N; hi.odx += 4L * (a.N >> 5); hi.osx += 4L * (a.N >> 4); }
+  const int r0 = dispatch_mfma<TYPE, MODE>(lo, kw, rg, st);
+  if (r0) return r0;
+  return dispatch_mfma<TYPE, MODE>(hi, kw, rg, st);
 }
 
 
@@ -1788,7 +1839,8 @@ int amdk8s_llm_qgemv(int type, int mode, const void* w0q, const void* w0qh, cons
                      const void* xf, int ldx, const void* norm_w, float eps,
                      const void* bias, void* out, int ldo, int N, int K, int T, int waves,
                      int rows_per_wg, void* ox8, void* odx, void* osx, void* stream) {
-  if (K % 256 || N <= 0 || T < 1 || T > kMaxTok) return 2;
+  if (T > kValuMaxTok) return 4;                // more tokens: the MFMA GEMV only
+  if (K % 256 || N <= 0 || T < 1) return 2;
   if (mode == kPair && !w1q) return 2;
   if (ox8) {                                  // pair → Q8 output: whole 32-row blocks per workgroup
     if (mode != kPair || N % 32 || !odx || !osx) return 2;
@@ -1845,7 +1897,7 @@ int amdk8s_llm_qgemv_mfma(int type, int mode, const void* w0q, const void* w0qh,
   if (type != kQ4K && type != kQ6K) return 2;
   if (mode == kPair && !w1q) return 2;
   if (!xf && !(x8 && dx && sx)) return 2;
-  if (xf && ldx % 4) return 2;
+  if (xf && (ldx % 4 || T > kValuMaxTok)) return 2;  // fp32-row prologue: steps of <= 4 tokens
   if (ox8 && (mode != kPair || N % 32 || !odx || !osx)) return 2;
   GemvArgs a{};
   a.w0 = {static_cast<const uint8_t*>(w0q), static_cast<const uint8_t*>(w0qh),
@@ -1869,13 +1921,13 @@ int amdk8s_llm_qgemv_mfma(int type, int mode, const void* w0q, const void* w0qh,
   if (rg == 0) kw = 0;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (type == kQ4K) {
-    if (mode == kStore) return dispatch_mfma<kQ4K, kStore>(a, kw, rg, st);
-    if (mode == kResid) return dispatch_mfma<kQ4K, kResid>(a, kw, rg, st);
-    if (mode == kPair) return dispatch_mfma<kQ4K, kPair>(a, kw, rg, st);
+    if (mode == kStore) return dispatch_mfma_split<kQ4K, kStore>(a, kw, rg, st);
+    if (mode == kResid) return dispatch_mfma_split<kQ4K, kResid>(a, kw, rg, st);
+    if (mode == kPair) return dispatch_mfma_split<kQ4K, kPair>(a, kw, rg, st);
   } else {
-    if (mode == kStore) return dispatch_mfma<kQ6K, kStore>(a, kw, rg, st);
-    if (mode == kResid) return dispatch_mfma<kQ6K, kResid>(a, kw, rg, st);
-    if (mode == kPair) return dispatch_mfma<kQ6K, kPair>(a, kw, rg, st);
+    if (mode == kStore) return dispatch_mfma_split<kQ6K, kStore>(a, kw, rg, st);
+    if (mode == kResid) return dispatch_mfma_split<kQ6K, kResid>(a, kw, rg, st);
+    if (mode == kPair) return dispatch_mfma_split<kQ6K, kPair>(a, kw, rg, st);
   }
   return 2;
 }
@@ -1912,7 +1964,8 @@ int amdk8s_llm_qgemv2(int type0, const void* w0q, const void* w0qh, const void* 
                       const void* bias1, void* out1, int ldo, const void* x8, const void* dx,
                       const void* sx, const void* xf, int ldx, const void* norm_w, float eps,
                       int K, int T, int waves, int rows_per_wg, void* stream) {
-  if (K % 256 || N0 <= 0 || N1 <= 0 || T < 1 || T > kMaxTok) return 2;
+  if (T > kValuMaxTok) return 4;
+  if (K % 256 || N0 <= 0 || N1 <= 0 || T < 1) return 2;
   if (!xf && !(x8 && dx && sx)) return 2;
   if (xf && ldx % 4) return 2;
   if ((type0 != kQ4K && type0 != kQ6K) || (type1 != kQ4K && type1 != kQ6K)) return 2;

@@ -205,7 +205,7 @@ def mfma(LK):
 
 
 @pytest.mark.parametrize("qt", ["Q4_K", "Q6_K"])
-@pytest.mark.parametrize("T", [1, 2, 3, 4])
+@pytest.mark.parametrize("T", [1, 2, 3, 4, 5, 8])
 @pytest.mark.parametrize("mode", ["store", "resid", "pair"])
 @pytest.mark.parametrize("N,K", [(320, 1536), (256, 3584), (96, 18944), (65536, 512)])
 def test_mfma_gemv_vs_fp32(dev, mfma, qt, T, mode, N, K):
@@ -250,22 +250,23 @@ def test_mfma_gemv_batch_invariant(dev, mfma, qt, K):
     w1, _ = _qw(64, K, getattr(gguf, qt), 32, dev)
     assert w0.mfma_pack() and w1.mfma_pack()
     torch.manual_seed(K + 1)
-    x = torch.randn(4, K, device=dev)
+    x = torch.randn(8, K, device=dev)
     nw = torch.rand(K, device=dev) + 0.5
     x8, dx, sx, _ = _q8(x, LK)
     for mode in (LK.STORE, LK.RESID, LK.PAIR):
         pw = w1 if mode == LK.PAIR else None
-        full = torch.ones(4, 64, device=dev)
+        full = torch.ones(8, 64, device=dev)       # 8 tokens: two quads (K = 18944: two launches)
         assert LK.qgemv(w0, x8, dx, sx, full, mode, w1=pw) == "mfma"
         fullf = torch.ones(4, 64, device=dev)
-        LK.qgemv(w0, None, None, None, fullf, mode, w1=pw, xf=x, norm_w=nw)
-        for T in (1, 2, 3):
+        LK.qgemv(w0, None, None, None, fullf, mode, w1=pw, xf=x[:4], norm_w=nw)
+        for T in (1, 2, 3, 4, 5, 7):
             part = torch.ones(T, 64, device=dev)
             LK.qgemv(w0, x8[:T], dx[:T], sx[:T], part, mode, w1=pw)
             assert torch.equal(part, full[:T]), (mode, T)
-            partf = torch.ones(T, 64, device=dev)
-            LK.qgemv(w0, None, None, None, partf, mode, w1=pw, xf=x[:T], norm_w=nw)
-            assert torch.equal(partf, fullf[:T]), (mode, T, "xf")
+            if T <= 3:
+                partf = torch.ones(T, 64, device=dev)
+                LK.qgemv(w0, None, None, None, partf, mode, w1=pw, xf=x[:T], norm_w=nw)
+                assert torch.equal(partf, fullf[:T]), (mode, T, "xf")
 
 
 @pytest.mark.parametrize("T", [1, 4])
@@ -515,16 +516,18 @@ def test_engine_batched_decode_equals_single(dev, tiny_gguf, norm_prologue, gemv
     single one (with norm_prologue) in the GEMV prologues."""
     from k8s_nvidia_gpus_amd.models.llm.synthetic import load
 
-    eng, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=True)
+    eng, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=True, slots=8)
     eng.norm_prologue = norm_prologue
-    prompts = [tok.encode(s) for s in ("hello", "the quick brown fox", "a cozy cabin in", "you")]
+    assert eng.max_T == (8 if gemv == "mfma" else 4)
+    prompts = [tok.encode(s) for s in ("hello", "the quick brown fox", "a cozy cabin in", "you",
+                                       "dogs", "one two three four", "x", "the end")]
     last = []
     for s, p in enumerate(prompts):
         eng.prefill(p, slot=s)
         last.append((int(p[-1]), len(p)))
-    toks = [7, 8, 9, 10]
-    batch = eng.decode(toks, [n for _, n in last], [0, 1, 2, 3]).clone()
-    for s in range(4):
+    toks = [7, 8, 9, 10, 11, 12, 13, 14]
+    batch = eng.decode(toks, [n for _, n in last], list(range(8))).clone()
+    for s in range(8):
         single = eng.decode([toks[s]], [last[s][1]], [s])[0]
         torch.testing.assert_close(batch[s], single, rtol=0, atol=0)
 

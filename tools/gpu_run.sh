@@ -71,7 +71,7 @@ for step in "$@"; do
         || fail "$step" $? "$OUT/proftester.log"
       grep -v '^{' "$OUT/proftester.log" | tail -8 ;;
     llm|llm:*)
-      toks="1,2,3,4"; [[ "$step" == llm:* ]] && toks="${step#llm:}"
+      toks="1,2,3,4,8"; [[ "$step" == llm:* ]] && toks="${step#llm:}"
       n=$(ls "$OUT"/llm_bench_*.json 2>/dev/null | wc -l)
       timeout -k 10 500 python -u tools/llm_bench.py --tokens "$toks" --out "$OUT/llm_bench_$n.json" \
         > "$OUT/llm_bench_$n.log" 2>&1 || fail "$step" $? "$OUT/llm_bench_$n.log"

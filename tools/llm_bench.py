@@ -8,7 +8,7 @@ random weights (no network for the checkpoint): bytes streamed per token are tho
 
 Reports, as one JSON line:
   * weight bytes and the HBM-roofline decode time per step (bytes / 6.3 TB/s measured copy peak);
-  * decode ms/step and tokens/s for T = 1..4 concurrent sequences (HIP-graph replay, greedy
+  * decode ms/step and tokens/s for T = 1..4 and 8 concurrent sequences (HIP-graph replay, greedy
     sampling of every step on the GPU, per-step host sync as a server does);
   * prefill tokens/s for a ``--prompt``-token prompt (fp16 dense path);
   * per-GEMV-shape achieved bandwidth (``--gemv``).
@@ -169,7 +169,7 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=128, help="decode steps per T")
     ap.add_argument("--ctx", type=int, default=4096, help="KV-cache context (reference --ctx-size)")
     ap.add_argument("--prompt", type=int, default=512)
-    ap.add_argument("--tokens", default="1,2,3,4", help="decode T list ('' = no decode timing)")
+    ap.add_argument("--tokens", default="1,2,3,4,8", help="decode T list ('' = no decode timing)")
     ap.add_argument("--gemv", action="store_true")
     ap.add_argument("--gemv-sweep4", action="store_true", help="also sweep the decomposition at T=4")
     ap.add_argument("--gemv-cases", default=",".join(GEMV_CASES), help="GEMV shapes to time")
@@ -195,7 +195,7 @@ def main(argv=None) -> int:
     t0 = time.perf_counter()
     w = ModelWeights.random(cfg, device=dev, seed=0)
     torch.cuda.synchronize()
-    eng = Engine(w, max_ctx=args.ctx, slots=4, dense=True)
+    eng = Engine(w, max_ctx=args.ctx, slots=8, dense=True)
     if args.norm_prologue_t:
         eng.norm_prologue_t = args.norm_prologue_t
     eng.dense_weights()
