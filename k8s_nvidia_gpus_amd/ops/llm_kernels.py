@@ -147,10 +147,10 @@ def qgemv(w0, x8, dx, sx, out, mode: int = STORE, w1=None, bias=None, ldo: int =
     a = w0.ptrs()
     b = w1.ptrs() if w1 is not None else (None, None, None, None)
     ref = xf if xf is not None else x8
-    rc = (_lib().amdk8s_llm_qgemv(w0.qtype, mode, *a, *b, _p(x8), _p(dx), _p(sx), _p(xf),
-                                   xf.stride(0) if xf is not None else 0, _p(norm_w), float(eps),
-                                   _p(bias), out.data_ptr(), ldo, w0.n, w0.k, t,
-                                   waves, rows_per_wg, *q8, _stream(ref))
+    rc = _lib().amdk8s_llm_qgemv(w0.qtype, mode, *a, *b, _p(x8), _p(dx), _p(sx), _p(xf),
+                                 xf.stride(0) if xf is not None else 0, _p(norm_w), float(eps),
+                                 _p(bias), out.data_ptr(), ldo, w0.n, w0.k, t,
+                                 waves, rows_per_wg, *q8, _stream(ref))
     if rc == 4:
         raise RuntimeError(f"qgemv: {t} tokens need the MFMA GEMV (gemv_impl MFMA and the "
                            f"weights' mfma_pack); the VALU kernel takes at most 4")
