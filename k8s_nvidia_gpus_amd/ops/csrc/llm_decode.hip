@@ -1752,7 +1752,7 @@ void gemv_shape(int type, int N, int K, int T, int& waves, int& rows) {
 
 // MFMA GEMV launch shapes (K-waves x row groups, swept with tools/llm_bench.py --gemv, profiles/r04/l):
 // pair (gate|up) 2 x 2 (a whole 32-row Q8 block per workgroup); long rows (K >= 8192: ffn_down)
-// 8 x 1; very tall matrices (lm_head) 2 x 2; the rest 2 x 1 (4 x 1 with the fp32 prologue).  4 = shape not covered (N % 16, fewer super-blocks than K-waves, LDS): use qgemv_kernel.
+// 8 x 1; very tall matrices (lm_head) 2 x 2; the rest 4 x 1 (q|k|v, o_proj: 2 x 1 measured the same).  4 = shape not covered (N % 16, fewer super-blocks than K-waves, LDS): use qgemv_kernel.
 template <int TYPE, int T, int MODE, int KW, int RG>
 int launch_mfma_one(const GemvArgs& a, hipStream_t st) {
   constexpr int D = MODE == kPair ? 2 : 3;          // pair: two matrices per slot (VGPR budget)
@@ -1768,15 +1768,23 @@ int launch_mfma_one(const GemvArgs& a, hipStream_t st) {
 template <int TYPE, int T, int MODE>
 int launch_mfma(const GemvArgs& a, int kw, int rg, hipStream_t st) {
   if (a.N % 16) return 4;
-  if (kw <= 0) {                                     // default shape
-    kw = MODE == kPair ? 2 : a.K >= 8192 ? 8 : 2;
-    rg = MODE == kPair || a.N >= 65536 ? 2 : 1;      // lm_head: 75.0 / 80.2 us at T = 1 / 4
-    // fp32 input: the RMSNorm prologue reduces over 4 waves in rmsnorm_q8's order (stage_x), so
-    // a prologue-normalised row quantises to the same bits as a rmsnorm_q8 one (batch invariance)
-    if (a.xf && kw * rg != 4 && a.K < 8192) kw = 4, rg = 1;
+  if (kw <= 0) {
+    // Default shape: a function of the matrix only (never of T or of the input form), so each
+    // matrix sums its K-split partials in one order at every T (batch invariance), and 4 waves
+    // wherever the fp32-row prologue may run (stage_x reduces the RMSNorm over 4 waves in
+    // rmsnorm_q8's order; models with dim >= 8192 use the prologue at every T)
+    const int nb = a.K >> 8;
+    if (MODE == kPair) kw = nb >= 2 ? 2 : 1, rg = 2;
+    else if (a.K >= 8192) kw = 8, rg = 1;
+    else if (a.N >= 65536 && nb >= 2) kw = 2, rg = 2;  // lm_head: 75.0 / 80.2 us at T = 1 / 4
+    else if (nb >= 4) kw = 4, rg = 1;
+    else if (nb >= 2) kw = 2, rg = 2;
+    else kw = 1, rg = 4;
   }
   if (MODE == kPair && a.ox8 && rg != 2) return 2;   // a whole 32-row Q8 block per workgroup
+  if (MODE == kPair && a.ox8 && kw * rg * 64 < 32 * T) return 2;   // emit_q8_block: 32 lanes/token
   switch (kw * 8 + rg) {
+    case 1 * 8 + 2: return launch_mfma_one<TYPE, T, MODE, 1, 2>(a, st);
     case 1 * 8 + 4: return launch_mfma_one<TYPE, T, MODE, 1, 4>(a, st);
     case 2 * 8 + 1: return launch_mfma_one<TYPE, T, MODE, 2, 1>(a, st);
     case 2 * 8 + 2: return launch_mfma_one<TYPE, T, MODE, 2, 2>(a, st);

@@ -283,9 +283,10 @@ def test_mfma_pair_q8_output_and_valu_agreement(dev, LK, T):
     x = torch.randn(T, K, device=dev)
     x8, dx, sx, _ = _q8(x, LK)
     valu = torch.empty(T, N, device=dev)
-    assert LK.qgemv(w0, x8, dx, sx, valu, LK.PAIR, w1=w1) == "valu"
-    prev = LK.gemv_impl(LK.GEMV_MFMA)
+    prev = LK.gemv_impl(LK.GEMV_VALU)
     try:
+        assert LK.qgemv(w0, x8, dx, sx, valu, LK.PAIR, w1=w1) == "valu"
+        LK.gemv_impl(LK.GEMV_MFMA)
         out = torch.empty(T, N, device=dev)
         assert LK.qgemv(w0, x8, dx, sx, out, LK.PAIR, w1=w1) == "mfma"
         o8 = torch.empty(T, N, dtype=torch.int8, device=dev)
@@ -433,12 +434,13 @@ def test_prologue_norm_equals_rmsnorm_kernel(dev, LK, K, T, packed):
     a = torch.zeros(T, 512, device=dev)
     ran = LK.qgemv(w, None, None, None, a, LK.STORE, xf=xf, norm_w=nw, eps=1e-6)
     assert ran == ("mfma" if packed and LK.gemv_impl() == LK.GEMV_MFMA else "valu")
+    # ... and the Q8-input launch below takes the same kernel and shape (one K-split order)
     x8 = torch.empty(T, K, dtype=torch.int8, device=dev)
     dx = torch.empty(T, K // 32, device=dev)
     sx = torch.empty(T, K // 16, device=dev)
     LK.rmsnorm_q8(xf, nw, 1e-6, x8, dx, sx)
     b = torch.zeros(T, 512, device=dev)
-    LK.qgemv(w, x8, dx, sx, b, LK.STORE)
+    assert LK.qgemv(w, x8, dx, sx, b, LK.STORE) == ran
     torch.testing.assert_close(a, b, rtol=0, atol=0)
 
 
