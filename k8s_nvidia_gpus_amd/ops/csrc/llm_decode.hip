@@ -877,10 +877,9 @@ __host__ __device__ inline MfmaLds mfma_lds(int type, int T, int K, int waves, i
 }
 
 // gate|up (pair, <= 4 tokens): 592 4-wave workgroups need 3 waves per SIMD to be co-resident
+// bid = the workgroup's index within this matrix's grid
 template <int TYPE, int T, int MODE, int KW, int RG, int D>
-__global__ void __launch_bounds__(KW * RG * 64)
-__attribute__((amdgpu_waves_per_eu(MODE == kPair && T <= 4 ? 3 : 1, 8)))
-qgemv_mfma_kernel(GemvArgs a) {
+__device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid) {
   extern __shared__ __align__(16) uint8_t lds[];
   constexpr int P = MODE == kPair ? 2 : 1;
   constexpr int NA = TYPE == kQ6K ? 4 : 2;          // uint4 of activation sums per block
@@ -890,7 +889,7 @@ qgemv_mfma_kernel(GemvArgs a) {
   const int rg = wave / KW, kw = wave % KW;
   const int kb0 = kw * nb / KW, n = (kw + 1) * nb / KW - kb0;    // host: nb >= KW, so n >= 1
   const int r = lane & 15, g = lane >> 4;
-  const int wrow0 = blockIdx.x * RG * 16;
+  const int wrow0 = bid * RG * 16;
   const long rb0 = (long)(min(wrow0 + rg * 16, a.N - 16) >> 4) * nb + kb0;   // host: N % 16 == 0
   // ring of D super-blocks: D - 1 in flight before the activations are staged
   MBlk<TYPE> w0[D], w1[D];
@@ -1033,6 +1032,23 @@ qgemv_mfma_kernel(GemvArgs a) {
       emit_q8_block<T>(a, q8s, wrow0);
     }
   }
+}
+
+template <int TYPE, int T, int MODE, int KW, int RG, int D>
+__global__ void __launch_bounds__(KW * RG * 64)
+__attribute__((amdgpu_waves_per_eu(MODE == kPair && T <= 4 ? 3 : 1, 8)))
+qgemv_mfma_kernel(GemvArgs a) {
+  qgemv_mfma_body<TYPE, T, MODE, KW, RG, D>(a, blockIdx.x);
+}
+
+// Two store-mode matrices of (possibly) different types over the same input in ONE launch (q|k
+// and v of Q4_K_M): workgroups [0, grid0) run a0.  Each keeps the shape and the arithmetic it has
+// alone, so a row's bits do not depend on which launch computed it.
+template <int TYPE0, int TYPE1, int T, int KW, int RG, int D>
+__global__ void __launch_bounds__(KW * RG * 64)
+qgemv2_mfma_kernel(GemvArgs a0, GemvArgs a1, int grid0) {
+  if ((int)blockIdx.x < grid0) qgemv_mfma_body<TYPE0, T, kStore, KW, RG, D>(a0, blockIdx.x);
+  else qgemv_mfma_body<TYPE1, T, kStore, KW, RG, D>(a1, blockIdx.x - grid0);
 }
 
 // ---------------------------------------------------------------- RMSNorm + Q8 activation quant
@@ -1765,22 +1781,24 @@ int launch_mfma_one(const GemvArgs& a, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+// Default shape: a function of the matrix only (never of T or of the input form), so each matrix
+// sums its K-split partials in one order at every T (batch invariance), and 4 waves wherever the
+// fp32-row prologue may run (stage_x reduces the RMSNorm over 4 waves in rmsnorm_q8's order;
+// models with dim >= 8192 use the prologue at every T).
+void mfma_shape(bool pair, int N, int K, int& kw, int& rg) {
+  const int nb = K >> 8;
+  if (pair) kw = nb >= 2 ? 2 : 1, rg = 2;
+  else if (K >= 8192) kw = 8, rg = 1;
+  else if (N >= 65536 && nb >= 2) kw = 2, rg = 2;    // lm_head: 75.0 / 80.2 us at T = 1 / 4
+  else if (nb >= 4) kw = 4, rg = 1;
+  else if (nb >= 2) kw = 2, rg = 2;
+  else kw = 1, rg = 4;
+}
+
 template <int TYPE, int T, int MODE>
 int launch_mfma(const GemvArgs& a, int kw, int rg, hipStream_t st) {
   if (a.N % 16) return 4;
-  if (kw <= 0) {
-    // Default shape: a function of the matrix only (never of T or of the input form), so each
-    // matrix sums its K-split partials in one order at every T (batch invariance), and 4 waves
-    // wherever the fp32-row prologue may run (stage_x reduces the RMSNorm over 4 waves in
-    // rmsnorm_q8's order; models with dim >= 8192 use the prologue at every T)
-    const int nb = a.K >> 8;
-    if (MODE == kPair) kw = nb >= 2 ? 2 : 1, rg = 2;
-    else if (a.K >= 8192) kw = 8, rg = 1;
-    else if (a.N >= 65536 && nb >= 2) kw = 2, rg = 2;  // lm_head: 75.0 / 80.2 us at T = 1 / 4
-    else if (nb >= 4) kw = 4, rg = 1;
-    else if (nb >= 2) kw = 2, rg = 2;
-    else kw = 1, rg = 4;
-  }
+  if (kw <= 0) mfma_shape(MODE == kPair, a.N, a.K, kw, rg);
   if (MODE == kPair && a.ox8 && rg != 2) return 2;   // a whole 32-row Q8 block per workgroup
   if (MODE == kPair && a.ox8 && kw * rg * 64 < 32 * T) return 2;   // emit_q8_block: 32 lanes/token
   switch (kw * 8 + rg) {
@@ -1830,6 +1848,47 @@ int dispatch_mfma_split(const GemvArgs& a, int kw, int rg, hipStream_t st) {
   return dispatch_mfma<TYPE, MODE>(hi, kw, rg, st);
 }
 
+
+template <int TYPE0, int TYPE1, int T, int KW, int RG>
+int launch_mfma2_one(const GemvArgs& a0, const GemvArgs& a1, hipStream_t st) {
+  constexpr int D = 3;
+  if ((a0.K >> 8) < KW) return 4;
+  const int lds = max(mfma_lds(TYPE0, T, a0.K, KW * RG, 1).total,
+                      mfma_lds(TYPE1, T, a0.K, KW * RG, 1).total);
+  if (lds > 160 * 1024) return 4;
+  const int g0 = (a0.N + 16 * RG - 1) / (16 * RG), g1 = (a1.N + 16 * RG - 1) / (16 * RG);
+  hipLaunchKernelGGL((qgemv2_mfma_kernel<TYPE0, TYPE1, T, KW, RG, D>), dim3(g0 + g1),
+                     dim3(KW * RG * 64), lds, st, a0, a1, g0);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+template <int TYPE0, int TYPE1, int T>
+int launch_mfma2(const GemvArgs& a0, const GemvArgs& a1, hipStream_t st) {
+  if (a0.N % 16 || a1.N % 16) return 4;
+  int kw = 0, rg = 0;
+  mfma_shape(false, a0.N + a1.N, a0.K, kw, rg);
+  switch (kw * 8 + rg) {
+    case 1 * 8 + 4: return launch_mfma2_one<TYPE0, TYPE1, T, 1, 4>(a0, a1, st);
+    case 2 * 8 + 2: return launch_mfma2_one<TYPE0, TYPE1, T, 2, 2>(a0, a1, st);
+    case 4 * 8 + 1: return launch_mfma2_one<TYPE0, TYPE1, T, 4, 1>(a0, a1, st);
+    default: return 4;
+  }
+}
+
+template <int TYPE0, int TYPE1>
+int dispatch_mfma2(const GemvArgs& a0, const GemvArgs& a1, hipStream_t st) {
+  switch (a0.T) {
+    case 1: return launch_mfma2<TYPE0, TYPE1, 1>(a0, a1, st);
+    case 2: return launch_mfma2<TYPE0, TYPE1, 2>(a0, a1, st);
+    case 3: return launch_mfma2<TYPE0, TYPE1, 3>(a0, a1, st);
+    case 4: return launch_mfma2<TYPE0, TYPE1, 4>(a0, a1, st);
+    case 5: return launch_mfma2<TYPE0, TYPE1, 5>(a0, a1, st);
+    case 6: return launch_mfma2<TYPE0, TYPE1, 6>(a0, a1, st);
+    case 7: return launch_mfma2<TYPE0, TYPE1, 7>(a0, a1, st);
+    case 8: return launch_mfma2<TYPE0, TYPE1, 8>(a0, a1, st);
+    default: return 2;
+  }
+}
 
 }  // namespace
 
@@ -1960,6 +2019,46 @@ int amdk8s_llm_mfma_pack(int type, const void* q, const void* qh, const void* sc
                        static_cast<uint8_t*>(mq), static_cast<uint8_t*>(mqh),
                        static_cast<uint8_t*>(msc), static_cast<uint32_t*>(md));
   return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// amdk8s_llm_qgemv2 on the int8 matrix cores over the MFMA-packed planes (q|k and v of different
+// quantisation types in one launch, up to 8 tokens).  4 = not covered (same types, N % 16, LDS):
+// launch the matrices with amdk8s_llm_qgemv_mfma.
+int amdk8s_llm_qgemv2_mfma(int type0, const void* w0q, const void* w0qh, const void* w0sc,
+                           const void* w0d, int N0, const void* bias0, void* out0, int type1,
+                           const void* w1q, const void* w1qh, const void* w1sc, const void* w1d,
+                           int N1, const void* bias1, void* out1, int ldo, const void* x8,
+                           const void* dx, const void* sx, const void* xf, int ldx,
+                           const void* norm_w, float eps, int K, int T, void* stream) {
+  if (K % 256 || N0 <= 0 || N1 <= 0 || T < 1 || T > kMaxTok) return 2;
+  if (!xf && !(x8 && dx && sx)) return 2;
+  if (xf && (ldx % 4 || T > kValuMaxTok)) return 2;
+  if (type0 == type1 || (type0 != kQ4K && type0 != kQ6K) || (type1 != kQ4K && type1 != kQ6K))
+    return 4;
+  GemvArgs a[2];
+  const int N[2] = {N0, N1};
+  const void* q[2][4] = {{w0q, w0qh, w0sc, w0d}, {w1q, w1qh, w1sc, w1d}};
+  const void* bias[2] = {bias0, bias1};
+  void* out[2] = {out0, out1};
+  for (int i = 0; i < 2; ++i) {
+    GemvArgs& g = a[i];
+    g = GemvArgs{};
+    g.w0 = {static_cast<const uint8_t*>(q[i][0]), static_cast<const uint8_t*>(q[i][1]),
+            static_cast<const int8_t*>(q[i][2]), static_cast<const uint16_t*>(q[i][3])};
+    g.x8 = static_cast<const int8_t*>(x8);
+    g.dx = static_cast<const float*>(dx);
+    g.sx = static_cast<const float*>(sx);
+    g.xf = static_cast<const float*>(xf);
+    g.ldx = ldx;
+    g.norm_w = static_cast<const float*>(norm_w);
+    g.eps = eps;
+    g.bias = static_cast<const float*>(bias[i]);
+    g.out = static_cast<float*>(out[i]);
+    g.ldo = ldo; g.N = N[i]; g.K = K; g.T = T; g.rows_per_wg = 0;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (type0 == kQ4K) return dispatch_mfma2<kQ4K, kQ6K>(a[0], a[1], st);
+  return dispatch_mfma2<kQ6K, kQ4K>(a[0], a[1], st);
 }
 
 // Two store-mode GEMVs over the same input in one launch: out_i[t][n] = W_i.x + bias_i (the

@@ -32,6 +32,9 @@ def _lib():
                                                                        vp, vp, ci, ci, ci, ci, ci,
                                                                        ci, vp, vp, vp, vp]
             lib.amdk8s_llm_qgemv_mfma.restype = ci
+            lib.amdk8s_llm_qgemv2_mfma.argtypes = [ci] + [vp] * 4 + [ci, vp, vp] + [ci] + [vp] * 4 \
+                + [ci, vp, vp, ci, vp, vp, vp, vp, ci, vp, cf, ci, ci, vp]
+            lib.amdk8s_llm_qgemv2_mfma.restype = ci
             lib.amdk8s_llm_mfma_pack.argtypes = [ci, vp, vp, vp, vp, ci, ci, vp, vp, vp, vp, vp]
             lib.amdk8s_llm_mfma_pack.restype = ci
             lib.amdk8s_llm_qgemv.argtypes = [ci, ci] + [vp] * 8 + [vp, vp, vp] \
@@ -168,6 +171,16 @@ def qgemv2(w0, w1, x8, dx, sx, out0, out1, bias0=None, bias1=None, rows_per_wg: 
     if out0.stride(0) != out1.stride(0) or w0.k != w1.k:
         raise ValueError("qgemv2: both outputs need one row stride and both matrices one K")
     ref = xf if xf is not None else x8
+    if _GEMV[0] == GEMV_MFMA and w0.mfma is not None and w1.mfma is not None:
+        rc = _lib().amdk8s_llm_qgemv2_mfma(
+            w0.qtype, *w0.mfma_ptrs(), w0.n, _p(bias0), out0.data_ptr(),
+            w1.qtype, *w1.mfma_ptrs(), w1.n, _p(bias1), out1.data_ptr(), out0.stride(0),
+            _p(x8), _p(dx), _p(sx), _p(xf), xf.stride(0) if xf is not None else 0, _p(norm_w),
+            float(eps), w0.k, ref.shape[0], _stream(ref))
+        if rc != 4:
+            _check(rc, "amdk8s_llm_qgemv2_mfma")
+            return True
+        return False            # packed matrices stay on the MFMA kernel: separate launches
     rc = _lib().amdk8s_llm_qgemv2(w0.qtype, *w0.ptrs(), w0.n, _p(bias0), out0.data_ptr(),
                                   w1.qtype, *w1.ptrs(), w1.n, _p(bias1), out1.data_ptr(),
                                   out0.stride(0), _p(x8), _p(dx), _p(sx), _p(xf),

@@ -466,6 +466,36 @@ def test_two_matrix_gemv_equals_two_launches(dev, LK, types, T, K):
     assert bool((out[:, 768:] == 3.0).all())
 
 
+@pytest.mark.parametrize("types", [("Q4_K", "Q6_K"), ("Q6_K", "Q4_K")])
+@pytest.mark.parametrize("T", [1, 2, 4, 8])
+def test_two_matrix_mfma_equals_two_launches(dev, mfma, types, T):
+    """q|k and v of different types in ONE MFMA launch: bit-identical to the two MFMA GEMVs,
+    from Q8 rows and (T <= 2) from fp32 rows through the RMSNorm prologue."""
+    from k8s_nvidia_gpus_amd.models.llm import gguf
+
+    LK = mfma
+    K = 3584
+    w0, _ = _qw(640, K, getattr(gguf, types[0]), 17, dev)
+    w1, _ = _qw(128, K, getattr(gguf, types[1]), 18, dev)
+    assert w0.mfma_pack() and w1.mfma_pack()
+    xf = torch.randn(T, K, device=dev) * 2
+    nw = torch.rand(K, device=dev) + 0.5
+    x8, dx, sx, _ = _q8(xf, LK)
+    bias = torch.randn(768, device=dev)
+    forms = [dict(x8=x8, dx=dx, sx=sx)] + ([dict(xf=xf, norm_w=nw)] if T <= 2 else [])
+    for f in forms:
+        q = (f.get("x8"), f.get("dx"), f.get("sx"))
+        kw = {k: v for k, v in f.items() if k in ("xf", "norm_w")}
+        ref = torch.zeros(T, 770, device=dev)
+        assert LK.qgemv(w0, *q, ref[:, :640], LK.STORE, bias=bias[:640], ldo=770, **kw) == "mfma"
+        assert LK.qgemv(w1, *q, ref[:, 640:], LK.STORE, bias=bias[640:], ldo=770, **kw) == "mfma"
+        out = torch.full((T, 770), 3.0, device=dev)
+        assert LK.qgemv2(w0, w1, *q, out[:, :640], out[:, 640:768], bias0=bias[:640],
+                         bias1=bias[640:], **kw)
+        torch.testing.assert_close(out[:, :768], ref[:, :768], rtol=0, atol=0)
+        assert bool((out[:, 768:] == 3.0).all())
+
+
 @pytest.fixture(scope="module")
 def tiny_gguf(tmp_path_factory):
     from k8s_nvidia_gpus_amd.models.llm import tiny
