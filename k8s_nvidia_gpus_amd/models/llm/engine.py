@@ -425,12 +425,14 @@ class Engine:
         self.stats["decode_steps"] += 1
         self.stats["decode_tokens"] += T
         if self.gpu:
-            out = []
-            for i in range(0, T, self.max_T):
-                out.append(self._decode_native(tokens[i:i + self.max_T],
-                                               positions[i:i + self.max_T],
-                                               slots[i:i + self.max_T]))
-            return out[0] if len(out) == 1 else torch.cat(out, 0)
+            if T <= self.max_T:
+                return self._decode_native(tokens, positions, slots)
+            # more sequences than one step takes: chunks of max_T reuse one step buffer, so each
+            # chunk's logits are copied out before the next chunk overwrites them
+            return torch.cat([self._decode_native(tokens[i:i + self.max_T],
+                                                  positions[i:i + self.max_T],
+                                                  slots[i:i + self.max_T]).clone()
+                              for i in range(0, T, self.max_T)], 0)
         rows = [self._forward_dense(torch.tensor([t]), s, p)
                 for t, p, s in zip(tokens, positions, slots)]
         return torch.stack(rows, 0)
