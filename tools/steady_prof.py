@@ -46,7 +46,7 @@ def llm_decode(T: int = 1):
     from k8s_nvidia_gpus_amd.models.llm.weights import ModelWeights
 
     w = ModelWeights.random(QWEN25_7B, device=torch.device("cuda", 0), seed=0)
-    eng = Engine(w, max_ctx=4096, slots=4, dense=True)
+    eng = Engine(w, max_ctx=4096, slots=8, dense=True)
     prompt = list(range(100, 612))
     for s in range(T):
         eng.prefill(prompt, slot=s)
@@ -66,7 +66,7 @@ def llm_prefill(P: int = 512):
     from k8s_nvidia_gpus_amd.models.llm.weights import ModelWeights
 
     w = ModelWeights.random(QWEN25_7B, device=torch.device("cuda", 0), seed=0)
-    eng = Engine(w, max_ctx=4096, slots=4, dense=True)
+    eng = Engine(w, max_ctx=4096, slots=8, dense=True)
     eng.dense_weights()
     prompt = list(range(100, 100 + P))
     return lambda: eng.prefill(prompt, slot=0)
