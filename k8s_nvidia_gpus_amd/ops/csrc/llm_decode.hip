@@ -1771,8 +1771,11 @@ void gemv_shape(int type, int N, int K, int T, int& waves, int& rows) {
 // 8 x 1; very tall matrices (lm_head) 2 x 2; the rest 4 x 1 (q|k|v, o_proj: 2 x 1 measured the same).  4 = shape not covered (N % 16, fewer super-blocks than K-waves, LDS): use qgemv_kernel.
 template <int TYPE, int T, int MODE, int KW, int RG>
 int launch_mfma_one(const GemvArgs& a, hipStream_t st) {
-  constexpr int D = MODE == kPair ? 2 : 3;          // pair: two matrices per slot (VGPR budget)
+  // ring depth: pair 2 (two matrices per slot, 3 waves/SIMD), else 3 (6 for ffn_down's 8-wave
+  // shape measured slower: Q6_K 13.9 -> 15.6 us, T = 1 1.629 -> 1.656 ms, profiles/r04/o)
+  constexpr int D = MODE == kPair ? 2 : 3;
   if ((a.K >> 8) < KW) return 4;
+  if (KW == 8 && T > 4) return 4;                   // register budget: tokens in two launches
   const MfmaLds L = mfma_lds(TYPE, T, a.K, KW * RG, MODE == kPair ? 2 : 1);
   if (L.total > 160 * 1024) return 4;
   const int grid = (a.N + 16 * RG - 1) / (16 * RG);
