@@ -961,7 +961,6 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
       for (int u = 0; u < NA; ++u) aux[u] = axb[q][kb * NA + u];
       acc[q] = mfma_block<TYPE>(q0, xa, dxv, aux, g, acc[q]);
       if constexpr (P == 2) acc1[q] = mfma_block<TYPE>(q1, xa, dxv, aux, g, acc1[q]);
-      if constexpr (NQ > 1) __builtin_amdgcn_sched_barrier(0);   // one quad's temporaries live
     }
   };
   // Whole groups of D steps: every step first refills the slot consumed one step ago with block
