@@ -1,0 +1,626 @@
+// Quantised GEMVs of the LLM decode step on the int8 matrix cores (gfx950): the MFMA-packed weight
+// planes, qgemv_mfma_kernel / qgemv2_mfma_kernel and their launchers.  Shared definitions:
+// llm_common.h; the VALU GEMV, attention and norm kernels: llm_decode.hip; measurements:
+// docs/llm_decode.md ("Round 4: the GEMVs on the int8 matrix cores").
+#include "llm_common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- MFMA GEMV (int8 matrix cores)
+// The VALU GEMV above spends ~90 VALU per lane and super-block at T = 4 (eight v_dot4 plus the
+// scale arithmetic per token on top of the weight decode), which makes steps of 2-4 tokens
+// VALU-bound (profiles/r04/f: gate|up 30 µs at T = 4 vs 20 µs at T = 1).  Here the integer
+// sub-block sums come from v_mfma_i32_16x16x64_i8 and only the per-sub-block scaling stays on the
+// VALU, once per (row, token, sub-block) instead of once per weight byte.
+//
+// Geometry: one wave = 16 weight rows (the MFMA's N) × a range of super-blocks; lane l loads row
+// l & 15, K-group g = l >> 4 (Q4_K: nibble bytes 16g.. of each 64-byte half of the super-block, so
+// each load instruction reads 64 contiguous bytes per row).  M = 16 = (token t, slot s): A row
+// (t, s) carries token t's activations in K-group s only (zeros in the other three), so output
+// (t, s) of row r is the sum over K-group s alone, and every K-group's 16 values of one MFMA lie in
+// one sub-block.  Four MFMAs per super-block leave lane l = (row l & 15, token l >> 4) with the
+// sub-block sums of its own row and token (mfma_q4_block).  Each lane then scales its own
+// (row, token) in a fixed order, so a token's bits never depend on how many tokens share the
+// launch (batch-invariant).
+// Super-blocks are split over KW waves (reduced in LDS in wave order); RG row groups per workgroup.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// The MFMA kernel reads an MFMA-packed copy of the planes (amdk8s_llm_mfma_pack), laid out per
+// (16-row group G, super-block b) so that each of a wave's loads per block reads whole contiguous
+// lines instead of a 64/16/4-byte piece of 16 different rows:
+//   Q4_K: q [2][16 rows][64 B] (bytes 64h.. of each row's nibbles), sc [16][4] dwords, d [16] dwords
+//   Q6_K: ql as Q4_K's q, qh [2][16][32 B], sc [16][16] int8 in natural order, d [16] dwords (f16)
+template <int TYPE> struct MBlk;
+template <> struct MBlk<kQ4K> { uint4 q0, q1, sc; uint32_t dd; };
+template <> struct MBlk<kQ6K> { uint4 q0, q1, h0, h1, sc; uint32_t dd; };
+
+template <int TYPE>
+__device__ __forceinline__ void mload(const QMat& w, long gb, int lane, MBlk<TYPE>& r) {
+  const int row = lane & 15, g = lane >> 4;
+  const uint8_t* q = w.q + gb * 2048 + row * 64 + g * 16;
+  r.q0 = ldnt(q);
+  r.q1 = ldnt(q + 1024);
+  if constexpr (TYPE == kQ6K) {
+    const uint8_t* h = w.qh + gb * 1024 + row * 32 + (g & 1) * 16;
+    r.h0 = ldnt(h);
+    r.h1 = ldnt(h + 512);
+    r.sc = ldnt(reinterpret_cast<const uint8_t*>(w.sc) + gb * 256 + row * 16);
+  } else {
+    r.sc = ldnt(reinterpret_cast<const uint32_t*>(w.sc) + gb * 64 + row * 4);
+  }
+  r.dd = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(w.d) + gb * 16 + row);
+}
+
+__device__ __forceinline__ i32x4 nib_lo(const uint4& v) {
+  const uint32_t m = 0x0f0f0f0fu;
+  return i32x4{(int)(v.x & m), (int)(v.y & m), (int)(v.z & m), (int)(v.w & m)};
+}
+__device__ __forceinline__ i32x4 nib_hi(const uint4& v) {
+  const uint32_t m = 0x0f0f0f0fu;
+  return i32x4{(int)((v.x >> 4) & m), (int)((v.y >> 4) & m), (int)((v.z >> 4) & m),
+               (int)((v.w >> 4) & m)};
+}
+// Q6_K: 6-bit values (0..63) of 4 bytes — low / high nibbles of q with the 2-bit fields at bit k /
+// k + 4 of each qh byte as bits 4-5
+__device__ __forceinline__ uint32_t q6lo(uint32_t q, uint32_t h, int k) {
+  return (q & 0x0f0f0f0fu) | (((h >> k) << 4) & 0x30303030u);
+}
+__device__ __forceinline__ uint32_t q6hi(uint32_t q, uint32_t h, int k) {
+  return ((q >> 4) & 0x0f0f0f0fu) | ((h >> k) & 0x30303030u);
+}
+
+// acc += this lane's (row, token) share of one super-block.
+// Q4_K: K-group g holds bytes 16g.. of each 64-byte half (q0: chunks 0-1, q1: chunks 2-3), so in
+//   MFMA m (0: q0 low nibbles, 1: q0 high, 2: q1 low, 3: q1 high) groups 2h and 2h + 1 carry the
+//   two 16-value halves of sub-block 2(2(m >> 1) + h) + (m & 1): c[2h] + c[2h + 1] is that
+//   sub-block.  acc += d * sum_j sc_j dx_j I_j - dmin * sum_j m_j sxp_j (aux = sxp, the dx-scaled
+//   sums of x per 32).
+// Q6_K: group g holds values 16g.. of each 64 (bytes 16g.. of the ql halves, qh fields of
+//   "l" / "32 + l" by g >> 1), so c_m[s] is the 16-value sub-block 4m + s.  Integer per 32-value
+//   pair: S = sc_j (I_j - 32 X_j) + sc_j+1 (I_j+1 - 32 X_j+1) (aux = X, the int sums of x per 16),
+//   then acc += d * sum_i dx_i S_i.
+template <int TYPE>
+__device__ __forceinline__ float mfma_block(const MBlk<TYPE>& w, const i32x4 (&xa)[4],
+                                            const float (&dxv)[8], const uint4 (&aux)[4], int g,
+                                            float acc) {
+  const i32x4 z = {0, 0, 0, 0};
+  if constexpr (TYPE == kQ4K) {
+    const i32x4 c0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(xa[0], nib_lo(w.q0), z, 0, 0, 0);
+    const i32x4 c1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(xa[1], nib_hi(w.q0), z, 0, 0, 0);
+    const i32x4 c2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(xa[2], nib_lo(w.q1), z, 0, 0, 0);
+    const i32x4 c3 = __builtin_amdgcn_mfma_i32_16x16x64_i8(xa[3], nib_hi(w.q1), z, 0, 0, 0);
+    const int I[8] = {c0[0] + c0[1], c1[0] + c1[1], c0[2] + c0[3], c1[2] + c1[3],
+                      c2[0] + c2[1], c3[0] + c3[1], c2[2] + c2[3], c3[2] + c3[3]};
+    const float spv[8] = {__uint_as_float(aux[0].x), __uint_as_float(aux[0].y),
+                          __uint_as_float(aux[0].z), __uint_as_float(aux[0].w),
+                          __uint_as_float(aux[1].x), __uint_as_float(aux[1].y),
+                          __uint_as_float(aux[1].z), __uint_as_float(aux[1].w)};
+    const uint32_t scw[4] = {w.sc.x, w.sc.y, w.sc.z, w.sc.w};
+    float sm = 0.f, mn = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float s0 = (float)(scw[i] & 0xffu), s1 = (float)((scw[i] >> 8) & 0xffu);
+      const float m0 = (float)((scw[i] >> 16) & 0xffu), m1 = (float)(scw[i] >> 24);
+      sm = __fmaf_rn((float)I[2 * i], __fmul_rn(s0, dxv[2 * i]), sm);
+      sm = __fmaf_rn((float)I[2 * i + 1], __fmul_rn(s1, dxv[2 * i + 1]), sm);
+      mn = __fmaf_rn(m0, spv[2 * i], mn);
+      mn = __fmaf_rn(m1, spv[2 * i + 1], mn);
+    }
+    acc = __fmaf_rn(h2f(w.dd & 0xffffu), sm, acc);
+    return __fmaf_rn(-h2f(w.dd >> 16), mn, acc);
+  } else {
+    const int k = 2 * (g >> 1);
+    const uint4 q0 = w.q0, q1 = w.q1, h0 = w.h0, h1 = w.h1;
+    const i32x4 b0 = {(int)q6lo(q0.x, h0.x, k), (int)q6lo(q0.y, h0.y, k), (int)q6lo(q0.z, h0.z, k),
+                      (int)q6lo(q0.w, h0.w, k)};
+    const i32x4 b1 = {(int)q6hi(q0.x, h0.x, k), (int)q6hi(q0.y, h0.y, k), (int)q6hi(q0.z, h0.z, k),
+                      (int)q6hi(q0.w, h0.w, k)};
+    const i32x4 b2 = {(int)q6lo(q1.x, h1.x, k), (int)q6lo(q1.y, h1.y, k), (int)q6lo(q1.z, h1.z, k),
+                      (int)q6lo(q1.w, h1.w, k)};
+    const i32x4 b3 = {(int)q6hi(q1.x, h1.x, k), (int)q6hi(q1.y, h1.y, k), (int)q6hi(q1.z, h1.z, k),
+                      (int)q6hi(q1.w, h1.w, k)};
+    const i32x4 c[4] = {__builtin_amdgcn_mfma_i32_16x16x64_i8(xa[0], b0, z, 0, 0, 0),
+                        __builtin_amdgcn_mfma_i32_16x16x64_i8(xa[1], b1, z, 0, 0, 0),
+                        __builtin_amdgcn_mfma_i32_16x16x64_i8(xa[2], b2, z, 0, 0, 0),
+                        __builtin_amdgcn_mfma_i32_16x16x64_i8(xa[3], b3, z, 0, 0, 0)};
+    const uint32_t X[16] = {aux[0].x, aux[0].y, aux[0].z, aux[0].w, aux[1].x, aux[1].y,
+                            aux[1].z, aux[1].w, aux[2].x, aux[2].y, aux[2].z, aux[2].w,
+                            aux[3].x, aux[3].y, aux[3].z, aux[3].w};
+    const uint32_t scw[4] = {w.sc.x, w.sc.y, w.sc.z, w.sc.w};
+    float blk = 0.f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const int j = 4 * m + 2 * pr;                 // sub-blocks j, j + 1: 32-group j / 2
+        const int s0 = (int)(int8_t)((scw[j >> 2] >> (8 * (j & 3))) & 0xffu);
+        const int s1 = (int)(int8_t)((scw[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 0xffu);
+        const int i0 = c[m][2 * pr] - 32 * (int)X[j];
+        const int i1 = c[m][2 * pr + 1] - 32 * (int)X[j + 1];
+        blk = __fmaf_rn((float)(s0 * i0 + s1 * i1), dxv[j >> 1], blk);
+      }
+    }
+    return __fmaf_rn(h2f(w.dd & 0xffffu), blk, acc);
+  }
+}
+
+// LDS after stage_x's arrays: [W][T] prologue scratch (rounded to 16 B), the per-type activation
+// sums (Q4_K sxp float [T][K/32], Q6_K X int [T][K/16]), 256 zero bytes (the A operand of
+// inactive lanes), the K-split partials [waves][token quads][P][64], q8s [T][32].
+struct MfmaLds { int aux, zero, kred, q8s, total; };
+__host__ __device__ inline MfmaLds mfma_lds(int type, int T, int K, int waves, int P) {
+  MfmaLds L;
+  const int nb = K >> 8;
+  const int base = T * (nb * 288 + (K >> 5) * 4 + (K >> 4) * 4);
+  const int red = ((waves * T * 4) + 15) & ~15;
+  L.aux = base + red;
+  L.zero = L.aux + T * (type == kQ6K ? K >> 4 : K >> 5) * 4;
+  L.kred = L.zero + 256;
+  L.q8s = L.kred + waves * ((T + 3) / 4) * P * 64 * 4;
+  L.total = L.q8s + T * 32 * 4;
+  return L;
+}
+
+// gate|up (pair, <= 4 tokens): 592 4-wave workgroups need 3 waves per SIMD to be co-resident
+// bid = the workgroup's index within this matrix's grid
+template <int TYPE, int T, int MODE, int KW, int RG, int D>
+__device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  constexpr int P = MODE == kPair ? 2 : 1;
+  constexpr int NA = TYPE == kQ6K ? 4 : 2;          // uint4 of activation sums per block
+  constexpr int NQ = (T + 3) / 4;                   // token quads: MFMA M = 4 tokens x 4 K-groups
+  const int K = a.K, nb = K >> 8;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int rg = wave / KW, kw = wave % KW;
+  const int kb0 = kw * nb / KW, n = (kw + 1) * nb / KW - kb0;    // host: nb >= KW, so n >= 1
+  const int r = lane & 15, g = lane >> 4;
+  const int wrow0 = bid * RG * 16;
+  const long rb0 = (long)(min(wrow0 + rg * 16, a.N - 16) >> 4) * nb + kb0;   // host: N % 16 == 0
+  // ring of D super-blocks: D - 1 in flight before the activations are staged
+  MBlk<TYPE> w0[D], w1[D];
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d) {
+    const long rb = rb0 + min(d, n - 1);
+    mload<TYPE>(a.w0, rb, lane, w0[d]);
+    if constexpr (P == 2) mload<TYPE>(a.w1, rb, lane, w1[d]);
+  }
+  const XView xv = stage_x<T>(a, lds);
+  const MfmaLds L = mfma_lds(TYPE, T, K, KW * RG, P);
+  if constexpr (TYPE == kQ4K) {
+    float* sxp = reinterpret_cast<float*>(lds + L.aux);
+    for (int i = threadIdx.x; i < T * (K >> 5); i += blockDim.x)
+      sxp[i] = xv.sxs[2 * i] + xv.sxs[2 * i + 1];
+  } else {
+    int* X = reinterpret_cast<int*>(lds + L.aux);
+    for (int i = threadIdx.x; i < T * (K >> 4); i += blockDim.x) {
+      const int t = i / (K >> 4), p = (i - t * (K >> 4)) << 4;
+      const uint4 v = *reinterpret_cast<const uint4*>(xv.xs + t * xv.xstride + xoff(p));
+      int sum = dot4z(v.x, 0x01010101u);
+      sum = dot4(v.y, 0x01010101u, sum);
+      sum = dot4(v.z, 0x01010101u, sum);
+      X[i] = dot4(v.w, 0x01010101u, sum);
+    }
+  }
+  if (threadIdx.x < 16) reinterpret_cast<uint4*>(lds + L.zero)[threadIdx.x] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  // A operand of quad q: lane l is row (t, s) = (4q + ((l & 15) >> 2), l & 3) of K-group g; live
+  // only for s == g.  MFMA m's 16 activations: Q4_K +0 / +32 / +128 / +160 from
+  // 64 (g >> 1) + 16 (g & 1); Q6_K +0 / +64 / +128 / +192 from 16 g (zero lanes: the zero bytes)
+  const int xb = TYPE == kQ6K ? 16 * g : 64 * (g >> 1) + 16 * (g & 1);
+  int xa0[NQ], xstep[NQ], xo1[NQ], xo2[NQ], xo3[NQ];
+  const float* dxb[NQ];
+  const uint4* axb[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int at = 4 * q + ((lane & 15) >> 2);
+    const bool live = (lane & 3) == g && at < T;
+    xa0[q] = live ? at * xv.xstride + xb : L.zero;
+    xstep[q] = live ? 288 : 0;
+    xo1[q] = live ? (TYPE == kQ6K ? 64 : 32) : 0;
+    xo2[q] = live ? 128 : 0;
+    xo3[q] = live ? (TYPE == kQ6K ? 192 : 160) : 0;
+    const int tt = min(4 * q + g, T - 1);            // this lane's output token in quad q
+    dxb[q] = xv.dxs + tt * (K >> 5);
+    axb[q] = reinterpret_cast<const uint4*>(lds + L.aux) + tt * nb * NA;
+  }
+  float acc[NQ], acc1[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) acc[q] = acc1[q] = 0.f;
+  auto compute = [&](const MBlk<TYPE>& q0, const MBlk<TYPE>& q1, int i) {
+    const int kb = kb0 + i;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const uint8_t* xp = lds + xa0[q] + kb * xstep[q];
+      i32x4 xa[4];
+      xa[0] = *reinterpret_cast<const i32x4*>(xp);
+      xa[1] = *reinterpret_cast<const i32x4*>(xp + xo1[q]);
+      xa[2] = *reinterpret_cast<const i32x4*>(xp + xo2[q]);
+      xa[3] = *reinterpret_cast<const i32x4*>(xp + xo3[q]);
+      float dxv[8];
+      const float4 d0 = *reinterpret_cast<const float4*>(dxb[q] + kb * 8);
+      const float4 d1 = *reinterpret_cast<const float4*>(dxb[q] + kb * 8 + 4);
+      dxv[0] = d0.x; dxv[1] = d0.y; dxv[2] = d0.z; dxv[3] = d0.w;
+      dxv[4] = d1.x; dxv[5] = d1.y; dxv[6] = d1.z; dxv[7] = d1.w;
+      uint4 aux[4];
+#pragma unroll
+      for (int u = 0; u < NA; ++u) aux[u] = axb[q][kb * NA + u];
+      acc[q] = mfma_block<TYPE>(q0, xa, dxv, aux, g, acc[q]);
+      if constexpr (P == 2) acc1[q] = mfma_block<TYPE>(q1, xa, dxv, aux, g, acc1[q]);
+    }
+  };
+  // Whole groups of D steps: every step first refills the slot consumed one step ago with block
+  // i + D - 1 (clamped: the last group re-reads the final block from L2), then computes slot d.
+  // No load sits under a branch (that makes the compiler drain every outstanding load at the
+  // join, which serialises the ring); the < D leftover blocks are computed after the loop from
+  // slots already in flight.
+  int i0 = 0;
+  for (; i0 + D <= n; i0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int ps = (d + D - 1) % D;
+      const long nxt = rb0 + min(i0 + d + D - 1, n - 1);
+      mload<TYPE>(a.w0, nxt, lane, w0[ps]);
+      if constexpr (P == 2) mload<TYPE>(a.w1, nxt, lane, w1[ps]);
+      // keep the refill ahead of this step's maths and the steps in ring order: the scheduler
+      // otherwise sinks the refills, and the next step's wait then drains them too
+      __builtin_amdgcn_sched_barrier(0);
+      compute(w0[d], w1[d], i0 + d);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d)
+    if (i0 + d < n) compute(w0[d], w1[d], i0 + d);
+  // K-split partials: wave kw = 0 of each row group adds its group's in wave order
+  float v[NQ], v1[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) v[q] = acc[q], v1[q] = acc1[q];
+  if constexpr (KW > 1) {
+    float* kred = reinterpret_cast<float*>(lds + L.kred);      // [waves][NQ][P][64]
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      kred[((wave * NQ + q) * P) * 64 + lane] = acc[q];
+      if constexpr (P == 2) kred[((wave * NQ + q) * P + 1) * 64 + lane] = acc1[q];
+    }
+    __syncthreads();
+    if (kw == 0) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        v[q] = 0.f; v1[q] = 0.f;
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+          v[q] += kred[(((rg * KW + k) * NQ + q) * P) * 64 + lane];
+          if constexpr (P == 2) v1[q] += kred[(((rg * KW + k) * NQ + q) * P + 1) * 64 + lane];
+        }
+      }
+    }
+  }
+  float* q8s = (MODE == kPair && a.ox8) ? reinterpret_cast<float*>(lds + L.q8s) : nullptr;
+  const int orow = wrow0 + rg * 16 + r;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int t = 4 * q + g;
+    if (kw == 0 && t < T && orow < a.N) {
+      float* o = a.out + (long)t * a.ldo + orow;
+      if constexpr (MODE == kStore) *o = v[q] + (a.bias ? a.bias[orow] : 0.f);
+      else if constexpr (MODE == kResid) *o += v[q];
+      else {
+        const float y = v[q] / (1.f + __expf(-v[q])) * v1[q];
+        if (q8s) q8s[t * 32 + rg * 16 + r] = y;
+        else *o = y;
+      }
+    }
+  }
+  if constexpr (MODE == kPair && RG == 2) {
+    if (q8s) {
+      __syncthreads();
+      emit_q8_block<T>(a, q8s, wrow0);
+    }
+  }
+}
+
+template <int TYPE, int T, int MODE, int KW, int RG, int D>
+__global__ void __launch_bounds__(KW * RG * 64)
+__attribute__((amdgpu_waves_per_eu(MODE == kPair && T <= 4 ? 3 : 1, 8)))
+qgemv_mfma_kernel(GemvArgs a) {
+  qgemv_mfma_body<TYPE, T, MODE, KW, RG, D>(a, blockIdx.x);
+}
+
+// Two store-mode matrices of (possibly) different types over the same input in ONE launch (q|k
+// and v of Q4_K_M): workgroups [0, grid0) run a0.  Each keeps the shape and the arithmetic it has
+// alone, so a row's bits do not depend on which launch computed it.
+template <int TYPE0, int TYPE1, int T, int KW, int RG, int D>
+__global__ void __launch_bounds__(KW * RG * 64)
+qgemv2_mfma_kernel(GemvArgs a0, GemvArgs a1, int grid0) {
+  if ((int)blockIdx.x < grid0) qgemv_mfma_body<TYPE0, T, kStore, KW, RG, D>(a0, blockIdx.x);
+  else qgemv_mfma_body<TYPE1, T, kStore, KW, RG, D>(a1, blockIdx.x - grid0);
+}
+
+// Repacked planes → the MFMA-packed copy (see mload): one thread per (row, super-block).
+// Q4_K: q [N][nb*128], sc [N][nb*4] dwords, d [N][nb] dwords.  Q6_K: ql [N][nb*128],
+// qh [N][nb*64], sc [N][nb*16] int8 (lane order, q6_scale_pos), d [N][nb] f16.
+template <int TYPE>
+__global__ void mfma_pack_kernel(QMat w, int N, int nb, uint8_t* __restrict__ mq,
+                                 uint8_t* __restrict__ mqh, uint8_t* __restrict__ msc,
+                                 uint32_t* __restrict__ md) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)N * nb) return;
+  const int row = (int)(i / nb), b = (int)(i % nb);
+  const long gb = (long)(row >> 4) * nb + b;
+  const int r = row & 15;
+  const uint4* src = reinterpret_cast<const uint4*>(w.q + i * 128);
+  uint4* dst = reinterpret_cast<uint4*>(mq + gb * 2048 + r * 64);
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dst[h * 64 + j] = src[h * 4 + j];
+  if constexpr (TYPE == kQ4K) {
+    reinterpret_cast<uint4*>(msc + gb * 256 + r * 16)[0] =
+        reinterpret_cast<const uint4*>(w.sc + i * 16)[0];
+    md[gb * 16 + r] = reinterpret_cast<const uint32_t*>(w.d)[i];
+  } else {
+    const uint4* hs = reinterpret_cast<const uint4*>(w.qh + i * 64);
+    uint4* hd = reinterpret_cast<uint4*>(mqh + gb * 1024 + r * 32);
+    hd[0] = hs[0]; hd[1] = hs[1];                   // half 0: qh bytes 0..31
+    hd[32] = hs[2]; hd[33] = hs[3];                 // half 1: bytes 32..63, 512 B further
+    uint8_t sc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) sc[j] = (uint8_t)w.sc[i * 16 + q6_scale_pos(j)];
+    uint32_t wv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      wv[j] = sc[4 * j] | (sc[4 * j + 1] << 8) | (sc[4 * j + 2] << 16) | ((uint32_t)sc[4 * j + 3] << 24);
+    reinterpret_cast<uint4*>(msc + gb * 256 + r * 16)[0] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+    md[gb * 16 + r] = w.d[i];
+  }
+}
+
+// MFMA GEMV launch shapes (K-waves x row groups, swept with tools/llm_bench.py --gemv, profiles/r04/l):
+// pair (gate|up) 2 x 2 (a whole 32-row Q8 block per workgroup); long rows (K >= 8192: ffn_down)
+// 8 x 1; very tall matrices (lm_head) 2 x 2; the rest 4 x 1 (q|k|v, o_proj: 2 x 1 measured the same).  4 = shape not covered (N % 16, fewer super-blocks than K-waves, LDS): use qgemv_kernel.
+template <int TYPE, int T, int MODE, int KW, int RG>
+int launch_mfma_one(const GemvArgs& a, hipStream_t st) {
+  // ring depth: pair 2 (two matrices per slot, 3 waves/SIMD), else 3 (6 for ffn_down's 8-wave
+  // shape measured slower: Q6_K 13.9 -> 15.6 us, T = 1 1.629 -> 1.656 ms, profiles/r04/o)
+  constexpr int D = MODE == kPair ? 2 : 3;
+  if ((a.K >> 8) < KW) return 4;
+  const MfmaLds L = mfma_lds(TYPE, T, a.K, KW * RG, MODE == kPair ? 2 : 1);
+  if (L.total > 160 * 1024) return 4;
+  const int grid = (a.N + 16 * RG - 1) / (16 * RG);
+  hipLaunchKernelGGL((qgemv_mfma_kernel<TYPE, T, MODE, KW, RG, D>), dim3(grid), dim3(KW * RG * 64),
+                     L.total, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// Default shape: a function of the matrix only (never of T or of the input form), so each matrix
+// sums its K-split partials in one order at every T (batch invariance), and 4 waves wherever the
+// fp32-row prologue may run (stage_x reduces the RMSNorm over 4 waves in rmsnorm_q8's order;
+// models with dim >= 8192 use the prologue at every T).
+void mfma_shape(bool pair, int N, int K, int& kw, int& rg) {
+  const int nb = K >> 8;
+  if (pair) kw = nb >= 2 ? 2 : 1, rg = 2;
+  else if (K >= 8192) kw = 8, rg = 1;
+  else if (N >= 65536 && nb >= 2) kw = 2, rg = 2;    // lm_head: 75.0 / 80.2 us at T = 1 / 4
+  else if (nb >= 4) kw = 4, rg = 1;
+  else if (nb >= 2) kw = 2, rg = 2;
+  else kw = 1, rg = 4;
+}
+
+template <int TYPE, int T, int MODE>
+int launch_mfma(const GemvArgs& a, int kw, int rg, hipStream_t st) {
+  if (a.N % 16) return 4;
+  if (kw <= 0) mfma_shape(MODE == kPair, a.N, a.K, kw, rg);
+  if (MODE == kPair && a.ox8 && rg != 2) return 2;   // a whole 32-row Q8 block per workgroup
+  if (MODE == kPair && a.ox8 && kw * rg * 64 < 32 * T) return 2;   // emit_q8_block: 32 lanes/token
+  // only the shapes mfma_shape picks are instantiated (build time)
+  if constexpr (MODE == kPair) {
+    if (kw == 2 && rg == 2) return launch_mfma_one<TYPE, T, MODE, 2, 2>(a, st);
+    if (kw == 1 && rg == 2) return launch_mfma_one<TYPE, T, MODE, 1, 2>(a, st);
+    return 2;
+  } else {
+    switch (kw * 8 + rg) {
+      case 1 * 8 + 4: return launch_mfma_one<TYPE, T, MODE, 1, 4>(a, st);
+      case 2 * 8 + 2: return launch_mfma_one<TYPE, T, MODE, 2, 2>(a, st);
+      case 4 * 8 + 1: return launch_mfma_one<TYPE, T, MODE, 4, 1>(a, st);
+      case 8 * 8 + 1:
+        if constexpr (T <= 4) return launch_mfma_one<TYPE, T, MODE, 8, 1>(a, st);
+        else return 4;                              // register budget: tokens in two launches
+      default: return 2;
+    }
+  }
+}
+
+// kw / rg: K-waves and 16-row groups per workgroup (0 = the default shape for the matrix)
+template <int TYPE, int MODE>
+int dispatch_mfma(const GemvArgs& a, int kw, int rg, hipStream_t st) {
+  switch (a.T) {
+    case 1: return launch_mfma<TYPE, 1, MODE>(a, kw, rg, st);
+    case 2: return launch_mfma<TYPE, 2, MODE>(a, kw, rg, st);
+    case 3: return launch_mfma<TYPE, 3, MODE>(a, kw, rg, st);
+    case 4: return launch_mfma<TYPE, 4, MODE>(a, kw, rg, st);
+    case 5: return launch_mfma<TYPE, 5, MODE>(a, kw, rg, st);
+    case 6: return launch_mfma<TYPE, 6, MODE>(a, kw, rg, st);
+    case 7: return launch_mfma<TYPE, 7, MODE>(a, kw, rg, st);
+    case 8: return launch_mfma<TYPE, 8, MODE>(a, kw, rg, st);
+    default: return 2;
+  }
+}
+
+// More than 4 tokens whose activations do not fit the LDS with T (ffn_down's K = 18944 at T > 4):
+// tokens [0, 4) and [4, T) as two launches.  Every token's arithmetic is the same in either form.
+template <int TYPE, int MODE>
+int dispatch_mfma_split(const GemvArgs& a, int kw, int rg, hipStream_t st) {
+  const int rc = dispatch_mfma<TYPE, MODE>(a, kw, rg, st);
+  if (rc != 4 || a.T <= 4) return rc;
+  GemvArgs lo = a, hi = a;
+  lo.T = 4;
+  hi.T = a.T - 4;
+  const long K = a.K;
+  if (hi.x8) { hi.x8 += 4 * K; hi.dx += 4 * (K >> 5); hi.sx += 4 * (K >> 4); }
+  if (hi.xf) hi.xf += 4L * a.ldx;
+  hi.out += 4L * a.ldo;
+  if (hi.ox8) { hi.ox8 += 4L * a.N; hi.odx += 4L * (a.N >> 5); hi.osx += 4L * (a.N >> 4); }
+  const int r0 = dispatch_mfma<TYPE, MODE>(lo, kw, rg, st);
+  if (r0) return r0;
+  return dispatch_mfma<TYPE, MODE>(hi, kw, rg, st);
+}
+
+
+template <int TYPE0, int TYPE1, int T, int KW, int RG>
+int launch_mfma2_one(const GemvArgs& a0, const GemvArgs& a1, hipStream_t st) {
+  constexpr int D = 3;
+  if ((a0.K >> 8) < KW) return 4;
+  const int lds = max(mfma_lds(TYPE0, T, a0.K, KW * RG, 1).total,
+                      mfma_lds(TYPE1, T, a0.K, KW * RG, 1).total);
+  if (lds > 160 * 1024) return 4;
+  const int g0 = (a0.N + 16 * RG - 1) / (16 * RG), g1 = (a1.N + 16 * RG - 1) / (16 * RG);
+  hipLaunchKernelGGL((qgemv2_mfma_kernel<TYPE0, TYPE1, T, KW, RG, D>), dim3(g0 + g1),
+                     dim3(KW * RG * 64), lds, st, a0, a1, g0);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+template <int TYPE0, int TYPE1, int T>
+int launch_mfma2(const GemvArgs& a0, const GemvArgs& a1, hipStream_t st) {
+  if (a0.N % 16 || a1.N % 16) return 4;
+  int kw = 0, rg = 0;
+  mfma_shape(false, a0.N + a1.N, a0.K, kw, rg);
+  switch (kw * 8 + rg) {
+    case 1 * 8 + 4: return launch_mfma2_one<TYPE0, TYPE1, T, 1, 4>(a0, a1, st);
+    case 2 * 8 + 2: return launch_mfma2_one<TYPE0, TYPE1, T, 2, 2>(a0, a1, st);
+    case 4 * 8 + 1: return launch_mfma2_one<TYPE0, TYPE1, T, 4, 1>(a0, a1, st);
+    default: return 4;
+  }
+}
+
+template <int TYPE0, int TYPE1>
+int dispatch_mfma2(const GemvArgs& a0, const GemvArgs& a1, hipStream_t st) {
+  switch (a0.T) {
+    case 1: return launch_mfma2<TYPE0, TYPE1, 1>(a0, a1, st);
+    case 2: return launch_mfma2<TYPE0, TYPE1, 2>(a0, a1, st);
+    case 3: return launch_mfma2<TYPE0, TYPE1, 3>(a0, a1, st);
+    case 4: return launch_mfma2<TYPE0, TYPE1, 4>(a0, a1, st);
+    case 5: return launch_mfma2<TYPE0, TYPE1, 5>(a0, a1, st);
+    case 6: return launch_mfma2<TYPE0, TYPE1, 6>(a0, a1, st);
+    case 7: return launch_mfma2<TYPE0, TYPE1, 7>(a0, a1, st);
+    case 8: return launch_mfma2<TYPE0, TYPE1, 8>(a0, a1, st);
+    default: return 2;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Quantised GEMV on the int8 matrix cores (qgemv_mfma_kernel) over the MFMA-packed planes (w*q /
+// w*qh / w*sc / w*d from amdk8s_llm_mfma_pack; qh: Q6_K only); arguments otherwise as
+// amdk8s_llm_qgemv.  kw / rows_per_wg: K-waves and rows (16 x row groups) per workgroup, 0 = the
+// default shape.  4 = shape not covered (N % 16, fewer super-blocks than K-waves, LDS): use
+// amdk8s_llm_qgemv on the plain planes.
+int amdk8s_llm_qgemv_mfma(int type, int mode, const void* w0q, const void* w0qh, const void* w0sc,
+                          const void* w0d, const void* w1q, const void* w1qh, const void* w1sc,
+                          const void* w1d, const void* x8, const void* dx, const void* sx,
+                          const void* xf, int ldx, const void* norm_w, float eps,
+                          const void* bias, void* out, int ldo, int N, int K, int T, int kw,
+                          int rows_per_wg, void* ox8, void* odx, void* osx, void* stream) {
+  if (K % 256 || N <= 0 || T < 1 || T > kMaxTok) return 2;
+  if (type != kQ4K && type != kQ6K) return 2;
+  if (mode == kPair && !w1q) return 2;
+  if (!xf && !(x8 && dx && sx)) return 2;
+  if (xf && (ldx % 4 || T > kValuMaxTok)) return 2;  // fp32-row prologue: steps of <= 4 tokens
+  if (ox8 && (mode != kPair || N % 32 || !odx || !osx)) return 2;
+  GemvArgs a{};
+  a.w0 = {static_cast<const uint8_t*>(w0q), static_cast<const uint8_t*>(w0qh),
+          static_cast<const int8_t*>(w0sc), static_cast<const uint16_t*>(w0d)};
+  a.w1 = {static_cast<const uint8_t*>(w1q), static_cast<const uint8_t*>(w1qh),
+          static_cast<const int8_t*>(w1sc), static_cast<const uint16_t*>(w1d)};
+  a.x8 = static_cast<const int8_t*>(x8);
+  a.dx = static_cast<const float*>(dx);
+  a.sx = static_cast<const float*>(sx);
+  a.xf = static_cast<const float*>(xf);
+  a.ldx = ldx;
+  a.norm_w = static_cast<const float*>(norm_w);
+  a.eps = eps;
+  a.bias = static_cast<const float*>(bias);
+  a.out = static_cast<float*>(out);
+  a.ldo = ldo; a.N = N; a.K = K; a.T = T; a.rows_per_wg = 0;
+  a.ox8 = static_cast<int8_t*>(ox8);
+  a.odx = static_cast<float*>(odx);
+  a.osx = static_cast<float*>(osx);
+  const int rg = ox8 ? 2 : (rows_per_wg > 0 && rows_per_wg % 16 == 0 ? rows_per_wg / 16 : 0);
+  if (rg == 0) kw = 0;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (type == kQ4K) {
+    if (mode == kStore) return dispatch_mfma_split<kQ4K, kStore>(a, kw, rg, st);
+    if (mode == kResid) return dispatch_mfma_split<kQ4K, kResid>(a, kw, rg, st);
+    if (mode == kPair) return dispatch_mfma_split<kQ4K, kPair>(a, kw, rg, st);
+  } else {
+    if (mode == kStore) return dispatch_mfma_split<kQ6K, kStore>(a, kw, rg, st);
+    if (mode == kResid) return dispatch_mfma_split<kQ6K, kResid>(a, kw, rg, st);
+    if (mode == kPair) return dispatch_mfma_split<kQ6K, kPair>(a, kw, rg, st);
+  }
+  return 2;
+}
+
+// Repacked planes (amdk8s_llm_q4k_repack / q6k_repack layout) → the MFMA-packed copy: mq
+// [N*nb*128] bytes, mqh [N*nb*64] bytes (Q6_K), msc [N*nb*16] bytes, md [N*nb] dwords.  N % 16 == 0.
+int amdk8s_llm_mfma_pack(int type, const void* q, const void* qh, const void* sc, const void* d,
+                         int N, int nb, void* mq, void* mqh, void* msc, void* md, void* stream) {
+  if (N <= 0 || N % 16 || nb <= 0 || (type != kQ4K && type != kQ6K)) return 2;
+  if (type == kQ6K && !(qh && mqh)) return 2;
+  const QMat w = {static_cast<const uint8_t*>(q), static_cast<const uint8_t*>(qh),
+                  static_cast<const int8_t*>(sc), static_cast<const uint16_t*>(d)};
+  const long n = (long)N * nb;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (type == kQ4K)
+    hipLaunchKernelGGL(mfma_pack_kernel<kQ4K>, grid, dim3(256), 0, st, w, N, nb,
+                       static_cast<uint8_t*>(mq), nullptr, static_cast<uint8_t*>(msc),
+                       static_cast<uint32_t*>(md));
+  else
+    hipLaunchKernelGGL(mfma_pack_kernel<kQ6K>, grid, dim3(256), 0, st, w, N, nb,
+                       static_cast<uint8_t*>(mq), static_cast<uint8_t*>(mqh),
+                       static_cast<uint8_t*>(msc), static_cast<uint32_t*>(md));
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// amdk8s_llm_qgemv2 on the int8 matrix cores over the MFMA-packed planes (q|k and v of different
+// quantisation types in one launch, up to 8 tokens).  4 = not covered (same types, N % 16, LDS):
+// launch the matrices with amdk8s_llm_qgemv_mfma.
+int amdk8s_llm_qgemv2_mfma(int type0, const void* w0q, const void* w0qh, const void* w0sc,
+                           const void* w0d, int N0, const void* bias0, void* out0, int type1,
+                           const void* w1q, const void* w1qh, const void* w1sc, const void* w1d,
+                           int N1, const void* bias1, void* out1, int ldo, const void* x8,
+                           const void* dx, const void* sx, const void* xf, int ldx,
+                           const void* norm_w, float eps, int K, int T, void* stream) {
+  if (K % 256 || N0 <= 0 || N1 <= 0 || T < 1 || T > kMaxTok) return 2;
+  if (!xf && !(x8 && dx && sx)) return 2;
+  if (xf && (ldx % 4 || T > kValuMaxTok)) return 2;
+  if (type0 == type1 || (type0 != kQ4K && type0 != kQ6K) || (type1 != kQ4K && type1 != kQ6K))
+    return 4;
+  GemvArgs a[2];
+  const int N[2] = {N0, N1};
+  const void* q[2][4] = {{w0q, w0qh, w0sc, w0d}, {w1q, w1qh, w1sc, w1d}};
+  const void* bias[2] = {bias0, bias1};
+  void* out[2] = {out0, out1};
+  for (int i = 0; i < 2; ++i) {
+    GemvArgs& g = a[i];
+    g = GemvArgs{};
+    g.w0 = {static_cast<const uint8_t*>(q[i][0]), static_cast<const uint8_t*>(q[i][1]),
+            static_cast<const int8_t*>(q[i][2]), static_cast<const uint16_t*>(q[i][3])};
+    g.x8 = static_cast<const int8_t*>(x8);
+    g.dx = static_cast<const float*>(dx);
+    g.sx = static_cast<const float*>(sx);
+    g.xf = static_cast<const float*>(xf);
+    g.ldx = ldx;
+    g.norm_w = static_cast<const float*>(norm_w);
+    g.eps = eps;
+    g.bias = static_cast<const float*>(bias[i]);
+    g.out = static_cast<float*>(out[i]);
+    g.ldo = ldo; g.N = N[i]; g.K = K; g.T = T; g.rows_per_wg = 0;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (type0 == kQ4K) return dispatch_mfma2<kQ4K, kQ6K>(a[0], a[1], st);
+  return dispatch_mfma2<kQ6K, kQ4K>(a[0], a[1], st);
+}
+
+}  // extern "C"
