@@ -33,6 +33,9 @@ sample fails gets that error, and no handler waits longer than ``--timeout`` sec
 Prompt caching (llama-server's ``cache_prompt``, on by default): every slot remembers which tokens
 its KV cache holds; a new request goes to the free slot sharing the longest prefix with its
 prompt, and only the rest of the prompt is prefilled (multi-turn chats re-send the whole history).
+As with llama-server, a reused prefix was computed in another prefill (a GEMM of another M), so
+the logits can differ in the last bits from an uncached prefill of the same prompt; decode itself
+is batch-invariant.
 """
 from __future__ import annotations
 
