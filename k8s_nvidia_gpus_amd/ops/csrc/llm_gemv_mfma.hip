@@ -7,7 +7,7 @@
 namespace {
 
 // ---------------------------------------------------------------- MFMA GEMV (int8 matrix cores)
-// The VALU GEMV above spends ~90 VALU per lane and super-block at T = 4 (eight v_dot4 plus the
+// The VALU GEMV (llm_decode.hip) spends ~90 VALU per lane and super-block at T = 4 (eight v_dot4 plus the
 // scale arithmetic per token on top of the weight decode), which makes steps of 2-4 tokens
 // VALU-bound (profiles/r04/f: gate|up 30 µs at T = 4 vs 20 µs at T = 1).  Here the integer
 // sub-block sums come from v_mfma_i32_16x16x64_i8 and only the per-sub-block scaling stays on the
@@ -19,10 +19,11 @@ namespace {
 // (t, s) carries token t's activations in K-group s only (zeros in the other three), so output
 // (t, s) of row r is the sum over K-group s alone, and every K-group's 16 values of one MFMA lie in
 // one sub-block.  Four MFMAs per super-block leave lane l = (row l & 15, token l >> 4) with the
-// sub-block sums of its own row and token (mfma_q4_block).  Each lane then scales its own
+// sub-block sums of its own row and token (mfma_block).  Each lane then scales its own
 // (row, token) in a fixed order, so a token's bits never depend on how many tokens share the
-// launch (batch-invariant).
-// Super-blocks are split over KW waves (reduced in LDS in wave order); RG row groups per workgroup.
+// launch (batch-invariant).  Steps of 5-8 tokens run a second token quad against the same weight
+// registers.  Super-blocks are split over KW waves (reduced in LDS in wave order); RG row groups
+// per workgroup; the shape is a function of the matrix only (mfma_shape).
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 // The MFMA kernel reads an MFMA-packed copy of the planes (amdk8s_llm_mfma_pack), laid out per
