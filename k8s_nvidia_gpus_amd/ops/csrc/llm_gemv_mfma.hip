@@ -25,6 +25,7 @@ namespace {
 // registers.  Super-blocks are split over KW waves (reduced in LDS in wave order); RG row groups
 // per workgroup; the shape is a function of the matrix only (mfma_shape).
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // The MFMA kernel reads an MFMA-packed copy of the planes (amdk8s_llm_mfma_pack), laid out per
 // (16-row group G, super-block b) so that each of a wave's loads per block reads whole contiguous
@@ -97,18 +98,21 @@ __device__ __forceinline__ float mfma_block(const MBlk<TYPE>& w, const i32x4 (&x
                           __uint_as_float(aux[1].x), __uint_as_float(aux[1].y),
                           __uint_as_float(aux[1].z), __uint_as_float(aux[1].w)};
     const uint32_t scw[4] = {w.sc.x, w.sc.y, w.sc.z, w.sc.w};
-    float sm = 0.f, mn = 0.f;
+    // even / odd sub-blocks in the two halves of packed-fp32 registers (v_pk_mul_f32 /
+    // v_pk_fma_f32: half the scaling instructions), added at the end in a fixed order
+    f32x2 sm = {0.f, 0.f}, mn = {0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float s0 = (float)(scw[i] & 0xffu), s1 = (float)((scw[i] >> 8) & 0xffu);
-      const float m0 = (float)((scw[i] >> 16) & 0xffu), m1 = (float)(scw[i] >> 24);
-      sm = __fmaf_rn((float)I[2 * i], __fmul_rn(s0, dxv[2 * i]), sm);
-      sm = __fmaf_rn((float)I[2 * i + 1], __fmul_rn(s1, dxv[2 * i + 1]), sm);
-      mn = __fmaf_rn(m0, spv[2 * i], mn);
-      mn = __fmaf_rn(m1, spv[2 * i + 1], mn);
+      const f32x2 sc2 = {(float)(scw[i] & 0xffu), (float)((scw[i] >> 8) & 0xffu)};
+      const f32x2 m2 = {(float)((scw[i] >> 16) & 0xffu), (float)(scw[i] >> 24)};
+      const f32x2 i2 = {(float)I[2 * i], (float)I[2 * i + 1]};
+      const f32x2 dx2 = {dxv[2 * i], dxv[2 * i + 1]};
+      const f32x2 sp2 = {spv[2 * i], spv[2 * i + 1]};
+      sm = __builtin_elementwise_fma(i2, sc2 * dx2, sm);
+      mn = __builtin_elementwise_fma(m2, sp2, mn);
     }
-    acc = __fmaf_rn(h2f(w.dd & 0xffffu), sm, acc);
-    return __fmaf_rn(-h2f(w.dd >> 16), mn, acc);
+    acc = __fmaf_rn(h2f(w.dd & 0xffffu), __fadd_rn(sm.x, sm.y), acc);
+    return __fmaf_rn(-h2f(w.dd >> 16), __fadd_rn(mn.x, mn.y), acc);
   } else {
     const int k = 2 * (g >> 1);
     const uint4 q0 = w.q0, q1 = w.q1, h0 = w.h0, h1 = w.h1;
