@@ -403,6 +403,9 @@ int launch_mfma_one(const GemvArgs& a, hipStream_t st) {
 // models with dim >= 8192 use the prologue at every T).
 void mfma_shape(bool pair, int N, int K, int& kw, int& rg) {
   const int nb = K >> 8;
+  // pair: 2 x 2.  1 x 2 (2 waves, whole K per wave) is faster alone (17.8 / 19.0 vs 18.5 / 20.4 us
+  // at T = 1 / 4) but, with its 2-wave RMSNorm prologue, slower in the step (T = 1 1.625 -> 1.664 ms,
+  // T = 8 2.94 -> 3.10 ms; profiles/r04/w)
   if (pair) kw = nb >= 2 ? 2 : 1, rg = 2;
   else if (K >= 8192) kw = 8, rg = 1;
   else if (N >= 65536 && nb >= 2) kw = 2, rg = 2;    // lm_head: 75.0 / 80.2 us at T = 1 / 4
