@@ -12,6 +12,7 @@
 #   bench            bench.py defaults (K=200 / W=20)
 #   native           amd-vectoradd, amd-gemm-validator (bf16 + fp8), amd-proftester
 #   llm[:<tokens>]   tools/llm_bench.py (decode T list, default 1,2,3,4) + prefill
+#   llm-ctx:<n>      tools/llm_bench.py decode T = 1,4,8 after an n-token prompt (long-context decode)
 #   gemv[:<cases>]   tools/llm_bench.py --gemv: cold-weight GEMV decomposition sweep, T = 1 and 4
 #   prof-bench       rocprofv3 --kernel-trace --stats of the driver's bench command
 #   prof-llm[:<T>]   rocprofv3 kernel trace of steady LLM decode at T tokens → per-kernel summary
@@ -87,6 +88,11 @@ for step in "$@"; do
         -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/prof_bench.log" 2>&1 \
         || fail "$step" $? "$OUT/prof_bench.log"
       find "$OUT/prof_bench" -name "*kernel_stats.csv" -exec head -6 {} \; | cut -c1-200 ;;
+    llm-ctx:*)
+      np="${step#llm-ctx:}"
+      timeout -k 10 500 python -u tools/llm_bench.py --tokens 1,4,8 --prompt "$np" --out "$OUT/llm_ctx_$np.json" \
+        > "$OUT/llm_ctx_$np.log" 2>&1 || fail "$step" $? "$OUT/llm_ctx_$np.log"
+      grep -E "decode|prefill" "$OUT/llm_ctx_$np.log" | grep -v '^{' ;;
     prof-llm|prof-llm:*)
       t=1; [[ "$step" == prof-llm:* ]] && t="${step#prof-llm:}"
       timeout -k 10 400 rocprofv3 --kernel-trace --output-format rocpd -d "$OUT/prof_llm_t$t" -o llm \
