@@ -266,6 +266,27 @@ struct AttnArgs {
   float* pml;
 };
 
+// Output dim dd of head h, token t: fp32 (optional) and Q8 with its 32-block scale and 16-block
+// scaled sums (the o_proj GEMV input); a 32-dim block = half a wave.
+__device__ __forceinline__ void attn_out_q8(float y, int h, int t, int dd, int H,
+                                            float* __restrict__ out, int8_t* __restrict__ x8,
+                                            float* __restrict__ dx, float* __restrict__ sx) {
+  const int K = H * kHeadDim;
+  const int col = h * kHeadDim + dd;
+  if (out) out[(long)t * K + col] = y;
+  float amax = fabsf(y);
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, kWave));
+  const float d = amax / 127.f;
+  const int qv = d > 0.f ? (int)__builtin_rintf(y / d) : 0;
+  x8[(long)t * K + col] = (int8_t)qv;
+  int s16 = qv;
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) s16 += __shfl_xor(s16, o, kWave);
+  if ((dd & 31) == 0) dx[(long)t * (K >> 5) + (col >> 5)] = d;
+  if ((dd & 15) == 0) sx[(long)t * (K >> 4) + (col >> 4)] = d * (float)s16;
+}
+
 // Merge the context chunks of head h of token t and quantise the attention output to Q8 (the o_proj
 // input): thread dd = one output dim; a 32-dim block = half a wave (dd & 31 within a wave).  One
 // pass over the chunks in groups of 8 with every partial of the group loaded before any maths
@@ -316,25 +337,11 @@ __device__ __forceinline__ void combine_heads(const float* __restrict__ po,
       m[k] = mn;
     }
   }
-  const int K = H * kHeadDim;
 #pragma unroll
   for (int k = 0; k < NH; ++k) {
     const int h = h0 + k * hstep;
     if (h >= hend) break;                            // uniform per wave (hstep multiple of waves)
-    const float y = den[k] > 0.f ? __fdiv_rn(v[k], den[k]) : 0.f;
-    const int col = h * kHeadDim + dd;
-    if (out) out[(long)t * K + col] = y;
-    float amax = fabsf(y);
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, kWave));
-    const float d = amax / 127.f;
-    const int qv = d > 0.f ? (int)__builtin_rintf(y / d) : 0;
-    x8[(long)t * K + col] = (int8_t)qv;
-    int s16 = qv;
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) s16 += __shfl_xor(s16, o, kWave);
-    if ((dd & 31) == 0) dx[(long)t * (K >> 5) + (col >> 5)] = d;
-    if ((dd & 15) == 0) sx[(long)t * (K >> 4) + (col >> 4)] = d * (float)s16;
+    attn_out_q8(den[k] > 0.f ? __fdiv_rn(v[k], den[k]) : 0.f, h, t, dd, H, out, x8, dx, sx);
   }
 }
 
@@ -349,6 +356,75 @@ __global__ void __launch_bounds__(128) attn_combine_q8_kernel(const float* __res
                                                               float* __restrict__ sx) {
   combine_heads<1>(po, pml, pos, H, nsplit, chunk, blockIdx.x, 1, H, blockIdx.y, threadIdx.x, out,
                    x8, dx, sx);
+}
+
+// Two-pass merge for the same (head, token) with 128 threads: every chunk's (max, sum) and the first
+// kCombBatch partial rows are loaded together; the max and the denominator are workgroup
+// reductions (the chunk weights go to LDS); the partial rows are then summed with their weights.
+// No online rescaling, so the row loads never wait on maths: one memory round trip per kCombBatch
+// chunks, where the online merge above takes one per 8 (its cost grew from 4.9 to 8.6 us between
+// 512 and 3584 positions, profiles/r04/z2).  nsplit <= kCombMaxSplit.
+constexpr int kCombBatch = 32;
+constexpr int kCombMaxSplit = 512;                  // max_ctx <= 32768 with 64-position chunks
+
+__global__ void __launch_bounds__(128) attn_combine2_q8_kernel(const float* __restrict__ po,
+                                                               const float* __restrict__ pml,
+                                                               const int* __restrict__ pos, int H,
+                                                               int nsplit, int chunk,
+                                                               float* __restrict__ out,
+                                                               int8_t* __restrict__ x8,
+                                                               float* __restrict__ dx,
+                                                               float* __restrict__ sx) {
+  constexpr int kPer = kCombMaxSplit / 128;
+  __shared__ float wts[kCombMaxSplit];
+  __shared__ float red[2][2];
+  const int h = blockIdx.x, t = blockIdx.y, dd = threadIdx.x, wave = dd >> 6;
+  const int ns = min(nsplit, (pos[t] + chunk) / chunk);
+  const long hb = ((long)t * H + h) * nsplit;
+  float ov[kCombBatch];                              // indices clamped: rows < ns are all written
+#pragma unroll
+  for (int u = 0; u < kCombBatch; ++u) ov[u] = po[(hb + min(u, ns - 1)) * kHeadDim + dd];
+  float mx[kPer], l[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const long sidx = hb + min(dd + 128 * k, ns - 1);
+    mx[k] = pml[sidx * 2];
+    l[k] = pml[sidx * 2 + 1];
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    if (dd + 128 * k >= ns) mx[k] = -INFINITY;
+    m = fmaxf(m, mx[k]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, kWave));
+  if ((dd & 63) == 0) red[0][wave] = m;
+  __syncthreads();
+  const float M = fmaxf(red[0][0], red[0][1]);
+  float dp = 0.f;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const float w = (M == -INFINITY || mx[k] == -INFINITY) ? 0.f : __expf(__fsub_rn(mx[k], M));
+    wts[dd + 128 * k] = w;
+    dp = __fmaf_rn(w, l[k], dp);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) dp = __fadd_rn(dp, __shfl_xor(dp, o, kWave));
+  if ((dd & 63) == 0) red[1][wave] = dp;
+  __syncthreads();
+  const float den = __fadd_rn(red[1][0], red[1][1]);
+  float v = 0.f;
+#pragma unroll
+  for (int u = 0; u < kCombBatch; ++u) v = __fmaf_rn(u < ns ? wts[u] : 0.f, ov[u], v);
+  for (int s0 = kCombBatch; s0 < ns; s0 += kCombBatch) {
+#pragma unroll
+    for (int u = 0; u < kCombBatch; ++u) ov[u] = po[(hb + min(s0 + u, ns - 1)) * kHeadDim + dd];
+#pragma unroll
+    for (int u = 0; u < kCombBatch; ++u)
+      v = __fmaf_rn(s0 + u < ns ? wts[min(s0 + u, kCombMaxSplit - 1)] : 0.f, ov[u], v);
+  }
+  attn_out_q8(den > 0.f ? __fdiv_rn(v, den) : 0.f, h, t, dd, H, out, x8, dx, sx);
 }
 
 template <int G>
@@ -985,7 +1061,8 @@ int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* 
                        st, aa);
   });
   if (rc) return rc;
-  hipLaunchKernelGGL(attn_combine_q8_kernel, dim3(H, T), dim3(128), 0, st,
+  hipLaunchKernelGGL(aa.nsplit <= kCombMaxSplit ? attn_combine2_q8_kernel : attn_combine_q8_kernel,
+                     dim3(H, T), dim3(128), 0, st,
                      static_cast<const float*>(po), static_cast<const float*>(pml),
                      static_cast<const int*>(pos), H, aa.nsplit, kAttnChunk, static_cast<float*>(out),
                      static_cast<int8_t*>(x8), static_cast<float*>(dx), static_cast<float*>(sx));

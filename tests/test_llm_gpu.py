@@ -361,6 +361,35 @@ def test_rope_kv_and_decode_attention(dev, LK, H, Hkv):
     assert ((xq - out).abs() <= dx.repeat_interleave(32, 1) * 0.5 + 1e-5).all()
 
 
+@pytest.mark.parametrize("max_ctx", [4096, 65536])
+def test_decode_attention_long_context(dev, LK, max_ctx):
+    """Up to 4096 positions the chunk merge takes more than one batch of partial rows (the two-pass
+    combine); at 65536 (1024 chunks > its LDS weight table) the launcher keeps the online merge.
+    Both vs the fp32 softmax reference."""
+    torch.manual_seed(11)
+    H, Hkv, slots, T = 28, 4, 2, 4
+    kc = (torch.randn(slots, Hkv, max_ctx, 128, device=dev) * 0.5).half()
+    vc = torch.randn(slots, Hkv, max_ctx, 128, device=dev).half()
+    pos = torch.tensor([4095, 2047, 5, 1090], dtype=torch.int32, device=dev)
+    slot = torch.tensor([0, 1, 0, 1], dtype=torch.int32, device=dev)
+    q = torch.randn(T, H * 128, device=dev)
+    nsplit = max_ctx // LK.attn_chunk()
+    po = torch.empty(T, H, nsplit, 128, device=dev)
+    pml = torch.empty(T, H, nsplit, 2, device=dev)
+    x8 = torch.empty(T, H * 128, dtype=torch.int8, device=dev)
+    dx = torch.empty(T, H * 4, device=dev)
+    sx = torch.empty(T, H * 8, device=dev)
+    out = torch.empty(T, H * 128, device=dev)
+    LK.attn_decode(q, pos, slot, kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128), po, pml,
+                   x8, dx, sx, out=out, span=max_ctx)
+    ref = _attn_ref(q, kc, vc, pos, slot, H, Hkv)
+    torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-3)
+    xq = (x8.float().view(T, -1, 32) * dx[..., None]).view(T, -1)
+    assert ((xq - out).abs() <= dx.repeat_interleave(32, 1) * 0.5 + 1e-5).all()
+    sums = (x8.float().view(T, -1, 16).sum(-1)) * dx.repeat_interleave(2, -1)
+    torch.testing.assert_close(sx, sums, rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.parametrize("H,Hkv", [(28, 4), (8, 8)])
 def test_fused_rope_attention_equals_separate_kernels(dev, LK, H, Hkv):
     """Distinct slots: RoPE + KV write inside the attention kernel == rope_kv + attention."""

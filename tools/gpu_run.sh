@@ -15,7 +15,7 @@
 #   llm-ctx:<n>      tools/llm_bench.py decode T = 1,4,8 after an n-token prompt (long-context decode)
 #   gemv[:<cases>]   tools/llm_bench.py --gemv: cold-weight GEMV decomposition sweep, T = 1 and 4
 #   prof-bench       rocprofv3 --kernel-trace --stats of the driver's bench command
-#   prof-llm[:<T>]   rocprofv3 kernel trace of steady LLM decode at T tokens → per-kernel summary
+#   prof-llm[:<T>[:<prompt>]]   rocprofv3 kernel trace of steady LLM decode at T tokens → per-kernel summary
 #   pmc-llm[:<T>]    tools/llm_pmc.sh: PMC passes (busy / VALU / wait shares, HBM bytes) at T tokens
 #   sd15 / wan       tools/sd15_bench.py / tools/wan_bench.py
 #   env:VAR=VALUE    export VAR for the following steps (A/B knobs)
@@ -94,9 +94,10 @@ for step in "$@"; do
         > "$OUT/llm_ctx_$np.log" 2>&1 || fail "$step" $? "$OUT/llm_ctx_$np.log"
       grep -E "decode|prefill" "$OUT/llm_ctx_$np.log" | grep -v '^{' ;;
     prof-llm|prof-llm:*)
-      t=1; [[ "$step" == prof-llm:* ]] && t="${step#prof-llm:}"
+      t=1; np=512; [[ "$step" == prof-llm:* ]] && t="${step#prof-llm:}"
+      [[ "$t" == *:* ]] && { np="${t#*:}"; t="${t%%:*}"; }
       timeout -k 10 400 rocprofv3 --kernel-trace --output-format rocpd -d "$OUT/prof_llm_t$t" -o llm \
-        -- python3 tools/steady_prof.py llm-decode --tokens "$t" --iters 20 --warmup 5 > "$OUT/prof_llm_t$t.log" 2>&1 \
+        -- python3 tools/steady_prof.py llm-decode --tokens "$t" --prompt "$np" --iters 20 --warmup 5 > "$OUT/prof_llm_t$t.log" 2>&1 \
         || fail "$step" $? "$OUT/prof_llm_t$t.log"
       db=$(find "$OUT/prof_llm_t$t" -name '*.db' | head -1)
       python3 tools/rocpd_summary.py "$db" --after-gap-ms 200 --per 20 --top 30 > "$OUT/llm_decode_t${t}_kernels.txt" \

@@ -40,14 +40,14 @@ def wan_step():
     return lambda: model(x, 0.7)
 
 
-def llm_decode(T: int = 1):
+def llm_decode(T: int = 1, P: int = 512):
     from k8s_nvidia_gpus_amd.models.llm.config import QWEN25_7B
     from k8s_nvidia_gpus_amd.models.llm.engine import Engine
     from k8s_nvidia_gpus_amd.models.llm.weights import ModelWeights
 
     w = ModelWeights.random(QWEN25_7B, device=torch.device("cuda", 0), seed=0)
     eng = Engine(w, max_ctx=4096, slots=8, dense=True)
-    prompt = list(range(100, 612))
+    prompt = list(range(100, 100 + P))
     for s in range(T):
         eng.prefill(prompt, slot=s)
     state = {"pos": len(prompt), "tok": [11] * T}
@@ -56,7 +56,7 @@ def llm_decode(T: int = 1):
         p = state["pos"]
         nxt = eng.decode_greedy(state["tok"], [p] * T, list(range(T)))
         state["tok"] = [int(x) % QWEN25_7B.vocab for x in nxt]
-        state["pos"] = p + 1 if p + 1 < 1000 else len(prompt)
+        state["pos"] = p + 1 if p + 1 < min(P + 488, 4000) else len(prompt)
     return step
 
 
@@ -76,10 +76,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("what", choices=["sd15-unet", "wan-step", "llm-decode", "llm-prefill"])
     ap.add_argument("--tokens", type=int, default=1, help="llm-decode: concurrent sequences")
+    ap.add_argument("--prompt", type=int, default=512, help="llm-decode: prompt tokens per sequence")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     a = ap.parse_args()
-    fn = (llm_decode(a.tokens) if a.what == "llm-decode" else llm_prefill() if a.what == "llm-prefill"
+    fn = (llm_decode(a.tokens, a.prompt) if a.what == "llm-decode" else llm_prefill() if a.what == "llm-prefill"
           else {"sd15-unet": sd15_unet, "wan-step": wan_step}[a.what]())
     for _ in range(a.warmup):
         fn()
