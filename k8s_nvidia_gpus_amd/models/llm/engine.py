@@ -131,6 +131,11 @@ class Engine:
                                           for w in [L.wo, L.wg, L.wu, L.wd] + list(L.wqkv)]
                 if not all([w.mfma_pack() for w in mats]):
                     self.max_T = min(self.max_T, 4)
+            if self.cfg.dim >= 8192:
+                # such models normalise in the 8-wave GEMV prologues at every T (one reduction
+                # order, so decode stays batch-invariant), and the prologue form takes at most 4
+                # tokens: larger batches run as steps of 4
+                self.max_T = min(self.max_T, 4)
         else:
             self.max_T = 4
         self.stats = {"decode_steps": 0, "decode_tokens": 0, "prefill_tokens": 0,

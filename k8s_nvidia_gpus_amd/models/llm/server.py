@@ -22,10 +22,11 @@ Request sampler fields are range-checked (400 on a non-finite temperature, ``rep
 at decode time ends only the request it belongs to.  Prompt tokenisation and template rendering
 run in the thread pool, never on the event loop.
 
-One scheduler thread owns the GPU: new requests are prefilled into free KV-cache slots, then every
-active sequence advances by one token per decode step — up to 4 sequences share each pass over
-the weights (``--parallel``).  Request handlers only wait on per-request queues, so the GPU is never
-driven from two threads (the reference's SD15 app had that hazard).  A request
+One scheduler thread owns the GPU: new requests take free KV-cache slots and their prompts are
+processed in chunks of ``--ubatch-size`` tokens, one chunk per loop iteration, between the decode
+steps of the sequences already generating — up to 8 sequences share each pass over the weights
+(``--parallel``).  Request handlers await per-request events that the scheduler sets, so the GPU is
+never driven from two threads (the reference's SD15 app had that hazard).  A request
 whose client goes away (stream closed, or the connection dropped while a blocking request waits)
 is cancelled and frees its KV slot at the next decode step; a request whose prefill or first
 sample fails gets that error, and no handler waits longer than ``--timeout`` seconds.
@@ -71,14 +72,17 @@ class Job:
     seed: Optional[int] = None
     cache_prompt: bool = True
     stop: List[str] = field(default_factory=list)
+    ignore_eos: bool = False
     out: "queue.Queue" = field(default_factory=queue.Queue)
     # scheduler state
     slot: int = -1
-    pos: int = 0
+    pos: int = 0               # tokens whose KV the slot holds: prompt progress, then + generated
+    decoding: bool = False     # the prompt is done; the job takes one token per decode step
     last: int = 0
     gen: List[int] = field(default_factory=list)
-    text: str = ""
-    emitted: int = 0
+    parts: List[str] = field(default_factory=list)   # emitted text pieces
+    tail: str = ""             # decoded but held back: it may be the start of a stop string
+    detok: Any = None          # tokenizer.StreamDecoder of this job
     generator: Optional[torch.Generator] = None
     t_submit: float = 0.0
     t_first: float = 0.0
@@ -86,6 +90,11 @@ class Job:
     finish: str = ""
     cancelled: bool = False
     n_cached: int = 0          # prompt tokens whose KV was reused from the slot
+    waker: Any = None          # (event loop, asyncio.Event) of the coroutine waiting on ``out``
+
+    @property
+    def text(self) -> str:
+        return "".join(self.parts)
 
 
 def common_prefix(a: List[int], b: List[int]) -> int:
@@ -96,21 +105,43 @@ def common_prefix(a: List[int], b: List[int]) -> int:
     return i
 
 
-class Scheduler:
-    """Continuous batching over the engine's KV-cache slots."""
+def _set_events(events) -> None:
+    for e in events:
+        e.set()
 
-    def __init__(self, engine: Engine, tok: Tokenizer, parallel: int = 4):
+
+class Scheduler:
+    """Continuous batching over the engine's KV-cache slots, with chunked prompt processing.
+
+    One loop iteration: admit pending requests into free slots → run ONE chunk (at most
+    ``ubatch`` tokens) of the oldest admitted prompt → one decode step of every sequence whose
+    prompt is done → wake the consumers.  A long prompt therefore stalls the running streams for
+    one chunk at a time, not for its whole prefill: llama-server's update loop does the same with
+    its ``n_ubatch`` prompt batches next to the decoding slots (reference
+    cluster-config/apps/llm/deployment.yaml:61,76-84 runs llama-server).  While no sequence is
+    decoding, chunks grow to ``batch`` tokens (llama-server's ``n_batch``).
+
+    Host work per generated token is independent of the length of the output: each token is
+    detokenised alone (``StreamDecoder``: incomplete UTF-8 carried over) and the stop strings are
+    searched only in the held-back tail plus the new text."""
+
+    def __init__(self, engine: Engine, tok: Tokenizer, parallel: int = 8, ubatch: int = 512,
+                 batch: Optional[int] = None):
         self.engine = engine
         self.tok = tok
         self.parallel = max(1, min(parallel, engine.slots))
+        self.ubatch = max(1, int(ubatch))
+        self.batch = max(self.ubatch, int(batch or self.ubatch))
         self.pending: "queue.Queue[Job]" = queue.Queue()
-        self.active: Dict[int, Job] = {}
-        self.slot_tokens: Dict[int, List[int]] = {}      # tokens whose KV each slot holds
+        self.active: Dict[int, Job] = {}                 # slot -> job (prompt or decode phase)
+        self.prefilling: List[Job] = []                  # admitted, prompt not done (FIFO)
+        self.slot_tokens: Dict[int, List[int]] = {}      # tokens whose KV each free slot holds
         self.stop_ids = set(tok.stop_ids())
         self.metrics = {"requests_total": 0, "prompt_tokens_total": 0, "tokens_predicted_total": 0,
                         "decode_steps_total": 0, "decode_seconds_total": 0.0,
-                        "prefill_seconds_total": 0.0, "requests_processing": 0,
-                        "prompt_tokens_cached_total": 0}
+                        "prefill_seconds_total": 0.0, "prefill_chunks_total": 0,
+                        "requests_processing": 0, "prompt_tokens_cached_total": 0}
+        self._touched: List[Job] = []
         self._run = True
         self._lock = threading.Lock()
         self.thread = threading.Thread(target=self._loop, name="llm-scheduler", daemon=True)
@@ -135,6 +166,26 @@ class Scheduler:
         self.thread.join(timeout=10)
 
     # ---------------------------------------------------------------- scheduler thread
+    def _put(self, job: Job, item) -> None:
+        job.out.put(item)
+        self._touched.append(job)
+
+    def _wake(self) -> None:
+        """One ``call_soon_threadsafe`` per event loop for everything this iteration produced."""
+        if not self._touched:
+            return
+        by_loop: Dict[Any, list] = {}
+        for j in self._touched:
+            w = j.waker
+            if w is not None:
+                by_loop.setdefault(w[0], []).append(w[1])
+        self._touched = []
+        for loop, events in by_loop.items():
+            try:
+                loop.call_soon_threadsafe(_set_events, events)
+            except RuntimeError:      # that loop has closed: nobody is waiting any more
+                pass
+
     def _free_slot(self, ids: Optional[List[int]] = None) -> int:
         """A free slot: the one whose cached tokens share the longest prefix with ``ids``, else
         the one with the least cached context (keeps other conversations' caches warm)."""
@@ -148,53 +199,73 @@ class Scheduler:
 
     def _release(self, job: Job) -> None:
         """Forget ``job``'s slot assignment; its KV (the first ``pos`` tokens) stays reusable."""
+        if job.slot < 0:
+            return
         self.slot_tokens[job.slot] = (job.ids + job.gen)[:job.pos]
-        self.active.pop(job.slot, None)
+        if self.active.get(job.slot) is job:
+            del self.active[job.slot]
+
+    def _fail(self, job: Job, e: Exception) -> None:
+        with self._lock:
+            self.metrics["requests_failed_total"] = self.metrics.get("requests_failed_total", 0) + 1
+        self._put(job, ("error", repr(e)))
+        self._release(job)
+
+    @staticmethod
+    def _recent(job: Job) -> List[int]:
+        """The history the sampler's repetition penalties look at (``repeat_last_n`` tokens of
+        prompt + output; all of it for -1) — not a copy of the whole sequence per token."""
+        n = job.params.repeat_last_n
+        if n < 0:
+            return job.ids + job.gen
+        if n == 0:
+            return []
+        g = job.gen[-n:]
+        if len(g) == n:
+            return g
+        return job.ids[max(0, len(job.ids) - (n - len(g))):] + g
 
     def _emit(self, job: Job, tok: int) -> bool:
         """Record a sampled token; returns True when the job is finished."""
         job.gen.append(tok)
         job.last = tok
-        if tok in self.stop_ids:
+        if tok in self.stop_ids and not job.ignore_eos:
             job.finish = "stop"
-            self._flush(job, final=True)
+            self._flush(job, job.detok.flush(), final=True)
             return True
-        text = self.tok.decode(job.gen)
-        cut = None
-        for s in job.stop:
-            i = text.find(s)
-            if i >= 0 and (cut is None or i < cut):
-                cut = i
-        if cut is not None:
-            job.text = text[:cut]
-            job.finish = "stop"
-            self._flush(job, final=True)
-            return True
-        job.text = text
+        new = job.detok.push(tok)
         if len(job.gen) >= job.max_new:
             job.finish = "length"
-            self._flush(job, final=True)
+            self._flush(job, new + job.detok.flush(), final=True)
             return True
-        self._flush(job, final=False)
-        return False
+        return self._flush(job, new, final=False)
 
-    def _flush(self, job: Job, final: bool) -> None:
-        text = job.text
+    def _flush(self, job: Job, new: str, final: bool) -> bool:
+        """Emit ``job.tail + new`` up to a stop string (then the job ends, reason "stop"), holding
+        back a suffix that may still grow into one.  Returns True when a stop string ended it."""
+        s = job.tail + new
+        cut = -1
+        for st in job.stop:
+            i = s.find(st)
+            if i >= 0 and (cut < 0 or i < cut):
+                cut = i
         hold = 0
-        if not final:
-            if text.endswith("�"):          # an incomplete UTF-8 sequence: wait for more bytes
-                hold = 1
-            for s in job.stop:                    # a stop string may be starting: hold its prefix
-                for k in range(min(len(s) - 1, len(text)), 0, -1):
-                    if text.endswith(s[:k]):
-                        hold = max(hold, k)
+        if cut >= 0:
+            s, final = s[:cut], True
+            job.finish = "stop"
+        elif not final:
+            for st in job.stop:                  # a stop string may be starting: hold its prefix
+                for k in range(min(len(st) - 1, len(s)), hold, -1):
+                    if s.endswith(st[:k]):
+                        hold = k
                         break
-        upto = len(text) - hold
-        if upto > job.emitted:
-            job.out.put(("text", text[job.emitted:upto]))
-            job.emitted = upto
+        piece, job.tail = s[:len(s) - hold], s[len(s) - hold:]
+        if piece:
+            job.parts.append(piece)
+            self._put(job, ("text", piece))
         if final:
-            job.out.put(("done", job))
+            self._put(job, ("done", job))
+        return cut >= 0
 
     def _admit(self) -> None:
         while len(self.active) < self.parallel:
@@ -207,47 +278,68 @@ class Scheduler:
             if job.cancelled:
                 continue
             slot = self._free_slot(job.ids if job.cache_prompt else None)
-            job.slot = slot
             try:
                 if job.params.temperature > 0:
                     dev = self.engine.device if self.engine.gpu else "cpu"
                     job.generator = torch.Generator(device=dev)
                     job.generator.manual_seed(job.seed if job.seed is not None
                                               else int.from_bytes(os.urandom(4), "little"))
-                # reuse the slot's KV for the shared prefix; at least one token is prefilled (its
-                # logits are the first sample)
-                n_past = 0
-                if job.cache_prompt:
-                    n_past = min(common_prefix(self.slot_tokens.get(slot, []), job.ids),
-                                 len(job.ids) - 1)
-                self.slot_tokens[slot] = []                 # the KV is being rewritten
-                job.n_cached = n_past
-                t0 = time.perf_counter()
-                logits = self.engine.prefill(job.ids[n_past:], slot, start=n_past)
-                tok = sample_token(logits, job.params, job.ids, job.generator)
-                job.t_prefill = time.perf_counter() - t0
-                job.t_first = time.perf_counter()
-                with self._lock:
-                    self.metrics["prompt_tokens_total"] += len(job.ids) - n_past
-                    self.metrics["prompt_tokens_cached_total"] += n_past
-                    self.metrics["prefill_seconds_total"] += job.t_prefill
-                    self.metrics["tokens_predicted_total"] += 1
-                job.pos = len(job.ids)
-                finished = self._emit(job, tok)
-            except Exception as e:  # noqa: BLE001 - this job fails; the others keep decoding
-                with self._lock:
-                    self.metrics["requests_failed_total"] = self.metrics.get("requests_failed_total", 0) + 1
-                job.out.put(("error", repr(e)))
+                job.detok = self.tok.stream()
+            except Exception as e:  # noqa: BLE001 - this job fails; the others keep going
+                self._fail(job, e)
                 continue
-            if finished:
-                self._release(job)
-            else:
-                self.active[slot] = job
+            # reuse the slot's KV for the shared prefix; at least one token is prefilled (its
+            # logits are the first sample)
+            n_past = 0
+            if job.cache_prompt:
+                n_past = min(common_prefix(self.slot_tokens.get(slot, []), job.ids),
+                             len(job.ids) - 1)
+            self.slot_tokens[slot] = []                 # the KV is being rewritten
+            job.slot, job.pos, job.n_cached = slot, n_past, n_past
+            self.active[slot] = job
+            self.prefilling.append(job)
+
+    def _prefill_chunk(self) -> None:
+        """One chunk of the oldest admitted prompt; its last chunk samples the first token."""
+        for j in [j for j in self.prefilling if j.cancelled]:
+            self.prefilling.remove(j)
+            self._release(j)
+        if not self.prefilling:
+            return
+        job = self.prefilling[0]
+        limit = self.ubatch if any(j.decoding for j in self.active.values()) else self.batch
+        n = min(limit, len(job.ids) - job.pos)
+        t0 = time.perf_counter()
+        try:
+            logits = self.engine.prefill(job.ids[job.pos:job.pos + n], job.slot, start=job.pos)
+            done = job.pos + n == len(job.ids)
+            tok = sample_token(logits, job.params, self._recent(job), job.generator) if done else None
+        except Exception as e:  # noqa: BLE001 - this job fails; the others keep decoding
+            self.prefilling.pop(0)
+            self._fail(job, e)
+            return
+        dt = time.perf_counter() - t0
+        job.pos += n
+        job.t_prefill += dt
+        with self._lock:
+            self.metrics["prompt_tokens_total"] += n
+            self.metrics["prefill_seconds_total"] += dt
+            self.metrics["prefill_chunks_total"] += 1
+        if not done:
+            return
+        self.prefilling.pop(0)
+        job.t_first = time.perf_counter()
+        job.decoding = True
+        with self._lock:
+            self.metrics["prompt_tokens_cached_total"] += job.n_cached
+            self.metrics["tokens_predicted_total"] += 1
+        if self._emit(job, int(tok)):
+            self._release(job)
 
     def _step(self) -> None:
-        jobs = [j for j in self.active.values() if not j.cancelled]
-        for j in [j for j in self.active.values() if j.cancelled]:
+        for j in [j for j in self.active.values() if j.decoding and j.cancelled]:
             self._release(j)
+        jobs = [j for j in self.active.values() if j.decoding]
         if not jobs:
             return
         t0 = time.perf_counter()
@@ -259,7 +351,7 @@ class Scheduler:
             toks = []
             for i, j in enumerate(jobs):
                 try:   # a request's own sampler failure ends that request only
-                    toks.append(sample_token(logits[i], j.params, j.ids + j.gen, j.generator))
+                    toks.append(sample_token(logits[i], j.params, self._recent(j), j.generator))
                 except Exception as e:  # noqa: BLE001
                     toks.append(e)
         dt = time.perf_counter() - t0
@@ -270,10 +362,7 @@ class Scheduler:
         for j, t in zip(jobs, toks):
             j.pos += 1          # the step wrote this job's KV either way
             if isinstance(t, Exception):
-                with self._lock:
-                    self.metrics["requests_failed_total"] = self.metrics.get("requests_failed_total", 0) + 1
-                j.out.put(("error", repr(t)))
-                self._release(j)
+                self._fail(j, t)
             elif self._emit(j, int(t)):
                 self._release(j)
 
@@ -282,12 +371,17 @@ class Scheduler:
             try:
                 self._admit()
                 self.metrics["requests_processing"] = len(self.active)
+                self._prefill_chunk()
+                self._wake()                 # a finished prompt's first token goes out now
                 self._step()
+                self._wake()
             except Exception as e:  # surface to every waiting request, keep serving
                 for j in list(self.active.values()):
-                    j.out.put(("error", repr(e)))
+                    self._put(j, ("error", repr(e)))
                 self.active.clear()
+                self.prefilling.clear()
                 self.slot_tokens.clear()
+                self._wake()
 
 
 # -------------------------------------------------------------------- HTTP layer
@@ -301,66 +395,84 @@ def _job_from(body: Dict[str, Any], ids: List[int], default_max: int,
         n = default_max
     return Job(ids=ids, max_new=int(n), params=SamplingParams.from_request(body, vocab),
                seed=None if body.get("seed") in (None, -1) else int(body["seed"]), stop=list(stop),
-               cache_prompt=bool(body.get("cache_prompt", True)))
+               cache_prompt=bool(body.get("cache_prompt", True)),
+               ignore_eos=bool(body.get("ignore_eos", False)))
 
 
 class RequestTimeout(RuntimeError):
     pass
 
 
-def _get(job: Job, deadline: float, poll: Optional[float] = None):
-    """Next (kind, value) of ``job``; raises RequestTimeout past ``deadline`` (perf_counter)."""
-    left = deadline - time.perf_counter()
-    if left <= 0:
-        job.cancelled = True
-        raise RequestTimeout("request timed out")
-    return job.out.get(timeout=left if poll is None else min(left, poll))
+async def _events(job: Job, timeout: float, disconnected=None):
+    """(kind, value) events of ``job`` as the scheduler produces them.  The scheduler wakes this
+    coroutine with one ``call_soon_threadsafe`` per event loop and step (``Scheduler._wake``), so a
+    waiting request holds no executor thread (polling through ``run_in_executor`` made
+    token delivery queue behind idle connections).  After 0.5 s without an event
+    ``disconnected()`` is polled: a client that went away while its job waits for a slot or
+    between tokens is noticed and the job cancelled (``ConnectionAbortedError``); past
+    ``timeout`` the job is cancelled and ``RequestTimeout`` raised."""
+    deadline = time.perf_counter() + timeout
+    loop = asyncio.get_running_loop()
+    ev = asyncio.Event()
+    job.waker = (loop, ev)                 # registered before the queue is looked at
+    try:
+        while True:
+            try:
+                kind, val = job.out.get_nowait()
+            except queue.Empty:
+                ev.clear()
+                if not job.out.empty():
+                    continue
+                left = deadline - time.perf_counter()
+                if left <= 0:
+                    job.cancelled = True
+                    raise RequestTimeout("request timed out")
+                tick = loop.call_later(min(left, 0.5), ev.set)
+                await ev.wait()
+                tick.cancel()
+                if job.out.empty() and disconnected is not None and await disconnected():
+                    job.cancelled = True
+                    raise ConnectionAbortedError("client disconnected")
+                continue
+            yield kind, val
+            if kind in ("done", "error"):
+                return
+    finally:
+        job.waker = None
 
 
 async def _collect(job: Job, timeout: float, disconnected=None) -> Job:
-    """Wait for ``job`` without holding a worker thread; cancels it when ``disconnected()`` (the
-    client went away) or past ``timeout``."""
-    deadline = time.perf_counter() + timeout
-    loop = asyncio.get_running_loop()
-    while True:
-        try:
-            kind, val = await loop.run_in_executor(None, _get, job, deadline, 0.5)
-        except queue.Empty:
-            if disconnected is not None and await disconnected():
-                job.cancelled = True
-                raise ConnectionAbortedError("client disconnected")
-            continue
+    """The finished ``job`` (RuntimeError on its error); see ``_events``."""
+    async for kind, val in _events(job, timeout, disconnected):
         if kind == "error":
             raise RuntimeError(val)
         if kind == "done":
             return val
+    raise RuntimeError("job ended without a result")
 
 
 async def _astream(job: Job, timeout: float, disconnected=None):
-    """Async events of ``job`` for a streaming response.  Polls every 0.5 s, so a client that goes
-    away while the job still waits in the pending queue (or between tokens) is noticed through
-    ``disconnected()`` and the job cancelled — its slot is freed at the next decode step instead of
-    after the whole ``timeout``."""
-    deadline = time.perf_counter() + timeout
-    loop = asyncio.get_running_loop()
+    """Events of ``job`` for a streaming response; a client that goes away (``disconnected()``,
+    or the response generator closed) cancels the job, whose slot is freed at the next step."""
     finished = False
     try:
-        while True:
-            try:
-                kind, val = await loop.run_in_executor(None, _get, job, deadline, 0.5)
-            except queue.Empty:
-                if disconnected is not None and await disconnected():
-                    return
-                continue
+        async for kind, val in _events(job, timeout, disconnected):
             if kind == "error":
                 raise RuntimeError(val)
             yield kind, val
             if kind == "done":
                 finished = True
                 return
+    except ConnectionAbortedError:
+        return
     finally:
         if not finished:
             job.cancelled = True
+
+
+def _usage(job: Job) -> Dict[str, int]:
+    return {"prompt_tokens": len(job.ids), "completion_tokens": len(job.gen),
+            "total_tokens": len(job.ids) + len(job.gen)}
 
 
 def _timings(job: Job) -> Dict[str, Any]:
@@ -500,13 +612,14 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
                                                      else obj, "created": created,
                                                      "model": state.get("model"),
                                                      "choices": [ch]}) + "\n\n"
-                    else:
+                    else:     # the last chunk carries usage and llama-server's timings
                         ch = {"index": 0, "finish_reason": val.finish}
                         ch["delta" if chat else "text"] = {} if chat else ""
                         yield "data: " + json.dumps({"id": rid, "object": obj + ".chunk" if chat
                                                      else obj, "created": created,
                                                      "model": state.get("model"),
-                                                     "choices": [ch]}) + "\n\n"
+                                                     "choices": [ch], "usage": _usage(val),
+                                                     "timings": _timings(val)}) + "\n\n"
                 yield "data: [DONE]\n\n"
             return StreamingResponse(gen(), media_type="text/event-stream")
         job = await wait(job, request)
@@ -517,8 +630,7 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
             choice["text"] = job.text
         return {"id": rid, "object": obj, "created": created, "model": state.get("model"),
                 "choices": [choice],
-                "usage": {"prompt_tokens": len(job.ids), "completion_tokens": len(job.gen),
-                          "total_tokens": len(job.ids) + len(job.gen)},
+                "usage": _usage(job),
                 "timings": _timings(job)}
 
     @app.post("/v1/completions")
@@ -607,7 +719,13 @@ def main(argv=None) -> int:
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=8080)
     ap.add_argument("-c", "--ctx-size", type=int, default=4096)
-    ap.add_argument("-np", "--parallel", type=int, default=4)
+    ap.add_argument("-np", "--parallel", type=int, default=8,
+                    help="KV-cache slots = sequences sharing one decode step (the engine steps "
+                         "up to 8 tokens per pass over the weights)")
+    ap.add_argument("-ub", "--ubatch-size", type=int, default=512,
+                    help="prompt tokens per chunk while other sequences decode (llama-server -ub)")
+    ap.add_argument("-b", "--batch-size", type=int, default=2048,
+                    help="prompt tokens per chunk while nothing decodes (llama-server -b)")
     ap.add_argument("-ngl", "--n-gpu-layers", type=int, default=999, help="accepted; all layers run on the GPU")
     ap.add_argument("-t", "--threads", type=int, default=0, help="accepted; the GPU does the work")
     ap.add_argument("-to", "--timeout", type=float, default=600.0,
@@ -623,7 +741,9 @@ def main(argv=None) -> int:
         eng, tok, name = build_engine(args)
         if eng.gpu:
             eng.capture(range(1, min(args.parallel, eng.max_T) + 1))   # HIP graphs before ready
-        state.update(tok=tok, model=name, scheduler=Scheduler(eng, tok, args.parallel))
+        state.update(tok=tok, model=name, scheduler=Scheduler(eng, tok, args.parallel,
+                                                            ubatch=args.ubatch_size,
+                                                            batch=args.batch_size))
         print(f"model {name} ready (ctx {eng.max_ctx}, parallel {args.parallel})", flush=True)
 
     threading.Thread(target=load_bg, daemon=True).start()

@@ -84,6 +84,27 @@ class Tokenizer:
     def decode(self, ids: Sequence[int], skip_special: bool = True) -> str:
         return self._tk.decode(list(ids), skip_special_tokens=skip_special)
 
+    def token_bytes(self) -> List[bytes]:
+        """The bytes every token id stands for (control tokens: ``b""``, as :meth:`decode` skips
+        them), in the byte-level decoder's rule: a token whose characters are all in the byte
+        alphabet maps through it, any other token to its own UTF-8.  Built once, on first use."""
+        tb = getattr(self, "_token_bytes", None)
+        if tb is None:
+            inv = {c: b for b, c in bytes_to_unicode().items()}
+            tb = []
+            for i, t in enumerate(self.tokens):
+                if i in self.special_ids:
+                    tb.append(b"")
+                elif all(c in inv for c in t):
+                    tb.append(bytes(inv[c] for c in t))
+                else:
+                    tb.append(t.encode("utf-8"))
+            self._token_bytes = tb
+        return tb
+
+    def stream(self) -> "StreamDecoder":
+        return StreamDecoder(self)
+
     def token_id(self, text: str) -> Optional[int]:
         return self.vocab.get(text)
 
@@ -159,3 +180,22 @@ def synthetic_vocab(size: int, corpus: str = "") -> Dict:
             "tokenizer.ggml.bos_token_id": tokens.index("<|endoftext|>"),
             "tokenizer.ggml.add_bos_token": False,
             "tokenizer.chat_template": QWEN25_TEMPLATE}
+
+
+class StreamDecoder:
+    """Incremental detokenisation for streaming: each pushed token costs its own bytes, whatever
+    the length of the text so far.  An incomplete UTF-8 sequence at the end is carried into the
+    next push; ``flush`` ends it as U+FFFD, so the concatenated pieces equal
+    ``Tokenizer.decode`` of the whole sequence (CPU test ``test_stream_decoder_equals_decode``)."""
+
+    def __init__(self, tok: Tokenizer):
+        import codecs
+
+        self._tb = tok.token_bytes()
+        self._dec = codecs.getincrementaldecoder("utf-8")("replace")
+
+    def push(self, tok_id: int) -> str:
+        return self._dec.decode(self._tb[tok_id])
+
+    def flush(self) -> str:
+        return self._dec.decode(b"", final=True)

@@ -668,9 +668,10 @@ def test_random_7b_layer_shapes_run(dev):
 
 
 def test_server_on_gpu_concurrent_answers_equal_sequential(dev, tiny_gguf):
-    """The llama-server-compatible API on the GPU engine: 6 concurrent greedy requests share
-    decode steps (continuous batching over 4 slots) and still return exactly their sequential
-    answers — the decode kernels are batch-invariant."""
+    """The llama-server-compatible API on the GPU engine: 10 concurrent greedy requests share
+    decode steps (continuous batching over 8 slots, prompts in 8-token chunks between the decode
+    steps) and still return exactly their sequential answers — the decode kernels are
+    batch-invariant and the chunk boundaries do not depend on the load (ubatch = batch)."""
     from concurrent.futures import ThreadPoolExecutor
 
     from fastapi.testclient import TestClient
@@ -678,29 +679,100 @@ def test_server_on_gpu_concurrent_answers_equal_sequential(dev, tiny_gguf):
     from k8s_nvidia_gpus_amd.models.llm.server import Scheduler, create_app
     from k8s_nvidia_gpus_amd.models.llm.synthetic import load
 
-    eng, tok = load(tiny_gguf, device=dev, max_ctx=512, slots=4)
-    eng.capture((1, 2, 3, 4))
-    state = {"scheduler": Scheduler(eng, tok, parallel=4), "tok": tok, "model": "tiny"}
+    eng, tok = load(tiny_gguf, device=dev, max_ctx=512, slots=8)
+    eng.capture(range(1, 9))
+    sched = Scheduler(eng, tok, parallel=8, ubatch=8, batch=8)
+    state = {"scheduler": sched, "tok": tok, "model": "tiny"}
     c = TestClient(create_app(state))
     try:
-        prompts = [f"a cozy cabin number {i} in the woods" for i in range(6)]
+        prompts = [f"a cozy cabin number {i} in the woods " * (1 + i % 3) for i in range(10)]
         # cache_prompt off: a slot's cached prefix of an earlier prompt would be prefilled in a
         # GEMM of another M than the full prompt (tile / split-K choice by shape), so the reuse
         # pattern, which depends on scheduling, could change bits; this test is about decode
         body = lambda p: {"prompt": p, "n_predict": 12, "temperature": 0,  # noqa: E731
-                          "cache_prompt": False}
+                          "cache_prompt": False, "ignore_eos": True}
         seq = [c.post("/completion", json=body(p)).json()["content"] for p in prompts]
-        m0 = dict(state["scheduler"].metrics)
-        with ThreadPoolExecutor(6) as ex:
+        m0 = dict(sched.metrics)
+        with ThreadPoolExecutor(10) as ex:
             par = list(ex.map(lambda p: c.post("/completion", json=body(p)).json()["content"],
                               prompts))
-        m1 = state["scheduler"].metrics
+        m1 = sched.metrics
         assert par == seq
         assert m1["tokens_predicted_total"] - m0["tokens_predicted_total"] > \
             m1["decode_steps_total"] - m0["decode_steps_total"]        # multi-sequence steps
+        assert m1["prefill_chunks_total"] - m0["prefill_chunks_total"] > len(prompts)
         r = c.post("/v1/chat/completions", json={
             "messages": [{"role": "user", "content": "hello"}], "max_tokens": 8,
             "temperature": 0}).json()
         assert r["usage"]["completion_tokens"] <= 8
     finally:
-        state["scheduler"].close()
+        sched.close()
+
+
+@pytest.mark.parametrize("chunk", [7, 64])
+def test_chunked_prefill_matches_monolithic(dev, tiny_gguf, chunk):
+    """a prompt prefilled in chunks (each chunk attends to the cached prefix
+    through an explicit causal mask) gives the monolithic prefill's logits and KV cache within
+    fp16 rounding, and the same greedy continuation."""
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load
+
+    eng, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=True, slots=2)
+    p = tok.encode("the lazy dog jumps over a helpful assistant in a cozy cabin " * 4)
+    mono = eng.prefill(p, 0).cpu()
+    for s in range(0, len(p), chunk):
+        last = eng.prefill(p[s:s + chunk], 1, start=s)
+    last = last.cpu()
+    assert torch.nn.functional.cosine_similarity(mono[None], last[None]).item() > 0.9995
+    torch.testing.assert_close(last, mono, rtol=2e-2, atol=5e-2)
+    n = len(p)
+    for cache in (eng.k_cache, eng.v_cache):
+        torch.testing.assert_close(cache[:, 1, :, :n].float(), cache[:, 0, :, :n].float(),
+                                   rtol=1e-2, atol=1e-2)
+    assert int(last.argmax()) == int(mono.argmax())
+
+
+def test_chunked_prefill_7b_shapes_long_prefix(dev):
+    """The 7B attention layout (28 q heads over 4 kv heads) with a 3000-token prefix: chunks of
+    512 against the monolithic prefill, logits and the cache tail."""
+    from dataclasses import replace
+
+    from k8s_nvidia_gpus_amd.models.llm import QWEN25_7B
+    from k8s_nvidia_gpus_amd.models.llm.engine import Engine
+    from k8s_nvidia_gpus_amd.models.llm.weights import ModelWeights
+
+    cfg = replace(QWEN25_7B, layers=2)
+    eng = Engine(ModelWeights.random(cfg, device=dev, seed=3), max_ctx=4096, slots=2, dense=True)
+    g = torch.Generator().manual_seed(0)
+    p = torch.randint(0, 150000, (3000,), generator=g).tolist()
+    mono = eng.prefill(p, 0).float().cpu()
+    for s in range(0, len(p), 512):
+        last = eng.prefill(p[s:s + 512], 1, start=s)
+    last = last.float().cpu()
+    assert torch.nn.functional.cosine_similarity(mono[None], last[None]).item() > 0.999
+    torch.testing.assert_close(eng.k_cache[:, 1, :, 2900:3000].float(),
+                               eng.k_cache[:, 0, :, 2900:3000].float(), rtol=2e-2, atol=2e-2)
+
+
+def test_wide_model_steps_of_5_to_8_tokens(dev):
+    """a model with dim >= 8192 normalises in the 8-wave GEMV prologues, which take
+    at most 4 tokens; its engine steps at most 4 tokens (larger batches run as steps of 4) and
+    5..8 sequences decode with the logits each gets alone."""
+    from dataclasses import replace
+
+    from k8s_nvidia_gpus_amd.models.llm import QWEN25_7B
+    from k8s_nvidia_gpus_amd.models.llm.engine import Engine
+    from k8s_nvidia_gpus_amd.models.llm.weights import ModelWeights
+
+    cfg = replace(QWEN25_7B, dim=8192, heads=64, kv_heads=8, ffn=2048, layers=1, vocab=4096)
+    eng = Engine(ModelWeights.random(cfg, device=dev, seed=2), max_ctx=512, slots=8, dense=True)
+    assert eng.max_T == 4
+    for s in range(8):
+        eng.prefill([1 + s, 2, 3], slot=s)
+    for T in (5, 8):
+        toks = list(range(10, 10 + T))
+        batch = eng.decode(toks, [3] * T, list(range(T))).clone()
+        assert torch.isfinite(batch).all()
+        for s in range(T):
+            torch.testing.assert_close(batch[s], eng.decode([toks[s]], [3], [s])[0],
+                                       rtol=0, atol=0)
+        assert eng.decode_greedy(toks, [3] * T, list(range(T))) == batch.argmax(-1).tolist()

@@ -311,6 +311,49 @@ def _json_patch(doc, ops):
     return doc
 
 
+def test_llm_deployment_runs_the_server_with_flags_it_accepts():
+    """the shipped server runs 8 slots (the engine's step takes up to 8 tokens)
+    with chunked prompts, and every flag of the Deployment's command line is one server.main
+    parses (substituted with the Deployment's env values)."""
+    import shlex
+
+    from k8s_nvidia_gpus_amd.models.llm import server as S
+
+    _, objs = resources_of(CC / "apps/llm")
+    (dep,) = [o for o in objs if o["kind"] == "Deployment" and o["metadata"]["name"] == "coder-llm"]
+    c = dep["spec"]["template"]["spec"]["containers"][0]
+    env = {e["name"]: e["value"] for e in c["env"]}
+    assert env["PARALLEL_SLOTS"] == "8" and env["UBATCH_SIZE"] == "512"
+    script = c["args"][0].replace("\\\n", " ")
+    line = script[script.index("-m k8s_nvidia_gpus_amd.models.llm.server") + 41:]
+    line = re.sub(r"\$\{(\w+)\}", lambda m: env[m.group(1)], line.splitlines()[0])
+    argv = shlex.split(line)
+    seen = {}
+
+    def fake_run(app, **kw):
+        seen["ok"] = True
+
+    import types
+    import sys
+
+    fake_uvicorn = types.SimpleNamespace(run=fake_run)
+    real = sys.modules.get("uvicorn")
+    sys.modules["uvicorn"] = fake_uvicorn
+    orig_thread = S.threading.Thread
+    S.threading.Thread = lambda *a, **k: types.SimpleNamespace(start=lambda: None)
+    try:
+        S.main(argv)
+    finally:
+        S.threading.Thread = orig_thread
+        if real is not None:
+            sys.modules["uvicorn"] = real
+        else:
+            del sys.modules["uvicorn"]
+    assert seen.get("ok")
+    assert "startupProbe" in c and c["startupProbe"]["failureThreshold"] * \
+        c["startupProbe"]["periodSeconds"] >= 300
+
+
 def test_llama_cpp_rocm_component_swaps_only_the_engine():
     """VERDICT r2 missing #6: upstream llama.cpp (ROCm) as a switchable engine for coder-llm — the
     component keeps the GPU contract (runtimeClass amd, amd.com/gpu, no visibility env), the
@@ -329,11 +372,13 @@ def test_llama_cpp_rocm_component_swaps_only_the_engine():
     script = c1["args"][0]
     assert "exec /app/llama-server" in script
     for flag in ("-m \"/models/${MODEL_FILE}\"", "--port 8080", "--ctx-size", "--n-gpu-layers",
-                 "--threads", "--parallel"):
+                 "--threads", "--parallel", "--ubatch-size"):
         assert flag in script, flag
-    for env in ("MODEL_FILE", "CTX_SIZE", "GPU_LAYERS", "CPU_THREADS", "PARALLEL_SLOTS"):
+    for env in ("MODEL_FILE", "CTX_SIZE", "GPU_LAYERS", "CPU_THREADS", "PARALLEL_SLOTS",
+                "UBATCH_SIZE"):
         assert any(e["name"] == env for e in c1["env"]) and "${%s}" % env in script
-    for key in ("ports", "readinessProbe", "livenessProbe", "resources", "volumeMounts", "env"):
+    for key in ("ports", "startupProbe", "readinessProbe", "livenessProbe", "resources",
+                "volumeMounts", "env"):
         assert c1[key] == c0[key], key
     assert out["spec"]["template"]["spec"]["runtimeClassName"] == "amd" and _gpu_request(c1)
     # the llm app documents the switch (commented: the in-tree engine stays the default)

@@ -13,6 +13,8 @@
 #   native           amd-vectoradd, amd-gemm-validator (bf16 + fp8), amd-proftester
 #   llm[:<tokens>]   tools/llm_bench.py (decode T list, default 1,2,3,4) + prefill
 #   llm-ctx:<n>      tools/llm_bench.py decode T = 1,4,8 after an n-token prompt (long-context decode)
+#   serve[:<args>]   tools/llm_serve_bench.py: the server under 1/4/8 streaming clients + a long-prompt
+#                    admission (args: comma-separated, '=' for spaces, e.g. serve:--clients=8,--gen=256)
 #   gemv[:<cases>]   tools/llm_bench.py --gemv: cold-weight GEMV decomposition sweep, T = 1 and 4
 #   prof-bench       rocprofv3 --kernel-trace --stats of the driver's bench command
 #   prof-llm[:<T>[:<prompt>]]   rocprofv3 kernel trace of steady LLM decode at T tokens → per-kernel summary
@@ -93,6 +95,14 @@ for step in "$@"; do
       timeout -k 10 500 python -u tools/llm_bench.py --tokens 1,4,8 --prompt "$np" --out "$OUT/llm_ctx_$np.json" \
         > "$OUT/llm_ctx_$np.log" 2>&1 || fail "$step" $? "$OUT/llm_ctx_$np.log"
       grep -E "decode|prefill" "$OUT/llm_ctx_$np.log" | grep -v '^{' ;;
+    serve|serve:*)
+      extra=""; [[ "$step" == serve:* ]] && extra="${step#serve:}"; extra="${extra//,/ }"
+      extra="${extra//=/ }"
+      n=$(ls "$OUT"/serve_*.json 2>/dev/null | wc -l)
+      # shellcheck disable=SC2086
+      timeout -k 10 900 python -u tools/llm_serve_bench.py $extra --server-log "$OUT/serve_server_$n.log" \
+        --out "$OUT/serve_$n.json" > "$OUT/serve_$n.log" 2>&1 || fail "$step" $? "$OUT/serve_$n.log"
+      grep -E "^(concurrency|admit|server ready)" "$OUT/serve_$n.log" | cut -c1-400 ;;
     prof-llm|prof-llm:*)
       t=1; np=512; [[ "$step" == prof-llm:* ]] && t="${step#prof-llm:}"
       [[ "$t" == *:* ]] && { np="${t#*:}"; t="${t%%:*}"; }

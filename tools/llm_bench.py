@@ -167,7 +167,9 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--layers", type=int, default=QWEN25_7B.layers)
     ap.add_argument("--steps", type=int, default=128, help="decode steps per T")
-    ap.add_argument("--ctx", type=int, default=4096, help="KV-cache context (reference --ctx-size)")
+    ap.add_argument("--ctx", type=int, default=0,
+                    help="KV-cache context (reference --ctx-size); 0 = max(4096, room for the "
+                         "prompt and every timed step)")
     ap.add_argument("--prompt", type=int, default=512)
     ap.add_argument("--tokens", default="1,2,3,4,8", help="decode T list ('' = no decode timing)")
     ap.add_argument("--gemv", action="store_true")
@@ -195,7 +197,8 @@ def main(argv=None) -> int:
     t0 = time.perf_counter()
     w = ModelWeights.random(cfg, device=dev, seed=0)
     torch.cuda.synchronize()
-    eng = Engine(w, max_ctx=args.ctx, slots=8, dense=True)
+    ctx = args.ctx or max(4096, args.prompt + args.steps + 64)
+    eng = Engine(w, max_ctx=ctx, slots=8, dense=True)
     if args.norm_prologue_t:
         eng.norm_prologue_t = args.norm_prologue_t
     eng.dense_weights()
