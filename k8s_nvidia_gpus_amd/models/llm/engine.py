@@ -220,6 +220,15 @@ class Engine:
             kj = torch.arange(end, device=self.device)[None, :]
             mask = kj <= qi
         mm, mm_res = self._dense_ops()
+        # a chunk after cached positions (chunked prefill, prompt-cache continuation): causal
+        # aligned bottom-right, which SDPA runs in its flash kernel; an explicit [P, end] mask
+        # takes the materialising path, 4-5x slower per layer at 2-32k positions
+        # (tools/debug/prefill_attn_probe.py, profiles/r05/prefill_attn_probe.log)
+        lowright = None
+        if P > 1 and start > 0 and self.prefill_gqa:
+            from torch.nn.attention.bias import causal_lower_right
+
+            lowright = causal_lower_right(P, end)
         xn = torch.empty(P, c.dim, dtype=dt, device=self.device)
         if self.prefill_qtok:          # [H][P][128] view of token-major storage: SDPA's output
             qh = torch.empty(P, c.heads, c.head_dim, dtype=dt,      # comes back token-major and
@@ -236,7 +245,7 @@ class Engine:
                 o = F.scaled_dot_product_attention(
                     qh[None], self.k_cache[i, slot, :, :end][None],
                     self.v_cache[i, slot, :, :end][None],
-                    attn_mask=None if (mask is None or start == 0) else mask[None, None],
+                    attn_mask=None if (mask is None or start == 0) else lowright,
                     is_causal=mask is not None and start == 0, enable_gqa=True)
             else:
                 kk = self.k_cache[i, slot, :, :end].repeat_interleave(c.group, 0)
@@ -480,6 +489,19 @@ class Engine:
             logits = self._decode_native(chunk, list(range(start + i, start + i + n)), [slot] * n)
             logits = logits[n - 1]
         return logits.clone()
+
+    def warmup(self, lengths: Sequence[int] = (1, 64, 512, 2048), slot: int = 0) -> None:
+        """Run the prompt path once per length, from position 0 and as a continuation chunk, so
+        the first request of each kind does not pay first-use costs (kernel images SDPA loads on
+        first use of a shape class, allocator growth: ~250 ms on the first 512-token prompt,
+        profiles/r05/serve).  Writes slot ``slot``'s KV, which the server then treats as empty."""
+        for n in lengths:
+            if 2 * n + 1 >= self.max_ctx:
+                continue
+            self.prefill([1] * n, slot, start=0)
+            self.prefill([1] * n, slot, start=n)
+        if self.gpu:
+            torch.cuda.synchronize(self.device)
 
     def capture(self, sizes: Sequence[int] = (1, 2, 3, 4)) -> None:
         """Capture every decode graph (batch sizes x attention-span buckets, sampled and greedy

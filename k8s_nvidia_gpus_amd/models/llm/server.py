@@ -42,7 +42,8 @@ from __future__ import annotations
 
 import argparse
 import asyncio
-import itertools
+import collections
+import gc
 import json
 import os
 import queue
@@ -142,6 +143,12 @@ class Scheduler:
                         "prefill_seconds_total": 0.0, "prefill_chunks_total": 0,
                         "requests_processing": 0, "prompt_tokens_cached_total": 0}
         self._touched: List[Job] = []
+        # per-iteration timings (GET /debug/iterations): start, admit / prefill / step / wake
+        # seconds, prompt tokens processed, sequences decoded; and the interpreter's GC pauses
+        self.trace: "collections.deque" = collections.deque(maxlen=8192)
+        self.gc_pauses: "collections.deque" = collections.deque(maxlen=1024)
+        self._gc_t0 = 0.0
+        gc.callbacks.append(self._gc_cb)
         self._run = True
         self._lock = threading.Lock()
         self.thread = threading.Thread(target=self._loop, name="llm-scheduler", daemon=True)
@@ -160,7 +167,18 @@ class Scheduler:
         self.pending.put(job)
         return job
 
+    def _gc_cb(self, phase, info) -> None:
+        if phase == "start":
+            self._gc_t0 = time.perf_counter()
+        else:
+            self.gc_pauses.append((self._gc_t0, time.perf_counter() - self._gc_t0,
+                                   info.get("generation", -1)))
+
     def close(self) -> None:
+        try:
+            gc.callbacks.remove(self._gc_cb)
+        except ValueError:
+            pass
         self._run = False
         self.pending.put(None)  # type: ignore[arg-type]
         self.thread.join(timeout=10)
@@ -299,13 +317,14 @@ class Scheduler:
             self.active[slot] = job
             self.prefilling.append(job)
 
-    def _prefill_chunk(self) -> None:
-        """One chunk of the oldest admitted prompt; its last chunk samples the first token."""
+    def _prefill_chunk(self) -> int:
+        """One chunk of the oldest admitted prompt; its last chunk samples the first token.
+        Returns the number of prompt tokens processed."""
         for j in [j for j in self.prefilling if j.cancelled]:
             self.prefilling.remove(j)
             self._release(j)
         if not self.prefilling:
-            return
+            return 0
         job = self.prefilling[0]
         limit = self.ubatch if any(j.decoding for j in self.active.values()) else self.batch
         n = min(limit, len(job.ids) - job.pos)
@@ -317,7 +336,7 @@ class Scheduler:
         except Exception as e:  # noqa: BLE001 - this job fails; the others keep decoding
             self.prefilling.pop(0)
             self._fail(job, e)
-            return
+            return 0
         dt = time.perf_counter() - t0
         job.pos += n
         job.t_prefill += dt
@@ -326,7 +345,7 @@ class Scheduler:
             self.metrics["prefill_seconds_total"] += dt
             self.metrics["prefill_chunks_total"] += 1
         if not done:
-            return
+            return n
         self.prefilling.pop(0)
         job.t_first = time.perf_counter()
         job.decoding = True
@@ -335,13 +354,15 @@ class Scheduler:
             self.metrics["tokens_predicted_total"] += 1
         if self._emit(job, int(tok)):
             self._release(job)
+        return n
 
-    def _step(self) -> None:
+    def _step(self) -> int:
+        """One decode step of every sequence past its prompt; returns how many."""
         for j in [j for j in self.active.values() if j.decoding and j.cancelled]:
             self._release(j)
         jobs = [j for j in self.active.values() if j.decoding]
         if not jobs:
-            return
+            return 0
         t0 = time.perf_counter()
         args = ([j.last for j in jobs], [j.pos for j in jobs], [j.slot for j in jobs])
         if all(j.params.plain_greedy for j in jobs) and hasattr(self.engine, "decode_greedy"):
@@ -365,16 +386,26 @@ class Scheduler:
                 self._fail(j, t)
             elif self._emit(j, int(t)):
                 self._release(j)
+        return len(jobs)
 
     def _loop(self) -> None:
+        clock = time.perf_counter
         while self._run:
             try:
+                t0 = clock()
                 self._admit()
                 self.metrics["requests_processing"] = len(self.active)
-                self._prefill_chunk()
+                t1 = clock()
+                n_prompt = self._prefill_chunk()
+                t2 = clock()
                 self._wake()                 # a finished prompt's first token goes out now
-                self._step()
+                t3 = clock()
+                n_dec = self._step()
+                t4 = clock()
                 self._wake()
+                if n_prompt or n_dec:
+                    self.trace.append((t0, t1 - t0, t2 - t1, t4 - t3, clock() - t4 + t3 - t2,
+                                       n_prompt, n_dec))
             except Exception as e:  # surface to every waiting request, keep serving
                 for j in list(self.active.values()):
                     self._put(j, ("error", repr(e)))
@@ -667,6 +698,17 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
         return [{"id": i, "n_ctx": s.engine.max_ctx, "is_processing": i in s.active,
                  "n_cached": len(s.slot_tokens.get(i, []))} for i in range(s.parallel)]
 
+    @app.get("/debug/iterations")
+    def iterations(n: int = 2048):
+        """The scheduler's last ``n`` loop iterations (perf_counter seconds, which is
+        CLOCK_MONOTONIC: comparable across processes) and GC pauses — what a stalled stream
+        waited on."""
+        s = sched()
+        keys = ("t", "admit_s", "prefill_s", "step_s", "wake_s", "prompt_tokens", "decoded")
+        its = [dict(zip(keys, x)) for x in list(s.trace)[-max(1, n):]]
+        gcs = [{"t": t, "s": d, "generation": g} for t, d, g in list(s.gc_pauses)]
+        return {"iterations": its, "gc_pauses": gcs}
+
     @app.get("/metrics")
     def metrics():
         s = state.get("scheduler")
@@ -741,6 +783,7 @@ def main(argv=None) -> int:
         eng, tok, name = build_engine(args)
         if eng.gpu:
             eng.capture(range(1, min(args.parallel, eng.max_T) + 1))   # HIP graphs before ready
+            eng.warmup()                                                # prompt path, first use
         state.update(tok=tok, model=name, scheduler=Scheduler(eng, tok, args.parallel,
                                                             ubatch=args.ubatch_size,
                                                             batch=args.batch_size))

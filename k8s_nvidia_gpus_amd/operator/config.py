@@ -56,8 +56,10 @@ DEFAULTS: Dict[str, Any] = {
         "gemmMinTflops": 900,
         "gemmFp8": True,             # also run the fp8 (OCP e4m3) MFMA GEMM
         "gemmFp8MinTflops": 1800,
-        "rocprof": False,            # run the GEMM step under rocprofv3 --kernel-trace --stats
-        "rocprofCounters": False,    # + one rocprofv3 --pmc pass: MFMA util, clock, L2 hit rate
+        # profile step (after the gate): the GEMMs under rocprofv3 --kernel-trace --stats, and one
+        # rocprofv3 --pmc pass (MFMA util, clock, L2 hit rate)
+        "rocprof": False,
+        "rocprofCounters": False,
         "bandwidth": True,           # amd-proftester: HBM copy, PCIe H2D/D2H, xGMI peer copies
         "hbmMinGBps": 4000,          # HBM3E copy (read + write bytes), per GPU
         "pcieMinGBps": 20,           # pinned host <-> device, each direction, per GPU
@@ -75,9 +77,19 @@ DEFAULTS: Dict[str, Any] = {
         # an absent socket fails the load steps (a node cannot prove a GPU is free); false only for
         # runs outside Kubernetes (bring-up rehearsal on a bare box), where every agent is free
         "podResourcesRequired": True,
-        # device plugin advertises a GPU Healthy only once every enabled load step has passed on it
-        # this boot (validated-devices.json), so pods cannot take GPUs before the first validation
+        # device plugin advertises a GPU Healthy only once the gate steps have passed on it this
+        # boot (validated-devices.json), so pods cannot take GPUs before the first validation
         "gateOnValidation": True,
+        # the per-device steps that open the gate (vectorAdd runs before them in the chain); the
+        # node-wide steps (bandwidth pairs, stress, rccl) only decide the node label and run after
+        # the gate opened — list them here too for the strict all-steps gate
+        "gateSteps": ["gemm"],
+        # node-wide steps start this long after the gate first opened this boot, so pods already
+        # pending for the node get their GPUs before the steps reserve the free ones
+        "gateGraceSeconds": 5,
+        # the device plugin's registration socket: a load step whose reservation is not acked while
+        # this socket accepts connections is deferred (never loads GPUs a live plugin may hand out)
+        "pluginSocket": "/var/lib/kubelet/device-plugins/amd-gpu.sock",
         # load steps reserve their GPUs (in-test.json → the plugin reports them Unhealthy) and wait
         # this long for the plugin's ack before re-reading PodResources
         "reserveAckSeconds": 15,
@@ -152,6 +164,11 @@ class OperatorConfig:
             raise ConfigError("exporter.port out of range")
         if float(r["validator"]["reserveAckSeconds"]) < 0 or float(r["validator"]["retryDeferredSeconds"]) <= 0:
             raise ConfigError("validator.reserveAckSeconds must be >= 0, retryDeferredSeconds > 0")
+        gs = r["validator"]["gateSteps"]
+        if not isinstance(gs, list) or any(x not in ("gemm", "bandwidth", "stress", "rccl") for x in gs):
+            raise ConfigError("validator.gateSteps must list load steps (gemm, bandwidth, stress, rccl)")
+        if float(r["validator"]["gateGraceSeconds"]) < 0:
+            raise ConfigError("validator.gateGraceSeconds must be >= 0")
         if int(r["validator"]["gemmSize"]) % 256:
             raise ConfigError("validator.gemmSize must be a multiple of 256 (MFMA block tile)")
         return self

@@ -383,6 +383,7 @@ class GpuCollector:
                 for r in (v.get("fp8") or {}).get("devices", []):
                     if r.get("tflops") is not None:
                         tflops8.add_metric([self.node, str(r.get("device"))], float(r["tflops"]))
+            if step in ("gemm", "profile") and isinstance(v, dict):
                 rc = v.get("rocprof_counters") or {}
                 for q in ("mfma_util_pct", "clock_ghz", "l2_hit_pct"):
                     if rc.get(q) is not None:

@@ -31,6 +31,23 @@ annotation ``amd.com/gpu.partition-state`` so it survives agent restarts and is 
 Convergence is per ASIC: every ASIC's current mode is read (a node whose change stopped half-way —
 ``set_compute`` raising on ASIC 3 after ASICs 0-2 switched — reads as ``mixed``, never as the head
 GPU's mode), and a reconcile re-applies the desired mode only to the ASICs that are off target.
+
+How the driver applies the two modes (and what the manager does about it):
+
+* **Memory partition (NPS) is hive-wide and needs a driver reload.**  It is applied ONCE per node,
+  before any compute change.  amd-smi's set call performs the reload itself (every KFD agent is
+  withdrawn and re-created, every processor handle becomes invalid); the manager then waits for
+  every ASIC to re-appear in the new mode.  A sysfs write only *requests* the mode for the next
+  reload: with ``partition.driverReloadCommand`` set the manager runs it (the GPUs are already
+  drained and quiesced), otherwise the change stops in state ``pending-reload`` (taint and pause
+  lifted, the GPUs keep serving in the old mode) instead of waiting out a re-enumeration that
+  cannot happen; later reconciles report the same state without draining again.
+* **Compute partition is per ASIC and re-enumerates that ASIC's agents** (SPX → CPX turns one
+  agent into eight, new render nodes and device IDs).  Handles are looked up fresh for every
+  write after a change (the amd-smi backend re-initialises its session), never reused.
+
+Between draining and the first write the manager checks again that no validator load step holds
+a reservation (``in-test.json``): one that started in that window is waited for.
 """
 from __future__ import annotations
 
@@ -84,7 +101,12 @@ def node_mode(modes: Dict[int, Tuple[str, str]]) -> Tuple[str, str]:
 
 
 class SysfsPartitionBackend:
-    """Writes ``current_{compute,memory}_partition`` of each ASIC's PCI device (needs root)."""
+    """Writes ``current_{compute,memory}_partition`` of each ASIC's PCI device (needs root).
+
+    A compute write re-partitions that ASIC at once; a memory write only requests the NPS mode,
+    which the driver applies at its next reload (``memory_reloads_driver`` False)."""
+
+    memory_reloads_driver = False
 
     def __init__(self, root: str = "/"):
         self.root = root
@@ -111,7 +133,8 @@ class PartitionManager:
                  apply_retries: int = 5, retry_backoff: float = 1.0,
                  ack_dir: str = pause_mod.ACK_DIR,
                  ack_components: Sequence[str] = pause_mod.COMPONENTS,
-                 reservation: Optional[str] = "/run/amd/validations/in-test.json"):
+                 reservation: Optional[str] = "/run/amd/validations/in-test.json",
+                 reload_cmd: Sequence[str] = (), run_cmd: Optional[Callable] = None):
         if drain_policy not in DRAIN_POLICIES:
             raise ValueError(f"drainPolicy must be one of {DRAIN_POLICIES}")
         self.client = client
@@ -134,6 +157,11 @@ class PartitionManager:
         self.ack_dir = ack_dir
         self.ack_components = tuple(ack_components)
         self.reservation = reservation
+        # argv that reloads amdgpu (e.g. a host script: modprobe -r amdgpu && modprobe amdgpu) for
+        # a sysfs-requested NPS change; empty: report pending-reload instead
+        self.reload_cmd = list(reload_cmd)
+        self.run_cmd = run_cmd or (lambda argv: __import__("subprocess").run(
+            list(argv), capture_output=True, text=True, timeout=600).returncode)
 
     # ---------------------------------------------------------------- helpers
     def _state(self, state: str, reason: str = "") -> None:
@@ -182,6 +210,12 @@ class PartitionManager:
             self.client.set_taint(self.node, TAINT_KEY, "", present=False)
             self._state("idle")
             return "idle"
+        mem_off = any(m != want_m for _, m in modes.values())
+        reloads = getattr(self.backend, "memory_reloads_driver", False)
+        if mem_off and not reloads and not self.reload_cmd:
+            annot = (self.client.get_node(self.node).get("metadata", {}).get("annotations") or {})
+            if str(annot.get(ANNOT_STATE, "")).startswith(f"pending-reload: {want_m}"):
+                return "pending-reload"      # requested before; only a driver reload applies it
         avail = topo_mod.available_partitions(self.root, asics[off[0]][0])
         if want_c not in avail:
             self._state("failed", f"{want_c} not in available {','.join(avail)}")
@@ -193,7 +227,8 @@ class PartitionManager:
         self.client.set_taint(self.node, TAINT_KEY, want_c, present=True)
         nonce = self._pause(True)
         self._state("draining", f"{cur_c}->{want_c} (drainPolicy {self.drain_policy})")
-        err = self.drain(time.monotonic() + self.drain_timeout)
+        deadline = time.monotonic() + self.drain_timeout
+        err = self.drain(deadline)
         if err:
             self._abort(err)
             return "failed"
@@ -203,45 +238,103 @@ class PartitionManager:
         if missing:
             log.warning("no pause ack from %s after %.0f s; applying anyway (EBUSY is retried)",
                         ",".join(missing), self.pause_ack_timeout)
-        # 3. apply to the off-target ASICs only, memory partition first (the compute split must
-        #    fit the memory layout)
-        self._state("applying", f"{want_c}/{want_m} on {len(off)} ASIC(s)")
-        done: List[str] = []
-        for uid in off:
-            head = asics[uid][0]
-            c_i, m_i = modes[uid]
+        err = self._wait_validator_idle(deadline)
+        if err:
+            self._abort(err)
+            return "failed"
+        # 3. memory partition: hive-wide, once per node, before any compute change
+        if mem_off:
+            head = asics[off[0]][0]
+            self._state("applying", f"memory partition {want_m} (hive-wide, driver reload)")
             try:
-                if m_i != want_m:
-                    self._apply(self.backend.set_memory, head, want_m)
-                if c_i != want_c:
-                    self._apply(self.backend.set_compute, head, want_c)
+                self._apply(self.backend.set_memory, head, want_m)
             except Exception as e:  # noqa: BLE001
-                self._abort(f"apply failed on {head.pci_bdf} after {len(done)} of {len(off)} "
+                self._abort(f"memory partition {want_m} failed on {head.pci_bdf}: {e}")
+                return "failed"
+            if not reloads:
+                if not self.reload_cmd:
+                    self._pause(False)
+                    self.client.set_taint(self.node, TAINT_KEY, "", present=False)
+                    self._state("pending-reload",
+                                f"{want_m} requested through sysfs; the amdgpu driver applies it "
+                                f"at its next reload (set partition.driverReloadCommand, or "
+                                f"reboot); compute {want_c} follows after that")
+                    return "pending-reload"
+                self._state("applying", f"reloading amdgpu for {want_m}: {' '.join(self.reload_cmd)}")
+                rc = self.run_cmd(self.reload_cmd)
+                if rc != 0:
+                    self._abort(f"driver reload command failed (rc={rc})")
+                    return "failed"
+            self._state("reenumerating", f"memory partition {want_m}")
+            got = self._wait_modes(lambda ms: all(m == want_m for _, m in ms.values()),
+                                   len(asics), f"every ASIC in {want_m}")
+            if isinstance(got, str):
+                self._abort(got)
+                return "failed"
+            topo = got
+            modes = asic_modes(topo)
+            asics = topo.asics()
+        # 4. compute partition per ASIC, each handle looked up fresh (the backend re-opens its
+        #    amd-smi session after every change)
+        c_off = sorted((uid for uid, (c, _) in modes.items() if c != want_c),
+                       key=lambda u: asics[u][0].pci_bdf)
+        self._state("applying", f"{want_c} on {len(c_off)} ASIC(s)")
+        done: List[str] = []
+        for uid in c_off:
+            head = asics[uid][0]
+            err = self._wait_validator_idle(deadline)
+            if err:
+                self._abort(err)
+                return "failed"
+            try:
+                self._apply(self.backend.set_compute, head, want_c)
+            except Exception as e:  # noqa: BLE001
+                self._abort(f"apply failed on {head.pci_bdf} after {len(done)} of {len(c_off)} "
                             f"ASIC(s) switched: {e}")
                 return "failed"
             done.append(head.pci_bdf)
-        # 4. wait for the driver to re-enumerate every ASIC in the new mode
+        # 5. wait for the driver to re-enumerate every ASIC in the new mode
         self._state("reenumerating")
-        expect = len(asics) * topo_mod.PARTITION_SPLIT[want_c]
-        deadline = time.monotonic() + self.reenum_timeout
-        while True:
-            try:
-                c, m, t2 = self.current()
-                if (c, m) == (want_c, want_m) and len(t2.gpus) == expect:
-                    break
-            except (PartitionError, FileNotFoundError):
-                pass
-            if time.monotonic() >= deadline:
-                self._abort(f"re-enumeration timeout (expected {expect} agents)")
-                return "failed"
-            self.sleep(self.poll)
-        # 5. resume (the paused clients re-open re-enumerated handles)
+        got = self._wait_modes(lambda ms: all(cm == (want_c, want_m) for cm in ms.values()),
+                               len(asics) * topo_mod.PARTITION_SPLIT[want_c],
+                               f"{want_c}/{want_m}")
+        if isinstance(got, str):
+            self._abort(got)
+            return "failed"
+        # 6. resume (the paused clients re-open re-enumerated handles)
         self._pause(False)
         self.client.set_taint(self.node, TAINT_KEY, "", present=False)
         self.client.set_node_labels(self.node, {"amd.com/gpu.compute-partition": want_c,
                                                 "amd.com/gpu.memory-partition": want_m})
-        self._state("idle", f"applied {want_c}/{want_m} on {len(off)} ASIC(s)")
+        # the new agents have new device IDs: with the validator's gate on they are allocatable
+        # once the validator (its hold loop sees the topology change) has re-run the GEMM on them
+        self._state("idle", f"applied {want_c}/{want_m} ({len(done)} compute, "
+                            f"{1 if mem_off else 0} memory change); new agents are allocatable "
+                            f"after the validator's GEMM pass on them")
         return "applied"
+
+    def _wait_modes(self, ok, agents: int, what: str):
+        """Poll the KFD topology until ``ok(asic modes)`` holds with ``agents`` agents; returns
+        the topology, or the failure reason past ``reenum_timeout``."""
+        deadline = time.monotonic() + self.reenum_timeout
+        while True:
+            try:
+                t = topo_mod.read_topology(self.root, self.min_gfx)
+                if t.gpus and ok(asic_modes(t)) and len(t.gpus) == agents:
+                    return t
+            except (PartitionError, FileNotFoundError):
+                pass
+            if time.monotonic() >= deadline:
+                return f"re-enumeration timeout (expected {agents} agents, {what})"
+            self.sleep(self.poll)
+
+    def _wait_validator_idle(self, deadline: float) -> Optional[str]:
+        """A validator load step that reserved GPUs after the drain finished is waited for."""
+        while self._validator_busy():
+            if time.monotonic() >= deadline:
+                return "drain timeout: a validator load step is still running"
+            self.sleep(self.poll)
+        return None
 
     def _validator_busy(self) -> bool:
         """A validator load step holds a live reservation (it is loading the GPUs right now)."""

@@ -17,10 +17,12 @@ the previous one's marker under ``/run/amd/validations``:
             for stressSeconds while amd-smi telemetry is sampled: no uncorrectable ECC error, no
             100 ms window below stressMinFraction of the mean rate, hotspot ≤ stressMaxHotspotC
   rccl      RCCL all-reduce over xGMI across all GPUs of the node: exact sums + bus bandwidth floor
+  profile   (optional, BASELINE config 3) the validator GEMMs again under rocprofv3: kernel trace +
+            stats, and one --pmc pass (MFMA utilisation, clock, L2 hit rate, FLOP check)
   plugin    a pod requesting amd.com/gpu: 1 is scheduled THROUGH the device plugin and passes
   report    node label amd.com/gpu.validated=true|partial|deferred|false, validator-ready marker
 
-The load steps (gemm, bandwidth, stress, rccl) never touch a GPU that kubelet has allocated to a
+The load steps (gemm, bandwidth, stress, rccl, profile) never touch a GPU that kubelet has allocated to a
 pod: the kubelet PodResources API (``podresources_api.py``) lists the device IDs pods hold, and the
 native tools run with ``ROCR_VISIBLE_DEVICES`` narrowed to the free agents.  Closing the window
 between that answer and the launch: the step first *reserves* its agents (``in-test.json``; the
@@ -32,7 +34,13 @@ absent or List failing) or an allocated ID that cannot be mapped *fails* the ste
 validated" is never reported as validated.  Every agent a load step passed on is recorded per
 fingerprint (``device-passes.json``); the agents on which every enabled load step passed this
 boot are published in ``validated-devices.json``, which the device plugin gates on
-(``gateOnValidation``).
+(``gateOnValidation``).  The gate is per device: it opens on the ``gateSteps`` (default: the GEMM,
+after vectorAdd earlier in the chain), so a GPU becomes allocatable seconds after the driver is up.
+The node-wide steps after it (bandwidth pairs, stress, RCCL, profiling) decide only the node label;
+they start ``gateGraceSeconds`` after the gate first opened, so pods already pending for the node get
+their GPUs first, and then reserve whatever is still free.  A reservation that a live device plugin
+(its registration socket accepts connections) does not ack defers the step: GPUs a serving plugin
+may still hand out are never loaded.
 
 A validator restart whose node fingerprint (boot id, amdgpu version, operator image, validator
 config, partition modes, agent set) equals the one of the last full pass re-uses that pass instead
@@ -62,8 +70,9 @@ from .config import OperatorConfig
 
 log = logging.getLogger("amd-gpu-validator")
 
-STEPS = ("driver", "runtime", "vectoradd", "gemm", "bandwidth", "stress", "rccl", "plugin", "report")
-LOAD_STEPS = ("gemm", "bandwidth", "stress", "rccl")
+STEPS = ("driver", "runtime", "vectoradd", "gemm", "bandwidth", "stress", "rccl", "profile", "plugin",
+         "report")
+LOAD_STEPS = ("gemm", "bandwidth", "stress", "rccl", "profile")
 LABEL_VALIDATED = "amd.com/gpu.validated"
 FINGERPRINT = "fingerprint.json"
 IN_TEST = "in-test.json"                  # {nonce, step, device_uids, expires}: plugin → Unhealthy
@@ -73,7 +82,7 @@ VALIDATED_DEVICES = "validated-devices.json"  # {boot_id, device_uids}: the plug
 LABEL_TRUE, LABEL_PARTIAL, LABEL_DEFERRED, LABEL_FALSE = "true", "partial", "deferred", "false"
 # upper bound of a load step's run time, for the reservation's expiry (a crashed validator must not
 # leave GPUs reported Unhealthy forever)
-STEP_TIMEOUT = {"gemm": 2400.0, "bandwidth": 900.0, "rccl": 900.0}
+STEP_TIMEOUT = {"gemm": 2400.0, "bandwidth": 900.0, "rccl": 900.0, "profile": 1200.0}
 # kubelet device ID -> device_uid, written by the device plugin (needed for deviceIdStrategy: index)
 DEVICE_ID_MAP = "/run/amd/device-plugin/ids.json"
 
@@ -256,10 +265,12 @@ class Validator:
                  bin_dir: Optional[str] = None, runner: Runner = default_runner, root: str = "/",
                  kube=None, node_name: Optional[str] = None, driver_wait: float = 120,
                  telemetry: Optional[Callable[[], List[Dict]]] = None,
-                 device_id_map: str = DEVICE_ID_MAP, pause_marker: Optional[str] = None):
+                 device_id_map: str = DEVICE_ID_MAP, pause_marker: Optional[str] = None,
+                 sleep: Callable[[float], None] = time.sleep):
         from .pause import PAUSE_MARKER
 
         self.cfg = config
+        self.sleep = sleep
         self.device_id_map = device_id_map
         # no load step starts while the partition manager switches modes
         self.pause_marker = pause_marker if pause_marker is not None else (
@@ -414,8 +425,13 @@ class Validator:
             if acked or time.monotonic() >= deadline:
                 break
             time.sleep(0.05)
-        busy, err = self._allocated(sc.devices)
         info: Dict = {"nonce": nonce, "acked": acked}
+        if not acked and self._plugin_serving():
+            # a serving plugin that has not published the reservation may still hand these GPUs
+            # to pods: load nothing (the caller defers the step)
+            info["unacked_live_plugin"] = True
+            return GpuScope(sc.devices, [], sc.allocated, sc.note, sc.split, from_kubelet=True), info
+        busy, err = self._allocated(sc.devices)
         if err:
             return GpuScope(sc.devices, [], busy or {}, "", sc.split, error=err), info
         busy = busy or {}
@@ -431,6 +447,27 @@ class Validator:
                                        "expires": time.time() + timeout})
         return narrowed, info
 
+    def _plugin_serving(self) -> bool:
+        """The device plugin's registration socket accepts a connection (a plugin is serving)."""
+        import socket
+
+        path = str(self.vcfg.get("pluginSocket") or "")
+        if not path:
+            return False
+        if not os.path.exists(path) and self.root != "/":
+            path = os.path.join(self.root, path.lstrip("/"))
+        if not os.path.exists(path):
+            return False
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.settimeout(0.5)
+        try:
+            s.connect(path)
+            return True
+        except OSError:
+            return False
+        finally:
+            s.close()
+
     def release(self) -> None:
         for name in (IN_TEST,):
             try:
@@ -440,7 +477,25 @@ class Validator:
 
     # ---------------------------------------------------------------- per-device passes (gate)
     def _gating_steps(self) -> List[str]:
-        return [s for s in LOAD_STEPS if self._enabled(s)] or ["driver"]
+        """The per-device steps whose passes open the plugin's gate (``gateSteps``, enabled ones);
+        the driver check alone when none is enabled."""
+        gs = list(self.vcfg.get("gateSteps") or ["gemm"])
+        return [s for s in LOAD_STEPS if s in gs and self._enabled(s)] or ["driver"]
+
+    def _wait_gate_grace(self, step: str) -> float:
+        """Node-wide steps start ``gateGraceSeconds`` after the gate first opened this boot, so a
+        pod pending for the node is allocated before they reserve the free GPUs.  Returns the
+        seconds waited."""
+        if not self.vcfg.get("gateOnValidation") or step in self._gating_steps():
+            return 0.0
+        doc = self._read_json(VALIDATED_DEVICES) or {}
+        if doc.get("boot_id") != self.fingerprint().get("boot_id") or not doc.get("opened"):
+            return 0.0
+        wait = float(doc["opened"]) + float(self.vcfg.get("gateGraceSeconds", 0)) - time.time()
+        if wait > 0:
+            self.sleep(wait)
+            return round(wait, 3)
+        return 0.0
 
     def record_pass(self, step: str, uids: Sequence[str]) -> List[str]:
         """Add ``uids`` to ``step``'s passes for the current fingerprint; republish the agents on
@@ -453,8 +508,13 @@ class Validator:
         self._write_json(DEVICE_PASSES, doc)
         sets = [set(doc["steps"].get(s, [])) for s in self._gating_steps()]
         validated = sorted(set.intersection(*sets)) if sets else []
+        prev = self._read_json(VALIDATED_DEVICES) or {}
+        opened = prev.get("opened") if (prev.get("boot_id") == fp.get("boot_id", "")
+                                        and prev.get("device_uids")) else None
+        if validated and opened is None:
+            opened = time.time()             # the gate opens now (first GPU allocatable)
         self._write_json(VALIDATED_DEVICES, {"boot_id": fp.get("boot_id", ""), "device_uids": validated,
-                                             "time": time.time()})
+                                             "time": time.time(), "opened": opened})
         return validated
 
     def validated_devices(self) -> List[str]:
@@ -597,18 +657,19 @@ class Validator:
             summary["flop_matches_shape"] = summary["mfma_flop"] == 2.0 * size ** 3
         return summary
 
-    def step_gemm(self) -> StepResult:
+    def _gemm_size(self) -> Tuple[int, int]:
         split = self._scope.split if self._scope else 1
         # a compute partition owns 1/split of the ASIC's CUs: per-partition floor and a GEMM sized
         # for 32 CUs (CPX) rather than the whole chip
-        size = int(self.vcfg["gemmSize"] if split == 1 else self.vcfg["gemmSizePartitioned"])
-        rocprof = bool(self.vcfg.get("rocprof"))
+        return int(self.vcfg["gemmSize"] if split == 1 else self.vcfg["gemmSizePartitioned"]), split
+
+    def step_gemm(self, rocprof: bool = False) -> StepResult:
+        """bf16 (+ fp8) GEMMs: numerics vs fp32 and the TFLOPS floor on every free GPU.  A gate
+        step, so it runs plain; the profiled runs are the ``profile`` step's."""
+        size, split = self._gemm_size()
         ok, detail, reason = self._gemm_run("bf16", size, float(self.vcfg["gemmMinTflops"]) / split,
                                             rocprof)
         detail["partition_split"] = split
-        if self.vcfg.get("rocprofCounters") and ok:
-            cus = min((int(d.get("cus", 256)) for d in detail["devices"]), default=256)
-            detail["rocprof_counters"] = self._gemm_counters(size, cus)
         if self.vcfg.get("gemmFp8"):
             ok8, detail8, reason8 = self._gemm_run("fp8", size,
                                                    float(self.vcfg["gemmFp8MinTflops"]) / split, rocprof)
@@ -616,6 +677,31 @@ class Validator:
             ok = ok and ok8
             reason = "; ".join(r for r in (reason, reason8) if r)
         return StepResult("gemm", bool(ok), detail, reason)
+
+    def step_profile(self) -> StepResult:
+        """BASELINE config 3, "the validator GEMM shown in rocprof": the GEMM runs again under
+        ``rocprofv3 --kernel-trace --stats`` (``rocprof``), then one separate ``--pmc`` pass
+        (``rocprofCounters``: MFMA utilisation, clock, L2 hit rate, the MFMA FLOPs the hardware
+        counted vs 2·n³).  After the gate: profiling is evidence, not admission."""
+        size, split = self._gemm_size()
+        detail: Dict = {"size": size, "partition_split": split}
+        ok, reason = True, ""
+        if self.vcfg.get("rocprof"):
+            r = self.step_gemm(rocprof=True)
+            ok, reason = r.passed, r.reason
+            detail["rocprof_kernels"] = r.detail.get("rocprof_kernels", [])
+            detail["devices"] = r.detail.get("devices", [])
+            if "fp8" in r.detail:
+                detail["fp8"] = {"rocprof_kernels": r.detail["fp8"].get("rocprof_kernels", []),
+                                 "devices": r.detail["fp8"].get("devices", [])}
+        if self.vcfg.get("rocprofCounters") and ok:
+            devs = detail.get("devices") or []
+            cus = min((int(d.get("cus", 256)) for d in devs), default=256 // split)
+            pmc = self._gemm_counters(size, cus)
+            detail["rocprof_counters"] = pmc
+            if pmc.get("error"):
+                ok, reason = False, pmc["error"]
+        return StepResult("profile", bool(ok), detail, reason)
 
     def step_bandwidth(self) -> StepResult:
         split = self._scope.split if self._scope else 1
@@ -825,6 +911,8 @@ class Validator:
             required.append("stress")
         if self.vcfg["rccl"]:
             required.append("rccl")
+        if self._enabled("profile"):
+            required.append("profile")
         if self.vcfg["pluginTest"]:
             required.append("plugin")
         return required
@@ -950,6 +1038,7 @@ class Validator:
             if prev is not None:
                 return StepResult(step, True, {"reused": "node fingerprint unchanged since the last "
                                                          "full validation", "previous": prev})
+            waited = self._wait_gate_grace(step)
             # a fresh kubelet answer per load step (steps run minutes apart)
             sc = self._scope = self.gpu_scope()
             if os.path.exists(self.pause_marker):
@@ -963,6 +1052,16 @@ class Validator:
                 if sc.known and sc.from_kubelet:
                     sc, reservation = self.reserve(step, sc)
                     self._scope = sc
+                    if waited:
+                        reservation["gate_grace_waited_s"] = waited
+                    if reservation.get("unacked_live_plugin"):
+                        return self._deferred(step, sc, "the device plugin is serving but did not "
+                                                        "ack the reservation: no GPU loaded",
+                                              reservation)
+                    if os.path.exists(self.pause_marker):
+                        # the partition manager started after the first check
+                        return self._deferred(step, sc, "partition change started while "
+                                                        "reserving", reservation)
                     if sc.error:
                         return StepResult(step, False, {"gpu_scope": sc.to_dict(),
                                                         "reservation": reservation}, sc.error)
@@ -994,6 +1093,8 @@ class Validator:
         return StepResult(step, False, detail, f"deferred: {why}", deferred=True)
 
     def _enabled(self, step: str) -> bool:
+        if step == "profile":
+            return bool(self.vcfg.get("rocprof") or self.vcfg.get("rocprofCounters"))
         return bool(self.vcfg[{"gemm": "gemm", "bandwidth": "bandwidth", "stress": "stress",
                                "rccl": "rccl"}[step]])
 
@@ -1003,7 +1104,13 @@ class Validator:
         elif step == "runtime":
             r = self.step_runtime()
         elif step == "vectoradd":
-            r = self.step_vectoradd() if self.vcfg["vectorAdd"] else StepResult("vectoradd", True, {"skipped": True})
+            if not self.vcfg["vectorAdd"]:
+                r = StepResult("vectoradd", True, {"skipped": True})
+            elif os.path.exists(self.pause_marker):       # no GPU work mid-switch
+                r = StepResult("vectoradd", False, {"deferred": "partition change in progress"},
+                               "deferred: partition change in progress", deferred=True)
+            else:
+                r = self.step_vectoradd()
         elif step == "gemm":
             r = self.step_gemm() if self.vcfg["gemm"] else StepResult("gemm", True, {"skipped": True})
         elif step == "bandwidth":
@@ -1021,6 +1128,8 @@ class Validator:
                 except (OSError, ValueError):
                     pass
                 r = self.step_rccl(gpus)
+        elif step == "profile":
+            r = self.step_profile() if self._enabled("profile") else StepResult("profile", True, {"skipped": True})
         elif step == "plugin":
             r = self.step_plugin() if self.vcfg["pluginTest"] else StepResult("plugin", True, {"skipped": True})
         elif step == "report":
@@ -1038,6 +1147,9 @@ def hold_loop(v: "Validator", marker_dir: str, interval: float = 30.0,
     * the GPU topology changed under it (a partition switch re-enumerated the agents), or
     * the node is ``deferred`` / ``partial`` and kubelet now shows a free GPU that has not been
       validated this boot (polled every ``retryDeferredSeconds``).
+    The topology is compared every iteration: after a partition switch the agents
+    have new UIDs, the gate is closed for all of them, and waiting out the retry period would
+    leave the node with zero allocatable GPUs for minutes.
     A container restart would not re-run init containers, so the chain is restarted by deleting
     this pod (the DaemonSet recreates it); without API access the container exits (code 3).
     Returns the exit code."""
@@ -1048,12 +1160,12 @@ def hold_loop(v: "Validator", marker_dir: str, interval: float = 30.0,
         if not os.path.exists(os.path.join(marker_dir, "driver-ready")):
             why = "driver-ready withdrawn"
             break
+        now = v._fingerprint()
+        if any(now.get(k) != v.fingerprint().get(k) for k in ("partition", "agents", "device_uids")):
+            why = "GPU topology changed (partition switch / GPU lost): re-validate"
+            break
         if time.monotonic() - last_check >= retry:
             last_check = time.monotonic()
-            now = v._fingerprint()
-            if any(now.get(k) != v.fingerprint().get(k) for k in ("partition", "agents", "device_uids")):
-                why = "GPU topology changed (partition switch / GPU lost): re-validate"
-                break
             label, _ = v.node_label()
             if label in (LABEL_DEFERRED, LABEL_PARTIAL):
                 pending = v.pending_devices()

@@ -365,7 +365,8 @@ def test_validator_gemm_step_under_rocprof(tmp_path):
         return 0, logs[dtype]
 
     cfg = load_config(text="validator: {rocprof: true, podResourcesRequired: false}\n")
-    r = Validator(cfg, str(tmp_path), bin_dir="/b", runner=runner).run_step("gemm")
+    # the profiled GEMMs are the profile step's (after the gate); the gate step runs them plain
+    r = Validator(cfg, str(tmp_path), bin_dir="/b", runner=runner).run_step("profile")
     assert r.passed and seen[0][:3] == ["rocprofv3", "--kernel-trace", "--stats"]
     assert r.detail["rocprof_kernels"][0]["name"] == "amdk8s_gemm_bf16_nt_256x256"
     assert r.detail["fp8"]["rocprof_kernels"][0]["name"] == "amdk8s_gemm_fp8_nt_256x256"

@@ -67,20 +67,21 @@ def test_validator_chain_with_native_binaries(tmp_path, native):
     cfg = load_config(text="expectedGpusPerNode: 1\nvalidator: {podResourcesRequired: false, gemmSize: 4096, gemmMinTflops: 600, "
                            "rccl: false, pluginTest: false, rocprofCounters: true}\n")
     v = Validator(cfg, str(tmp_path), bin_dir=str(native))
-    for step in ("driver", "vectoradd", "gemm", "bandwidth"):
+    for step in ("driver", "vectoradd", "gemm", "bandwidth", "profile"):
         r = v.run_step(step)
         assert r.passed, (step, r.reason)
     (tmp_path / "runtime-ready").write_text("1")  # no runtime installer on the box
     assert v.run_step("report").passed
     gemm = json.loads((tmp_path / "gemm.json").read_text())
     assert all(d["tflops"] > 600 for d in gemm["devices"])
-    pmc = gemm["rocprof_counters"]
+    pmc = json.loads((tmp_path / "profile.json").read_text())["rocprof_counters"]
     assert pmc.get("flop_matches_shape") is True, pmc  # MFMA FLOPs counted == 2·4096³
     assert 50 < pmc["mfma_util_pct"] <= 100 and 1.0 < pmc["clock_ghz"] < 2.5
     out = os.environ.get("AMDK8S_EVIDENCE_DIR")
     if out:
         os.makedirs(out, exist_ok=True)
-        for f in ("driver.json", "vectoradd.json", "gemm.json", "bandwidth.json", "report.json"):
+        for f in ("driver.json", "vectoradd.json", "gemm.json", "bandwidth.json", "profile.json",
+                  "report.json"):
             with open(tmp_path / f) as src, open(os.path.join(out, "validator_" + f), "w") as dst:
                 dst.write(src.read())
 

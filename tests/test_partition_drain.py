@@ -246,3 +246,147 @@ def test_drain_waits_for_a_running_validator_load_step(tmp_path, api, client):
     res.write_text(json.dumps({"nonce": "n", "device_uids": [], "expires": time.time() + 3600}))
     assert _mgr(client, root, tmp_path, Backend(root), drain_timeout=0.05).reconcile() == "failed"
     assert "validator load step" in api.nodes["gpu-node-1"]["metadata"]["annotations"][pm.ANNOT_STATE]
+
+
+# ----------------------------------------------------------------------------- driver semantics
+def test_amdsmi_hive_spx_nps1_to_cpx_nps2_with_handle_invalidation(tmp_path, api, client):
+    """against the hardware-faithful fake (NPS hive-wide with a driver reload
+    that kills the amd-smi session; a compute change invalidates that ASIC's handles) the manager
+    applies NPS2 ONCE, waits for the reload, re-opens amd-smi and switches every ASIC to CPX."""
+    from fakes.amdsmi_partition import FakeAmdSmiHive
+    from k8s_nvidia_gpus_amd.operator.partition_amdsmi import AmdSmiPartitionBackend
+
+    root = fake_sysfs.build_node(tmp_path / "r")
+    api.nodes["gpu-node-1"]["metadata"]["labels"][pm.LABEL_MEM_DESIRED] = "NPS2"
+    hive = FakeAmdSmiHive(root)
+    backend = AmdSmiPartitionBackend(hive)
+    assert _mgr(client, root, tmp_path, backend).reconcile() == "applied"
+    mem = [c for c in hive.calls if c[0] == "memory"]
+    assert hive.reloads == 1 and len(mem) == 1 and mem[0][2] == "NPS2"        # once per node
+    assert sorted(c[1] for c in hive.calls if c[0] == "compute") == list(range(8))
+    topo = read_topology(str(root), 90500)
+    assert len(topo.gpus) == 64
+    assert {(g.compute_partition, g.memory_partition) for g in topo.gpus} == {("CPX", "NPS2")}
+    state = api.nodes["gpu-node-1"]["metadata"]["annotations"][pm.ANNOT_STATE]
+    assert state.startswith("idle: applied CPX/NPS2") and "validator" in state
+    assert _mgr(client, root, tmp_path, backend).reconcile() == "idle"
+
+
+def test_a_per_asic_nps_loop_on_one_session_fails_on_the_faithful_fake(tmp_path):
+    """What the round-4 manager did — NPS per ASIC through the session opened at start — meets a
+    dead session after the first (hive-wide) reload."""
+    from fakes.amdsmi_partition import FakeAmdSmiHive
+
+    root = fake_sysfs.build_node(tmp_path / "r")
+    hive = FakeAmdSmiHive(root)
+    hive.amdsmi_init()
+    hs = hive.amdsmi_get_processor_handles()
+    hive.amdsmi_set_gpu_memory_partition(hs[0], hive.AmdSmiMemoryPartitionType.NPS2)
+    with pytest.raises(RuntimeError, match="stale"):
+        hive.amdsmi_set_gpu_memory_partition(hs[1], hive.AmdSmiMemoryPartitionType.NPS2)
+    with pytest.raises(RuntimeError, match="reload"):
+        hive.amdsmi_get_processor_handles()
+    hive.amdsmi_shut_down()
+    hive.amdsmi_init()
+    hs = hive.amdsmi_get_processor_handles()
+    hive.amdsmi_set_gpu_compute_partition(hs[2], hive.AmdSmiComputePartitionType.CPX)
+    with pytest.raises(RuntimeError, match="stale"):         # that ASIC's handle is gone
+        hive.amdsmi_set_gpu_compute_partition(hs[2], hive.AmdSmiComputePartitionType.SPX)
+    hive.amdsmi_get_gpu_device_bdf(hs[3])                    # other ASICs' handles still valid
+    assert len(hive.amdsmi_get_processor_handles()) == 7 + 8
+
+
+class DriverSysfs(pm.SysfsPartitionBackend):
+    """The real sysfs writes on the fake tree plus what amdgpu does with them: a compute write
+    re-partitions that ASIC at once; a memory write only requests the NPS mode, which a driver
+    reload (``reload``) applies to the whole hive."""
+
+    def __init__(self, root):
+        super().__init__(str(root))
+        self.requested = None
+        self.reloads = 0
+
+    BDFS = [g["bdf"] for g in fake_sysfs.LAYOUT["gpus"][:8]]     # build_node's ASIC order
+
+    def _modes(self):
+        heads = {g.pci_bdf: g for g in read_topology(self.root, 90500).gpus}
+        return ([heads[b].compute_partition for b in self.BDFS],
+                [heads[b].memory_partition for b in self.BDFS])
+
+    def set_compute(self, dev, mode):
+        super().set_compute(dev, mode)
+        c, m = self._modes()
+        c[self.BDFS.index(dev.pci_bdf)] = mode
+        fake_sysfs.set_partition(self.root, 8, c, m)
+
+    def set_memory(self, dev, mode):
+        path = os.path.join(self.root, "sys/class/drm", f"card{dev.card_minor}", "device",
+                            "current_memory_partition")
+        old = open(path).read()
+        super().set_memory(dev, mode)           # the write goes through ...
+        with open(path, "w") as f:              # ... but reads back the running mode until a reload
+            f.write(old)
+        self.requested = mode
+
+    def reload(self):
+        c, _ = self._modes()
+        self.reloads += 1
+        fake_sysfs.set_partition(self.root, 8, c, [self.requested] * 8)
+        return 0
+
+
+def test_sysfs_nps_request_ends_in_pending_reload_then_a_reload_command_completes_it(
+        tmp_path, api, client):
+    root = fake_sysfs.build_node(tmp_path / "r")
+    api.nodes["gpu-node-1"]["metadata"]["labels"][pm.LABEL_MEM_DESIRED] = "NPS2"
+    api.add_pod("llm", "coder-llm-7d9f", "gpu-node-1", gpus=1)
+    backend = DriverSysfs(root)
+    mgr = _mgr(client, root, tmp_path, backend, reenum_timeout=0.05)
+    assert mgr.reconcile() == "pending-reload"
+    node = api.nodes["gpu-node-1"]
+    state = node["metadata"]["annotations"][pm.ANNOT_STATE]
+    assert state.startswith("pending-reload: NPS2") and "driverReloadCommand" in state
+    assert not [t for t in node["spec"].get("taints", []) if t["key"] == pm.TAINT_KEY]
+    assert not os.path.exists(tmp_path / "run/partition-in-progress")
+    assert {g.memory_partition for g in read_topology(str(root), 90500).gpus} == {"NPS1"}
+    assert backend.requested == "NPS2" and api.evictions == [("llm", "coder-llm-7d9f")]
+    # the next reconcile neither drains again nor times out: the request stands
+    api.add_pod("llm", "coder-llm-new", "gpu-node-1", gpus=1)
+    assert mgr.reconcile() == "pending-reload" and len(api.evictions) == 1
+    # with a reload command configured the change completes
+    runs = []
+    mgr2 = _mgr(client, root, tmp_path, backend, reload_cmd=["/host/reload-amdgpu.sh"], reenum_timeout=5,
+                run_cmd=lambda argv: runs.append(argv) or backend.reload())
+    assert mgr2.reconcile() == "applied" and runs == [["/host/reload-amdgpu.sh"]]
+    topo = read_topology(str(root), 90500)
+    assert len(topo.gpus) == 64 and backend.reloads == 1
+    assert {(g.compute_partition, g.memory_partition) for g in topo.gpus} == {("CPX", "NPS2")}
+
+
+def test_validator_step_started_after_the_drain_is_waited_for(tmp_path, api, client):
+    """a validator reservation that appears after the drain (between the drain and the
+    write) holds the apply until it is released."""
+    root = fake_sysfs.build_node(tmp_path / "r")
+    res = tmp_path / "run/validations/in-test.json"
+    res.parent.mkdir(parents=True)
+    seen = []
+
+    def acks(*a, **k):
+        # the validator reserves right after the drain finished
+        res.write_text(json.dumps({"nonce": "n", "device_uids": [], "expires": time.time() + 3600}))
+        return {}
+
+    def sleep(_s):
+        seen.append(res.exists())
+        if len(seen) == 3:
+            res.unlink()                       # its step finished
+
+    backend = Backend(root)
+    mgr = _mgr(client, root, tmp_path, backend, sleep=sleep, ack_components=("x",))
+    orig = pause_mod.acks
+    pause_mod.acks = lambda nonce, d, comps: (acks(), {c: True for c in comps})[1]
+    try:
+        assert mgr.reconcile() == "applied"
+    finally:
+        pause_mod.acks = orig
+    assert seen[:3] == [True, True, True] and len(backend.applied) == 8

@@ -380,7 +380,7 @@ def test_rocprof_counter_summary_on_real_mi355x_csv():
     assert 1300 < s["tflops_profiled"] < 2000
 
 
-def test_gemm_step_runs_a_counter_pass(tmp_path):
+def test_profile_step_runs_a_counter_pass(tmp_path):
     import shutil
 
     cfg = load_config(text="validator: {podResourcesRequired: false, gemmMinTflops: 900, rocprofCounters: true, gemmFp8: false}\n")
@@ -398,6 +398,9 @@ def test_gemm_step_runs_a_counter_pass(tmp_path):
 
     v = Validator(cfg, str(tmp_path), bin_dir="/x", runner=runner)
     g = v.run_step("gemm")
+    assert g.passed, g.reason and "rocprof_counters" not in g.detail    # the gate step runs plain
+    assert all(c[0] != "rocprofv3" for c in calls)
+    g = v.run_step("profile")
     assert g.passed, g.reason
     rc = g.detail["rocprof_counters"]
     assert rc["flop_matches_shape"] is True and rc["mfma_util_pct"] > 70

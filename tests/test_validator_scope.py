@@ -410,3 +410,116 @@ def test_index_device_ids_map_through_the_plugin_file(tmp_path):
         res = Validator(cfg, str(tmp_path / "m3"), bin_dir="/x", runner=r2, root=str(root),
                         device_id_map=str(tmp_path / "missing.json")).run_step("gemm")
     assert not res.passed and "cannot map" in res.reason and r2.calls == []
+
+
+def test_gate_opens_on_the_gemm_and_a_pending_pod_gets_its_gpu_before_rccl(tmp_path):
+    """on an 8-agent node the plugin advertises the GPUs Healthy as soon as the
+    per-device GEMM passed; the node-wide RCCL step waits ``gateGraceSeconds`` after the gate
+    opened, a pod pending for the node is allocated GPU 0 in that window, and RCCL then reserves
+    and loads only the other 7 (GPU 0 never appears in its reservation)."""
+    import threading
+
+    from k8s_nvidia_gpus_amd.operator import deviceplugin_api as api
+    from k8s_nvidia_gpus_amd.operator.device_plugin import AmdGpuDevicePlugin, ValidationGate
+
+    root = _node(tmp_path)
+    cfg, sock = _cfg(tmp_path, ", rccl: true, reserveAckSeconds: 5, gateGraceSeconds: 3")
+    uids = _uids(root)
+    marker = tmp_path / "m"
+    _chain_markers(marker, ("driver", "runtime", "vectoradd"))
+    gate = ValidationGate(str(marker), root=str(root), gate=True)
+    plugin = AmdGpuDevicePlugin(cfg, root=str(root), kubelet_dir=str(tmp_path / "kd"),
+                                pause_marker=None, dev_prefix=str(root / "dev"), gate=gate,
+                                ecc_fn=lambda d: 0)
+    health = lambda: {d.ID: d.health for d in plugin.list_response().devices}  # noqa: E731
+    stop = threading.Event()
+    loop = threading.Thread(target=plugin.run, kwargs={"poll": 0.02, "stop_event": stop,
+                                                        "health_interval": 60}, daemon=True)
+    pods = {}
+    seen = {}
+    reservations = []
+
+    class R(Runner):
+        def __call__(self, argv, timeout):
+            reservations.append(json.loads((marker / IN_TEST).read_text())["device_uids"])
+            return super().__call__(argv, timeout)
+
+    def grace_sleep(secs):
+        # the grace window: the gate is open; kubelet hands GPU 0 to the pending pod
+        time.sleep(0.2)
+        seen["health_in_grace"] = health()
+        seen["grace"] = secs
+        pods[("llm", "coder-llm-0")] = [("amd.com/gpu", [uids[0]])]
+
+    r = R({"amd-gemm-validator": (0, _gemm_log(8, 1500.0)), "rccl-allreduce-bench": (0, RCCL_8GPU)})
+    loop.start()
+    try:
+        with FakePodResources(sock, pods):
+            v = Validator(cfg, str(marker), bin_dir="/x", runner=r, root=str(root), sleep=grace_sleep)
+            assert set(health().values()) == {api.UNHEALTHY}          # gate closed at boot
+            g = v.run_step("gemm")
+            assert g.passed and sorted(g.detail["validated_devices"]) == sorted(uids)
+            rc = v.run_step("rccl")
+    finally:
+        stop.set()
+        loop.join(5)
+    assert all(seen["health_in_grace"][u] == api.HEALTHY for u in uids)   # allocatable pre-RCCL
+    assert 0 < seen["grace"] <= 3
+    assert rc.passed and rc.detail["reservation"]["gate_grace_waited_s"] > 0
+    assert uids[0] not in reservations[-1] and len(reservations[-1]) == 7
+    assert _narrowed(r.calls[-1]) == [str(i) for i in range(1, 8)]      # RCCL never touched GPU 0
+    doc = json.loads((marker / VALIDATED_DEVICES).read_text())
+    assert sorted(doc["device_uids"]) == sorted(uids) and doc["opened"] <= time.time()
+
+
+def test_a_serving_plugin_that_never_acks_defers_the_load_step(tmp_path):
+    """the plugin's registration socket accepts connections but the reservation
+    is never acked (a plugin stuck in an amd-smi call) → the step is deferred and no GPU is loaded;
+    without any plugin socket the step proceeds after reserveAckSeconds."""
+    import socket as socketlib
+
+    root = _node(tmp_path)
+    psock = tmp_path / "dp" / "amd-gpu.sock"
+    psock.parent.mkdir()
+    cfg, sock = _cfg(tmp_path, f", rccl: false, reserveAckSeconds: 0.3, pluginSocket: {psock}")
+    srv = socketlib.socket(socketlib.AF_UNIX, socketlib.SOCK_STREAM)
+    srv.bind(str(psock))
+    srv.listen(8)
+    r = Runner({"amd-gemm-validator": (0, _gemm_log(8, 1500.0))})
+    try:
+        with FakePodResources(sock, {}):
+            v = Validator(cfg, str(tmp_path / "m"), bin_dir="/x", runner=r, root=str(root))
+            g = v.run_step("gemm")
+    finally:
+        srv.close()
+    assert g.deferred and not g.passed and "did not ack" in g.reason
+    assert g.detail["reservation"]["unacked_live_plugin"] and r.calls == []
+    assert not (tmp_path / "m" / IN_TEST).exists()          # the reservation was withdrawn
+    psock.unlink()                                          # no plugin at all: proceed
+    with FakePodResources(sock, {}):
+        g = Validator(cfg, str(tmp_path / "m2"), bin_dir="/x", runner=r, root=str(root)).run_step("gemm")
+    assert g.passed and not g.detail["reservation"]["acked"] and r.calls
+
+
+def test_partition_started_during_the_reservation_defers_the_step(tmp_path):
+    """the pause marker appears after the first check (the partition manager drained
+    while the validator reserved): the step is deferred after the reservation, nothing loads."""
+    from k8s_nvidia_gpus_amd.operator import pause as pause_mod
+
+    root = _node(tmp_path)
+    cfg, sock = _cfg(tmp_path, ", rccl: false, reserveAckSeconds: 0.2")
+    pause = tmp_path / "pause"
+
+    class Racing(FakePodResources):
+        def List(self, request, context):  # noqa: N802
+            if self.calls == 1:                       # the re-read after the reservation
+                pause_mod.start_pause(str(pause), str(tmp_path / "acks"))
+            return super().List(request, context)
+
+    r = Runner({"amd-gemm-validator": (0, _gemm_log(8, 1500.0))})
+    with Racing(sock, {}):
+        v = Validator(cfg, str(tmp_path / "m"), bin_dir="/x", runner=r, root=str(root),
+                      pause_marker=str(pause))
+        g = v.run_step("gemm")
+    assert g.deferred and "partition change started" in g.reason and r.calls == []
+    assert v.run_step("vectoradd").deferred

@@ -102,7 +102,11 @@ for step in "$@"; do
       # shellcheck disable=SC2086
       timeout -k 10 900 python -u tools/llm_serve_bench.py $extra --server-log "$OUT/serve_server_$n.log" \
         --out "$OUT/serve_$n.json" > "$OUT/serve_$n.log" 2>&1 || fail "$step" $? "$OUT/serve_$n.log"
-      grep -E "^(concurrency|admit|server ready)" "$OUT/serve_$n.log" | cut -c1-400 ;;
+      grep -E "^(concurrency|admit|server ready)" "$OUT/serve_$n.log" | cut -c1-900 ;;
+    attn-probe)
+      timeout -k 10 300 python -u tools/debug/prefill_attn_probe.py > "$OUT/prefill_attn_probe.log" 2>&1 \
+        || fail "$step" $? "$OUT/prefill_attn_probe.log"
+      cut -c1-200 "$OUT/prefill_attn_probe.log" ;;
     prof-llm|prof-llm:*)
       t=1; np=512; [[ "$step" == prof-llm:* ]] && t="${step#prof-llm:}"
       [[ "$t" == *:* ]] && { np="${t#*:}"; t="${t%%:*}"; }

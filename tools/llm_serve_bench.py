@@ -184,6 +184,18 @@ async def run(args, base):
                     gaps_all.append(b - a)
                     if b > t_in and a < t_first:       # a gap overlapping the admission
                         gaps.append(b - a)
+            # what the scheduler did meanwhile (same CLOCK_MONOTONIC as perf_counter here)
+            async with cl.session.get(cl.base + "/debug/iterations") as r:
+                dbg = await r.json()
+            its = [x for x in dbg["iterations"] if t_in - 0.05 <= x["t"] <= t_first + 0.05]
+            worst = sorted(its, key=lambda x: -(x["admit_s"] + x["prefill_s"] + x["step_s"]
+                                                + x["wake_s"]))[:6]
+            gcs = [g for g in dbg["gc_pauses"] if t_in - 0.05 <= g["t"] <= t_first + 0.05]
+            out["admit_trace"] = {
+                "iterations": len(its),
+                "worst": [{k: (round(v * 1e3, 2) if k.endswith("_s") else v) for k, v in x.items()
+                           if k != "t"} | {"at_ms": round((x["t"] - t_in) * 1e3, 1)} for x in worst],
+                "gc_pauses_ms": [round(g["s"] * 1e3, 2) for g in gcs]}
             out["admit"] = {"running_streams": n - 1, "long_prompt_tokens": long_n,
                             "long_ttft_ms": round((t_first - t_in) * 1e3, 1),
                             "worst_gap_during_admit_ms": round(max(gaps) * 1e3, 2) if gaps else None,
@@ -192,6 +204,7 @@ async def run(args, base):
                             "itl_ms_p99": round(pct(gaps_all, 99) * 1e3, 2),
                             "long_timings": lrec.get("timings")}
             print(f"admit {out['admit']}", file=sys.stderr, flush=True)
+            print(f"admit_trace {out['admit_trace']}", file=sys.stderr, flush=True)
         out["metrics"] = await metrics(cl)
     finally:
         await cl.close()
