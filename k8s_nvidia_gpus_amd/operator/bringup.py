@@ -10,14 +10,24 @@ socket side (:class:`.kubelet_stub.KubeletStub`, the same stand-in the CPU tests
 
   driver      kfd-probe sees the expected gfx950 agents and opens /dev/kfd + render nodes
   runtime     amd-container-runtime + CDI spec installed (into the work dir's host prefix)
-  plugin      device plugin serves, registers with kubelet, first ListAndWatch: healthy devices
+  plugin      device plugin serves, registers with kubelet, first ListAndWatch
+  vectoradd   (gated order) the validator's vectorAdd on every GPU
+  gemm        (gated order) the validator's bf16 + fp8 GEMMs: the per-device gate step
+  allocatable (gated order) ListAndWatch turns a GPU Healthy (validated-devices.json)
   allocate    kubelet's GetPreferredAllocation + Allocate for ``amd.com/gpu: 1``
   create      the runtime shim edits the pod's OCI spec from the Allocate annotations: /dev/kfd +
               exactly the allocated render node, with device-cgroup rules
   container   the pod's process (amd-vectoradd, reference protocol) on the allocated GPU
               → time_to_first_gpu_pod_s
-  validate    (optional) the validator chain: vectorAdd, bf16/fp8 GEMM, bandwidth, report
+  validate    (optional) the rest of the validator chain (ungated order: all of it) → report
               → time_to_validated_s
+
+Two orders.  **Gated** (``gated=True``, the shipped configuration: ``validator.gateOnValidation``)
+builds the plugin with the :class:`ValidationGate`, so no GPU is advertised Healthy before the
+validator's per-device gate steps (vectorAdd, then the GEMMs of ``gateSteps``) passed on it; the
+first pod is allocated only after that, and the node-wide steps (bandwidth, stress, RCCL,
+profiling) run after the pod.  **Ungated** is the order without the gate (plugin → pod → chain).
+``main`` runs both and reports the two times to first GPU pod side by side.
 
 The reference has no such measurement; it budgets 90 minutes for its in-cluster driver build alone
 (reference cluster-config/apps/gpu-operator/helmrelease.yaml:7).  What this does NOT include: API
@@ -80,12 +90,16 @@ def rehearse(cfg: OperatorConfig, bin_dir: str, workdir: Optional[str] = None, r
              validate: bool = True, runner=default_runner,
              container_runner: ContainerRunner = _run_container,
              container_cmd: Optional[Sequence[str]] = None, timeout: float = 120.0,
-             driver_wait: float = 120.0) -> Dict:
+             driver_wait: float = 120.0, gated: Optional[bool] = None) -> Dict:
     """Run the node-local bring-up once; returns a JSON-able report (raises nothing: a failed stage
-    ends the run and is reported)."""
-    from .device_plugin import AmdGpuDevicePlugin
+    ends the run and is reported).  ``gated``: the validation-gated order (default: the config's
+    ``validator.gateOnValidation``)."""
+    from .device_plugin import AmdGpuDevicePlugin, ValidationGate
     from .kubelet_stub import KubeletStub
     from .runtime import install_runtime
+
+    if gated is None:
+        gated = bool(cfg.section("validator").get("gateOnValidation", True))
 
     own_tmp = workdir is None
     workdir = workdir or tempfile.mkdtemp(prefix="amdk8s-bringup-")
@@ -95,7 +109,8 @@ def rehearse(cfg: OperatorConfig, bin_dir: str, workdir: Optional[str] = None, r
     t0 = time.monotonic()
     wall0 = time.time()
     stages: List[Stage] = []
-    report: Dict = {"check": "bringup", "root": root, "workdir": workdir, "start_time": wall0}
+    report: Dict = {"check": "bringup", "root": root, "workdir": workdir, "start_time": wall0,
+                    "order": "gated" if gated else "ungated"}
     dev_root = "" if root == "/" else root.rstrip("/")
     plugin = kubelet = None
     stop = threading.Event()
@@ -117,6 +132,10 @@ def rehearse(cfg: OperatorConfig, bin_dir: str, workdir: Optional[str] = None, r
     vraw["validator"]["pluginTest"] = False
     # a bare box has no kubelet: every agent is free (in a cluster an absent socket fails the step)
     vraw["validator"]["podResourcesRequired"] = False
+    kdir = os.path.join(workdir, "kubelet-device-plugins")
+    if len(kdir) > 80:  # unix socket paths are limited to 107 bytes
+        kdir = tempfile.mkdtemp(prefix="amdk8s-kubelet-")
+    vraw["validator"]["pluginSocket"] = os.path.join(kdir, "amd-gpu.sock")
     v = Validator(OperatorConfig(vraw), markers, bin_dir=bin_dir, runner=runner, root=root,
                   driver_wait=driver_wait)
     state: Dict = {}
@@ -134,24 +153,48 @@ def rehearse(cfg: OperatorConfig, bin_dir: str, workdir: Optional[str] = None, r
 
         def plugin_up():
             nonlocal plugin, kubelet
-            kdir = os.path.join(workdir, "kubelet-device-plugins")
-            if len(kdir) > 80:  # unix socket paths are limited to 107 bytes
-                kdir = tempfile.mkdtemp(prefix="amdk8s-kubelet-")
+            if not kdir.startswith(workdir):
                 state["kdir_tmp"] = kdir
             kubelet = KubeletStub(kdir).start()
+            gate = ValidationGate(markers, root=root, gate=True) if gated else None
             plugin = AmdGpuDevicePlugin(cfg, root=root, kubelet_dir=kdir, pause_marker=None,
-                                        dev_prefix=os.path.join(dev_root or "/", "dev"))
-            threading.Thread(target=plugin.run, kwargs={"poll": 0.05, "stop_event": stop},
+                                        dev_prefix=os.path.join(dev_root or "/", "dev"), gate=gate)
+            threading.Thread(target=plugin.run, kwargs={"poll": 0.02, "stop_event": stop},
                              daemon=True).start()
             if not kubelet.registered.wait(timeout):
                 raise BringupError("device plugin never registered with kubelet")
             reg = kubelet.registrations[-1]
             ch, stub = kubelet.plugin_stub()
-            first = next(stub.ListAndWatch(api.Empty(), timeout=timeout))
+            watch = stub.ListAndWatch(api.Empty(), timeout=timeout + 3600)
+            first = next(watch)
             healthy = [d.ID for d in first.devices if d.health == api.HEALTHY]
-            state.update(channel=ch, stub=stub, healthy=healthy)
-            return {"_ok": bool(healthy), "resource": reg.resource_name, "endpoint": reg.endpoint,
-                    "advertised": len(first.devices), "healthy": len(healthy)}
+            state.update(channel=ch, stub=stub, healthy=healthy, watch=watch)
+            # gated: nothing is Healthy before the validator's gate steps passed this boot
+            return {"_ok": bool(first.devices) and (gated or bool(healthy)),
+                    "resource": reg.resource_name, "endpoint": reg.endpoint,
+                    "advertised": len(first.devices), "healthy": len(healthy), "gated": gated}
+
+        def gate_step(name):
+            def run():
+                r = v.run_step(name)
+                out = {"_ok": r.passed, "duration_s": r.detail.get("duration_s"), "reason": r.reason}
+                if name == "gemm":
+                    out["tflops"] = [d.get("tflops") for d in r.detail.get("devices", [])]
+                    out["validated_devices"] = len(r.detail.get("validated_devices") or [])
+                return out
+            return run
+
+        def allocatable():
+            """The next ListAndWatch answers until a GPU turns Healthy (kubelet can allocate)."""
+            healthy: List[str] = []
+            n = 0
+            for resp in state["watch"]:
+                n += 1
+                healthy = [d.ID for d in resp.devices if d.health == api.HEALTHY]
+                if healthy:
+                    break
+            state["healthy"] = healthy
+            return {"_ok": bool(healthy), "healthy": len(healthy), "updates": n}
 
         def allocate():
             stub = state["stub"]
@@ -209,6 +252,11 @@ def rehearse(cfg: OperatorConfig, bin_dir: str, workdir: Optional[str] = None, r
         stage("driver", driver)
         stage("runtime", runtime)
         stage("plugin", plugin_up)
+        gate_steps = ["vectoradd"] + [s for s in v._gating_steps() if s != "driver"]
+        if gated:
+            for name in gate_steps:
+                stage(name, gate_step(name))
+            stage("allocatable", allocatable)
         stage("allocate", allocate)
         stage("create", create)
         stage("container", container)
@@ -216,7 +264,9 @@ def rehearse(cfg: OperatorConfig, bin_dir: str, workdir: Optional[str] = None, r
         if validate:
             def validator_chain():
                 out = {}
-                for s in ("vectoradd", "gemm", "bandwidth", "stress", "rccl"):
+                for s in ("vectoradd", "gemm", "bandwidth", "stress", "rccl", "profile"):
+                    if gated and s in gate_steps:
+                        continue                 # ran before the pod
                     r = v.run_step(s)
                     out[s] = {"passed": r.passed, "duration_s": r.detail.get("duration_s"),
                               "reason": r.reason}
@@ -252,13 +302,24 @@ def rehearse(cfg: OperatorConfig, bin_dir: str, workdir: Optional[str] = None, r
 
 
 def main(args, cfg: OperatorConfig, bin_dir: str) -> int:
-    rep = rehearse(cfg, bin_dir, workdir=args.workdir, root=args.root,
-                   validate=not args.no_validate)
-    for s in rep["stages"]:
-        print(f"{s['name']:10s} {'ok  ' if s['ok'] else 'FAIL'} {s['start_s']:8.3f} -> {s['end_s']:8.3f} s"
-              + ("" if s["ok"] else f"  {s['detail'].get('error') or s['detail']}"))
-    print(json.dumps(rep))
-    return 0 if rep["passed"] else 1
+    """The shipped (gated) order with the validator chain, then the ungated order up to the
+    first pod; one JSON document with both times to first GPU pod."""
+    reps = {}
+    for order in ("gated", "ungated"):
+        wd = os.path.join(args.workdir, order) if args.workdir else None
+        reps[order] = rehearse(cfg, bin_dir, workdir=wd, root=args.root,
+                               validate=(order == "gated") and not args.no_validate,
+                               gated=(order == "gated"))
+        for s in reps[order]["stages"]:
+            print(f"{order:8s} {s['name']:11s} {'ok  ' if s['ok'] else 'FAIL'} "
+                  f"{s['start_s']:8.3f} -> {s['end_s']:8.3f} s"
+                  + ("" if s["ok"] else f"  {s['detail'].get('error') or s['detail']}"))
+    doc = {"check": "bringup", "time_to_first_gpu_pod_s": {
+        o: r["time_to_first_gpu_pod_s"] for o, r in reps.items()},
+        "time_to_validated_s": reps["gated"]["time_to_validated_s"],
+        "passed": all(r["passed"] for r in reps.values()), **reps}
+    print(json.dumps(doc))
+    return 0 if doc["passed"] else 1
 
 
 __all__ = ["rehearse", "main", "json_lines"]

@@ -41,16 +41,28 @@ def runner(argv, timeout):
     return 0, LOGS[name]
 
 
-def test_rehearsal_reaches_first_pod_and_validated(tmp_path, bins):
+@pytest.mark.parametrize("gated", [True, False])
+def test_rehearsal_reaches_first_pod_and_validated(tmp_path, bins, gated):
+    """Gated (the shipped order): the plugin advertises nothing Healthy until the validator's
+    vectorAdd and GEMM passed, the pod comes after them, the node-wide steps after the pod.
+    Ungated: plugin → pod → the whole chain."""
     root = fake_sysfs.build_node(tmp_path / "node")
-    cfg = load_config(text="expectedGpusPerNode: 8\n")
+    cfg = load_config(text="expectedGpusPerNode: 8\nvalidator: {gateGraceSeconds: 0}\n")
     rep = bringup.rehearse(cfg, bins, workdir=str(tmp_path / "work"), root=str(root), runner=runner,
-                           container_cmd=CONTAINER_OK, timeout=30)
+                           container_cmd=CONTAINER_OK, timeout=30, gated=gated)
     names = [s["name"] for s in rep["stages"]]
-    assert names == ["driver", "runtime", "plugin", "allocate", "create", "container", "validate"], rep
-    assert rep["passed"], rep
+    pod = ["allocate", "create", "container", "validate"]
+    if gated:
+        assert names == ["driver", "runtime", "plugin", "vectoradd", "gemm", "allocatable"] + pod, rep
+    else:
+        assert names == ["driver", "runtime", "plugin"] + pod, rep
+    assert rep["passed"] and rep["order"] == ("gated" if gated else "ungated"), rep
     st = {s["name"]: s for s in rep["stages"]}
-    assert st["plugin"]["detail"]["healthy"] == 8 and st["plugin"]["detail"]["resource"] == "amd.com/gpu"
+    assert st["plugin"]["detail"]["advertised"] == 8 and st["plugin"]["detail"]["resource"] == "amd.com/gpu"
+    assert st["plugin"]["detail"]["healthy"] == (0 if gated else 8)
+    if gated:
+        assert st["allocatable"]["detail"]["healthy"] == 8 and st["gemm"]["detail"]["validated_devices"] == 8
+        assert "gemm" not in st["validate"]["detail"] and "bandwidth" in st["validate"]["detail"]
     nodes = st["create"]["detail"]["device_nodes"]
     assert nodes[0] == "/dev/dri/renderD" + st["allocate"]["detail"]["annotations"]["amd.com/gpu.render-minors"]
     assert nodes[1] == "/dev/kfd" and len(nodes) == 2  # exactly one GPU injected

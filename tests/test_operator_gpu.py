@@ -145,25 +145,31 @@ def test_bench_py_rccl_path_under_torchrun_one_rank():
     assert tel is None or "error" in tel or tel["samples"] >= 1
 
 
-def test_node_bringup_rehearsal_on_real_hardware(tmp_path, native):
+@pytest.mark.parametrize("gated", [True, False])
+def test_node_bringup_rehearsal_on_real_hardware(tmp_path, native, gated):
     """Node-local time-to-first-GPU-pod: real kfd-probe, runtime shim + CDI, device plugin over gRPC
-    (kubelet stand-in), Allocate, OCI spec edit, vectorAdd on the allocated GPU, validator chain."""
+    (kubelet stand-in), Allocate, OCI spec edit, vectorAdd on the allocated GPU, validator chain.
+    Gated (shipped): the plugin advertises the GPU only after the validator's vectorAdd + GEMMs
+    passed on it, and the first pod is allocated then (<= 5 s)."""
     import torch
 
     from k8s_nvidia_gpus_amd.operator import bringup
 
     n = torch.cuda.device_count()
     cfg = load_config(text=f"expectedGpusPerNode: {n}\n")
-    rep = bringup.rehearse(cfg, str(native), workdir=str(tmp_path / "work"))
+    rep = bringup.rehearse(cfg, str(native), workdir=str(tmp_path / "work"), gated=gated)
     assert rep["passed"], json.dumps(rep["stages"][-1])
     st = {s["name"]: s for s in rep["stages"]}
-    assert st["plugin"]["detail"]["healthy"] == n
+    assert st["plugin"]["detail"]["healthy"] == (0 if gated else n)
+    if gated:
+        assert st["allocatable"]["detail"]["healthy"] == n
+        assert rep["time_to_first_gpu_pod_s"] <= 5.0, rep["time_to_first_gpu_pod_s"]
     assert st["create"]["detail"]["device_nodes"][-1] == "/dev/kfd"
     assert rep["time_to_first_gpu_pod_s"] < 30 and rep["time_to_validated_s"] < 120
     out = os.environ.get("AMDK8S_EVIDENCE_DIR")
     if out:
         os.makedirs(out, exist_ok=True)
-        with open(os.path.join(out, "bringup.json"), "w") as f:
+        with open(os.path.join(out, f"bringup_{'gated' if gated else 'ungated'}.json"), "w") as f:
             json.dump(rep, f, indent=1)
 
 

@@ -13,6 +13,9 @@
 #   native           amd-vectoradd, amd-gemm-validator (bf16 + fp8), amd-proftester
 #   llm[:<tokens>]   tools/llm_bench.py (decode T list, default 1,2,3,4) + prefill
 #   llm-ctx:<n>      tools/llm_bench.py decode T = 1,4,8 after an n-token prompt (long-context decode)
+#   bringup          operator bring-up rehearsal with the shipped ConfigMap config: gated + ungated
+#                    time-to-first-GPU-pod (python -m k8s_nvidia_gpus_amd.operator bringup)
+#   attn-probe       tools/debug/prefill_attn_probe.py (chunked-prefill attention formulations)
 #   serve[:<args>]   tools/llm_serve_bench.py: the server under 1/4/8 streaming clients + a long-prompt
 #                    admission (args: comma-separated, '=' for spaces, e.g. serve:--clients=8,--gen=256)
 #   gemv[:<cases>]   tools/llm_bench.py --gemv: cold-weight GEMV decomposition sweep, T = 1 and 4
@@ -103,6 +106,20 @@ for step in "$@"; do
       timeout -k 10 900 python -u tools/llm_serve_bench.py $extra --server-log "$OUT/serve_server_$n.log" \
         --out "$OUT/serve_$n.json" > "$OUT/serve_$n.log" 2>&1 || fail "$step" $? "$OUT/serve_$n.log"
       grep -E "^(concurrency|admit|server ready)" "$OUT/serve_$n.log" | cut -c1-900 ;;
+    bringup)
+      # the shipped operator config (ConfigMap), narrowed to this box's GPU count
+      python3 - "$OUT/operator.yaml" <<'PYEOF'
+import sys, yaml
+cm = yaml.safe_load(open("cluster-config/apps/amd-gpu-operator/config.yaml"))
+cfg = yaml.safe_load(cm["data"]["operator.yaml"])
+import torch
+cfg["expectedGpusPerNode"] = torch.cuda.device_count()
+open(sys.argv[1], "w").write(yaml.safe_dump(cfg))
+PYEOF
+      timeout -k 10 600 python3 -m k8s_nvidia_gpus_amd.operator bringup --config "$OUT/operator.yaml" \
+        --workdir "$OUT/bringup_work" > "$OUT/bringup.log" 2>&1 || fail "$step" $? "$OUT/bringup.log"
+      grep -v '^{' "$OUT/bringup.log" | tail -24; grep '^{' "$OUT/bringup.log" | tail -1 > "$OUT/bringup.json"
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('time_to_first_gpu_pod_s', d['time_to_first_gpu_pod_s'], 'time_to_validated_s', d['time_to_validated_s'])" "$OUT/bringup.json" ;;
     attn-probe)
       timeout -k 10 300 python -u tools/debug/prefill_attn_probe.py > "$OUT/prefill_attn_probe.log" 2>&1 \
         || fail "$step" $? "$OUT/prefill_attn_probe.log"

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # PMC passes over a short Qwen2.5-7B-shaped decode (tools/llm_bench.py), counters only with
-# --kernel-trace (pool rules).  Summary per kernel: duration, effective clock, wait / busy shares,
+# --kernel-trace (pool rules).  Summary per kernel: duration, wait / busy shares,
 # HBM read bytes.
 set -euo pipefail
 cd "$(dirname "$0")/.."

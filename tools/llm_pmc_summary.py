@@ -1,5 +1,10 @@
 #!/usr/bin/env python3
-"""Per-kernel summary of rocprofv3 counter CSVs from tools/llm_pmc.sh (LLM decode kernels)."""
+"""Per-kernel summary of rocprofv3 counter CSVs from tools/llm_pmc.sh (LLM decode kernels).
+
+No clock column: GRBM_GUI_ACTIVE accumulates over the dispatch window rocprofv3 brackets, which
+for these 5-20 us kernels is longer than the kernel's own timestamps, so GRBM / duration read as
+3-7 GHz on a <= 2.4 GHz part.  The clock of a long kernel comes from the validator's
+GEMM counter pass (operator/validator.py rocprof_counter_summary) or amd-smi telemetry."""
 import collections
 import csv
 import glob
@@ -27,8 +32,6 @@ def main(pattern):
         m = {c: sum(v) / len(v) for c, v in acc[k].items()}
         d = sum(bykey[k]) / len(bykey[k])
         line = f"{k:52s} n={len(bykey[k]):4d} {d / 1e3:8.2f} us"
-        if "GRBM_GUI_ACTIVE" in m:
-            line += f"  clk {m['GRBM_GUI_ACTIVE'] / 8 / d:5.2f} GHz"
         if "SQ_WAVE_CYCLES" in m and m["SQ_WAVE_CYCLES"]:
             wc = m["SQ_WAVE_CYCLES"]
             line += (f"  wait {m.get('SQ_WAIT_INST_ANY', 0) / wc:5.2f} valu "
