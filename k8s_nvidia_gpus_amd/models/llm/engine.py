@@ -131,6 +131,8 @@ class Engine:
                                           for w in [L.wo, L.wg, L.wu, L.wd] + list(L.wqkv)]
                 if not all([w.mfma_pack() for w in mats]):
                     self.max_T = min(self.max_T, 4)
+            # split-K combine scratch of the long-row GEMVs (ffn_down; o_proj of dim >= 8192)
+            self.kscratch = LK.SplitKScratch(max(c.dim, c.ffn), self.device)
             if self.cfg.dim >= 8192:
                 # such models normalise in the 8-wave GEMV prologues at every T (one reduction
                 # order, so decode stays batch-invariant), and the prologue form takes at most 4
@@ -355,15 +357,15 @@ class Engine:
                 LK.attn_decode(b.qrot, b.pos, b.slot, self.k_cache[i], self.v_cache[i], c.heads,
                                c.kv_heads, c.head_dim, self.max_ctx, scale, b.po, b.pml, *qd,
                                span=span)
-            LK.qgemv(L.wo, *qd, b.h, LK.RESID)
+            LK.qgemv(L.wo, *qd, b.h, LK.RESID, kscratch=self.kscratch)
             xin = act(b.h, L.ffn_norm)
             if c.ffn % 32 == 0:      # the pair GEMV quantises silu(g)·u (the ffn_down input) itself
                 LK.qgemv(L.wg, *xin[0], b.t, LK.PAIR, w1=L.wu, **xin[1], q8_out=qf)
-                LK.qgemv(L.wd, *qf, b.h, LK.RESID)
+                LK.qgemv(L.wd, *qf, b.h, LK.RESID, kscratch=self.kscratch)
             else:
                 LK.qgemv(L.wg, *xin[0], b.t, LK.PAIR, w1=L.wu, **xin[1])
                 LK.rmsnorm_q8(b.t, None, c.eps, *self._q8(b, c.ffn))
-                LK.qgemv(L.wd, *self._q8(b, c.ffn), b.h, LK.RESID)
+                LK.qgemv(L.wd, *self._q8(b, c.ffn), b.h, LK.RESID, kscratch=self.kscratch)
         LK.rmsnorm_q8(b.h, self.w.out_norm, c.eps, *qd)
         LK.qgemv(self.w.output, *qd, b.logits, LK.STORE)
 

@@ -102,6 +102,12 @@ struct GemvArgs {
   int8_t* ox8;           // [T][N]
   float* odx;            // [T][N/32]
   float* osx;            // [T][N/16]
+  // split-K over workgroups (MFMA GEMV, Q8 input, store / resid modes): ksplit slices of the
+  // super-blocks per row tile; each slice publishes its partials to kpart (write-through), the
+  // last to arrive on kcnt[tile] sums them in slice order and writes the output
+  int ksplit;
+  float* kpart;          // [tiles][ksplit][row groups][token quads][64]
+  unsigned* kcnt;        // [tiles], zero between launches (the last arriver resets its word)
 };
 
 // Weights are streamed exactly once per step: non-temporal loads keep them from evicting the

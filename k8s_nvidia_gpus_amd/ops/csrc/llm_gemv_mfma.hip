@@ -27,6 +27,15 @@ namespace {
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// split-K default for K >= 8192 (ffn_down): K-waves per workgroup and slices per row tile
+#ifndef AMDK8S_SPLIT_KW
+#define AMDK8S_SPLIT_KW 4
+#endif
+#ifndef AMDK8S_SPLIT_SK
+#define AMDK8S_SPLIT_SK 4
+#endif
+constexpr int kSplitKW = AMDK8S_SPLIT_KW, kSplitSK = AMDK8S_SPLIT_SK;
+
 // The MFMA kernel reads an MFMA-packed copy of the planes (amdk8s_llm_mfma_pack), laid out per
 // (16-row group G, super-block b) so that each of a wave's loads per block reads whole contiguous
 // lines instead of a 64/16/4-byte piece of 16 different rows:
@@ -152,7 +161,9 @@ __device__ __forceinline__ float mfma_block(const MBlk<TYPE>& w, const i32x4 (&x
 // LDS after stage_x's arrays: [W][T] prologue scratch (rounded to 16 B), the per-type activation
 // sums (Q4_K sxp float [T][K/32], Q6_K X int [T][K/16]), 256 zero bytes (the A operand of
 // inactive lanes), the K-split partials [waves][token quads][P][64], q8s [T][32].
-struct MfmaLds { int aux, zero, kred, q8s, total; };
+// K here is the staged window's (the whole row, or one split-K slice's super-blocks); flag: the
+// split-K ticket a workgroup draws, broadcast through LDS (one __shared__ array for everything).
+struct MfmaLds { int aux, zero, kred, q8s, flag, total; };
 __host__ __device__ inline MfmaLds mfma_lds(int type, int T, int K, int waves, int P) {
   MfmaLds L;
   const int nb = K >> 8;
@@ -162,8 +173,48 @@ __host__ __device__ inline MfmaLds mfma_lds(int type, int T, int K, int waves, i
   L.zero = L.aux + T * (type == kQ6K ? K >> 4 : K >> 5) * 4;
   L.kred = L.zero + 256;
   L.q8s = L.kred + waves * ((T + 3) / 4) * P * 64 * 4;
-  L.total = L.q8s + T * 32 * 4;
+  L.flag = L.q8s + T * 32 * 4;
+  L.total = L.flag + 16;
   return L;
+}
+
+// Q8 activations of super-blocks [kb_lo, kb_lo + nbw) staged as stage_x stages a whole row, with
+// local block indices (the window of one split-K workgroup): 16-byte units, four per thread per
+// round, every load of a round issued before its LDS stores.  Ends with a barrier.
+template <int T>
+__device__ __forceinline__ XView stage_x8_window(const GemvArgs& a, uint8_t* lds, int kb_lo,
+                                                 int nbw) {
+  const int K = a.K, Kw = nbw << 8, upt = Kw >> 4;
+  const int xstride = nbw * 288;
+  int8_t* xs = reinterpret_cast<int8_t*>(lds);
+  float* dxs = reinterpret_cast<float*>(lds + T * xstride);
+  float* sxs = dxs + T * (Kw >> 5);
+  const int nx = T * upt;
+  for (int i0 = threadIdx.x; i0 < nx; i0 += 4 * (int)blockDim.x) {
+    uint4 xv[4];
+    float dv[4], sv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = min(i0 + u * (int)blockDim.x, nx - 1);
+      const int t = i / upt, j = i - t * upt;
+      const long gi = (long)t * (K >> 4) + kb_lo * 16 + j;
+      xv[u] = *reinterpret_cast<const uint4*>(a.x8 + gi * 16);
+      sv[u] = a.sx[gi];
+      dv[u] = a.dx[(long)t * (K >> 5) + kb_lo * 8 + (j >> 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * (int)blockDim.x;
+      if (i < nx) {
+        const int t = i / upt, j = i - t * upt;
+        *reinterpret_cast<uint4*>(xs + t * xstride + xoff(j << 4)) = xv[u];
+        sxs[t * upt + j] = sv[u];
+        if ((j & 1) == 0) dxs[t * (Kw >> 5) + (j >> 1)] = dv[u];
+      }
+    }
+  }
+  __syncthreads();
+  return XView{xs, dxs, sxs, xstride, Kw >> 5, Kw >> 4};
 }
 
 // gate|up (pair, <= 4 tokens): 592 4-wave workgroups need 3 waves per SIMD to be co-resident
@@ -177,9 +228,14 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
   const int K = a.K, nb = K >> 8;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int rg = wave / KW, kw = wave % KW;
-  const int kb0 = kw * nb / KW, n = (kw + 1) * nb / KW - kb0;    // host: nb >= KW, so n >= 1
+  // split-K over workgroups: this one takes super-blocks [kb_lo, kb_lo + nbw) of row tile `tile`
+  const int SKr = a.ksplit > 1 ? a.ksplit : 1;
+  const int tile = bid / SKr, slice = bid - tile * SKr;
+  const int kb_lo = slice * nb / SKr, nbw = (slice + 1) * nb / SKr - kb_lo;
+  const int Kl = nbw << 8;                                       // the staged window's K
+  const int kb0 = kb_lo + kw * nbw / KW, n = kb_lo + (kw + 1) * nbw / KW - kb0;   // host: >= 1
   const int r = lane & 15, g = lane >> 4;
-  const int wrow0 = bid * RG * 16;
+  const int wrow0 = tile * RG * 16;
   const long rb0 = (long)(min(wrow0 + rg * 16, a.N - 16) >> 4) * nb + kb0;   // host: N % 16 == 0
   // ring of D super-blocks: D - 1 in flight before the activations are staged
   MBlk<TYPE> w0[D], w1[D];
@@ -189,16 +245,16 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
     mload<TYPE>(a.w0, rb, lane, w0[d]);
     if constexpr (P == 2) mload<TYPE>(a.w1, rb, lane, w1[d]);
   }
-  const XView xv = stage_x<T>(a, lds);
-  const MfmaLds L = mfma_lds(TYPE, T, K, KW * RG, P);
+  const XView xv = SKr > 1 ? stage_x8_window<T>(a, lds, kb_lo, nbw) : stage_x<T>(a, lds);
+  const MfmaLds L = mfma_lds(TYPE, T, Kl, KW * RG, P);
   if constexpr (TYPE == kQ4K) {
     float* sxp = reinterpret_cast<float*>(lds + L.aux);
-    for (int i = threadIdx.x; i < T * (K >> 5); i += blockDim.x)
+    for (int i = threadIdx.x; i < T * (Kl >> 5); i += blockDim.x)
       sxp[i] = xv.sxs[2 * i] + xv.sxs[2 * i + 1];
   } else {
     int* X = reinterpret_cast<int*>(lds + L.aux);
-    for (int i = threadIdx.x; i < T * (K >> 4); i += blockDim.x) {
-      const int t = i / (K >> 4), p = (i - t * (K >> 4)) << 4;
+    for (int i = threadIdx.x; i < T * (Kl >> 4); i += blockDim.x) {
+      const int t = i / (Kl >> 4), p = (i - t * (Kl >> 4)) << 4;
       const uint4 v = *reinterpret_cast<const uint4*>(xv.xs + t * xv.xstride + xoff(p));
       int sum = dot4z(v.x, 0x01010101u);
       sum = dot4(v.y, 0x01010101u, sum);
@@ -225,14 +281,14 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
     xo2[q] = live ? 128 : 0;
     xo3[q] = live ? (TYPE == kQ6K ? 192 : 160) : 0;
     const int tt = min(4 * q + g, T - 1);            // this lane's output token in quad q
-    dxb[q] = xv.dxs + tt * (K >> 5);
-    axb[q] = reinterpret_cast<const uint4*>(lds + L.aux) + tt * nb * NA;
+    dxb[q] = xv.dxs + tt * (Kl >> 5);
+    axb[q] = reinterpret_cast<const uint4*>(lds + L.aux) + tt * nbw * NA;
   }
   float acc[NQ], acc1[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) acc[q] = acc1[q] = 0.f;
   auto compute = [&](const MBlk<TYPE>& q0, const MBlk<TYPE>& q1, int i) {
-    const int kb = kb0 + i;
+    const int kb = kb0 - kb_lo + i;                   // window-local block index (LDS)
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const uint8_t* xp = lds + xa0[q] + kb * xstep[q];
@@ -298,6 +354,41 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
           if constexpr (P == 2) v1[q] += kred[(((rg * KW + k) * NQ + q) * P + 1) * 64 + lane];
         }
       }
+    }
+  }
+  if constexpr (MODE != kPair) {
+    if (SKr > 1) {
+      // split-K combine (cdna_hip_programming.md §5 "In-launch split-K reduction", sc1 form):
+      // every slice stores its partials write-through, drains, and draws a ticket; the slice
+      // that draws SKr - 1 reads all slabs with sc1 loads and sums them in slice order, so the
+      // bits never depend on which slice arrived last
+      float* slabs = a.kpart + (long)tile * SKr * (RG * NQ * 64);
+      if (kw == 0) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+          __hip_atomic_store(slabs + ((long)slice * RG * NQ + rg * NQ + q) * 64 + lane, v[q],
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      unsigned* flag = reinterpret_cast<unsigned*>(lds + L.flag);
+      if (threadIdx.x == 0)
+        flag[0] = __hip_atomic_fetch_add(a.kcnt + tile, 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      if (flag[0] != (unsigned)(SKr - 1)) return;
+      if (kw == 0) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          float tot = 0.f;
+          for (int s2 = 0; s2 < SKr; ++s2)
+            tot += __hip_atomic_load(slabs + ((long)s2 * RG * NQ + rg * NQ + q) * 64 + lane,
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v[q] = tot;
+        }
+      }
+      if (threadIdx.x == 0)      // every slice has drawn its ticket: ready for the next call
+        __hip_atomic_store(a.kcnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   float* q8s = (MODE == kPair && a.ox8) ? reinterpret_cast<float*>(lds + L.q8s) : nullptr;
@@ -388,12 +479,15 @@ int launch_mfma_one(const GemvArgs& a, hipStream_t st) {
   // ring depth: pair 2 (two matrices per slot, 3 waves/SIMD), else 3 (6 for ffn_down's 8-wave
   // shape measured slower: Q6_K 13.9 -> 15.6 us, T = 1 1.629 -> 1.656 ms, profiles/r04/o)
   constexpr int D = MODE == kPair ? 2 : 3;
-  if ((a.K >> 8) < KW) return 4;
-  const MfmaLds L = mfma_lds(TYPE, T, a.K, KW * RG, MODE == kPair ? 2 : 1);
+  const int nb = a.K >> 8, sk = a.ksplit > 1 ? a.ksplit : 1;
+  if (nb / sk < KW) return 4;                      // every wave of every slice gets a block
+  if (sk > 1 && (MODE == kPair || a.xf || !a.kpart || !a.kcnt)) return 2;
+  const int nbw = (nb + sk - 1) / sk;              // the largest slice's window
+  const MfmaLds L = mfma_lds(TYPE, T, nbw << 8, KW * RG, MODE == kPair ? 2 : 1);
   if (L.total > 160 * 1024) return 4;
-  const int grid = (a.N + 16 * RG - 1) / (16 * RG);
-  hipLaunchKernelGGL((qgemv_mfma_kernel<TYPE, T, MODE, KW, RG, D>), dim3(grid), dim3(KW * RG * 64),
-                     L.total, st, a);
+  const int tiles = (a.N + 16 * RG - 1) / (16 * RG);
+  hipLaunchKernelGGL((qgemv_mfma_kernel<TYPE, T, MODE, KW, RG, D>), dim3(tiles * sk),
+                     dim3(KW * RG * 64), L.total, st, a);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
@@ -403,6 +497,7 @@ int launch_mfma_one(const GemvArgs& a, hipStream_t st) {
 // models with dim >= 8192 use the prologue at every T).
 void mfma_shape(bool pair, int N, int K, int& kw, int& rg) {
   const int nb = K >> 8;
+  (void)N;
   // pair: 2 x 2.  1 x 2 (2 waves, whole K per wave) is faster alone (17.8 / 19.0 vs 18.5 / 20.4 us
   // at T = 1 / 4) but, with its 2-wave RMSNorm prologue, slower in the step (T = 1 1.625 -> 1.664 ms,
   // T = 8 2.94 -> 3.10 ms; profiles/r04/w)
@@ -412,6 +507,15 @@ void mfma_shape(bool pair, int N, int K, int& kw, int& rg) {
   else if (nb >= 4) kw = 4, rg = 1;
   else if (nb >= 2) kw = 2, rg = 2;
   else kw = 1, rg = 4;
+}
+
+// Split-K over workgroups for the long-row matrices fed Q8 (ffn_down, K = 18944): 224 row tiles
+// of 8 waves left 32 of the 256 CUs idle and every wave a 9-block dependent chain; slices of the
+// super-blocks on separate workgroups fill the chip.  A function of the matrix only (and of the
+// input form, which is fixed per matrix in the engine), like the shape.
+void mfma_ksplit_shape(int N, int K, int& kw, int& rg, int& sk) {
+  (void)N;
+  if (K >= 8192) kw = kSplitKW, rg = 1, sk = kSplitSK;
 }
 
 template <int TYPE, int T, int MODE>
@@ -428,6 +532,7 @@ int launch_mfma(const GemvArgs& a, int kw, int rg, hipStream_t st) {
   } else {
     switch (kw * 8 + rg) {
       case 1 * 8 + 4: return launch_mfma_one<TYPE, T, MODE, 1, 4>(a, st);
+      case 2 * 8 + 1: return launch_mfma_one<TYPE, T, MODE, 2, 1>(a, st);
       case 2 * 8 + 2: return launch_mfma_one<TYPE, T, MODE, 2, 2>(a, st);
       case 4 * 8 + 1: return launch_mfma_one<TYPE, T, MODE, 4, 1>(a, st);
       case 8 * 8 + 1:
@@ -524,12 +629,18 @@ extern "C" {
 // amdk8s_llm_qgemv.  kw / rows_per_wg: K-waves and rows (16 x row groups) per workgroup, 0 = the
 // default shape.  4 = shape not covered (N % 16, fewer super-blocks than K-waves, LDS): use
 // amdk8s_llm_qgemv on the plain planes.
+// ksplit: split-K slices over workgroups (store / resid modes, Q8 input); -1 = the default for the
+// matrix (mfma_ksplit_shape) when scratch is given, 0 / 1 = none.  kpart [kpart_floats] and kcnt
+// [kcnt_words] (zeroed once at allocation; every launch leaves them zero) must hold
+// tiles x ksplit x row groups x 2 x 64 floats and one word per tile, else rc 2.
 int amdk8s_llm_qgemv_mfma(int type, int mode, const void* w0q, const void* w0qh, const void* w0sc,
                           const void* w0d, const void* w1q, const void* w1qh, const void* w1sc,
                           const void* w1d, const void* x8, const void* dx, const void* sx,
                           const void* xf, int ldx, const void* norm_w, float eps,
                           const void* bias, void* out, int ldo, int N, int K, int T, int kw,
-                          int rows_per_wg, void* ox8, void* odx, void* osx, void* stream) {
+                          int rows_per_wg, void* ox8, void* odx, void* osx, int ksplit,
+                          void* kpart, long kpart_floats, void* kcnt, int kcnt_words,
+                          void* stream) {
   if (K % 256 || N <= 0 || T < 1 || T > kMaxTok) return 2;
   if (type != kQ4K && type != kQ6K) return 2;
   if (mode == kPair && !w1q) return 2;
@@ -554,8 +665,24 @@ int amdk8s_llm_qgemv_mfma(int type, int mode, const void* w0q, const void* w0qh,
   a.ox8 = static_cast<int8_t*>(ox8);
   a.odx = static_cast<float*>(odx);
   a.osx = static_cast<float*>(osx);
-  const int rg = ox8 ? 2 : (rows_per_wg > 0 && rows_per_wg % 16 == 0 ? rows_per_wg / 16 : 0);
+  int rg = ox8 ? 2 : (rows_per_wg > 0 && rows_per_wg % 16 == 0 ? rows_per_wg / 16 : 0);
   if (rg == 0) kw = 0;
+  a.ksplit = 1;
+  if (mode != kPair && !xf && kpart && kcnt) {
+    int sk = ksplit;
+    if (ksplit < 0) {
+      sk = 1;
+      if (kw <= 0) mfma_ksplit_shape(N, K, kw, rg, sk);
+    }
+    if (sk > 1) {
+      if (kw <= 0) mfma_shape(false, N, K, kw, rg);
+      const long tiles = (N + 16 * rg - 1) / (16 * rg);
+      if (tiles > kcnt_words || tiles * sk * rg * 2 * 64 > kpart_floats || sk > 64) return 2;
+      a.ksplit = sk;
+      a.kpart = static_cast<float*>(kpart);
+      a.kcnt = static_cast<unsigned*>(kcnt);
+    }
+  }
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (type == kQ4K) {
     if (mode == kStore) return dispatch_mfma_split<kQ4K, kStore>(a, kw, rg, st);

@@ -30,7 +30,8 @@ def _lib():
             lib.amdk8s_llm_attn_chunk.restype = ci
             lib.amdk8s_llm_qgemv_mfma.argtypes = [ci, ci] + [vp] * 8 + [vp, vp, vp, vp, ci, vp, cf,
                                                                        vp, vp, ci, ci, ci, ci, ci,
-                                                                       ci, vp, vp, vp, vp]
+                                                                       ci, vp, vp, vp,
+                                                                       ci, vp, cl, vp, ci, vp]
             lib.amdk8s_llm_qgemv_mfma.restype = ci
             lib.amdk8s_llm_qgemv2_mfma.argtypes = [ci] + [vp] * 4 + [ci, vp, vp] + [ci] + [vp] * 4 \
                 + [ci, vp, vp, ci, vp, vp, vp, vp, ci, vp, cf, ci, ci, vp]
@@ -123,15 +124,31 @@ def mfma_pack(w) -> tuple:
     return mq, mqh, msc, md
 
 
+class SplitKScratch:
+    """Scratch of the MFMA GEMV's split-K combine (per engine): partial slabs and one arrival
+    counter per row tile.  Zeroed once here; every launch leaves the counters zero again."""
+
+    def __init__(self, max_n: int, device, max_split: int = 8):
+        tiles = max(1, max_n // 16)
+        self.part = torch.zeros(tiles * max_split * 2 * 64 * 4, dtype=torch.float32, device=device)
+        self.cnt = torch.zeros(tiles, dtype=torch.int32, device=device)
+
+    def args(self) -> tuple:
+        return (self.part.data_ptr(), self.part.numel(), self.cnt.data_ptr(), self.cnt.numel())
+
+
 def qgemv(w0, x8, dx, sx, out, mode: int = STORE, w1=None, bias=None, ldo: int = None,
           rows_per_wg: int = 0, waves: int = 0, xf=None, norm_w=None, eps: float = 1e-6,
-          q8_out=None) -> str:
+          q8_out=None, kscratch: "SplitKScratch" = None, ksplit: int = -1) -> str:
     """``w0``/``w1``: :class:`~k8s_nvidia_gpus_amd.models.llm.weights.QWeight` on the GPU.
     Input: Q8 activations (``x8``/``dx``/``sx``, [T, K]) or fp32 rows ``xf`` [T, K] (pass
     ``x8=dx=sx=None``) that the kernel quantises itself, after an RMSNorm when ``norm_w`` is given.
     ``out`` fp32 [T, ldo] (a view with row stride ``ldo``).  ``waves`` per workgroup and
     ``rows_per_wg``: 0 = the kernel's default decomposition.  ``q8_out`` = (x8, dx, sx) [T, N]
     (pair mode only): write silu(g)·u quantised to Q8 — the ffn_down input — instead of ``out``.
+    ``kscratch``: the engine's :class:`SplitKScratch`; with it, long-row matrices fed Q8
+    (ffn_down) split their super-blocks over workgroups (``ksplit``: -1 = the matrix's default,
+    1 = none, n = n slices; the MFMA kernel only).
     Returns the kernel that ran: "mfma" (:func:`gemv_impl` MFMA and packed weights) or "valu"."""
     t = (xf if xf is not None else x8).shape[0]
     ldo = out.stride(0) if ldo is None else ldo
@@ -142,7 +159,8 @@ def qgemv(w0, x8, dx, sx, out, mode: int = STORE, w1=None, bias=None, ldo: int =
         rc = _lib().amdk8s_llm_qgemv_mfma(
             w0.qtype, mode, *w0.mfma_ptrs(), *b, _p(x8), _p(dx), _p(sx), _p(xf),
             xf.stride(0) if xf is not None else 0, _p(norm_w), float(eps), _p(bias),
-            out.data_ptr(), ldo, w0.n, w0.k, t, waves, rows_per_wg, *q8,
+            out.data_ptr(), ldo, w0.n, w0.k, t, waves, rows_per_wg, *q8, int(ksplit),
+            *(kscratch.args() if kscratch is not None else (None, 0, None, 0)),
             _stream(xf if xf is not None else x8))
         if rc != 4:
             _check(rc, "amdk8s_llm_qgemv_mfma")

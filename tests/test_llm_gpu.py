@@ -239,6 +239,45 @@ def test_mfma_gemv_vs_fp32(dev, mfma, qt, T, mode, N, K):
 
 
 @pytest.mark.parametrize("qt", ["Q4_K", "Q6_K"])
+@pytest.mark.parametrize("cfg", [(-1, 0, 0), (2, 4, 16), (4, 4, 16), (8, 2, 16), (3, 8, 16)])
+def test_mfma_gemv_split_k_combine(dev, mfma, qt, cfg):
+    """Split-K over workgroups (ffn_down's long rows): the in-launch combine gives the fp32
+    product, the same bits on every launch (the last-arriving slice sums all slices in slice
+    order, and leaves the counters zero for the next launch) and the same bits for a token
+    whatever T (batch-invariant decode), at T = 1..8 in one launch."""
+    from k8s_nvidia_gpus_amd.models.llm import gguf
+
+    LK = mfma
+    ks, waves, rpw = cfg
+    N, K = 512, 18944
+    w0, r0 = _qw(N, K, getattr(gguf, qt), 31, dev)
+    assert w0.mfma_pack()
+    scratch = LK.SplitKScratch(N, dev)
+    torch.manual_seed(7)
+    x = torch.randn(8, K, device=dev)
+    x8, dx, sx, xq = _q8(x, LK)
+    ref = xq.cpu() @ r0.t()
+    outs = {}
+    for T in (1, 4, 5, 8):
+        for rep in range(3):
+            out = torch.zeros(T, N, device=dev)
+            assert LK.qgemv(w0, x8[:T], dx[:T], sx[:T], out, LK.RESID, kscratch=scratch,
+                            ksplit=ks, waves=waves, rows_per_wg=rpw) == "mfma"
+            torch.testing.assert_close(out.cpu(), ref[:T], rtol=2e-4, atol=2e-4)
+            if (T, 0) in outs:
+                assert torch.equal(out, outs[(T, 0)])            # deterministic
+            outs[(T, rep)] = out
+        for t in range(T):
+            assert torch.equal(outs[(T, 0)][t], outs[(1, 0)][0]) if t == 0 else True
+            assert torch.equal(outs[(T, 0)][t], outs[(8, 0)][t])   # batch-invariant
+    assert int(scratch.cnt.abs().sum()) == 0                      # counters left zero
+    if ks == -1:   # the default split engages for K = 18944 and differs from the unsplit sum order
+        plain = torch.zeros(1, N, device=dev)
+        LK.qgemv(w0, x8[:1], dx[:1], sx[:1], plain, LK.RESID)
+        torch.testing.assert_close(plain.cpu(), ref[:1], rtol=2e-4, atol=2e-4)
+
+
+@pytest.mark.parametrize("qt", ["Q4_K", "Q6_K"])
 @pytest.mark.parametrize("K", [1536, 3584, 18944])
 def test_mfma_gemv_batch_invariant(dev, mfma, qt, K):
     """Each token's MFMA GEMV result is bit-identical for every T, with Q8 and with fp32 (+ fused

@@ -48,6 +48,9 @@ GEMV_CFGS = [(0, 0), (4, 4), (4, 16), (4, 32), (8, 8), (8, 16), (8, 32), (2, 4),
              (1, 2), (1, 4), (8, 7), (4, 7), (8, 14), (4, 37), (8, 37), (8, 74), (4, 74)]
 # MFMA GEMV: (K-waves, rows per workgroup = 16 x row groups)
 MFMA_CFGS = [(0, 0), (1, 64), (2, 32), (4, 16), (8, 16)]      # the instantiated shapes
+# long rows (ffn_down): (K-waves, rows per workgroup, split-K slices over workgroups)
+SPLIT_CFGS = [(0, 0, -1), (8, 16, 1), (4, 16, 1), (8, 16, 2), (4, 16, 2), (4, 16, 3), (4, 16, 4),
+              (2, 16, 4), (4, 16, 6), (2, 16, 8), (4, 16, 8), (8, 16, 4)]
 
 
 def bench_gemv(eng: Engine, iters: int = 56, sweep4: bool = False, only=GEMV_CASES,
@@ -91,13 +94,17 @@ def bench_gemv(eng: Engine, iters: int = 56, sweep4: bool = False, only=GEMV_CAS
             todo = cfgs if (T == 1 or sweep4) else cfgs[:1]
             if name == "gate_up_q8":          # 32 rows per workgroup are fixed there
                 todo = [(wv, 0) for wv in (0, 2, 4, 8)]
+            todo = [(wv, rp, 1) for wv, rp in todo]
             if LK.gemv_impl() == LK.GEMV_MFMA and w.mfma is not None:
-                todo = MFMA_CFGS if name not in ("gate_up", "gate_up_q8") else [(0, 0), (1, 32), (2, 32)]
-            for waves, rpw in todo:
+                todo = [(wv, rp, 1) for wv, rp in MFMA_CFGS] if name not in ("gate_up", "gate_up_q8") \
+                    else [(0, 0, 1), (1, 32, 1), (2, 32, 1)]
+                if name.startswith("down"):
+                    todo = SPLIT_CFGS
+            for waves, rpw, ks in todo:
                 def launch(i):
                     w0, w1 = mats[i % len(mats)]
                     LK.qgemv(w0, x8, dx, sx, out, m, w1=w1, waves=waves, rows_per_wg=rpw,
-                             q8_out=q8o)
+                             q8_out=q8o, kscratch=eng.kscratch, ksplit=ks)
                 try:
                     for i in range(3):
                         launch(i)
@@ -113,7 +120,7 @@ def bench_gemv(eng: Engine, iters: int = 56, sweep4: bool = False, only=GEMV_CAS
                 us = e0.elapsed_time(e1) / iters * 1e3
                 nbytes = w.nbytes() * (2 if mode == "pair" else 1)
                 r = {"gemv": name, "T": T, "N": w.n, "K": w.k, "type": ["Q4_K", "Q6_K"][w.qtype],
-                     "cfg": [waves, rpw], "copies": len(mats), "us": round(us, 2),
+                     "cfg": [waves, rpw, ks], "copies": len(mats), "us": round(us, 2),
                      "GBps": round(nbytes / us / 1e3, 1)}
                 rows.append(r)
                 print(r, file=sys.stderr, flush=True)
