@@ -97,7 +97,8 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
                                 uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
                                 int ldc, int order, int nt_store,
                                 const uint16_t* __restrict__ bias = nullptr,
-                                W4aResid resid = W4aResid{}) {
+                                W4aResid resid = W4aResid{}, int ksplit = 1,
+                                long slice_stride = 0) {
   constexpr bool H = SCHED == kF16;
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
 
@@ -111,7 +112,10 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
   const int tiles_m = (M + BM - 1) / BM;
   const int tiles_n = N / BN;
   const int nwg = tiles_m * tiles_n;
-  const int bid = blockIdx.x;
+  // split-K (the partial last wave of amdk8s_gemm_w4a_hybrid): ksplit adjacent workgroups share
+  // one tile, each a contiguous range of its K-tiles, writing a 16-bit partial tile to its slice
+  const int ks = ksplit > 1 ? ksplit : 1;
+  const int bid = blockIdx.x / ks, slice = blockIdx.x - bid * ks;
   int m0, n0;
   {
     int tm, tn;
@@ -119,6 +123,7 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
     m0 = tm * BM;
     n0 = tn * BN;
   }
+  if (ks > 1) C += slice * slice_stride;
 
   // ---- operands of the generated body (register map in tools/gen_gemm_w4a_kloop.py) ----
   const uint32_t lda_b = (uint32_t)lda * 2, ldb_b = (uint32_t)ldb * 2;
@@ -137,13 +142,15 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
   const uint32_t rb1 = lds0 + (2 + wc) * HALF_BYTES + fo1;
   const uint32_t cbase = lds0 + (wr * 128 + frow) * C_STRIDE + (wc * 128 + fq * 4) * 2;
   const uint32_t dma_lds = lds0 + wave * 1024;
-  const uint64_t a_addr = (uint64_t)(uintptr_t)A + (uint64_t)m0 * lda_b;
-  const uint64_t b_addr = (uint64_t)(uintptr_t)B + (uint64_t)n0 * ldb_b;
+  const int t_all = K / BK;
+  const int t_lo = slice * t_all / ks;
+  const uint64_t a_addr = (uint64_t)(uintptr_t)A + (uint64_t)m0 * lda_b + (uint64_t)t_lo * BK * 2;
+  const uint64_t b_addr = (uint64_t)(uintptr_t)B + (uint64_t)n0 * ldb_b + (uint64_t)t_lo * BK * 2;
   const uint32_t a_lo = (uint32_t)a_addr, a_hi = (uint32_t)(a_addr >> 32);
   const uint32_t b_lo = (uint32_t)b_addr, b_hi = (uint32_t)(b_addr >> 32);
   // the last row panel's descriptor ends at row M: the DMA reads zeros past it (M tail)
   const uint32_t nrec_a = (uint32_t)min(BM, M - m0) * lda_b, nrec_b = 256u * ldb_b;
-  const int T = K / BK;
+  const int T = (slice + 1) * t_all / ks - t_lo;
 
 #define AMDK8S_W4A_OPERANDS                                                                \
   : "s"(T), "s"(a_lo), "s"(a_hi), "s"(nrec_a), "s"(b_lo), "s"(b_hi), "s"(nrec_b), "s"(lda_b),  \
@@ -250,16 +257,16 @@ int launch_w4a(const void* A, const void* B, void* C, int M, int N, int K, int l
   uint16_t* c = (uint16_t*)C;
   if (sched == kF16)
     hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4a<kF16>, dim3(nwg), dim3(NT), 0, stream, a, b,
-                       c, M, N, K, lda, ldb, ldc, sb, nt);
+                       c, M, N, K, lda, ldb, ldc, sb, nt, nullptr, W4aResid{}, 1, 0L);
   else if (sched == 1)
     hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4a<1>, dim3(nwg), dim3(NT), 0, stream, a, b, c,
-                       M, N, K, lda, ldb, ldc, sb, nt);
+                       M, N, K, lda, ldb, ldc, sb, nt, nullptr, W4aResid{}, 1, 0L);
   else if (sched == 2)
     hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4a<2>, dim3(nwg), dim3(NT), 0, stream, a, b, c,
-                       M, N, K, lda, ldb, ldc, sb, nt);
+                       M, N, K, lda, ldb, ldc, sb, nt, nullptr, W4aResid{}, 1, 0L);
   else
     hipLaunchKernelGGL(amdk8s_gemm_bf16_nt_256x256_w4a<0>, dim3(nwg), dim3(NT), 0, stream, a, b, c,
-                       M, N, K, lda, ldb, ldc, sb, nt);
+                       M, N, K, lda, ldb, ldc, sb, nt, nullptr, W4aResid{}, 1, 0L);
   return (int)hipGetLastError();
 }
 }  // namespace
@@ -294,7 +301,7 @@ extern "C" int amdk8s_gemm_w4a_epi(int epi, int dtype, const void* A, const void
   const W4aResid r{x, gate, ldx, rows_per_gate > 0 ? rows_per_gate : M, gate_stride};
   auto launch = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(tm * tn), dim3(NT), 0, stream, a, b, c, M, N, K, lda, ldb, ldc,
-                       sb, 0, bs, r);
+                       sb, 0, bs, r, 1, 0L);
   };
   constexpr int S = AMDK8S_W4A_DEFAULT_SCHEDULE;
   if (dtype == 0) {
@@ -320,4 +327,106 @@ extern "C" int amdk8s_gemm_bf16_nt_w4a(const void* A, const void* B, void* C, in
 extern "C" int amdk8s_gemm_f16_nt_w4a(const void* A, const void* B, void* C, int M, int N, int K,
                                       int lda, int ldb, int ldc, hipStream_t stream) {
   return launch_w4a(A, B, C, M, N, K, lda, ldb, ldc, stream, true);
+}
+
+// ---------------------------------------------------------------- partial last wave (hybrid)
+// A grid of 256×256 tiles that fills the chip 1 < waves < 2 times (the LLM's gate|up prefill
+// GEMM at 512 tokens: 2 × 148 = 296 tiles on 256 CUs, one workgroup per CU) runs its second round
+// with 40 of 256 CUs busy.  The hybrid runs whole waves of tiles as usual (the first na columns),
+// and the remaining columns' tiles split over K across the idle CUs: ksplit workgroups per tile
+// write 16-bit partial tiles to a workspace, and a finalize pass sums them in fp32 (+ bias).
+
+template <bool H>
+__global__ void __launch_bounds__(256)
+w4a_splitk_finalize(const uint16_t* __restrict__ ws, int S, long slice_stride, int M, int Nb,
+                    uint16_t* __restrict__ C, int ldc, const uint16_t* __restrict__ bias) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;   // one 8-column group
+  const int groups = Nb >> 3;
+  if (i >= (long)M * groups) return;
+  const int m = (int)(i / groups), c = (int)(i - (long)m * groups) * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < S; ++s) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(ws + s * slice_stride + (long)m * Nb + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc[2 * e] += w4a_lo<H>(v[e]);
+      acc[2 * e + 1] += w4a_hi<H>(v[e]);
+    }
+  }
+  u32x4 o;
+  if (bias) {
+    const u32x4 b = *reinterpret_cast<const u32x4*>(bias + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc[2 * e] += w4a_lo<H>(b[e]);
+      acc[2 * e + 1] += w4a_hi<H>(b[e]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = w4a_pack<H>(acc[2 * e], acc[2 * e + 1]);
+  *reinterpret_cast<u32x4*>(C + (long)m * ldc + c) = o;
+}
+
+// The hybrid's plan: na = columns run as whole waves (a multiple of 256, possibly 0 — then the
+// plain kernel is the better choice) and ks = K slices per tile of the rest; ks = 1: no hybrid.
+extern "C" void amdk8s_gemm_w4a_hybrid_plan(int M, int N, int K, int cus, int* na, int* ks) {
+  const int tm = (M + BM - 1) / BM, tn = N / BN, tiles = tm * tn, T = K / BK;
+  *na = N;
+  *ks = 1;
+  if (N % BN || cus <= 0 || tiles <= cus) return;
+  const int full = tiles / cus * cus;             // tiles of the whole waves
+  const int tn_a = full / tm;                     // whole columns inside them
+  const int rest = (tn - tn_a) * tm;
+  if (tn_a <= 0 || rest <= 0 || rest * 2 > cus) return;   // last wave at least half full: plain
+  int s = cus / rest;
+  s = s < T / 8 ? s : T / 8;                      // >= 8 K-tiles per slice (the ring's depth)
+  s = s < 16 ? s : 16;
+  if (s < 2) return;
+  *na = tn_a * BN;
+  *ks = s;
+}
+
+// C[M, N] = A·Bᵀ (+ bias) with the partial last wave split over K (see above); ws: ks × M × (N - na)
+// 16-bit elements (dtype as the operands).  epi 0 = plain, 1 = + bias.
+extern "C" int amdk8s_gemm_w4a_hybrid(int epi, int dtype, const void* A, const void* B, void* C,
+                                      const void* bias, int M, int N, int K, int lda, int ldb,
+                                      int ldc, int na, int ks, void* ws, long ws_elems,
+                                      hipStream_t stream) {
+  if (epi != kEpiNone && epi != kEpiBias) return (int)hipErrorInvalidValue;
+  if (M <= 0 || N % BN || K % BK || na % BN || na <= 0 || na >= N || ks < 2) return (int)hipErrorInvalidValue;
+  const int nb = N - na;
+  if ((long)ks * M * nb > ws_elems || !ws || ((uintptr_t)ws & 15)) return (int)hipErrorInvalidValue;
+  if (K / BK < ks) return (int)hipErrorInvalidValue;
+  int rc = amdk8s_gemm_w4a_epi(epi, dtype, A, B, C, bias, nullptr, nullptr, M, na, K, lda, ldb, ldc,
+                               0, 0, 0, stream);
+  if (rc) return rc;
+  if (lda % 8 || ldb % 8 || ldc % 8 || ((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15)
+    return (int)hipErrorInvalidValue;
+  const int tm = (M + BM - 1) / BM, tn = nb / BN;
+  const int sb = amdk8s::tile_order_arg(tm, tn);
+  const uint16_t* a = (const uint16_t*)A;
+  const uint16_t* b = (const uint16_t*)B + (size_t)na * ldb;
+  uint16_t* w = (uint16_t*)ws;
+  const long stride = (long)M * nb;
+  constexpr int S = AMDK8S_W4A_DEFAULT_SCHEDULE;
+  if (dtype == 0)
+    hipLaunchKernelGGL((amdk8s_gemm_bf16_nt_256x256_w4a<kF16, kEpiNone>), dim3(tm * tn * ks), dim3(NT),
+                       0, stream, a, b, w, M, nb, K, lda, ldb, nb, sb, 0, nullptr, W4aResid{}, ks,
+                       stride);
+  else
+    hipLaunchKernelGGL((amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiNone>), dim3(tm * tn * ks), dim3(NT),
+                       0, stream, a, b, w, M, nb, K, lda, ldb, nb, sb, 0, nullptr, W4aResid{}, ks,
+                       stride);
+  rc = (int)hipGetLastError();
+  if (rc) return rc;
+  const long groups = (long)M * (nb / 8);
+  const uint16_t* bs = epi == kEpiBias ? (const uint16_t*)bias + na : nullptr;
+  uint16_t* c = (uint16_t*)C + na;
+  if (dtype == 0)
+    hipLaunchKernelGGL(w4a_splitk_finalize<true>, dim3((unsigned)((groups + 255) / 256)), dim3(256),
+                       0, stream, w, ks, stride, M, nb, c, ldc, bs);
+  else
+    hipLaunchKernelGGL(w4a_splitk_finalize<false>, dim3((unsigned)((groups + 255) / 256)), dim3(256),
+                       0, stream, w, ks, stride, M, nb, c, ldc, bs);
+  return (int)hipGetLastError();
 }

@@ -45,6 +45,12 @@ def _lib():
             lib.amdk8s_gemm_w4a_epi.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci,
                                                 ci, ci, ci, vp]
             lib.amdk8s_gemm_w4a_epi.restype = ci
+            lib.amdk8s_gemm_w4a_hybrid_plan.argtypes = [ci, ci, ci, ci, ctypes.POINTER(ci),
+                                                         ctypes.POINTER(ci)]
+            lib.amdk8s_gemm_w4a_hybrid_plan.restype = None
+            lib.amdk8s_gemm_w4a_hybrid.argtypes = [ci, ci, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci,
+                                                   ci, ci, vp, ctypes.c_long, vp]
+            lib.amdk8s_gemm_w4a_hybrid.restype = ci
             lib.amdk8s_gemm_epi_set_tile.argtypes = [ci]
             lib.amdk8s_gemm_epi_set_tile.restype = None
             lib.amdk8s_gemm_epi_set_splits.argtypes = [ci]
@@ -163,6 +169,45 @@ def _w4a(epi: int, x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor],
         raise RuntimeError(f"amdk8s_gemm_w4a_epi failed (rc={rc}, M={m} N={n} K={k}, epi={epi})")
 
 
+# A 256×256 grid that fills the chip 1 < waves < 2 times runs its partial last wave split over K on
+# the otherwise idle CUs (amdk8s_gemm_w4a_hybrid); AMDK8S_GEMM_HYBRID=0 turns it off (A/B runs).
+_HYBRID = os.environ.get("AMDK8S_GEMM_HYBRID", "1") != "0"
+_CUS = {}
+
+
+def _cus(dev) -> int:
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    if i not in _CUS:
+        _CUS[i] = torch.cuda.get_device_properties(i).multi_processor_count
+    return _CUS[i]
+
+
+def hybrid_plan(m: int, n: int, k: int, cus: int = 256) -> tuple:
+    """(whole-wave columns na, K slices of the rest): ks == 1 means the plain w4a launch."""
+    na, ks = ctypes.c_int(), ctypes.c_int()
+    _lib().amdk8s_gemm_w4a_hybrid_plan(m, n, k, cus, ctypes.byref(na), ctypes.byref(ks))
+    return na.value, ks.value
+
+
+def _w4a_hybrid(epi: int, x2, w, b, out) -> bool:
+    """The hybrid for store / bias epilogues; False when its plan is the plain launch."""
+    if not _HYBRID or epi not in (0, 1):
+        return False
+    m, k = x2.shape
+    n = w.shape[0]
+    na, ks = hybrid_plan(m, n, k, _cus(x2.device))
+    if ks <= 1:
+        return False
+    ws = torch.empty(ks * m * (n - na), dtype=x2.dtype, device=x2.device)
+    rc = _lib().amdk8s_gemm_w4a_hybrid(
+        epi, _DT[x2.dtype], x2.data_ptr(), w.data_ptr(), out.data_ptr(),
+        b.data_ptr() if b is not None else None, m, n, k, x2.stride(0), w.stride(0),
+        out.stride(0), na, ks, ws.data_ptr(), ws.numel(), _stream(x2))
+    if rc != 0:
+        raise RuntimeError(f"amdk8s_gemm_w4a_hybrid failed (rc={rc}, M={m} N={n} K={k})")
+    return True
+
+
 def _aligned16(*ts) -> bool:
     return all(t is None or t.data_ptr() % 16 == 0 for t in ts)
 
@@ -177,7 +222,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
     if use_w4a(x2.shape[0], n, x2.shape[1], x.dtype) and _aligned16(x2, w, bb):
         if gelu and bb is None:
             bb = torch.zeros(n, dtype=x.dtype, device=x.device)
-        _w4a(2 if gelu else (0 if bb is None else 1), x2, w, bb, out)
+        epi = 2 if gelu else (0 if bb is None else 1)
+        if not _w4a_hybrid(epi, x2, w, bb, out):
+            _w4a(epi, x2, w, bb, out)
     else:
         _run(EPI_GELU if gelu else EPI_STORE, x2, w, bb, out, None, None, 0, 0, n, 0)
     return out.view(*x.shape[:-1], n)

@@ -247,3 +247,33 @@ def test_split_k_gated_residual(GE, gated):
     want = res + _ref(x, w, None).view(1, m, n) * (gate[:, None, :] if gated else 1.0)
     GE.linear_residual_(res, x, w, None, gate)
     torch.testing.assert_close(res, want, rtol=5e-3, atol=5e-3)
+
+
+@pytest.mark.parametrize("m,n,k", [(512, 37888, 3584), (300, 76800, 1024), (3584, 37888, 3584)])
+@pytest.mark.parametrize("bias", [True, False])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_w4a_partial_last_wave_split_over_k(GE, m, n, k, bias, dtype):
+    """a 256×256 grid filling the chip 1 < waves < 2 times (the LLM gate|up
+    prefill GEMM at 512 tokens: 296 tiles on 256 CUs) runs its whole waves plainly and its partial
+    last wave split over K on the idle CUs (16-bit partial tiles summed in fp32): the hybrid's
+    plan engages and the product equals the fp32 reference."""
+    dev = torch.device("cuda")
+    na, ks = GE.hybrid_plan(m, n, k, GE._cus(dev))
+    assert 0 < na < n and ks >= 2, (na, ks)
+    g = torch.Generator(device=dev).manual_seed(m + n)
+    x = torch.randn(m, k, generator=g, device=dev).to(dtype)
+    w = (torch.randn(n, k, generator=g, device=dev) / k ** 0.5).to(dtype)
+    b = torch.randn(n, generator=g, device=dev).to(dtype) if bias else None
+    y = GE.linear(x, w, b)
+    ref = _ref(x, w, b)
+    tol = 2e-2 if dtype == torch.bfloat16 else 5e-3
+    torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+    # the split columns agree with the plain kernel's to 16-bit rounding
+    prev = GE._HYBRID
+    GE._HYBRID = False
+    try:
+        plain = GE.linear(x, w, b)
+    finally:
+        GE._HYBRID = prev
+    torch.testing.assert_close(y[:, na:].float(), plain[:, na:].float(), rtol=tol, atol=tol)
+    assert torch.equal(y[:, :na], plain[:, :na])            # whole waves: the same kernel

@@ -15,6 +15,7 @@
 #   llm-ctx:<n>      tools/llm_bench.py decode T = 1,4,8 after an n-token prompt (long-context decode)
 #   bringup          operator bring-up rehearsal with the shipped ConfigMap config: gated + ungated
 #                    time-to-first-GPU-pod (python -m k8s_nvidia_gpus_amd.operator bringup)
+#   prefill-gemm[:M,..]  tools/llm_prefill_gemm_probe.py --quick (planner pick, w4a plain, hipBLASLt)
 #   attn-probe       tools/debug/prefill_attn_probe.py (chunked-prefill attention formulations)
 #   serve[:<args>]   tools/llm_serve_bench.py: the server under 1/4/8 streaming clients + a long-prompt
 #                    admission (args: comma-separated, '=' for spaces, e.g. serve:--clients=8,--gen=256)
@@ -120,6 +121,13 @@ PYEOF
         --workdir "$OUT/bringup_work" > "$OUT/bringup.log" 2>&1 || fail "$step" $? "$OUT/bringup.log"
       grep -v '^{' "$OUT/bringup.log" | tail -24; grep '^{' "$OUT/bringup.log" | tail -1 > "$OUT/bringup.json"
       python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('time_to_first_gpu_pod_s', d['time_to_first_gpu_pod_s'], 'time_to_validated_s', d['time_to_validated_s'])" "$OUT/bringup.json" ;;
+    prefill-gemm|prefill-gemm:*)
+      ms="512"; [[ "$step" == prefill-gemm:* ]] && ms="${step#prefill-gemm:}"
+      for m in ${ms//,/ }; do
+        timeout -k 10 300 python -u tools/llm_prefill_gemm_probe.py --m "$m" --quick \
+          --out "$OUT/prefill_gemm_$m.json" > "$OUT/prefill_gemm_$m.log" 2>&1 || fail "$step" $? "$OUT/prefill_gemm_$m.log"
+        grep "^{" "$OUT/prefill_gemm_$m.log" | cut -c1-220
+      done ;;
     attn-probe)
       timeout -k 10 300 python -u tools/debug/prefill_attn_probe.py > "$OUT/prefill_attn_probe.log" 2>&1 \
         || fail "$step" $? "$OUT/prefill_attn_probe.log"

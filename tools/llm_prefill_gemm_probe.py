@@ -35,6 +35,7 @@ def bench(fn, iters=30):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, default=512)
+    ap.add_argument("--quick", action="store_true", help="planner / w4a / torch only (no sweep)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -55,8 +56,15 @@ def main() -> int:
             rows.append(r)
             print(r, flush=True)
 
-        rec(f"auto plan={GE.plan(m, n, k)} w4a={GE.use_w4a(m, n, k, x.dtype)}", bench(run))
+        rec(f"auto plan={GE.plan(m, n, k)} w4a={GE.use_w4a(m, n, k, x.dtype)} "
+            f"hybrid={GE.hybrid_plan(m, n, k)}", bench(run))
+        if GE.use_w4a(m, n, k, x.dtype):
+            GE._HYBRID = False
+            rec("w4a plain (no partial-wave split)", bench(run))
+            GE._HYBRID = True
         rec("torch", bench(lambda: F.linear(x, w)))
+        if a.quick:
+            continue
         wide = GE._WIDE
         GE._WIDE = "epi"
         for tile in range(len(GE.TILES)):
