@@ -1069,6 +1069,14 @@ class Validator:
                         return self._deferred(step, sc, "every free GPU was allocated to a pod "
                                                         "while being reserved", reservation)
                 r = self._run_load_step(step)
+                if reservation is not None:
+                    # the residual window (docs/runbook.md): a pod admitted after the re-read but
+                    # before kubelet applied the Unhealthy update shows up here, after the fact
+                    after, err2 = self._allocated(sc.devices)
+                    late = {u: after[u] for u in sc.free_uids if after and u in after}
+                    if late:
+                        r.detail["allocated_during_step"] = late
+                        log.warning("%s: GPU(s) allocated to pods while under test: %s", step, late)
             finally:
                 if reservation is not None:
                     self.release()

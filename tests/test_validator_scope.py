@@ -195,7 +195,7 @@ def test_gpu_allocated_between_list_and_launch_is_left_untouched(tmp_path):
     with _RacingPodResources(sock, {}, late) as fake:
         v = Validator(cfg, str(tmp_path / "m"), bin_dir="/x", runner=r, root=str(root))
         g = v.run_step("gemm")
-    assert fake.calls == 2                                  # answer, reserve, re-read
+    assert fake.calls == 3                  # answer, reserve + re-read, after the step
     assert g.passed
     assert g.detail["reservation"]["taken_while_reserving"] == {uids[3]: "llm/coder-llm-0"}
     assert _narrowed(r.calls[0]) == ["0", "1", "2", "4", "5", "6", "7"]   # GPU 3 never loaded
@@ -523,3 +523,22 @@ def test_partition_started_during_the_reservation_defers_the_step(tmp_path):
         g = v.run_step("gemm")
     assert g.deferred and "partition change started" in g.reason and r.calls == []
     assert v.run_step("vectoradd").deferred
+
+
+def test_a_pod_admitted_during_the_step_is_recorded(tmp_path):
+    """The residual window: a pod kubelet admitted after the post-reservation re-read shows up in
+    the step result's allocated_during_step (PodResources is read once more after the load)."""
+    root = _node(tmp_path)
+    cfg, sock = _cfg(tmp_path, ", rccl: false, reserveAckSeconds: 0.1")
+    uids = _uids(root)
+    pods = {}
+
+    class R(Runner):
+        def __call__(self, argv, timeout):
+            pods[("late", "pod-0")] = [("amd.com/gpu", [uids[4]])]      # admitted mid-step
+            return super().__call__(argv, timeout)
+
+    with FakePodResources(sock, pods):
+        g = Validator(cfg, str(tmp_path / "m"), bin_dir="/x", root=str(root),
+                      runner=R({"amd-gemm-validator": (0, _gemm_log(8, 1500.0))})).run_step("gemm")
+    assert g.passed and g.detail["allocated_during_step"] == {uids[4]: "late/pod-0"}
