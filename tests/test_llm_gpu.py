@@ -267,9 +267,8 @@ def test_mfma_gemv_split_k_combine(dev, mfma, qt, cfg):
             if (T, 0) in outs:
                 assert torch.equal(out, outs[(T, 0)])            # deterministic
             outs[(T, rep)] = out
-        for t in range(T):
-            assert torch.equal(outs[(T, 0)][t], outs[(1, 0)][0]) if t == 0 else True
-            assert torch.equal(outs[(T, 0)][t], outs[(8, 0)][t])   # batch-invariant
+    for T in (1, 4, 5):                                           # batch-invariant
+        assert torch.equal(outs[(T, 0)], outs[(8, 0)][:T])
     assert int(scratch.cnt.abs().sum()) == 0                      # counters left zero
     if ks == -1:   # the default split engages for K = 18944 and differs from the unsplit sum order
         plain = torch.zeros(1, N, device=dev)
