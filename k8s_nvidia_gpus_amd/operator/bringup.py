@@ -102,7 +102,8 @@ def rehearse(cfg: OperatorConfig, bin_dir: str, workdir: Optional[str] = None, r
         gated = bool(cfg.section("validator").get("gateOnValidation", True))
 
     own_tmp = workdir is None
-    workdir = workdir or tempfile.mkdtemp(prefix="amdk8s-bringup-")
+    # absolute: gRPC unix-socket addresses (the kubelet stand-in, the plugin) must not be relative
+    workdir = os.path.abspath(workdir or tempfile.mkdtemp(prefix="amdk8s-bringup-"))
     markers = os.path.join(workdir, "run-amd-validations")
     host = os.path.join(workdir, "host")
     os.makedirs(markers, exist_ok=True)

@@ -27,12 +27,17 @@ namespace {
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// split-K default for K >= 8192 (ffn_down): K-waves per workgroup and slices per row tile
+// split-K default for K >= 8192 (ffn_down): K-waves per workgroup and slices per row tile.
+// Measured and left off (SK 1): at T = 1 every split lost to the unsplit 8-wave shape — Q4_K
+// ffn_down 10.8 us unsplit vs 12.1 (4 waves x 2 slices) .. 22.5 us (8 x 4), Q6_K 14.3 vs 15.8 ..
+// 27.7 us, and the whole step 1.62 -> 1.79 ms with 4 x 4 (profiles/r05/gemv_split_k.log): the
+// write-through partials, the ticket and the last slice's sc1 re-read cost more than the idle
+// CUs of the 224-tile grid.  The combine stays for A/B sweeps (ksplit > 1).
 #ifndef AMDK8S_SPLIT_KW
-#define AMDK8S_SPLIT_KW 4
+#define AMDK8S_SPLIT_KW 8
 #endif
 #ifndef AMDK8S_SPLIT_SK
-#define AMDK8S_SPLIT_SK 4
+#define AMDK8S_SPLIT_SK 1
 #endif
 constexpr int kSplitKW = AMDK8S_SPLIT_KW, kSplitSK = AMDK8S_SPLIT_SK;
 

@@ -150,8 +150,11 @@ _WIDE = os.environ.get("AMDK8S_GEMM_WIDE", "w4a")
 
 
 def use_w4a(m: int, n: int, k: int, dtype: torch.dtype) -> bool:
+    """256×256 tiles whenever they fill at least 3/4 of the chip: the LLM prefill's q|k|v and o_proj
+    at 3584 tokens (252 / 196 tiles) ran 136 / 137 us on the wave-grid family against hipBLASLt's
+    90 / 75 (profiles/r05/prefill_gemm_3584.log)."""
     return (_WIDE == "w4a" and dtype in _DT and n % 256 == 0 and k % 64 == 0
-            and ((m + 255) // 256) * (n // 256) >= 256)
+            and ((m + 255) // 256) * (n // 256) >= 192)
 
 
 def _w4a(epi: int, x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor],

@@ -98,3 +98,6 @@ def test_use_w4a_routing():
     assert not GE.use_w4a(5120, 1540, 1536, torch.bfloat16)    # N % 256
     assert not GE.use_w4a(5120, 4608, 1500, torch.bfloat16)    # K % 64
     assert not GE.use_w4a(512, 1536, 1536, torch.bfloat16)     # 2 x 6 tiles: far from filling
+    # 3/4 of a wave and up (LLM prefill q|k|v and o_proj at 3584 tokens: 252 / 196 tiles)
+    assert GE.use_w4a(3584, 4608, 3584, torch.float16) and GE.use_w4a(3584, 3584, 3584, torch.float16)
+    assert not GE.use_w4a(2560, 4608, 3584, torch.float16)     # 10 x 18 = 180 tiles
