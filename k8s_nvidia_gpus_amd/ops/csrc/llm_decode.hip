@@ -358,73 +358,102 @@ __global__ void __launch_bounds__(128) attn_combine_q8_kernel(const float* __res
                    x8, dx, sx);
 }
 
-// Two-pass merge for the same (head, token) with 128 threads: every chunk's (max, sum) and the first
-// kCombBatch partial rows are loaded together; the max and the denominator are workgroup
-// reductions (the chunk weights go to LDS); the partial rows are then summed with their weights.
-// No online rescaling, so the row loads never wait on maths: one memory round trip per kCombBatch
-// chunks, where the online merge above takes one per 8 (its cost grew from 4.9 to 8.6 us between
-// 512 and 3584 positions, profiles/r04/z2).  nsplit <= kCombMaxSplit.
+// Two-pass merge of the chunks of head h of token t, with 128·G threads (G row groups of 128 dims):
+// every chunk's (max, sum) loads at once (PER per thread, up to kCombMaxSplit chunks); the max and
+// the denominator are workgroup reductions (the chunk weights go to LDS); then each of ng row groups
+// sums a contiguous range of the partial rows with their weights, kCombBatch row loads in flight at
+// a time, and the group sums add up in group order.  ng = min(G, ceil(ns / kCombBatch)) depends only
+// on this token's own chunk count, and G only on the engine's max_ctx (the launcher), so a token's
+// bits never depend on the batch it runs in.  At 32k positions (512 chunks) the 128-
+// thread form took 16 dependent row batches per head (~1 ms per 28-layer step at T = 1,
+// profiles/r05); eight groups take two.
 constexpr int kCombBatch = 32;
-constexpr int kCombMaxSplit = 512;                  // max_ctx <= 32768 with 64-position chunks
+constexpr int kCombMaxSplit = 1024;                 // max_ctx <= 65536 with 64-position chunks
 
-__global__ void __launch_bounds__(128) attn_combine2_q8_kernel(const float* __restrict__ po,
-                                                               const float* __restrict__ pml,
-                                                               const int* __restrict__ pos, int H,
-                                                               int nsplit, int chunk,
-                                                               float* __restrict__ out,
-                                                               int8_t* __restrict__ x8,
-                                                               float* __restrict__ dx,
-                                                               float* __restrict__ sx) {
-  constexpr int kPer = kCombMaxSplit / 128;
+template <int G>
+__global__ void __launch_bounds__(128 * G) attn_combine2_q8_kernel(const float* __restrict__ po,
+                                                                   const float* __restrict__ pml,
+                                                                   const int* __restrict__ pos,
+                                                                   int H, int nsplit, int chunk,
+                                                                   float* __restrict__ out,
+                                                                   int8_t* __restrict__ x8,
+                                                                   float* __restrict__ dx,
+                                                                   float* __restrict__ sx) {
+  constexpr int NT = 128 * G, NW = NT / kWave, PER = kCombMaxSplit / NT;
   __shared__ float wts[kCombMaxSplit];
-  __shared__ float red[2][2];
-  const int h = blockIdx.x, t = blockIdx.y, dd = threadIdx.x, wave = dd >> 6;
+  __shared__ float red[2][NW];
+  __shared__ float part[G][kHeadDim];
+  const int h = blockIdx.x, t = blockIdx.y, tid = threadIdx.x, wave = tid >> 6;
+  const int dd = tid & (kHeadDim - 1), grp = tid >> 7;
   const int ns = min(nsplit, (pos[t] + chunk) / chunk);
   const long hb = ((long)t * H + h) * nsplit;
-  float ov[kCombBatch];                              // indices clamped: rows < ns are all written
+  const int ng = min(G, (ns + kCombBatch - 1) / kCombBatch);
+  const int gl = grp < ng ? grp * ns / ng : 0, gh = grp < ng ? (grp + 1) * ns / ng : 0;
+  // this group's first row batch, in flight with the (max, sum) loads (indices clamped into the
+  // written rows: rows of other groups or past ns are read but weighted 0)
+  float ov[kCombBatch];
 #pragma unroll
-  for (int u = 0; u < kCombBatch; ++u) ov[u] = po[(hb + min(u, ns - 1)) * kHeadDim + dd];
-  float mx[kPer], l[kPer];
+  for (int u = 0; u < kCombBatch; ++u) ov[u] = po[(hb + min(gl + u, ns - 1)) * kHeadDim + dd];
+  float mx[PER], l[PER];
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const long sidx = hb + min(dd + 128 * k, ns - 1);
+  for (int k = 0; k < PER; ++k) {
+    const long sidx = hb + min(tid + NT * k, ns - 1);
     mx[k] = pml[sidx * 2];
     l[k] = pml[sidx * 2 + 1];
   }
   float m = -INFINITY;
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    if (dd + 128 * k >= ns) mx[k] = -INFINITY;
+  for (int k = 0; k < PER; ++k) {
+    if (tid + NT * k >= ns) mx[k] = -INFINITY;
     m = fmaxf(m, mx[k]);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, kWave));
-  if ((dd & 63) == 0) red[0][wave] = m;
+  if ((tid & 63) == 0) red[0][wave] = m;
   __syncthreads();
-  const float M = fmaxf(red[0][0], red[0][1]);
+  float M = red[0][0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) M = fmaxf(M, red[0][w]);
   float dp = 0.f;
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {
+  for (int k = 0; k < PER; ++k) {
     const float w = (M == -INFINITY || mx[k] == -INFINITY) ? 0.f : __expf(__fsub_rn(mx[k], M));
-    wts[dd + 128 * k] = w;
+    wts[tid + NT * k] = w;
     dp = __fmaf_rn(w, l[k], dp);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) dp = __fadd_rn(dp, __shfl_xor(dp, o, kWave));
-  if ((dd & 63) == 0) red[1][wave] = dp;
+  if ((tid & 63) == 0) red[1][wave] = dp;
   __syncthreads();
-  const float den = __fadd_rn(red[1][0], red[1][1]);
+  float den = red[1][0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) den = __fadd_rn(den, red[1][w]);
   float v = 0.f;
+  for (int s0 = gl; s0 < gh; s0 += kCombBatch) {
+    if (s0 != gl) {
 #pragma unroll
-  for (int u = 0; u < kCombBatch; ++u) v = __fmaf_rn(u < ns ? wts[u] : 0.f, ov[u], v);
-  for (int s0 = kCombBatch; s0 < ns; s0 += kCombBatch) {
-#pragma unroll
-    for (int u = 0; u < kCombBatch; ++u) ov[u] = po[(hb + min(s0 + u, ns - 1)) * kHeadDim + dd];
+      for (int u = 0; u < kCombBatch; ++u) ov[u] = po[(hb + min(s0 + u, ns - 1)) * kHeadDim + dd];
+    }
 #pragma unroll
     for (int u = 0; u < kCombBatch; ++u)
-      v = __fmaf_rn(s0 + u < ns ? wts[min(s0 + u, kCombMaxSplit - 1)] : 0.f, ov[u], v);
+      v = __fmaf_rn(s0 + u < gh ? wts[min(s0 + u, kCombMaxSplit - 1)] : 0.f, ov[u], v);
+  }
+  if (G > 1) {
+    part[grp][dd] = v;
+    __syncthreads();
+    if (grp != 0) return;
+    v = part[0][dd];
+#pragma unroll
+    for (int g = 1; g < G; ++g)
+      if (g < ng) v = __fadd_rn(v, part[g][dd]);
   }
   attn_out_q8(den > 0.f ? __fdiv_rn(v, den) : 0.f, h, t, dd, H, out, x8, dx, sx);
+}
+
+// Row groups of the merge for an engine whose KV cache holds max_ctx positions.
+inline int comb_groups(int max_ctx) {
+  const int chunks = max_ctx / kAttnChunk;
+  return chunks <= 128 ? 1 : chunks <= 256 ? 2 : chunks <= 512 ? 4 : 8;
 }
 
 template <int G>
@@ -1061,11 +1090,38 @@ int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* 
                        st, aa);
   });
   if (rc) return rc;
-  hipLaunchKernelGGL(aa.nsplit <= kCombMaxSplit ? attn_combine2_q8_kernel : attn_combine_q8_kernel,
-                     dim3(H, T), dim3(128), 0, st,
-                     static_cast<const float*>(po), static_cast<const float*>(pml),
-                     static_cast<const int*>(pos), H, aa.nsplit, kAttnChunk, static_cast<float*>(out),
-                     static_cast<int8_t*>(x8), static_cast<float*>(dx), static_cast<float*>(sx));
+  // the merge kernel and its row groups follow max_ctx (fixed per engine), never this launch's
+  // span: a token's bits must not depend on the longest sequence it is batched with
+  const float* po_c = static_cast<const float*>(po);
+  const float* pml_c = static_cast<const float*>(pml);
+  const int* pos_c = static_cast<const int*>(pos);
+  float* out_f = static_cast<float*>(out);
+  int8_t* x8_c = static_cast<int8_t*>(x8);
+  float* dx_f = static_cast<float*>(dx);
+  float* sx_f = static_cast<float*>(sx);
+  if (max_ctx / kAttnChunk > kCombMaxSplit) {
+    hipLaunchKernelGGL(attn_combine_q8_kernel, dim3(H, T), dim3(128), 0, st, po_c, pml_c, pos_c, H,
+                       aa.nsplit, kAttnChunk, out_f, x8_c, dx_f, sx_f);
+  } else {
+    switch (comb_groups(max_ctx)) {
+      case 1:
+        hipLaunchKernelGGL(attn_combine2_q8_kernel<1>, dim3(H, T), dim3(128), 0, st, po_c, pml_c,
+                           pos_c, H, aa.nsplit, kAttnChunk, out_f, x8_c, dx_f, sx_f);
+        break;
+      case 2:
+        hipLaunchKernelGGL(attn_combine2_q8_kernel<2>, dim3(H, T), dim3(256), 0, st, po_c, pml_c,
+                           pos_c, H, aa.nsplit, kAttnChunk, out_f, x8_c, dx_f, sx_f);
+        break;
+      case 4:
+        hipLaunchKernelGGL(attn_combine2_q8_kernel<4>, dim3(H, T), dim3(512), 0, st, po_c, pml_c,
+                           pos_c, H, aa.nsplit, kAttnChunk, out_f, x8_c, dx_f, sx_f);
+        break;
+      default:
+        hipLaunchKernelGGL(attn_combine2_q8_kernel<8>, dim3(H, T), dim3(1024), 0, st, po_c, pml_c,
+                           pos_c, H, aa.nsplit, kAttnChunk, out_f, x8_c, dx_f, sx_f);
+        break;
+    }
+  }
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
