@@ -46,7 +46,8 @@ def llm_decode(T: int = 1, P: int = 512):
     from k8s_nvidia_gpus_amd.models.llm.weights import ModelWeights
 
     w = ModelWeights.random(QWEN25_7B, device=torch.device("cuda", 0), seed=0)
-    eng = Engine(w, max_ctx=4096, slots=8, dense=True)
+    ctx = max(4096, P + 512)
+    eng = Engine(w, max_ctx=ctx, slots=8, dense=True)
     prompt = list(range(100, 100 + P))
     for s in range(T):
         eng.prefill(prompt, slot=s)
@@ -56,7 +57,7 @@ def llm_decode(T: int = 1, P: int = 512):
         p = state["pos"]
         nxt = eng.decode_greedy(state["tok"], [p] * T, list(range(T)))
         state["tok"] = [int(x) % QWEN25_7B.vocab for x in nxt]
-        state["pos"] = p + 1 if p + 1 < min(P + 488, 4000) else len(prompt)
+        state["pos"] = p + 1 if p + 1 < min(P + 488, ctx - 8) else len(prompt)
     return step
 
 
