@@ -55,6 +55,13 @@ HIP_FLAGS = [
     "-Wno-unused-result",
 ]
 
+# per-translation-unit extra flags of the kernel library
+FILE_FLAGS = {
+    # SLP packs the P.V update into v_pk_fma_f32 and keeps a chunk's weights live at once
+    # (224-256 VGPRs at 7 q heads per kv head); scalar v_fma needs 165 (llm_attn.hip header)
+    "llm_attn.hip": ["-fno-slp-vectorize"],
+}
+
 
 @dataclass
 class NativeTarget:
@@ -133,7 +140,8 @@ def build_kernel_library(force: bool = False, verbose: bool = False, jobs: int =
 
     def compile_one(pair):
         s, o = pair
-        _run([HIPCC, *HIP_FLAGS, f"-I{CSRC_DIR}", "-c", str(s), "-o", str(o)], verbose)
+        _run([HIPCC, *HIP_FLAGS, *FILE_FLAGS.get(s.name, []), f"-I{CSRC_DIR}", "-c", str(s), "-o",
+              str(o)], verbose)
 
     if todo:
         with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:

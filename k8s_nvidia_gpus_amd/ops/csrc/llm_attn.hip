@@ -1,0 +1,585 @@
+// Split-context decode attention of the in-tree Qwen2 LLM engine (k8s_nvidia_gpus_amd/models/llm),
+// gfx950: flash-decoding over the fp16 KV cache, fused RoPE + KV write, and the chunk merge that
+// emits the Q8 activations of the o_proj input (llm_decode.hip has the rest of the decode path).
+//
+// Its own translation unit because it is built with -fno-slp-vectorize (ops/build.py): the SLP
+// vectoriser pairs the two output dims of the P.V update into v_pk_fma_f32, which needs every
+// weight of a chunk converted and live at once — 224-256 VGPRs at G = 7, one wave per SIMD —
+// where the scalar v_fma form needs 165.  (The VALU GEMV in llm_decode.hip wants the packed form.)
+#include "llm_common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- split-context decode attention
+// grid (Hkv, attn_parts_max(span), T); 256 threads.  One workgroup: the G = H/Hkv q heads of one
+// kv head over cpw consecutive 64-position chunks (one partial).  Per chunk — scores: 4 lanes per
+// position (32 dims each, all four 16-byte K loads in flight), softmax by one wave (lane =
+// position), P.V: wave w takes 16 positions with all 16 V loads in flight, lane = 2 dims — while
+// the next chunk's K / V loads are in flight.  Writes the unnormalised partial output and
+// (max, sum) per head.
+//
+// Chunks per workgroup (cpw) follow the token's own length only: 1 up to 8192 positions, then 2,
+// 4, 8 — at most kAttnParts partials per head up to 65536 positions.  At 32k positions the one-
+// chunk form launched 2000 workgroups of one HBM burst each per layer (20 us for 64 MB, ~3.2 TB/s,
+// plus a 10.7 us merge of 500 partials per head: profiles/r05/llm_decode_32k_vs_512_kernels_r05f);
+// four streamed chunks per workgroup keep loads in flight across chunks and leave 125 partials.
+// The split depends on nothing but the token, so its bits do not depend on its batch.
+constexpr int kAttnParts = 128;
+constexpr int kAttnMaxCpw = 8;
+__host__ __device__ __forceinline__ int attn_cpw(int len) {
+  int c = 1;
+  while (c < kAttnMaxCpw && len > kAttnChunk * kAttnParts * c) c <<= 1;
+  return c;
+}
+__host__ __device__ __forceinline__ int attn_parts(int len) {
+  const int w = kAttnChunk * attn_cpw(len);
+  return (len + w - 1) / w;
+}
+// the most partials of any length <= span (within one cpw band the count grows with the length,
+// and each band ends at kAttnParts)
+inline int attn_parts_max(int span) {
+  int m = attn_parts(span);
+  for (int e = kAttnChunk * kAttnParts; e < span; e <<= 1) m = m > attn_parts(e) ? m : attn_parts(e);
+  return m;
+}
+
+// Fused form (qkv != null): the workgroup rotates its q heads from the raw q|k|v projection
+// itself, and the one workgroup per (token, kv head) whose chunk holds the new position also
+// rotates k, writes K/V to the cache and uses them from LDS — which replaces rope_kv_kernel and its
+// launch.  Valid when every token of the step is in its own slot (decode); chunked prefill of one
+// sequence through this path keeps the separate rope_kv_kernel.
+struct AttnArgs {
+  const float* q;        // rotated q [T][H*128] (unfused)
+  const float* qkv;      // raw projection [T][ldq] (fused) or null
+  int ldq;
+  const float* cos_t;
+  const float* sin_t;
+  const int* pos;
+  const int* slot;
+  uint16_t* kc;
+  uint16_t* vc;
+  int H, Hkv, max_ctx, nsplit;
+  float scale;
+  float* po;
+  float* pml;
+};
+
+// Output dim dd of head h, token t: fp32 (optional) and Q8 with its 32-block scale and 16-block
+// scaled sums (the o_proj GEMV input); a 32-dim block = half a wave.
+__device__ __forceinline__ void attn_out_q8(float y, int h, int t, int dd, int H,
+                                            float* __restrict__ out, int8_t* __restrict__ x8,
+                                            float* __restrict__ dx, float* __restrict__ sx) {
+  const int K = H * kHeadDim;
+  const int col = h * kHeadDim + dd;
+  if (out) out[(long)t * K + col] = y;
+  float amax = fabsf(y);
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, kWave));
+  const float d = amax / 127.f;
+  const int qv = d > 0.f ? (int)__builtin_rintf(y / d) : 0;
+  x8[(long)t * K + col] = (int8_t)qv;
+  int s16 = qv;
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) s16 += __shfl_xor(s16, o, kWave);
+  if ((dd & 31) == 0) dx[(long)t * (K >> 5) + (col >> 5)] = d;
+  if ((dd & 15) == 0) sx[(long)t * (K >> 4) + (col >> 4)] = d * (float)s16;
+}
+
+// Merge the context chunks of head h of token t and quantise the attention output to Q8 (the o_proj
+// input): thread dd = one output dim; a 32-dim block = half a wave (dd & 31 within a wave).  One
+// pass over the chunks in groups of 8 with every partial of the group loaded before any maths
+// (online max: one memory round trip per 8 chunks), explicit roundings.
+template <int NH>
+__device__ __forceinline__ void combine_heads(const float* __restrict__ po,
+                                              const float* __restrict__ pml,
+                                              const int* __restrict__ pos, int H, int nsplit,
+                                              int h0, int hstep, int hend, int t, int dd,
+                                              float* __restrict__ out, int8_t* __restrict__ x8,
+                                              float* __restrict__ dx, float* __restrict__ sx) {
+  const int ns = min(nsplit, attn_parts(pos[t] + 1));
+  long hb[NH];
+#pragma unroll
+  for (int k = 0; k < NH; ++k) hb[k] = ((long)t * H + min(h0 + k * hstep, hend - 1)) * nsplit;
+  float m[NH], den[NH], v[NH];
+#pragma unroll
+  for (int k = 0; k < NH; ++k) { m[k] = -INFINITY; den[k] = 0.f; v[k] = 0.f; }
+  for (int s0 = 0; s0 < ns; s0 += 8) {
+    float mx[NH][8], l[NH][8], ov[NH][8];
+#pragma unroll
+    for (int k = 0; k < NH; ++k)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {                  // indices clamped, extra terms masked below
+        const long sidx = hb[k] + min(s0 + u, ns - 1);
+        mx[k][u] = pml[sidx * 2];
+        l[k][u] = pml[sidx * 2 + 1];
+        ov[k][u] = po[sidx * kHeadDim + dd];
+      }
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      float mn = m[k];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (s0 + u < ns) mn = fmaxf(mn, mx[k][u]);
+      if (mn == -INFINITY) continue;                 // nothing attended yet
+      // explicit roundings (no fp-contract choice left to the compiler): the same bits for any NH
+      const float sc = m[k] == -INFINITY ? 0.f : __expf(__fsub_rn(m[k], mn));
+      den[k] = __fmul_rn(den[k], sc);
+      v[k] = __fmul_rn(v[k], sc);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float wgt =
+            (s0 + u < ns && mx[k][u] != -INFINITY) ? __expf(__fsub_rn(mx[k][u], mn)) : 0.f;
+        den[k] = __fmaf_rn(wgt, l[k][u], den[k]);
+        v[k] = __fmaf_rn(wgt, ov[k][u], v[k]);
+      }
+      m[k] = mn;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NH; ++k) {
+    const int h = h0 + k * hstep;
+    if (h >= hend) break;                            // uniform per wave (hstep multiple of waves)
+    attn_out_q8(den[k] > 0.f ? __fdiv_rn(v[k], den[k]) : 0.f, h, t, dd, H, out, x8, dx, sx);
+  }
+}
+
+// grid (H, T), 128 threads.
+__global__ void __launch_bounds__(128) attn_combine_q8_kernel(const float* __restrict__ po,
+                                                              const float* __restrict__ pml,
+                                                              const int* __restrict__ pos, int H,
+                                                              int nsplit,
+                                                              float* __restrict__ out,
+                                                              int8_t* __restrict__ x8,
+                                                              float* __restrict__ dx,
+                                                              float* __restrict__ sx) {
+  combine_heads<1>(po, pml, pos, H, nsplit, blockIdx.x, 1, H, blockIdx.y, threadIdx.x, out,
+                   x8, dx, sx);
+}
+
+// Two-pass merge of the chunks of head h of token t, with 128·G threads (G row groups of 128 dims):
+// every chunk's (max, sum) loads at once (PER per thread, up to kCombMaxSplit chunks); the max and
+// the denominator are workgroup reductions (the chunk weights go to LDS); then each of ng row groups
+// sums a contiguous range of the partial rows with their weights, kCombBatch row loads in flight at
+// a time, and the group sums add up in group order.  ng = min(G, ceil(ns / kCombBatch)) depends only
+// on this token's own chunk count, and G only on the engine's max_ctx (the launcher), so a token's
+// bits never depend on the batch it runs in.  At 32k positions with one chunk per
+// partial (512 per head) the 128-thread form took 16 dependent row batches per head (~1 ms per
+// 28-layer step at T = 1, profiles/r05); with streamed chunks (<= 128 partials up to 65536
+// positions) four groups take one batch each.
+constexpr int kCombBatch = 32;
+constexpr int kCombMaxSplit = 1024;                 // max_ctx <= 524288 (8 chunks per partial)
+
+template <int G>
+__global__ void __launch_bounds__(128 * G) attn_combine2_q8_kernel(const float* __restrict__ po,
+                                                                   const float* __restrict__ pml,
+                                                                   const int* __restrict__ pos,
+                                                                   int H, int nsplit,
+                                                                   float* __restrict__ out,
+                                                                   int8_t* __restrict__ x8,
+                                                                   float* __restrict__ dx,
+                                                                   float* __restrict__ sx) {
+  constexpr int NT = 128 * G, NW = NT / kWave, PER = kCombMaxSplit / NT;
+  __shared__ float wts[kCombMaxSplit];
+  __shared__ float red[2][NW];
+  __shared__ float part[G][kHeadDim];
+  const int h = blockIdx.x, t = blockIdx.y, tid = threadIdx.x, wave = tid >> 6;
+  const int dd = tid & (kHeadDim - 1), grp = tid >> 7;
+  const int ns = min(nsplit, attn_parts(pos[t] + 1));
+  const long hb = ((long)t * H + h) * nsplit;
+  const int ng = min(G, (ns + kCombBatch - 1) / kCombBatch);
+  const int gl = grp < ng ? grp * ns / ng : 0, gh = grp < ng ? (grp + 1) * ns / ng : 0;
+  // this group's first row batch, in flight with the (max, sum) loads (indices clamped into the
+  // written rows: rows of other groups or past ns are read but weighted 0)
+  float ov[kCombBatch];
+#pragma unroll
+  for (int u = 0; u < kCombBatch; ++u) ov[u] = po[(hb + min(gl + u, ns - 1)) * kHeadDim + dd];
+  float mx[PER], l[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const long sidx = hb + min(tid + NT * k, ns - 1);
+    mx[k] = pml[sidx * 2];
+    l[k] = pml[sidx * 2 + 1];
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (tid + NT * k >= ns) mx[k] = -INFINITY;
+    m = fmaxf(m, mx[k]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, kWave));
+  if ((tid & 63) == 0) red[0][wave] = m;
+  __syncthreads();
+  float M = red[0][0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) M = fmaxf(M, red[0][w]);
+  float dp = 0.f;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const float w = (M == -INFINITY || mx[k] == -INFINITY) ? 0.f : __expf(__fsub_rn(mx[k], M));
+    wts[tid + NT * k] = w;
+    dp = __fmaf_rn(w, l[k], dp);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) dp = __fadd_rn(dp, __shfl_xor(dp, o, kWave));
+  if ((tid & 63) == 0) red[1][wave] = dp;
+  __syncthreads();
+  float den = red[1][0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) den = __fadd_rn(den, red[1][w]);
+  float v = 0.f;
+  for (int s0 = gl; s0 < gh; s0 += kCombBatch) {
+    if (s0 != gl) {
+#pragma unroll
+      for (int u = 0; u < kCombBatch; ++u) ov[u] = po[(hb + min(s0 + u, ns - 1)) * kHeadDim + dd];
+    }
+#pragma unroll
+    for (int u = 0; u < kCombBatch; ++u)
+      v = __fmaf_rn(s0 + u < gh ? wts[min(s0 + u, kCombMaxSplit - 1)] : 0.f, ov[u], v);
+  }
+  if (G > 1) {
+    part[grp][dd] = v;
+    __syncthreads();
+    if (grp != 0) return;
+    v = part[0][dd];
+#pragma unroll
+    for (int g = 1; g < G; ++g)
+      if (g < ng) v = __fadd_rn(v, part[g][dd]);
+  }
+  attn_out_q8(den > 0.f ? __fdiv_rn(v, den) : 0.f, h, t, dd, H, out, x8, dx, sx);
+}
+
+// Row groups of the merge for an engine whose KV cache holds max_ctx positions: one row batch
+// per group at the engine's longest partial count (128 partials, every max_ctx >= 8192: 4 groups).
+inline int comb_groups(int max_ctx) {
+  const int parts = attn_parts_max(max_ctx);
+  return parts <= kCombBatch ? 1 : parts <= 2 * kCombBatch ? 2 : parts <= 4 * kCombBatch ? 4 : 8;
+}
+
+template <int G>
+__global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
+  const float* __restrict__ q = a.q;
+  const int* __restrict__ pos = a.pos;
+  const int* __restrict__ slot = a.slot;
+  const uint16_t* __restrict__ kc = a.kc;
+  const uint16_t* __restrict__ vc = a.vc;
+  const int H = a.H, Hkv = a.Hkv, max_ctx = a.max_ctx, nsplit = a.nsplit;
+  const float scale = a.scale;
+  float* __restrict__ po = a.po;
+  float* __restrict__ pml = a.pml;
+  __shared__ float qs[G][kHeadDim];
+  __shared__ __align__(16) uint16_t knew[kHeadDim];   // the new position's rotated K (fp16)
+  __shared__ __align__(16) uint16_t vnew[kHeadDim];   // and its V
+  __shared__ float ps[2][G][kAttnChunk];              // by chunk parity: two barriers per chunk
+  __shared__ float alph[2][G];
+  __shared__ float opart[4][G][kHeadDim];
+  const int kh = blockIdx.x, sp = blockIdx.y, t = blockIdx.z;
+  const int len = pos[t] + 1;
+  const int cpw = attn_cpw(len);
+  const int w0 = sp * kAttnChunk * cpw;                 // this workgroup's first position
+  if (w0 >= len) return;                                // past the token's partials: never merged
+  const int nc = min(cpw, (len - w0 + kAttnChunk - 1) / kAttnChunk);   // chunks streamed here
+  const long pidx = ((long)t * H + kh * G) * nsplit + sp;   // + g * nsplit
+  const long cbase = ((long)slot[t] * Hkv + kh) * max_ctx * kHeadDim;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int pi = threadIdx.x >> 2, qd = threadIdx.x & 3;
+  // chunk c's rows.  Scores: 4 lanes per position, 32 dims each; P.V: wave w → positions
+  // w*16 .. w*16+15, lane = 2 dims.  Every load is unconditional: a load under a divergent branch
+  // ends its basic block and the join waits for it.  The V rows are one base address plus
+  // immediate offsets (a per-row clamp kept 16 row indices live across the loop); rows past the
+  // token are still inside the cache (max_ctx % 64 == 0) and are zeroed before use.
+  auto load_chunk = [&](int c, uint4 (&kv)[4], uint32_t (&vv)[16]) __attribute__((always_inline)) {
+    const int p0 = w0 + c * kAttnChunk, n = min(kAttnChunk, len - p0);
+    const uint4* kr = reinterpret_cast<const uint4*>(kc + cbase + (long)(p0 + min(pi, n - 1))
+                                                     * kHeadDim + qd * 32);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) kv[e] = kr[e];
+    const uint32_t* vr = reinterpret_cast<const uint32_t*>(
+        vc + cbase + (long)(p0 + wave * 16) * kHeadDim) + lane;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) vv[j] = vr[j * (kHeadDim / 2)];
+  };
+  uint4 kv[4];
+  uint32_t vv[16];
+  load_chunk(0, kv, vv);                                // K and V of chunk 0 before any q work
+  const int pnew = len - 1;
+  const bool own = a.qkv != nullptr && pnew >= w0 && pnew < w0 + kAttnChunk * cpw;
+  if (a.qkv) {
+    const float* row = a.qkv + (long)t * a.ldq;
+    const float* ct = a.cos_t + (long)pnew * (kHeadDim / 2);
+    const float* st = a.sin_t + (long)pnew * (kHeadDim / 2);
+    // every load of the q rotation and of the new k / v row in flight at once (indices clamped,
+    // no load under a branch), then the maths and the stores
+    constexpr int QR = (G * (kHeadDim / 2) + 255) / 256;   // rotation pairs per thread
+    float qx0[QR], qx1[QR], qc[QR], qsn[QR];
+#pragma unroll
+    for (int u = 0; u < QR; ++u) {
+      const int i = min((int)threadIdx.x + 256 * u, G * (kHeadDim / 2) - 1);
+      const int g = i / (kHeadDim / 2), j = i % (kHeadDim / 2);
+      qx0[u] = row[(kh * G + g) * kHeadDim + j];
+      qx1[u] = row[(kh * G + g) * kHeadDim + j + kHeadDim / 2];
+      qc[u] = ct[j];
+      qsn[u] = st[j];
+    }
+    const int jk = threadIdx.x & (kHeadDim / 2 - 1), ev = threadIdx.x & (kHeadDim - 1);
+    const float k0 = row[(H + kh) * kHeadDim + jk], k1 = row[(H + kh) * kHeadDim + jk + kHeadDim / 2];
+    const float vn = row[(H + Hkv + kh) * kHeadDim + ev];
+#pragma unroll
+    for (int u = 0; u < QR; ++u) {
+      const int i = (int)threadIdx.x + 256 * u;
+      if (i < G * (kHeadDim / 2)) {
+        const int g = i / (kHeadDim / 2), j = i % (kHeadDim / 2);
+        qs[g][j] = rope_lo(qx0[u], qx1[u], qc[u], qsn[u]) * scale;
+        qs[g][j + kHeadDim / 2] = rope_hi(qx0[u], qx1[u], qc[u], qsn[u]) * scale;
+      }
+    }
+    if (own) {
+      const long cpos = cbase + (long)pnew * kHeadDim;
+      if (threadIdx.x < kHeadDim / 2) {
+        const float c = qc[0], sn = qsn[0];          // thread j < 64 loaded ct[j] / st[j] at u = 0
+        const uint16_t h0 = f2h(rope_lo(k0, k1, c, sn)), h1 = f2h(rope_hi(k0, k1, c, sn));
+        a.kc[cpos + jk] = h0;
+        a.kc[cpos + jk + kHeadDim / 2] = h1;
+        knew[jk] = h0;
+        knew[jk + kHeadDim / 2] = h1;
+      }
+      if (threadIdx.x < kHeadDim) {
+        const uint16_t hv = f2h(vn);
+        a.vc[cpos + ev] = hv;
+        vnew[ev] = hv;
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < G * kHeadDim; i += blockDim.x)
+      qs[i / kHeadDim][i % kHeadDim] = q[(long)t * H * kHeadDim + (kh * G) * kHeadDim + i] * scale;
+  }
+  __syncthreads();
+  // online softmax over the chunks: the running max / sum of head g live in wave g % 4 (slot
+  // g / 4); every wave rescales its P.V accumulators by the chunk's alpha = exp(M_old - M_new).
+  // One chunk (cpw = 1, every length <= 8192) gives exactly the single-chunk arithmetic.
+  constexpr int GW = (G + 3) / 4;
+  float mrun[GW], lrun[GW];
+#pragma unroll
+  for (int k = 0; k < GW; ++k) { mrun[k] = -INFINITY; lrun[k] = 0.f; }
+  float o[G][2];
+#pragma unroll
+  for (int g = 0; g < G; ++g) o[g][0] = o[g][1] = 0.f;
+#pragma unroll 1
+  for (int c = 0; c < nc; ++c) {
+    uint4 kn[4];
+    uint32_t vn[16];
+    // the next chunk in flight during this one's maths (the last chunk re-reads itself from L2:
+    // a branch here or around the swap below splits the loop body, and the scheduler then
+    // issues every P.V weight read ahead of the FMAs — 256 VGPRs at G = 7)
+    load_chunk(min(c + 1, nc - 1), kn, vn);
+    // q stays in LDS: without this compiler barrier the loop-invariant q reads (G x 32 floats per
+    // thread) are hoisted into registers — 256 VGPRs, one wave per SIMD
+    __asm__ volatile("" ::: "memory");
+    const int p0 = w0 + c * kAttnChunk, n = min(kAttnChunk, len - p0), par = c & 1;
+    const int jn = pnew - p0;                           // the new position in this chunk?
+    if (own && jn >= 0 && jn < kAttnChunk) {           // its rows were loaded before they were written
+      uint4 kq[4];                                      // (uniform branch, per-lane selects)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) kq[e] = reinterpret_cast<const uint4*>(knew)[qd * 4 + e];
+      const uint32_t vq = reinterpret_cast<const uint32_t*>(vnew)[lane];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {                    // per component: a select of two uint4
+        const bool nw = pi == jn;                       // lvalues is a pointer select (scratch)
+        kv[e].x = nw ? kq[e].x : kv[e].x;
+        kv[e].y = nw ? kq[e].y : kv[e].y;
+        kv[e].z = nw ? kq[e].z : kv[e].z;
+        kv[e].w = nw ? kq[e].w : kv[e].w;
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) vv[j] = j == jn - wave * 16 ? vq : vv[j];
+    }
+    {
+      const int nv = n - wave * 16;                     // rows past the token: 0 (ps is 0 there)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) vv[j] = j < nv ? vv[j] : 0u;
+    }
+    float sc[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) sc[g] = 0.f;
+#pragma unroll
+    for (int e4 = 0; e4 < 4; ++e4) {
+      const uint32_t kw[4] = {kv[e4].x, kv[e4].y, kv[e4].z, kv[e4].w};
+      float kf[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        kf[2 * e] = h2f(kw[e] & 0xffffu);
+        kf[2 * e + 1] = h2f(kw[e] >> 16);
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sc[g] += kf[e] * qs[g][qd * 32 + e4 * 8 + e];
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      sc[g] += __shfl_xor(sc[g], 1, kWave);
+      sc[g] += __shfl_xor(sc[g], 2, kWave);
+    }
+    if (qd == 0) {
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        ps[par][g][pi] = pi < n ? sc[g] : -INFINITY;
+    }
+    __syncthreads();
+    // softmax: head g on wave g % 4 (lane = position), LDS-free cross-lane max / sum
+#pragma unroll
+    for (int k = 0; k < GW; ++k) {
+      const int g = 4 * k + wave;
+      if (g < G) {
+        const float s = ps[par][g][lane];
+        const float mn = fmaxf(mrun[k], wave_max_fast(s));
+        const float p = lane < n ? __expf(s - mn) : 0.f;
+        ps[par][g][lane] = p;
+        const float al = __expf(mrun[k] - mn);          // 0 for the first chunk
+        lrun[k] = lrun[k] * al + wave_sum_fast(p);
+        mrun[k] = mn;
+        if (lane == 0) alph[par][g] = al;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float al = alph[par][g];
+      o[g][0] *= al;
+      o[g][1] *= al;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float v0 = h2f(vv[j] & 0xffffu), v1 = h2f(vv[j] >> 16);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float pw = ps[par][g][wave * 16 + j];
+        o[g][0] += pw * v0;
+        o[g][1] += pw * v1;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) kv[e] = kn[e];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) vv[j] = vn[j];
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    opart[wave][g][2 * lane] = o[g][0];
+    opart[wave][g][2 * lane + 1] = o[g][1];
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < GW; ++k) {
+      const int g = 4 * k + wave;
+      if (g < G) {
+        float* dst = pml + (pidx + (long)g * nsplit) * 2;
+        dst[0] = mrun[k];
+        dst[1] = lrun[k];
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < G * kHeadDim; i += blockDim.x) {
+    const int g = i / kHeadDim, dd = i % kHeadDim;
+    const float v = opart[0][g][dd] + opart[1][g][dd] + opart[2][g][dd] + opart[3][g][dd];
+    po[(pidx + (long)g * nsplit) * kHeadDim + dd] = v;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int amdk8s_llm_attn_chunk() { return kAttnChunk; }
+
+// Decode attention over the KV cache + combine + Q8 quantisation of the output.
+// po/pml: workspace [T][H][nsplit][128] / [T][H][nsplit][2]; out (nullable) fp32 [T][H*128].
+// span: positions covered by this launch (a multiple of 64, <= max_ctx, > every pos[t]); the
+// caller buckets it so a captured graph does not launch empty chunks up to max_ctx.
+// qkv (nullable): the raw q|k|v projection [T][ldq] — fused RoPE + KV write (distinct slots
+// only, see attn_decode_kernel); q is then unused.
+int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* cos_t,
+                           const void* sin_t, const void* pos, const void* slot, void* kc,
+                           void* vc, int H, int Hkv, int head_dim, int max_ctx, int span,
+                           float scale, void* po, void* pml, void* out, void* x8, void* dx,
+                           void* sx, int T, void* stream) {
+  if (span <= 0) span = max_ctx;
+  if (head_dim != kHeadDim || H % Hkv || H / Hkv > kMaxGroup || max_ctx % kAttnChunk ||
+      span % kAttnChunk || span > max_ctx || T < 1)
+    return 2;
+  if (!qkv && !q) return 2;
+  if (qkv && (!cos_t || !sin_t)) return 2;
+  if (!(x8 && dx && sx)) return 2;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  AttnArgs aa{};
+  aa.q = static_cast<const float*>(q);
+  aa.qkv = static_cast<const float*>(qkv);
+  aa.ldq = ldq;
+  aa.cos_t = static_cast<const float*>(cos_t);
+  aa.sin_t = static_cast<const float*>(sin_t);
+  aa.pos = static_cast<const int*>(pos);
+  aa.slot = static_cast<const int*>(slot);
+  aa.kc = static_cast<uint16_t*>(kc);
+  aa.vc = static_cast<uint16_t*>(vc);
+  aa.H = H; aa.Hkv = Hkv; aa.max_ctx = max_ctx; aa.scale = scale;
+  aa.po = static_cast<float*>(po);
+  aa.pml = static_cast<float*>(pml);
+  // the GQA group size is a template parameter: fully unrolled head loops, no per-head branches
+  auto by_group = [&](auto launch) -> int {
+    switch (H / Hkv) {
+      case 1: launch(std::integral_constant<int, 1>{}); break;
+      case 2: launch(std::integral_constant<int, 2>{}); break;
+      case 3: launch(std::integral_constant<int, 3>{}); break;
+      case 4: launch(std::integral_constant<int, 4>{}); break;
+      case 5: launch(std::integral_constant<int, 5>{}); break;
+      case 6: launch(std::integral_constant<int, 6>{}); break;
+      case 7: launch(std::integral_constant<int, 7>{}); break;
+      case 8: launch(std::integral_constant<int, 8>{}); break;
+      default: return 2;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+  };
+  aa.nsplit = span / kAttnChunk;                         // partial-row stride of po / pml
+  const int rc = by_group([&](auto g) {
+    hipLaunchKernelGGL(attn_decode_kernel<decltype(g)::value>, dim3(Hkv, attn_parts_max(span), T),
+                       dim3(256), 0, st, aa);
+  });
+  if (rc) return rc;
+  // the merge kernel and its row groups follow max_ctx (fixed per engine), never this launch's
+  // span: a token's bits must not depend on the longest sequence it is batched with
+  const float* po_c = static_cast<const float*>(po);
+  const float* pml_c = static_cast<const float*>(pml);
+  const int* pos_c = static_cast<const int*>(pos);
+  float* out_f = static_cast<float*>(out);
+  int8_t* x8_c = static_cast<int8_t*>(x8);
+  float* dx_f = static_cast<float*>(dx);
+  float* sx_f = static_cast<float*>(sx);
+  if (attn_parts_max(max_ctx) > kCombMaxSplit) {
+    hipLaunchKernelGGL(attn_combine_q8_kernel, dim3(H, T), dim3(128), 0, st, po_c, pml_c, pos_c, H,
+                       aa.nsplit, out_f, x8_c, dx_f, sx_f);
+  } else {
+    switch (comb_groups(max_ctx)) {
+      case 1:
+        hipLaunchKernelGGL(attn_combine2_q8_kernel<1>, dim3(H, T), dim3(128), 0, st, po_c, pml_c,
+                           pos_c, H, aa.nsplit, out_f, x8_c, dx_f, sx_f);
+        break;
+      case 2:
+        hipLaunchKernelGGL(attn_combine2_q8_kernel<2>, dim3(H, T), dim3(256), 0, st, po_c, pml_c,
+                           pos_c, H, aa.nsplit, out_f, x8_c, dx_f, sx_f);
+        break;
+      case 4:
+        hipLaunchKernelGGL(attn_combine2_q8_kernel<4>, dim3(H, T), dim3(512), 0, st, po_c, pml_c,
+                           pos_c, H, aa.nsplit, out_f, x8_c, dx_f, sx_f);
+        break;
+      default:
+        hipLaunchKernelGGL(attn_combine2_q8_kernel<8>, dim3(H, T), dim3(1024), 0, st, po_c, pml_c,
+                           pos_c, H, aa.nsplit, out_f, x8_c, dx_f, sx_f);
+        break;
+    }
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+}  // extern "C"

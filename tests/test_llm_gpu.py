@@ -401,10 +401,11 @@ def test_rope_kv_and_decode_attention(dev, LK, H, Hkv):
 
 @pytest.mark.parametrize("max_ctx", [4096, 32768, 65536, 131072])
 def test_decode_attention_long_context(dev, LK, max_ctx):
-    """The chunk merge at every row-group size (1 group up to 8192 positions, 8 at 32768 and 65536:
-    up to 1024 chunks, with several row batches per group) and, past 65536, the online merge — vs
-    the fp32 softmax reference; and a sequence alone gives the bits it gets batched with a longer
-    one (the merge follows max_ctx, not the launch's span: ADVICE r4)."""
+    """Streamed chunks per workgroup (1 up to 8192 positions, then 2 / 4 / 8: at 70000 positions
+    137 partials of 512) and the merge's row groups (from max_ctx: 2 at 4096, 4 at 32768 / 65536,
+    8 at 131072) vs the fp32 softmax reference; and a sequence alone gives the bits it gets
+    batched with a longer one (the split and the merge follow the token and max_ctx, never the
+    launch's span or batch: ADVICE r4)."""
     torch.manual_seed(11)
     H, Hkv, slots, T = 28, 4, 2, 4
     kc = (torch.randn(slots, Hkv, max_ctx, 128, device=dev) * 0.5).half()
@@ -434,19 +435,28 @@ def test_decode_attention_long_context(dev, LK, max_ctx):
                    po[:1], pml[:1], x8[:1].clone(), dx[:1].clone(), sx[:1].clone(), out=one,
                    span=256)
     assert torch.equal(one[0], out[2])
+    # ... and the long one alone, with the smallest span that covers it
+    span = (far + 1 + 63) // 64 * 64
+    LK.attn_decode(q[:1], pos[:1], slot[:1], kc, vc, H, Hkv, 128, max_ctx, 1 / math.sqrt(128),
+                   po[:1], pml[:1], x8[:1].clone(), dx[:1].clone(), sx[:1].clone(), out=one,
+                   span=span)
+    assert torch.equal(one[0], out[0])
 
 
-@pytest.mark.parametrize("H,Hkv", [(28, 4), (8, 8)])
-def test_fused_rope_attention_equals_separate_kernels(dev, LK, H, Hkv):
+@pytest.mark.parametrize("H,Hkv,max_ctx,positions", [
+    (28, 4, 1024, (0, 63, 64, 700)), (8, 8, 1024, (0, 63, 64, 700)),
+    # workgroups of 2 and 4 streamed chunks; the new position in chunk 1, 1, 2 and 3 of its group
+    (28, 4, 32768, (9064, 16500, 20100, 30200))])
+def test_fused_rope_attention_equals_separate_kernels(dev, LK, H, Hkv, max_ctx, positions):
     """Distinct slots: RoPE + KV write inside the attention kernel == rope_kv + attention."""
     from k8s_nvidia_gpus_amd.models.llm.engine import rope_tables
 
     torch.manual_seed(3)
-    max_ctx, slots, T = 1024, 4, 4
+    slots, T = 4, 4
     base_k = (torch.randn(slots, Hkv, max_ctx, 128, device=dev) * 0.5).half()
     base_v = torch.randn(slots, Hkv, max_ctx, 128, device=dev).half()
     cos, sin = rope_tables(max_ctx, 128, 1.0e6, dev)
-    pos = torch.tensor([0, 63, 64, 700], dtype=torch.int32, device=dev)
+    pos = torch.tensor(positions, dtype=torch.int32, device=dev)
     slot = torch.tensor([3, 0, 1, 2], dtype=torch.int32, device=dev)
     qkv = torch.randn(T, (H + 2 * Hkv) * 128, device=dev)
     outs = []
@@ -470,6 +480,8 @@ def test_fused_rope_attention_equals_separate_kernels(dev, LK, H, Hkv):
         outs.append((kc, vc, out))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     torch.testing.assert_close(outs[1][2], outs[0][2], rtol=1e-5, atol=1e-5)
+    ref = _attn_ref(qrot, outs[0][0], outs[0][1], pos, slot, H, Hkv)
+    torch.testing.assert_close(outs[1][2], ref, rtol=1e-3, atol=1e-3)
 
 
 @pytest.mark.parametrize("T", [1, 4])

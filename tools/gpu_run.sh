@@ -135,12 +135,13 @@ PYEOF
     prof-llm|prof-llm:*)
       t=1; np=512; [[ "$step" == prof-llm:* ]] && t="${step#prof-llm:}"
       [[ "$t" == *:* ]] && { np="${t#*:}"; t="${t%%:*}"; }
-      timeout -k 10 400 rocprofv3 --kernel-trace --output-format rocpd -d "$OUT/prof_llm_t$t" -o llm \
-        -- python3 tools/steady_prof.py llm-decode --tokens "$t" --prompt "$np" --iters 20 --warmup 5 > "$OUT/prof_llm_t$t.log" 2>&1 \
-        || fail "$step" $? "$OUT/prof_llm_t$t.log"
-      db=$(find "$OUT/prof_llm_t$t" -name '*.db' | head -1)
-      python3 tools/rocpd_summary.py "$db" --after-gap-ms 200 --per 20 --top 30 > "$OUT/llm_decode_t${t}_kernels.txt" \
-        && head -24 "$OUT/llm_decode_t${t}_kernels.txt" | cut -c1-170 ;;
+      tag="t${t}_p${np}"
+      timeout -k 10 400 rocprofv3 --kernel-trace --output-format rocpd -d "$OUT/prof_llm_$tag" -o llm \
+        -- python3 tools/steady_prof.py llm-decode --tokens "$t" --prompt "$np" --iters 20 --warmup 5 > "$OUT/prof_llm_$tag.log" 2>&1 \
+        || fail "$step" $? "$OUT/prof_llm_$tag.log"
+      db=$(find "$OUT/prof_llm_$tag" -name '*.db' | head -1)
+      python3 tools/rocpd_summary.py "$db" --after-gap-ms 200 --per 20 --top 30 > "$OUT/llm_decode_${tag}_kernels.txt" \
+        && head -24 "$OUT/llm_decode_${tag}_kernels.txt" | cut -c1-170 ;;
     pmc-llm|pmc-llm:*)
       t=1; [[ "$step" == pmc-llm:* ]] && t="${step#pmc-llm:}"
       OUT="$OUT/llm_pmc_t$t" TOKENS=$t timeout -k 10 400 tools/llm_pmc.sh > "$OUT/llm_pmc_t$t.txt" 2>&1 \
