@@ -55,12 +55,8 @@ HIP_FLAGS = [
     "-Wno-unused-result",
 ]
 
-# per-translation-unit extra flags of the kernel library
-FILE_FLAGS = {
-    # SLP packs the P.V update into v_pk_fma_f32 and keeps a chunk's weights live at once
-    # (224-256 VGPRs at 7 q heads per kv head); scalar v_fma needs 165 (llm_attn.hip header)
-    "llm_attn.hip": ["-fno-slp-vectorize"],
-}
+# per-translation-unit extra flags of the kernel library (A/B builds: AMDK8S_HIP_DEFINES)
+FILE_FLAGS: dict = {}
 
 
 @dataclass

@@ -1,30 +1,24 @@
 // Split-context decode attention of the in-tree Qwen2 LLM engine (k8s_nvidia_gpus_amd/models/llm),
 // gfx950: flash-decoding over the fp16 KV cache, fused RoPE + KV write, and the chunk merge that
 // emits the Q8 activations of the o_proj input (llm_decode.hip has the rest of the decode path).
-//
-// Its own translation unit because it is built with -fno-slp-vectorize (ops/build.py): the SLP
-// vectoriser pairs the two output dims of the P.V update into v_pk_fma_f32, which needs every
-// weight of a chunk converted and live at once — 224-256 VGPRs at G = 7, one wave per SIMD —
-// where the scalar v_fma form needs 165.  (The VALU GEMV in llm_decode.hip wants the packed form.)
 #include "llm_common.h"
 
 namespace {
 
 // ---------------------------------------------------------------- split-context decode attention
 // grid (Hkv, attn_parts_max(span), T); 256 threads.  One workgroup: the G = H/Hkv q heads of one
-// kv head over cpw consecutive 64-position chunks (one partial).  Per chunk — scores: 4 lanes per
-// position (32 dims each, all four 16-byte K loads in flight), softmax by one wave (lane =
-// position), P.V: wave w takes 16 positions with all 16 V loads in flight, lane = 2 dims — while
-// the next chunk's K / V loads are in flight.  Writes the unnormalised partial output and
-// (max, sum) per head.
+// kv head over cpw consecutive 64-position chunks (one partial); writes the unnormalised partial
+// output and (max, sum) per head (attn_decode_kernel).
 //
 // Chunks per workgroup (cpw) follow the token's own length only: 1 up to 8192 positions, then 2,
-// 4, 8 — at most kAttnParts partials per head up to 65536 positions.  At 32k positions the one-
-// chunk form launched 2000 workgroups of one HBM burst each per layer (20 us for 64 MB, ~3.2 TB/s,
-// plus a 10.7 us merge of 500 partials per head: profiles/r05/llm_decode_32k_vs_512_kernels_r05f);
-// four streamed chunks per workgroup keep loads in flight across chunks and leave 125 partials.
+// 4, 8 — at most kAttnParts partials per head up to 65536 positions.  At 32k positions one chunk
+// per workgroup meant 2000 workgroups per layer and a 10.7 us merge of 500 partials per head
+// (profiles/r05/llm_decode_32k_vs_512_kernels_r05f); four chunks leave 125 partials (merge 6.0 us).
 // The split depends on nothing but the token, so its bits do not depend on its batch.
-constexpr int kAttnParts = 128;
+#ifndef AMDK8S_ATTN_PARTS
+#define AMDK8S_ATTN_PARTS 128
+#endif
+constexpr int kAttnParts = AMDK8S_ATTN_PARTS;
 constexpr int kAttnMaxCpw = 8;
 __host__ __device__ __forceinline__ int attn_cpw(int len) {
   int c = 1;
@@ -256,6 +250,20 @@ inline int comb_groups(int max_ctx) {
   return parts <= kCombBatch ? 1 : parts <= 2 * kCombBatch ? 2 : parts <= 4 * kCombBatch ? 4 : 8;
 }
 
+// cpw chunks of 64 positions per workgroup (attn_cpw).  Each wave streams its own 16
+// positions of every chunk with its own online softmax, so the chunk loop has no barrier; the four
+// waves' (max, sum, output) merge once at the end.  Scores on the matrix cores
+// (v_mfma_f32_16x16x32_f16: A = the q heads as fp16 rows, kept in registers for every chunk, B =
+// the K rows straight from memory, 16 contiguous bytes per lane); P.V on the VALU in fp32, each
+// weight broadcast from the lane that holds it (v_readlane).  q is rounded to fp16 for the MFMA
+// (llama.cpp's flash-attention kernels do the same); scores, softmax and P.V accumulate in fp32.
+// Measured per 28-layer T = 1 step (profiles/r05/README.md): at 32000 positions attention + merge
+// 30.8 -> 25.6 us per layer (the VALU score loop read all G x 128 q values from LDS per position:
+// LDS-bound, 22.7 us streamed vs 20.1 us with one chunk per workgroup); at 512 positions 10.6 ->
+// 12.0 us (occupancy 3 vs 5 waves per SIMD, 139 vs 93 VGPRs).
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
 template <int G>
 __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   const float* __restrict__ q = a.q;
@@ -270,9 +278,8 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   __shared__ float qs[G][kHeadDim];
   __shared__ __align__(16) uint16_t knew[kHeadDim];   // the new position's rotated K (fp16)
   __shared__ __align__(16) uint16_t vnew[kHeadDim];   // and its V
-  __shared__ float ps[2][G][kAttnChunk];              // by chunk parity: two barriers per chunk
-  __shared__ float alph[2][G];
-  __shared__ float opart[4][G][kHeadDim];
+  __shared__ float wml[4][G][2];                      // per wave: running max, sum
+  __shared__ float wo[4][G][kHeadDim];                // per wave: unnormalised output
   const int kh = blockIdx.x, sp = blockIdx.y, t = blockIdx.z;
   const int len = pos[t] + 1;
   const int cpw = attn_cpw(len);
@@ -282,34 +289,30 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   const long pidx = ((long)t * H + kh * G) * nsplit + sp;   // + g * nsplit
   const long cbase = ((long)slot[t] * Hkv + kh) * max_ctx * kHeadDim;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int pi = threadIdx.x >> 2, qd = threadIdx.x & 3;
-  // chunk c's rows.  Scores: 4 lanes per position, 32 dims each; P.V: wave w → positions
-  // w*16 .. w*16+15, lane = 2 dims.  Every load is unconditional: a load under a divergent branch
-  // ends its basic block and the join waits for it.  The V rows are one base address plus
-  // immediate offsets (a per-row clamp kept 16 row indices live across the loop); rows past the
-  // token are still inside the cache (max_ctx % 64 == 0) and are zeroed before use.
-  auto load_chunk = [&](int c, uint4 (&kv)[4], uint32_t (&vv)[16]) __attribute__((always_inline)) {
-    const int p0 = w0 + c * kAttnChunk, n = min(kAttnChunk, len - p0);
-    const uint4* kr = reinterpret_cast<const uint4*>(kc + cbase + (long)(p0 + min(pi, n - 1))
-                                                     * kHeadDim + qd * 32);
+  const int pr = lane & 15, kg = lane >> 4;             // MFMA column (position) / K-group
+  // this wave's 16 positions of chunk c: K rows (lane: position pr, dims 32 s + 8 kg .. + 7 for
+  // s = 0..3) and V rows (lane: dims 2 lane, 2 lane + 1 of each of the 16).  Unconditional loads:
+  // K positions clamped into the token, V rows past it are inside the cache (max_ctx % 64 == 0)
+  // and zeroed before use.
+  auto load_rows = [&](int c, uint4 (&kr)[4], uint32_t (&vr)[16]) __attribute__((always_inline)) {
+    const int pb = w0 + c * kAttnChunk + wave * 16;
+    const uint4* kp = reinterpret_cast<const uint4*>(kc + cbase + (long)min(pb + pr, len - 1)
+                                                     * kHeadDim) + kg;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) kv[e] = kr[e];
-    const uint32_t* vr = reinterpret_cast<const uint32_t*>(
-        vc + cbase + (long)(p0 + wave * 16) * kHeadDim) + lane;
+    for (int s = 0; s < 4; ++s) kr[s] = kp[4 * s];
+    const uint32_t* vp = reinterpret_cast<const uint32_t*>(vc + cbase + (long)pb * kHeadDim) + lane;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) vv[j] = vr[j * (kHeadDim / 2)];
+    for (int j = 0; j < 16; ++j) vr[j] = vp[j * (kHeadDim / 2)];
   };
-  uint4 kv[4];
-  uint32_t vv[16];
-  load_chunk(0, kv, vv);                                // K and V of chunk 0 before any q work
+  uint4 ka[4];
+  uint32_t va[16];
+  load_rows(0, ka, va);                                 // chunk 0 in flight during the q work
   const int pnew = len - 1;
   const bool own = a.qkv != nullptr && pnew >= w0 && pnew < w0 + kAttnChunk * cpw;
   if (a.qkv) {
     const float* row = a.qkv + (long)t * a.ldq;
     const float* ct = a.cos_t + (long)pnew * (kHeadDim / 2);
     const float* st = a.sin_t + (long)pnew * (kHeadDim / 2);
-    // every load of the q rotation and of the new k / v row in flight at once (indices clamped,
-    // no load under a branch), then the maths and the stores
     constexpr int QR = (G * (kHeadDim / 2) + 255) / 256;   // rotation pairs per thread
     float qx0[QR], qx1[QR], qc[QR], qsn[QR];
 #pragma unroll
@@ -354,137 +357,133 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
       qs[i / kHeadDim][i % kHeadDim] = q[(long)t * H * kHeadDim + (kh * G) * kHeadDim + i] * scale;
   }
   __syncthreads();
-  // online softmax over the chunks: the running max / sum of head g live in wave g % 4 (slot
-  // g / 4); every wave rescales its P.V accumulators by the chunk's alpha = exp(M_old - M_new).
-  // One chunk (cpw = 1, every length <= 8192) gives exactly the single-chunk arithmetic.
-  constexpr int GW = (G + 3) / 4;
-  float mrun[GW], lrun[GW];
+  // A fragments: q head pr (zero rows past G), dims 32 s + 8 kg .. + 7, fp16
+  h8 qa[4];
 #pragma unroll
-  for (int k = 0; k < GW; ++k) { mrun[k] = -INFINITY; lrun[k] = 0.f; }
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      qa[s][j] = (_Float16)(pr < G ? qs[min(pr, G - 1)][32 * s + 8 * kg + j] : 0.f);
+  // running max / sum of head rows 4 kg + i (the same in the 16 lanes of a K-group), output dims
+  // 2 lane, 2 lane + 1 of every head
+  float mrun[4], lrun[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { mrun[i] = -INFINITY; lrun[i] = 0.f; }
   float o[G][2];
 #pragma unroll
   for (int g = 0; g < G; ++g) o[g][0] = o[g][1] = 0.f;
-#pragma unroll 1
-  for (int c = 0; c < nc; ++c) {
-    uint4 kn[4];
-    uint32_t vn[16];
-    // the next chunk in flight during this one's maths (the last chunk re-reads itself from L2:
-    // a branch here or around the swap below splits the loop body, and the scheduler then
-    // issues every P.V weight read ahead of the FMAs — 256 VGPRs at G = 7)
-    load_chunk(min(c + 1, nc - 1), kn, vn);
-    // q stays in LDS: without this compiler barrier the loop-invariant q reads (G x 32 floats per
-    // thread) are hoisted into registers — 256 VGPRs, one wave per SIMD
-    __asm__ volatile("" ::: "memory");
-    const int p0 = w0 + c * kAttnChunk, n = min(kAttnChunk, len - p0), par = c & 1;
-    const int jn = pnew - p0;                           // the new position in this chunk?
-    if (own && jn >= 0 && jn < kAttnChunk) {           // its rows were loaded before they were written
-      uint4 kq[4];                                      // (uniform branch, per-lane selects)
+  auto chunk = [&](int c, uint4 (&kr)[4], uint32_t (&vr)[16]) __attribute__((always_inline)) {
+    const int pb = w0 + c * kAttnChunk + wave * 16;
+    const int jn = pnew - pb;                           // the new position among these 16?
+    if (own && jn >= 0 && jn < 16) {                    // its rows were loaded before they were written
+      uint4 kq[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) kq[e] = reinterpret_cast<const uint4*>(knew)[qd * 4 + e];
+      for (int s = 0; s < 4; ++s) kq[s] = reinterpret_cast<const uint4*>(knew)[4 * s + kg];
       const uint32_t vq = reinterpret_cast<const uint32_t*>(vnew)[lane];
+      const bool nw = pr == jn;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {                    // per component: a select of two uint4
-        const bool nw = pi == jn;                       // lvalues is a pointer select (scratch)
-        kv[e].x = nw ? kq[e].x : kv[e].x;
-        kv[e].y = nw ? kq[e].y : kv[e].y;
-        kv[e].z = nw ? kq[e].z : kv[e].z;
-        kv[e].w = nw ? kq[e].w : kv[e].w;
+      for (int s = 0; s < 4; ++s) {                     // per component (a uint4 select is a
+        kr[s].x = nw ? kq[s].x : kr[s].x;               // pointer select: scratch)
+        kr[s].y = nw ? kq[s].y : kr[s].y;
+        kr[s].z = nw ? kq[s].z : kr[s].z;
+        kr[s].w = nw ? kq[s].w : kr[s].w;
       }
 #pragma unroll
-      for (int j = 0; j < 16; ++j) vv[j] = j == jn - wave * 16 ? vq : vv[j];
+      for (int j = 0; j < 16; ++j) vr[j] = j == jn ? vq : vr[j];
     }
-    {
-      const int nv = n - wave * 16;                     // rows past the token: 0 (ps is 0 there)
+    const int nv = len - pb;                            // rows of these 16 inside the token
 #pragma unroll
-      for (int j = 0; j < 16; ++j) vv[j] = j < nv ? vv[j] : 0u;
+    for (int j = 0; j < 16; ++j) vr[j] = j < nv ? vr[j] : 0u;
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      h8 kb;
+      __builtin_memcpy(&kb, &kr[s], sizeof(kb));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(qa[s], kb, acc, 0, 0, 0);
     }
-    float sc[G];
+    // acc[i] = score of head 4 kg + i at position pb + pr
+    float p[4], al[4];
 #pragma unroll
-    for (int g = 0; g < G; ++g) sc[g] = 0.f;
+    for (int i = 0; i < 4; ++i) {
+      const float s = pr < nv ? acc[i] : -INFINITY;
+      float mx = s;
 #pragma unroll
-    for (int e4 = 0; e4 < 4; ++e4) {
-      const uint32_t kw[4] = {kv[e4].x, kv[e4].y, kv[e4].z, kv[e4].w};
-      float kf[8];
+      for (int x = 1; x < 16; x <<= 1) mx = fmaxf(mx, __shfl_xor(mx, x, 16));
+      const float mn = fmaxf(mrun[i], mx);
+      const float mref = mn == -INFINITY ? 0.f : mn;    // nothing attended yet: every term is 0
+      p[i] = __expf(s - mref);
+      al[i] = __expf(mrun[i] - mref);
+      float ls = p[i];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        kf[2 * e] = h2f(kw[e] & 0xffffu);
-        kf[2 * e + 1] = h2f(kw[e] >> 16);
-      }
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sc[g] += kf[e] * qs[g][qd * 32 + e4 * 8 + e];
-      }
+      for (int x = 1; x < 16; x <<= 1) ls += __shfl_xor(ls, x, 16);
+      lrun[i] = lrun[i] * al[i] + ls;
+      mrun[i] = mn;
     }
+    // P.V: weight (head g, position j) is p[g & 3] of lane j + 16 (g >> 2)
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      sc[g] += __shfl_xor(sc[g], 1, kWave);
-      sc[g] += __shfl_xor(sc[g], 2, kWave);
-    }
-    if (qd == 0) {
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-        ps[par][g][pi] = pi < n ? sc[g] : -INFINITY;
-    }
-    __syncthreads();
-    // softmax: head g on wave g % 4 (lane = position), LDS-free cross-lane max / sum
-#pragma unroll
-    for (int k = 0; k < GW; ++k) {
-      const int g = 4 * k + wave;
-      if (g < G) {
-        const float s = ps[par][g][lane];
-        const float mn = fmaxf(mrun[k], wave_max_fast(s));
-        const float p = lane < n ? __expf(s - mn) : 0.f;
-        ps[par][g][lane] = p;
-        const float al = __expf(mrun[k] - mn);          // 0 for the first chunk
-        lrun[k] = lrun[k] * al + wave_sum_fast(p);
-        mrun[k] = mn;
-        if (lane == 0) alph[par][g] = al;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const float al = alph[par][g];
-      o[g][0] *= al;
-      o[g][1] *= al;
+      const float a2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(al[g & 3]), 16 * (g >> 2)));
+      o[g][0] *= a2;
+      o[g][1] *= a2;
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const float v0 = h2f(vv[j] & 0xffffu), v1 = h2f(vv[j] >> 16);
+      const float v0 = h2f(vr[j] & 0xffffu), v1 = h2f(vr[j] >> 16);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        const float pw = ps[par][g][wave * 16 + j];
+        const float pw = __int_as_float(
+            __builtin_amdgcn_readlane(__float_as_int(p[g & 3]), j + 16 * (g >> 2)));
         o[g][0] += pw * v0;
         o[g][1] += pw * v1;
       }
     }
+  };
+  // ping-pong register buffers, the next chunk's loads issued before this chunk's maths.  A copy
+  // between the buffers would wait for the loads it copies (every chunk a full HBM round trip),
+  // and a load under a branch leaves the wait counter unknown at the join, where the compiler
+  // then waits for it too — so the loads past the last chunk are issued anyway, clamped to it
+  // (an L2 re-read).
+  uint4 kb[4];
+  uint32_t vb[16];
+#pragma unroll 1
+  for (int c = 0; c < nc; c += 2) {
+    load_rows(min(c + 1, nc - 1), kb, vb);
+    chunk(c, ka, va);
+    load_rows(min(c + 2, nc - 1), ka, va);
+    if (c + 1 < nc) chunk(c + 1, kb, vb);
+  }
+  // merge the four waves
+  if (pr == 0) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) kv[e] = kn[e];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) vv[j] = vn[j];
+    for (int i = 0; i < 4; ++i) {
+      const int g = 4 * kg + i;
+      if (g < G) { wml[wave][g][0] = mrun[i]; wml[wave][g][1] = lrun[i]; }
+    }
   }
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    opart[wave][g][2 * lane] = o[g][0];
-    opart[wave][g][2 * lane + 1] = o[g][1];
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < GW; ++k) {
-      const int g = 4 * k + wave;
-      if (g < G) {
-        float* dst = pml + (pidx + (long)g * nsplit) * 2;
-        dst[0] = mrun[k];
-        dst[1] = lrun[k];
-      }
-    }
+    wo[wave][g][2 * lane] = o[g][0];
+    wo[wave][g][2 * lane + 1] = o[g][1];
   }
   __syncthreads();
   for (int i = threadIdx.x; i < G * kHeadDim; i += blockDim.x) {
     const int g = i / kHeadDim, dd = i % kHeadDim;
-    const float v = opart[0][g][dd] + opart[1][g][dd] + opart[2][g][dd] + opart[3][g][dd];
+    float m = wml[0][g][0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) m = fmaxf(m, wml[w][g][0]);
+    float v = 0.f, l = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float e = wml[w][g][0] == -INFINITY ? 0.f : __expf(wml[w][g][0] - m);
+      v += e * wo[w][g][dd];
+      l += e * wml[w][g][1];
+    }
     po[(pidx + (long)g * nsplit) * kHeadDim + dd] = v;
+    if (dd == 0) {
+      float* dst = pml + (pidx + (long)g * nsplit) * 2;
+      dst[0] = m;
+      dst[1] = l;
+    }
   }
 }
 

@@ -420,9 +420,20 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
   }
 }
 
+// A/B knobs (build-time): the pair kernel's ring depth and its waves-per-SIMD floor.  D = 3 needs
+// 2 waves/SIMD (214 VGPRs; at 3 it spills): T = 1 1.680 -> 1.739 ms, T = 4 2.046 -> 2.065 ms
+// (gate|up's 592 workgroups no longer co-resident; session r05g)
+#ifndef AMDK8S_PAIR_D
+#define AMDK8S_PAIR_D 2
+#endif
+#ifndef AMDK8S_PAIR_WPE
+#define AMDK8S_PAIR_WPE 3
+#endif
+constexpr int kPairD = AMDK8S_PAIR_D;
+
 template <int TYPE, int T, int MODE, int KW, int RG, int D>
 __global__ void __launch_bounds__(KW * RG * 64)
-__attribute__((amdgpu_waves_per_eu(MODE == kPair && T <= 4 ? 3 : 1, 8)))
+__attribute__((amdgpu_waves_per_eu(MODE == kPair && T <= 4 ? AMDK8S_PAIR_WPE : 1, 8)))
 qgemv_mfma_kernel(GemvArgs a) {
   qgemv_mfma_body<TYPE, T, MODE, KW, RG, D>(a, blockIdx.x);
 }
@@ -483,7 +494,7 @@ template <int TYPE, int T, int MODE, int KW, int RG>
 int launch_mfma_one(const GemvArgs& a, hipStream_t st) {
   // ring depth: pair 2 (two matrices per slot, 3 waves/SIMD), else 3 (6 for ffn_down's 8-wave
   // shape measured slower: Q6_K 13.9 -> 15.6 us, T = 1 1.629 -> 1.656 ms, profiles/r04/o)
-  constexpr int D = MODE == kPair ? 2 : 3;
+  constexpr int D = MODE == kPair ? kPairD : 3;
   const int nb = a.K >> 8, sk = a.ksplit > 1 ? a.ksplit : 1;
   if (nb / sk < KW) return 4;                      // every wave of every slice gets a block
   if (sk > 1 && (MODE == kPair || a.xf || !a.kpart || !a.kcnt)) return 2;

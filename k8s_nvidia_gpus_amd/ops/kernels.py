@@ -15,6 +15,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+from pathlib import Path
 from typing import Optional
 
 import torch
@@ -103,9 +104,10 @@ def library(build_if_missing: bool = True) -> ctypes.CDLL:
     with _lock:
         if _lib is not None:
             return _lib
-        path = _build.KERNEL_LIB
-        stale = (not path.exists()) or any(
-            s.stat().st_mtime > path.stat().st_mtime for s in _build.kernel_sources())
+        alt = os.environ.get("AMDK8S_KERNEL_LIB")     # A/B: a variant build of the same sources
+        path = Path(alt) if alt else _build.KERNEL_LIB
+        stale = not alt and ((not path.exists()) or any(
+            s.stat().st_mtime > path.stat().st_mtime for s in _build.kernel_sources()))
         if stale and build_if_missing and _build.toolchain_available() \
                 and os.environ.get("AMDK8S_NO_BUILD") != "1":
             _build.build_kernel_library()
