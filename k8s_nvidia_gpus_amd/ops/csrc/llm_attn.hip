@@ -10,13 +10,19 @@ namespace {
 // kv head over cpw consecutive 64-position chunks (one partial); writes the unnormalised partial
 // output and (max, sum) per head (attn_decode_kernel).
 //
-// Chunks per workgroup (cpw) follow the token's own length only: 1 up to 8192 positions, then 2,
-// 4, 8 — at most kAttnParts partials per head up to 65536 positions.  At 32k positions one chunk
-// per workgroup meant 2000 workgroups per layer and a 10.7 us merge of 500 partials per head
-// (profiles/r05/llm_decode_32k_vs_512_kernels_r05f); four chunks leave 125 partials (merge 6.0 us).
+// Chunks per workgroup (cpw) follow the token's own length only: 1 up to 4096 positions, then 2,
+// 4, 8 — at most kAttnParts = 64 partials per head up to 32768 positions.  At 32k positions one
+// chunk per workgroup meant 2000 workgroups per layer and a 10.7 us merge of 500 partials per head
+// (profiles/r05/llm_decode_32k_vs_512_kernels_r05f).  Swept at 32000 positions (session r05n,
+// T = 1 / 4 / 8 tok/s): 128 partials 475 / 1119 / 1321, 64 partials 482 / 1181 / 1397; a third
+// chunk buffer per wave (kAttnRing 3) lost at both (212 VGPRs).
 // The split depends on nothing but the token, so its bits do not depend on its batch.
+#ifndef AMDK8S_ATTN_RING
+#define AMDK8S_ATTN_RING 2
+#endif
+constexpr int kAttnRing = AMDK8S_ATTN_RING;           // chunk buffers per wave (attn_decode_kernel)
 #ifndef AMDK8S_ATTN_PARTS
-#define AMDK8S_ATTN_PARTS 128
+#define AMDK8S_ATTN_PARTS 64
 #endif
 constexpr int kAttnParts = AMDK8S_ATTN_PARTS;
 constexpr int kAttnMaxCpw = 8;
@@ -158,8 +164,8 @@ __global__ void __launch_bounds__(128) attn_combine_q8_kernel(const float* __res
 // on this token's own chunk count, and G only on the engine's max_ctx (the launcher), so a token's
 // bits never depend on the batch it runs in.  At 32k positions with one chunk per
 // partial (512 per head) the 128-thread form took 16 dependent row batches per head (~1 ms per
-// 28-layer step at T = 1, profiles/r05); with streamed chunks (<= 128 partials up to 65536
-// positions) four groups take one batch each.
+// 28-layer step at T = 1, profiles/r05); with streamed chunks (<= 64 partials up to 32768
+// positions) two groups take one batch each.
 constexpr int kCombBatch = 32;
 constexpr int kCombMaxSplit = 1024;                 // max_ctx <= 524288 (8 chunks per partial)
 
@@ -244,28 +250,45 @@ __global__ void __launch_bounds__(128 * G) attn_combine2_q8_kernel(const float* 
 }
 
 // Row groups of the merge for an engine whose KV cache holds max_ctx positions: one row batch
-// per group at the engine's longest partial count (128 partials, every max_ctx >= 8192: 4 groups).
+// per group at the engine's longest partial count (64 partials, every max_ctx >= 4096: 2 groups).
 inline int comb_groups(int max_ctx) {
   const int parts = attn_parts_max(max_ctx);
   return parts <= kCombBatch ? 1 : parts <= 2 * kCombBatch ? 2 : parts <= 4 * kCombBatch ? 4 : 8;
 }
 
-// cpw chunks of 64 positions per workgroup (attn_cpw).  Each wave streams its own 16
-// positions of every chunk with its own online softmax, so the chunk loop has no barrier; the four
-// waves' (max, sum, output) merge once at the end.  Scores on the matrix cores
-// (v_mfma_f32_16x16x32_f16: A = the q heads as fp16 rows, kept in registers for every chunk, B =
-// the K rows straight from memory, 16 contiguous bytes per lane); P.V on the VALU in fp32, each
-// weight broadcast from the lane that holds it (v_readlane).  q is rounded to fp16 for the MFMA
-// (llama.cpp's flash-attention kernels do the same); scores, softmax and P.V accumulate in fp32.
-// Measured per 28-layer T = 1 step (profiles/r05/README.md): at 32000 positions attention + merge
-// 30.8 -> 25.6 us per layer (the VALU score loop read all G x 128 q values from LDS per position:
-// LDS-bound, 22.7 us streamed vs 20.1 us with one chunk per workgroup); at 512 positions 10.6 ->
-// 12.0 us (occupancy 3 vs 5 waves per SIMD, 139 vs 93 VGPRs).
+// cpw chunks of 64 positions per workgroup (attn_cpw).  Each wave streams its own 16 positions of
+// every chunk with its own online softmax, so the chunk loop has no barrier; the four waves'
+// (max, sum, output) merge once at the end.  Both products run on the matrix cores:
+// * scores S^T = K q^T (v_mfma_f32_16x16x32_f16): A = the K rows straight from memory (16
+//   contiguous bytes per lane), B = the q heads as fp16, held in registers for every chunk; lane l
+//   gets head l & 15 at positions 4 (l >> 4) .. + 3, so each lane keeps the online max / sum of
+//   one head;
+// * O += P V (v_mfma_f32_16x16x16_f16): A = those P values as they lie (fp16), B = the V rows,
+//   loaded as whole 1 KiB row groups, written to a per-wave LDS image and read back transposed
+//   with ds_read_b64_tr_b16 (cdna_hip_programming.md T10; the XOR-swizzled 256-byte-row image of
+//   its "(b)" layout).
+// q and P are rounded to fp16 for the MFMA (llama.cpp's flash-attention kernels do the same);
+// scores, softmax and the output accumulate in fp32.  History (profiles/r05/README.md): one
+// chunk per workgroup on the VALU took 20.1 + 10.7 us (attention + merge) per 32k layer; VALU
+// scores read every q value from LDS once per position (LDS-bound, 22.7 us streamed); MFMA
+// scores with a v_readlane VALU P.V 19.6 + 6.0 us.
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4 lds_s4;
 
+// byte offset of 16-byte chunk ch (0..15) of row `row` in a [16][128 x fp16] V image
+__device__ __forceinline__ int vimg_off(int row, int ch) {
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+#ifndef AMDK8S_ATTN_WPE
+#define AMDK8S_ATTN_WPE 1
+#endif
 template <int G>
-__global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMDK8S_ATTN_WPE)))
+attn_decode_kernel(AttnArgs a) {
   const float* __restrict__ q = a.q;
   const int* __restrict__ pos = a.pos;
   const int* __restrict__ slot = a.slot;
@@ -278,7 +301,8 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   __shared__ float qs[G][kHeadDim];
   __shared__ __align__(16) uint16_t knew[kHeadDim];   // the new position's rotated K (fp16)
   __shared__ __align__(16) uint16_t vnew[kHeadDim];   // and its V
-  __shared__ float wml[4][G][2];                      // per wave: running max, sum
+  __shared__ __align__(16) uint8_t vimg[4][16 * 256]; // per wave: the chunk's V rows
+  __shared__ float wml[4][16][2];                     // per wave: running max, sum per head
   __shared__ float wo[4][G][kHeadDim];                // per wave: unnormalised output
   const int kh = blockIdx.x, sp = blockIdx.y, t = blockIdx.z;
   const int len = pos[t] + 1;
@@ -289,24 +313,27 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
   const long pidx = ((long)t * H + kh * G) * nsplit + sp;   // + g * nsplit
   const long cbase = ((long)slot[t] * Hkv + kh) * max_ctx * kHeadDim;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int pr = lane & 15, kg = lane >> 4;             // MFMA column (position) / K-group
-  // this wave's 16 positions of chunk c: K rows (lane: position pr, dims 32 s + 8 kg .. + 7 for
-  // s = 0..3) and V rows (lane: dims 2 lane, 2 lane + 1 of each of the 16).  Unconditional loads:
-  // K positions clamped into the token, V rows past it are inside the cache (max_ctx % 64 == 0)
-  // and zeroed before use.
-  auto load_rows = [&](int c, uint4 (&kr)[4], uint32_t (&vr)[16]) __attribute__((always_inline)) {
+  const int pr = lane & 15, kg = lane >> 4;
+  // this wave's 16 positions of chunk c.  K: lane = (position pr, dims 32 s + 8 kg .. + 7 for
+  // s = 0..3), positions clamped into the token.  V: lane = (row 4 r + kg, dims 8 pr .. + 7 for
+  // r = 0..3): 1 KiB contiguous per instruction; rows past the token are inside the cache
+  // (max_ctx % 64 == 0) and zeroed before use.  Every load unconditional.
+  auto load_rows = [&](int c, uint4 (&kr)[4], uint4 (&vr)[4]) __attribute__((always_inline)) {
     const int pb = w0 + c * kAttnChunk + wave * 16;
     const uint4* kp = reinterpret_cast<const uint4*>(kc + cbase + (long)min(pb + pr, len - 1)
                                                      * kHeadDim) + kg;
 #pragma unroll
     for (int s = 0; s < 4; ++s) kr[s] = kp[4 * s];
-    const uint32_t* vp = reinterpret_cast<const uint32_t*>(vc + cbase + (long)pb * kHeadDim) + lane;
+    const uint4* vp = reinterpret_cast<const uint4*>(vc + cbase + (long)(pb + kg) * kHeadDim) + pr;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) vr[j] = vp[j * (kHeadDim / 2)];
+    for (int r = 0; r < 4; ++r) vr[r] = vp[r * 4 * (kHeadDim / 8)];
   };
-  uint4 ka[4];
-  uint32_t va[16];
-  load_rows(0, ka, va);                                 // chunk 0 in flight during the q work
+  // ring of R chunk buffers (R - 1 chunks in flight during a chunk's maths), constant indices
+  uint4 kr[kAttnRing][4];
+  uint4 vr[kAttnRing][4];
+#pragma unroll
+  for (int r = 0; r < kAttnRing - 1; ++r)               // in flight during the q work
+    load_rows(min(r, nc - 1), kr[r], vr[r]);
   const int pnew = len - 1;
   const bool own = a.qkv != nullptr && pnew >= w0 && pnew < w0 + kAttnChunk * cpw;
   if (a.qkv) {
@@ -357,114 +384,123 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
       qs[i / kHeadDim][i % kHeadDim] = q[(long)t * H * kHeadDim + (kh * G) * kHeadDim + i] * scale;
   }
   __syncthreads();
-  // A fragments: q head pr (zero rows past G), dims 32 s + 8 kg .. + 7, fp16
+  // B fragments of the scores: q head pr (zero rows past G), dims 32 s + 8 kg .. + 7, fp16
   h8 qa[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s)
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       qa[s][j] = (_Float16)(pr < G ? qs[min(pr, G - 1)][32 * s + 8 * kg + j] : 0.f);
-  // running max / sum of head rows 4 kg + i (the same in the 16 lanes of a K-group), output dims
-  // 2 lane, 2 lane + 1 of every head
-  float mrun[4], lrun[4];
+  float mrun = -INFINITY, lrun = 0.f;                   // head pr
+  f4 o[8];                                              // O[head 4 kg + i][dim 16 n + pr]
 #pragma unroll
-  for (int i = 0; i < 4; ++i) { mrun[i] = -INFINITY; lrun[i] = 0.f; }
-  float o[G][2];
-#pragma unroll
-  for (int g = 0; g < G; ++g) o[g][0] = o[g][1] = 0.f;
-  auto chunk = [&](int c, uint4 (&kr)[4], uint32_t (&vr)[16]) __attribute__((always_inline)) {
+  for (int n = 0; n < 8; ++n) o[n] = f4{0.f, 0.f, 0.f, 0.f};
+  uint8_t* img = vimg[wave];
+  // transposed-read address of n-tile 0 (lane 4 q + p of its 16-lane group: row 4 kg + q,
+  // columns 4 p .. 4 p + 3 of the tile); tile n adds 2 chunks, which the XOR keeps inside the
+  // same 64-byte half-row pair only up to the swizzle: recomputed per tile (constants fold)
+  const int tq = pr >> 2, tp = pr & 3;
+  auto chunk = [&](int c, uint4 (&kb)[4], uint4 (&vb)[4]) __attribute__((always_inline)) {
     const int pb = w0 + c * kAttnChunk + wave * 16;
     const int jn = pnew - pb;                           // the new position among these 16?
     if (own && jn >= 0 && jn < 16) {                    // its rows were loaded before they were written
       uint4 kq[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) kq[s] = reinterpret_cast<const uint4*>(knew)[4 * s + kg];
-      const uint32_t vq = reinterpret_cast<const uint32_t*>(vnew)[lane];
+      const uint4 vq = reinterpret_cast<const uint4*>(vnew)[pr];
       const bool nw = pr == jn;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {                     // per component (a uint4 select is a
-        kr[s].x = nw ? kq[s].x : kr[s].x;               // pointer select: scratch)
-        kr[s].y = nw ? kq[s].y : kr[s].y;
-        kr[s].z = nw ? kq[s].z : kr[s].z;
-        kr[s].w = nw ? kq[s].w : kr[s].w;
+        kb[s].x = nw ? kq[s].x : kb[s].x;               // pointer select: scratch)
+        kb[s].y = nw ? kq[s].y : kb[s].y;
+        kb[s].z = nw ? kq[s].z : kb[s].z;
+        kb[s].w = nw ? kq[s].w : kb[s].w;
       }
 #pragma unroll
-      for (int j = 0; j < 16; ++j) vr[j] = j == jn ? vq : vr[j];
+      for (int r = 0; r < 4; ++r) {
+        const bool vw = 4 * r + kg == jn;
+        vb[r].x = vw ? vq.x : vb[r].x;
+        vb[r].y = vw ? vq.y : vb[r].y;
+        vb[r].z = vw ? vq.z : vb[r].z;
+        vb[r].w = vw ? vq.w : vb[r].w;
+      }
     }
     const int nv = len - pb;                            // rows of these 16 inside the token
 #pragma unroll
-    for (int j = 0; j < 16; ++j) vr[j] = j < nv ? vr[j] : 0u;
+    for (int r = 0; r < 4; ++r) {
+      const bool in = 4 * r + kg < nv;
+      const uint4 z = in ? vb[r] : make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4*>(img + vimg_off(4 * r + kg, pr)) = z;
+    }
+    // scores: acc[i] = S[position 4 kg + i][head pr]
     f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      h8 kb;
-      __builtin_memcpy(&kb, &kr[s], sizeof(kb));
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(qa[s], kb, acc, 0, 0, 0);
+      h8 ka;
+      __builtin_memcpy(&ka, &kb[s], sizeof(ka));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ka, qa[s], acc, 0, 0, 0);
     }
-    // acc[i] = score of head 4 kg + i at position pb + pr
-    float p[4], al[4];
+    float sc[4];
+    float mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float s = pr < nv ? acc[i] : -INFINITY;
-      float mx = s;
-#pragma unroll
-      for (int x = 1; x < 16; x <<= 1) mx = fmaxf(mx, __shfl_xor(mx, x, 16));
-      const float mn = fmaxf(mrun[i], mx);
-      const float mref = mn == -INFINITY ? 0.f : mn;    // nothing attended yet: every term is 0
-      p[i] = __expf(s - mref);
-      al[i] = __expf(mrun[i] - mref);
-      float ls = p[i];
-#pragma unroll
-      for (int x = 1; x < 16; x <<= 1) ls += __shfl_xor(ls, x, 16);
-      lrun[i] = lrun[i] * al[i] + ls;
-      mrun[i] = mn;
+      sc[i] = 4 * kg + i < nv ? acc[i] : -INFINITY;
+      mx = fmaxf(mx, sc[i]);
     }
-    // P.V: weight (head g, position j) is p[g & 3] of lane j + 16 (g >> 2)
+    mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+    const float mn = fmaxf(mrun, mx);
+    const float mref = mn == -INFINITY ? 0.f : mn;      // nothing attended yet: every term is 0
+    const float al = __expf(mrun - mref);
+    h4 pa;
+    float ls = 0.f;
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const float a2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(al[g & 3]), 16 * (g >> 2)));
-      o[g][0] *= a2;
-      o[g][1] *= a2;
+    for (int i = 0; i < 4; ++i) {
+      const float p = __expf(sc[i] - mref);
+      pa[i] = (_Float16)p;
+      ls += p;
     }
+    ls += __shfl_xor(ls, 16, kWave);
+    ls += __shfl_xor(ls, 32, kWave);
+    lrun = lrun * al + ls;
+    mrun = mn;
+    // rescale: output row 4 kg + i takes the alpha of head 4 kg + i (lane 4 kg + i)
+    f4 a4;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float v0 = h2f(vr[j] & 0xffffu), v1 = h2f(vr[j] >> 16);
+    for (int i = 0; i < 4; ++i) a4[i] = __shfl(al, 4 * kg + i, kWave);
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const float pw = __int_as_float(
-            __builtin_amdgcn_readlane(__float_as_int(p[g & 3]), j + 16 * (g >> 2)));
-        o[g][0] += pw * v0;
-        o[g][1] += pw * v1;
-      }
+    for (int n = 0; n < 8; ++n) o[n] *= a4;
+    // P.V: B = V[position 4 kg + j][dim 16 n + pr] from the image, transposed
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const int off = vimg_off(4 * kg + tq, 2 * n + (tp >> 1)) + 8 * (tp & 1);
+      const s4 braw = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + off));
+      h4 bv;
+      __builtin_memcpy(&bv, &braw, sizeof(bv));
+      o[n] = __builtin_amdgcn_mfma_f32_16x16x16f16(pa, bv, o[n], 0, 0, 0);
     }
   };
-  // ping-pong register buffers, the next chunk's loads issued before this chunk's maths.  A copy
-  // between the buffers would wait for the loads it copies (every chunk a full HBM round trip),
-  // and a load under a branch leaves the wait counter unknown at the join, where the compiler
-  // then waits for it too — so the loads past the last chunk are issued anyway, clamped to it
-  // (an L2 re-read).
-  uint4 kb[4];
-  uint32_t vb[16];
+  // the ring: before each chunk's maths, the load of the chunk R - 1 ahead goes into the slot
+  // consumed one step ago.  A copy between buffers would wait for the loads it copies (every chunk
+  // a full HBM round trip), and a load under a branch leaves the wait counter unknown at the join,
+  // where the compiler then waits for it too — so the loads past the last chunk are issued
+  // anyway, clamped to it (an L2 re-read).
 #pragma unroll 1
-  for (int c = 0; c < nc; c += 2) {
-    load_rows(min(c + 1, nc - 1), kb, vb);
-    chunk(c, ka, va);
-    load_rows(min(c + 2, nc - 1), ka, va);
-    if (c + 1 < nc) chunk(c + 1, kb, vb);
-  }
-  // merge the four waves
-  if (pr == 0) {
+  for (int c = 0; c < nc; c += kAttnRing) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int g = 4 * kg + i;
-      if (g < G) { wml[wave][g][0] = mrun[i]; wml[wave][g][1] = lrun[i]; }
+    for (int r = 0; r < kAttnRing; ++r) {
+      const int nx = (r + kAttnRing - 1) % kAttnRing;
+      load_rows(min(c + r + kAttnRing - 1, nc - 1), kr[nx], vr[nx]);
+      if (r == 0 || c + r < nc) chunk(c + r, kr[r], vr[r]);
     }
   }
+  // merge the four waves
+  if (kg == 0) { wml[wave][pr][0] = mrun; wml[wave][pr][1] = lrun; }
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    wo[wave][g][2 * lane] = o[g][0];
-    wo[wave][g][2 * lane + 1] = o[g][1];
-  }
+  for (int n = 0; n < 8; ++n)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (4 * kg + i < G) wo[wave][min(4 * kg + i, G - 1)][16 * n + pr] = o[n][i];
   __syncthreads();
   for (int i = threadIdx.x; i < G * kHeadDim; i += blockDim.x) {
     const int g = i / kHeadDim, dd = i % kHeadDim;

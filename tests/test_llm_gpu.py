@@ -401,8 +401,8 @@ def test_rope_kv_and_decode_attention(dev, LK, H, Hkv):
 
 @pytest.mark.parametrize("max_ctx", [4096, 32768, 65536, 131072])
 def test_decode_attention_long_context(dev, LK, max_ctx):
-    """Streamed chunks per workgroup (1 up to 8192 positions, then 2 / 4 / 8: at 70000 positions
-    137 partials of 512) and the merge's row groups (from max_ctx: 2 at 4096, 4 at 32768 / 65536,
+    """Streamed chunks per workgroup (1 up to 4096 positions, then 2 / 4 / 8: at 70000 positions
+    137 partials of 512) and the merge's row groups (from max_ctx: 2 at 4096 / 32768, 4 at 65536,
     8 at 131072) vs the fp32 softmax reference; and a sequence alone gives the bits it gets
     batched with a longer one (the split and the merge follow the token and max_ctx, never the
     launch's span or batch: ADVICE r4)."""
@@ -445,7 +445,7 @@ def test_decode_attention_long_context(dev, LK, max_ctx):
 
 @pytest.mark.parametrize("H,Hkv,max_ctx,positions", [
     (28, 4, 1024, (0, 63, 64, 700)), (8, 8, 1024, (0, 63, 64, 700)),
-    # workgroups of 2 and 4 streamed chunks; the new position in chunk 1, 1, 2 and 3 of its group
+    # workgroups of 4 and 8 streamed chunks; the new position in chunk 1, 1, 2 and 7 of its group
     (28, 4, 32768, (9064, 16500, 20100, 30200))])
 def test_fused_rope_attention_equals_separate_kernels(dev, LK, H, Hkv, max_ctx, positions):
     """Distinct slots: RoPE + KV write inside the attention kernel == rope_kv + attention."""
