@@ -271,23 +271,44 @@ inline int comb_groups(int max_ctx) {
 // scores, softmax and the output accumulate in fp32.  History (profiles/r05/README.md): one
 // chunk per workgroup on the VALU took 20.1 + 10.7 us (attention + merge) per 32k layer; VALU
 // scores read every q value from LDS once per position (LDS-bound, 22.7 us streamed); MFMA
-// scores with a v_readlane VALU P.V 19.6 + 6.0 us.
+// scores with a v_readlane VALU P.V 19.6 + 6.0 us; both products on MFMA with 64 partials per
+// head 17.2 + 5.3 us; q fragments straight from memory (no LDS staging, no barrier) 16.6 + 5.2.
+// Measured and rejected (session r05n / r05t): a third chunk buffer per wave, 8 waves per
+// workgroup (two chunk parities), 128 or 256 partials per head, a 168-VGPR cap (3 waves/SIMD).
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef short s4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4 lds_s4;
 
+// x of lane l ^ 16 / l ^ 32 on the VALU (v_permlane16/32_swap: a half-row exchange; with both
+// operands x, the swapped-in copy is the partner's value): no LDS round trip, unlike __shfl_xor
+__device__ __forceinline__ float lane_xor16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float((threadIdx.x & 16) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float lane_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+}
+
 // byte offset of 16-byte chunk ch (0..15) of row `row` in a [16][128 x fp16] V image
 __device__ __forceinline__ int vimg_off(int row, int ch) {
   return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
 }
 
+#ifndef AMDK8S_ATTN_WAVES
+#define AMDK8S_ATTN_WAVES 4
+#endif
+constexpr int kAttnWaves = AMDK8S_ATTN_WAVES;         // 4 or 8 waves per workgroup
+#ifndef AMDK8S_ATTN_FAST1
+#define AMDK8S_ATTN_FAST1 1
+#endif
 #ifndef AMDK8S_ATTN_WPE
 #define AMDK8S_ATTN_WPE 1
 #endif
 template <int G>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMDK8S_ATTN_WPE)))
+__global__ void __launch_bounds__(64 * kAttnWaves) __attribute__((amdgpu_waves_per_eu(AMDK8S_ATTN_WPE)))
 attn_decode_kernel(AttnArgs a) {
   const float* __restrict__ q = a.q;
   const int* __restrict__ pos = a.pos;
@@ -298,12 +319,12 @@ attn_decode_kernel(AttnArgs a) {
   const float scale = a.scale;
   float* __restrict__ po = a.po;
   float* __restrict__ pml = a.pml;
-  __shared__ float qs[G][kHeadDim];
   __shared__ __align__(16) uint16_t knew[kHeadDim];   // the new position's rotated K (fp16)
   __shared__ __align__(16) uint16_t vnew[kHeadDim];   // and its V
-  __shared__ __align__(16) uint8_t vimg[4][16 * 256]; // per wave: the chunk's V rows
-  __shared__ float wml[4][16][2];                     // per wave: running max, sum per head
-  __shared__ float wo[4][G][kHeadDim];                // per wave: unnormalised output
+  constexpr int NW = kAttnWaves, NT = 64 * NW, NPAR = NW / 4;
+  __shared__ __align__(16) uint8_t vimg[NW][16 * 256];  // per wave: the chunk's V rows
+  __shared__ float wml[NW][16][2];                    // per wave: running max, sum per head
+  __shared__ float wo[NW][G][kHeadDim];               // per wave: unnormalised output
   const int kh = blockIdx.x, sp = blockIdx.y, t = blockIdx.z;
   const int len = pos[t] + 1;
   const int cpw = attn_cpw(len);
@@ -314,17 +335,21 @@ attn_decode_kernel(AttnArgs a) {
   const long cbase = ((long)slot[t] * Hkv + kh) * max_ctx * kHeadDim;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int pr = lane & 15, kg = lane >> 4;
+  // wave = (chunk parity wpar, 16-position slot wsub): it streams chunks wpar, wpar + NPAR, ...
+  const int wsub = wave & 3, wpar = wave >> 2;
+  const int ncw = nc > wpar ? (nc - wpar + NPAR - 1) / NPAR : 0;   // this wave's chunks
   // this wave's 16 positions of chunk c.  K: lane = (position pr, dims 32 s + 8 kg .. + 7 for
   // s = 0..3), positions clamped into the token.  V: lane = (row 4 r + kg, dims 8 pr .. + 7 for
   // r = 0..3): 1 KiB contiguous per instruction; rows past the token are inside the cache
   // (max_ctx % 64 == 0) and zeroed before use.  Every load unconditional.
   auto load_rows = [&](int c, uint4 (&kr)[4], uint4 (&vr)[4]) __attribute__((always_inline)) {
-    const int pb = w0 + c * kAttnChunk + wave * 16;
+    const int pb = w0 + (c * NPAR + wpar) * kAttnChunk + wsub * 16;
     const uint4* kp = reinterpret_cast<const uint4*>(kc + cbase + (long)min(pb + pr, len - 1)
                                                      * kHeadDim) + kg;
 #pragma unroll
     for (int s = 0; s < 4; ++s) kr[s] = kp[4 * s];
-    const uint4* vp = reinterpret_cast<const uint4*>(vc + cbase + (long)(pb + kg) * kHeadDim) + pr;
+    const uint4* vp = reinterpret_cast<const uint4*>(                  // an idle wave's rows may
+        vc + cbase + (long)(min(pb, max_ctx - 16) + kg) * kHeadDim) + pr;  // pass max_ctx: clamped
 #pragma unroll
     for (int r = 0; r < 4; ++r) vr[r] = vp[r * 4 * (kHeadDim / 8)];
   };
@@ -333,64 +358,81 @@ attn_decode_kernel(AttnArgs a) {
   uint4 vr[kAttnRing][4];
 #pragma unroll
   for (int r = 0; r < kAttnRing - 1; ++r)               // in flight during the q work
-    load_rows(min(r, nc - 1), kr[r], vr[r]);
+    load_rows(min(r, max(ncw - 1, 0)), kr[r], vr[r]);
   const int pnew = len - 1;
   const bool own = a.qkv != nullptr && pnew >= w0 && pnew < w0 + kAttnChunk * cpw;
-  if (a.qkv) {
-    const float* row = a.qkv + (long)t * a.ldq;
-    const float* ct = a.cos_t + (long)pnew * (kHeadDim / 2);
-    const float* st = a.sin_t + (long)pnew * (kHeadDim / 2);
-    constexpr int QR = (G * (kHeadDim / 2) + 255) / 256;   // rotation pairs per thread
-    float qx0[QR], qx1[QR], qc[QR], qsn[QR];
-#pragma unroll
-    for (int u = 0; u < QR; ++u) {
-      const int i = min((int)threadIdx.x + 256 * u, G * (kHeadDim / 2) - 1);
-      const int g = i / (kHeadDim / 2), j = i % (kHeadDim / 2);
-      qx0[u] = row[(kh * G + g) * kHeadDim + j];
-      qx1[u] = row[(kh * G + g) * kHeadDim + j + kHeadDim / 2];
-      qc[u] = ct[j];
-      qsn[u] = st[j];
-    }
-    const int jk = threadIdx.x & (kHeadDim / 2 - 1), ev = threadIdx.x & (kHeadDim - 1);
-    const float k0 = row[(H + kh) * kHeadDim + jk], k1 = row[(H + kh) * kHeadDim + jk + kHeadDim / 2];
-    const float vn = row[(H + Hkv + kh) * kHeadDim + ev];
-#pragma unroll
-    for (int u = 0; u < QR; ++u) {
-      const int i = (int)threadIdx.x + 256 * u;
-      if (i < G * (kHeadDim / 2)) {
-        const int g = i / (kHeadDim / 2), j = i % (kHeadDim / 2);
-        qs[g][j] = rope_lo(qx0[u], qx1[u], qc[u], qsn[u]) * scale;
-        qs[g][j + kHeadDim / 2] = rope_hi(qx0[u], qx1[u], qc[u], qsn[u]) * scale;
-      }
-    }
-    if (own) {
-      const long cpos = cbase + (long)pnew * kHeadDim;
-      if (threadIdx.x < kHeadDim / 2) {
-        const float c = qc[0], sn = qsn[0];          // thread j < 64 loaded ct[j] / st[j] at u = 0
-        const uint16_t h0 = f2h(rope_lo(k0, k1, c, sn)), h1 = f2h(rope_hi(k0, k1, c, sn));
-        a.kc[cpos + jk] = h0;
-        a.kc[cpos + jk + kHeadDim / 2] = h1;
-        knew[jk] = h0;
-        knew[jk + kHeadDim / 2] = h1;
-      }
-      if (threadIdx.x < kHeadDim) {
-        const uint16_t hv = f2h(vn);
-        a.vc[cpos + ev] = hv;
-        vnew[ev] = hv;
-      }
-    }
-  } else {
-    for (int i = threadIdx.x; i < G * kHeadDim; i += blockDim.x)
-      qs[i / kHeadDim][i % kHeadDim] = q[(long)t * H * kHeadDim + (kh * G) * kHeadDim + i] * scale;
-  }
-  __syncthreads();
-  // B fragments of the scores: q head pr (zero rows past G), dims 32 s + 8 kg .. + 7, fp16
+  // B fragments of the scores, straight from memory: q head pr (zero rows past G), dims
+  // 32 s + 8 kg .. + 7, fp16.  With the fused RoPE the lane's dims pair up with their rotation
+  // partners (d, d + 64: s and s + 2) in its own registers, so no LDS round trip or barrier.
   h8 qa[4];
+  {
+    const int hq = kh * G + min(pr, G - 1);
+    float qv[4][8];
+    if (a.qkv) {
+      const float* row = a.qkv + (long)t * a.ldq + hq * kHeadDim;
+      const float* ct = a.cos_t + (long)pnew * (kHeadDim / 2);
+      const float* st = a.sin_t + (long)pnew * (kHeadDim / 2);
+      float x[4][8], cs[2][8], sn[2][8];
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
+      for (int s = 0; s < 4; ++s) {
+        const float4 u0 = *reinterpret_cast<const float4*>(row + 32 * s + 8 * kg);
+        const float4 u1 = *reinterpret_cast<const float4*>(row + 32 * s + 8 * kg + 4);
+        x[s][0] = u0.x; x[s][1] = u0.y; x[s][2] = u0.z; x[s][3] = u0.w;
+        x[s][4] = u1.x; x[s][5] = u1.y; x[s][6] = u1.z; x[s][7] = u1.w;
+      }
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      qa[s][j] = (_Float16)(pr < G ? qs[min(pr, G - 1)][32 * s + 8 * kg + j] : 0.f);
+      for (int s = 0; s < 2; ++s) {
+        const float4 c0 = *reinterpret_cast<const float4*>(ct + 32 * s + 8 * kg);
+        const float4 c1 = *reinterpret_cast<const float4*>(ct + 32 * s + 8 * kg + 4);
+        const float4 s0 = *reinterpret_cast<const float4*>(st + 32 * s + 8 * kg);
+        const float4 s1 = *reinterpret_cast<const float4*>(st + 32 * s + 8 * kg + 4);
+        cs[s][0] = c0.x; cs[s][1] = c0.y; cs[s][2] = c0.z; cs[s][3] = c0.w;
+        cs[s][4] = c1.x; cs[s][5] = c1.y; cs[s][6] = c1.z; cs[s][7] = c1.w;
+        sn[s][0] = s0.x; sn[s][1] = s0.y; sn[s][2] = s0.z; sn[s][3] = s0.w;
+        sn[s][4] = s1.x; sn[s][5] = s1.y; sn[s][6] = s1.z; sn[s][7] = s1.w;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          qv[s][jj] = rope_lo(x[s][jj], x[s + 2][jj], cs[s][jj], sn[s][jj]) * scale;
+          qv[s + 2][jj] = rope_hi(x[s][jj], x[s + 2][jj], cs[s][jj], sn[s][jj]) * scale;
+        }
+    } else {
+      const float* row = q + (long)t * H * kHeadDim + hq * kHeadDim;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) qv[s][jj] = row[32 * s + 8 * kg + jj] * scale;
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) qa[s][jj] = (_Float16)(pr < G ? qv[s][jj] : 0.f);
+  }
+  // the one workgroup per (token, kv head) whose range holds the new position rotates its k,
+  // writes K / V to the cache and keeps them in LDS for the chunk that reads them (uniform)
+  if (own) {
+    const float* row = a.qkv + (long)t * a.ldq;
+    const long cpos = cbase + (long)pnew * kHeadDim;
+    const int jk = threadIdx.x & (kHeadDim / 2 - 1), ev = threadIdx.x & (kHeadDim - 1);
+    if (threadIdx.x < kHeadDim / 2) {
+      const float c = a.cos_t[(long)pnew * (kHeadDim / 2) + jk];
+      const float sn = a.sin_t[(long)pnew * (kHeadDim / 2) + jk];
+      const float k0 = row[(H + kh) * kHeadDim + jk], k1 = row[(H + kh) * kHeadDim + jk + kHeadDim / 2];
+      const uint16_t h0 = f2h(rope_lo(k0, k1, c, sn)), h1 = f2h(rope_hi(k0, k1, c, sn));
+      a.kc[cpos + jk] = h0;
+      a.kc[cpos + jk + kHeadDim / 2] = h1;
+      knew[jk] = h0;
+      knew[jk + kHeadDim / 2] = h1;
+    }
+    if (threadIdx.x < kHeadDim) {
+      const uint16_t hv = f2h(row[(H + Hkv + kh) * kHeadDim + ev]);
+      a.vc[cpos + ev] = hv;
+      vnew[ev] = hv;
+    }
+    __syncthreads();
+  }
   float mrun = -INFINITY, lrun = 0.f;                   // head pr
   f4 o[8];                                              // O[head 4 kg + i][dim 16 n + pr]
 #pragma unroll
@@ -401,7 +443,7 @@ attn_decode_kernel(AttnArgs a) {
   // same 64-byte half-row pair only up to the swizzle: recomputed per tile (constants fold)
   const int tq = pr >> 2, tp = pr & 3;
   auto chunk = [&](int c, uint4 (&kb)[4], uint4 (&vb)[4]) __attribute__((always_inline)) {
-    const int pb = w0 + c * kAttnChunk + wave * 16;
+    const int pb = w0 + (c * NPAR + wpar) * kAttnChunk + wsub * 16;
     const int jn = pnew - pb;                           // the new position among these 16?
     if (own && jn >= 0 && jn < 16) {                    // its rows were loaded before they were written
       uint4 kq[4];
@@ -447,8 +489,8 @@ attn_decode_kernel(AttnArgs a) {
       sc[i] = 4 * kg + i < nv ? acc[i] : -INFINITY;
       mx = fmaxf(mx, sc[i]);
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+    mx = fmaxf(mx, lane_xor16(mx));
+    mx = fmaxf(mx, lane_xor32(mx));
     const float mn = fmaxf(mrun, mx);
     const float mref = mn == -INFINITY ? 0.f : mn;      // nothing attended yet: every term is 0
     const float al = __expf(mrun - mref);
@@ -460,14 +502,19 @@ attn_decode_kernel(AttnArgs a) {
       pa[i] = (_Float16)p;
       ls += p;
     }
-    ls += __shfl_xor(ls, 16, kWave);
-    ls += __shfl_xor(ls, 32, kWave);
+    ls += lane_xor16(ls);
+    ls += lane_xor32(ls);
     lrun = lrun * al + ls;
     mrun = mn;
-    // rescale: output row 4 kg + i takes the alpha of head 4 kg + i (lane 4 kg + i)
+    // rescale: output row 4 kg + i takes the alpha of head 4 kg + i (lane 4 kg + i); rows past
+    // G (kg >= 2 when G <= 8) are padding
     f4 a4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a4[i] = __shfl(al, 4 * kg + i, kWave);
+    for (int i = 0; i < 4; ++i) {
+      const float lo = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(al), i));
+      const float hi = G > 4 ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(al), 4 + i)) : lo;
+      a4[i] = kg == 0 ? lo : hi;
+    }
 #pragma unroll
     for (int n = 0; n < 8; ++n) o[n] *= a4;
     // P.V: B = V[position 4 kg + j][dim 16 n + pr] from the image, transposed
@@ -485,16 +532,20 @@ attn_decode_kernel(AttnArgs a) {
   // a full HBM round trip), and a load under a branch leaves the wait counter unknown at the join,
   // where the compiler then waits for it too — so the loads past the last chunk are issued
   // anyway, clamped to it (an L2 re-read).
+  if (AMDK8S_ATTN_FAST1 && ncw == 1) {                  // one chunk (every token <= 4096): no ring
+    chunk(0, kr[0], vr[0]);
+  } else if (ncw > 1) {
 #pragma unroll 1
-  for (int c = 0; c < nc; c += kAttnRing) {
+    for (int c = 0; c < ncw; c += kAttnRing) {
 #pragma unroll
-    for (int r = 0; r < kAttnRing; ++r) {
-      const int nx = (r + kAttnRing - 1) % kAttnRing;
-      load_rows(min(c + r + kAttnRing - 1, nc - 1), kr[nx], vr[nx]);
-      if (r == 0 || c + r < nc) chunk(c + r, kr[r], vr[r]);
+      for (int r = 0; r < kAttnRing; ++r) {
+        const int nx = (r + kAttnRing - 1) % kAttnRing;
+        load_rows(min(c + r + kAttnRing - 1, ncw - 1), kr[nx], vr[nx]);
+        if (r == 0 || c + r < ncw) chunk(c + r, kr[r], vr[r]);
+      }
     }
   }
-  // merge the four waves
+  // merge the waves (an idle wave: max -inf, sum 0, output 0 — weight 0)
   if (kg == 0) { wml[wave][pr][0] = mrun; wml[wave][pr][1] = lrun; }
 #pragma unroll
   for (int n = 0; n < 8; ++n)
@@ -506,10 +557,10 @@ attn_decode_kernel(AttnArgs a) {
     const int g = i / kHeadDim, dd = i % kHeadDim;
     float m = wml[0][g][0];
 #pragma unroll
-    for (int w = 1; w < 4; ++w) m = fmaxf(m, wml[w][g][0]);
+    for (int w = 1; w < NW; ++w) m = fmaxf(m, wml[w][g][0]);
     float v = 0.f, l = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const float e = wml[w][g][0] == -INFINITY ? 0.f : __expf(wml[w][g][0] - m);
       v += e * wo[w][g][dd];
       l += e * wml[w][g][1];
@@ -579,7 +630,7 @@ int amdk8s_llm_attn_decode(const void* q, const void* qkv, int ldq, const void* 
   aa.nsplit = span / kAttnChunk;                         // partial-row stride of po / pml
   const int rc = by_group([&](auto g) {
     hipLaunchKernelGGL(attn_decode_kernel<decltype(g)::value>, dim3(Hkv, attn_parts_max(span), T),
-                       dim3(256), 0, st, aa);
+                       dim3(64 * kAttnWaves), 0, st, aa);
   });
   if (rc) return rc;
   // the merge kernel and its row groups follow max_ctx (fixed per engine), never this launch's
