@@ -108,3 +108,28 @@ def test_loadgen_kernels_use_the_intended_instructions(tmp_path):
     assert text.count("v_pk_fma_f32") >= 32 and text.count("v_mfma_f64_16x16x4") >= 16
     assert "global_load_dwordx4" in text and "global_store_dwordx4" in text
     assert " nt" in text and "scratch_" not in text
+
+
+def test_kernel_library_override_is_loaded_as_named(tmp_path, monkeypatch):
+    """AMDK8S_KERNEL_LIB (A/B builds of the same sources, e.g. -DAMDK8S_ATTN_PARTS=...) is loaded
+    as given — never rebuilt over, and a missing file is an error, not a silent fallback."""
+    from k8s_nvidia_gpus_amd.ops import kernels as K
+
+    monkeypatch.setattr(K, "_lib", None)
+    monkeypatch.setenv("AMDK8S_KERNEL_LIB", str(tmp_path / "missing.so"))
+    calls = []
+    monkeypatch.setattr(K._build, "build_kernel_library", lambda *a, **k: calls.append(1))
+    with pytest.raises(K.KernelLibraryError):
+        K.library()
+    assert not calls
+    monkeypatch.setattr(K, "_lib", None)
+
+
+def test_attention_build_knobs_default_to_the_measured_choice():
+    """The decode-attention A/B knobs (llm_attn.hip) default to what the round-5 sweeps chose:
+    64 partials per head, a 2-deep chunk ring, 4 waves per workgroup, the one-chunk fast path."""
+    src = (B.CSRC_DIR / "llm_attn.hip").read_text()
+    for knob, val in [("AMDK8S_ATTN_PARTS", "64"), ("AMDK8S_ATTN_RING", "2"),
+                      ("AMDK8S_ATTN_WAVES", "4"), ("AMDK8S_ATTN_FAST1", "1"),
+                      ("AMDK8S_ATTN_WPE", "1")]:
+        assert f"#define {knob} {val}\n" in src, knob
