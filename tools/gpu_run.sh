@@ -22,6 +22,7 @@
 #   gemv[:<cases>]   tools/llm_bench.py --gemv: cold-weight GEMV decomposition sweep, T = 1 and 4
 #   prof-bench       rocprofv3 --kernel-trace --stats of the driver's bench command
 #   prof-llm[:<T>[:<prompt>]]   rocprofv3 kernel trace of steady LLM decode at T tokens → per-kernel summary
+#   prof-prefill     the same for a 512-token prompt prefill
 #   pmc-llm[:<T>]    tools/llm_pmc.sh: PMC passes (busy / VALU / wait shares, HBM bytes) at T tokens
 #   sd15 / wan       tools/sd15_bench.py / tools/wan_bench.py
 #   env:VAR=VALUE    export VAR for the following steps (A/B knobs)
@@ -142,6 +143,13 @@ PYEOF
       db=$(find "$OUT/prof_llm_$tag" -name '*.db' | head -1)
       python3 tools/rocpd_summary.py "$db" --after-gap-ms 200 --per 20 --top 30 > "$OUT/llm_decode_${tag}_kernels.txt" \
         && head -24 "$OUT/llm_decode_${tag}_kernels.txt" | cut -c1-170 ;;
+    prof-prefill)
+      timeout -k 10 400 rocprofv3 --kernel-trace --output-format rocpd -d "$OUT/prof_prefill" -o prefill \
+        -- python3 tools/steady_prof.py llm-prefill --iters 10 --warmup 3 > "$OUT/prof_prefill.log" 2>&1 \
+        || fail "$step" $? "$OUT/prof_prefill.log"
+      db=$(find "$OUT/prof_prefill" -name '*.db' | head -1)
+      python3 tools/rocpd_summary.py "$db" --after-gap-ms 200 --per 10 --top 30 > "$OUT/llm_prefill_kernels.txt" \
+        && head -30 "$OUT/llm_prefill_kernels.txt" | cut -c1-170 ;;
     pmc-llm|pmc-llm:*)
       t=1; [[ "$step" == pmc-llm:* ]] && t="${step#pmc-llm:}"
       OUT="$OUT/llm_pmc_t$t" TOKENS=$t timeout -k 10 400 tools/llm_pmc.sh > "$OUT/llm_pmc_t$t.txt" 2>&1 \
