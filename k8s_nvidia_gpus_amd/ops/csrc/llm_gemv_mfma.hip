@@ -429,6 +429,7 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
 #ifndef AMDK8S_PAIR_WPE
 #define AMDK8S_PAIR_WPE 3
 #endif
+// Q6_K pairs (5 planes per slot) spill 336-428 bytes per lane at 3 waves/SIMD: 2 at every T.
 // Steps of 5-8 tokens (two token quads per wave): without a floor the pair kernel took 209 VGPRs
 // + 64 AGPRs, one wave per SIMD, so gate|up's 592 workgroups ran in 2.3 rounds (32.1 us at T = 8);
 // at 2 waves/SIMD (252 VGPRs, no spill) 24.4 us, T = 8 step 3.02 -> 2.82 ms (session r05ac).
@@ -439,7 +440,8 @@ constexpr int kPairD = AMDK8S_PAIR_D;
 
 template <int TYPE, int T, int MODE, int KW, int RG, int D>
 __global__ void __launch_bounds__(KW * RG * 64)
-__attribute__((amdgpu_waves_per_eu(MODE == kPair ? (T <= 4 ? AMDK8S_PAIR_WPE : AMDK8S_PAIR_WPE8) : 1, 8)))
+__attribute__((amdgpu_waves_per_eu(
+    MODE == kPair ? (T <= 4 && TYPE == kQ4K ? AMDK8S_PAIR_WPE : AMDK8S_PAIR_WPE8) : 1, 8)))
 qgemv_mfma_kernel(GemvArgs a) {
   qgemv_mfma_body<TYPE, T, MODE, KW, RG, D>(a, blockIdx.x);
 }
