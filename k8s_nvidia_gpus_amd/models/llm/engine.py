@@ -28,7 +28,7 @@ from __future__ import annotations
 import math
 import time
 from dataclasses import dataclass
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -263,6 +263,54 @@ class Engine:
         LK.rmsnorm_f16(x[-1:], self.w.out_norm, c.eps, xn[:1])
         return mm(xn[:1], W["out"]).float()[0]
 
+    def _forward_dense_native_multi(self, segs) -> torch.Tensor:
+        """Prompt chunks of several sequences in one pass (llama-server fills one batch with the
+        prompt tokens of every slot that needs them, reference cluster-config/apps/llm/
+        deployment.yaml:76-84): the GEMMs and glue kernels run over all rows at once, RoPE + the
+        KV write and attention per sequence.  ``segs``: [(tokens, slot, start)]; returns the
+        last-token logits of each chunk, fp32 [len(segs), vocab]."""
+        c, LK = self.cfg, self.LK
+        W = self.dense_weights()
+        dt = torch.float16
+        lens = [int(t.numel()) for t, _, _ in segs]
+        offs = [0]
+        for n in lens:
+            offs.append(offs[-1] + n)
+        P = offs[-1]
+        x = self.embed(torch.cat([t for t, _, _ in segs]))   # fp32 [P, dim]
+        mm, mm_res = self._dense_ops()
+        from torch.nn.attention.bias import causal_lower_right
+
+        lowright = [causal_lower_right(n, st + n) if n > 1 and st > 0 else None
+                    for n, (_, _, st) in zip(lens, segs)]
+        xn = torch.empty(P, c.dim, dtype=dt, device=self.device)
+        qh = torch.empty(P, c.heads, c.head_dim, dtype=dt, device=self.device).transpose(0, 1)
+        o = torch.empty(P, c.dim, dtype=dt, device=self.device)
+        t = torch.empty(P, c.ffn, dtype=dt, device=self.device)
+        for i, L in enumerate(self.w.layers):
+            LK.rmsnorm_f16(x, L.attn_norm, c.eps, xn)
+            qkv = mm(xn, W[f"{i}.qkv"], W[f"{i}.bqkv"])
+            for s, (_, slot, st) in enumerate(segs):
+                a, b = offs[s], offs[s + 1]
+                LK.rope_kv_f16(qkv[a:b], self.cos, self.sin, st, c.heads, c.kv_heads,
+                               self.max_ctx, qh[:, a:b], self.k_cache[i, slot], self.v_cache[i, slot])
+            for s, (_, slot, st) in enumerate(segs):
+                a, b = offs[s], offs[s + 1]
+                n, end = b - a, st + b - a
+                os_ = F.scaled_dot_product_attention(
+                    qh[None, :, a:b], self.k_cache[i, slot, :, :end][None],
+                    self.v_cache[i, slot, :, :end][None], attn_mask=lowright[s],
+                    is_causal=n > 1 and st == 0, enable_gqa=True)
+                o[a:b] = os_[0].transpose(0, 1).reshape(n, c.dim)
+            x = mm_res(x, o, W[f"{i}.o"])
+            LK.rmsnorm_f16(x, L.ffn_norm, c.eps, xn)
+            LK.swiglu_f16(mm(xn, W[f"{i}.gu"]), t)
+            x = mm_res(x, t, W[f"{i}.down"])
+        last = torch.tensor([b - 1 for b in offs[1:]], device=self.device)
+        xl = x.index_select(0, last)
+        LK.rmsnorm_f16(xl, self.w.out_norm, c.eps, xn[:len(segs)])
+        return mm(xn[:len(segs)], W["out"]).float()
+
     def _dense_ops(self):
         """Prompt-processing GEMMs: on the GPU the hand-written fp16 MFMA GEMMs
         (``ops/gemm_epi.py``: tile / split-K planned per shape, the residual add of o_proj and
@@ -492,16 +540,43 @@ class Engine:
             logits = logits[n - 1]
         return logits.clone()
 
+    def prefill_many(self, items: Sequence[Tuple[Sequence[int], int, int]]) -> List[torch.Tensor]:
+        """Prompt chunks of several sequences ``[(tokens, slot, start)]`` (distinct slots) in one
+        pass on the GPU prompt path; each chunk's last-token logits [vocab].  Elsewhere (CPU, the
+        decode-kernel prompt path) the chunks run one after the other."""
+        items = [(list(t), int(s), int(st)) for t, s, st in items]
+        slots = [s for _, s, _ in items]
+        native = (self.gpu and self.dense and self.prefill_native and self.prefill_gqa
+                  and self.prefill_qtok and self.cfg.head_dim == 128 and self.cfg.dim <= 8192
+                  and self.cfg.dim % 8 == 0 and self.cfg.ffn % 8 == 0)
+        if len(items) == 1 or not native or len(set(slots)) != len(slots):
+            return [self.prefill(t, s, st) for t, s, st in items]
+        for t, _, st in items:
+            if not t:
+                raise ValueError("prefill: empty prompt")
+            if st + len(t) > self.max_ctx:
+                raise ValueError(f"prompt of {len(t)} tokens at {st} exceeds the context "
+                                 f"({self.max_ctx})")
+        self.stats["prefill_tokens"] += sum(len(t) for t, _, _ in items)
+        logits = self._forward_dense_native_multi(
+            [(torch.tensor(t, device=self.device), s, st) for t, s, st in items])
+        return [logits[i] for i in range(len(items))]
+
     def warmup(self, lengths: Sequence[int] = (1, 64, 512, 2048), slot: int = 0) -> None:
         """Run the prompt path once per length, from position 0 and as a continuation chunk, so
         the first request of each kind does not pay first-use costs (kernel images SDPA loads on
         first use of a shape class, allocator growth: ~250 ms on the first 512-token prompt,
-        profiles/r05/serve).  Writes slot ``slot``'s KV, which the server then treats as empty."""
+        profiles/r05/serve).  Writes the KV of slot ``slot`` (and the first position of slots
+        0..7), which the server then treats as empty."""
         for n in lengths:
             if 2 * n + 1 >= self.max_ctx:
                 continue
             self.prefill([1] * n, slot, start=0)
             self.prefill([1] * n, slot, start=n)
+        # prompt batches of 2..8 slots: their last-token rows meet the output matrix as M = 2..8
+        # (a first use there cost ~50 ms of a batch's time to first token, session r05ai)
+        for k in range(2, min(8, self.slots) + 1):
+            self.prefill_many([([1], s, 0) for s in range(k)])
         if self.gpu:
             torch.cuda.synchronize(self.device)
 

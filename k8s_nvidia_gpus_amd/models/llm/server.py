@@ -127,7 +127,7 @@ class Scheduler:
     searched only in the held-back tail plus the new text."""
 
     def __init__(self, engine: Engine, tok: Tokenizer, parallel: int = 8, ubatch: int = 512,
-                 batch: Optional[int] = None):
+                 batch: Optional[int] = None, autostart: bool = True):
         self.engine = engine
         self.tok = tok
         self.parallel = max(1, min(parallel, engine.slots))
@@ -152,7 +152,14 @@ class Scheduler:
         self._run = True
         self._lock = threading.Lock()
         self.thread = threading.Thread(target=self._loop, name="llm-scheduler", daemon=True)
-        self.thread.start()
+        if autostart:
+            self.thread.start()
+
+    def start(self) -> None:
+        """Start the scheduler thread (``autostart=False``: after queueing requests, e.g. so that
+        several are admitted in one iteration)."""
+        if not self.thread.is_alive():
+            self.thread.start()
 
     def submit(self, job: Job) -> Job:
         if len(job.ids) == 0:
@@ -181,7 +188,8 @@ class Scheduler:
             pass
         self._run = False
         self.pending.put(None)  # type: ignore[arg-type]
-        self.thread.join(timeout=10)
+        if self.thread.is_alive():
+            self.thread.join(timeout=10)
 
     # ---------------------------------------------------------------- scheduler thread
     def _put(self, job: Job, item) -> None:
@@ -318,43 +326,67 @@ class Scheduler:
             self.prefilling.append(job)
 
     def _prefill_chunk(self) -> int:
-        """One chunk of the oldest admitted prompt; its last chunk samples the first token.
-        Returns the number of prompt tokens processed."""
+        """One prompt batch: chunks of the admitted prompts, oldest first, up to the batch's
+        token budget (``ubatch`` while other sequences decode, ``batch`` otherwise) — like
+        llama-server, which fills one batch with the prompt tokens of every slot that needs them.
+        A prompt's last chunk samples its first token.  Returns the number of prompt tokens."""
         for j in [j for j in self.prefilling if j.cancelled]:
             self.prefilling.remove(j)
             self._release(j)
         if not self.prefilling:
             return 0
-        job = self.prefilling[0]
-        limit = self.ubatch if any(j.decoding for j in self.active.values()) else self.batch
-        n = min(limit, len(job.ids) - job.pos)
+        budget = self.ubatch if any(j.decoding for j in self.active.values()) else self.batch
+        work = []
+        for job in self.prefilling:
+            n = min(budget, len(job.ids) - job.pos)
+            if n <= 0:
+                break
+            work.append((job, n))
+            budget -= n
+            if budget == 0:
+                break
         t0 = time.perf_counter()
-        try:
-            logits = self.engine.prefill(job.ids[job.pos:job.pos + n], job.slot, start=job.pos)
-            done = job.pos + n == len(job.ids)
-            tok = sample_token(logits, job.params, self._recent(job), job.generator) if done else None
-        except Exception as e:  # noqa: BLE001 - this job fails; the others keep decoding
-            self.prefilling.pop(0)
-            self._fail(job, e)
-            return 0
-        dt = time.perf_counter() - t0
-        job.pos += n
-        job.t_prefill += dt
-        with self._lock:
-            self.metrics["prompt_tokens_total"] += n
-            self.metrics["prefill_seconds_total"] += dt
-            self.metrics["prefill_chunks_total"] += 1
-        if not done:
-            return n
-        self.prefilling.pop(0)
-        job.t_first = time.perf_counter()
-        job.decoding = True
-        with self._lock:
-            self.metrics["prompt_tokens_cached_total"] += job.n_cached
-            self.metrics["tokens_predicted_total"] += 1
-        if self._emit(job, int(tok)):
-            self._release(job)
-        return n
+        many = getattr(self.engine, "prefill_many", None)
+        results = {}
+        if many is not None and len(work) > 1:
+            try:
+                out = many([(job.ids[job.pos:job.pos + n], job.slot, job.pos) for job, n in work])
+                results = {id(job): lg for (job, _), lg in zip(work, out)}
+            except Exception:  # noqa: BLE001 - retried one by one below, so only the bad one fails
+                results = {}
+        total = 0
+        for job, n in work:
+            try:
+                logits = results.get(id(job))
+                if logits is None:
+                    logits = self.engine.prefill(job.ids[job.pos:job.pos + n], job.slot,
+                                                 start=job.pos)
+                done = job.pos + n == len(job.ids)
+                tok = (sample_token(logits, job.params, self._recent(job), job.generator)
+                       if done else None)
+            except Exception as e:  # noqa: BLE001 - this job fails; the others keep decoding
+                self.prefilling.remove(job)
+                self._fail(job, e)
+                continue
+            dt = time.perf_counter() - t0
+            job.pos += n
+            job.t_prefill += dt
+            total += n
+            with self._lock:
+                self.metrics["prompt_tokens_total"] += n
+                self.metrics["prefill_seconds_total"] += dt
+                self.metrics["prefill_chunks_total"] += 1
+            if not done:
+                continue
+            self.prefilling.remove(job)
+            job.t_first = time.perf_counter()
+            job.decoding = True
+            with self._lock:
+                self.metrics["prompt_tokens_cached_total"] += job.n_cached
+                self.metrics["tokens_predicted_total"] += 1
+            if self._emit(job, int(tok)):
+                self._release(job)
+        return total
 
     def _step(self) -> int:
         """One decode step of every sequence past its prompt; returns how many."""

@@ -789,6 +789,33 @@ def test_chunked_prefill_matches_monolithic(dev, tiny_gguf, chunk):
     assert int(last.argmax()) == int(mono.argmax())
 
 
+def test_prefill_many_equals_separate_prefills(dev, tiny_gguf):
+    """Prompt chunks of three slots in one pass (GEMMs over all rows, RoPE + KV write and
+    attention per sequence): a fresh prompt, a single-token chunk and a continuation after a
+    cached prefix give each sequence's own prefill logits and KV within fp16 rounding (the GEMMs
+    see a different M), with the same greedy token."""
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load
+
+    eng, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=True, slots=6)
+    a = tok.encode("the lazy dog jumps over a helpful assistant " * 3)
+    b = tok.encode("hello")[:1]
+    c = tok.encode("a cozy cabin in the woods, the quick brown fox " * 2)
+    pre = 17
+    eng.prefill(c[:pre], 2)                  # slot 2's cached prefix
+    eng.prefill(c[:pre], 5)                  # and the reference slot's
+    ref = [eng.prefill(a, 3).cpu(), eng.prefill(b, 4).cpu(), eng.prefill(c[pre:], 5, start=pre).cpu()]
+    out = eng.prefill_many([(a, 0, 0), (b, 1, 0), (c[pre:], 2, pre)])
+    for got, want in zip(out, ref):
+        got = got.cpu()
+        assert torch.nn.functional.cosine_similarity(got[None], want[None]).item() > 0.9995
+        torch.testing.assert_close(got, want, rtol=2e-2, atol=5e-2)
+        assert int(got.argmax()) == int(want.argmax())
+    for cache in (eng.k_cache, eng.v_cache):
+        for s_new, s_ref, n in ((0, 3, len(a)), (1, 4, 1), (2, 5, len(c))):
+            torch.testing.assert_close(cache[:, s_new, :, :n].float(), cache[:, s_ref, :, :n].float(),
+                                       rtol=1e-2, atol=1e-2)
+
+
 def test_chunked_prefill_7b_shapes_long_prefix(dev):
     """The 7B attention layout (28 q heads over 4 kv heads) with a 3000-token prefix: chunks of
     512 against the monolithic prefill, logits and the cache tail."""

@@ -135,6 +135,45 @@ def test_batch_size_chunks_when_nothing_decodes(tiny_model):
     assert sizes[0] == 32 and sum(sizes) == len(ids)
 
 
+def test_prompts_of_several_slots_share_one_batch(tiny_model):
+    """Prompts admitted together are processed in one prompt batch (llama-server fills a batch
+    with the prompt tokens of every slot that needs them), oldest first, within the token budget;
+    each answer equals the answer it gets alone."""
+    from k8s_nvidia_gpus_amd.models.llm import server as S
+
+    eng, tok = _load(tiny_model)
+    calls = []
+    real_many = eng.prefill_many
+
+    def prefill_many(items):
+        calls.append([(slot, start, len(ids)) for ids, slot, start in items])
+        return real_many(items)
+
+    eng.prefill_many = prefill_many
+    prompts = [tok.encode(t) for t in ("a cozy cabin in the woods", "hello world, hello",
+                                       "the quick brown fox jumps over the lazy dog. " * 3)]
+    sched = S.Scheduler(eng, tok, parallel=3, ubatch=8, batch=24, autostart=False)
+    try:
+        jobs = [sched.submit(S.Job(ids=ids, max_new=6, ignore_eos=True)) for ids in prompts]
+        sched.start()                                      # all three admitted in one iteration
+        for j in jobs:
+            _wait(j)
+    finally:
+        sched.close()
+    first = calls[0]
+    assert len(first) >= 2, calls                          # one batch, several slots
+    assert sum(n for _, _, n in first) <= 24               # the batch budget
+    assert [n for _, _, n in first][:2] == [len(prompts[0]), len(prompts[1])]
+    for ids, j in zip(prompts, jobs):
+        eng2, _ = _load(tiny_model)
+        sched2 = S.Scheduler(eng2, tok, parallel=1, ubatch=4096)
+        try:
+            alone = _wait(sched2.submit(S.Job(ids=ids, max_new=6, ignore_eos=True)))
+        finally:
+            sched2.close()
+        assert alone.gen == j.gen
+
+
 class ScriptedEngine:
     """Engine stand-in whose greedy output is a fixed token script (positions map to script
     indices), so stop-string cases can be built from known text."""

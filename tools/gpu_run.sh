@@ -129,6 +129,10 @@ PYEOF
           --out "$OUT/prefill_gemm_$m.json" > "$OUT/prefill_gemm_$m.log" 2>&1 || fail "$step" $? "$OUT/prefill_gemm_$m.log"
         grep "^{" "$OUT/prefill_gemm_$m.log" | cut -c1-220
       done ;;
+    prefill-many)
+      timeout -k 10 400 python -u tools/debug/prefill_many_probe.py > "$OUT/prefill_many_probe.log" 2>&1 \
+        || fail "$step" $? "$OUT/prefill_many_probe.log"
+      grep '^{' "$OUT/prefill_many_probe.log" ;;
     attn-probe)
       timeout -k 10 300 python -u tools/debug/prefill_attn_probe.py > "$OUT/prefill_attn_probe.log" 2>&1 \
         || fail "$step" $? "$OUT/prefill_attn_probe.log"
