@@ -6,7 +6,7 @@
 namespace {
 
 // ---------------------------------------------------------------- split-context decode attention
-// grid (Hkv, attn_parts_max(span), T); 256 threads.  One workgroup: the G = H/Hkv q heads of one
+// grid (Hkv, attn_parts_max(span), T); 64 x kAttnWaves threads.  One workgroup: the G = H/Hkv q heads of one
 // kv head over cpw consecutive 64-position chunks (one partial); writes the unnormalised partial
 // output and (max, sum) per head (attn_decode_kernel).
 //
