@@ -320,3 +320,20 @@ def test_waiting_requests_hold_no_executor_thread(tiny_model):
     finally:
         sched.close()
     assert all(o[-1] == "done" for o in outs)
+
+
+def test_prefill_many_equals_one_by_one_and_validates(tiny_model):
+    """``Engine.prefill_many`` off the GPU prompt path runs the chunks one after the other: the
+    same logits and KV as separate prefills; an empty chunk or one past the context is rejected."""
+    eng, tok = _load(tiny_model, slots=4)
+    a, b = tok.encode("a cozy cabin in the woods"), tok.encode("hello world")
+    got = eng.prefill_many([(a, 0, 0), (b, 1, 0)])
+    eng2, _ = _load(tiny_model, slots=4)
+    want = [eng2.prefill(a, 0), eng2.prefill(b, 1)]
+    for g, w in zip(got, want):
+        torch.testing.assert_close(g, w)
+    torch.testing.assert_close(eng.k_cache[:, :2], eng2.k_cache[:, :2])
+    with pytest.raises(ValueError):
+        eng.prefill_many([(a, 2, 0), ([], 3, 0)])
+    with pytest.raises(ValueError):
+        eng.prefill_many([(a, 2, 0), (b, 3, eng.max_ctx - 1)])
