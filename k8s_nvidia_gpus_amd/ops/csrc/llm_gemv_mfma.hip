@@ -436,12 +436,18 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
 #ifndef AMDK8S_PAIR_WPE8
 #define AMDK8S_PAIR_WPE8 2
 #endif
+// Q4_K store / resid GEMVs at 5-8 tokens: 170-176 VGPRs left them at 2 waves/SIMD; 3 fit
+// without a spill (Q6_K would spill 172-232 B/lane, so it keeps the compiler's choice)
+#ifndef AMDK8S_NP_WPE8
+#define AMDK8S_NP_WPE8 3
+#endif
 constexpr int kPairD = AMDK8S_PAIR_D;
 
 template <int TYPE, int T, int MODE, int KW, int RG, int D>
 __global__ void __launch_bounds__(KW * RG * 64)
 __attribute__((amdgpu_waves_per_eu(
-    MODE == kPair ? (T <= 4 && TYPE == kQ4K ? AMDK8S_PAIR_WPE : AMDK8S_PAIR_WPE8) : 1, 8)))
+    MODE == kPair ? (T <= 4 && TYPE == kQ4K ? AMDK8S_PAIR_WPE : AMDK8S_PAIR_WPE8)
+                  : (T > 4 && TYPE == kQ4K ? AMDK8S_NP_WPE8 : 1), 8)))
 qgemv_mfma_kernel(GemvArgs a) {
   qgemv_mfma_body<TYPE, T, MODE, KW, RG, D>(a, blockIdx.x);
 }
