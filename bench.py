@@ -9,7 +9,11 @@ w4a, whose K-loop is generated assembly), on random [-1,1) operands (synthetic d
 N grows → weak scaling.
 
 Launch contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 under
-``torch.distributed.run`` with one rank per GPU (RCCL backend).  W untimed steps, then exactly K
+``torch.distributed.run`` with one rank per GPU (RCCL backend).  A plain ``python bench.py --gpus N``
+(N > 1, no WORLD_SIZE) starts that torchrun itself as a child process after counting GPU agents in
+the KFD sysfs topology (fewer than N → exit 2), so it can never report a 1-GPU number for N; under
+torchrun, WORLD_SIZE != --gpus is an error, and the JSON carries every rank's PCI BDF (checked
+distinct) and the process group's own world size.  W untimed steps, then exactly K
 timed steps bracketed by barrier + synchronize on both sides; the MAX elapsed over ranks is used;
 rank 0 prints ONE JSON line.  Before the W warmup steps each rank runs the GEMM back-to-back for
 ``--settle-ms`` (default 250 ms, untimed) so that the timed window measures sustained throughput
@@ -68,6 +72,110 @@ def native_first_gpu_result():
     return round(time.time() - t0, 3) if "Test PASSED" in out else None
 
 
+def _peek_args(argv):
+    """(--gpus, --launcher, --cpu-smoke) from argv without argparse's exit-on-error (the full
+    parser runs later, in the ranks)."""
+    gpus, launcher = 1, "auto"
+    for i, a in enumerate(argv):
+        for flag in ("--gpus", "--launcher"):
+            val = None
+            if a == flag and i + 1 < len(argv):
+                val = argv[i + 1]
+            elif a.startswith(flag + "="):
+                val = a.split("=", 1)[1]
+            if val is None:
+                continue
+            if flag == "--gpus":
+                try:
+                    gpus = int(val)
+                except ValueError:
+                    pass
+            else:
+                launcher = val
+    return gpus, launcher, "--cpu-smoke" in argv
+
+
+def visible_gpu_agents(root=None):
+    """GPU agents this process could open, from the KFD sysfs topology (never a HIP call: the
+    launcher parent must not initialise the GPU before it starts the ranks).  A
+    HIP/ROCR/CUDA_VISIBLE_DEVICES list narrows the count.  Returns (count, detail)."""
+    from k8s_nvidia_gpus_amd.utils.topology import read_topology
+
+    root = root or os.environ.get("AMDK8S_SYSFS_ROOT", "/")
+    topo = read_topology(root)
+    n = len(topo.gpus)
+    detail = f"{n} GPU agent(s) in {os.path.join(root, 'sys/class/kfd/kfd/topology')}"
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v:       # unset or empty: no narrowing (an empty list would fail loudly in the ranks)
+            ids = [d for d in v.split(",") if d.strip()]
+            if len(ids) < n:
+                n = len(ids)
+                detail += f", {var}={v!r} leaves {n}"
+    return n, detail
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(argv, nproc: int, smoke: bool) -> int:
+    """``python bench.py --gpus N`` (N > 1, no WORLD_SIZE): start one rank per GPU under
+    ``torch.distributed.run`` as a CHILD process (never an exec: see the launch rules) and relay its
+    stdout — rank 0's one JSON line — and its exit code.  Refuses (exit 2) when fewer than N GPU
+    agents are visible instead of silently measuring fewer GPUs.  This process imports neither
+    torch nor HIP."""
+    if not smoke or os.environ.get("AMDK8S_SYSFS_ROOT"):
+        try:
+            have, detail = visible_gpu_agents()
+        except (OSError, FileNotFoundError) as e:
+            print(f"bench.py: --gpus {nproc}: cannot count GPU agents ({e})", file=sys.stderr)
+            return 2
+        if have < nproc:
+            print(f"bench.py: --gpus {nproc} but only {detail}; refusing to measure fewer GPUs",
+                  file=sys.stderr)
+            return 2
+    rest = []
+    skip = False
+    for i, a in enumerate(argv):       # the ranks must not try to launch again
+        if skip:
+            skip = False
+            continue
+        if a == "--launcher":
+            skip = True
+            continue
+        if a.startswith("--launcher="):
+            continue
+        rest.append(a)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + rest
+    env = dict(os.environ, AMDK8S_BENCH_LAUNCHER="torchrun (spawned by bench.py)")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    print(f"bench.py: launching {nproc} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in proc.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return proc.wait()
+
+
+if __name__ == "__main__" and "WORLD_SIZE" not in os.environ:
+    _gpus, _launcher, _smoke = _peek_args(sys.argv[1:])
+    if _launcher not in ("auto", "torchrun", "none"):
+        print(f"bench.py: --launcher must be auto|torchrun|none, not {_launcher!r}", file=sys.stderr)
+        sys.exit(2)
+    if _gpus > 1 and _launcher == "none":
+        print(f"bench.py: --gpus {_gpus} needs one rank per GPU; run it under torch.distributed.run "
+              "or drop --launcher none", file=sys.stderr)
+        sys.exit(2)
+    if _gpus > 1 or _launcher == "torchrun":
+        sys.exit(self_launch(sys.argv[1:], _gpus, _smoke))
+
 _NATIVE_TTFR = native_first_gpu_result()
 
 import torch  # noqa: E402
@@ -92,6 +200,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-telemetry", action="store_true", help="no amd-smi sampling")
     ap.add_argument("--no-allreduce", action="store_true")
     ap.add_argument("--no-fp8", action="store_true", help="skip the fp8 GEMM extra measurement")
+    ap.add_argument("--launcher", choices=("auto", "torchrun", "none"), default="auto",
+                    help="auto: a plain run with --gpus N > 1 starts N ranks under "
+                         "torch.distributed.run itself; torchrun: do so even for N = 1")
     ap.add_argument("--cpu-smoke", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -191,12 +302,28 @@ def check_numerics(K, a, b, c, samples: int = 1024) -> float:
     return float((err / (ref.abs() + 1.0)).max().item())
 
 
+def rank_identity(device: torch.device) -> dict:
+    """Which GPU this rank measured: PCI BDF (distinct across ranks, checked), device index, host."""
+    import socket
+
+    from k8s_nvidia_gpus_amd.parallel.telemetry import device_bdf
+
+    return {"rank": int(os.environ.get("RANK", "0")),
+            "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+            "device": str(device),
+            "bdf": device_bdf(device.index or 0) if device.type == "cuda" else None,
+            "host": socket.gethostname()}
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if world != args.gpus:
+        # a mismatched launch would report a different N than the one asked for
+        if rank == 0:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
     # torchrun with one rank still takes the RCCL path (a 1-GPU rehearsal of the N>1 code)
     distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
     smoke = args.cpu_smoke
@@ -275,8 +402,19 @@ def main(argv=None) -> int:
         per_rank = [round(float(x.item()), 2) for x in gathered]
         tels = [None] * world
         dist.all_gather_object(tels, tel)
+        pg_world = dist.get_world_size()
+        ranks = [None] * world
+        dist.all_gather_object(ranks, rank_identity(device))
     else:
         tels = [tel]
+        pg_world = None
+        ranks = [rank_identity(device)]
+    if not smoke:
+        bdfs = [r["bdf"] for r in ranks]
+        if None in bdfs or len(set(bdfs)) != len(bdfs):
+            raise RuntimeError(f"ranks did not each get their own GPU: {bdfs}")
+    if distributed and pg_world != args.gpus:
+        raise RuntimeError(f"process group has {pg_world} ranks, --gpus {args.gpus}")
     fp8_tflops = None
     if not smoke and not args.no_fp8 and K.gemm_fp8_shape_supported(s, s, s):
         del a, b
@@ -333,6 +471,12 @@ def main(argv=None) -> int:
                            "w4a": "amdk8s_gemm_bf16_nt_256x256_w4a"}
                 .get(variant, "torch.matmul (cpu smoke)"),
             },
+            "world_size": world,
+            "process_group_world_size": pg_world,
+            "process_group_backend": (dist.get_backend() if distributed else None),
+            "launcher": os.environ.get("AMDK8S_BENCH_LAUNCHER",
+                                       "torchrun" if distributed else "single process"),
+            "ranks": ranks,
             "tflops_per_gpu": round(value / world, 2),
             "tflops_per_rank": per_rank,
             "settle": {"ms": 0.0 if smoke else args.settle_ms, "launches": settle_launches},

@@ -115,6 +115,69 @@ def test_bench_py_distributed_contract_on_cpu(world):
     assert 0 < doc["value"] <= sum(doc["tflops_per_rank"]) * 1.01 + 0.01 * world
 
 
+def _plain_bench(args, env_extra=None, timeout=300):
+    env = dict(os.environ, PYTHONPATH=str(REPO), OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TORCHELASTIC_RUN_ID"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, "bench.py"] + args, capture_output=True, text=True,
+                          env=env, cwd=str(REPO), timeout=timeout)
+
+
+def test_bench_py_plain_gpus_n_self_launches_n_ranks():
+    """``python bench.py --gpus 2`` without a launcher starts 2 ranks itself (VERDICT r05 weak 1:
+    it used to print n_gpus 1 with rc 0) and relays rank 0's single JSON line."""
+    p = _plain_bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--cpu-smoke", "--size", "256",
+                      "--no-allreduce"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    doc = json.loads(lines[0])
+    assert doc["n_gpus"] == 2 and doc["world_size"] == 2
+    assert doc["process_group_world_size"] == 2 and doc["process_group_backend"] == "gloo"
+    assert len(doc["tflops_per_rank"]) == 2
+    assert [r["rank"] for r in doc["ranks"]] == [0, 1]
+    assert doc["launcher"].startswith("torchrun (spawned")
+
+
+def test_bench_py_refuses_more_gpus_than_visible_agents(tmp_path):
+    """--gpus 3 on a node with 2 visible GPU agents exits non-zero before starting any rank."""
+    from tests.fakes.sysfs import build_node
+
+    root = build_node(tmp_path, n_gpus=2)
+    p = _plain_bench(["--gpus", "3", "--steps", "1", "--warmup", "0", "--cpu-smoke", "--size", "256"],
+                     {"AMDK8S_SYSFS_ROOT": str(root)})
+    assert p.returncode == 2, (p.stdout, p.stderr)
+    assert "only 2 GPU agent" in p.stderr and not p.stdout.strip()
+    # the same node with 2 GPUs asked for runs
+    p = _plain_bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--cpu-smoke", "--size", "128",
+                      "--no-allreduce"], {"AMDK8S_SYSFS_ROOT": str(root)})
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert json.loads(p.stdout.strip().splitlines()[-1])["n_gpus"] == 2
+    # HIP_VISIBLE_DEVICES narrows what is visible
+    p = _plain_bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--cpu-smoke", "--size", "128"],
+                     {"AMDK8S_SYSFS_ROOT": str(root), "HIP_VISIBLE_DEVICES": "1"})
+    assert p.returncode == 2 and "HIP_VISIBLE_DEVICES" in p.stderr
+
+
+def test_bench_py_world_size_mismatch_is_an_error():
+    """Under torchrun, WORLD_SIZE != --gpus fails instead of reporting the other N."""
+    p = _torchrun(["bench.py", "--gpus", "3", "--steps", "1", "--warmup", "0", "--cpu-smoke",
+                   "--size", "128"], 2)
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert "WORLD_SIZE=2" in p.stderr
+
+
+def test_bench_py_single_gpu_path_unchanged():
+    """N = 1 without a launcher stays one process (BENCH comparability across rounds)."""
+    p = _plain_bench(["--steps", "1", "--warmup", "0", "--cpu-smoke", "--size", "128"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    doc = json.loads(p.stdout.strip().splitlines()[-1])
+    assert doc["n_gpus"] == 1 and doc["launcher"] == "single process"
+    assert doc["process_group_world_size"] is None and "launching" not in p.stderr
+
+
 def test_bench_settle_phase_bounds():
     """bench.settle(): untimed launches until settle_ms of synchronized time, capped, off at 0."""
     import importlib.util
