@@ -266,8 +266,10 @@ class PartitionManager:
                     self._abort(f"driver reload command failed (rc={rc})")
                     return "failed"
             self._state("reenumerating", f"memory partition {want_m}")
+            # the reload keeps every ASIC's compute mode, so a CPX ASIC comes back as 8 agents
+            agents = sum(topo_mod.PARTITION_SPLIT.get(c, 1) for c, _ in modes.values())
             got = self._wait_modes(lambda ms: all(m == want_m for _, m in ms.values()),
-                                   len(asics), f"every ASIC in {want_m}")
+                                   agents, f"every ASIC in {want_m}")
             if isinstance(got, str):
                 self._abort(got)
                 return "failed"

@@ -272,6 +272,39 @@ def test_amdsmi_hive_spx_nps1_to_cpx_nps2_with_handle_invalidation(tmp_path, api
     assert _mgr(client, root, tmp_path, backend).reconcile() == "idle"
 
 
+def test_amdsmi_hive_cpx_nps1_to_cpx_nps2_waits_for_64_agents(tmp_path, api, client):
+    """a node already in CPX keeps CPX through the NPS reload, so the re-enumeration
+    wait must expect 8 agents per ASIC (it expected one per ASIC and timed out into `failed`)."""
+    from fakes.amdsmi_partition import FakeAmdSmiHive
+    from k8s_nvidia_gpus_amd.operator.partition_amdsmi import AmdSmiPartitionBackend
+
+    root = fake_sysfs.build_node(tmp_path / "r", compute_partition="CPX")
+    api.nodes["gpu-node-1"]["metadata"]["labels"][pm.LABEL_MEM_DESIRED] = "NPS2"
+    hive = FakeAmdSmiHive(root, compute="CPX")
+    backend = AmdSmiPartitionBackend(hive)
+    assert _mgr(client, root, tmp_path, backend, reenum_timeout=2).reconcile() == "applied"
+    assert hive.reloads == 1 and not [c for c in hive.calls if c[0] == "compute"]
+    topo = read_topology(str(root), 90500)
+    assert len(topo.gpus) == 64
+    assert {(g.compute_partition, g.memory_partition) for g in topo.gpus} == {("CPX", "NPS2")}
+    labels = api.nodes["gpu-node-1"]["metadata"]["labels"]
+    assert labels["amd.com/gpu.memory-partition"] == "NPS2"
+
+
+def test_sysfs_reload_command_cpx_nps1_to_cpx_nps2(tmp_path, api, client):
+    """The same CPX/NPS1 -> CPX/NPS2 change through sysfs writes plus the driver reload command."""
+    root = fake_sysfs.build_node(tmp_path / "r", compute_partition="CPX")
+    api.nodes["gpu-node-1"]["metadata"]["labels"][pm.LABEL_MEM_DESIRED] = "NPS2"
+    backend = DriverSysfs(root)
+    runs = []
+    mgr = _mgr(client, root, tmp_path, backend, reload_cmd=["/host/reload-amdgpu.sh"],
+               reenum_timeout=2, run_cmd=lambda argv: runs.append(argv) or backend.reload())
+    assert mgr.reconcile() == "applied" and runs == [["/host/reload-amdgpu.sh"]]
+    topo = read_topology(str(root), 90500)
+    assert len(topo.gpus) == 64 and backend.reloads == 1
+    assert {(g.compute_partition, g.memory_partition) for g in topo.gpus} == {("CPX", "NPS2")}
+
+
 def test_a_per_asic_nps_loop_on_one_session_fails_on_the_faithful_fake(tmp_path):
     """What the round-4 manager did — NPS per ASIC through the session opened at start — meets a
     dead session after the first (hive-wide) reload."""
