@@ -116,6 +116,9 @@ class Engine:
         self.prefill_native = True
         self.prefill_gqa = True
         self.prefill_qtok = True
+        # prompt attention on the hand-written causal GQA kernel over the cache slabs
+        # (ops/csrc/llm_prefill_attn.hip); False = PyTorch SDPA (the oracle of its tests)
+        self.prefill_attn_native = True
         # rejected variants (in-launch attention combine, fused residual norm, combine in the o_proj
         # prologue, MFMA attention, Infinity-Cache prefetch, ...): docs/experiments/llm_decode_rejected.md
         if self.gpu:
@@ -238,11 +241,23 @@ class Engine:
         else:
             qh = torch.empty(c.heads, P, c.head_dim, dtype=dt, device=self.device)
         t = torch.empty(P, c.ffn, dtype=dt, device=self.device)
+        native_attn = self.prefill_attn_native and self.prefill_qtok
+        if native_attn:
+            o = torch.empty(P, c.dim, dtype=dt, device=self.device)
+            oh = o.view(P, c.heads, c.head_dim).transpose(0, 1)
+        scale = 1.0 / math.sqrt(c.head_dim)
         for i, L in enumerate(self.w.layers):
             LK.rmsnorm_f16(x, L.attn_norm, c.eps, xn)
             qkv = mm(xn, W[f"{i}.qkv"], W[f"{i}.bqkv"])
             LK.rope_kv_f16(qkv, self.cos, self.sin, start, c.heads, c.kv_heads, self.max_ctx, qh,
                            self.k_cache[i, slot], self.v_cache[i, slot])
+            if native_attn:            # hand-written causal GQA kernel, K/V read in place
+                LK.prefill_attn(qh, self.k_cache[i, slot], self.v_cache[i, slot], oh, start, scale)
+                x = mm_res(x, o, W[f"{i}.o"])
+                LK.rmsnorm_f16(x, L.ffn_norm, c.eps, xn)
+                LK.swiglu_f16(mm(xn, W[f"{i}.gu"]), t)
+                x = mm_res(x, t, W[f"{i}.down"])
+                continue
             if self.prefill_gqa:       # K/V read in place by SDPA's GQA path; causal flag from 0
                 o = F.scaled_dot_product_attention(
                     qh[None], self.k_cache[i, slot, :, :end][None],
@@ -297,6 +312,11 @@ class Engine:
             for s, (_, slot, st) in enumerate(segs):
                 a, b = offs[s], offs[s + 1]
                 n, end = b - a, st + b - a
+                if self.prefill_attn_native:
+                    LK.prefill_attn(qh[:, a:b], self.k_cache[i, slot], self.v_cache[i, slot],
+                                    o[a:b].view(n, c.heads, c.head_dim).transpose(0, 1), st,
+                                    1.0 / math.sqrt(c.head_dim))
+                    continue
                 os_ = F.scaled_dot_product_attention(
                     qh[None, :, a:b], self.k_cache[i, slot, :, :end][None],
                     self.v_cache[i, slot, :, :end][None], attn_mask=lowright[s],

@@ -115,11 +115,23 @@ def _penalise(x: torch.Tensor, p: SamplingParams, history: Sequence[int]) -> tor
     return x - counts * p.frequency_penalty - seen.to(x.dtype) * p.presence_penalty
 
 
+def _one_hot(like: torch.Tensor, tok: int) -> torch.Tensor:
+    d = torch.zeros(like.numel(), dtype=torch.float32, device=like.device)
+    d[tok] = 1.0
+    return d
+
+
 def sample_token(logits: torch.Tensor, p: SamplingParams, history: Sequence[int] = (),
-                 generator: Optional[torch.Generator] = None) -> int:
-    """One token from fp logits [vocab] under ``p``; ``history`` = prompt + generated ids."""
+                 generator: Optional[torch.Generator] = None,
+                 dist_out: Optional[dict] = None) -> int:
+    """One token from fp logits [vocab] under ``p``; ``history`` = prompt + generated ids.
+    ``dist_out``: receives ``"probs"``, the distribution the token was drawn from (after the whole
+    sampler chain; one-hot when greedy) — llama-server's ``post_sampling_probs``."""
     if p.plain_greedy:
-        return int(torch.argmax(logits).item())
+        tok = int(torch.argmax(logits).item())
+        if dist_out is not None:
+            dist_out["probs"] = _one_hot(logits, tok)
+        return tok
     x = logits.float().clone()
     for tok, b in p.logit_bias.items():
         x[tok] += b
@@ -130,7 +142,10 @@ def sample_token(logits: torch.Tensor, p: SamplingParams, history: Sequence[int]
     if p.temperature <= 0.0:
         if not torch.isfinite(x.max()):
             raise NoTokenLeft("no token left to sample (every candidate was banned)")
-        return int(torch.argmax(x).item())
+        tok = int(torch.argmax(x).item())
+        if dist_out is not None:
+            dist_out["probs"] = _one_hot(x, tok)
+        return tok
     if p.top_k and p.top_k > 0:
         kth = torch.topk(x, min(p.top_k, x.numel())).values[-1]
         x = x.masked_fill(x < kth, -float("inf"))
@@ -149,4 +164,6 @@ def sample_token(logits: torch.Tensor, p: SamplingParams, history: Sequence[int]
     probs = torch.softmax((x - top) / p.temperature, -1)
     if generator is not None and generator.device != probs.device:
         probs = probs.to(generator.device)
+    if dist_out is not None:
+        dist_out["probs"] = probs
     return int(torch.multinomial(probs, 1, generator=generator).item())

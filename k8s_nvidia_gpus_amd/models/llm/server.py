@@ -10,7 +10,11 @@ layer is on the GPU) and serves the endpoints clients of that pod use:
 * ``POST /completion`` (llama.cpp native: ``prompt``, ``n_predict``, ``seed``, ``stop``,
   ``stream``, ``cache_prompt`` and the sampler fields of ``sampling.py`` — temperature, top_k,
   top_p, min_p, repeat_penalty / repeat_last_n, presence / frequency penalty, logit_bias) with
-  llama.cpp's ``timings`` block;
+  llama.cpp's ``timings`` block; ``n_probs`` (+ ``post_sampling_probs``) adds llama-server's
+  ``completion_probabilities``; ``grammar`` (GBNF), ``json_schema`` and ``response_format``
+  constrain the output (grammar.py) — OpenAI's ``logprobs`` / ``top_logprobs`` likewise.  A field
+  the server cannot honour (``n`` > 1, a schema keyword outside grammar.py's subset) is answered
+  with HTTP 400 naming it, never silently ignored;
 * ``POST /v1/completions`` and ``POST /v1/chat/completions`` (OpenAI; the prompt is rendered with
   the model file's own ``tokenizer.chat_template`` — chat_template.py — ChatML when it has none;
   ``tools`` are passed to the template; ``stream`` as server-sent events);
@@ -35,8 +39,11 @@ Prompt caching (llama-server's ``cache_prompt``, on by default): every slot reme
 its KV cache holds; a new request goes to the free slot sharing the longest prefix with its
 prompt, and only the rest of the prompt is prefilled (multi-turn chats re-send the whole history).
 As with llama-server, a reused prefix was computed in another prefill (a GEMM of another M), so
-the logits can differ in the last bits from an uncached prefill of the same prompt; decode itself
-is batch-invariant.
+the logits can differ in the last bits from an uncached prefill of the same prompt.  Prompts
+admitted in the same iteration are prefilled together (one GEMM over all their rows), so the same
+holds with concurrent traffic: a seeded or greedy request can differ in the last bits, and rarely
+in a token, depending on which prompts arrived with it — ``--no-prompt-batch`` prefills every
+prompt alone for runs that must reproduce exactly.  Decode itself is batch-invariant.
 """
 from __future__ import annotations
 
@@ -45,6 +52,7 @@ import asyncio
 import collections
 import gc
 import json
+import math
 import os
 import queue
 import threading
@@ -92,6 +100,16 @@ class Job:
     cancelled: bool = False
     n_cached: int = 0          # prompt tokens whose KV was reused from the slot
     waker: Any = None          # (event loop, asyncio.Event) of the coroutine waiting on ``out``
+    grammar: Any = None        # grammar.GrammarState: constrained decoding (grammar / JSON)
+    n_probs: int = 0           # top-n probabilities per generated token (n_probs / logprobs)
+    want_probs: bool = False   # record each generated token's probability entry
+    post_probs: bool = False   # entries from the sampler's final distribution, not the logits
+    probs: List[dict] = field(default_factory=list)
+
+    @property
+    def fast_greedy(self) -> bool:
+        """argmax of the raw logits is all this job needs (the in-graph greedy step applies)."""
+        return self.params.plain_greedy and self.grammar is None and not self.want_probs
 
     @property
     def text(self) -> str:
@@ -127,9 +145,14 @@ class Scheduler:
     searched only in the held-back tail plus the new text."""
 
     def __init__(self, engine: Engine, tok: Tokenizer, parallel: int = 8, ubatch: int = 512,
-                 batch: Optional[int] = None, autostart: bool = True):
+                 batch: Optional[int] = None, autostart: bool = True, prompt_batch: bool = True):
         self.engine = engine
         self.tok = tok
+        # prompt chunks of several slots in one pass (engine.prefill_many): its GEMMs run at an M
+        # that depends on which prompts arrived together, so a prompt's logits can differ in the
+        # last bits with the traffic; False prefills every prompt alone (--no-prompt-batch), for
+        # runs that must reproduce bit for bit (ADVICE r5)
+        self.prompt_batch = prompt_batch
         self.parallel = max(1, min(parallel, engine.slots))
         self.ubatch = max(1, int(ubatch))
         self.batch = max(self.ubatch, int(batch or self.ubatch))
@@ -141,6 +164,7 @@ class Scheduler:
         self.metrics = {"requests_total": 0, "prompt_tokens_total": 0, "tokens_predicted_total": 0,
                         "decode_steps_total": 0, "decode_seconds_total": 0.0,
                         "prefill_seconds_total": 0.0, "prefill_chunks_total": 0,
+                        "prefill_batches_total": 0,
                         "requests_processing": 0, "prompt_tokens_cached_total": 0}
         self._touched: List[Job] = []
         # per-iteration timings (GET /debug/iterations): start, admit / prefill / step / wake
@@ -251,6 +275,54 @@ class Scheduler:
             return g
         return job.ids[max(0, len(job.ids) - (n - len(g))):] + g
 
+    def _sample(self, job: Job, logits: torch.Tensor) -> int:
+        """The job's next token from ``logits`` [vocab]: its sampler chain, under its grammar as
+        llama.cpp's common sampler does (keep the draw when the grammar accepts it, else mask
+        every rejected token and draw again), and its probability entry when it asked for one."""
+        dist: Optional[dict] = {} if job.post_probs else None
+        hist = self._recent(job)
+        tok = sample_token(logits, job.params, hist, job.generator, dist_out=dist)
+        g = job.grammar
+        if g is not None and not g.accepts(tok):
+            mask = g.mask(logits.numel(), logits.device)
+            if not bool(mask.any()):
+                from .grammar import GrammarError
+
+                raise GrammarError("no token of the vocabulary can continue the grammar here")
+            tok = sample_token(logits.masked_fill(~mask, -float("inf")), job.params, hist,
+                               job.generator, dist_out=dist)
+        if g is not None:
+            g.advance(tok)
+        if job.want_probs:
+            entry = self._probs_entry(job, logits, tok, dist)
+            job.probs.append(entry)
+            self._put(job, ("probs", entry))
+        return tok
+
+    def _piece(self, tid: int) -> dict:
+        bs = self.tok.token_bytes()[tid] if 0 <= tid < len(self.tok.token_bytes()) else b""
+        return {"id": tid, "token": bs.decode("utf-8", "replace") if bs else
+                self.tok.decode([tid], skip_special=False), "bytes": list(bs)}
+
+    def _probs_entry(self, job: Job, logits: torch.Tensor, tok: int, dist) -> dict:
+        """llama-server's per-token entry: the token, its log-probability under the model's
+        softmax (or, post_probs, its probability in the sampler's final distribution) and the
+        n most likely alternatives."""
+        if job.post_probs:
+            p = dist["probs"].float()
+            k = min(job.n_probs, int((p > 0).sum().item())) if job.n_probs else 0
+            top = torch.topk(p, k) if k else None
+            e = dict(self._piece(tok), prob=float(p[tok].item()))
+            e["top"] = ([dict(self._piece(int(i)), prob=float(v)) for v, i in
+                         zip(top.values.tolist(), top.indices.tolist())] if top is not None else [])
+            return e
+        lp = torch.log_softmax(logits.float(), -1)
+        top = torch.topk(lp, min(job.n_probs, lp.numel())) if job.n_probs else None
+        e = dict(self._piece(tok), logprob=float(lp[tok].item()))
+        e["top"] = ([dict(self._piece(int(i)), logprob=float(v)) for v, i in
+                     zip(top.values.tolist(), top.indices.tolist())] if top is not None else [])
+        return e
+
     def _emit(self, job: Job, tok: int) -> bool:
         """Record a sampled token; returns True when the job is finished."""
         job.gen.append(tok)
@@ -260,6 +332,11 @@ class Scheduler:
             self._flush(job, job.detok.flush(), final=True)
             return True
         new = job.detok.push(tok)
+        if job.grammar is not None and job.grammar.finished:
+            # the grammar admits nothing but the end: the answer is complete
+            job.finish = "stop"
+            self._flush(job, new + job.detok.flush(), final=True)
+            return True
         if len(job.gen) >= job.max_new:
             job.finish = "length"
             self._flush(job, new + job.detok.flush(), final=True)
@@ -346,35 +423,41 @@ class Scheduler:
             if budget == 0:
                 break
         t0 = time.perf_counter()
-        many = getattr(self.engine, "prefill_many", None)
+        many = getattr(self.engine, "prefill_many", None) if self.prompt_batch else None
         results = {}
+        batch_s = 0.0
         if many is not None and len(work) > 1:
             try:
                 out = many([(job.ids[job.pos:job.pos + n], job.slot, job.pos) for job, n in work])
                 results = {id(job): lg for (job, _), lg in zip(work, out)}
             except Exception:  # noqa: BLE001 - retried one by one below, so only the bad one fails
                 results = {}
+            batch_s = time.perf_counter() - t0
+        n_batched = sum(n for job, n in work if id(job) in results)
         total = 0
         for job, n in work:
+            t_job = time.perf_counter()
             try:
                 logits = results.get(id(job))
                 if logits is None:
                     logits = self.engine.prefill(job.ids[job.pos:job.pos + n], job.slot,
                                                  start=job.pos)
                 done = job.pos + n == len(job.ids)
-                tok = (sample_token(logits, job.params, self._recent(job), job.generator)
-                       if done else None)
+                tok = self._sample(job, logits) if done else None
             except Exception as e:  # noqa: BLE001 - this job fails; the others keep decoding
                 self.prefilling.remove(job)
                 self._fail(job, e)
                 continue
-            dt = time.perf_counter() - t0
+            # each job is charged its own time: its own prefill (+ sampling), or its token share
+            # of the shared batch; the batch wall time is counted once below
+            own = time.perf_counter() - t_job
+            if id(job) in results:
+                own += batch_s * n / max(n_batched, 1)
             job.pos += n
-            job.t_prefill += dt
+            job.t_prefill += own
             total += n
             with self._lock:
                 self.metrics["prompt_tokens_total"] += n
-                self.metrics["prefill_seconds_total"] += dt
                 self.metrics["prefill_chunks_total"] += 1
             if not done:
                 continue
@@ -386,6 +469,10 @@ class Scheduler:
                 self.metrics["tokens_predicted_total"] += 1
             if self._emit(job, int(tok)):
                 self._release(job)
+        if work:
+            with self._lock:
+                self.metrics["prefill_seconds_total"] += time.perf_counter() - t0
+                self.metrics["prefill_batches_total"] += 1
         return total
 
     def _step(self) -> int:
@@ -397,14 +484,14 @@ class Scheduler:
             return 0
         t0 = time.perf_counter()
         args = ([j.last for j in jobs], [j.pos for j in jobs], [j.slot for j in jobs])
-        if all(j.params.plain_greedy for j in jobs) and hasattr(self.engine, "decode_greedy"):
+        if all(j.fast_greedy for j in jobs) and hasattr(self.engine, "decode_greedy"):
             toks = self.engine.decode_greedy(*args)       # argmax inside the step's graph
         else:
             logits = self.engine.decode(*args)
             toks = []
             for i, j in enumerate(jobs):
                 try:   # a request's own sampler failure ends that request only
-                    toks.append(sample_token(logits[i], j.params, self._recent(j), j.generator))
+                    toks.append(self._sample(j, logits[i]))
                 except Exception as e:  # noqa: BLE001
                     toks.append(e)
         dt = time.perf_counter() - t0
@@ -448,18 +535,104 @@ class Scheduler:
 
 
 # -------------------------------------------------------------------- HTTP layer
+def _int_field(body: Dict[str, Any], key: str, lo: int, hi: int) -> Optional[int]:
+    v = body.get(key)
+    if v is None:
+        return None
+    if isinstance(v, bool) or not isinstance(v, int) or not lo <= v <= hi:
+        raise ValueError(f"{key} must be an integer in [{lo}, {hi}], got {v!r}")
+    return v
+
+
+def _probs_request(body: Dict[str, Any], api: str, vocab: Optional[int]) -> tuple:
+    """(record entries, top-n, post-sampling) from llama-server's ``n_probs`` /
+    ``post_sampling_probs`` or OpenAI's ``logprobs`` (+ ``top_logprobs`` for chat)."""
+    vmax = int(vocab or 1 << 20)
+    post = body.get("post_sampling_probs")
+    if post is not None and not isinstance(post, bool):
+        raise ValueError("post_sampling_probs must be a boolean")
+    if api == "chat":
+        lp = body.get("logprobs")
+        if lp is not None and not isinstance(lp, bool):
+            raise ValueError("logprobs must be a boolean for chat completions")
+        top = _int_field(body, "top_logprobs", 0, 20)
+        if top is not None and not lp:
+            raise ValueError("top_logprobs needs logprobs: true")
+        n = _int_field(body, "n_probs", 0, vmax) or 0
+        return bool(lp) or n > 0, (top if top is not None else n), bool(post)
+    if api == "completions":
+        lp = body.get("logprobs")
+        if lp is not None and (isinstance(lp, bool) or not isinstance(lp, int) or lp < 0
+                               or lp > min(vmax, 100)):
+            raise ValueError("logprobs must be an integer in [0, 100] for completions")
+        n = _int_field(body, "n_probs", 0, vmax) or 0
+        return lp is not None or n > 0, (lp if lp is not None else n), bool(post)
+    n = _int_field(body, "n_probs", 0, vmax) or 0
+    return n > 0, n, bool(post)
+
+
 def _job_from(body: Dict[str, Any], ids: List[int], default_max: int,
-              vocab: Optional[int] = None) -> Job:
+              vocab: Optional[int] = None, tok: Optional[Tokenizer] = None,
+              stop_ids=(), api: str = "native") -> Job:
+    """A request body -> Job.  Fields the server cannot honour are rejected (ValueError -> HTTP
+    400) rather than ignored: ``n`` other than 1, a grammar / schema outside what
+    grammar.py enforces, malformed probability requests."""
+    from .grammar import GrammarState, grammar_from_request, matcher_for
+
+    n_choices = body.get("n")
+    if n_choices is not None and n_choices != 1:
+        raise ValueError("n: only one choice per request is supported (n = 1)")
     stop = body.get("stop") or []
     if isinstance(stop, str):
         stop = [stop]
     n = body.get("n_predict", body.get("max_tokens", body.get("max_completion_tokens")))
     if n is None or int(n) < 0:
         n = default_max
+    want, n_probs, post = _probs_request(body, api, vocab)
+    src = grammar_from_request(body)
+    gstate = None
+    if src is not None:
+        if tok is None:
+            raise ValueError("grammar: this server has no tokenizer to constrain with")
+        gstate = GrammarState(matcher_for(src), tok, stop_ids)
     return Job(ids=ids, max_new=int(n), params=SamplingParams.from_request(body, vocab),
                seed=None if body.get("seed") in (None, -1) else int(body["seed"]), stop=list(stop),
                cache_prompt=bool(body.get("cache_prompt", True)),
-               ignore_eos=bool(body.get("ignore_eos", False)))
+               ignore_eos=bool(body.get("ignore_eos", False)), grammar=gstate,
+               n_probs=int(n_probs), want_probs=want, post_probs=post)
+
+
+def _native_probs(entries: List[dict], post: bool) -> List[dict]:
+    """llama-server's ``completion_probabilities`` items."""
+    key, tkey = ("prob", "top_probs") if post else ("logprob", "top_logprobs")
+    return [{"id": e["id"], "token": e["token"], "bytes": e["bytes"], key: e[key],
+             tkey: [{"id": t["id"], "token": t["token"], "bytes": t["bytes"], key: t[key]}
+                    for t in e["top"]]} for e in entries]
+
+
+def _chat_logprobs(entries: List[dict]) -> Dict[str, Any]:
+    """OpenAI chat ``choices[].logprobs``."""
+    def lp(e):
+        return e["logprob"] if "logprob" in e else (math.log(e["prob"]) if e["prob"] > 0
+                                                     else -9999.0)
+    return {"content": [{"token": e["token"], "logprob": lp(e), "bytes": e["bytes"],
+                         "top_logprobs": [{"token": t["token"], "logprob": lp(t),
+                                           "bytes": t["bytes"]} for t in e["top"]]}
+                        for e in entries]}
+
+
+def _completion_logprobs(entries: List[dict], offset: int = 0) -> Dict[str, Any]:
+    """OpenAI (legacy) completions ``choices[].logprobs``."""
+    def lp(e):
+        return e["logprob"] if "logprob" in e else (math.log(e["prob"]) if e["prob"] > 0
+                                                     else -9999.0)
+    offs = []
+    for e in entries:
+        offs.append(offset)
+        offset += len(e["token"])
+    return {"tokens": [e["token"] for e in entries], "token_logprobs": [lp(e) for e in entries],
+            "top_logprobs": [{t["token"]: lp(t) for t in e["top"]} for e in entries],
+            "text_offset": offs}
 
 
 class RequestTimeout(RuntimeError):
@@ -613,10 +786,11 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
     def detokenize(body: Dict[str, Any]):
         return {"content": state["tok"].decode(body.get("tokens", []))}
 
-    def submit(body, ids, default_max):
+    def submit(body, ids, default_max, api="native"):
         s = sched()
         try:
-            return s.submit(_job_from(body, ids, default_max, s.engine.cfg.vocab))
+            return s.submit(_job_from(body, ids, default_max, s.engine.cfg.vocab, state["tok"],
+                                      s.stop_ids, api))
         except ValueError as e:
             raise HTTPException(400, str(e))
 
@@ -636,32 +810,52 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
         job = submit(body, await aencode(body.get("prompt", "")), s.engine.max_ctx)
         if body.get("stream"):
             async def gen():
+                pend: List[dict] = []
                 async for kind, val in _astream(job, request_timeout, request.is_disconnected):
+                    if kind == "probs":
+                        pend.append(val)
+                        continue
                     if kind == "text":
-                        yield "data: " + json.dumps({"content": val, "stop": False}) + "\n\n"
+                        d = {"content": val, "stop": False}
                     else:
-                        yield "data: " + json.dumps({"content": "", "stop": True,
-                                                     "timings": _timings(val)}) + "\n\n"
+                        d = {"content": "", "stop": True, "timings": _timings(val)}
+                    if job.want_probs and pend:
+                        d["completion_probabilities"] = _native_probs(pend, job.post_probs)
+                        pend = []
+                    yield "data: " + json.dumps(d) + "\n\n"
             return StreamingResponse(gen(), media_type="text/event-stream")
         job = await wait(job, request)
-        return {"content": job.text, "stop": True, "model": state.get("model"),
-                "tokens_predicted": len(job.gen), "tokens_evaluated": len(job.ids),
-                "tokens_cached": job.pos,
-                "stopped_eos": job.finish == "stop" and job.gen[-1] in s.stop_ids,
-                "stopped_limit": job.finish == "length",
-                "stopped_word": job.finish == "stop" and job.gen[-1] not in s.stop_ids,
-                "timings": _timings(job)}
+        out = {"content": job.text, "stop": True, "model": state.get("model"),
+               "tokens_predicted": len(job.gen), "tokens_evaluated": len(job.ids),
+               "tokens_cached": job.pos,
+               "stopped_eos": job.finish == "stop" and job.gen[-1] in s.stop_ids,
+               "stopped_limit": job.finish == "length",
+               "stopped_word": (job.finish == "stop" and job.gen[-1] not in s.stop_ids
+                                and job.grammar is None),
+               "timings": _timings(job)}
+        if job.want_probs:
+            out["completion_probabilities"] = _native_probs(job.probs, job.post_probs)
+        return out
 
     async def openai(body, ids, chat: bool, request: Request):
         s = sched()
-        job = submit(body, ids, 16 if not chat else s.engine.max_ctx)
+        job = submit(body, ids, 16 if not chat else s.engine.max_ctx,
+                     "chat" if chat else "completions")
+
+        def lp_block(entries, offset=0):
+            return _chat_logprobs(entries) if chat else _completion_logprobs(entries, offset)
         rid = ("chatcmpl-" if chat else "cmpl-") + uuid.uuid4().hex[:24]
         created = int(time.time())
         obj = "chat.completion" if chat else "text_completion"
         if body.get("stream"):
             async def gen():
                 first = True
+                pend: List[dict] = []
+                sent = 0
                 async for kind, val in _astream(job, request_timeout, request.is_disconnected):
+                    if kind == "probs":
+                        pend.append(val)
+                        continue
                     if kind == "text":
                         if chat:
                             delta = {"content": val}
@@ -670,6 +864,10 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
                             ch = {"index": 0, "delta": delta, "finish_reason": None}
                         else:
                             ch = {"index": 0, "text": val, "finish_reason": None}
+                        if job.want_probs:
+                            ch["logprobs"] = lp_block(pend, sent)
+                            sent += sum(len(e["token"]) for e in pend)
+                            pend = []
                         first = False
                         yield "data: " + json.dumps({"id": rid, "object": obj + ".chunk" if chat
                                                      else obj, "created": created,
@@ -678,6 +876,8 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
                     else:     # the last chunk carries usage and llama-server's timings
                         ch = {"index": 0, "finish_reason": val.finish}
                         ch["delta" if chat else "text"] = {} if chat else ""
+                        if job.want_probs and pend:
+                            ch["logprobs"] = lp_block(pend, sent)
                         yield "data: " + json.dumps({"id": rid, "object": obj + ".chunk" if chat
                                                      else obj, "created": created,
                                                      "model": state.get("model"),
@@ -686,7 +886,8 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
                 yield "data: [DONE]\n\n"
             return StreamingResponse(gen(), media_type="text/event-stream")
         job = await wait(job, request)
-        choice = {"index": 0, "finish_reason": job.finish, "logprobs": None}
+        choice = {"index": 0, "finish_reason": job.finish,
+                  "logprobs": lp_block(job.probs) if job.want_probs else None}
         if chat:
             choice["message"] = {"role": "assistant", "content": job.text}
         else:
@@ -802,6 +1003,9 @@ def main(argv=None) -> int:
                     help="prompt tokens per chunk while nothing decodes (llama-server -b)")
     ap.add_argument("-ngl", "--n-gpu-layers", type=int, default=999, help="accepted; all layers run on the GPU")
     ap.add_argument("-t", "--threads", type=int, default=0, help="accepted; the GPU does the work")
+    ap.add_argument("--no-prompt-batch", action="store_true",
+                    help="prefill every prompt alone instead of batching the prompts admitted "
+                         "together: a prompt's logits then never depend on concurrent traffic")
     ap.add_argument("-to", "--timeout", type=float, default=600.0,
                     help="seconds a request may wait for its result (then 504 and cancelled)")
     args = ap.parse_args(argv)
@@ -818,7 +1022,8 @@ def main(argv=None) -> int:
             eng.warmup()                                                # prompt path, first use
         state.update(tok=tok, model=name, scheduler=Scheduler(eng, tok, args.parallel,
                                                             ubatch=args.ubatch_size,
-                                                            batch=args.batch_size))
+                                                            batch=args.batch_size,
+                                                            prompt_batch=not args.no_prompt_batch))
         print(f"model {name} ready (ctx {eng.max_ctx}, parallel {args.parallel})", flush=True)
 
     threading.Thread(target=load_bg, daemon=True).start()

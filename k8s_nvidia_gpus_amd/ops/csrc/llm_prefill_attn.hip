@@ -1,0 +1,437 @@
+// Causal GQA prompt attention straight from the KV-cache slab (LLM prefill), gfx950, head dim 128.
+//
+//   O[p, h] = softmax_j≤start+p( q[p, h] · K[g(h), j] · scale ) V[g(h), j]     g(h) = h / group
+//
+// The prompt path of the in-tree Qwen2 engine (models/llm/engine.py) — the counterpart of the
+// flash-attention llama-server runs over a prompt batch (reference cluster-config/apps/llm/
+// deployment.yaml:61,78-84).  A chunk of P prompt tokens sits at positions start .. start+P-1 of one
+// sequence slot; its keys are every cached position 0 .. start+P-1 (causal, aligned bottom-right).
+//
+// Layout of the work:
+// * GQA: the query rows of one KV head are flattened token-major, row = p * group + (h % group), so
+//   one workgroup of NW waves × 32 rows covers every head of the group for ~NW·32/group tokens and
+//   each 64-key K/V tile is staged through LDS ONCE for all of them (7 q heads per KV head on
+//   Qwen2.5-7B) — and the causal boundary of a 32-row wave spans only ~5 positions.
+// * Causal: a workgroup loops over the key tiles up to its last token; a wave skips the tiles past
+//   its own last token (wave-uniform branch, it still helps stage tiles) and masks per lane only
+//   on the tiles that straddle its diagonal.
+// * K/V are read in place: kc / vc point at the slot's [Hkv][max_ctx][128] fp16 slabs; q and the
+//   output are token-major [P][H][128] views (any token / head stride).
+// * Split over keys: a long context with few query rows (a 512-token chunk at position 31 488 has
+//   4 KV heads × 28 row blocks) would leave most of the 256 CUs idle, so the key tiles are cut into
+//   `nsplit` ranges; each workgroup writes unnormalised fp32 partials + (max, sum) and a combine
+//   launch merges them.  nsplit = 1 writes the normalised output directly.
+// The inner loop is the one of attn_d128.hip: Sᵀ = K·Qᵀ and Oᵀ += Vᵀ·Pᵀ on v_mfma_f32_32x32x16 with
+// Qᵀ in registers, softmax in registers (a lane owns one query row), deferred max rescaling,
+// XOR-swizzled LDS images, transposed V reads (ds_read_b64_tr_b16), double-buffered tiles.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int kD = 128;
+constexpr int kKeys = 64;                 // keys per tile
+constexpr int kRB = 256;                  // LDS row bytes (128 fp16)
+constexpr int kCR = kD / 8;               // 16-byte chunks per row
+constexpr int kTile = kKeys * kRB;        // 16 KiB per operand tile
+constexpr int kBuf = 2 * kTile;           // K + V
+constexpr int kLds = 2 * kBuf;            // double buffered: 64 KiB
+constexpr int kKsteps = kD / 16;
+constexpr int kDblk = kD / 32;
+constexpr float kNoMax = -1e30f;          // finite "no score yet" (a fully masked row stays NaN-free)
+
+__device__ __forceinline__ int kswz(int row, int ch) { return ch ^ (row & 15); }
+__device__ __forceinline__ int vswz(int row, int ch) { return ch ^ ((row & 3) << 2); }
+
+template <bool BF16>
+__device__ __forceinline__ f32x16 mfma32(const s16x8 a, const s16x8 b, const f32x16 c) {
+  if constexpr (BF16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+template <bool BF16>
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  if constexpr (BF16) {
+    const bf16x2 v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(uint32_t, v);
+  } else {
+    return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(lo, hi));
+  }
+}
+
+struct Args {
+  const uint16_t* q;
+  const uint16_t* k;
+  const uint16_t* v;
+  uint16_t* o;
+  float* opart;      // [nsplit][P*H][128] (nsplit > 1)
+  float* ml;         // [nsplit][P*H][2]   (max, sum)
+  long sq_tok, sq_head, so_tok, so_head, skv_head;   // element strides (key row stride = 128)
+  int P, start, H, Hkv, group, nrb, nsplit, tps;
+  float c;           // scale * log2(e)
+};
+
+template <bool BF16, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) {
+  constexpr int NT = NW * 64;
+  constexpr int NCH = kKeys * kCR;
+  constexpr int CH = NCH / NT;
+  static_assert(NCH % NT == 0, "tile chunks per thread");
+  __shared__ __attribute__((aligned(16))) char lds[kLds];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+
+  // XCD-major block -> work item (consecutive work items share an XCD and so its L2); work order:
+  // row block fastest (latest tokens first: they own the most key tiles), then KV head, then split
+  int work;
+  {
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, idx = bid >> 3;
+    const int qn = nwg >> 3, rem = nwg & 7;
+    work = (xcd < rem ? xcd * (qn + 1) : rem * (qn + 1) + (xcd - rem) * qn) + idx;
+  }
+  const int rbi = work % a.nrb;
+  const int rest = work / a.nrb;
+  const int g = rest % a.Hkv;
+  const int split = rest / a.Hkv;
+  const int rb = a.nrb - 1 - rbi;
+
+  const int rows = a.P * a.group;            // query rows of this KV head
+  const long rowsH = (long)a.P * a.H;        // query rows of the whole chunk (partials' index)
+  const int R0 = rb * (NW * 32);
+  const int p_hi_wg = min(a.P - 1, (R0 + NW * 32 - 1) / a.group);
+  const int kend = a.start + p_hi_wg + 1;    // keys [0, kend) reach this workgroup
+  const int nt_wg = (kend + kKeys - 1) / kKeys;
+  const int t0 = split * a.tps, t1 = min(nt_wg, t0 + a.tps);
+
+  // this lane's query row
+  const int row = R0 + wave * 32 + r;
+  const bool valid = row < rows;
+  const int p = valid ? row / a.group : a.P - 1;
+  const int head = g * a.group + (valid ? row - p * a.group : 0);
+  const int qpos = a.start + p;
+  const long grow = (long)p * a.H + head;
+
+  if (t0 >= t1) {                            // nothing of this split reaches the workgroup
+    if (valid && h == 0)
+      *reinterpret_cast<float2*>(a.ml + 2 * ((long)split * rowsH + grow)) = make_float2(kNoMax, 0.f);
+    return;
+  }
+
+  // this wave's token range (wave-uniform)
+  const int wrow0 = R0 + wave * 32;
+  const bool wave_valid = wrow0 < rows;
+  const int pw_lo = wrow0 / a.group;
+  const int pw_hi = min(a.P - 1, (wrow0 + 31) / a.group);
+
+  const uint16_t* kb = a.k + (long)g * a.skv_head;
+  const uint16_t* vb = a.v + (long)g * a.skv_head;
+
+  s16x8 qf[kKsteps];
+  {
+    const uint16_t* qr = a.q + (long)p * a.sq_tok + (long)head * a.sq_head;
+#pragma unroll
+    for (int s = 0; s < kKsteps; ++s) qf[s] = *reinterpret_cast<const s16x8*>(qr + 16 * s + 8 * h);
+  }
+
+  f32x16 o[kDblk];
+#pragma unroll
+  for (int t = 0; t < kDblk; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[t][i] = 0.f;
+  float m = kNoMax, l = 0.f;
+
+  uint4 kr[CH], vr[CH];
+  auto load_tile = [&](int kbase) {
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int c = tid + j * NT, krow = c / kCR, ch = c - krow * kCR;
+      const int key = kbase + krow;
+      if (key < kend) {
+        kr[j] = *reinterpret_cast<const uint4*>(kb + (long)key * kD + ch * 8);
+        vr[j] = *reinterpret_cast<const uint4*>(vb + (long)key * kD + ch * 8);
+      } else {                               // past the last query: zeros (never NaN * 0)
+        kr[j] = make_uint4(0, 0, 0, 0);
+        vr[j] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* kl = lds + buf * kBuf;
+    char* vl = kl + kTile;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int c = tid + j * NT, krow = c / kCR, ch = c - krow * kCR;
+      *reinterpret_cast<uint4*>(kl + krow * kRB + (kswz(krow, ch) << 4)) = kr[j];
+      *reinterpret_cast<uint4*>(vl + krow * kRB + (vswz(krow, ch) << 4)) = vr[j];
+    }
+  };
+
+  const int kofs = r * kRB;
+  const int g16 = lane >> 4, qq = (lane & 15) >> 2, pl = lane & 3;
+  const int vcol_chunk = 2 * (g16 & 1) + (pl >> 1);
+  const int vsub = 8 * (pl & 1);
+  const int vrow = 4 * h + qq;
+  const float thr = 8.f / a.c;
+
+  load_tile(t0 * kKeys);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = t0; kt < t1; ++kt) {
+    const int kbase = kt * kKeys;
+    const int buf = (kt - t0) & 1;
+    const char* kl = lds + buf * kBuf;
+    const char* vl = kl + kTile;
+    if (kt + 1 < t1) load_tile(kbase + kKeys);
+
+    if (wave_valid && kbase <= a.start + pw_hi) {
+      f32x16 s[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[b][i] = 0.f;
+#pragma unroll
+        for (int st = 0; st < kKsteps; ++st) {
+          const s16x8 kf = *reinterpret_cast<const s16x8*>(
+              kl + b * 32 * kRB + kofs + (kswz(r, 2 * st + h) << 4));
+          s[b] = mfma32<BF16>(kf, qf[st], s[b]);
+        }
+      }
+      if (kbase + kKeys - 1 > a.start + pw_lo) {     // the tile straddles this wave's diagonal
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (kbase + 32 * b + 8 * (i >> 2) + 4 * h + (i & 3) > qpos) s[b][i] = -INFINITY;
+      }
+
+      float lmax = s[0][0];
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) lmax = fmaxf(lmax, s[b][i]);
+      if (__builtin_amdgcn_ballot_w64(lmax > m + thr) != 0) {
+        const float tmax = fmaxf(lmax, __shfl_xor(lmax, 32, 64));
+        const float mnew = fmaxf(m, tmax);
+        const float alpha = __builtin_amdgcn_exp2f((m - mnew) * a.c);
+        m = mnew;
+        l *= alpha;
+#pragma unroll
+        for (int t = 0; t < kDblk; ++t) o[t] *= alpha;
+      }
+      const float mc = m * a.c;
+      s16x8 pf[4];
+      float rs0 = 0.f, rs1 = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int b = ks >> 1, base = 8 * (ks & 1);
+        float e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) e[j] = __builtin_amdgcn_exp2f(fmaf(s[b][base + j], a.c, -mc));
+        rs0 += (e[0] + e[1]) + (e[2] + e[3]);
+        rs1 += (e[4] + e[5]) + (e[6] + e[7]);
+        pf[ks] = __builtin_bit_cast(
+            s16x8, make_uint4(pack2<BF16>(e[0], e[1]), pack2<BF16>(e[2], e[3]),
+                              pack2<BF16>(e[4], e[5]), pack2<BF16>(e[6], e[7])));
+      }
+      l += rs0 + rs1;
+
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int r0 = 16 * ks + vrow, r1 = r0 + 8;
+        const char* v0 = vl + r0 * kRB + vsub;
+        const char* v1 = vl + r1 * kRB + vsub;
+#pragma unroll
+        for (int db = 0; db < kDblk; ++db) {
+          const int c0 = vswz(r0, 4 * db + vcol_chunk), c1 = vswz(r1, 4 * db + vcol_chunk);
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(v0 + (c0 << 4)));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(v1 + (c1 << 4)));
+          const s16x8 vf = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          o[db] = mfma32<BF16>(vf, pf[ks], o[db]);
+        }
+      }
+    }
+
+    if (kt + 1 < t1) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds O[row][32db + 8(i>>2) + 4h + (i&3)] (unnormalised), its half of the sum
+  const float lt = l + __shfl_xor(l, 32, 64);
+  if (!valid) return;
+  if (a.nsplit == 1) {
+    const float inv = 1.f / lt;
+    uint16_t* orow = a.o + (long)p * a.so_tok + (long)head * a.so_head;
+#pragma unroll
+    for (int db = 0; db < kDblk; ++db)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        uint2 w;
+        w.x = pack2<BF16>(o[db][4 * gq] * inv, o[db][4 * gq + 1] * inv);
+        w.y = pack2<BF16>(o[db][4 * gq + 2] * inv, o[db][4 * gq + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + 32 * db + 8 * gq + 4 * h) = w;
+      }
+    return;
+  }
+  const long prow = (long)split * rowsH + grow;
+  float* op = a.opart + prow * kD;
+#pragma unroll
+  for (int db = 0; db < kDblk; ++db)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq)
+      *reinterpret_cast<float4*>(op + 32 * db + 8 * gq + 4 * h) =
+          make_float4(o[db][4 * gq], o[db][4 * gq + 1], o[db][4 * gq + 2], o[db][4 * gq + 3]);
+  if (h == 0) *reinterpret_cast<float2*>(a.ml + 2 * prow) = make_float2(m, lt);
+}
+
+// one wave per query row (p, h): merge the nsplit partials -> normalised output
+template <bool BF16>
+__global__ __launch_bounds__(256) void prefill_attn_combine(const Args a) {
+  const long rowsH = (long)a.P * a.H;
+  const long grow = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (grow >= rowsH) return;
+  float M = kNoMax;
+  for (int s = 0; s < a.nsplit; ++s) {
+    const float2 ml = *reinterpret_cast<const float2*>(a.ml + 2 * ((long)s * rowsH + grow));
+    if (ml.y > 0.f) M = fmaxf(M, ml.x);
+  }
+  float L = 0.f, x0 = 0.f, x1 = 0.f;
+  for (int s = 0; s < a.nsplit; ++s) {
+    const long prow = (long)s * rowsH + grow;
+    const float2 ml = *reinterpret_cast<const float2*>(a.ml + 2 * prow);
+    if (!(ml.y > 0.f)) continue;               // empty split: its partial O was never written
+    const float w = __builtin_amdgcn_exp2f((ml.x - M) * a.c);
+    const float2 v = *reinterpret_cast<const float2*>(a.opart + prow * kD + 2 * lane);
+    L = fmaf(ml.y, w, L);
+    x0 = fmaf(v.x, w, x0);
+    x1 = fmaf(v.y, w, x1);
+  }
+  const float inv = 1.f / L;
+  const int p = (int)(grow / a.H), head = (int)(grow - (long)p * a.H);
+  *reinterpret_cast<uint32_t*>(a.o + (long)p * a.so_tok + (long)head * a.so_head + 2 * lane) =
+      pack2<BF16>(x0 * inv, x1 * inv);
+}
+
+struct Plan {
+  int nw, nrb, nsplit, tps;
+};
+
+Plan make_plan(int P, int start, int H, int Hkv, int nsplit_req, int nw_req) {
+  Plan pl;
+  const int group = H / Hkv;
+  const long rows = (long)P * group;
+  // 8-wave workgroups when there are enough rows to fill the chip with them, else 4
+  pl.nw = (nw_req == 4 || nw_req == 8) ? nw_req : ((rows + 255) / 256 * Hkv >= 512 ? 8 : 4);
+  pl.nrb = (int)((rows + pl.nw * 32 - 1) / (pl.nw * 32));
+  const int ntiles = (start + P + kKeys - 1) / kKeys;
+  const long base = (long)pl.nrb * Hkv;
+  int ns;
+  if (nsplit_req > 0) {
+    ns = nsplit_req;
+  } else {
+    // split the keys until ~2 workgroups per CU are busy, keeping >= 16 tiles per split
+    ns = (int)((512 + base - 1) / base);
+    ns = min(ns, max(1, ntiles / 16));
+    ns = min(ns, 32);
+  }
+  ns = max(1, min(ns, ntiles));
+  pl.tps = (ntiles + ns - 1) / ns;
+  pl.nsplit = (ntiles + pl.tps - 1) / pl.tps;
+  return pl;
+}
+
+template <bool BF16, int NW>
+int launch(Args a, const Plan& pl, hipStream_t stream) {
+  const long nwg = (long)pl.nrb * a.Hkv * pl.nsplit;
+  if (nwg <= 0 || nwg > 0x7fffffff) return -1;
+  hipLaunchKernelGGL((prefill_attn_kernel<BF16, NW>), dim3((unsigned)nwg), dim3(NW * 64), 0, stream,
+                     a);
+  if (hipGetLastError() != hipSuccess) return -2;
+  if (pl.nsplit > 1) {
+    const long rowsH = (long)a.P * a.H;
+    hipLaunchKernelGGL((prefill_attn_combine<BF16>), dim3((unsigned)((rowsH + 3) / 4)), dim3(256), 0,
+                       stream, a);
+    if (hipGetLastError() != hipSuccess) return -2;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// fp32 workspace bytes the call with these arguments needs (0 when it does not split)
+long amdk8s_llm_prefill_attn_workspace(int P, int start, int H, int Hkv, int nsplit, int nw) {
+  if (P <= 0 || H <= 0 || Hkv <= 0 || H % Hkv != 0 || start < 0) return -1;
+  const Plan pl = make_plan(P, start, H, Hkv, nsplit, nw);
+  if (pl.nsplit == 1) return 0;
+  return (long)pl.nsplit * P * H * (kD + 2) * 4;
+}
+
+// Plan of the call: out[0] = waves per workgroup, out[1] = key splits, out[2] = tiles per split.
+int amdk8s_llm_prefill_attn_plan(int P, int start, int H, int Hkv, int nsplit, int nw, int* out) {
+  if (P <= 0 || H <= 0 || Hkv <= 0 || H % Hkv != 0 || start < 0) return -1;
+  const Plan pl = make_plan(P, start, H, Hkv, nsplit, nw);
+  out[0] = pl.nw;
+  out[1] = pl.nsplit;
+  out[2] = pl.tps;
+  return 0;
+}
+
+// q: [P] x [H] rows of 128 (strides sq_tok / sq_head elements); kc / vc: one slot's [Hkv][.][128]
+// slabs (stride skv_head), positions 0 .. start+P-1 valid; o: [P] x [H] rows (so_tok / so_head).
+// dtype 0 = fp16, 1 = bf16.  work: >= amdk8s_llm_prefill_attn_workspace(...) bytes.
+int amdk8s_llm_prefill_attn(const void* q, long sq_tok, long sq_head, const void* kc,
+                            const void* vc, long skv_head, void* o, long so_tok, long so_head, int P,
+                            int start, int H, int Hkv, float scale, void* work, long work_bytes,
+                            int nsplit, int nw, int dtype, hipStream_t stream) {
+  if (P <= 0 || H <= 0 || Hkv <= 0 || H % Hkv != 0 || start < 0) return -1;
+  if ((sq_tok | sq_head | so_tok | so_head | skv_head) % 8 != 0) return -3;
+  if ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(kc) |
+       reinterpret_cast<uintptr_t>(vc) | reinterpret_cast<uintptr_t>(o)) % 16 != 0)
+    return -3;
+  if ((long)P * (H / Hkv) > 0x7fffffffL) return -1;
+  const Plan pl = make_plan(P, start, H, Hkv, nsplit, nw);
+  const long need = pl.nsplit == 1 ? 0 : (long)pl.nsplit * P * H * (kD + 2) * 4;
+  if (need > work_bytes || (need > 0 && (reinterpret_cast<uintptr_t>(work) % 16) != 0)) return -4;
+  Args a;
+  a.q = static_cast<const uint16_t*>(q);
+  a.k = static_cast<const uint16_t*>(kc);
+  a.v = static_cast<const uint16_t*>(vc);
+  a.o = static_cast<uint16_t*>(o);
+  a.opart = static_cast<float*>(work);
+  a.ml = a.opart + (long)pl.nsplit * P * H * kD;
+  a.sq_tok = sq_tok;
+  a.sq_head = sq_head;
+  a.so_tok = so_tok;
+  a.so_head = so_head;
+  a.skv_head = skv_head;
+  a.P = P;
+  a.start = start;
+  a.H = H;
+  a.Hkv = Hkv;
+  a.group = H / Hkv;
+  a.nrb = pl.nrb;
+  a.nsplit = pl.nsplit;
+  a.tps = pl.tps;
+  a.c = scale * 1.4426950408889634f;
+  if (dtype == 1)
+    return pl.nw == 8 ? launch<true, 8>(a, pl, stream) : launch<true, 4>(a, pl, stream);
+  return pl.nw == 8 ? launch<false, 8>(a, pl, stream) : launch<false, 4>(a, pl, stream);
+}
+
+}  // extern "C"

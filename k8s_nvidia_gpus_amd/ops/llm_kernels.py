@@ -305,3 +305,65 @@ def swiglu_f16(gu, t) -> None:
     p, f = t.shape
     _check(_lib().amdk8s_llm_swiglu_f16(gu.data_ptr(), p, f, t.data_ptr(), _stream(gu)),
            "amdk8s_llm_swiglu_f16")
+
+
+# ---------------------------------------------------------------------- prompt attention (llm_prefill_attn.hip)
+_ATTN_WORK: dict = {}
+
+
+def _declare_prefill_attn(lib) -> None:
+    if getattr(lib, "_prefill_attn_declared", False):
+        return
+    vp, ci, cl, cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
+    lib.amdk8s_llm_prefill_attn.argtypes = [vp, cl, cl, vp, vp, cl, vp, cl, cl, ci, ci, ci, ci, cf,
+                                            vp, cl, ci, ci, ci, vp]
+    lib.amdk8s_llm_prefill_attn.restype = ci
+    lib.amdk8s_llm_prefill_attn_workspace.argtypes = [ci, ci, ci, ci, ci, ci]
+    lib.amdk8s_llm_prefill_attn_workspace.restype = cl
+    lib.amdk8s_llm_prefill_attn_plan.argtypes = [ci, ci, ci, ci, ci, ci, ctypes.POINTER(ci)]
+    lib.amdk8s_llm_prefill_attn_plan.restype = ci
+    lib._prefill_attn_declared = True
+
+
+def prefill_attn_plan(P: int, start: int, heads: int, kv_heads: int, nsplit: int = 0,
+                      nw: int = 0) -> dict:
+    """The launch plan the kernel picks: waves per workgroup, key splits, key tiles per split."""
+    lib = _lib()
+    _declare_prefill_attn(lib)
+    out = (ctypes.c_int * 3)()
+    _check(lib.amdk8s_llm_prefill_attn_plan(P, start, heads, kv_heads, nsplit, nw, out),
+           "amdk8s_llm_prefill_attn_plan")
+    return {"waves": out[0], "nsplit": out[1], "tiles_per_split": out[2]}
+
+
+def prefill_attn(q, kc, vc, out, start: int, scale: float, nsplit: int = 0, nw: int = 0) -> None:
+    """Causal GQA attention of a prompt chunk against one slot's KV-cache slabs, in place.
+
+    ``q`` / ``out``: [H, P, 128] views (unit inner stride, any head / token strides — the engine's
+    token-major storage); ``kc`` / ``vc``: the slot's [Hkv, max_ctx, 128] slabs, positions
+    0 .. start+P-1 written.  Query p sits at position start + p and sees keys 0 .. start + p.
+    ``nsplit`` / ``nw``: 0 = the kernel's plan (:func:`prefill_attn_plan`)."""
+    H, P, D = q.shape
+    hkv = kc.shape[0]
+    if D != 128 or tuple(out.shape) != (H, P, D) or q.stride(2) != 1 or out.stride(2) != 1:
+        raise ValueError(f"prefill_attn: q {tuple(q.shape)} / out {tuple(out.shape)} must be "
+                         f"[H, P, 128] with a unit inner stride")
+    if kc.shape != vc.shape or kc.shape[2] != 128 or kc.stride(1) != 128 or kc.stride(2) != 1 \
+            or vc.stride() != kc.stride() or kc.shape[1] < start + P or H % hkv:
+        raise ValueError("prefill_attn: kc / vc must be [Hkv, >= start+P, 128] slabs with rows of 128")
+    if q.dtype != kc.dtype or out.dtype != q.dtype or q.dtype not in (torch.float16, torch.bfloat16):
+        raise ValueError("prefill_attn: q, kc, vc, out must share fp16 or bf16")
+    lib = _lib()
+    _declare_prefill_attn(lib)
+    need = int(lib.amdk8s_llm_prefill_attn_workspace(P, start, H, hkv, nsplit, nw))
+    if need < 0:
+        raise ValueError("prefill_attn: bad shape")
+    work = _ATTN_WORK.get(q.device)
+    if need and (work is None or work.numel() * 4 < need):
+        work = torch.empty((need + 3) // 4 + (1 << 20), dtype=torch.float32, device=q.device)
+        _ATTN_WORK[q.device] = work
+    _check(lib.amdk8s_llm_prefill_attn(
+        q.data_ptr(), q.stride(1), q.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0),
+        out.data_ptr(), out.stride(1), out.stride(0), P, int(start), H, hkv, float(scale),
+        _p(work) if need else None, work.numel() * 4 if need else 0, int(nsplit), int(nw),
+        int(q.dtype == torch.bfloat16), _stream(q)), "amdk8s_llm_prefill_attn")

@@ -533,10 +533,10 @@ def test_bad_sampler_fields_are_400_and_a_failing_sampler_ends_only_its_job(clie
     assert r.status_code == 200
     real = S.sample_token
 
-    def flaky(logits, p, history=(), generator=None):
+    def flaky(logits, p, history=(), generator=None, dist_out=None):
         if p.top_k == 7 and len(history) > len(tok.encode("boom")):   # the doomed job, in _step
             raise RuntimeError("sampler exploded")
-        return real(logits, p, history, generator)
+        return real(logits, p, history, generator, dist_out=dist_out)
 
     monkeypatch.setattr(S, "sample_token", flaky)
     ids_a, ids_b = tok.encode("hello"), tok.encode("boom")

@@ -661,8 +661,9 @@ def test_dense_prefill_matches_native_prefill(dev, tiny_gguf):
     assert torch.nn.functional.cosine_similarity(la[None], lb[None]).item() > 0.99
 
 
-@pytest.mark.parametrize("gqa,qtok", [(False, False), (True, False), (True, True)])
-def test_native_prefill_equals_torch_prefill(dev, tiny_gguf, gqa, qtok):
+@pytest.mark.parametrize("gqa,qtok,attn", [(False, False, False), (True, False, False),
+                                            (True, True, False), (True, True, True)])
+def test_native_prefill_equals_torch_prefill(dev, tiny_gguf, gqa, qtok, attn):
     """The fused prefill glue (RMSNorm -> fp16, RoPE + KV write, SwiGLU kernels) against the
     PyTorch formulation of the same dense fp16 forward: logits and the written KV cache agree,
     for a prompt from position 0 and a continuation at position > 0 (q head-major or
@@ -672,6 +673,7 @@ def test_native_prefill_equals_torch_prefill(dev, tiny_gguf, gqa, qtok):
     a, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=True)
     a.prefill_gqa = gqa
     a.prefill_qtok = qtok
+    a.prefill_attn_native = attn           # hand-written prompt attention vs SDPA
     b, _ = load(tiny_gguf, device=dev, max_ctx=512, dense=True)
     b.prefill_native = False
     p = tok.encode("the lazy dog jumps over a helpful assistant " * 3)

@@ -1,0 +1,97 @@
+"""MI355X numerics of the hand-written causal GQA prompt attention (ops/csrc/llm_prefill_attn.hip)
+against an fp32 softmax reference: a chunk of P queries at positions start .. start+P-1 reading the
+K/V of one cache slot in place (VERDICT r5 "Next round" 2)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def LK():
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+    from k8s_nvidia_gpus_amd.ops import kernels, llm_kernels
+
+    kernels.library()            # fail loudly if the HIP library is missing
+    return llm_kernels
+
+
+def _case(H, Hkv, P, start, dtype=torch.float16, seed=0, max_ctx=None):
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(seed)
+    end = start + P
+    max_ctx = max_ctx or (end + 255) // 256 * 256 + 256
+    # token-major q storage [P][H][128], viewed [H][P][128] as the engine does
+    q = torch.randn(P, H, 128, device=dev, generator=g).to(dtype).transpose(0, 1)
+    kc = torch.full((Hkv, max_ctx, 128), float("nan"), device=dev, dtype=dtype)
+    vc = torch.full((Hkv, max_ctx, 128), float("nan"), device=dev, dtype=dtype)
+    kc[:, :end] = torch.randn(Hkv, end, 128, device=dev, generator=g).to(dtype)
+    vc[:, :end] = torch.randn(Hkv, end, 128, device=dev, generator=g).to(dtype)
+    return q, kc, vc
+
+
+def _ref(q, kc, vc, start):
+    H, P, _ = q.shape
+    Hkv = kc.shape[0]
+    end = start + P
+    k = kc[:, :end].float().repeat_interleave(H // Hkv, 0)
+    v = vc[:, :end].float().repeat_interleave(H // Hkv, 0)
+    s = q.float() @ k.transpose(-1, -2) / math.sqrt(128)
+    qi = torch.arange(start, end, device=q.device)[:, None]
+    kj = torch.arange(end, device=q.device)[None, :]
+    s = s.masked_fill(kj > qi, float("-inf"))
+    return torch.softmax(s, -1) @ v
+
+
+@pytest.mark.parametrize("H,Hkv", [(28, 4), (4, 2)])
+@pytest.mark.parametrize("P", [1, 7, 64, 512])
+@pytest.mark.parametrize("start", [0, 1, 511, 3000, 31488])
+def test_prefill_attention_vs_fp32(LK, H, Hkv, P, start):
+    q, kc, vc = _case(H, Hkv, P, start)
+    out = torch.full((P, H, 128), float("nan"), device=q.device, dtype=q.dtype).transpose(0, 1)
+    LK.prefill_attn(q, kc, vc, out, start, 1 / math.sqrt(128))
+    ref = _ref(q, kc, vc, start)
+    assert torch.isfinite(out).all()
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=3e-3)
+
+
+@pytest.mark.parametrize("nsplit,nw", [(1, 4), (1, 8), (3, 4), (7, 8), (64, 4)])
+def test_prefill_attention_forced_plans_agree(LK, nsplit, nw):
+    """Every split count / workgroup size gives the fp32 answer (splits past the last tile of a
+    workgroup are empty and must not leak into the combine)."""
+    H, Hkv, P, start = 28, 4, 200, 1000
+    q, kc, vc = _case(H, Hkv, P, start, seed=1)
+    out = torch.empty(P, H, 128, device=q.device, dtype=q.dtype).transpose(0, 1)
+    LK.prefill_attn(q, kc, vc, out, start, 1 / math.sqrt(128), nsplit=nsplit, nw=nw)
+    torch.testing.assert_close(out.float(), _ref(q, kc, vc, start), rtol=1e-2, atol=3e-3)
+
+
+def test_prefill_attention_bf16(LK):
+    H, Hkv, P, start = 28, 4, 96, 700
+    q, kc, vc = _case(H, Hkv, P, start, dtype=torch.bfloat16, seed=2)
+    out = torch.empty(P, H, 128, device=q.device, dtype=q.dtype).transpose(0, 1)
+    LK.prefill_attn(q, kc, vc, out, start, 1 / math.sqrt(128))
+    torch.testing.assert_close(out.float(), _ref(q, kc, vc, start), rtol=2e-2, atol=1.5e-2)
+
+
+def test_prefill_attention_plan_fills_the_chip(LK):
+    """A 512-query chunk at 31 488 splits its keys (4 KV heads x few row blocks alone would idle
+    most CUs); a prompt from position 0 runs unsplit."""
+    long = LK.prefill_attn_plan(512, 31488, 28, 4)
+    assert long["nsplit"] > 1
+    assert LK.prefill_attn_plan(32000, 0, 28, 4)["nsplit"] == 1
+    assert LK.prefill_attn_plan(512, 0, 28, 4)["nsplit"] == 1
+
+
+def test_prefill_attention_rejects_bad_layouts(LK):
+    q, kc, vc = _case(4, 2, 8, 0)
+    out = torch.empty(4, 8, 128, device=q.device, dtype=q.dtype)
+    with pytest.raises(ValueError):
+        LK.prefill_attn(q, kc, vc, out[:, :4], 0, 0.1)
+    with pytest.raises(ValueError):              # slab shorter than start + P
+        LK.prefill_attn(q, kc[:, :4], vc[:, :4], out, 0, 0.1)
+    with pytest.raises(ValueError):
+        LK.prefill_attn(q.float(), kc, vc, out, 0, 0.1)

@@ -39,7 +39,9 @@ def timed(fn, iters=20):
 
 def main():
     dev = torch.device("cuda")
-    H, Hkv, d, P = 28, 4, 128, 512
+    H, Hkv, d = 28, 4, 128
+    P = int(os.environ.get("PROBE_P", "512"))
+    only = os.environ.get("PROBE_VARIANTS")
     g = torch.Generator(device=dev).manual_seed(0)
     for start in [0, 1536, 3072, 8192, 16384, 31488]:
         end = start + P
@@ -81,14 +83,16 @@ def main():
         variants["split"] = split
         try:
             from k8s_nvidia_gpus_amd.ops import llm_kernels as LK
-            if hasattr(LK, "prefill_attention"):
-                out = torch.empty(P, H, d, device=dev, dtype=torch.float16)
-                qt = q[0].transpose(0, 1).contiguous()           # [P][H][d] token-major
-                variants["hand"] = lambda: LK.prefill_attention(
-                    qt.transpose(0, 1), k[0], v[0], start, 1 / math.sqrt(d), out).transpose(0, 1)[None]
+            out = torch.empty(H, P, d, device=dev, dtype=torch.float16)
+            variants["hand"] = lambda: LK.prefill_attn(q[0], k[0], v[0], out, start,
+                                                       1 / math.sqrt(d)) or out[None]
+            plan = LK.prefill_attn_plan(P, start, H, Hkv)
+            print(json.dumps({"variant": "hand_plan", "start": start, **plan}), flush=True)
         except Exception as e:  # noqa: BLE001
             print(json.dumps({"variant": "hand", "error": repr(e)[:200]}), flush=True)
         for name, fn in variants.items():
+            if only and name not in only.split(","):
+                continue
             try:
                 o = fn()
                 err = (o[:, :4].float() - ref).abs().max().item()
