@@ -794,6 +794,14 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
         except ValueError as e:
             raise HTTPException(400, str(e))
 
+    async def prewarm(body: Dict[str, Any]) -> None:
+        """A constrained request needs the vocabulary's byte trie (~2 s once for a 152k
+        vocabulary): build it in the thread pool, not on the event loop or the GPU thread."""
+        if any(body.get(k) for k in ("grammar", "json_schema", "response_format")):
+            from .grammar import trie_for
+
+            await run_in_threadpool(trie_for, state["tok"])
+
     async def wait(job: Job, request: Request) -> Job:
         try:
             return await _collect(job, request_timeout, request.is_disconnected)
@@ -807,6 +815,7 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
     @app.post("/completion")
     async def completion(body: Dict[str, Any], request: Request):
         s = sched()
+        await prewarm(body)
         job = submit(body, await aencode(body.get("prompt", "")), s.engine.max_ctx)
         if body.get("stream"):
             async def gen():
@@ -839,6 +848,7 @@ def create_app(state: Dict[str, Any], request_timeout: float = 600.0):
 
     async def openai(body, ids, chat: bool, request: Request):
         s = sched()
+        await prewarm(body)
         job = submit(body, ids, 16 if not chat else s.engine.max_ctx,
                      "chat" if chat else "completions")
 
