@@ -382,7 +382,9 @@ extern "C" void amdk8s_gemm_w4a_hybrid_plan(int M, int N, int K, int cus, int* n
   if (tn_a <= 0 || rest <= 0 || rest * 2 > cus) return;   // last wave at least half full: plain
   int s = cus / rest;
   s = s < T / 8 ? s : T / 8;                      // >= 8 K-tiles per slice (the ring's depth)
-  s = s < 16 ? s : 16;
+  // each slice's partial tile is rounded to 16 bits before the fp32 sum: at most 8 of them (the
+  // caller runs the hybrid for fp16 only — 11 mantissa bits — never bf16)
+  s = s < 8 ? s : 8;
   if (s < 2) return;
   *na = tn_a * BN;
   *ks = s;

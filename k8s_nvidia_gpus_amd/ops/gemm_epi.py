@@ -193,8 +193,10 @@ def hybrid_plan(m: int, n: int, k: int, cus: int = 256) -> tuple:
 
 
 def _w4a_hybrid(epi: int, x2, w, b, out) -> bool:
-    """The hybrid for store / bias epilogues; False when its plan is the plain launch."""
-    if not _HYBRID or epi not in (0, 1):
+    """The hybrid for store / bias epilogues; False when its plan is the plain launch.  fp16
+    only: its K slices meet as 16-bit partial tiles (the K-loop's C image in LDS is 16-bit), and
+    8 roundings at bf16's 8 mantissa bits would cost visible accuracy."""
+    if not _HYBRID or epi not in (0, 1) or x2.dtype != torch.float16:
         return False
     m, k = x2.shape
     n = w.shape[0]

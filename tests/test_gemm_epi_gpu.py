@@ -259,21 +259,24 @@ def test_w4a_partial_last_wave_split_over_k(GE, m, n, k, bias, dtype):
     plan engages and the product equals the fp32 reference."""
     dev = torch.device("cuda")
     na, ks = GE.hybrid_plan(m, n, k, GE._cus(dev))
-    assert 0 < na < n and ks >= 2, (na, ks)
+    assert 0 < na < n and 2 <= ks <= 8, (na, ks)
     g = torch.Generator(device=dev).manual_seed(m + n)
     x = torch.randn(m, k, generator=g, device=dev).to(dtype)
     w = (torch.randn(n, k, generator=g, device=dev) / k ** 0.5).to(dtype)
     b = torch.randn(n, generator=g, device=dev).to(dtype) if bias else None
     y = GE.linear(x, w, b)
     ref = _ref(x, w, b)
-    tol = 2e-2 if dtype == torch.bfloat16 else 5e-3
+    tol = 1e-2 if dtype == torch.bfloat16 else 5e-3
     torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
-    # the split columns agree with the plain kernel's to 16-bit rounding
     prev = GE._HYBRID
     GE._HYBRID = False
     try:
         plain = GE.linear(x, w, b)
     finally:
         GE._HYBRID = prev
-    torch.testing.assert_close(y[:, na:].float(), plain[:, na:].float(), rtol=tol, atol=tol)
+    if dtype == torch.bfloat16:                 # bf16 never takes the hybrid (ADVICE r5)
+        assert torch.equal(y, plain)
+        return
+    # the split columns agree with the plain kernel's to fp16 rounding
+    torch.testing.assert_close(y[:, na:].float(), plain[:, na:].float(), rtol=3e-3, atol=3e-3)
     assert torch.equal(y[:, :na], plain[:, :na])            # whole waves: the same kernel
