@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -331,24 +333,34 @@ struct Plan {
 };
 
 Plan make_plan(int P, int start, int H, int Hkv, int nsplit_req, int nw_req) {
+  // Measured on MI355X (tools/debug/prefill_attn_sweep.py, profiles/r06/prefill_attn_sweep.log):
+  // * a prompt from position 0, or enough 4-wave row blocks to fill the chip: 4 waves, no split
+  //   (512 @ 0: 17.6 us vs 22.5 with 8 waves; 8192 @ 0: 681 vs 725; any split only adds work);
+  // * a chunk with many rows after a long prefix: 8 waves (each K/V tile feeds 256 rows) and the
+  //   keys split until the grid is ONE round of 8-wave workgroups (<= 256; 512 @ 31488: 4 splits
+  //   268 us, 5 splits 353, 8 splits 288; 512 @ 3072: 4 splits 51.1 us);
+  // * few rows (a short chunk, a single token) after a long prefix: 4 waves, splits up to 256
+  //   workgroups (64 @ 8192: 12-16 splits 36.8-37.3 us vs 8 waves 43-49).
   Plan pl;
   const int group = H / Hkv;
   const long rows = (long)P * group;
-  // 8-wave workgroups when there are enough rows to fill the chip with them, else 4
-  pl.nw = (nw_req == 4 || nw_req == 8) ? nw_req : ((rows + 255) / 256 * Hkv >= 512 ? 8 : 4);
-  pl.nrb = (int)((rows + pl.nw * 32 - 1) / (pl.nw * 32));
   const int ntiles = (start + P + kKeys - 1) / kKeys;
-  const long base = (long)pl.nrb * Hkv;
-  int ns;
-  if (nsplit_req > 0) {
-    ns = nsplit_req;
-  } else {
-    // split the keys until ~2 workgroups per CU are busy, keeping >= 16 tiles per split
-    ns = (int)((512 + base - 1) / base);
-    ns = min(ns, max(1, ntiles / 16));
-    ns = min(ns, 32);
+  const long base4 = (rows + 127) / 128 * Hkv, base8 = (rows + 255) / 256 * Hkv;
+  int nw = 4, ns = 1;
+  if (start > 0 && base4 < 256) {
+    const int ns8 = (int)std::min<long>(256 / base8, ntiles / 12);
+    if (rows >= 1024 && ns8 >= 2) {
+      nw = 8;
+      ns = ns8;
+    } else {
+      ns = (int)std::max<long>(1, std::min<long>(256 / base4, ntiles / 8));
+    }
   }
-  ns = max(1, min(ns, ntiles));
+  if (nw_req == 4 || nw_req == 8) nw = nw_req;
+  if (nsplit_req > 0) ns = nsplit_req;
+  pl.nw = nw;
+  pl.nrb = (int)((rows + nw * 32 - 1) / (nw * 32));
+  ns = std::max(1, std::min(ns, ntiles));
   pl.tps = (ntiles + ns - 1) / ns;
   pl.nsplit = (ntiles + pl.tps - 1) / pl.tps;
   return pl;

@@ -37,10 +37,13 @@ def main() -> int:
     ap.add_argument("--m", type=int, default=512)
     ap.add_argument("--quick", action="store_true", help="planner / w4a / torch only (no sweep)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--only", default="", help="comma-separated GEMM names (qkv,o,gate_up,down)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     rows = []
     for name, n, k, kind in SHAPES:
+        if a.only and name not in a.only.split(","):
+            continue
         m = a.m
         x = torch.randn(m, k, device=dev, dtype=torch.float16)
         w = torch.randn(n, k, device=dev, dtype=torch.float16) / k ** 0.5
@@ -68,7 +71,7 @@ def main() -> int:
         wide = GE._WIDE
         GE._WIDE = "epi"
         for tile in range(len(GE.TILES)):
-            for sp in (1, 2, 4):
+            for sp in (1, 2, 3, 4, 6, 8):
                 GE.set_tile(tile)
                 GE.set_splits(sp)
                 try:
