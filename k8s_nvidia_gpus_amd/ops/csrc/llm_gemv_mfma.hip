@@ -40,6 +40,11 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 #define AMDK8S_SPLIT_SK 1
 #endif
 constexpr int kSplitKW = AMDK8S_SPLIT_KW, kSplitSK = AMDK8S_SPLIT_SK;
+// Wave partials are summed in groups of this many waves (then the group sums in order): the
+// unsplit 8-wave ffn_down of 1-4 tokens and its 2-slice x 4-wave form for 5-8 tokens (one pass
+// over the weights; their activations do not fit one workgroup's LDS) then add the same numbers
+// in the same order — decode stays batch-invariant.
+constexpr int kRedGroup = 4;
 
 // The MFMA kernel reads an MFMA-packed copy of the planes (amdk8s_llm_mfma_pack), laid out per
 // (16-row group G, super-block b) so that each of a wave's loads per block reads whole contiguous
@@ -238,7 +243,11 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
   const int tile = bid / SKr, slice = bid - tile * SKr;
   const int kb_lo = slice * nb / SKr, nbw = (slice + 1) * nb / SKr - kb_lo;
   const int Kl = nbw << 8;                                       // the staged window's K
-  const int kb0 = kb_lo + kw * nbw / KW, n = kb_lo + (kw + 1) * nbw / KW - kb0;   // host: >= 1
+  // this wave's super-blocks: part gw of the row cut into SKr x KW parts (inside this slice's
+  // window), so an unsplit KW-wave launch and a split one of the same SKr x KW give every wave
+  // the same blocks
+  const int gw = slice * KW + kw, tw = SKr * KW;
+  const int kb0 = gw * nb / tw, n = (gw + 1) * nb / tw - kb0;    // host: >= 1
   const int r = lane & 15, g = lane >> 4;
   const int wrow0 = tile * RG * 16;
   const long rb0 = (long)(min(wrow0 + rg * 16, a.N - 16) >> 4) * nb + kb0;   // host: N % 16 == 0
@@ -350,13 +359,23 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
     }
     __syncthreads();
     if (kw == 0) {
+      // in groups of kRedGroup waves, then the group sums in order: an 8-wave launch adds
+      // (w0+..+w3) + (w4+..+w7), exactly what a 2-slice x 4-wave split-K launch of the same row
+      // computes (each slice one group, the combine adds the slices in order)
+      constexpr int GRP = KW < kRedGroup ? KW : kRedGroup;
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
         v[q] = 0.f; v1[q] = 0.f;
 #pragma unroll
-        for (int k = 0; k < KW; ++k) {
-          v[q] += kred[(((rg * KW + k) * NQ + q) * P) * 64 + lane];
-          if constexpr (P == 2) v1[q] += kred[(((rg * KW + k) * NQ + q) * P + 1) * 64 + lane];
+        for (int k0 = 0; k0 < KW; k0 += GRP) {
+          float gs = 0.f, gs1 = 0.f;
+#pragma unroll
+          for (int k = k0; k < k0 + GRP; ++k) {
+            gs += kred[(((rg * KW + k) * NQ + q) * P) * 64 + lane];
+            if constexpr (P == 2) gs1 += kred[(((rg * KW + k) * NQ + q) * P + 1) * 64 + lane];
+          }
+          v[q] += gs;
+          if constexpr (P == 2) v1[q] += gs1;
         }
       }
     }
@@ -543,9 +562,19 @@ void mfma_shape(bool pair, int N, int K, int& kw, int& rg) {
 // of 8 waves left 32 of the 256 CUs idle and every wave a 9-block dependent chain; slices of the
 // super-blocks on separate workgroups fill the chip.  A function of the matrix only (and of the
 // input form, which is fixed per matrix in the engine), like the shape.
-void mfma_ksplit_shape(int N, int K, int& kw, int& rg, int& sk) {
+void mfma_ksplit_shape(int N, int K, int T, int& kw, int& rg, int& sk) {
   (void)N;
-  if (K >= 8192) kw = kSplitKW, rg = 1, sk = kSplitSK;
+  if (K < 8192) return;
+  kw = kSplitKW, rg = 1, sk = kSplitSK;
+  // 5-8 tokens: 8 tokens' activations of the whole row do not fit the LDS, so instead of two
+  // launches (tokens 0-3, 4-7: the weights streamed twice) each row tile runs as 2 slices of 4
+  // waves — the same 8 parts of the row as the 8-wave launch, one pass over the weights
+  // (AMDK8S_DOWN_ONEPASS=0: the two-launch form, for A/B runs)
+  static const int onepass = [] {
+    const char* e = getenv("AMDK8S_DOWN_ONEPASS");
+    return !(e && e[0] == '0');
+  }();
+  if (T > 4 && onepass && kSplitKW == 8 && kSplitSK == 1) kw = 4, sk = 2;
 }
 
 template <int TYPE, int T, int MODE>
@@ -702,7 +731,7 @@ int amdk8s_llm_qgemv_mfma(int type, int mode, const void* w0q, const void* w0qh,
     int sk = ksplit;
     if (ksplit < 0) {
       sk = 1;
-      if (kw <= 0) mfma_ksplit_shape(N, K, kw, rg, sk);
+      if (kw <= 0) mfma_ksplit_shape(N, K, T, kw, rg, sk);
     }
     if (sk > 1) {
       if (kw <= 0) mfma_shape(false, N, K, kw, rg);

@@ -727,6 +727,32 @@ def test_random_7b_layer_shapes_run(dev):
     assert cos > 0.98, cos
 
 
+def test_7b_shapes_eight_token_step_equals_single_steps(dev):
+    """at 5-8 tokens ffn_down (K = 18944) runs as ONE pass over its weights
+    (2 slices x 4 waves per row tile, the same 8 parts of the row and the same grouped sum as the
+    8-wave launch of 1-4 tokens): an 8-sequence step gives every sequence the bits of its own
+    single-sequence step, at the real 7B shapes."""
+    from dataclasses import replace
+
+    from k8s_nvidia_gpus_amd.models.llm import QWEN25_7B
+    from k8s_nvidia_gpus_amd.models.llm.engine import Engine
+    from k8s_nvidia_gpus_amd.models.llm.weights import ModelWeights
+
+    cfg = replace(QWEN25_7B, layers=2)
+    eng = Engine(ModelWeights.random(cfg, device=dev, seed=5), max_ctx=512, slots=8, dense=True)
+    if eng.max_T < 8:
+        pytest.skip("8-token steps need the MFMA GEMV")
+    prompts = [[1 + s, 2, 3 + s] for s in range(8)]
+    for s, p in enumerate(prompts):
+        eng.prefill(p, slot=s)
+    toks = [7 + s for s in range(8)]
+    batch = eng.decode(toks, [3] * 8, list(range(8))).clone()
+    assert torch.isfinite(batch).all()
+    for s in (0, 3, 7):
+        single = eng.decode([toks[s]], [3], [s])[0]
+        assert torch.equal(batch[s], single), s
+
+
 def test_server_on_gpu_concurrent_answers_equal_sequential(dev, tiny_gguf):
     """The llama-server-compatible API on the GPU engine: 10 concurrent greedy requests share
     decode steps (continuous batching over 8 slots, prompts in 8-token chunks between the decode
