@@ -40,6 +40,8 @@
 //   * XCD-aware bijective block remap + GROUP_M tile order (neighbouring tiles share A / B panels in
 //     one XCD's L2).
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -537,6 +539,15 @@ void amdk8s_gemm_epi_plan(int M, int N, int K, int* tile_out, int* splits_out) {
     tile = g_tile;
     const long nwg = tile_grid(tile, M, N);
     splits = nwg >= 224 ? 1 : max_splits((int)((224 + nwg - 1) / nwg));
+  } else if (M <= 1024 && N >= 2048 && N <= 8192 && K >= 2048 && K <= 4096) {
+    // narrow projections at prompt-chunk M (the LLM prefill's q|k|v N = 4608 and o_proj N = 3584
+    // at M = 128 .. 1024): 128x64 tiles, split over K up to ~384 workgroups.  Swept per M
+    // (tools/llm_prefill_gemm_probe.py, profiles/r06/prefill_gemm_narrow_*.log): q|k|v 21.4 / 26.4
+    // / 34.5 / 76.9 -> 17.8 / 22.0 / 31.7 / 62.5 us and o_proj 18.4 / 22.6 / 30.2 / 43.0 -> 16.3 /
+    // 20.0 / 27.3 / 39.5 us at M = 128 / 256 / 512 / 1024 against the plan below
+    tile = 2;
+    const long nwg = tile_grid(2, M, N);
+    splits = nwg >= 256 ? 1 : max_splits((int)std::min<long>(8, (384 + nwg - 1) / nwg));
   } else {
     bool done = false;
     // a 4- or 8-wave tile whose grid nearly fills the chip runs unsplit: the split's finalize

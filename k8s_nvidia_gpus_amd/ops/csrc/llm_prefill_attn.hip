@@ -353,7 +353,7 @@ Plan make_plan(int P, int start, int H, int Hkv, int nsplit_req, int nw_req) {
       nw = 8;
       ns = ns8;
     } else {
-      ns = (int)std::max<long>(1, std::min<long>(256 / base4, ntiles / 8));
+      ns = (int)std::max<long>(1, std::min<long>(std::min<long>(256 / base4, ntiles / 8), 32));
     }
   }
   if (nw_req == 4 || nw_req == 8) nw = nw_req;

@@ -36,6 +36,9 @@ def _model(m, n, k):
     """The planner's rules, restated: 8-/4-wave tile with >= 160 WGs unsplit; else the largest tile
     that reaches 192 WGs with >= 8 K-tiles per split (<= 16 splits); else 64x64, max splits."""
     kt = k // 64
+    if m <= 1024 and 2048 <= n <= 8192 and 2048 <= k <= 4096:   # narrow prefill projections
+        g = _grid(2, m, n)
+        return GE.TILES[2], 1 if g >= 256 else max(1, min(-(-384 // g), 8, kt // 8, 16))
     for t in (0, 1):
         if _grid(t, m, n) >= 160:
             return GE.TILES[t], 1
@@ -53,6 +56,9 @@ def _model(m, n, k):
     ((8192, 320, 2880), ((128, 128), 1)),     # SD 64^2 conv (implicit GEMM), 192 tiles unsplit
     ((2048, 640, 5760), ((256, 128), 5)),     # SD 32^2 conv: 80 big tiles x 5 splits
     ((512, 3584, 18944), ((256, 128), 4)),    # LLM prefill FFN down, 512-token chunk
+    ((512, 4608, 3584), ((128, 64), 1)),      # LLM prefill q|k|v, 512-token chunk (r06 sweep)
+    ((512, 3584, 3584), ((128, 64), 2)),      # LLM prefill o_proj
+    ((128, 4608, 3584), ((128, 64), 6)),      # q|k|v of a 128-token chunk
 ])
 def test_plan_measured_shapes(ge, shape, expect):
     assert ge.plan(*shape) == expect
