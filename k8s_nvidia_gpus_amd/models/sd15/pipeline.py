@@ -173,6 +173,8 @@ class StableDiffusion:
     @torch.no_grad()
     def encode_prompt(self, prompts: Sequence[str], negative: Sequence[str]) -> torch.Tensor:
         ids = torch.tensor(self.tokenizer(list(negative) + list(prompts)), device=self.device)
+        if self.device.type == "cuda" and self.dtype in (torch.float16, torch.bfloat16):
+            return self.text_encoder.native(ids, use_graph=self.runner.use_graphs)
         return self.text_encoder(ids)
 
     def _noise(self, n: int, h: int, w: int, generator) -> torch.Tensor:

@@ -104,6 +104,7 @@ struct Args {
   int H, Lq, Lk, nqb;
   long sqb, sqr, skb, skr, svb, svr, sob, sor;  // batch / row strides in elements
   float c;                                       // scale * log2(e)
+  int causal;                                    // 1: query i sees keys 0 .. i (top-left aligned)
 };
 
 template <bool BF16, int NW, int D>
@@ -188,7 +189,9 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_m32_kernel(const Args a) {
   const int vsub = 8 * (p & 1);
   const int vrow = 4 * h + qq;
 
-  const int ntiles = (a.Lk + kKeys - 1) / kKeys;
+  // causal: no key past the workgroup's last query row (workgroup-uniform)
+  const int klim = a.causal ? min(a.Lk, qblk * (NW * 32) + NW * 32) : a.Lk;
+  const int ntiles = (klim + kKeys - 1) / kKeys;
   const float thr = 8.f / a.c;                   // deferred-max margin in raw score units
   load_tile(0);
   if constexpr (G::PAD) {      // pad columns of both buffers read as zeros for the whole kernel
@@ -216,13 +219,16 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_m32_kernel(const Args a) {
         s[b] = mfma32<BF16>(kf, qf[st], s[b]);
       }
     }
-    // keys past Lk (zero rows in the image) score -inf
-    if (kbase + kKeys > a.Lk) {
+    // keys past Lk (zero rows in the image) score -inf; causal: so do keys past the query
+    if (kbase + kKeys > a.Lk || (a.causal && kbase + kKeys - 1 > q0)) {
+      const int qi = a.causal ? q0 + r : 0x7fffffff;
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if (kbase + 32 * b + 8 * (i >> 2) + 4 * h + (i & 3) >= a.Lk) s[b][i] = -INFINITY;
+        for (int i = 0; i < 16; ++i) {
+          const int key = kbase + 32 * b + 8 * (i >> 2) + 4 * h + (i & 3);
+          if (key >= a.Lk || key > qi) s[b][i] = -INFINITY;
+        }
     }
 
     // ---- online softmax with a deferred max (rescale only when a score passes m + 8/c)
@@ -337,10 +343,31 @@ int amdk8s_attention_m32_supported(int d) {
 
 // Same contract as amdk8s_attention_fwd (sd_attention.hip): element strides, 16-byte aligned rows,
 // output row stride `sor`, batch stride Lq*sor; dtype 0 = fp16, 1 = bf16.
+static int m32_fwd(const void* q, const void* k, const void* v, void* o, int N, int H, int Lq,
+                   int Lk, int d, int sqb, int sqr, int skb, int skr, int svb, int svr, int sor,
+                   float scale, int dtype, int causal, hipStream_t stream);
+
 int amdk8s_attention_m32_fwd(const void* q, const void* k, const void* v, void* o, int N, int H,
                              int Lq, int Lk, int d, int sqb, int sqr, int skb, int skr, int svb,
                              int svr, int sor, float scale, int dtype, hipStream_t stream) {
+  return m32_fwd(q, k, v, o, N, H, Lq, Lk, d, sqb, sqr, skb, skr, svb, svr, sor, scale, dtype, 0,
+                 stream);
+}
+
+// Causal self-attention (query i attends to keys 0 .. i; Lq == Lk): the CLIP text encoder of SD1.5
+// (77 tokens, d = 64), same contract as amdk8s_attention_m32_fwd otherwise.
+int amdk8s_attention_causal_fwd(const void* q, const void* k, const void* v, void* o, int N, int H,
+                                int L, int d, int sqb, int sqr, int skb, int skr, int svb, int svr,
+                                int sor, float scale, int dtype, hipStream_t stream) {
+  return m32_fwd(q, k, v, o, N, H, L, L, d, sqb, sqr, skb, skr, svb, svr, sor, scale, dtype, 1,
+                 stream);
+}
+
+static int m32_fwd(const void* q, const void* k, const void* v, void* o, int N, int H, int Lq,
+                   int Lk, int d, int sqb, int sqr, int skb, int skr, int svb, int svr, int sor,
+                   float scale, int dtype, int causal, hipStream_t stream) {
   if (N <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || !amdk8s_attention_m32_supported(d)) return -1;
+  if (causal && Lq != Lk) return -1;
   if ((sqr | skr | svr | sqb | skb | svb | sor) % 8 != 0) return -3;
   if ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o)) % 16 != 0)
@@ -363,6 +390,7 @@ int amdk8s_attention_m32_fwd(const void* q, const void* k, const void* v, void* 
   a.sob = (long)Lq * sor;
   a.sor = sor;
   a.c = scale * 1.4426950408889634f;
+  a.causal = causal;
   // 8 waves (256 query rows) per workgroup: at the Wan shapes it beats 4 waves even where it
   // leaves CUs idle (2x12 heads x 2560 tokens = 240 workgroups: 88 vs 99 us; 32 760 tokens:
   // 12.4 vs 13.6 ms — profiles/r03/attn_probe_v1.log); 4 waves only for very short sequences

@@ -219,3 +219,30 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
         float(scale), _DTYPE[q.dtype], _stream(q))
     _check(rc, "amdk8s_attention_fwd")
     return o
+
+
+def attention_causal(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
+                     scale: float) -> torch.Tensor:
+    """Causal self-attention (query i sees keys 0 .. i) per head on the 32x32x16 flash kernel
+    (``csrc/attn_d128.hip``, head dims 40 / 64 / 80 / 128 / 160); q/k/v ``[N, L, H*d]`` with unit
+    inner stride (any row / batch stride), fp16 or bf16.  The CLIP text encoder's attention."""
+    n, L, c = q.shape
+    d = c // heads
+    lib = _lib()
+    if not getattr(lib, "_causal_declared", False):
+        ci, vp = ctypes.c_int, ctypes.c_void_p
+        lib.amdk8s_attention_causal_fwd.argtypes = [vp, vp, vp, vp] + [ci] * 11 + \
+            [ctypes.c_float, ci, vp]
+        lib.amdk8s_attention_causal_fwd.restype = ci
+        lib._causal_declared = True
+    if q.dtype not in _DTYPE or k.shape != q.shape or v.shape != q.shape or c % heads:
+        raise ValueError(f"attention_causal: q/k/v {tuple(q.shape)} {q.dtype}")
+    if q.stride(-1) != 1 or k.stride(-1) != 1 or v.stride(-1) != 1:
+        raise ValueError("attention_causal: unit inner stride required")
+    o = torch.empty((n, L, c), dtype=q.dtype, device=q.device)
+    rc = lib.amdk8s_attention_causal_fwd(
+        q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), n, heads, L, d,
+        q.stride(0), q.stride(1), k.stride(0), k.stride(1), v.stride(0), v.stride(1), o.stride(1),
+        float(scale), _DTYPE[q.dtype], _stream(q))
+    _check(rc, "amdk8s_attention_causal_fwd")
+    return o
