@@ -347,6 +347,6 @@ def test_clip_text_encoder_native_matches_torch(dev):
     assert torch.isfinite(eager).all()
     torch.testing.assert_close(eager, ref, rtol=3e-2, atol=3e-2)
     assert torch.equal(graphed, eager)
-    assert torch.equal(again, eager[:2])
+    torch.testing.assert_close(again, eager[:2], rtol=1e-2, atol=1e-2)   # other M: other GEMM plan
     cos = torch.nn.functional.cosine_similarity(eager.flatten(), ref.flatten(), dim=0)
     assert cos > 0.9999
