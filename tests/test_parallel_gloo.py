@@ -294,6 +294,9 @@ def test_bench_timed_window_order():
         assert len(calls) == before
     summ = s.summary()
     assert summ["gfxclk_mhz_mean"] == 2100 and 1 <= summ["samples"] < len(s.rows)
+    assert summ["coverage"] in ("window", "tail-only") and summ["window_ms"] >= 20
+    assert summ["coverage"] == ("window" if summ["samples"] >= 3 else "tail-only")
+    assert summ["pre_window"]["samples"] >= 1 and summ["pre_window"]["gfxclk_mhz_mean"] == 2100
     assert calls[-1] == "shutdown"
 
 
