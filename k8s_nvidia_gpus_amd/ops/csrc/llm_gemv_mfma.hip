@@ -566,15 +566,19 @@ void mfma_ksplit_shape(int N, int K, int T, int& kw, int& rg, int& sk) {
   (void)N;
   if (K < 8192) return;
   kw = kSplitKW, rg = 1, sk = kSplitSK;
-  // 5-8 tokens: 8 tokens' activations of the whole row do not fit the LDS, so instead of two
-  // launches (tokens 0-3, 4-7: the weights streamed twice) each row tile runs as 2 slices of 4
-  // waves — the same 8 parts of the row as the 8-wave launch, one pass over the weights
-  // (AMDK8S_DOWN_ONEPASS=0: the two-launch form, for A/B runs)
-  static const int onepass = [] {
+  // 5-8 tokens: their activations of the whole row do not fit one workgroup's LDS, so the
+  // default is two launches (tokens 0-3 and 4..T-1: the weights streamed twice).  The one-pass
+  // form runs each row tile as 2 slices of 4 waves (the same 8 parts of the row as the 8-wave
+  // launch, so the bits are the same), but its 8-token window takes 135 KB of LDS: one 4-wave
+  // workgroup per CU, 448 of them in 1.75 rounds.  Measured per step (profiles/r06/
+  // llm_bench_down_{onepass,twopass}_T5-8.log): T = 5 2.640 vs 2.700 ms, T = 6 2.882 vs 2.787,
+  // T = 7 3.001 vs 2.842, T = 8 3.036 vs 2.881 — one pass for T = 5 only.
+  // AMDK8S_DOWN_ONEPASS=<max T> moves the crossover (0: never) for A/B runs.
+  static const int onepass_max = [] {
     const char* e = getenv("AMDK8S_DOWN_ONEPASS");
-    return !(e && e[0] == '0');
+    return e ? atoi(e) : 5;
   }();
-  if (T > 4 && onepass && kSplitKW == 8 && kSplitSK == 1) kw = 4, sk = 2;
+  if (T > 4 && T <= onepass_max && kSplitKW == 8 && kSplitSK == 1) kw = 4, sk = 2;
 }
 
 template <int TYPE, int T, int MODE>

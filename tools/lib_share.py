@@ -12,6 +12,12 @@ a ``rocprofv3 --kernel-trace --stats`` run (its ``*kernel_stats.csv``) as
 and print each class's share of the GPU time, with its largest kernels.
 
     python tools/lib_share.py gpurun_out/prof/<host>/<pid>_kernel_stats.csv [--top 5]
+    python tools/lib_share.py run_kernel_trace.csv --window-ms 223   # the last 223 ms only
+
+A ``*kernel_trace.csv`` (one row per dispatch) can be cut to a window at the end of the run:
+MIOpen's ``find`` benchmarks every candidate solver (naive ones included) on the first call of a
+convolution shape, so whole-run stats over-count library time; the steady-state request is the
+last ``--window-ms`` of GPU time (``--skip-ms``: leave out that much at the very end).
 """
 from __future__ import annotations
 
@@ -53,7 +59,8 @@ def classify(name: str, mine: set) -> str:
         return "hipBLASLt"
     if re.search(r"\battn_fwd\b|triton", name, re.I):
         return "AOTriton"
-    if re.search(r"miopen|MIOpen|naive_conv|igemm|ck::|ck_tile|Im2Col|batchnorm|gridwise", name):
+    if re.search(r"miopen|MIOpen|naive_conv|igemm|ck::|ck_tile|ck\d+tensor_operation|Im2Col|"
+                 r"batchnorm|gridwise|SubTensorOp", name):
         return "MIOpen"
     if "at::" in name or "c10::" in name or name.startswith("void at"):
         return "torch"
@@ -64,20 +71,36 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
     ap.add_argument("--top", type=int, default=5)
+    ap.add_argument("--window-ms", type=float, default=0.0,
+                    help="kernel-trace input: only dispatches in the last this many ms")
+    ap.add_argument("--skip-ms", type=float, default=0.0,
+                    help="kernel-trace input: end the window this many ms before the last dispatch")
     a = ap.parse_args(argv)
     mine = ours()
     by = defaultdict(float)
     calls = defaultdict(int)
     top = defaultdict(list)
     with open(a.csv) as f:
-        for row in csv.DictReader(f):
-            name = row.get("Name") or row.get("KernelName") or ""
-            ns = float(row.get("TotalDurationNs") or row.get("TotalDuration") or 0)
-            c = int(float(row.get("Calls") or 0))
-            k = classify(name, mine)
-            by[k] += ns
-            calls[k] += c
-            top[k].append((ns, c, name))
+        rows = list(csv.DictReader(f))
+    if rows and "Start_Timestamp" in rows[0]:            # per-dispatch trace: aggregate here
+        ends = [int(r["End_Timestamp"]) for r in rows]
+        hi = max(ends) - a.skip_ms * 1e6
+        lo = hi - a.window_ms * 1e6 if a.window_ms > 0 else -1
+        agg = defaultdict(lambda: [0.0, 0])
+        for r in rows:
+            st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            if st >= lo and en <= hi:
+                agg[r["Kernel_Name"]][0] += en - st
+                agg[r["Kernel_Name"]][1] += 1
+        rows = [{"Name": n, "TotalDurationNs": v[0], "Calls": v[1]} for n, v in agg.items()]
+    for row in rows:
+        name = row.get("Name") or row.get("KernelName") or ""
+        ns = float(row.get("TotalDurationNs") or row.get("TotalDuration") or 0)
+        c = int(float(row.get("Calls") or 0))
+        k = classify(name, mine)
+        by[k] += ns
+        calls[k] += c
+        top[k].append((ns, c, name))
     total = sum(by.values()) or 1.0
     print(f"# {a.csv}: {total / 1e6:.3f} ms of kernel time")
     for k, ns in sorted(by.items(), key=lambda kv: -kv[1]):
