@@ -77,6 +77,7 @@ struct QMat {            // one quantised weight matrix [N, K], repacked at load
                          //   sc[2c] | sc[2c+1] << 8 | m[2c] << 16 | m[2c+1] << 24;
                          // Q6_K: scales [N][nb][16] ordered so lane `sub` reads bytes 2sub, 2sub+1
   const uint16_t* d;     // Q4_K: [N][nb] dwords (d | dmin << 16);  Q6_K: [N][nb] f16
+  int temporal = 0;      // MFMA GEMV: default-policy weight loads (a second launch re-reads them)
 };
 
 // Q6_K: stored scale position of GGUF scale index i (pairs (i, i+4) adjacent per lane).

@@ -55,21 +55,32 @@ template <int TYPE> struct MBlk;
 template <> struct MBlk<kQ4K> { uint4 q0, q1, sc; uint32_t dd; };
 template <> struct MBlk<kQ6K> { uint4 q0, q1, h0, h1, sc; uint32_t dd; };
 
-template <int TYPE>
+// POL 0: non-temporal loads (a weight read once per step); 1: default policy, so the bytes stay
+// in the Infinity Cache for a second launch that reads the same weights right after (the 5-8
+// token ffn_down's second token quad)
+template <int POL>
+__device__ __forceinline__ uint4 wld(const void* p) {
+  if constexpr (POL == 0) return ldnt(p);
+  else return *reinterpret_cast<const uint4*>(p);
+}
+
+template <int TYPE, int POL = 0>
 __device__ __forceinline__ void mload(const QMat& w, long gb, int lane, MBlk<TYPE>& r) {
   const int row = lane & 15, g = lane >> 4;
   const uint8_t* q = w.q + gb * 2048 + row * 64 + g * 16;
-  r.q0 = ldnt(q);
-  r.q1 = ldnt(q + 1024);
+  r.q0 = wld<POL>(q);
+  r.q1 = wld<POL>(q + 1024);
   if constexpr (TYPE == kQ6K) {
     const uint8_t* h = w.qh + gb * 1024 + row * 32 + (g & 1) * 16;
-    r.h0 = ldnt(h);
-    r.h1 = ldnt(h + 512);
-    r.sc = ldnt(reinterpret_cast<const uint8_t*>(w.sc) + gb * 256 + row * 16);
+    r.h0 = wld<POL>(h);
+    r.h1 = wld<POL>(h + 512);
+    r.sc = wld<POL>(reinterpret_cast<const uint8_t*>(w.sc) + gb * 256 + row * 16);
   } else {
-    r.sc = ldnt(reinterpret_cast<const uint32_t*>(w.sc) + gb * 64 + row * 4);
+    r.sc = wld<POL>(reinterpret_cast<const uint32_t*>(w.sc) + gb * 64 + row * 4);
   }
-  r.dd = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(w.d) + gb * 16 + row);
+  const uint32_t* dp = reinterpret_cast<const uint32_t*>(w.d) + gb * 16 + row;
+  if constexpr (POL == 0) r.dd = __builtin_nontemporal_load(dp);
+  else r.dd = *dp;
 }
 
 __device__ __forceinline__ i32x4 nib_lo(const uint4& v) {
@@ -229,7 +240,7 @@ __device__ __forceinline__ XView stage_x8_window(const GemvArgs& a, uint8_t* lds
 
 // gate|up (pair, <= 4 tokens): 592 4-wave workgroups need 3 waves per SIMD to be co-resident
 // bid = the workgroup's index within this matrix's grid
-template <int TYPE, int T, int MODE, int KW, int RG, int D>
+template <int TYPE, int T, int MODE, int KW, int RG, int D, int POL = 0>
 __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid) {
   extern __shared__ __align__(16) uint8_t lds[];
   constexpr int P = MODE == kPair ? 2 : 1;
@@ -256,8 +267,8 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
 #pragma unroll
   for (int d = 0; d < D - 1; ++d) {
     const long rb = rb0 + min(d, n - 1);
-    mload<TYPE>(a.w0, rb, lane, w0[d]);
-    if constexpr (P == 2) mload<TYPE>(a.w1, rb, lane, w1[d]);
+    mload<TYPE, POL>(a.w0, rb, lane, w0[d]);
+    if constexpr (P == 2) mload<TYPE, POL>(a.w1, rb, lane, w1[d]);
   }
   const XView xv = SKr > 1 ? stage_x8_window<T>(a, lds, kb_lo, nbw) : stage_x<T>(a, lds);
   const MfmaLds L = mfma_lds(TYPE, T, Kl, KW * RG, P);
@@ -334,8 +345,8 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
     for (int d = 0; d < D; ++d) {
       const int ps = (d + D - 1) % D;
       const long nxt = rb0 + min(i0 + d + D - 1, n - 1);
-      mload<TYPE>(a.w0, nxt, lane, w0[ps]);
-      if constexpr (P == 2) mload<TYPE>(a.w1, nxt, lane, w1[ps]);
+      mload<TYPE, POL>(a.w0, nxt, lane, w0[ps]);
+      if constexpr (P == 2) mload<TYPE, POL>(a.w1, nxt, lane, w1[ps]);
       // keep the refill ahead of this step's maths and the steps in ring order: the scheduler
       // otherwise sinks the refills, and the next step's wait then drains them too
       __builtin_amdgcn_sched_barrier(0);
@@ -462,13 +473,13 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
 #endif
 constexpr int kPairD = AMDK8S_PAIR_D;
 
-template <int TYPE, int T, int MODE, int KW, int RG, int D>
+template <int TYPE, int T, int MODE, int KW, int RG, int D, int POL = 0>
 __global__ void __launch_bounds__(KW * RG * 64)
 __attribute__((amdgpu_waves_per_eu(
     MODE == kPair ? (T <= 4 && TYPE == kQ4K ? AMDK8S_PAIR_WPE : AMDK8S_PAIR_WPE8)
                   : (T > 4 && TYPE == kQ4K ? AMDK8S_NP_WPE8 : 1), 8)))
 qgemv_mfma_kernel(GemvArgs a) {
-  qgemv_mfma_body<TYPE, T, MODE, KW, RG, D>(a, blockIdx.x);
+  qgemv_mfma_body<TYPE, T, MODE, KW, RG, D, POL>(a, blockIdx.x);
 }
 
 // Two store-mode matrices of (possibly) different types over the same input in ONE launch (q|k
@@ -535,6 +546,13 @@ int launch_mfma_one(const GemvArgs& a, hipStream_t st) {
   const MfmaLds L = mfma_lds(TYPE, T, nbw << 8, KW * RG, MODE == kPair ? 2 : 1);
   if (L.total > 160 * 1024) return 4;
   const int tiles = (a.N + 16 * RG - 1) / (16 * RG);
+  if constexpr (MODE == kResid && KW == 8 && T <= 4) {
+    if (a.w0.temporal) {          // the two-launch 5-8 token ffn_down (dispatch_mfma_split)
+      hipLaunchKernelGGL((qgemv_mfma_kernel<TYPE, T, MODE, KW, RG, D, 1>), dim3(tiles * sk),
+                         dim3(KW * RG * 64), L.total, st, a);
+      return hipGetLastError() == hipSuccess ? 0 : 1;
+    }
+  }
   hipLaunchKernelGGL((qgemv_mfma_kernel<TYPE, T, MODE, KW, RG, D>), dim3(tiles * sk),
                      dim3(KW * RG * 64), L.total, st, a);
   return hipGetLastError() == hipSuccess ? 0 : 1;
@@ -631,6 +649,13 @@ int dispatch_mfma_split(const GemvArgs& a, int kw, int rg, hipStream_t st) {
   GemvArgs lo = a, hi = a;
   lo.T = 4;
   hi.T = a.T - 4;
+  // the second launch re-reads the first one's weights: default-policy loads in both keep them
+  // in the 256 MB Infinity Cache in between (AMDK8S_SPLIT_TEMPORAL=0: non-temporal, A/B runs)
+  static const bool temporal = [] {
+    const char* e = getenv("AMDK8S_SPLIT_TEMPORAL");
+    return !(e && e[0] == '0');
+  }();
+  lo.w0.temporal = hi.w0.temporal = temporal ? 1 : 0;
   const long K = a.K;
   if (hi.x8) { hi.x8 += 4 * K; hi.dx += 4 * (K >> 5); hi.sx += 4 * (K >> 4); }
   if (hi.xf) hi.xf += 4L * a.ldx;
