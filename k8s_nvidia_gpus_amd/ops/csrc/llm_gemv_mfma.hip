@@ -649,11 +649,13 @@ int dispatch_mfma_split(const GemvArgs& a, int kw, int rg, hipStream_t st) {
   GemvArgs lo = a, hi = a;
   lo.T = 4;
   hi.T = a.T - 4;
-  // the second launch re-reads the first one's weights: default-policy loads in both keep them
-  // in the 256 MB Infinity Cache in between (AMDK8S_SPLIT_TEMPORAL=0: non-temporal, A/B runs)
+  // The second launch re-reads the first one's weights.  Default-policy loads in both (to keep
+  // them in the 256 MB Infinity Cache in between) measured SLOWER than non-temporal ones: T = 6
+  // 2.856 vs 2.771 ms, T = 8 2.963 vs 2.879 (profiles/r06/llm_bench_down_temporal.log); kept as
+  // an A/B knob, AMDK8S_SPLIT_TEMPORAL=1.
   static const bool temporal = [] {
     const char* e = getenv("AMDK8S_SPLIT_TEMPORAL");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   lo.w0.temporal = hi.w0.temporal = temporal ? 1 : 0;
   const long K = a.K;

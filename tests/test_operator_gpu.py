@@ -145,6 +145,36 @@ def test_bench_py_rccl_path_under_torchrun_one_rank():
     assert tel is None or "error" in tel or tel["samples"] >= 1
 
 
+def test_bench_py_self_launched_torchrun_matches_plain_run():
+    """``bench.py --gpus 1 --launcher torchrun`` (the self-launch path a plain
+    ``--gpus N`` takes) measures the same GEMM as the plain single-process run, within 2 %, and
+    reports the rank's own PCI BDF and the process group's world size."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parent.parent
+    common = ["--gpus", "1", "--steps", "100", "--warmup", "10", "--no-fp8", "--no-allreduce",
+              "--no-telemetry"]
+    env = dict(os.environ, PYTHONPATH=str(repo))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TORCHELASTIC_RUN_ID"):
+        env.pop(k, None)
+    docs = []
+    for extra in ([], ["--launcher", "torchrun"]):
+        p = subprocess.run([sys.executable, "bench.py"] + common + extra, capture_output=True,
+                           text=True, cwd=str(repo), timeout=300, env=env)
+        assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1, p.stdout
+        docs.append(json.loads(lines[0]))
+    plain, launched = docs
+    assert plain["launcher"] == "single process" and launched["launcher"].startswith("torchrun")
+    assert launched["process_group_world_size"] == 1 and launched["n_gpus"] == 1
+    assert plain["ranks"][0]["bdf"] and plain["ranks"][0]["bdf"] == launched["ranks"][0]["bdf"]
+    assert launched["value"] == pytest.approx(plain["value"], rel=0.02), (plain["value"],
+                                                                          launched["value"])
+
+
 @pytest.mark.parametrize("gated", [True, False])
 def test_node_bringup_rehearsal_on_real_hardware(tmp_path, native, gated):
     """Node-local time-to-first-GPU-pod: real kfd-probe, runtime shim + CDI, device plugin over gRPC
