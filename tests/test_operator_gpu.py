@@ -160,19 +160,23 @@ def test_bench_py_self_launched_torchrun_matches_plain_run():
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TORCHELASTIC_RUN_ID"):
         env.pop(k, None)
     docs = []
-    for extra in ([], ["--launcher", "torchrun"]):
+    # plain, self-launched, plain: the launched run is compared with the plain runs on both sides
+    # of it, so a drift of the chip's sustained clock between back-to-back runs is not read as a
+    # launcher cost
+    for extra in ([], ["--launcher", "torchrun"], []):
         p = subprocess.run([sys.executable, "bench.py"] + common + extra, capture_output=True,
                            text=True, cwd=str(repo), timeout=300, env=env)
         assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
         lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
         assert len(lines) == 1, p.stdout
         docs.append(json.loads(lines[0]))
-    plain, launched = docs
+    plain, launched, plain2 = docs
     assert plain["launcher"] == "single process" and launched["launcher"].startswith("torchrun")
     assert launched["process_group_world_size"] == 1 and launched["n_gpus"] == 1
     assert plain["ranks"][0]["bdf"] and plain["ranks"][0]["bdf"] == launched["ranks"][0]["bdf"]
-    assert launched["value"] == pytest.approx(plain["value"], rel=0.02), (plain["value"],
-                                                                          launched["value"])
+    lo = min(plain["value"], plain2["value"]) * 0.98
+    hi = max(plain["value"], plain2["value"]) * 1.02
+    assert lo <= launched["value"] <= hi, (plain["value"], launched["value"], plain2["value"])
 
 
 @pytest.mark.parametrize("gated", [True, False])
