@@ -233,10 +233,15 @@ def settle(step, sync, settle_ms: float, chunk: int = 8, max_launches: int = 400
     return n
 
 
-def timed_window(step, sync, barrier, steps: int, warmup: int, settle_ms: float, sampler=None):
-    """settle → warmup → [sync, barrier, sync] → t0 → K steps → [sync, barrier, sync] → t1.
+def timed_window(step, sync, barrier, steps: int, warmup: int, settle_ms: float, sampler=None,
+                 stats=None):
+    """settle → warmup → [sync, barrier, sync] → t0 → K steps → sync → t1 → [barrier, sync].
 
-    Returns ``(elapsed_s, settle_launches)``.  The sampler (already constructed: ``amdsmi_init``
+    Returns ``(elapsed_s, settle_launches)``: this rank's t1 − t0, the caller takes the MAX over
+    ranks.  The closing barrier aligns the ranks but is not inside the elapsed time: a 1-rank RCCL
+    barrier cost a self-launched ``--gpus 1`` run 3.8 % of a 100-step window (1626.8 vs 1691.1 /
+    1692.4 TFLOPS plain, r06), which at the driver's 20 steps would understate every N > 1 point;
+    ``stats["end_barrier_ms"]`` records what it took.  The sampler (already constructed: ``amdsmi_init``
     and the handle scan are the slow part) starts its thread *before* the settle phase; inside the
     bracket it is only told the clock (``mark_start``/``mark_end``) and is held quiet while the K
     steps are launched (``hold`` … ``mark_launched``: no GIL contention with the launches).
@@ -264,11 +269,14 @@ def timed_window(step, sync, barrier, steps: int, warmup: int, settle_ms: float,
         if sampler is not None:
             sampler.mark_launched()     # sample while the enqueued steps run, not between launches
         sync()
-        barrier()
-        sync()
-        elapsed = time.perf_counter() - t0
+        t1 = time.perf_counter()
         if sampler is not None:
             sampler.mark_end()
+        barrier()
+        sync()
+        if stats is not None:
+            stats["end_barrier_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
+        elapsed = t1 - t0
     finally:
         if sampler is not None:
             sampler.__exit__(None, None, None)
@@ -385,8 +393,9 @@ def main(argv=None) -> int:
     sampler = (telemetry.timed(period=0.005,
                                device_index=device.index if device.index is not None else 0)
                if not smoke and not args.no_telemetry else None)
+    wstats: dict = {}
     elapsed, settle_launches = timed_window(step, sync, barrier, args.steps, args.warmup,
-                                            0.0 if smoke else args.settle_ms, sampler)
+                                            0.0 if smoke else args.settle_ms, sampler, wstats)
     tel = sampler.summary() if sampler is not None else None
 
     flop_per_gpu = 2.0 * s * s * s * args.steps
@@ -480,6 +489,7 @@ def main(argv=None) -> int:
             "tflops_per_gpu": round(value / world, 2),
             "tflops_per_rank": per_rank,
             "settle": {"ms": 0.0 if smoke else args.settle_ms, "launches": settle_launches},
+            "end_barrier_ms": wstats.get("end_barrier_ms"),
             "time_to_first_gpu_result_s": round(ttfr, 3) if ttfr is not None else None,
             "time_to_first_gpu_result_native_s": _NATIVE_TTFR,
             "numerics_max_rel_err": max_rel_err,

@@ -251,6 +251,10 @@ def test_bench_timed_window_order():
     assert set(log[last_warm + 1:i_start + 1]) <= {"sync", "barrier", "hold", "mark_start"}
     assert log[last_warm + 1] == "hold"             # quiet before the GPU drains the warmup
     assert log[i_start + 1] == "step" and log[-1] == "exit"
+    # the window closes at this rank's own sync: the aligning barrier comes after mark_end
+    i_end = log.index("mark_end")
+    assert log[i_end - 1] == "sync" and "barrier" not in log[i_start:i_end]
+    assert "barrier" in log[i_end:]
     # held quiet while the K steps are launched, sampling again while they execute
     i_launched = log.index("mark_launched")
     assert log.index("hold") < i_start and log[i_start:i_launched].count("step") == 20 and "sync" not in log[i_start:i_launched]
