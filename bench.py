@@ -341,7 +341,14 @@ def main(argv=None) -> int:
     from k8s_nvidia_gpus_amd.parallel.collectives import init_distributed, sweep
 
     if distributed:
-        device = init_distributed("gloo" if smoke else "nccl")
+        pg = "gloo" if smoke else os.environ.get("AMDK8S_BENCH_PG", "nccl")
+        if pg == "gloo" and not smoke:       # A/B probe: timing barriers on the CPU, GPU compute
+            local = int(os.environ.get("LOCAL_RANK", "0"))
+            torch.cuda.set_device(local)
+            init_distributed("gloo")
+            device = torch.device("cuda", local)
+        else:
+            device = init_distributed(pg)
     elif smoke:
         device = torch.device("cpu")
     else:
