@@ -13,7 +13,9 @@ Launch contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for
 (N > 1, no WORLD_SIZE) starts that torchrun itself as a child process after counting GPU agents in
 the KFD sysfs topology (fewer than N → exit 2), so it can never report a 1-GPU number for N; under
 torchrun, WORLD_SIZE != --gpus is an error, and the JSON carries every rank's PCI BDF (checked
-distinct) and the process group's own world size.  W untimed steps, then exactly K
+distinct) and the process group's own world size.  The ranks synchronise the timed windows over a
+host (gloo) group and create the RCCL group after them, for the all-reduce sweep: an initialised
+RCCL communicator slowed the GEMM 3-5 % (see main()).  W untimed steps, then exactly K
 timed steps bracketed by barrier + synchronize on both sides; the MAX elapsed over ranks is used;
 rank 0 prints ONE JSON line.  Before the W warmup steps each rank runs the GEMM back-to-back for
 ``--settle-ms`` (default 250 ms, untimed) so that the timed window measures sustained throughput
@@ -340,15 +342,25 @@ def main(argv=None) -> int:
         return 2
     from k8s_nvidia_gpus_amd.parallel.collectives import init_distributed, sweep
 
+    # Process groups (N > 1, or torchrun with one rank): the default group is gloo, on the host —
+    # the timing barriers and the gathering of per-rank results; the RCCL group (xGMI) is created
+    # after the timed windows, for the all-reduce bus-bandwidth sweep.  An initialised RCCL
+    # communicator cost the GEMM itself 3-5 % (one rank under torchrun: 1588 / 1615 / 1618 TFLOPS
+    # with the RCCL group vs 1663 with gloo and 1672 plain, profiles/r06/bench_pg_probe.log), which
+    # would read as a scaling loss at every N > 1.  AMDK8S_BENCH_PG=nccl: RCCL from the start
+    # (barriers included), for A/B runs.
+    rccl_first = os.environ.get("AMDK8S_BENCH_PG", "gloo") == "nccl"
+    rccl = None
     if distributed:
-        pg = "gloo" if smoke else os.environ.get("AMDK8S_BENCH_PG", "nccl")
-        if pg == "gloo" and not smoke:       # A/B probe: timing barriers on the CPU, GPU compute
+        if smoke:
+            device = init_distributed("gloo")
+        else:
             local = int(os.environ.get("LOCAL_RANK", "0"))
             torch.cuda.set_device(local)
             init_distributed("gloo")
             device = torch.device("cuda", local)
-        else:
-            device = init_distributed(pg)
+            if rccl_first:
+                rccl = dist.new_group(backend="nccl", device_id=device)
     elif smoke:
         device = torch.device("cpu")
     else:
@@ -394,7 +406,7 @@ def main(argv=None) -> int:
 
     def barrier():
         if distributed:
-            dist.barrier()
+            dist.barrier(group=rccl)            # gloo (host) unless AMDK8S_BENCH_PG=nccl
 
     # amd-smi init + handle scan happen here, before the settle phase (see timed_window)
     sampler = (telemetry.timed(period=0.005,
@@ -408,11 +420,11 @@ def main(argv=None) -> int:
     flop_per_gpu = 2.0 * s * s * s * args.steps
     per_rank = [round(flop_per_gpu / elapsed / 1e12, 2)]
     if distributed:
-        t = torch.tensor([elapsed, ttfr or 0.0], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed, ttfr or 0.0], dtype=torch.float64)      # host tensors: gloo
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0].item())
         ttfr = float(t[1].item()) if ttfr is not None else None
-        mine = torch.tensor([per_rank[0]], device=device, dtype=torch.float64)
+        mine = torch.tensor([per_rank[0]], dtype=torch.float64)
         gathered = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(gathered, mine)
         per_rank = [round(float(x.item()), 2) for x in gathered]
@@ -442,7 +454,7 @@ def main(argv=None) -> int:
 
         e8, _ = timed_window(step8, sync, barrier, args.steps, args.warmup, args.settle_ms)
         if distributed:
-            t = torch.tensor([e8], device=device, dtype=torch.float64)
+            t = torch.tensor([e8], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             e8 = float(t[0].item())
         fp8_tflops = flop_per_gpu * world / e8 / 1e12
@@ -451,9 +463,11 @@ def main(argv=None) -> int:
     busbw = None
     ar_sweep = None
     if distributed and not args.no_allreduce:
+        if rccl is None and not smoke:          # now that the GEMM windows are done
+            rccl = dist.new_group(backend="nccl", device_id=device)
         top = (4 if smoke else args.allreduce_mib) << 20
         rows = sweep("all_reduce", 1 << 20, top, factor=4, iters=3 if smoke else 10,
-                     warmup=1 if smoke else 3, device=device)
+                     warmup=1 if smoke else 3, device=device, group=rccl)
         bad = sum(r.wrong for r in rows)
         if bad:
             raise RuntimeError(f"all-reduce returned {bad} wrong elements")
@@ -490,6 +504,9 @@ def main(argv=None) -> int:
             "world_size": world,
             "process_group_world_size": pg_world,
             "process_group_backend": (dist.get_backend() if distributed else None),
+            "allreduce_backend": (dist.get_backend(rccl) if rccl is not None else
+                                  ("gloo" if distributed and smoke and not args.no_allreduce
+                                   else None)),
             "launcher": os.environ.get("AMDK8S_BENCH_LAUNCHER",
                                        "torchrun" if distributed else "single process"),
             "ranks": ranks,

@@ -91,38 +91,39 @@ def _sync(device: torch.device) -> None:
         torch.cuda.synchronize(device)
 
 
-def _max_over_ranks(x: float, device: torch.device) -> float:
+def _max_over_ranks(x: float, device: torch.device, group=None) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
 
 
-def _check_and_prepare(op: str, nbytes: int, dtype: torch.dtype, device, rank: int, world: int):
+def _check_and_prepare(op: str, nbytes: int, dtype: torch.dtype, device, rank: int, world: int,
+                       group=None):
     """Build input/output buffers, run the op once, count wrong elements exactly."""
     esize = torch.tensor([], dtype=dtype).element_size()
     count = max(world, nbytes // esize)
     count -= count % world  # scatter-type ops need divisibility
     if op == "all_reduce":
         x = torch.full((count,), float(rank + 1), dtype=dtype, device=device)
-        dist.all_reduce(x)
+        dist.all_reduce(x, group=group)
         expect = world * (world + 1) / 2
         wrong = int((x != expect).sum().item())
-        return (lambda: dist.all_reduce(x)), wrong, count * esize
+        return (lambda: dist.all_reduce(x, group=group)), wrong, count * esize
     if op == "all_gather":
         per = count // world
         x = torch.full((per,), float(rank + 1), dtype=dtype, device=device)
         out = torch.empty((per * world,), dtype=dtype, device=device)
-        dist.all_gather_into_tensor(out, x)
+        dist.all_gather_into_tensor(out, x, group=group)
         expect = torch.arange(1, world + 1, dtype=dtype, device=device).repeat_interleave(per)
         wrong = int((out != expect).sum().item())
-        return (lambda: dist.all_gather_into_tensor(out, x)), wrong, per * world * esize
+        return (lambda: dist.all_gather_into_tensor(out, x, group=group)), wrong, per * world * esize
     if op == "reduce_scatter":
         per = count // world
         x = torch.full((per * world,), float(rank + 1), dtype=dtype, device=device)
         out = torch.empty((per,), dtype=dtype, device=device)
-        dist.reduce_scatter_tensor(out, x)
+        dist.reduce_scatter_tensor(out, x, group=group)
         wrong = int((out != world * (world + 1) / 2).sum().item())
-        return (lambda: dist.reduce_scatter_tensor(out, x)), wrong, per * world * esize
+        return (lambda: dist.reduce_scatter_tensor(out, x, group=group)), wrong, per * world * esize
     if op == "all_to_all":
         per = count // world
         # chunk j of rank r carries the value r*world + j; after the exchange chunk j of rank r
@@ -130,35 +131,38 @@ def _check_and_prepare(op: str, nbytes: int, dtype: torch.dtype, device, rank: i
         x = (torch.arange(world, device=device, dtype=torch.float32) + rank * world).to(dtype)
         x = x.repeat_interleave(per)
         out = torch.empty_like(x)
-        dist.all_to_all_single(out, x)
+        dist.all_to_all_single(out, x, group=group)
         expect = (torch.arange(world, device=device, dtype=torch.float32) * world + rank).to(dtype)
         wrong = int((out != expect.repeat_interleave(per)).sum().item())
-        return (lambda: dist.all_to_all_single(out, x)), wrong, per * world * esize
+        return (lambda: dist.all_to_all_single(out, x, group=group)), wrong, per * world * esize
     if op == "broadcast":
         x = torch.full((count,), float(rank + 1), dtype=dtype, device=device)
-        dist.broadcast(x, src=0)
+        dist.broadcast(x, src=0, group=group)
         wrong = int((x != 1).sum().item())
-        return (lambda: dist.broadcast(x, src=0)), wrong, count * esize
+        return (lambda: dist.broadcast(x, src=0, group=group)), wrong, count * esize
     raise ValueError(f"unknown collective {op!r}")
 
 
 def measure(op: str, nbytes: int, dtype: torch.dtype = torch.float32, iters: int = 20,
-            warmup: int = 5, device: Optional[torch.device] = None) -> CollectiveResult:
-    rank, world = dist.get_rank(), dist.get_world_size()
+            warmup: int = 5, device: Optional[torch.device] = None, group=None) -> CollectiveResult:
+    """One collective's time (MAX over ranks) and correctness; ``group``: the process group to
+    run it on (default: the default group)."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
     device = device or (torch.device("cuda", torch.cuda.current_device())
-                        if torch.cuda.is_available() and dist.get_backend() == "nccl" else torch.device("cpu"))
-    fn, wrong, size = _check_and_prepare(op, nbytes, dtype, device, rank, world)
-    wrong = int(_max_over_ranks(float(wrong), device))
+                        if torch.cuda.is_available() and dist.get_backend(group) == "nccl"
+                        else torch.device("cpu"))
+    fn, wrong, size = _check_and_prepare(op, nbytes, dtype, device, rank, world, group)
+    wrong = int(_max_over_ranks(float(wrong), device, group))
     for _ in range(warmup):
         fn()
     _sync(device)
-    dist.barrier()
+    dist.barrier(group=group)
     t0 = time.perf_counter()
     for _ in range(iters):
         fn()
     _sync(device)
     dt = (time.perf_counter() - t0) / iters
-    dt = _max_over_ranks(dt, device)
+    dt = _max_over_ranks(dt, device, group)
     algbw = size / dt / 1e9
     return CollectiveResult(op, size, str(dtype).replace("torch.", ""), world, dt * 1e6, algbw,
                             algbw * BUSBW_FACTOR[op](world) if world > 1 else algbw, wrong)
