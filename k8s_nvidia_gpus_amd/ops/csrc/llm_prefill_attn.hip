@@ -97,7 +97,7 @@ __global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) 
   const int r = lane & 31, h = lane >> 5;
 
   // XCD-major block -> work item (consecutive work items share an XCD and so its L2); work order:
-  // row block fastest (zigzag, below), then KV head, then split
+  // row block fastest (heaviest first, below), then KV head, then split
   int work;
   {
     const int nwg = gridDim.x, bid = blockIdx.x;
@@ -109,11 +109,11 @@ __global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) 
   const int rest = work / a.nrb;
   const int g = rest % a.Hkv;
   const int split = rest / a.Hkv;
-  // zigzag over the row blocks (heaviest, lightest, 2nd heaviest, 2nd lightest, ...): a causal row
-  // block's work grows with its position, and each XCD takes a contiguous run of work items, so
-  // plain heaviest-first order gave one XCD a head's heavy half and the next XCD its light half
-  // (the chip waited on the heavy ones); any run of this order holds heavy + light pairs
-  const int rb = (rbi & 1) ? (rbi >> 1) : a.nrb - 1 - (rbi >> 1);
+  // heaviest first (a causal row block's work grows with its position).  Measured and rejected:
+  // a zigzag order (heaviest, lightest, 2nd heaviest, ...) meant to give every XCD's run of work
+  // items the same mix — 8192 @ 0 681 -> 730 us, 2048 @ 0 62.7 -> 69.9 us
+  // (profiles/r06/prefill_attn_sweep_zigzag.log)
+  const int rb = a.nrb - 1 - rbi;
 
   const int rows = a.P * a.group;            // query rows of this KV head
   const long rowsH = (long)a.P * a.H;        // query rows of the whole chunk (partials' index)
