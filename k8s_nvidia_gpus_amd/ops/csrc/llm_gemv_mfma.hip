@@ -199,6 +199,19 @@ __host__ __device__ inline MfmaLds mfma_lds(int type, int T, int K, int waves, i
   return L;
 }
 
+// SX layout: [waves][2 slots][T x (288 + 32 + na x 16) + 256 zero bytes] activation rings, then
+// as mfma_lds from the (unused) zero bytes on (aux unused)
+__host__ __device__ inline MfmaLds mfma_lds_sx(int T, int na, int waves, int P) {
+  MfmaLds L;
+  L.aux = 0;
+  L.zero = waves * 2 * (T * (320 + na * 16) + 256);
+  L.kred = L.zero + 256;
+  L.q8s = L.kred + waves * ((T + 3) / 4) * P * 64 * 4;
+  L.flag = L.q8s + T * 32 * 4;
+  L.total = L.flag + 16;
+  return L;
+}
+
 // Q8 activations of super-blocks [kb_lo, kb_lo + nbw) staged as stage_x stages a whole row, with
 // local block indices (the window of one split-K workgroup): 16-byte units, four per thread per
 // round, every load of a round issued before its LDS stores.  Ends with a barrier.
@@ -240,7 +253,12 @@ __device__ __forceinline__ XView stage_x8_window(const GemvArgs& a, uint8_t* lds
 
 // gate|up (pair, <= 4 tokens): 592 4-wave workgroups need 3 waves per SIMD to be co-resident
 // bid = the workgroup's index within this matrix's grid
-template <int TYPE, int T, int MODE, int KW, int RG, int D, int POL = 0>
+// SX 1 (5-8 tokens, Q8 input, unsplit): no whole-row staging — each wave streams its own
+// super-blocks' activations (x, dx and the per-type sums of every token) through a private
+// two-slot LDS ring, one block ahead of its maths: ffn_down's 8 x 18944 activations do not fit
+// the LDS at once, and this keeps the 8-wave shape (and so the T <= 4 bits) in one pass over the
+// weights
+template <int TYPE, int T, int MODE, int KW, int RG, int D, int POL = 0, int SX = 0>
 __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid) {
   extern __shared__ __align__(16) uint8_t lds[];
   constexpr int P = MODE == kPair ? 2 : 1;
@@ -270,25 +288,103 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
     mload<TYPE, POL>(a.w0, rb, lane, w0[d]);
     if constexpr (P == 2) mload<TYPE, POL>(a.w1, rb, lane, w1[d]);
   }
-  const XView xv = SKr > 1 ? stage_x8_window<T>(a, lds, kb_lo, nbw) : stage_x<T>(a, lds);
-  const MfmaLds L = mfma_lds(TYPE, T, Kl, KW * RG, P);
-  if constexpr (TYPE == kQ4K) {
-    float* sxp = reinterpret_cast<float*>(lds + L.aux);
-    for (int i = threadIdx.x; i < T * (Kl >> 5); i += blockDim.x)
-      sxp[i] = xv.sxs[2 * i] + xv.sxs[2 * i + 1];
+  // SX ring slot: x [T][288] (the staged row's block layout), dx [T][8], sums [T][NA x 4 dwords],
+  // 256 zero bytes (the A operand of this slot's inactive lanes: every fragment read is then one
+  // base register plus constant offsets)
+  constexpr int SXZ = T * (320 + NA * 16), SXS = SXZ + 256;
+  const int sxbase = wave * 2 * SXS;
+  // staging through registers (a direct-to-LDS load in flight would make every use of a weight
+  // load wait for it); buffer loads: one 32-bit offset register per stream instead of a pointer
+  uint4 sr_x0, sr_x1;                // two 16-byte x units per lane and block (80-128 for 5-8 tokens)
+  float4 sr_d, sr_s;
+  const __amdgpu_buffer_rsrc_t rs_x =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(a.x8), (short)0, T * K, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_d =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.dx), (short)0, T * (K >> 3), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_s =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.sx), (short)0, T * (K >> 2), 0x00020000);
+  uint32_t vo_x0 = 0, vo_x1 = 0, vo_d = 0, vo_s = 0;
+  if constexpr (SX) {
+    const int c1 = min(lane + 64, T * 16 - 1), cd = min(lane, 2 * T - 1), cs = min(lane, 4 * T - 1);
+    vo_x0 = (uint32_t)((lane >> 4) * K + (lane & 15) * 16);
+    vo_x1 = (uint32_t)((c1 >> 4) * K + (c1 & 15) * 16);
+    vo_d = (uint32_t)(((cd >> 1) * (K >> 5) + (cd & 1) * 4) * 4);
+    vo_s = (uint32_t)(((cs >> 2) * (K >> 4) + (cs & 3) * 4) * 4);
+  }
+  // one super-block (global index kb) of every token into the staging registers
+  auto sx_load = [&](int kb) {
+    const uint32_t ox = (uint32_t)kb * 256u, od = (uint32_t)kb * 32u;
+    sr_x0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_x, vo_x0 + ox, 0, 0));
+    sr_x1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_x, vo_x1 + ox, 0, 0));
+    sr_d = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs_d, vo_d + od, 0, 0));
+    if constexpr (TYPE == kQ4K)
+      sr_s = __builtin_bit_cast(float4,
+                                __builtin_amdgcn_raw_buffer_load_b128(rs_s, vo_s + 2 * od, 0, 0));
+  };
+  // the staging registers → ring slot s, with the sums the staged path computes (same arithmetic)
+  auto sx_store = [&](int s) {
+    uint8_t* base = lds + sxbase + s * SXS;
+    auto put = [&](int c, const uint4& v) {
+      *reinterpret_cast<uint4*>(base + (c >> 4) * 288 + (c & 15) * 16) = v;
+      if constexpr (TYPE == kQ6K) {
+        int sum = dot4z(v.x, 0x01010101u);
+        sum = dot4(v.y, 0x01010101u, sum);
+        sum = dot4(v.z, 0x01010101u, sum);
+        reinterpret_cast<int*>(base + T * 320)[c] = dot4(v.w, 0x01010101u, sum);
+      }
+    };
+    put(lane, sr_x0);
+    if (lane + 64 < T * 16) put(lane + 64, sr_x1);
+    if (lane < 2 * T) *reinterpret_cast<float4*>(base + T * 288 + lane * 16) = sr_d;
+    if constexpr (TYPE == kQ4K) {
+      if (lane < 4 * T)
+        *reinterpret_cast<float2*>(base + T * 320 + lane * 8) =
+            make_float2(sr_s.x + sr_s.y, sr_s.z + sr_s.w);
+    }
+  };
+  // step i: block i + 1 (loaded one step ago) into its slot, then block i + 2's loads — issued
+  // before the step's weight refill, so waiting for them never waits for that refill
+  auto sx_step = [&](int i) {
+    if constexpr (SX) {
+      sx_store((i + 1) & 1);
+      sx_load(kb0 + min(i + 2, n - 1));
+    }
+  };
+  XView xv{};
+  MfmaLds L;
+  if constexpr (SX) {
+    static_assert(T > 4, "the activation ring stages 80-128 x units per block");
+    L = mfma_lds_sx(T, NA, KW * RG, P);
+    if (lane < 32) {                     // both slots' zero bytes (this wave only reads them)
+      uint4* z = reinterpret_cast<uint4*>(lds + sxbase + (lane >> 4) * SXS + SXZ);
+      z[lane & 15] = make_uint4(0, 0, 0, 0);
+    }
+    sx_load(kb0);
+    sx_store(0);
+    sx_load(kb0 + min(1, n - 1));
   } else {
-    int* X = reinterpret_cast<int*>(lds + L.aux);
-    for (int i = threadIdx.x; i < T * (Kl >> 4); i += blockDim.x) {
-      const int t = i / (Kl >> 4), p = (i - t * (Kl >> 4)) << 4;
-      const uint4 v = *reinterpret_cast<const uint4*>(xv.xs + t * xv.xstride + xoff(p));
-      int sum = dot4z(v.x, 0x01010101u);
-      sum = dot4(v.y, 0x01010101u, sum);
-      sum = dot4(v.z, 0x01010101u, sum);
-      X[i] = dot4(v.w, 0x01010101u, sum);
+    xv = SKr > 1 ? stage_x8_window<T>(a, lds, kb_lo, nbw) : stage_x<T>(a, lds);
+    L = mfma_lds(TYPE, T, Kl, KW * RG, P);
+    if constexpr (TYPE == kQ4K) {
+      float* sxp = reinterpret_cast<float*>(lds + L.aux);
+      for (int i = threadIdx.x; i < T * (Kl >> 5); i += blockDim.x)
+        sxp[i] = xv.sxs[2 * i] + xv.sxs[2 * i + 1];
+    } else {
+      int* X = reinterpret_cast<int*>(lds + L.aux);
+      for (int i = threadIdx.x; i < T * (Kl >> 4); i += blockDim.x) {
+        const int t = i / (Kl >> 4), p = (i - t * (Kl >> 4)) << 4;
+        const uint4 v = *reinterpret_cast<const uint4*>(xv.xs + t * xv.xstride + xoff(p));
+        int sum = dot4z(v.x, 0x01010101u);
+        sum = dot4(v.y, 0x01010101u, sum);
+        sum = dot4(v.z, 0x01010101u, sum);
+        X[i] = dot4(v.w, 0x01010101u, sum);
+      }
     }
   }
-  if (threadIdx.x < 16) reinterpret_cast<uint4*>(lds + L.zero)[threadIdx.x] = make_uint4(0, 0, 0, 0);
-  __syncthreads();
+  if constexpr (!SX) {
+    if (threadIdx.x < 16) reinterpret_cast<uint4*>(lds + L.zero)[threadIdx.x] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+  }
   // A operand of quad q: lane l is row (t, s) = (4q + ((l & 15) >> 2), l & 3) of K-group g; live
   // only for s == g.  MFMA m's 16 activations: Q4_K +0 / +32 / +128 / +160 from
   // 64 (g >> 1) + 16 (g & 1); Q6_K +0 / +64 / +128 / +192 from 16 g (zero lanes: the zero bytes)
@@ -300,20 +396,35 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
   for (int q = 0; q < NQ; ++q) {
     const int at = 4 * q + ((lane & 15) >> 2);
     const bool live = (lane & 3) == g && at < T;
-    xa0[q] = live ? at * xv.xstride + xb : L.zero;
-    xstep[q] = live ? 288 : 0;
-    xo1[q] = live ? (TYPE == kQ6K ? 64 : 32) : 0;
-    xo2[q] = live ? 128 : 0;
-    xo3[q] = live ? (TYPE == kQ6K ? 192 : 160) : 0;
+    if constexpr (SX) {                 // dead lanes: the slot's zero bytes, same offsets
+      xa0[q] = sxbase + (live ? at * 288 + xb : SXZ);
+      xstep[q] = SXS;
+      xo1[q] = TYPE == kQ6K ? 64 : 32;
+      xo2[q] = 128;
+      xo3[q] = TYPE == kQ6K ? 192 : 160;
+    } else {
+      xa0[q] = live ? at * xv.xstride + xb : L.zero;
+      xstep[q] = live ? 288 : 0;
+      xo1[q] = live ? (TYPE == kQ6K ? 64 : 32) : 0;
+      xo2[q] = live ? 128 : 0;
+      xo3[q] = live ? (TYPE == kQ6K ? 192 : 160) : 0;
+    }
     const int tt = min(4 * q + g, T - 1);            // this lane's output token in quad q
-    dxb[q] = xv.dxs + tt * (Kl >> 5);
-    axb[q] = reinterpret_cast<const uint4*>(lds + L.aux) + tt * nbw * NA;
+    if constexpr (SX) {
+      dxb[q] = reinterpret_cast<const float*>(lds + sxbase + T * 288) + tt * 8;
+      axb[q] = reinterpret_cast<const uint4*>(lds + sxbase + T * 320) + tt * NA;
+    } else {
+      dxb[q] = xv.dxs + tt * (Kl >> 5);
+      axb[q] = reinterpret_cast<const uint4*>(lds + L.aux) + tt * nbw * NA;
+    }
   }
+  // per-block strides: the staged row's next block, or the ring's other slot
+  constexpr int DSTEP = SX ? SXS / 4 : 8, ASTEP = SX ? SXS / 16 : NA;
   float acc[NQ], acc1[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) acc[q] = acc1[q] = 0.f;
   auto compute = [&](const MBlk<TYPE>& q0, const MBlk<TYPE>& q1, int i) {
-    const int kb = kb0 - kb_lo + i;                   // window-local block index (LDS)
+    const int kb = SX ? (i & 1) : kb0 - kb_lo + i;    // window-local block index / ring slot
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const uint8_t* xp = lds + xa0[q] + kb * xstep[q];
@@ -323,15 +434,17 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
       xa[2] = *reinterpret_cast<const i32x4*>(xp + xo2[q]);
       xa[3] = *reinterpret_cast<const i32x4*>(xp + xo3[q]);
       float dxv[8];
-      const float4 d0 = *reinterpret_cast<const float4*>(dxb[q] + kb * 8);
-      const float4 d1 = *reinterpret_cast<const float4*>(dxb[q] + kb * 8 + 4);
+      const float4 d0 = *reinterpret_cast<const float4*>(dxb[q] + kb * DSTEP);
+      const float4 d1 = *reinterpret_cast<const float4*>(dxb[q] + kb * DSTEP + 4);
       dxv[0] = d0.x; dxv[1] = d0.y; dxv[2] = d0.z; dxv[3] = d0.w;
       dxv[4] = d1.x; dxv[5] = d1.y; dxv[6] = d1.z; dxv[7] = d1.w;
       uint4 aux[4];
 #pragma unroll
-      for (int u = 0; u < NA; ++u) aux[u] = axb[q][kb * NA + u];
+      for (int u = 0; u < NA; ++u) aux[u] = axb[q][kb * ASTEP + u];
       acc[q] = mfma_block<TYPE>(q0, xa, dxv, aux, g, acc[q]);
       if constexpr (P == 2) acc1[q] = mfma_block<TYPE>(q1, xa, dxv, aux, g, acc1[q]);
+      // SX: one quad's fragments live at a time (both at once spill at 2 waves/SIMD)
+      if constexpr (SX) __builtin_amdgcn_sched_barrier(0);
     }
   };
   // Whole groups of D steps: every step first refills the slot consumed one step ago with block
@@ -345,6 +458,7 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
     for (int d = 0; d < D; ++d) {
       const int ps = (d + D - 1) % D;
       const long nxt = rb0 + min(i0 + d + D - 1, n - 1);
+      sx_step(i0 + d);
       mload<TYPE, POL>(a.w0, nxt, lane, w0[ps]);
       if constexpr (P == 2) mload<TYPE, POL>(a.w1, nxt, lane, w1[ps]);
       // keep the refill ahead of this step's maths and the steps in ring order: the scheduler
@@ -356,7 +470,10 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
   }
 #pragma unroll
   for (int d = 0; d < D - 1; ++d)
-    if (i0 + d < n) compute(w0[d], w1[d], i0 + d);
+    if (i0 + d < n) {
+      sx_step(i0 + d);
+      compute(w0[d], w1[d], i0 + d);
+    }
   // K-split partials: wave kw = 0 of each row group adds its group's in wave order
   float v[NQ], v1[NQ];
 #pragma unroll
@@ -473,13 +590,13 @@ __device__ __forceinline__ void qgemv_mfma_body(const GemvArgs& a, const int bid
 #endif
 constexpr int kPairD = AMDK8S_PAIR_D;
 
-template <int TYPE, int T, int MODE, int KW, int RG, int D, int POL = 0>
+template <int TYPE, int T, int MODE, int KW, int RG, int D, int POL = 0, int SX = 0>
 __global__ void __launch_bounds__(KW * RG * 64)
 __attribute__((amdgpu_waves_per_eu(
     MODE == kPair ? (T <= 4 && TYPE == kQ4K ? AMDK8S_PAIR_WPE : AMDK8S_PAIR_WPE8)
-                  : (T > 4 && TYPE == kQ4K ? AMDK8S_NP_WPE8 : 1), 8)))
+                  : (SX ? 2 : (T > 4 && TYPE == kQ4K ? AMDK8S_NP_WPE8 : 1)), 8)))
 qgemv_mfma_kernel(GemvArgs a) {
-  qgemv_mfma_body<TYPE, T, MODE, KW, RG, D, POL>(a, blockIdx.x);
+  qgemv_mfma_body<TYPE, T, MODE, KW, RG, D, POL, SX>(a, blockIdx.x);
 }
 
 // Two store-mode matrices of (possibly) different types over the same input in ONE launch (q|k
@@ -558,6 +675,32 @@ int launch_mfma_one(const GemvArgs& a, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+// 5-8 tokens on the 8-wave long-row shape (ffn_down): the activation-ring form (SX), one pass
+// over the weights with the T <= 4 launch's parts and reduction order.  AMDK8S_DOWN_SX=0: the
+// two-launch form instead (A/B runs).
+static bool sx_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("AMDK8S_DOWN_SX");
+    return !e || e[0] != '0';
+  }();
+  return on;
+}
+
+template <int TYPE, int T, int MODE>
+int launch_mfma_sx(const GemvArgs& a, hipStream_t st) {
+  // ring depth: Q6_K 2 (its 3-deep weight ring spills 17-31 VGPRs next to two token quads and the
+  // staging registers at 2 waves/SIMD), Q4_K 3 (230 VGPRs)
+  constexpr int KW = 8, RG = 1, D = TYPE == kQ6K ? 2 : 3, NA = TYPE == kQ6K ? 4 : 2;
+  if ((a.K >> 8) < KW || a.xf || a.ksplit > 1 || !sx_enabled()) return 4;
+  if ((reinterpret_cast<uintptr_t>(a.x8) | reinterpret_cast<uintptr_t>(a.dx) |
+       reinterpret_cast<uintptr_t>(a.sx)) & 15) return 4;       // 16-byte staging loads
+  const MfmaLds L = mfma_lds_sx(T, NA, KW * RG, 1);
+  if (L.total > 160 * 1024) return 4;
+  hipLaunchKernelGGL((qgemv_mfma_kernel<TYPE, T, MODE, KW, RG, D, 0, 1>), dim3(a.N / 16),
+                     dim3(KW * RG * 64), L.total, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 // Default shape: a function of the matrix only (never of T or of the input form), so each matrix
 // sums its K-split partials in one order at every T (batch invariance), and 4 waves wherever the
 // fp32-row prologue may run (stage_x reduces the RMSNorm over 4 waves in rmsnorm_q8's order;
@@ -590,11 +733,14 @@ void mfma_ksplit_shape(int N, int K, int T, int& kw, int& rg, int& sk) {
   // launch, so the bits are the same), but its 8-token window takes 135 KB of LDS: one 4-wave
   // workgroup per CU, 448 of them in 1.75 rounds.  Measured per step (profiles/r06/
   // llm_bench_down_{onepass,twopass}_T5-8.log): T = 5 2.640 vs 2.700 ms, T = 6 2.882 vs 2.787,
-  // T = 7 3.001 vs 2.842, T = 8 3.036 vs 2.881 — one pass for T = 5 only.
-  // AMDK8S_DOWN_ONEPASS=<max T> moves the crossover (0: never) for A/B runs.
+  // T = 7 3.001 vs 2.842, T = 8 3.036 vs 2.881 — one pass for T = 5 only.  Both lost to the
+  // activation-ring form (launch_mfma_sx: the unsplit 8-wave shape, one pass, activations streamed
+  // per wave): T = 5 / 6 / 7 / 8 2.298 / 2.358 / 2.412 / 2.446 ms vs two launches 2.633 / 2.770 /
+  // 2.850 / 2.882 (profiles/r06/llm_bench_down_sx_T1-8.log, _sx_off_T5-8.log), so with it on the
+  // split form is never the default.  AMDK8S_DOWN_ONEPASS=<max T> forces it for A/B runs.
   static const int onepass_max = [] {
     const char* e = getenv("AMDK8S_DOWN_ONEPASS");
-    return e ? atoi(e) : 5;
+    return e ? atoi(e) : (sx_enabled() ? 0 : 5);
   }();
   if (T > 4 && T <= onepass_max && kSplitKW == 8 && kSplitSK == 1) kw = 4, sk = 2;
 }
@@ -618,7 +764,7 @@ int launch_mfma(const GemvArgs& a, int kw, int rg, hipStream_t st) {
       case 4 * 8 + 1: return launch_mfma_one<TYPE, T, MODE, 4, 1>(a, st);
       case 8 * 8 + 1:
         if constexpr (T <= 4) return launch_mfma_one<TYPE, T, MODE, 8, 1>(a, st);
-        else return 4;                              // register budget: tokens in two launches
+        else return launch_mfma_sx<TYPE, T, MODE>(a, st);   // 4: tokens in two launches
       default: return 2;
     }
   }

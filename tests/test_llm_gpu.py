@@ -729,9 +729,9 @@ def test_random_7b_layer_shapes_run(dev):
 
 def test_7b_shapes_eight_token_step_equals_single_steps(dev):
     """at 5-8 tokens ffn_down (K = 18944) runs as ONE pass over its weights
-    (2 slices x 4 waves per row tile, the same 8 parts of the row and the same grouped sum as the
-    8-wave launch of 1-4 tokens): an 8-sequence step gives every sequence the bits of its own
-    single-sequence step, at the real 7B shapes."""
+    (the 8-wave launch of 1-4 tokens, each wave streaming its own super-blocks' activations through
+    an LDS ring: the same 8 parts of the row and the same grouped sum): an 8-sequence step gives
+    every sequence the bits of its own single-sequence step, at the real 7B shapes."""
     from dataclasses import replace
 
     from k8s_nvidia_gpus_amd.models.llm import QWEN25_7B
