@@ -34,6 +34,7 @@ import torch
 import torch.nn.functional as F
 
 from .config import LLMConfig
+from k8s_nvidia_gpus_amd.ops.llm_kernels import gate_up_interleave, gate_up_split
 
 NORM_PROLOGUE_T = 2     # steps of up to this many tokens normalise in the GEMV prologues
 from .weights import ModelWeights, QWeight
@@ -147,6 +148,21 @@ class Engine:
                       "graph_captures": 0}
 
     # ------------------------------------------------------------------ dense weights (prefill / CPU)
+    @property
+    def gu_blk(self) -> int:
+        """Row-block size of the dense gate|up weight's interleave (0: [gate; up] halves)."""
+        return 128 if self.cfg.ffn % 128 == 0 else 0
+
+    def _gate_up(self, mm, xn: torch.Tensor, w: torch.Tensor, t: torch.Tensor) -> None:
+        """t = silu(xn·gateᵀ) · (xn·upᵀ) (fp16, GPU prefill): one GEMM with the SwiGLU in its
+        epilogue where the shape runs on the 256×256 kernel, else the GEMM and swiglu_f16."""
+        if self.gu_blk:
+            from k8s_nvidia_gpus_amd.ops import gemm_epi as GE
+
+            if GE.supported(xn, w) and GE.linear_swiglu(xn, w, t) is not None:
+                return
+        self.LK.swiglu_f16(mm(xn, w), t, self.gu_blk)
+
     def dense_weights(self) -> Dict[str, torch.Tensor]:
         if self._dense_w is None:
             dt = torch.float16 if self.gpu else torch.float32
@@ -155,7 +171,11 @@ class Engine:
                 d[f"{i}.qkv"] = torch.cat([w.dequant(dt) for w in L.wqkv], 0)
                 d[f"{i}.bqkv"] = L.bqkv.to(dt)
                 d[f"{i}.o"] = L.wo.dequant(dt)
-                d[f"{i}.gu"] = torch.cat([L.wg.dequant(dt), L.wu.dequant(dt)], 0)
+                if self.gu_blk:      # 128-row gate|up blocks: the fused-SwiGLU GEMM's layout
+                    d[f"{i}.gu"] = gate_up_interleave(L.wg.dequant(dt), L.wu.dequant(dt),
+                                                      self.gu_blk)
+                else:
+                    d[f"{i}.gu"] = torch.cat([L.wg.dequant(dt), L.wu.dequant(dt)], 0)
                 d[f"{i}.down"] = L.wd.dequant(dt)
             d["out"] = self.w.output.dequant(dt)
             self._dense_w = d
@@ -202,7 +222,9 @@ class Engine:
             x = mm_res(x, o, W[f"{i}.o"])
             xn = (x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + c.eps) * L.ffn_norm).to(dt)
             gu = mm(xn, W[f"{i}.gu"]).float()
-            t = F.silu(gu[:, :c.ffn]) * gu[:, c.ffn:]
+            g, u = (gate_up_split(gu, self.gu_blk) if self.gu_blk
+                    else (gu[:, :c.ffn], gu[:, c.ffn:]))
+            t = F.silu(g) * u
             x = mm_res(x, t.to(dt), W[f"{i}.down"])
         xl = x[-1:]
         xn = (xl * torch.rsqrt(xl.pow(2).mean(-1, keepdim=True) + c.eps) * self.w.out_norm).to(dt)
@@ -255,7 +277,7 @@ class Engine:
                 LK.prefill_attn(qh, self.k_cache[i, slot], self.v_cache[i, slot], oh, start, scale)
                 x = mm_res(x, o, W[f"{i}.o"])
                 LK.rmsnorm_f16(x, L.ffn_norm, c.eps, xn)
-                LK.swiglu_f16(mm(xn, W[f"{i}.gu"]), t)
+                self._gate_up(mm, xn, W[f"{i}.gu"], t)
                 x = mm_res(x, t, W[f"{i}.down"])
                 continue
             if self.prefill_gqa:       # K/V read in place by SDPA's GQA path; causal flag from 0
@@ -273,7 +295,7 @@ class Engine:
             o = o[0].transpose(0, 1).reshape(P, c.dim)
             x = mm_res(x, o, W[f"{i}.o"])
             LK.rmsnorm_f16(x, L.ffn_norm, c.eps, xn)
-            LK.swiglu_f16(mm(xn, W[f"{i}.gu"]), t)
+            self._gate_up(mm, xn, W[f"{i}.gu"], t)
             x = mm_res(x, t, W[f"{i}.down"])
         LK.rmsnorm_f16(x[-1:], self.w.out_norm, c.eps, xn[:1])
         return mm(xn[:1], W["out"]).float()[0]
@@ -324,7 +346,7 @@ class Engine:
                 o[a:b] = os_[0].transpose(0, 1).reshape(n, c.dim)
             x = mm_res(x, o, W[f"{i}.o"])
             LK.rmsnorm_f16(x, L.ffn_norm, c.eps, xn)
-            LK.swiglu_f16(mm(xn, W[f"{i}.gu"]), t)
+            self._gate_up(mm, xn, W[f"{i}.gu"], t)
             x = mm_res(x, t, W[f"{i}.down"])
         last = torch.tensor([b - 1 for b in offs[1:]], device=self.device)
         xl = x.index_select(0, last)

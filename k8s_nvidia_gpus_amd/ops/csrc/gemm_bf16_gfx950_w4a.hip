@@ -53,7 +53,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 // (v_mfma_f32_16x16x32_f16, fp16 C) — same fragment layout, LDS image and cycles as bf16.
 constexpr int kF16 = 16;
 
-constexpr int kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiResid = 3;
+constexpr int kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiResid = 3, kEpiSwiGLU = 4;
 
 // Two 16-bit C values of one dword → fp32 (bf16, or fp16 under the kF16 schedule).
 template <bool H>
@@ -83,6 +83,11 @@ struct W4aResid {
   const float* gate;
   int ldx, rows_per_gate, gate_stride;
 };
+
+// silu(g) · u of the 16-bit-rounded gate and up products, exactly as the LLM prefill's separate
+// swiglu_f16 pass computes it from the stored gate|up tensor (llm_prefill.hip), so fusing it
+// changes no bits
+__device__ __forceinline__ float w4a_swiglu(float g, float u) { return g / (1.f + __expf(-g)) * u; }
 
 __device__ __forceinline__ float w4a_gelu_tanh(float v) {
   // 0.5 v (1 + tanh(√(2/π)(v + 0.044715 v³))) = v · sigmoid(2u) = v / (1 + 2^t), t = −2u·log2 e:
@@ -166,8 +171,32 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
   __syncthreads();  // every wave's quarter of the bf16 C image is in LDS
 
   // ---- 16-B coalesced stores of the 256×256 bf16 tile ----
-  char* cbase_g = reinterpret_cast<char*>(C) + ((size_t)m0 * ldc + n0) * 2;
   const size_t ldc_b = (size_t)ldc * 2;
+  const int rows_valid = min(BM, M - m0);
+  if constexpr (EPI == kEpiSwiGLU) {
+    // B rows come tile-interleaved (each 256-row tile: 128 gate rows, then the same 128 up rows):
+    // columns c and c + 128 of the C image are the gate and up of output column n0 / 2 + c, so the
+    // tile stores 256 × 128 outputs, silu(gate) · up, and the 2F-wide product never leaves LDS
+    char* obase = reinterpret_cast<char*>(C) + ((size_t)m0 * ldc + n0 / 2) * 2;
+#pragma unroll 4
+    for (int it = 0; it < BM * (BN / 2) * 2 / (NT * 16); ++it) {
+      const int row = it * 16 + (tid >> 4);
+      const int ch = tid & 15;
+      const u32x4 g = *reinterpret_cast<const u32x4*>(lds + row * C_STRIDE + ch * 16);
+      const u32x4 u = *reinterpret_cast<const u32x4*>(lds + row * C_STRIDE + (ch + 16) * 16);
+      if (row >= rows_valid) continue;
+      u32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        o[e] = w4a_pack<H>(w4a_swiglu(w4a_lo<H>(g[e]), w4a_lo<H>(u[e])),
+                           w4a_swiglu(w4a_hi<H>(g[e]), w4a_hi<H>(u[e])));
+      u32x4* dst = reinterpret_cast<u32x4*>(obase + row * ldc_b + ch * 16);
+      if (nt_store) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(dst), "v"(o) : "memory");
+      else *dst = o;
+    }
+    return;
+  }
+  char* cbase_g = reinterpret_cast<char*>(C) + ((size_t)m0 * ldc + n0) * 2;
   float bv[8];
   if constexpr (EPI != kEpiNone) {   // this thread's 8 columns are the same in every row it stores
     u32x4 braw = {0u, 0u, 0u, 0u};
@@ -178,7 +207,6 @@ amdk8s_gemm_bf16_nt_256x256_w4a(const uint16_t* __restrict__ A, const uint16_t* 
       bv[2 * e + 1] = w4a_hi<H>(braw[e]);
     }
   }
-  const int rows_valid = min(BM, M - m0);
 #pragma unroll 4
   for (int it = 0; it < BM * BN * 2 / (NT * 16); ++it) {
     const int row = it * 8 + (tid >> 5);
@@ -273,19 +301,22 @@ int launch_w4a(const void* A, const void* B, void* C, int M, int N, int K, int l
 
 // Any M >= 1 (N % 256 == 0, K % 64 == 0); epi 0 = plain, 1 = + bias, 2 = gelu_tanh(+ bias),
 // 3 = x[m, n] += gate[m / rows_per_gate, n] · (C + bias) (fp32 x, C not written; bias / gate may
-// be null).  dtype 1 = bf16, 0 = fp16 (operands, bias, C).
+// be null), 4 = SwiGLU of tile-interleaved gate|up rows (C [M, N / 2], bias unused).
+// dtype 1 = bf16, 0 = fp16 (operands, bias, C).
 extern "C" int amdk8s_gemm_w4a_epi(int epi, int dtype, const void* A, const void* B, void* C,
                                    const void* bias, float* x, const float* gate, int M, int N,
                                    int K, int lda, int ldb, int ldc, int ldx, int rows_per_gate,
                                    int gate_stride, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || N % BN || K % BK) return (int)hipErrorInvalidValue;
-  if (epi < kEpiNone || epi > kEpiResid) return (int)hipErrorInvalidValue;
+  if (epi < kEpiNone || epi > kEpiSwiGLU) return (int)hipErrorInvalidValue;
   if (lda % 8 || ldb % 8 || lda < K || ldb < K) return (int)hipErrorInvalidValue;
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)bias) & 15) return (int)hipErrorInvalidValue;
   if (epi == kEpiResid) {
     if (!x || ldx % 4 || ldx < N || ((uintptr_t)x & 15)) return (int)hipErrorInvalidValue;
     if (gate && (rows_per_gate <= 0 || gate_stride % 4 || ((uintptr_t)gate & 15)))
       return (int)hipErrorInvalidValue;
+  } else if (epi == kEpiSwiGLU) {
+    if (!C || ldc % 8 || ldc < N / 2 || ((uintptr_t)C & 15)) return (int)hipErrorInvalidValue;
   } else {
     if (!C || ldc % 8 || ldc < N || ((uintptr_t)C & 15)) return (int)hipErrorInvalidValue;
     if (epi != kEpiNone && !bias) return (int)hipErrorInvalidValue;
@@ -308,11 +339,13 @@ extern "C" int amdk8s_gemm_w4a_epi(int epi, int dtype, const void* A, const void
     if (epi == kEpiBias) launch(amdk8s_gemm_bf16_nt_256x256_w4a<kF16, kEpiBias>);
     else if (epi == kEpiBiasGelu) launch(amdk8s_gemm_bf16_nt_256x256_w4a<kF16, kEpiBiasGelu>);
     else if (epi == kEpiResid) launch(amdk8s_gemm_bf16_nt_256x256_w4a<kF16, kEpiResid>);
+    else if (epi == kEpiSwiGLU) launch(amdk8s_gemm_bf16_nt_256x256_w4a<kF16, kEpiSwiGLU>);
     else launch(amdk8s_gemm_bf16_nt_256x256_w4a<kF16, kEpiNone>);
   } else {
     if (epi == kEpiBias) launch(amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiBias>);
     else if (epi == kEpiBiasGelu) launch(amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiBiasGelu>);
     else if (epi == kEpiResid) launch(amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiResid>);
+    else if (epi == kEpiSwiGLU) launch(amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiSwiGLU>);
     else launch(amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiNone>);
   }
   return (int)hipGetLastError();
@@ -367,6 +400,78 @@ w4a_splitk_finalize(const uint16_t* __restrict__ ws, int S, long slice_stride, i
   *reinterpret_cast<u32x4*>(C + (long)m * ldc + c) = o;
 }
 
+// The same for SwiGLU (tile-interleaved gate|up, see kEpiSwiGLU): output column group c of the
+// rest is gate column (c / 128) · 256 + c % 128 and up column + 128; each sum is rounded to 16 bits
+// (what the plain finalize stores) before silu(gate) · up.
+template <bool H>
+__global__ void __launch_bounds__(256)
+w4a_splitk_finalize_swiglu(const uint16_t* __restrict__ ws, int S, long slice_stride, int M,
+                           int Nb, uint16_t* __restrict__ C, int ldc) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;   // one 8-column output group
+  const int groups = Nb >> 4;
+  if (i >= (long)M * groups) return;
+  const int m = (int)(i / groups), oc = (int)(i - (long)m * groups) * 8;
+  const int gc = (oc >> 7) * 256 + (oc & 127);
+  float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, u[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < S; ++s) {
+    const u32x4 vg = *reinterpret_cast<const u32x4*>(ws + s * slice_stride + (long)m * Nb + gc);
+    const u32x4 vu = *reinterpret_cast<const u32x4*>(ws + s * slice_stride + (long)m * Nb + gc + 128);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      g[2 * e] += w4a_lo<H>(vg[e]);
+      g[2 * e + 1] += w4a_hi<H>(vg[e]);
+      u[2 * e] += w4a_lo<H>(vu[e]);
+      u[2 * e + 1] += w4a_hi<H>(vu[e]);
+    }
+  }
+  u32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t gr = w4a_pack<H>(g[2 * e], g[2 * e + 1]), ur = w4a_pack<H>(u[2 * e], u[2 * e + 1]);
+    o[e] = w4a_pack<H>(w4a_swiglu(w4a_lo<H>(gr), w4a_lo<H>(ur)),
+                       w4a_swiglu(w4a_hi<H>(gr), w4a_hi<H>(ur)));
+  }
+  *reinterpret_cast<u32x4*>(C + (long)m * ldc + oc) = o;
+}
+
+// Split-K residual finalize: x[m, n] += Σ_s partial_s[m, n] (+ bias), fp32 sums of the 16-bit
+// partial tiles in slice order, straight into the fp32 residual stream.
+template <bool H>
+__global__ void __launch_bounds__(256)
+w4a_splitk_finalize_resid(const uint16_t* __restrict__ ws, int S, long slice_stride, int M, int N,
+                          float* __restrict__ x, int ldx, const uint16_t* __restrict__ bias) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;   // one 8-column group
+  const int groups = N >> 3;
+  if (i >= (long)M * groups) return;
+  const int m = (int)(i / groups), c = (int)(i - (long)m * groups) * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < S; ++s) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(ws + s * slice_stride + (long)m * N + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc[2 * e] += w4a_lo<H>(v[e]);
+      acc[2 * e + 1] += w4a_hi<H>(v[e]);
+    }
+  }
+  if (bias) {
+    const u32x4 b = *reinterpret_cast<const u32x4*>(bias + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc[2 * e] += w4a_lo<H>(b[e]);
+      acc[2 * e + 1] += w4a_hi<H>(b[e]);
+    }
+  }
+  f32x4* xp = reinterpret_cast<f32x4*>(x + (long)m * ldx + c);
+  f32x4 x0 = xp[0], x1 = xp[1];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    x0[e] += acc[e];
+    x1[e] += acc[4 + e];
+  }
+  xp[0] = x0;
+  xp[1] = x1;
+}
+
 // The hybrid's plan: na = columns run as whole waves (a multiple of 256, possibly 0 — then the
 // plain kernel is the better choice) and ks = K slices per tile of the rest; ks = 1: no hybrid.
 extern "C" void amdk8s_gemm_w4a_hybrid_plan(int M, int N, int K, int cus, int* na, int* ks) {
@@ -391,12 +496,12 @@ extern "C" void amdk8s_gemm_w4a_hybrid_plan(int M, int N, int K, int cus, int* n
 }
 
 // C[M, N] = A·Bᵀ (+ bias) with the partial last wave split over K (see above); ws: ks × M × (N - na)
-// 16-bit elements (dtype as the operands).  epi 0 = plain, 1 = + bias.
+// 16-bit elements (dtype as the operands).  epi 0 = plain, 1 = + bias, 4 = SwiGLU (C [M, N / 2]).
 extern "C" int amdk8s_gemm_w4a_hybrid(int epi, int dtype, const void* A, const void* B, void* C,
                                       const void* bias, int M, int N, int K, int lda, int ldb,
                                       int ldc, int na, int ks, void* ws, long ws_elems,
                                       hipStream_t stream) {
-  if (epi != kEpiNone && epi != kEpiBias) return (int)hipErrorInvalidValue;
+  if (epi != kEpiNone && epi != kEpiBias && epi != kEpiSwiGLU) return (int)hipErrorInvalidValue;
   if (M <= 0 || N % BN || K % BK || na % BN || na <= 0 || na >= N || ks < 2) return (int)hipErrorInvalidValue;
   const int nb = N - na;
   if ((long)ks * M * nb > ws_elems || !ws || ((uintptr_t)ws & 15)) return (int)hipErrorInvalidValue;
@@ -423,6 +528,17 @@ extern "C" int amdk8s_gemm_w4a_hybrid(int epi, int dtype, const void* A, const v
                        stride);
   rc = (int)hipGetLastError();
   if (rc) return rc;
+  if (epi == kEpiSwiGLU) {
+    const long og = (long)M * (nb / 16);
+    uint16_t* c = (uint16_t*)C + na / 2;
+    if (dtype == 0)
+      hipLaunchKernelGGL(w4a_splitk_finalize_swiglu<true>, dim3((unsigned)((og + 255) / 256)),
+                         dim3(256), 0, stream, w, ks, stride, M, nb, c, ldc);
+    else
+      hipLaunchKernelGGL(w4a_splitk_finalize_swiglu<false>, dim3((unsigned)((og + 255) / 256)),
+                         dim3(256), 0, stream, w, ks, stride, M, nb, c, ldc);
+    return (int)hipGetLastError();
+  }
   const long groups = (long)M * (nb / 8);
   const uint16_t* bs = epi == kEpiBias ? (const uint16_t*)bias + na : nullptr;
   uint16_t* c = (uint16_t*)C + na;
@@ -432,5 +548,86 @@ extern "C" int amdk8s_gemm_w4a_hybrid(int epi, int dtype, const void* A, const v
   else
     hipLaunchKernelGGL(w4a_splitk_finalize<false>, dim3((unsigned)((groups + 255) / 256)), dim3(256),
                        0, stream, w, ks, stride, M, nb, c, ldc, bs);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------- split-K over every tile
+// A 256×256 grid far below the chip (the LLM prefill's q|k|v, o_proj and ffn_down at 512 tokens:
+// 36 / 28 / 28 tiles on 256 CUs) otherwise runs on the smaller wave-grid tiles at a fraction of
+// this kernel's rate.  Here every tile splits over K: ks workgroups per tile each run a contiguous
+// range of its K-tiles into a 16-bit partial tile (fp16 only, like the hybrid: at most 8 roundings
+// at 11 mantissa bits), and a finalize pass sums the slices in fp32 in slice order and applies the
+// epilogue (store / + bias / += into the fp32 residual stream / SwiGLU).
+extern "C" void amdk8s_gemm_w4a_splitk_plan(int M, int N, int K, int cus, int* ks) {
+  *ks = 1;
+  if (M < 256 || N % BN || K % BK || cus <= 0) return;
+  const int tiles = ((M + BM - 1) / BM) * (N / BN), T = K / BK;
+  if (tiles * 4 >= cus * 3) return;               // the plain grid fills >= 3/4 of the chip
+  int s = cus / tiles;
+  s = s < T / 6 ? s : T / 6;                      // >= 6 K-tiles per slice (ring fill + drain)
+  s = s < 8 ? s : 8;
+  if (s >= 2) *ks = s;
+}
+
+extern "C" int amdk8s_gemm_w4a_splitk(int epi, int dtype, const void* A, const void* B, void* C,
+                                      const void* bias, float* x, int M, int N, int K, int lda,
+                                      int ldb, int ldc, int ldx, int ks, void* ws, long ws_elems,
+                                      hipStream_t stream) {
+  if (epi != kEpiNone && epi != kEpiBias && epi != kEpiResid && epi != kEpiSwiGLU)
+    return (int)hipErrorInvalidValue;
+  if (M <= 0 || N <= 0 || N % BN || K % BK || ks < 2 || K / BK < ks) return (int)hipErrorInvalidValue;
+  if ((long)ks * M * N > ws_elems || !ws || ((uintptr_t)ws & 15)) return (int)hipErrorInvalidValue;
+  if (lda % 8 || ldb % 8 || lda < K || ldb < K) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)bias) & 15) return (int)hipErrorInvalidValue;
+  if (256ull * (unsigned long long)(lda > ldb ? lda : ldb) * 2 >= (1ull << 31))
+    return (int)hipErrorInvalidValue;
+  if (epi == kEpiResid) {
+    if (!x || ldx % 4 || ldx < N || ((uintptr_t)x & 15)) return (int)hipErrorInvalidValue;
+  } else {
+    const int w = epi == kEpiSwiGLU ? N / 2 : N;
+    if (!C || ldc % 8 || ldc < w || ((uintptr_t)C & 15)) return (int)hipErrorInvalidValue;
+    if (epi == kEpiBias && !bias) return (int)hipErrorInvalidValue;
+  }
+  const int tm = (M + BM - 1) / BM, tn = N / BN;
+  const int sb = amdk8s::tile_order_arg(tm, tn);
+  const uint16_t* a = (const uint16_t*)A;
+  const uint16_t* b = (const uint16_t*)B;
+  uint16_t* w = (uint16_t*)ws;
+  const long stride = (long)M * N;
+  constexpr int S = AMDK8S_W4A_DEFAULT_SCHEDULE;
+  if (dtype == 0)
+    hipLaunchKernelGGL((amdk8s_gemm_bf16_nt_256x256_w4a<kF16, kEpiNone>), dim3(tm * tn * ks), dim3(NT),
+                       0, stream, a, b, w, M, N, K, lda, ldb, N, sb, 0, nullptr, W4aResid{}, ks, stride);
+  else
+    hipLaunchKernelGGL((amdk8s_gemm_bf16_nt_256x256_w4a<S, kEpiNone>), dim3(tm * tn * ks), dim3(NT),
+                       0, stream, a, b, w, M, N, K, lda, ldb, N, sb, 0, nullptr, W4aResid{}, ks, stride);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  const uint16_t* bs = epi == kEpiBias || epi == kEpiResid ? (const uint16_t*)bias : nullptr;
+  uint16_t* c = (uint16_t*)C;
+  const unsigned g8 = (unsigned)(((long)M * (N / 8) + 255) / 256);
+  const unsigned g16 = (unsigned)(((long)M * (N / 16) + 255) / 256);
+  if (epi == kEpiResid) {
+    if (dtype == 0)
+      hipLaunchKernelGGL(w4a_splitk_finalize_resid<true>, dim3(g8), dim3(256), 0, stream, w, ks,
+                         stride, M, N, x, ldx, bs);
+    else
+      hipLaunchKernelGGL(w4a_splitk_finalize_resid<false>, dim3(g8), dim3(256), 0, stream, w, ks,
+                         stride, M, N, x, ldx, bs);
+  } else if (epi == kEpiSwiGLU) {
+    if (dtype == 0)
+      hipLaunchKernelGGL(w4a_splitk_finalize_swiglu<true>, dim3(g16), dim3(256), 0, stream, w, ks,
+                         stride, M, N, c, ldc);
+    else
+      hipLaunchKernelGGL(w4a_splitk_finalize_swiglu<false>, dim3(g16), dim3(256), 0, stream, w, ks,
+                         stride, M, N, c, ldc);
+  } else {
+    if (dtype == 0)
+      hipLaunchKernelGGL(w4a_splitk_finalize<true>, dim3(g8), dim3(256), 0, stream, w, ks, stride, M,
+                         N, c, ldc, bs);
+    else
+      hipLaunchKernelGGL(w4a_splitk_finalize<false>, dim3(g8), dim3(256), 0, stream, w, ks, stride, M,
+                         N, c, ldc, bs);
+  }
   return (int)hipGetLastError();
 }

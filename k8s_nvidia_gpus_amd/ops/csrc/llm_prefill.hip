@@ -12,7 +12,7 @@
 //                 [H][P][128] for SDPA (any head / position strides: the engine stores it as
 //                 [P][H][128], so SDPA's output comes back in token-major order) and rotated k / v
 //                 written to the fp16 KV cache at positions start .. start + P - 1
-//   swiglu_f16    gate|up fp16 [P][2F] -> silu(gate) * up fp16 [P][F]
+//   swiglu_f16    gate|up fp16 [P][2F] -> silu(gate) * up fp16 [P][F] (halves or 128-blocks)
 // The arithmetic is fp32 in registers; the RoPE uses the same explicit roundings as the decode
 // kernels (llm_decode.hip).
 #include <hip/hip_runtime.h>
@@ -131,14 +131,18 @@ __global__ void __launch_bounds__(256) rope_kv_f16_kernel(const uint16_t* __rest
 }
 
 // grid-stride over P * F / 8; thread = 8 outputs
+// blk 0: gate|up rows [gate F | up F]; blk > 0: interleaved in blocks of blk (gate columns
+// [2 blk j, 2 blk j + blk), then the same blk up columns) — the layout the fused-SwiGLU GEMM
+// epilogue reads (gemm_bf16_gfx950_w4a.hip, kEpiSwiGLU)
 __global__ void __launch_bounds__(256) swiglu_f16_kernel(const uint16_t* __restrict__ gu, int P,
-                                                         int F, uint16_t* __restrict__ t) {
+                                                         int F, int blk, uint16_t* __restrict__ t) {
   const long n8 = (long)P * (F >> 3);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8;
        i += (long)gridDim.x * blockDim.x) {
     const long p = i / (F >> 3), c = (i - p * (F >> 3)) * 8;
-    const uint4 g = *reinterpret_cast<const uint4*>(gu + p * 2 * F + c);
-    const uint4 u = *reinterpret_cast<const uint4*>(gu + p * 2 * F + F + c);
+    const long gc = blk ? (c / blk) * 2 * blk + c % blk : c, uo = blk ? blk : F;
+    const uint4 g = *reinterpret_cast<const uint4*>(gu + p * 2 * F + gc);
+    const uint4 u = *reinterpret_cast<const uint4*>(gu + p * 2 * F + gc + uo);
     const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, uw[4] = {u.x, u.y, u.z, u.w};
     uint32_t o[4];
 #pragma unroll
@@ -180,12 +184,12 @@ int amdk8s_llm_rope_kv_f16(const void* qkv, int ldq, const void* cos_t, const vo
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
-int amdk8s_llm_swiglu_f16(const void* gu, int P, int F, void* t, void* stream) {
-  if (F % 8 || P < 1) return 2;
+int amdk8s_llm_swiglu_f16(const void* gu, int P, int F, int blk, void* t, void* stream) {
+  if (F % 8 || P < 1 || blk < 0 || blk % 8 || (blk && F % blk)) return 2;
   const long n8 = (long)P * (F / 8);
   const int grid = (int)((n8 + 255) / 256 < 4096 ? (n8 + 255) / 256 : 4096);
   hipLaunchKernelGGL(swiglu_f16_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const uint16_t*>(gu), P, F, static_cast<uint16_t*>(t));
+                     static_cast<const uint16_t*>(gu), P, F, blk, static_cast<uint16_t*>(t));
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

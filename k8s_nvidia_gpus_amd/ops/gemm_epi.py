@@ -51,6 +51,11 @@ def _lib():
             lib.amdk8s_gemm_w4a_hybrid.argtypes = [ci, ci, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci,
                                                    ci, ci, vp, ctypes.c_long, vp]
             lib.amdk8s_gemm_w4a_hybrid.restype = ci
+            lib.amdk8s_gemm_w4a_splitk_plan.argtypes = [ci, ci, ci, ci, ctypes.POINTER(ci)]
+            lib.amdk8s_gemm_w4a_splitk_plan.restype = None
+            lib.amdk8s_gemm_w4a_splitk.argtypes = [ci, ci, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci,
+                                                   ci, ci, ci, vp, ctypes.c_long, vp]
+            lib.amdk8s_gemm_w4a_splitk.restype = ci
             lib.amdk8s_gemm_epi_set_tile.argtypes = [ci]
             lib.amdk8s_gemm_epi_set_tile.restype = None
             lib.amdk8s_gemm_epi_set_splits.argtypes = [ci]
@@ -68,13 +73,19 @@ def _stream(t: torch.Tensor) -> int:
 TILES = ((256, 128), (128, 128), (128, 64), (64, 64))
 
 
+_PINS = {"tile": -1, "splits": -1}
+
+
 def set_tile(tile: int) -> None:
-    """Pin the wave-grid kernel family's block tile (index into TILES); -1 = the planner."""
+    """Pin the wave-grid kernel family's block tile (index into TILES); -1 = the planner.  A pin
+    also keeps shapes off the split-K w4a form, so the pinned kernel is the one that runs."""
+    _PINS["tile"] = int(tile)
     _lib().amdk8s_gemm_epi_set_tile(int(tile))
 
 
 def set_splits(s: int) -> None:
     """Pin the split-K factor (1 = never split); -1 = the planner."""
+    _PINS["splits"] = int(s)
     _lib().amdk8s_gemm_epi_set_splits(int(s))
 
 
@@ -193,10 +204,10 @@ def hybrid_plan(m: int, n: int, k: int, cus: int = 256) -> tuple:
 
 
 def _w4a_hybrid(epi: int, x2, w, b, out) -> bool:
-    """The hybrid for store / bias epilogues; False when its plan is the plain launch.  fp16
-    only: its K slices meet as 16-bit partial tiles (the K-loop's C image in LDS is 16-bit), and
-    8 roundings at bf16's 8 mantissa bits would cost visible accuracy."""
-    if not _HYBRID or epi not in (0, 1) or x2.dtype != torch.float16:
+    """The hybrid for store / bias / SwiGLU epilogues; False when its plan is the plain launch.
+    fp16 only: its K slices meet as 16-bit partial tiles (the K-loop's C image in LDS is 16-bit),
+    and 8 roundings at bf16's 8 mantissa bits would cost visible accuracy."""
+    if not _HYBRID or epi not in (0, 1, EPI_W4A_SWIGLU) or x2.dtype != torch.float16:
         return False
     m, k = x2.shape
     n = w.shape[0]
@@ -217,6 +228,45 @@ def _aligned16(*ts) -> bool:
     return all(t is None or t.data_ptr() % 16 == 0 for t in ts)
 
 
+# A 256×256 grid far below the chip (LLM prefill chunks: q|k|v, o_proj, ffn_down at 512 tokens)
+# runs with every tile split over K (amdk8s_gemm_w4a_splitk; fp16 only, like the hybrid)
+# instead of on the wave-grid family; AMDK8S_GEMM_W4A_SPLITK=0 turns it off (A/B runs).
+_W4A_SPLITK = os.environ.get("AMDK8S_GEMM_W4A_SPLITK", "1") != "0"
+
+
+def splitk_plan(m: int, n: int, k: int, cus: int = 256) -> int:
+    """K slices per 256×256 tile of the split-K w4a form (1: not used for this shape)."""
+    ks = ctypes.c_int()
+    _lib().amdk8s_gemm_w4a_splitk_plan(m, n, k, cus, ctypes.byref(ks))
+    return ks.value
+
+
+def _w4a_splitk(epi: int, x2, w, b, out=None, res=None) -> bool:
+    """The split-K w4a form with epilogue ``epi`` (0 store, 1 + bias, 3 += res fp32, 4 SwiGLU);
+    False when it does not apply (dtype, layout, or the planner keeps the shape elsewhere)."""
+    if (not _W4A_SPLITK or _WIDE != "w4a" or x2.dtype != torch.float16 or w.dtype != x2.dtype
+            or _PINS["tile"] >= 0 or _PINS["splits"] >= 0):
+        return False
+    m, k = x2.shape
+    n = w.shape[0]
+    if (w.stride(-1) != 1 or w.stride(0) % 8 or x2.stride(0) % 8
+            or not _aligned16(x2, w, b, out, res)):
+        return False
+    if out is not None and (out.stride(-1) != 1 or out.stride(0) % 8):
+        return False
+    ks = splitk_plan(m, n, k, _cus(x2.device))
+    if ks <= 1:
+        return False
+    ws = torch.empty(ks * m * n, dtype=x2.dtype, device=x2.device)
+    rc = _lib().amdk8s_gemm_w4a_splitk(
+        epi, _DT[x2.dtype], x2.data_ptr(), w.data_ptr(), _ptr(out), _ptr(b), _ptr(res), m, n, k,
+        x2.stride(0), w.stride(0), out.stride(0) if out is not None else 0, n, ks, ws.data_ptr(),
+        ws.numel(), _stream(x2))
+    if rc != 0:
+        raise RuntimeError(f"amdk8s_gemm_w4a_splitk failed (rc={rc}, M={m} N={n} K={k}, epi={epi})")
+    return True
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
            gelu: bool = False) -> torch.Tensor:
     """``x·wᵀ + b`` (tanh-GELU with ``gelu``) in x's dtype: ``x`` [..., K], ``w`` [N, K]."""
@@ -230,9 +280,37 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
         epi = 2 if gelu else (0 if bb is None else 1)
         if not _w4a_hybrid(epi, x2, w, bb, out):
             _w4a(epi, x2, w, bb, out)
-    else:
+    elif gelu or not _w4a_splitk(0 if bb is None else 1, x2, w, bb, out):
         _run(EPI_GELU if gelu else EPI_STORE, x2, w, bb, out, None, None, 0, 0, n, 0)
     return out.view(*x.shape[:-1], n)
+
+
+EPI_W4A_SWIGLU = 4
+
+
+def linear_swiglu(x: torch.Tensor, w: torch.Tensor,
+                  out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """``silu(gate) · up`` of ``x·wᵀ`` in one GEMM: ``w`` [2F, K] holds gate|up rows interleaved
+    in 128-row blocks (``llm_kernels.gate_up_interleave``), so every 256×256 tile carries matching
+    gate and up columns and its epilogue writes its 256 × 128 share of the [M, F] result from
+    LDS — the [M, 2F] product is never stored.  The arithmetic is the separate swiglu_f16 pass's on the
+    16-bit products, so the bits match that path.  None when the shape is not on the 256×256
+    kernel (the caller runs the GEMM and swiglu_f16 instead)."""
+    x2 = _rows(x)
+    m, k = x2.shape
+    n = w.shape[0]
+    if (x.dtype not in _DT or w.dtype != x.dtype or n % 256 or k % 64 or not _aligned16(x2, w)
+            or w.stride(-1) != 1 or w.stride(0) % 8):
+        return None
+    if out is None:
+        out = torch.empty((m, n // 2), dtype=x.dtype, device=x.device)
+    elif out.shape != (m, n // 2) or out.stride(-1) != 1 or out.stride(0) % 8 or not _aligned16(out):
+        raise ValueError(f"linear_swiglu: out {tuple(out.shape)} is not a [{m}, {n // 2}] row-major tensor")
+    if use_w4a(m, n, k, x.dtype):
+        if not _w4a_hybrid(EPI_W4A_SWIGLU, x2, w, None, out):
+            _w4a(EPI_W4A_SWIGLU, x2, w, None, out)
+        return out
+    return out if _w4a_splitk(EPI_W4A_SWIGLU, x2, w, None, out) else None
 
 
 def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -263,7 +341,7 @@ def linear_residual_(res: torch.Tensor, x: torch.Tensor, w: torch.Tensor,
     bb = _bias(b, n, x.dtype)
     if use_w4a(x2.shape[0], n, x2.shape[1], x.dtype) and _aligned16(x2, w, bb, res, gate):
         _w4a(3, x2, w, bb, None, res, gate, rows_per_gate, gstride)
-    else:
+    elif gate is not None or not _w4a_splitk(3, x2, w, bb, None, res):
         _run(EPI_RESID, x2, w, bb, None, res, gate, rows_per_gate, gstride, 0, n)
     return res
 

@@ -66,7 +66,7 @@ def _lib():
             lib.amdk8s_llm_rope_kv_f16.argtypes = [vp, ci, vp, vp, ci, ci, ci, ci, ci, ci, cl, cl,
                                                    vp, vp, vp, vp]
             lib.amdk8s_llm_rope_kv_f16.restype = ci
-            lib.amdk8s_llm_swiglu_f16.argtypes = [vp, ci, ci, vp, vp]
+            lib.amdk8s_llm_swiglu_f16.argtypes = [vp, ci, ci, ci, vp, vp]
             lib.amdk8s_llm_swiglu_f16.restype = ci
             _declared = True
     return lib
@@ -300,11 +300,30 @@ def rope_kv_f16(qkv, cos_t, sin_t, start: int, heads: int, kv_heads: int, max_ct
                                          _stream(qkv)), "amdk8s_llm_rope_kv_f16")
 
 
-def swiglu_f16(gu, t) -> None:
-    """t (fp16 [P, F]) = silu(gu[:, :F]) * gu[:, F:] for gu fp16 [P, 2F] (both contiguous)."""
+def swiglu_f16(gu, t, blk: int = 0) -> None:
+    """t (fp16 [P, F]) = silu(gate) * up for gu fp16 [P, 2F] (both contiguous): gate = gu[:, :F],
+    up = gu[:, F:] (blk 0), or gate|up interleaved in blocks of ``blk`` columns
+    (``gate_up_interleave``)."""
     p, f = t.shape
-    _check(_lib().amdk8s_llm_swiglu_f16(gu.data_ptr(), p, f, t.data_ptr(), _stream(gu)),
+    _check(_lib().amdk8s_llm_swiglu_f16(gu.data_ptr(), p, f, int(blk), t.data_ptr(), _stream(gu)),
            "amdk8s_llm_swiglu_f16")
+
+
+def gate_up_interleave(wg, wu, blk: int = 128):
+    """[2F, K] rows of gate and up interleaved in blocks of ``blk`` rows (gate rows blk·j..,
+    then the same up rows): the layout whose 256-row GEMM tiles hold matching gate and up
+    columns, so the SwiGLU runs in the GEMM epilogue (gemm_epi.linear_swiglu)."""
+    f, k = wg.shape
+    if f % blk:
+        raise ValueError(f"gate rows {f} are not a multiple of {blk}")
+    return torch.stack([wg.view(f // blk, blk, k), wu.view(f // blk, blk, k)], 1).reshape(2 * f, k)
+
+
+def gate_up_split(gu, blk: int = 128):
+    """Inverse view of ``gate_up_interleave`` on a product [.., 2F]: (gate, up) [.., F] each."""
+    f2 = gu.shape[-1]
+    v = gu.reshape(*gu.shape[:-1], f2 // (2 * blk), 2, blk)
+    return v[..., 0, :].reshape(*gu.shape[:-1], f2 // 2), v[..., 1, :].reshape(*gu.shape[:-1], f2 // 2)
 
 
 # ---------------------------------------------------------------------- prompt attention (llm_prefill_attn.hip)

@@ -280,3 +280,89 @@ def test_w4a_partial_last_wave_split_over_k(GE, m, n, k, bias, dtype):
     # the split columns agree with the plain kernel's to fp16 rounding
     torch.testing.assert_close(y[:, na:].float(), plain[:, na:].float(), rtol=3e-3, atol=3e-3)
     assert torch.equal(y[:, :na], plain[:, :na])            # whole waves: the same kernel
+
+
+@pytest.mark.parametrize("m,f,k", [(512, 18944, 3584), (1024, 6144, 1024), (700, 9472, 512)])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_w4a_swiglu_epilogue_equals_gemm_then_swiglu(GE, m, f, k, dtype):
+    """SwiGLU in the 256×256 kernel's epilogue (tile-interleaved gate|up rows; the LLM prefill's
+    gate|up at 512 tokens runs it as the hybrid, whose K-split finalize applies it too): the same
+    bits as the stored [M, 2F] product followed by the swiglu_f16 pass (fp16), and the fp32
+    reference to rounding."""
+    from k8s_nvidia_gpus_amd.ops import llm_kernels as LK
+
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(m + f)
+    x = torch.randn(m, k, generator=g, device=dev).to(dtype)
+    wg = (torch.randn(f, k, generator=g, device=dev) / k ** 0.5).to(dtype)
+    wu = (torch.randn(f, k, generator=g, device=dev) / k ** 0.5).to(dtype)
+    w = LK.gate_up_interleave(wg, wu)
+    gate, up = LK.gate_up_split(w.float().t())
+    assert torch.equal(gate, wg.float().t()) and torch.equal(up, wu.float().t())
+    t = GE.linear_swiglu(x, w)
+    assert t is not None and t.shape == (m, f)
+    prod = GE.linear(x, w)                       # the same kernel (and plan), stored
+    gp, up_ = LK.gate_up_split(prod.float())
+    ref16 = (F.silu(gp) * up_)
+    ref = F.silu(x.float() @ wg.float().t()) * (x.float() @ wu.float().t())
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-2
+    torch.testing.assert_close(t.float(), ref, rtol=tol, atol=tol)
+    torch.testing.assert_close(t.float(), ref16, rtol=tol / 4, atol=tol / 4)
+    if dtype == torch.float16:                   # bit-equal to the two-pass fp16 path
+        t2 = torch.empty_like(t)
+        LK.swiglu_f16(prod, t2, 128)
+        assert torch.equal(t, t2)
+    if m == 512 and dtype == torch.float16:     # the prefill shape takes the hybrid
+        assert GE.hybrid_plan(m, 2 * f, k, GE._cus(dev))[1] > 1
+
+
+def test_swiglu_f16_block_layout_matches_halves(GE):
+    """swiglu_f16 on the 128-block interleaved layout gives the bits of the halves layout."""
+    from k8s_nvidia_gpus_amd.ops import llm_kernels as LK
+
+    dev = torch.device("cuda")
+    p, f = 37, 384
+    gate = torch.randn(p, f, device=dev).half()
+    up = torch.randn(p, f, device=dev).half()
+    halves = torch.cat([gate, up], 1).contiguous()
+    inter = LK.gate_up_interleave(gate.t().contiguous(), up.t().contiguous()).t().contiguous()
+    a, b = torch.empty(p, f, device=dev).half(), torch.empty(p, f, device=dev).half()
+    LK.swiglu_f16(halves, a)
+    LK.swiglu_f16(inter, b, 128)
+    assert torch.equal(a, b)
+    torch.testing.assert_close(a.float(), F.silu(gate.float()) * up.float(), rtol=2e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize("m,n,k", [(512, 4608, 3584), (512, 3584, 3584), (512, 3584, 18944),
+                                   (300, 1536, 1536)])
+@pytest.mark.parametrize("epi", ["store", "bias", "resid"])
+def test_w4a_split_k_every_tile(GE, m, n, k, epi):
+    """The LLM prefill chunk's narrow GEMMs (q|k|v, o_proj, ffn_down at 512 tokens: 28-36 tiles of
+    256×256) on the 256×256 kernel with every tile split over K (16-bit partial tiles, fp32 sums in
+    slice order in the finalize, which applies the epilogue): the planner engages, and store /
+    + bias / += into the fp32 residual stream equal the fp32 reference (fp16)."""
+    dev = torch.device("cuda")
+    ks = GE.splitk_plan(m, n, k, GE._cus(dev))
+    assert 2 <= ks <= 8, ks
+    g = torch.Generator(device=dev).manual_seed(m * 7 + n + k)
+    x = torch.randn(m, k, generator=g, device=dev).half()
+    w = (torch.randn(n, k, generator=g, device=dev) / k ** 0.5).half()
+    b = torch.randn(n, generator=g, device=dev).half() if epi != "store" else None
+    ref = _ref(x, w, b)
+    if epi == "resid":
+        res = torch.randn(m, n, generator=g, device=dev)
+        want = res + ref
+        GE.linear_residual_(res, x, w, b)
+        torch.testing.assert_close(res, want, rtol=5e-3, atol=5e-3)
+        return
+    y = GE.linear(x, w, b)
+    torch.testing.assert_close(y.float(), ref, rtol=5e-3, atol=5e-3)
+    # deterministic: the slices are summed in a fixed order
+    assert torch.equal(y, GE.linear(x, w, b))
+    # a pinned wave-grid tile keeps the shape off the split form (the A/B contract of set_tile)
+    GE.set_tile(0)
+    try:
+        y2 = GE.linear(x, w, b)
+    finally:
+        GE.set_tile(-1)
+    torch.testing.assert_close(y2.float(), ref, rtol=5e-3, atol=5e-3)

@@ -107,3 +107,19 @@ def test_use_w4a_routing():
     # 3/4 of a wave and up (LLM prefill q|k|v and o_proj at 3584 tokens: 252 / 196 tiles)
     assert GE.use_w4a(3584, 4608, 3584, torch.float16) and GE.use_w4a(3584, 3584, 3584, torch.float16)
     assert not GE.use_w4a(2560, 4608, 3584, torch.float16)     # 10 x 18 = 180 tiles
+
+
+@pytest.mark.parametrize("shape,ks", [
+    ((512, 4608, 3584), 7),      # LLM prefill q|k|v chunk: 36 tiles x 7 slices
+    ((512, 3584, 3584), 8),      # o_proj: 28 x 8
+    ((512, 3584, 18944), 8),     # ffn_down: 28 x 8
+    ((300, 1536, 1536), 4),      # 12 tiles, 24 K-tiles: >= 6 per slice
+    ((8192, 1536, 1536), 1),     # 192 tiles fill 3/4 of the chip: plain
+    ((512, 37888, 3584), 1),     # gate|up: 296 tiles (the hybrid's case)
+    ((128, 4608, 3584), 1),      # below one 256-row panel: the wave-grid family
+    ((512, 4608, 320), 1),       # 5 K-tiles: nothing to split
+])
+def test_w4a_splitk_plan(ge, shape, ks):
+    """Split-K over every 256×256 tile (amdk8s_gemm_w4a_splitk_plan): slices fill the chip, at
+    most 8 (16-bit partial tiles), at least 6 K-tiles each, only when the plain grid is < 3/4."""
+    assert ge.splitk_plan(*shape) == ks

@@ -623,3 +623,22 @@ def test_file_template_drives_chat_prompts_and_unsupported_files_are_refused(tmp
         write_synthetic_gguf(q, tiny(), extra_metadata=extra)
         with pytest.raises(ValueError, match=needle):
             load(q, device="cpu", max_ctx=256, slots=1)
+
+
+def test_gate_up_interleave_round_trip():
+    """The prefill's gate|up weight layout (128-row blocks: the fused-SwiGLU GEMM's tiles hold
+    matching gate and up columns): the product's columns split back into gate and up exactly."""
+    from k8s_nvidia_gpus_amd.ops.llm_kernels import gate_up_interleave, gate_up_split
+
+    torch.manual_seed(0)
+    f, k = 384, 40
+    wg, wu = torch.randn(f, k), torch.randn(f, k)
+    w = gate_up_interleave(wg, wu)
+    assert w.shape == (2 * f, k)
+    assert torch.equal(w[128:256], wu[:128]) and torch.equal(w[256:384], wg[128:256])
+    x = torch.randn(5, k)
+    g, u = gate_up_split(x @ w.t())
+    torch.testing.assert_close(g, x @ wg.t())
+    torch.testing.assert_close(u, x @ wu.t())
+    with pytest.raises(ValueError):
+        gate_up_interleave(torch.randn(100, k), torch.randn(100, k))

@@ -43,7 +43,8 @@ def main():
     P = int(os.environ.get("PROBE_P", "512"))
     only = os.environ.get("PROBE_VARIANTS")
     g = torch.Generator(device=dev).manual_seed(0)
-    for start in [0, 1536, 3072, 8192, 16384, 31488]:
+    starts = [int(v) for v in os.environ.get("PROBE_STARTS", "0,1536,3072,8192,16384,31488").split(",")]
+    for start in starts:
         end = start + P
         q = torch.randn(1, H, P, d, device=dev, dtype=torch.float16, generator=g)
         k = torch.randn(1, Hkv, end, d, device=dev, dtype=torch.float16, generator=g)

@@ -38,6 +38,9 @@ def main() -> int:
     ap.add_argument("--quick", action="store_true", help="planner / w4a / torch only (no sweep)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default="", help="comma-separated GEMM names (qkv,o,gate_up,down)")
+    ap.add_argument("--cold", action="store_true",
+                    help="cycle through weight copies totalling > 512 MB, so every call streams its "
+                         "weights from HBM as in a prefill (not from the Infinity Cache)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     rows = []
@@ -46,12 +49,17 @@ def main() -> int:
             continue
         m = a.m
         x = torch.randn(m, k, device=dev, dtype=torch.float16)
-        w = torch.randn(n, k, device=dev, dtype=torch.float16) / k ** 0.5
+        copies = max(1, -(-(512 << 20) // (n * k * 2))) if a.cold else 1
+        ws = [torch.randn(n, k, device=dev, dtype=torch.float16) / k ** 0.5 for _ in range(copies)]
+        w = ws[0]
         res = torch.zeros(m, n, device=dev)
         flop = 2.0 * m * n * k
+        it = [0]
 
         def run():
-            return GE.linear(x, w) if kind == "store" else GE.linear_residual_(res, x, w)
+            wi = ws[it[0] % copies]
+            it[0] += 1
+            return GE.linear(x, wi) if kind == "store" else GE.linear_residual_(res, x, wi)
 
         def rec(variant, us):
             r = {"gemm": name, "m": m, "n": n, "k": k, "variant": variant, "us": round(us, 1),
@@ -60,12 +68,22 @@ def main() -> int:
             print(r, flush=True)
 
         rec(f"auto plan={GE.plan(m, n, k)} w4a={GE.use_w4a(m, n, k, x.dtype)} "
-            f"hybrid={GE.hybrid_plan(m, n, k)}", bench(run))
+            f"hybrid={GE.hybrid_plan(m, n, k)} splitk={GE.splitk_plan(m, n, k)}"
+            f"{' cold' if a.cold else ''}", bench(run))
         if GE.use_w4a(m, n, k, x.dtype):
             GE._HYBRID = False
             rec("w4a plain (no partial-wave split)", bench(run))
             GE._HYBRID = True
-        rec("torch", bench(lambda: F.linear(x, w)))
+        if GE.splitk_plan(m, n, k) > 1:
+            GE._W4A_SPLITK = False
+            rec(f"wave-grid plan={GE.plan(m, n, k)} (split-K w4a off)", bench(run))
+            GE._W4A_SPLITK = True
+
+        def tl():
+            wi = ws[it[0] % copies]
+            it[0] += 1
+            return F.linear(x, wi)
+        rec("torch", bench(tl))
         if a.quick:
             continue
         wide = GE._WIDE
