@@ -163,6 +163,21 @@ class Engine:
                 return
         self.LK.swiglu_f16(mm(xn, w), t, self.gu_blk)
 
+    def _res_norm(self, mm_res, x: torch.Tensor, a: torch.Tensor, w: torch.Tensor,
+                  norm_w: Optional[torch.Tensor], xn: torch.Tensor) -> torch.Tensor:
+        """x += a·wᵀ, then (norm_w given) xn = fp16 RMSNorm(x) · norm_w (GPU prefill): one GEMM
+        whose split-K finalize also normalises where the shape runs on the split-K 256×256 form
+        (same bits as the two passes), else the residual GEMM and rmsnorm_f16."""
+        if norm_w is not None:
+            from k8s_nvidia_gpus_amd.ops import gemm_epi as GE
+
+            if GE.supported(a, w) and GE.linear_residual_norm_(x, a, w, norm_w, self.cfg.eps, xn):
+                return x
+        x = mm_res(x, a, w)
+        if norm_w is not None:
+            self.LK.rmsnorm_f16(x, norm_w, self.cfg.eps, xn)
+        return x
+
     def dense_weights(self) -> Dict[str, torch.Tensor]:
         if self._dense_w is None:
             dt = torch.float16 if self.gpu else torch.float32
@@ -268,17 +283,24 @@ class Engine:
             o = torch.empty(P, c.dim, dtype=dt, device=self.device)
             oh = o.view(P, c.heads, c.head_dim).transpose(0, 1)
         scale = 1.0 / math.sqrt(c.head_dim)
-        for i, L in enumerate(self.w.layers):
-            LK.rmsnorm_f16(x, L.attn_norm, c.eps, xn)
+        layers = self.w.layers
+        normed = False                 # xn already holds this layer's attn_norm output
+        for i, L in enumerate(layers):
+            if not normed:
+                LK.rmsnorm_f16(x, L.attn_norm, c.eps, xn)
+            normed = False
             qkv = mm(xn, W[f"{i}.qkv"], W[f"{i}.bqkv"])
             LK.rope_kv_f16(qkv, self.cos, self.sin, start, c.heads, c.kv_heads, self.max_ctx, qh,
                            self.k_cache[i, slot], self.v_cache[i, slot])
             if native_attn:            # hand-written causal GQA kernel, K/V read in place
                 LK.prefill_attn(qh, self.k_cache[i, slot], self.v_cache[i, slot], oh, start, scale)
-                x = mm_res(x, o, W[f"{i}.o"])
-                LK.rmsnorm_f16(x, L.ffn_norm, c.eps, xn)
+                x = self._res_norm(mm_res, x, o, W[f"{i}.o"], L.ffn_norm, xn)
                 self._gate_up(mm, xn, W[f"{i}.gu"], t)
-                x = mm_res(x, t, W[f"{i}.down"])
+                if i + 1 < len(layers):     # ffn_down's finalize also writes the next attn_norm
+                    x = self._res_norm(mm_res, x, t, W[f"{i}.down"], layers[i + 1].attn_norm, xn)
+                    normed = True
+                else:
+                    x = mm_res(x, t, W[f"{i}.down"])
                 continue
             if self.prefill_gqa:       # K/V read in place by SDPA's GQA path; causal flag from 0
                 o = F.scaled_dot_product_attention(
@@ -324,8 +346,12 @@ class Engine:
         qh = torch.empty(P, c.heads, c.head_dim, dtype=dt, device=self.device).transpose(0, 1)
         o = torch.empty(P, c.dim, dtype=dt, device=self.device)
         t = torch.empty(P, c.ffn, dtype=dt, device=self.device)
-        for i, L in enumerate(self.w.layers):
-            LK.rmsnorm_f16(x, L.attn_norm, c.eps, xn)
+        layers = self.w.layers
+        normed = False                 # xn already holds this layer's attn_norm output
+        for i, L in enumerate(layers):
+            if not normed:
+                LK.rmsnorm_f16(x, L.attn_norm, c.eps, xn)
+            normed = False
             qkv = mm(xn, W[f"{i}.qkv"], W[f"{i}.bqkv"])
             for s, (_, slot, st) in enumerate(segs):
                 a, b = offs[s], offs[s + 1]
@@ -344,10 +370,13 @@ class Engine:
                     self.v_cache[i, slot, :, :end][None], attn_mask=lowright[s],
                     is_causal=n > 1 and st == 0, enable_gqa=True)
                 o[a:b] = os_[0].transpose(0, 1).reshape(n, c.dim)
-            x = mm_res(x, o, W[f"{i}.o"])
-            LK.rmsnorm_f16(x, L.ffn_norm, c.eps, xn)
+            x = self._res_norm(mm_res, x, o, W[f"{i}.o"], L.ffn_norm, xn)
             self._gate_up(mm, xn, W[f"{i}.gu"], t)
-            x = mm_res(x, t, W[f"{i}.down"])
+            if i + 1 < len(layers):
+                x = self._res_norm(mm_res, x, t, W[f"{i}.down"], layers[i + 1].attn_norm, xn)
+                normed = True
+            else:
+                x = mm_res(x, t, W[f"{i}.down"])
         last = torch.tensor([b - 1 for b in offs[1:]], device=self.device)
         xl = x.index_select(0, last)
         LK.rmsnorm_f16(xl, self.w.out_norm, c.eps, xn[:len(segs)])

@@ -27,8 +27,9 @@ at decode time ends only the request it belongs to.  Prompt tokenisation and tem
 run in the thread pool, never on the event loop.
 
 One scheduler thread owns the GPU: new requests take free KV-cache slots and their prompts are
-processed in chunks of ``--ubatch-size`` tokens, one chunk per loop iteration, between the decode
-steps of the sequences already generating — up to 8 sequences share each pass over the weights
+processed between the decode steps of the sequences already generating — prompts that fit the
+``--batch-size`` budget whole, a longer one in chunks of ``--ubatch-size`` tokens, one chunk per
+loop iteration — up to 8 sequences share each pass over the weights
 (``--parallel``).  Request handlers await per-request events that the scheduler sets, so the GPU is
 never driven from two threads (the reference's SD15 app had that hazard).  A request
 whose client goes away (stream closed, or the connection dropped while a blocking request waits)
@@ -132,13 +133,14 @@ def _set_events(events) -> None:
 class Scheduler:
     """Continuous batching over the engine's KV-cache slots, with chunked prompt processing.
 
-    One loop iteration: admit pending requests into free slots → run ONE chunk (at most
-    ``ubatch`` tokens) of the oldest admitted prompt → one decode step of every sequence whose
-    prompt is done → wake the consumers.  A long prompt therefore stalls the running streams for
-    one chunk at a time, not for its whole prefill: llama-server's update loop does the same with
-    its ``n_ubatch`` prompt batches next to the decoding slots (reference
-    cluster-config/apps/llm/deployment.yaml:61,76-84 runs llama-server).  While no sequence is
-    decoding, chunks grow to ``batch`` tokens (llama-server's ``n_batch``).
+    One loop iteration: admit pending requests into free slots → one prompt batch → one decode
+    step of every sequence whose prompt is done → wake the consumers.  The prompt batch takes the
+    admitted prompts oldest first: every prompt whose rest fits the ``batch`` budget
+    (llama-server's ``n_batch``) whole, so a burst of requests starts decoding together, and of a
+    prompt that does not fit one chunk — at most ``ubatch`` tokens while other sequences decode.
+    A long prompt therefore stalls the running streams for one chunk at a time, not for its whole
+    prefill (llama-server's update loop fills one n_batch with the decoding slots' tokens and the
+    prompt tokens; reference cluster-config/apps/llm/deployment.yaml:61,76-84 runs llama-server).
 
     Host work per generated token is independent of the length of the output: each token is
     detokenised alone (``StreamDecoder``: incomplete UTF-8 carried over) and the stop strings are
@@ -412,16 +414,28 @@ class Scheduler:
             self._release(j)
         if not self.prefilling:
             return 0
-        budget = self.ubatch if any(j.decoding for j in self.active.values()) else self.batch
+        # Prompts that finish inside the batch (``batch`` tokens, llama-server's n_batch) are
+        # taken whole: a burst of new requests all start decoding within an iteration or two.  A
+        # prompt that does not fit is cut into chunks — of at most ``ubatch`` tokens while other
+        # sequences decode, so a long prompt stalls the running streams one ubatch at a time.
+        decoding = any(j.decoding for j in self.active.values())
+        budget = self.batch
         work = []
         for job in self.prefilling:
-            n = min(budget, len(job.ids) - job.pos)
-            if n <= 0:
+            rem = len(job.ids) - job.pos
+            if rem <= 0:
                 break
-            work.append((job, n))
-            budget -= n
-            if budget == 0:
-                break
+            if rem <= budget:
+                work.append((job, rem))
+                budget -= rem
+                if budget == 0:
+                    break
+                continue
+            if not decoding:
+                work.append((job, budget))
+            elif not work:
+                work.append((job, min(budget, self.ubatch)))
+            break
         t0 = time.perf_counter()
         many = getattr(self.engine, "prefill_many", None) if self.prompt_batch else None
         results = {}

@@ -472,6 +472,89 @@ w4a_splitk_finalize_resid(const uint16_t* __restrict__ ws, int S, long slice_str
   xp[1] = x1;
 }
 
+// The same with the next RMSNorm fused (the LLM prefill: o_proj → ffn_norm, ffn_down → the next
+// layer's attn_norm): one workgroup per row (N % 8 == 0, N <= 8192), 8-column chunks tid + 256 u.
+// x is updated exactly as w4a_splitk_finalize_resid does, and y = fp16(x · r · w) with the sum of
+// squares in rmsnorm_f16's order (llm_prefill.hip), so the bits equal the two-pass path.
+template <bool H>
+__global__ void __launch_bounds__(256)
+w4a_splitk_finalize_resid_norm(const uint16_t* __restrict__ ws, int S, long slice_stride, int N,
+                               float* __restrict__ x, int ldx, const uint16_t* __restrict__ bias,
+                               const float* __restrict__ nw, float eps, uint16_t* __restrict__ y,
+                               int ldy) {
+  constexpr int CH = 4;
+  __shared__ float red[4];
+  const int m = blockIdx.x, tid = threadIdx.x, nch = N >> 3;
+  float* xr = x + (long)m * ldx;
+  float e[CH][8];
+#pragma unroll
+  for (int u = 0; u < CH; ++u) {
+    const int c = tid + 256 * u;
+    if (c >= nch) break;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < S; ++s) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(ws + s * slice_stride + (long)m * N + c * 8);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[2 * q] += w4a_lo<H>(v[q]);
+        acc[2 * q + 1] += w4a_hi<H>(v[q]);
+      }
+    }
+    if (bias) {
+      const u32x4 b = *reinterpret_cast<const u32x4*>(bias + c * 8);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[2 * q] += w4a_lo<H>(b[q]);
+        acc[2 * q + 1] += w4a_hi<H>(b[q]);
+      }
+    }
+    f32x4* xp = reinterpret_cast<f32x4*>(xr + c * 8);
+    f32x4 x0 = xp[0], x1 = xp[1];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      x0[q] += acc[q];
+      x1[q] += acc[4 + q];
+    }
+    xp[0] = x0;
+    xp[1] = x1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      e[u][q] = x0[q];
+      e[u][4 + q] = x1[q];
+    }
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int u = 0; u < CH; ++u)
+    if (tid + 256 * u < nch) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss = __fmaf_rn(e[u][i], e[u][i], ss);
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  const float r = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)N + eps);
+  uint16_t* yr = y + (long)m * ldy;
+#pragma unroll
+  for (int u = 0; u < CH; ++u) {
+    const int c = tid + 256 * u;
+    if (c >= nch) break;
+    const f32x4 wa = *reinterpret_cast<const f32x4*>(nw + c * 8);
+    const f32x4 wb = *reinterpret_cast<const f32x4*>(nw + c * 8 + 4);
+    const float ww[8] = {wa[0], wa[1], wa[2], wa[3], wb[0], wb[1], wb[2], wb[3]};
+    u32x4 pk;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const _Float16 lo = (_Float16)(e[u][2 * i] * r * ww[2 * i]);
+      const _Float16 hi = (_Float16)(e[u][2 * i + 1] * r * ww[2 * i + 1]);
+      pk[i] = (uint32_t)__builtin_bit_cast(uint16_t, lo) |
+              ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+    }
+    *reinterpret_cast<u32x4*>(yr + c * 8) = pk;
+  }
+}
+
 // The hybrid's plan: na = columns run as whole waves (a multiple of 256, possibly 0 — then the
 // plain kernel is the better choice) and ks = K slices per tile of the rest; ks = 1: no hybrid.
 extern "C" void amdk8s_gemm_w4a_hybrid_plan(int M, int N, int K, int cus, int* na, int* ks) {
@@ -569,9 +652,12 @@ extern "C" void amdk8s_gemm_w4a_splitk_plan(int M, int N, int K, int cus, int* k
   if (s >= 2) *ks = s;
 }
 
+// norm_w (epi 3 only, may be null): also y[m] = fp16(rmsnorm(x[m]) · norm_w) of the updated rows
+// (y [M][ldy], N <= 8192), the prefill's next RMSNorm in the same pass.
 extern "C" int amdk8s_gemm_w4a_splitk(int epi, int dtype, const void* A, const void* B, void* C,
                                       const void* bias, float* x, int M, int N, int K, int lda,
                                       int ldb, int ldc, int ldx, int ks, void* ws, long ws_elems,
+                                      const float* norm_w, float eps, void* y, int ldy,
                                       hipStream_t stream) {
   if (epi != kEpiNone && epi != kEpiBias && epi != kEpiResid && epi != kEpiSwiGLU)
     return (int)hipErrorInvalidValue;
@@ -583,7 +669,11 @@ extern "C" int amdk8s_gemm_w4a_splitk(int epi, int dtype, const void* A, const v
     return (int)hipErrorInvalidValue;
   if (epi == kEpiResid) {
     if (!x || ldx % 4 || ldx < N || ((uintptr_t)x & 15)) return (int)hipErrorInvalidValue;
+    if (norm_w && (dtype != 0 || N > 8192 || !y || ldy % 8 || ldy < N ||
+                   (((uintptr_t)y | (uintptr_t)norm_w) & 15)))
+      return (int)hipErrorInvalidValue;
   } else {
+    if (norm_w) return (int)hipErrorInvalidValue;
     const int w = epi == kEpiSwiGLU ? N / 2 : N;
     if (!C || ldc % 8 || ldc < w || ((uintptr_t)C & 15)) return (int)hipErrorInvalidValue;
     if (epi == kEpiBias && !bias) return (int)hipErrorInvalidValue;
@@ -607,7 +697,10 @@ extern "C" int amdk8s_gemm_w4a_splitk(int epi, int dtype, const void* A, const v
   uint16_t* c = (uint16_t*)C;
   const unsigned g8 = (unsigned)(((long)M * (N / 8) + 255) / 256);
   const unsigned g16 = (unsigned)(((long)M * (N / 16) + 255) / 256);
-  if (epi == kEpiResid) {
+  if (epi == kEpiResid && norm_w) {
+    hipLaunchKernelGGL(w4a_splitk_finalize_resid_norm<true>, dim3(M), dim3(256), 0, stream, w, ks,
+                       stride, N, x, ldx, bs, norm_w, eps, (uint16_t*)y, ldy);
+  } else if (epi == kEpiResid) {
     if (dtype == 0)
       hipLaunchKernelGGL(w4a_splitk_finalize_resid<true>, dim3(g8), dim3(256), 0, stream, w, ks,
                          stride, M, N, x, ldx, bs);

@@ -48,6 +48,19 @@ constexpr int kBuf = 2 * kTile;           // K + V
 constexpr int kLds = 2 * kBuf;            // double buffered: 64 KiB
 constexpr int kKsteps = kD / 16;
 constexpr int kDblk = kD / 32;
+// A/B knobs (build-time): the tile loop unrolled by two (constant buffer parity, so every LDS
+// read is a hoisted register + an immediate), and the first score MFMA with a zero C operand
+// instead of zeroed accumulators.  Measured with tools/debug/attn_ab.sh (profiles/r06/attn_ab/):
+// the unroll costs 4-6 % (8192 @ 0 728 vs 689-697 us, 512 @ 31488 316 vs 297-300 us: it cuts
+// ~50 VALU per tile, but the loop is not issue-bound — PMC: MFMA busy 29 %, 7.6 VALU per MFMA,
+// profiles/r06/prefill_attn_pmc_8192.txt), the zero C is neutral; the hoisted offsets alone
+// (default) are within 1 % of the round-6 loop.
+#ifndef AMDK8S_PA_UNROLL2
+#define AMDK8S_PA_UNROLL2 0
+#endif
+#ifndef AMDK8S_PA_ZEROC
+#define AMDK8S_PA_ZEROC 0
+#endif
 constexpr float kNoMax = -1e30f;          // finite "no score yet" (a fully masked row stays NaN-free)
 
 __device__ __forceinline__ int kswz(int row, int ch) { return ch ^ (row & 15); }
@@ -186,19 +199,25 @@ __global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) 
     }
   };
 
-  const int kofs = r * kRB;
   const int g16 = lane >> 4, qq = (lane & 15) >> 2, pl = lane & 3;
   const int vcol_chunk = 2 * (g16 & 1) + (pl >> 1);
   const int vsub = 8 * (pl & 1);
   const int vrow = 4 * h + qq;
   const float thr = 8.f / a.c;
+  // per-lane LDS offsets, hoisted out of the tile loop (the XOR swizzles do not distribute over
+  // the per-step offsets, so the compiler recomputed them every tile): K row r, chunk 2 st + h;
+  // V rows 16 ks + vrow (+ 8), whose swizzle (row & 3) does not depend on ks, column block db.
+  // The buffer parity, b, ks and the + 8 rows are then immediate offsets of the ds_reads.
+  int koff[kKsteps], voff[kDblk];
+#pragma unroll
+  for (int st = 0; st < kKsteps; ++st) koff[st] = r * kRB + (kswz(r, 2 * st + h) << 4);
+#pragma unroll
+  for (int db = 0; db < kDblk; ++db)
+    voff[db] = vrow * kRB + vsub + ((4 * (db ^ (vrow & 3)) + vcol_chunk) << 4);
 
-  load_tile(t0 * kKeys);
-  store_tile(0);
-  __syncthreads();
-  for (int kt = t0; kt < t1; ++kt) {
+  // one key tile from LDS buffer BUF (a compile-time parity: the loop below is unrolled by two)
+  auto tile = [&](const int kt, const int buf) {
     const int kbase = kt * kKeys;
-    const int buf = (kt - t0) & 1;
     const char* kl = lds + buf * kBuf;
     const char* vl = kl + kTile;
     if (kt + 1 < t1) load_tile(kbase + kKeys);
@@ -207,12 +226,18 @@ __global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) 
       f32x16 s[2];
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
+#if AMDK8S_PA_ZEROC
+        const f32x16 z = {};
+        s[b] = mfma32<BF16>(*reinterpret_cast<const s16x8*>(kl + b * 32 * kRB + koff[0]), qf[0], z);
+        constexpr int st0 = 1;
+#else
 #pragma unroll
         for (int i = 0; i < 16; ++i) s[b][i] = 0.f;
+        constexpr int st0 = 0;
+#endif
 #pragma unroll
-        for (int st = 0; st < kKsteps; ++st) {
-          const s16x8 kf = *reinterpret_cast<const s16x8*>(
-              kl + b * 32 * kRB + kofs + (kswz(r, 2 * st + h) << 4));
+        for (int st = st0; st < kKsteps; ++st) {
+          const s16x8 kf = *reinterpret_cast<const s16x8*>(kl + b * 32 * kRB + koff[st]);
           s[b] = mfma32<BF16>(kf, qf[st], s[b]);
         }
       }
@@ -257,14 +282,11 @@ __global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) 
 
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const int r0 = 16 * ks + vrow, r1 = r0 + 8;
-        const char* v0 = vl + r0 * kRB + vsub;
-        const char* v1 = vl + r1 * kRB + vsub;
 #pragma unroll
         for (int db = 0; db < kDblk; ++db) {
-          const int c0 = vswz(r0, 4 * db + vcol_chunk), c1 = vswz(r1, 4 * db + vcol_chunk);
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(v0 + (c0 << 4)));
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(v1 + (c1 << 4)));
+          const char* v0 = vl + 16 * ks * kRB + voff[db];
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)v0);
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(v0 + 8 * kRB));
           const s16x8 vf = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           o[db] = mfma32<BF16>(vf, pf[ks], o[db]);
         }
@@ -273,7 +295,19 @@ __global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) 
 
     if (kt + 1 < t1) store_tile(buf ^ 1);
     __syncthreads();
+  };
+
+  load_tile(t0 * kKeys);
+  store_tile(0);
+  __syncthreads();
+#if AMDK8S_PA_UNROLL2
+  for (int kt = t0; kt < t1; kt += 2) {      // the buffer parity a constant in each half
+    tile(kt, 0);
+    if (kt + 1 < t1) tile(kt + 1, 1);
   }
+#else
+  for (int kt = t0; kt < t1; ++kt) tile(kt, (kt - t0) & 1);
+#endif
 
   // epilogue: lane holds O[row][32db + 8(i>>2) + 4h + (i&3)] (unnormalised), its half of the sum
   const float lt = l + __shfl_xor(l, 32, 64);

@@ -54,7 +54,8 @@ def _lib():
             lib.amdk8s_gemm_w4a_splitk_plan.argtypes = [ci, ci, ci, ci, ctypes.POINTER(ci)]
             lib.amdk8s_gemm_w4a_splitk_plan.restype = None
             lib.amdk8s_gemm_w4a_splitk.argtypes = [ci, ci, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci,
-                                                   ci, ci, ci, vp, ctypes.c_long, vp]
+                                                   ci, ci, ci, vp, ctypes.c_long, vp,
+                                                   ctypes.c_float, vp, ci, vp]
             lib.amdk8s_gemm_w4a_splitk.restype = ci
             lib.amdk8s_gemm_epi_set_tile.argtypes = [ci]
             lib.amdk8s_gemm_epi_set_tile.restype = None
@@ -241,9 +242,10 @@ def splitk_plan(m: int, n: int, k: int, cus: int = 256) -> int:
     return ks.value
 
 
-def _w4a_splitk(epi: int, x2, w, b, out=None, res=None) -> bool:
+def _w4a_splitk(epi: int, x2, w, b, out=None, res=None, norm=None) -> bool:
     """The split-K w4a form with epilogue ``epi`` (0 store, 1 + bias, 3 += res fp32, 4 SwiGLU);
-    False when it does not apply (dtype, layout, or the planner keeps the shape elsewhere)."""
+    False when it does not apply (dtype, layout, or the planner keeps the shape elsewhere).
+    ``norm`` (epi 3): (weight fp32 [N], eps, y fp16 [M, N]) — y = RMSNorm of the updated rows."""
     if (not _W4A_SPLITK or _WIDE != "w4a" or x2.dtype != torch.float16 or w.dtype != x2.dtype
             or _PINS["tile"] >= 0 or _PINS["splits"] >= 0):
         return False
@@ -254,6 +256,11 @@ def _w4a_splitk(epi: int, x2, w, b, out=None, res=None) -> bool:
         return False
     if out is not None and (out.stride(-1) != 1 or out.stride(0) % 8):
         return False
+    nw, eps, y = norm if norm is not None else (None, 0.0, None)
+    if norm is not None and (n > 8192 or nw.dtype != torch.float32 or not nw.is_contiguous()
+                             or y.dtype != torch.float16 or y.stride(-1) != 1 or y.stride(0) % 8
+                             or not _aligned16(nw, y)):
+        return False
     ks = splitk_plan(m, n, k, _cus(x2.device))
     if ks <= 1:
         return False
@@ -261,7 +268,8 @@ def _w4a_splitk(epi: int, x2, w, b, out=None, res=None) -> bool:
     rc = _lib().amdk8s_gemm_w4a_splitk(
         epi, _DT[x2.dtype], x2.data_ptr(), w.data_ptr(), _ptr(out), _ptr(b), _ptr(res), m, n, k,
         x2.stride(0), w.stride(0), out.stride(0) if out is not None else 0, n, ks, ws.data_ptr(),
-        ws.numel(), _stream(x2))
+        ws.numel(), _ptr(nw), float(eps), _ptr(y), y.stride(0) if y is not None else 0,
+        _stream(x2))
     if rc != 0:
         raise RuntimeError(f"amdk8s_gemm_w4a_splitk failed (rc={rc}, M={m} N={n} K={k}, epi={epi})")
     return True
@@ -344,6 +352,22 @@ def linear_residual_(res: torch.Tensor, x: torch.Tensor, w: torch.Tensor,
     elif gate is not None or not _w4a_splitk(3, x2, w, bb, None, res):
         _run(EPI_RESID, x2, w, bb, None, res, gate, rows_per_gate, gstride, 0, n)
     return res
+
+
+def linear_residual_norm_(res: torch.Tensor, x: torch.Tensor, w: torch.Tensor,
+                          norm_w: torch.Tensor, eps: float, y: torch.Tensor) -> bool:
+    """``res += x·wᵀ`` and ``y = fp16(RMSNorm(res) · norm_w)`` in one GEMM + one finalize pass,
+    when the shape runs on the split-K 256×256 form (the LLM prefill chunk's o_proj and
+    ffn_down).  The bits are those of ``linear_residual_`` followed by the rmsnorm_f16 kernel.
+    Returns False without doing anything when it does not apply (the caller runs the two)."""
+    if res.dtype != torch.float32 or not res.is_contiguous() or res.shape[-1] != w.shape[0]:
+        return False
+    x2 = _rows(x)
+    if res.numel() != x2.shape[0] * w.shape[0] or y.shape != res.shape:
+        return False
+    if use_w4a(x2.shape[0], w.shape[0], x2.shape[1], x.dtype):
+        return False
+    return _w4a_splitk(3, x2, w, None, None, res, (norm_w, eps, y))
 
 
 def linear_add(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], r: torch.Tensor,

@@ -366,3 +366,33 @@ def test_w4a_split_k_every_tile(GE, m, n, k, epi):
     finally:
         GE.set_tile(-1)
     torch.testing.assert_close(y2.float(), ref, rtol=5e-3, atol=5e-3)
+
+
+@pytest.mark.parametrize("k", [3584, 18944])
+def test_w4a_split_k_residual_with_fused_rmsnorm(GE, k):
+    """The prefill chunk's o_proj / ffn_down: the split-K finalize adds the product into the fp32
+    residual stream and writes the next RMSNorm's fp16 rows in the same pass — the same bits as
+    the residual GEMM followed by rmsnorm_f16."""
+    from k8s_nvidia_gpus_amd.ops import llm_kernels as LK
+
+    dev = torch.device("cuda")
+    m, n = 512, 3584
+    g = torch.Generator(device=dev).manual_seed(k)
+    x = torch.randn(m, k, generator=g, device=dev).half()
+    w = (torch.randn(n, k, generator=g, device=dev) / k ** 0.5).half()
+    res = torch.randn(m, n, generator=g, device=dev)
+    nw = torch.rand(n, generator=g, device=dev) + 0.5
+    r1, y1 = res.clone(), torch.empty(m, n, device=dev, dtype=torch.float16)
+    assert GE.linear_residual_norm_(r1, x, w, nw, 1e-6, y1)
+    r2, y2 = res.clone(), torch.empty(m, n, device=dev, dtype=torch.float16)
+    GE.linear_residual_(r2, x, w)
+    LK.rmsnorm_f16(r2, nw, 1e-6, y2)
+    assert torch.equal(r1, r2)
+    assert torch.equal(y1, y2)
+    want = res + _ref(x, w, None)
+    torch.testing.assert_close(r1, want, rtol=5e-3, atol=5e-3)
+    # a shape the split form does not take: nothing done, the caller runs the two passes
+    big = torch.randn(4096, k, generator=g, device=dev).half()
+    rb = torch.zeros(4096, n, device=dev)
+    assert not GE.linear_residual_norm_(rb, big, w, nw, 1e-6, torch.empty_like(rb).half())
+    assert int(rb.abs().sum()) == 0

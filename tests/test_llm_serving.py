@@ -337,3 +337,53 @@ def test_prefill_many_equals_one_by_one_and_validates(tiny_model):
         eng.prefill_many([(a, 2, 0), ([], 3, 0)])
     with pytest.raises(ValueError):
         eng.prefill_many([(a, 2, 0), (b, 3, eng.max_ctx - 1)])
+
+
+def test_short_prompts_fitting_the_batch_are_taken_whole_while_decoding(tiny_model):
+    """While a sequence decodes, prompts whose rest fits the batch budget are prefilled whole in
+    one iteration (a burst of requests starts decoding together); a prompt that does not fit is
+    still cut into ubatch chunks."""
+    from k8s_nvidia_gpus_amd.models.llm import server as S
+
+    eng, tok = _load(tiny_model)
+    calls = []
+    real_many, real_prefill = eng.prefill_many, eng.prefill
+
+    def prefill_many(items):
+        calls.append([len(ids) for ids, _, _ in items])
+        return real_many(items)
+
+    def prefill(ids, slot, start=0):
+        calls.append([len(ids)])
+        return real_prefill(ids, slot, start)
+
+    real_decode = eng.decode
+
+    def decode(toks, pos, slots):
+        time.sleep(0.002)                  # keep the first sequence decoding throughout
+        return real_decode(toks, pos, slots)
+
+    eng.prefill_many, eng.prefill, eng.decode = prefill_many, prefill, decode
+    sched = S.Scheduler(eng, tok, parallel=4, ubatch=8, batch=64)
+    try:
+        a = sched.submit(S.Job(ids=tok.encode("hello"), max_new=150, ignore_eos=True))
+        while not a.gen:
+            time.sleep(0.001)
+        n0 = len(calls)
+        short = [tok.encode(t) for t in ("a cozy cabin in the woods by a river",
+                                         "the quick brown fox jumps over it")]
+        assert all(8 < len(ids) <= 32 for ids in short)
+        jobs = [sched.submit(S.Job(ids=ids, max_new=3, ignore_eos=True)) for ids in short]
+        longer = tok.encode("the lazy dog sleeps in the sun all day long. " * 6)
+        assert len(longer) > 64
+        c = sched.submit(S.Job(ids=longer, max_new=3, ignore_eos=True))
+        for j in jobs + [c]:
+            _wait(j)
+        assert not a.finish                      # it decoded all along
+        _wait(a)
+    finally:
+        sched.close()
+    later = [n for batch in calls[n0:] for n in batch]
+    assert len(short[0]) in later and len(short[1]) in later       # each taken whole
+    # the long one in ubatch chunks until its rest fits the batch (then that rest whole)
+    assert 8 * sum(1 for n in later if n == 8) >= len(longer) - 64

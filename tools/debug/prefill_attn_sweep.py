@@ -42,10 +42,13 @@ def main(argv):
         out = torch.empty(H, P, d, device=dev, dtype=torch.float16)
         auto = LK.prefill_attn_plan(P, start, H, Hkv)
         flop = 4 * H * d * P * (start + (P + 1) / 2)
-        us = timed(lambda: LK.prefill_attn(q, k, v, out, start, 1 / math.sqrt(d)))
+        us = timed(lambda: LK.prefill_attn(q, k, v, out, start, 1 / math.sqrt(d)),
+                   iters=int(os.environ.get("SWEEP_ITERS", "20")))
         print(json.dumps({"P": P, "start": start, "plan": "auto", **auto, "us": round(us, 1),
                           "tflops": round(flop / us / 1e6, 1)}), flush=True)
         ntiles = (end + 63) // 64
+        if os.environ.get("SWEEP_AUTO_ONLY") == "1":
+            continue
         for nw in (4, 8):
             for ns in (1, 2, 3, 4, 6, 8, 12, 16, 24):
                 if ns > ntiles:
