@@ -414,10 +414,11 @@ class Scheduler:
             self._release(j)
         if not self.prefilling:
             return 0
-        # Prompts that finish inside the batch (``batch`` tokens, llama-server's n_batch) are
-        # taken whole: a burst of new requests all start decoding within an iteration or two.  A
-        # prompt that does not fit is cut into chunks — of at most ``ubatch`` tokens while other
-        # sequences decode, so a long prompt stalls the running streams one ubatch at a time.
+        # Prompts that fit the batch (``batch`` tokens, llama-server's n_batch) whole are taken
+        # whole: a burst of new requests all start decoding within an iteration or two.  A prompt
+        # that does not fit is cut into chunks — of at most ``ubatch`` tokens while other
+        # sequences decode, down to its last one (its tail is not taken whole either), so a long
+        # prompt stalls the running streams one ubatch at a time.
         decoding = any(j.decoding for j in self.active.values())
         budget = self.batch
         work = []
@@ -425,16 +426,16 @@ class Scheduler:
             rem = len(job.ids) - job.pos
             if rem <= 0:
                 break
-            if rem <= budget:
+            if rem <= budget and (not decoding or job.pos == job.n_cached):
                 work.append((job, rem))
                 budget -= rem
                 if budget == 0:
                     break
                 continue
             if not decoding:
-                work.append((job, budget))
+                work.append((job, min(rem, budget)))
             elif not work:
-                work.append((job, min(budget, self.ubatch)))
+                work.append((job, min(rem, budget, self.ubatch)))
             break
         t0 = time.perf_counter()
         many = getattr(self.engine, "prefill_many", None) if self.prompt_batch else None

@@ -61,6 +61,11 @@ constexpr int kDblk = kD / 32;
 #ifndef AMDK8S_PA_ZEROC
 #define AMDK8S_PA_ZEROC 0
 #endif
+// write the next tile into LDS after the barrier (with the tile after it in flight) instead of
+// before it
+#ifndef AMDK8S_PA_WAB
+#define AMDK8S_PA_WAB 0
+#endif
 constexpr float kNoMax = -1e30f;          // finite "no score yet" (a fully masked row stays NaN-free)
 
 __device__ __forceinline__ int kswz(int row, int ch) { return ch ^ (row & 15); }
@@ -220,7 +225,15 @@ __global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) 
     const int kbase = kt * kKeys;
     const char* kl = lds + buf * kBuf;
     const char* vl = kl + kTile;
+#if AMDK8S_PA_WAB
+    // write-after-barrier staging: tile kt + 1 (in registers since the previous tile) into the
+    // buffer every wave finished reading before the barrier that ended the previous tile, then
+    // tile kt + 2's loads — their latency spans this tile's maths
+    if (kt + 1 < t1) store_tile(buf ^ 1);
+    if (kt + 2 < t1) load_tile(kbase + 2 * kKeys);
+#else
     if (kt + 1 < t1) load_tile(kbase + kKeys);
+#endif
 
     if (wave_valid && kbase <= a.start + pw_hi) {
       f32x16 s[2];
@@ -293,12 +306,17 @@ __global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) 
       }
     }
 
+#if !AMDK8S_PA_WAB
     if (kt + 1 < t1) store_tile(buf ^ 1);
+#endif
     __syncthreads();
   };
 
   load_tile(t0 * kKeys);
   store_tile(0);
+#if AMDK8S_PA_WAB
+  if (t0 + 1 < t1) load_tile((t0 + 1) * kKeys);
+#endif
   __syncthreads();
 #if AMDK8S_PA_UNROLL2
   for (int kt = t0; kt < t1; kt += 2) {      // the buffer parity a constant in each half

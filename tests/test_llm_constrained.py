@@ -277,9 +277,11 @@ def test_batched_prompts_add_one_batch_time_to_prefill_seconds(tiny_model):
     m = sched.metrics
     assert slow.calls == 1 and m["prefill_batches_total"] == 1
     assert m["prefill_chunks_total"] == 3
-    assert 0.2 <= m["prefill_seconds_total"] < 0.35, m        # once, not 3 x 0.2
+    assert 0.2 <= m["prefill_seconds_total"] < 0.5, m         # once, not 3 x 0.2
     shares = [j.t_prefill for j in jobs]
-    assert all(s < 0.2 for s in shares) and sum(shares) == pytest.approx(0.2, abs=0.08)
+    # token shares of that one batch time (so each below it, and summing to it)
+    assert all(s < m["prefill_seconds_total"] for s in shares)
+    assert sum(shares) == pytest.approx(m["prefill_seconds_total"], rel=1e-6)
 
 
 def test_no_prompt_batch_prefills_each_prompt_alone(tiny_model):

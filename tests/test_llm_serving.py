@@ -385,5 +385,5 @@ def test_short_prompts_fitting_the_batch_are_taken_whole_while_decoding(tiny_mod
         sched.close()
     later = [n for batch in calls[n0:] for n in batch]
     assert len(short[0]) in later and len(short[1]) in later       # each taken whole
-    # the long one in ubatch chunks until its rest fits the batch (then that rest whole)
-    assert 8 * sum(1 for n in later if n == 8) >= len(longer) - 64
+    # the long one in ubatch chunks, down to its last one
+    assert 8 * sum(1 for n in later if n == 8) >= len(longer) - 8
