@@ -641,9 +641,19 @@ extern "C" int amdk8s_gemm_w4a_hybrid(int epi, int dtype, const void* A, const v
 // range of its K-tiles into a 16-bit partial tile (fp16 only, like the hybrid: at most 8 roundings
 // at 11 mantissa bits), and a finalize pass sums the slices in fp32 in slice order and applies the
 // epilogue (store / + bias / += into the fp32 residual stream / SwiGLU).
+// A/B sweeps: amdk8s_gemm_w4a_splitk_set_ks(k) pins the slice count of every shape the planner
+// takes (k >= 2, capped at the K-tile count), 0 = the planner's.
+static int g_splitk_pin = 0;
+extern "C" void amdk8s_gemm_w4a_splitk_set_ks(int k) { g_splitk_pin = k > 0 ? k : 0; }
+
 extern "C" void amdk8s_gemm_w4a_splitk_plan(int M, int N, int K, int cus, int* ks) {
   *ks = 1;
   if (M < 256 || N % BN || K % BK || cus <= 0) return;
+  if (g_splitk_pin >= 2) {
+    const int tiles = ((M + BM - 1) / BM) * (N / BN);
+    if (tiles * 4 < cus * 3) *ks = g_splitk_pin < K / BK ? g_splitk_pin : K / BK;
+    return;
+  }
   const int tiles = ((M + BM - 1) / BM) * (N / BN), T = K / BK;
   if (tiles * 4 >= cus * 3) return;               // the plain grid fills >= 3/4 of the chip
   int s = cus / tiles;

@@ -51,6 +51,8 @@ def _lib():
             lib.amdk8s_gemm_w4a_hybrid.argtypes = [ci, ci, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci,
                                                    ci, ci, vp, ctypes.c_long, vp]
             lib.amdk8s_gemm_w4a_hybrid.restype = ci
+            lib.amdk8s_gemm_w4a_splitk_set_ks.argtypes = [ci]
+            lib.amdk8s_gemm_w4a_splitk_set_ks.restype = None
             lib.amdk8s_gemm_w4a_splitk_plan.argtypes = [ci, ci, ci, ci, ctypes.POINTER(ci)]
             lib.amdk8s_gemm_w4a_splitk_plan.restype = None
             lib.amdk8s_gemm_w4a_splitk.argtypes = [ci, ci, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci,
@@ -233,6 +235,11 @@ def _aligned16(*ts) -> bool:
 # runs with every tile split over K (amdk8s_gemm_w4a_splitk; fp16 only, like the hybrid)
 # instead of on the wave-grid family; AMDK8S_GEMM_W4A_SPLITK=0 turns it off (A/B runs).
 _W4A_SPLITK = os.environ.get("AMDK8S_GEMM_W4A_SPLITK", "1") != "0"
+
+
+def set_w4a_splitk(ks: int) -> None:
+    """Pin the split-K w4a form's slice count (A/B sweeps; 0 = the planner)."""
+    _lib().amdk8s_gemm_w4a_splitk_set_ks(int(ks))
 
 
 def splitk_plan(m: int, n: int, k: int, cus: int = 256) -> int:

@@ -38,6 +38,8 @@ def main() -> int:
     ap.add_argument("--quick", action="store_true", help="planner / w4a / torch only (no sweep)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default="", help="comma-separated GEMM names (qkv,o,gate_up,down)")
+    ap.add_argument("--splitk-sweep", action="store_true",
+                    help="time the split-K w4a form at every slice count 2..8")
     ap.add_argument("--cold", action="store_true",
                     help="cycle through weight copies totalling > 512 MB, so every call streams its "
                          "weights from HBM as in a prefill (not from the Infinity Cache)")
@@ -74,6 +76,11 @@ def main() -> int:
             GE._HYBRID = False
             rec("w4a plain (no partial-wave split)", bench(run))
             GE._HYBRID = True
+        if GE.splitk_plan(m, n, k) > 1 and a.splitk_sweep:
+            for ks in (2, 3, 4, 5, 6, 7, 8):
+                GE.set_w4a_splitk(ks)
+                rec(f"split-K w4a ks={GE.splitk_plan(m, n, k)}", bench(run))
+            GE.set_w4a_splitk(0)
         if GE.splitk_plan(m, n, k) > 1:
             GE._W4A_SPLITK = False
             rec(f"wave-grid plan={GE.plan(m, n, k)} (split-K w4a off)", bench(run))
