@@ -659,7 +659,10 @@ extern "C" void amdk8s_gemm_w4a_splitk_plan(int M, int N, int K, int cus, int* k
   int s = cus / tiles;
   s = s < T / 6 ? s : T / 6;                      // >= 6 K-tiles per slice (ring fill + drain)
   s = s < 8 ? s : 8;
-  if (s >= 2) *ks = s;
+  // and only when the split grid fills >= 3/4 of the chip: at 256 tokens o_proj / ffn_down (14
+  // tiles x 8 = 112 workgroups) lost to the wave-grid family, 24.6 / 60.4 vs 22.5 / 54.6 us
+  // (profiles/r06/prefill_gemm_256_splitk_sweep.log)
+  if (s >= 2 && tiles * s * 4 >= cus * 3) *ks = s;
 }
 
 // norm_w (epi 3 only, may be null): also y[m] = fp16(rmsnorm(x[m]) · norm_w) of the updated rows

@@ -113,7 +113,9 @@ def test_use_w4a_routing():
     ((512, 4608, 3584), 7),      # LLM prefill q|k|v chunk: 36 tiles x 7 slices
     ((512, 3584, 3584), 8),      # o_proj: 28 x 8
     ((512, 3584, 18944), 8),     # ffn_down: 28 x 8
-    ((300, 1536, 1536), 4),      # 12 tiles, 24 K-tiles: >= 6 per slice
+    ((300, 1536, 1536), 1),      # 12 tiles x 4 slices: the split grid would not fill the chip
+    ((700, 3584, 3584), 6),      # 42 tiles (M tail) x 6
+    ((256, 3584, 18944), 1),     # 14 tiles x 8 = 112 workgroups: the wave-grid family wins
     ((8192, 1536, 1536), 1),     # 192 tiles fill 3/4 of the chip: plain
     ((512, 37888, 3584), 1),     # gate|up: 296 tiles (the hybrid's case)
     ((128, 4608, 3584), 1),      # below one 256-row panel: the wave-grid family
@@ -121,5 +123,6 @@ def test_use_w4a_routing():
 ])
 def test_w4a_splitk_plan(ge, shape, ks):
     """Split-K over every 256×256 tile (amdk8s_gemm_w4a_splitk_plan): slices fill the chip, at
-    most 8 (16-bit partial tiles), at least 6 K-tiles each, only when the plain grid is < 3/4."""
+    most 8 (16-bit partial tiles), at least 6 K-tiles each, only when the plain grid is < 3/4 of
+    the chip and the split grid >= 3/4."""
     assert ge.splitk_plan(*shape) == ks
