@@ -78,6 +78,25 @@ class StepBuffers:
     meta: torch.Tensor = None        # int32 [3, T] on the GPU: tok / pos / slot are its rows
     host: torch.Tensor = None        # pinned staging copy of meta
     host_evt: torch.cuda.Event = None
+    ids_host: List[torch.Tensor] = None   # two pinned [T] landing buffers of decode_greedy_async
+    ids_flip: int = 0
+
+
+class GreedyStep:
+    """An enqueued greedy decode step (``Engine.decode_greedy_async``): ``result()`` waits for its
+    token ids.  ``chainable`` is set when the next step may take its tokens straight from this
+    one's device buffer (same batch size, one engine call)."""
+
+    def __init__(self, value: Optional[List[int]] = None, host: Optional[torch.Tensor] = None,
+                 event: Optional[torch.cuda.Event] = None, buffers: Optional["StepBuffers"] = None):
+        self._value, self._host, self._event, self.buffers = value, host, event, buffers
+        self.chainable = buffers is not None
+
+    def result(self) -> List[int]:
+        if self._value is None:
+            self._event.synchronize()
+            self._value = self._host.tolist()
+        return self._value
 
 
 class Engine:
@@ -415,6 +434,9 @@ class Engine:
             b = StepBuffers(
                 T=T, tok=meta[0], pos=meta[1], slot=meta[2], meta=meta,
                 host=torch.zeros(3, T, dtype=torch.int32).pin_memory(),
+                # decode_greedy_async's landing buffers, pinned here (at graph capture) rather than
+                # at a request's first step
+                ids_host=[torch.zeros(T, dtype=torch.int32).pin_memory() for _ in range(2)],
                 ids=torch.zeros(T, dtype=torch.int32, device=dev),
                 h=torch.zeros(T, c.dim, **f32),
                 x8=torch.zeros(T, kmax, dtype=torch.int8, device=dev),
@@ -504,17 +526,25 @@ class Engine:
                      **pro)
             off += w.n
 
-    def _decode_native(self, tokens: Sequence[int], positions: Sequence[int],
+    def _decode_native(self, tokens: Optional[Sequence[int]], positions: Sequence[int],
                        slots: Sequence[int], greedy: bool = False) -> torch.Tensor:
-        T = len(tokens)
+        """``tokens`` None: the tokens are the previous greedy step's ids of this batch size,
+        still on the GPU (a chained step, ``decode_greedy_async``)."""
+        T = len(positions)
         b = self._buffers(T)
         # one H2D copy per step from a pinned staging row (three synchronous pageable copies cost
         # ~3 x 10 us of idle GPU per token); the event guards the row against being rewritten
         # before the previous step's copy has read it
         if b.host_evt is not None:
             b.host_evt.synchronize()
-        b.host.copy_(torch.tensor([list(tokens), list(positions), list(slots)], dtype=torch.int32))
-        b.meta.copy_(b.host, non_blocking=True)
+        if tokens is None:
+            b.host[1:].copy_(torch.tensor([list(positions), list(slots)], dtype=torch.int32))
+            b.meta[1:].copy_(b.host[1:], non_blocking=True)
+            b.meta[0].copy_(b.ids)                      # device to device, in stream order
+        else:
+            b.host.copy_(torch.tensor([list(tokens), list(positions), list(slots)],
+                                      dtype=torch.int32))
+            b.meta.copy_(b.host, non_blocking=True)
         if b.host_evt is None:
             b.host_evt = torch.cuda.Event()
         b.host_evt.record()
@@ -592,6 +622,40 @@ class Engine:
             out += self._decode_native(tokens[i:i + self.max_T], positions[i:i + self.max_T],
                                        slots[i:i + self.max_T], greedy=True).tolist()
         return out
+
+    def decode_greedy_async(self, tokens: Optional[Sequence[int]], positions: Sequence[int],
+                            slots: Sequence[int],
+                            chain: Optional[GreedyStep] = None) -> GreedyStep:
+        """:meth:`decode_greedy` without waiting: the step is enqueued and its ids are copied to a
+        pinned host buffer behind it, so the caller can do its host work for the previous step
+        while this one runs.  ``tokens`` None with ``chain`` (a chainable step of the same batch
+        size whose sequences are these, in this order): the tokens are ``chain``'s ids, read on
+        the GPU — the next step is enqueued before ``chain``'s result reaches the host."""
+        T = len(positions)
+        if T == 0:
+            raise ValueError("decode: no tokens")
+        if tokens is None and (chain is None or not chain.chainable or chain.buffers.T != T):
+            raise ValueError("decode_greedy_async: a chained step needs a chainable step of the "
+                             "same size")
+        if not self.gpu or T > self.max_T:
+            toks = list(tokens) if tokens is not None else chain.result()
+            return GreedyStep(value=self.decode_greedy(toks, positions, slots))
+        for p in positions:
+            if p >= self.max_ctx:
+                raise ValueError(f"position {p} beyond the context ({self.max_ctx})")
+        self.stats["decode_steps"] += 1
+        self.stats["decode_tokens"] += T
+        ids = self._decode_native(tokens, positions, slots, greedy=True)
+        b = self._buffers(T)
+        if b.ids_host is None:
+            b.ids_host = [torch.zeros(T, dtype=torch.int32).pin_memory() for _ in range(2)]
+        # two landing buffers: the previous step's may still be read by the caller
+        host = b.ids_host[b.ids_flip]
+        b.ids_flip ^= 1
+        host.copy_(ids, non_blocking=True)
+        evt = torch.cuda.Event()
+        evt.record()
+        return GreedyStep(host=host, event=evt, buffers=b)
 
     def prefill(self, tokens: Sequence[int], slot: int, start: int = 0) -> torch.Tensor:
         """Process prompt tokens of one sequence; returns the logits of its last token [vocab]."""

@@ -147,7 +147,8 @@ class Scheduler:
     searched only in the held-back tail plus the new text."""
 
     def __init__(self, engine: Engine, tok: Tokenizer, parallel: int = 8, ubatch: int = 512,
-                 batch: Optional[int] = None, autostart: bool = True, prompt_batch: bool = True):
+                 batch: Optional[int] = None, autostart: bool = True, prompt_batch: bool = True,
+                 pipeline: bool = True):
         self.engine = engine
         self.tok = tok
         # prompt chunks of several slots in one pass (engine.prefill_many): its GEMMs run at an M
@@ -155,6 +156,10 @@ class Scheduler:
         # last bits with the traffic; False prefills every prompt alone (--no-prompt-batch), for
         # runs that must reproduce bit for bit
         self.prompt_batch = prompt_batch
+        # greedy steps of an unchanged batch enqueued back to back (_step_pipelined); False: every
+        # step waits for its tokens before the next one is enqueued
+        self.pipeline = pipeline
+        self._inflight = None                            # (jobs, GreedyStep, t0) of the step in flight
         self.parallel = max(1, min(parallel, engine.slots))
         self.ubatch = max(1, int(ubatch))
         self.batch = max(self.ubatch, int(batch or self.ubatch))
@@ -414,6 +419,9 @@ class Scheduler:
             self._release(j)
         if not self.prefilling:
             return 0
+        # a decode step still in flight finishes first: the prompt batch's wall time (one sync)
+        # then covers the prompt work only
+        self._flush_inflight()
         # Prompts that fit the batch (``batch`` tokens, llama-server's n_batch) whole are taken
         # whole: a burst of new requests all start decoding within an iteration or two.  A prompt
         # that does not fit is cut into chunks — of at most ``ubatch`` tokens while other
@@ -491,13 +499,75 @@ class Scheduler:
                 self.metrics["prefill_batches_total"] += 1
         return total
 
+    def _consume(self, jobs: List[Job], toks: List[int]) -> int:
+        """Tokens of a finished step: advance, emit, release the finished.  A job that left
+        the batch while the step was in flight (finished or cancelled) gets nothing."""
+        n = 0
+        for j, t in zip(jobs, toks):
+            if self.active.get(j.slot) is not j or not j.decoding:
+                continue
+            j.pos += 1          # the step wrote this job's KV
+            n += 1
+            if self._emit(j, int(t)):
+                self._release(j)
+        with self._lock:
+            self.metrics["tokens_predicted_total"] += n
+        return n
+
+    def _flush_inflight(self) -> int:
+        """Wait for the step in flight (if any) and hand out its tokens."""
+        infl, self._inflight = self._inflight, None
+        if infl is None:
+            return 0
+        jobs, step, t0 = infl
+        toks = step.result()
+        with self._lock:
+            self.metrics["decode_seconds_total"] += time.perf_counter() - t0
+        return self._consume(jobs, toks)
+
+    def _step_pipelined(self, jobs: List[Job]) -> int:
+        """Greedy steps of an unchanged batch run back to back on the GPU: the next step is
+        enqueued (its tokens read on the GPU from the in-flight step's ids) before the in-flight
+        step's tokens are detokenised and sent, so the host work of a step hides under the next
+        one.  When the batch changes, the in-flight step is flushed first."""
+        infl = self._inflight
+        if infl is not None and [id(j) for j in infl[0]] == [id(j) for j in jobs] and \
+                infl[1].chainable:
+            t0 = time.perf_counter()
+            nxt = self.engine.decode_greedy_async(None, [j.pos + 1 for j in jobs],
+                                                  [j.slot for j in jobs], chain=infl[1])
+            with self._lock:
+                self.metrics["decode_steps_total"] += 1
+            n = self._flush_inflight()
+            self._inflight = (jobs, nxt, t0)
+            return n
+        n = self._flush_inflight()
+        jobs = [j for j in self.active.values() if j.decoding and not j.cancelled]
+        if not jobs or not all(j.fast_greedy for j in jobs):
+            return n
+        t0 = time.perf_counter()
+        step = self.engine.decode_greedy_async([j.last for j in jobs], [j.pos for j in jobs],
+                                               [j.slot for j in jobs])
+        with self._lock:
+            self.metrics["decode_steps_total"] += 1
+        self._inflight = (jobs, step, t0)
+        return n
+
     def _step(self) -> int:
-        """One decode step of every sequence past its prompt; returns how many."""
+        """One decode step of every sequence past its prompt; returns how many tokens were
+        handed out."""
         for j in [j for j in self.active.values() if j.decoding and j.cancelled]:
             self._release(j)
         jobs = [j for j in self.active.values() if j.decoding]
         if not jobs:
-            return 0
+            return self._flush_inflight()
+        if self.pipeline and all(j.fast_greedy for j in jobs) and \
+                hasattr(self.engine, "decode_greedy_async"):
+            return self._step_pipelined(jobs)
+        n_flushed = self._flush_inflight()
+        jobs = [j for j in self.active.values() if j.decoding]
+        if not jobs:
+            return n_flushed
         t0 = time.perf_counter()
         args = ([j.last for j in jobs], [j.pos for j in jobs], [j.slot for j in jobs])
         if all(j.fast_greedy for j in jobs) and hasattr(self.engine, "decode_greedy"):
@@ -521,7 +591,7 @@ class Scheduler:
                 self._fail(j, t)
             elif self._emit(j, int(t)):
                 self._release(j)
-        return len(jobs)
+        return n_flushed + len(jobs)
 
     def _loop(self) -> None:
         clock = time.perf_counter

@@ -893,3 +893,31 @@ def test_wide_model_steps_of_5_to_8_tokens(dev):
             torch.testing.assert_close(batch[s], eng.decode([toks[s]], [3], [s])[0],
                                        rtol=0, atol=0)
         assert eng.decode_greedy(toks, [3] * T, list(range(T))) == batch.argmax(-1).tolist()
+
+
+def test_chained_async_greedy_steps_equal_decode_greedy(dev, tiny_gguf):
+    """decode_greedy_async with the tokens read on the GPU from the previous step's ids (the
+    server's pipelined steps) gives the tokens of host-fed decode_greedy steps, step for step."""
+    from k8s_nvidia_gpus_amd.models.llm.synthetic import load
+
+    a, tok = load(tiny_gguf, device=dev, max_ctx=512, dense=True, slots=4)
+    b, _ = load(tiny_gguf, device=dev, max_ctx=512, dense=True, slots=4)
+    prompts = [tok.encode(t) for t in ("a cozy cabin", "hello world, hello", "the lazy dog")]
+    for s, p in enumerate(prompts):
+        a.prefill(p, slot=s)
+        b.prefill(p, slot=s)
+    slots = [0, 1, 2]
+    pos = [len(p) for p in prompts]
+    last = [7, 9, 11]
+    step = a.decode_greedy_async(last, pos, slots)
+    assert step.chainable
+    want, cur = [], list(last)
+    for k in range(12):
+        nxt = a.decode_greedy_async(None, [q + k + 1 for q in pos], slots, chain=step)
+        got = step.result()
+        ref = b.decode_greedy(cur, [q + k for q in pos], slots)
+        assert got == ref, k
+        want.append(ref)
+        cur = ref
+        step = nxt
+    step.result()

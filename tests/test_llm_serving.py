@@ -387,3 +387,58 @@ def test_short_prompts_fitting_the_batch_are_taken_whole_while_decoding(tiny_mod
     assert len(short[0]) in later and len(short[1]) in later       # each taken whole
     # the long one in ubatch chunks, down to its last one
     assert 8 * sum(1 for n in later if n == 8) >= len(longer) - 8
+
+
+class ChainedStepEngine:
+    """CPU engine wrapper whose greedy steps are chainable, as the GPU engine's are: a chained
+    step reads its tokens from the in-flight step (``decode_greedy_async(None, ..., chain=)``)."""
+
+    def __init__(self, eng):
+        self._eng = eng
+        self.calls = []
+
+    def __getattr__(self, name):
+        return getattr(self._eng, name)
+
+    def decode_greedy_async(self, tokens, positions, slots, chain=None):
+        from types import SimpleNamespace
+
+        from k8s_nvidia_gpus_amd.models.llm.engine import GreedyStep
+
+        self.calls.append("chained" if tokens is None else "host")
+        if tokens is None:
+            assert chain is not None and chain.chainable and chain.buffers.T == len(positions)
+            tokens = chain.result()
+        step = GreedyStep(value=self._eng.decode_greedy(tokens, positions, slots))
+        step.chainable, step.buffers = True, SimpleNamespace(T=len(positions))
+        return step
+
+
+def test_pipelined_greedy_steps_give_the_unpipelined_answers(tiny_model):
+    """Greedy steps of an unchanged batch are enqueued back to back, the next one fed on the
+    in-flight step's tokens; sequences finishing mid-chain (different max_new, a stop string)
+    get no extra token, and every answer equals the one-step-at-a-time scheduler's."""
+    from k8s_nvidia_gpus_amd.models.llm import server as S
+
+    eng, tok = _load(tiny_model)
+    prompts = [tok.encode(t) for t in ("a cozy cabin", "hello world", "the lazy dog", "one two")]
+    lens = [5, 17, 9, 30]
+
+    def run(pipeline, engine):
+        sched = S.Scheduler(engine, tok, parallel=4, ubatch=64, autostart=False, pipeline=pipeline)
+        try:
+            jobs = [sched.submit(S.Job(ids=ids, max_new=n, ignore_eos=True))
+                    for ids, n in zip(prompts, lens)]
+            sched.start()
+            return [_wait(j) for j in jobs], sched
+        finally:
+            sched.close()
+
+    chained = ChainedStepEngine(eng)
+    got, sched = run(True, chained)
+    eng2, _ = _load(tiny_model)
+    want, _ = run(False, eng2)
+    for g, w, n in zip(got, want, lens):
+        assert g.gen == w.gen and len(g.gen) == n and g.text == w.text
+    assert chained.calls.count("chained") > 10                 # the steps did chain
+    assert sched.metrics["tokens_predicted_total"] == sum(lens)

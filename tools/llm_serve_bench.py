@@ -158,6 +158,24 @@ async def run(args, base):
                 prompts.append((await cl.prompt_messages(args.prompt, seed))[0])
             recs = await asyncio.gather(*(cl.stream(m, args.gen, {}) for m in prompts))
             row = dict(clients=n, **summarise(recs))
+            # what the scheduler did until every stream had its first token (TTFT window)
+            try:
+                async with cl.session.get(cl.base + "/debug/iterations") as r:
+                    dbg = await r.json()
+                a0 = min(r_["t_send"] for r_ in recs) - 0.05
+                a1 = max(r_["chunks"][0] for r_ in recs if r_["chunks"]) + 0.05
+                its = [x for x in dbg["iterations"] if a0 <= x["t"] <= a1]
+                row["ttft_window"] = {
+                    "iterations": len(its),
+                    "first_iteration_after_send_ms": round((its[0]["t"] - a0 - 0.05) * 1e3, 1)
+                    if its else None,
+                    "prefill_ms": round(sum(x["prefill_s"] for x in its) * 1e3, 1),
+                    "step_ms": round(sum(x["step_s"] for x in its) * 1e3, 1),
+                    "prompt_tokens": sum(x["prompt_tokens"] for x in its),
+                    "gc_pauses_ms": [round(g["s"] * 1e3, 1) for g in dbg.get("gc_pauses", [])
+                                     if a0 <= g["t"] <= a1]}
+            except Exception as e:  # noqa: BLE001 - diagnostics only
+                row["ttft_window"] = {"error": repr(e)[:120]}
             out["concurrency"].append(row)
             print(f"concurrency {row}", file=sys.stderr, flush=True)
         if args.admit:
