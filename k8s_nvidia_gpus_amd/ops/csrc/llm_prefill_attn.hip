@@ -103,16 +103,22 @@ struct Args {
   float c;           // scale * log2(e)
 };
 
-template <bool BF16, int NW>
-__global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) {
+// KS key slots: the NW waves are NW / KS row waves x KS key slots.  Each step stages KS
+// consecutive key tiles and slot j's waves take tile j of them, so a row block's chain of tiles is
+// KS times shorter; the slots' (max, sum, O) merge through LDS at the end.  For grids that leave
+// the chip idle (a short prompt from position 0: 112 four-wave workgroups for 512 tokens).
+template <bool BF16, int NW, int KS>
+__global__ __launch_bounds__(NW * 64, KS == 1 ? 2 : 1) void prefill_attn_kernel(const Args a) {
   constexpr int NT = NW * 64;
+  constexpr int RW = NW / KS;                // row waves: the workgroup's rows are RW x 32
   constexpr int NCH = kKeys * kCR;
-  constexpr int CH = NCH / NT;
-  static_assert(NCH % NT == 0, "tile chunks per thread");
-  __shared__ __attribute__((aligned(16))) char lds[kLds];
+  constexpr int CH = KS * NCH / NT;          // 16-byte chunks per thread and step (KS tiles)
+  static_assert(NCH % NT == 0 && NW % KS == 0, "tile chunks per thread");
+  __shared__ __attribute__((aligned(16))) char lds[KS * kLds];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
+  const int rw = KS == 1 ? wave : wave % RW, ksl = KS == 1 ? 0 : wave / RW;
 
   // XCD-major block -> work item (consecutive work items share an XCD and so its L2); work order:
   // row block fastest (heaviest first, below), then KV head, then split
@@ -135,14 +141,14 @@ __global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) 
 
   const int rows = a.P * a.group;            // query rows of this KV head
   const long rowsH = (long)a.P * a.H;        // query rows of the whole chunk (partials' index)
-  const int R0 = rb * (NW * 32);
-  const int p_hi_wg = min(a.P - 1, (R0 + NW * 32 - 1) / a.group);
+  const int R0 = rb * (RW * 32);
+  const int p_hi_wg = min(a.P - 1, (R0 + RW * 32 - 1) / a.group);
   const int kend = a.start + p_hi_wg + 1;    // keys [0, kend) reach this workgroup
   const int nt_wg = (kend + kKeys - 1) / kKeys;
   const int t0 = split * a.tps, t1 = min(nt_wg, t0 + a.tps);
 
   // this lane's query row
-  const int row = R0 + wave * 32 + r;
+  const int row = R0 + rw * 32 + r;
   const bool valid = row < rows;
   const int p = valid ? row / a.group : a.P - 1;
   const int head = g * a.group + (valid ? row - p * a.group : 0);
@@ -156,7 +162,7 @@ __global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) 
   }
 
   // this wave's token range (wave-uniform)
-  const int wrow0 = R0 + wave * 32;
+  const int wrow0 = R0 + rw * 32;
   const bool wave_valid = wrow0 < rows;
   const int pw_lo = wrow0 / a.group;
   const int pw_hi = min(a.P - 1, (wrow0 + 31) / a.group);
@@ -182,8 +188,8 @@ __global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) 
   auto load_tile = [&](int kbase) {
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-      const int c = tid + j * NT, krow = c / kCR, ch = c - krow * kCR;
-      const int key = kbase + krow;
+      const int c = tid + j * NT, ti = c / NCH, cc = c - ti * NCH, krow = cc / kCR;
+      const int ch = cc - krow * kCR, key = kbase + ti * kKeys + krow;
       if (key < kend) {
         kr[j] = *reinterpret_cast<const uint4*>(kb + (long)key * kD + ch * 8);
         vr[j] = *reinterpret_cast<const uint4*>(vb + (long)key * kD + ch * 8);
@@ -194,11 +200,12 @@ __global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) 
     }
   };
   auto store_tile = [&](int buf) {
-    char* kl = lds + buf * kBuf;
-    char* vl = kl + kTile;
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-      const int c = tid + j * NT, krow = c / kCR, ch = c - krow * kCR;
+      const int c = tid + j * NT, ti = c / NCH, cc = c - ti * NCH, krow = cc / kCR;
+      const int ch = cc - krow * kCR;
+      char* kl = lds + (buf * KS + ti) * kBuf;
+      char* vl = kl + kTile;
       *reinterpret_cast<uint4*>(kl + krow * kRB + (kswz(krow, ch) << 4)) = kr[j];
       *reinterpret_cast<uint4*>(vl + krow * kRB + (vswz(krow, ch) << 4)) = vr[j];
     }
@@ -220,22 +227,24 @@ __global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) 
   for (int db = 0; db < kDblk; ++db)
     voff[db] = vrow * kRB + vsub + ((4 * (db ^ (vrow & 3)) + vcol_chunk) << 4);
 
-  // one key tile from LDS buffer BUF (a compile-time parity: the loop below is unrolled by two)
+  // one step: key tiles kt .. kt + KS - 1 in LDS buffer BUF, this wave's slot takes kt + ksl
+  // (BUF a compile-time parity when the loop below is unrolled by two)
   auto tile = [&](const int kt, const int buf) {
-    const int kbase = kt * kKeys;
-    const char* kl = lds + buf * kBuf;
+    const int kstep = kt * kKeys;
+    const int kbase = kstep + ksl * kKeys;
+    const char* kl = lds + (buf * KS + ksl) * kBuf;
     const char* vl = kl + kTile;
 #if AMDK8S_PA_WAB
-    // write-after-barrier staging: tile kt + 1 (in registers since the previous tile) into the
-    // buffer every wave finished reading before the barrier that ended the previous tile, then
-    // tile kt + 2's loads — their latency spans this tile's maths
-    if (kt + 1 < t1) store_tile(buf ^ 1);
-    if (kt + 2 < t1) load_tile(kbase + 2 * kKeys);
+    // write-after-barrier staging: step kt + KS (in registers since the previous step) into the
+    // buffer every wave finished reading before the barrier that ended the previous step, then
+    // step kt + 2 KS's loads — their latency spans this step's maths
+    if (kt + KS < t1) store_tile(buf ^ 1);
+    if (kt + 2 * KS < t1) load_tile(kstep + 2 * KS * kKeys);
 #else
-    if (kt + 1 < t1) load_tile(kbase + kKeys);
+    if (kt + KS < t1) load_tile(kstep + KS * kKeys);
 #endif
 
-    if (wave_valid && kbase <= a.start + pw_hi) {
+    if (wave_valid && kt + ksl < t1 && kbase <= a.start + pw_hi) {
       f32x16 s[2];
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
@@ -307,7 +316,7 @@ __global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) 
     }
 
 #if !AMDK8S_PA_WAB
-    if (kt + 1 < t1) store_tile(buf ^ 1);
+    if (kt + KS < t1) store_tile(buf ^ 1);
 #endif
     __syncthreads();
   };
@@ -315,17 +324,58 @@ __global__ __launch_bounds__(NW * 64, 2) void prefill_attn_kernel(const Args a) 
   load_tile(t0 * kKeys);
   store_tile(0);
 #if AMDK8S_PA_WAB
-  if (t0 + 1 < t1) load_tile((t0 + 1) * kKeys);
+  if (t0 + KS < t1) load_tile((t0 + KS) * kKeys);
 #endif
   __syncthreads();
 #if AMDK8S_PA_UNROLL2
-  for (int kt = t0; kt < t1; kt += 2) {      // the buffer parity a constant in each half
+  for (int kt = t0; kt < t1; kt += 2 * KS) {  // the buffer parity a constant in each half
     tile(kt, 0);
-    if (kt + 1 < t1) tile(kt + 1, 1);
+    if (kt + KS < t1) tile(kt + KS, 1);
   }
 #else
-  for (int kt = t0; kt < t1; ++kt) tile(kt, (kt - t0) & 1);
+  for (int kt = t0; kt < t1; kt += KS) tile(kt, ((kt - t0) / KS) & 1);
 #endif
+
+  if constexpr (KS > 1) {
+    // merge the key slots (the last step ended with a barrier, so the tile buffers are free):
+    // slots 1.. write (O, m, l) per lane, slot 0 rescales both to the larger max and adds.  An
+    // empty slot has m = kNoMax, l = 0, O = 0 and weight 0.
+    float4* mo = reinterpret_cast<float4*>(lds);
+    float* mls = reinterpret_cast<float*>(lds + (KS - 1) * RW * kDblk * 4 * 64 * 16);
+    if (ksl > 0) {
+      float4* dst = mo + ((ksl - 1) * RW + rw) * kDblk * 4 * 64 + lane;
+#pragma unroll
+      for (int db = 0; db < kDblk; ++db)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq)
+          dst[(db * 4 + gq) * 64] = make_float4(o[db][4 * gq], o[db][4 * gq + 1], o[db][4 * gq + 2],
+                                                o[db][4 * gq + 3]);
+      mls[((ksl - 1) * RW + rw) * 128 + lane] = m;
+      mls[((ksl - 1) * RW + rw) * 128 + 64 + lane] = l;
+    }
+    __syncthreads();
+    if (ksl > 0) return;
+#pragma unroll
+    for (int s = 1; s < KS; ++s) {
+      const float m2 = mls[((s - 1) * RW + rw) * 128 + lane];
+      const float l2 = mls[((s - 1) * RW + rw) * 128 + 64 + lane];
+      const float M = fmaxf(m, m2);
+      const float w1 = __builtin_amdgcn_exp2f((m - M) * a.c), w2 = __builtin_amdgcn_exp2f((m2 - M) * a.c);
+      const float4* src = mo + ((s - 1) * RW + rw) * kDblk * 4 * 64 + lane;
+#pragma unroll
+      for (int db = 0; db < kDblk; ++db)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const float4 v = src[(db * 4 + gq) * 64];
+          o[db][4 * gq] = fmaf(o[db][4 * gq], w1, v.x * w2);
+          o[db][4 * gq + 1] = fmaf(o[db][4 * gq + 1], w1, v.y * w2);
+          o[db][4 * gq + 2] = fmaf(o[db][4 * gq + 2], w1, v.z * w2);
+          o[db][4 * gq + 3] = fmaf(o[db][4 * gq + 3], w1, v.w * w2);
+        }
+      l = fmaf(l, w1, l2 * w2);
+      m = M;
+    }
+  }
 
   // epilogue: lane holds O[row][32db + 8(i>>2) + 4h + (i&3)] (unnormalised), its half of the sum
   const float lt = l + __shfl_xor(l, 32, 64);
@@ -385,10 +435,10 @@ __global__ __launch_bounds__(256) void prefill_attn_combine(const Args a) {
 }
 
 struct Plan {
-  int nw, nrb, nsplit, tps;
+  int nw, ks, nrb, nsplit, tps;
 };
 
-Plan make_plan(int P, int start, int H, int Hkv, int nsplit_req, int nw_req) {
+Plan make_plan(int P, int start, int H, int Hkv, int nsplit_req, int nw_req, int ks_req) {
   // Measured on MI355X (tools/debug/prefill_attn_sweep.py, profiles/r06/prefill_attn_sweep.log):
   // * a prompt from position 0, or enough 4-wave row blocks to fill the chip: 4 waves, no split
   //   (512 @ 0: 17.6 us vs 22.5 with 8 waves; 8192 @ 0: 681 vs 725; any split only adds work);
@@ -412,22 +462,34 @@ Plan make_plan(int P, int start, int H, int Hkv, int nsplit_req, int nw_req) {
       ns = (int)std::max<long>(1, std::min<long>(std::min<long>(256 / base4, ntiles / 8), 32));
     }
   }
+  // key slots, for a prompt from position 0 whose 4-wave grid is under one round (profiles/r06/
+  // prefill_attn_sweep_key_slots.log): up to half a round, 4 waves as 2 row waves x 2 slots
+  // (512 @ 0: 14.1 vs 17.1 us; 256 @ 0: 10.4 vs 11.0), else 8 waves as 4 x 2 (1024 @ 0: 25.4 vs
+  // 28.2); a full round or more keeps one slot (2048 @ 0: 62.4 vs 68.7 with 8 x 2)
+  int ks = 1;
+  if (start == 0 && ns == 1 && base4 <= 256) {
+    ks = 2;
+    if (base4 * 2 > 256) nw = 8;
+  }
   if (nw_req == 4 || nw_req == 8) nw = nw_req;
   if (nsplit_req > 0) ns = nsplit_req;
+  if (ks_req == 1 || ks_req == 2) ks = ks_req;
   pl.nw = nw;
-  pl.nrb = (int)((rows + nw * 32 - 1) / (nw * 32));
+  pl.ks = ks;
+  const int rbr = nw / ks * 32;                // rows per row block
+  pl.nrb = (int)((rows + rbr - 1) / rbr);
   ns = std::max(1, std::min(ns, ntiles));
   pl.tps = (ntiles + ns - 1) / ns;
   pl.nsplit = (ntiles + pl.tps - 1) / pl.tps;
   return pl;
 }
 
-template <bool BF16, int NW>
+template <bool BF16, int NW, int KS>
 int launch(Args a, const Plan& pl, hipStream_t stream) {
   const long nwg = (long)pl.nrb * a.Hkv * pl.nsplit;
   if (nwg <= 0 || nwg > 0x7fffffff) return -1;
-  hipLaunchKernelGGL((prefill_attn_kernel<BF16, NW>), dim3((unsigned)nwg), dim3(NW * 64), 0, stream,
-                     a);
+  hipLaunchKernelGGL((prefill_attn_kernel<BF16, NW, KS>), dim3((unsigned)nwg), dim3(NW * 64), 0,
+                     stream, a);
   if (hipGetLastError() != hipSuccess) return -2;
   if (pl.nsplit > 1) {
     const long rowsH = (long)a.P * a.H;
@@ -443,20 +505,24 @@ int launch(Args a, const Plan& pl, hipStream_t stream) {
 extern "C" {
 
 // fp32 workspace bytes the call with these arguments needs (0 when it does not split)
-long amdk8s_llm_prefill_attn_workspace(int P, int start, int H, int Hkv, int nsplit, int nw) {
+long amdk8s_llm_prefill_attn_workspace(int P, int start, int H, int Hkv, int nsplit, int nw,
+                                       int ks) {
   if (P <= 0 || H <= 0 || Hkv <= 0 || H % Hkv != 0 || start < 0) return -1;
-  const Plan pl = make_plan(P, start, H, Hkv, nsplit, nw);
+  const Plan pl = make_plan(P, start, H, Hkv, nsplit, nw, ks);
   if (pl.nsplit == 1) return 0;
   return (long)pl.nsplit * P * H * (kD + 2) * 4;
 }
 
-// Plan of the call: out[0] = waves per workgroup, out[1] = key splits, out[2] = tiles per split.
-int amdk8s_llm_prefill_attn_plan(int P, int start, int H, int Hkv, int nsplit, int nw, int* out) {
+// Plan of the call: out[0] = waves per workgroup, out[1] = key splits, out[2] = tiles per split,
+// out[3] = key slots per workgroup.
+int amdk8s_llm_prefill_attn_plan(int P, int start, int H, int Hkv, int nsplit, int nw, int ks,
+                                 int* out) {
   if (P <= 0 || H <= 0 || Hkv <= 0 || H % Hkv != 0 || start < 0) return -1;
-  const Plan pl = make_plan(P, start, H, Hkv, nsplit, nw);
+  const Plan pl = make_plan(P, start, H, Hkv, nsplit, nw, ks);
   out[0] = pl.nw;
   out[1] = pl.nsplit;
   out[2] = pl.tps;
+  out[3] = pl.ks;
   return 0;
 }
 
@@ -466,14 +532,14 @@ int amdk8s_llm_prefill_attn_plan(int P, int start, int H, int Hkv, int nsplit, i
 int amdk8s_llm_prefill_attn(const void* q, long sq_tok, long sq_head, const void* kc,
                             const void* vc, long skv_head, void* o, long so_tok, long so_head, int P,
                             int start, int H, int Hkv, float scale, void* work, long work_bytes,
-                            int nsplit, int nw, int dtype, hipStream_t stream) {
+                            int nsplit, int nw, int ks, int dtype, hipStream_t stream) {
   if (P <= 0 || H <= 0 || Hkv <= 0 || H % Hkv != 0 || start < 0) return -1;
   if ((sq_tok | sq_head | so_tok | so_head | skv_head) % 8 != 0) return -3;
   if ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(kc) |
        reinterpret_cast<uintptr_t>(vc) | reinterpret_cast<uintptr_t>(o)) % 16 != 0)
     return -3;
   if ((long)P * (H / Hkv) > 0x7fffffffL) return -1;
-  const Plan pl = make_plan(P, start, H, Hkv, nsplit, nw);
+  const Plan pl = make_plan(P, start, H, Hkv, nsplit, nw, ks);
   const long need = pl.nsplit == 1 ? 0 : (long)pl.nsplit * P * H * (kD + 2) * 4;
   if (need > work_bytes || (need > 0 && (reinterpret_cast<uintptr_t>(work) % 16) != 0)) return -4;
   Args a;
@@ -497,9 +563,12 @@ int amdk8s_llm_prefill_attn(const void* q, long sq_tok, long sq_head, const void
   a.nsplit = pl.nsplit;
   a.tps = pl.tps;
   a.c = scale * 1.4426950408889634f;
-  if (dtype == 1)
-    return pl.nw == 8 ? launch<true, 8>(a, pl, stream) : launch<true, 4>(a, pl, stream);
-  return pl.nw == 8 ? launch<false, 8>(a, pl, stream) : launch<false, 4>(a, pl, stream);
+  if (dtype == 1) {
+    if (pl.ks == 2) return pl.nw == 8 ? launch<true, 8, 2>(a, pl, stream) : launch<true, 4, 2>(a, pl, stream);
+    return pl.nw == 8 ? launch<true, 8, 1>(a, pl, stream) : launch<true, 4, 1>(a, pl, stream);
+  }
+  if (pl.ks == 2) return pl.nw == 8 ? launch<false, 8, 2>(a, pl, stream) : launch<false, 4, 2>(a, pl, stream);
+  return pl.nw == 8 ? launch<false, 8, 1>(a, pl, stream) : launch<false, 4, 1>(a, pl, stream);
 }
 
 }  // extern "C"

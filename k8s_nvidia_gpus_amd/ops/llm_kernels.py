@@ -335,33 +335,35 @@ def _declare_prefill_attn(lib) -> None:
         return
     vp, ci, cl, cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
     lib.amdk8s_llm_prefill_attn.argtypes = [vp, cl, cl, vp, vp, cl, vp, cl, cl, ci, ci, ci, ci, cf,
-                                            vp, cl, ci, ci, ci, vp]
+                                            vp, cl, ci, ci, ci, ci, vp]
     lib.amdk8s_llm_prefill_attn.restype = ci
-    lib.amdk8s_llm_prefill_attn_workspace.argtypes = [ci, ci, ci, ci, ci, ci]
+    lib.amdk8s_llm_prefill_attn_workspace.argtypes = [ci, ci, ci, ci, ci, ci, ci]
     lib.amdk8s_llm_prefill_attn_workspace.restype = cl
-    lib.amdk8s_llm_prefill_attn_plan.argtypes = [ci, ci, ci, ci, ci, ci, ctypes.POINTER(ci)]
+    lib.amdk8s_llm_prefill_attn_plan.argtypes = [ci, ci, ci, ci, ci, ci, ci, ctypes.POINTER(ci)]
     lib.amdk8s_llm_prefill_attn_plan.restype = ci
     lib._prefill_attn_declared = True
 
 
 def prefill_attn_plan(P: int, start: int, heads: int, kv_heads: int, nsplit: int = 0,
-                      nw: int = 0) -> dict:
-    """The launch plan the kernel picks: waves per workgroup, key splits, key tiles per split."""
+                      nw: int = 0, ks: int = 0) -> dict:
+    """The launch plan the kernel picks: waves per workgroup, key splits, key tiles per split,
+    key slots per workgroup (``ks``: the waves split each step's keys, merged in LDS)."""
     lib = _lib()
     _declare_prefill_attn(lib)
-    out = (ctypes.c_int * 3)()
-    _check(lib.amdk8s_llm_prefill_attn_plan(P, start, heads, kv_heads, nsplit, nw, out),
+    out = (ctypes.c_int * 4)()
+    _check(lib.amdk8s_llm_prefill_attn_plan(P, start, heads, kv_heads, nsplit, nw, ks, out),
            "amdk8s_llm_prefill_attn_plan")
-    return {"waves": out[0], "nsplit": out[1], "tiles_per_split": out[2]}
+    return {"waves": out[0], "nsplit": out[1], "tiles_per_split": out[2], "key_slots": out[3]}
 
 
-def prefill_attn(q, kc, vc, out, start: int, scale: float, nsplit: int = 0, nw: int = 0) -> None:
+def prefill_attn(q, kc, vc, out, start: int, scale: float, nsplit: int = 0, nw: int = 0,
+                 ks: int = 0) -> None:
     """Causal GQA attention of a prompt chunk against one slot's KV-cache slabs, in place.
 
     ``q`` / ``out``: [H, P, 128] views (unit inner stride, any head / token strides — the engine's
     token-major storage); ``kc`` / ``vc``: the slot's [Hkv, max_ctx, 128] slabs, positions
     0 .. start+P-1 written.  Query p sits at position start + p and sees keys 0 .. start + p.
-    ``nsplit`` / ``nw``: 0 = the kernel's plan (:func:`prefill_attn_plan`)."""
+    ``nsplit`` / ``nw`` / ``ks``: 0 = the kernel's plan (:func:`prefill_attn_plan`)."""
     H, P, D = q.shape
     hkv = kc.shape[0]
     if D != 128 or tuple(out.shape) != (H, P, D) or q.stride(2) != 1 or out.stride(2) != 1:
@@ -374,7 +376,7 @@ def prefill_attn(q, kc, vc, out, start: int, scale: float, nsplit: int = 0, nw: 
         raise ValueError("prefill_attn: q, kc, vc, out must share fp16 or bf16")
     lib = _lib()
     _declare_prefill_attn(lib)
-    need = int(lib.amdk8s_llm_prefill_attn_workspace(P, start, H, hkv, nsplit, nw))
+    need = int(lib.amdk8s_llm_prefill_attn_workspace(P, start, H, hkv, nsplit, nw, ks))
     if need < 0:
         raise ValueError("prefill_attn: bad shape")
     work = _ATTN_WORK.get(q.device)
@@ -384,5 +386,5 @@ def prefill_attn(q, kc, vc, out, start: int, scale: float, nsplit: int = 0, nw: 
     _check(lib.amdk8s_llm_prefill_attn(
         q.data_ptr(), q.stride(1), q.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0),
         out.data_ptr(), out.stride(1), out.stride(0), P, int(start), H, hkv, float(scale),
-        _p(work) if need else None, work.numel() * 4 if need else 0, int(nsplit), int(nw),
+        _p(work) if need else None, work.numel() * 4 if need else 0, int(nsplit), int(nw), int(ks),
         int(q.dtype == torch.bfloat16), _stream(q)), "amdk8s_llm_prefill_attn")

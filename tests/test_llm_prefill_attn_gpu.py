@@ -69,6 +69,21 @@ def test_prefill_attention_forced_plans_agree(LK, nsplit, nw):
     torch.testing.assert_close(out.float(), _ref(q, kc, vc, start), rtol=1e-2, atol=3e-3)
 
 
+@pytest.mark.parametrize("nw", [4, 8])
+@pytest.mark.parametrize("P,start,nsplit", [(512, 0, 1), (37, 0, 1), (1, 0, 1), (200, 1000, 1),
+                                            (200, 1000, 3), (64, 8192, 16)])
+def test_prefill_attention_key_slots_agree(LK, nw, P, start, nsplit):
+    """Two key slots per workgroup (each step's two tiles go to different waves, merged in LDS)
+    give the fp32 answer, with and without a key split, including row blocks whose last step has
+    one tile (an empty slot)."""
+    H, Hkv = 28, 4
+    q, kc, vc = _case(H, Hkv, P, start, seed=3)
+    out = torch.full((P, H, 128), float("nan"), device=q.device, dtype=q.dtype).transpose(0, 1)
+    LK.prefill_attn(q, kc, vc, out, start, 1 / math.sqrt(128), nsplit=nsplit, nw=nw, ks=2)
+    assert torch.isfinite(out).all()
+    torch.testing.assert_close(out.float(), _ref(q, kc, vc, start), rtol=1e-2, atol=3e-3)
+
+
 def test_prefill_attention_bf16(LK):
     H, Hkv, P, start = 28, 4, 96, 700
     q, kc, vc = _case(H, Hkv, P, start, dtype=torch.bfloat16, seed=2)
@@ -84,6 +99,10 @@ def test_prefill_attention_plan_fills_the_chip(LK):
     assert long["nsplit"] > 1
     assert LK.prefill_attn_plan(32000, 0, 28, 4)["nsplit"] == 1
     assert LK.prefill_attn_plan(512, 0, 28, 4)["nsplit"] == 1
+    assert LK.prefill_attn_plan(512, 0, 28, 4)["key_slots"] == 2      # 112 workgroups otherwise
+    assert LK.prefill_attn_plan(1024, 0, 28, 4)["key_slots"] == 2
+    assert LK.prefill_attn_plan(1024, 0, 28, 4)["waves"] == 8
+    assert LK.prefill_attn_plan(2048, 0, 28, 4)["key_slots"] == 1
 
 
 def test_prefill_attention_rejects_bad_layouts(LK):

@@ -49,15 +49,17 @@ def main(argv):
         ntiles = (end + 63) // 64
         if os.environ.get("SWEEP_AUTO_ONLY") == "1":
             continue
-        for nw in (4, 8):
-            for ns in (1, 2, 3, 4, 6, 8, 12, 16, 24):
-                if ns > ntiles:
-                    continue
-                us = timed(lambda: LK.prefill_attn(q, k, v, out, start, 1 / math.sqrt(d),
-                                                   nsplit=ns, nw=nw))
-                print(json.dumps({"P": P, "start": start, "waves": nw, "nsplit": ns,
-                                  "us": round(us, 1), "tflops": round(flop / us / 1e6, 1)}),
-                      flush=True)
+        splits = [int(x) for x in os.environ.get("SWEEP_SPLITS", "1,2,3,4,6,8,12,16,24").split(",")]
+        for ks in (1, 2):
+            for nw in (4, 8):
+                for ns in splits:
+                    if ns > ntiles:
+                        continue
+                    us = timed(lambda: LK.prefill_attn(q, k, v, out, start, 1 / math.sqrt(d),
+                                                       nsplit=ns, nw=nw, ks=ks))
+                    print(json.dumps({"P": P, "start": start, "waves": nw, "key_slots": ks,
+                                      "nsplit": ns, "us": round(us, 1),
+                                      "tflops": round(flop / us / 1e6, 1)}), flush=True)
 
 
 if __name__ == "__main__":
