@@ -66,6 +66,12 @@ constexpr int kDblk = kD / 32;
 #ifndef AMDK8S_PA_WAB
 #define AMDK8S_PA_WAB 0
 #endif
+// score MFMAs: the two 32-key chains interleaved with each K fragment read one step ahead (a
+// sched_group_barrier pattern), instead of the compiler's order, which ran one chain's 8 reads
+// and MFMAs back to back, each MFMA waiting on its own LDS round trip
+#ifndef AMDK8S_PA_SCHED
+#define AMDK8S_PA_SCHED 0
+#endif
 constexpr float kNoMax = -1e30f;          // finite "no score yet" (a fully masked row stays NaN-free)
 
 __device__ __forceinline__ int kswz(int row, int ch) { return ch ^ (row & 15); }
@@ -246,6 +252,31 @@ __global__ __launch_bounds__(NW * 64, KS == 1 ? 2 : 1) void prefill_attn_kernel(
 
     if (wave_valid && kt + ksl < t1 && kbase <= a.start + pw_hi) {
       f32x16 s[2];
+#if AMDK8S_PA_SCHED
+      // the two 32-key chains interleaved, each K fragment read AMDK8S_PA_SCHED steps ahead of
+      // its MFMA (the order is the sched_group_barrier pattern below)
+      {
+        constexpr int DP = AMDK8S_PA_SCHED;
+        s16x8 kf[2][kKsteps];
+#pragma unroll
+        for (int st = 0; st < kKsteps; ++st) {
+          kf[0][st] = *reinterpret_cast<const s16x8*>(kl + koff[st]);
+          kf[1][st] = *reinterpret_cast<const s16x8*>(kl + 32 * kRB + koff[st]);
+        }
+        const f32x16 z = {};
+#pragma unroll
+        for (int st = 0; st < kKsteps; ++st) {
+          s[0] = mfma32<BF16>(kf[0][st], qf[st], st ? s[0] : z);
+          s[1] = mfma32<BF16>(kf[1][st], qf[st], st ? s[1] : z);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * DP, 0);         // DS reads
+#pragma unroll
+        for (int st = 0; st < kKsteps; ++st) {
+          if (st + DP < kKsteps) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);            // MFMA
+        }
+      }
+#else
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
 #if AMDK8S_PA_ZEROC
@@ -263,6 +294,7 @@ __global__ __launch_bounds__(NW * 64, KS == 1 ? 2 : 1) void prefill_attn_kernel(
           s[b] = mfma32<BF16>(kf, qf[st], s[b]);
         }
       }
+#endif
       if (kbase + kKeys - 1 > a.start + pw_lo) {     // the tile straddles this wave's diagonal
 #pragma unroll
         for (int b = 0; b < 2; ++b)

@@ -67,7 +67,7 @@ def llm_prefill(P: int = 512):
     from k8s_nvidia_gpus_amd.models.llm.weights import ModelWeights
 
     w = ModelWeights.random(QWEN25_7B, device=torch.device("cuda", 0), seed=0)
-    eng = Engine(w, max_ctx=4096, slots=8, dense=True)
+    eng = Engine(w, max_ctx=max(4096, P + 256), slots=1 if P > 4096 else 8, dense=True)
     eng.dense_weights()
     prompt = list(range(100, 100 + P))
     return lambda: eng.prefill(prompt, slot=0)
@@ -77,11 +77,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("what", choices=["sd15-unet", "wan-step", "llm-decode", "llm-prefill"])
     ap.add_argument("--tokens", type=int, default=1, help="llm-decode: concurrent sequences")
-    ap.add_argument("--prompt", type=int, default=512, help="llm-decode: prompt tokens per sequence")
+    ap.add_argument("--prompt", type=int, default=512, help="llm-decode / llm-prefill: prompt tokens (per sequence)")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     a = ap.parse_args()
-    fn = (llm_decode(a.tokens, a.prompt) if a.what == "llm-decode" else llm_prefill() if a.what == "llm-prefill"
+    fn = (llm_decode(a.tokens, a.prompt) if a.what == "llm-decode" else llm_prefill(a.prompt) if a.what == "llm-prefill"
           else {"sd15-unet": sd15_unet, "wan-step": wan_step}[a.what]())
     for _ in range(a.warmup):
         fn()
