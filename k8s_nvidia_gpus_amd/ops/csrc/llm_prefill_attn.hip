@@ -26,6 +26,7 @@
 // XOR-swizzled LDS images, transposed V reads (ds_read_b64_tr_b16), double-buffered tiles.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -494,6 +495,15 @@ Plan make_plan(int P, int start, int H, int Hkv, int nsplit_req, int nw_req, int
       ns = (int)std::max<long>(1, std::min<long>(std::min<long>(256 / base4, ntiles / 8), 32));
     }
   }
+  // a grid of a round or more with long key runs: 8 waves, each staged K/V tile feeding 256 rows
+  // (profiles/r06/prefill_attn_sweep_long.log: 32000 @ 0 10.07 vs 10.73 ms, 16384 @ 0 2.54 vs
+  // 2.72, 12288 @ 0 1.52 vs 1.61, 4096 @ 28000 1.85 vs 2.12, 16384 @ 16384 6.67 vs 7.21; 8192 @ 0
+  // and 8192 @ 8192 within 1 %)
+  static const bool long8 = [] {                // AMDK8S_PA_LONG8=0: 4 waves (A/B runs)
+    const char* e = getenv("AMDK8S_PA_LONG8");
+    return !e || e[0] != '0';
+  }();
+  if (long8 && base4 >= 256 && start + P >= 12288) nw = 8;
   // key slots, for a prompt from position 0 whose 4-wave grid is under one round (profiles/r06/
   // prefill_attn_sweep_key_slots.log): up to half a round, 4 waves as 2 row waves x 2 slots
   // (512 @ 0: 14.1 vs 17.1 us; 256 @ 0: 10.4 vs 11.0), else 8 waves as 4 x 2 (1024 @ 0: 25.4 vs

@@ -103,6 +103,9 @@ def test_prefill_attention_plan_fills_the_chip(LK):
     assert LK.prefill_attn_plan(1024, 0, 28, 4)["key_slots"] == 2
     assert LK.prefill_attn_plan(1024, 0, 28, 4)["waves"] == 8
     assert LK.prefill_attn_plan(2048, 0, 28, 4)["key_slots"] == 1
+    assert LK.prefill_attn_plan(2048, 0, 28, 4)["waves"] == 4
+    assert LK.prefill_attn_plan(32000, 0, 28, 4)["waves"] == 8     # long key runs
+    assert LK.prefill_attn_plan(4096, 28000, 28, 4)["waves"] == 8
 
 
 def test_prefill_attention_rejects_bad_layouts(LK):
