@@ -84,6 +84,15 @@ def test_prefill_attention_key_slots_agree(LK, nw, P, start, nsplit):
     torch.testing.assert_close(out.float(), _ref(q, kc, vc, start), rtol=1e-2, atol=3e-3)
 
 
+def test_prefill_attention_key_slots_bf16(LK):
+    H, Hkv, P, start = 28, 4, 300, 0
+    q, kc, vc = _case(H, Hkv, P, start, dtype=torch.bfloat16, seed=4)
+    assert LK.prefill_attn_plan(P, start, H, Hkv)["key_slots"] == 2
+    out = torch.empty(P, H, 128, device=q.device, dtype=q.dtype).transpose(0, 1)
+    LK.prefill_attn(q, kc, vc, out, start, 1 / math.sqrt(128))
+    torch.testing.assert_close(out.float(), _ref(q, kc, vc, start), rtol=2e-2, atol=1.5e-2)
+
+
 def test_prefill_attention_bf16(LK):
     H, Hkv, P, start = 28, 4, 96, 700
     q, kc, vc = _case(H, Hkv, P, start, dtype=torch.bfloat16, seed=2)
