@@ -62,16 +62,20 @@ constexpr int kDblk = kD / 32;
 #ifndef AMDK8S_PA_ZEROC
 #define AMDK8S_PA_ZEROC 0
 #endif
-// write the next tile into LDS after the barrier (with the tile after it in flight) instead of
-// before it
+// WAB: write the next tile into LDS after the barrier (with the tile after it in flight) instead
+// of before it.  SCHED: the score MFMAs' two 32-key chains interleaved, each K fragment read SCHED
+// steps ahead (a sched_group_barrier pattern), instead of the compiler's order, which runs one
+// chain's 8 reads and MFMAs back to back, each MFMA waiting on its own LDS round trip.
+// -1 = per shape, from tools/debug/attn_ab.sh (profiles/r06/attn_ab_long/): with 8 waves WAB and
+// SCHED 2 together take 32000 @ 0 10.02-10.09 -> 9.55-9.65 ms, 4096 @ 28000 1.844 -> 1.787-1.794,
+// 512 @ 31488 260 -> 254 us; with key slots SCHED 2 takes 512 @ 0 13.2 -> 12.9-13.0 us (WAB
+// 13.5); the 4-wave one-slot kernel keeps neither (8192 @ 0 within 1 %, profiles/r06/
+// attn_ab_sched/)
 #ifndef AMDK8S_PA_WAB
-#define AMDK8S_PA_WAB 0
+#define AMDK8S_PA_WAB -1
 #endif
-// score MFMAs: the two 32-key chains interleaved with each K fragment read one step ahead (a
-// sched_group_barrier pattern), instead of the compiler's order, which ran one chain's 8 reads
-// and MFMAs back to back, each MFMA waiting on its own LDS round trip
 #ifndef AMDK8S_PA_SCHED
-#define AMDK8S_PA_SCHED 0
+#define AMDK8S_PA_SCHED -1
 #endif
 constexpr float kNoMax = -1e30f;          // finite "no score yet" (a fully masked row stays NaN-free)
 
@@ -126,6 +130,8 @@ __global__ __launch_bounds__(NW * 64, KS == 1 ? 2 : 1) void prefill_attn_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int rw = KS == 1 ? wave : wave % RW, ksl = KS == 1 ? 0 : wave / RW;
+  constexpr bool WAB = AMDK8S_PA_WAB < 0 ? NW == 8 : AMDK8S_PA_WAB != 0;
+  constexpr int SCHED = AMDK8S_PA_SCHED < 0 ? (NW == 8 || KS == 2 ? 2 : 0) : AMDK8S_PA_SCHED;
 
   // XCD-major block -> work item (consecutive work items share an XCD and so its L2); work order:
   // row block fastest (heaviest first, below), then KV head, then split
@@ -241,23 +247,22 @@ __global__ __launch_bounds__(NW * 64, KS == 1 ? 2 : 1) void prefill_attn_kernel(
     const int kbase = kstep + ksl * kKeys;
     const char* kl = lds + (buf * KS + ksl) * kBuf;
     const char* vl = kl + kTile;
-#if AMDK8S_PA_WAB
-    // write-after-barrier staging: step kt + KS (in registers since the previous step) into the
-    // buffer every wave finished reading before the barrier that ended the previous step, then
-    // step kt + 2 KS's loads — their latency spans this step's maths
-    if (kt + KS < t1) store_tile(buf ^ 1);
-    if (kt + 2 * KS < t1) load_tile(kstep + 2 * KS * kKeys);
-#else
-    if (kt + KS < t1) load_tile(kstep + KS * kKeys);
-#endif
+    if constexpr (WAB) {
+      // write-after-barrier staging: step kt + KS (in registers since the previous step) into the
+      // buffer every wave finished reading before the barrier that ended the previous step, then
+      // step kt + 2 KS's loads — their latency spans this step's maths
+      if (kt + KS < t1) store_tile(buf ^ 1);
+      if (kt + 2 * KS < t1) load_tile(kstep + 2 * KS * kKeys);
+    } else {
+      if (kt + KS < t1) load_tile(kstep + KS * kKeys);
+    }
 
     if (wave_valid && kt + ksl < t1 && kbase <= a.start + pw_hi) {
       f32x16 s[2];
-#if AMDK8S_PA_SCHED
-      // the two 32-key chains interleaved, each K fragment read AMDK8S_PA_SCHED steps ahead of
-      // its MFMA (the order is the sched_group_barrier pattern below)
-      {
-        constexpr int DP = AMDK8S_PA_SCHED;
+      if constexpr (SCHED > 0) {
+        // the two 32-key chains interleaved, each K fragment read SCHED steps ahead of its MFMA
+        // (the order is the sched_group_barrier pattern below)
+        constexpr int DP = SCHED;
         s16x8 kf[2][kKsteps];
 #pragma unroll
         for (int st = 0; st < kKsteps; ++st) {
@@ -276,8 +281,7 @@ __global__ __launch_bounds__(NW * 64, KS == 1 ? 2 : 1) void prefill_attn_kernel(
           if (st + DP < kKsteps) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
           __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);            // MFMA
         }
-      }
-#else
+      } else {
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
 #if AMDK8S_PA_ZEROC
@@ -295,7 +299,7 @@ __global__ __launch_bounds__(NW * 64, KS == 1 ? 2 : 1) void prefill_attn_kernel(
           s[b] = mfma32<BF16>(kf, qf[st], s[b]);
         }
       }
-#endif
+      }
       if (kbase + kKeys - 1 > a.start + pw_lo) {     // the tile straddles this wave's diagonal
 #pragma unroll
         for (int b = 0; b < 2; ++b)
@@ -348,17 +352,17 @@ __global__ __launch_bounds__(NW * 64, KS == 1 ? 2 : 1) void prefill_attn_kernel(
       }
     }
 
-#if !AMDK8S_PA_WAB
-    if (kt + KS < t1) store_tile(buf ^ 1);
-#endif
+    if constexpr (!WAB) {
+      if (kt + KS < t1) store_tile(buf ^ 1);
+    }
     __syncthreads();
   };
 
   load_tile(t0 * kKeys);
   store_tile(0);
-#if AMDK8S_PA_WAB
-  if (t0 + KS < t1) load_tile((t0 + KS) * kKeys);
-#endif
+  if constexpr (WAB) {
+    if (t0 + KS < t1) load_tile((t0 + KS) * kKeys);
+  }
   __syncthreads();
 #if AMDK8S_PA_UNROLL2
   for (int kt = t0; kt < t1; kt += 2 * KS) {  // the buffer parity a constant in each half
