@@ -482,37 +482,47 @@ Plan make_plan(int P, int start, int H, int Hkv, int nsplit_req, int nw_req, int
   // * a chunk with many rows after a long prefix: 8 waves (each K/V tile feeds 256 rows) and the
   //   keys split until the grid is ONE round of 8-wave workgroups (<= 256; 512 @ 31488: 4 splits
   //   268 us, 5 splits 353, 8 splits 288; 512 @ 3072: 4 splits 51.1 us);
-  // * few rows (a short chunk, a single token) after a long prefix: 4 waves, splits up to 256
-  //   workgroups (64 @ 8192: 12-16 splits 36.8-37.3 us vs 8 waves 43-49).
+  // * few rows (a short chunk, a single token) after a long prefix: 4-wave row blocks, splits up
+  //   to 256 workgroups (64 @ 8192: 12-16 splits 36.8-37.3 us vs 8 waves 43-49); since the key
+  //   slots, the same row blocks as 8 waves x 2 slots (below).
   Plan pl;
   const int group = H / Hkv;
   const long rows = (long)P * group;
   const int ntiles = (start + P + kKeys - 1) / kKeys;
   const long base4 = (rows + 127) / 128 * Hkv, base8 = (rows + 255) / 256 * Hkv;
-  int nw = 4, ns = 1;
+  int nw = 4, ns = 1, ks = 1;
   if (start > 0 && base4 < 256) {
     const int ns8 = (int)std::min<long>(256 / base8, ntiles / 12);
     if (rows >= 1024 && ns8 >= 2) {
       nw = 8;
       ns = ns8;
+    } else if (ntiles >= 128) {
+      // few rows after 8k+ positions: 8 waves as 4 row waves x 2 key slots (the 4-wave row block,
+      // each step's two tiles to different waves), about half the splits (profiles/r06/
+      // prefill_attn_plan_ab.log, same process: 64 @ 8192 34.6-37.2 vs 36.2-37.2 us, 128 @ 16000
+      // 52.1-53.1 vs 55.9-57.9, one token at 31000 44.5-44.9 vs 48.0-49.1; after shorter
+      // prefixes the split count gets too small: 7 @ 3000 29.7 vs 18.9, 200 @ 1000 26.1 vs 23.5)
+      nw = 8;
+      ks = 2;
+      ns = (int)std::max<long>(1, std::min<long>(std::min<long>(256 / base4, ntiles / 16), 32));
     } else {
       ns = (int)std::max<long>(1, std::min<long>(std::min<long>(256 / base4, ntiles / 8), 32));
     }
   }
   // a grid of a round or more with long key runs: 8 waves, each staged K/V tile feeding 256 rows
   // (profiles/r06/prefill_attn_sweep_long.log: 32000 @ 0 10.07 vs 10.73 ms, 16384 @ 0 2.54 vs
-  // 2.72, 12288 @ 0 1.52 vs 1.61, 4096 @ 28000 1.85 vs 2.12, 16384 @ 16384 6.67 vs 7.21; 8192 @ 0
-  // and 8192 @ 8192 within 1 %)
+  // 2.72, 12288 @ 0 1.52 vs 1.61, 4096 @ 28000 1.85 vs 2.12, 16384 @ 16384 6.67 vs 7.21; with
+  // its write-after-barrier staging, profiles/r06/prefill_attn_sweep_8w_wab.log: 8192 @ 0 639 vs
+  // 672 us, 4096 @ 0 182 vs 205, 3584 @ 0 145 vs 160; 2048 @ 0 a tie)
   static const bool long8 = [] {                // AMDK8S_PA_LONG8=0: 4 waves (A/B runs)
     const char* e = getenv("AMDK8S_PA_LONG8");
     return !e || e[0] != '0';
   }();
-  if (long8 && base4 >= 256 && start + P >= 12288) nw = 8;
+  if (long8 && base4 >= 256 && start + P >= 3072) nw = 8;
   // key slots, for a prompt from position 0 whose 4-wave grid is under one round (profiles/r06/
   // prefill_attn_sweep_key_slots.log): up to half a round, 4 waves as 2 row waves x 2 slots
   // (512 @ 0: 14.1 vs 17.1 us; 256 @ 0: 10.4 vs 11.0), else 8 waves as 4 x 2 (1024 @ 0: 25.4 vs
   // 28.2); a full round or more keeps one slot (2048 @ 0: 62.4 vs 68.7 with 8 x 2)
-  int ks = 1;
   if (start == 0 && ns == 1 && base4 <= 256) {
     ks = 2;
     if (base4 * 2 > 256) nw = 8;

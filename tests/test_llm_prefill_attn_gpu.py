@@ -65,7 +65,7 @@ def test_prefill_attention_forced_plans_agree(LK, nsplit, nw):
     H, Hkv, P, start = 28, 4, 200, 1000
     q, kc, vc = _case(H, Hkv, P, start, seed=1)
     out = torch.empty(P, H, 128, device=q.device, dtype=q.dtype).transpose(0, 1)
-    LK.prefill_attn(q, kc, vc, out, start, 1 / math.sqrt(128), nsplit=nsplit, nw=nw)
+    LK.prefill_attn(q, kc, vc, out, start, 1 / math.sqrt(128), nsplit=nsplit, nw=nw, ks=1)
     torch.testing.assert_close(out.float(), _ref(q, kc, vc, start), rtol=1e-2, atol=3e-3)
 
 
@@ -114,6 +114,9 @@ def test_prefill_attention_plan_fills_the_chip(LK):
     assert LK.prefill_attn_plan(2048, 0, 28, 4)["key_slots"] == 1
     assert LK.prefill_attn_plan(2048, 0, 28, 4)["waves"] == 4
     assert LK.prefill_attn_plan(32000, 0, 28, 4)["waves"] == 8     # long key runs
+    assert LK.prefill_attn_plan(4096, 0, 28, 4)["waves"] == 8
+    few = LK.prefill_attn_plan(64, 8192, 28, 4)                     # few rows, long prefix
+    assert few["key_slots"] == 2 and few["nsplit"] > 1
     assert LK.prefill_attn_plan(4096, 28000, 28, 4)["waves"] == 8
 
 
