@@ -56,8 +56,11 @@ constexpr int kDblk = kD / 32;
 // ~50 VALU per tile, but the loop is not issue-bound — PMC: MFMA busy 29 %, 7.6 VALU per MFMA,
 // profiles/r06/prefill_attn_pmc_8192.txt), the zero C is neutral; the hoisted offsets alone
 // (default) are within 1 % of the round-6 loop.
+// -1 = per shape: the 8-wave one-slot kernel (write-after-barrier staging, prefetch schedule)
+// unrolls by two — 32000 @ 0 9.42-9.46 -> 8.89-8.93 ms, 8192 @ 0 642-643 -> 609-610 us,
+// 4096 @ 28000 1.75 -> 1.69 ms, 512 @ 31488 249 -> 242 us (profiles/r06/attn_ab_8w/)
 #ifndef AMDK8S_PA_UNROLL2
-#define AMDK8S_PA_UNROLL2 0
+#define AMDK8S_PA_UNROLL2 -1
 #endif
 #ifndef AMDK8S_PA_ZEROC
 #define AMDK8S_PA_ZEROC 0
@@ -131,6 +134,7 @@ __global__ __launch_bounds__(NW * 64, KS == 1 ? 2 : 1) void prefill_attn_kernel(
   const int r = lane & 31, h = lane >> 5;
   const int rw = KS == 1 ? wave : wave % RW, ksl = KS == 1 ? 0 : wave / RW;
   constexpr bool WAB = AMDK8S_PA_WAB < 0 ? NW == 8 : AMDK8S_PA_WAB != 0;
+  constexpr bool UNROLL2 = AMDK8S_PA_UNROLL2 < 0 ? NW == 8 && KS == 1 : AMDK8S_PA_UNROLL2 != 0;
   constexpr int SCHED = AMDK8S_PA_SCHED < 0 ? (NW == 8 || KS == 2 ? 2 : 0) : AMDK8S_PA_SCHED;
 
   // XCD-major block -> work item (consecutive work items share an XCD and so its L2); work order:
@@ -364,14 +368,14 @@ __global__ __launch_bounds__(NW * 64, KS == 1 ? 2 : 1) void prefill_attn_kernel(
     if (t0 + KS < t1) load_tile((t0 + KS) * kKeys);
   }
   __syncthreads();
-#if AMDK8S_PA_UNROLL2
-  for (int kt = t0; kt < t1; kt += 2 * KS) {  // the buffer parity a constant in each half
-    tile(kt, 0);
-    if (kt + KS < t1) tile(kt + KS, 1);
+  if constexpr (UNROLL2) {
+    for (int kt = t0; kt < t1; kt += 2 * KS) {  // the buffer parity a constant in each half
+      tile(kt, 0);
+      if (kt + KS < t1) tile(kt + KS, 1);
+    }
+  } else {
+    for (int kt = t0; kt < t1; kt += KS) tile(kt, ((kt - t0) / KS) & 1);
   }
-#else
-  for (int kt = t0; kt < t1; kt += KS) tile(kt, ((kt - t0) / KS) & 1);
-#endif
 
   if constexpr (KS > 1) {
     // merge the key slots (the last step ended with a barrier, so the tile buffers are free):
