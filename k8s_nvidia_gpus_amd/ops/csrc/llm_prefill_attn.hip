@@ -517,12 +517,13 @@ Plan make_plan(int P, int start, int H, int Hkv, int nsplit_req, int nw_req, int
   // (profiles/r06/prefill_attn_sweep_long.log: 32000 @ 0 10.07 vs 10.73 ms, 16384 @ 0 2.54 vs
   // 2.72, 12288 @ 0 1.52 vs 1.61, 4096 @ 28000 1.85 vs 2.12, 16384 @ 16384 6.67 vs 7.21; with
   // its write-after-barrier staging, profiles/r06/prefill_attn_sweep_8w_wab.log: 8192 @ 0 639 vs
-  // 672 us, 4096 @ 0 182 vs 205, 3584 @ 0 145 vs 160; 2048 @ 0 a tie)
+  // 672 us, 4096 @ 0 182 vs 205, 3584 @ 0 145 vs 160; unrolled by two, profiles/r06/
+  // prefill_attn_sweep_8w_u2.log: 2048 @ 0 60.9 vs 63.7 us, 2560 @ 0 89.4 vs 95.5; 1536 @ 0 a tie)
   static const bool long8 = [] {                // AMDK8S_PA_LONG8=0: 4 waves (A/B runs)
     const char* e = getenv("AMDK8S_PA_LONG8");
     return !e || e[0] != '0';
   }();
-  if (long8 && base4 >= 256 && start + P >= 3072) nw = 8;
+  if (long8 && base4 >= 256 && start + P >= 2048) nw = 8;
   // key slots, for a prompt from position 0 whose 4-wave grid is under one round (profiles/r06/
   // prefill_attn_sweep_key_slots.log): up to half a round, 4 waves as 2 row waves x 2 slots
   // (512 @ 0: 14.1 vs 17.1 us; 256 @ 0: 10.4 vs 11.0), else 8 waves as 4 x 2 (1024 @ 0: 25.4 vs

@@ -112,7 +112,8 @@ def test_prefill_attention_plan_fills_the_chip(LK):
     assert LK.prefill_attn_plan(1024, 0, 28, 4)["key_slots"] == 2
     assert LK.prefill_attn_plan(1024, 0, 28, 4)["waves"] == 8
     assert LK.prefill_attn_plan(2048, 0, 28, 4)["key_slots"] == 1
-    assert LK.prefill_attn_plan(2048, 0, 28, 4)["waves"] == 4
+    assert LK.prefill_attn_plan(1536, 0, 28, 4)["waves"] == 4
+    assert LK.prefill_attn_plan(2048, 0, 28, 4)["waves"] == 8
     assert LK.prefill_attn_plan(32000, 0, 28, 4)["waves"] == 8     # long key runs
     assert LK.prefill_attn_plan(4096, 0, 28, 4)["waves"] == 8
     few = LK.prefill_attn_plan(64, 8192, 28, 4)                     # few rows, long prefix
