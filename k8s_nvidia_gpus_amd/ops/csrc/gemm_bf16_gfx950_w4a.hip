@@ -41,7 +41,12 @@ constexpr int NT = 256;
 constexpr int HALF_BYTES = 128 * BK * 2;     // 128 rows × 128 B
 constexpr int C_STRIDE = BN * 2 + 16;        // padded epilogue row (matches the generator)
 constexpr int LDS_BYTES = BM * C_STRIDE;     // 135168 ≥ 2 × 64 KiB K-tile buffers
-constexpr int GROUP_M = 8;
+#ifndef AMDK8S_W4_GROUP_M
+#define AMDK8S_W4_GROUP_M 8
+#endif
+// A/B knob (build-time).  At M = 32000 (a 32k prompt) 4 and 16 are within 1-2 % of 8 on q|k|v,
+// o_proj and gate|up, better and worse by shape (profiles/r06/gemm32k_group_m/)
+constexpr int GROUP_M = AMDK8S_W4_GROUP_M;
 
 typedef __attribute__((address_space(3))) char lds_char;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
