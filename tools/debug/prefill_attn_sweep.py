@@ -36,10 +36,14 @@ def main(argv):
         [(512, 0), (512, 3072), (512, 31488), (64, 8192), (2048, 0), (8192, 0)]
     for P, start in cases:
         end = start + P
-        q = torch.randn(H, P, d, device=dev, dtype=torch.float16)
+        if os.environ.get("SWEEP_TOKEN_MAJOR") == "1":     # the engine's [P][H][128] storage
+            q = torch.randn(P, H, d, device=dev, dtype=torch.float16).transpose(0, 1)
+            out = torch.empty(P, H, d, device=dev, dtype=torch.float16).transpose(0, 1)
+        else:
+            q = torch.randn(H, P, d, device=dev, dtype=torch.float16)
+            out = torch.empty(H, P, d, device=dev, dtype=torch.float16)
         k = torch.randn(Hkv, end, d, device=dev, dtype=torch.float16)
         v = torch.randn(Hkv, end, d, device=dev, dtype=torch.float16)
-        out = torch.empty(H, P, d, device=dev, dtype=torch.float16)
         auto = LK.prefill_attn_plan(P, start, H, Hkv)
         flop = 4 * H * d * P * (start + (P + 1) / 2)
         us = timed(lambda: LK.prefill_attn(q, k, v, out, start, 1 / math.sqrt(d)),
